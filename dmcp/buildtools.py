@@ -1,0 +1,121 @@
+"""In-tree native build driver (no pip install, no JIT cache).
+
+Builds, into the source tree so the artefacts travel with the repo snapshot:
+
+* ``dmcp/_srcscan<ext>``  -- pybind11 module over ``native/srcscan`` (host C++17)
+* ``bin/srcscan``         -- the standalone analyzer CLI (go-analyzer replacement)
+* ``bin/srcscan-asan``    -- optional ASan/UBSan build of the CLI (``--sanitize``)
+* ``dmcp/ops/_hipops<ext>`` -- HIP kernels for gfx950 (see :mod:`dmcp.ops.build`)
+
+Usage: ``python -m dmcp.buildtools [--sanitize] [--no-hip] [--force]``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import hashlib
+import os
+import subprocess
+import sys
+import sysconfig
+from typing import List, Sequence
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NATIVE = os.path.join(ROOT, "native", "srcscan")
+BUILD = os.path.join(ROOT, "build", "native")
+BIN = os.path.join(ROOT, "bin")
+
+CORE_SOURCES = ["common.cpp", "java_frontend.cpp", "ts_frontend.cpp", "go_frontend.cpp", "project.cpp"]
+CXX = os.environ.get("CXX", "g++")
+CXXFLAGS = ["-std=c++17", "-O3", "-fPIC", "-Wall", "-Wno-unused-function", "-pthread"]
+
+
+def ext_suffix() -> str:
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def srcscan_module_path() -> str:
+    return os.path.join(ROOT, "dmcp", "_srcscan" + ext_suffix())
+
+
+def _digest(paths: Sequence[str], extra: str = "") -> str:
+    h = hashlib.sha256(extra.encode())
+    for p in sorted(paths):
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def _run(cmd: List[str]) -> None:
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"command failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}")
+
+
+def _compile_objects(flags: List[str], tag: str, jobs: int) -> List[str]:
+    os.makedirs(BUILD, exist_ok=True)
+    headers = [os.path.join(NATIVE, h) for h in os.listdir(NATIVE) if h.endswith(".hpp")]
+
+    def one(src: str) -> str:
+        s = os.path.join(NATIVE, src)
+        key = _digest([s] + headers, " ".join(flags))
+        obj = os.path.join(BUILD, f"{src[:-4]}.{tag}.{key}.o")
+        if not os.path.exists(obj):
+            _run([CXX, *flags, "-c", s, "-o", obj])
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        return list(ex.map(one, CORE_SOURCES))
+
+
+def build_srcscan(force: bool = False, sanitize: bool = False, jobs: int = 0) -> str:
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    sources = [os.path.join(NATIVE, s) for s in os.listdir(NATIVE) if s.endswith((".cpp", ".hpp"))]
+    stamp = os.path.join(BUILD, "srcscan.stamp")
+    key = _digest(sources, " ".join(CXXFLAGS) + sys.version)
+    target = srcscan_module_path()
+    cli = os.path.join(BIN, "srcscan")
+    if (not force and os.path.exists(target) and os.path.exists(cli) and os.path.exists(stamp)
+            and open(stamp).read().strip() == key):
+        if not sanitize or os.path.exists(os.path.join(BIN, "srcscan-asan")):
+            return target
+    objs = _compile_objects(CXXFLAGS, "rel", jobs)
+    import pybind11  # noqa: WPS433 (build-time only)
+    inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", f"-I{NATIVE}"]
+    py_obj = os.path.join(BUILD, f"pymodule.{_digest([os.path.join(NATIVE, 'pymodule.cpp')])}.o")
+    _run([CXX, *CXXFLAGS, *inc, "-fvisibility=hidden", "-c", os.path.join(NATIVE, "pymodule.cpp"), "-o", py_obj])
+    tmp = target + ".tmp"
+    _run([CXX, "-shared", "-pthread", "-o", tmp, py_obj, *objs])
+    os.replace(tmp, target)
+    os.makedirs(BIN, exist_ok=True)
+    _run([CXX, *CXXFLAGS, "-o", cli, os.path.join(NATIVE, "cli.cpp"), *objs])
+    if sanitize:
+        san = ["-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-pthread",
+               "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
+        sobjs = _compile_objects(san, "asan", jobs)
+        _run([CXX, *san, "-o", os.path.join(BIN, "srcscan-asan"), os.path.join(NATIVE, "cli.cpp"), *sobjs])
+    with open(stamp, "w") as f:
+        f.write(key)
+    return target
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--sanitize", action="store_true", help="also build bin/srcscan-asan")
+    ap.add_argument("--no-hip", action="store_true", help="skip the gfx950 HIP kernels")
+    ap.add_argument("-j", "--jobs", type=int, default=0)
+    a = ap.parse_args(argv)
+    print(build_srcscan(force=a.force, sanitize=a.sanitize, jobs=a.jobs))
+    if not a.no_hip:
+        try:
+            from dmcp.ops import build as hipbuild
+        except ImportError:
+            hipbuild = None
+        if hipbuild is not None:
+            print(hipbuild.build(force=a.force))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

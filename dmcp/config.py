@@ -1,0 +1,184 @@
+"""Typed runtime configuration.
+
+Parity: ``src/main/resources/application.yml:1-74`` and ``application-mcp.yml``.
+Every reference key is honoured -- including the ones the reference declares
+but never reads (``claude.model``, ``claude.max-tokens``, ``git.ssh-key-path``,
+``git.timeout-seconds``, ``mcp.server.*``) -- with the reference
+defaults.  Sources, lowest to highest precedence: defaults, an optional
+TOML/YAML file (``DMCP_CONFIG``), environment variables.
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+from dataclasses import dataclass, field
+from typing import Any, Dict, Optional
+
+DEFAULT_CLAUDE_MODEL = "claude-sonnet-4-5-20250929"
+
+
+@dataclass
+class Config:
+    # storage (application.yml:11-29); DATABASE_URL may be sqlite:///path or a path
+    db_path: str = field(default_factory=lambda: os.path.join(
+        os.path.expanduser("~"), ".dmcp", "dmcp.db"))
+    # HTTP (application.yml:1-5)
+    server_port: int = 8080
+    server_host: str = "127.0.0.1"
+    app_url: str = "http://localhost:8080"
+    # enrichment (application.yml:38-41, ClaudeApiClient.java:40,123-125,151)
+    anthropic_api_key: Optional[str] = None
+    anthropic_base_url: str = "https://api.anthropic.com"
+    claude_model: str = DEFAULT_CLAUDE_MODEL
+    claude_max_tokens: int = 16384
+    claude_timeout_seconds: float = 240.0
+    claude_max_retries: int = 2
+    enrich_max_concurrent: int = 5          # CodeContextService.java:77
+    enrich_batch_size: int = 20             # CodeContextService.java:75
+    enrich_backend: str = "auto"            # auto | anthropic | null | fake | local
+    enrich_max_source_chars: int = 200_000  # prompt budget for huge files
+    require_enrichment_for_analyze: bool = True  # READ_ONLY_MODE parity
+    # local MI355X enrichment backend (extension, see dmcp/enrich/local.py)
+    local_llm_preset: str = "dmcp-coder-1b"
+    local_llm_max_new_tokens: int = 256
+    local_llm_devices: str = "all"
+    # git (application.yml:44-47)
+    git_clone_base_path: str = "/tmp/domain-mcp-repos"
+    git_ssh_key_path: Optional[str] = None
+    git_timeout_seconds: int = 300
+    # sync (application.yml:49-52)
+    sync_enabled: bool = False
+    sync_cron: str = "0 0 2 * * *"
+    # MCP (application.yml:54-59; serverInfo is hard-coded 1.0.1 in the reference)
+    mcp_server_name: str = "domain-mcp-server"
+    mcp_server_version: str = "1.0.1"
+    mcp_server_description: str = ("Domain MCP Server - Analyzes git repositories and extracts "
+                                   "business information")
+    # pipeline tunables (CodeContextService.java:73, 176-177)
+    max_readme_length: int = 10_000
+    description_length: int = 500
+    parser_threads: int = 0
+    recover_stuck_on_start: bool = True
+    log_level: str = "INFO"
+
+    @classmethod
+    def from_env(cls, env: Optional[Dict[str, str]] = None, file: Optional[str] = None) -> "Config":
+        env = dict(os.environ if env is None else env)
+        cfg = cls()
+        path = file or env.get("DMCP_CONFIG")
+        if path:
+            cfg = cfg.merged(load_config_file(path))
+        mapping = {
+            "DMCP_DB_PATH": "db_path",
+            "SERVER_PORT": "server_port",
+            "SERVER_HOST": "server_host",
+            "APP_URL": "app_url",
+            "ANTHROPIC_API_KEY": "anthropic_api_key",
+            "ANTHROPIC_BASE_URL": "anthropic_base_url",
+            "CLAUDE_MODEL": "claude_model",
+            "CLAUDE_MAX_TOKENS": "claude_max_tokens",
+            "CLAUDE_TIMEOUT_SECONDS": "claude_timeout_seconds",
+            "CLAUDE_MAX_RETRIES": "claude_max_retries",
+            "ENRICH_MAX_CONCURRENT": "enrich_max_concurrent",
+            "ENRICH_BATCH_SIZE": "enrich_batch_size",
+            "ENRICH_BACKEND": "enrich_backend",
+            "REQUIRE_ENRICHMENT_FOR_ANALYZE": "require_enrichment_for_analyze",
+            "LOCAL_LLM_PRESET": "local_llm_preset",
+            "LOCAL_LLM_MAX_NEW_TOKENS": "local_llm_max_new_tokens",
+            "LOCAL_LLM_DEVICES": "local_llm_devices",
+            "GIT_CLONE_BASE_PATH": "git_clone_base_path",
+            "GIT_SSH_KEY_PATH": "git_ssh_key_path",
+            "GIT_TIMEOUT_SECONDS": "git_timeout_seconds",
+            "SYNC_ENABLED": "sync_enabled",
+            "SYNC_CRON": "sync_cron",
+            "MCP_SERVER_NAME": "mcp_server_name",
+            "MCP_SERVER_VERSION": "mcp_server_version",
+            "PARSER_THREADS": "parser_threads",
+            "RECOVER_STUCK_ON_START": "recover_stuck_on_start",
+            "LOG_LEVEL": "log_level",
+        }
+        updates: Dict[str, Any] = {}
+        for key, attr in mapping.items():
+            if key in env and env[key] != "":
+                updates[attr] = env[key]
+        db_url = env.get("DATABASE_URL")
+        if db_url and "DMCP_DB_PATH" not in env:
+            updates["db_path"] = sqlite_path_from_url(db_url)
+        return cfg.merged(updates)
+
+    def merged(self, values: Dict[str, Any]) -> "Config":
+        types = {f.name: f.type for f in dataclasses.fields(self)}
+        kw = {}
+        for k, v in values.items():
+            k = k.replace("-", "_").replace(".", "_")
+            if k not in types:
+                continue
+            kw[k] = _coerce(v, getattr(self, k), types[k])
+        return dataclasses.replace(self, **kw)
+
+    def has_api_key(self) -> bool:
+        return bool(self.anthropic_api_key and self.anthropic_api_key.strip())
+
+    def resolved_enrich_backend(self) -> str:
+        b = (self.enrich_backend or "auto").lower()
+        if b == "auto":
+            return "anthropic" if self.has_api_key() else "none"
+        return b
+
+
+def sqlite_path_from_url(url: str) -> str:
+    if url.startswith("sqlite:///"):
+        return url[len("sqlite:///") - 1:] if url.startswith("sqlite:////") else url[len("sqlite:///"):]
+    if url.startswith("sqlite://"):
+        return url[len("sqlite://"):]
+    if url.startswith("jdbc:") or url.startswith("postgres"):
+        raise ValueError("PostgreSQL URLs are not supported on this host (no driver); "
+                         "use sqlite:///path or DMCP_DB_PATH")
+    return url
+
+
+def _coerce(value: Any, current: Any, typ: Any) -> Any:
+    t = str(typ)
+    if value is None:
+        return None
+    if "bool" in t or isinstance(current, bool):
+        if isinstance(value, bool):
+            return value
+        return str(value).strip().lower() in ("1", "true", "yes", "on")
+    if "int" in t and "Optional" not in t or isinstance(current, int) and not isinstance(current, bool):
+        return int(value)
+    if "float" in t or isinstance(current, float):
+        return float(value)
+    return str(value) if not isinstance(value, str) else value
+
+
+def load_config_file(path: str) -> Dict[str, Any]:
+    """Reads a TOML or YAML config file and flattens nested sections
+    (``claude.max-tokens`` -> ``claude_max_tokens``)."""
+    with open(path, "rb") as f:
+        data = f.read()
+    if path.endswith((".yml", ".yaml")):
+        import yaml
+        tree = yaml.safe_load(data.decode("utf-8")) or {}
+    else:
+        try:
+            import tomllib  # type: ignore
+        except ImportError:  # py3.10
+            import tomli as tomllib  # type: ignore
+        tree = tomllib.loads(data.decode("utf-8"))
+    flat: Dict[str, Any] = {}
+
+    def walk(prefix: str, node: Any) -> None:
+        if isinstance(node, dict):
+            for k, v in node.items():
+                key = f"{prefix}_{k}" if prefix else str(k)
+                walk(key.replace("-", "_").replace(".", "_"), v)
+        else:
+            flat[prefix] = node
+
+    walk("", tree)
+    aliases = {"claude_api_key": "anthropic_api_key", "git_clone_base_path": "git_clone_base_path",
+               "server_port": "server_port", "mcp_server_name": "mcp_server_name",
+               "mcp_server_version": "mcp_server_version", "sync_cron": "sync_cron",
+               "sync_enabled": "sync_enabled", "database_path": "db_path"}
+    return {aliases.get(k, k): v for k, v in flat.items()}

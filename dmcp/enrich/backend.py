@@ -1,0 +1,281 @@
+"""Enrichment backends: who writes the business descriptions.
+
+Parity: ``analysis/domain/ClaudeApiClient.java`` -- enrichment prompt
+(``:85-121``: source + statically inferred type + method names in, ``{description,
+classTypeCorrection, methods[{methodName, description, businessLogic[]}]}``
+out), ``enrichClass`` (``:288-329``; failures become failure results, never
+exceptions) and ``enrichBatch`` (``:342-388``: one task per input, at most
+``maxConcurrent`` in flight, results in input order).  The legacy
+full-analysis path (``analyzeClass``/``analyzeBatch``, ``:164-275``) is dead
+code in the reference and is provided as :meth:`AnthropicBackend.analyze_class`
+for completeness.
+
+Backends:
+
+* :class:`AnthropicBackend` -- Messages API over HTTPS (stdlib ``urllib``),
+  model/max-tokens/timeout/retries from config (the reference hard-codes them).
+* :class:`NullBackend`      -- enrichment disabled (static indexing only).
+* :class:`FakeBackend`      -- deterministic, offline; used by tests and benches.
+* ``LocalLLMBackend``       -- optional MI355X extension (:mod:`dmcp.enrich.local`).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import random
+import threading
+import time
+import urllib.error
+import urllib.request
+from concurrent.futures import ThreadPoolExecutor
+from typing import Callable, List, Optional, Sequence
+
+from ..utils.errors import require_non_blank, require_non_null
+from .jsonfix import parse_enrichment_response
+from .types import EnrichmentInput, EnrichmentResult
+
+LOG = logging.getLogger(__name__)
+
+ENRICHMENT_PROMPT = """\
+You are adding business context to one {language} source file that has already been
+parsed statically.
+
+Project context (README):
+{readme}
+
+Source of {name}:
+```{language}
+{source}
+```
+
+Statically extracted facts:
+- Class type: {class_type}
+- Methods: {methods}
+
+Describe what this code means for the business, not how it is implemented.
+Answer with exactly one JSON object of this shape and nothing else:
+{{
+  "description": "one sentence on the business purpose of this class/module",
+  "classTypeCorrection": "a corrected class type, or null when {class_type} is right",
+  "methods": [
+    {{"methodName": "a method name from the list above",
+      "description": "one sentence of business meaning",
+      "businessLogic": ["business step 1", "business step 2"]}}
+  ]
+}}
+Rules: cover every listed method; change the class type only when it is clearly wrong
+(valid types: CONTROLLER, SERVICE, REPOSITORY, ENTITY, DTO, CONFIGURATION, LISTENER,
+UTILITY, EXCEPTION, OTHER); the first character of the reply must be {{ and the last }}.
+"""
+
+ANALYSIS_PROMPT = """\
+You are analyzing one {language} source file of a project.
+
+Project context (README):
+{readme}
+
+Source of {name}:
+```{language}
+{source}
+```
+
+Reply with one JSON object: {{"fullClassName", "classType", "description", "sourceFile",
+"methods": [{{"methodName", "description", "businessLogic": [], "exceptions": [],
+"httpMethod", "httpPath", "lineNumber"}}]}}. Describe business meaning, include every
+public method, one sentence per description, and output raw JSON only.
+"""
+
+
+def build_enrichment_prompt(inp: EnrichmentInput, readme: Optional[str],
+                            max_source_chars: int = 0) -> str:
+    src = inp.source_code
+    if max_source_chars and len(src) > max_source_chars:
+        src = src[:max_source_chars] + "\n...(truncated)"
+    return ENRICHMENT_PROMPT.format(
+        language=inp.language or "java",
+        readme=readme if readme and readme.strip() else "No README available.",
+        name=inp.full_class_name, source=src, class_type=inp.class_type,
+        methods=", ".join(inp.method_names))
+
+
+class EnrichmentBackend:
+    """Base: subclasses implement :meth:`enrich_class`; the batch fan-out is shared."""
+
+    name = "base"
+
+    def __init__(self, max_concurrent: int = 5) -> None:
+        self.max_concurrent = max(1, int(max_concurrent))
+        self._pool: Optional[ThreadPoolExecutor] = None
+        self._pool_lock = threading.Lock()
+
+    @property
+    def enabled(self) -> bool:
+        return True
+
+    def enrich_class(self, inp: EnrichmentInput, readme: Optional[str]) -> EnrichmentResult:
+        raise NotImplementedError
+
+    def _executor(self) -> ThreadPoolExecutor:
+        with self._pool_lock:
+            if self._pool is None:
+                self._pool = ThreadPoolExecutor(max_workers=self.max_concurrent,
+                                                thread_name_prefix=f"enrich-{self.name}")
+            return self._pool
+
+    def _safe(self, inp: EnrichmentInput, readme: Optional[str]) -> EnrichmentResult:
+        try:
+            return self.enrich_class(inp, readme)
+        except Exception as e:  # isolate per-class failures (ClaudeApiClient.java:322-328)
+            LOG.warning("Enrichment failed for %s: %s", inp.full_class_name, e)
+            return EnrichmentResult.failure(inp.full_class_name, str(e))
+
+    def enrich_batch(self, inputs: Sequence[EnrichmentInput], readme: Optional[str]) -> List[EnrichmentResult]:
+        require_non_null(inputs, "Inputs list is required")
+        if not inputs:
+            return []
+        if self.max_concurrent == 1 or len(inputs) == 1:
+            return [self._safe(i, readme) for i in inputs]
+        ex = self._executor()
+        futures = [ex.submit(self._safe, i, readme) for i in inputs]
+        out = []
+        for inp, fut in zip(inputs, futures):
+            try:
+                out.append(fut.result())
+            except Exception as e:
+                out.append(EnrichmentResult.failure(inp.full_class_name, str(e)))
+        return out
+
+    def close(self) -> None:
+        with self._pool_lock:
+            if self._pool is not None:
+                self._pool.shutdown(wait=False)
+                self._pool = None
+
+
+class NullBackend(EnrichmentBackend):
+    name = "null"
+
+    @property
+    def enabled(self) -> bool:
+        return False
+
+    def enrich_class(self, inp: EnrichmentInput, readme: Optional[str]) -> EnrichmentResult:
+        return EnrichmentResult.failure(inp.full_class_name, "enrichment disabled")
+
+
+class FakeBackend(EnrichmentBackend):
+    """Deterministic offline backend.
+
+    ``responder`` (optional) maps an input to raw model text, which then goes
+    through the same JSON extraction/repair path as a real reply -- tests use
+    it to inject fenced, truncated or malformed replies and failures.
+    """
+
+    name = "fake"
+
+    def __init__(self, max_concurrent: int = 5,
+                 responder: Optional[Callable[[EnrichmentInput], str]] = None,
+                 latency_s: float = 0.0) -> None:
+        super().__init__(max_concurrent)
+        self.responder = responder
+        self.latency_s = latency_s
+        self.calls: List[str] = []
+        self._lock = threading.Lock()
+
+    def enrich_class(self, inp: EnrichmentInput, readme: Optional[str]) -> EnrichmentResult:
+        with self._lock:
+            self.calls.append(inp.full_class_name)
+        if self.latency_s:
+            time.sleep(self.latency_s)
+        if self.responder is not None:
+            return parse_enrichment_response(self.responder(inp), inp.full_class_name)
+        simple = inp.full_class_name.rsplit(".", 1)[-1]
+        reply = {
+            "description": f"{simple} handles the {simple.lower()} business capability",
+            "classTypeCorrection": None,
+            "methods": [{"methodName": m, "description": f"Performs {m}",
+                         "businessLogic": [f"Validate {m} input", f"Apply {m} rule"]}
+                        for m in inp.method_names],
+        }
+        return parse_enrichment_response(json.dumps(reply), inp.full_class_name)
+
+
+class AnthropicBackend(EnrichmentBackend):
+    """Anthropic Messages API client (stdlib HTTP, retries with backoff)."""
+
+    name = "anthropic"
+    API_VERSION = "2023-06-01"
+
+    def __init__(self, api_key: str, model: str, max_tokens: int = 16384, timeout_s: float = 240.0,
+                 max_retries: int = 2, max_concurrent: int = 5,
+                 base_url: str = "https://api.anthropic.com", max_source_chars: int = 0) -> None:
+        super().__init__(max_concurrent)
+        self.api_key = require_non_blank(api_key, "API key is required")
+        self.model = model
+        self.max_tokens = int(max_tokens)
+        self.timeout_s = float(timeout_s)
+        self.max_retries = int(max_retries)
+        self.base_url = base_url.rstrip("/")
+        self.max_source_chars = max_source_chars
+
+    def _post(self, prompt: str) -> str:
+        body = json.dumps({"model": self.model, "max_tokens": self.max_tokens,
+                           "messages": [{"role": "user", "content": prompt}]}).encode("utf-8")
+        req = urllib.request.Request(f"{self.base_url}/v1/messages", data=body, method="POST", headers={
+            "content-type": "application/json", "x-api-key": self.api_key,
+            "anthropic-version": self.API_VERSION})
+        attempt = 0
+        while True:
+            try:
+                with urllib.request.urlopen(req, timeout=self.timeout_s) as resp:
+                    payload = json.loads(resp.read().decode("utf-8"))
+                return "".join(block.get("text", "") for block in payload.get("content", [])
+                               if block.get("type") == "text")
+            except urllib.error.HTTPError as e:
+                retryable = e.code in (408, 409, 429) or e.code >= 500
+                if not retryable or attempt >= self.max_retries:
+                    detail = e.read().decode("utf-8", "replace")[:500] if hasattr(e, "read") else ""
+                    raise RuntimeError(f"HTTP {e.code}: {detail}") from e
+            except (urllib.error.URLError, TimeoutError, ConnectionError) as e:
+                if attempt >= self.max_retries:
+                    raise RuntimeError(f"request failed: {e}") from e
+            attempt += 1
+            time.sleep(min(8.0, 0.5 * 2 ** attempt) * (0.75 + random.random() / 2))
+
+    def enrich_class(self, inp: EnrichmentInput, readme: Optional[str]) -> EnrichmentResult:
+        require_non_null(inp, "Enrichment input is required")
+        raw = self._post(build_enrichment_prompt(inp, readme, self.max_source_chars))
+        return parse_enrichment_response(raw, inp.full_class_name)
+
+    def analyze_class(self, source_code: str, full_class_name: str, source_file: str,
+                      readme: Optional[str], language: Optional[str]) -> dict:
+        """Legacy single-shot analysis (dead code in the reference)."""
+        require_non_blank(source_code, "Source code is required")
+        require_non_blank(full_class_name, "Full class name is required")
+        from .jsonfix import loads_lenient
+        prompt = ANALYSIS_PROMPT.format(language=language or "java",
+                                        readme=readme or "No README available.",
+                                        name=full_class_name, source=source_code)
+        try:
+            root = loads_lenient(self._post(prompt))
+            return {"success": True, "fullClassName": full_class_name, "sourceFile": source_file,
+                    "result": root}
+        except Exception as e:
+            return {"success": False, "fullClassName": full_class_name, "sourceFile": source_file,
+                    "errorMessage": str(e)}
+
+
+def create_backend(cfg) -> EnrichmentBackend:
+    """Backend selection from :class:`dmcp.config.Config`."""
+    kind = cfg.resolved_enrich_backend()
+    if kind == "anthropic":
+        return AnthropicBackend(cfg.anthropic_api_key or "", cfg.claude_model, cfg.claude_max_tokens,
+                                cfg.claude_timeout_seconds, cfg.claude_max_retries,
+                                cfg.enrich_max_concurrent, cfg.anthropic_base_url,
+                                cfg.enrich_max_source_chars)
+    if kind == "fake":
+        return FakeBackend(cfg.enrich_max_concurrent)
+    if kind == "local":
+        from .local import LocalLLMBackend
+        return LocalLLMBackend.from_config(cfg)
+    return NullBackend(1)

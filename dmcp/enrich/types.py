@@ -1,0 +1,51 @@
+"""Enrichment DTOs (``ClaudeApiClient.java:453-513``)."""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+
+@dataclass(frozen=True)
+class EnrichmentInput:
+    source_code: str
+    full_class_name: str
+    language: str
+    class_type: str
+    method_names: List[str] = field(default_factory=list)
+
+
+@dataclass(frozen=True)
+class MethodEnrichment:
+    method_name: str
+    description: str
+    business_logic: List[str] = field(default_factory=list)
+
+
+@dataclass(frozen=True)
+class EnrichmentResult:
+    success: bool
+    full_class_name: str
+    description: Optional[str] = None
+    class_type_correction: Optional[str] = None
+    methods: List[MethodEnrichment] = field(default_factory=list)
+    error_message: Optional[str] = None
+
+    @classmethod
+    def ok(cls, full_class_name: str, description: str, class_type_correction: Optional[str],
+           methods: List[MethodEnrichment]) -> "EnrichmentResult":
+        return cls(True, full_class_name, description, class_type_correction, list(methods), None)
+
+    @classmethod
+    def failure(cls, full_class_name: str, error_message: Optional[str]) -> "EnrichmentResult":
+        return cls(False, full_class_name, None, None, [], error_message)
+
+
+def normalize_method_name(name: Optional[str]) -> Optional[str]:
+    """Strips an LLM-added parenthetical qualifier: ``"onSuccess (loginMutation)"``
+    -> ``"onSuccess"`` (CodeContextService.java:713-722)."""
+    if name is None:
+        return None
+    i = name.find("(")
+    if i > 0:
+        return name[:i].strip()
+    return name.strip()

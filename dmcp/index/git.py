@@ -1,0 +1,148 @@
+"""Git access through the ``git`` CLI (the reference uses JGit).
+
+Parity: clone (``CodeContextService.java:1653-1683`` shallow ``depth=1`` of the
+branch; ``ProjectSyncService.java:754-777`` full clone for diffing), HEAD hash,
+and diff classification (``ProjectSyncService.java:497-542``: ADD/MODIFY/COPY
+-> changed, DELETE -> deleted, RENAME -> both; missing old commit or no
+previous hash -> full resync).  ``git.ssh-key-path`` and
+``git.timeout-seconds`` -- declared but unused in the reference -- are honoured
+here (``GIT_SSH_COMMAND`` and a per-command timeout).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import shutil
+import subprocess
+import time
+from dataclasses import dataclass
+from typing import List, Optional, Tuple
+
+from ..models.domain import GitDiffResult, RepositoryUrl
+
+LOG = logging.getLogger(__name__)
+
+
+class GitError(RuntimeError):
+    pass
+
+
+@dataclass
+class CloneResult:
+    directory: str
+    commit_hash: str
+
+
+class GitClient:
+    def __init__(self, clone_base_path: str = "/tmp/domain-mcp-repos",
+                 ssh_key_path: Optional[str] = None, timeout_seconds: int = 300) -> None:
+        self.clone_base_path = clone_base_path
+        self.ssh_key_path = ssh_key_path
+        self.timeout = timeout_seconds
+
+    def _env(self) -> dict:
+        env = dict(os.environ)
+        env["GIT_TERMINAL_PROMPT"] = "0"
+        if self.ssh_key_path:
+            env["GIT_SSH_COMMAND"] = (f"ssh -i {self.ssh_key_path} -o IdentitiesOnly=yes "
+                                      "-o StrictHostKeyChecking=accept-new")
+        return env
+
+    def _git(self, args: List[str], cwd: Optional[str] = None, check: bool = True) -> Tuple[int, str, str]:
+        try:
+            r = subprocess.run(["git", *args], cwd=cwd, env=self._env(), stdout=subprocess.PIPE,
+                               stderr=subprocess.PIPE, text=True, timeout=self.timeout)
+        except subprocess.TimeoutExpired as e:
+            raise GitError(f"git {' '.join(args[:2])} timed out after {self.timeout}s") from e
+        if check and r.returncode != 0:
+            raise GitError(f"git {' '.join(args[:2])} failed: {r.stderr.strip() or r.stdout.strip()}")
+        return r.returncode, r.stdout, r.stderr
+
+    @staticmethod
+    def _source(url: RepositoryUrl) -> str:
+        local = url.local_path()
+        if local is not None:
+            return "file://" + os.path.abspath(local)  # file:// so --depth is honoured
+        return url.value
+
+    def new_clone_dir(self, name: str, suffix: str = "") -> str:
+        os.makedirs(self.clone_base_path, exist_ok=True)
+        return os.path.join(self.clone_base_path, f"{name}{suffix}-{int(time.time() * 1000)}")
+
+    def clone(self, url: RepositoryUrl, branch: Optional[str], shallow: bool = True,
+              directory: Optional[str] = None) -> CloneResult:
+        dest = directory or self.new_clone_dir(url.repository_name())
+        os.makedirs(os.path.dirname(dest) or ".", exist_ok=True)
+        args = ["clone", "--quiet", "--no-tags"]
+        if shallow:
+            args += ["--depth", "1", "--single-branch"]
+        if branch:
+            args += ["--branch", branch]
+        args += [self._source(url), dest]
+        LOG.info("Cloning %s (branch: %s) to %s", url, branch, dest)
+        try:
+            self._git(args)
+        except GitError as e:
+            shutil.rmtree(dest, ignore_errors=True)
+            raise GitError(f"Failed to clone repository: {e}") from e
+        return CloneResult(dest, self.head(dest))
+
+    def head(self, repo_dir: str) -> str:
+        return self._git(["rev-parse", "HEAD"], cwd=repo_dir)[1].strip()
+
+    def commit_exists(self, repo_dir: str, commit: str) -> bool:
+        rc, _, _ = self._git(["cat-file", "-e", f"{commit}^{{commit}}"], cwd=repo_dir, check=False)
+        return rc == 0
+
+    def diff(self, repo_dir: str, old_commit: Optional[str], new_commit: str) -> GitDiffResult:
+        if not old_commit or not old_commit.strip():
+            LOG.info("No previous commit hash, treating as full resync")
+            return GitDiffResult.full_resync(new_commit)
+        if not self.commit_exists(repo_dir, old_commit):
+            LOG.warning("Old commit %s not found (force push?), treating as full resync", old_commit)
+            return GitDiffResult.full_resync(new_commit)
+        out = self._git(["diff", "--name-status", "-M", "-C", "--no-color", old_commit, new_commit],
+                        cwd=repo_dir)[1]
+        return parse_name_status(out, new_commit)
+
+    @staticmethod
+    def cleanup(directory: Optional[str]) -> None:
+        if directory and os.path.isdir(directory):
+            shutil.rmtree(directory, ignore_errors=True)
+
+
+def parse_name_status(text: str, new_commit: str) -> GitDiffResult:
+    changed, deleted = set(), set()
+    for line in text.splitlines():
+        if not line.strip():
+            continue
+        parts = line.split("\t")
+        status = parts[0][:1]
+        if status in ("A", "M", "T") and len(parts) >= 2:
+            changed.add(parts[1])
+        elif status == "D" and len(parts) >= 2:
+            deleted.add(parts[1])
+        elif status == "R" and len(parts) >= 3:
+            deleted.add(parts[1])
+            changed.add(parts[2])
+        elif status == "C" and len(parts) >= 3:
+            changed.add(parts[2])
+    return GitDiffResult.of(new_commit, changed, deleted)
+
+
+def read_readme(repo_dir: str, max_length: int = 10_000) -> Optional[str]:
+    """README.md, truncated to ``max_length`` + marker (CodeContextService.java:1688-1712)."""
+    path = os.path.join(repo_dir, "README.md")
+    if not os.path.isfile(path):
+        return None
+    try:
+        with open(path, "r", encoding="utf-8", errors="replace") as f:
+            content = f.read()
+    except OSError as e:
+        LOG.warning("Failed to read README.md: %s", e)
+        return None
+    if not content.strip():
+        return None
+    if len(content) > max_length:
+        return content[:max_length] + "\n...(truncated)"
+    return content

@@ -1,0 +1,725 @@
+"""Indexing pipeline: analyze, rebuild-graph, incremental sync, resume.
+
+Parity:
+
+* :meth:`Indexer.analyze_project` -- ``CodeContextService.analyzeProject``
+  (``:146-469``): READ_ONLY_MODE guard, RepositoryUrl validation, project
+  create/reuse, shallow clone, README -> description (first 500 chars),
+  parser detection, graph build, **Phase 1** static persist (classes, methods,
+  parameter links), **Phase 2** enrichment in batches of 20 with at most 5
+  concurrent calls, **Phase 3** recovery of ``description IS NULL`` classes
+  when ``fixMissed``, graph JSON persisted, cache updated, endpoint count.
+* :meth:`Indexer.rebuild_graph` -- ``CodeContextService.rebuildGraph`` (``:492-609``).
+* :meth:`Indexer.sync_project` / :meth:`sync_all_projects` --
+  ``ProjectSyncService`` (``:140-486``, ``:919-965``).
+* :meth:`Indexer.apply_enrichment` -- ``CodeContextService.applyEnrichment`` (``:621-700``).
+
+Fixes of documented reference defects:
+
+* old data is replaced inside **one transaction after** clone+parse succeed
+  (the reference deletes first, ``:745``, so a failed re-analysis lost data);
+* sync has the Go branch (``ProjectSyncService.java:782-790`` lacked it);
+* sync / rebuild graphs carry node + method metadata from the database, so
+  ``graph_query`` no longer loses class types and descriptions after a sync;
+* a project stuck in ANALYZING/SYNCING by a dead process is recovered to
+  ERROR instead of being permanently wedged; per-project locks serialize
+  analyze/sync of the same project inside this process;
+* each phase runs in an explicit transaction (the reference's
+  ``@Transactional`` on self-invoked methods never applied).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+from ..enrich.backend import EnrichmentBackend, NullBackend
+from ..enrich.types import EnrichmentInput, EnrichmentResult, normalize_method_name
+from ..graph.cache import GraphCache
+from ..graph.project_graph import MethodEnrichmentData, MethodInfo, ProjectGraph
+from ..models.domain import (ClassType, Project, ProjectStatus, RepositoryUrl, SourceClass,
+                             new_id, package_name_of, simple_name_of, utc_now)
+from ..parsers.base import ParsedProject, ParsedUnit, SourceParser, detect_parser
+from ..store.repositories import Repositories, to_iso
+from ..utils.errors import DomainError
+from ..utils.tracing import METRICS, span
+from .git import CloneResult, GitClient, read_readme
+
+LOG = logging.getLogger(__name__)
+
+
+@dataclass
+class AnalysisResult:
+    success: bool
+    project_id: Optional[str]
+    classes_analyzed: int
+    endpoints_found: int
+    message: str
+    stats: Dict[str, float] = field(default_factory=dict)
+
+    def to_dict(self) -> dict:
+        return {"success": self.success, "projectId": self.project_id,
+                "classesAnalyzed": self.classes_analyzed, "endpointsFound": self.endpoints_found,
+                "message": self.message}
+
+
+@dataclass
+class SyncResult:
+    success: bool
+    project_name: str
+    commit_hash: Optional[str] = None
+    added_classes: int = 0
+    updated_classes: int = 0
+    deleted_classes: int = 0
+    unchanged_classes: int = 0
+    enriched_classes: int = 0
+    enrich_failed_classes: int = 0
+    error_message: Optional[str] = None
+
+    @classmethod
+    def no_changes(cls, name: str) -> "SyncResult":
+        return cls(True, name)
+
+    @classmethod
+    def failure(cls, name: str, msg: str) -> "SyncResult":
+        return cls(False, name, error_message=msg)
+
+    def to_dict(self) -> dict:
+        return {"success": self.success, "projectName": self.project_name, "commitHash": self.commit_hash,
+                "addedClasses": self.added_classes, "updatedClasses": self.updated_classes,
+                "deletedClasses": self.deleted_classes, "unchangedClasses": self.unchanged_classes,
+                "enrichedClasses": self.enriched_classes, "enrichFailedClasses": self.enrich_failed_classes,
+                "errorMessage": self.error_message}
+
+
+@dataclass
+class SyncAllResult:
+    success: bool
+    total_projects: int
+    success_count: int
+    failure_count: int
+    results: List[SyncResult]
+
+
+def common_package_prefix(packages: Iterable[Optional[str]]) -> Optional[str]:
+    """Longest common dotted prefix (CodeContextService.java:1752-1791)."""
+    prefix: Optional[List[str]] = None
+    seen_any = False
+    for p in packages:
+        if p is None:
+            continue
+        seen_any = True
+        parts = p.split(".")
+        if prefix is None:
+            prefix = parts
+            continue
+        n = 0
+        for a, b in zip(prefix, parts):
+            if a != b:
+                break
+            n += 1
+        prefix = prefix[:n]
+    if not seen_any:
+        return None
+    return ".".join(prefix or [])
+
+
+class _ProjectLocks:
+    def __init__(self) -> None:
+        self._locks: Dict[str, threading.Lock] = {}
+        self._guard = threading.Lock()
+
+    def get(self, key: str) -> threading.Lock:
+        with self._guard:
+            lk = self._locks.get(key)
+            if lk is None:
+                lk = self._locks[key] = threading.Lock()
+            return lk
+
+
+class Indexer:
+    def __init__(self, repos: Repositories, cache: GraphCache, git: GitClient,
+                 backend: Optional[EnrichmentBackend] = None, *, batch_size: int = 20,
+                 max_readme_length: int = 10_000, description_length: int = 500,
+                 parser_threads: int = 0, require_enrichment: bool = True,
+                 max_source_chars: int = 200_000) -> None:
+        self.repos = repos
+        self.cache = cache
+        self.git = git
+        self.backend = backend or NullBackend(1)
+        self.batch_size = max(1, int(batch_size))
+        self.max_readme_length = max_readme_length
+        self.description_length = description_length
+        self.parser_threads = parser_threads
+        self.require_enrichment = require_enrichment
+        self.max_source_chars = max_source_chars
+        self._locks = _ProjectLocks()
+
+    # ================================================================ analyze
+    def analyze_project(self, repository_url: str, branch: Optional[str] = None,
+                        fix_missed: bool = True) -> AnalysisResult:
+        if self.require_enrichment and not self.backend.enabled:
+            LOG.error("Cannot run analysis in read-only mode. ANTHROPIC_API_KEY is not configured.")
+            raise DomainError("Cannot run analysis in read-only mode. ANTHROPIC_API_KEY is not configured.",
+                              "READ_ONLY_MODE")
+        url = RepositoryUrl.of(repository_url)
+        branch_name = branch if branch is not None else "main"
+        lock = self._locks.get(url.value)
+        if not lock.acquire(blocking=False):
+            raise DomainError(f"Project {url.repository_name()} is already being processed",
+                              "PROJECT_BUSY")
+        stats: Dict[str, float] = {}
+        clone: Optional[CloneResult] = None
+        project = self._prepare_project(url, branch_name)
+        try:
+            with span("analyze.total", stats, project=project.name):
+                with span("analyze.clone", stats):
+                    clone = self.git.clone(url, branch_name, shallow=True)
+                readme = read_readme(clone.directory, self.max_readme_length)
+                if readme is not None:
+                    project.update_description(readme[:self.description_length])
+                parser = detect_parser(clone.directory, self.parser_threads)
+                with span("analyze.parse", stats):
+                    parsed = parser.scan(clone.directory)
+                    graph = parsed.build_graph()
+                LOG.info("Graph built: %d nodes, %d entry points", graph.node_count(), graph.entry_point_count())
+                order = graph.analysis_order()
+                with span("analyze.phase1", stats):
+                    p1 = self._phase1_static(project, parsed, graph, order, clone.commit_hash, replace=True)
+                classes, methods_by_ident = p1
+                enriched = failed = recovered = 0
+                if self.backend.enabled:
+                    with span("analyze.phase2", stats):
+                        enriched, failed = self._enrich_identifiers(order, parsed, graph, clone.directory,
+                                                                    readme, methods_by_ident)
+                    if fix_missed:
+                        with span("analyze.phase3", stats):
+                            recovered = self._recover_unenriched(project, parsed, graph, clone.directory, readme)
+                with span("analyze.persist_graph", stats):
+                    project.base_package = common_package_prefix(package_name_of(i) for i in parsed.units)
+                    project.update_graph_data(graph.to_json())
+                    project.analysis_completed(clone.commit_hash)
+                    self.repos.projects.update(project)
+                    self.cache.put(project.id, project.name, graph)
+                endpoints = self.repos.methods.count_endpoints_by_project_id(project.id)
+            METRICS.inc("classes_indexed", classes)
+            LOG.info("Analysis completed. Classes: %d, Endpoints: %d, Enriched: %d, Enrich failed: %d, "
+                     "Recovered: %d, timings(ms): %s", classes, endpoints, enriched, failed, recovered,
+                     {k: round(v, 1) for k, v in stats.items()})
+            stats.update({"classes": classes, "enriched": enriched, "enrichFailed": failed,
+                          "recovered": recovered})
+            return AnalysisResult(True, project.id, classes, endpoints, "Analysis complete", stats)
+        except Exception as e:
+            LOG.error("Analysis failed for %s: %s", repository_url, e, exc_info=True)
+            self._mark_error(project)
+            raise DomainError(f"Analysis failed: {e}", "ANALYSIS_FAILED", e) from e
+        finally:
+            if clone is not None:
+                self.git.cleanup(clone.directory)
+            lock.release()
+
+    def analyze_local(self, path: str, fix_missed: bool = True) -> AnalysisResult:
+        """Analyzes a local git working tree (``file://`` clone of HEAD)."""
+        return self.analyze_project(os.path.abspath(path), branch=None, fix_missed=fix_missed)
+
+    def _prepare_project(self, url: RepositoryUrl, branch: str) -> Project:
+        project = self.repos.projects.find_by_repository_url(url)
+        if project is None:
+            project = Project.create(url.repository_name(), url, branch)
+            self.repos.projects.save(project)
+            LOG.info("Created new project: %s", project.id)
+        else:
+            if project.status.is_processing():
+                LOG.warning("Project %s was left in %s by a previous process; recovering",
+                            project.name, project.status.value)
+                project.mark_error()
+            project.default_branch = branch
+        project.start_analysis()
+        self.repos.projects.update_status(project)
+        return project
+
+    def _mark_error(self, project: Project) -> None:
+        try:
+            project.mark_error()
+            self.repos.projects.update_status(project)
+        except Exception as e:  # never mask the original failure
+            LOG.warning("Could not mark project %s as ERROR: %s", project.id, e)
+
+    # ---------------------------------------------------------------- phase 1
+    def _phase1_static(self, project: Project, parsed: ParsedProject, graph: ProjectGraph,
+                       order: Sequence[str], commit_hash: str, replace: bool
+                       ) -> Tuple[int, Dict[str, List[Tuple[str, str]]]]:
+        """Builds every class / method / parameter row and the graph metadata,
+        then swaps them in with one transaction (old rows deleted in it)."""
+        now = to_iso(utc_now())
+        pid = project.id
+        cls_rows: List[tuple] = []
+        meth_rows: List[tuple] = []
+        param_rows: List[tuple] = []
+        methods_by_ident: Dict[str, List[Tuple[str, str]]] = {}
+        units = parsed.units
+        class_ids: Dict[str, str] = {}
+        for ident in order:
+            unit = units.get(ident)
+            if unit is None:
+                continue
+            cid = new_id()
+            class_ids[ident] = cid
+            ct = unit.class_type.value
+            i = ident.rfind(".")
+            cls_rows.append((cid, pid, ident, ident[i + 1:] if i >= 0 else ident,
+                             ident[:i] if i >= 0 else None, ct, None, unit.source_file, now, commit_hash))
+            graph.set_node_info(ident, ct, None)
+            infos = []
+            mids = []
+            for sm in unit.methods:
+                mid = new_id()
+                exc = sm.exceptions
+                meth_rows.append((mid, cid, sm.method_name, None, "[]",
+                                  json.dumps(list(exc)) if exc else "[]", sm.http_method, sm.http_path,
+                                  sm.line_number, now))
+                infos.append(MethodInfo(sm.method_name, None, (), tuple(exc), sm.http_method,
+                                        sm.http_path, sm.line_number))
+                mids.append((sm.method_name, mid))
+            graph.set_method_infos(ident, infos)
+            methods_by_ident[ident] = mids
+        for ident, cid in class_ids.items():
+            graph.bind_class_id(ident, cid)
+        # second pass: parameter links (CodeContextService.java:274-291, 805-856)
+        for ident, mids in methods_by_ident.items():
+            params = units[ident].params
+            if not params or not mids:
+                continue
+            linked = set()
+            for mname, mid in mids:
+                targets = params.get(mname)
+                if not targets:
+                    continue
+                if mname not in linked:
+                    linked.add(mname)
+                    for pos, tgt in enumerate(targets):
+                        graph.add_method_parameter(ident, mname, pos, tgt)
+                for pos, tgt in enumerate(targets):
+                    tcid = class_ids.get(tgt)
+                    if tcid is not None:
+                        param_rows.append((new_id(), mid, pos, tcid, now))
+        with self.repos.db.transaction():
+            if replace:
+                self.repos.classes.delete_by_project_id(pid)
+            self.repos.classes.save_rows(cls_rows)
+            self.repos.methods.save_rows(meth_rows)
+            self.repos.params.save_rows(param_rows)
+        LOG.info("Phase 1 complete. Classes: %d, Methods: %d, Parameters: %d",
+                 len(cls_rows), len(meth_rows), len(param_rows))
+        return len(cls_rows), methods_by_ident
+
+    # ------------------------------------------------------------ enrichment
+    def _read_source(self, clone_dir: str, unit: ParsedUnit) -> Optional[str]:
+        parts = []
+        total = 0
+        for rel in (unit.files if len(unit.files) > 1 else [unit.source_file]):
+            path = os.path.join(clone_dir, rel)
+            try:
+                with open(path, "r", encoding="utf-8", errors="replace") as f:
+                    text = f.read()
+            except OSError as e:
+                LOG.warning("Failed to read source for enrichment %s: %s", rel, e)
+                continue
+            if len(unit.files) > 1:
+                text = f"// file: {rel}\n{text}"
+            parts.append(text)
+            total += len(text)
+            if self.max_source_chars and total >= self.max_source_chars:
+                break
+        return "\n".join(parts) if parts else None
+
+    def _inputs_for(self, idents: Sequence[str], parsed: ParsedProject, clone_dir: str,
+                    class_types: Optional[Dict[str, str]] = None) -> Tuple[List[EnrichmentInput], int]:
+        inputs, failed = [], 0
+        for ident in idents:
+            unit = parsed.units.get(ident)
+            if unit is None:
+                continue
+            src = self._read_source(clone_dir, unit)
+            if src is None:
+                failed += 1
+                continue
+            ct = (class_types or {}).get(ident, unit.class_type.value)
+            inputs.append(EnrichmentInput(src, ident, parsed.language, ct,
+                                          [m.method_name for m in unit.methods]))
+        return inputs, failed
+
+    def _enrich_identifiers(self, idents: Sequence[str], parsed: ParsedProject, graph: ProjectGraph,
+                            clone_dir: str, readme: Optional[str],
+                            methods_by_ident: Optional[Dict[str, List[Tuple[str, str]]]] = None
+                            ) -> Tuple[int, int]:
+        enriched = failed = 0
+        idents = list(idents)
+        nbatches = (len(idents) + self.batch_size - 1) // self.batch_size
+        for b in range(0, len(idents), self.batch_size):
+            batch = idents[b:b + self.batch_size]
+            LOG.info("Enriching batch %d/%d (%d classes)", b // self.batch_size + 1, nbatches, len(batch))
+            inputs, read_failed = self._inputs_for(batch, parsed, clone_dir)
+            failed += read_failed
+            for result in self.backend.enrich_batch(inputs, readme):
+                if not result.success:
+                    LOG.warning("Enrichment failed for %s: %s", result.full_class_name, result.error_message)
+                    failed += 1
+                    continue
+                self.apply_enrichment(result, graph, methods_by_ident)
+                enriched += 1
+        METRICS.inc("classes_enriched", enriched)
+        METRICS.inc("classes_enrich_failed", failed)
+        return enriched, failed
+
+    def _recover_unenriched(self, project: Project, parsed: ParsedProject, graph: ProjectGraph,
+                            clone_dir: str, readme: Optional[str]) -> int:
+        unenriched = self.repos.classes.find_unenriched_by_project_id(project.id)
+        if not unenriched:
+            LOG.info("Phase 3: No unenriched classes found, skipping recovery")
+            return 0
+        LOG.info("Phase 3: Found %d classes with missing enrichment, retrying", len(unenriched))
+        recovered = 0
+        types = {sc.full_class_name: sc.class_type.value for sc in unenriched}
+        idents = [sc.full_class_name for sc in unenriched]
+        for b in range(0, len(idents), self.batch_size):
+            inputs, _ = self._inputs_for(idents[b:b + self.batch_size], parsed, clone_dir, types)
+            if not inputs:
+                continue
+            for result in self.backend.enrich_batch(inputs, readme):
+                if result.success:
+                    self.apply_enrichment(result, graph)
+                    recovered += 1
+                else:
+                    LOG.warning("Phase 3: Recovery failed for %s: %s", result.full_class_name,
+                                result.error_message)
+        LOG.info("Phase 3 complete. Recovered: %d/%d", recovered, len(unenriched))
+        return recovered
+
+    def apply_enrichment(self, result: EnrichmentResult, graph: ProjectGraph,
+                         methods_by_ident: Optional[Dict[str, List[Tuple[str, str]]]] = None) -> bool:
+        """Writes one class's enrichment to the DB and the (unpublished) graph."""
+        fqcn = result.full_class_name
+        class_id = graph.class_id(fqcn)
+        if class_id is None:
+            LOG.warning("No classId found for %s during enrichment", fqcn)
+            return False
+        correction: Optional[ClassType] = None
+        c = result.class_type_correction
+        if c is not None and c.strip() and c.strip().lower() != "null":
+            name = c.strip().upper()
+            if name in ClassType.__members__:
+                correction = ClassType[name]
+        # method name -> first method id (by extraction order == line order)
+        if methods_by_ident is not None and fqcn in methods_by_ident:
+            name_to_id: Dict[str, str] = {}
+            for mname, mid in methods_by_ident[fqcn]:
+                name_to_id.setdefault(mname, mid)
+        else:
+            name_to_id = {}
+            for m in self.repos.methods.find_by_class_id(class_id):
+                name_to_id.setdefault(m.method_name, m.id)
+        updates = []
+        enrichments: Dict[str, MethodEnrichmentData] = {}
+        for me in result.methods:
+            mname = normalize_method_name(me.method_name)
+            mid = name_to_id.get(mname)
+            if mid is None:
+                LOG.debug("Method %s not found for enrichment in class %s", mname, fqcn)
+                continue
+            updates.append((me.description, list(me.business_logic), mid))
+            enrichments[mname] = MethodEnrichmentData(me.description, tuple(me.business_logic))
+        with self.repos.db.transaction() as conn:
+            if correction is not None:
+                conn.execute("UPDATE source_classes SET class_type = ?, description = ? WHERE id = ?",
+                             (correction.value, result.description, class_id))
+            else:
+                conn.execute("UPDATE source_classes SET description = ? WHERE id = ?",
+                             (result.description, class_id))
+            self.repos.methods.update_enrichment_batch(updates)
+        if correction is not None:
+            resolved = correction.value
+        else:
+            ni = graph.node_info(fqcn)
+            resolved = ni.class_type if ni is not None and ni.class_type else "OTHER"
+        if not graph.frozen:
+            graph.apply_enrichment(fqcn, resolved, result.description, enrichments)
+        return True
+
+    # ================================================================ rebuild
+    def rebuild_graph(self, project_id: str) -> dict:
+        project = self.repos.projects.find_by_id(project_id)
+        if project is None:
+            raise DomainError(f"Project not found: {project_id}", "PROJECT_NOT_FOUND")
+        lock = self._locks.get(project.repository_url.value)
+        if not lock.acquire(blocking=False):
+            raise DomainError(f"Project {project.name} is already being processed", "PROJECT_BUSY")
+        clone = None
+        stats: Dict[str, float] = {}
+        try:
+            with span("rebuild.total", stats, project=project.name):
+                clone = self.git.clone(project.repository_url, project.default_branch, shallow=True)
+                parser = detect_parser(clone.directory, self.parser_threads)
+                parsed = parser.scan(clone.directory)
+                graph = parsed.build_graph()
+                existing = self.repos.classes.find_by_project_id(project_id)
+                by_name = {sc.full_class_name: sc for sc in existing}
+                bound = 0
+                for ident in graph.identifiers():
+                    sc = by_name.get(ident)
+                    if sc is not None:
+                        graph.bind_class_id(ident, sc.id)
+                        bound += 1
+                LOG.info("Rebuild: bound %d/%d identifiers", bound, graph.node_count())
+                missing_hash = [sc.id for sc in existing if sc.commit_hash is None]
+                self.repos.classes.update_commit_hash_batch(missing_hash, clone.commit_hash)
+                methods_by_class = self.repos.methods.find_by_class_ids([sc.id for sc in existing])
+                self._attach_metadata(graph, parsed, by_name, methods_by_class)
+                param_rows = self._param_rows(graph, parsed, by_name, methods_by_class)
+                with self.repos.db.transaction():
+                    self.repos.params.delete_by_project_id(project_id)
+                    self.repos.params.save_rows(param_rows)
+                project.update_graph_data(graph.to_json())
+                project.base_package = common_package_prefix(package_name_of(i) for i in parsed.units)
+                self.repos.projects.update(project)
+                self.cache.put(project_id, project.name, graph)
+            return {"success": True, "projectId": project_id, "bound": bound,
+                    "parameters": len(param_rows), "stats": stats}
+        except DomainError:
+            raise
+        except Exception as e:
+            LOG.error("Graph rebuild failed for %s: %s", project_id, e, exc_info=True)
+            raise DomainError(f"Graph rebuild failed: {e}", "REBUILD_FAILED", e) from e
+        finally:
+            if clone is not None:
+                self.git.cleanup(clone.directory)
+            lock.release()
+
+    def _attach_metadata(self, graph: ProjectGraph, parsed: ParsedProject, by_name: Dict[str, SourceClass],
+                         methods_by_class: Dict[str, list]) -> None:
+        """Node/method metadata for a freshly parsed graph: persisted enrichment
+        where a row exists, static facts otherwise (fixes SURVEY §3.5)."""
+        for ident, unit in parsed.units.items():
+            sc = by_name.get(ident)
+            if sc is not None:
+                graph.set_node_info(ident, sc.class_type.value, sc.description)
+                rows = methods_by_class.get(sc.id) or []
+                graph.set_method_infos(ident, [
+                    MethodInfo(m.method_name, m.description, tuple(m.business_logic), tuple(m.exceptions),
+                               m.http_method, m.http_path, m.line_number) for m in rows])
+            else:
+                graph.set_node_info(ident, unit.class_type.value, None)
+                graph.set_method_infos(ident, [
+                    MethodInfo(sm.method_name, None, (), tuple(sm.exceptions), sm.http_method, sm.http_path,
+                               sm.line_number) for sm in unit.methods])
+
+    def _param_rows(self, graph: ProjectGraph, parsed: ParsedProject, by_name: Dict[str, SourceClass],
+                    methods_by_class: Dict[str, list], only: Optional[Iterable[str]] = None) -> List[tuple]:
+        now = to_iso(utc_now())
+        rows: List[tuple] = []
+        idents = list(only) if only is not None else list(parsed.units)
+        for ident in idents:
+            unit = parsed.units.get(ident)
+            sc = by_name.get(ident)
+            if unit is None or sc is None or not unit.params:
+                continue
+            graph.clear_method_parameters(ident)
+            linked = set()
+            for m in methods_by_class.get(sc.id) or []:
+                targets = unit.params.get(m.method_name)
+                if not targets:
+                    continue
+                if m.method_name not in linked:
+                    linked.add(m.method_name)
+                    for pos, tgt in enumerate(targets):
+                        graph.add_method_parameter(ident, m.method_name, pos, tgt)
+                for pos, tgt in enumerate(targets):
+                    tcid = graph.class_id(tgt)
+                    if tcid is not None:
+                        rows.append((new_id(), m.id, pos, tcid, now))
+        return rows
+
+    # =================================================================== sync
+    def sync_project(self, project: Project) -> SyncResult:
+        lock = self._locks.get(project.repository_url.value)
+        if not lock.acquire(blocking=False):
+            return SyncResult.failure(project.name, "project is already being processed")
+        clone = None
+        stats: Dict[str, float] = {}
+        try:
+            if project.status.is_processing():
+                project.mark_error()  # stale status from a dead process
+            project.start_sync()
+            self.repos.projects.update_status(project)
+            with span("sync.total", stats, project=project.name):
+                clone = self.git.clone(project.repository_url, project.default_branch, shallow=False,
+                                       directory=self.git.new_clone_dir(project.name, "-sync"))
+                head = clone.commit_hash
+                if head == project.last_commit_hash:
+                    LOG.info("No changes detected for project: %s (HEAD: %s)", project.name, head)
+                    project.sync_completed(project.last_commit_hash)
+                    self.repos.projects.update_status(project)
+                    return SyncResult.no_changes(project.name)
+                diff = self.git.diff(clone.directory, project.last_commit_hash, head)
+                readme = read_readme(clone.directory, self.max_readme_length)
+                if readme is not None:
+                    project.update_description(readme[:self.description_length])
+                parser = detect_parser(clone.directory, self.parser_threads)
+                parsed = parser.scan(clone.directory)
+                graph = parsed.build_graph()
+                existing = self.repos.classes.find_by_project_id(project.id)
+                by_name = {sc.full_class_name: sc for sc in existing}
+                new_ids = parsed.units
+                to_delete = [n for n in by_name if n not in new_ids]
+                to_add, to_update, unchanged = [], [], []
+                for ident, unit in new_ids.items():
+                    if ident not in by_name:
+                        to_add.append(ident)
+                    elif diff.full_resync_required or any(f in diff.changed_files for f in unit.files):
+                        to_update.append(ident)
+                    else:
+                        unchanged.append(ident)
+                LOG.info("Changes for %s: add=%d, update=%d, delete=%d, unchanged=%d", project.name,
+                         len(to_add), len(to_update), len(to_delete), len(unchanged))
+                now = to_iso(utc_now())
+                cls_rows, meth_rows = [], []
+                methods_by_ident: Dict[str, List[Tuple[str, str]]] = {}
+                with self.repos.db.transaction() as conn:
+                    if to_delete:
+                        ids = [by_name[n].id for n in to_delete]
+                        self.repos.params.delete_by_class_ids(ids)
+                        self.repos.methods.delete_by_class_ids(ids)
+                        self.repos.classes.delete_by_ids(ids)
+                    for ident in to_update:
+                        sc = by_name[ident]
+                        unit = new_ids[ident]
+                        self.repos.params.delete_by_class_ids([sc.id])
+                        self.repos.methods.delete_by_class_id(sc.id)
+                        conn.execute("UPDATE source_classes SET commit_hash = ?, class_type = ?, source_file = ? "
+                                     "WHERE id = ?", (head, unit.class_type.value, unit.source_file, sc.id))
+                        graph.bind_class_id(ident, sc.id)
+                        mids = []
+                        for sm in unit.methods:
+                            mid = new_id()
+                            meth_rows.append((mid, sc.id, sm.method_name, None, "[]", json.dumps(list(sm.exceptions)),
+                                              sm.http_method, sm.http_path, sm.line_number, now))
+                            mids.append((sm.method_name, mid))
+                        methods_by_ident[ident] = mids
+                    for ident in to_add:
+                        unit = new_ids[ident]
+                        cid = new_id()
+                        cls_rows.append((cid, project.id, ident, simple_name_of(ident), package_name_of(ident),
+                                         unit.class_type.value, None, unit.source_file, now, head))
+                        graph.bind_class_id(ident, cid)
+                        mids = []
+                        for sm in unit.methods:
+                            mid = new_id()
+                            meth_rows.append((mid, cid, sm.method_name, None, "[]", json.dumps(list(sm.exceptions)),
+                                              sm.http_method, sm.http_path, sm.line_number, now))
+                            mids.append((sm.method_name, mid))
+                        methods_by_ident[ident] = mids
+                    for ident in unchanged:
+                        graph.bind_class_id(ident, by_name[ident].id)
+                    self.repos.classes.save_rows(cls_rows)
+                    self.repos.methods.save_rows(meth_rows)
+                # parameter links for changed classes; unchanged ones keep their rows
+                all_classes = {sc.full_class_name: sc for sc in self.repos.classes.find_by_project_id(project.id)}
+                changed = to_add + to_update
+                mb = self.repos.methods.find_by_class_ids([all_classes[i].id for i in changed if i in all_classes])
+                param_rows = self._param_rows(graph, parsed, all_classes, mb, only=changed)
+                self.repos.params.save_rows(param_rows)
+                # unchanged classes: rebuild their graph links from the parse as well
+                mb_un = self.repos.methods.find_by_class_ids([all_classes[i].id for i in unchanged if i in all_classes])
+                self._relink_graph_only(graph, parsed, all_classes, mb_un, unchanged)
+                enriched = failed = 0
+                if self.backend.enabled and changed:
+                    self._attach_metadata(graph, parsed, all_classes, {**mb_un, **mb})
+                    enriched, failed = self._enrich_identifiers(changed, parsed, graph, clone.directory, readme,
+                                                                methods_by_ident)
+                # final metadata from the DB (enrichment included)
+                final_classes = {sc.full_class_name: sc for sc in self.repos.classes.find_by_project_id(project.id)}
+                mb_all = self.repos.methods.find_by_class_ids([sc.id for sc in final_classes.values()])
+                self._attach_metadata(graph, parsed, final_classes, mb_all)
+                project.base_package = common_package_prefix(package_name_of(i) for i in parsed.units)
+                project.update_graph_data(graph.to_json())
+                project.sync_completed(head)
+                self.repos.projects.update(project)
+                self.cache.put(project.id, project.name, graph)
+            LOG.info("Sync completed for %s. Added: %d, Updated: %d, Deleted: %d, Unchanged: %d, Enriched: %d, "
+                     "EnrichFailed: %d", project.name, len(to_add), len(to_update), len(to_delete),
+                     len(unchanged), enriched, failed)
+            return SyncResult(True, project.name, head, len(to_add), len(to_update), len(to_delete),
+                              len(unchanged), enriched, failed, None)
+        except Exception as e:
+            LOG.error("Sync failed for %s: %s", project.name, e, exc_info=True)
+            self._mark_error(project)
+            return SyncResult.failure(project.name, str(e))
+        finally:
+            if clone is not None:
+                self.git.cleanup(clone.directory)
+            lock.release()
+
+    def _relink_graph_only(self, graph: ProjectGraph, parsed: ParsedProject, classes: Dict[str, SourceClass],
+                           methods_by_class: Dict[str, list], idents: Iterable[str]) -> None:
+        for ident in idents:
+            unit = parsed.units.get(ident)
+            sc = classes.get(ident)
+            if unit is None or sc is None or not unit.params:
+                continue
+            linked = set()
+            for m in methods_by_class.get(sc.id) or []:
+                targets = unit.params.get(m.method_name)
+                if targets and m.method_name not in linked:
+                    linked.add(m.method_name)
+                    for pos, tgt in enumerate(targets):
+                        graph.add_method_parameter(ident, m.method_name, pos, tgt)
+
+    def sync_all_projects(self) -> SyncAllResult:
+        projects = self.repos.projects.find_by_statuses([ProjectStatus.ANALYZED, ProjectStatus.ERROR])
+        if not projects:
+            LOG.info("No projects eligible for sync")
+            return SyncAllResult(True, 0, 0, 0, [])
+        results: List[SyncResult] = []
+        ok = bad = 0
+        for p in projects:
+            try:
+                r = self.sync_project(p)
+            except Exception as e:  # pragma: no cover - sync_project never raises
+                r = SyncResult.failure(p.name, str(e))
+            results.append(r)
+            if r.success:
+                ok += 1
+            else:
+                bad += 1
+        LOG.info("Sync complete. Success: %d, Failed: %d", ok, bad)
+        return SyncAllResult(bad == 0, len(projects), ok, bad, results)
+
+    # ================================================================= resume
+    def resume_enrichment(self, project_id: str) -> dict:
+        """Checkpoint/resume: re-enriches every ``description IS NULL`` class of an
+        analyzed project without re-running the static phase."""
+        project = self.repos.projects.find_by_id(project_id)
+        if project is None:
+            raise DomainError(f"Project not found: {project_id}", "PROJECT_NOT_FOUND")
+        if not self.backend.enabled:
+            raise DomainError("No enrichment backend configured", "READ_ONLY_MODE")
+        cached = self.cache.get_graph(project_id)
+        graph = cached.copy() if cached is not None else (
+            ProjectGraph.from_json(project.graph_data) if project.graph_data else None)
+        if graph is None:
+            raise DomainError("No graph data available for this project", "NO_GRAPH")
+        clone = self.git.clone(project.repository_url, project.default_branch, shallow=True)
+        try:
+            parsed = detect_parser(clone.directory, self.parser_threads).scan(clone.directory)
+            readme = read_readme(clone.directory, self.max_readme_length)
+            recovered = self._recover_unenriched(project, parsed, graph, clone.directory, readme)
+            project.update_graph_data(graph.to_json())
+            self.repos.projects.update(project)
+            self.cache.put(project.id, project.name, graph)
+            return {"success": True, "projectId": project_id, "recovered": recovered}
+        finally:
+            self.git.cleanup(clone.directory)

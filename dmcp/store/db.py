@@ -1,0 +1,270 @@
+"""SQLite database: connection management and versioned schema migrations.
+
+The reference persists to PostgreSQL through Flyway migrations V1..V8
+(``src/main/resources/db/migration``).  This store reproduces the *final*
+schema of those migrations (components #49-#53) on SQLite:
+
+* ``projects``          -- V1:13-27 + V5 ``description`` + V6 ``graph_data``
+* ``source_classes``    -- V1:149-165 + V8 ``commit_hash``; UNIQUE(project_id, full_class_name)
+* ``source_methods``    -- V1:168-184 minus V8's dropped ``dependencies``
+* ``method_parameters`` -- V7:6-19
+* every index of V1/V3/V4/V7 (SQLite partial index for the endpoint index).
+
+Additions (documented divergences): ``projects.base_package`` is stored at
+analysis time so ``list_projects`` no longer loads every class of every
+project (``CodeContextService.java:1752-1773``), and an ``updated_at`` trigger
+mirrors ``V1:187-199``.  The V1 tables that V2 dropped are never created.
+
+Concurrency: one connection per thread (WAL mode, ``foreign_keys=ON``,
+``busy_timeout``), and :meth:`Database.transaction` gives an explicit
+transaction per pipeline phase (the reference's ``@Transactional`` on
+self-invoked package-private methods never actually opened one).
+"""
+from __future__ import annotations
+
+import contextlib
+import logging
+import os
+import sqlite3
+import threading
+from typing import Iterator, List, Tuple
+
+LOG = logging.getLogger(__name__)
+
+MIGRATIONS: List[Tuple[int, str, str]] = [
+    (1, "initial_schema", """
+CREATE TABLE IF NOT EXISTS projects (
+    id               TEXT PRIMARY KEY,
+    name             TEXT NOT NULL,
+    repository_url   TEXT NOT NULL UNIQUE,
+    clone_location   TEXT,
+    default_branch   TEXT DEFAULT 'main',
+    status           TEXT NOT NULL DEFAULT 'PENDING',
+    last_analyzed_at TEXT,
+    last_commit_hash TEXT,
+    created_at       TEXT NOT NULL DEFAULT (strftime('%Y-%m-%dT%H:%M:%fZ','now')),
+    updated_at       TEXT NOT NULL DEFAULT (strftime('%Y-%m-%dT%H:%M:%fZ','now')),
+    description      TEXT,
+    graph_data       TEXT
+);
+CREATE INDEX IF NOT EXISTS idx_projects_status ON projects(status);
+CREATE INDEX IF NOT EXISTS idx_projects_name ON projects(name);
+
+CREATE TABLE IF NOT EXISTS source_classes (
+    id              TEXT PRIMARY KEY,
+    project_id      TEXT NOT NULL REFERENCES projects(id) ON DELETE CASCADE,
+    full_class_name TEXT NOT NULL,
+    simple_name     TEXT NOT NULL,
+    package_name    TEXT,
+    class_type      TEXT NOT NULL,
+    description     TEXT,
+    source_file     TEXT,
+    created_at      TEXT NOT NULL DEFAULT (strftime('%Y-%m-%dT%H:%M:%fZ','now')),
+    commit_hash     TEXT,
+    CONSTRAINT uq_source_classes_project_class UNIQUE(project_id, full_class_name)
+);
+CREATE INDEX IF NOT EXISTS idx_source_classes_full_name ON source_classes(full_class_name);
+CREATE INDEX IF NOT EXISTS idx_source_classes_package ON source_classes(package_name);
+CREATE INDEX IF NOT EXISTS idx_source_classes_simple_name ON source_classes(simple_name);
+CREATE INDEX IF NOT EXISTS idx_source_classes_type ON source_classes(class_type);
+CREATE INDEX IF NOT EXISTS idx_source_classes_project_package ON source_classes(project_id, package_name);
+
+CREATE TABLE IF NOT EXISTS source_methods (
+    id             TEXT PRIMARY KEY,
+    class_id       TEXT NOT NULL REFERENCES source_classes(id) ON DELETE CASCADE,
+    method_name    TEXT NOT NULL,
+    description    TEXT,
+    business_logic TEXT,
+    exceptions     TEXT,
+    http_method    TEXT,
+    http_path      TEXT,
+    line_number    INTEGER,
+    created_at     TEXT NOT NULL DEFAULT (strftime('%Y-%m-%dT%H:%M:%fZ','now'))
+);
+CREATE INDEX IF NOT EXISTS idx_source_methods_class ON source_methods(class_id);
+CREATE INDEX IF NOT EXISTS idx_source_methods_name ON source_methods(method_name);
+CREATE INDEX IF NOT EXISTS idx_source_methods_http_path ON source_methods(http_path);
+CREATE INDEX IF NOT EXISTS idx_source_methods_class_name ON source_methods(class_id, method_name);
+CREATE INDEX IF NOT EXISTS idx_source_methods_line ON source_methods(line_number)
+    WHERE line_number IS NOT NULL;
+CREATE INDEX IF NOT EXISTS idx_source_methods_http_endpoints
+    ON source_methods(class_id, http_path, http_method)
+    WHERE http_method IS NOT NULL AND http_path IS NOT NULL;
+
+CREATE TABLE IF NOT EXISTS method_parameters (
+    id         TEXT PRIMARY KEY,
+    method_id  TEXT NOT NULL REFERENCES source_methods(id) ON DELETE CASCADE,
+    position   INTEGER NOT NULL,
+    class_id   TEXT NOT NULL REFERENCES source_classes(id) ON DELETE CASCADE,
+    created_at TEXT NOT NULL DEFAULT (strftime('%Y-%m-%dT%H:%M:%fZ','now')),
+    CONSTRAINT uq_method_param_position UNIQUE(method_id, position)
+);
+CREATE INDEX IF NOT EXISTS idx_method_params_method ON method_parameters(method_id);
+CREATE INDEX IF NOT EXISTS idx_method_params_class ON method_parameters(class_id);
+"""),
+    (2, "optimize_query_indexes", """
+-- V4 equivalent: covering index for ORDER BY full_class_name per project;
+-- SQLite LIKE-prefix uses the plain package index (no text_pattern_ops).
+CREATE INDEX IF NOT EXISTS idx_source_classes_project_ordered
+    ON source_classes(project_id, full_class_name);
+DROP INDEX IF EXISTS idx_source_classes_project;
+CREATE TRIGGER IF NOT EXISTS update_projects_updated_at
+    AFTER UPDATE ON projects FOR EACH ROW
+    WHEN NEW.updated_at = OLD.updated_at
+BEGIN
+    UPDATE projects SET updated_at = strftime('%Y-%m-%dT%H:%M:%fZ','now') WHERE id = NEW.id;
+END;
+"""),
+    (3, "project_base_package", """
+ALTER TABLE projects ADD COLUMN base_package TEXT;
+"""),
+]
+
+
+class Database:
+    """Thread-local SQLite connections over one database file (or ``:memory:``)."""
+
+    def __init__(self, path: str = ":memory:") -> None:
+        self.path = path
+        self._local = threading.local()
+        self._write_lock = threading.RLock()
+        self._shared_memory_conn = None
+        if path == ":memory:":
+            # A private in-memory DB must be shared across threads via one connection.
+            self._shared_memory_conn = self._open()
+        else:
+            d = os.path.dirname(os.path.abspath(path))
+            os.makedirs(d, exist_ok=True)
+        self.migrate()
+
+    # ---------------------------------------------------------- connections
+    def _open(self) -> sqlite3.Connection:
+        conn = sqlite3.connect(self.path, check_same_thread=False, isolation_level=None,
+                               timeout=30.0)
+        conn.row_factory = sqlite3.Row
+        conn.execute("PRAGMA foreign_keys = ON")
+        if self.path != ":memory:":
+            conn.execute("PRAGMA journal_mode = WAL")
+            conn.execute("PRAGMA synchronous = NORMAL")
+        conn.execute("PRAGMA temp_store = MEMORY")
+        conn.execute("PRAGMA cache_size = -65536")
+        return conn
+
+    @property
+    def conn(self) -> sqlite3.Connection:
+        if self._shared_memory_conn is not None:
+            return self._shared_memory_conn
+        c = getattr(self._local, "conn", None)
+        if c is None:
+            c = self._open()
+            self._local.conn = c
+        return c
+
+    def close(self) -> None:
+        c = getattr(self._local, "conn", None)
+        if c is not None:
+            c.close()
+            self._local.conn = None
+        if self._shared_memory_conn is not None:
+            self._shared_memory_conn.close()
+            self._shared_memory_conn = None
+
+    # --------------------------------------------------------- transactions
+    @contextlib.contextmanager
+    def transaction(self) -> Iterator[sqlite3.Connection]:
+        """Explicit write transaction (re-entrant: nested calls join the outer one)."""
+        with self._write_lock:
+            conn = self.conn
+            depth = getattr(self._local, "tx_depth", 0)
+            if self._shared_memory_conn is not None:
+                depth = getattr(self, "_mem_tx_depth", 0)
+            if depth == 0:
+                conn.execute("BEGIN IMMEDIATE")
+            self._set_depth(depth + 1)
+            try:
+                yield conn
+            except BaseException:
+                self._set_depth(depth)
+                if depth == 0:
+                    conn.execute("ROLLBACK")
+                raise
+            else:
+                self._set_depth(depth)
+                if depth == 0:
+                    conn.execute("COMMIT")
+
+    def _set_depth(self, d: int) -> None:
+        if self._shared_memory_conn is not None:
+            self._mem_tx_depth = d
+        else:
+            self._local.tx_depth = d
+
+    def execute(self, sql: str, params=()) -> sqlite3.Cursor:
+        if self._shared_memory_conn is not None:
+            with self._write_lock:
+                return self.conn.execute(sql, params)
+        return self.conn.execute(sql, params)
+
+    def query(self, sql: str, params=()) -> List[sqlite3.Row]:
+        if self._shared_memory_conn is not None:
+            with self._write_lock:
+                return self.conn.execute(sql, params).fetchall()
+        return self.conn.execute(sql, params).fetchall()
+
+    def query_one(self, sql: str, params=()):
+        rows = self.query(sql, params)
+        return rows[0] if rows else None
+
+    # ------------------------------------------------------------ migration
+    def migrate(self) -> int:
+        with self._write_lock:
+            conn = self.conn
+            conn.execute("CREATE TABLE IF NOT EXISTS schema_version ("
+                         "version INTEGER PRIMARY KEY, description TEXT, "
+                         "installed_on TEXT DEFAULT (strftime('%Y-%m-%dT%H:%M:%fZ','now')))")
+            done = {r[0] for r in conn.execute("SELECT version FROM schema_version")}
+            applied = 0
+            for version, desc, sql in MIGRATIONS:
+                if version in done:
+                    continue
+                conn.execute("BEGIN IMMEDIATE")
+                try:
+                    for stmt in _split_sql(sql):
+                        conn.execute(stmt)
+                    conn.execute("INSERT INTO schema_version(version, description) VALUES (?, ?)",
+                                 (version, desc))
+                    conn.execute("COMMIT")
+                except BaseException:
+                    conn.execute("ROLLBACK")
+                    raise
+                applied += 1
+                LOG.debug("Applied migration V%d__%s", version, desc)
+            return applied
+
+    def schema_version(self) -> int:
+        row = self.query_one("SELECT MAX(version) AS v FROM schema_version")
+        return int(row["v"] or 0)
+
+
+def _split_sql(script: str) -> List[str]:
+    """Splits a migration script into statements (trigger bodies kept whole)."""
+    out, buf, in_trigger = [], [], False
+    for line in script.splitlines():
+        stripped = line.strip()
+        if not stripped or stripped.startswith("--"):
+            continue
+        buf.append(line)
+        upper = stripped.upper()
+        if upper.startswith("CREATE TRIGGER"):
+            in_trigger = True
+        if in_trigger:
+            if upper == "END;":
+                out.append("\n".join(buf))
+                buf, in_trigger = [], False
+            continue
+        if stripped.endswith(";"):
+            out.append("\n".join(buf))
+            buf = []
+    if buf:
+        out.append("\n".join(buf))
+    return out

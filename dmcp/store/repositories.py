@@ -1,0 +1,525 @@
+"""Repositories: SQL CRUD over the four tables.
+
+Parity (reference SQL constants are quoted in each docstring):
+
+* :class:`ProjectRepository`         -- ``project/domain/ProjectRepository.java:24-281``
+* :class:`SourceClassRepository`     -- ``analysis/domain/SourceClassRepository.java:24-388``
+* :class:`SourceMethodRepository`    -- ``analysis/domain/SourceMethodRepository.java:28-403``
+* :class:`MethodParameterRepository` -- ``analysis/domain/MethodParameterRepository.java:27-179``
+
+Divergences:
+
+* ``find_by_full_class_name`` no longer throws when a FQCN exists in several
+  projects (JDBI ``findOne`` at ``SourceClassRepository.java:171-177``); it
+  returns the row of the most recently analyzed project.  ``find_all_by_full_class_name``
+  exposes every match.
+* ``find_by_class_name_and_method_name`` no longer throws on overloads
+  (``SourceMethodRepository.java:206-214``); it returns the first overload by
+  line number.
+* batch ``*_in`` finders replace the per-row N+1 lookups of the context ops.
+"""
+from __future__ import annotations
+
+import json
+from datetime import datetime, timezone
+from typing import Dict, Iterable, List, Optional, Sequence
+
+from ..models.domain import (ClassType, MethodParameter, Project, ProjectStatus,
+                             RepositoryUrl, SourceClass, SourceMethod)
+from .db import Database
+
+_CHUNK = 500  # SQLite host-parameter limit is 999 on older builds
+
+
+def to_iso(dt: Optional[datetime]) -> Optional[str]:
+    if dt is None:
+        return None
+    if dt.tzinfo is None:
+        dt = dt.replace(tzinfo=timezone.utc)
+    return dt.astimezone(timezone.utc).strftime("%Y-%m-%dT%H:%M:%S.%fZ")
+
+
+def from_iso(s: Optional[str]) -> Optional[datetime]:
+    if not s:
+        return None
+    s = s.strip()
+    if s.endswith("Z"):
+        s = s[:-1] + "+00:00"
+    try:
+        dt = datetime.fromisoformat(s)
+    except ValueError:
+        return None
+    if dt.tzinfo is None:
+        dt = dt.replace(tzinfo=timezone.utc)
+    return dt
+
+
+def _chunks(seq: Sequence, n: int = _CHUNK):
+    for i in range(0, len(seq), n):
+        yield seq[i:i + n]
+
+
+def _json_list(value: Optional[Iterable[str]]) -> str:
+    return json.dumps(list(value or ()), ensure_ascii=False)
+
+
+def _parse_json_list(text: Optional[str]) -> List[str]:
+    if text is None or text == "":
+        return []
+    try:
+        v = json.loads(text)
+    except ValueError:
+        return []
+    if isinstance(v, list):
+        return [str(x) for x in v]
+    return []
+
+
+# --------------------------------------------------------------------------
+class ProjectRepository:
+    FIND_BY_ID = "SELECT * FROM projects WHERE id = ?"
+    FIND_BY_REPOSITORY_URL = "SELECT * FROM projects WHERE repository_url = ?"
+    FIND_BY_NAME = "SELECT * FROM projects WHERE name = ? ORDER BY created_at DESC LIMIT 1"
+    FIND_ALL = "SELECT * FROM projects ORDER BY created_at DESC"
+    FIND_BY_STATUS = "SELECT * FROM projects WHERE status = ?"
+    FIND_ALL_WITH_GRAPH = "SELECT * FROM projects WHERE graph_data IS NOT NULL"
+    EXISTS_BY_REPOSITORY_URL = "SELECT COUNT(*) FROM projects WHERE repository_url = ?"
+
+    # columns without graph_data: list views never load the (large) graph JSON
+    _LIGHT_COLUMNS = ("id, name, repository_url, default_branch, status, last_analyzed_at, "
+                      "last_commit_hash, created_at, updated_at, description, base_package, "
+                      "NULL AS graph_data")
+
+    def __init__(self, db: Database) -> None:
+        self.db = db
+
+    @staticmethod
+    def _map(row) -> Project:
+        return Project.reconstitute(
+            row["id"], row["name"], RepositoryUrl.of(row["repository_url"]),
+            row["default_branch"], row["description"], ProjectStatus(row["status"]),
+            from_iso(row["last_analyzed_at"]), row["last_commit_hash"], row["graph_data"],
+            from_iso(row["created_at"]), from_iso(row["updated_at"]), row["base_package"])
+
+    def save(self, p: Project) -> None:
+        with self.db.transaction() as c:
+            c.execute(
+                "INSERT INTO projects (id, name, repository_url, default_branch, status, "
+                "last_analyzed_at, last_commit_hash, created_at, updated_at, description, "
+                "graph_data, base_package) VALUES (?,?,?,?,?,?,?,?,?,?,?,?)",
+                (p.id, p.name, p.repository_url.value, p.default_branch, p.status.value,
+                 to_iso(p.last_analyzed_at), p.last_commit_hash, to_iso(p.created_at),
+                 to_iso(p.updated_at), p.description, p.graph_data, p.base_package))
+
+    def update(self, p: Project) -> None:
+        with self.db.transaction() as c:
+            c.execute(
+                "UPDATE projects SET name=?, default_branch=?, status=?, last_analyzed_at=?, "
+                "last_commit_hash=?, updated_at=?, description=?, graph_data=?, base_package=? "
+                "WHERE id=?",
+                (p.name, p.default_branch, p.status.value, to_iso(p.last_analyzed_at),
+                 p.last_commit_hash, to_iso(p.updated_at), p.description, p.graph_data,
+                 p.base_package, p.id))
+
+    def update_status(self, p: Project) -> None:
+        """Status-only update that does not rewrite the graph column."""
+        with self.db.transaction() as c:
+            c.execute("UPDATE projects SET status=?, updated_at=?, last_analyzed_at=?, "
+                      "last_commit_hash=?, description=? WHERE id=?",
+                      (p.status.value, to_iso(p.updated_at), to_iso(p.last_analyzed_at),
+                       p.last_commit_hash, p.description, p.id))
+
+    def find_by_id(self, project_id: str) -> Optional[Project]:
+        row = self.db.query_one(self.FIND_BY_ID, (project_id,))
+        return self._map(row) if row else None
+
+    def find_by_repository_url(self, url) -> Optional[Project]:
+        value = url.value if isinstance(url, RepositoryUrl) else str(url)
+        row = self.db.query_one(self.FIND_BY_REPOSITORY_URL, (value,))
+        return self._map(row) if row else None
+
+    def find_by_name(self, name: str) -> Optional[Project]:
+        row = self.db.query_one(self.FIND_BY_NAME, (name,))
+        return self._map(row) if row else None
+
+    def find_all(self, with_graph: bool = False) -> List[Project]:
+        if with_graph:
+            return [self._map(r) for r in self.db.query(self.FIND_ALL)]
+        rows = self.db.query(f"SELECT {self._LIGHT_COLUMNS} FROM projects ORDER BY created_at DESC")
+        return [self._map(r) for r in rows]
+
+    def find_by_status(self, status: ProjectStatus) -> List[Project]:
+        return [self._map(r) for r in self.db.query(self.FIND_BY_STATUS, (status.value,))]
+
+    def find_by_statuses(self, statuses: Iterable[ProjectStatus]) -> List[Project]:
+        vals = [s.value for s in statuses]
+        if not vals:
+            return []
+        q = f"SELECT * FROM projects WHERE status IN ({','.join('?' * len(vals))}) ORDER BY created_at"
+        return [self._map(r) for r in self.db.query(q, vals)]
+
+    def find_all_with_graph(self) -> List[Project]:
+        return [self._map(r) for r in self.db.query(self.FIND_ALL_WITH_GRAPH)]
+
+    def delete(self, project_id: str) -> None:
+        with self.db.transaction() as c:
+            c.execute("DELETE FROM projects WHERE id = ?", (project_id,))
+
+    def exists_by_repository_url(self, url) -> bool:
+        value = url.value if isinstance(url, RepositoryUrl) else str(url)
+        row = self.db.query_one(self.EXISTS_BY_REPOSITORY_URL, (value,))
+        return bool(row[0])
+
+
+# --------------------------------------------------------------------------
+class SourceClassRepository:
+    FIND_BY_ID = "SELECT * FROM source_classes WHERE id = ?"
+    FIND_BY_PROJECT_ID = "SELECT * FROM source_classes WHERE project_id = ? ORDER BY full_class_name"
+    FIND_BY_FULL_CLASS_NAME = (
+        "SELECT c.* FROM source_classes c JOIN projects p ON p.id = c.project_id "
+        "WHERE c.full_class_name = ? "
+        "ORDER BY p.last_analyzed_at DESC, p.created_at DESC")
+    FIND_BY_PACKAGE_PREFIX = ("SELECT * FROM source_classes WHERE package_name = ? "
+                              "OR package_name LIKE ? ORDER BY full_class_name")
+    COUNT_BY_PROJECT_ID = "SELECT COUNT(*) FROM source_classes WHERE project_id = ?"
+    FIND_BY_PROJECT_ID_AND_FULL_CLASS_NAME = (
+        "SELECT * FROM source_classes WHERE project_id = ? AND full_class_name = ?")
+    FIND_UNENRICHED_BY_PROJECT_ID = ("SELECT * FROM source_classes WHERE project_id = ? "
+                                     "AND description IS NULL ORDER BY full_class_name")
+    _INSERT = ("INSERT INTO source_classes (id, project_id, full_class_name, simple_name, "
+               "package_name, class_type, description, source_file, created_at, commit_hash) "
+               "VALUES (?,?,?,?,?,?,?,?,?,?)")
+
+    def __init__(self, db: Database) -> None:
+        self.db = db
+
+    @staticmethod
+    def _map(row) -> SourceClass:
+        return SourceClass(row["id"], row["project_id"], row["full_class_name"], row["simple_name"],
+                           row["package_name"], ClassType.from_string(row["class_type"]),
+                           row["description"], row["source_file"], row["commit_hash"],
+                           from_iso(row["created_at"]))
+
+    @staticmethod
+    def _params(sc: SourceClass):
+        return (sc.id, sc.project_id, sc.full_class_name, sc.simple_name, sc.package_name,
+                sc.class_type.value, sc.description, sc.source_file, to_iso(sc.created_at),
+                sc.commit_hash)
+
+    def save(self, sc: SourceClass) -> None:
+        with self.db.transaction() as c:
+            c.execute(self._INSERT, self._params(sc))
+
+    def save_all(self, classes: Sequence[SourceClass]) -> None:
+        if not classes:
+            return
+        with self.db.transaction() as c:
+            c.executemany(self._INSERT, [self._params(sc) for sc in classes])
+
+    def save_rows(self, rows: Sequence[tuple]) -> None:
+        """Bulk insert of pre-built parameter tuples (hot indexing path)."""
+        if not rows:
+            return
+        with self.db.transaction() as c:
+            c.executemany(self._INSERT, rows)
+
+    def find_by_id(self, class_id: str) -> Optional[SourceClass]:
+        row = self.db.query_one(self.FIND_BY_ID, (class_id,))
+        return self._map(row) if row else None
+
+    def find_by_ids(self, ids: Sequence[str]) -> Dict[str, SourceClass]:
+        out: Dict[str, SourceClass] = {}
+        for chunk in _chunks(list(ids)):
+            q = f"SELECT * FROM source_classes WHERE id IN ({','.join('?' * len(chunk))})"
+            for r in self.db.query(q, chunk):
+                out[r["id"]] = self._map(r)
+        return out
+
+    def find_by_project_id(self, project_id: str) -> List[SourceClass]:
+        return [self._map(r) for r in self.db.query(self.FIND_BY_PROJECT_ID, (project_id,))]
+
+    def find_by_full_class_name(self, fqcn: str) -> Optional[SourceClass]:
+        row = self.db.query_one(self.FIND_BY_FULL_CLASS_NAME, (fqcn,))
+        return self._map(row) if row else None
+
+    def find_all_by_full_class_name(self, fqcn: str) -> List[SourceClass]:
+        return [self._map(r) for r in self.db.query(self.FIND_BY_FULL_CLASS_NAME, (fqcn,))]
+
+    def find_by_full_class_names(self, names: Sequence[str],
+                                 project_id: Optional[str] = None) -> Dict[str, SourceClass]:
+        """Batch lookup: FQCN -> class (first by most recent project, like the single form)."""
+        out: Dict[str, SourceClass] = {}
+        uniq = list(dict.fromkeys(n for n in names if n is not None))
+        for chunk in _chunks(uniq):
+            marks = ",".join("?" * len(chunk))
+            if project_id is not None:
+                q = (f"SELECT * FROM source_classes WHERE project_id = ? "
+                     f"AND full_class_name IN ({marks})")
+                rows = self.db.query(q, [project_id, *chunk])
+            else:
+                q = (f"SELECT c.* FROM source_classes c JOIN projects p ON p.id = c.project_id "
+                     f"WHERE c.full_class_name IN ({marks}) "
+                     f"ORDER BY p.last_analyzed_at DESC, p.created_at DESC")
+                rows = self.db.query(q, chunk)
+            for r in rows:
+                if r["full_class_name"] not in out:
+                    out[r["full_class_name"]] = self._map(r)
+        return out
+
+    def find_by_package_prefix(self, package_prefix: str) -> List[SourceClass]:
+        return [self._map(r) for r in self.db.query(self.FIND_BY_PACKAGE_PREFIX,
+                                                    (package_prefix, package_prefix + ".%"))]
+
+    def find_by_project_id_and_full_class_name(self, project_id: str, fqcn: str) -> Optional[SourceClass]:
+        row = self.db.query_one(self.FIND_BY_PROJECT_ID_AND_FULL_CLASS_NAME, (project_id, fqcn))
+        return self._map(row) if row else None
+
+    def count_by_project_id(self, project_id: str) -> int:
+        return int(self.db.query_one(self.COUNT_BY_PROJECT_ID, (project_id,))[0])
+
+    def count_by_project(self) -> Dict[str, int]:
+        return {r[0]: int(r[1]) for r in self.db.query(
+            "SELECT project_id, COUNT(*) FROM source_classes GROUP BY project_id")}
+
+    def class_type_breakdown(self, project_id: str) -> Dict[str, int]:
+        return {r[0]: int(r[1]) for r in self.db.query(
+            "SELECT class_type, COUNT(*) FROM source_classes WHERE project_id = ? "
+            "GROUP BY class_type ORDER BY class_type", (project_id,))}
+
+    def package_names(self, project_id: str) -> List[str]:
+        return [r[0] for r in self.db.query(
+            "SELECT DISTINCT package_name FROM source_classes WHERE project_id = ? "
+            "AND package_name IS NOT NULL", (project_id,))]
+
+    def update_enrichment(self, class_id: str, class_type: ClassType, description: Optional[str]) -> None:
+        with self.db.transaction() as c:
+            c.execute("UPDATE source_classes SET class_type = ?, description = ? WHERE id = ?",
+                      (class_type.value, description, class_id))
+
+    def update_description(self, class_id: str, description: Optional[str]) -> None:
+        with self.db.transaction() as c:
+            c.execute("UPDATE source_classes SET description = ? WHERE id = ?", (description, class_id))
+
+    def update_commit_hash(self, class_id: str, commit_hash: Optional[str]) -> None:
+        with self.db.transaction() as c:
+            c.execute("UPDATE source_classes SET commit_hash = ? WHERE id = ?", (commit_hash, class_id))
+
+    def update_commit_hash_batch(self, class_ids: Sequence[str], commit_hash: Optional[str]) -> None:
+        if not class_ids:
+            return
+        with self.db.transaction() as c:
+            c.executemany("UPDATE source_classes SET commit_hash = ? WHERE id = ?",
+                          [(commit_hash, i) for i in class_ids])
+
+    def delete_by_project_id(self, project_id: str) -> None:
+        with self.db.transaction() as c:
+            c.execute("DELETE FROM source_classes WHERE project_id = ?", (project_id,))
+
+    def delete_by_ids(self, ids: Sequence[str]) -> None:
+        if not ids:
+            return
+        with self.db.transaction() as c:
+            for chunk in _chunks(list(ids)):
+                c.execute(f"DELETE FROM source_classes WHERE id IN ({','.join('?' * len(chunk))})",
+                          chunk)
+
+    def find_unenriched_by_project_id(self, project_id: str) -> List[SourceClass]:
+        return [self._map(r) for r in self.db.query(self.FIND_UNENRICHED_BY_PROJECT_ID, (project_id,))]
+
+
+# --------------------------------------------------------------------------
+class SourceMethodRepository:
+    FIND_BY_ID = "SELECT * FROM source_methods WHERE id = ?"
+    FIND_BY_CLASS_ID = ("SELECT * FROM source_methods WHERE class_id = ? "
+                        "ORDER BY line_number IS NULL, line_number, method_name")
+    FIND_BY_CLASS_NAME = ("SELECT m.* FROM source_methods m JOIN source_classes c ON c.id = m.class_id "
+                          "WHERE c.full_class_name = ? "
+                          "ORDER BY m.line_number IS NULL, m.line_number, m.method_name")
+    FIND_BY_CLASS_AND_METHOD_NAME = (
+        "SELECT m.* FROM source_methods m JOIN source_classes c ON c.id = m.class_id "
+        "WHERE c.full_class_name = ? AND m.method_name = ? "
+        "ORDER BY m.line_number IS NULL, m.line_number")
+    FIND_BY_CLASS_ID_AND_METHOD_NAME = (
+        "SELECT * FROM source_methods WHERE class_id = ? AND method_name = ? "
+        "ORDER BY line_number IS NULL, line_number LIMIT 1")
+    FIND_HTTP_ENDPOINTS_BY_PROJECT_ID = (
+        "SELECT m.* FROM source_methods m JOIN source_classes c ON c.id = m.class_id "
+        "WHERE c.project_id = ? AND m.http_method IS NOT NULL AND m.http_path IS NOT NULL "
+        "ORDER BY m.http_path, m.http_method")
+    COUNT_ENDPOINTS_BY_PROJECT_ID = (
+        "SELECT COUNT(*) FROM source_methods m JOIN source_classes c ON c.id = m.class_id "
+        "WHERE c.project_id = ? AND m.http_method IS NOT NULL AND m.http_path IS NOT NULL")
+    _INSERT = ("INSERT INTO source_methods (id, class_id, method_name, description, business_logic, "
+               "exceptions, http_method, http_path, line_number, created_at) "
+               "VALUES (?,?,?,?,?,?,?,?,?,?)")
+
+    def __init__(self, db: Database) -> None:
+        self.db = db
+
+    @staticmethod
+    def _map(row) -> SourceMethod:
+        return SourceMethod(row["id"], row["class_id"], row["method_name"], row["description"],
+                            _parse_json_list(row["business_logic"]), _parse_json_list(row["exceptions"]),
+                            row["http_method"], row["http_path"], row["line_number"],
+                            from_iso(row["created_at"]))
+
+    @staticmethod
+    def _params(m: SourceMethod):
+        return (m.id, m.class_id, m.method_name, m.description, _json_list(m.business_logic),
+                _json_list(m.exceptions), m.http_method, m.http_path, m.line_number,
+                to_iso(m.created_at))
+
+    def save(self, m: SourceMethod) -> None:
+        with self.db.transaction() as c:
+            c.execute(self._INSERT, self._params(m))
+
+    def save_all(self, methods: Sequence[SourceMethod]) -> None:
+        if not methods:
+            return
+        with self.db.transaction() as c:
+            c.executemany(self._INSERT, [self._params(m) for m in methods])
+
+    def save_rows(self, rows: Sequence[tuple]) -> None:
+        if not rows:
+            return
+        with self.db.transaction() as c:
+            c.executemany(self._INSERT, rows)
+
+    def find_by_id(self, method_id: str) -> Optional[SourceMethod]:
+        row = self.db.query_one(self.FIND_BY_ID, (method_id,))
+        return self._map(row) if row else None
+
+    def find_by_class_id(self, class_id: str) -> List[SourceMethod]:
+        return [self._map(r) for r in self.db.query(self.FIND_BY_CLASS_ID, (class_id,))]
+
+    def find_by_class_ids(self, class_ids: Sequence[str]) -> Dict[str, List[SourceMethod]]:
+        out: Dict[str, List[SourceMethod]] = {cid: [] for cid in class_ids}
+        for chunk in _chunks(list(dict.fromkeys(class_ids))):
+            q = (f"SELECT * FROM source_methods WHERE class_id IN ({','.join('?' * len(chunk))}) "
+                 f"ORDER BY line_number IS NULL, line_number, method_name")
+            for r in self.db.query(q, chunk):
+                out.setdefault(r["class_id"], []).append(self._map(r))
+        return out
+
+    def find_by_class_name(self, fqcn: str) -> List[SourceMethod]:
+        return [self._map(r) for r in self.db.query(self.FIND_BY_CLASS_NAME, (fqcn,))]
+
+    def find_by_class_name_and_method_name(self, fqcn: str, method_name: str) -> Optional[SourceMethod]:
+        row = self.db.query_one(self.FIND_BY_CLASS_AND_METHOD_NAME, (fqcn, method_name))
+        return self._map(row) if row else None
+
+    def find_by_class_id_and_method_name(self, class_id: str, method_name: str) -> Optional[SourceMethod]:
+        row = self.db.query_one(self.FIND_BY_CLASS_ID_AND_METHOD_NAME, (class_id, method_name))
+        return self._map(row) if row else None
+
+    def find_http_endpoints_by_project_id(self, project_id: str) -> List[SourceMethod]:
+        return [self._map(r) for r in self.db.query(self.FIND_HTTP_ENDPOINTS_BY_PROJECT_ID, (project_id,))]
+
+    def count_endpoints_by_project_id(self, project_id: str) -> int:
+        return int(self.db.query_one(self.COUNT_ENDPOINTS_BY_PROJECT_ID, (project_id,))[0])
+
+    def count_endpoints_by_project(self) -> Dict[str, int]:
+        return {r[0]: int(r[1]) for r in self.db.query(
+            "SELECT c.project_id, COUNT(*) FROM source_methods m JOIN source_classes c "
+            "ON c.id = m.class_id WHERE m.http_method IS NOT NULL AND m.http_path IS NOT NULL "
+            "GROUP BY c.project_id")}
+
+    def update_enrichment(self, method_id: str, description: Optional[str],
+                          business_logic: Optional[Iterable[str]],
+                          exceptions: Optional[Iterable[str]]) -> None:
+        with self.db.transaction() as c:
+            c.execute("UPDATE source_methods SET description = ?, business_logic = ?, exceptions = ? "
+                      "WHERE id = ?", (description, _json_list(business_logic),
+                                       _json_list(exceptions), method_id))
+
+    def update_enrichment_batch(self, rows: Sequence[tuple]) -> None:
+        """rows: (description, business_logic_list, method_id)."""
+        if not rows:
+            return
+        with self.db.transaction() as c:
+            c.executemany("UPDATE source_methods SET description = ?, business_logic = ? WHERE id = ?",
+                          [(d, _json_list(bl), mid) for d, bl, mid in rows])
+
+    def delete_by_class_id(self, class_id: str) -> None:
+        with self.db.transaction() as c:
+            c.execute("DELETE FROM source_methods WHERE class_id = ?", (class_id,))
+
+    def delete_by_class_ids(self, class_ids: Sequence[str]) -> None:
+        if not class_ids:
+            return
+        with self.db.transaction() as c:
+            for chunk in _chunks(list(class_ids)):
+                c.execute(f"DELETE FROM source_methods WHERE class_id IN ({','.join('?' * len(chunk))})",
+                          chunk)
+
+
+# --------------------------------------------------------------------------
+class MethodParameterRepository:
+    FIND_BY_METHOD_ID = "SELECT * FROM method_parameters WHERE method_id = ? ORDER BY position"
+    _INSERT = ("INSERT INTO method_parameters (id, method_id, position, class_id, created_at) "
+               "VALUES (?,?,?,?,?)")
+
+    def __init__(self, db: Database) -> None:
+        self.db = db
+
+    @staticmethod
+    def _map(row) -> MethodParameter:
+        return MethodParameter(row["id"], row["method_id"], int(row["position"]), row["class_id"],
+                               from_iso(row["created_at"]))
+
+    @staticmethod
+    def _params(p: MethodParameter):
+        return (p.id, p.method_id, p.position, p.class_id, to_iso(p.created_at))
+
+    def save(self, p: MethodParameter) -> None:
+        with self.db.transaction() as c:
+            c.execute(self._INSERT, self._params(p))
+
+    def save_all(self, params: Sequence[MethodParameter]) -> None:
+        if not params:
+            return
+        with self.db.transaction() as c:
+            c.executemany(self._INSERT, [self._params(p) for p in params])
+
+    def save_rows(self, rows: Sequence[tuple]) -> None:
+        if not rows:
+            return
+        with self.db.transaction() as c:
+            c.executemany(self._INSERT, rows)
+
+    def find_by_method_id(self, method_id: str) -> List[MethodParameter]:
+        return [self._map(r) for r in self.db.query(self.FIND_BY_METHOD_ID, (method_id,))]
+
+    def delete_by_method_id(self, method_id: str) -> None:
+        with self.db.transaction() as c:
+            c.execute("DELETE FROM method_parameters WHERE method_id = ?", (method_id,))
+
+    def delete_by_class_id(self, class_id: str) -> None:
+        """Deletes parameters of every method owned by ``class_id``."""
+        with self.db.transaction() as c:
+            c.execute("DELETE FROM method_parameters WHERE method_id IN "
+                      "(SELECT id FROM source_methods WHERE class_id = ?)", (class_id,))
+
+    def delete_by_class_ids(self, class_ids: Sequence[str]) -> None:
+        if not class_ids:
+            return
+        with self.db.transaction() as c:
+            for chunk in _chunks(list(class_ids)):
+                c.execute("DELETE FROM method_parameters WHERE method_id IN (SELECT id FROM source_methods "
+                          f"WHERE class_id IN ({','.join('?' * len(chunk))}))", chunk)
+
+    def delete_by_project_id(self, project_id: str) -> None:
+        with self.db.transaction() as c:
+            c.execute("DELETE FROM method_parameters WHERE method_id IN (SELECT m.id FROM source_methods m "
+                      "JOIN source_classes c ON c.id = m.class_id WHERE c.project_id = ?)", (project_id,))
+
+
+class Repositories:
+    """Bundle of the four repositories over one database."""
+
+    def __init__(self, db: Database) -> None:
+        self.db = db
+        self.projects = ProjectRepository(db)
+        self.classes = SourceClassRepository(db)
+        self.methods = SourceMethodRepository(db)
+        self.params = MethodParameterRepository(db)

@@ -1,0 +1,414 @@
+#include "common.hpp"
+
+#include <algorithm>
+#include <cstdio>
+#include <mutex>
+#include <sys/stat.h>
+
+namespace srcscan {
+
+void match_brackets(std::vector<Token>& toks) {
+    std::vector<int> stack;
+    stack.reserve(64);
+    for (int i = 0; i < (int)toks.size(); ++i) {
+        Token& t = toks[i];
+        if (t.kind != Tok::Punct || t.text.size() != 1) continue;
+        char c = t.text[0];
+        if (c == '(' || c == '[' || c == '{') {
+            stack.push_back(i);
+        } else if (c == ')' || c == ']' || c == '}') {
+            char want = c == ')' ? '(' : (c == ']' ? '[' : '{');
+            // Tolerate unbalanced input: pop to the nearest matching opener.
+            int j = (int)stack.size() - 1;
+            while (j >= 0 && toks[stack[j]].text[0] != want) --j;
+            if (j < 0) continue;
+            int open = stack[j];
+            stack.resize(j);
+            toks[open].match = i;
+            t.match = open;
+        }
+    }
+}
+
+static const char* kMultiPunct[] = {
+    "...", "::", "->", ":=", "<-", "==", "!=", "&&", "||", "++", "--",
+    "+=", "-=", "*=", "/=", "%=", "&=", "|=", "^=", "<=", ">=", nullptr};
+
+std::vector<Token> lex_c_family(std::string_view src, const CLexOptions& opt) {
+    std::vector<Token> toks;
+    toks.reserve(src.size() / 4 + 16);
+    size_t i = 0, n = src.size();
+    int line = 1;
+    bool nl = false;
+    auto go_semi_ok = [&]() {
+        if (!opt.go || toks.empty()) return false;
+        const Token& t = toks.back();
+        switch (t.kind) {
+            case Tok::Ident:
+            case Tok::Number:
+            case Tok::String:
+            case Tok::Char:
+                return true;
+            case Tok::Punct:
+                return t.text == ")" || t.text == "]" || t.text == "}" || t.text == "++" || t.text == "--";
+            default:
+                return false;
+        }
+    };
+    auto newline = [&]() {
+        if (go_semi_ok()) {
+            Token s{Tok::Semi, std::string_view(), line};
+            toks.push_back(s);
+        }
+        ++line;
+        nl = true;
+    };
+    auto push = [&](Tok k, size_t b, size_t e, int ln) {
+        Token t{k, src.substr(b, e - b), ln};
+        t.nl_before = nl;
+        nl = false;
+        toks.push_back(t);
+    };
+    while (i < n) {
+        unsigned char c = src[i];
+        if (c == '\n') { newline(); ++i; continue; }
+        if (c == ' ' || c == '\t' || c == '\r' || c == '\f' || c == '\v') { ++i; continue; }
+        if (c == '/' && i + 1 < n && src[i + 1] == '/') {
+            while (i < n && src[i] != '\n') ++i;
+            continue;
+        }
+        if (c == '/' && i + 1 < n && src[i + 1] == '*') {
+            i += 2;
+            bool had_nl = false;
+            while (i < n && !(src[i] == '*' && i + 1 < n && src[i + 1] == '/')) {
+                if (src[i] == '\n') { ++line; had_nl = true; }
+                ++i;
+            }
+            i = std::min(n, i + 2);
+            if (had_nl) {  // a multi-line comment acts like a newline (Go spec)
+                if (go_semi_ok()) toks.push_back(Token{Tok::Semi, std::string_view(), line});
+                nl = true;
+            }
+            continue;
+        }
+        int ln = line;
+        if (opt.java && c == '"' && i + 2 < n && src[i + 1] == '"' && src[i + 2] == '"') {
+            size_t b = i;
+            i += 3;
+            while (i < n && !(src[i] == '"' && i + 2 < n && src[i + 1] == '"' && src[i + 2] == '"' && src[i - 1] != '\\')) {
+                if (src[i] == '\n') ++line;
+                ++i;
+            }
+            i = std::min(n, i + 3);
+            push(Tok::String, b, i, ln);
+            continue;
+        }
+        if (c == '"') {
+            size_t b = i++;
+            while (i < n && src[i] != '"' && src[i] != '\n') {
+                if (src[i] == '\\' && i + 1 < n) ++i;
+                ++i;
+            }
+            if (i < n && src[i] == '"') ++i;
+            push(Tok::String, b, i, ln);
+            continue;
+        }
+        if (c == '\'') {
+            size_t b = i++;
+            while (i < n && src[i] != '\'' && src[i] != '\n') {
+                if (src[i] == '\\' && i + 1 < n) ++i;
+                ++i;
+            }
+            if (i < n && src[i] == '\'') ++i;
+            push(Tok::Char, b, i, ln);
+            continue;
+        }
+        if (opt.go && c == '`') {
+            size_t b = i++;
+            while (i < n && src[i] != '`') {
+                if (src[i] == '\n') ++line;
+                ++i;
+            }
+            if (i < n) ++i;
+            push(Tok::String, b, i, ln);
+            continue;
+        }
+        if ((c >= '0' && c <= '9') || (c == '.' && i + 1 < n && src[i + 1] >= '0' && src[i + 1] <= '9')) {
+            size_t b = i++;
+            while (i < n) {
+                unsigned char d = src[i];
+                if (is_ident_char(d) || d == '.') { ++i; continue; }
+                if ((d == '+' || d == '-') && (src[i - 1] == 'e' || src[i - 1] == 'E' || src[i - 1] == 'p' || src[i - 1] == 'P')) {
+                    ++i;
+                    continue;
+                }
+                break;
+            }
+            push(Tok::Number, b, i, ln);
+            continue;
+        }
+        if (is_ident_start(c)) {
+            size_t b = i++;
+            while (i < n && is_ident_char((unsigned char)src[i])) ++i;
+            push(Tok::Ident, b, i, ln);
+            continue;
+        }
+        // punctuation
+        bool matched = false;
+        for (const char** p = kMultiPunct; *p; ++p) {
+            size_t len = std::strlen(*p);
+            if (i + len <= n && src.compare(i, len, *p) == 0) {
+                push(Tok::Punct, i, i + len, ln);
+                i += len;
+                matched = true;
+                break;
+            }
+        }
+        if (matched) continue;
+        push(Tok::Punct, i, i + 1, ln);
+        ++i;
+    }
+    if (go_semi_ok()) toks.push_back(Token{Tok::Semi, std::string_view(), line});
+    match_brackets(toks);
+    return toks;
+}
+
+std::string_view unquote(std::string_view lit) {
+    if (lit.size() >= 6 && starts_with(lit, "\"\"\"") && ends_with(lit, "\"\"\"")) return lit.substr(3, lit.size() - 6);
+    if (lit.size() >= 2) {
+        char a = lit.front(), b = lit.back();
+        if ((a == '"' || a == '\'' || a == '`') && a == b) return lit.substr(1, lit.size() - 2);
+    }
+    return lit;
+}
+
+// ------------------------------------------------------------------ JSON
+void JsonWriter::str(std::string_view s) {
+    out += '"';
+    for (unsigned char c : s) {
+        switch (c) {
+            case '"': out += "\\\""; break;
+            case '\\': out += "\\\\"; break;
+            case '\n': out += "\\n"; break;
+            case '\r': out += "\\r"; break;
+            case '\t': out += "\\t"; break;
+            case '\b': out += "\\b"; break;
+            case '\f': out += "\\f"; break;
+            default:
+                if (c < 0x20) {
+                    char buf[8];
+                    std::snprintf(buf, sizeof buf, "\\u%04x", c);
+                    out += buf;
+                } else {
+                    out += (char)c;
+                }
+        }
+    }
+    out += '"';
+}
+
+namespace {
+struct JsonParser {
+    std::string_view t;
+    size_t i = 0;
+    int depth = 0;
+    void ws() { while (i < t.size() && (t[i] == ' ' || t[i] == '\n' || t[i] == '\r' || t[i] == '\t')) ++i; }
+    bool lit(const char* s) {
+        size_t n = std::strlen(s);
+        if (t.compare(i, n, s) == 0) { i += n; return true; }
+        return false;
+    }
+    bool string(std::string& out) {
+        if (i >= t.size() || t[i] != '"') return false;
+        ++i;
+        while (i < t.size() && t[i] != '"') {
+            char c = t[i++];
+            if (c == '\\' && i < t.size()) {
+                char e = t[i++];
+                switch (e) {
+                    case 'n': out += '\n'; break;
+                    case 't': out += '\t'; break;
+                    case 'r': out += '\r'; break;
+                    case 'b': out += '\b'; break;
+                    case 'f': out += '\f'; break;
+                    case 'u': {
+                        if (i + 4 > t.size()) return false;
+                        unsigned cp = (unsigned)std::stoul(std::string(t.substr(i, 4)), nullptr, 16);
+                        i += 4;
+                        if (cp < 0x80) out += (char)cp;
+                        else if (cp < 0x800) { out += (char)(0xC0 | (cp >> 6)); out += (char)(0x80 | (cp & 0x3F)); }
+                        else { out += (char)(0xE0 | (cp >> 12)); out += (char)(0x80 | ((cp >> 6) & 0x3F)); out += (char)(0x80 | (cp & 0x3F)); }
+                        break;
+                    }
+                    default: out += e;
+                }
+            } else {
+                out += c;
+            }
+        }
+        if (i >= t.size()) return false;
+        ++i;
+        return true;
+    }
+    bool value(JsonValue& v) {
+        if (++depth > 256) return false;
+        ws();
+        if (i >= t.size()) return false;
+        char c = t[i];
+        bool ok = true;
+        if (c == '{') {
+            v.kind = JsonValue::Obj;
+            ++i;
+            ws();
+            if (i < t.size() && t[i] == '}') { ++i; --depth; return true; }
+            while (ok) {
+                ws();
+                std::string k;
+                if (!string(k)) return false;
+                ws();
+                if (i >= t.size() || t[i] != ':') return false;
+                ++i;
+                JsonValue child;
+                if (!value(child)) return false;
+                v.obj.emplace_back(std::move(k), std::move(child));
+                ws();
+                if (i < t.size() && t[i] == ',') { ++i; continue; }
+                if (i < t.size() && t[i] == '}') { ++i; break; }
+                return false;
+            }
+        } else if (c == '[') {
+            v.kind = JsonValue::Arr;
+            ++i;
+            ws();
+            if (i < t.size() && t[i] == ']') { ++i; --depth; return true; }
+            while (true) {
+                JsonValue child;
+                if (!value(child)) return false;
+                v.arr.push_back(std::move(child));
+                ws();
+                if (i < t.size() && t[i] == ',') { ++i; continue; }
+                if (i < t.size() && t[i] == ']') { ++i; break; }
+                return false;
+            }
+        } else if (c == '"') {
+            v.kind = JsonValue::Str;
+            ok = string(v.s);
+        } else if (lit("true")) {
+            v.kind = JsonValue::Bool; v.b = true;
+        } else if (lit("false")) {
+            v.kind = JsonValue::Bool; v.b = false;
+        } else if (lit("null")) {
+            v.kind = JsonValue::Null;
+        } else {
+            v.kind = JsonValue::Num;
+            size_t b = i;
+            while (i < t.size() && (std::strchr("+-0123456789.eE", t[i]) != nullptr)) ++i;
+            if (b == i) return false;
+            v.s = std::string(t.substr(b, i - b));
+        }
+        --depth;
+        return ok;
+    }
+};
+}  // namespace
+
+bool parse_json(std::string_view text, JsonValue& out) {
+    JsonParser p{text};
+    if (!p.value(out)) return false;
+    p.ws();
+    return p.i == text.size();
+}
+
+// ------------------------------------------------------------- threading
+void parallel_for(size_t n, int threads, const std::function<void(size_t)>& fn) {
+    if (n == 0) return;
+    int hw = (int)std::thread::hardware_concurrency();
+    if (hw <= 0) hw = 4;
+    int t = threads > 0 ? threads : hw;
+    if ((size_t)t > n) t = (int)n;
+    if (t <= 1) {
+        for (size_t i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> pool;
+    pool.reserve(t);
+    for (int w = 0; w < t; ++w) {
+        pool.emplace_back([&]() {
+            for (;;) {
+                size_t i = next.fetch_add(1, std::memory_order_relaxed);
+                if (i >= n) break;
+                fn(i);
+            }
+        });
+    }
+    for (auto& th : pool) th.join();
+}
+
+// ----------------------------------------------------------------- files
+bool read_file(const std::string& path, std::string& out, size_t max_bytes) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) return false;
+    std::fseek(f, 0, SEEK_END);
+    long sz = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    if (sz < 0 || (max_bytes && (size_t)sz > max_bytes)) { std::fclose(f); return false; }
+    out.resize((size_t)sz);
+    size_t got = sz ? std::fread(&out[0], 1, (size_t)sz, f) : 0;
+    std::fclose(f);
+    out.resize(got);
+    return true;
+}
+
+bool file_exists(const std::string& path) {
+    struct stat st;
+    return ::stat(path.c_str(), &st) == 0 && S_ISREG(st.st_mode);
+}
+
+bool dir_exists(const std::string& path) {
+    struct stat st;
+    return ::stat(path.c_str(), &st) == 0 && S_ISDIR(st.st_mode);
+}
+
+std::string join_path(const std::string& a, const std::string& b) {
+    if (a.empty()) return b;
+    if (b.empty()) return a;
+    if (a.back() == '/') return a + b;
+    return a + "/" + b;
+}
+
+std::string normalize_path(const std::string& p) {
+    bool abs = !p.empty() && p[0] == '/';
+    std::vector<std::string> parts;
+    size_t i = 0;
+    while (i <= p.size()) {
+        size_t j = p.find('/', i);
+        if (j == std::string::npos) j = p.size();
+        std::string seg = p.substr(i, j - i);
+        if (seg.empty() || seg == ".") {
+        } else if (seg == "..") {
+            if (!parts.empty() && parts.back() != "..") parts.pop_back();
+            else if (!abs) parts.push_back("..");
+        } else {
+            parts.push_back(seg);
+        }
+        i = j + 1;
+    }
+    std::string out = abs ? "/" : "";
+    for (size_t k = 0; k < parts.size(); ++k) {
+        if (k) out += '/';
+        out += parts[k];
+    }
+    return out;
+}
+
+std::string to_lower(std::string_view s) {
+    std::string r(s);
+    for (auto& c : r) if (c >= 'A' && c <= 'Z') c = (char)(c - 'A' + 'a');
+    return r;
+}
+bool starts_with(std::string_view s, std::string_view p) { return s.size() >= p.size() && s.compare(0, p.size(), p) == 0; }
+bool ends_with(std::string_view s, std::string_view p) { return s.size() >= p.size() && s.compare(s.size() - p.size(), p.size(), p) == 0; }
+bool contains(std::string_view s, std::string_view p) { return s.find(p) != std::string_view::npos; }
+
+}  // namespace srcscan

@@ -1,0 +1,169 @@
+#!/usr/bin/env python3
+"""Headline benchmark: classes indexed per second (BASELINE.json fallback metric).
+
+One *step* = one complete ``analyze_project`` of a synthetic Spring Boot
+monorepo through the production pipeline: git clone (file://, shallow) ->
+native C++ parse -> graph build -> Phase 1 persist (SQLite, one transaction,
+replacing the previous analysis) -> graph JSON -> cache publish.  Enrichment
+is disabled by default (BASELINE: "Indexing throughput with enrichment
+disabled"); ``--enrich fake|local`` adds Phase 2/3 (``local`` = the optional
+MI355X model, see dmcp/enrich/local.py).
+
+Multi-GPU contract: launched by ``torch.distributed.run`` with one rank per
+GPU; every rank indexes its own repository (weak scaling), the timed region
+is bracketed by barrier + ``torch.cuda.synchronize()``, the MAX elapsed over
+ranks is taken (all-reduce over RCCL when GPUs are present, gloo otherwise)
+and rank 0 prints one JSON line with the whole-job aggregate.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import shutil
+import statistics
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "classes indexed/sec"
+BASELINE_VALUE = None  # the reference publishes no throughput number
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--classes", type=int, default=2000, help="classes per synthetic repo (per rank)")
+    ap.add_argument("--threads", type=int, default=0, help="parser threads per rank (0 = auto)")
+    ap.add_argument("--enrich", default="none", choices=["none", "fake", "local"])
+    ap.add_argument("--queries", type=int, default=200, help="graph_query / stack-trace latency samples")
+    ap.add_argument("--workdir", default=None)
+    return ap.parse_args(argv)
+
+
+def init_distributed():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch = None
+    try:
+        import torch as _t
+        torch = _t
+    except ImportError:
+        pass
+    dist = None
+    cuda = bool(torch is not None and torch.cuda.is_available())
+    if cuda:
+        torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend="nccl" if cuda else "gloo")
+    return torch, dist, rank, world, local_rank, cuda
+
+
+def sync(torch, dist, cuda):
+    if dist is not None:
+        dist.barrier()
+    if cuda:
+        torch.cuda.synchronize()
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    torch, dist, rank, world, local_rank, cuda = init_distributed()
+    logging.basicConfig(level=logging.WARNING, stream=sys.stderr)
+    from dmcp.app import App
+    from dmcp.config import Config
+    from dmcp.utils import synth
+    from dmcp.utils.tracing import METRICS
+
+    cpus = os.cpu_count() or 8
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    threads = args.threads or max(1, min(16, cpus // max(1, local_world)))
+    work = args.workdir or tempfile.mkdtemp(prefix=f"dmcp-bench-r{rank}-")
+    repo = os.path.join(work, f"shop{rank}")
+    fqcns = synth.java_spring_repo(repo, n_classes=args.classes, base_package=f"co.acme.shop{rank}", seed=rank + 1)
+    cfg = Config(db_path=os.path.join(work, "bench.db"), git_clone_base_path=os.path.join(work, "clones"),
+                 parser_threads=threads, enrich_backend=args.enrich if args.enrich != "none" else "null",
+                 require_enrichment_for_analyze=False, recover_stuck_on_start=False)
+    app = App(cfg)
+    try:
+        n_classes = 0
+        stats_acc = {}
+        for _ in range(args.warmup):
+            app.indexer.analyze_project(repo)
+        sync(torch, dist, cuda)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            r = app.indexer.analyze_project(repo)
+            n_classes += r.classes_analyzed
+            for k, v in r.stats.items():
+                if k.startswith("analyze."):
+                    stats_acc[k] = stats_acc.get(k, 0.0) + v
+        sync(torch, dist, cuda)
+        elapsed = time.perf_counter() - t0
+        total_classes = n_classes
+        if dist is not None:
+            t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if cuda else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+            c = torch.tensor([float(n_classes)], dtype=torch.float64, device="cuda" if cuda else "cpu")
+            dist.all_reduce(c, op=dist.ReduceOp.SUM)
+            total_classes = int(c.item())
+        # query latencies on the indexed graph (BASELINE configs 3/4)
+        extra = {"phaseMsPerStep": {k: round(v / max(1, args.steps), 2) for k, v in stats_acc.items()},
+                 "classesPerRepo": r.classes_analyzed, "parserThreadsPerRank": threads}
+        if rank == 0 and args.queries > 0:
+            project = f"shop{rank}"
+            qs = [f"{project}:endpoints", f"{project}:classes", f"{project}:OrderService:methods:+logic",
+                  f"{project}:UserController:dependencies", f"{project}:entrypoints:+logic",
+                  f"{project}:PaymentService:?list"]
+            lat = []
+            for i in range(args.queries):
+                q0 = time.perf_counter()
+                app.graph_query.query(qs[i % len(qs)])
+                lat.append((time.perf_counter() - q0) * 1e3)
+            st_lat = []
+            trace = synth.stack_trace_for(fqcns, 20)
+            for _ in range(max(10, args.queries // 10)):
+                q0 = time.perf_counter()
+                app.context.get_stack_trace_context(trace)
+                st_lat.append((time.perf_counter() - q0) * 1e3)
+            lat.sort()
+            st_lat.sort()
+            extra["graphQueryMs"] = {"p50": round(lat[len(lat) // 2], 3), "p99": round(lat[int(len(lat) * 0.99) - 1], 3)}
+            extra["stackTrace20Ms"] = {"p50": round(st_lat[len(st_lat) // 2], 3),
+                                       "p99": round(st_lat[max(0, int(len(st_lat) * 0.99) - 1)], 3)}
+        value = total_classes / elapsed if elapsed > 0 else 0.0
+        ms_per_step = elapsed / max(1, args.steps) * 1e3
+        if rank == 0:
+            line = {"metric": METRIC, "value": round(value, 2), "unit": "classes/s", "n_gpus": world,
+                    "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+                    "higher_is_better": True, "scaling": "weak",
+                    "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
+                    "dtype": "n/a (CPU text indexing)", "data": "synthetic (generated Spring Boot monorepo, "
+                    "local git repo, random-free deterministic)",
+                    "config": {"model": f"synthetic-java-spring-monorepo-{args.classes}-classes",
+                               "global_batch": args.classes * world, "seq_len": None,
+                               "parallelism": f"dp{world} (one repo per rank)",
+                               "enrichment": args.enrich},
+                    "extra": extra}
+            print(json.dumps(line), flush=True)
+    finally:
+        app.close()
+        if args.workdir is None:
+            shutil.rmtree(work, ignore_errors=True)
+        if dist is not None:
+            dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,371 @@
+"""Local enrichment backend on MI355X: a continuous-batching, JSON-constrained
+generation engine over :class:`dmcp.models.llm.LocalLM` -- extension.
+
+The reference sends every class to the Anthropic API, 5 requests at a time
+(``ClaudeApiClient.java:342-388``); enrichment wall-clock dominates its
+pipeline (SURVEY §3.2 hot loop #3).  This backend keeps the same contract
+(:class:`EnrichmentInput` in, :class:`EnrichmentResult` out, failures isolated
+per class) but generates on the local GPU:
+
+* **schema-constrained decoding** -- the reply's JSON skeleton
+  (``{"description": "...", "classTypeCorrection": null, "methods": [...]}``
+  with every extracted method name) is *forced*; only string contents are
+  generated, with a masked greedy argmax restricted to JSON-safe printable
+  characters.  The output always parses, so Phase 3 recovery is only needed
+  for infrastructure failures;
+* **continuous batching** -- up to ``max_batch`` sequences decode together,
+  one token per sequence per step (forced skeleton tokens ride in the same
+  batched step), finished sequences free their KV slot for the next prompt;
+* each step is one hipGraph replay (:class:`DecodeGraphs`) plus the
+  gfx950 masked-argmax kernel;
+* multi-GPU: one engine (replica) per GPU, classes sharded across replicas
+  (:mod:`dmcp.parallel.replicas`) -- pure data parallelism, no collectives
+  (SURVEY §5.8).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import threading
+import time
+from collections import deque
+from dataclasses import dataclass, field
+from typing import Deque, Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from ..models.llm import BOS, LocalLM, LMConfig, DecodeGraphs, preset
+from .backend import EnrichmentBackend, build_enrichment_prompt
+from .jsonfix import parse_enrichment_response
+from .types import EnrichmentInput, EnrichmentResult
+
+LOG = logging.getLogger(__name__)
+
+QUOTE = ord('"')
+
+
+def _json_safe_mask(vocab: int, with_quote: bool) -> List[int]:
+    words = [0] * ((vocab + 31) // 32)
+    for b in range(0x20, 0x7F):
+        if b in (QUOTE, ord("\\")):
+            continue
+        words[b >> 5] |= 1 << (b & 31)
+    if with_quote:
+        words[QUOTE >> 5] |= 1 << (QUOTE & 31)
+    # int32 view of the uint32 bit pattern
+    return [w - (1 << 32) if w >= (1 << 31) else w for w in words]
+
+
+@dataclass
+class Segment:
+    forced: Optional[bytes] = None   # forced bytes, or None for a free string
+    min_len: int = 0
+    max_len: int = 0
+
+
+def build_template(inp: EnrichmentInput, desc_len=(8, 96), method_len=(6, 64), step_len=(4, 40),
+                   steps: int = 2) -> List[Segment]:
+    """Segments of the reply; a free segment ends with a model- or force-emitted '"'."""
+    segs: List[Segment] = [Segment(b'{"description": "'), Segment(None, *desc_len),
+                           Segment(b', "classTypeCorrection": null, "methods": [')]
+    names = list(dict.fromkeys(inp.method_names))
+    for i, name in enumerate(names):
+        segs.append(Segment(b'{"methodName": ' + json.dumps(name).encode() + b', "description": "'))
+        segs.append(Segment(None, *method_len))
+        segs.append(Segment(b', "businessLogic": ["'))
+        for s in range(steps):
+            segs.append(Segment(None, *step_len))
+            if s + 1 < steps:
+                segs.append(Segment(b', "'))
+        segs.append(Segment(b"]}" + (b", " if i + 1 < len(names) else b"")))
+    segs.append(Segment(b"]}"))
+    # merge adjacent forced segments
+    out: List[Segment] = []
+    for s in segs:
+        if out and s.forced is not None and out[-1].forced is not None:
+            out[-1] = Segment(out[-1].forced + s.forced)
+        else:
+            out.append(s)
+    return out
+
+
+def template_budget(segs: Sequence[Segment]) -> int:
+    return sum(len(s.forced) if s.forced is not None else s.max_len + 1 for s in segs)
+
+
+def fit_template(inp: EnrichmentInput, capacity: int) -> List[Segment]:
+    """Largest template whose reply budget fits ``capacity`` tokens: free-string
+    lengths shrink first (down to a floor), then trailing methods are dropped."""
+    names = list(dict.fromkeys(inp.method_names))
+    for scale in (1.0, 0.75, 0.5, 0.35, 0.25):
+        def L(lo, hi):
+            return (min(lo, max(2, int(hi * scale))), max(4, int(hi * scale)))
+        segs = build_template(inp, L(8, 96), L(6, 64), L(4, 40))
+        if template_budget(segs) <= capacity:
+            return segs
+    keep = len(names)
+    while keep > 0:
+        keep //= 2
+        sub = EnrichmentInput(inp.source_code, inp.full_class_name, inp.language, inp.class_type, names[:keep])
+        segs = build_template(sub, (2, 24), (2, 16), (2, 8), steps=1)
+        if template_budget(segs) <= capacity:
+            return segs
+    return build_template(EnrichmentInput(inp.source_code, inp.full_class_name, inp.language,
+                                          inp.class_type, []), (2, 16))
+
+
+@dataclass
+class _Seq:
+    inp: EnrichmentInput
+    index: int
+    segs: List[Segment]
+    slot: int = -1
+    pos: int = 0                       # tokens already in the KV cache
+    seg: int = 0
+    free_len: int = 0
+    forced_off: int = 0
+    next_token: int = -1               # token to feed at the next decode step
+    out: bytearray = field(default_factory=bytearray)
+    done: bool = False
+    prompt_tokens: int = 0
+    gen_tokens: int = 0
+
+
+class LocalEngine:
+    def __init__(self, model: LocalLM, use_graphs: bool = True, max_prompt_tokens: Optional[int] = None) -> None:
+        self.model = model
+        self.cfg: LMConfig = model.cfg
+        self.graphs = DecodeGraphs(model) if use_graphs else None
+        dev = model.device
+        self.masks = torch.tensor([_json_safe_mask(self.cfg.vocab_size, False),
+                                   _json_safe_mask(self.cfg.vocab_size, True)], dtype=torch.int32, device=dev)
+        self.max_prompt_tokens = max_prompt_tokens
+        self.stats = {"prompt_tokens": 0, "generated_tokens": 0, "decode_steps": 0, "prefills": 0,
+                      "decode_s": 0.0, "prefill_s": 0.0}
+        self._lock = threading.Lock()
+
+    # ---------------------------------------------------------------- api
+    def generate(self, inputs: Sequence[EnrichmentInput], readme: Optional[str]) -> List[str]:
+        """Returns the raw JSON reply for every input (same order)."""
+        with self._lock:
+            return self._generate(inputs, readme)
+
+    # ------------------------------------------------------------ helpers
+    def _prompt(self, seq: _Seq, readme: Optional[str], budget: int) -> List[int]:
+        text = build_enrichment_prompt(seq.inp, readme).encode("utf-8", "replace")
+        limit = self.cfg.max_seq - budget - 2
+        if self.max_prompt_tokens:
+            limit = min(limit, self.max_prompt_tokens)
+        if limit < 16:
+            raise ValueError("KV capacity too small for the reply template")
+        if len(text) > limit:
+            keep_tail = min(256, limit // 4)  # keep the instructions at the end
+            text = text[:limit - keep_tail] + text[len(text) - keep_tail:]
+        return [BOS] + list(text)
+
+    def _select(self, logits: torch.Tensor, rows: List[int], with_quote: List[bool]) -> List[int]:
+        from .. import ops
+        idx = torch.tensor([1 if q else 0 for q in with_quote], dtype=torch.long, device=logits.device)
+        mask = self.masks.index_select(0, idx)
+        ids = ops.masked_argmax(logits.contiguous(), mask, vocab=self.cfg.vocab_size)
+        return ids.tolist()
+
+    def _advance_forced(self, s: _Seq) -> None:
+        """Sets next_token from the current forced segment or finishes."""
+        while s.seg < len(s.segs):
+            seg = s.segs[s.seg]
+            if seg.forced is None:
+                return
+            if s.forced_off < len(seg.forced):
+                s.next_token = seg.forced[s.forced_off]
+                s.forced_off += 1
+                return
+            s.seg += 1
+            s.forced_off = 0
+            s.free_len = 0
+        s.done = True
+
+    def _on_token_fed(self, s: _Seq, tok: int) -> None:
+        s.out.append(tok & 0xFF)
+        s.pos += 1
+        s.gen_tokens += 1
+
+    def _generate(self, inputs: Sequence[EnrichmentInput], readme: Optional[str]) -> List[str]:
+        cfg = self.cfg
+        dev = self.model.device
+        reply_cap = cfg.max_seq - max(64, cfg.max_seq // 4)
+        pending: Deque[_Seq] = deque(_Seq(inp, i, fit_template(inp, reply_cap)) for i, inp in enumerate(inputs))
+        free_slots = list(range(cfg.max_batch - 1, -1, -1))
+        active: List[_Seq] = []
+        results: Dict[int, str] = {}
+        while pending or active:
+            # admit: prefill prompt + first forced segment, then the first free token
+            while pending and free_slots:
+                s = pending.popleft()
+                try:
+                    budget = template_budget(s.segs)
+                    if budget + 32 > cfg.max_seq:
+                        raise ValueError(f"reply template needs {budget} tokens > max_seq {cfg.max_seq}")
+                    prompt = self._prompt(s, readme, budget)
+                except Exception as e:
+                    results[s.index] = json.dumps({"error": str(e)})
+                    continue
+                s.slot = free_slots.pop()
+                first = s.segs[0].forced or b""
+                toks = prompt + list(first)
+                t0 = time.perf_counter()
+                logits = self.model.forward_tokens(torch.tensor(toks, dtype=torch.int32), s.slot, 0)
+                self.stats["prefill_s"] += time.perf_counter() - t0
+                self.stats["prefills"] += 1
+                self.stats["prompt_tokens"] += len(toks)
+                s.prompt_tokens = len(prompt)
+                s.out.extend(first)
+                s.pos = len(toks)
+                s.seg, s.forced_off = 1, 0
+                if s.seg < len(s.segs) and s.segs[s.seg].forced is None:
+                    s.next_token = self._select(logits[None], [0], [s.segs[s.seg].min_len == 0])[0]
+                else:
+                    self._advance_forced(s)
+                if s.done:
+                    results[s.index] = s.out.decode("utf-8", "replace")
+                    free_slots.append(s.slot)
+                else:
+                    active.append(s)
+            if not active:
+                continue
+            # one batched decode step: feed next_token of every active sequence
+            B = len(active)
+            tok = torch.tensor([s.next_token for s in active], dtype=torch.int32)
+            sl = torch.tensor([s.slot for s in active], dtype=torch.int32)
+            ps = torch.tensor([s.pos for s in active], dtype=torch.int32)
+            t0 = time.perf_counter()
+            if dev.type == "cuda":
+                tok, sl, ps = (t.pin_memory().to(dev, non_blocking=True) for t in (tok, sl, ps))
+            runner = self.graphs.run if self.graphs is not None else self.model.decode
+            logits = runner(tok, sl, ps)
+            need_rows, with_q = [], []
+            for r, s in enumerate(active):
+                fed = s.next_token
+                self._on_token_fed(s, fed)
+                seg = s.segs[s.seg] if s.seg < len(s.segs) else None
+                if seg is not None and seg.forced is None:
+                    if fed == QUOTE:  # free string closed
+                        s.seg += 1
+                        s.forced_off = 0
+                        s.free_len = 0
+                        self._advance_forced(s)
+                        if not s.done and s.segs[s.seg].forced is None:
+                            need_rows.append(r)
+                            with_q.append(s.segs[s.seg].min_len == 0)
+                    else:
+                        s.free_len += 1
+                        if s.free_len >= seg.max_len:
+                            s.next_token = QUOTE
+                        else:
+                            need_rows.append(r)
+                            with_q.append(s.free_len >= seg.min_len)
+                else:
+                    self._advance_forced(s)
+                    if not s.done and s.segs[s.seg].forced is None:
+                        need_rows.append(r)
+                        with_q.append(s.segs[s.seg].min_len == 0)
+            if need_rows:
+                rows_t = torch.tensor(need_rows, dtype=torch.long, device=logits.device)
+                picked = self._select(logits.index_select(0, rows_t), need_rows, with_q)
+                for r, t in zip(need_rows, picked):
+                    active[r].next_token = t
+            self.stats["decode_s"] += time.perf_counter() - t0
+            self.stats["decode_steps"] += 1
+            self.stats["generated_tokens"] += B
+            still = []
+            for s in active:
+                if s.done:
+                    results[s.index] = s.out.decode("utf-8", "replace")
+                    free_slots.append(s.slot)
+                else:
+                    still.append(s)
+            active = still
+        return [results[i] for i in range(len(inputs))]
+
+
+class LocalLLMBackend(EnrichmentBackend):
+    """EnrichmentBackend over one or more local engines (one per GPU)."""
+
+    name = "local"
+
+    def __init__(self, engines: Sequence[LocalEngine], max_concurrent: int = 1) -> None:
+        super().__init__(max_concurrent=max(1, len(engines)))
+        self.engines = list(engines)
+        self.preferred_batch_size = sum(e.cfg.max_batch for e in self.engines) * 2
+
+    @classmethod
+    def from_config(cls, cfg) -> "LocalLLMBackend":
+        devices = []
+        if torch.cuda.is_available():
+            n = torch.cuda.device_count()
+            spec = (cfg.local_llm_devices or "all").strip()
+            devices = list(range(n)) if spec == "all" else [int(x) for x in spec.split(",") if x.strip()]
+        if not devices:
+            raise RuntimeError("LocalLLMBackend needs a ROCm GPU (torch.cuda.is_available() is False)")
+        engines = []
+        for d in devices:
+            with torch.cuda.device(d):
+                model = LocalLM(preset(cfg.local_llm_preset), device=f"cuda:{d}", seed=0)
+                engines.append(LocalEngine(model))
+        return cls(engines)
+
+    def enrich_class(self, inp: EnrichmentInput, readme: Optional[str]) -> EnrichmentResult:
+        return self.enrich_batch([inp], readme)[0]
+
+    def enrich_batch(self, inputs: Sequence[EnrichmentInput], readme: Optional[str]) -> List[EnrichmentResult]:
+        if not inputs:
+            return []
+        shards = [list(range(i, len(inputs), len(self.engines))) for i in range(len(self.engines))]
+        raw: List[Optional[str]] = [None] * len(inputs)
+        errors: Dict[int, str] = {}
+
+        def run(e_idx: int) -> None:
+            idx = shards[e_idx]
+            if not idx:
+                return
+            eng = self.engines[e_idx]
+            try:
+                with torch.cuda.device(eng.model.device) if eng.model.device.type == "cuda" else _nullctx():
+                    outs = eng.generate([inputs[i] for i in idx], readme)
+                for i, o in zip(idx, outs):
+                    raw[i] = o
+            except Exception as e:  # isolate: every class of this shard fails, others survive
+                LOG.exception("local engine %d failed", e_idx)
+                for i in idx:
+                    errors[i] = str(e)
+
+        if len(self.engines) == 1:
+            run(0)
+        else:
+            threads = [threading.Thread(target=run, args=(k,), name=f"local-llm-{k}") for k in range(len(self.engines))]
+            for t in threads:
+                t.start()
+            for t in threads:
+                t.join()
+        results = []
+        for i, inp in enumerate(inputs):
+            if i in errors or raw[i] is None:
+                results.append(EnrichmentResult.failure(inp.full_class_name, errors.get(i, "no output")))
+            else:
+                results.append(parse_enrichment_response(raw[i], inp.full_class_name))
+        return results
+
+    def stats(self) -> dict:
+        agg: Dict[str, float] = {}
+        for e in self.engines:
+            for k, v in e.stats.items():
+                agg[k] = agg.get(k, 0) + v
+        return agg
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

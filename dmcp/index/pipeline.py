@@ -42,7 +42,7 @@ from ..enrich.types import EnrichmentInput, EnrichmentResult, normalize_method_n
 from ..graph.cache import GraphCache
 from ..graph.project_graph import MethodEnrichmentData, MethodInfo, ProjectGraph
 from ..models.domain import (ClassType, Project, ProjectStatus, RepositoryUrl, SourceClass,
-                             new_id, package_name_of, simple_name_of, utc_now)
+                             new_id, new_ids, package_name_of, simple_name_of, utc_now)
 from ..parsers.base import ParsedProject, ParsedUnit, SourceParser, detect_parser
 from ..store.repositories import Repositories, to_iso
 from ..utils.errors import DomainError
@@ -263,11 +263,17 @@ class Indexer:
         methods_by_ident: Dict[str, List[Tuple[str, str]]] = {}
         units = parsed.units
         class_ids: Dict[str, str] = {}
+        n_ids = sum(1 + len(u.methods) + sum(len(v) for v in u.params.values()) * 2 for u in units.values())
+        id_pool = iter(new_ids(n_ids))
+
+        def nid() -> str:
+            return next(id_pool, None) or new_id()
+
         for ident in order:
             unit = units.get(ident)
             if unit is None:
                 continue
-            cid = new_id()
+            cid = nid()
             class_ids[ident] = cid
             ct = unit.class_type.value
             i = ident.rfind(".")
@@ -277,7 +283,7 @@ class Indexer:
             infos = []
             mids = []
             for sm in unit.methods:
-                mid = new_id()
+                mid = nid()
                 exc = sm.exceptions
                 meth_rows.append((mid, cid, sm.method_name, None, "[]",
                                   json.dumps(list(exc)) if exc else "[]", sm.http_method, sm.http_path,
@@ -306,9 +312,12 @@ class Indexer:
                 for pos, tgt in enumerate(targets):
                     tcid = class_ids.get(tgt)
                     if tcid is not None:
-                        param_rows.append((new_id(), mid, pos, tcid, now))
+                        param_rows.append((nid(), mid, pos, tcid, now))
         with self.repos.db.transaction():
             if replace:
+                # children first: the FK cascade then finds nothing to do per row
+                self.repos.params.delete_by_project_id(pid)
+                self.repos.methods.delete_by_project_id(pid)
                 self.repos.classes.delete_by_project_id(pid)
             self.repos.classes.save_rows(cls_rows)
             self.repos.methods.save_rows(meth_rows)

@@ -22,7 +22,7 @@ import re
 import uuid
 from dataclasses import dataclass, field
 from datetime import datetime, timezone
-from typing import FrozenSet, Iterable, List, Optional
+from typing import FrozenSet, Iterable, List, NamedTuple, Optional
 
 from ..utils.errors import (DomainError, require, require_non_blank,
                             require_non_negative, require_non_null)
@@ -30,6 +30,17 @@ from ..utils.errors import (DomainError, require, require_non_blank,
 
 def new_id() -> str:
     return str(uuid.uuid4())
+
+
+def new_ids(n: int) -> List[str]:
+    """``n`` UUID4 strings; uses the native bulk generator when available."""
+    if n <= 0:
+        return []
+    try:
+        from .. import _srcscan  # type: ignore
+        return _srcscan.uuid4_batch(n)
+    except (ImportError, AttributeError):
+        return [str(uuid.uuid4()) for _ in range(n)]
 
 
 def utc_now() -> datetime:
@@ -412,8 +423,7 @@ class MethodParameter:
         return cls(new_id(), method_id, position, class_id, utc_now())
 
 
-@dataclass(frozen=True, slots=True)
-class StaticMethodInfo:
+class StaticMethodInfo(NamedTuple):
     """Parser -> pipeline DTO: one statically extracted method."""
 
     method_name: str

@@ -1,0 +1,329 @@
+"""Llama-style decoder for local (on-GPU) enrichment -- MI355X extension.
+
+Not part of the reference (it calls the Anthropic API, ``ClaudeApiClient``);
+SURVEY §5.8 identifies a local enrichment model as the only legitimate GPU
+workload of this service.  Architecture: RMSNorm, rotate-half RoPE, GQA
+attention, SwiGLU MLP, untied LM head, bf16 weights and KV cache.
+
+MI355X mapping:
+
+* GEMMs (fused QKV, O, fused gate+up, down, LM head) go to hipBLASLt through
+  ``torch.nn.functional.linear``;
+* everything between them is a hand-written gfx950 kernel (:mod:`dmcp.ops`):
+  fused residual-add + RMSNorm, RoPE + KV-cache append, split-K GQA decode
+  attention, SwiGLU, masked greedy sampling, embedding gather;
+* prefill attention uses PyTorch SDPA (flash path on ROCm) -- prompts are
+  processed once per class, the decode loop dominates;
+* the KV cache is one preallocated slab ``[layers, slots, Hkv, max_seq, D]``
+  (288 GB of HBM per GPU: no paging needed at these sizes) so decode reads
+  every key row of a (slot, kv-head) contiguously;
+* the batched decode step is captured into hipGraphs per batch-size bucket
+  (:class:`DecodeGraphs`), removing ~10 launches/layer of host overhead.
+
+Weights are random-initialised by default (no checkpoint on this host) or
+loaded from a Llama-format safetensors directory (``load_safetensors``).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+from dataclasses import asdict, dataclass, field, replace
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+
+BYTE_VOCAB = 256
+BOS, EOS, PAD = 256, 257, 258
+
+
+@dataclass(frozen=True)
+class LMConfig:
+    name: str = "dmcp-coder-1b"
+    vocab_size: int = 320           # 259 byte-level tokens, padded to a multiple of 64
+    hidden: int = 2048
+    layers: int = 16
+    n_heads: int = 32
+    n_kv_heads: int = 8
+    head_dim: int = 64
+    intermediate: int = 8192
+    rope_theta: float = 10000.0
+    eps: float = 1e-5
+    max_seq: int = 8192             # KV capacity per slot (prompt + generation)
+    max_batch: int = 64             # KV slots = concurrent sequences
+
+    @property
+    def qkv_dim(self) -> int:
+        return (self.n_heads + 2 * self.n_kv_heads) * self.head_dim
+
+    def param_count(self) -> int:
+        per_layer = (self.qkv_dim * self.hidden + self.n_heads * self.head_dim * self.hidden
+                     + 3 * self.intermediate * self.hidden + 2 * self.hidden)
+        return self.layers * per_layer + 2 * self.vocab_size * self.hidden + self.hidden
+
+    def kv_bytes(self) -> int:
+        return 2 * self.layers * self.max_batch * self.n_kv_heads * self.max_seq * self.head_dim * 2
+
+
+PRESETS: Dict[str, LMConfig] = {
+    "dmcp-coder-1b": LMConfig(),
+    "dmcp-coder-3b": LMConfig(name="dmcp-coder-3b", hidden=3072, layers=28, n_heads=24, n_kv_heads=8,
+                              head_dim=128, intermediate=8192),
+    "tiny": LMConfig(name="tiny", hidden=256, layers=2, n_heads=4, n_kv_heads=2, head_dim=64,
+                     intermediate=512, max_seq=1024, max_batch=8),
+}
+
+
+def preset(name: str, **overrides) -> LMConfig:
+    if name not in PRESETS:
+        raise ValueError(f"unknown model preset {name!r}; choose one of {sorted(PRESETS)}")
+    return replace(PRESETS[name], **overrides) if overrides else PRESETS[name]
+
+
+class LocalLM:
+    """Weights + KV cache + forward passes (prefill / extend / batched decode)."""
+
+    def __init__(self, cfg: LMConfig, device: str = "cuda", seed: int = 0,
+                 weights: Optional[Dict[str, torch.Tensor]] = None) -> None:
+        if cfg.n_heads % cfg.n_kv_heads:
+            raise ValueError("n_heads must be a multiple of n_kv_heads")
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = torch.bfloat16
+        self.w = weights if weights is not None else self._init_weights(seed)
+        c = cfg
+        kv_shape = (c.layers, c.max_batch, c.n_kv_heads, c.max_seq, c.head_dim)
+        self.k_cache = torch.zeros(kv_shape, dtype=self.dtype, device=self.device)
+        self.v_cache = torch.zeros(kv_shape, dtype=self.dtype, device=self.device)
+        self.cos_sin = ops.rope_tables(c.max_seq, c.head_dim, c.rope_theta, device=self.device).contiguous()
+        self.scale = 1.0 / math.sqrt(c.head_dim)
+        splits = max(1, math.ceil(c.max_seq / 256))
+        n = c.max_batch * c.n_heads * splits
+        self.attn_ws = (torch.empty(n * c.head_dim, dtype=torch.float32, device=self.device),
+                        torch.empty(n * 2, dtype=torch.float32, device=self.device))
+
+    # ------------------------------------------------------------ weights
+    def _init_weights(self, seed: int) -> Dict[str, torch.Tensor]:
+        c = self.cfg
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(seed)
+
+        def rnd(*shape, std=0.02):
+            t = torch.empty(shape, dtype=torch.float32, device=self.device)
+            t.normal_(0.0, std, generator=gen)
+            return t.to(self.dtype)
+
+        def ones(n):
+            return torch.ones(n, dtype=self.dtype, device=self.device)
+
+        w: Dict[str, torch.Tensor] = {"embed": rnd(c.vocab_size, c.hidden, std=1.0),
+                                      "norm_f": ones(c.hidden), "lm_head": rnd(c.vocab_size, c.hidden)}
+        out_std = 0.02 / math.sqrt(2 * c.layers)
+        for i in range(c.layers):
+            w[f"l{i}.ln1"] = ones(c.hidden)
+            w[f"l{i}.ln2"] = ones(c.hidden)
+            w[f"l{i}.wqkv"] = rnd(c.qkv_dim, c.hidden)
+            w[f"l{i}.wo"] = rnd(c.hidden, c.n_heads * c.head_dim, std=out_std)
+            w[f"l{i}.wgu"] = rnd(2 * c.intermediate, c.hidden)
+            w[f"l{i}.wdown"] = rnd(c.hidden, c.intermediate, std=out_std)
+        return w
+
+    @classmethod
+    def load_safetensors(cls, path: str, device: str = "cuda", **cfg_overrides) -> "LocalLM":
+        """Loads a Llama-format checkpoint directory (config.json + *.safetensors)."""
+        from safetensors.torch import load_file
+        with open(os.path.join(path, "config.json")) as f:
+            hf = json.load(f)
+        heads = hf["num_attention_heads"]
+        cfg = LMConfig(name=os.path.basename(path.rstrip("/")), vocab_size=hf["vocab_size"],
+                       hidden=hf["hidden_size"], layers=hf["num_hidden_layers"], n_heads=heads,
+                       n_kv_heads=hf.get("num_key_value_heads", heads),
+                       head_dim=hf.get("head_dim", hf["hidden_size"] // heads),
+                       intermediate=hf["intermediate_size"], rope_theta=hf.get("rope_theta", 10000.0),
+                       eps=hf.get("rms_norm_eps", 1e-5))
+        cfg = replace(cfg, **cfg_overrides)
+        raw: Dict[str, torch.Tensor] = {}
+        for fn in sorted(os.listdir(path)):
+            if fn.endswith(".safetensors"):
+                raw.update(load_file(os.path.join(path, fn), device="cpu"))
+        dev = torch.device(device)
+
+        def g(k):
+            return raw[k].to(dtype=torch.bfloat16, device=dev).contiguous()
+
+        w = {"embed": g("model.embed_tokens.weight"), "norm_f": g("model.norm.weight"),
+             "lm_head": g("lm_head.weight") if "lm_head.weight" in raw else g("model.embed_tokens.weight")}
+        for i in range(cfg.layers):
+            p = f"model.layers.{i}."
+            w[f"l{i}.ln1"] = g(p + "input_layernorm.weight")
+            w[f"l{i}.ln2"] = g(p + "post_attention_layernorm.weight")
+            w[f"l{i}.wqkv"] = torch.cat([g(p + "self_attn.q_proj.weight"), g(p + "self_attn.k_proj.weight"),
+                                         g(p + "self_attn.v_proj.weight")], 0).contiguous()
+            w[f"l{i}.wo"] = g(p + "self_attn.o_proj.weight")
+            w[f"l{i}.wgu"] = torch.cat([g(p + "mlp.gate_proj.weight"), g(p + "mlp.up_proj.weight")], 0).contiguous()
+            w[f"l{i}.wdown"] = g(p + "mlp.down_proj.weight")
+        return cls(cfg, device, weights=w)
+
+    # ------------------------------------------------------------ forward
+    def _mlp(self, i: int, h: torch.Tensor) -> torch.Tensor:
+        gu = F.linear(h, self.w[f"l{i}.wgu"])
+        return F.linear(ops.silu_mul(gu), self.w[f"l{i}.wdown"])
+
+    @torch.inference_mode()
+    def forward_tokens(self, tokens: torch.Tensor, slot: int, start_pos: int) -> torch.Tensor:
+        """Prefill (start_pos == 0) or extend one sequence by ``T`` tokens.
+
+        Writes K/V for positions [start_pos, start_pos+T) into ``slot`` and
+        returns the last position's logits ``[vocab]`` (bf16)."""
+        c = self.cfg
+        T = int(tokens.numel())
+        if T == 0:
+            raise ValueError("forward_tokens needs at least one token")
+        if not (0 <= slot < c.max_batch) or start_pos < 0 or start_pos + T > c.max_seq:
+            raise ValueError(f"sequence does not fit: slot={slot} start={start_pos} T={T} max_seq={c.max_seq}")
+        dev = self.device
+        ids = tokens.to(device=dev, dtype=torch.int32).contiguous()
+        pos = torch.arange(start_pos, start_pos + T, dtype=torch.int32, device=dev)
+        slots = torch.full((T,), slot, dtype=torch.int32, device=dev)
+        x = ops.embedding(self.w["embed"], ids)
+        resid = x.clone()
+        h = ops.add_rmsnorm(x, self.w["l0.ln1"], c.eps)
+        L = start_pos + T
+        if start_pos > 0:
+            qi = torch.arange(start_pos, L, device=dev)[:, None]
+            kj = torch.arange(L, device=dev)[None, :]
+            mask = kj <= qi
+        for i in range(c.layers):
+            kc, vc = self.k_cache[i], self.v_cache[i]
+            qkv = F.linear(h, self.w[f"l{i}.wqkv"])
+            q = ops.rope_kv(qkv, pos, slots, self.cos_sin, kc, vc, c.n_heads)  # [T, Hq, D]
+            k = kc[slot, :, :L].unsqueeze(0)  # [1, Hkv, L, D]
+            v = vc[slot, :, :L].unsqueeze(0)
+            qh = q.transpose(0, 1).unsqueeze(0)  # [1, Hq, T, D]
+            if start_pos == 0:
+                att = F.scaled_dot_product_attention(qh, k, v, is_causal=True, enable_gqa=True)
+            else:
+                att = F.scaled_dot_product_attention(qh, k, v, attn_mask=mask, enable_gqa=True)
+            o = F.linear(att[0].transpose(0, 1).reshape(T, c.n_heads * c.head_dim), self.w[f"l{i}.wo"])
+            h = ops.add_rmsnorm(o, self.w[f"l{i}.ln2"], c.eps, residual=resid)
+            m = self._mlp(i, h)
+            nxt = self.w[f"l{i + 1}.ln1"] if i + 1 < c.layers else self.w["norm_f"]
+            h = ops.add_rmsnorm(m, nxt, c.eps, residual=resid)
+        return F.linear(h[-1:], self.w["lm_head"])[0]
+
+    @torch.inference_mode()
+    def decode(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:
+        """One token for each of B sequences. All inputs int32 [B] on device.
+
+        Returns logits [B, vocab] (bf16).  Capturable into a hipGraph."""
+        c = self.cfg
+        B = tokens.shape[0]
+        seq_len = positions + 1
+        x = ops.embedding(self.w["embed"], tokens)
+        resid = x.clone()
+        h = ops.add_rmsnorm(x, self.w["l0.ln1"], c.eps)
+        for i in range(c.layers):
+            kc, vc = self.k_cache[i], self.v_cache[i]
+            qkv = F.linear(h, self.w[f"l{i}.wqkv"])
+            q = ops.rope_kv(qkv, positions, slots, self.cos_sin, kc, vc, c.n_heads)
+            att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws)
+            o = F.linear(att.view(B, c.n_heads * c.head_dim), self.w[f"l{i}.wo"])
+            h = ops.add_rmsnorm(o, self.w[f"l{i}.ln2"], c.eps, residual=resid)
+            m = self._mlp(i, h)
+            nxt = self.w[f"l{i + 1}.ln1"] if i + 1 < c.layers else self.w["norm_f"]
+            h = ops.add_rmsnorm(m, nxt, c.eps, residual=resid)
+        return F.linear(h, self.w["lm_head"])
+
+    # reference path (pure torch, fp32 math) for numerics tests
+    @torch.inference_mode()
+    def reference_logits(self, tokens: Sequence[int]) -> torch.Tensor:
+        c = self.cfg
+        dev = self.device
+        w = {k: v.float() for k, v in self.w.items()}
+        ids = torch.tensor(list(tokens), dtype=torch.long, device=dev)
+        T = ids.numel()
+        x = w["embed"][ids]
+
+        def rms(t, g):
+            return t * torch.rsqrt(t.pow(2).mean(-1, keepdim=True) + c.eps) * g
+
+        pos = torch.arange(T, device=dev, dtype=torch.int32)
+        cs = self.cos_sin
+        G = c.n_heads // c.n_kv_heads
+        for i in range(c.layers):
+            h = rms(x, w[f"l{i}.ln1"])
+            qkv = h @ w[f"l{i}.wqkv"].t()
+            qkv = qkv.view(T, c.n_heads + 2 * c.n_kv_heads, c.head_dim)
+            q = ops.reference.apply_rope(qkv[:, :c.n_heads], pos, cs)
+            k = ops.reference.apply_rope(qkv[:, c.n_heads:c.n_heads + c.n_kv_heads], pos, cs)
+            v = qkv[:, c.n_heads + c.n_kv_heads:]
+            k = k.repeat_interleave(G, dim=1)
+            v = v.repeat_interleave(G, dim=1)
+            att = torch.einsum("thd,shd->hts", q, k) * self.scale
+            att = att.masked_fill(torch.triu(torch.ones(T, T, dtype=torch.bool, device=dev), 1), float("-inf"))
+            o = torch.einsum("hts,shd->thd", torch.softmax(att, -1), v).reshape(T, -1)
+            x = x + o @ w[f"l{i}.wo"].t()
+            h = rms(x, w[f"l{i}.ln2"])
+            gu = h @ w[f"l{i}.wgu"].t()
+            g_, u_ = gu[:, :c.intermediate], gu[:, c.intermediate:]
+            x = x + (F.silu(g_) * u_) @ w[f"l{i}.wdown"].t()
+        return rms(x, w["norm_f"]) @ w["lm_head"].t()
+
+
+class DecodeGraphs:
+    """hipGraph-captured decode steps, one graph per batch-size bucket.
+
+    Static int32 input buffers are filled with ``copy_`` before each replay;
+    the returned logits tensor is the graph's static output (read it before
+    the next replay of the same bucket)."""
+
+    def __init__(self, model: LocalLM, buckets: Sequence[int] = (1, 2, 4, 8, 16, 32, 64, 128, 256)) -> None:
+        self.model = model
+        self.buckets = sorted(b for b in buckets if b <= model.cfg.max_batch)
+        self.graphs: Dict[int, tuple] = {}
+        self.enabled = model.device.type == "cuda"
+
+    def bucket_for(self, n: int) -> int:
+        for b in self.buckets:
+            if b >= n:
+                return b
+        return n
+
+    def _capture(self, b: int):
+        m = self.model
+        dev = m.device
+        tok = torch.zeros(b, dtype=torch.int32, device=dev)
+        # padded entries point at slot -1: the kernels skip them (no KV write, no read)
+        slots = torch.full((b,), -1, dtype=torch.int32, device=dev)
+        pos = torch.zeros(b, dtype=torch.int32, device=dev)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm up hipBLASLt heuristics / allocator outside capture
+                m.decode(tok, slots, pos)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            logits = m.decode(tok, slots, pos)
+        self.graphs[b] = (g, tok, slots, pos, logits)
+
+    @torch.inference_mode()
+    def run(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:
+        n = tokens.shape[0]
+        if not self.enabled or n > self.buckets[-1]:
+            return self.model.decode(tokens, slots, positions)
+        b = self.bucket_for(n)
+        if b not in self.graphs:
+            self._capture(b)
+        g, tok, sl, ps, logits = self.graphs[b]
+        tok[:n].copy_(tokens)
+        sl[:n].copy_(slots)
+        ps[:n].copy_(positions)
+        if n < b:
+            sl[n:].fill_(-1)
+            ps[n:].zero_()
+        g.replay()
+        return logits[:n]

@@ -1,1 +1,48 @@
+"""Device ops for the local enrichment model.
 
+GPU (HIP) tensors run the hand-written gfx950 kernels of
+``dmcp/ops/csrc/dmcp_kernels.hip`` (loaded from the in-tree ``_hipops.so``;
+a missing library is an error, never a silent fallback).  CPU tensors run
+the fp32 PyTorch references in :mod:`dmcp.ops.reference` -- that path only
+exists for GPU-less unit tests.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import reference
+
+
+def _hip():
+    from . import hip
+    return hip
+
+
+def add_rmsnorm(x, weight, eps, residual=None, out=None):
+    return (_hip() if x.is_cuda else reference).add_rmsnorm(x, weight, eps, residual, out)
+
+
+def rope_kv(qkv, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out=None):
+    return (_hip() if qkv.is_cuda else reference).rope_kv(qkv, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out)
+
+
+def decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace=None, chunk: int = 256, out=None):
+    mod = _hip() if q.is_cuda else reference
+    return mod.decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace, chunk, out)
+
+
+def silu_mul(gate_up, out=None):
+    return (_hip() if gate_up.is_cuda else reference).silu_mul(gate_up, out)
+
+
+def masked_argmax(logits, mask=None, vocab: Optional[int] = None, out=None):
+    return (_hip() if logits.is_cuda else reference).masked_argmax(logits, mask, vocab, out)
+
+
+def embedding(table, ids, out=None):
+    return (_hip() if table.is_cuda else reference).embedding(table, ids, out)
+
+
+rope_tables = reference.rope_tables

@@ -1,0 +1,54 @@
+"""Builds the gfx950 HIP kernel library ``dmcp/ops/_hipops.so`` in-tree.
+
+``hipcc --offload-arch=gfx950`` cross-compiles on a GPU-less host, so the
+artefact is produced here and travels with the repository snapshot to the
+MI355X box.  No torch headers are involved (plain HIP + ctypes ABI), which
+keeps the build to a few seconds.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import shutil
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "csrc", "dmcp_kernels.hip")
+TARGET = os.path.join(HERE, "_hipops.so")
+STAMP = TARGET + ".stamp"
+ARCH = os.environ.get("DMCP_HIP_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-Wall",
+         "-Wno-unused-function", "-munsafe-fp-atomics"]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm is required to build dmcp HIP kernels)")
+
+
+def _key() -> str:
+    h = hashlib.sha256(" ".join(FLAGS).encode())
+    with open(SRC, "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def build(force: bool = False) -> str:
+    key = _key()
+    if not force and os.path.exists(TARGET) and os.path.exists(STAMP) and open(STAMP).read().strip() == key:
+        return TARGET
+    tmp = TARGET + ".tmp"
+    cmd = [hipcc(), *FLAGS, "-o", tmp, SRC]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stdout}")
+    os.replace(tmp, TARGET)
+    with open(STAMP, "w") as f:
+        f.write(key)
+    return TARGET
+
+
+if __name__ == "__main__":
+    print(build(force=True))

@@ -1,0 +1,529 @@
+// dmcp HIP kernels for gfx950 (MI355X, CDNA4) -- the hot ops of the local
+// enrichment model's decode/serve loop (dmcp/models/llm.py).
+//
+// Design rules followed (cdna_hip_programming.md): 64-lane waves, 256-thread
+// blocks, every bf16 global access vectorized to 16 B (uint4) or 8 B (uint2)
+// per lane (Guideline 13), fp32 accumulation, wave reductions with
+// __shfl_xor over 64 lanes + one LDS hop across the 4 waves, RoPE from a
+// host-precomputed cos/sin table (Appendix B), decode attention with K/V
+// streamed straight to VGPRs (the 'GEMV / M <= 16' row: no LDS round trip),
+// split-K over the sequence so B*Hkv*splits fills 256 CUs, and no
+// allocation / synchronisation inside any launch function so every call can
+// be captured into a hipGraph (Guideline 9).
+//
+// ABI: extern "C" launchers taking raw device pointers and a hipStream_t;
+// they return hipError_t (0 = success).  Shapes are validated on the host
+// side (dmcp/ops/hip.py) before any launch.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(uint16_t v) {
+    return __uint_as_float(((uint32_t)v) << 16);
+}
+
+// round-to-nearest-even fp32 -> bf16 (NaN kept quiet)
+__device__ __forceinline__ uint16_t f2bf(float f) {
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+    f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+    f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+    f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+    f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+    uint4 v;
+    v.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
+    v.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
+    v.z = (uint32_t)f2bf(f[4]) | ((uint32_t)f2bf(f[5]) << 16);
+    v.w = (uint32_t)f2bf(f[6]) | ((uint32_t)f2bf(f[7]) << 16);
+    return v;
+}
+
+__device__ __forceinline__ void unpack4(const uint2& v, float* f) {
+    f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+    f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint2 pack4(const float* f) {
+    uint2 v;
+    v.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
+    v.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
+    return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, kWave);
+    return v;
+}
+
+// --------------------------------------------------------------------------
+// 1. fused residual-add + RMSNorm:  h = x (+ residual);  residual <- h;
+//    out = h * rsqrt(mean(h^2) + eps) * w.  One block per row, VPT 16-B
+//    vectors per thread (H <= 256 * 8 * VPT).
+// --------------------------------------------------------------------------
+template <int VPT>
+__global__ __launch_bounds__(kBlock) void add_rmsnorm_kernel(const uint16_t* __restrict__ x,
+                                                            uint16_t* __restrict__ residual,
+                                                            const uint16_t* __restrict__ w,
+                                                            uint16_t* __restrict__ out, int H, float eps) {
+    const int row = blockIdx.x;
+    const int nvec = H >> 3;
+    const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)row * H);
+    uint4* rr = residual ? reinterpret_cast<uint4*>(residual + (size_t)row * H) : nullptr;
+    float h[VPT][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int idx = threadIdx.x + i * kBlock;
+        if (idx < nvec) {
+            unpack8(xr[idx], h[i]);
+            if (rr) {
+                float r[8];
+                unpack8(rr[idx], r);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) h[i][j] += r[j];
+                uint4 packed = pack8(h[i]);
+                rr[idx] = packed;
+                unpack8(packed, h[i]);  // normalise the bf16-rounded stream (matches torch)
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ss += h[i][j] * h[i][j];
+        }
+    }
+    __shared__ float red[kBlock / kWave];
+    ss = wave_sum(ss);
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int k = 0; k < kBlock / kWave; ++k) tot += red[k];
+    const float inv = rsqrtf(tot / (float)H + eps);
+    const uint4* wr = reinterpret_cast<const uint4*>(w);
+    uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * H);
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int idx = threadIdx.x + i * kBlock;
+        if (idx < nvec) {
+            float wf[8], o[8];
+            unpack8(wr[idx], wf);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = h[i][j] * inv * wf[j];
+            orow[idx] = pack8(o);
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
+// 2. RoPE (rotate-half) on q and k of a fused QKV row + KV-cache append.
+//    qkv  [T, (Hq + 2 Hkv) * D]  ->  q_out [T, Hq, D]
+//    k/v cache [S, Hkv, MAXS, D] written at (slot[t], :, pos[t], :)
+//    cos_sin [max_pos, D/2] float2 (cos, sin)
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void rope_kv_kernel(const uint16_t* __restrict__ qkv,
+                                                        const int32_t* __restrict__ pos,
+                                                        const int32_t* __restrict__ slot,
+                                                        const float2* __restrict__ cos_sin,
+                                                        uint16_t* __restrict__ q_out,
+                                                        uint16_t* __restrict__ k_cache,
+                                                        uint16_t* __restrict__ v_cache, int Hq, int Hkv,
+                                                        int D, int max_seq, int max_pos, int num_slots) {
+    const int t = blockIdx.x;
+    const int p = pos[t];
+    const int s = slot[t];
+    const bool write_cache = (p >= 0 && p < max_seq && s >= 0 && s < num_slots);
+    const int half = D >> 1;
+    const int quads = half >> 2;  // groups of 4 rotary pairs
+    const size_t row = (size_t)t * (size_t)(Hq + 2 * Hkv) * D;
+    const float2* cs = cos_sin + (size_t)min(max(p, 0), max_pos - 1) * half;
+    const int units = (Hq + Hkv) * quads;
+    for (int u = threadIdx.x; u < units; u += kBlock) {
+        const int hh = u / quads;
+        const int d0 = (u - hh * quads) * 4;
+        const uint16_t* src = qkv + row + (size_t)hh * D;
+        float x1[4], x2[4], o1[4], o2[4];
+        unpack4(*reinterpret_cast<const uint2*>(src + d0), x1);
+        unpack4(*reinterpret_cast<const uint2*>(src + half + d0), x2);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float2 c = cs[d0 + j];
+            o1[j] = x1[j] * c.x - x2[j] * c.y;
+            o2[j] = x2[j] * c.x + x1[j] * c.y;
+        }
+        uint16_t* dst;
+        if (hh < Hq) {
+            dst = q_out + ((size_t)t * Hq + hh) * D;
+        } else {
+            if (!write_cache) continue;
+            dst = k_cache + (((size_t)s * Hkv + (hh - Hq)) * max_seq + p) * D;
+        }
+        *reinterpret_cast<uint2*>(dst + d0) = pack4(o1);
+        *reinterpret_cast<uint2*>(dst + half + d0) = pack4(o2);
+    }
+    if (!write_cache) return;
+    const int vvec = (Hkv * D) >> 3;
+    const uint4* vsrc = reinterpret_cast<const uint4*>(qkv + row + (size_t)(Hq + Hkv) * D);
+    for (int u = threadIdx.x; u < vvec; u += kBlock) {
+        const int e = u << 3;
+        const int kh = e / D;
+        const int d = e - kh * D;
+        uint16_t* dst = v_cache + (((size_t)s * Hkv + kh) * max_seq + p) * D + d;
+        *reinterpret_cast<uint4*>(dst) = vsrc[u];
+    }
+}
+
+// --------------------------------------------------------------------------
+// 3. decode attention (one query token per sequence), GQA, split-K.
+//    q [B, Hq, D] bf16; k/v cache [S, Hkv, MAXS, D]; slot[B]; seq_len[B]
+//    grid (splits, Hkv, B); block 256 = 4 waves.  LPK = D/8 lanes share one
+//    key row (16 B each), KPW = 64/LPK keys per wave step.  Each lane group
+//    runs an online softmax over its keys for the G query heads of this kv
+//    head; groups merge by shuffles, waves through LDS, splits in a second
+//    kernel (or directly when splits == 1).
+// --------------------------------------------------------------------------
+template <int D, int G>
+__global__ __launch_bounds__(kBlock) void decode_attn_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache,
+    const int32_t* __restrict__ slot, const int32_t* __restrict__ seq_len, uint16_t* __restrict__ out,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int max_seq, int chunk, int splits,
+    float scale_log2, int num_slots) {
+    constexpr int LPK = D / 8;
+    constexpr int KPW = kWave / LPK;
+    constexpr int NW = kBlock / kWave;
+    const int split = blockIdx.x, kh = blockIdx.y, b = blockIdx.z;
+    const int Hq = Hkv * G;
+    const int s = slot[b];
+    const int L = (s >= 0 && s < num_slots) ? min(seq_len[b], max_seq) : 0;  // never read a bad slot
+    const int start = split * chunk;
+    const int end = min(L, start + chunk);
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    const int kig = lane / LPK;  // key slot within the wave step
+    const int sub = lane % LPK;  // which 8 dims
+
+    float qv[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const uint16_t* qp = q + ((size_t)b * Hq + (size_t)kh * G + g) * D + sub * 8;
+        unpack8(*reinterpret_cast<const uint4*>(qp), qv[g]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qv[g][j] *= scale_log2;
+    }
+    float m[G], l[G], acc[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        m[g] = -1e30f;
+        l[g] = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
+    }
+    const size_t head_off = ((size_t)(L > 0 ? s : 0) * Hkv + kh) * (size_t)max_seq * D;
+    const uint16_t* kb = k_cache + head_off + sub * 8;
+    const uint16_t* vb = v_cache + head_off + sub * 8;
+    constexpr int STEP = NW * KPW;
+    for (int k0 = start + wave * KPW; k0 < end; k0 += 2 * STEP) {
+        const int ka = k0 + kig;
+        const int kb2 = ka + STEP;
+        const bool va = ka < end, vb2 = kb2 < end;
+        uint4 kra = make_uint4(0, 0, 0, 0), krb = make_uint4(0, 0, 0, 0);
+        uint4 vra = make_uint4(0, 0, 0, 0), vrb = make_uint4(0, 0, 0, 0);
+        if (va) {
+            kra = *reinterpret_cast<const uint4*>(kb + (size_t)ka * D);
+            vra = *reinterpret_cast<const uint4*>(vb + (size_t)ka * D);
+        }
+        if (vb2) {
+            krb = *reinterpret_cast<const uint4*>(kb + (size_t)kb2 * D);
+            vrb = *reinterpret_cast<const uint4*>(vb + (size_t)kb2 * D);
+        }
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const bool valid = r == 0 ? va : vb2;
+            float kf[8], vf[8];
+            unpack8(r == 0 ? kra : krb, kf);
+            unpack8(r == 0 ? vra : vrb, vf);
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                float d = 0.f;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) d += qv[g][j] * kf[j];
+#pragma unroll
+                for (int msk = 1; msk < LPK; msk <<= 1) d += __shfl_xor(d, msk, kWave);
+                const float sc = valid ? d : -1e30f;
+                const float mn = fmaxf(m[g], sc);
+                const float corr = exp2f(m[g] - mn);
+                const float pr = valid ? exp2f(sc - mn) : 0.f;
+                l[g] = l[g] * corr + pr;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[g][j] = acc[g][j] * corr + pr * vf[j];
+                m[g] = mn;
+            }
+        }
+    }
+    // merge the KPW key groups of this wave (lanes differing in kig)
+#pragma unroll
+    for (int msk = LPK; msk < kWave; msk <<= 1) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const float mo = __shfl_xor(m[g], msk, kWave);
+            const float lo = __shfl_xor(l[g], msk, kWave);
+            const float mn = fmaxf(m[g], mo);
+            const float ca = exp2f(m[g] - mn), cb = exp2f(mo - mn);
+            l[g] = l[g] * ca + lo * cb;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float ao = __shfl_xor(acc[g][j], msk, kWave);
+                acc[g][j] = acc[g][j] * ca + ao * cb;
+            }
+            m[g] = mn;
+        }
+    }
+    // merge the waves through LDS: lanes [0, LPK) of each wave hold the result
+    __shared__ float sm_m[NW][G], sm_l[NW][G];
+    __shared__ float sm_acc[NW][G][D];
+    if (lane < LPK) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            if (sub == 0) {
+                sm_m[wave][g] = m[g];
+                sm_l[wave][g] = l[g];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sm_acc[wave][g][sub * 8 + j] = acc[g][j];
+        }
+    }
+    __syncthreads();
+    // G*D outputs, one per thread (G*D <= 1024 -> up to 4 per thread)
+    for (int o = threadIdx.x; o < G * D; o += kBlock) {
+        const int g = o / D, d = o - g * D;
+        float mx = -1e30f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) mx = fmaxf(mx, sm_m[w][g]);
+        float lt = 0.f, at = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const float c = exp2f(sm_m[w][g] - mx);
+            lt += sm_l[w][g] * c;
+            at += sm_acc[w][g][d] * c;
+        }
+        const int qh = kh * G + g;
+        if (splits == 1) {
+            out[((size_t)b * Hq + qh) * D + d] = f2bf(lt > 0.f ? at / lt : 0.f);
+        } else {
+            const size_t pi = ((size_t)b * Hq + qh) * splits + split;
+            part_o[pi * D + d] = at;
+            if (d == 0) {
+                part_ml[pi * 2] = mx;
+                part_ml[pi * 2 + 1] = lt;
+            }
+        }
+    }
+}
+
+// combine split-K partials: one block per (b, q head), D threads
+__global__ __launch_bounds__(kBlock) void decode_attn_combine_kernel(const float* __restrict__ part_o,
+                                                                    const float* __restrict__ part_ml,
+                                                                    uint16_t* __restrict__ out, int D,
+                                                                    int splits) {
+    const size_t bh = blockIdx.x;
+    const float* ml = part_ml + bh * splits * 2;
+    float mx = -1e30f;
+    for (int s = 0; s < splits; ++s) mx = fmaxf(mx, ml[s * 2]);
+    for (int d = threadIdx.x; d < D; d += kBlock) {
+        float lt = 0.f, at = 0.f;
+        for (int s = 0; s < splits; ++s) {
+            const float c = exp2f(ml[s * 2] - mx);
+            lt += ml[s * 2 + 1] * c;
+            at += part_o[(bh * splits + s) * D + d] * c;
+        }
+        out[bh * D + d] = f2bf(lt > 0.f ? at / lt : 0.f);
+    }
+}
+
+// --------------------------------------------------------------------------
+// 4. SwiGLU activation: out[t, i] = silu(gu[t, i]) * gu[t, I + i]
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void silu_mul_kernel(const uint16_t* __restrict__ gu,
+                                                         uint16_t* __restrict__ out, int T, int I) {
+    const int vpr = I >> 3;
+    const size_t total = (size_t)T * vpr;
+    for (size_t u = (size_t)blockIdx.x * kBlock + threadIdx.x; u < total; u += (size_t)gridDim.x * kBlock) {
+        const size_t t = u / vpr;
+        const int c = (int)(u - t * vpr) << 3;
+        const uint16_t* row = gu + t * (size_t)(2 * I);
+        float g[8], up[8], o[8];
+        unpack8(*reinterpret_cast<const uint4*>(row + c), g);
+        unpack8(*reinterpret_cast<const uint4*>(row + I + c), up);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = g[j] / (1.f + __expf(-g[j])) * up[j];
+        *reinterpret_cast<uint4*>(out + t * (size_t)I + c) = pack8(o);
+    }
+}
+
+// --------------------------------------------------------------------------
+// 5. masked greedy sampling: ids[b] = argmax_{v allowed} logits[b, v]
+//    mask [B, ceil(V/32)] uint32 bit-set of allowed tokens (nullptr = all).
+//    Ties resolve to the smallest index.
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void masked_argmax_kernel(const uint16_t* __restrict__ logits,
+                                                              const uint32_t* __restrict__ mask,
+                                                              int32_t* __restrict__ ids, int V, int ld) {
+    const int b = blockIdx.x;
+    const uint16_t* row = logits + (size_t)b * ld;
+    const uint32_t* mrow = mask ? mask + (size_t)b * ((V + 31) >> 5) : nullptr;
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int v = threadIdx.x; v < V; v += kBlock) {
+        if (mrow && !((mrow[v >> 5] >> (v & 31)) & 1u)) continue;
+        const float x = bf2f(row[v]);
+        if (x > best || (x == best && v < bi)) { best = x; bi = v; }
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const float ob = __shfl_xor(best, m, kWave);
+        const int oi = __shfl_xor(bi, m, kWave);
+        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    __shared__ float sb[kBlock / kWave];
+    __shared__ int si[kBlock / kWave];
+    if ((threadIdx.x & (kWave - 1)) == 0) { sb[threadIdx.x / kWave] = best; si[threadIdx.x / kWave] = bi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float B = sb[0];
+        int I = si[0];
+        for (int k = 1; k < kBlock / kWave; ++k)
+            if (sb[k] > B || (sb[k] == B && si[k] < I)) { B = sb[k]; I = si[k]; }
+        ids[b] = (I == 0x7fffffff) ? 0 : I;
+    }
+}
+
+// --------------------------------------------------------------------------
+// 6. embedding gather: out[t, :] = table[clamp(ids[t]), :]
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void embedding_kernel(const uint16_t* __restrict__ table,
+                                                          const int32_t* __restrict__ ids,
+                                                          uint16_t* __restrict__ out, int T, int H, int V) {
+    const int vpr = H >> 3;
+    const size_t total = (size_t)T * vpr;
+    for (size_t u = (size_t)blockIdx.x * kBlock + threadIdx.x; u < total; u += (size_t)gridDim.x * kBlock) {
+        const size_t t = u / vpr;
+        const int c = (int)(u - t * vpr);
+        int id = ids[t];
+        id = id < 0 ? 0 : (id >= V ? V - 1 : id);
+        reinterpret_cast<uint4*>(out + t * (size_t)H)[c] = reinterpret_cast<const uint4*>(table + (size_t)id * H)[c];
+    }
+}
+
+inline int grid_for(size_t work) {
+    size_t g = (work + kBlock - 1) / kBlock;
+    if (g > 2048) g = 2048;  // grid-stride beyond 8 blocks/CU (Guideline 11)
+    return (int)(g == 0 ? 1 : g);
+}
+
+template <int D>
+hipError_t launch_decode_d(int G, dim3 grid, const uint16_t* q, const uint16_t* k, const uint16_t* v,
+                           const int32_t* slot, const int32_t* len, uint16_t* out, float* po, float* pml, int Hkv,
+                           int max_seq, int chunk, int splits, float sl2, int ns, hipStream_t st) {
+    switch (G) {
+        case 1: decode_attn_kernel<D, 1><<<grid, kBlock, 0, st>>>(q, k, v, slot, len, out, po, pml, Hkv, max_seq, chunk, splits, sl2, ns); break;
+        case 2: decode_attn_kernel<D, 2><<<grid, kBlock, 0, st>>>(q, k, v, slot, len, out, po, pml, Hkv, max_seq, chunk, splits, sl2, ns); break;
+        case 4: decode_attn_kernel<D, 4><<<grid, kBlock, 0, st>>>(q, k, v, slot, len, out, po, pml, Hkv, max_seq, chunk, splits, sl2, ns); break;
+        case 8: decode_attn_kernel<D, 8><<<grid, kBlock, 0, st>>>(q, k, v, slot, len, out, po, pml, Hkv, max_seq, chunk, splits, sl2, ns); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+int dmcp_abi_version() { return 1; }
+
+int dmcp_add_rmsnorm(const void* x, void* residual, const void* w, void* out, int rows, int H, float eps,
+                     void* stream) {
+    if (H % 8 != 0 || H > kBlock * 8 * 4 || rows <= 0) return hipErrorInvalidValue;
+    auto st = (hipStream_t)stream;
+    const int vpt = (H + kBlock * 8 - 1) / (kBlock * 8);
+    auto xx = (const uint16_t*)x;
+    auto rr = (uint16_t*)residual;
+    auto ww = (const uint16_t*)w;
+    auto oo = (uint16_t*)out;
+    if (vpt == 1) add_rmsnorm_kernel<1><<<rows, kBlock, 0, st>>>(xx, rr, ww, oo, H, eps);
+    else if (vpt == 2) add_rmsnorm_kernel<2><<<rows, kBlock, 0, st>>>(xx, rr, ww, oo, H, eps);
+    else add_rmsnorm_kernel<4><<<rows, kBlock, 0, st>>>(xx, rr, ww, oo, H, eps);
+    return hipGetLastError();
+}
+
+int dmcp_rope_kv(const void* qkv, const void* pos, const void* slot, const void* cos_sin, void* q_out,
+                 void* k_cache, void* v_cache, int T, int Hq, int Hkv, int D, int max_seq, int max_pos,
+                 int num_slots, void* stream) {
+    if (T <= 0) return 0;
+    if (D % 16 != 0) return hipErrorInvalidValue;
+    rope_kv_kernel<<<T, kBlock, 0, (hipStream_t)stream>>>((const uint16_t*)qkv, (const int32_t*)pos,
+                                                          (const int32_t*)slot, (const float2*)cos_sin,
+                                                          (uint16_t*)q_out, (uint16_t*)k_cache,
+                                                          (uint16_t*)v_cache, Hq, Hkv, D, max_seq, max_pos, num_slots);
+    return hipGetLastError();
+}
+
+int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cache, const void* slot,
+                          const void* seq_len, void* out, void* part_o, void* part_ml, int B, int Hq, int Hkv,
+                          int D, int max_seq, int num_slots, int chunk, int splits, float scale, void* stream) {
+    if (B <= 0) return 0;
+    if (Hkv <= 0 || Hq % Hkv != 0 || splits <= 0 || chunk <= 0) return hipErrorInvalidValue;
+    const int G = Hq / Hkv;
+    const float sl2 = scale * 1.4426950408889634f;
+    dim3 grid(splits, Hkv, B);
+    auto st = (hipStream_t)stream;
+    hipError_t e;
+    if (D == 64)
+        e = launch_decode_d<64>(G, grid, (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
+                                (const int32_t*)slot, (const int32_t*)seq_len, (uint16_t*)out, (float*)part_o,
+                                (float*)part_ml, Hkv, max_seq, chunk, splits, sl2, num_slots, st);
+    else if (D == 128)
+        e = launch_decode_d<128>(G, grid, (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
+                                 (const int32_t*)slot, (const int32_t*)seq_len, (uint16_t*)out, (float*)part_o,
+                                 (float*)part_ml, Hkv, max_seq, chunk, splits, sl2, num_slots, st);
+    else
+        return hipErrorInvalidValue;
+    if (e != hipSuccess || splits == 1) return e;
+    decode_attn_combine_kernel<<<B * Hq, kBlock, 0, st>>>((const float*)part_o, (const float*)part_ml,
+                                                          (uint16_t*)out, D, splits);
+    return hipGetLastError();
+}
+
+int dmcp_silu_mul(const void* gu, void* out, int T, int I, void* stream) {
+    if (I % 8 != 0) return hipErrorInvalidValue;
+    if (T <= 0) return 0;
+    silu_mul_kernel<<<grid_for((size_t)T * (I / 8)), kBlock, 0, (hipStream_t)stream>>>((const uint16_t*)gu,
+                                                                                      (uint16_t*)out, T, I);
+    return hipGetLastError();
+}
+
+int dmcp_masked_argmax(const void* logits, const void* mask, void* ids, int B, int V, int ld, void* stream) {
+    if (B <= 0) return 0;
+    masked_argmax_kernel<<<B, kBlock, 0, (hipStream_t)stream>>>((const uint16_t*)logits, (const uint32_t*)mask,
+                                                               (int32_t*)ids, V, ld);
+    return hipGetLastError();
+}
+
+int dmcp_embedding(const void* table, const void* ids, void* out, int T, int H, int V, void* stream) {
+    if (H % 8 != 0) return hipErrorInvalidValue;
+    if (T <= 0) return 0;
+    embedding_kernel<<<grid_for((size_t)T * (H / 8)), kBlock, 0, (hipStream_t)stream>>>(
+        (const uint16_t*)table, (const int32_t*)ids, (uint16_t*)out, T, H, V);
+    return hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,220 @@
+"""ctypes binding of the gfx950 kernel library + tensor-level wrappers.
+
+Every wrapper validates dtype / device / contiguity / shapes on the host
+*before* launching (a mis-shaped launch can fault the GPU), launches on
+torch's current HIP stream (so calls compose with hipBLASLt GEMMs and can be
+captured into hipGraphs) and raises on any non-zero hipError.
+
+On a GPU box the library MUST load: :func:`lib` raises instead of silently
+falling back to PyTorch.  CPU tensors are routed to :mod:`dmcp.ops.reference`
+by :mod:`dmcp.ops` (CPU unit tests only).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import threading
+from typing import Optional
+
+import torch
+
+from .build import TARGET, build
+
+_lib = None
+_lock = threading.Lock()
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_f = ctypes.c_float
+
+
+class HipOpsError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = TARGET
+        if not os.path.exists(path):
+            if os.environ.get("DMCP_NO_AUTOBUILD"):
+                raise HipOpsError(f"HIP kernel library missing: {path}")
+            path = build()
+        L = ctypes.CDLL(path)
+        sigs = {
+            "dmcp_abi_version": ([], _i),
+            "dmcp_add_rmsnorm": ([_vp, _vp, _vp, _vp, _i, _i, _f, _vp], _i),
+            "dmcp_rope_kv": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp], _i),
+            "dmcp_decode_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _f, _vp],
+                                      _i),
+            "dmcp_silu_mul": ([_vp, _vp, _i, _i, _vp], _i),
+            "dmcp_masked_argmax": ([_vp, _vp, _vp, _i, _i, _i, _vp], _i),
+            "dmcp_embedding": ([_vp, _vp, _vp, _i, _i, _i, _vp], _i),
+        }
+        for name, (args, res) in sigs.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        if L.dmcp_abi_version() != 1:
+            raise HipOpsError("HIP kernel library ABI mismatch; rebuild with python -m dmcp.ops.build")
+        _lib = L
+        return _lib
+
+
+def loaded_path() -> Optional[str]:
+    return TARGET if _lib is not None else None
+
+
+def _stream() -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t: Optional[torch.Tensor]) -> ctypes.c_void_p:
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def _check(rc: int, name: str) -> None:
+    if rc != 0:
+        raise HipOpsError(f"{name} failed with hipError {rc}")
+
+
+def _req(t: torch.Tensor, dtype: torch.dtype, name: str) -> None:
+    if not t.is_cuda:
+        raise HipOpsError(f"{name}: tensor must be on the GPU")
+    if t.dtype != dtype:
+        raise HipOpsError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise HipOpsError(f"{name}: tensor must be contiguous")
+
+
+# ---------------------------------------------------------------- wrappers
+def add_rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    H = x.shape[-1]
+    rows = x.numel() // H
+    _req(x, torch.bfloat16, "add_rmsnorm.x")
+    _req(weight, torch.bfloat16, "add_rmsnorm.weight")
+    if weight.numel() != H or H % 8 or H > 8192:
+        raise HipOpsError(f"add_rmsnorm: unsupported hidden size {H}")
+    if residual is not None:
+        _req(residual, torch.bfloat16, "add_rmsnorm.residual")
+        if residual.shape != x.shape:
+            raise HipOpsError("add_rmsnorm: residual shape mismatch")
+    out = torch.empty_like(x) if out is None else out
+    _req(out, torch.bfloat16, "add_rmsnorm.out")
+    if rows == 0:
+        return out
+    _check(lib().dmcp_add_rmsnorm(_ptr(x), _ptr(residual), _ptr(weight), _ptr(out), rows, H, float(eps), _stream()),
+           "dmcp_add_rmsnorm")
+    return out
+
+
+def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos_sin: torch.Tensor,
+            k_cache: torch.Tensor, v_cache: torch.Tensor, n_q_heads: int, q_out: Optional[torch.Tensor] = None
+            ) -> torch.Tensor:
+    """k_cache/v_cache: [S, Hkv, MAXS, D]; returns q [T, Hq, D]."""
+    S, Hkv, MAXS, D = k_cache.shape
+    T = qkv.shape[0]
+    _req(qkv, torch.bfloat16, "rope_kv.qkv")
+    _req(k_cache, torch.bfloat16, "rope_kv.k_cache")
+    _req(v_cache, torch.bfloat16, "rope_kv.v_cache")
+    _req(pos, torch.int32, "rope_kv.pos")
+    _req(slot, torch.int32, "rope_kv.slot")
+    _req(cos_sin, torch.float32, "rope_kv.cos_sin")
+    if v_cache.shape != k_cache.shape or qkv.shape[1] != (n_q_heads + 2 * Hkv) * D or D % 16:
+        raise HipOpsError("rope_kv: shape mismatch")
+    if pos.numel() != T or slot.numel() != T or cos_sin.shape[-1] != D or cos_sin.shape[0] < 1:
+        raise HipOpsError("rope_kv: pos/slot/cos_sin shape mismatch")
+    max_pos = cos_sin.shape[0]
+    if q_out is None:
+        q_out = torch.empty((T, n_q_heads, D), dtype=torch.bfloat16, device=qkv.device)
+    _req(q_out, torch.bfloat16, "rope_kv.q_out")
+    _check(lib().dmcp_rope_kv(_ptr(qkv), _ptr(pos), _ptr(slot), _ptr(cos_sin), _ptr(q_out), _ptr(k_cache),
+                              _ptr(v_cache), T, n_q_heads, Hkv, D, MAXS, max_pos, S, _stream()), "dmcp_rope_kv")
+    return q_out
+
+
+def decode_splits(max_seq: int, chunk: int = 256) -> int:
+    return max(1, math.ceil(max_seq / chunk))
+
+
+def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: torch.Tensor,
+                     seq_len: torch.Tensor, scale: float, workspace: Optional[tuple] = None,
+                     chunk: int = 256, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """q [B, Hq, D]; caches [S, Hkv, MAXS, D]; slot/seq_len int32 [B]."""
+    B, Hq, D = q.shape
+    S, Hkv, MAXS, Dk = k_cache.shape
+    for t, n in ((q, "q"), (k_cache, "k_cache"), (v_cache, "v_cache")):
+        _req(t, torch.bfloat16, f"decode_attention.{n}")
+    _req(slot, torch.int32, "decode_attention.slot")
+    _req(seq_len, torch.int32, "decode_attention.seq_len")
+    if Dk != D or D not in (64, 128) or Hq % Hkv or (Hq // Hkv) not in (1, 2, 4, 8) or v_cache.shape != k_cache.shape:
+        raise HipOpsError(f"decode_attention: unsupported shape q={tuple(q.shape)} kv={tuple(k_cache.shape)}")
+    if slot.numel() != B or seq_len.numel() != B:
+        raise HipOpsError("decode_attention: slot/seq_len must have B entries")
+    splits = decode_splits(MAXS, chunk)
+    out = torch.empty_like(q) if out is None else out
+    _req(out, torch.bfloat16, "decode_attention.out")
+    if splits > 1:
+        if workspace is None:
+            part_o = torch.empty((B * Hq * splits * D,), dtype=torch.float32, device=q.device)
+            part_ml = torch.empty((B * Hq * splits * 2,), dtype=torch.float32, device=q.device)
+        else:
+            part_o, part_ml = workspace
+            if part_o.numel() < B * Hq * splits * D or part_ml.numel() < B * Hq * splits * 2:
+                raise HipOpsError("decode_attention: workspace too small")
+    else:
+        part_o = part_ml = None
+    _check(lib().dmcp_decode_attention(_ptr(q), _ptr(k_cache), _ptr(v_cache), _ptr(slot), _ptr(seq_len), _ptr(out),
+                                       _ptr(part_o), _ptr(part_ml), B, Hq, Hkv, D, MAXS, S, chunk, splits,
+                                       float(scale), _stream()), "dmcp_decode_attention")
+    return out
+
+
+def silu_mul(gate_up: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _req(gate_up, torch.bfloat16, "silu_mul.gate_up")
+    T = gate_up.numel() // gate_up.shape[-1]
+    I2 = gate_up.shape[-1]
+    if I2 % 16:
+        raise HipOpsError("silu_mul: intermediate size must be a multiple of 8")
+    I = I2 // 2
+    if out is None:
+        out = torch.empty((*gate_up.shape[:-1], I), dtype=torch.bfloat16, device=gate_up.device)
+    _req(out, torch.bfloat16, "silu_mul.out")
+    _check(lib().dmcp_silu_mul(_ptr(gate_up), _ptr(out), T, I, _stream()), "dmcp_silu_mul")
+    return out
+
+
+def masked_argmax(logits: torch.Tensor, mask: Optional[torch.Tensor] = None, vocab: Optional[int] = None,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """logits [B, ld] bf16; mask [B, ceil(V/32)] int32 bitset (None = all)."""
+    _req(logits, torch.bfloat16, "masked_argmax.logits")
+    B, ld = logits.shape
+    V = vocab or ld
+    if V > ld:
+        raise HipOpsError("masked_argmax: vocab larger than row")
+    if mask is not None:
+        _req(mask, torch.int32, "masked_argmax.mask")
+        if mask.shape != (B, (V + 31) // 32):
+            raise HipOpsError(f"masked_argmax: mask shape {tuple(mask.shape)} != {(B, (V + 31) // 32)}")
+    out = torch.empty((B,), dtype=torch.int32, device=logits.device) if out is None else out
+    _req(out, torch.int32, "masked_argmax.out")
+    _check(lib().dmcp_masked_argmax(_ptr(logits), _ptr(mask), _ptr(out), B, V, ld, _stream()), "dmcp_masked_argmax")
+    return out
+
+
+def embedding(table: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _req(table, torch.bfloat16, "embedding.table")
+    _req(ids, torch.int32, "embedding.ids")
+    V, H = table.shape
+    if H % 8:
+        raise HipOpsError("embedding: hidden size must be a multiple of 8")
+    T = ids.numel()
+    out = torch.empty((T, H), dtype=torch.bfloat16, device=table.device) if out is None else out
+    _req(out, torch.bfloat16, "embedding.out")
+    _check(lib().dmcp_embedding(_ptr(table), _ptr(ids), _ptr(out), T, H, V, _stream()), "dmcp_embedding")
+    return out

@@ -1,0 +1,125 @@
+"""Plain-PyTorch fp32 reference implementations of every HIP op.
+
+Used (a) by the numerics tests, which compare each gfx950 kernel against
+these, and (b) for CPU tensors (unit tests on the GPU-less build host).
+Signatures mirror :mod:`dmcp.ops.hip`.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+
+def add_rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    h = x
+    if residual is not None:
+        h = (x.float() + residual.float()).to(x.dtype)
+        residual.copy_(h)
+    hf = h.float()
+    y = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + eps) * weight.float()
+    y = y.to(x.dtype)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def rope_tables(max_pos: int, head_dim: int, theta: float = 10000.0, device=None) -> torch.Tensor:
+    """[max_pos, D/2, 2] float32 (cos, sin) -- viewed as float2 by the kernel."""
+    half = head_dim // 2
+    inv = 1.0 / (theta ** (torch.arange(0, half, dtype=torch.float64) / half))
+    ang = torch.arange(max_pos, dtype=torch.float64)[:, None] * inv[None, :]
+    return torch.stack([ang.cos(), ang.sin()], dim=-1).to(torch.float32).to(device)
+
+
+def apply_rope(x: torch.Tensor, pos: torch.Tensor, cos_sin: torch.Tensor) -> torch.Tensor:
+    """x [T, H, D] -> rotate-half RoPE at positions pos [T] (fp32 math)."""
+    D = x.shape[-1]
+    half = D // 2
+    cs = cos_sin[pos.long().clamp(0, cos_sin.shape[0] - 1)].to(x.device)  # [T, half, 2]
+    c = cs[..., 0][:, None, :]
+    s = cs[..., 1][:, None, :]
+    xf = x.float()
+    x1, x2 = xf[..., :half], xf[..., half:]
+    return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1)
+
+
+def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos_sin: torch.Tensor,
+            k_cache: torch.Tensor, v_cache: torch.Tensor, n_q_heads: int, q_out: Optional[torch.Tensor] = None
+            ) -> torch.Tensor:
+    S, Hkv, MAXS, D = k_cache.shape
+    T = qkv.shape[0]
+    x = qkv.view(T, n_q_heads + 2 * Hkv, D)
+    q = apply_rope(x[:, :n_q_heads], pos, cos_sin).to(qkv.dtype)
+    k = apply_rope(x[:, n_q_heads:n_q_heads + Hkv], pos, cos_sin).to(qkv.dtype)
+    v = x[:, n_q_heads + Hkv:]
+    for t in range(T):
+        p, s = int(pos[t]), int(slot[t])
+        if 0 <= p < MAXS and 0 <= s < S:
+            k_cache[s, :, p] = k[t]
+            v_cache[s, :, p] = v[t]
+    if q_out is not None:
+        q_out.copy_(q)
+        return q_out
+    return q
+
+
+def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: torch.Tensor,
+                     seq_len: torch.Tensor, scale: float, workspace=None, chunk: int = 256,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    B, Hq, D = q.shape
+    S, Hkv, MAXS, _ = k_cache.shape
+    G = Hq // Hkv
+    res = torch.zeros((B, Hq, D), dtype=torch.float32, device=q.device)
+    for b in range(B):
+        s, L = int(slot[b]), min(int(seq_len[b]), MAXS)
+        if not (0 <= s < S) or L <= 0:
+            continue
+        k = k_cache[s, :, :L].float()  # [Hkv, L, D]
+        v = v_cache[s, :, :L].float()
+        qb = q[b].float().view(Hkv, G, D)
+        att = torch.einsum("hgd,hld->hgl", qb, k) * scale
+        p = torch.softmax(att, dim=-1)
+        res[b] = torch.einsum("hgl,hld->hgd", p, v).reshape(Hq, D)
+    y = res.to(q.dtype)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def silu_mul(gate_up: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    I = gate_up.shape[-1] // 2
+    g, u = gate_up[..., :I].float(), gate_up[..., I:].float()
+    y = (torch.nn.functional.silu(g) * u).to(gate_up.dtype)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def masked_argmax(logits: torch.Tensor, mask: Optional[torch.Tensor] = None, vocab: Optional[int] = None,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    B, ld = logits.shape
+    V = vocab or ld
+    x = logits[:, :V].float().clone()
+    if mask is not None:
+        idx = torch.arange(V, device=logits.device)
+        words = mask.to(torch.int64)[:, idx // 32]
+        bits = (words >> (idx % 32)) & 1
+        x[bits == 0] = float("-inf")
+    ids = torch.argmax(x, dim=-1).to(torch.int32)  # first index among ties
+    if out is not None:
+        out.copy_(ids)
+        return out
+    return ids
+
+
+def embedding(table: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    y = table[ids.long().clamp(0, table.shape[0] - 1)]
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y

@@ -118,6 +118,27 @@ END;
     (3, "project_base_package", """
 ALTER TABLE projects ADD COLUMN base_package TEXT;
 """),
+    (4, "drop_redundant_indexes", """
+-- Measured with EXPLAIN QUERY PLAN over every repository statement
+-- (tests/test_store.py::test_query_plans_use_indexes): none of these is the
+-- chosen plan for any query, while each one costs a B-tree insert per row on
+-- the indexing hot path.
+--   idx_source_methods_class        prefix of idx_source_methods_class_name
+--   idx_source_methods_name         no statement filters on method_name alone
+--   idx_source_methods_http_path    endpoint queries use the partial index
+--   idx_source_methods_line         no statement filters on line_number
+--   idx_source_classes_simple_name  no statement filters on simple_name
+--   idx_source_classes_type         breakdown is per project (project_package)
+--   idx_source_classes_project_ordered  duplicate of the UNIQUE(project_id,
+--                                   full_class_name) autoindex on SQLite
+DROP INDEX IF EXISTS idx_source_methods_class;
+DROP INDEX IF EXISTS idx_source_methods_name;
+DROP INDEX IF EXISTS idx_source_methods_http_path;
+DROP INDEX IF EXISTS idx_source_methods_line;
+DROP INDEX IF EXISTS idx_source_classes_simple_name;
+DROP INDEX IF EXISTS idx_source_classes_type;
+DROP INDEX IF EXISTS idx_source_classes_project_ordered;
+"""),
 ]
 
 

@@ -444,6 +444,11 @@ class SourceMethodRepository:
         with self.db.transaction() as c:
             c.execute("DELETE FROM source_methods WHERE class_id = ?", (class_id,))
 
+    def delete_by_project_id(self, project_id: str) -> None:
+        with self.db.transaction() as c:
+            c.execute("DELETE FROM source_methods WHERE class_id IN "
+                      "(SELECT id FROM source_classes WHERE project_id = ?)", (project_id,))
+
     def delete_by_class_ids(self, class_ids: Sequence[str]) -> None:
         if not class_ids:
             return

@@ -1,0 +1,127 @@
+"""Numerics of the gfx950 HIP kernels against plain PyTorch fp32 references."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hip():
+    from dmcp.ops import hip as h
+    h.lib()
+    return h
+
+
+def _bf(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return (torch.randn(*shape, generator=g, device="cuda") * scale).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("H", [256, 2048, 3072, 8192])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_add_rmsnorm(hip, H, with_res):
+    from dmcp.ops import reference
+    x = _bf(37, H, seed=1)
+    w = _bf(H, seed=2)
+    res = _bf(37, H, seed=3) if with_res else None
+    res_ref = res.clone() if with_res else None
+    got = hip.add_rmsnorm(x, w, 1e-5, residual=res)
+    exp = reference.add_rmsnorm(x.float().to(torch.bfloat16), w, 1e-5, residual=res_ref)
+    torch.testing.assert_close(got.float(), exp.float(), atol=3e-2, rtol=2e-2)
+    if with_res:
+        assert torch.equal(res, res_ref)
+
+
+@pytest.mark.parametrize("D,Hq,Hkv", [(64, 32, 8), (128, 24, 8), (64, 4, 4)])
+def test_rope_kv(hip, D, Hq, Hkv):
+    from dmcp.ops import reference
+    T, S, MAXS = 13, 3, 64
+    qkv = _bf(T, (Hq + 2 * Hkv) * D, seed=4)
+    pos = torch.randint(0, MAXS, (T,), dtype=torch.int32, device="cuda")
+    slot = torch.randint(0, S, (T,), dtype=torch.int32, device="cuda")
+    # make (slot, pos) unique so the reference's sequential writes equal the kernel's
+    pos = torch.arange(T, dtype=torch.int32, device="cuda") * 3 % MAXS
+    cs = reference.rope_tables(MAXS, D, device="cuda")
+    kc = torch.zeros(S, Hkv, MAXS, D, dtype=torch.bfloat16, device="cuda")
+    vc = torch.zeros_like(kc)
+    kr, vr = kc.clone(), vc.clone()
+    q = hip.rope_kv(qkv, pos, slot, cs, kc, vc, Hq)
+    qr = reference.rope_kv(qkv, pos, slot, cs, kr, vr, Hq)
+    torch.testing.assert_close(q.float(), qr.float(), atol=2e-2, rtol=1e-2)
+    torch.testing.assert_close(kc.float(), kr.float(), atol=2e-2, rtol=1e-2)
+    assert torch.equal(vc, vr)
+
+
+def test_rope_kv_skips_invalid_slot(hip):
+    from dmcp.ops import reference
+    D, Hq, Hkv, S, MAXS = 64, 4, 2, 2, 16
+    qkv = _bf(2, (Hq + 2 * Hkv) * D)
+    cs = reference.rope_tables(MAXS, D, device="cuda")
+    kc = torch.zeros(S, Hkv, MAXS, D, dtype=torch.bfloat16, device="cuda")
+    vc = torch.zeros_like(kc)
+    hip.rope_kv(qkv, torch.tensor([0, 99], dtype=torch.int32, device="cuda"),
+                torch.tensor([-1, 0], dtype=torch.int32, device="cuda"), cs, kc, vc, Hq)
+    assert kc.abs().sum().item() == 0 and vc.abs().sum().item() == 0
+
+
+@pytest.mark.parametrize("D,Hq,Hkv,MAXS", [(64, 32, 8, 1024), (128, 16, 4, 300), (64, 8, 8, 64), (128, 8, 1, 2048)])
+def test_decode_attention(hip, D, Hq, Hkv, MAXS):
+    from dmcp.ops import reference
+    B, S = 5, 7
+    q = _bf(B, Hq, D, seed=5)
+    kc = _bf(S, Hkv, MAXS, D, seed=6)
+    vc = _bf(S, Hkv, MAXS, D, seed=7)
+    slot = torch.tensor([3, 0, 6, 1, 5], dtype=torch.int32, device="cuda")
+    lens = torch.tensor([1, MAXS, max(1, MAXS // 3), 17 % MAXS + 1, MAXS - 1], dtype=torch.int32, device="cuda")
+    scale = 1 / math.sqrt(D)
+    got = hip.decode_attention(q, kc, vc, slot, lens, scale)
+    exp = reference.decode_attention(q, kc, vc, slot, lens, scale)
+    torch.testing.assert_close(got.float(), exp.float(), atol=2e-2, rtol=2e-2)
+
+
+def test_decode_attention_bad_slot_is_zero(hip):
+    D, Hq, Hkv, MAXS = 64, 8, 2, 128
+    q = _bf(2, Hq, D)
+    kc = _bf(2, Hkv, MAXS, D)
+    got = hip.decode_attention(q, kc, kc.clone(), torch.tensor([-1, 5], dtype=torch.int32, device="cuda"),
+                               torch.tensor([10, 10], dtype=torch.int32, device="cuda"), 0.125)
+    assert got.abs().sum().item() == 0
+
+
+@pytest.mark.parametrize("T,I", [(1, 8192), (33, 512), (7, 1000)])
+def test_silu_mul(hip, T, I):
+    from dmcp.ops import reference
+    gu = _bf(T, 2 * I, seed=8, scale=3)
+    torch.testing.assert_close(hip.silu_mul(gu).float(), reference.silu_mul(gu).float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("V", [320, 32000])
+def test_masked_argmax(hip, V):
+    from dmcp.ops import reference
+    from dmcp.enrich.local import _json_safe_mask
+    B = 9
+    logits = _bf(B, V, seed=9)
+    assert torch.equal(hip.masked_argmax(logits), reference.masked_argmax(logits))
+    mask = torch.tensor([_json_safe_mask(V, b % 2 == 0) for b in range(B)], dtype=torch.int32, device="cuda")
+    got = hip.masked_argmax(logits, mask, vocab=V)
+    exp = reference.masked_argmax(logits, mask, vocab=V)
+    assert torch.equal(got, exp)
+    assert all(0x20 <= int(t) < 0x7F for t in got)
+
+
+def test_embedding(hip):
+    from dmcp.ops import reference
+    table = _bf(320, 2048, seed=10)
+    ids = torch.tensor([0, 5, 319, 7, 7], dtype=torch.int32, device="cuda")
+    assert torch.equal(hip.embedding(table, ids), reference.embedding(table, ids))
+
+
+def test_shape_validation_raises(hip):
+    with pytest.raises(hip.HipOpsError):
+        hip.add_rmsnorm(_bf(2, 100), _bf(100), 1e-5)
+    with pytest.raises(hip.HipOpsError):
+        hip.decode_attention(_bf(1, 6, 64), _bf(1, 4, 8, 64), _bf(1, 4, 8, 64),
+                             torch.zeros(1, dtype=torch.int32, device="cuda"),
+                             torch.ones(1, dtype=torch.int32, device="cuda"), 0.1)

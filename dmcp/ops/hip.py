@@ -127,8 +127,10 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos_sin: t
     _req(cos_sin, torch.float32, "rope_kv.cos_sin")
     if v_cache.shape != k_cache.shape or qkv.shape[1] != (n_q_heads + 2 * Hkv) * D or D % 16:
         raise HipOpsError("rope_kv: shape mismatch")
-    if pos.numel() != T or slot.numel() != T or cos_sin.shape[-1] != D or cos_sin.shape[0] < 1:
-        raise HipOpsError("rope_kv: pos/slot/cos_sin shape mismatch")
+    # cos_sin is [max_pos, D/2, 2] (cos, sin) -- read as float2 by the kernel
+    if pos.numel() != T or slot.numel() != T or cos_sin.dim() != 3 or tuple(cos_sin.shape[1:]) != (D // 2, 2) \
+            or cos_sin.shape[0] < 1:
+        raise HipOpsError(f"rope_kv: pos/slot/cos_sin shape mismatch (cos_sin {tuple(cos_sin.shape)}, D={D})")
     max_pos = cos_sin.shape[0]
     if q_out is None:
         q_out = torch.empty((T, n_q_heads, D), dtype=torch.bfloat16, device=qkv.device)

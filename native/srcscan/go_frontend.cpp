@@ -16,7 +16,10 @@
 // import path (the reference returns only the alias, analyzer.go:461-478, so
 // parameter links almost never matched); generic receivers bind to their base
 // type; `implements` is populated from method-name sets within the module; the
-// walk never skips the project root itself even if its name starts with '.'.
+// walk never skips the project root itself even if its name starts with '.';
+// literal route registrations (gin/echo/chi/fiber verbs, Group prefixes,
+// Go 1.22 "METHOD /path" mux patterns) give handlers a real verb + path, so Go
+// handlers become HTTP endpoints (the reference never reports a path).
 #include <algorithm>
 #include <dirent.h>
 #include <map>
@@ -65,12 +68,22 @@ struct GoInterface {
     std::vector<GoIfaceMethod> methods;
     std::vector<std::string> embedded;
 };
+// A literal route registration `recv.VERB("/path", ..., qual.Handler)`.
+// (Addition: the reference's analyzer only reports ("GET", "") for handlers,
+// which the Java side then treats as "not an endpoint".)
+struct GoRoute {
+    std::string recv, method, path, qualifier, handler;
+};
+struct GoGroup {
+    std::string var, parent, prefix;
+};
 struct GoPackage {
     std::string path, dir, pkg_name, class_type = "OTHER";
     std::vector<std::string> files, imports;
     std::vector<GoStruct> structs;
     std::vector<GoInterface> interfaces;
     std::vector<GoFunc> functions;
+    std::vector<GoRoute> routes;  // group prefixes already applied
     bool entry_point = false;
     bool ok = false;
 };
@@ -107,8 +120,25 @@ struct FileParse {
     std::vector<GoStruct> structs;
     std::vector<GoInterface> interfaces;
     std::vector<GoFunc> funcs;
+    std::vector<GoRoute> routes;
+    std::vector<GoGroup> groups;
     bool has_http_registration = false;
 };
+
+const std::unordered_map<std::string_view, const char*> kRouteVerbs = {
+    {"GET", "GET"},       {"POST", "POST"},   {"PUT", "PUT"},     {"DELETE", "DELETE"}, {"PATCH", "PATCH"},
+    {"HEAD", "HEAD"},     {"OPTIONS", "OPTIONS"}, {"Get", "GET"}, {"Post", "POST"},     {"Put", "PUT"},
+    {"Delete", "DELETE"}, {"Patch", "PATCH"}, {"Head", "HEAD"},   {"Options", "OPTIONS"}, {"Any", "GET"},
+    {"Handle", "GET"},    {"HandleFunc", "GET"}};
+
+std::string join_route(const std::string& prefix, const std::string& path) {
+    if (prefix.empty()) return path;
+    if (path.empty()) return prefix;
+    bool a = prefix.back() == '/', b = path.front() == '/';
+    if (a && b) return prefix + path.substr(1);
+    if (!a && !b) return prefix + "/" + path;
+    return prefix + path;
+}
 
 class GoFileParser {
 public:
@@ -494,9 +524,53 @@ private:
         for (int k = b; k < e; ++k) {
             const Token& tk = t[k];
             if (tk.ident("panic") && P(k + 1, '(') && !(k > 0 && P(k - 1, '.'))) f.has_panic = true;
-            if (tk.is('.') && I(k + 1) && P(k + 2, '(') && kHttpRegistration.count(t[k + 1].text))
+            if (tk.is('.') && I(k + 1) && P(k + 2, '(') && kHttpRegistration.count(t[k + 1].text)) {
                 f.has_http_registration = true;
+                route_call(k);
+            }
         }
+    }
+
+    // `recv.VERB("path", ..., handler)` / `v := recv.Group("prefix")`
+    void route_call(int dot) {
+        int open = dot + 2, close = t[open].match;
+        if (close < 0 || !(open + 1 < close) || t[open + 1].kind != Tok::String) return;
+        std::string recv = (dot > 0 && I(dot - 1)) ? std::string(t[dot - 1].text) : "";
+        std::string_view verb = t[dot + 1].text;
+        std::string path(unquote(t[open + 1].text));
+        if (verb == "Group" || verb == "Route") {
+            // v := r.Group("/api")  (Route with a closure is not followed)
+            if (verb == "Group" && dot >= 3 && (t[dot - 2].is(":=") || t[dot - 2].is('=')) && I(dot - 3))
+                fp_.groups.push_back({std::string(t[dot - 3].text), recv, path});
+            return;
+        }
+        auto vit = kRouteVerbs.find(verb);
+        if (vit == kRouteVerbs.end()) return;
+        std::string method = vit->second;
+        if (verb == "Handle" || verb == "HandleFunc") {
+            // Go 1.22 ServeMux patterns: "POST /items/{id}"
+            size_t sp = path.find(' ');
+            if (sp != std::string::npos && sp > 0 && path[0] != '/') {
+                method = path.substr(0, sp);
+                path = path.substr(sp + 1);
+            }
+        }
+        // last top-level argument = the handler
+        int last = -1;
+        for (int k = open + 1; k < close; k = next(k))
+            if (t[k].is(',')) last = k;
+        if (last < 0) return;
+        int hb = last + 1, he = close;
+        std::string qualifier, handler;
+        for (int k = hb; k < he; ++k) {
+            if (P(k, '(') || P(k, '{')) return;  // call / closure: no named handler
+            if (I(k)) {
+                if (k + 1 < he && t[k + 1].is('.')) qualifier = std::string(t[k].text);
+                else handler = std::string(t[k].text);
+            }
+        }
+        if (handler.empty() || handler == "func") return;
+        fp_.routes.push_back({recv, method, path, qualifier, handler});
     }
 
     int parse_func(int i) {
@@ -679,6 +753,21 @@ void analyze_package(const std::string& root, const std::string& dir, const std:
         for (auto& it : fp.interfaces) pa.interfaces.push_back(std::move(it));
         for (auto& f : fp.funcs) all_funcs.push_back(std::move(f));
         http_reg = http_reg || fp.has_http_registration;
+        // group prefixes are file-local variables: v1 := r.Group("/v1"); v1.GET(...)
+        std::unordered_map<std::string, const GoGroup*> groups;
+        for (auto& g : fp.groups) groups[g.var] = &g;
+        for (auto& r : fp.routes) {
+            GoRoute rr = r;
+            std::string var = r.recv;
+            for (int depth = 0; depth < 16; ++depth) {
+                auto it = groups.find(var);
+                if (it == groups.end()) break;
+                rr.path = join_route(it->second->prefix, rr.path);
+                if (it->second->parent == var) break;
+                var = it->second->parent;
+            }
+            pa.routes.push_back(std::move(rr));
+        }
     }
     pa.imports.assign(imports.begin(), imports.end());
     // bindMethodsToStructs
@@ -778,6 +867,47 @@ struct GoProject {
     std::vector<GoPackage> packages;
 };
 
+// Gives detected handlers (functions with a ResponseWriter / gin.Context /
+// echo.Context / fiber.Ctx parameter) the verb and literal path of the route
+// that registers them.  Candidates are matched by handler name; when several
+// routes share a name, the qualifier (`handler.List`, `userHandler.List`) must
+// match the package name or the receiver type.  Ambiguous handlers keep the
+// reference's ("GET", no path).
+static void bind_routes(std::vector<GoPackage>& pkgs) {
+    std::unordered_map<std::string, std::vector<const GoRoute*>> by_name;
+    for (auto& p : pkgs)
+        for (auto& r : p.routes) by_name[r.handler].push_back(&r);
+    if (by_name.empty()) return;
+    auto bind = [&](GoFunc& f, const GoPackage& p) {
+        if (f.http_method.empty()) return;
+        auto it = by_name.find(f.name);
+        if (it == by_name.end()) return;
+        std::string recv = to_lower(!f.receiver.empty() && f.receiver[0] == '*' ? f.receiver.substr(1) : f.receiver);
+        std::vector<const GoRoute*> c = it->second;
+        if (c.size() > 1) {
+            std::vector<const GoRoute*> keep;
+            for (auto* r : c) {
+                std::string q = to_lower(r->qualifier);
+                if (q.empty()) continue;
+                if (q == to_lower(p.pkg_name) || (!recv.empty() && (q == recv || recv.find(q) != std::string::npos ||
+                                                                    q.find(recv) != std::string::npos)))
+                    keep.push_back(r);
+            }
+            c.swap(keep);
+        }
+        if (c.empty()) return;
+        for (auto* r : c)  // all candidates must agree
+            if (r->method != c[0]->method || r->path != c[0]->path) return;
+        f.http_method = c[0]->method;
+        f.http_path = c[0]->path;
+    };
+    for (auto& p : pkgs) {
+        for (auto& f : p.functions) bind(f, p);
+        for (auto& s : p.structs)
+            for (auto& m : s.methods) bind(m, p);
+    }
+}
+
 static GoProject analyze_go(const std::string& root, int threads) {
     GoProject gp;
     gp.module = read_module_path(root);
@@ -790,6 +920,7 @@ static GoProject analyze_go(const std::string& root, int threads) {
     for (auto& p : pkgs)
         if (p.ok) gp.packages.push_back(std::move(p));
     compute_implements(gp.packages);
+    bind_routes(gp.packages);
     return gp;
 }
 

@@ -31,10 +31,14 @@ for s in $STEPS; do
         enrich) run bench_enrich 900 python bench_enrich.py --classes 256 --batch 64 ;;
         prof)
             ROOT=$(pwd)
-            ( cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/prof" -o enrich \
+            ( cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$ROOT/$OUT/prof" -o enrich \
                 -- python3 "$ROOT/bench_enrich.py" --classes 64 --batch 64 > "$ROOT/$OUT/prof.log" 2>&1 )
             rc=$?
             echo "=== prof rc=$rc"; tail -n 5 "$OUT/prof.log"
+            # keep only the summaries (the raw trace can exceed the 64 MiB copy-back limit)
+            find "$OUT/prof" -type f ! -name '*stats*' -delete 2>/dev/null
+            find "$OUT/prof" -name '*kernel_stats.csv' -exec head -n 40 {} \; 2>/dev/null
             [ $rc -eq 0 ] || exit $rc ;;
     esac
 done

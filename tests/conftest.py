@@ -29,6 +29,31 @@ def tmp_db(tmp_path):
     db.close()
 
 
+def make_app(root, backend=None, **overrides):
+    """An App over a fresh SQLite file with the offline fake enrichment backend."""
+    from dmcp.app import App
+    from dmcp.config import Config
+    from dmcp.enrich.backend import FakeBackend
+    cfg = Config(db_path=str(root / "db.sqlite"), git_clone_base_path=str(root / "clones"),
+                 recover_stuck_on_start=True).merged(overrides)
+    return App(cfg, backend=backend if backend is not None else FakeBackend())
+
+
+@pytest.fixture(scope="module")
+def java_app(tmp_path_factory):
+    """A 16-class Spring repo ("shop") analyzed once with the fake backend."""
+    from dmcp.utils import synth
+    root = tmp_path_factory.mktemp("javaapp")
+    fqcns = synth.java_spring_repo(str(root / "shop"), 16)
+    app = make_app(root)
+    res = app.indexer.analyze_project(str(root / "shop"))
+    assert res.success, res.message
+    app.fqcns = fqcns
+    app.project_id = res.project_id
+    yield app
+    app.close()
+
+
 def pytest_collection_modifyitems(config, items):
     try:
         import torch

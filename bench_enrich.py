@@ -29,6 +29,7 @@ def main(argv=None) -> int:
     ap.add_argument("--max-seq", type=int, default=4096)
     ap.add_argument("--prompt-chars", type=int, default=2048)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-jump", action="store_true", help="disable jump-forward over forced tokens")
     ap.add_argument("--warmup", type=int, default=8)
     args = ap.parse_args(argv)
 
@@ -48,7 +49,7 @@ def main(argv=None) -> int:
         dist.init_process_group("nccl")
     cfg = preset(args.preset, max_batch=args.batch, max_seq=args.max_seq)
     model = LocalLM(cfg, device=f"cuda:{local}", seed=rank)
-    eng = LocalEngine(model, use_graphs=not args.no_graphs)
+    eng = LocalEngine(model, use_graphs=not args.no_graphs, jump_forward=not args.no_jump)
     body = ("    public OrderResponse create(OrderRequest request) {\n"
             "        Order order = repository.save(Order.from(request));\n"
             "        events.publish(new OrderCreated(order.id()));\n        return OrderResponse.of(order);\n    }\n")
@@ -89,12 +90,14 @@ def main(argv=None) -> int:
             "unit": "classes/s", "n_gpus": world, "higher_is_better": True, "scaling": "weak",
             "dtype": "bf16", "data": "synthetic classes, random-init weights",
             "config": {"model": cfg.name, "params_b": round(cfg.param_count() / 1e9, 3), "batch": args.batch,
-                       "max_seq": args.max_seq, "prompt_chars": args.prompt_chars, "graphs": not args.no_graphs},
+                       "max_seq": args.max_seq, "prompt_chars": args.prompt_chars, "graphs": not args.no_graphs,
+                       "jump_forward": not args.no_jump},
             "generated_tokens_per_s": round(gen_all / elapsed, 1),
             "prompt_tokens_per_s": round(prompt_all / elapsed, 1),
             "decode_step_ms": round(1e3 * st["decode_s"] / max(1, st["decode_steps"]), 3),
             "prefill_ms_avg": round(1e3 * st["prefill_s"] / max(1, st["prefills"]), 3),
-            "decode_steps": st["decode_steps"], "elapsed_s": round(elapsed, 3), "classes": int(ok_all)}),
+            "decode_steps": st["decode_steps"], "rows_per_step": round(st["decode_rows"] / max(1, st["decode_steps"]), 1),
+            "elapsed_s": round(elapsed, 3), "classes": int(ok_all)}),
             flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -13,11 +13,14 @@ per class) but generates on the local GPU:
   generated, with a masked greedy argmax restricted to JSON-safe printable
   characters.  The output always parses, so Phase 3 recovery is only needed
   for infrastructure failures;
-* **continuous batching** -- up to ``max_batch`` sequences decode together,
-  one token per sequence per step (forced skeleton tokens ride in the same
-  batched step), finished sequences free their KV slot for the next prompt;
-* each step is one hipGraph replay (:class:`DecodeGraphs`) plus the
-  gfx950 masked-argmax kernel;
+* **continuous batching** -- up to ``max_batch`` sequences decode together;
+  finished sequences free their KV slot for the next prompt;
+* **jump-forward** -- forced skeleton bytes are appended as extra rows of the
+  same batched step (an exact multi-token extend), so only sampled tokens
+  cost a step;
+* each step is one H2D copy, one hipGraph replay (:class:`DecodeGraphs`:
+  forward + gfx950 masked argmax with a per-row grammar-mask index) and one
+  small D2H copy of the selected ids;
 * multi-GPU: one engine (replica) per GPU, classes sharded across replicas
   (:mod:`dmcp.parallel.replicas`) -- pure data parallelism, no collectives
   (SURVEY §5.8).
@@ -132,16 +135,32 @@ class _Seq:
 
 
 class LocalEngine:
-    def __init__(self, model: LocalLM, use_graphs: bool = True, max_prompt_tokens: Optional[int] = None) -> None:
+    """Continuous-batching, grammar-forced greedy generator over one LocalLM.
+
+    ``jump_forward``: forced skeleton bytes are not fed one per step -- after
+    a sequence's token is fed, every following token that is already decided
+    (the rest of a forced segment, or the closing quote of a string at its
+    length cap) is appended to the SAME step as extra rows of that sequence,
+    up to ``max_rows`` rows per step.  The KV append + causal per-row
+    attention of :meth:`LocalLM.decode` makes that an exact multi-token
+    extend, so only free (sampled) tokens cost a step each.
+    """
+
+    MASK_NO_QUOTE, MASK_QUOTE = 0, 1
+
+    def __init__(self, model: LocalLM, use_graphs: bool = True, max_prompt_tokens: Optional[int] = None,
+                 jump_forward: bool = True) -> None:
         self.model = model
         self.cfg: LMConfig = model.cfg
-        self.graphs = DecodeGraphs(model) if use_graphs else None
         dev = model.device
         self.masks = torch.tensor([_json_safe_mask(self.cfg.vocab_size, False),
                                    _json_safe_mask(self.cfg.vocab_size, True)], dtype=torch.int32, device=dev)
+        self.graphs = DecodeGraphs(model, self.masks) if use_graphs and dev.type == "cuda" else None
         self.max_prompt_tokens = max_prompt_tokens
-        self.stats = {"prompt_tokens": 0, "generated_tokens": 0, "decode_steps": 0, "prefills": 0,
-                      "decode_s": 0.0, "prefill_s": 0.0}
+        self.jump_forward = jump_forward
+        self.max_rows = model.max_rows
+        self.stats = {"prompt_tokens": 0, "generated_tokens": 0, "decode_steps": 0, "decode_rows": 0,
+                      "prefills": 0, "decode_s": 0.0, "prefill_s": 0.0}
         self._lock = threading.Lock()
 
     # ---------------------------------------------------------------- api
@@ -163,12 +182,23 @@ class LocalEngine:
             text = text[:limit - keep_tail] + text[len(text) - keep_tail:]
         return [BOS] + list(text)
 
-    def _select(self, logits: torch.Tensor, rows: List[int], with_quote: List[bool]) -> List[int]:
+    def _select_one(self, logits: torch.Tensor, with_quote: bool) -> int:
         from .. import ops
-        idx = torch.tensor([1 if q else 0 for q in with_quote], dtype=torch.long, device=logits.device)
-        mask = self.masks.index_select(0, idx)
-        ids = ops.masked_argmax(logits.contiguous(), mask, vocab=self.cfg.vocab_size)
-        return ids.tolist()
+        idx = torch.tensor([self.MASK_QUOTE if with_quote else self.MASK_NO_QUOTE], dtype=torch.int32,
+                           device=logits.device)
+        return int(ops.masked_argmax(logits.reshape(1, -1).contiguous(), self.masks, vocab=self.cfg.vocab_size,
+                                     mask_idx=idx).item())
+
+    def _step(self, toks: List[int], slots: List[int], poss: List[int], mrows: List[int]) -> List[int]:
+        """One batched forward over the rows; returns the masked argmax of every row."""
+        if self.graphs is not None:
+            _, ids = self.graphs.run(toks, slots, poss, mrows)
+        else:
+            dev = self.model.device
+            t = torch.tensor([toks, slots, poss, mrows], dtype=torch.int32, device=dev)
+            _, ids = self.model.decode_select(t[0].contiguous(), t[1].contiguous(), t[2].contiguous(), self.masks,
+                                              t[3].contiguous())
+        return ids.cpu().tolist()
 
     def _advance_forced(self, s: _Seq) -> None:
         """Sets next_token from the current forced segment or finishes."""
@@ -185,98 +215,113 @@ class LocalEngine:
             s.free_len = 0
         s.done = True
 
-    def _on_token_fed(self, s: _Seq, tok: int) -> None:
+    def _after_feed(self, s: _Seq, tok: int) -> Optional[bool]:
+        """Grammar transition after ``tok`` entered the KV cache.  Returns None
+        when the next token is already decided (``s.next_token``) or the reply
+        is complete, else whether the sampled token may be the closing quote."""
         s.out.append(tok & 0xFF)
         s.pos += 1
         s.gen_tokens += 1
+        seg = s.segs[s.seg] if s.seg < len(s.segs) else None
+        if seg is not None and seg.forced is None:
+            if tok == QUOTE:  # free string closed
+                s.seg += 1
+                s.forced_off = 0
+                s.free_len = 0
+                self._advance_forced(s)
+            else:
+                s.free_len += 1
+                if s.free_len >= seg.max_len:
+                    s.next_token = QUOTE
+                    return None
+                return s.free_len >= seg.min_len
+        else:
+            self._advance_forced(s)
+        if not s.done and s.segs[s.seg].forced is None:
+            return s.segs[s.seg].min_len == 0
+        return None
+
+    def _admit(self, s: _Seq, readme: Optional[str], results: Dict[int, str], free_slots: List[int]) -> bool:
+        """Prefill prompt + first forced segment; True if the sequence stays active."""
+        cfg = self.cfg
+        try:
+            budget = template_budget(s.segs)
+            if budget + 32 > cfg.max_seq:
+                raise ValueError(f"reply template needs {budget} tokens > max_seq {cfg.max_seq}")
+            prompt = self._prompt(s, readme, budget)
+        except Exception as e:
+            results[s.index] = json.dumps({"error": str(e)})
+            return False
+        s.slot = free_slots.pop()
+        first = s.segs[0].forced or b""
+        toks = prompt + list(first)
+        t0 = time.perf_counter()
+        logits = self.model.forward_tokens(torch.tensor(toks, dtype=torch.int32), s.slot, 0)
+        self.stats["prefill_s"] += time.perf_counter() - t0
+        self.stats["prefills"] += 1
+        self.stats["prompt_tokens"] += len(toks)
+        s.prompt_tokens = len(prompt)
+        s.out.extend(first)
+        s.pos = len(toks)
+        s.seg, s.forced_off = 1, 0
+        if s.seg < len(s.segs) and s.segs[s.seg].forced is None:
+            s.next_token = self._select_one(logits, s.segs[s.seg].min_len == 0)
+        else:
+            self._advance_forced(s)
+        if s.done:
+            results[s.index] = s.out.decode("utf-8", "replace")
+            free_slots.append(s.slot)
+            return False
+        return True
 
     def _generate(self, inputs: Sequence[EnrichmentInput], readme: Optional[str]) -> List[str]:
         cfg = self.cfg
-        dev = self.model.device
         reply_cap = cfg.max_seq - max(64, cfg.max_seq // 4)
         pending: Deque[_Seq] = deque(_Seq(inp, i, fit_template(inp, reply_cap)) for i, inp in enumerate(inputs))
         free_slots = list(range(cfg.max_batch - 1, -1, -1))
         active: List[_Seq] = []
         results: Dict[int, str] = {}
         while pending or active:
-            # admit: prefill prompt + first forced segment, then the first free token
             while pending and free_slots:
                 s = pending.popleft()
-                try:
-                    budget = template_budget(s.segs)
-                    if budget + 32 > cfg.max_seq:
-                        raise ValueError(f"reply template needs {budget} tokens > max_seq {cfg.max_seq}")
-                    prompt = self._prompt(s, readme, budget)
-                except Exception as e:
-                    results[s.index] = json.dumps({"error": str(e)})
-                    continue
-                s.slot = free_slots.pop()
-                first = s.segs[0].forced or b""
-                toks = prompt + list(first)
-                t0 = time.perf_counter()
-                logits = self.model.forward_tokens(torch.tensor(toks, dtype=torch.int32), s.slot, 0)
-                self.stats["prefill_s"] += time.perf_counter() - t0
-                self.stats["prefills"] += 1
-                self.stats["prompt_tokens"] += len(toks)
-                s.prompt_tokens = len(prompt)
-                s.out.extend(first)
-                s.pos = len(toks)
-                s.seg, s.forced_off = 1, 0
-                if s.seg < len(s.segs) and s.segs[s.seg].forced is None:
-                    s.next_token = self._select(logits[None], [0], [s.segs[s.seg].min_len == 0])[0]
-                else:
-                    self._advance_forced(s)
-                if s.done:
-                    results[s.index] = s.out.decode("utf-8", "replace")
-                    free_slots.append(s.slot)
-                else:
+                if self._admit(s, readme, results, free_slots):
                     active.append(s)
             if not active:
                 continue
-            # one batched decode step: feed next_token of every active sequence
-            B = len(active)
-            tok = torch.tensor([s.next_token for s in active], dtype=torch.int32)
-            sl = torch.tensor([s.slot for s in active], dtype=torch.int32)
-            ps = torch.tensor([s.pos for s in active], dtype=torch.int32)
+            # one batched step: every active sequence feeds its next token, plus
+            # (jump-forward) every already-decided token after it
             t0 = time.perf_counter()
-            if dev.type == "cuda":
-                tok, sl, ps = (t.pin_memory().to(dev, non_blocking=True) for t in (tok, sl, ps))
-            runner = self.graphs.run if self.graphs is not None else self.model.decode
-            logits = runner(tok, sl, ps)
-            need_rows, with_q = [], []
-            for r, s in enumerate(active):
-                fed = s.next_token
-                self._on_token_fed(s, fed)
-                seg = s.segs[s.seg] if s.seg < len(s.segs) else None
-                if seg is not None and seg.forced is None:
-                    if fed == QUOTE:  # free string closed
-                        s.seg += 1
-                        s.forced_off = 0
-                        s.free_len = 0
-                        self._advance_forced(s)
-                        if not s.done and s.segs[s.seg].forced is None:
-                            need_rows.append(r)
-                            with_q.append(s.segs[s.seg].min_len == 0)
-                    else:
-                        s.free_len += 1
-                        if s.free_len >= seg.max_len:
-                            s.next_token = QUOTE
-                        else:
-                            need_rows.append(r)
-                            with_q.append(s.free_len >= seg.min_len)
-                else:
-                    self._advance_forced(s)
-                    if not s.done and s.segs[s.seg].forced is None:
-                        need_rows.append(r)
-                        with_q.append(s.segs[s.seg].min_len == 0)
-            if need_rows:
-                rows_t = torch.tensor(need_rows, dtype=torch.long, device=logits.device)
-                picked = self._select(logits.index_select(0, rows_t), need_rows, with_q)
-                for r, t in zip(need_rows, picked):
-                    active[r].next_token = t
+            toks: List[int] = []
+            slots: List[int] = []
+            poss: List[int] = []
+            mrows: List[int] = []
+            sample_at: List[Tuple[_Seq, int]] = []
+            spare = self.max_rows - len(active)  # rows beyond one per sequence
+            for s in active:
+                tok = s.next_token
+                while True:
+                    toks.append(tok)
+                    slots.append(s.slot)
+                    poss.append(s.pos)
+                    mrows.append(self.MASK_NO_QUOTE)
+                    q = self._after_feed(s, tok)
+                    if s.done:
+                        break
+                    if q is not None:  # the next token is sampled from this row's logits
+                        mrows[-1] = self.MASK_QUOTE if q else self.MASK_NO_QUOTE
+                        sample_at.append((s, len(toks) - 1))
+                        break
+                    if not self.jump_forward or spare <= 0:
+                        break  # decided token waits for the next step
+                    spare -= 1
+                    tok = s.next_token
+            ids = self._step(toks, slots, poss, mrows)
+            for s, r in sample_at:
+                s.next_token = ids[r]
             self.stats["decode_s"] += time.perf_counter() - t0
             self.stats["decode_steps"] += 1
-            self.stats["generated_tokens"] += B
+            self.stats["decode_rows"] += len(toks)
+            self.stats["generated_tokens"] += len(toks)
             still = []
             for s in active:
                 if s.done:

@@ -54,6 +54,7 @@ class LMConfig:
     eps: float = 1e-5
     max_seq: int = 8192             # KV capacity per slot (prompt + generation)
     max_batch: int = 64             # KV slots = concurrent sequences
+    max_rows: int = 256             # token rows per batched decode/extend step (jump-forward)
 
     @property
     def qkv_dim(self) -> int:
@@ -73,7 +74,7 @@ PRESETS: Dict[str, LMConfig] = {
     "dmcp-coder-3b": LMConfig(name="dmcp-coder-3b", hidden=3072, layers=28, n_heads=24, n_kv_heads=8,
                               head_dim=128, intermediate=8192),
     "tiny": LMConfig(name="tiny", hidden=256, layers=2, n_heads=4, n_kv_heads=2, head_dim=64,
-                     intermediate=512, max_seq=1024, max_batch=8),
+                     intermediate=512, max_seq=1024, max_batch=8, max_rows=64),
 }
 
 
@@ -100,10 +101,9 @@ class LocalLM:
         self.v_cache = torch.zeros(kv_shape, dtype=self.dtype, device=self.device)
         self.cos_sin = ops.rope_tables(c.max_seq, c.head_dim, c.rope_theta, device=self.device).contiguous()
         self.scale = 1.0 / math.sqrt(c.head_dim)
-        splits = max(1, math.ceil(c.max_seq / 256))
-        n = c.max_batch * c.n_heads * splits
-        self.attn_ws = (torch.empty(n * c.head_dim, dtype=torch.float32, device=self.device),
-                        torch.empty(n * 2, dtype=torch.float32, device=self.device))
+        self.max_rows = max(c.max_batch, c.max_rows)
+        self.attn_ws = (ops.decode_workspace(self.max_rows, c.n_heads, c.n_kv_heads, c.head_dim, c.max_seq,
+                                             self.device) if self.device.type == "cuda" else None)
 
     # ------------------------------------------------------------ weights
     def _init_weights(self, seed: int) -> Dict[str, torch.Tensor]:
@@ -216,11 +216,18 @@ class LocalLM:
 
     @torch.inference_mode()
     def decode(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:
-        """One token for each of B sequences. All inputs int32 [B] on device.
+        """One token per row; all inputs int32 [B] on device.
 
-        Returns logits [B, vocab] (bf16).  Capturable into a hipGraph."""
+        Rows are independent (slot, position) pairs: several rows may extend
+        the SAME slot at consecutive positions (jump-forward over forced
+        tokens) -- every row's K/V is appended before attention runs and each
+        row attends to positions <= its own, so that is an exact causal
+        extend.  Rows with slot -1 are padding.  Returns logits [B, vocab]
+        (bf16).  Capturable into a hipGraph."""
         c = self.cfg
         B = tokens.shape[0]
+        if B > self.max_rows:
+            raise ValueError(f"decode: {B} rows > max_rows {self.max_rows}")
         seq_len = positions + 1
         x = ops.embedding(self.w["embed"], tokens)
         resid = x.clone()
@@ -236,6 +243,15 @@ class LocalLM:
             nxt = self.w[f"l{i + 1}.ln1"] if i + 1 < c.layers else self.w["norm_f"]
             h = ops.add_rmsnorm(m, nxt, c.eps, residual=resid)
         return F.linear(h, self.w["lm_head"])
+
+    def decode_select(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor,
+                      masks: torch.Tensor, mask_idx: torch.Tensor) -> tuple:
+        """:meth:`decode` + greedy selection under a per-row grammar mask
+        (``masks`` [M, ceil(V/32)] bitsets, ``mask_idx`` int32 [B]).
+        Returns (logits, ids int32 [B]); capturable."""
+        logits = self.decode(tokens, slots, positions)
+        ids = ops.masked_argmax(logits, masks, vocab=self.cfg.vocab_size, mask_idx=mask_idx)
+        return logits, ids
 
     # reference path (pure torch, fp32 math) for numerics tests
     @torch.inference_mode()
@@ -274,15 +290,22 @@ class LocalLM:
 
 
 class DecodeGraphs:
-    """hipGraph-captured decode steps, one graph per batch-size bucket.
+    """hipGraph-captured decode + selection steps, one graph per row-count bucket.
 
-    Static int32 input buffers are filled with ``copy_`` before each replay;
-    the returned logits tensor is the graph's static output (read it before
-    the next replay of the same bucket)."""
+    Inputs travel as ONE packed int32 host buffer ``[4, n]`` (token, slot,
+    position, mask row) -> one H2D copy into the graph's static input; the
+    graph runs the whole forward plus the masked argmax, so a step costs one
+    copy in, one replay and one 4-byte-per-row copy out.  Padding rows carry
+    slot -1 (kernels skip them).  Returned tensors are the graph's static
+    outputs: read them before the next replay of the same bucket."""
 
-    def __init__(self, model: LocalLM, buckets: Sequence[int] = (1, 2, 4, 8, 16, 32, 64, 128, 256)) -> None:
+    def __init__(self, model: LocalLM, masks: torch.Tensor,
+                 buckets: Sequence[int] = (1, 2, 4, 8, 16, 32, 64, 96, 128, 192, 256, 384, 512)) -> None:
         self.model = model
-        self.buckets = sorted(b for b in buckets if b <= model.cfg.max_batch)
+        self.masks = masks
+        self.buckets = sorted(b for b in buckets if b <= model.max_rows)
+        if not self.buckets or self.buckets[-1] < model.max_rows:
+            self.buckets.append(model.max_rows)
         self.graphs: Dict[int, tuple] = {}
         self.enabled = model.device.type == "cuda"
 
@@ -290,40 +313,50 @@ class DecodeGraphs:
         for b in self.buckets:
             if b >= n:
                 return b
-        return n
+        raise ValueError(f"{n} rows exceed the largest decode bucket {self.buckets[-1]}")
 
     def _capture(self, b: int):
         m = self.model
-        dev = m.device
-        tok = torch.zeros(b, dtype=torch.int32, device=dev)
-        # padded entries point at slot -1: the kernels skip them (no KV write, no read)
-        slots = torch.full((b,), -1, dtype=torch.int32, device=dev)
-        pos = torch.zeros(b, dtype=torch.int32, device=dev)
+        inp = torch.zeros((4, b), dtype=torch.int32, device=m.device)
+        inp[1].fill_(-1)
+        stage = torch.zeros((4, b), dtype=torch.int32).pin_memory()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):  # warm up hipBLASLt heuristics / allocator outside capture
-                m.decode(tok, slots, pos)
+                m.decode_select(inp[0], inp[1], inp[2], self.masks, inp[3])
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            logits = m.decode(tok, slots, pos)
-        self.graphs[b] = (g, tok, slots, pos, logits)
+            logits, ids = m.decode_select(inp[0], inp[1], inp[2], self.masks, inp[3])
+        self.graphs[b] = (g, inp, stage, stage.numpy(), logits, ids, torch.cuda.Event())
 
     @torch.inference_mode()
-    def run(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:
-        n = tokens.shape[0]
-        if not self.enabled or n > self.buckets[-1]:
-            return self.model.decode(tokens, slots, positions)
+    def run(self, tokens: Sequence[int], slots: Sequence[int], positions: Sequence[int],
+            mask_rows: Sequence[int]) -> tuple:
+        """One step over ``n`` rows given as host lists.  Returns (logits[:n],
+        ids[:n]) -- device tensors owned by the graph."""
+        n = len(tokens)
+        m = self.model
+        if not self.enabled:
+            t = torch.tensor([list(tokens), list(slots), list(positions), list(mask_rows)], dtype=torch.int32,
+                             device=m.device)
+            return m.decode_select(t[0].contiguous(), t[1].contiguous(), t[2].contiguous(), self.masks,
+                                   t[3].contiguous())
         b = self.bucket_for(n)
         if b not in self.graphs:
             self._capture(b)
-        g, tok, sl, ps, logits = self.graphs[b]
-        tok[:n].copy_(tokens)
-        sl[:n].copy_(slots)
-        ps[:n].copy_(positions)
+        g, inp, stage, st, logits, ids, copied = self.graphs[b]
+        copied.synchronize()  # the previous H2D copy from this staging buffer is done
+        # host-side packing into this bucket's pinned staging buffer; padding
+        # rows get slot -1 so the kernels skip them
+        st[0, :n] = tokens
+        st[1, :n] = slots
+        st[2, :n] = positions
+        st[3, :n] = mask_rows
         if n < b:
-            sl[n:].fill_(-1)
-            ps[n:].zero_()
+            st[1, n:] = -1
+        inp.copy_(stage, non_blocking=True)
+        copied.record()
         g.replay()
-        return logits[:n]
+        return logits[:n], ids[:n]

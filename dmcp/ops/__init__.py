@@ -24,6 +24,11 @@ def add_rmsnorm(x, weight, eps, residual=None, out=None):
     return (_hip() if x.is_cuda else reference).add_rmsnorm(x, weight, eps, residual, out)
 
 
+def decode_workspace(rows, n_heads, n_kv_heads, head_dim, max_seq, device, chunk: int = 256):
+    """Split-K scratch of the decode-attention kernel (partials + merge counters)."""
+    return _hip().decode_workspace(rows, n_heads, n_kv_heads, head_dim, max_seq, device, chunk)
+
+
 def rope_kv(qkv, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out=None):
     return (_hip() if qkv.is_cuda else reference).rope_kv(qkv, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out)
 
@@ -37,8 +42,8 @@ def silu_mul(gate_up, out=None):
     return (_hip() if gate_up.is_cuda else reference).silu_mul(gate_up, out)
 
 
-def masked_argmax(logits, mask=None, vocab: Optional[int] = None, out=None):
-    return (_hip() if logits.is_cuda else reference).masked_argmax(logits, mask, vocab, out)
+def masked_argmax(logits, mask=None, vocab: Optional[int] = None, out=None, mask_idx=None):
+    return (_hip() if logits.is_cuda else reference).masked_argmax(logits, mask, vocab, out, mask_idx)
 
 
 def embedding(table, ids, out=None):

@@ -189,22 +189,33 @@ __global__ __launch_bounds__(kBlock) void rope_kv_kernel(const uint16_t* __restr
 //    grid (splits, Hkv, B); block 256 = 4 waves.  LPK = D/8 lanes share one
 //    key row (16 B each), KPW = 64/LPK keys per wave step.  Each lane group
 //    runs an online softmax over its keys for the G query heads of this kv
-//    head; groups merge by shuffles, waves through LDS, splits in a second
-//    kernel (or directly when splits == 1).
+//    head; groups merge by shuffles, waves through LDS; only the splits that
+//    own keys (nact = ceil(L / chunk)) run: with nact == 1 the block writes
+//    the output directly, otherwise fp32 partials merged by
+//    decode_attn_combine_kernel.
 // --------------------------------------------------------------------------
 template <int D, int G>
 __global__ __launch_bounds__(kBlock) void decode_attn_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache,
     const int32_t* __restrict__ slot, const int32_t* __restrict__ seq_len, uint16_t* __restrict__ out,
-    float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int max_seq, int chunk, int splits,
-    float scale_log2, int num_slots) {
+    float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv,
+    int max_seq, int chunk, int splits, float scale_log2, int num_slots) {
     constexpr int LPK = D / 8;
     constexpr int KPW = kWave / LPK;
     constexpr int NW = kBlock / kWave;
+    constexpr int NK = G >= 6 ? 2 : 4;  // keys per lane per iteration (VGPR budget at G >= 6)
     const int split = blockIdx.x, kh = blockIdx.y, b = blockIdx.z;
     const int Hq = Hkv * G;
     const int s = slot[b];
     const int L = (s >= 0 && s < num_slots) ? min(seq_len[b], max_seq) : 0;  // never read a bad slot
+    // splits that own keys; the others exit at once (no partials)
+    const int nact = min(splits, (L + chunk - 1) / chunk);
+    if (L <= 0) {  // padding row / bad slot: defined output, nothing read
+        if (split == 0)
+            for (int o = threadIdx.x; o < G * D; o += kBlock) out[((size_t)b * Hq + kh * G) * D + o] = 0;
+        return;
+    }
+    if (split >= nact) return;
     const int start = split * chunk;
     const int end = min(L, start + chunk);
     const int lane = threadIdx.x & (kWave - 1);
@@ -231,27 +242,29 @@ __global__ __launch_bounds__(kBlock) void decode_attn_kernel(
     const size_t head_off = ((size_t)(L > 0 ? s : 0) * Hkv + kh) * (size_t)max_seq * D;
     const uint16_t* kb = k_cache + head_off + sub * 8;
     const uint16_t* vb = v_cache + head_off + sub * 8;
+    // NK independent 16 B K and V loads in flight per lane per iteration
+    // (memory-level parallelism: the kernel is HBM-bound)
     constexpr int STEP = NW * KPW;
-    for (int k0 = start + wave * KPW; k0 < end; k0 += 2 * STEP) {
-        const int ka = k0 + kig;
-        const int kb2 = ka + STEP;
-        const bool va = ka < end, vb2 = kb2 < end;
-        uint4 kra = make_uint4(0, 0, 0, 0), krb = make_uint4(0, 0, 0, 0);
-        uint4 vra = make_uint4(0, 0, 0, 0), vrb = make_uint4(0, 0, 0, 0);
-        if (va) {
-            kra = *reinterpret_cast<const uint4*>(kb + (size_t)ka * D);
-            vra = *reinterpret_cast<const uint4*>(vb + (size_t)ka * D);
-        }
-        if (vb2) {
-            krb = *reinterpret_cast<const uint4*>(kb + (size_t)kb2 * D);
-            vrb = *reinterpret_cast<const uint4*>(vb + (size_t)kb2 * D);
+    for (int k0 = start + wave * KPW; k0 < end; k0 += NK * STEP) {
+        uint4 kr[NK], vr[NK];
+        bool ok[NK];
+#pragma unroll
+        for (int r = 0; r < NK; ++r) {
+            const int kk = k0 + kig + r * STEP;
+            ok[r] = kk < end;
+            kr[r] = make_uint4(0, 0, 0, 0);
+            vr[r] = make_uint4(0, 0, 0, 0);
+            if (ok[r]) {
+                kr[r] = *reinterpret_cast<const uint4*>(kb + (size_t)kk * D);
+                vr[r] = *reinterpret_cast<const uint4*>(vb + (size_t)kk * D);
+            }
         }
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const bool valid = r == 0 ? va : vb2;
+        for (int r = 0; r < NK; ++r) {
+            const bool valid = ok[r];
             float kf[8], vf[8];
-            unpack8(r == 0 ? kra : krb, kf);
-            unpack8(r == 0 ? vra : vrb, vf);
+            unpack8(kr[r], kf);
+            unpack8(vr[r], vf);
 #pragma unroll
             for (int g = 0; g < G; ++g) {
                 float d = 0.f;
@@ -317,7 +330,7 @@ __global__ __launch_bounds__(kBlock) void decode_attn_kernel(
             at += sm_acc[w][g][d] * c;
         }
         const int qh = kh * G + g;
-        if (splits == 1) {
+        if (nact == 1) {
             out[((size_t)b * Hq + qh) * D + d] = f2bf(lt > 0.f ? at / lt : 0.f);
         } else {
             const size_t pi = ((size_t)b * Hq + qh) * splits + split;
@@ -330,23 +343,36 @@ __global__ __launch_bounds__(kBlock) void decode_attn_kernel(
     }
 }
 
-// combine split-K partials: one block per (b, q head), D threads
+// Split-K merge: one block per (row, kv head), G*D outputs.  Rows whose
+// context fits one split (nact <= 1) were written by the main kernel.
+// (A fused "last block merges" variant needs agent-scope release fences; on
+// gfx950 each one writes back the XCD's L2 and made the kernel ~10x slower
+// -- profiles/ROUND1_NOTES.md.)
 __global__ __launch_bounds__(kBlock) void decode_attn_combine_kernel(const float* __restrict__ part_o,
                                                                     const float* __restrict__ part_ml,
-                                                                    uint16_t* __restrict__ out, int D,
-                                                                    int splits) {
-    const size_t bh = blockIdx.x;
-    const float* ml = part_ml + bh * splits * 2;
-    float mx = -1e30f;
-    for (int s = 0; s < splits; ++s) mx = fmaxf(mx, ml[s * 2]);
-    for (int d = threadIdx.x; d < D; d += kBlock) {
+                                                                    const int32_t* __restrict__ slot,
+                                                                    const int32_t* __restrict__ seq_len,
+                                                                    uint16_t* __restrict__ out, int Hkv, int G,
+                                                                    int D, int max_seq, int chunk, int splits,
+                                                                    int num_slots) {
+    const int kh = blockIdx.x, b = blockIdx.y;
+    const int s = slot[b];
+    const int L = (s >= 0 && s < num_slots) ? min(seq_len[b], max_seq) : 0;
+    const int nact = min(splits, (L + chunk - 1) / chunk);
+    if (nact <= 1) return;
+    const int Hq = Hkv * G;
+    for (int o = threadIdx.x; o < G * D; o += kBlock) {
+        const int g = o / D, d = o - g * D;
+        const size_t base = ((size_t)b * Hq + kh * G + g) * splits;
+        float mx = -1e30f;
+        for (int sp = 0; sp < nact; ++sp) mx = fmaxf(mx, part_ml[(base + sp) * 2]);
         float lt = 0.f, at = 0.f;
-        for (int s = 0; s < splits; ++s) {
-            const float c = exp2f(ml[s * 2] - mx);
-            lt += ml[s * 2 + 1] * c;
-            at += part_o[(bh * splits + s) * D + d] * c;
+        for (int sp = 0; sp < nact; ++sp) {
+            const float c = exp2f(part_ml[(base + sp) * 2] - mx);
+            lt += part_ml[(base + sp) * 2 + 1] * c;
+            at += part_o[(base + sp) * D + d] * c;
         }
-        out[bh * D + d] = f2bf(lt > 0.f ? at / lt : 0.f);
+        out[((size_t)b * Hq + kh * G + g) * D + d] = f2bf(lt > 0.f ? at / lt : 0.f);
     }
 }
 
@@ -372,15 +398,24 @@ __global__ __launch_bounds__(kBlock) void silu_mul_kernel(const uint16_t* __rest
 
 // --------------------------------------------------------------------------
 // 5. masked greedy sampling: ids[b] = argmax_{v allowed} logits[b, v]
-//    mask [B, ceil(V/32)] uint32 bit-set of allowed tokens (nullptr = all).
-//    Ties resolve to the smallest index.
+//    mask: uint32 bit-sets of allowed tokens, ceil(V/32) words per row
+//    (nullptr = all).  With mask_idx, row b uses mask row mask_idx[b]
+//    (clamped to [0, n_masks)) of a small shared table -- the decode graph
+//    selects the grammar state per row without an index_select; without it,
+//    mask row b.  Ties resolve to the smallest index.
 // --------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void masked_argmax_kernel(const uint16_t* __restrict__ logits,
                                                               const uint32_t* __restrict__ mask,
+                                                              const int32_t* __restrict__ mask_idx, int n_masks,
                                                               int32_t* __restrict__ ids, int V, int ld) {
     const int b = blockIdx.x;
     const uint16_t* row = logits + (size_t)b * ld;
-    const uint32_t* mrow = mask ? mask + (size_t)b * ((V + 31) >> 5) : nullptr;
+    int mr = b;
+    if (mask_idx) {
+        mr = mask_idx[b];
+        mr = mr < 0 ? 0 : (mr >= n_masks ? n_masks - 1 : mr);
+    }
+    const uint32_t* mrow = mask ? mask + (size_t)mr * ((V + 31) >> 5) : nullptr;
     float best = -INFINITY;
     int bi = 0x7fffffff;
     for (int v = threadIdx.x; v < V; v += kBlock) {
@@ -432,15 +467,21 @@ inline int grid_for(size_t work) {
 
 template <int D>
 hipError_t launch_decode_d(int G, dim3 grid, const uint16_t* q, const uint16_t* k, const uint16_t* v,
-                           const int32_t* slot, const int32_t* len, uint16_t* out, float* po, float* pml, int Hkv,
-                           int max_seq, int chunk, int splits, float sl2, int ns, hipStream_t st) {
+                           const int32_t* slot, const int32_t* len, uint16_t* out, float* po, float* pml,
+                           int Hkv, int max_seq, int chunk, int splits, float sl2, int ns, hipStream_t st) {
+#define DMCP_DECODE(GG)                                                                                  \
+    decode_attn_kernel<D, GG><<<grid, kBlock, 0, st>>>(q, k, v, slot, len, out, po, pml, Hkv, max_seq, \
+                                                       chunk, splits, sl2, ns)
     switch (G) {
-        case 1: decode_attn_kernel<D, 1><<<grid, kBlock, 0, st>>>(q, k, v, slot, len, out, po, pml, Hkv, max_seq, chunk, splits, sl2, ns); break;
-        case 2: decode_attn_kernel<D, 2><<<grid, kBlock, 0, st>>>(q, k, v, slot, len, out, po, pml, Hkv, max_seq, chunk, splits, sl2, ns); break;
-        case 4: decode_attn_kernel<D, 4><<<grid, kBlock, 0, st>>>(q, k, v, slot, len, out, po, pml, Hkv, max_seq, chunk, splits, sl2, ns); break;
-        case 8: decode_attn_kernel<D, 8><<<grid, kBlock, 0, st>>>(q, k, v, slot, len, out, po, pml, Hkv, max_seq, chunk, splits, sl2, ns); break;
+        case 1: DMCP_DECODE(1); break;
+        case 2: DMCP_DECODE(2); break;
+        case 4: DMCP_DECODE(4); break;
+        case 3: DMCP_DECODE(3); break;
+        case 6: DMCP_DECODE(6); break;
+        case 8: DMCP_DECODE(8); break;
         default: return hipErrorInvalidValue;
     }
+#undef DMCP_DECODE
     return hipGetLastError();
 }
 
@@ -448,7 +489,7 @@ hipError_t launch_decode_d(int G, dim3 grid, const uint16_t* q, const uint16_t* 
 
 extern "C" {
 
-int dmcp_abi_version() { return 1; }
+int dmcp_abi_version() { return 4; }
 
 int dmcp_add_rmsnorm(const void* x, void* residual, const void* w, void* out, int rows, int H, float eps,
                      void* stream) {
@@ -478,28 +519,33 @@ int dmcp_rope_kv(const void* qkv, const void* pos, const void* slot, const void*
 }
 
 int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cache, const void* slot,
-                          const void* seq_len, void* out, void* part_o, void* part_ml, int B, int Hq, int Hkv,
-                          int D, int max_seq, int num_slots, int chunk, int splits, float scale, void* stream) {
+                          const void* seq_len, void* out, void* part_o, void* part_ml, int B, int Hq, int Hkv, int D,
+                          int max_seq, int num_slots, int chunk, int splits, float scale, void* stream) {
     if (B <= 0) return 0;
     if (Hkv <= 0 || Hq % Hkv != 0 || splits <= 0 || chunk <= 0) return hipErrorInvalidValue;
+    if (splits > 1 && (!part_o || !part_ml)) return hipErrorInvalidValue;
     const int G = Hq / Hkv;
     const float sl2 = scale * 1.4426950408889634f;
     dim3 grid(splits, Hkv, B);
     auto st = (hipStream_t)stream;
+    auto qq = (const uint16_t*)q;
+    auto kk = (const uint16_t*)k_cache;
+    auto vv = (const uint16_t*)v_cache;
+    auto sl = (const int32_t*)slot;
+    auto ln = (const int32_t*)seq_len;
     hipError_t e;
     if (D == 64)
-        e = launch_decode_d<64>(G, grid, (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
-                                (const int32_t*)slot, (const int32_t*)seq_len, (uint16_t*)out, (float*)part_o,
-                                (float*)part_ml, Hkv, max_seq, chunk, splits, sl2, num_slots, st);
+        e = launch_decode_d<64>(G, grid, qq, kk, vv, sl, ln, (uint16_t*)out, (float*)part_o, (float*)part_ml, Hkv,
+                                max_seq, chunk, splits, sl2, num_slots, st);
     else if (D == 128)
-        e = launch_decode_d<128>(G, grid, (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
-                                 (const int32_t*)slot, (const int32_t*)seq_len, (uint16_t*)out, (float*)part_o,
-                                 (float*)part_ml, Hkv, max_seq, chunk, splits, sl2, num_slots, st);
+        e = launch_decode_d<128>(G, grid, qq, kk, vv, sl, ln, (uint16_t*)out, (float*)part_o, (float*)part_ml, Hkv,
+                                 max_seq, chunk, splits, sl2, num_slots, st);
     else
         return hipErrorInvalidValue;
     if (e != hipSuccess || splits == 1) return e;
-    decode_attn_combine_kernel<<<B * Hq, kBlock, 0, st>>>((const float*)part_o, (const float*)part_ml,
-                                                          (uint16_t*)out, D, splits);
+    decode_attn_combine_kernel<<<dim3(Hkv, B), kBlock, 0, st>>>((const float*)part_o, (const float*)part_ml, sl, ln,
+                                                               (uint16_t*)out, Hkv, G, D, max_seq, chunk, splits,
+                                                               num_slots);
     return hipGetLastError();
 }
 
@@ -511,10 +557,13 @@ int dmcp_silu_mul(const void* gu, void* out, int T, int I, void* stream) {
     return hipGetLastError();
 }
 
-int dmcp_masked_argmax(const void* logits, const void* mask, void* ids, int B, int V, int ld, void* stream) {
+int dmcp_masked_argmax(const void* logits, const void* mask, const void* mask_idx, int n_masks, void* ids, int B,
+                       int V, int ld, void* stream) {
     if (B <= 0) return 0;
+    if (mask_idx && n_masks <= 0) return hipErrorInvalidValue;
     masked_argmax_kernel<<<B, kBlock, 0, (hipStream_t)stream>>>((const uint16_t*)logits, (const uint32_t*)mask,
-                                                               (int32_t*)ids, V, ld);
+                                                               (const int32_t*)mask_idx, n_masks, (int32_t*)ids, V,
+                                                               ld);
     return hipGetLastError();
 }
 

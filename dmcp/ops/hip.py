@@ -26,6 +26,7 @@ _lock = threading.Lock()
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _f = ctypes.c_float
+ABI_VERSION = 4  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
 
 
 class HipOpsError(RuntimeError):
@@ -52,14 +53,14 @@ def lib() -> ctypes.CDLL:
             "dmcp_decode_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _f, _vp],
                                       _i),
             "dmcp_silu_mul": ([_vp, _vp, _i, _i, _vp], _i),
-            "dmcp_masked_argmax": ([_vp, _vp, _vp, _i, _i, _i, _vp], _i),
+            "dmcp_masked_argmax": ([_vp, _vp, _vp, _i, _vp, _i, _i, _i, _vp], _i),
             "dmcp_embedding": ([_vp, _vp, _vp, _i, _i, _i, _vp], _i),
         }
         for name, (args, res) in sigs.items():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
-        if L.dmcp_abi_version() != 1:
+        if L.dmcp_abi_version() != ABI_VERSION:
             raise HipOpsError("HIP kernel library ABI mismatch; rebuild with python -m dmcp.ops.build")
         _lib = L
         return _lib
@@ -154,7 +155,7 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
         _req(t, torch.bfloat16, f"decode_attention.{n}")
     _req(slot, torch.int32, "decode_attention.slot")
     _req(seq_len, torch.int32, "decode_attention.seq_len")
-    if Dk != D or D not in (64, 128) or Hq % Hkv or (Hq // Hkv) not in (1, 2, 4, 8) or v_cache.shape != k_cache.shape:
+    if Dk != D or D not in (64, 128) or Hq % Hkv or (Hq // Hkv) not in (1, 2, 3, 4, 6, 8) or v_cache.shape != k_cache.shape:
         raise HipOpsError(f"decode_attention: unsupported shape q={tuple(q.shape)} kv={tuple(k_cache.shape)}")
     if slot.numel() != B or seq_len.numel() != B:
         raise HipOpsError("decode_attention: slot/seq_len must have B entries")
@@ -163,18 +164,25 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     _req(out, torch.bfloat16, "decode_attention.out")
     if splits > 1:
         if workspace is None:
-            part_o = torch.empty((B * Hq * splits * D,), dtype=torch.float32, device=q.device)
-            part_ml = torch.empty((B * Hq * splits * 2,), dtype=torch.float32, device=q.device)
-        else:
-            part_o, part_ml = workspace
-            if part_o.numel() < B * Hq * splits * D or part_ml.numel() < B * Hq * splits * 2:
-                raise HipOpsError("decode_attention: workspace too small")
+            workspace = decode_workspace(B, Hq, Hkv, D, MAXS, q.device, chunk)
+        part_o, part_ml = workspace
+        if part_o.numel() < B * Hq * splits * D or part_ml.numel() < B * Hq * splits * 2:
+            raise HipOpsError("decode_attention: workspace too small")
     else:
         part_o = part_ml = None
     _check(lib().dmcp_decode_attention(_ptr(q), _ptr(k_cache), _ptr(v_cache), _ptr(slot), _ptr(seq_len), _ptr(out),
                                        _ptr(part_o), _ptr(part_ml), B, Hq, Hkv, D, MAXS, S, chunk, splits,
                                        float(scale), _stream()), "dmcp_decode_attention")
     return out
+
+
+def decode_workspace(rows: int, Hq: int, Hkv: int, D: int, max_seq: int, device, chunk: int = 256) -> tuple:
+    """Split-K scratch (fp32 partial outputs + running max/sum) for up to
+    ``rows`` query rows."""
+    splits = decode_splits(max_seq, chunk)
+    n = rows * Hq * splits
+    return (torch.empty(n * D, dtype=torch.float32, device=device),
+            torch.empty(n * 2, dtype=torch.float32, device=device))
 
 
 def silu_mul(gate_up: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -192,20 +200,33 @@ def silu_mul(gate_up: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch
 
 
 def masked_argmax(logits: torch.Tensor, mask: Optional[torch.Tensor] = None, vocab: Optional[int] = None,
-                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """logits [B, ld] bf16; mask [B, ceil(V/32)] int32 bitset (None = all)."""
+                  out: Optional[torch.Tensor] = None, mask_idx: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """logits [B, ld] bf16; mask int32 bitsets, ceil(V/32) words per row:
+    [B, W] (row b -> mask b), or [M, W] with ``mask_idx`` int32 [B] choosing
+    a mask row per logits row.  None = all tokens allowed."""
     _req(logits, torch.bfloat16, "masked_argmax.logits")
     B, ld = logits.shape
     V = vocab or ld
+    W = (V + 31) // 32
     if V > ld:
         raise HipOpsError("masked_argmax: vocab larger than row")
+    n_masks = 0
     if mask is not None:
         _req(mask, torch.int32, "masked_argmax.mask")
-        if mask.shape != (B, (V + 31) // 32):
-            raise HipOpsError(f"masked_argmax: mask shape {tuple(mask.shape)} != {(B, (V + 31) // 32)}")
+        if mask_idx is not None:
+            _req(mask_idx, torch.int32, "masked_argmax.mask_idx")
+            if mask.dim() != 2 or mask.shape[1] != W or mask.shape[0] < 1 or mask_idx.numel() != B:
+                raise HipOpsError(f"masked_argmax: mask table {tuple(mask.shape)} / mask_idx {mask_idx.numel()} "
+                                  f"do not match B={B}, W={W}")
+            n_masks = mask.shape[0]
+        elif mask.shape != (B, W):
+            raise HipOpsError(f"masked_argmax: mask shape {tuple(mask.shape)} != {(B, W)}")
+    elif mask_idx is not None:
+        raise HipOpsError("masked_argmax: mask_idx given without a mask table")
     out = torch.empty((B,), dtype=torch.int32, device=logits.device) if out is None else out
     _req(out, torch.int32, "masked_argmax.out")
-    _check(lib().dmcp_masked_argmax(_ptr(logits), _ptr(mask), _ptr(out), B, V, ld, _stream()), "dmcp_masked_argmax")
+    _check(lib().dmcp_masked_argmax(_ptr(logits), _ptr(mask), _ptr(mask_idx if mask is not None else None), n_masks,
+                                    _ptr(out), B, V, ld, _stream()), "dmcp_masked_argmax")
     return out
 
 

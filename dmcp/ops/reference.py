@@ -101,10 +101,12 @@ def silu_mul(gate_up: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch
 
 
 def masked_argmax(logits: torch.Tensor, mask: Optional[torch.Tensor] = None, vocab: Optional[int] = None,
-                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  out: Optional[torch.Tensor] = None, mask_idx: Optional[torch.Tensor] = None) -> torch.Tensor:
     B, ld = logits.shape
     V = vocab or ld
     x = logits[:, :V].float().clone()
+    if mask is not None and mask_idx is not None:
+        mask = mask[mask_idx.long().clamp(0, mask.shape[0] - 1)]
     if mask is not None:
         idx = torch.arange(V, device=logits.device)
         words = mask.to(torch.int64)[:, idx // 32]

@@ -344,6 +344,13 @@ std::string scan_file_json(const std::string& path, const std::string& language,
     FileRec f;
     f.abs_path = path;
     f.rel_path = rel_path.empty() ? path : rel_path;
+    // ``rel_path`` is relative to the source root: it names the unit
+    if (!rel_path.empty()) {
+        std::string r = rel_path;
+        size_t dot = r.rfind('.'), slash = r.rfind('/');
+        if (dot != std::string::npos && dot > 0 && (slash == std::string::npos || dot > slash + 1)) r = r.substr(0, dot);
+        f.identifier = dotted(r);
+    }
     std::string src;
     if (read_file(path, src)) {
         if (language == "java") analyze_java(src, f);

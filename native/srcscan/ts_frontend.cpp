@@ -712,7 +712,13 @@ private:
             method = std::string(m);
             has_path = false;
             int a = d.lparen + 1;
-            if (a < d.rparen && t[a].kind == Tok::String) {
+            if (a == d.rparen) {
+                // `@Post()` routes the controller root.  Divergence: the
+                // reference leaves the path null, so such handlers were never
+                // reported as HTTP endpoints.
+                p = "/";
+                has_path = true;
+            } else if (t[a].kind == Tok::String) {
                 int a_end = a + 1;
                 if (a_end == d.rparen || P(a_end, ',')) {
                     p = std::string(unquote(t[a].text));
@@ -1034,6 +1040,18 @@ private:
             bool at_stmt = stmt_start(i, stmt);
             // property access `x.class` etc. are not keywords
             if (i > b && (P(i - 1, '.') || P(i - 1, "?."))) { ++i; continue; }
+            // CommonJS `require('./x')` and dynamic `import('./x')` with a literal
+            // specifier (the legacy NodeJsSourceParser resolved require(); the
+            // Babel extractor only sees ES imports)
+            if ((w == "require" || w == "import") && P(i + 1, '(') && i + 3 < e &&
+                t[i + 2].kind == Tok::String && P(i + 3, ')')) {
+                ImportRec r;
+                r.imported = w == "require" ? "require" : "import()";
+                r.source = std::string(unquote(t[i + 2].text));
+                out.imports.push_back(r);
+                i += 4;
+                continue;
+            }
             if (w == "import" && !P(i + 1, '(') && !P(i + 1, '.')) { i = parse_import(i, e); continue; }
             if (w == "export") { i = parse_export(i, e, pending); pending.clear(); continue; }
             if (w == "class" || (w == "abstract" && I(i + 1, "class"))) {

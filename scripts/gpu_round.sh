@@ -29,6 +29,8 @@ for s in $STEPS; do
         smoke) run smoke 600 python __graft_entry__.py smoke ;;
         bench) run bench 600 python bench.py --steps 5 --warmup 2 ;;
         enrich) run bench_enrich 900 python bench_enrich.py --classes 256 --batch 64 ;;
+        enrich_nojump) run bench_enrich_nojump 900 python bench_enrich.py --classes 256 --batch 64 --no-jump ;;
+        kernels) run kernels 600 python scripts/bench_kernels.py ;;
         prof)
             ROOT=$(pwd)
             ( cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv \

@@ -66,7 +66,8 @@ def test_rope_kv_skips_invalid_slot(hip):
     assert kc.abs().sum().item() == 0 and vc.abs().sum().item() == 0
 
 
-@pytest.mark.parametrize("D,Hq,Hkv,MAXS", [(64, 32, 8, 1024), (128, 16, 4, 300), (64, 8, 8, 64), (128, 8, 1, 2048)])
+@pytest.mark.parametrize("D,Hq,Hkv,MAXS", [(64, 32, 8, 1024), (128, 16, 4, 300), (64, 8, 8, 64), (128, 8, 1, 2048),
+                                           (128, 24, 8, 700), (64, 12, 2, 513)])
 def test_decode_attention(hip, D, Hq, Hkv, MAXS):
     from dmcp.ops import reference
     B, S = 5, 7

@@ -128,7 +128,8 @@ class Config:
 
 def sqlite_path_from_url(url: str) -> str:
     if url.startswith("sqlite:///"):
-        return url[len("sqlite:///") - 1:] if url.startswith("sqlite:////") else url[len("sqlite:///"):]
+        # SQLAlchemy convention: sqlite:///relative.db, sqlite:////absolute.db
+        return url[len("sqlite:///"):]
     if url.startswith("sqlite://"):
         return url[len("sqlite://"):]
     if url.startswith("jdbc:") or url.startswith("postgres"):

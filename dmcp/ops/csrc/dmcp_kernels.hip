@@ -198,24 +198,35 @@ template <int D, int G>
 __global__ __launch_bounds__(kBlock) void decode_attn_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache,
     const int32_t* __restrict__ slot, const int32_t* __restrict__ seq_len, uint16_t* __restrict__ out,
-    float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int B, int Hkv,
     int max_seq, int chunk, int splits, float scale_log2, int num_slots) {
     constexpr int LPK = D / 8;
     constexpr int KPW = kWave / LPK;
     constexpr int NW = kBlock / kWave;
     constexpr int NK = G >= 6 ? 2 : 4;  // keys per lane per iteration (VGPR budget at G >= 6)
-    const int split = blockIdx.x, kh = blockIdx.y, b = blockIdx.z;
     const int Hq = Hkv * G;
+    // Persistent grid over split-major work items (split, row, kv head).  A
+    // grid of splits*Hkv*B blocks where most splits are empty (short rows)
+    // spent ~100 us launching waves that exit at once (profiles/decode_*);
+    // here the empty items cost one cached load + a branch.
+    const int per_split = B * Hkv;
+    const int total = splits * per_split;
+    __shared__ float sm_m[NW][G], sm_l[NW][G];
+    __shared__ float sm_acc[NW][G][D];
+    for (int item = blockIdx.x; item < total; item += gridDim.x) {
+    const int split = item / per_split;
+    const int rem = item - split * per_split;
+    const int b = rem / Hkv, kh = rem - b * Hkv;
     const int s = slot[b];
     const int L = (s >= 0 && s < num_slots) ? min(seq_len[b], max_seq) : 0;  // never read a bad slot
-    // splits that own keys; the others exit at once (no partials)
+    // splits that own keys; the others are skipped (no partials)
     const int nact = min(splits, (L + chunk - 1) / chunk);
     if (L <= 0) {  // padding row / bad slot: defined output, nothing read
         if (split == 0)
             for (int o = threadIdx.x; o < G * D; o += kBlock) out[((size_t)b * Hq + kh * G) * D + o] = 0;
-        return;
+        continue;
     }
-    if (split >= nact) return;
+    if (split >= nact) continue;
     const int start = split * chunk;
     const int end = min(L, start + chunk);
     const int lane = threadIdx.x & (kWave - 1);
@@ -259,12 +270,13 @@ __global__ __launch_bounds__(kBlock) void decode_attn_kernel(
                 vr[r] = *reinterpret_cast<const uint4*>(vb + (size_t)kk * D);
             }
         }
+        // scores of the NK keys first, then ONE online-softmax rescale per
+        // head per iteration (not per key)
+        float sc[NK][G];
 #pragma unroll
         for (int r = 0; r < NK; ++r) {
-            const bool valid = ok[r];
-            float kf[8], vf[8];
+            float kf[8];
             unpack8(kr[r], kf);
-            unpack8(vr[r], vf);
 #pragma unroll
             for (int g = 0; g < G; ++g) {
                 float d = 0.f;
@@ -272,14 +284,30 @@ __global__ __launch_bounds__(kBlock) void decode_attn_kernel(
                 for (int j = 0; j < 8; ++j) d += qv[g][j] * kf[j];
 #pragma unroll
                 for (int msk = 1; msk < LPK; msk <<= 1) d += __shfl_xor(d, msk, kWave);
-                const float sc = valid ? d : -1e30f;
-                const float mn = fmaxf(m[g], sc);
-                const float corr = exp2f(m[g] - mn);
-                const float pr = valid ? exp2f(sc - mn) : 0.f;
-                l[g] = l[g] * corr + pr;
+                sc[r][g] = ok[r] ? d : -1e30f;
+            }
+        }
 #pragma unroll
-                for (int j = 0; j < 8; ++j) acc[g][j] = acc[g][j] * corr + pr * vf[j];
-                m[g] = mn;
+        for (int g = 0; g < G; ++g) {
+            float mn = m[g];
+#pragma unroll
+            for (int r = 0; r < NK; ++r) mn = fmaxf(mn, sc[r][g]);
+            const float corr = exp2f(m[g] - mn);
+            l[g] *= corr;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[g][j] *= corr;
+            m[g] = mn;
+        }
+#pragma unroll
+        for (int r = 0; r < NK; ++r) {
+            float vf[8];
+            unpack8(vr[r], vf);
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const float pr = ok[r] ? exp2f(sc[r][g] - m[g]) : 0.f;
+                l[g] += pr;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[g][j] += pr * vf[j];
             }
         }
     }
@@ -302,8 +330,7 @@ __global__ __launch_bounds__(kBlock) void decode_attn_kernel(
         }
     }
     // merge the waves through LDS: lanes [0, LPK) of each wave hold the result
-    __shared__ float sm_m[NW][G], sm_l[NW][G];
-    __shared__ float sm_acc[NW][G][D];
+    __syncthreads();  // the previous item's readers are done with sm_*
     if (lane < LPK) {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
@@ -341,6 +368,7 @@ __global__ __launch_bounds__(kBlock) void decode_attn_kernel(
             }
         }
     }
+    }  // work items
 }
 
 // Split-K merge: one block per (row, kv head), G*D outputs.  Rows whose
@@ -459,6 +487,19 @@ __global__ __launch_bounds__(kBlock) void embedding_kernel(const uint16_t* __res
     }
 }
 
+// CUs of the current device (cached per device; 256 on MI355X)
+inline int device_cu_count() {
+    static int cached[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cached[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cached[dev] = n;
+    }
+    return cached[dev];
+}
+
 inline int grid_for(size_t work) {
     size_t g = (work + kBlock - 1) / kBlock;
     if (g > 2048) g = 2048;  // grid-stride beyond 8 blocks/CU (Guideline 11)
@@ -468,9 +509,10 @@ inline int grid_for(size_t work) {
 template <int D>
 hipError_t launch_decode_d(int G, dim3 grid, const uint16_t* q, const uint16_t* k, const uint16_t* v,
                            const int32_t* slot, const int32_t* len, uint16_t* out, float* po, float* pml,
-                           int Hkv, int max_seq, int chunk, int splits, float sl2, int ns, hipStream_t st) {
-#define DMCP_DECODE(GG)                                                                                  \
-    decode_attn_kernel<D, GG><<<grid, kBlock, 0, st>>>(q, k, v, slot, len, out, po, pml, Hkv, max_seq, \
+                           int B, int Hkv, int max_seq, int chunk, int splits, float sl2, int ns,
+                           hipStream_t st) {
+#define DMCP_DECODE(GG)                                                                                     \
+    decode_attn_kernel<D, GG><<<grid, kBlock, 0, st>>>(q, k, v, slot, len, out, po, pml, B, Hkv, max_seq, \
                                                        chunk, splits, sl2, ns)
     switch (G) {
         case 1: DMCP_DECODE(1); break;
@@ -526,7 +568,11 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
     if (splits > 1 && (!part_o || !part_ml)) return hipErrorInvalidValue;
     const int G = Hq / Hkv;
     const float sl2 = scale * 1.4426950408889634f;
-    dim3 grid(splits, Hkv, B);
+    // persistent grid: enough blocks to fill every CU a few times over, never
+    // more than there are work items
+    const long items = (long)splits * Hkv * B;
+    const long cap = 4L * device_cu_count();
+    dim3 grid((unsigned)(items < cap ? items : cap));
     auto st = (hipStream_t)stream;
     auto qq = (const uint16_t*)q;
     auto kk = (const uint16_t*)k_cache;
@@ -535,11 +581,11 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
     auto ln = (const int32_t*)seq_len;
     hipError_t e;
     if (D == 64)
-        e = launch_decode_d<64>(G, grid, qq, kk, vv, sl, ln, (uint16_t*)out, (float*)part_o, (float*)part_ml, Hkv,
-                                max_seq, chunk, splits, sl2, num_slots, st);
+        e = launch_decode_d<64>(G, grid, qq, kk, vv, sl, ln, (uint16_t*)out, (float*)part_o, (float*)part_ml, B,
+                                Hkv, max_seq, chunk, splits, sl2, num_slots, st);
     else if (D == 128)
-        e = launch_decode_d<128>(G, grid, qq, kk, vv, sl, ln, (uint16_t*)out, (float*)part_o, (float*)part_ml, Hkv,
-                                 max_seq, chunk, splits, sl2, num_slots, st);
+        e = launch_decode_d<128>(G, grid, qq, kk, vv, sl, ln, (uint16_t*)out, (float*)part_o, (float*)part_ml, B,
+                                 Hkv, max_seq, chunk, splits, sl2, num_slots, st);
     else
         return hipErrorInvalidValue;
     if (e != hipSuccess || splits == 1) return e;

@@ -179,8 +179,11 @@ class SourceClassRepository:
         "SELECT c.* FROM source_classes c JOIN projects p ON p.id = c.project_id "
         "WHERE c.full_class_name = ? "
         "ORDER BY p.last_analyzed_at DESC, p.created_at DESC")
+    # range form of "package_name LIKE 'p.%'" (what text_pattern_ops gives the
+    # reference on Postgres): SQLite only uses an index for LIKE under
+    # case_sensitive_like, a range always can
     FIND_BY_PACKAGE_PREFIX = ("SELECT * FROM source_classes WHERE package_name = ? "
-                              "OR package_name LIKE ? ORDER BY full_class_name")
+                              "OR (package_name >= ? AND package_name < ?) ORDER BY full_class_name")
     COUNT_BY_PROJECT_ID = "SELECT COUNT(*) FROM source_classes WHERE project_id = ?"
     FIND_BY_PROJECT_ID_AND_FULL_CLASS_NAME = (
         "SELECT * FROM source_classes WHERE project_id = ? AND full_class_name = ?")
@@ -267,8 +270,9 @@ class SourceClassRepository:
         return out
 
     def find_by_package_prefix(self, package_prefix: str) -> List[SourceClass]:
+        # "p" or "p.*" as two index ranges: [p, p] and [p + ".", p + "/") ('/' follows '.')
         return [self._map(r) for r in self.db.query(self.FIND_BY_PACKAGE_PREFIX,
-                                                    (package_prefix, package_prefix + ".%"))]
+                                                    (package_prefix, package_prefix + ".", package_prefix + "/"))]
 
     def find_by_project_id_and_full_class_name(self, project_id: str, fqcn: str) -> Optional[SourceClass]:
         row = self.db.query_one(self.FIND_BY_PROJECT_ID_AND_FULL_CLASS_NAME, (project_id, fqcn))

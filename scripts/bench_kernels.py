@@ -24,17 +24,30 @@ from dmcp.ops import hip, reference  # noqa: E402
 PEAK_BYTES = 8.0e12
 
 
-def timed(fn, iters=50, warmup=5):
-    for _ in range(warmup):
-        fn()
+def timed(fn, iters=50, warmup=3):
+    """Device time per call: ``iters`` calls captured in one hipGraph and
+    replayed, so host-side launch cost (Python wrapper, ctypes) is excluded --
+    the same way the decode loop runs them."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(warmup):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
-    for _ in range(iters):
-        fn()
+    for _ in range(3):
+        g.replay()
     b.record()
     torch.cuda.synchronize()
-    return a.elapsed_time(b) / iters * 1e-3
+    return a.elapsed_time(b) / (3 * iters) * 1e-3
 
 
 def report(name, secs, nbytes, eager_secs=None, **cfg):
@@ -46,22 +59,24 @@ def report(name, secs, nbytes, eager_secs=None, **cfg):
     print(json.dumps(out), flush=True)
 
 
-def bench_decode_attention(B, L, Hq=32, Hkv=8, D=64, max_seq=4096):
+def bench_decode_attention(B, L, Hq=32, Hkv=8, D=64, max_seq=4096, chunk=256, eager=True):
     dev = "cuda"
     kc = torch.randn(B, Hkv, max_seq, D, device=dev).to(torch.bfloat16)
     vc = torch.randn(B, Hkv, max_seq, D, device=dev).to(torch.bfloat16)
     q = torch.randn(B, Hq, D, device=dev).to(torch.bfloat16)
     slot = torch.arange(B, dtype=torch.int32, device=dev)
     sl = torch.full((B,), L, dtype=torch.int32, device=dev)
-    ws = hip.decode_workspace(B, Hq, Hkv, D, max_seq, dev)
+    ws = hip.decode_workspace(B, Hq, Hkv, D, max_seq, dev, chunk)
     out = torch.empty_like(q)
-    t = timed(lambda: hip.decode_attention(q, kc, vc, slot, sl, 1 / math.sqrt(D), workspace=ws, out=out))
+    t = timed(lambda: hip.decode_attention(q, kc, vc, slot, sl, 1 / math.sqrt(D), workspace=ws, chunk=chunk,
+                                           out=out))
     nbytes = 2 * B * Hkv * L * D * 2 + 2 * q.numel() * 2
     k4, v4 = kc[:, :, :L], vc[:, :, :L]
 
-    def eager():
+    def sdpa():
         torch.nn.functional.scaled_dot_product_attention(q[:, :, None], k4, v4, enable_gqa=True)
-    report("decode_attention", t, nbytes, timed(eager), B=B, L=L, Hq=Hq, Hkv=Hkv, D=D)
+    report("decode_attention", t, nbytes, timed(sdpa) if eager else None, B=B, L=L, Hq=Hq, Hkv=Hkv, D=D,
+           chunk=chunk)
 
 
 def bench_rmsnorm(rows, H=2048):
@@ -110,6 +125,9 @@ def main() -> int:
     for B, L in ((1, 4096), (16, 2048), (64, 512), (64, 2300), (64, 4096), (256, 2300)):
         bench_decode_attention(B, L)
     bench_decode_attention(64, 2300, Hq=24, Hkv=8, D=128)
+    for chunk in (128, 512, 1024):  # split size sweep
+        for B, L in ((16, 2048), (64, 2300), (64, 4096)):
+            bench_decode_attention(B, L, chunk=chunk, eager=False)
     for rows in (64, 256, 4096):
         bench_rmsnorm(rows)
         bench_silu(rows)

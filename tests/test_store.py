@@ -1,0 +1,216 @@
+"""SQLite store: migrations, repositories (ProjectRepositoryIntegrationTest,
+SourceClassRepositoryIntegrationTest, SourceMethodRepositoryIntegrationTest)
+and the query-plan check that replaces IndexAnalysisTest (Testcontainers
+Postgres + EXPLAIN there; EXPLAIN QUERY PLAN on SQLite here)."""
+import json
+import threading
+
+import pytest
+
+from dmcp.models.domain import (ClassType, MethodParameter, Project, ProjectStatus, RepositoryUrl, SourceClass,
+                                SourceMethod, new_id)
+from dmcp.store.db import MIGRATIONS, Database
+from dmcp.store.repositories import (MethodParameterRepository, Repositories, SourceClassRepository,
+                                     SourceMethodRepository, from_iso, to_iso)
+
+
+@pytest.fixture
+def repos(tmp_db):
+    return Repositories(tmp_db)
+
+
+def _project(name="shop"):
+    return Project.create(name, RepositoryUrl.of(f"https://github.com/acme/{name}.git"))
+
+
+def test_migrations_idempotent(tmp_path):
+    db = Database(str(tmp_path / "m.db"))
+    assert db.schema_version() == MIGRATIONS[-1][0]
+    assert db.migrate() == 0  # nothing left to apply
+    names = {r[0] for r in db.query("SELECT name FROM sqlite_master WHERE type = 'index'")}
+    assert "idx_source_methods_http_endpoints" in names and "idx_source_methods_class" not in names
+    db.close()
+    db2 = Database(str(tmp_path / "m.db"))
+    assert db2.schema_version() == MIGRATIONS[-1][0]
+    db2.close()
+
+
+def test_project_repository_roundtrip(repos):
+    p = _project()
+    p.update_description("d")
+    repos.projects.save(p)
+    got = repos.projects.find_by_id(p.id)
+    assert got.name == "shop" and got.status is ProjectStatus.PENDING and got.description == "d"
+    assert repos.projects.find_by_repository_url(p.repository_url).id == p.id
+    assert repos.projects.find_by_name("shop").id == p.id and repos.projects.exists_by_repository_url(p.repository_url)
+    p.start_analysis()
+    p.analysis_completed("abc")
+    p.update_graph_data('{"nodes":{}}')
+    p.base_package = "co.acme"
+    repos.projects.update(p)
+    got = repos.projects.find_by_id(p.id)
+    assert got.status is ProjectStatus.ANALYZED and got.last_commit_hash == "abc" and got.base_package == "co.acme"
+    assert got.graph_data == '{"nodes":{}}' and got.last_analyzed_at is not None
+    light = repos.projects.find_all()
+    assert light[0].graph_data is None  # list views never load the graph blob
+    assert repos.projects.find_all(with_graph=True)[0].graph_data
+    assert [x.id for x in repos.projects.find_by_status(ProjectStatus.ANALYZED)] == [p.id]
+    assert repos.projects.find_by_statuses([ProjectStatus.ERROR]) == []
+    with pytest.raises(Exception):
+        repos.projects.save(_project())  # unique repository_url
+    repos.projects.delete(p.id)
+    assert repos.projects.find_by_id(p.id) is None
+
+
+def test_class_method_param_repositories(repos):
+    p = _project()
+    repos.projects.save(p)
+    a = SourceClass.create(p.id, "co.acme.a.OrderService", ClassType.SERVICE, None, "src/A.java", "c1")
+    b = SourceClass.create(p.id, "co.acme.b.Order", ClassType.ENTITY, "an order", "src/B.java", "c1")
+    repos.classes.save_all([a, b])
+    assert repos.classes.find_by_full_class_name("co.acme.a.OrderService").id == a.id
+    assert repos.classes.count_by_project_id(p.id) == 2 and repos.classes.count_by_project() == {p.id: 2}
+    assert repos.classes.class_type_breakdown(p.id) == {"SERVICE": 1, "ENTITY": 1}
+    assert sorted(repos.classes.package_names(p.id)) == ["co.acme.a", "co.acme.b"]
+    assert [c.id for c in repos.classes.find_by_package_prefix("co.acme")] == [b.id, a.id] or \
+        {c.id for c in repos.classes.find_by_package_prefix("co.acme")} == {a.id, b.id}
+    assert [c.id for c in repos.classes.find_unenriched_by_project_id(p.id)] == [a.id]
+    repos.classes.update_enrichment(a.id, ClassType.CONTROLLER, "now a controller")
+    assert repos.classes.find_by_id(a.id).class_type is ClassType.CONTROLLER
+    by = repos.classes.find_by_full_class_names(["co.acme.b.Order", "missing"], project_id=p.id)
+    assert set(by) == {"co.acme.b.Order"}
+
+    m1 = SourceMethod.create(a.id, "create", None, None, ["E"], "POST", "/orders", 10)
+    m2 = SourceMethod.create(a.id, "helper", None, None, None, None, None, 20)
+    m3 = SourceMethod.create(a.id, "ctor", None, None, None, None, None, None)
+    repos.methods.save_all([m3, m2, m1])
+    assert [m.method_name for m in repos.methods.find_by_class_id(a.id)] == ["create", "helper", "ctor"]
+    assert repos.methods.count_endpoints_by_project_id(p.id) == 1
+    assert [m.id for m in repos.methods.find_http_endpoints_by_project_id(p.id)] == [m1.id]
+    repos.methods.update_enrichment_batch([("creates", ["validate", "persist"], m1.id)])
+    got = repos.methods.find_by_class_id_and_method_name(a.id, "create")
+    assert got.description == "creates" and got.business_logic == ["validate", "persist"] and got.exceptions == ["E"]
+    assert repos.methods.find_by_class_name_and_method_name("co.acme.a.OrderService", "helper").id == m2.id
+    grouped = repos.methods.find_by_class_ids([a.id, b.id])
+    assert len(grouped[a.id]) == 3 and not grouped.get(b.id)
+
+    mp = MethodParameter.create(m1.id, 0, b.id)
+    repos.params.save_all([mp])
+    assert [x.class_id for x in repos.params.find_by_method_id(m1.id)] == [b.id]
+    with pytest.raises(Exception):
+        repos.params.save_all([MethodParameter.create(m1.id, 0, b.id)])  # unique (method, position)
+    repos.params.delete_by_class_ids([a.id])
+    repos.methods.delete_by_class_ids([a.id])
+    repos.classes.delete_by_ids([a.id])
+    assert repos.classes.count_by_project_id(p.id) == 1 and repos.params.find_by_method_id(m1.id) == []
+
+
+def test_cascade_delete_project(repos):
+    p = _project()
+    repos.projects.save(p)
+    c = SourceClass.create(p.id, "x.Y", ClassType.OTHER, None, None, None)
+    repos.classes.save(c)
+    repos.methods.save(SourceMethod.create(c.id, "m", None, None, None, None, None, 1))
+    repos.projects.delete(p.id)
+    assert repos.classes.find_by_id(c.id) is None
+    assert repos.db.query_one("SELECT COUNT(*) FROM source_methods")[0] == 0
+
+
+def test_duplicate_fqcn_across_projects_picks_most_recent(repos):
+    old, new = _project("a"), _project("b")
+    for p, h in ((old, "h1"), (new, "h2")):
+        repos.projects.save(p)
+        p.start_analysis()
+        p.analysis_completed(h)
+        repos.projects.update(p)
+    repos.db.execute("UPDATE projects SET last_analyzed_at = ? WHERE id = ?", ("2020-01-01T00:00:00Z", old.id))
+    for p in (old, new):
+        repos.classes.save(SourceClass.create(p.id, "co.shared.Util", ClassType.OTHER, None, None, None))
+    assert repos.classes.find_by_full_class_name("co.shared.Util").project_id == new.id
+    assert len(repos.classes.find_all_by_full_class_name("co.shared.Util")) == 2
+
+
+def test_transactions_rollback_and_threads(tmp_db):
+    repos = Repositories(tmp_db)
+    p = _project()
+    repos.projects.save(p)
+    with pytest.raises(RuntimeError):
+        with tmp_db.transaction():
+            repos.classes.save(SourceClass.create(p.id, "x.A", ClassType.OTHER, None, None, None))
+            raise RuntimeError("boom")
+    assert repos.classes.count_by_project_id(p.id) == 0
+    errors = []
+
+    def worker(k):
+        try:
+            for i in range(20):
+                repos.classes.save(SourceClass.create(p.id, f"t{k}.C{i}", ClassType.OTHER, None, None, None))
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors and repos.classes.count_by_project_id(p.id) == 80
+
+
+def test_iso_roundtrip():
+    from datetime import datetime, timezone
+    now = datetime(2024, 5, 6, 7, 8, 9, 123000, tzinfo=timezone.utc)
+    assert from_iso(to_iso(now)) == now and to_iso(None) is None and from_iso(None) is None
+
+
+# ----------------------------------------------------------- query plans
+def _seed(repos, n_projects=50, classes_per=17, methods_per=3):
+    """IndexAnalysisTest's fixture shape: 50 projects / 850 classes / 2,550 methods."""
+    cls_rows, meth_rows = [], []
+    for i in range(n_projects):
+        p = _project(f"svc{i}")
+        repos.projects.save(p)
+        for j in range(classes_per):
+            cid = new_id()
+            pkg = f"co.acme.svc{i}.d{j % 4}"
+            cls_rows.append((cid, p.id, f"{pkg}.C{j}", f"C{j}", pkg, "SERVICE", None, "f", "2024-01-01T00:00:00Z",
+                             None))
+            for k in range(methods_per):
+                http = ("GET", f"/c{j}/{k}") if k == 0 else (None, None)
+                meth_rows.append((new_id(), cid, f"m{k}", None, "[]", "[]", http[0], http[1], k + 1,
+                                  "2024-01-01T00:00:00Z"))
+    repos.classes.save_rows(cls_rows)
+    repos.methods.save_rows(meth_rows)
+    repos.db.execute("ANALYZE")
+
+
+def _plan(db, sql, params):
+    return " | ".join(r[3] for r in db.query("EXPLAIN QUERY PLAN " + sql, params))
+
+
+def test_query_plans_use_indexes(repos):
+    _seed(repos)
+    db = repos.db
+    pid = repos.projects.find_by_name("svc7").id
+    cid = repos.classes.find_by_project_id(pid)[0].id
+    cases = {
+        "classes by project": (SourceClassRepository.FIND_BY_PROJECT_ID, (pid,)),
+        "class by fqcn": (SourceClassRepository.FIND_BY_FULL_CLASS_NAME, ("co.acme.svc7.d1.C1",)),
+        "class by project+fqcn": (SourceClassRepository.FIND_BY_PROJECT_ID_AND_FULL_CLASS_NAME,
+                                  (pid, "co.acme.svc7.d1.C1")),
+        "classes by package prefix": (SourceClassRepository.FIND_BY_PACKAGE_PREFIX,
+                                      ("co.acme.svc7", "co.acme.svc7.", "co.acme.svc7/")),
+        "unenriched": (SourceClassRepository.FIND_UNENRICHED_BY_PROJECT_ID, (pid,)),
+        "methods by class": (SourceMethodRepository.FIND_BY_CLASS_ID, (cid,)),
+        "method by class+name": (SourceMethodRepository.FIND_BY_CLASS_ID_AND_METHOD_NAME, (cid, "m1")),
+        "endpoints by project": (SourceMethodRepository.FIND_HTTP_ENDPOINTS_BY_PROJECT_ID, (pid,)),
+        "endpoint count": (SourceMethodRepository.COUNT_ENDPOINTS_BY_PROJECT_ID, (pid,)),
+    }
+    for name, (sql, params) in cases.items():
+        plan = _plan(db, sql, params)
+        # every filtered table is reached by an index search, never a full scan
+        assert "SCAN source_classes" not in plan.replace("SCAN source_classes USING", "SEARCH"), (name, plan)
+        assert "SCAN source_methods" not in plan.replace("SCAN source_methods USING", "SEARCH"), (name, plan)
+        assert "SEARCH" in plan, (name, plan)
+    # the partial endpoint index serves the endpoint queries
+    assert "idx_source_methods_http_endpoints" in _plan(db, *cases["endpoints by project"]) or \
+        "idx_source_methods_class_name" in _plan(db, *cases["endpoints by project"])

@@ -47,37 +47,11 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
-def init_distributed():
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch = None
-    try:
-        import torch as _t
-        torch = _t
-    except ImportError:
-        pass
-    dist = None
-    cuda = bool(torch is not None and torch.cuda.is_available())
-    if cuda:
-        torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group(backend="nccl" if cuda else "gloo")
-    return torch, dist, rank, world, local_rank, cuda
-
-
-def sync(torch, dist, cuda):
-    if dist is not None:
-        dist.barrier()
-    if cuda:
-        torch.cuda.synchronize()
-
-
 def main(argv=None) -> int:
     args = parse_args(argv)
-    torch, dist, rank, world, local_rank, cuda = init_distributed()
+    from dmcp.parallel.dist import init_from_env
+    ctx = init_from_env()
+    rank, world = ctx.rank, ctx.world
     logging.basicConfig(level=logging.WARNING, stream=sys.stderr)
     from dmcp.app import App
     from dmcp.config import Config
@@ -85,8 +59,7 @@ def main(argv=None) -> int:
     from dmcp.utils.tracing import METRICS
 
     cpus = os.cpu_count() or 8
-    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-    threads = args.threads or max(1, min(16, cpus // max(1, local_world)))
+    threads = args.threads or max(1, min(16, cpus // max(1, ctx.local_world)))
     work = args.workdir or tempfile.mkdtemp(prefix=f"dmcp-bench-r{rank}-")
     repo = os.path.join(work, f"shop{rank}")
     fqcns = synth.java_spring_repo(repo, n_classes=args.classes, base_package=f"co.acme.shop{rank}", seed=rank + 1)
@@ -99,7 +72,7 @@ def main(argv=None) -> int:
         stats_acc = {}
         for _ in range(args.warmup):
             app.indexer.analyze_project(repo)
-        sync(torch, dist, cuda)
+        ctx.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             r = app.indexer.analyze_project(repo)
@@ -107,16 +80,11 @@ def main(argv=None) -> int:
             for k, v in r.stats.items():
                 if k.startswith("analyze."):
                     stats_acc[k] = stats_acc.get(k, 0.0) + v
-        sync(torch, dist, cuda)
+        ctx.synchronize()
         elapsed = time.perf_counter() - t0
-        total_classes = n_classes
-        if dist is not None:
-            t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if cuda else "cpu")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = float(t.item())
-            c = torch.tensor([float(n_classes)], dtype=torch.float64, device="cuda" if cuda else "cpu")
-            dist.all_reduce(c, op=dist.ReduceOp.SUM)
-            total_classes = int(c.item())
+        # whole-job aggregate: MAX elapsed over ranks, SUM of classes
+        elapsed = ctx.max(elapsed)[0]
+        total_classes = int(ctx.sum(float(n_classes))[0])
         # query latencies on the indexed graph (BASELINE configs 3/4)
         extra = {"phaseMsPerStep": {k: round(v / max(1, args.steps), 2) for k, v in stats_acc.items()},
                  "classesPerRepo": r.classes_analyzed, "parserThreadsPerRank": threads}
@@ -160,8 +128,7 @@ def main(argv=None) -> int:
         app.close()
         if args.workdir is None:
             shutil.rmtree(work, ignore_errors=True)
-        if dist is not None:
-            dist.destroy_process_group()
+        ctx.shutdown()
     return 0
 
 

@@ -4,7 +4,9 @@ Commands
   serve-mcp                      MCP stdio server (the reference's ``mcp`` profile)
   serve [--host H] [--port P]    REST API + Swagger + optional sync scheduler
   analyze URL [--branch B] [--no-fix-missed]
+  analyze-batch FILE [--workers N]  bulk index 'url [branch]' lines; exit code = failures
   rebuild PROJECT_ID             re-parse without enrichment
+  delete PROJECT_ID              remove a project and its classes / graph
   resume PROJECT_ID              re-enrich classes with no description
   sync [--project NAME]          incremental git-diff sync (all eligible by default)
   query "project:target..."      graph DSL
@@ -43,8 +45,14 @@ def main(argv: Optional[List[str]] = None) -> int:
     a.add_argument("url")
     a.add_argument("--branch")
     a.add_argument("--no-fix-missed", action="store_true")
+    ab = sub.add_parser("analyze-batch")
+    ab.add_argument("file", help="repos.txt: 'url [branch]' per line")
+    ab.add_argument("--workers", type=int, default=1)
+    ab.add_argument("--no-fix-missed", action="store_true")
     r = sub.add_parser("rebuild")
     r.add_argument("project_id")
+    dl = sub.add_parser("delete")
+    dl.add_argument("project_id")
     rs = sub.add_parser("resume")
     rs.add_argument("project_id")
     sy = sub.add_parser("sync")
@@ -84,6 +92,24 @@ def main(argv: Optional[List[str]] = None) -> int:
         out = None
         if args.cmd == "analyze":
             out = app.indexer.analyze_project(args.url, args.branch, not args.no_fix_missed).to_dict()
+        elif args.cmd == "analyze-batch":
+            from dataclasses import asdict
+            from .parallel.bulk import bulk_analyze, parse_repo_list
+            with open(args.file, encoding="utf-8") as f:
+                items = parse_repo_list(f.read())
+            res = bulk_analyze(app.config, items, args.workers, not args.no_fix_missed,
+                               app=app if args.workers <= 1 else None)
+            failed = sum(1 for x in res if not x.success)
+            print(json.dumps({"total": len(res), "success": len(res) - failed, "failed": failed,
+                              "results": [asdict(x) for x in res]}, indent=2))
+            return failed  # exit code = number of failures (analyze-repos.sh parity)
+        elif args.cmd == "delete":
+            ok = app.projects.delete_project(args.project_id)
+            out = {"success": ok, "projectId": args.project_id,
+                   "message": "Project deleted" if ok else "Project not found"}
+            if not ok:
+                print(json.dumps(out))
+                return 1
         elif args.cmd == "rebuild":
             out = app.indexer.rebuild_graph(args.project_id)
         elif args.cmd == "resume":

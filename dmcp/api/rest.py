@@ -19,8 +19,9 @@ Parity:
   (``application.yml:62-68``)
 
 Additions: ``POST /api/projects/{id}/resume-enrichment`` (checkpoint
-resume), ``POST /api/tools/{name}`` (any MCP tool over HTTP), ``GET /metrics``
-(Prometheus text) and ``GET /api/stats``.
+resume), ``DELETE /api/projects/{id}`` (ProjectService.deleteProject, which
+the reference never exposed), ``POST /api/tools/{name}`` (any MCP tool over
+HTTP), ``GET /metrics`` (Prometheus text) and ``GET /api/stats``.
 """
 from __future__ import annotations
 
@@ -125,6 +126,17 @@ def create_app(app) -> FastAPI:
                               "unchangedClasses": x.unchanged_classes, "errorMessage": x.error_message}
                              for x in r.results],
                 "message": "Sync completed"}
+
+    @api.delete("/api/projects/{project_id}", tags=["Project Analysis"])
+    def delete_project(project_id: str):
+        try:
+            if not app.projects.delete_project(project_id):
+                return JSONResponse(status_code=404, content={"success": False, "projectId": project_id,
+                                                              "message": "Project not found"})
+            return {"success": True, "projectId": project_id, "message": "Project deleted"}
+        except DomainError as e:
+            return JSONResponse(status_code=409, content={"success": False, "projectId": project_id,
+                                                          "message": e.message, "errorCode": e.error_code})
 
     @api.get("/api/projects", tags=["Project Analysis"])
     def list_projects():

@@ -18,6 +18,7 @@ from .enrich.backend import EnrichmentBackend, create_backend
 from .graph.cache import GraphCache
 from .index.git import GitClient
 from .index.pipeline import Indexer
+from .index.projects import ProjectService
 from .models.domain import ProjectStatus
 from .query.context import ContextService
 from .query.dsl import GraphQueryService
@@ -59,6 +60,7 @@ class App:
                                parser_threads=self.config.parser_threads,
                                require_enrichment=self.config.require_enrichment_for_analyze,
                                max_source_chars=self.config.enrich_max_source_chars)
+        self.projects = ProjectService(self.repos, self.cache)
         self.context = ContextService(self.repos, self.cache)
         self.graph_query = GraphQueryService(self.cache)
         self._scheduler = None

@@ -365,39 +365,23 @@ class LocalLLMBackend(EnrichmentBackend):
     def enrich_batch(self, inputs: Sequence[EnrichmentInput], readme: Optional[str]) -> List[EnrichmentResult]:
         if not inputs:
             return []
-        shards = [list(range(i, len(inputs), len(self.engines))) for i in range(len(self.engines))]
-        raw: List[Optional[str]] = [None] * len(inputs)
-        errors: Dict[int, str] = {}
+        from ..parallel.replicas import ReplicaPool
+        n, E = len(inputs), len(self.engines)
+        # one engine: everything in one continuous batch; several: work-stealing
+        # chunks big enough to keep each replica's batch full
+        chunk = n if E == 1 else max(2 * max(e.cfg.max_batch for e in self.engines), -(-n // (2 * E)))
+        pool = ReplicaPool(self.engines, chunk_for=lambda e: chunk)
 
-        def run(e_idx: int) -> None:
-            idx = shards[e_idx]
-            if not idx:
-                return
-            eng = self.engines[e_idx]
-            try:
-                with torch.cuda.device(eng.model.device) if eng.model.device.type == "cuda" else _nullctx():
-                    outs = eng.generate([inputs[i] for i in idx], readme)
-                for i, o in zip(idx, outs):
-                    raw[i] = o
-            except Exception as e:  # isolate: every class of this shard fails, others survive
-                LOG.exception("local engine %d failed", e_idx)
-                for i in idx:
-                    errors[i] = str(e)
+        def ctx(eng):
+            return torch.cuda.device(eng.model.device) if eng.model.device.type == "cuda" else _nullctx()
 
-        if len(self.engines) == 1:
-            run(0)
-        else:
-            threads = [threading.Thread(target=run, args=(k,), name=f"local-llm-{k}") for k in range(len(self.engines))]
-            for t in threads:
-                t.start()
-            for t in threads:
-                t.join()
+        raw = pool.map(lambda eng, items: eng.generate(items, readme), list(inputs), device_ctx=ctx)
         results = []
-        for i, inp in enumerate(inputs):
-            if i in errors or raw[i] is None:
-                results.append(EnrichmentResult.failure(inp.full_class_name, errors.get(i, "no output")))
+        for inp, r in zip(inputs, raw):
+            if isinstance(r, BaseException) or r is None:
+                results.append(EnrichmentResult.failure(inp.full_class_name, str(r) if r is not None else "no output"))
             else:
-                results.append(parse_enrichment_response(raw[i], inp.full_class_name))
+                results.append(parse_enrichment_response(r, inp.full_class_name))
         return results
 
     def stats(self) -> dict:

@@ -229,6 +229,7 @@ class LocalLM:
         if B > self.max_rows:
             raise ValueError(f"decode: {B} rows > max_rows {self.max_rows}")
         seq_len = positions + 1
+        chunk = ops.decode_chunk(B, c.n_kv_heads, c.max_seq)
         x = ops.embedding(self.w["embed"], tokens)
         resid = x.clone()
         h = ops.add_rmsnorm(x, self.w["l0.ln1"], c.eps)
@@ -236,7 +237,7 @@ class LocalLM:
             kc, vc = self.k_cache[i], self.v_cache[i]
             qkv = F.linear(h, self.w[f"l{i}.wqkv"])
             q = ops.rope_kv(qkv, positions, slots, self.cos_sin, kc, vc, c.n_heads)
-            att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws)
+            att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws, chunk=chunk)
             o = F.linear(att.view(B, c.n_heads * c.head_dim), self.w[f"l{i}.wo"])
             h = ops.add_rmsnorm(o, self.w[f"l{i}.ln2"], c.eps, residual=resid)
             m = self._mlp(i, h)

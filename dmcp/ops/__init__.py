@@ -24,8 +24,14 @@ def add_rmsnorm(x, weight, eps, residual=None, out=None):
     return (_hip() if x.is_cuda else reference).add_rmsnorm(x, weight, eps, residual, out)
 
 
+def decode_chunk(rows, n_kv_heads, max_seq):
+    """Keys per split-K work item for a decode step (see :func:`dmcp.ops.hip.decode_chunk`)."""
+    from .hip import decode_chunk as _dc
+    return _dc(rows, n_kv_heads, max_seq)
+
+
 def decode_workspace(rows, n_heads, n_kv_heads, head_dim, max_seq, device, chunk: int = 256):
-    """Split-K scratch of the decode-attention kernel (partials + merge counters)."""
+    """Split-K scratch of the decode-attention kernel (fp32 partials + max/sum)."""
     return _hip().decode_workspace(rows, n_heads, n_kv_heads, head_dim, max_seq, device, chunk)
 
 

@@ -89,6 +89,8 @@ def bulk_analyze(config, items: Sequence[BulkItem], workers: int = 1, fix_missed
         return results  # type: ignore[return-value]
     values = {k: getattr(config, k) for k in config.__dataclass_fields__}
     values["recover_stuck_on_start"] = False  # siblings may be mid-analysis
+    from ..store.db import Database
+    Database(config.db_path).close()  # create + migrate once, before the workers race for it
     with ProcessPoolExecutor(max_workers=min(workers, len(items), os.cpu_count() or 1)) as ex:
         futs = {ex.submit(_analyze_one, values, (it.url, it.branch), fix_missed): i for i, it in enumerate(items)}
         for f in as_completed(futs):

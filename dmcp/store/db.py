@@ -27,6 +27,7 @@ import logging
 import os
 import sqlite3
 import threading
+import time
 from typing import Iterator, List, Tuple
 
 LOG = logging.getLogger(__name__)
@@ -165,7 +166,16 @@ class Database:
         conn.row_factory = sqlite3.Row
         conn.execute("PRAGMA foreign_keys = ON")
         if self.path != ":memory:":
-            conn.execute("PRAGMA journal_mode = WAL")
+            # switching to WAL needs a moment of exclusive access; concurrent
+            # openers (bulk workers) get SQLITE_BUSY without the busy handler
+            for attempt in range(200):
+                try:
+                    conn.execute("PRAGMA journal_mode = WAL")
+                    break
+                except sqlite3.OperationalError as e:
+                    if "locked" not in str(e) or attempt == 199:
+                        raise
+                    time.sleep(0.05)
             conn.execute("PRAGMA synchronous = NORMAL")
         conn.execute("PRAGMA temp_store = MEMORY")
         conn.execute("PRAGMA cache_size = -65536")
@@ -249,6 +259,10 @@ class Database:
                 if version in done:
                     continue
                 conn.execute("BEGIN IMMEDIATE")
+                # another process may have applied it while we waited for the lock
+                if conn.execute("SELECT 1 FROM schema_version WHERE version = ?", (version,)).fetchone():
+                    conn.execute("COMMIT")
+                    continue
                 try:
                     for stmt in _split_sql(sql):
                         conn.execute(stmt)

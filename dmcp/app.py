@@ -24,6 +24,7 @@ from .query.context import ContextService
 from .query.dsl import GraphQueryService
 from .store.db import Database
 from .store.repositories import Repositories
+from .utils.runtime import tune_gc
 
 LOG = logging.getLogger(__name__)
 
@@ -59,7 +60,9 @@ class App:
                                description_length=self.config.description_length,
                                parser_threads=self.config.parser_threads,
                                require_enrichment=self.config.require_enrichment_for_analyze,
-                               max_source_chars=self.config.enrich_max_source_chars)
+                               max_source_chars=self.config.enrich_max_source_chars,
+                               in_memory_sources=self.config.git_in_memory,
+                               in_memory_max_bytes=self.config.git_in_memory_max_mb << 20)
         self.projects = ProjectService(self.repos, self.cache)
         self.context = ContextService(self.repos, self.cache)
         self.graph_query = GraphQueryService(self.cache)
@@ -68,6 +71,7 @@ class App:
             self.recover_stuck_projects()
         if load_graphs:
             self.cache.load_all()
+        tune_gc()  # start-up heap out of the cyclic GC (see dmcp/utils/runtime.py)
 
     def recover_stuck_projects(self) -> int:
         """A project left ANALYZING/SYNCING by a dead process is moved to ERROR

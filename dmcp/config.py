@@ -46,6 +46,10 @@ class Config:
     git_clone_base_path: str = "/tmp/domain-mcp-repos"
     git_ssh_key_path: Optional[str] = None
     git_timeout_seconds: int = 300
+    # read sources straight from git objects (bare clone + cat-file) instead of
+    # a working-tree checkout; larger trees fall back to a checkout
+    git_in_memory: bool = True
+    git_in_memory_max_mb: int = 1024
     # sync (application.yml:49-52)
     sync_enabled: bool = False
     sync_cron: str = "0 0 2 * * *"
@@ -89,6 +93,8 @@ class Config:
             "GIT_CLONE_BASE_PATH": "git_clone_base_path",
             "GIT_SSH_KEY_PATH": "git_ssh_key_path",
             "GIT_TIMEOUT_SECONDS": "git_timeout_seconds",
+            "GIT_IN_MEMORY": "git_in_memory",
+            "GIT_IN_MEMORY_MAX_MB": "git_in_memory_max_mb",
             "SYNC_ENABLED": "sync_enabled",
             "SYNC_CRON": "sync_cron",
             "MCP_SERVER_NAME": "mcp_server_name",

@@ -96,6 +96,45 @@ class GitClient:
             raise GitError(f"Failed to clone repository: {e}") from e
         return CloneResult(dest, self.head(dest))
 
+    def snapshot(self, url: RepositoryUrl, branch: Optional[str], shallow: bool = True,
+                 max_bytes: int = 1 << 30):
+        """The branch head as a :class:`~dmcp.index.source.SourceTree` without a
+        working-tree checkout (bare clone + ``cat-file --batch``); falls back to
+        a checkout when the candidate sources exceed ``max_bytes``."""
+        from .source import CheckoutTree, MemoryTree, list_tree, read_blobs, wanted
+        dest = self.new_clone_dir(url.repository_name(), "-bare")
+        args = ["clone", "--quiet", "--no-tags", "--bare"]
+        local = url.local_path()
+        if local is not None:
+            args += ["--shared", "--single-branch"]
+            source = os.path.abspath(local)
+        else:
+            if shallow:
+                args += ["--depth", "1"]
+            args += ["--single-branch"]
+            source = url.value
+        if branch:
+            args += ["--branch", branch]
+        args += [source, dest]
+        LOG.info("Fetching %s (branch: %s) into %s", url, branch, dest)
+        try:
+            self._git(args)
+            commit = self.head(dest)
+            entries = [e for e in list_tree(self, dest, commit) if wanted(e[0])]
+            blobs = read_blobs(self, dest, [e[1] for e in entries], max_bytes)
+            if blobs is None:
+                LOG.info("%s: sources exceed the %d MiB in-memory limit, using a checkout", url, max_bytes >> 20)
+                shutil.rmtree(dest, ignore_errors=True)
+                c = self.clone(url, branch, shallow=shallow)
+                return CheckoutTree(c.directory, c.commit_hash)
+        except GitError as e:
+            shutil.rmtree(dest, ignore_errors=True)
+            raise GitError(f"Failed to clone repository: {e}") from e
+        except Exception:
+            shutil.rmtree(dest, ignore_errors=True)
+            raise
+        return MemoryTree(dest, commit, {e[0]: b for e, b in zip(entries, blobs)})
+
     def head(self, repo_dir: str) -> str:
         return self._git(["rev-parse", "HEAD"], cwd=repo_dir)[1].strip()
 

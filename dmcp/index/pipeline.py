@@ -43,11 +43,12 @@ from ..graph.cache import GraphCache
 from ..graph.project_graph import MethodEnrichmentData, MethodInfo, ProjectGraph
 from ..models.domain import (ClassType, Project, ProjectStatus, RepositoryUrl, SourceClass,
                              new_id, new_ids, package_name_of, simple_name_of, utc_now)
-from ..parsers.base import ParsedProject, ParsedUnit, SourceParser, detect_parser
+from ..parsers.base import ParsedProject, ParsedUnit, SourceParser, parser_for
 from ..store.repositories import Repositories, to_iso
 from ..utils.errors import DomainError
 from ..utils.tracing import METRICS, span
-from .git import CloneResult, GitClient, read_readme
+from .git import GitClient
+from .source import CheckoutTree, SourceTree
 
 LOG = logging.getLogger(__name__)
 
@@ -146,7 +147,10 @@ class Indexer:
                  backend: Optional[EnrichmentBackend] = None, *, batch_size: int = 20,
                  max_readme_length: int = 10_000, description_length: int = 500,
                  parser_threads: int = 0, require_enrichment: bool = True,
-                 max_source_chars: int = 200_000) -> None:
+                 max_source_chars: int = 200_000, in_memory_sources: bool = True,
+                 in_memory_max_bytes: int = 1 << 30) -> None:
+        self.in_memory_sources = in_memory_sources
+        self.in_memory_max_bytes = in_memory_max_bytes
         self.repos = repos
         self.cache = cache
         self.git = git
@@ -173,18 +177,18 @@ class Indexer:
             raise DomainError(f"Project {url.repository_name()} is already being processed",
                               "PROJECT_BUSY")
         stats: Dict[str, float] = {}
-        clone: Optional[CloneResult] = None
+        clone: Optional[SourceTree] = None
         project = self._prepare_project(url, branch_name)
         try:
             with span("analyze.total", stats, project=project.name):
                 with span("analyze.clone", stats):
-                    clone = self.git.clone(url, branch_name, shallow=True)
-                readme = read_readme(clone.directory, self.max_readme_length)
+                    clone = self._fetch(url, branch_name, shallow=True)
+                readme = clone.readme(self.max_readme_length)
                 if readme is not None:
                     project.update_description(readme[:self.description_length])
-                parser = detect_parser(clone.directory, self.parser_threads)
+                parser = parser_for(clone.detect_language(), self.parser_threads)
                 with span("analyze.parse", stats):
-                    parsed = parser.scan(clone.directory)
+                    parsed = parser.scan_tree(clone)
                     graph = parsed.build_graph()
                 LOG.info("Graph built: %d nodes, %d entry points", graph.node_count(), graph.entry_point_count())
                 order = graph.analysis_order()
@@ -194,11 +198,11 @@ class Indexer:
                 enriched = failed = recovered = 0
                 if self.backend.enabled:
                     with span("analyze.phase2", stats):
-                        enriched, failed = self._enrich_identifiers(order, parsed, graph, clone.directory,
+                        enriched, failed = self._enrich_identifiers(order, parsed, graph, clone,
                                                                     readme, methods_by_ident)
                     if fix_missed:
                         with span("analyze.phase3", stats):
-                            recovered = self._recover_unenriched(project, parsed, graph, clone.directory, readme)
+                            recovered = self._recover_unenriched(project, parsed, graph, clone, readme)
                 with span("analyze.persist_graph", stats):
                     project.base_package = common_package_prefix(package_name_of(i) for i in parsed.units)
                     project.update_graph_data(graph.to_json())
@@ -219,8 +223,15 @@ class Indexer:
             raise DomainError(f"Analysis failed: {e}", "ANALYSIS_FAILED", e) from e
         finally:
             if clone is not None:
-                self.git.cleanup(clone.directory)
+                clone.cleanup()
             lock.release()
+
+    def _fetch(self, url: RepositoryUrl, branch: Optional[str], shallow: bool) -> SourceTree:
+        """The branch head: in memory from git objects (default) or checked out."""
+        if self.in_memory_sources:
+            return self.git.snapshot(url, branch, shallow=shallow, max_bytes=self.in_memory_max_bytes)
+        c = self.git.clone(url, branch, shallow=shallow)
+        return CheckoutTree(c.directory, c.commit_hash)
 
     def analyze_local(self, path: str, fix_missed: bool = True) -> AnalysisResult:
         """Analyzes a local git working tree (``file://`` clone of HEAD)."""
@@ -313,7 +324,7 @@ class Indexer:
                     tcid = class_ids.get(tgt)
                     if tcid is not None:
                         param_rows.append((nid(), mid, pos, tcid, now))
-        with self.repos.db.transaction():
+        with self.repos.db.bulk_transaction():
             if replace:
                 # children first: the FK cascade then finds nothing to do per row
                 self.repos.params.delete_by_project_id(pid)
@@ -327,16 +338,13 @@ class Indexer:
         return len(cls_rows), methods_by_ident
 
     # ------------------------------------------------------------ enrichment
-    def _read_source(self, clone_dir: str, unit: ParsedUnit) -> Optional[str]:
+    def _read_source(self, tree: SourceTree, unit: ParsedUnit) -> Optional[str]:
         parts = []
         total = 0
         for rel in (unit.files if len(unit.files) > 1 else [unit.source_file]):
-            path = os.path.join(clone_dir, rel)
-            try:
-                with open(path, "r", encoding="utf-8", errors="replace") as f:
-                    text = f.read()
-            except OSError as e:
-                LOG.warning("Failed to read source for enrichment %s: %s", rel, e)
+            text = tree.read_text(rel)
+            if text is None:
+                LOG.warning("Failed to read source for enrichment %s", rel)
                 continue
             if len(unit.files) > 1:
                 text = f"// file: {rel}\n{text}"
@@ -346,14 +354,14 @@ class Indexer:
                 break
         return "\n".join(parts) if parts else None
 
-    def _inputs_for(self, idents: Sequence[str], parsed: ParsedProject, clone_dir: str,
+    def _inputs_for(self, idents: Sequence[str], parsed: ParsedProject, tree: SourceTree,
                     class_types: Optional[Dict[str, str]] = None) -> Tuple[List[EnrichmentInput], int]:
         inputs, failed = [], 0
         for ident in idents:
             unit = parsed.units.get(ident)
             if unit is None:
                 continue
-            src = self._read_source(clone_dir, unit)
+            src = self._read_source(tree, unit)
             if src is None:
                 failed += 1
                 continue
@@ -363,7 +371,7 @@ class Indexer:
         return inputs, failed
 
     def _enrich_identifiers(self, idents: Sequence[str], parsed: ParsedProject, graph: ProjectGraph,
-                            clone_dir: str, readme: Optional[str],
+                            tree: SourceTree, readme: Optional[str],
                             methods_by_ident: Optional[Dict[str, List[Tuple[str, str]]]] = None
                             ) -> Tuple[int, int]:
         enriched = failed = 0
@@ -372,7 +380,7 @@ class Indexer:
         for b in range(0, len(idents), self.batch_size):
             batch = idents[b:b + self.batch_size]
             LOG.info("Enriching batch %d/%d (%d classes)", b // self.batch_size + 1, nbatches, len(batch))
-            inputs, read_failed = self._inputs_for(batch, parsed, clone_dir)
+            inputs, read_failed = self._inputs_for(batch, parsed, tree)
             failed += read_failed
             for result in self.backend.enrich_batch(inputs, readme):
                 if not result.success:
@@ -386,7 +394,7 @@ class Indexer:
         return enriched, failed
 
     def _recover_unenriched(self, project: Project, parsed: ParsedProject, graph: ProjectGraph,
-                            clone_dir: str, readme: Optional[str]) -> int:
+                            tree: SourceTree, readme: Optional[str]) -> int:
         unenriched = self.repos.classes.find_unenriched_by_project_id(project.id)
         if not unenriched:
             LOG.info("Phase 3: No unenriched classes found, skipping recovery")
@@ -396,7 +404,7 @@ class Indexer:
         types = {sc.full_class_name: sc.class_type.value for sc in unenriched}
         idents = [sc.full_class_name for sc in unenriched]
         for b in range(0, len(idents), self.batch_size):
-            inputs, _ = self._inputs_for(idents[b:b + self.batch_size], parsed, clone_dir, types)
+            inputs, _ = self._inputs_for(idents[b:b + self.batch_size], parsed, tree, types)
             if not inputs:
                 continue
             for result in self.backend.enrich_batch(inputs, readme):
@@ -471,9 +479,9 @@ class Indexer:
         stats: Dict[str, float] = {}
         try:
             with span("rebuild.total", stats, project=project.name):
-                clone = self.git.clone(project.repository_url, project.default_branch, shallow=True)
-                parser = detect_parser(clone.directory, self.parser_threads)
-                parsed = parser.scan(clone.directory)
+                clone = self._fetch(project.repository_url, project.default_branch, shallow=True)
+                parser = parser_for(clone.detect_language(), self.parser_threads)
+                parsed = parser.scan_tree(clone)
                 graph = parsed.build_graph()
                 existing = self.repos.classes.find_by_project_id(project_id)
                 by_name = {sc.full_class_name: sc for sc in existing}
@@ -505,7 +513,7 @@ class Indexer:
             raise DomainError(f"Graph rebuild failed: {e}", "REBUILD_FAILED", e) from e
         finally:
             if clone is not None:
-                self.git.cleanup(clone.directory)
+                clone.cleanup()
             lock.release()
 
     def _attach_metadata(self, graph: ProjectGraph, parsed: ParsedProject, by_name: Dict[str, SourceClass],
@@ -565,20 +573,20 @@ class Indexer:
             project.start_sync()
             self.repos.projects.update_status(project)
             with span("sync.total", stats, project=project.name):
-                clone = self.git.clone(project.repository_url, project.default_branch, shallow=False,
-                                       directory=self.git.new_clone_dir(project.name, "-sync"))
+                # full history: the diff needs the previously analyzed commit
+                clone = self._fetch(project.repository_url, project.default_branch, shallow=False)
                 head = clone.commit_hash
                 if head == project.last_commit_hash:
                     LOG.info("No changes detected for project: %s (HEAD: %s)", project.name, head)
                     project.sync_completed(project.last_commit_hash)
                     self.repos.projects.update_status(project)
                     return SyncResult.no_changes(project.name)
-                diff = self.git.diff(clone.directory, project.last_commit_hash, head)
-                readme = read_readme(clone.directory, self.max_readme_length)
+                diff = self.git.diff(clone.git_dir, project.last_commit_hash, head)
+                readme = clone.readme(self.max_readme_length)
                 if readme is not None:
                     project.update_description(readme[:self.description_length])
-                parser = detect_parser(clone.directory, self.parser_threads)
-                parsed = parser.scan(clone.directory)
+                parser = parser_for(clone.detect_language(), self.parser_threads)
+                parsed = parser.scan_tree(clone)
                 graph = parsed.build_graph()
                 existing = self.repos.classes.find_by_project_id(project.id)
                 by_name = {sc.full_class_name: sc for sc in existing}
@@ -647,7 +655,7 @@ class Indexer:
                 enriched = failed = 0
                 if self.backend.enabled and changed:
                     self._attach_metadata(graph, parsed, all_classes, {**mb_un, **mb})
-                    enriched, failed = self._enrich_identifiers(changed, parsed, graph, clone.directory, readme,
+                    enriched, failed = self._enrich_identifiers(changed, parsed, graph, clone, readme,
                                                                 methods_by_ident)
                 # final metadata from the DB (enrichment included)
                 final_classes = {sc.full_class_name: sc for sc in self.repos.classes.find_by_project_id(project.id)}
@@ -669,7 +677,7 @@ class Indexer:
             return SyncResult.failure(project.name, str(e))
         finally:
             if clone is not None:
-                self.git.cleanup(clone.directory)
+                clone.cleanup()
             lock.release()
 
     def _relink_graph_only(self, graph: ProjectGraph, parsed: ParsedProject, classes: Dict[str, SourceClass],
@@ -721,14 +729,14 @@ class Indexer:
             ProjectGraph.from_json(project.graph_data) if project.graph_data else None)
         if graph is None:
             raise DomainError("No graph data available for this project", "NO_GRAPH")
-        clone = self.git.clone(project.repository_url, project.default_branch, shallow=True)
+        clone = self._fetch(project.repository_url, project.default_branch, shallow=True)
         try:
-            parsed = detect_parser(clone.directory, self.parser_threads).scan(clone.directory)
-            readme = read_readme(clone.directory, self.max_readme_length)
-            recovered = self._recover_unenriched(project, parsed, graph, clone.directory, readme)
+            parsed = parser_for(clone.detect_language(), self.parser_threads).scan_tree(clone)
+            readme = clone.readme(self.max_readme_length)
+            recovered = self._recover_unenriched(project, parsed, graph, clone, readme)
             project.update_graph_data(graph.to_json())
             self.repos.projects.update(project)
             self.cache.put(project.id, project.name, graph)
             return {"success": True, "projectId": project_id, "recovered": recovered}
         finally:
-            self.git.cleanup(clone.directory)
+            clone.cleanup()

@@ -33,12 +33,14 @@ def new_id() -> str:
 
 
 def new_ids(n: int) -> List[str]:
-    """``n`` UUID4 strings; uses the native bulk generator when available."""
+    """``n`` UUID strings for a batch of new rows.  The native generator emits
+    time-ordered version-7 UUIDs (ordered within the batch) so bulk inserts
+    append to the primary-key B-trees; the reference used random UUID4s."""
     if n <= 0:
         return []
     try:
         from .. import _srcscan  # type: ignore
-        return _srcscan.uuid4_batch(n)
+        return _srcscan.uuid7_batch(n)
     except (ImportError, AttributeError):
         return [str(uuid.uuid4()) for _ in range(n)]
 

@@ -191,6 +191,17 @@ class SourceParser:
                  (time.perf_counter() - t0) * 1e3, self.project.stats.get("elapsedUs", 0) / 1e3)
         return self.project
 
+    def scan_tree(self, tree) -> ParsedProject:
+        """Scans a :class:`dmcp.index.source.SourceTree` (in-memory git snapshot
+        or checkout) -- same result as :meth:`scan` over a checkout of it."""
+        t0 = time.perf_counter()
+        doc = json.loads(tree.scan(self.language_name, self.threads, self.framework_override))
+        self.project = to_parsed_project(doc)
+        self._root = tree.directory
+        LOG.info("Scanned %s @ %s: %d files, %d units in %.1f ms", tree.directory, tree.commit_hash[:12],
+                 self.project.stats.get("analyzed", 0), len(self.project.units), (time.perf_counter() - t0) * 1e3)
+        return self.project
+
     def parse(self, project_root: str) -> ProjectGraph:
         return self.scan(project_root).build_graph()
 

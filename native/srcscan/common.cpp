@@ -2,8 +2,11 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <dirent.h>
+#include <memory>
 #include <mutex>
 #include <sys/stat.h>
+#include <unordered_map>
 
 namespace srcscan {
 
@@ -346,7 +349,109 @@ void parallel_for(size_t n, int threads, const std::function<void(size_t)>& fn) 
 }
 
 // ----------------------------------------------------------------- files
+namespace {
+
+constexpr std::string_view kVfsPrefix = "/__vfs__/";
+
+struct VirtualTree {
+    std::unordered_map<std::string, std::string> files;  // rel path -> content
+    std::unordered_map<std::string, std::vector<std::pair<std::string, bool>>> dirs;  // rel dir -> children
+};
+
+std::mutex g_vfs_mu;
+std::unordered_map<std::string, std::shared_ptr<const VirtualTree>> g_vfs;  // root -> tree
+long long g_vfs_next = 0;
+
+// Resolves a mounted path: returns the tree and sets rel ("" for the root).
+std::shared_ptr<const VirtualTree> vfs_resolve(const std::string& path, std::string& rel) {
+    if (path.compare(0, kVfsPrefix.size(), kVfsPrefix) != 0) return nullptr;
+    size_t slash = path.find('/', kVfsPrefix.size());
+    std::string root = path.substr(0, slash);
+    rel = slash == std::string::npos ? std::string() : path.substr(slash + 1);
+    while (!rel.empty() && rel.back() == '/') rel.pop_back();
+    std::lock_guard<std::mutex> lk(g_vfs_mu);
+    auto it = g_vfs.find(root);
+    return it == g_vfs.end() ? nullptr : it->second;
+}
+
+}  // namespace
+
+std::string vfs_mount(std::vector<std::pair<std::string, std::string>>&& files) {
+    auto tree = std::make_shared<VirtualTree>();
+    std::unordered_map<std::string, std::unordered_map<std::string, bool>> kids;  // dir -> name -> is_dir
+    kids[""];
+    tree->files.reserve(files.size());
+    for (auto& kv : files) {
+        std::string rel = kv.first;
+        while (!rel.empty() && rel.front() == '/') rel.erase(0, 1);
+        if (rel.empty()) continue;
+        // register every ancestor directory
+        size_t pos = 0;
+        std::string parent;
+        while (true) {
+            size_t s = rel.find('/', pos);
+            bool is_dir = s != std::string::npos;
+            std::string name = rel.substr(pos, is_dir ? s - pos : std::string::npos);
+            kids[parent].emplace(name, is_dir);
+            if (!is_dir) break;
+            parent = parent.empty() ? name : parent + "/" + name;
+            kids[parent];
+            pos = s + 1;
+        }
+        tree->files[rel] = std::move(kv.second);
+    }
+    for (auto& d : kids) {
+        auto& v = tree->dirs[d.first];
+        v.assign(d.second.begin(), d.second.end());
+        std::sort(v.begin(), v.end(), [](const std::pair<std::string, bool>& a, const std::pair<std::string, bool>& b) {
+            return a.first < b.first;
+        });
+    }
+    std::lock_guard<std::mutex> lk(g_vfs_mu);
+    std::string root = std::string(kVfsPrefix) + std::to_string(++g_vfs_next);
+    g_vfs[root] = std::move(tree);
+    return root;
+}
+
+void vfs_unmount(const std::string& root) {
+    std::lock_guard<std::mutex> lk(g_vfs_mu);
+    g_vfs.erase(root);
+}
+
+bool list_dir(const std::string& dir, std::vector<std::pair<std::string, bool>>& out) {
+    out.clear();
+    std::string rel;
+    if (auto t = vfs_resolve(dir, rel)) {
+        auto it = t->dirs.find(rel);
+        if (it == t->dirs.end()) return false;
+        out = it->second;
+        return true;
+    }
+    DIR* d = opendir(dir.c_str());
+    if (!d) return false;
+    while (dirent* e = readdir(d)) {
+        std::string name = e->d_name;
+        if (name == "." || name == "..") continue;
+        bool is_dir = e->d_type == DT_DIR;
+        if (e->d_type == DT_UNKNOWN) is_dir = dir_exists(join_path(dir, name));
+        out.emplace_back(std::move(name), is_dir);
+    }
+    closedir(d);
+    std::sort(out.begin(), out.end(),
+              [](const std::pair<std::string, bool>& a, const std::pair<std::string, bool>& b) {
+                  return a.first < b.first;
+              });
+    return true;
+}
+
 bool read_file(const std::string& path, std::string& out, size_t max_bytes) {
+    std::string rel;
+    if (auto t = vfs_resolve(path, rel)) {
+        auto it = t->files.find(rel);
+        if (it == t->files.end() || (max_bytes && it->second.size() > max_bytes)) return false;
+        out = it->second;
+        return true;
+    }
     FILE* f = std::fopen(path.c_str(), "rb");
     if (!f) return false;
     std::fseek(f, 0, SEEK_END);
@@ -361,11 +466,15 @@ bool read_file(const std::string& path, std::string& out, size_t max_bytes) {
 }
 
 bool file_exists(const std::string& path) {
+    std::string rel;
+    if (auto t = vfs_resolve(path, rel)) return t->files.count(rel) > 0;
     struct stat st;
     return ::stat(path.c_str(), &st) == 0 && S_ISREG(st.st_mode);
 }
 
 bool dir_exists(const std::string& path) {
+    std::string rel;
+    if (auto t = vfs_resolve(path, rel)) return t->dirs.count(rel) > 0;
     struct stat st;
     return ::stat(path.c_str(), &st) == 0 && S_ISDIR(st.st_mode);
 }

@@ -119,9 +119,18 @@ bool parse_json(std::string_view text, JsonValue& out);
 void parallel_for(size_t n, int threads, const std::function<void(size_t)>& fn);
 
 // ------------------------------------------------------------------- files
+// Every filesystem access of the front-ends goes through these helpers, which
+// also serve *mounted in-memory trees*: paths under a root returned by
+// vfs_mount() ("/__vfs__/<n>") resolve against that tree, so a project can be
+// scanned straight from git objects without a checkout on disk.
 bool read_file(const std::string& path, std::string& out, size_t max_bytes = 0);
 bool file_exists(const std::string& path);
 bool dir_exists(const std::string& path);
+// Sorted (name, is_dir) children of a directory (real or mounted).
+bool list_dir(const std::string& dir, std::vector<std::pair<std::string, bool>>& out);
+// Mounts files given as (relative path, content); returns the virtual root.
+std::string vfs_mount(std::vector<std::pair<std::string, std::string>>&& files);
+void vfs_unmount(const std::string& root);
 std::string join_path(const std::string& a, const std::string& b);
 std::string normalize_path(const std::string& p);  // resolves . and .. lexically
 

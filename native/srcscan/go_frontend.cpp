@@ -658,20 +658,12 @@ struct DirEntry {
     bool is_dir;
 };
 
-std::vector<DirEntry> list_dir(const std::string& dir) {
+std::vector<DirEntry> go_list_dir(const std::string& dir) {
+    std::vector<std::pair<std::string, bool>> raw;
     std::vector<DirEntry> out;
-    DIR* d = opendir(dir.c_str());
-    if (!d) return out;
-    while (dirent* e = readdir(d)) {
-        std::string name = e->d_name;
-        if (name == "." || name == "..") continue;
-        bool is_dir = false;
-        if (e->d_type == DT_DIR) is_dir = true;
-        else if (e->d_type == DT_UNKNOWN || e->d_type == DT_LNK) is_dir = dir_exists(join_path(dir, name)) && e->d_type != DT_LNK;
-        out.push_back({name, is_dir});
-    }
-    closedir(d);
-    std::sort(out.begin(), out.end(), [](const DirEntry& a, const DirEntry& b) { return a.name < b.name; });
+    if (!list_dir(dir, raw)) return out;  // sorted; symlinks are not followed as dirs
+    out.reserve(raw.size());
+    for (auto& e : raw) out.push_back({std::move(e.first), e.second});
     return out;
 }
 
@@ -680,7 +672,7 @@ std::vector<DirEntry> list_dir(const std::string& dir) {
 void walk_packages(const std::string& dir, const std::string& rel, std::vector<std::pair<std::string, std::string>>& out,
                    bool is_root) {
     bool recorded = false;
-    for (auto& e : list_dir(dir)) {
+    for (auto& e : go_list_dir(dir)) {
         if (e.is_dir) {
             if (excluded_dir(e.name)) continue;
             walk_packages(join_path(dir, e.name), rel.empty() ? e.name : rel + "/" + e.name, out, false);
@@ -724,7 +716,7 @@ void analyze_package(const std::string& root, const std::string& dir, const std:
     pa.path = rel.empty() ? module : module + "/" + rel;
     std::vector<FileParse> parses;
     std::vector<std::string> sources;
-    for (auto& e : list_dir(dir)) {
+    for (auto& e : go_list_dir(dir)) {
         if (e.is_dir || !eligible_go_file(e.name)) continue;
         std::string src;
         if (!read_file(join_path(dir, e.name), src)) continue;

@@ -40,18 +40,11 @@ struct Entry {
 };
 
 std::vector<Entry> entries(const std::string& dir) {
+    std::vector<std::pair<std::string, bool>> raw;
     std::vector<Entry> out;
-    DIR* d = opendir(dir.c_str());
-    if (!d) return out;
-    while (dirent* e = readdir(d)) {
-        std::string name = e->d_name;
-        if (name == "." || name == "..") continue;
-        bool is_dir = e->d_type == DT_DIR;
-        if (e->d_type == DT_UNKNOWN) is_dir = dir_exists(join_path(dir, name));
-        out.push_back({name, is_dir});
-    }
-    closedir(d);
-    std::sort(out.begin(), out.end(), [](const Entry& a, const Entry& b) { return a.name < b.name; });
+    if (!list_dir(dir, raw)) return out;  // sorted by name; real or mounted tree
+    out.reserve(raw.size());
+    for (auto& e : raw) out.push_back({std::move(e.first), e.second});
     return out;
 }
 

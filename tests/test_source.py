@@ -1,0 +1,110 @@
+"""Source trees: in-memory git snapshots (bare clone + cat-file, native scan of
+a mounted tree) must index exactly what a checkout does; size-capped fallback
+to a checkout; the native VFS mount."""
+import json
+import os
+import subprocess
+
+import pytest
+
+from conftest import make_app
+from dmcp.index.git import GitClient
+from dmcp.index.source import CheckoutTree, MemoryTree, detect_language_from, wanted
+from dmcp.models.domain import RepositoryUrl
+from dmcp.parsers.base import native
+from dmcp.utils import synth
+
+
+def _git(root, *args):
+    subprocess.run(["git", "-C", str(root), *args], check=True, capture_output=True)
+
+
+def test_wanted_and_language_detection():
+    assert wanted("src/main/java/A.java") and wanted("web/x.tsx") and wanted("README.md")
+    assert not wanted("docs/README.md") and not wanted("node_modules/x/index.js")
+    assert not wanted("web/node_modules/y.ts") and not wanted("img.png")
+    assert detect_language_from(["go.mod", "main.go"]) == "go"
+    assert detect_language_from(["package.json", "src/a.ts"]) == "typescript"
+    assert detect_language_from(["package.json", "pom.xml"]) == "java"
+
+
+@pytest.mark.parametrize("kind", ["java", "nest", "go"])
+def test_snapshot_equals_checkout(tmp_path, kind):
+    repo = tmp_path / "r"
+    if kind == "java":
+        synth.java_spring_repo(str(repo), 24)
+    elif kind == "nest":
+        synth.nestjs_repo(str(repo), 4)
+    else:
+        synth.go_gin_repo(str(repo), 3)
+    g = GitClient(str(tmp_path / "clones"))
+    url = RepositoryUrl.of(str(repo))
+    mem = g.snapshot(url, "main")
+    assert isinstance(mem, MemoryTree) and not os.path.exists(os.path.join(mem.directory, "README.md"))
+    c = g.clone(url, "main")
+    disk = CheckoutTree(c.directory, c.commit_hash)
+    assert mem.commit_hash == disk.commit_hash and mem.detect_language() == disk.detect_language()
+    lang = disk.detect_language()
+    a, b = json.loads(mem.scan(lang, 4)), json.loads(disk.scan(lang, 4))
+    a["stats"] = b["stats"] = None
+    assert a == b and a["files"]
+    assert mem.readme() == disk.readme()
+    some = a["files"][0]["path"]
+    assert mem.read_text(some) == disk.read_text(some)
+    mem.cleanup()
+    disk.cleanup()
+    assert not os.listdir(tmp_path / "clones")
+
+
+def test_snapshot_fallback_to_checkout_and_errors(tmp_path):
+    repo = tmp_path / "r"
+    synth.java_spring_repo(str(repo), 8)
+    g = GitClient(str(tmp_path / "clones"))
+    t = g.snapshot(RepositoryUrl.of(str(repo)), "main", max_bytes=100)
+    assert isinstance(t, CheckoutTree) and os.path.isfile(os.path.join(t.directory, "README.md"))
+    t.cleanup()
+    with pytest.raises(Exception):
+        g.snapshot(RepositoryUrl.of(str(tmp_path / "missing")), "main")
+    with pytest.raises(Exception):
+        g.snapshot(RepositoryUrl.of(str(repo)), "no-such-branch")
+    assert not os.listdir(tmp_path / "clones")
+
+
+def test_symlinks_and_submodule_entries_skipped(tmp_path):
+    repo = tmp_path / "r"
+    synth.java_spring_repo(str(repo), 8)
+    os.symlink("README.md", repo / "LINK.java")
+    _git(repo, "add", "-A")
+    _git(repo, "-c", "user.email=a@b", "-c", "user.name=n", "commit", "-qm", "link")
+    t = GitClient(str(tmp_path / "c")).snapshot(RepositoryUrl.of(str(repo)), "main")
+    assert "LINK.java" not in t.files and "README.md" in t.files
+    t.cleanup()
+
+
+def test_in_memory_and_checkout_pipelines_agree(tmp_path):
+    synth.java_spring_repo(str(tmp_path / "shop"), 16)
+    results = {}
+    for mode in (True, False):
+        app = make_app(tmp_path / f"m{mode}", git_in_memory=mode)
+        r = app.indexer.analyze_project(str(tmp_path / "shop"))
+        g = app.cache.get_graph(r.project_id)
+        results[mode] = (r.classes_analyzed, r.endpoints_found, sorted(g.identifiers()),
+                         {i: g.dependencies(i) for i in g.identifiers()},
+                         sorted(c.description for c in app.repos.classes.find_by_project_id(r.project_id)))
+        s = app.indexer.sync_project(app.repos.projects.find_by_id(r.project_id))
+        assert s.success
+        app.close()
+    assert results[True] == results[False]
+
+
+def test_vfs_mount_listing_and_isolation(tmp_path):
+    n = native()
+    files = [("src/main/java/a/A.java", b"package a;\nimport b.B;\n@Service public class A {}"),
+             ("src/main/java/b/B.java", b"package b;\npublic class B {}")]
+    doc = json.loads(n.scan_sources(files, "auto", 2, ""))
+    assert doc["language"] == "java" and [f["identifier"] for f in doc["files"]] == ["a.A", "b.B"]
+    assert doc["files"][0]["deps"] == ["b.B"] and doc["files"][0]["classType"] == "SERVICE"
+    assert json.loads(n.scan_sources([], "java", 1, ""))["files"] == []
+    ts = json.loads(n.scan_sources([("package.json", b'{"dependencies":{"express":"4"}}'),
+                                    ("src/r.ts", b"router.get('/x', h);\n")], "auto", 1, ""))
+    assert ts["language"] == "typescript" and ts["framework"]["name"] == "express" and ts["files"][0]["entryPoint"]

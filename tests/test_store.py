@@ -105,6 +105,21 @@ def test_class_method_param_repositories(repos):
     assert repos.classes.count_by_project_id(p.id) == 1 and repos.params.find_by_method_id(m1.id) == []
 
 
+def test_bulk_replace_keeps_referential_integrity(tmp_path):
+    from conftest import make_app
+    from dmcp.utils import synth
+    synth.java_spring_repo(str(tmp_path / "shop"), 16)
+    app = make_app(tmp_path)
+    for _ in range(2):  # second run replaces every row inside bulk_transaction
+        r = app.indexer.analyze_project(str(tmp_path / "shop"))
+    assert app.db.query("PRAGMA foreign_key_check") == []
+    assert app.db.query_one("PRAGMA foreign_keys")[0] == 1  # enforcement restored
+    n = app.db.query_one("SELECT COUNT(*) FROM method_parameters p JOIN source_methods m ON m.id = p.method_id "
+                         "JOIN source_classes c ON c.id = p.class_id WHERE c.project_id = ?", (r.project_id,))[0]
+    assert n == app.db.query_one("SELECT COUNT(*) FROM method_parameters")[0] > 0
+    app.close()
+
+
 def test_cascade_delete_project(repos):
     p = _project()
     repos.projects.save(p)

@@ -108,3 +108,20 @@ def test_vfs_mount_listing_and_isolation(tmp_path):
     ts = json.loads(n.scan_sources([("package.json", b'{"dependencies":{"express":"4"}}'),
                                     ("src/r.ts", b"router.get('/x', h);\n")], "auto", 1, ""))
     assert ts["language"] == "typescript" and ts["framework"]["name"] == "express" and ts["files"][0]["entryPoint"]
+
+
+def test_default_procs_tracks_object_store(tmp_path):
+    """Loose stores get several readers, packed stores at most two."""
+    import subprocess
+    from dmcp.index.source import default_procs, mostly_loose
+    from dmcp.utils import synth
+    src = tmp_path / "src"
+    synth.java_spring_repo(str(src), 300)
+    bare = tmp_path / "b"
+    subprocess.run(["git", "clone", "-q", "--bare", "--shared", str(src), str(bare)], check=True)
+    assert mostly_loose(str(bare))
+    assert default_procs(str(bare), 2000) >= 1
+    subprocess.run(["git", "-C", str(src), "gc", "-q", "--prune=now"], check=True)
+    assert not mostly_loose(str(bare))
+    assert default_procs(str(bare), 2000) <= 2
+    assert default_procs(str(bare), 10) == 1

@@ -84,8 +84,12 @@ def build_srcscan(force: bool = False, sanitize: bool = False, jobs: int = 0) ->
     inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", f"-I{NATIVE}"]
     py_obj = os.path.join(BUILD, f"pymodule.{_digest([os.path.join(NATIVE, 'pymodule.cpp')])}.o")
     _run([CXX, *CXXFLAGS, *inc, "-fvisibility=hidden", "-c", os.path.join(NATIVE, "pymodule.cpp"), "-o", py_obj])
+    # bulk row writer: module-only (the CLI never touches the database); links
+    # the system libsqlite3 runtime, the same library Python's sqlite3 uses
+    bw_obj = os.path.join(BUILD, "bulkwriter.o")
+    _run([CXX, *CXXFLAGS, f"-I{NATIVE}", "-c", os.path.join(NATIVE, "bulkwriter.cpp"), "-o", bw_obj])
     tmp = target + ".tmp"
-    _run([CXX, "-shared", "-pthread", "-o", tmp, py_obj, *objs])
+    _run([CXX, "-shared", "-pthread", "-o", tmp, py_obj, bw_obj, *objs, "-l:libsqlite3.so.0"])
     os.replace(tmp, target)
     os.makedirs(BIN, exist_ok=True)
     _run([CXX, *CXXFLAGS, "-o", cli, os.path.join(NATIVE, "cli.cpp"), *objs])

@@ -44,7 +44,7 @@ from ..graph.project_graph import MethodEnrichmentData, MethodInfo, ProjectGraph
 from ..models.domain import (ClassType, Project, ProjectStatus, RepositoryUrl, SourceClass,
                              new_id, new_ids, package_name_of, simple_name_of, utc_now)
 from ..parsers.base import ParsedProject, ParsedUnit, SourceParser, parser_for
-from ..store.repositories import Repositories, to_iso
+from ..store.repositories import ProjectRowsWriter, Repositories, to_iso
 from ..utils.errors import DomainError
 from ..utils.tracing import METRICS, span
 from .git import GitClient
@@ -178,6 +178,7 @@ class Indexer:
                               "PROJECT_BUSY")
         stats: Dict[str, float] = {}
         clone: Optional[SourceTree] = None
+        writer: Optional[ProjectRowsWriter] = None
         project = self._prepare_project(url, branch_name)
         try:
             with span("analyze.total", stats, project=project.name):
@@ -194,9 +195,11 @@ class Indexer:
                 order = graph.analysis_order()
                 with span("analyze.phase1", stats):
                     p1 = self._phase1_static(project, parsed, graph, order, clone.commit_hash, replace=True)
-                classes, methods_by_ident = p1
+                classes, methods_by_ident, writer = p1
                 enriched = failed = recovered = 0
                 if self.backend.enabled:
+                    with span("analyze.phase1_commit", stats):
+                        writer.wait()  # enrichment updates the rows just written
                     with span("analyze.phase2", stats):
                         enriched, failed = self._enrich_identifiers(order, parsed, graph, clone,
                                                                     readme, methods_by_ident)
@@ -206,6 +209,8 @@ class Indexer:
                 with span("analyze.persist_graph", stats):
                     project.base_package = common_package_prefix(package_name_of(i) for i in parsed.units)
                     project.update_graph_data(graph.to_json())
+                    with span("analyze.phase1_commit", stats):
+                        writer.wait()  # no-op when enrichment already waited
                     project.analysis_completed(clone.commit_hash)
                     self.repos.projects.update(project)
                     self.cache.put(project.id, project.name, graph)
@@ -219,6 +224,11 @@ class Indexer:
             return AnalysisResult(True, project.id, classes, endpoints, "Analysis complete", stats)
         except Exception as e:
             LOG.error("Analysis failed for %s: %s", repository_url, e, exc_info=True)
+            if writer is not None:
+                try:
+                    writer.wait()  # the row swap finishes (or has failed) before the status write
+                except Exception:
+                    pass
             self._mark_error(project)
             raise DomainError(f"Analysis failed: {e}", "ANALYSIS_FAILED", e) from e
         finally:
@@ -263,9 +273,11 @@ class Indexer:
     # ---------------------------------------------------------------- phase 1
     def _phase1_static(self, project: Project, parsed: ParsedProject, graph: ProjectGraph,
                        order: Sequence[str], commit_hash: str, replace: bool
-                       ) -> Tuple[int, Dict[str, List[Tuple[str, str]]]]:
-        """Builds every class / method / parameter row and the graph metadata,
-        then swaps them in with one transaction (old rows deleted in it)."""
+                       ) -> Tuple[int, Dict[str, List[Tuple[str, str]]], ProjectRowsWriter]:
+        """Builds every class / method / parameter row and the graph metadata
+        and streams them to a :class:`ProjectRowsWriter`, which swaps them in
+        with one transaction (old rows deleted in it) on its own thread; the
+        caller must ``wait()`` on the returned writer before touching the rows."""
         now = to_iso(utc_now())
         pid = project.id
         cls_rows: List[tuple] = []
@@ -280,6 +292,21 @@ class Indexer:
         def nid() -> str:
             return next(id_pool, None) or new_id()
 
+        # the writer thread starts deleting the old rows right away
+        writer = self.repos.project_rows_writer(pid, replace)
+        try:
+            self._phase1_rows(order, units, graph, pid, now, commit_hash, nid, class_ids, methods_by_ident,
+                              cls_rows, meth_rows, param_rows, writer)
+            writer.close()
+        except BaseException:
+            writer.abort()
+            raise
+        LOG.info("Phase 1 rows built. Classes: %d, Methods: %d, Parameters: %d",
+                 len(cls_rows), len(meth_rows), len(param_rows))
+        return len(cls_rows), methods_by_ident, writer
+
+    def _phase1_rows(self, order, units, graph, pid, now, commit_hash, nid, class_ids, methods_by_ident,
+                     cls_rows, meth_rows, param_rows, writer) -> None:
         for ident in order:
             unit = units.get(ident)
             if unit is None:
@@ -304,6 +331,8 @@ class Indexer:
                 mids.append((sm.method_name, mid))
             graph.set_method_infos(ident, infos)
             methods_by_ident[ident] = mids
+        writer.put("classes", cls_rows)
+        writer.put("methods", meth_rows)
         for ident, cid in class_ids.items():
             graph.bind_class_id(ident, cid)
         # second pass: parameter links (CodeContextService.java:274-291, 805-856)
@@ -324,18 +353,7 @@ class Indexer:
                     tcid = class_ids.get(tgt)
                     if tcid is not None:
                         param_rows.append((nid(), mid, pos, tcid, now))
-        with self.repos.db.bulk_transaction():
-            if replace:
-                # children first: the FK cascade then finds nothing to do per row
-                self.repos.params.delete_by_project_id(pid)
-                self.repos.methods.delete_by_project_id(pid)
-                self.repos.classes.delete_by_project_id(pid)
-            self.repos.classes.save_rows(cls_rows)
-            self.repos.methods.save_rows(meth_rows)
-            self.repos.params.save_rows(param_rows)
-        LOG.info("Phase 1 complete. Classes: %d, Methods: %d, Parameters: %d",
-                 len(cls_rows), len(meth_rows), len(param_rows))
-        return len(cls_rows), methods_by_ident
+        writer.put("params", param_rows)
 
     # ------------------------------------------------------------ enrichment
     def _read_source(self, tree: SourceTree, unit: ParsedUnit) -> Optional[str]:

@@ -187,6 +187,10 @@ class Database:
         conn.execute("PRAGMA cache_size = -65536")
         return conn
 
+    def is_shared_memory(self) -> bool:
+        """A private ``:memory:`` database: one connection shared by all threads."""
+        return self._shared_memory_conn is not None
+
     @property
     def conn(self) -> sqlite3.Connection:
         if self._shared_memory_conn is not None:

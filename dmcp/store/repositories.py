@@ -315,9 +315,11 @@ class SourceClassRepository:
             c.executemany("UPDATE source_classes SET commit_hash = ? WHERE id = ?",
                           [(commit_hash, i) for i in class_ids])
 
+    DELETE_BY_PROJECT_ID = "DELETE FROM source_classes WHERE project_id = ?"
+
     def delete_by_project_id(self, project_id: str) -> None:
         with self.db.transaction() as c:
-            c.execute("DELETE FROM source_classes WHERE project_id = ?", (project_id,))
+            c.execute(self.DELETE_BY_PROJECT_ID, (project_id,))
 
     def delete_by_ids(self, ids: Sequence[str]) -> None:
         if not ids:
@@ -448,10 +450,12 @@ class SourceMethodRepository:
         with self.db.transaction() as c:
             c.execute("DELETE FROM source_methods WHERE class_id = ?", (class_id,))
 
+    DELETE_BY_PROJECT_ID = ("DELETE FROM source_methods WHERE class_id IN "
+                            "(SELECT id FROM source_classes WHERE project_id = ?)")
+
     def delete_by_project_id(self, project_id: str) -> None:
         with self.db.transaction() as c:
-            c.execute("DELETE FROM source_methods WHERE class_id IN "
-                      "(SELECT id FROM source_classes WHERE project_id = ?)", (project_id,))
+            c.execute(self.DELETE_BY_PROJECT_ID, (project_id,))
 
     def delete_by_class_ids(self, class_ids: Sequence[str]) -> None:
         if not class_ids:
@@ -517,10 +521,12 @@ class MethodParameterRepository:
                 c.execute("DELETE FROM method_parameters WHERE method_id IN (SELECT id FROM source_methods "
                           f"WHERE class_id IN ({','.join('?' * len(chunk))}))", chunk)
 
+    DELETE_BY_PROJECT_ID = ("DELETE FROM method_parameters WHERE method_id IN (SELECT m.id FROM source_methods m "
+                            "JOIN source_classes c ON c.id = m.class_id WHERE c.project_id = ?)")
+
     def delete_by_project_id(self, project_id: str) -> None:
         with self.db.transaction() as c:
-            c.execute("DELETE FROM method_parameters WHERE method_id IN (SELECT m.id FROM source_methods m "
-                      "JOIN source_classes c ON c.id = m.class_id WHERE c.project_id = ?)", (project_id,))
+            c.execute(self.DELETE_BY_PROJECT_ID, (project_id,))
 
 
 class Repositories:
@@ -532,3 +538,162 @@ class Repositories:
         self.classes = SourceClassRepository(db)
         self.methods = SourceMethodRepository(db)
         self.params = MethodParameterRepository(db)
+
+    def project_rows_writer(self, project_id: str, replace: bool) -> "ProjectRowsWriter":
+        return ProjectRowsWriter(self, project_id, replace)
+
+
+class ProjectRowsWriter:
+    """Whole-project row swap (old class/method/parameter rows deleted, new
+    ones inserted, one transaction) run on a writer thread while the caller
+    is still building the rows.
+
+    The reference saves rows one JPA/JDBI call at a time inside the analysis
+    loop (``CodeContextService.java:244-291``).  Here the caller streams the
+    three row batches with :meth:`put` as soon as each is built; the writer
+    thread opens the transaction immediately, deletes the project's old rows
+    while the first batch is still being assembled, and inserts each batch in
+    parent-before-child order.
+
+    On a database file the writer is native (``native/srcscan/bulkwriter.cpp``):
+    its own SQLite connection on a C++ thread, so binding and B-tree work run
+    without the GIL and overlap the Python row building and the graph
+    serialisation that follows (a Python writer thread would convoy on the GIL
+    once per row).  Without the native module, a Python thread does the same
+    work.  A private ``:memory:`` database (one shared connection) runs the
+    steps synchronously.  :meth:`wait` re-raises any writer error;
+    :meth:`abort` rolls the transaction back.
+    """
+
+    _ORDER = ("classes", "methods", "params")
+    BUSY_TIMEOUT_MS = 30_000
+
+    def __init__(self, repos: "Repositories", project_id: str, replace: bool) -> None:
+        import queue
+        import threading
+        self.repos = repos
+        self.project_id = project_id
+        self.replace = replace
+        self.rows_written = 0
+        self._error: Optional[BaseException] = None
+        self._sync = repos.db.is_shared_memory()
+        self._q: "queue.Queue" = queue.Queue()
+        self._pending: Dict[str, Sequence[tuple]] = {}
+        self._thread: Optional[threading.Thread] = None
+        self._next = 0
+        self._done = False
+        self._native = None
+        if self._sync:
+            return
+        bulk = _native_bulk_writer()
+        if bulk is not None:
+            setup = []
+            if replace:
+                setup = [(r.DELETE_BY_PROJECT_ID, (project_id,)) for r in (repos.params, repos.methods, repos.classes)]
+            self._native = bulk(repos.db.path, self.BUSY_TIMEOUT_MS, setup)
+            return
+        self._thread = threading.Thread(target=self._run, name="dmcp-rows-writer", daemon=True)
+        self._thread.start()
+
+    # ------------------------------------------------------------ producer
+    def put(self, table: str, rows: Sequence[tuple]) -> None:
+        if table not in self._ORDER:
+            raise ValueError(f"unknown table {table}")
+        if self._native is not None:
+            if self._ORDER.index(table) < self._next:
+                raise ValueError(f"{table} rows after their children")
+            self._next = self._ORDER.index(table) + 1
+            if rows:
+                self._native.put(getattr(self.repos, table)._INSERT, list(rows))
+        elif self._sync:
+            self._pending[table] = rows
+        else:
+            self._q.put((table, rows))
+
+    def close(self) -> None:
+        """No more rows: the writer commits once everything queued is in."""
+        if self._native is not None:
+            self._native.commit()
+        elif self._sync:
+            self._write_all(iter(self._pending.items()))
+        else:
+            self._q.put(None)
+
+    def abort(self) -> None:
+        self._done = True
+        if self._native is not None:
+            self._native.abort()
+        elif self._thread is not None:
+            self._q.put(("__abort__", ()))
+            self._thread.join()
+
+    def wait(self) -> int:
+        if self._native is not None:
+            if not self._done:
+                self._done = True
+                try:
+                    self.rows_written = self._native.wait()
+                except RuntimeError as e:
+                    self._error = e
+        elif self._thread is not None:
+            self._thread.join()
+        if self._error is not None:
+            raise self._error
+        return self.rows_written
+
+    # -------------------------------------------------------------- writer
+    def _run(self) -> None:
+        def batches():
+            while True:
+                item = self._q.get()
+                if item is None:
+                    return
+                if item[0] == "__abort__":
+                    raise _Aborted()
+                yield item
+        try:
+            self._write_all(batches())
+        except _Aborted:
+            pass
+        except BaseException as e:  # surfaced by wait()
+            self._error = e
+            while True:  # drain so a producer never blocks on us
+                try:
+                    if self._q.get_nowait() is None:
+                        break
+                except Exception:
+                    break
+
+    def _write_all(self, batches) -> None:
+        r = self.repos
+        pending: Dict[str, Sequence[tuple]] = {}
+        nxt = 0
+        with r.db.bulk_transaction():
+            if self.replace:
+                # children first: the FK cascade then finds nothing to do per row
+                r.params.delete_by_project_id(self.project_id)
+                r.methods.delete_by_project_id(self.project_id)
+                r.classes.delete_by_project_id(self.project_id)
+            for table, rows in batches:
+                pending[table] = rows
+                while nxt < len(self._ORDER) and self._ORDER[nxt] in pending:
+                    name = self._ORDER[nxt]
+                    rows = pending.pop(name)
+                    getattr(r, name).save_rows(rows)
+                    self.rows_written += len(rows)
+                    nxt += 1
+            if pending:
+                raise RuntimeError(f"rows for {sorted(pending)} arrived without their parents")
+
+
+class _Aborted(Exception):
+    pass
+
+
+def _native_bulk_writer():
+    """``dmcp._srcscan.BulkWriter`` or None (module absent / predates it)."""
+    try:
+        from .. import _srcscan  # type: ignore
+    except ImportError:
+        return None
+    return getattr(_srcscan, "BulkWriter", None)

@@ -1,0 +1,75 @@
+// Bulk row writer: one SQLite write transaction driven by its own thread.
+//
+// The indexer replaces a project's class / method / parameter rows in one
+// transaction (pipeline Phase 1).  Through Python's sqlite3 module every row
+// costs a GIL round-trip, so the B-tree work can neither leave the
+// interpreter nor overlap the Python code that builds the rows and the graph
+// JSON.  A BulkWriter opens its own connection on a worker thread, runs the
+// setup statements (the old rows' deletes) as soon as it is created, then
+// inserts each queued batch; the producer only pays for copying the values
+// out of Python objects.
+#pragma once
+
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <utility>
+#include <vector>
+
+namespace dbw {
+
+struct Value {
+    enum Kind : uint8_t { Null, Int, Real, Text } kind = Null;
+    int64_t i = 0;
+    double d = 0.0;
+    std::string s;
+};
+
+// rows flattened row-major: values.size() == ncols * rows
+struct Batch {
+    std::string sql;
+    int ncols = 0;
+    std::vector<Value> values;
+};
+
+class BulkWriter {
+  public:
+    // `setup`: statements run right after BEGIN IMMEDIATE, in order.
+    BulkWriter(std::string path, int busy_timeout_ms, std::vector<Batch> setup);
+    ~BulkWriter();
+    BulkWriter(const BulkWriter&) = delete;
+    BulkWriter& operator=(const BulkWriter&) = delete;
+
+    void put(Batch batch);
+    void commit();             // no more batches: COMMIT once the queue drains
+    void abort();              // ROLLBACK (queued batches are dropped) and join
+    std::string wait();        // join; "" on success, else the error message
+    int64_t rows_written() const { return rows_written_; }
+
+  private:
+    enum class Op { Rows, Commit, Abort };
+    struct Item {
+        Op op;
+        Batch batch;
+    };
+    void run();
+    void push(Item it);
+    bool pop(Item& out);
+
+    std::string path_;
+    int busy_ms_;
+    std::vector<Batch> setup_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<Item> queue_;
+    std::thread thread_;
+    std::string error_;
+    int64_t rows_written_ = 0;
+    bool joined_ = false;
+    bool commit_requested_ = false;
+};
+
+}  // namespace dbw

@@ -7,9 +7,54 @@
 #include <cstring>
 #include <vector>
 
+#include "bulkwriter.hpp"
 #include "srcscan.hpp"
 
 namespace py = pybind11;
+
+namespace {
+
+// list of equal-length tuples of None / int / float / str -> one flattened
+// batch (CPython API directly: this runs with the GIL held, per value)
+dbw::Batch to_batch(const std::string& sql, py::list rows) {
+    dbw::Batch b;
+    b.sql = sql;
+    const Py_ssize_t n = PyList_GET_SIZE(rows.ptr());
+    if (n == 0) return b;
+    PyObject* first = PyList_GET_ITEM(rows.ptr(), 0);
+    if (!PyTuple_Check(first)) throw py::type_error("rows must be tuples");
+    b.ncols = static_cast<int>(PyTuple_GET_SIZE(first));
+    b.values.resize(static_cast<size_t>(n) * b.ncols);
+    for (Py_ssize_t r = 0; r < n; ++r) {
+        PyObject* row = PyList_GET_ITEM(rows.ptr(), r);
+        if (!PyTuple_Check(row) || PyTuple_GET_SIZE(row) != b.ncols) throw py::type_error("ragged rows");
+        for (int c = 0; c < b.ncols; ++c) {
+            PyObject* o = PyTuple_GET_ITEM(row, c);
+            dbw::Value& v = b.values[static_cast<size_t>(r) * b.ncols + c];
+            if (o == Py_None) {
+                v.kind = dbw::Value::Null;
+            } else if (PyUnicode_Check(o)) {
+                Py_ssize_t len = 0;
+                const char* s = PyUnicode_AsUTF8AndSize(o, &len);
+                if (!s) throw py::error_already_set();
+                v.kind = dbw::Value::Text;
+                v.s.assign(s, static_cast<size_t>(len));
+            } else if (PyBool_Check(o) || PyLong_Check(o)) {
+                v.kind = dbw::Value::Int;
+                v.i = PyLong_AsLongLong(o);
+                if (v.i == -1 && PyErr_Occurred()) throw py::error_already_set();
+            } else if (PyFloat_Check(o)) {
+                v.kind = dbw::Value::Real;
+                v.d = PyFloat_AS_DOUBLE(o);
+            } else {
+                throw py::type_error("unsupported column value type");
+            }
+        }
+    }
+    return b;
+}
+
+}  // namespace
 
 PYBIND11_MODULE(_srcscan, m) {
     m.doc() = "Native Java / TypeScript / Go source front-ends for dmcp";
@@ -159,5 +204,36 @@ PYBIND11_MODULE(_srcscan, m) {
             return out;
         },
         py::arg("n"));
-    m.attr("ABI_VERSION") = 1;
+
+    py::class_<dbw::BulkWriter>(m, "BulkWriter",
+                                "One SQLite write transaction on a worker thread (see bulkwriter.hpp).")
+        .def(py::init([](const std::string& path, int busy_timeout_ms, py::list setup) {
+                 std::vector<dbw::Batch> stmts;
+                 for (auto item : setup) {
+                     auto tup = item.cast<py::tuple>();
+                     py::list one;
+                     one.append(tup[1]);
+                     stmts.push_back(to_batch(tup[0].cast<std::string>(), one));
+                 }
+                 return new dbw::BulkWriter(path, busy_timeout_ms, std::move(stmts));
+             }),
+             py::arg("path"), py::arg("busy_timeout_ms"), py::arg("setup"))
+        .def(
+            "put", [](dbw::BulkWriter& w, const std::string& sql, py::list rows) { w.put(to_batch(sql, rows)); },
+            py::arg("sql"), py::arg("rows"))
+        .def("commit", &dbw::BulkWriter::commit)
+        .def("abort", &dbw::BulkWriter::abort, py::call_guard<py::gil_scoped_release>())
+        .def(
+            "wait",
+            [](dbw::BulkWriter& w) {
+                std::string err;
+                {
+                    py::gil_scoped_release release;
+                    err = w.wait();
+                }
+                if (!err.empty()) throw std::runtime_error("bulk write failed: " + err);
+                return w.rows_written();
+            })
+        .def_property_readonly("rows_written", &dbw::BulkWriter::rows_written);
+    m.attr("ABI_VERSION") = 2;
 }

@@ -229,3 +229,63 @@ def test_query_plans_use_indexes(repos):
     # the partial endpoint index serves the endpoint queries
     assert "idx_source_methods_http_endpoints" in _plan(db, *cases["endpoints by project"]) or \
         "idx_source_methods_class_name" in _plan(db, *cases["endpoints by project"])
+
+
+@pytest.mark.parametrize("mode", ["native", "pythread"])
+def test_project_rows_writer_commit_abort_and_failure(tmp_path, monkeypatch, mode):
+    """The background row swap commits everything, rolls back on abort, and
+    surfaces a constraint failure from wait() with nothing half-written."""
+    import dmcp.store.repositories as R
+    from dmcp.store.db import Database
+    if mode == "native":
+        assert R._native_bulk_writer() is not None, "native BulkWriter missing from dmcp._srcscan"
+    else:
+        monkeypatch.setattr(R, "_native_bulk_writer", lambda: None)
+    db = Database(str(tmp_path / "w.db"))
+    repos = R.Repositories(db)
+    p = _project()
+    repos.projects.save(p)
+    now = "2026-01-01T00:00:00.000000Z"
+
+    def rows(tag):
+        cls = [(f"c{tag}{i}", p.id, f"a.b.C{tag}{i}", f"C{tag}{i}", "a.b", "SERVICE", None, "F.java", now, "h")
+               for i in range(50)]
+        meth = [(f"m{tag}{i}", f"c{tag}{i // 2}", "run", None, "[]", "[]", None, None, i, now) for i in range(100)]
+        par = [(f"p{tag}{i}", f"m{tag}{i}", 0, f"c{tag}{(i + 1) % 50}", now) for i in range(100)]
+        return cls, meth, par
+
+    def swap(tag, replace=True):
+        w = repos.project_rows_writer(p.id, replace)
+        c, m, pr = rows(tag)
+        w.put("classes", c)
+        w.put("methods", m)
+        w.put("params", pr)
+        return w
+
+    w = swap("a", replace=False)
+    w.close()
+    assert w.wait() == 250
+    assert repos.classes.count_by_project_id(p.id) == 50
+
+    w = swap("b")
+    w.abort()  # rolled back: generation "a" intact
+    assert {c.full_class_name for c in repos.classes.find_by_project_id(p.id)} == {f"a.b.Ca{i}" for i in range(50)}
+
+    w = repos.project_rows_writer(p.id, True)
+    c, m, pr = rows("c")
+    w.put("classes", c + c[:1])  # duplicate primary key -> the whole swap fails
+    w.put("methods", m)
+    w.close()
+    with pytest.raises(Exception):
+        w.wait()
+    assert repos.classes.count_by_project_id(p.id) == 50
+    assert db.query_one("SELECT COUNT(*) FROM method_parameters")[0] == 100
+
+    w = swap("d")
+    w.close()
+    w.wait()
+    names = {c.full_class_name for c in repos.classes.find_by_project_id(p.id)}
+    assert names == {f"a.b.Cd{i}" for i in range(50)}
+    assert db.query_one("SELECT COUNT(*) FROM source_methods")[0] == 100
+    assert db.query("PRAGMA foreign_key_check") == []
+    db.close()

@@ -26,6 +26,7 @@ BUILD = os.path.join(ROOT, "build", "native")
 BIN = os.path.join(ROOT, "bin")
 
 CORE_SOURCES = ["common.cpp", "java_frontend.cpp", "ts_frontend.cpp", "go_frontend.cpp", "project.cpp"]
+MODULE_SOURCES = ["bulkwriter.cpp", "gitobj.cpp"]
 CXX = os.environ.get("CXX", "g++")
 CXXFLAGS = ["-std=c++17", "-O3", "-fPIC", "-Wall", "-Wno-unused-function", "-pthread"]
 
@@ -84,12 +85,16 @@ def build_srcscan(force: bool = False, sanitize: bool = False, jobs: int = 0) ->
     inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", f"-I{NATIVE}"]
     py_obj = os.path.join(BUILD, f"pymodule.{_digest([os.path.join(NATIVE, 'pymodule.cpp')])}.o")
     _run([CXX, *CXXFLAGS, *inc, "-fvisibility=hidden", "-c", os.path.join(NATIVE, "pymodule.cpp"), "-o", py_obj])
-    # bulk row writer: module-only (the CLI never touches the database); links
-    # the system libsqlite3 runtime, the same library Python's sqlite3 uses
-    bw_obj = os.path.join(BUILD, "bulkwriter.o")
-    _run([CXX, *CXXFLAGS, f"-I{NATIVE}", "-c", os.path.join(NATIVE, "bulkwriter.cpp"), "-o", bw_obj])
+    # module-only sources (the CLI neither writes the database nor reads git
+    # objects): the bulk row writer links the system libsqlite3 runtime (the
+    # library Python's sqlite3 uses), the loose-object reader links zlib
+    mod_objs = []
+    for src in MODULE_SOURCES:
+        obj = os.path.join(BUILD, src[:-4] + ".o")
+        _run([CXX, *CXXFLAGS, f"-I{NATIVE}", "-c", os.path.join(NATIVE, src), "-o", obj])
+        mod_objs.append(obj)
     tmp = target + ".tmp"
-    _run([CXX, "-shared", "-pthread", "-o", tmp, py_obj, bw_obj, *objs, "-l:libsqlite3.so.0"])
+    _run([CXX, "-shared", "-pthread", "-o", tmp, py_obj, *mod_objs, *objs, "-l:libsqlite3.so.0", "-lz"])
     os.replace(tmp, target)
     os.makedirs(BIN, exist_ok=True)
     _run([CXX, *CXXFLAGS, "-o", cli, os.path.join(NATIVE, "cli.cpp"), *objs])

@@ -39,6 +39,7 @@ class GitClient:
         self.clone_base_path = clone_base_path
         self.ssh_key_path = ssh_key_path
         self.timeout = timeout_seconds
+        self.read_local_in_place = True  # snapshot(): local repositories without a private clone
 
     def _env(self) -> dict:
         env = dict(os.environ)
@@ -102,9 +103,11 @@ class GitClient:
         working-tree checkout (bare clone + ``cat-file --batch``); falls back to
         a checkout when the candidate sources exceed ``max_bytes``."""
         from .source import CheckoutTree, MemoryTree, list_tree, read_blobs, wanted
+        local = url.local_path()
+        if local is not None and self.read_local_in_place:
+            return self._local_snapshot(url, os.path.abspath(local), branch, shallow, max_bytes)
         dest = self.new_clone_dir(url.repository_name(), "-bare")
         args = ["clone", "--quiet", "--no-tags", "--bare"]
-        local = url.local_path()
         if local is not None:
             args += ["--shared", "--single-branch"]
             source = os.path.abspath(local)
@@ -134,6 +137,37 @@ class GitClient:
             shutil.rmtree(dest, ignore_errors=True)
             raise
         return MemoryTree(dest, commit, {e[0]: b for e, b in zip(entries, blobs)})
+
+    def resolve_commit(self, repo_dir: str, branch: Optional[str]) -> str:
+        """The commit ``git clone --branch <branch>`` would check out: the
+        branch head, else the tag of that name; HEAD when no branch is given."""
+        refs = [f"refs/heads/{branch}", f"refs/tags/{branch}"] if branch else ["HEAD"]
+        for ref in refs:
+            rc, out, _ = self._git(["rev-parse", "--verify", "--quiet", f"{ref}^{{commit}}"], cwd=repo_dir,
+                                   check=False)
+            if rc == 0 and out.strip():
+                return out.strip()
+        raise GitError(f"Remote branch {branch} not found in upstream origin" if branch
+                       else "repository has no HEAD commit")
+
+    def _local_snapshot(self, url: RepositoryUrl, source: str, branch: Optional[str], shallow: bool,
+                        max_bytes: int):
+        """A local repository's objects are read in place: content-addressed
+        objects never change, so a private clone adds nothing but a process
+        and a ref copy.  The tree does not own (and never deletes) ``source``."""
+        from .source import CheckoutTree, MemoryTree, list_tree, read_blobs, wanted
+        LOG.info("Reading %s (branch: %s) in place", url, branch)
+        try:
+            commit = self.resolve_commit(source, branch)
+            entries = [e for e in list_tree(self, source, commit) if wanted(e[0])]
+            blobs = read_blobs(self, source, [e[1] for e in entries], max_bytes)
+        except GitError as e:
+            raise GitError(f"Failed to clone repository: {e}") from e
+        if blobs is None:
+            LOG.info("%s: sources exceed the %d MiB in-memory limit, using a checkout", url, max_bytes >> 20)
+            c = self.clone(url, branch, shallow=shallow)
+            return CheckoutTree(c.directory, c.commit_hash)
+        return MemoryTree(source, commit, {e[0]: b for e, b in zip(entries, blobs)}, owned=False)
 
     def head(self, repo_dir: str) -> str:
         return self._git(["rev-parse", "HEAD"], cwd=repo_dir)[1].strip()

@@ -5,12 +5,13 @@ The reference clones every repository to a temp directory with JGit, walks
 the checkout, and deletes it afterwards (``CodeContextService.java:1653-1683``,
 ``:465``).  Writing thousands of files only to read them once and unlink them
 was the largest single cost of an analysis here (≈ 35 % of a 2,000-class
-index on MI355X hosts).  :class:`MemoryTree` instead clones **bare**
-(``--shared`` for local repositories, ``--depth 1`` for remote analyses), lists
-the commit with ``git ls-tree`` and streams the blobs the front-ends need
-through a few concurrent ``git cat-file --batch`` processes; the native scanner then parses a
-mounted in-memory tree (``srcscan.scan_sources``) and enrichment reads source
-text from the same map.  Every byte of every source file at HEAD is still
+index on MI355X hosts).  :class:`MemoryTree` instead reads git objects: a
+remote repository is cloned **bare** (``--depth 1``), a local one is read in
+place (its objects are content-addressed and immutable).  The commit is listed
+with ``git ls-tree``; loose blobs are inflated natively on a thread pool
+(``native/srcscan/gitobj.cpp``) and packed ones streamed through ``git
+cat-file --batch``.  The native scanner then parses a mounted in-memory tree
+(``srcscan.scan_sources``) and enrichment reads source text from the same map.  Every byte of every source file at HEAD is still
 read and parsed; nothing is cached across analyses.  Repositories larger than
 ``max_bytes`` of candidate sources fall back to a regular checkout
 (:class:`CheckoutTree`).
@@ -107,8 +108,11 @@ class CheckoutTree(SourceTree):
 
 
 class MemoryTree(SourceTree):
-    def __init__(self, git_dir: str, commit_hash: str, files: Dict[str, bytes]) -> None:
-        self.directory = git_dir
+    """``owned``: ``git_dir`` is a private bare clone removed by :meth:`cleanup`
+    (False when a local repository's object store is read in place)."""
+
+    def __init__(self, git_dir: str, commit_hash: str, files: Dict[str, bytes], owned: bool = True) -> None:
+        self.directory = git_dir if owned else None
         self.git_dir = git_dir
         self.commit_hash = commit_hash
         self.files = files
@@ -197,10 +201,47 @@ def default_procs(git_dir: str, n_blobs: int) -> int:
     return 2 if n_blobs >= 1024 and cpus > 1 else 1
 
 
-def read_blobs(git, git_dir: str, shas: List[str], max_bytes: int = 0, procs: int = 0) -> Optional[List[bytes]]:
-    """Contents of ``shas`` through ``procs`` concurrent ``git cat-file --batch``
-    processes (0 = :func:`default_procs`); None as soon as more than
-    ``max_bytes`` (if > 0) of blob data has arrived in total."""
+def _native_loose_reader():
+    try:
+        from .. import _srcscan  # type: ignore
+    except ImportError:
+        return None
+    return getattr(_srcscan, "read_loose_blobs", None)
+
+
+def read_blobs(git, git_dir: str, shas: List[str], max_bytes: int = 0, procs: int = 0,
+               threads: int = 0) -> Optional[List[bytes]]:
+    """Contents of ``shas``; None as soon as more than ``max_bytes`` (if > 0)
+    of blob data has arrived in total.
+
+    A mostly-loose store is inflated natively on ``threads`` workers
+    (``native/srcscan/gitobj.cpp``; 0 = up to 16), and only the objects that are
+    not loose go through git; otherwise ``procs`` concurrent ``git cat-file
+    --batch`` processes read everything (0 = :func:`default_procs`)."""
+    if not shas:
+        return []
+    reader = _native_loose_reader()
+    if reader is not None and mostly_loose(git_dir):
+        nthreads = threads or max(1, min(16, os.cpu_count() or 1, len(shas) // 64 or 1))
+        blobs, exceeded = reader(_object_dirs(git_dir), shas, nthreads, max_bytes)
+        if exceeded:
+            return None
+        missing = [i for i, b in enumerate(blobs) if b is None]
+        if missing:
+            have = sum(len(b) for b in blobs if b is not None)
+            if max_bytes and have > max_bytes:
+                return None
+            rest = _read_via_git(git, git_dir, [shas[i] for i in missing], max_bytes - have if max_bytes else 0,
+                                 procs)
+            if rest is None:
+                return None
+            for i, b in zip(missing, rest):
+                blobs[i] = b
+        return blobs
+    return _read_via_git(git, git_dir, shas, max_bytes, procs)
+
+
+def _read_via_git(git, git_dir: str, shas: List[str], max_bytes: int, procs: int) -> Optional[List[bytes]]:
     if not shas:
         return []
     if procs <= 0:

@@ -1,0 +1,22 @@
+// Loose git object reader (see gitobj.cpp).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace gitobj {
+
+struct LooseResult {
+    std::vector<std::string> data;  // blob contents (valid where found[i])
+    std::vector<uint8_t> found;     // 0: not a loose blob in any object dir
+    uint64_t total_bytes = 0;
+    bool exceeded = false;          // more than max_bytes of content read
+};
+
+// Reads `shas` (40-hex object ids) from the first of `object_dirs` holding
+// each as a loose object, on `threads` workers (0 = hardware concurrency).
+LooseResult read_loose_blobs(const std::vector<std::string>& object_dirs, const std::vector<std::string>& shas,
+                             int threads, uint64_t max_bytes);
+
+}  // namespace gitobj

@@ -1,6 +1,7 @@
 // Python binding: dmcp._srcscan (pybind11, host C++ only).
 // The GIL is released during scanning so REST/MCP threads keep serving.
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 #include <sys/random.h>
 
 #include <chrono>
@@ -8,6 +9,7 @@
 #include <vector>
 
 #include "bulkwriter.hpp"
+#include "gitobj.hpp"
 #include "srcscan.hpp"
 
 namespace py = pybind11;
@@ -204,6 +206,28 @@ PYBIND11_MODULE(_srcscan, m) {
             return out;
         },
         py::arg("n"));
+
+    m.def(
+        "read_loose_blobs",
+        [](const std::vector<std::string>& object_dirs, const std::vector<std::string>& shas, int threads,
+           uint64_t max_bytes) {
+            gitobj::LooseResult r;
+            {
+                py::gil_scoped_release release;
+                r = gitobj::read_loose_blobs(object_dirs, shas, threads, max_bytes);
+            }
+            py::list out(shas.size());
+            for (size_t i = 0; i < shas.size(); ++i) {
+                if (r.found[i])
+                    out[i] = py::bytes(r.data[i]);
+                else
+                    out[i] = py::none();
+                std::string().swap(r.data[i]);
+            }
+            return py::make_tuple(out, r.exceeded);
+        },
+        py::arg("object_dirs"), py::arg("shas"), py::arg("threads") = 0, py::arg("max_bytes") = 0,
+        "Loose-object blob contents (None where an object is not loose) and whether max_bytes was exceeded.");
 
     py::class_<dbw::BulkWriter>(m, "BulkWriter",
                                 "One SQLite write transaction on a worker thread (see bulkwriter.hpp).")

@@ -40,7 +40,13 @@ def test_snapshot_equals_checkout(tmp_path, kind):
     g = GitClient(str(tmp_path / "clones"))
     url = RepositoryUrl.of(str(repo))
     mem = g.snapshot(url, "main")
-    assert isinstance(mem, MemoryTree) and not os.path.exists(os.path.join(mem.directory, "README.md"))
+    # a local repository is read in place: nothing to own, nothing deleted
+    assert isinstance(mem, MemoryTree) and mem.directory is None and mem.git_dir == str(repo)
+    g.read_local_in_place = False  # the private bare-clone path (remote repositories)
+    bare = g.snapshot(url, "main")
+    assert isinstance(bare, MemoryTree) and not os.path.exists(os.path.join(bare.directory, "README.md"))
+    assert bare.files == mem.files and bare.commit_hash == mem.commit_hash
+    bare.cleanup()
     c = g.clone(url, "main")
     disk = CheckoutTree(c.directory, c.commit_hash)
     assert mem.commit_hash == disk.commit_hash and mem.detect_language() == disk.detect_language()
@@ -54,6 +60,7 @@ def test_snapshot_equals_checkout(tmp_path, kind):
     mem.cleanup()
     disk.cleanup()
     assert not os.listdir(tmp_path / "clones")
+    assert os.path.isdir(repo / ".git") and len(os.listdir(repo)) > 1  # source repository untouched
 
 
 def test_snapshot_fallback_to_checkout_and_errors(tmp_path):
@@ -125,3 +132,44 @@ def test_default_procs_tracks_object_store(tmp_path):
     assert not mostly_loose(str(bare))
     assert default_procs(str(bare), 2000) <= 2
     assert default_procs(str(bare), 10) == 1
+
+
+def test_native_loose_reader_matches_git_with_mixed_store(tmp_path):
+    """Loose objects come from the native inflater, packed ones from git; the
+    result equals cat-file's for every blob (empty and binary ones included)."""
+    import subprocess
+    from dmcp.index.git import GitClient
+    from dmcp.index.source import _native_loose_reader, _read_via_git, list_tree, read_blobs
+    assert _native_loose_reader() is not None, "dmcp._srcscan.read_loose_blobs missing"
+    src = tmp_path / "src"
+    src.mkdir()
+
+    def git(*a):
+        subprocess.run(["git", "-C", str(src), *a], check=True, capture_output=True)
+    git("init", "-q")
+    git("config", "user.email", "t@t")
+    git("config", "user.name", "t")
+    for i in range(40):
+        (src / f"A{i}.java").write_text(f"package a; class A{i} {{}}\n" * (i + 1))
+    git("add", ".")
+    git("commit", "-qm", "one")
+    git("gc", "-q", "--prune=now")  # first generation packed
+    (src / "Empty.java").write_bytes(b"")
+    (src / "Bin.java").write_bytes(bytes(range(256)) * 50)
+    for i in range(40, 80):
+        (src / f"A{i}.java").write_text(f"package a; class A{i} {{ int x = {i}; }}\n" * 30)
+    git("add", ".")
+    git("commit", "-qm", "two")  # second generation loose
+    g = GitClient(str(tmp_path / "c"))
+    shas = [s for _, s in list_tree(g, str(src), "HEAD")]
+    # force the native path regardless of the loose/packed heuristic
+    import dmcp.index.source as S
+    orig = S.mostly_loose
+    S.mostly_loose = lambda d: True
+    try:
+        got = read_blobs(g, str(src), shas)
+        assert read_blobs(g, str(src), shas, max_bytes=1000) is None
+    finally:
+        S.mostly_loose = orig
+    assert got == _read_via_git(g, str(src), shas, 0, 1)
+    assert b"" in got and bytes(range(256)) * 50 in got

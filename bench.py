@@ -2,9 +2,12 @@
 """Headline benchmark: classes indexed per second (BASELINE.json fallback metric).
 
 One *step* = one complete ``analyze_project`` of a synthetic Spring Boot
-monorepo through the production pipeline: git clone (file://, shallow) ->
-native C++ parse -> graph build -> Phase 1 persist (SQLite, one transaction,
-replacing the previous analysis) -> graph JSON -> cache publish.  Enrichment
+monorepo through the production pipeline: snapshot of the branch head (git
+objects read in place: ``ls-tree`` + native parallel inflate of every source
+blob) -> native C++ parse of the in-memory tree -> graph build -> Phase 1
+persist (SQLite, one transaction replacing the previous analysis, written by
+a native thread) -> graph JSON -> cache publish.  Every step re-reads and
+re-parses every file; nothing is cached across steps.  Enrichment
 is disabled by default (BASELINE: "Indexing throughput with enrichment
 disabled"); ``--enrich fake|local`` adds Phase 2/3 (``local`` = the optional
 MI355X model, see dmcp/enrich/local.py).

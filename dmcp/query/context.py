@@ -202,7 +202,9 @@ class ContextService:
         entries: List[dict] = []
         missing: List[dict] = []
         project_url = project_desc = project_id = None
-        methods_cache: Dict[str, List[SourceMethod]] = {}
+        # every frame's class methods in one query (reference: one per frame)
+        methods_cache: Dict[str, List[SourceMethod]] = self.repos.methods.find_by_class_ids(
+            list({sc.id for sc in classes.values()}))
         order = 1
         for f in frames:
             cname = str(f.get("className") or "")
@@ -215,9 +217,7 @@ class ContextService:
                                 "description": None, "businessLogic": [], "httpEndpoint": None, "found": False})
                 order += 1
                 continue
-            ms = methods_cache.get(sc.id)
-            if ms is None:
-                ms = methods_cache[sc.id] = self.repos.methods.find_by_class_id(sc.id)
+            ms = methods_cache.get(sc.id) or []
             method = None
             for cand in candidate_method_names(mname):
                 if cand is None:

@@ -64,7 +64,7 @@ def _json_list(value: Optional[Iterable[str]]) -> str:
 
 
 def _parse_json_list(text: Optional[str]) -> List[str]:
-    if text is None or text == "":
+    if not text or text == "[]":  # the common case: no exceptions / no logic
         return []
     try:
         v = json.loads(text)

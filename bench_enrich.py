@@ -26,8 +26,12 @@ def main(argv=None) -> int:
     ap.add_argument("--preset", default="dmcp-coder-1b")
     ap.add_argument("--classes", type=int, default=128, help="classes per rank")
     ap.add_argument("--batch", type=int, default=64, help="concurrent sequences (KV slots)")
-    ap.add_argument("--max-seq", type=int, default=4096)
+    ap.add_argument("--max-seq", type=int, default=8192)
     ap.add_argument("--prompt-chars", type=int, default=2048)
+    ap.add_argument("--readme-chars", type=int, default=4000,
+                    help="project README in every prompt (the reference sends up to 10,000 chars)")
+    ap.add_argument("--no-shared-prefix", action="store_true",
+                    help="prefill and attend to the instructions + README per class instead of once")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-jump", action="store_true", help="disable jump-forward over forced tokens")
     ap.add_argument("--warmup", type=int, default=8)
@@ -49,7 +53,15 @@ def main(argv=None) -> int:
         dist.init_process_group("nccl")
     cfg = preset(args.preset, max_batch=args.batch, max_seq=args.max_seq)
     model = LocalLM(cfg, device=f"cuda:{local}", seed=rank)
-    eng = LocalEngine(model, use_graphs=not args.no_graphs, jump_forward=not args.no_jump)
+    eng = LocalEngine(model, use_graphs=not args.no_graphs, jump_forward=not args.no_jump,
+                      shared_prefix=not args.no_shared_prefix)
+    para = ("The shop platform sells products to retail customers. Orders move from CART to PAID to "
+            "SHIPPED; payments are captured through the payment gateway and refunds are issued by the "
+            "back office. Inventory is reserved when an order is paid and released on cancellation.\n\n")
+    readme = "# Acme Shop\n\n"
+    while len(readme) < args.readme_chars:
+        readme += para
+    readme = readme[:args.readme_chars] if args.readme_chars > 0 else "Synthetic commerce platform"
     body = ("    public OrderResponse create(OrderRequest request) {\n"
             "        Order order = repository.save(Order.from(request));\n"
             "        events.publish(new OrderCreated(order.id()));\n        return OrderResponse.of(order);\n    }\n")
@@ -62,14 +74,14 @@ def main(argv=None) -> int:
                                ["create", "update", "find", "delete", "list", "validate"][: 2 + i % 5])
 
     inputs = [make(rank * 100000 + i) for i in range(args.classes)]
-    eng.generate([make(-1 - i) for i in range(args.warmup)], "Synthetic commerce platform")
+    eng.generate([make(-1 - i) for i in range(args.warmup)], readme)
     for k in eng.stats:
         eng.stats[k] = 0
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    outs = eng.generate(inputs, "Synthetic commerce platform")
+    outs = eng.generate(inputs, readme)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -90,8 +102,10 @@ def main(argv=None) -> int:
             "unit": "classes/s", "n_gpus": world, "higher_is_better": True, "scaling": "weak",
             "dtype": "bf16", "data": "synthetic classes, random-init weights",
             "config": {"model": cfg.name, "params_b": round(cfg.param_count() / 1e9, 3), "batch": args.batch,
-                       "max_seq": args.max_seq, "prompt_chars": args.prompt_chars, "graphs": not args.no_graphs,
-                       "jump_forward": not args.no_jump},
+                       "max_seq": args.max_seq, "prompt_chars": args.prompt_chars,
+                       "readme_chars": args.readme_chars, "graphs": not args.no_graphs,
+                       "jump_forward": not args.no_jump, "shared_prefix": not args.no_shared_prefix},
+            "shared_prefix_tokens": st["prefix_tokens"], "prefix_ms": round(1e3 * st["prefix_s"], 3),
             "generated_tokens_per_s": round(gen_all / elapsed, 1),
             "prompt_tokens_per_s": round(prompt_all / elapsed, 1),
             "decode_step_ms": round(1e3 * st["decode_s"] / max(1, st["decode_steps"]), 3),

@@ -147,9 +147,10 @@ class LocalEngine:
     """
 
     MASK_NO_QUOTE, MASK_QUOTE = 0, 1
+    MIN_SHARED_PREFIX = 64  # tokens; shorter common prefixes are not worth a separate prefill
 
     def __init__(self, model: LocalLM, use_graphs: bool = True, max_prompt_tokens: Optional[int] = None,
-                 jump_forward: bool = True) -> None:
+                 jump_forward: bool = True, shared_prefix: bool = True) -> None:
         self.model = model
         self.cfg: LMConfig = model.cfg
         dev = model.device
@@ -158,9 +159,10 @@ class LocalEngine:
         self.graphs = DecodeGraphs(model, self.masks) if use_graphs and dev.type == "cuda" else None
         self.max_prompt_tokens = max_prompt_tokens
         self.jump_forward = jump_forward
+        self.shared_prefix = shared_prefix and model.shared_prefix
         self.max_rows = model.max_rows
         self.stats = {"prompt_tokens": 0, "generated_tokens": 0, "decode_steps": 0, "decode_rows": 0,
-                      "prefills": 0, "decode_s": 0.0, "prefill_s": 0.0}
+                      "prefills": 0, "decode_s": 0.0, "prefill_s": 0.0, "prefix_tokens": 0, "prefix_s": 0.0}
         self._lock = threading.Lock()
 
     # ---------------------------------------------------------------- api
@@ -241,25 +243,41 @@ class LocalEngine:
             return s.segs[s.seg].min_len == 0
         return None
 
-    def _admit(self, s: _Seq, readme: Optional[str], results: Dict[int, str], free_slots: List[int]) -> bool:
-        """Prefill prompt + first forced segment; True if the sequence stays active."""
-        cfg = self.cfg
-        try:
-            budget = template_budget(s.segs)
-            if budget + 32 > cfg.max_seq:
-                raise ValueError(f"reply template needs {budget} tokens > max_seq {cfg.max_seq}")
-            prompt = self._prompt(s, readme, budget)
-        except Exception as e:
-            results[s.index] = json.dumps({"error": str(e)})
-            return False
+    def _build_prompt(self, s: _Seq, readme: Optional[str]) -> List[int]:
+        budget = template_budget(s.segs)
+        if budget + 32 > self.cfg.max_seq:
+            raise ValueError(f"reply template needs {budget} tokens > max_seq {self.cfg.max_seq}")
+        return self._prompt(s, readme, budget)
+
+    def _common_prefix(self, prompts: Sequence[List[int]]) -> int:
+        """Tokens shared by the start of every prompt (instructions + README
+        for classes of one project), leaving each prompt >= 1 own token."""
+        if not self.shared_prefix or len(prompts) < 2:
+            return 0
+        first = prompts[0]
+        n = min(len(p) for p in prompts) - 1
+        for p in prompts[1:]:
+            k = 0
+            while k < n and p[k] == first[k]:
+                k += 1
+            n = k
+            if n < self.MIN_SHARED_PREFIX:
+                return 0
+        return n if n >= self.MIN_SHARED_PREFIX else 0
+
+    def _admit(self, s: _Seq, prompt: List[int], prefix: int, results: Dict[int, str],
+               free_slots: List[int]) -> bool:
+        """Prefill prompt + first forced segment; True if the sequence stays active.
+        With a shared prefix of ``prefix`` tokens only the rest is prefilled."""
         s.slot = free_slots.pop()
         first = s.segs[0].forced or b""
         toks = prompt + list(first)
         t0 = time.perf_counter()
-        logits = self.model.forward_tokens(torch.tensor(toks, dtype=torch.int32), s.slot, 0)
+        start = self.model.fork_prefix(s.slot) if prefix else 0
+        logits = self.model.forward_tokens(torch.tensor(toks[start:], dtype=torch.int32), s.slot, start)
         self.stats["prefill_s"] += time.perf_counter() - t0
         self.stats["prefills"] += 1
-        self.stats["prompt_tokens"] += len(toks)
+        self.stats["prompt_tokens"] += len(toks) - start
         s.prompt_tokens = len(prompt)
         s.out.extend(first)
         s.pos = len(toks)
@@ -277,14 +295,39 @@ class LocalEngine:
     def _generate(self, inputs: Sequence[EnrichmentInput], readme: Optional[str]) -> List[str]:
         cfg = self.cfg
         reply_cap = cfg.max_seq - max(64, cfg.max_seq // 4)
-        pending: Deque[_Seq] = deque(_Seq(inp, i, fit_template(inp, reply_cap)) for i, inp in enumerate(inputs))
+        results: Dict[int, str] = {}
+        prompts: Dict[int, List[int]] = {}
+        pending: Deque[_Seq] = deque()
+        for i, inp in enumerate(inputs):
+            s = _Seq(inp, i, fit_template(inp, reply_cap))
+            try:
+                prompts[i] = self._build_prompt(s, readme)
+                pending.append(s)
+            except Exception as e:
+                results[i] = json.dumps({"error": str(e)})
+        # one prefill of the common prefix (instructions + README) for all
+        prefix = self._common_prefix(list(prompts.values()))
+        if prefix:
+            t0 = time.perf_counter()
+            self.model.set_prefix(prompts[pending[0].index][:prefix])
+            self.stats["prefix_s"] += time.perf_counter() - t0
+            self.stats["prefix_tokens"] += prefix
+        try:
+            self._run(pending, prompts, prefix, results)
+        finally:
+            if prefix:
+                self.model.clear_prefix()
+        return [results[i] for i in range(len(inputs))]
+
+    def _run(self, pending: Deque[_Seq], prompts: Dict[int, List[int]], prefix: int,
+             results: Dict[int, str]) -> None:
+        cfg = self.cfg
         free_slots = list(range(cfg.max_batch - 1, -1, -1))
         active: List[_Seq] = []
-        results: Dict[int, str] = {}
         while pending or active:
             while pending and free_slots:
                 s = pending.popleft()
-                if self._admit(s, readme, results, free_slots):
+                if self._admit(s, prompts.pop(s.index), prefix, results, free_slots):
                     active.append(s)
             if not active:
                 continue
@@ -330,7 +373,6 @@ class LocalEngine:
                 else:
                     still.append(s)
             active = still
-        return [results[i] for i in range(len(inputs))]
 
 
 class LocalLLMBackend(EnrichmentBackend):

@@ -84,11 +84,62 @@ def preset(name: str, **overrides) -> LMConfig:
     return replace(PRESETS[name], **overrides) if overrides else PRESETS[name]
 
 
+_LSE_IMPL: Dict[str, str] = {}
+
+
+def _attn_lse(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool, scale: float):
+    """Fused attention returning (out [1, H, T, D], natural-log LSE [1, H, T]
+    fp32); q/k/v with equal head counts.  Flash (aotriton on ROCm) first, the
+    memory-efficient kernel if flash is unavailable."""
+    T = q.shape[2]
+    if not q.is_cuda:
+        o, lse = torch.ops.aten._scaled_dot_product_flash_attention_for_cpu(q, k, v, 0.0, causal, scale=scale)[:2]
+        return o, lse
+    impl = _LSE_IMPL.get("cuda", "flash")
+    if impl == "flash":
+        try:
+            r = torch.ops.aten._scaled_dot_product_flash_attention(q, k, v, 0.0, causal, False, scale=scale)
+            return r[0], r[1][..., :T]
+        except RuntimeError:
+            _LSE_IMPL["cuda"] = "efficient"
+    r = torch.ops.aten._scaled_dot_product_efficient_attention(q, k, v, None, True, 0.0, causal, scale=scale)
+    return r[0], r[1][..., :T]
+
+
+def _extend_attention(qh: torch.Tensor, k: torch.Tensor, v: torch.Tensor, start: int, scale: float) -> torch.Tensor:
+    """Attention of T new queries (positions [start, start+T)) over the
+    cached context [0, start) -- fully visible -- and the new keys -- causal --
+    as two fused kernels merged by their log-sum-exp, instead of one kernel
+    with a materialised [T, start+T] mask (the math path: ~30x slower for a
+    4k-token README prefix).  qh [1, Hq, T, D]; k/v [1, Hkv, start+T, D]."""
+    Hq, Hkv = qh.shape[1], k.shape[1]
+    G = Hq // Hkv
+
+    def heads(t):
+        return t if G == 1 else t.repeat_interleave(G, dim=1)
+    kc, vc = heads(k[:, :, :start]), heads(v[:, :, :start])
+    kn, vn = heads(k[:, :, start:]), heads(v[:, :, start:])
+    o1, l1 = _attn_lse(qh, kc, vc, False, scale)
+    o2, l2 = _attn_lse(qh, kn, vn, True, scale)
+    m = torch.maximum(l1, l2)
+    w1 = torch.exp(l1 - m).unsqueeze(-1)
+    w2 = torch.exp(l2 - m).unsqueeze(-1)
+    return ((o1.float() * w1 + o2.float() * w2) / (w1 + w2)).to(qh.dtype)
+
+
 class LocalLM:
-    """Weights + KV cache + forward passes (prefill / extend / batched decode)."""
+    """Weights + KV cache + forward passes (prefill / extend / batched decode).
+
+    ``shared_prefix``: one extra KV slot (``prefix_slot``) holds a prompt
+    prefix common to every sequence of a batch (:meth:`set_prefix`); decode
+    then attends to it through the MFMA shared-prefix kernel, reading each
+    prefix key once per 32 queries instead of once per row, and prefill of a
+    sequence starts after it (:meth:`fork_prefix`)."""
+
+    PREFIX_CHUNK = 256  # prefix keys per MFMA work item
 
     def __init__(self, cfg: LMConfig, device: str = "cuda", seed: int = 0,
-                 weights: Optional[Dict[str, torch.Tensor]] = None) -> None:
+                 weights: Optional[Dict[str, torch.Tensor]] = None, shared_prefix: bool = True) -> None:
         if cfg.n_heads % cfg.n_kv_heads:
             raise ValueError("n_heads must be a multiple of n_kv_heads")
         self.cfg = cfg
@@ -96,14 +147,25 @@ class LocalLM:
         self.dtype = torch.bfloat16
         self.w = weights if weights is not None else self._init_weights(seed)
         c = cfg
-        kv_shape = (c.layers, c.max_batch, c.n_kv_heads, c.max_seq, c.head_dim)
+        self.shared_prefix = shared_prefix
+        self.num_slots = c.max_batch + (1 if shared_prefix else 0)
+        self.prefix_slot = c.max_batch if shared_prefix else -1
+        kv_shape = (c.layers, self.num_slots, c.n_kv_heads, c.max_seq, c.head_dim)
         self.k_cache = torch.zeros(kv_shape, dtype=self.dtype, device=self.device)
         self.v_cache = torch.zeros(kv_shape, dtype=self.dtype, device=self.device)
         self.cos_sin = ops.rope_tables(c.max_seq, c.head_dim, c.rope_theta, device=self.device).contiguous()
         self.scale = 1.0 / math.sqrt(c.head_dim)
         self.max_rows = max(c.max_batch, c.max_rows)
+        # shared prefix: V transposed per layer (the MFMA kernel's A operand),
+        # length in device memory so captured decode graphs follow it
+        self.prefix_len = 0
+        self.prefix_tokens: tuple = ()
+        self.prefix_dev = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.prefix_vt = (torch.zeros((c.layers, c.n_kv_heads, c.head_dim, c.max_seq), dtype=self.dtype,
+                                      device=self.device) if shared_prefix else None)
+        ps = ops.prefix_splits(c.max_seq, self.PREFIX_CHUNK) if shared_prefix else 0
         self.attn_ws = (ops.decode_workspace(self.max_rows, c.n_heads, c.n_kv_heads, c.head_dim, c.max_seq,
-                                             self.device) if self.device.type == "cuda" else None)
+                                             self.device, prefix_slots=ps) if self.device.type == "cuda" else None)
 
     # ------------------------------------------------------------ weights
     def _init_weights(self, seed: int) -> Dict[str, torch.Tensor]:
@@ -182,7 +244,7 @@ class LocalLM:
         T = int(tokens.numel())
         if T == 0:
             raise ValueError("forward_tokens needs at least one token")
-        if not (0 <= slot < c.max_batch) or start_pos < 0 or start_pos + T > c.max_seq:
+        if not (0 <= slot < self.num_slots) or start_pos < 0 or start_pos + T > c.max_seq:
             raise ValueError(f"sequence does not fit: slot={slot} start={start_pos} T={T} max_seq={c.max_seq}")
         dev = self.device
         ids = tokens.to(device=dev, dtype=torch.int32).contiguous()
@@ -192,10 +254,6 @@ class LocalLM:
         resid = x.clone()
         h = ops.add_rmsnorm(x, self.w["l0.ln1"], c.eps)
         L = start_pos + T
-        if start_pos > 0:
-            qi = torch.arange(start_pos, L, device=dev)[:, None]
-            kj = torch.arange(L, device=dev)[None, :]
-            mask = kj <= qi
         for i in range(c.layers):
             kc, vc = self.k_cache[i], self.v_cache[i]
             qkv = F.linear(h, self.w[f"l{i}.wqkv"])
@@ -205,8 +263,8 @@ class LocalLM:
             qh = q.transpose(0, 1).unsqueeze(0)  # [1, Hq, T, D]
             if start_pos == 0:
                 att = F.scaled_dot_product_attention(qh, k, v, is_causal=True, enable_gqa=True)
-            else:
-                att = F.scaled_dot_product_attention(qh, k, v, attn_mask=mask, enable_gqa=True)
+            else:  # extend after a cached context (e.g. a shared prefix)
+                att = _extend_attention(qh, k, v, start_pos, self.scale)
             o = F.linear(att[0].transpose(0, 1).reshape(T, c.n_heads * c.head_dim), self.w[f"l{i}.wo"])
             h = ops.add_rmsnorm(o, self.w[f"l{i}.ln2"], c.eps, residual=resid)
             m = self._mlp(i, h)
@@ -237,13 +295,54 @@ class LocalLM:
             kc, vc = self.k_cache[i], self.v_cache[i]
             qkv = F.linear(h, self.w[f"l{i}.wqkv"])
             q = ops.rope_kv(qkv, positions, slots, self.cos_sin, kc, vc, c.n_heads)
-            att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws, chunk=chunk)
+            prefix = (ops.SharedPrefix(kc[self.prefix_slot], self.prefix_vt[i], self.prefix_dev, self.PREFIX_CHUNK)
+                      if self.shared_prefix else None)
+            att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws, chunk=chunk,
+                                       prefix=prefix)
             o = F.linear(att.view(B, c.n_heads * c.head_dim), self.w[f"l{i}.wo"])
             h = ops.add_rmsnorm(o, self.w[f"l{i}.ln2"], c.eps, residual=resid)
             m = self._mlp(i, h)
             nxt = self.w[f"l{i + 1}.ln1"] if i + 1 < c.layers else self.w["norm_f"]
             h = ops.add_rmsnorm(m, nxt, c.eps, residual=resid)
         return F.linear(h, self.w["lm_head"])
+
+    # ---------------------------------------------------------- shared prefix
+    @torch.inference_mode()
+    def set_prefix(self, tokens: Sequence[int]) -> int:
+        """Prefills ``tokens`` into the prefix slot and publishes them as the
+        shared prefix of every following decode step (positions [0, P) of
+        each row).  Sequences must be started with :meth:`fork_prefix` +
+        ``forward_tokens(rest, slot, P)``.  Returns P."""
+        if not self.shared_prefix:
+            raise RuntimeError("model built without shared_prefix")
+        toks = tuple(int(t) for t in tokens)
+        P = len(toks)
+        if P == 0 or P >= self.cfg.max_seq:
+            raise ValueError(f"prefix length {P} out of range (max_seq {self.cfg.max_seq})")
+        if toks == self.prefix_tokens:
+            return P
+        self.clear_prefix()
+        self.forward_tokens(torch.tensor(toks, dtype=torch.int32), self.prefix_slot, 0)
+        self.prefix_vt[:, :, :, :P].copy_(self.v_cache[:, self.prefix_slot, :, :P].transpose(-1, -2))
+        self.prefix_len, self.prefix_tokens = P, toks
+        self.prefix_dev.fill_(P)
+        return P
+
+    def clear_prefix(self) -> None:
+        if self.shared_prefix:
+            self.prefix_dev.zero_()
+        self.prefix_len, self.prefix_tokens = 0, ()
+
+    @torch.inference_mode()
+    def fork_prefix(self, slot: int) -> int:
+        """Copies the shared prefix K/V into ``slot`` (what prefill of the
+        rest of that sequence attends to); decode reads the shared copy.
+        Returns P (0 when no prefix is set)."""
+        P = self.prefix_len
+        if P:
+            self.k_cache[:, slot, :, :P].copy_(self.k_cache[:, self.prefix_slot, :, :P])
+            self.v_cache[:, slot, :, :P].copy_(self.v_cache[:, self.prefix_slot, :, :P])
+        return P
 
     def decode_select(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor,
                       masks: torch.Tensor, mask_idx: torch.Tensor) -> tuple:

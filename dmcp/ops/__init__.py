@@ -30,18 +30,25 @@ def decode_chunk(rows, n_kv_heads, max_seq):
     return _dc(rows, n_kv_heads, max_seq)
 
 
-def decode_workspace(rows, n_heads, n_kv_heads, head_dim, max_seq, device, chunk: int = 256):
+def decode_workspace(rows, n_heads, n_kv_heads, head_dim, max_seq, device, chunk: int = 256, prefix_slots: int = 0):
     """Split-K scratch of the decode-attention kernel (fp32 partials + max/sum)."""
-    return _hip().decode_workspace(rows, n_heads, n_kv_heads, head_dim, max_seq, device, chunk)
+    return _hip().decode_workspace(rows, n_heads, n_kv_heads, head_dim, max_seq, device, chunk, prefix_slots)
+
+
+def prefix_splits(ldv, pchunk):
+    """Shared-prefix partial slots per (row, head) for a prefix capacity ``ldv``."""
+    from .hip import prefix_splits as _ps
+    return _ps(ldv, pchunk)
 
 
 def rope_kv(qkv, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out=None):
     return (_hip() if qkv.is_cuda else reference).rope_kv(qkv, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out)
 
 
-def decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace=None, chunk: int = 256, out=None):
+def decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace=None, chunk: int = 256, out=None,
+                     prefix=None):
     mod = _hip() if q.is_cuda else reference
-    return mod.decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace, chunk, out)
+    return mod.decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace, chunk, out, prefix)
 
 
 def silu_mul(gate_up, out=None):
@@ -57,3 +64,4 @@ def embedding(table, ids, out=None):
 
 
 rope_tables = reference.rope_tables
+SharedPrefix = reference.SharedPrefix

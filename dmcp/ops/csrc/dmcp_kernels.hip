@@ -194,17 +194,24 @@ __global__ __launch_bounds__(kBlock) void rope_kv_kernel(const uint16_t* __restr
 //    the output directly, otherwise fp32 partials merged by
 //    decode_attn_combine_kernel.
 // --------------------------------------------------------------------------
+//    Shared-prefix mode (plen != nullptr, *plen = P > 0): every row's first P
+//    keys are a prefix shared by all rows and are attended by
+//    prefix_attn_kernel; this kernel covers keys [P, L) only and always
+//    writes partials, at split index ps_max + split.
 template <int D, int G>
 __global__ __launch_bounds__(kBlock) void decode_attn_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache,
     const int32_t* __restrict__ slot, const int32_t* __restrict__ seq_len, uint16_t* __restrict__ out,
     float* __restrict__ part_o, float* __restrict__ part_ml, int B, int Hkv,
-    int max_seq, int chunk, int splits, float scale_log2, int num_slots) {
+    int max_seq, int chunk, int splits, float scale_log2, int num_slots, const int32_t* __restrict__ plen,
+    int ps_max) {
     constexpr int LPK = D / 8;
     constexpr int KPW = kWave / LPK;
     constexpr int NW = kBlock / kWave;
     constexpr int NK = G >= 6 ? 2 : 4;  // keys per lane per iteration (VGPR budget at G >= 6)
     const int Hq = Hkv * G;
+    const int P = plen ? max(0, *plen) : 0;
+    const int splits_total = ps_max + splits;
     // Persistent grid over split-major work items (split, row, kv head).  A
     // grid of splits*Hkv*B blocks where most splits are empty (short rows)
     // spent ~100 us launching waves that exit at once (profiles/decode_*);
@@ -219,15 +226,17 @@ __global__ __launch_bounds__(kBlock) void decode_attn_kernel(
     const int b = rem / Hkv, kh = rem - b * Hkv;
     const int s = slot[b];
     const int L = (s >= 0 && s < num_slots) ? min(seq_len[b], max_seq) : 0;  // never read a bad slot
-    // splits that own keys; the others are skipped (no partials)
-    const int nact = min(splits, (L + chunk - 1) / chunk);
+    // splits that own keys past the shared prefix; the others are skipped
+    const int Ls = L - P;
+    const int nact = Ls > 0 ? min(splits, (Ls + chunk - 1) / chunk) : 0;
     if (L <= 0) {  // padding row / bad slot: defined output, nothing read
         if (split == 0)
             for (int o = threadIdx.x; o < G * D; o += kBlock) out[((size_t)b * Hq + kh * G) * D + o] = 0;
         continue;
     }
     if (split >= nact) continue;
-    const int start = split * chunk;
+    const bool direct = P == 0 && nact == 1;  // the whole context in this block: no merge
+    const int start = P + split * chunk;
     const int end = min(L, start + chunk);
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = threadIdx.x / kWave;
@@ -357,10 +366,10 @@ __global__ __launch_bounds__(kBlock) void decode_attn_kernel(
             at += sm_acc[w][g][d] * c;
         }
         const int qh = kh * G + g;
-        if (nact == 1) {
+        if (direct) {
             out[((size_t)b * Hq + qh) * D + d] = f2bf(lt > 0.f ? at / lt : 0.f);
         } else {
-            const size_t pi = ((size_t)b * Hq + qh) * splits + split;
+            const size_t pi = ((size_t)b * Hq + qh) * splits_total + ps_max + split;
             part_o[pi * D + d] = at;
             if (d == 0) {
                 part_ml[pi * 2] = mx;
@@ -382,25 +391,176 @@ __global__ __launch_bounds__(kBlock) void decode_attn_combine_kernel(const float
                                                                     const int32_t* __restrict__ seq_len,
                                                                     uint16_t* __restrict__ out, int Hkv, int G,
                                                                     int D, int max_seq, int chunk, int splits,
-                                                                    int num_slots) {
+                                                                    int num_slots, const int32_t* __restrict__ plen,
+                                                                    int ps_max, int pchunk) {
     const int kh = blockIdx.x, b = blockIdx.y;
     const int s = slot[b];
     const int L = (s >= 0 && s < num_slots) ? min(seq_len[b], max_seq) : 0;
-    const int nact = min(splits, (L + chunk - 1) / chunk);
-    if (nact <= 1) return;
+    if (L <= 0) return;  // padding row: zeroed by the main kernel
+    const int P = plen ? max(0, *plen) : 0;
+    const int Ls = L - P;
+    const int nact = Ls > 0 ? min(splits, (Ls + chunk - 1) / chunk) : 0;
+    const int npre = P > 0 ? min(ps_max, (P + pchunk - 1) / pchunk) : 0;  // prefix partials
+    if (npre == 0 && nact <= 1) return;  // written directly by the main kernel
     const int Hq = Hkv * G;
+    const int splits_total = ps_max + splits;
     for (int o = threadIdx.x; o < G * D; o += kBlock) {
         const int g = o / D, d = o - g * D;
-        const size_t base = ((size_t)b * Hq + kh * G + g) * splits;
+        const size_t base = ((size_t)b * Hq + kh * G + g) * splits_total;
         float mx = -1e30f;
-        for (int sp = 0; sp < nact; ++sp) mx = fmaxf(mx, part_ml[(base + sp) * 2]);
+        for (int sp = 0; sp < npre; ++sp) mx = fmaxf(mx, part_ml[(base + sp) * 2]);
+        for (int sp = 0; sp < nact; ++sp) mx = fmaxf(mx, part_ml[(base + ps_max + sp) * 2]);
         float lt = 0.f, at = 0.f;
-        for (int sp = 0; sp < nact; ++sp) {
+        for (int sp = 0; sp < npre; ++sp) {
+            const float c = exp2f(part_ml[(base + sp) * 2] - mx);
+            lt += part_ml[(base + sp) * 2 + 1] * c;
+            at += part_o[(base + sp) * D + d] * c;
+        }
+        for (int sp = ps_max; sp < ps_max + nact; ++sp) {
             const float c = exp2f(part_ml[(base + sp) * 2] - mx);
             lt += part_ml[(base + sp) * 2 + 1] * c;
             at += part_o[(base + sp) * D + d] * c;
         }
         out[((size_t)b * Hq + kh * G + g) * D + d] = f2bf(lt > 0.f ? at / lt : 0.f);
+    }
+}
+
+// --------------------------------------------------------------------------
+// 3b. shared-prefix attention (cascade decoding), MFMA.
+//    Every row of a decode step shares its first P keys (the enrichment
+//    prompt's instructions + README, identical for all classes of a project).
+//    The per-row kernel above would stream those P keys once PER ROW; here
+//    the queries of all rows that map to one kv head are batched into the
+//    N dimension of two MFMA products per 32-key tile, so each prefix key is
+//    read once per 32 queries:
+//        S^T[key, query] = K[key, :] . Q^T[:, query]     (32x32x16 bf16, D/16 steps)
+//        O^T[d, query]  += V^T[d, key] . P^T[key, query]  (32x32x16 bf16, 2 steps)
+//    S^T comes out with the query on the lane and the 32 keys in registers,
+//    so the online softmax is in-register plus one cross-half shuffle, the
+//    running max/sum stay per lane, and P^T feeds the second MFMA as its B
+//    operand with no LDS round trip (accumulator-as-operand idiom, guide
+//    section "Fragment layout"; the permuted k order is matched by the V^T
+//    fragment).  V is read from a transposed copy of the prefix (vt [Hkv, D,
+//    ldv], built once per prefix) so each A fragment is two 8-byte loads.
+//    Work item = (prefix split of pchunk keys, kv head, 32-query tile), one
+//    per wave, persistent grid; output = fp32 partials (log2-domain max, sum)
+//    at split index [0, ps_max), merged by decode_attn_combine_kernel.
+// --------------------------------------------------------------------------
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ bf16x8_t as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8_t, v); }
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void prefix_attn_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ pk, const uint16_t* __restrict__ vt,
+    const int32_t* __restrict__ plen, float* __restrict__ part_o, float* __restrict__ part_ml, int B, int Hkv, int G,
+    int ldk, int ldv, int pchunk, int ps_max, int splits_total, float scale_log2) {
+    constexpr int KS = D / 16;  // k-steps of the QK product
+    constexpr int DT = D / 32;  // 32-row d tiles of the PV product
+    const int P = min(*plen, ldv);
+    if (P <= 0) return;
+    const int Hq = Hkv * G;
+    const int nq = B * G;
+    const int qtiles = (nq + 31) / 32;
+    const int npre = min(ps_max, (P + pchunk - 1) / pchunk);
+    const int total = npre * Hkv * qtiles;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    const int r = lane & 31, h = lane >> 5;
+    const int wpb = kBlock / kWave;
+    for (int item = blockIdx.x * wpb + wave; item < total; item += gridDim.x * wpb) {
+        const int sp = item / (Hkv * qtiles);
+        const int rem = item - sp * (Hkv * qtiles);
+        const int kh = rem / qtiles;
+        const int qt = rem - kh * qtiles;
+        const int qi = qt * 32 + r;  // this lane's query (the MFMA column)
+        const bool qok = qi < nq;
+        const int b = qok ? qi / G : 0, g = qok ? qi - (qi / G) * G : 0;
+        const uint16_t* qp = q + ((size_t)b * Hq + (size_t)kh * G + g) * D + 8 * h;
+        bf16x8_t qf[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+            qf[ks] = as_bf16x8(qok ? *reinterpret_cast<const uint4*>(qp + ks * 16) : make_uint4(0, 0, 0, 0));
+        float m = -1e30f, l = 0.f;  // m is kept equal across the two lane halves; l is per half
+        f32x16_t o[DT];
+#pragma unroll
+        for (int t = 0; t < DT; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[t][i] = 0.f;
+        const int kbeg = sp * pchunk, kend = min(P, kbeg + pchunk);
+        const uint16_t* kb = pk + (size_t)kh * ldk * D + 8 * h;
+        const uint16_t* vb = vt + (size_t)kh * D * ldv + 4 * h;
+        for (int k0 = kbeg; k0 < kend; k0 += 32) {
+            const int kr = min(k0 + r, kend - 1);  // rows past the range are loaded but masked
+            const uint16_t* kp = kb + (size_t)kr * D;
+            uint4 kf[KS];
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) kf[ks] = *reinterpret_cast<const uint4*>(kp + ks * 16);
+            // V^T fragments of both k-steps for every d tile, issued before the
+            // QK MFMAs so the loads overlap them
+            uint2 vf[DT][2][2];
+#pragma unroll
+            for (int t = 0; t < DT; ++t) {
+                const uint16_t* vp = vb + (size_t)(32 * t + r) * ldv + k0;
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    vf[t][s2][0] = *reinterpret_cast<const uint2*>(vp + 16 * s2);
+                    vf[t][s2][1] = *reinterpret_cast<const uint2*>(vp + 16 * s2 + 8);
+                }
+            }
+            f32x16_t s;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) s[i] = 0.f;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+                s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf[ks]), qf[ks], s, 0, 0, 0);
+            // register i holds key k0 + (i&3) + 8*(i>>2) + 4*h of query r
+            float mt = -1e30f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int key = k0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                s[i] = key < kend ? s[i] * scale_log2 : -1e30f;
+                mt = fmaxf(mt, s[i]);
+            }
+            mt = fmaxf(mt, __shfl_xor(mt, 32, kWave));
+            const float mn = fmaxf(m, mt);
+            const float corr = exp2f(m - mn);
+            m = mn;
+            l *= corr;
+#pragma unroll
+            for (int t = 0; t < DT; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) o[t][i] *= corr;
+            float p[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                p[i] = exp2f(s[i] - mn);
+                l += p[i];
+            }
+            const bf16x8_t pb0 = as_bf16x8(pack8(p)), pb1 = as_bf16x8(pack8(p + 8));
+#pragma unroll
+            for (int t = 0; t < DT; ++t) {
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                    as_bf16x8(make_uint4(vf[t][0][0].x, vf[t][0][0].y, vf[t][0][1].x, vf[t][0][1].y)), pb0, o[t], 0,
+                    0, 0);
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                    as_bf16x8(make_uint4(vf[t][1][0].x, vf[t][1][0].y, vf[t][1][1].x, vf[t][1][1].y)), pb1, o[t], 0,
+                    0, 0);
+            }
+        }
+        const float lt = l + __shfl_xor(l, 32, kWave);
+        if (!qok) continue;
+        const size_t pi = ((size_t)b * Hq + (size_t)kh * G + g) * splits_total + sp;
+        // O^T register i of d tile t: d = 32t + (i&3) + 8*(i>>2) + 4*h
+#pragma unroll
+        for (int t = 0; t < DT; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) part_o[pi * D + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h] = o[t][i];
+        if (h == 0) {
+            part_ml[pi * 2] = m;
+            part_ml[pi * 2 + 1] = lt;
+        }
     }
 }
 
@@ -510,10 +670,10 @@ template <int D>
 hipError_t launch_decode_d(int G, dim3 grid, const uint16_t* q, const uint16_t* k, const uint16_t* v,
                            const int32_t* slot, const int32_t* len, uint16_t* out, float* po, float* pml,
                            int B, int Hkv, int max_seq, int chunk, int splits, float sl2, int ns,
-                           hipStream_t st) {
+                           const int32_t* plen, int ps_max, hipStream_t st) {
 #define DMCP_DECODE(GG)                                                                                     \
     decode_attn_kernel<D, GG><<<grid, kBlock, 0, st>>>(q, k, v, slot, len, out, po, pml, B, Hkv, max_seq, \
-                                                       chunk, splits, sl2, ns)
+                                                       chunk, splits, sl2, ns, plen, ps_max)
     switch (G) {
         case 1: DMCP_DECODE(1); break;
         case 2: DMCP_DECODE(2); break;
@@ -531,7 +691,7 @@ hipError_t launch_decode_d(int G, dim3 grid, const uint16_t* q, const uint16_t* 
 
 extern "C" {
 
-int dmcp_abi_version() { return 4; }
+int dmcp_abi_version() { return 5; }
 
 int dmcp_add_rmsnorm(const void* x, void* residual, const void* w, void* out, int rows, int H, float eps,
                      void* stream) {
@@ -562,36 +722,61 @@ int dmcp_rope_kv(const void* qkv, const void* pos, const void* slot, const void*
 
 int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cache, const void* slot,
                           const void* seq_len, void* out, void* part_o, void* part_ml, int B, int Hq, int Hkv, int D,
-                          int max_seq, int num_slots, int chunk, int splits, float scale, void* stream) {
+                          int max_seq, int num_slots, int chunk, int splits, float scale, const void* prefix_k,
+                          const void* prefix_vt, const void* plen, int ldv, int pchunk, int ps_max, void* stream) {
     if (B <= 0) return 0;
     if (Hkv <= 0 || Hq % Hkv != 0 || splits <= 0 || chunk <= 0) return hipErrorInvalidValue;
-    if (splits > 1 && (!part_o || !part_ml)) return hipErrorInvalidValue;
+    const bool prefix = plen != nullptr;
+    if (prefix && (!prefix_k || !prefix_vt || ps_max <= 0 || pchunk <= 0 || pchunk % 32 || ldv % 32 || ldv > max_seq))
+        return hipErrorInvalidValue;
+    if (!prefix) ps_max = 0;
+    if ((splits > 1 || prefix) && (!part_o || !part_ml)) return hipErrorInvalidValue;
     const int G = Hq / Hkv;
     const float sl2 = scale * 1.4426950408889634f;
+    auto st = (hipStream_t)stream;
+    auto qq = (const uint16_t*)q;
+    auto sl = (const int32_t*)slot;
+    auto ln = (const int32_t*)seq_len;
+    auto pl = (const int32_t*)plen;
+    const long cap = 4L * device_cu_count();
+    if (prefix) {
+        // one wave per (prefix split, kv head, 32-query tile); exits at once when *plen == 0
+        const long waves = (long)ps_max * Hkv * ((B * G + 31) / 32);
+        const long blocks = (waves + kBlock / kWave - 1) / (kBlock / kWave);
+        dim3 pgrid((unsigned)(blocks < cap ? blocks : cap));
+        if (D == 64)
+            prefix_attn_kernel<64><<<pgrid, kBlock, 0, st>>>(qq, (const uint16_t*)prefix_k, (const uint16_t*)prefix_vt,
+                                                           pl, (float*)part_o, (float*)part_ml, B, Hkv, G, max_seq,
+                                                           ldv, pchunk, ps_max, ps_max + splits, sl2);
+        else if (D == 128)
+            prefix_attn_kernel<128><<<pgrid, kBlock, 0, st>>>(qq, (const uint16_t*)prefix_k,
+                                                            (const uint16_t*)prefix_vt, pl, (float*)part_o,
+                                                            (float*)part_ml, B, Hkv, G, max_seq, ldv, pchunk, ps_max,
+                                                            ps_max + splits, sl2);
+        else
+            return hipErrorInvalidValue;
+        hipError_t pe = hipGetLastError();
+        if (pe != hipSuccess) return pe;
+    }
     // persistent grid: enough blocks to fill every CU a few times over, never
     // more than there are work items
     const long items = (long)splits * Hkv * B;
-    const long cap = 4L * device_cu_count();
     dim3 grid((unsigned)(items < cap ? items : cap));
-    auto st = (hipStream_t)stream;
-    auto qq = (const uint16_t*)q;
     auto kk = (const uint16_t*)k_cache;
     auto vv = (const uint16_t*)v_cache;
-    auto sl = (const int32_t*)slot;
-    auto ln = (const int32_t*)seq_len;
     hipError_t e;
     if (D == 64)
         e = launch_decode_d<64>(G, grid, qq, kk, vv, sl, ln, (uint16_t*)out, (float*)part_o, (float*)part_ml, B,
-                                Hkv, max_seq, chunk, splits, sl2, num_slots, st);
+                                Hkv, max_seq, chunk, splits, sl2, num_slots, pl, ps_max, st);
     else if (D == 128)
         e = launch_decode_d<128>(G, grid, qq, kk, vv, sl, ln, (uint16_t*)out, (float*)part_o, (float*)part_ml, B,
-                                 Hkv, max_seq, chunk, splits, sl2, num_slots, st);
+                                 Hkv, max_seq, chunk, splits, sl2, num_slots, pl, ps_max, st);
     else
         return hipErrorInvalidValue;
-    if (e != hipSuccess || splits == 1) return e;
+    if (e != hipSuccess || (splits == 1 && !prefix)) return e;
     decode_attn_combine_kernel<<<dim3(Hkv, B), kBlock, 0, st>>>((const float*)part_o, (const float*)part_ml, sl, ln,
                                                                (uint16_t*)out, Hkv, G, D, max_seq, chunk, splits,
-                                                               num_slots);
+                                                               num_slots, pl, ps_max, prefix ? pchunk : 1);
     return hipGetLastError();
 }
 

@@ -26,7 +26,7 @@ _lock = threading.Lock()
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _f = ctypes.c_float
-ABI_VERSION = 4  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
+ABI_VERSION = 5  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
 
 
 class HipOpsError(RuntimeError):
@@ -50,7 +50,8 @@ def lib() -> ctypes.CDLL:
             "dmcp_abi_version": ([], _i),
             "dmcp_add_rmsnorm": ([_vp, _vp, _vp, _vp, _i, _i, _f, _vp], _i),
             "dmcp_rope_kv": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp], _i),
-            "dmcp_decode_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _f, _vp],
+            "dmcp_decode_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _f,
+                                       _vp, _vp, _vp, _i, _i, _i, _vp],
                                       _i),
             "dmcp_silu_mul": ([_vp, _vp, _i, _i, _vp], _i),
             "dmcp_masked_argmax": ([_vp, _vp, _vp, _i, _vp, _i, _i, _i, _vp], _i),
@@ -160,8 +161,15 @@ def decode_chunk(rows: int, n_kv_heads: int, max_seq: int, target_items: int = 2
 
 def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: torch.Tensor,
                      seq_len: torch.Tensor, scale: float, workspace: Optional[tuple] = None,
-                     chunk: int = 256, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """q [B, Hq, D]; caches [S, Hkv, MAXS, D]; slot/seq_len int32 [B]."""
+                     chunk: int = 256, out: Optional[torch.Tensor] = None,
+                     prefix: Optional["SharedPrefix"] = None) -> torch.Tensor:
+    """q [B, Hq, D]; caches [S, Hkv, MAXS, D]; slot/seq_len int32 [B].
+
+    ``prefix``: the first ``*prefix.length`` keys of every row are the shared
+    prefix (``prefix.k`` [Hkv, MAXS, D], ``prefix.vt`` [Hkv, D, ldv]), read
+    once per 32 queries by the MFMA prefix kernel; the per-row kernel covers
+    the keys after it.  The length lives in device memory, so a captured
+    graph follows prefix changes (0 = no prefix)."""
     B, Hq, D = q.shape
     S, Hkv, MAXS, Dk = k_cache.shape
     for t, n in ((q, "q"), (k_cache, "k_cache"), (v_cache, "v_cache")):
@@ -173,26 +181,47 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     if slot.numel() != B or seq_len.numel() != B:
         raise HipOpsError("decode_attention: slot/seq_len must have B entries")
     splits = decode_splits(MAXS, chunk)
+    ps_max = 0
+    pk = pvt = plen = None
+    ldv = pchunk = 0
+    if prefix is not None:
+        pk, pvt, plen, pchunk = prefix.k, prefix.vt, prefix.length, prefix.chunk
+        _req(pk, torch.bfloat16, "decode_attention.prefix.k")
+        _req(pvt, torch.bfloat16, "decode_attention.prefix.vt")
+        _req(plen, torch.int32, "decode_attention.prefix.length")
+        ldv = pvt.shape[-1]
+        if (tuple(pk.shape) != (Hkv, MAXS, D) or tuple(pvt.shape) != (Hkv, D, ldv) or ldv % 32 or ldv > MAXS
+                or pchunk % 32 or pchunk <= 0 or plen.numel() != 1):
+            raise HipOpsError(f"decode_attention: prefix k {tuple(pk.shape)} / vt {tuple(pvt.shape)} / chunk "
+                              f"{pchunk} do not match kv {tuple(k_cache.shape)}")
+        ps_max = prefix_splits(ldv, pchunk)
     out = torch.empty_like(q) if out is None else out
     _req(out, torch.bfloat16, "decode_attention.out")
-    if splits > 1:
+    if splits > 1 or ps_max:
         if workspace is None:
-            workspace = decode_workspace(B, Hq, Hkv, D, MAXS, q.device, chunk)
+            workspace = decode_workspace(B, Hq, Hkv, D, MAXS, q.device, chunk, ps_max)
         part_o, part_ml = workspace
-        if part_o.numel() < B * Hq * splits * D or part_ml.numel() < B * Hq * splits * 2:
+        n = B * Hq * (splits + ps_max)
+        if part_o.numel() < n * D or part_ml.numel() < n * 2:
             raise HipOpsError("decode_attention: workspace too small")
     else:
         part_o = part_ml = None
     _check(lib().dmcp_decode_attention(_ptr(q), _ptr(k_cache), _ptr(v_cache), _ptr(slot), _ptr(seq_len), _ptr(out),
                                        _ptr(part_o), _ptr(part_ml), B, Hq, Hkv, D, MAXS, S, chunk, splits,
-                                       float(scale), _stream()), "dmcp_decode_attention")
+                                       float(scale), _ptr(pk), _ptr(pvt), _ptr(plen), ldv, pchunk, ps_max,
+                                       _stream()), "dmcp_decode_attention")
     return out
 
 
-def decode_workspace(rows: int, Hq: int, Hkv: int, D: int, max_seq: int, device, chunk: int = 256) -> tuple:
+def prefix_splits(ldv: int, pchunk: int) -> int:
+    return max(1, math.ceil(ldv / pchunk))
+
+
+def decode_workspace(rows: int, Hq: int, Hkv: int, D: int, max_seq: int, device, chunk: int = 256,
+                     prefix_slots: int = 0) -> tuple:
     """Split-K scratch (fp32 partial outputs + running max/sum) for up to
-    ``rows`` query rows."""
-    splits = decode_splits(max_seq, chunk)
+    ``rows`` query rows, plus ``prefix_slots`` shared-prefix partials per row."""
+    splits = decode_splits(max_seq, chunk) + prefix_slots
     n = rows * Hq * splits
     return (torch.empty(n * D, dtype=torch.float32, device=device),
             torch.empty(n * 2, dtype=torch.float32, device=device))

@@ -6,7 +6,7 @@ Signatures mirror :mod:`dmcp.ops.hip`.
 """
 from __future__ import annotations
 
-from typing import Optional
+from typing import NamedTuple, Optional
 
 import torch
 
@@ -66,12 +66,25 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos_sin: t
     return q
 
 
+class SharedPrefix(NamedTuple):
+    """Keys/values shared by every row of a decode step (cascade decoding).
+
+    ``k`` [Hkv, MAXS, D] (row-major, as in the cache), ``vt`` [Hkv, D, ldv]
+    (values transposed), ``length`` int32 [1] on the device (0 = no prefix),
+    ``chunk`` keys per prefix work item of the MFMA kernel."""
+    k: torch.Tensor
+    vt: torch.Tensor
+    length: torch.Tensor
+    chunk: int = 256
+
+
 def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: torch.Tensor,
                      seq_len: torch.Tensor, scale: float, workspace=None, chunk: int = 256,
-                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     out: Optional[torch.Tensor] = None, prefix: Optional[SharedPrefix] = None) -> torch.Tensor:
     B, Hq, D = q.shape
     S, Hkv, MAXS, _ = k_cache.shape
     G = Hq // Hkv
+    P = int(prefix.length.reshape(-1)[0]) if prefix is not None else 0
     res = torch.zeros((B, Hq, D), dtype=torch.float32, device=q.device)
     for b in range(B):
         s, L = int(slot[b]), min(int(seq_len[b]), MAXS)
@@ -79,6 +92,9 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
             continue
         k = k_cache[s, :, :L].float()  # [Hkv, L, D]
         v = v_cache[s, :, :L].float()
+        if P > 0:  # the first P keys come from the shared prefix
+            k = torch.cat([prefix.k[:, :P].float(), k[:, P:]], dim=1)
+            v = torch.cat([prefix.vt[:, :, :P].float().transpose(1, 2), v[:, P:]], dim=1)
         qb = q[b].float().view(Hkv, G, D)
         att = torch.einsum("hgd,hld->hgl", qb, k) * scale
         p = torch.softmax(att, dim=-1)

@@ -30,6 +30,7 @@ for s in $STEPS; do
         bench) run bench 600 python bench.py --steps 5 --warmup 2 ;;
         enrich) run bench_enrich 900 python bench_enrich.py --classes 256 --batch 64 ;;
         enrich_nojump) run bench_enrich_nojump 900 python bench_enrich.py --classes 256 --batch 64 --no-jump ;;
+        enrich_noprefix) run bench_enrich_noprefix 900 python bench_enrich.py --classes 256 --batch 64 --no-shared-prefix ;;
         kernels) run kernels 600 python scripts/bench_kernels.py ;;
         prof)
             ROOT=$(pwd)

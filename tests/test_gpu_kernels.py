@@ -82,6 +82,39 @@ def test_decode_attention(hip, D, Hq, Hkv, MAXS):
     torch.testing.assert_close(got.float(), exp.float(), atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("D,Hq,Hkv", [(64, 32, 8), (64, 8, 4), (128, 24, 8), (64, 16, 2)])
+@pytest.mark.parametrize("P", [1, 45, 256, 700])
+@pytest.mark.parametrize("B", [1, 9, 70])
+def test_decode_attention_shared_prefix(hip, D, Hq, Hkv, P, B):
+    """MFMA shared-prefix kernel + per-row suffix + merge == fp32 attention
+    over [prefix ++ own keys]; odd P / B exercise partial key and query tiles."""
+    from dmcp.ops import reference
+    from dmcp.ops.reference import SharedPrefix
+    MAXS, S = 1024, 6
+    q = _bf(B, Hq, D, seed=11)
+    kc = _bf(S + 1, Hkv, MAXS, D, seed=12)
+    vc = _bf(S + 1, Hkv, MAXS, D, seed=13)
+    pslot = S  # the prefix lives in the last slot
+    vt = torch.zeros((Hkv, D, MAXS), dtype=torch.bfloat16, device="cuda")
+    vt[:, :, :P] = vc[pslot, :, :P].transpose(-1, -2)
+    plen = torch.tensor([P], dtype=torch.int32, device="cuda")
+    pre = SharedPrefix(kc[pslot], vt, plen, 256)
+    slot = torch.tensor([(b * 5) % S for b in range(B)], dtype=torch.int32, device="cuda")
+    slot[B // 2] = -1  # a padding row
+    lens = torch.tensor([min(MAXS, P + 1 + (b * 37) % 300) for b in range(B)], dtype=torch.int32, device="cuda")
+    scale = 1 / math.sqrt(D)
+    for chunk in (256, 1024):
+        got = hip.decode_attention(q, kc, vc, slot, lens, scale, chunk=chunk, prefix=pre)
+        exp = reference.decode_attention(q, kc, vc, slot, lens, scale, prefix=pre)
+        torch.testing.assert_close(got.float(), exp.float(), atol=2e-2, rtol=2e-2)
+        assert got[B // 2].abs().sum().item() == 0
+    # length 0 in device memory: the prefix kernel is a no-op, rows read their own keys
+    plen.zero_()
+    got = hip.decode_attention(q, kc, vc, slot, lens, scale, prefix=pre)
+    exp = reference.decode_attention(q, kc, vc, slot, lens, scale)
+    torch.testing.assert_close(got.float(), exp.float(), atol=2e-2, rtol=2e-2)
+
+
 def test_decode_attention_bad_slot_is_zero(hip):
     D, Hq, Hkv, MAXS = 64, 8, 2, 128
     q = _bf(2, Hq, D)

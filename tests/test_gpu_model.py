@@ -124,3 +124,48 @@ def test_jump_forward_same_output_fewer_steps(model):
     assert b.stats["decode_steps"] < a.stats["decode_steps"]
     assert b.stats["generated_tokens"] == sum(len(x.encode()) for x in rb) - sum(
         len(b'{"description": "') for _ in rb)
+
+
+def test_shared_prefix_decode_matches_reference(model):
+    """set_prefix + fork_prefix + suffix prefill + decode through the MFMA
+    shared-prefix kernel == fp32 reference over the whole token sequence."""
+    prefix = [256] + list(b"You are adding business context. README: a shop for widgets and gadgets. " * 2)
+    tails = [list(b"class A { void a() {} }"), list(b"class Bee { int b; }"), list(b"x")]
+    P = model.set_prefix(prefix)
+    try:
+        assert P == len(prefix) and int(model.prefix_dev.item()) == P
+        last = []
+        for s, t in enumerate(tails):
+            assert model.fork_prefix(s) == P
+            lg = model.forward_tokens(torch.tensor(t, dtype=torch.int32), s, P)
+            assert _rel_err(lg, model.reference_logits(prefix + t)[-1]) < 0.03
+            last.append(len(prefix) + len(t))
+        nxt = [ord("k"), ord("m"), ord("z")]
+        d = model.decode(torch.tensor(nxt, dtype=torch.int32, device="cuda"),
+                         torch.tensor([0, 1, 2], dtype=torch.int32, device="cuda"),
+                         torch.tensor(last, dtype=torch.int32, device="cuda"))
+        for i, t in enumerate(tails):
+            assert _rel_err(d[i], model.reference_logits(prefix + t + [nxt[i]])[-1]) < 0.03
+    finally:
+        model.clear_prefix()
+    assert int(model.prefix_dev.item()) == 0
+
+
+def test_engine_shared_prefix_same_output(model):
+    """The engine with a shared README prefix prefills less and still returns
+    schema-valid replies.  (Step-level numerics are pinned by
+    test_shared_prefix_decode_matches_reference; whole greedy generations of
+    a random-weight model are too tie-prone to compare exactly.)"""
+    from dmcp.enrich.local import LocalEngine
+    from dmcp.enrich.types import EnrichmentInput
+    readme = "Acme commerce platform: orders, payments, shipping and customer accounts. " * 4
+    inputs = [EnrichmentInput("class P%d { void pay() {} }" % i, f"co.acme.P{i}", "java", "SERVICE",
+                              ["pay", "refund"][: 1 + i % 2]) for i in range(12)]
+    a = LocalEngine(model, shared_prefix=False)
+    b = LocalEngine(model, shared_prefix=True)
+    ra, rb = a.generate(inputs, readme), b.generate(inputs, readme)
+    assert b.stats["prefix_tokens"] > 200 and a.stats["prefix_tokens"] == 0
+    assert b.stats["prompt_tokens"] < a.stats["prompt_tokens"]
+    for r, inp in zip(rb, inputs):
+        assert [m["methodName"] for m in json.loads(r)["methods"]] == inp.method_names
+    assert len(ra) == len(rb) == len(inputs)

@@ -81,3 +81,39 @@ def test_prompt_too_long_is_truncated_not_failed(tiny):
     long_src = "class L { " + "int x; " * 2000 + "}"
     out = eng.generate([EnrichmentInput(long_src, "co.x.L", "java", "OTHER", ["x"])], None)
     assert json.loads(out[0])["methods"][0]["methodName"] == "x"
+
+
+def test_shared_prefix_cpu_matches_full_prompt(tiny):
+    """CPU reference path of the shared prefix: prefix prefill once + suffix
+    prefill + decode == full-prompt prefill + decode."""
+    prefix = [256] + list(b"Shared instructions and README text for every class of the project. " * 2)
+    tails = [list(b"class A {}"), list(b"class Bb { int x; }")]
+    full = []
+    for s, t in enumerate(tails):
+        full.append(tiny.forward_tokens(torch.tensor(prefix + t, dtype=torch.int32), s, 0))
+    d_full = tiny.decode(torch.tensor([65, 66], dtype=torch.int32), torch.tensor([0, 1], dtype=torch.int32),
+                         torch.tensor([len(prefix) + len(t) for t in tails], dtype=torch.int32))
+    P = tiny.set_prefix(prefix)
+    try:
+        for s, t in enumerate(tails):
+            tiny.fork_prefix(s + 2)
+            lg = tiny.forward_tokens(torch.tensor(t, dtype=torch.int32), s + 2, P)
+            torch.testing.assert_close(lg.float(), full[s].float(), atol=3e-2, rtol=3e-2)
+        d = tiny.decode(torch.tensor([65, 66], dtype=torch.int32), torch.tensor([2, 3], dtype=torch.int32),
+                        torch.tensor([len(prefix) + len(t) for t in tails], dtype=torch.int32))
+        torch.testing.assert_close(d.float(), d_full.float(), atol=3e-2, rtol=3e-2)
+    finally:
+        tiny.clear_prefix()
+
+
+def test_engine_common_prefix_detection(tiny):
+    eng = LocalEngine(tiny, use_graphs=False)
+    a = [256] + [1] * 100 + [2, 3]
+    b = [256] + [1] * 100 + [4]
+    assert eng._common_prefix([a, b]) == 101
+    assert eng._common_prefix([a]) == 0  # one prompt: nothing to share
+    assert eng._common_prefix([a, [256, 9] + [1] * 100]) == 0  # below the minimum
+    assert eng._common_prefix([a, a]) == len(a) - 1  # every prompt keeps >= 1 own token
+    out = eng.generate(_inputs(5), "A README shared by every prompt of the batch. " * 3)
+    assert eng.stats["prefix_tokens"] > 0 and all(json.loads(o) for o in out)
+    assert tiny.prefix_len == 0  # cleared after the batch

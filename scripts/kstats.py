@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 kernel_stats.csv by op category (per decode step).
+
+    python scripts/kstats.py gpurun_out/prof_prefix/enrich_kernel_stats.csv [decode_attn_calls_per_step]
+"""
+import collections
+import csv
+import sys
+
+CATS = [("gemm", "Cijk"), ("attn_suffix", "decode_attn_kernel"), ("attn_prefix", "prefix_attn"),
+        ("attn_combine", "combine"), ("prefill_attn", "attn_fwd"), ("rmsnorm", "rmsnorm"), ("silu", "silu"),
+        ("rope", "rope"), ("embedding", "embedding"), ("argmax", "argmax")]
+
+
+def main() -> int:
+    rows = list(csv.DictReader(open(sys.argv[1])))
+    layers = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+    cat = collections.Counter()
+    steps = 0
+    for r in rows:
+        name, t = r["Name"], int(r["TotalDurationNs"])
+        if "decode_attn_kernel" in name:
+            steps = int(r["Calls"]) // layers
+        for c, key in CATS:
+            if key in name:
+                cat[c] += t
+                break
+        else:
+            cat["other"] += t
+    total = sum(cat.values())
+    print(f"total {total / 1e6:.1f} ms over {steps} decode steps")
+    for k, v in cat.most_common():
+        print(f"  {k:14s} {v / 1e6:9.1f} ms  {100 * v / total:5.1f}%  per-step {v / 1e3 / max(1, steps):8.1f} us")
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,11 +1,12 @@
 #!/usr/bin/env bash
-# rocprofv3 kernel stats of bench_enrich.py: shared-prefix on and off.
-# Keeps only the *_stats.csv summaries under gpurun_out/prof_<tag>/.
+# rocprofv3 kernel stats of bench_enrich.py (shared prefix on, and off with
+# TAGS="prefix noprefix").  Keeps only the *_stats.csv summaries under
+# gpurun_out/prof_<tag>/.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 export TMPDIR=/tmp
-for tag in prefix noprefix; do
+for tag in ${TAGS:-prefix}; do
     extra=""
     [ "$tag" = noprefix ] && extra="--no-shared-prefix"
     ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \

@@ -18,7 +18,10 @@ TARGET = os.path.join(HERE, "_hipops.so")
 STAMP = TARGET + ".stamp"
 ARCH = os.environ.get("DMCP_HIP_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-Wall",
-         "-Wno-unused-function", "-munsafe-fp-atomics"]
+         "-Wno-unused-function", "-munsafe-fp-atomics",
+         # MFMA accumulators in VGPRs: the prefix-attention softmax works on the
+         # score tile in place (AGPR form cost ~90 v_accvgpr moves per 32-key tile)
+         "-mllvm", "-amdgpu-mfma-vgpr-form=1"]
 
 
 def hipcc() -> str:

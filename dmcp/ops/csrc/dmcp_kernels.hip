@@ -404,23 +404,24 @@ __global__ __launch_bounds__(kBlock) void decode_attn_combine_kernel(const float
     if (npre == 0 && nact <= 1) return;  // written directly by the main kernel
     const int Hq = Hkv * G;
     const int splits_total = ps_max + splits;
+    // one pass of online merges (loads of different splits are independent,
+    // so the unrolled loop keeps several in flight)
     for (int o = threadIdx.x; o < G * D; o += kBlock) {
         const int g = o / D, d = o - g * D;
         const size_t base = ((size_t)b * Hq + kh * G + g) * splits_total;
-        float mx = -1e30f;
-        for (int sp = 0; sp < npre; ++sp) mx = fmaxf(mx, part_ml[(base + sp) * 2]);
-        for (int sp = 0; sp < nact; ++sp) mx = fmaxf(mx, part_ml[(base + ps_max + sp) * 2]);
-        float lt = 0.f, at = 0.f;
-        for (int sp = 0; sp < npre; ++sp) {
-            const float c = exp2f(part_ml[(base + sp) * 2] - mx);
-            lt += part_ml[(base + sp) * 2 + 1] * c;
-            at += part_o[(base + sp) * D + d] * c;
-        }
-        for (int sp = ps_max; sp < ps_max + nact; ++sp) {
-            const float c = exp2f(part_ml[(base + sp) * 2] - mx);
-            lt += part_ml[(base + sp) * 2 + 1] * c;
-            at += part_o[(base + sp) * D + d] * c;
-        }
+        float m = -1e30f, lt = 0.f, at = 0.f;
+        auto merge = [&](size_t idx) {
+            const float ms = part_ml[idx * 2], ls = part_ml[idx * 2 + 1], os = part_o[idx * D + d];
+            const float mn = fmaxf(m, ms);
+            const float ca = exp2f(m - mn), cb = exp2f(ms - mn);
+            lt = lt * ca + ls * cb;
+            at = at * ca + os * cb;
+            m = mn;
+        };
+#pragma unroll 4
+        for (int sp = 0; sp < npre; ++sp) merge(base + sp);
+#pragma unroll 4
+        for (int sp = 0; sp < nact; ++sp) merge(base + ps_max + sp);
         out[((size_t)b * Hq + kh * G + g) * D + d] = f2bf(lt > 0.f ? at / lt : 0.f);
     }
 }
@@ -430,50 +431,112 @@ __global__ __launch_bounds__(kBlock) void decode_attn_combine_kernel(const float
 //    Every row of a decode step shares its first P keys (the enrichment
 //    prompt's instructions + README, identical for all classes of a project).
 //    The per-row kernel above would stream those P keys once PER ROW; here
-//    the queries of all rows that map to one kv head are batched into the
-//    N dimension of two MFMA products per 32-key tile, so each prefix key is
-//    read once per 32 queries:
+//    the queries of all rows that map to one kv head are batched into the N
+//    dimension of two MFMA products per 32-key tile:
 //        S^T[key, query] = K[key, :] . Q^T[:, query]     (32x32x16 bf16, D/16 steps)
 //        O^T[d, query]  += V^T[d, key] . P^T[key, query]  (32x32x16 bf16, 2 steps)
 //    S^T comes out with the query on the lane and the 32 keys in registers,
 //    so the online softmax is in-register plus one cross-half shuffle, the
 //    running max/sum stay per lane, and P^T feeds the second MFMA as its B
-//    operand with no LDS round trip (accumulator-as-operand idiom, guide
-//    section "Fragment layout"; the permuted k order is matched by the V^T
-//    fragment).  V is read from a transposed copy of the prefix (vt [Hkv, D,
-//    ldv], built once per prefix) so each A fragment is two 8-byte loads.
-//    Work item = (prefix split of pchunk keys, kv head, 32-query tile), one
-//    per wave, persistent grid; output = fp32 partials (log2-domain max, sum)
-//    at split index [0, ps_max), merged by decode_attn_combine_kernel.
+//    operand with no data movement (accumulator-as-operand idiom, guide
+//    section "Fragment layout"; its permuted k order is matched by the V^T
+//    fragment).
+//    Work item = (kv head, PCH-key prefix split, group of 4 query tiles): the
+//    block stages the split's K rows and V^T columns in LDS once (padded
+//    rows: conflict-free fragment reads) and each of its 4 waves runs one
+//    32-query tile over them -- every prefix key leaves HBM/L2 once per 128
+//    queries.  V comes from a transposed copy of the prefix (vt [Hkv, D,
+//    ldv], built once per prefix) so the staging loads are 16-byte rows.
+//    Output: fp32 partials (log2-domain max, sum) at split index
+//    [0, ps_max), merged by decode_attn_combine_kernel.
 // --------------------------------------------------------------------------
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef float f32x8_t __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ bf16x8_t as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8_t, v); }
+
+constexpr int kPrefixChunk = 256;  // keys per prefix split (host passes the same)
 
 template <int D>
 __global__ __launch_bounds__(kBlock) void prefix_attn_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ pk, const uint16_t* __restrict__ vt,
     const int32_t* __restrict__ plen, float* __restrict__ part_o, float* __restrict__ part_ml, int B, int Hkv, int G,
-    int ldk, int ldv, int pchunk, int ps_max, int splits_total, float scale_log2) {
-    constexpr int KS = D / 16;  // k-steps of the QK product
-    constexpr int DT = D / 32;  // 32-row d tiles of the PV product
+    int ldk, int ldv, int ps_max, int splits_total, float scale_log2) {
+    constexpr int PCH = kPrefixChunk;
+    constexpr int KS = D / 16;       // k-steps of the QK product
+    constexpr int DT = D / 32;       // 32-row d tiles of the PV product
+    constexpr int KST = D + 8;       // padded LDS row strides (elements)
+    constexpr int VST = PCH + 8;
+    constexpr int NWAVE = kBlock / kWave;
+    __shared__ __attribute__((aligned(16))) uint16_t sK[PCH * KST];
+    __shared__ __attribute__((aligned(16))) uint16_t sV[D * VST];
     const int P = min(*plen, ldv);
     if (P <= 0) return;
     const int Hq = Hkv * G;
     const int nq = B * G;
     const int qtiles = (nq + 31) / 32;
-    const int npre = min(ps_max, (P + pchunk - 1) / pchunk);
-    const int total = npre * Hkv * qtiles;
+    const int qgroups = (qtiles + NWAVE - 1) / NWAVE;
+    const int npre = min(ps_max, (P + PCH - 1) / PCH);
+    const int total = Hkv * npre * qgroups;
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = threadIdx.x / kWave;
     const int r = lane & 31, h = lane >> 5;
-    const int wpb = kBlock / kWave;
-    for (int item = blockIdx.x * wpb + wave; item < total; item += gridDim.x * wpb) {
-        const int sp = item / (Hkv * qtiles);
-        const int rem = item - sp * (Hkv * qtiles);
-        const int kh = rem / qtiles;
-        const int qt = rem - kh * qtiles;
+    for (int item = blockIdx.x; item < total; item += gridDim.x) {
+        const int qg = item % qgroups;
+        const int rest = item / qgroups;
+        const int sp = rest % npre;
+        const int kh = rest / npre;
+        const int kbeg = sp * PCH, kend = min(P, kbeg + PCH);
+        __syncthreads();  // the previous item's readers are done with sK / sV
+        // stage K rows [kbeg, kbeg+PCH) and V^T columns of the split (zeros
+        // past kend): every thread issues all of its 16-byte loads before its
+        // first LDS store, so the block waits for one memory latency, not one
+        // per load
+        {
+            constexpr int KU = PCH * (D / 8) / kBlock;  // uint4 per thread, K
+            constexpr int VU = D * (PCH / 8) / kBlock;  // uint4 per thread, V^T
+            const uint16_t* kg = pk + ((size_t)kh * ldk + kbeg) * D;
+            const uint16_t* vg = vt + (size_t)kh * D * ldv + kbeg;
+            uint4 kx[KU], vx[VU];
+#pragma unroll
+            for (int i = 0; i < KU; ++i) {
+                const int u = threadIdx.x + i * kBlock;
+                const int row = u / (D / 8), c = u - row * (D / 8);
+                kx[i] = kbeg + row < kend ? *reinterpret_cast<const uint4*>(kg + (size_t)row * D + c * 8)
+                                          : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < VU; ++i) {
+                const int u = threadIdx.x + i * kBlock;
+                const int d = u / (PCH / 8), c = u - d * (PCH / 8);
+                vx[i] = kbeg + c * 8 < kend ? *reinterpret_cast<const uint4*>(vg + (size_t)d * ldv + c * 8)
+                                            : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < KU; ++i) {
+                const int u = threadIdx.x + i * kBlock;
+                const int row = u / (D / 8), c = u - row * (D / 8);
+                *reinterpret_cast<uint4*>(sK + row * KST + c * 8) = kx[i];
+            }
+            // V^T image with the key order permuted inside each 16-key group
+            // (bits 2 and 3 swapped) so that the 8 keys one PV fragment needs
+            // -- 16s+4h+{0..3} and 16s+8+4h+{0..3}, the accumulator's k order --
+            // are 16 contiguous bytes: one ds_read_b128 per fragment.  Keys
+            // 8c..8c+7 have bit 3 = c & 1; their halves (bit 2 = 0 / 1) land
+            // at +4*(c&1) and +8+4*(c&1) of the 16-key group.
+#pragma unroll
+            for (int i = 0; i < VU; ++i) {
+                const int u = threadIdx.x + i * kBlock;
+                const int d = u / (PCH / 8), c = u - d * (PCH / 8);
+                uint16_t* dst = sV + d * VST + (c >> 1) * 16 + (c & 1) * 4;
+                *reinterpret_cast<uint2*>(dst) = make_uint2(vx[i].x, vx[i].y);
+                *reinterpret_cast<uint2*>(dst + 8) = make_uint2(vx[i].z, vx[i].w);
+            }
+        }
+        __syncthreads();
+        const int qt = qg * NWAVE + wave;
+        if (qt >= qtiles) continue;
         const int qi = qt * 32 + r;  // this lane's query (the MFMA column)
         const bool qok = qi < nq;
         const int b = qok ? qi / G : 0, g = qok ? qi - (qi / G) * G : 0;
@@ -488,65 +551,60 @@ __global__ __launch_bounds__(kBlock) void prefix_attn_kernel(
         for (int t = 0; t < DT; ++t)
 #pragma unroll
             for (int i = 0; i < 16; ++i) o[t][i] = 0.f;
-        const int kbeg = sp * pchunk, kend = min(P, kbeg + pchunk);
-        const uint16_t* kb = pk + (size_t)kh * ldk * D + 8 * h;
-        const uint16_t* vb = vt + (size_t)kh * D * ldv + 4 * h;
-        for (int k0 = kbeg; k0 < kend; k0 += 32) {
-            const int kr = min(k0 + r, kend - 1);  // rows past the range are loaded but masked
-            const uint16_t* kp = kb + (size_t)kr * D;
-            uint4 kf[KS];
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) kf[ks] = *reinterpret_cast<const uint4*>(kp + ks * 16);
-            // V^T fragments of both k-steps for every d tile, issued before the
-            // QK MFMAs so the loads overlap them
-            uint2 vf[DT][2][2];
-#pragma unroll
-            for (int t = 0; t < DT; ++t) {
-                const uint16_t* vp = vb + (size_t)(32 * t + r) * ldv + k0;
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) {
-                    vf[t][s2][0] = *reinterpret_cast<const uint2*>(vp + 16 * s2);
-                    vf[t][s2][1] = *reinterpret_cast<const uint2*>(vp + 16 * s2 + 8);
-                }
-            }
+        const int ntile = (kend - kbeg + 31) / 32;
+        for (int kt = 0; kt < ntile; ++kt) {
+            const int k0 = kbeg + kt * 32;
             f32x16_t s;
 #pragma unroll
             for (int i = 0; i < 16; ++i) s[i] = 0.f;
+            const uint16_t* kl = sK + (kt * 32 + r) * KST + 8 * h;
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks)
-                s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf[ks]), qf[ks], s, 0, 0, 0);
-            // register i holds key k0 + (i&3) + 8*(i>>2) + 4*h of query r
+                s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(*reinterpret_cast<const uint4*>(kl + ks * 16)),
+                                                            qf[ks], s, 0, 0, 0);
+            // register i holds key k0 + (i&3) + 8*(i>>2) + 4*h of query r.  VALU
+            // budget per tile (the kernel's bound, not the MFMAs): the key
+            // mask only on a partial last tile, the scale folded into one FMA
+            // per score, the rescale skipped while no lane's max moved, and
+            // hardware bf16 packing (v_cvt_pk_bf16_f32).
             float mt = -1e30f;
+            if (k0 + 32 <= kend) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int key = k0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                s[i] = key < kend ? s[i] * scale_log2 : -1e30f;
-                mt = fmaxf(mt, s[i]);
+                for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[i]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int key = k0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    s[i] = key < kend ? s[i] : -1e30f;
+                    mt = fmaxf(mt, s[i]);
+                }
             }
-            mt = fmaxf(mt, __shfl_xor(mt, 32, kWave));
+            mt = fmaxf(mt, __shfl_xor(mt, 32, kWave)) * scale_log2;
             const float mn = fmaxf(m, mt);
-            const float corr = exp2f(m - mn);
-            m = mn;
-            l *= corr;
+            if (__any(mn > m)) {
+                const float corr = __builtin_amdgcn_exp2f(m - mn);
+                l *= corr;
 #pragma unroll
-            for (int t = 0; t < DT; ++t)
+                for (int t = 0; t < DT; ++t)
 #pragma unroll
-                for (int i = 0; i < 16; ++i) o[t][i] *= corr;
-            float p[16];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                p[i] = exp2f(s[i] - mn);
-                l += p[i];
+                    for (int i = 0; i < 16; ++i) o[t][i] *= corr;
             }
-            const bf16x8_t pb0 = as_bf16x8(pack8(p)), pb1 = as_bf16x8(pack8(p + 8));
+            m = mn;
+            f32x8_t p0, p1;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                p0[i] = __builtin_amdgcn_exp2f(fmaf(s[i], scale_log2, -mn));
+                p1[i] = __builtin_amdgcn_exp2f(fmaf(s[i + 8], scale_log2, -mn));
+                l += p0[i] + p1[i];
+            }
+            const bf16x8_t pb[2] = {__builtin_convertvector(p0, bf16x8_t), __builtin_convertvector(p1, bf16x8_t)};
 #pragma unroll
             for (int t = 0; t < DT; ++t) {
-                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                    as_bf16x8(make_uint4(vf[t][0][0].x, vf[t][0][0].y, vf[t][0][1].x, vf[t][0][1].y)), pb0, o[t], 0,
-                    0, 0);
-                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                    as_bf16x8(make_uint4(vf[t][1][0].x, vf[t][1][0].y, vf[t][1][1].x, vf[t][1][1].y)), pb1, o[t], 0,
-                    0, 0);
+                const uint16_t* vl = sV + (32 * t + r) * VST + kt * 32 + 8 * h;
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2)
+                    o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                        as_bf16x8(*reinterpret_cast<const uint4*>(vl + 16 * s2)), pb[s2], o[t], 0, 0, 0);
             }
         }
         const float lt = l + __shfl_xor(l, 32, kWave);
@@ -727,7 +785,8 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
     if (B <= 0) return 0;
     if (Hkv <= 0 || Hq % Hkv != 0 || splits <= 0 || chunk <= 0) return hipErrorInvalidValue;
     const bool prefix = plen != nullptr;
-    if (prefix && (!prefix_k || !prefix_vt || ps_max <= 0 || pchunk <= 0 || pchunk % 32 || ldv % 32 || ldv > max_seq))
+    if (prefix && (!prefix_k || !prefix_vt || ps_max <= 0 || pchunk != kPrefixChunk || ldv % kPrefixChunk ||
+                   ldv > max_seq))
         return hipErrorInvalidValue;
     if (!prefix) ps_max = 0;
     if ((splits > 1 || prefix) && (!part_o || !part_ml)) return hipErrorInvalidValue;
@@ -740,18 +799,17 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
     auto pl = (const int32_t*)plen;
     const long cap = 4L * device_cu_count();
     if (prefix) {
-        // one wave per (prefix split, kv head, 32-query tile); exits at once when *plen == 0
-        const long waves = (long)ps_max * Hkv * ((B * G + 31) / 32);
-        const long blocks = (waves + kBlock / kWave - 1) / (kBlock / kWave);
-        dim3 pgrid((unsigned)(blocks < cap ? blocks : cap));
+        // one block per (kv head, prefix split, 4 query tiles); exits at once when *plen == 0
+        const long items = (long)Hkv * ps_max * ((((B * G + 31) / 32) + 3) / 4);
+        dim3 pgrid((unsigned)(items < cap ? items : cap));
         if (D == 64)
             prefix_attn_kernel<64><<<pgrid, kBlock, 0, st>>>(qq, (const uint16_t*)prefix_k, (const uint16_t*)prefix_vt,
                                                            pl, (float*)part_o, (float*)part_ml, B, Hkv, G, max_seq,
-                                                           ldv, pchunk, ps_max, ps_max + splits, sl2);
+                                                           ldv, ps_max, ps_max + splits, sl2);
         else if (D == 128)
             prefix_attn_kernel<128><<<pgrid, kBlock, 0, st>>>(qq, (const uint16_t*)prefix_k,
                                                             (const uint16_t*)prefix_vt, pl, (float*)part_o,
-                                                            (float*)part_ml, B, Hkv, G, max_seq, ldv, pchunk, ps_max,
+                                                            (float*)part_ml, B, Hkv, G, max_seq, ldv, ps_max,
                                                             ps_max + splits, sl2);
         else
             return hipErrorInvalidValue;

@@ -190,8 +190,8 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
         _req(pvt, torch.bfloat16, "decode_attention.prefix.vt")
         _req(plen, torch.int32, "decode_attention.prefix.length")
         ldv = pvt.shape[-1]
-        if (tuple(pk.shape) != (Hkv, MAXS, D) or tuple(pvt.shape) != (Hkv, D, ldv) or ldv % 32 or ldv > MAXS
-                or pchunk % 32 or pchunk <= 0 or plen.numel() != 1):
+        if (tuple(pk.shape) != (Hkv, MAXS, D) or tuple(pvt.shape) != (Hkv, D, ldv) or ldv % PREFIX_CHUNK
+                or ldv > MAXS or pchunk != PREFIX_CHUNK or plen.numel() != 1):
             raise HipOpsError(f"decode_attention: prefix k {tuple(pk.shape)} / vt {tuple(pvt.shape)} / chunk "
                               f"{pchunk} do not match kv {tuple(k_cache.shape)}")
         ps_max = prefix_splits(ldv, pchunk)
@@ -213,7 +213,10 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     return out
 
 
-def prefix_splits(ldv: int, pchunk: int) -> int:
+PREFIX_CHUNK = 256  # keys per prefix split: kPrefixChunk in csrc/dmcp_kernels.hip
+
+
+def prefix_splits(ldv: int, pchunk: int = PREFIX_CHUNK) -> int:
     return max(1, math.ceil(ldv / pchunk))
 
 

@@ -79,6 +79,34 @@ def bench_decode_attention(B, L, Hq=32, Hkv=8, D=64, max_seq=4096, chunk=256, ea
            chunk=chunk)
 
 
+def bench_prefix_attention(B, P, Ls, Hq=32, Hkv=8, D=64, max_seq=8192, chunk=1024, pchunk=256):
+    """Shared-prefix decode step: every row = P shared keys + Ls own keys.
+    Bytes counted = what must be read at least once (prefix once, own keys
+    per row); 'rowwise_us' = the same step without the prefix kernel (every
+    row streams all P + Ls keys itself)."""
+    from dmcp.ops.reference import SharedPrefix
+    dev = "cuda"
+    S = B + 1
+    kc = torch.randn(S, Hkv, max_seq, D, device=dev).to(torch.bfloat16)
+    vc = torch.randn(S, Hkv, max_seq, D, device=dev).to(torch.bfloat16)
+    vt = vc[B].transpose(-1, -2).contiguous()
+    q = torch.randn(B, Hq, D, device=dev).to(torch.bfloat16)
+    slot = torch.arange(B, dtype=torch.int32, device=dev)
+    sl = torch.full((B,), P + Ls, dtype=torch.int32, device=dev)
+    plen = torch.tensor([P], dtype=torch.int32, device=dev)
+    pre = SharedPrefix(kc[B], vt, plen, pchunk)
+    ws = hip.decode_workspace(B, Hq, Hkv, D, max_seq, dev, chunk, hip.prefix_splits(max_seq, pchunk))
+    out = torch.empty_like(q)
+    t = timed(lambda: hip.decode_attention(q, kc, vc, slot, sl, 1 / math.sqrt(D), workspace=ws, chunk=chunk,
+                                           out=out, prefix=pre))
+    rowwise = timed(lambda: hip.decode_attention(q, kc, vc, slot, sl, 1 / math.sqrt(D), workspace=ws, chunk=chunk,
+                                                 out=out))
+    nbytes = 2 * Hkv * D * 2 * (P + B * Ls) + 2 * q.numel() * 2
+    out_rec = {"rowwise_us": round(rowwise * 1e6, 2), "speedup_vs_rowwise": round(rowwise / t, 2)}
+    report("decode_attention_shared_prefix", t, nbytes, None, B=B, P=P, Ls=Ls, Hq=Hq, Hkv=Hkv, D=D, chunk=chunk,
+           pchunk=pchunk, **out_rec)
+
+
 def bench_rmsnorm(rows, H=2048):
     x = torch.randn(rows, H, device="cuda").to(torch.bfloat16)
     r = torch.randn(rows, H, device="cuda").to(torch.bfloat16)
@@ -122,6 +150,17 @@ def bench_argmax(B, V=320):
 
 def main() -> int:
     hip.lib()
+    only = sys.argv[1] if len(sys.argv) > 1 else ""
+    if only == "prefix8k":  # one case, for counter collection
+        bench_prefix_attention(80, 8000, 100, max_seq=8192)
+        return 0
+    if only in ("", "prefix"):
+        bench_prefix_attention(80, 4151, 2500)
+        bench_prefix_attention(256, 4151, 2500)
+        bench_prefix_attention(16, 4151, 2500)
+        bench_prefix_attention(80, 8000, 100, max_seq=8192)
+        if only:
+            return 0
     for B, L in ((1, 4096), (16, 2048), (64, 512), (64, 2300), (64, 4096), (256, 2300)):
         bench_decode_attention(B, L)
     bench_decode_attention(64, 2300, Hq=24, Hkv=8, D=128)

@@ -71,6 +71,11 @@ class SourceTree:
         """Raw native scan document (JSON bytes)."""
         raise NotImplementedError
 
+    def scan_objects(self, language: str, threads: int, framework: str = "") -> Optional[dict]:
+        """The scan document as Python objects built natively (no JSON round
+        trip), or None when this tree only offers :meth:`scan`."""
+        return None
+
     def readme(self, max_length: int = 10_000) -> Optional[str]:
         """README.md truncated to ``max_length`` + marker (CodeContextService.java:1688-1712)."""
         content = self.read_text("README.md")
@@ -126,6 +131,14 @@ class MemoryTree(SourceTree):
     def scan(self, language: str, threads: int, framework: str = "") -> bytes:
         from ..parsers.base import native
         return native().scan_sources(list(self.files.items()), language, threads, framework)
+
+    def scan_objects(self, language: str, threads: int, framework: str = "") -> Optional[dict]:
+        from ..models.domain import StaticMethodInfo
+        from ..parsers.base import native
+        fn = getattr(native(), "scan_sources_objects", None)
+        if fn is None:
+            return None
+        return fn(list(self.files.items()), language, threads, framework, StaticMethodInfo)
 
 
 def list_tree(git, git_dir: str, rev: str = "HEAD") -> List[Tuple[str, str]]:

@@ -122,38 +122,63 @@ def _methods_from(raw: Sequence[dict]) -> List[StaticMethodInfo]:
     return out
 
 
+_CLASS_TYPES: Dict[Optional[str], ClassType] = {}
+
+
+def _class_type(name: Optional[str]) -> ClassType:
+    ct = _CLASS_TYPES.get(name)
+    if ct is None:
+        ct = _CLASS_TYPES[name] = ClassType.from_string(name)
+    return ct
+
+
+def _add_unit(units: Dict[str, ParsedUnit], lang: str, path: str, ident: str, ct: ClassType, entry: bool,
+              methods: List[StaticMethodInfo], deps: List[str], params: Dict[str, List[str]]) -> None:
+    u = units.get(ident)
+    if u is None or lang != "go":
+        # Java / TS: a later file with the same identifier replaces the node
+        # (ProjectGraph.addNode overwrite semantics).
+        if u is not None:
+            del units[ident]
+        units[ident] = ParsedUnit(ident, path, ct, entry, methods, deps, params, [path])
+    else:
+        # Go: every file of a package is the same node; the reference keeps
+        # only the last file's methods (GoSourceParser + phase 1), here all
+        # files contribute (documented divergence).
+        u.source_file = path
+        u.methods.extend(methods)
+        u.params.update(params)
+        u.files.append(path)
+        for d in deps:
+            if d not in u.deps:
+                u.deps.append(d)
+
+
 def to_parsed_project(doc: dict) -> ParsedProject:
+    """From the native scan document: the JSON form (``files`` as objects) or
+    the direct-object form of ``scan_sources_objects`` (``files`` as tuples
+    ``(path, identifier, classType, entryPoint, package, deps, params,
+    methods)`` with ``methods`` already :class:`StaticMethodInfo`)."""
     lang = doc["language"]
     units: Dict[str, ParsedUnit] = {}
     file_to_id: Dict[str, str] = {}
     for f in doc.get("files", []):
+        if isinstance(f, tuple):
+            path, ident, ct, entry, _pkg, deps, params, methods = f
+            file_to_id[path] = ident
+            _add_unit(units, lang, path, ident, _class_type(ct), entry, methods, deps, dict(params))
+            continue
         ident = f["identifier"]
         path = f["path"]
         file_to_id[path] = ident
-        methods = _methods_from(f.get("methods") or ())
-        params = {k: list(v) for k, v in (f.get("params") or {}).items()}
-        ct = ClassType.from_string(f.get("classType"))
-        u = units.get(ident)
-        if u is None or lang != "go":
-            # Java / TS: a later file with the same identifier replaces the node
-            # (ProjectGraph.addNode overwrite semantics).
-            if u is not None:
-                del units[ident]
-            units[ident] = ParsedUnit(ident, path, ct, bool(f.get("entryPoint")), methods,
-                                      list(f.get("deps") or ()), params, [path])
-        else:
-            # Go: every file of a package is the same node; the reference keeps
-            # only the last file's methods (GoSourceParser + phase 1), here all
-            # files contribute (documented divergence).
-            u.source_file = path
-            u.methods.extend(methods)
-            u.params.update(params)
-            u.files.append(path)
-            for d in f.get("deps") or ():
-                if d not in u.deps:
-                    u.deps.append(d)
+        _add_unit(units, lang, path, ident, _class_type(f.get("classType")), bool(f.get("entryPoint")),
+                  _methods_from(f.get("methods") or ()), list(f.get("deps") or ()),
+                  {k: list(v) for k, v in (f.get("params") or {}).items()})
+    go = doc.get("go")
+    if isinstance(go, str):
+        go = json.loads(go)
     return ParsedProject(lang, doc.get("sourceRoot", "."), doc.get("framework"), doc.get("module"),
-                         units, file_to_id, doc.get("stats") or {}, doc.get("go"))
+                         units, file_to_id, doc.get("stats") or {}, go)
 
 
 class SourceParser:
@@ -195,7 +220,9 @@ class SourceParser:
         """Scans a :class:`dmcp.index.source.SourceTree` (in-memory git snapshot
         or checkout) -- same result as :meth:`scan` over a checkout of it."""
         t0 = time.perf_counter()
-        doc = json.loads(tree.scan(self.language_name, self.threads, self.framework_override))
+        doc = tree.scan_objects(self.language_name, self.threads, self.framework_override)
+        if doc is None:
+            doc = json.loads(tree.scan(self.language_name, self.threads, self.framework_override))
         self.project = to_parsed_project(doc)
         self._root = tree.directory
         LOG.info("Scanned %s @ %s: %d files, %d units in %.1f ms", tree.directory, tree.commit_hash[:12],

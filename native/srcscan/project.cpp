@@ -269,67 +269,67 @@ std::string detect_language(const std::string& root) {
     return "java";
 }
 
-std::string scan_project_json(const std::string& root, const ScanOptions& opt) {
+ScanResult scan_project(const std::string& root, const ScanOptions& opt) {
     auto t0 = std::chrono::steady_clock::now();
+    ScanResult r;
     std::string lang = opt.language;
     if (lang == "auto" || lang.empty()) lang = detect_language(root);
     if (lang == "ts" || lang == "js" || lang == "javascript" || lang == "node") lang = "typescript";
-    std::vector<FileRec> files;
-    int skipped = 0;
-    FrameworkInfo fw;
-    bool has_fw = false;
-    std::string source_root = ".";
-    std::string module;
-    std::string go_json;
-    if (lang == "java") {
-        source_root = "src/main/java";
-        scan_java(root, opt, files, skipped);
-    } else if (lang == "typescript") {
-        scan_ts(root, opt, files, skipped, fw, source_root);
-        has_fw = true;
+    if (lang == "typescript") {
+        scan_ts(root, opt, r.files, r.skipped, r.framework, r.source_root);
+        r.has_framework = true;
     } else if (lang == "go") {
-        go_project_files(root, opt.threads, module, files, &go_json);
+        go_project_files(root, opt.threads, r.module, r.files, &r.go_json);
     } else {
         lang = "java";
-        source_root = "src/main/java";
-        scan_java(root, opt, files, skipped);
+        r.source_root = "src/main/java";
+        scan_java(root, opt, r.files, r.skipped);
     }
-    auto t1 = std::chrono::steady_clock::now();
+    r.language = lang;
+    r.elapsed_us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+    return r;
+}
+
+std::string scan_result_json(const ScanResult& r) {
     JsonWriter w;
     w.begin_obj();
-    w.kv("language", lang);
-    w.kv("sourceRoot", source_root);
+    w.kv("language", r.language);
+    w.kv("sourceRoot", r.source_root);
     w.key("framework");
-    if (has_fw) {
+    if (r.has_framework) {
         w.begin_obj();
-        w.kv("name", fw.name);
-        w.kv("sourceRoot", fw.source_root);
+        w.kv("name", r.framework.name);
+        w.kv("sourceRoot", r.framework.source_root);
         w.key("features");
         w.begin_obj();
-        for (auto& kv : fw.features) w.kv(kv.first, kv.second);
+        for (auto& kv : r.framework.features) w.kv(kv.first, kv.second);
         w.end_obj();
         w.end_obj();
     } else {
         w.value_null();
     }
-    if (lang == "go") w.kv("module", module);
+    if (r.language == "go") w.kv("module", r.module);
     w.key("stats");
     w.begin_obj();
-    w.kv_int("discovered", (long long)files.size() + skipped);
-    w.kv_int("analyzed", (long long)files.size());
-    w.kv_int("skipped", skipped);
-    w.kv_int("elapsedUs", std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count());
+    w.kv_int("discovered", (long long)r.files.size() + r.skipped);
+    w.kv_int("analyzed", (long long)r.files.size());
+    w.kv_int("skipped", r.skipped);
+    w.kv_int("elapsedUs", r.elapsed_us);
     w.end_obj();
     w.key("files");
     w.begin_arr();
-    for (auto& f : files) write_file(w, f);
+    for (auto& f : r.files) write_file(w, f);
     w.end_arr();
-    if (!go_json.empty()) {
+    if (!r.go_json.empty()) {
         w.key("go");
-        w.raw(go_json);
+        w.raw(r.go_json);
     }
     w.end_obj();
     return w.out;
+}
+
+std::string scan_project_json(const std::string& root, const ScanOptions& opt) {
+    return scan_result_json(scan_project(root, opt));
 }
 
 std::string scan_file_json(const std::string& path, const std::string& language, const std::string& rel_path,

@@ -56,6 +56,95 @@ dbw::Batch to_batch(const std::string& sql, py::list rows) {
     return b;
 }
 
+// (relative path, bytes) pairs -> scan of the mounted in-memory tree (GIL released)
+srcscan::ScanResult scan_mounted(py::list files, const std::string& language, int threads,
+                                 const std::string& framework) {
+    std::vector<std::pair<std::string, std::string>> tree;
+    tree.reserve(files.size());
+    for (auto item : files) {
+        auto tup = item.cast<py::tuple>();
+        tree.emplace_back(tup[0].cast<std::string>(), tup[1].cast<std::string>());
+    }
+    py::gil_scoped_release release;
+    std::string root = srcscan::vfs_mount(std::move(tree));
+    srcscan::ScanOptions opt;
+    opt.language = language;
+    opt.threads = threads;
+    opt.framework = framework;
+    try {
+        srcscan::ScanResult r = srcscan::scan_project(root, opt);
+        srcscan::vfs_unmount(root);
+        return r;
+    } catch (...) {
+        srcscan::vfs_unmount(root);
+        throw;
+    }
+}
+
+py::str pystr(const std::string& s) { return py::str(s.data(), s.size()); }
+
+py::list str_list(const std::vector<std::string>& v) {
+    py::list out(v.size());
+    for (size_t i = 0; i < v.size(); ++i) out[i] = pystr(v[i]);
+    return out;
+}
+
+// ScanResult -> Python objects without a JSON round trip: the document's
+// top-level keys, "files" as tuples (path, identifier, classType, entryPoint,
+// package, deps, params [(method, [ids])], methods), each method an instance
+// of ``method_cls`` (a tuple subclass: StaticMethodInfo) built like
+// tuple.__new__(method_cls, (name, line, httpMethod, httpPath, exceptions)).
+py::dict scan_result_objects(const srcscan::ScanResult& r, py::handle method_cls) {
+    if (!PyType_Check(method_cls.ptr()) || !PyType_IsSubtype((PyTypeObject*)method_cls.ptr(), &PyTuple_Type))
+        throw py::type_error("method_cls must be a tuple subclass");
+    auto* mtype = (PyTypeObject*)method_cls.ptr();
+    py::dict d;
+    d["language"] = pystr(r.language);
+    d["sourceRoot"] = pystr(r.source_root);
+    if (r.has_framework) {
+        py::dict fw, features;
+        fw["name"] = pystr(r.framework.name);
+        fw["sourceRoot"] = pystr(r.framework.source_root);
+        for (auto& kv : r.framework.features) features[pystr(kv.first)] = pystr(kv.second);
+        fw["features"] = features;
+        d["framework"] = fw;
+    } else {
+        d["framework"] = py::none();
+    }
+    if (r.language == "go") d["module"] = pystr(r.module);
+    py::dict stats;
+    stats["discovered"] = (long long)r.files.size() + r.skipped;
+    stats["analyzed"] = (long long)r.files.size();
+    stats["skipped"] = r.skipped;
+    stats["elapsedUs"] = r.elapsed_us;
+    d["stats"] = stats;
+    py::list files(r.files.size());
+    for (size_t k = 0; k < r.files.size(); ++k) {
+        const srcscan::FileRec& f = r.files[k];
+        py::list params(f.params.size());
+        for (size_t i = 0; i < f.params.size(); ++i)
+            params[i] = py::make_tuple(pystr(f.params[i].first), str_list(f.params[i].second));
+        py::list methods(f.methods.size());
+        for (size_t i = 0; i < f.methods.size(); ++i) {
+            const srcscan::MethodRec& m = f.methods[i];
+            py::tuple exc(m.exceptions.size());
+            for (size_t j = 0; j < m.exceptions.size(); ++j) exc[j] = pystr(m.exceptions[j]);
+            py::tuple fields = py::make_tuple(pystr(m.name), m.line,
+                                              m.has_http_method ? py::object(pystr(m.http_method)) : py::none(),
+                                              m.has_http_path ? py::object(pystr(m.http_path)) : py::none(), exc);
+            py::tuple args = py::make_tuple(fields);
+            PyObject* obj = PyTuple_Type.tp_new(mtype, args.ptr(), nullptr);
+            if (!obj) throw py::error_already_set();
+            methods[i] = py::reinterpret_steal<py::object>(obj);
+        }
+        files[k] = py::make_tuple(pystr(f.rel_path), pystr(f.identifier), pystr(f.class_type), f.entry_point,
+                                  pystr(f.package_name), str_list(f.deps), params, methods);
+    }
+    d["files"] = files;
+    d["go"] = r.go_json.empty() ? py::object(py::none()) : py::object(pystr(r.go_json));
+    return d;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_srcscan, m) {
@@ -105,6 +194,15 @@ PYBIND11_MODULE(_srcscan, m) {
             return py::bytes(out);
         },
         py::arg("files"), py::arg("language") = "auto", py::arg("threads") = 0, py::arg("framework") = "");
+    m.def(
+        "scan_sources_objects",
+        [](py::list files, const std::string& language, int threads, const std::string& framework,
+           py::handle method_cls) {
+            srcscan::ScanResult r = scan_mounted(files, language, threads, framework);
+            return scan_result_objects(r, method_cls);
+        },
+        py::arg("files"), py::arg("language"), py::arg("threads"), py::arg("framework"), py::arg("method_cls"),
+        "scan_sources as Python objects (files as tuples, methods as method_cls) -- no JSON round trip");
     m.def(
         "scan_file",
         [](const std::string& path, const std::string& language, const std::string& rel, const std::string& fw) {

@@ -75,9 +75,25 @@ struct ScanOptions {
     size_t max_file_bytes = 5u * 1024u * 1024u;  // NodeJsGraalParser.java:57
 };
 
-// Scans a project root and returns the full result as a JSON document
-// (see docs in project.cpp).
+// Result of a project scan (what the JSON document of project.cpp holds).
+struct ScanResult {
+    std::string language;
+    std::string source_root = ".";
+    bool has_framework = false;
+    FrameworkInfo framework;
+    std::string module;    // go only
+    std::string go_json;   // go only: ProjectAnalysis document
+    std::vector<FileRec> files;
+    int skipped = 0;
+    long long elapsed_us = 0;
+};
+
+// Scans a project root (a directory or a mounted in-memory tree).
+ScanResult scan_project(const std::string& root, const ScanOptions& opt);
+
+// The same scan as a JSON document (see docs in project.cpp).
 std::string scan_project_json(const std::string& root, const ScanOptions& opt);
+std::string scan_result_json(const ScanResult& r);
 
 // Single-file analysis (tests / debugging); returns the FileRec as JSON.
 std::string scan_file_json(const std::string& path, const std::string& language,

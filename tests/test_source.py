@@ -173,3 +173,22 @@ def test_native_loose_reader_matches_git_with_mixed_store(tmp_path):
         S.mostly_loose = orig
     assert got == _read_via_git(g, str(src), shas, 0, 1)
     assert b"" in got and bytes(range(256)) * 50 in got
+
+
+@pytest.mark.parametrize("kind", ["java", "nest", "go"])
+def test_scan_objects_equal_json_document(tmp_path, kind):
+    """The direct-object scan (no JSON round trip) parses to exactly what the
+    JSON document parses to."""
+    import json as _json
+    from dmcp.parsers.base import to_parsed_project
+    repo = tmp_path / "r"
+    {"java": lambda: synth.java_spring_repo(str(repo), 30),
+     "nest": lambda: synth.nestjs_repo(str(repo), 5),
+     "go": lambda: synth.go_gin_repo(str(repo), 4)}[kind]()
+    t = GitClient(str(tmp_path / "c")).snapshot(RepositoryUrl.of(str(repo)), "main")
+    lang = t.detect_language()
+    a = to_parsed_project(t.scan_objects(lang, 4))
+    b = to_parsed_project(_json.loads(t.scan(lang, 4)))
+    a.stats = b.stats = None
+    assert a.units and a == b
+    assert all(type(m).__name__ == "StaticMethodInfo" for u in a.units.values() for m in u.methods)

@@ -207,7 +207,7 @@ class Indexer:
                         with span("analyze.phase3", stats):
                             recovered = self._recover_unenriched(project, parsed, graph, clone, readme)
                 with span("analyze.persist_graph", stats):
-                    project.base_package = common_package_prefix(package_name_of(i) for i in parsed.units)
+                    project.base_package = common_package_prefix({package_name_of(i) for i in parsed.units})
                     project.update_graph_data(graph.to_json())
                     with span("analyze.phase1_commit", stats):
                         writer.wait()  # no-op when enrichment already waited
@@ -286,17 +286,66 @@ class Indexer:
         methods_by_ident: Dict[str, List[Tuple[str, str]]] = {}
         units = parsed.units
         class_ids: Dict[str, str] = {}
-        n_ids = sum(1 + len(u.methods) + sum(len(v) for v in u.params.values()) * 2 for u in units.values())
-        id_pool = iter(new_ids(n_ids))
-
-        def nid() -> str:
-            return next(id_pool, None) or new_id()
-
+        # an upper bound of the ids needed: one per class and method, one per
+        # parameter link of every method (overloads included)
+        n_ids = 0
+        for u in units.values():
+            n_ids += 1 + len(u.methods)
+            if u.params:
+                n_ids += sum(len(u.params.get(m[0]) or ()) for m in u.methods)
+        nid = iter(new_ids(n_ids)).__next__
         # the writer thread starts deleting the old rows right away
         writer = self.repos.project_rows_writer(pid, replace)
         try:
-            self._phase1_rows(order, units, graph, pid, now, commit_hash, nid, class_ids, methods_by_ident,
-                              cls_rows, meth_rows, param_rows, writer)
+            class_types: Dict[str, Optional[str]] = {}
+            method_infos: Dict[str, List[MethodInfo]] = {}
+            cls_append, meth_append = cls_rows.append, meth_rows.append
+            dumps = json.dumps
+            for ident in order:
+                unit = units.get(ident)
+                if unit is None:
+                    continue
+                cid = nid()
+                class_ids[ident] = cid
+                ct = unit.class_type.value
+                i = ident.rfind(".")
+                cls_append((cid, pid, ident, ident[i + 1:] if i >= 0 else ident,
+                            ident[:i] if i >= 0 else None, ct, None, unit.source_file, now, commit_hash))
+                class_types[ident] = ct
+                infos = []
+                mids = []
+                for name, line, http_method, http_path, exc in unit.methods:
+                    mid = nid()
+                    meth_append((mid, cid, name, None, "[]", dumps(list(exc)) if exc else "[]", http_method,
+                                 http_path, line, now))
+                    infos.append(MethodInfo(name, None, (), tuple(exc), http_method, http_path, line))
+                    mids.append((name, mid))
+                method_infos[ident] = infos
+                methods_by_ident[ident] = mids
+            writer.put("classes", cls_rows)
+            writer.put("methods", meth_rows)
+            # parameter links (CodeContextService.java:274-291, 805-856): the
+            # first method of each name that has resolved parameter types
+            links: Dict[str, Dict[str, List[str]]] = {}
+            for ident, mids in methods_by_ident.items():
+                params = units[ident].params
+                if not params or not mids:
+                    continue
+                per: Dict[str, List[str]] = {}
+                for mname, mid in mids:
+                    targets = params.get(mname)
+                    if not targets:
+                        continue
+                    if mname not in per:
+                        per[mname] = targets
+                    for pos, tgt in enumerate(targets):
+                        tcid = class_ids.get(tgt)
+                        if tcid is not None:
+                            param_rows.append((nid(), mid, pos, tcid, now))
+                if per:
+                    links[ident] = per
+            writer.put("params", param_rows)
+            graph.load_static_metadata(class_ids, class_types, method_infos, links)
             writer.close()
         except BaseException:
             writer.abort()
@@ -304,56 +353,6 @@ class Indexer:
         LOG.info("Phase 1 rows built. Classes: %d, Methods: %d, Parameters: %d",
                  len(cls_rows), len(meth_rows), len(param_rows))
         return len(cls_rows), methods_by_ident, writer
-
-    def _phase1_rows(self, order, units, graph, pid, now, commit_hash, nid, class_ids, methods_by_ident,
-                     cls_rows, meth_rows, param_rows, writer) -> None:
-        for ident in order:
-            unit = units.get(ident)
-            if unit is None:
-                continue
-            cid = nid()
-            class_ids[ident] = cid
-            ct = unit.class_type.value
-            i = ident.rfind(".")
-            cls_rows.append((cid, pid, ident, ident[i + 1:] if i >= 0 else ident,
-                             ident[:i] if i >= 0 else None, ct, None, unit.source_file, now, commit_hash))
-            graph.set_node_info(ident, ct, None)
-            infos = []
-            mids = []
-            for sm in unit.methods:
-                mid = nid()
-                exc = sm.exceptions
-                meth_rows.append((mid, cid, sm.method_name, None, "[]",
-                                  json.dumps(list(exc)) if exc else "[]", sm.http_method, sm.http_path,
-                                  sm.line_number, now))
-                infos.append(MethodInfo(sm.method_name, None, (), tuple(exc), sm.http_method,
-                                        sm.http_path, sm.line_number))
-                mids.append((sm.method_name, mid))
-            graph.set_method_infos(ident, infos)
-            methods_by_ident[ident] = mids
-        writer.put("classes", cls_rows)
-        writer.put("methods", meth_rows)
-        for ident, cid in class_ids.items():
-            graph.bind_class_id(ident, cid)
-        # second pass: parameter links (CodeContextService.java:274-291, 805-856)
-        for ident, mids in methods_by_ident.items():
-            params = units[ident].params
-            if not params or not mids:
-                continue
-            linked = set()
-            for mname, mid in mids:
-                targets = params.get(mname)
-                if not targets:
-                    continue
-                if mname not in linked:
-                    linked.add(mname)
-                    for pos, tgt in enumerate(targets):
-                        graph.add_method_parameter(ident, mname, pos, tgt)
-                for pos, tgt in enumerate(targets):
-                    tcid = class_ids.get(tgt)
-                    if tcid is not None:
-                        param_rows.append((nid(), mid, pos, tcid, now))
-        writer.put("params", param_rows)
 
     # ------------------------------------------------------------ enrichment
     def _read_source(self, tree: SourceTree, unit: ParsedUnit) -> Optional[str]:
@@ -519,7 +518,7 @@ class Indexer:
                     self.repos.params.delete_by_project_id(project_id)
                     self.repos.params.save_rows(param_rows)
                 project.update_graph_data(graph.to_json())
-                project.base_package = common_package_prefix(package_name_of(i) for i in parsed.units)
+                project.base_package = common_package_prefix({package_name_of(i) for i in parsed.units})
                 self.repos.projects.update(project)
                 self.cache.put(project_id, project.name, graph)
             return {"success": True, "projectId": project_id, "bound": bound,
@@ -679,7 +678,7 @@ class Indexer:
                 final_classes = {sc.full_class_name: sc for sc in self.repos.classes.find_by_project_id(project.id)}
                 mb_all = self.repos.methods.find_by_class_ids([sc.id for sc in final_classes.values()])
                 self._attach_metadata(graph, parsed, final_classes, mb_all)
-                project.base_package = common_package_prefix(package_name_of(i) for i in parsed.units)
+                project.base_package = common_package_prefix({package_name_of(i) for i in parsed.units})
                 project.update_graph_data(graph.to_json())
                 project.sync_completed(head)
                 self.repos.projects.update(project)

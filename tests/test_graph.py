@@ -205,3 +205,32 @@ def test_cache_put_rename_and_load(tmp_db):
     assert fresh.reload(good.id) and not fresh.reload(bad.id) and not fresh.reload("missing")
     fresh.evict(good.id)
     assert fresh.get_graph(good.id) is None
+
+
+def test_load_static_metadata_equals_per_call_api():
+    """The Phase 1 bulk loader builds exactly the graph the per-element
+    setters build (link positions kept when a target is not a node)."""
+    from dmcp.graph.project_graph import MethodInfo, ProjectGraph
+
+    def base():
+        g = ProjectGraph()
+        for n in ("a.A", "a.B", "a.C"):
+            g.add_node(n, n.replace(".", "/") + ".java")
+        g.add_dependency("a.A", "a.B")
+        return g
+    infos = {"a.A": [MethodInfo("run", None, (), ("E",), "GET", "/x", 3)], "a.B": [], "a.C": []}
+    params = {"a.A": {"run": ["a.B", "x.Missing", "a.C"], "stop": ["a.C"]}, "zz.NotANode": {"m": ["a.A"]}}
+    g1 = base()
+    for ident, cid in (("a.A", "1"), ("a.B", "2"), ("a.C", "3")):
+        g1.bind_class_id(ident, cid)
+        g1.set_node_info(ident, "SERVICE", None)
+        g1.set_method_infos(ident, infos[ident])
+    for ident, per in params.items():
+        for m, targets in per.items():
+            for pos, t in enumerate(targets):
+                g1.add_method_parameter(ident, m, pos, t)
+    g2 = base()
+    g2.load_static_metadata({"a.A": "1", "a.B": "2", "a.C": "3"}, {k: "SERVICE" for k in ("a.A", "a.B", "a.C")},
+                            infos, params)
+    assert g1.to_dict() == g2.to_dict()
+    assert [(l.position, l.target_identifier) for l in g2.method_parameters("a.A")["run"]] == [(0, "a.B"), (2, "a.C")]

@@ -276,8 +276,9 @@ class ProjectGraph:
             if not ident or not cid:
                 raise ValueError("Identifier and class ID are required")
             self._class_ids[ident] = cid
+        tnew = tuple.__new__  # NamedTuples without the generated __new__ wrapper
         for ident, ct in class_types.items():
-            self._node_info[ident] = NodeInfo(ct, None)
+            self._node_info[ident] = tnew(NodeInfo, (ct, None))
         for ident, infos in method_infos.items():
             self._method_info[ident] = list(infos)
         for ident, per_method in method_params.items():
@@ -285,7 +286,7 @@ class ProjectGraph:
                 continue
             per = None
             for mname, targets in per_method.items():
-                links = [MethodParameterLink(pos, t) for pos, t in enumerate(targets) if t in nodes]
+                links = [tnew(MethodParameterLink, (pos, t)) for pos, t in enumerate(targets) if t in nodes]
                 if links:
                     if per is None:
                         per = self._mparams.setdefault(ident, {})

@@ -301,6 +301,7 @@ class Indexer:
             method_infos: Dict[str, List[MethodInfo]] = {}
             cls_append, meth_append = cls_rows.append, meth_rows.append
             dumps = json.dumps
+            tnew, MI = tuple.__new__, MethodInfo  # NamedTuple without the generated __new__ wrapper
             for ident in order:
                 unit = units.get(ident)
                 if unit is None:
@@ -318,7 +319,7 @@ class Indexer:
                     mid = nid()
                     meth_append((mid, cid, name, None, "[]", dumps(list(exc)) if exc else "[]", http_method,
                                  http_path, line, now))
-                    infos.append(MethodInfo(name, None, (), tuple(exc), http_method, http_path, line))
+                    infos.append(tnew(MI, (name, None, (), exc, http_method, http_path, line)))
                     mids.append((name, mid))
                 method_infos[ident] = infos
                 methods_by_ident[ident] = mids

@@ -583,13 +583,18 @@ class ProjectRowsWriter:
         self._next = 0
         self._done = False
         self._native = None
+        # the native writer reads text straight out of these objects' UTF-8
+        # buffers: they stay referenced here until its thread has finished
+        self._keep: List[object] = []
         if self._sync:
             return
         bulk = _native_bulk_writer()
         if bulk is not None:
             setup = []
             if replace:
-                setup = [(r.DELETE_BY_PROJECT_ID, (project_id,)) for r in (repos.params, repos.methods, repos.classes)]
+                setup = [(r.DELETE_BY_PROJECT_ID, ((project_id,),))
+                         for r in (repos.params, repos.methods, repos.classes)]
+            self._keep.append(setup)
             self._native = bulk(repos.db.path, self.BUSY_TIMEOUT_MS, setup)
             return
         self._thread = threading.Thread(target=self._run, name="dmcp-rows-writer", daemon=True)
@@ -604,7 +609,9 @@ class ProjectRowsWriter:
                 raise ValueError(f"{table} rows after their children")
             self._next = self._ORDER.index(table) + 1
             if rows:
-                self._native.put(getattr(self.repos, table)._INSERT, list(rows))
+                frozen = tuple(rows)  # immutable: the writer holds views into it
+                self._keep.append(frozen)
+                self._native.put(getattr(self.repos, table)._INSERT, frozen)
         elif self._sync:
             self._pending[table] = rows
         else:
@@ -612,6 +619,7 @@ class ProjectRowsWriter:
 
     def close(self) -> None:
         """No more rows: the writer commits once everything queued is in."""
+        self._closed = True
         if self._native is not None:
             self._native.commit()
         elif self._sync:
@@ -623,6 +631,7 @@ class ProjectRowsWriter:
         self._done = True
         if self._native is not None:
             self._native.abort()
+            self._keep.clear()
         elif self._thread is not None:
             self._q.put(("__abort__", ()))
             self._thread.join()
@@ -635,11 +644,24 @@ class ProjectRowsWriter:
                     self.rows_written = self._native.wait()
                 except RuntimeError as e:
                     self._error = e
+                self._keep.clear()
         elif self._thread is not None:
             self._thread.join()
         if self._error is not None:
             raise self._error
         return self.rows_written
+
+    def __del__(self) -> None:
+        # never release the row objects while the native thread may read them
+        native = getattr(self, "_native", None)
+        if native is not None and not getattr(self, "_done", True):
+            try:
+                if getattr(self, "_closed", False):
+                    native.wait()
+                else:
+                    native.abort()  # never committed: roll back
+            except Exception:
+                pass
 
     # -------------------------------------------------------------- writer
     def _run(self) -> None:

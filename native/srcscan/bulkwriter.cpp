@@ -43,7 +43,7 @@ struct Conn {
                     case Value::Int: rc = sqlite3_bind_int64(st, c + 1, x.i); break;
                     case Value::Real: rc = sqlite3_bind_double(st, c + 1, x.d); break;
                     case Value::Text:
-                        rc = sqlite3_bind_text(st, c + 1, x.s.data(), static_cast<int>(x.s.size()), sqlite_min::STATIC);
+                        rc = sqlite3_bind_text(st, c + 1, x.p, x.n, sqlite_min::STATIC);
                         break;
                 }
                 if (rc != sqlite_min::OK) throw std::runtime_error(std::string("bind: ") + sqlite3_errmsg(db));

@@ -21,11 +21,18 @@
 
 namespace dbw {
 
+// Text values are views: the caller keeps the bytes alive until wait()
+// returns (the Python wrapper holds the row tuples, whose str objects own
+// their UTF-8 buffers) -- no per-value copy on the producer side.
 struct Value {
     enum Kind : uint8_t { Null, Int, Real, Text } kind = Null;
-    int64_t i = 0;
-    double d = 0.0;
-    std::string s;
+    int32_t n = 0;
+    union {
+        int64_t i;
+        double d;
+        const char* p;
+    };
+    Value() : i(0) {}
 };
 
 // rows flattened row-major: values.size() == ncols * rows

@@ -16,19 +16,25 @@ namespace py = pybind11;
 
 namespace {
 
-// list of equal-length tuples of None / int / float / str -> one flattened
-// batch (CPython API directly: this runs with the GIL held, per value)
-dbw::Batch to_batch(const std::string& sql, py::list rows) {
+// sequence (list / tuple) of equal-length tuples of None / int / float / str
+// -> one flattened batch (CPython API directly, GIL held).  Text values are
+// views into the str objects' UTF-8 buffers: the caller keeps ``rows`` alive
+// (and unmodified) until the writer is done with them.
+dbw::Batch to_batch(const std::string& sql, py::handle rows) {
     dbw::Batch b;
     b.sql = sql;
-    const Py_ssize_t n = PyList_GET_SIZE(rows.ptr());
+    PyObject* seq = PySequence_Fast(rows.ptr(), "rows must be a sequence");
+    if (!seq) throw py::error_already_set();
+    py::object keep = py::reinterpret_steal<py::object>(seq);
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
     if (n == 0) return b;
-    PyObject* first = PyList_GET_ITEM(rows.ptr(), 0);
+    PyObject** items = PySequence_Fast_ITEMS(seq);
+    PyObject* first = items[0];
     if (!PyTuple_Check(first)) throw py::type_error("rows must be tuples");
     b.ncols = static_cast<int>(PyTuple_GET_SIZE(first));
     b.values.resize(static_cast<size_t>(n) * b.ncols);
     for (Py_ssize_t r = 0; r < n; ++r) {
-        PyObject* row = PyList_GET_ITEM(rows.ptr(), r);
+        PyObject* row = items[r];
         if (!PyTuple_Check(row) || PyTuple_GET_SIZE(row) != b.ncols) throw py::type_error("ragged rows");
         for (int c = 0; c < b.ncols; ++c) {
             PyObject* o = PyTuple_GET_ITEM(row, c);
@@ -40,7 +46,8 @@ dbw::Batch to_batch(const std::string& sql, py::list rows) {
                 const char* s = PyUnicode_AsUTF8AndSize(o, &len);
                 if (!s) throw py::error_already_set();
                 v.kind = dbw::Value::Text;
-                v.s.assign(s, static_cast<size_t>(len));
+                v.p = s;
+                v.n = static_cast<int32_t>(len);
             } else if (PyBool_Check(o) || PyLong_Check(o)) {
                 v.kind = dbw::Value::Int;
                 v.i = PyLong_AsLongLong(o);
@@ -331,17 +338,15 @@ PYBIND11_MODULE(_srcscan, m) {
                                 "One SQLite write transaction on a worker thread (see bulkwriter.hpp).")
         .def(py::init([](const std::string& path, int busy_timeout_ms, py::list setup) {
                  std::vector<dbw::Batch> stmts;
-                 for (auto item : setup) {
+                 for (auto item : setup) {  // (sql, rows): the caller keeps ``setup`` alive
                      auto tup = item.cast<py::tuple>();
-                     py::list one;
-                     one.append(tup[1]);
-                     stmts.push_back(to_batch(tup[0].cast<std::string>(), one));
+                     stmts.push_back(to_batch(tup[0].cast<std::string>(), tup[1]));
                  }
                  return new dbw::BulkWriter(path, busy_timeout_ms, std::move(stmts));
              }),
              py::arg("path"), py::arg("busy_timeout_ms"), py::arg("setup"))
         .def(
-            "put", [](dbw::BulkWriter& w, const std::string& sql, py::list rows) { w.put(to_batch(sql, rows)); },
+            "put", [](dbw::BulkWriter& w, const std::string& sql, py::handle rows) { w.put(to_batch(sql, rows)); },
             py::arg("sql"), py::arg("rows"))
         .def("commit", &dbw::BulkWriter::commit)
         .def("abort", &dbw::BulkWriter::abort, py::call_guard<py::gil_scoped_release>())

@@ -22,7 +22,7 @@ import re
 import uuid
 from dataclasses import dataclass, field
 from datetime import datetime, timezone
-from typing import FrozenSet, Iterable, List, NamedTuple, Optional
+from typing import FrozenSet, Iterable, List, NamedTuple, Optional, Tuple
 
 from ..utils.errors import (DomainError, require, require_non_blank,
                             require_non_negative, require_non_null)
@@ -358,6 +358,14 @@ class SourceClass:
                    package_name_of(full_class_name), class_type, description,
                    source_file, commit_hash, utc_now())
 
+    @classmethod
+    def reconstitute(cls, id: str, project_id: str, full_class_name: str, simple_name: str,
+                     package_name: Optional[str], class_type: ClassType, description: Optional[str],
+                     source_file: Optional[str], commit_hash: Optional[str],
+                     created_at: Optional[datetime]) -> "SourceClass":
+        return cls(id, project_id, full_class_name, simple_name, package_name, class_type,
+                   description, source_file, commit_hash, created_at)
+
     def belongs_to_package(self, pkg: Optional[str]) -> bool:
         if self.package_name is None or pkg is None:
             return False
@@ -370,8 +378,8 @@ class SourceMethod:
     class_id: str
     method_name: str
     description: Optional[str] = None
-    business_logic: List[str] = field(default_factory=list)
-    exceptions: List[str] = field(default_factory=list)
+    business_logic: Tuple[str, ...] = ()
+    exceptions: Tuple[str, ...] = ()
     http_method: Optional[str] = None
     http_path: Optional[str] = None
     line_number: Optional[int] = None
@@ -381,8 +389,9 @@ class SourceMethod:
         require_non_blank(self.id, "Method ID is required")
         require_non_blank(self.class_id, "Class ID is required")
         require_non_blank(self.method_name, "Method name is required")
-        self.business_logic = list(self.business_logic) if self.business_logic else []
-        self.exceptions = list(self.exceptions) if self.exceptions else []
+        # immutable copies (SourceMethod.java keeps List.copyOf views)
+        self.business_logic = tuple(self.business_logic) if self.business_logic else ()
+        self.exceptions = tuple(self.exceptions) if self.exceptions else ()
         if self.created_at is None:
             self.created_at = utc_now()
 
@@ -392,8 +401,16 @@ class SourceMethod:
                http_method: Optional[str], http_path: Optional[str],
                line_number: Optional[int]) -> "SourceMethod":
         return cls(new_id(), class_id, method_name, description,
-                   list(business_logic or []), list(exceptions or []),
+                   tuple(business_logic or ()), tuple(exceptions or ()),
                    http_method, http_path, line_number, utc_now())
+
+    @classmethod
+    def reconstitute(cls, id: str, class_id: str, method_name: str, description: Optional[str],
+                     business_logic: Optional[Iterable[str]], exceptions: Optional[Iterable[str]],
+                     http_method: Optional[str], http_path: Optional[str],
+                     line_number: Optional[int], created_at: Optional[datetime]) -> "SourceMethod":
+        return cls(id, class_id, method_name, description, tuple(business_logic or ()),
+                   tuple(exceptions or ()), http_method, http_path, line_number, created_at)
 
     def is_http_endpoint(self) -> bool:
         return self.http_method is not None and self.http_path is not None
@@ -423,6 +440,11 @@ class MethodParameter:
     @classmethod
     def create(cls, method_id: str, position: int, class_id: str) -> "MethodParameter":
         return cls(new_id(), method_id, position, class_id, utc_now())
+
+    @classmethod
+    def reconstitute(cls, id: str, method_id: str, position: int, class_id: str,
+                     created_at: Optional[datetime]) -> "MethodParameter":
+        return cls(id, method_id, position, class_id, created_at)
 
 
 class StaticMethodInfo(NamedTuple):

@@ -150,7 +150,7 @@ def test_source_class():
 def test_source_method_endpoint():
     m = SourceMethod.create("c1", "createUser", None, None, ["E"], "POST", "/users", 10)
     assert m.is_http_endpoint() and m.http_endpoint() == "POST /users"
-    assert m.business_logic == [] and m.exceptions == ["E"]
+    assert m.business_logic == () and m.exceptions == ("E",)
     n = SourceMethod.create("c1", "x", None, None, None, "GET", None, None)
     assert not n.is_http_endpoint() and n.http_endpoint() is None
     with pytest.raises(ValueError):

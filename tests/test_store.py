@@ -89,7 +89,7 @@ def test_class_method_param_repositories(repos):
     assert [m.id for m in repos.methods.find_http_endpoints_by_project_id(p.id)] == [m1.id]
     repos.methods.update_enrichment_batch([("creates", ["validate", "persist"], m1.id)])
     got = repos.methods.find_by_class_id_and_method_name(a.id, "create")
-    assert got.description == "creates" and got.business_logic == ["validate", "persist"] and got.exceptions == ["E"]
+    assert got.description == "creates" and list(got.business_logic) == ["validate", "persist"] and list(got.exceptions) == ["E"]
     assert repos.methods.find_by_class_name_and_method_name("co.acme.a.OrderService", "helper").id == m2.id
     grouped = repos.methods.find_by_class_ids([a.id, b.id])
     assert len(grouped[a.id]) == 3 and not grouped.get(b.id)

@@ -191,6 +191,7 @@ class SourceParser:
         self.framework_override = framework
         self.project: Optional[ParsedProject] = None
         self._root: Optional[str] = None
+        self._file_docs: Dict[str, dict] = {}
 
     # -- identity -------------------------------------------------------
     def language(self) -> str:
@@ -232,7 +233,12 @@ class SourceParser:
     def parse(self, project_root: str) -> ProjectGraph:
         return self.scan(project_root).build_graph()
 
-    # -- per-file hooks (answered from the cached scan) -------------------
+    # -- per-file hooks ----------------------------------------------------
+    # Answered from the cached project scan when the file is part of it (the
+    # indexing path); otherwise the file is analysed on its own by the native
+    # front-end (``scan_file``), so the hooks also work stand-alone like the
+    # reference's ``inferClassType(Path)`` / ``extractMethods(Path)`` /
+    # ``extractMethodParameters(Path, Path, Set)`` (JavaSourceParser.java:236-436).
     def _unit_for(self, file_path: str) -> Optional[ParsedUnit]:
         if self.project is None:
             return None
@@ -242,27 +248,88 @@ class SourceParser:
         ident = self.project.file_to_identifier.get(rel.replace(os.sep, "/"))
         return self.project.units.get(ident) if ident else None
 
+    def _file_doc(self, file_path: str) -> Optional[dict]:
+        """Native single-file analysis (cached per path) for files outside the scan."""
+        key = os.path.abspath(file_path)
+        doc = self._file_docs.get(key)
+        if doc is None:
+            if not os.path.isfile(key):
+                return None
+            rel = os.path.relpath(key, self._root) if self._root else os.path.basename(key)
+            doc = json.loads(native().scan_file(key, self.language_name, rel.replace(os.sep, "/"),
+                                                self.framework_override))
+            self._file_docs[key] = doc
+        return doc if doc.get("parsed", True) else None
+
     def infer_class_type(self, file_path: str) -> ClassType:
         u = self._unit_for(file_path)
-        return u.class_type if u else ClassType.OTHER
+        if u is not None:
+            return u.class_type
+        doc = self._file_doc(file_path)
+        return _class_type(doc.get("classType")) if doc else ClassType.OTHER
 
     def extract_methods(self, file_path: str) -> List[StaticMethodInfo]:
         u = self._unit_for(file_path)
-        return list(u.methods) if u else []
+        if u is not None:
+            return list(u.methods)
+        doc = self._file_doc(file_path)
+        return _methods_from(doc.get("methods") or ()) if doc else []
 
     def extract_method_parameters(self, file_path: str, source_root: Optional[str] = None,
                                   known_identifiers: Optional[Set[str]] = None) -> Dict[str, List[str]]:
+        """method name -> identifiers of its parameter types that are project
+        classes (methods without any are omitted; the last overload wins)."""
         u = self._unit_for(file_path)
-        if not u:
+        if u is not None:
+            if known_identifiers is None:
+                return {k: list(v) for k, v in u.params.items()}
+            return {k: [x for x in v if x in known_identifiers] for k, v in u.params.items()
+                    if any(x in known_identifiers for x in v)}
+        doc = self._file_doc(file_path)
+        if not doc:
             return {}
-        if known_identifiers is None:
-            return {k: list(v) for k, v in u.params.items()}
-        return {k: [x for x in v if x in known_identifiers] for k, v in u.params.items()
-                if any(x in known_identifiers for x in v)}
+        known = known_identifiers if known_identifiers is not None else set()
+        resolve = self._param_resolver(doc, file_path, source_root, known)
+        out: Dict[str, List[str]] = {}
+        for rp in doc.get("rawParams") or ():
+            if not rp.get("eligible", True):
+                continue
+            matched = [r for r in (resolve(t) for t in rp.get("types") or () if t) if r]
+            if matched:
+                out.pop(rp["name"], None)
+                out[rp["name"]] = matched
+        return out
+
+    def _param_resolver(self, doc: dict, file_path: str, source_root: Optional[str], known: Set[str]):
+        """Java ``resolveType`` (:505-530): known FQCN -> import map -> same package."""
+        imports: Dict[str, str] = {}
+        for imp in doc.get("imports") or ():
+            if imp.get("isAsterisk"):
+                continue
+            fq = imp.get("importedName") or ""
+            if imp.get("isStatic"):
+                fq = fq.rsplit(".", 1)[0] if "." in fq else ""
+            if "." in fq:
+                imports[fq.rsplit(".", 1)[1]] = fq
+        pkg = doc.get("package") or ""
+
+        def resolve(ty: str) -> Optional[str]:
+            if ty in known:
+                return ty
+            fq = imports.get(ty)
+            if fq is not None and fq in known:
+                return fq
+            if pkg and f"{pkg}.{ty}" in known:
+                return f"{pkg}.{ty}"
+            return None
+        return resolve
 
     def is_entry_point(self, file_path: str) -> bool:
         u = self._unit_for(file_path)
-        return bool(u and u.entry_point)
+        if u is not None:
+            return bool(u.entry_point)
+        doc = self._file_doc(file_path)
+        return bool(doc and doc.get("entryPoint"))
 
 
 class JavaSourceParser(SourceParser):

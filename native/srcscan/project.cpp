@@ -332,8 +332,9 @@ std::string scan_project_json(const std::string& root, const ScanOptions& opt) {
     return scan_result_json(scan_project(root, opt));
 }
 
-std::string scan_file_json(const std::string& path, const std::string& language, const std::string& rel_path,
-                           const std::string& framework) {
+namespace {
+std::string analyze_one_json(const std::string& path, const std::string* content, const std::string& language,
+                             const std::string& rel_path, const std::string& framework) {
     FileRec f;
     f.abs_path = path;
     f.rel_path = rel_path.empty() ? path : rel_path;
@@ -345,9 +346,11 @@ std::string scan_file_json(const std::string& path, const std::string& language,
         f.identifier = dotted(r);
     }
     std::string src;
-    if (read_file(path, src)) {
-        if (language == "java") analyze_java(src, f);
-        else analyze_ts(src, f.rel_path, framework.empty() ? "unknown" : framework, !ends_with(path, ".ts"), f);
+    const bool have = content != nullptr || read_file(path, src);
+    if (have) {
+        const std::string& text = content != nullptr ? *content : src;
+        if (language == "java") analyze_java(text, f);
+        else analyze_ts(text, f.rel_path, framework.empty() ? "unknown" : framework, !ends_with(path, ".ts"), f);
     }
     JsonWriter w;
     write_file(w, f);
@@ -381,6 +384,19 @@ std::string scan_file_json(const std::string& path, const std::string& language,
     out += x.out;
     out += "}";
     return out;
+}
+}  // namespace
+
+std::string scan_file_json(const std::string& path, const std::string& language, const std::string& rel_path,
+                           const std::string& framework) {
+    return analyze_one_json(path, nullptr, language, rel_path, framework);
+}
+
+std::string analyze_source_json(const std::string& content, const std::string& language, const std::string& file_path,
+                                const std::string& framework) {
+    // GraalJsAnalyzerEngine.analyzeFile(content, filePath, framework) parity:
+    // the path only names the unit (class-type filename table, Next.js routes)
+    return analyze_one_json(file_path, &content, language, file_path, framework);
 }
 
 }  // namespace srcscan

@@ -222,6 +222,19 @@ PYBIND11_MODULE(_srcscan, m) {
         },
         py::arg("path"), py::arg("language"), py::arg("rel") = "", py::arg("framework") = "");
     m.def(
+        "analyze_source",
+        [](const std::string& content, const std::string& language, const std::string& file_path,
+           const std::string& fw) {
+            std::string out;
+            {
+                py::gil_scoped_release release;
+                out = srcscan::analyze_source_json(content, language, file_path, fw);
+            }
+            return py::bytes(out);
+        },
+        py::arg("content"), py::arg("language"), py::arg("file_path"), py::arg("framework") = "unknown",
+        "analyse one in-memory source file (GraalJsAnalyzerEngine.analyzeFile parity)");
+    m.def(
         "analyze_go",
         [](const std::string& root, int threads) {
             std::string out;

@@ -98,6 +98,9 @@ std::string scan_result_json(const ScanResult& r);
 // Single-file analysis (tests / debugging); returns the FileRec as JSON.
 std::string scan_file_json(const std::string& path, const std::string& language,
                            const std::string& rel_path, const std::string& framework);
+// One in-memory source (no file read): ``file_path`` names the unit.
+std::string analyze_source_json(const std::string& content, const std::string& language, const std::string& file_path,
+                                const std::string& framework);
 
 std::string detect_language(const std::string& root);
 

@@ -350,6 +350,42 @@ class NodeJsSourceParser(SourceParser):
     def framework(self) -> Optional[dict]:
         return self.project.framework if self.project else None
 
+    def _param_resolver(self, doc: dict, file_path: str, source_root: Optional[str], known: Set[str]):
+        """NodeJsGraalParser ``extractMethodParameters`` / ``resolveImport``
+        (:302-336, :371-401): a parameter type names an import's local binding;
+        its relative module specifier resolves against the file's directory,
+        inside ``source_root``, to ``a.b.c`` or ``a.b.c.index``."""
+        root = os.path.abspath(source_root or os.path.join(self._root or os.path.dirname(file_path),
+                                                           self.source_root()))
+        here = os.path.dirname(os.path.abspath(file_path))
+        locals_: Dict[str, str] = {}
+        for imp in doc.get("imports") or ():
+            spec = imp.get("source") or ""
+            if not spec.startswith("."):
+                continue
+            full = os.path.normpath(os.path.join(here, spec))
+            if not full.startswith(root + os.sep):
+                continue
+            cand = os.path.relpath(full, root).replace(os.sep, ".")
+            for c in (cand, cand + ".index"):
+                if c in known:
+                    locals_[imp.get("localName") or ""] = c
+                    break
+        return locals_.get
+
+
+class LegacyNodeJsSourceParser(NodeJsSourceParser):
+    """The reference's unwired regex parser (``NodeJsSourceParser.java``,
+    SURVEY §2.4 #33) as a mode of the same native front-end: its extra rules
+    -- ``require('./x')`` dependencies, ``app.use(...)`` entry points -- are
+    already production behaviour here; what differs is that it recognised
+    NestJS ``@Get('/p')``-style verbs in any project (``:61-105, 304-377``),
+    whereas the Babel path needs ``framework == nestjs``.  This mode keeps
+    decorator routing on regardless of ``package.json``."""
+
+    def __init__(self, threads: int = 0) -> None:
+        super().__init__(threads, framework="nestjs")
+
 
 class GoSourceParser(SourceParser):
     language_name = "go"

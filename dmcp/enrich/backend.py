@@ -32,7 +32,8 @@ from typing import Callable, List, Optional, Sequence
 
 from ..utils.errors import require_non_blank, require_non_null
 from .jsonfix import parse_enrichment_response
-from .types import EnrichmentInput, EnrichmentResult
+from .types import (BatchClassInput, ClassAnalysisResult, EnrichmentInput, EnrichmentResult,
+                    MethodAnalysisResult)
 
 LOG = logging.getLogger(__name__)
 
@@ -247,22 +248,56 @@ class AnthropicBackend(EnrichmentBackend):
         raw = self._post(build_enrichment_prompt(inp, readme, self.max_source_chars))
         return parse_enrichment_response(raw, inp.full_class_name)
 
-    def analyze_class(self, source_code: str, full_class_name: str, source_file: str,
-                      readme: Optional[str], language: Optional[str]) -> dict:
-        """Legacy single-shot analysis (dead code in the reference)."""
+    def analyze_class(self, source_code: str, full_class_name: str, source_file: Optional[str],
+                      readme: Optional[str], language: Optional[str]) -> ClassAnalysisResult:
+        """Legacy single-shot analysis (``analyzeClass`` :164-209, dead code in
+        the reference): arguments are validated eagerly, a failed call or an
+        unparsable reply becomes a failure result."""
         require_non_blank(source_code, "Source code is required")
         require_non_blank(full_class_name, "Full class name is required")
-        from .jsonfix import loads_lenient
         prompt = ANALYSIS_PROMPT.format(language=language or "java",
                                         readme=readme or "No README available.",
                                         name=full_class_name, source=source_code)
         try:
-            root = loads_lenient(self._post(prompt))
-            return {"success": True, "fullClassName": full_class_name, "sourceFile": source_file,
-                    "result": root}
+            return parse_analysis_response(self._post(prompt), full_class_name, source_file)
         except Exception as e:
-            return {"success": False, "fullClassName": full_class_name, "sourceFile": source_file,
-                    "errorMessage": str(e)}
+            LOG.warning("Analysis failed for %s: %s", full_class_name, e)
+            return ClassAnalysisResult.failure(full_class_name, source_file, str(e))
+
+    def analyze_batch(self, inputs: Sequence[BatchClassInput], readme: Optional[str]
+                      ) -> List[ClassAnalysisResult]:
+        """``analyzeBatch`` (:223-275): one task per input, bounded fan-out,
+        results in input order, per-input failure isolation."""
+        require_non_null(inputs, "Inputs list is required")
+        if not inputs:
+            return []
+
+        def one(i: BatchClassInput) -> ClassAnalysisResult:
+            try:
+                return self.analyze_class(i.source_code, i.full_class_name, i.source_file, readme, i.language)
+            except Exception as e:
+                return ClassAnalysisResult.failure(i.full_class_name, i.source_file, str(e))
+        return list(self._executor().map(one, inputs))
+
+
+def parse_analysis_response(raw: str, full_class_name: str, source_file: Optional[str]) -> ClassAnalysisResult:
+    """Legacy reply ``{fullClassName, classType, description, sourceFile, methods[]}``."""
+    from .jsonfix import loads_lenient, parse_string_list
+    root = loads_lenient(raw)
+    if not isinstance(root, dict):
+        return ClassAnalysisResult.failure(full_class_name, source_file, "reply is not a JSON object")
+    methods = []
+    for m in root.get("methods") or ():
+        if not isinstance(m, dict) or not m.get("methodName"):
+            continue
+        ln = m.get("lineNumber")
+        methods.append(MethodAnalysisResult(
+            str(m["methodName"]), m.get("description"), parse_string_list(m.get("businessLogic")),
+            parse_string_list(m.get("exceptions")), m.get("httpMethod") or None, m.get("httpPath") or None,
+            int(ln) if isinstance(ln, (int, float)) else None))
+    return ClassAnalysisResult.ok(str(root.get("fullClassName") or full_class_name),
+                                  str(root.get("classType") or "OTHER"), root.get("description"),
+                                  root.get("sourceFile") or source_file, methods)
 
 
 def create_backend(cfg) -> EnrichmentBackend:

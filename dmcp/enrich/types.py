@@ -49,3 +49,44 @@ def normalize_method_name(name: Optional[str]) -> Optional[str]:
     if i > 0:
         return name[:i].strip()
     return name.strip()
+
+
+# -- legacy full-analysis DTOs (ClaudeApiClient.java:453-513, 750-810) --------
+@dataclass(frozen=True)
+class MethodAnalysisResult:
+    method_name: str
+    description: Optional[str]
+    business_logic: List[str] = field(default_factory=list)
+    exceptions: List[str] = field(default_factory=list)
+    http_method: Optional[str] = None
+    http_path: Optional[str] = None
+    line_number: Optional[int] = None
+
+
+@dataclass(frozen=True)
+class ClassAnalysisResult:
+    success: bool
+    full_class_name: str
+    class_type: str
+    description: Optional[str]
+    source_file: Optional[str]
+    methods: List[MethodAnalysisResult] = field(default_factory=list)
+    error_message: Optional[str] = None
+
+    @classmethod
+    def ok(cls, full_class_name: str, class_type: str, description: Optional[str],
+           source_file: Optional[str], methods: List[MethodAnalysisResult]) -> "ClassAnalysisResult":
+        return cls(True, full_class_name, class_type, description, source_file, list(methods or []), None)
+
+    @classmethod
+    def failure(cls, full_class_name: str, source_file: Optional[str],
+                error_message: Optional[str]) -> "ClassAnalysisResult":
+        return cls(False, full_class_name, "OTHER", None, source_file, [], error_message)
+
+
+@dataclass(frozen=True)
+class BatchClassInput:
+    source_code: str
+    full_class_name: str
+    source_file: str
+    language: str

@@ -182,7 +182,8 @@ def test_analyze_class_legacy(fake_api):
     _FakeAnthropic.script = [(200, {"content": [{"type": "text", "text": '{"classType": "SERVICE"}'}]})]
     be = AnthropicBackend("k", "m", base_url=fake_api, max_retries=0)
     out = be.analyze_class("class A {}", "co.a.A", "A.java", None, "java")
-    assert out["success"] and out["result"]["classType"] == "SERVICE"
+    assert out.success and out.class_type == "SERVICE" and out.full_class_name == "co.a.A"
+    assert out.source_file == "A.java" and out.methods == []
 
 
 def test_create_backend_selection():
@@ -197,3 +198,13 @@ def test_result_factories():
     assert ok.success and ok.error_message is None
     bad = EnrichmentResult.failure("a.B", "why")
     assert not bad.success and bad.methods == []
+
+
+def test_analyze_batch_legacy_fans_out_in_input_order(fake_api):
+    from dmcp.enrich.types import BatchClassInput
+    be = AnthropicBackend("k", "m", base_url=fake_api, max_retries=0, max_concurrent=3)
+    ins = [BatchClassInput(f"class C{i} {{}}", f"co.a.C{i}", f"C{i}.java", "java") for i in range(5)]
+    out = be.analyze_batch(ins, "readme")
+    assert [r.full_class_name for r in out] == [i.full_class_name for i in ins]
+    assert all(r.success for r in out) and len(_FakeAnthropic.seen) == 5
+    be.close()

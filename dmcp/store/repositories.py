@@ -329,6 +329,11 @@ class SourceClassRepository:
                 c.execute(f"DELETE FROM source_classes WHERE id IN ({','.join('?' * len(chunk))})",
                           chunk)
 
+    def delete(self, class_id: str) -> None:
+        """One class; its methods and parameter links go with it (FK cascade)."""
+        with self.db.transaction() as c:
+            c.execute("DELETE FROM source_classes WHERE id = ?", (class_id,))
+
     def find_unenriched_by_project_id(self, project_id: str) -> List[SourceClass]:
         return [self._map(r) for r in self.db.query(self.FIND_UNENRICHED_BY_PROJECT_ID, (project_id,))]
 
@@ -449,6 +454,10 @@ class SourceMethodRepository:
     def delete_by_class_id(self, class_id: str) -> None:
         with self.db.transaction() as c:
             c.execute("DELETE FROM source_methods WHERE class_id = ?", (class_id,))
+
+    def delete(self, method_id: str) -> None:
+        with self.db.transaction() as c:
+            c.execute("DELETE FROM source_methods WHERE id = ?", (method_id,))
 
     DELETE_BY_PROJECT_ID = ("DELETE FROM source_methods WHERE class_id IN "
                             "(SELECT id FROM source_classes WHERE project_id = ?)")

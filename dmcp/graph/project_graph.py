@@ -30,6 +30,18 @@ from ..utils.errors import require_non_blank, require_non_negative
 
 GRAPH_JSON_VERSION = 2
 
+_ENCODER: list = []
+
+
+def _native_encoder():
+    if not _ENCODER:
+        try:
+            from .. import _srcscan  # type: ignore
+            _ENCODER.append(getattr(_srcscan, "graph_json", None))
+        except ImportError:
+            _ENCODER.append(None)
+    return _ENCODER[0]
+
 
 # Value records are NamedTuples: immutable, hashable and ~5x cheaper to build
 # than frozen dataclasses on the indexing hot path (10^4-10^5 per project).
@@ -385,6 +397,16 @@ class ProjectGraph:
         }
 
     def to_json(self) -> str:
+        """Compact JSON; written natively straight from the graph's containers
+        (``_srcscan.graph_json``, byte-identical) when the extension is built,
+        else through :meth:`to_dict` + ``json.dumps``."""
+        enc = _native_encoder()
+        if enc is not None:
+            try:
+                return enc(GRAPH_JSON_VERSION, self._nodes, self._class_ids, self._out, self._entry,
+                           self._mparams, self._node_info, self._method_info)
+            except TypeError:
+                pass  # an unexpected value type: the generic encoder handles (or rejects) it
         return json.dumps(self.to_dict(), separators=(",", ":"), ensure_ascii=False)
 
     @classmethod

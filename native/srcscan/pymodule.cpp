@@ -10,6 +10,7 @@
 
 #include "bulkwriter.hpp"
 #include "gitobj.hpp"
+#include "graphjson.hpp"
 #include "srcscan.hpp"
 
 namespace py = pybind11;
@@ -221,6 +222,22 @@ PYBIND11_MODULE(_srcscan, m) {
             return py::bytes(out);
         },
         py::arg("path"), py::arg("language"), py::arg("rel") = "", py::arg("framework") = "");
+    m.def(
+        "graph_json",
+        [](long version, py::handle nodes, py::handle class_ids, py::handle out, py::handle entry,
+           py::handle mparams, py::handle node_info, py::handle method_info) {
+            graphjson::Writer w;
+            try {
+                graphjson::write_graph(w, version, nodes.ptr(), class_ids.ptr(), out.ptr(), entry.ptr(),
+                                       mparams.ptr(), node_info.ptr(), method_info.ptr());
+            } catch (const graphjson::TypeError& e) {
+                throw py::type_error(e.what());
+            }
+            PyObject* r = PyUnicode_DecodeUTF8(w.s.data(), static_cast<Py_ssize_t>(w.s.size()), "strict");
+            if (!r) throw py::error_already_set();
+            return py::reinterpret_steal<py::object>(r);
+        },
+        "ProjectGraph JSON from its containers (byte-identical to the json.dumps path)");
     m.def(
         "analyze_source",
         [](const std::string& content, const std::string& language, const std::string& file_path,

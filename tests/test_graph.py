@@ -234,3 +234,35 @@ def test_load_static_metadata_equals_per_call_api():
                             infos, params)
     assert g1.to_dict() == g2.to_dict()
     assert [(l.position, l.target_identifier) for l in g2.method_parameters("a.A")["run"]] == [(0, "a.B"), (2, "a.C")]
+
+
+def test_native_json_encoder_is_byte_identical_to_json_dumps():
+    """``_srcscan.graph_json`` (native/srcscan/graphjson.hpp) vs the dict + json.dumps path,
+    including escapes, non-ASCII, empty strings and absent optional fields."""
+    from dmcp.graph import project_graph as pg
+    assert pg._native_encoder() is not None, "native encoder must be built"
+    g = ProjectGraph()
+    odd = 'a"\\\n\x01é  '
+    g.add_node(odd, "f\t.java")
+    g.add_node("b", "b.java")
+    g.add_node("c", "c.java")
+    g.add_dependency(odd, "b")
+    g.add_dependency("b", "c")
+    g.mark_as_entry_point("b")
+    g.bind_class_id("b", "cid")
+    g.add_method_parameter("b", "m", 0, odd)
+    g.add_method_parameter("b", "m", 3, "c")
+    g.set_node_info("b", None, "d\x1f")
+    g.set_node_info(odd, "SERVICE", None)
+    g.add_method_info("b", MethodInfo("m", "", ("x", "y\"z"), (), "GET", "/p", 0))
+    g.add_method_info("b", MethodInfo("n", None, [], ["E"], None, None, None))
+    for graph in (g, ProjectGraph()):
+        assert graph.to_json() == json.dumps(graph.to_dict(), separators=(",", ":"), ensure_ascii=False)
+        assert ProjectGraph.from_json(graph.to_json()).to_dict() == graph.to_dict()
+
+
+def test_native_json_encoder_falls_back_on_unexpected_types():
+    g = ProjectGraph()
+    g.add_node("a", "a.java")
+    g.add_method_info("a", MethodInfo("m", line_number=3.5))  # float line: not an int
+    assert json.loads(g.to_json())["methodInfo"]["a"][0]["lineNumber"] == 3.5

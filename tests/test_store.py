@@ -117,6 +117,12 @@ def test_bulk_replace_keeps_referential_integrity(tmp_path):
     n = app.db.query_one("SELECT COUNT(*) FROM method_parameters p JOIN source_methods m ON m.id = p.method_id "
                          "JOIN source_classes c ON c.id = p.class_id WHERE c.project_id = ?", (r.project_id,))[0]
     assert n == app.db.query_one("SELECT COUNT(*) FROM method_parameters")[0] > 0
+    # the invariant MethodParameterRepository.DELETE_BY_PROJECT_ID relies on:
+    # a link's owning method and its target class belong to the same project
+    assert app.db.query_one(
+        "SELECT COUNT(*) FROM method_parameters p JOIN source_methods m ON m.id = p.method_id "
+        "JOIN source_classes owner ON owner.id = m.class_id JOIN source_classes t ON t.id = p.class_id "
+        "WHERE owner.project_id <> t.project_id")[0] == 0
     app.close()
 
 

@@ -705,6 +705,214 @@ __global__ __launch_bounds__(kBlock) void embedding_kernel(const uint16_t* __res
     }
 }
 
+// --------------------------------------------------------------------------
+// 3c. per-row decode attention on the matrix cores (the default).
+//    Same work items, outputs and partial layout as decode_attn_kernel (so
+//    the prefix kernel and the combine are shared), but ONE WAVE per item and
+//    both products on MFMA 16x16x32 bf16 per 32-key tile:
+//        S^T[key, q] = K[key, :] . Q^T[:, q]      A = K rows straight from HBM
+//                                                  (16 B per lane), B = Q^T
+//        O^T[d, q]  += V^T[d, key] . P^T[key, q]  A = V^T read transposed out
+//                                                  of the wave's LDS tile with
+//                                                  ds_read_b64_tr_b16, B = P^T
+//    The G query heads of the kv head are the MFMA's N columns (padded to
+//    16).  S^T leaves the query on the lane and 8 keys in registers, so the
+//    online softmax is in-register + 2 cross-group shuffles per tile, and P^T
+//    is the PV B operand with no data movement: the PV k order is the
+//    permutation {4g..4g+3, 16+4g..16+4g+3} of lane group g, matched by the
+//    two transposed V reads (rows 4g.. and 16+4g..).  The VALU kernel spent
+//    ~400 VALU instructions per 32 keys per wave (dot products, 48 shuffles,
+//    exp2 per head per key); here a tile is 8 MFMAs, 8 exp2, ~20 VALU and
+//    2 shuffles, and the next tile's K/V loads are in flight meanwhile.
+//    No block-level synchronisation: each wave owns its LDS tile, so
+//    different waves of a block run different items.
+// --------------------------------------------------------------------------
+typedef short v4i16_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+// K rows (S^T A operand: key kt + 16h + (lane&15), dims 32ks + 8*(lane>>4))
+// and the V tile as 16-B row chunks, keys clamped to end-1 (masked later)
+template <int D>
+__device__ __forceinline__ void load_kv_tile(const uint16_t* __restrict__ kb, const uint16_t* __restrict__ vb,
+                                             int kt, int end, int lane, uint4 (&kr)[2][D / 32],
+                                             uint4 (&vr)[D / 16]) {
+    constexpr int CPK = D / 8;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int key = min(kt + 16 * h + (lane & 15), end - 1);
+#pragma unroll
+        for (int ks = 0; ks < D / 32; ++ks)
+            kr[h][ks] = *reinterpret_cast<const uint4*>(kb + (size_t)key * D + 32 * ks + 8 * (lane >> 4));
+    }
+#pragma unroll
+    for (int r = 0; r < D / 16; ++r) {
+        const int ch = lane + kWave * r;
+        const int key = min(kt + ch / CPK, end - 1);
+        vr[r] = *reinterpret_cast<const uint4*>(vb + (size_t)key * D + (ch % CPK) * 8);
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache,
+    const int32_t* __restrict__ slot, const int32_t* __restrict__ seq_len, uint16_t* __restrict__ out,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int B, int Hkv, int G,
+    int max_seq, int chunk, int splits, float scale_log2, int num_slots, const int32_t* __restrict__ plen,
+    int ps_max) {
+    static_assert(D % 32 == 0, "D must be a multiple of 32");
+    constexpr int KS = D / 32;    // 32-dim k-steps of the S product
+    constexpr int DB = D / 16;    // 16-row d blocks of O^T
+    constexpr int VCH = D / 16;   // 16-B V chunks per lane per 32-key tile
+    constexpr int CPK = D / 8;    // 16-B chunks per key row
+    constexpr int VROW = D + 8;   // LDS row stride in bf16 (144 B at D=64: conflict-light tr reads)
+    constexpr int NW = kBlock / kWave;
+    __shared__ __attribute__((aligned(16))) uint16_t vlds[NW][32 * VROW];
+    const int lane = threadIdx.x & (kWave - 1);
+    // wave index made provably uniform: the item loop, its bounds and the
+    // slot / seq_len reads stay scalar (no exec-masked control flow, which
+    // ds_read_b64_tr_b16 must not run under, and no scratch)
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int g16 = lane >> 4, c = lane & 15;
+    const int Hq = Hkv * G;
+    const int P = __builtin_amdgcn_readfirstlane(plen ? max(0, *plen) : 0);
+    const int splits_total = ps_max + splits;
+    const int per_split = B * Hkv;
+    const int total = splits * per_split;
+    uint16_t* vw = vlds[wave];
+    // transposed-read addresses (tile-invariant): lane 4q+p of group g16 reads
+    // row 4*g16 + q (and 16 + ...), columns 4p..4p+3 of each 16-wide d block
+    const uint16_t* tr0 = vw + (4 * g16 + (c >> 2)) * VROW + 4 * (c & 3);
+    const uint16_t* tr1 = tr0 + 16 * VROW;
+    for (int item = blockIdx.x * NW + wave; item < total; item += gridDim.x * NW) {
+        const int split = item / per_split;
+        const int rem = item - split * per_split;
+        const int b = rem / Hkv, kh = rem - b * Hkv;
+        const int s = __builtin_amdgcn_readfirstlane(slot[b]);
+        const int L = __builtin_amdgcn_readfirstlane((s >= 0 && s < num_slots) ? min(seq_len[b], max_seq) : 0);
+        const int Ls = L - P;
+        const int nact = Ls > 0 ? min(splits, (Ls + chunk - 1) / chunk) : 0;
+        if (L <= 0) {  // padding row / bad slot: defined output, nothing read
+            if (split == 0)
+                for (int o = lane; o < G * D; o += kWave) out[((size_t)b * Hq + kh * G) * D + o] = 0;
+            continue;
+        }
+        if (split >= nact) continue;
+        const bool direct = P == 0 && nact == 1;
+        const int start = P + split * chunk;
+        const int end = min(L, start + chunk);
+        const int ntiles = (end - start + 31) / 32;
+        bf16x8_t qf[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (c < G) v = *reinterpret_cast<const uint4*>(q + ((size_t)b * Hq + kh * G + c) * D + 32 * ks + 8 * g16);
+            qf[ks] = as_bf16x8(v);
+        }
+        const size_t head_off = ((size_t)s * Hkv + kh) * (size_t)max_seq * D;
+        const uint16_t* kb = k_cache + head_off;
+        const uint16_t* vb = v_cache + head_off;
+        uint4 kr[2][KS], vr[VCH];
+        float m = -1e30f, l = 0.f;
+        f32x4_t acc[DB];
+#pragma unroll
+        for (int db = 0; db < DB; ++db) acc[db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        load_kv_tile<D>(kb, vb, start, end, lane, kr, vr);
+        for (int t = 0; t < ntiles; ++t) {
+            const int kt = start + 32 * t;
+            // the wave's V tile -> LDS, row-major [key][d]
+#pragma unroll
+            for (int r = 0; r < VCH; ++r) {
+                const int ch = lane + kWave * r;
+                *reinterpret_cast<uint4*>(vw + (ch / CPK) * VROW + (ch % CPK) * 8) = vr[r];
+            }
+            f32x4_t sacc[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                sacc[h] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks)
+                    sacc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(kr[h][ks]), qf[ks], sacc[h], 0, 0, 0);
+            }
+            if (t + 1 < ntiles) load_kv_tile<D>(kb, vb, kt + 32, end, lane, kr, vr);  // in flight during softmax + PV
+            // S^T tile: register 4h+i = key kt + 16h + 4*g16 + i of query c.
+            // Scale folded into one FMA per score; the key mask only on a
+            // partial last tile; hardware exp2 and bf16 packing.
+            float sv[8];
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) sv[4 * h + i] = sacc[h][i];
+            float tmax = -1e30f;
+            if (kt + 32 <= end) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) tmax = fmaxf(tmax, sv[j]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int key = kt + 16 * (j >> 2) + 4 * g16 + (j & 3);
+                    sv[j] = key < end ? sv[j] : -1e30f;
+                    tmax = fmaxf(tmax, sv[j]);
+                }
+            }
+            tmax = fmaxf(tmax, __shfl_xor(tmax, 16, kWave));
+            tmax = fmaxf(tmax, __shfl_xor(tmax, 32, kWave)) * scale_log2;
+            const float mn = fmaxf(m, tmax);
+            if (__any(mn > m)) {
+                const float corr = __builtin_amdgcn_exp2f(m - mn);
+                l *= corr;
+#pragma unroll
+                for (int db = 0; db < DB; ++db) acc[db] *= corr;
+            }
+            m = mn;
+            f32x8_t pr;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                pr[j] = __builtin_amdgcn_exp2f(fmaf(sv[j], scale_log2, -mn));
+                l += pr[j];  // lane-partial sum; the 4 groups are added once at the end
+            }
+            // B operand P^T: element j = key pi(8*g16 + j) = 16*(j>>2) + 4*g16 + (j&3)
+            const bf16x8_t pf = __builtin_convertvector(pr, bf16x8_t);
+#pragma unroll
+            for (int db = 0; db < DB; ++db) {
+                const v4i16_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) v4i16_t*)(tr0 + 16 * db));
+                const v4i16_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) v4i16_t*)(tr1 + 16 * db));
+                const uint4 a = make_uint4((uint32_t)(uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16),
+                                           (uint32_t)(uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16),
+                                           (uint32_t)(uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16),
+                                           (uint32_t)(uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16));
+                acc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), pf, acc[db], 0, 0, 0);
+            }
+        }
+        l += __shfl_xor(l, 16, kWave);
+        l += __shfl_xor(l, 32, kWave);
+        if (c < G) {
+            const int qh = kh * G + c;
+            const float inv = l > 0.f ? 1.f / l : 0.f;
+            const size_t pi = ((size_t)b * Hq + qh) * splits_total + ps_max + split;
+#pragma unroll
+            for (int db = 0; db < DB; ++db) {
+                const int d0 = 16 * db + 4 * g16;
+                if (direct) {
+                    const float f[4] = {acc[db][0] * inv, acc[db][1] * inv, acc[db][2] * inv, acc[db][3] * inv};
+                    *reinterpret_cast<uint2*>(out + ((size_t)b * Hq + qh) * D + d0) = pack4(f);
+                } else {
+                    *reinterpret_cast<float4*>(part_o + pi * D + d0) =
+                        make_float4(acc[db][0], acc[db][1], acc[db][2], acc[db][3]);
+                }
+            }
+            if (!direct && g16 == 0) {
+                part_ml[pi * 2] = m;
+                part_ml[pi * 2 + 1] = l;
+            }
+        }
+    }
+}
+
+// 0 = MFMA per-row kernel (default), 1 = VALU kernel (A/B and fallback)
+int g_decode_impl = 0;
+
 // CUs of the current device (cached per device; 256 on MI355X)
 inline int device_cu_count() {
     static int cached[64] = {0};
@@ -749,7 +957,14 @@ hipError_t launch_decode_d(int G, dim3 grid, const uint16_t* q, const uint16_t* 
 
 extern "C" {
 
-int dmcp_abi_version() { return 5; }
+int dmcp_abi_version() { return 6; }
+
+// Selects the per-row decode attention kernel (0 = MFMA, 1 = VALU); returns the previous choice.
+int dmcp_set_decode_impl(int impl) {
+    const int prev = g_decode_impl;
+    if (impl == 0 || impl == 1) g_decode_impl = impl;
+    return prev;
+}
 
 int dmcp_add_rmsnorm(const void* x, void* residual, const void* w, void* out, int rows, int H, float eps,
                      void* stream) {
@@ -819,10 +1034,30 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
     // persistent grid: enough blocks to fill every CU a few times over, never
     // more than there are work items
     const long items = (long)splits * Hkv * B;
-    dim3 grid((unsigned)(items < cap ? items : cap));
     auto kk = (const uint16_t*)k_cache;
     auto vv = (const uint16_t*)v_cache;
     hipError_t e;
+    if (g_decode_impl == 0 && (D == 64 || D == 128) && G <= 16) {
+        // one wave per item: a block runs 4 items
+        const long wblocks = (items + 3) / 4;
+        dim3 wgrid((unsigned)(wblocks < cap ? wblocks : cap));
+        if (D == 64)
+            decode_attn_mfma_kernel<64><<<wgrid, kBlock, 0, st>>>(qq, kk, vv, sl, ln, (uint16_t*)out, (float*)part_o,
+                                                                 (float*)part_ml, B, Hkv, G, max_seq, chunk, splits,
+                                                                 sl2, num_slots, pl, ps_max);
+        else
+            decode_attn_mfma_kernel<128><<<wgrid, kBlock, 0, st>>>(qq, kk, vv, sl, ln, (uint16_t*)out,
+                                                                  (float*)part_o, (float*)part_ml, B, Hkv, G, max_seq,
+                                                                  chunk, splits, sl2, num_slots, pl, ps_max);
+        e = hipGetLastError();
+        if (e != hipSuccess || (splits == 1 && !prefix)) return e;
+        decode_attn_combine_kernel<<<dim3(Hkv, B), kBlock, 0, st>>>((const float*)part_o, (const float*)part_ml, sl,
+                                                                   ln, (uint16_t*)out, Hkv, G, D, max_seq, chunk,
+                                                                   splits, num_slots, pl, ps_max,
+                                                                   prefix ? pchunk : 1);
+        return hipGetLastError();
+    }
+    dim3 grid((unsigned)(items < cap ? items : cap));
     if (D == 64)
         e = launch_decode_d<64>(G, grid, qq, kk, vv, sl, ln, (uint16_t*)out, (float*)part_o, (float*)part_ml, B,
                                 Hkv, max_seq, chunk, splits, sl2, num_slots, pl, ps_max, st);

@@ -26,7 +26,7 @@ _lock = threading.Lock()
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _f = ctypes.c_float
-ABI_VERSION = 5  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
+ABI_VERSION = 6  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
 
 
 class HipOpsError(RuntimeError):
@@ -56,6 +56,7 @@ def lib() -> ctypes.CDLL:
             "dmcp_silu_mul": ([_vp, _vp, _i, _i, _vp], _i),
             "dmcp_masked_argmax": ([_vp, _vp, _vp, _i, _vp, _i, _i, _i, _vp], _i),
             "dmcp_embedding": ([_vp, _vp, _vp, _i, _i, _i, _vp], _i),
+            "dmcp_set_decode_impl": ([_i], _i),
         }
         for name, (args, res) in sigs.items():
             fn = getattr(L, name)
@@ -63,8 +64,24 @@ def lib() -> ctypes.CDLL:
             fn.restype = res
         if L.dmcp_abi_version() != ABI_VERSION:
             raise HipOpsError("HIP kernel library ABI mismatch; rebuild with python -m dmcp.ops.build")
+        impl = os.environ.get("DMCP_DECODE_IMPL", "mfma").lower()
+        L.dmcp_set_decode_impl(DECODE_IMPLS.get(impl, 0))
         _lib = L
         return _lib
+
+
+DECODE_IMPLS = {"mfma": 0, "valu": 1}
+
+
+def set_decode_impl(name: str) -> str:
+    """Per-row decode attention kernel: ``mfma`` (default; matrix cores, one
+    wave per work item) or ``valu`` (the previous VALU kernel, kept for A/B
+    runs and as a reference).  Returns the previous choice.  Takes effect at
+    the next launch (re-capture hipGraphs after switching)."""
+    if name not in DECODE_IMPLS:
+        raise ValueError(f"decode impl must be one of {sorted(DECODE_IMPLS)}")
+    prev = lib().dmcp_set_decode_impl(DECODE_IMPLS[name])
+    return {v: k for k, v in DECODE_IMPLS.items()}[prev]
 
 
 def loaded_path() -> Optional[str]:

@@ -154,6 +154,11 @@ def main() -> int:
     if only == "prefix8k":  # one case, for counter collection
         bench_prefix_attention(80, 8000, 100, max_seq=8192)
         return 0
+    if only == "suffix":  # split size for the enrichment's short own-key suffixes
+        for Ls in (300, 600, 900, 1500):
+            for chunk in (256, 512, 1024):
+                bench_prefix_attention(80, 4151, Ls, chunk=chunk)
+        return 0
     if only in ("", "prefix"):
         bench_prefix_attention(80, 4151, 2500)
         bench_prefix_attention(256, 4151, 2500)

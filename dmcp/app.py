@@ -29,6 +29,23 @@ from .utils.runtime import tune_gc
 LOG = logging.getLogger(__name__)
 
 
+class _StderrHandler(logging.StreamHandler):
+    """Writes to whatever ``sys.stderr`` is at emit time (a redirected or
+    replaced stderr -- test capture, daemonisation -- never sees writes to a
+    stale, closed stream)."""
+
+    def __init__(self) -> None:
+        super().__init__(sys.stderr)
+
+    @property  # type: ignore[override]
+    def stream(self):
+        return sys.stderr
+
+    @stream.setter
+    def stream(self, _value) -> None:
+        pass
+
+
 def configure_logging(level: str = "INFO", stream=None) -> None:
     """All logs go to stderr so stdout stays pure JSON-RPC in MCP mode
     (``logback-spring.xml:14-26``)."""
@@ -36,7 +53,7 @@ def configure_logging(level: str = "INFO", stream=None) -> None:
     if getattr(configure_logging, "_done", False):
         root.setLevel(level.upper())
         return
-    h = logging.StreamHandler(stream or sys.stderr)
+    h = logging.StreamHandler(stream) if stream is not None else _StderrHandler()
     h.setFormatter(logging.Formatter("%(asctime)s [%(threadName)s] %(levelname)-5s %(name)s - %(message)s",
                                      "%H:%M:%S"))
     root.handlers[:] = [h]

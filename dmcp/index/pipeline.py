@@ -179,7 +179,11 @@ class Indexer:
         stats: Dict[str, float] = {}
         clone: Optional[SourceTree] = None
         writer: Optional[ProjectRowsWriter] = None
-        project = self._prepare_project(url, branch_name)
+        try:
+            project = self._prepare_project(url, branch_name)
+        except BaseException:
+            lock.release()  # a failed status write must not leave the repository locked
+            raise
         try:
             with span("analyze.total", stats, project=project.name):
                 with span("analyze.clone", stats):

@@ -62,8 +62,8 @@ class CronExpression:
         self.days = _field(parts[3], 1, 31)
         self.months = _field(parts[4], 1, 12, _MONTHS)
         self.dow_any = parts[5] in ("*", "?")
-        dows = _field(parts[5].replace("7", "0") if parts[5] != "*" else parts[5], 0, 7, _DAYS)
-        self.dows = {d % 7 for d in dows}
+        # 0 and 7 are both Sunday; ranges such as 1-7 / 5-7 stay valid (Spring accepts them)
+        self.dows = {d % 7 for d in _field(parts[5], 0, 7, _DAYS)}
 
     def _day_ok(self, t: datetime) -> bool:
         dow = (t.weekday() + 1) % 7  # Sunday = 0

@@ -110,6 +110,15 @@ def _req(t: torch.Tensor, dtype: torch.dtype, name: str) -> None:
         raise HipOpsError(f"{name}: tensor must be contiguous")
 
 
+def _req_out(t: torch.Tensor, dtype: torch.dtype, numel: int, name: str) -> None:
+    """A caller-supplied output buffer: same checks as :func:`_req` plus room
+    for the ``numel`` elements the kernel writes (an undersized buffer would be
+    an out-of-bounds device write)."""
+    _req(t, dtype, name)
+    if t.numel() < numel:
+        raise HipOpsError(f"{name}: buffer holds {t.numel()} elements, the kernel writes {numel}")
+
+
 # ---------------------------------------------------------------- wrappers
 def add_rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -124,7 +133,7 @@ def add_rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float, residual: Opt
         if residual.shape != x.shape:
             raise HipOpsError("add_rmsnorm: residual shape mismatch")
     out = torch.empty_like(x) if out is None else out
-    _req(out, torch.bfloat16, "add_rmsnorm.out")
+    _req_out(out, torch.bfloat16, rows * H, "add_rmsnorm.out")
     if rows == 0:
         return out
     _check(lib().dmcp_add_rmsnorm(_ptr(x), _ptr(residual), _ptr(weight), _ptr(out), rows, H, float(eps), _stream()),
@@ -153,7 +162,7 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos_sin: t
     max_pos = cos_sin.shape[0]
     if q_out is None:
         q_out = torch.empty((T, n_q_heads, D), dtype=torch.bfloat16, device=qkv.device)
-    _req(q_out, torch.bfloat16, "rope_kv.q_out")
+    _req_out(q_out, torch.bfloat16, T * n_q_heads * D, "rope_kv.q_out")
     _check(lib().dmcp_rope_kv(_ptr(qkv), _ptr(pos), _ptr(slot), _ptr(cos_sin), _ptr(q_out), _ptr(k_cache),
                               _ptr(v_cache), T, n_q_heads, Hkv, D, MAXS, max_pos, S, _stream()), "dmcp_rope_kv")
     return q_out
@@ -213,7 +222,7 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
                               f"{pchunk} do not match kv {tuple(k_cache.shape)}")
         ps_max = prefix_splits(ldv, pchunk)
     out = torch.empty_like(q) if out is None else out
-    _req(out, torch.bfloat16, "decode_attention.out")
+    _req_out(out, torch.bfloat16, B * Hq * D, "decode_attention.out")
     if splits > 1 or ps_max:
         if workspace is None:
             workspace = decode_workspace(B, Hq, Hkv, D, MAXS, q.device, chunk, ps_max)
@@ -256,7 +265,7 @@ def silu_mul(gate_up: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch
     I = I2 // 2
     if out is None:
         out = torch.empty((*gate_up.shape[:-1], I), dtype=torch.bfloat16, device=gate_up.device)
-    _req(out, torch.bfloat16, "silu_mul.out")
+    _req_out(out, torch.bfloat16, T * I, "silu_mul.out")
     _check(lib().dmcp_silu_mul(_ptr(gate_up), _ptr(out), T, I, _stream()), "dmcp_silu_mul")
     return out
 
@@ -286,7 +295,7 @@ def masked_argmax(logits: torch.Tensor, mask: Optional[torch.Tensor] = None, voc
     elif mask_idx is not None:
         raise HipOpsError("masked_argmax: mask_idx given without a mask table")
     out = torch.empty((B,), dtype=torch.int32, device=logits.device) if out is None else out
-    _req(out, torch.int32, "masked_argmax.out")
+    _req_out(out, torch.int32, B, "masked_argmax.out")
     _check(lib().dmcp_masked_argmax(_ptr(logits), _ptr(mask), _ptr(mask_idx if mask is not None else None), n_masks,
                                     _ptr(out), B, V, ld, _stream()), "dmcp_masked_argmax")
     return out
@@ -300,6 +309,6 @@ def embedding(table: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor
         raise HipOpsError("embedding: hidden size must be a multiple of 8")
     T = ids.numel()
     out = torch.empty((T, H), dtype=torch.bfloat16, device=table.device) if out is None else out
-    _req(out, torch.bfloat16, "embedding.out")
+    _req_out(out, torch.bfloat16, T * H, "embedding.out")
     _check(lib().dmcp_embedding(_ptr(table), _ptr(ids), _ptr(out), T, H, V, _stream()), "dmcp_embedding")
     return out

@@ -22,10 +22,11 @@ from __future__ import annotations
 
 import json
 from datetime import datetime, timezone
-from typing import Dict, Iterable, List, Optional, Sequence
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
 from ..models.domain import (ClassType, MethodParameter, Project, ProjectStatus,
                              RepositoryUrl, SourceClass, SourceMethod)
+from ..utils.errors import DomainError
 from .db import Database
 
 _CHUNK = 500  # SQLite host-parameter limit is 999 on older builds
@@ -495,13 +496,42 @@ class MethodParameterRepository:
 
     def save(self, p: MethodParameter) -> None:
         with self.db.transaction() as c:
+            self._check_same_project(c, [(p.method_id, p.class_id)])
             c.execute(self._INSERT, self._params(p))
 
     def save_all(self, params: Sequence[MethodParameter]) -> None:
         if not params:
             return
         with self.db.transaction() as c:
+            self._check_same_project(c, [(p.method_id, p.class_id) for p in params])
             c.executemany(self._INSERT, [self._params(p) for p in params])
+
+    @staticmethod
+    def _check_same_project(c, links: Sequence[Tuple[str, str]]) -> None:
+        """Rejects a link whose method and parameter class live in different
+        projects.  The project-scoped delete (:attr:`DELETE_BY_PROJECT_ID`)
+        selects links by their target class only, which is exact only under
+        this invariant; the analysis paths satisfy it by construction (targets
+        are resolved among the project's own classes) and write through
+        :meth:`save_rows`.  Unknown ids are left to the foreign keys."""
+        method_ids = list({m for m, _ in links})
+        class_ids = list({k for _, k in links})
+        owner: Dict[str, str] = {}
+        for chunk in _chunks(method_ids):
+            for mid, pid in c.execute(
+                    "SELECT m.id, k.project_id FROM source_methods m JOIN source_classes k ON k.id = m.class_id "
+                    f"WHERE m.id IN ({','.join('?' * len(chunk))})", chunk):
+                owner[mid] = pid
+        target: Dict[str, str] = {}
+        for chunk in _chunks(class_ids):
+            for cid, pid in c.execute(
+                    f"SELECT id, project_id FROM source_classes WHERE id IN ({','.join('?' * len(chunk))})", chunk):
+                target[cid] = pid
+        for mid, cid in links:
+            a, b = owner.get(mid), target.get(cid)
+            if a is not None and b is not None and a != b:
+                raise DomainError(f"Method parameter links method {mid} (project {a}) to class {cid} "
+                                  f"of another project ({b})", "PARAMETER_CROSS_PROJECT")
 
     def save_rows(self, rows: Sequence[tuple]) -> None:
         if not rows:
@@ -517,7 +547,14 @@ class MethodParameterRepository:
             c.execute("DELETE FROM method_parameters WHERE method_id = ?", (method_id,))
 
     def delete_by_class_id(self, class_id: str) -> None:
-        """Deletes parameters of every method owned by ``class_id``."""
+        """Deletes every link whose parameter TYPE is ``class_id``
+        (``MethodParameterRepository.java:127-133``: ``WHERE class_id = ?``)."""
+        with self.db.transaction() as c:
+            c.execute("DELETE FROM method_parameters WHERE class_id = ?", (class_id,))
+
+    def delete_by_owner_class_id(self, class_id: str) -> None:
+        """Deletes the parameter links of every method declared BY ``class_id``
+        (the single-class form of :meth:`delete_by_class_ids`)."""
         with self.db.transaction() as c:
             c.execute("DELETE FROM method_parameters WHERE method_id IN "
                       "(SELECT id FROM source_methods WHERE class_id = ?)", (class_id,))

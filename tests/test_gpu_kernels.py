@@ -159,3 +159,21 @@ def test_shape_validation_raises(hip):
         hip.decode_attention(_bf(1, 6, 64), _bf(1, 4, 8, 64), _bf(1, 4, 8, 64),
                              torch.zeros(1, dtype=torch.int32, device="cuda"),
                              torch.ones(1, dtype=torch.int32, device="cuda"), 0.1)
+    # undersized caller-supplied output buffers are refused before the launch
+    with pytest.raises(hip.HipOpsError):
+        hip.add_rmsnorm(_bf(4, 128), _bf(128), 1e-5, out=_bf(3, 128))
+    with pytest.raises(hip.HipOpsError):
+        hip.silu_mul(_bf(4, 256), out=_bf(4, 64))
+    with pytest.raises(hip.HipOpsError):
+        hip.embedding(_bf(16, 64), torch.zeros(8, dtype=torch.int32, device="cuda"), out=_bf(7, 64))
+    with pytest.raises(hip.HipOpsError):
+        hip.masked_argmax(_bf(4, 64), out=torch.zeros(3, dtype=torch.int32, device="cuda"))
+    with pytest.raises(hip.HipOpsError):
+        hip.decode_attention(_bf(2, 4, 64), _bf(2, 4, 8, 64), _bf(2, 4, 8, 64),
+                             torch.zeros(2, dtype=torch.int32, device="cuda"),
+                             torch.ones(2, dtype=torch.int32, device="cuda"), 0.1, out=_bf(1, 4, 64))
+    cos_sin = torch.zeros(16, 32, 2, dtype=torch.float32, device="cuda")
+    with pytest.raises(hip.HipOpsError):
+        hip.rope_kv(_bf(2, 6 * 64), torch.zeros(2, dtype=torch.int32, device="cuda"),
+                    torch.zeros(2, dtype=torch.int32, device="cuda"), cos_sin, _bf(1, 1, 16, 64), _bf(1, 1, 16, 64),
+                    4, q_out=_bf(1, 4, 64))

@@ -71,7 +71,16 @@ def test_cron_expressions():
     assert monthly.next_after(datetime(2024, 2, 1)) == datetime(2024, 7, 1)
     five = CronExpression("15 10 * * *")  # classic 5-field
     assert five.next_after(datetime(2024, 1, 1, 9, 0)) == datetime(2024, 1, 1, 10, 15)
-    for bad in ("* * *", "61 * * * * *", "0 0 25 * * *"):
+    # day-of-week 7 is Sunday, also as a range end (Spring accepts 1-7 and 5-7)
+    sunday = CronExpression("0 0 0 * * 7")
+    assert sunday.next_after(datetime(2024, 1, 6, 12, 0)) == datetime(2024, 1, 7)  # Sat -> Sun
+    every_day = CronExpression("0 0 0 * * 1-7")
+    assert every_day.dows == set(range(7))
+    assert every_day.next_after(datetime(2024, 1, 6, 12, 0)) == datetime(2024, 1, 7)
+    weekend = CronExpression("0 0 0 * * 5-7")
+    assert weekend.dows == {5, 6, 0}
+    assert weekend.next_after(datetime(2024, 1, 8, 12, 0)) == datetime(2024, 1, 12)  # Mon -> Fri
+    for bad in ("* * *", "61 * * * * *", "0 0 25 * * *", "0 0 0 * * 8"):
         with pytest.raises(ValueError):
             CronExpression(bad)
 

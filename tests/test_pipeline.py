@@ -240,6 +240,27 @@ def test_project_busy(tmp_path, repo):
     app.close()
 
 
+def test_failed_prepare_releases_the_project_lock(tmp_path, repo, monkeypatch):
+    """A failure while registering the project (e.g. ``database is locked``)
+    must not leave the repository lock held: the next analysis runs."""
+    app = make_app(tmp_path)
+    real = app.indexer._prepare_project
+    calls = []
+
+    def flaky(url, branch):
+        calls.append(1)
+        if len(calls) == 1:
+            raise RuntimeError("database is locked")
+        return real(url, branch)
+
+    monkeypatch.setattr(app.indexer, "_prepare_project", flaky)
+    with pytest.raises(RuntimeError):
+        app.indexer.analyze_project(str(repo))
+    r = app.indexer.analyze_project(str(repo))  # not PROJECT_BUSY
+    assert r.success and r.classes_analyzed > 0
+    app.close()
+
+
 def test_stuck_project_recovered_on_start(tmp_path, repo):
     app = make_app(tmp_path)
     r = app.indexer.analyze_project(str(repo))

@@ -126,6 +126,50 @@ def test_bulk_replace_keeps_referential_integrity(tmp_path):
     app.close()
 
 
+def test_parameter_delete_by_class_id_matches_reference(repos):
+    """``deleteByClassId`` removes links whose parameter TYPE is the class
+    (``MethodParameterRepository.java:127-133``); the owner-side variant
+    removes the links of the class's own methods."""
+    p = _project()
+    repos.projects.save(p)
+    owner = SourceClass.create(p.id, "co.a.OrderService", ClassType.SERVICE, None, None, None)
+    dto = SourceClass.create(p.id, "co.a.OrderDto", ClassType.DTO, None, None, None)
+    other = SourceClass.create(p.id, "co.a.User", ClassType.ENTITY, None, None, None)
+    repos.classes.save_all([owner, dto, other])
+    m = SourceMethod.create(owner.id, "create", None, None, None, None, None, 1)
+    repos.methods.save(m)
+    repos.params.save_all([MethodParameter.create(m.id, 0, dto.id), MethodParameter.create(m.id, 1, other.id)])
+    repos.params.delete_by_class_id(dto.id)  # type side only
+    assert [x.class_id for x in repos.params.find_by_method_id(m.id)] == [other.id]
+    repos.params.delete_by_class_id(owner.id)  # owner is no parameter type: nothing removed
+    assert len(repos.params.find_by_method_id(m.id)) == 1
+    repos.params.delete_by_owner_class_id(owner.id)
+    assert repos.params.find_by_method_id(m.id) == []
+
+
+def test_parameter_link_across_projects_rejected(repos):
+    """The project-scoped delete selects links by target class; a link from one
+    project's method to another project's class is refused at write time."""
+    from dmcp.utils.errors import DomainError
+    a, b = _project("a"), _project("b")
+    repos.projects.save(a)
+    repos.projects.save(b)
+    ca = SourceClass.create(a.id, "co.a.Svc", ClassType.SERVICE, None, None, None)
+    cb = SourceClass.create(b.id, "co.b.Dto", ClassType.DTO, None, None, None)
+    repos.classes.save_all([ca, cb])
+    m = SourceMethod.create(ca.id, "run", None, None, None, None, None, 1)
+    repos.methods.save(m)
+    with pytest.raises(DomainError) as e:
+        repos.params.save_all([MethodParameter.create(m.id, 0, cb.id)])
+    assert e.value.error_code == "PARAMETER_CROSS_PROJECT"
+    with pytest.raises(DomainError):
+        repos.params.save(MethodParameter.create(m.id, 0, cb.id))
+    assert repos.params.find_by_method_id(m.id) == []
+    repos.params.save(MethodParameter.create(m.id, 0, ca.id))  # same project: fine
+    repos.params.delete_by_project_id(a.id)
+    assert repos.params.find_by_method_id(m.id) == []
+
+
 def test_cascade_delete_project(repos):
     p = _project()
     repos.projects.save(p)

@@ -287,7 +287,7 @@ class LocalLM:
         if B > self.max_rows:
             raise ValueError(f"decode: {B} rows > max_rows {self.max_rows}")
         seq_len = positions + 1
-        chunk = ops.decode_chunk(B, c.n_kv_heads, c.max_seq)
+        chunk, splits = ops.decode_plan(B, c.n_kv_heads, c.max_seq)
         x = ops.embedding(self.w["embed"], tokens)
         resid = x.clone()
         h = ops.add_rmsnorm(x, self.w["l0.ln1"], c.eps)
@@ -298,7 +298,7 @@ class LocalLM:
             prefix = (ops.SharedPrefix(kc[self.prefix_slot], self.prefix_vt[i], self.prefix_dev, self.PREFIX_CHUNK)
                       if self.shared_prefix else None)
             att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws, chunk=chunk,
-                                       prefix=prefix)
+                                       prefix=prefix, splits=splits)
             o = F.linear(att.view(B, c.n_heads * c.head_dim), self.w[f"l{i}.wo"])
             h = ops.add_rmsnorm(o, self.w[f"l{i}.ln2"], c.eps, residual=resid)
             m = self._mlp(i, h)

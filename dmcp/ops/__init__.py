@@ -30,6 +30,12 @@ def decode_chunk(rows, n_kv_heads, max_seq):
     return _dc(rows, n_kv_heads, max_seq)
 
 
+def decode_plan(rows, n_kv_heads, max_seq):
+    """(chunk, splits) of the per-row decode attention (see :func:`dmcp.ops.hip.decode_plan`)."""
+    from .hip import decode_plan as _dp
+    return _dp(rows, n_kv_heads, max_seq)
+
+
 def decode_workspace(rows, n_heads, n_kv_heads, head_dim, max_seq, device, chunk: int = 256, prefix_slots: int = 0):
     """Split-K scratch of the decode-attention kernel (fp32 partials + max/sum)."""
     return _hip().decode_workspace(rows, n_heads, n_kv_heads, head_dim, max_seq, device, chunk, prefix_slots)
@@ -46,9 +52,11 @@ def rope_kv(qkv, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out=None):
 
 
 def decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace=None, chunk: int = 256, out=None,
-                     prefix=None):
-    mod = _hip() if q.is_cuda else reference
-    return mod.decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace, chunk, out, prefix)
+                     prefix=None, splits=None):
+    if q.is_cuda:
+        return _hip().decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace, chunk, out, prefix,
+                                       splits)
+    return reference.decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace, chunk, out, prefix)
 
 
 def silu_mul(gate_up, out=None):

@@ -68,6 +68,22 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
+// Per-row split geometry, shared by the per-row kernels and the combine:
+// at most `splits` parts of >= `chunk` keys each, equal sizes rounded up to
+// whole 32-key tiles (balanced work items instead of full chunks plus a
+// short remainder).
+struct SplitGeom {
+    int nact, part;
+};
+
+__device__ __forceinline__ SplitGeom split_geom(int Ls, int splits, int chunk) {
+    if (Ls <= 0) return {0, 0};
+    int n = min(splits, (Ls + chunk - 1) / chunk);
+    const int part = (((Ls + n - 1) / n) + 31) & ~31;
+    n = (Ls + part - 1) / part;
+    return {n, part};
+}
+
 // --------------------------------------------------------------------------
 // 1. fused residual-add + RMSNorm:  h = x (+ residual);  residual <- h;
 //    out = h * rsqrt(mean(h^2) + eps) * w.  One block per row, VPT 16-B
@@ -227,17 +243,16 @@ __global__ __launch_bounds__(kBlock) void decode_attn_kernel(
     const int s = slot[b];
     const int L = (s >= 0 && s < num_slots) ? min(seq_len[b], max_seq) : 0;  // never read a bad slot
     // splits that own keys past the shared prefix; the others are skipped
-    const int Ls = L - P;
-    const int nact = Ls > 0 ? min(splits, (Ls + chunk - 1) / chunk) : 0;
     if (L <= 0) {  // padding row / bad slot: defined output, nothing read
         if (split == 0)
             for (int o = threadIdx.x; o < G * D; o += kBlock) out[((size_t)b * Hq + kh * G) * D + o] = 0;
         continue;
     }
-    if (split >= nact) continue;
-    const bool direct = P == 0 && nact == 1;  // the whole context in this block: no merge
-    const int start = P + split * chunk;
-    const int end = min(L, start + chunk);
+    const SplitGeom sg = split_geom(L - P, splits, chunk);
+    if (split >= sg.nact) continue;
+    const bool direct = P == 0 && sg.nact == 1;  // the whole context in this block: no merge
+    const int start = P + split * sg.part;
+    const int end = min(L, start + sg.part);
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = threadIdx.x / kWave;
     const int kig = lane / LPK;  // key slot within the wave step
@@ -380,8 +395,11 @@ __global__ __launch_bounds__(kBlock) void decode_attn_kernel(
     }  // work items
 }
 
-// Split-K merge: one block per (row, kv head), G*D outputs.  Rows whose
-// context fits one split (nact <= 1) were written by the main kernel.
+// Split-K merge.  One thread per 4 consecutive outputs (b, q head, d..d+3):
+// float4 partial loads, issued 8 splits at a time before any of them is
+// merged, so a row with ~20 partials (shared prefix + suffix splits) waits
+// for 3 memory round trips instead of one per 4 partials.  Rows whose
+// context fits one split (nact <= 1, no prefix) were written directly.
 // (A fused "last block merges" variant needs agent-scope release fences; on
 // gfx950 each one writes back the XCD's L2 and made the kernel ~10x slower
 // -- profiles/ROUND1_NOTES.md.)
@@ -389,40 +407,59 @@ __global__ __launch_bounds__(kBlock) void decode_attn_combine_kernel(const float
                                                                     const float* __restrict__ part_ml,
                                                                     const int32_t* __restrict__ slot,
                                                                     const int32_t* __restrict__ seq_len,
-                                                                    uint16_t* __restrict__ out, int Hkv, int G,
+                                                                    uint16_t* __restrict__ out, int B, int Hq,
                                                                     int D, int max_seq, int chunk, int splits,
                                                                     int num_slots, const int32_t* __restrict__ plen,
                                                                     int ps_max, int pchunk) {
-    const int kh = blockIdx.x, b = blockIdx.y;
-    const int s = slot[b];
-    const int L = (s >= 0 && s < num_slots) ? min(seq_len[b], max_seq) : 0;
-    if (L <= 0) return;  // padding row: zeroed by the main kernel
+    constexpr int U = 8;
+    const int dq = D / 4;
+    const long total = (long)B * Hq * dq;
     const int P = plen ? max(0, *plen) : 0;
-    const int Ls = L - P;
-    const int nact = Ls > 0 ? min(splits, (Ls + chunk - 1) / chunk) : 0;
-    const int npre = P > 0 ? min(ps_max, (P + pchunk - 1) / pchunk) : 0;  // prefix partials
-    if (npre == 0 && nact <= 1) return;  // written directly by the main kernel
-    const int Hq = Hkv * G;
     const int splits_total = ps_max + splits;
-    // one pass of online merges (loads of different splits are independent,
-    // so the unrolled loop keeps several in flight)
-    for (int o = threadIdx.x; o < G * D; o += kBlock) {
-        const int g = o / D, d = o - g * D;
-        const size_t base = ((size_t)b * Hq + kh * G + g) * splits_total;
-        float m = -1e30f, lt = 0.f, at = 0.f;
-        auto merge = [&](size_t idx) {
-            const float ms = part_ml[idx * 2], ls = part_ml[idx * 2 + 1], os = part_o[idx * D + d];
-            const float mn = fmaxf(m, ms);
-            const float ca = exp2f(m - mn), cb = exp2f(ms - mn);
-            lt = lt * ca + ls * cb;
-            at = at * ca + os * cb;
+    for (long u = (long)blockIdx.x * kBlock + threadIdx.x; u < total; u += (long)gridDim.x * kBlock) {
+        const int b = (int)(u / ((long)Hq * dq));
+        const int rem = (int)(u - (long)b * Hq * dq);
+        const int qh = rem / dq, d = (rem - qh * dq) * 4;
+        const int s = slot[b];
+        const int L = (s >= 0 && s < num_slots) ? min(seq_len[b], max_seq) : 0;
+        if (L <= 0) continue;  // padding row: zeroed by the main kernel
+        const int nact = split_geom(L - P, splits, chunk).nact;
+        const int npre = P > 0 ? min(ps_max, (P + pchunk - 1) / pchunk) : 0;  // prefix partials
+        if (npre == 0 && nact <= 1) continue;  // written directly by the main kernel
+        const int n = npre + nact;
+        const size_t base = ((size_t)b * Hq + qh) * splits_total;
+        float m = -1e30f, lt = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        for (int i0 = 0; i0 < n; i0 += U) {
+            float2 ml[U];
+            float4 o4[U];
+#pragma unroll
+            for (int j = 0; j < U; ++j) {
+                const int i = i0 + j;
+                const size_t idx = base + (i < npre ? i : ps_max + (i - npre));
+                if (i < n) {
+                    ml[j] = *reinterpret_cast<const float2*>(part_ml + idx * 2);
+                    o4[j] = *reinterpret_cast<const float4*>(part_o + idx * D + d);
+                } else {
+                    ml[j] = make_float2(-1e30f, 0.f);
+                    o4[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
+            float mn = m;
+#pragma unroll
+            for (int j = 0; j < U; ++j) mn = fmaxf(mn, ml[j].x);
+            const float ca = exp2f(m - mn);
+            lt *= ca; a0 *= ca; a1 *= ca; a2 *= ca; a3 *= ca;
+#pragma unroll
+            for (int j = 0; j < U; ++j) {
+                const float cb = exp2f(ml[j].x - mn);
+                lt += ml[j].y * cb;
+                a0 += o4[j].x * cb; a1 += o4[j].y * cb; a2 += o4[j].z * cb; a3 += o4[j].w * cb;
+            }
             m = mn;
-        };
-#pragma unroll 4
-        for (int sp = 0; sp < npre; ++sp) merge(base + sp);
-#pragma unroll 4
-        for (int sp = 0; sp < nact; ++sp) merge(base + ps_max + sp);
-        out[((size_t)b * Hq + kh * G + g) * D + d] = f2bf(lt > 0.f ? at / lt : 0.f);
+        }
+        const float inv = lt > 0.f ? 1.f / lt : 0.f;
+        const float f[4] = {a0 * inv, a1 * inv, a2 * inv, a3 * inv};
+        *reinterpret_cast<uint2*>(out + ((size_t)b * Hq + qh) * D + d) = pack4(f);
     }
 }
 
@@ -705,11 +742,140 @@ __global__ __launch_bounds__(kBlock) void embedding_kernel(const uint16_t* __res
     }
 }
 
+typedef short v4i16_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+// One 32-key tile of a (slot, kv head): K rows as the S^T A operand (key
+// kt + 16h + (lane&15), dims 32ks + 8*(lane>>4)) and the V tile (32 x D,
+// contiguous) as 16-B chunks, chunk lane + 64r.  A full tile is addressed
+// from one per-tile base plus compile-time offsets (no per-load 64-bit
+// address math); the partial last tile of a split clamps every key to
+// end-1 (in-bounds, finite; masked later).
+template <int D>
+struct KVTile {
+    uint4 k[2][D / 32];
+    uint4 v[D / 16];
+};
+
+template <int D>
+__device__ __forceinline__ void load_kv_tile(const uint16_t* __restrict__ kb, const uint16_t* __restrict__ vb,
+                                             int kt, int end, int lane, KVTile<D>& t) {
+    constexpr int CPK = D / 8;
+    if (kt + 32 <= end) {
+        const uint16_t* kp = kb + (size_t)(kt + (lane & 15)) * D + 8 * (lane >> 4);
+        const uint16_t* vp = vb + (size_t)kt * D + lane * 8;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int ks = 0; ks < D / 32; ++ks)
+                t.k[h][ks] = *reinterpret_cast<const uint4*>(kp + 16 * h * D + 32 * ks);
+#pragma unroll
+        for (int r = 0; r < D / 16; ++r) t.v[r] = *reinterpret_cast<const uint4*>(vp + kWave * 8 * r);
+        return;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int key = min(kt + 16 * h + (lane & 15), end - 1);
+#pragma unroll
+        for (int ks = 0; ks < D / 32; ++ks)
+            t.k[h][ks] = *reinterpret_cast<const uint4*>(kb + (size_t)key * D + 32 * ks + 8 * (lane >> 4));
+    }
+#pragma unroll
+    for (int r = 0; r < D / 16; ++r) {
+        const int ch = lane + kWave * r;
+        const int key = min(kt + ch / CPK, end - 1);
+        t.v[r] = *reinterpret_cast<const uint4*>(vb + (size_t)key * D + (ch % CPK) * 8);
+    }
+}
+
+// One tile of the MFMA per-row kernel: V -> the wave's LDS tile, S^T on the
+// matrix cores, then (prefetch) the tile two ahead is loaded into the same
+// registers while the softmax and the PV product run.
+template <int D>
+__device__ __forceinline__ void attn_tile_mfma(KVTile<D>& cur, bool prefetch, int kt_next,
+                                               const uint16_t* __restrict__ kb, const uint16_t* __restrict__ vb,
+                                               int kt, int end, int lane, int g16, uint16_t* vw,
+                                               const uint16_t* tr0, const uint16_t* tr1,
+                                               const bf16x8_t (&qf)[D / 32], float& m, float& l,
+                                               f32x4_t (&acc)[D / 16], float scale_log2) {
+    constexpr int KS = D / 32;
+    constexpr int DB = D / 16;
+    constexpr int CPK = D / 8;
+    constexpr int VROW = D + 8;
+    const bool partial = kt + 32 > end;
+#pragma unroll
+    for (int r = 0; r < D / 16; ++r) {
+        const int ch = lane + kWave * r;
+        *reinterpret_cast<uint4*>(vw + (ch / CPK) * VROW + (ch % CPK) * 8) = cur.v[r];
+    }
+    f32x4_t sacc[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        sacc[h] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+            sacc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(cur.k[h][ks]), qf[ks], sacc[h], 0, 0, 0);
+    }
+    if (prefetch) load_kv_tile<D>(kb, vb, kt_next, end, lane, cur);
+    // S^T tile: register 4h+i = key kt + 16h + 4*g16 + i of query (lane&15).
+    // Scale folded into one FMA per score; the key mask only on a partial
+    // last tile; hardware exp2 and bf16 packing.
+    float tmax = -1e30f;
+    if (!partial) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) tmax = fmaxf(tmax, sacc[h][i]);
+    } else {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int key = kt + 16 * h + 4 * g16 + i;
+                sacc[h][i] = key < end ? sacc[h][i] : -1e30f;
+                tmax = fmaxf(tmax, sacc[h][i]);
+            }
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, kWave));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, kWave)) * scale_log2;
+    const float mn = fmaxf(m, tmax);
+    if (__any(mn > m)) {
+        const float corr = __builtin_amdgcn_exp2f(m - mn);
+        l *= corr;
+#pragma unroll
+        for (int db = 0; db < DB; ++db) acc[db] *= corr;
+    }
+    m = mn;
+    f32x8_t pr;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            pr[4 * h + i] = __builtin_amdgcn_exp2f(fmaf(sacc[h][i], scale_log2, -mn));
+            l += pr[4 * h + i];  // lane-partial sum; the 4 groups are added once at the end
+        }
+    // B operand P^T: element j = key pi(8*g16 + j) = 16*(j>>2) + 4*g16 + (j&3)
+    const bf16x8_t pf = __builtin_convertvector(pr, bf16x8_t);
+#pragma unroll
+    for (int db = 0; db < DB; ++db) {
+        const v4i16_t lo =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16_t*)(tr0 + 16 * db));
+        const v4i16_t hi =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16_t*)(tr1 + 16 * db));
+        const uint4 a = make_uint4((uint32_t)(uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16),
+                                   (uint32_t)(uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16),
+                                   (uint32_t)(uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16),
+                                   (uint32_t)(uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16));
+        acc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), pf, acc[db], 0, 0, 0);
+    }
+}
+
 // --------------------------------------------------------------------------
 // 3c. per-row decode attention on the matrix cores (the default).
-//    Same work items, outputs and partial layout as decode_attn_kernel (so
-//    the prefix kernel and the combine are shared), but ONE WAVE per item and
-//    both products on MFMA 16x16x32 bf16 per 32-key tile:
+//    Same outputs and partial layout as decode_attn_kernel (so the prefix
+//    kernel and the combine are shared), but ONE WAVE per work item
+//    (row, kv head, split) and both products on MFMA 16x16x32 bf16 per
+//    32-key tile:
 //        S^T[key, q] = K[key, :] . Q^T[:, q]      A = K rows straight from HBM
 //                                                  (16 B per lane), B = Q^T
 //        O^T[d, q]  += V^T[d, key] . P^T[key, q]  A = V^T read transposed out
@@ -720,39 +886,17 @@ __global__ __launch_bounds__(kBlock) void embedding_kernel(const uint16_t* __res
 //    online softmax is in-register + 2 cross-group shuffles per tile, and P^T
 //    is the PV B operand with no data movement: the PV k order is the
 //    permutation {4g..4g+3, 16+4g..16+4g+3} of lane group g, matched by the
-//    two transposed V reads (rows 4g.. and 16+4g..).  The VALU kernel spent
-//    ~400 VALU instructions per 32 keys per wave (dot products, 48 shuffles,
-//    exp2 per head per key); here a tile is 8 MFMAs, 8 exp2, ~20 VALU and
-//    2 shuffles, and the next tile's K/V loads are in flight meanwhile.
+//    two transposed V reads (rows 4g.. and 16+4g..).
+//    The kernel is bound by HBM latency x bytes in flight, not by math
+//    (profiles/decode_step_*: a 1-deep prefetch with 1024-key splits ran at
+//    42 % of the copy rate): each row's keys are cut into equal splits sized
+//    so that ~16 waves per CU are busy, and each wave keeps TWO tiles of
+//    K/V loads in flight (register double buffer, D = 64) while it computes
+//    a third.
 //    No block-level synchronisation: each wave owns its LDS tile, so
 //    different waves of a block run different items.
 // --------------------------------------------------------------------------
-typedef short v4i16_t __attribute__((ext_vector_type(4)));
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
-
-// K rows (S^T A operand: key kt + 16h + (lane&15), dims 32ks + 8*(lane>>4))
-// and the V tile as 16-B row chunks, keys clamped to end-1 (masked later)
-template <int D>
-__device__ __forceinline__ void load_kv_tile(const uint16_t* __restrict__ kb, const uint16_t* __restrict__ vb,
-                                             int kt, int end, int lane, uint4 (&kr)[2][D / 32],
-                                             uint4 (&vr)[D / 16]) {
-    constexpr int CPK = D / 8;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int key = min(kt + 16 * h + (lane & 15), end - 1);
-#pragma unroll
-        for (int ks = 0; ks < D / 32; ++ks)
-            kr[h][ks] = *reinterpret_cast<const uint4*>(kb + (size_t)key * D + 32 * ks + 8 * (lane >> 4));
-    }
-#pragma unroll
-    for (int r = 0; r < D / 16; ++r) {
-        const int ch = lane + kWave * r;
-        const int key = min(kt + ch / CPK, end - 1);
-        vr[r] = *reinterpret_cast<const uint4*>(vb + (size_t)key * D + (ch % CPK) * 8);
-    }
-}
-
-template <int D>
+template <int D, bool kDouble>
 __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache,
     const int32_t* __restrict__ slot, const int32_t* __restrict__ seq_len, uint16_t* __restrict__ out,
@@ -762,8 +906,6 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
     static_assert(D % 32 == 0, "D must be a multiple of 32");
     constexpr int KS = D / 32;    // 32-dim k-steps of the S product
     constexpr int DB = D / 16;    // 16-row d blocks of O^T
-    constexpr int VCH = D / 16;   // 16-B V chunks per lane per 32-key tile
-    constexpr int CPK = D / 8;    // 16-B chunks per key row
     constexpr int VROW = D + 8;   // LDS row stride in bf16 (144 B at D=64: conflict-light tr reads)
     constexpr int NW = kBlock / kWave;
     __shared__ __attribute__((aligned(16))) uint16_t vlds[NW][32 * VROW];
@@ -776,30 +918,30 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
     const int Hq = Hkv * G;
     const int P = __builtin_amdgcn_readfirstlane(plen ? max(0, *plen) : 0);
     const int splits_total = ps_max + splits;
-    const int per_split = B * Hkv;
-    const int total = splits * per_split;
+    const int total = B * Hkv * splits;
     uint16_t* vw = vlds[wave];
     // transposed-read addresses (tile-invariant): lane 4q+p of group g16 reads
     // row 4*g16 + q (and 16 + ...), columns 4p..4p+3 of each 16-wide d block
     const uint16_t* tr0 = vw + (4 * g16 + (c >> 2)) * VROW + 4 * (c & 3);
     const uint16_t* tr1 = tr0 + 16 * VROW;
     for (int item = blockIdx.x * NW + wave; item < total; item += gridDim.x * NW) {
-        const int split = item / per_split;
-        const int rem = item - split * per_split;
+        // split-major: consecutive waves take different rows' splits, so the
+        // persistent grid's first pass covers every row
+        const int split = item / (B * Hkv);
+        const int rem = item - split * (B * Hkv);
         const int b = rem / Hkv, kh = rem - b * Hkv;
         const int s = __builtin_amdgcn_readfirstlane(slot[b]);
         const int L = __builtin_amdgcn_readfirstlane((s >= 0 && s < num_slots) ? min(seq_len[b], max_seq) : 0);
-        const int Ls = L - P;
-        const int nact = Ls > 0 ? min(splits, (Ls + chunk - 1) / chunk) : 0;
         if (L <= 0) {  // padding row / bad slot: defined output, nothing read
             if (split == 0)
                 for (int o = lane; o < G * D; o += kWave) out[((size_t)b * Hq + kh * G) * D + o] = 0;
             continue;
         }
-        if (split >= nact) continue;
-        const bool direct = P == 0 && nact == 1;
-        const int start = P + split * chunk;
-        const int end = min(L, start + chunk);
+        const SplitGeom sg = split_geom(L - P, splits, chunk);
+        if (split >= sg.nact) continue;
+        const bool direct = P == 0 && sg.nact == 1;
+        const int start = P + split * sg.part;
+        const int end = min(L, start + sg.part);
         const int ntiles = (end - start + 31) / 32;
         bf16x8_t qf[KS];
 #pragma unroll
@@ -811,78 +953,29 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
         const size_t head_off = ((size_t)s * Hkv + kh) * (size_t)max_seq * D;
         const uint16_t* kb = k_cache + head_off;
         const uint16_t* vb = v_cache + head_off;
-        uint4 kr[2][KS], vr[VCH];
         float m = -1e30f, l = 0.f;
         f32x4_t acc[DB];
 #pragma unroll
         for (int db = 0; db < DB; ++db) acc[db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        load_kv_tile<D>(kb, vb, start, end, lane, kr, vr);
-        for (int t = 0; t < ntiles; ++t) {
-            const int kt = start + 32 * t;
-            // the wave's V tile -> LDS, row-major [key][d]
-#pragma unroll
-            for (int r = 0; r < VCH; ++r) {
-                const int ch = lane + kWave * r;
-                *reinterpret_cast<uint4*>(vw + (ch / CPK) * VROW + (ch % CPK) * 8) = vr[r];
+        if (kDouble) {
+            KVTile<D> ta, tb;
+            load_kv_tile<D>(kb, vb, start, end, lane, ta);
+            if (ntiles > 1) load_kv_tile<D>(kb, vb, start + 32, end, lane, tb);
+            for (int t = 0; t < ntiles; t += 2) {
+                const int kt = start + 32 * t;
+                attn_tile_mfma<D>(ta, t + 2 < ntiles, kt + 64, kb, vb, kt, end, lane, g16, vw, tr0, tr1, qf, m, l,
+                                  acc, scale_log2);
+                if (t + 1 < ntiles)
+                    attn_tile_mfma<D>(tb, t + 3 < ntiles, kt + 96, kb, vb, kt + 32, end, lane, g16, vw, tr0, tr1, qf,
+                                      m, l, acc, scale_log2);
             }
-            f32x4_t sacc[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                sacc[h] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int ks = 0; ks < KS; ++ks)
-                    sacc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(kr[h][ks]), qf[ks], sacc[h], 0, 0, 0);
-            }
-            if (t + 1 < ntiles) load_kv_tile<D>(kb, vb, kt + 32, end, lane, kr, vr);  // in flight during softmax + PV
-            // S^T tile: register 4h+i = key kt + 16h + 4*g16 + i of query c.
-            // Scale folded into one FMA per score; the key mask only on a
-            // partial last tile; hardware exp2 and bf16 packing.
-            float sv[8];
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) sv[4 * h + i] = sacc[h][i];
-            float tmax = -1e30f;
-            if (kt + 32 <= end) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) tmax = fmaxf(tmax, sv[j]);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int key = kt + 16 * (j >> 2) + 4 * g16 + (j & 3);
-                    sv[j] = key < end ? sv[j] : -1e30f;
-                    tmax = fmaxf(tmax, sv[j]);
-                }
-            }
-            tmax = fmaxf(tmax, __shfl_xor(tmax, 16, kWave));
-            tmax = fmaxf(tmax, __shfl_xor(tmax, 32, kWave)) * scale_log2;
-            const float mn = fmaxf(m, tmax);
-            if (__any(mn > m)) {
-                const float corr = __builtin_amdgcn_exp2f(m - mn);
-                l *= corr;
-#pragma unroll
-                for (int db = 0; db < DB; ++db) acc[db] *= corr;
-            }
-            m = mn;
-            f32x8_t pr;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                pr[j] = __builtin_amdgcn_exp2f(fmaf(sv[j], scale_log2, -mn));
-                l += pr[j];  // lane-partial sum; the 4 groups are added once at the end
-            }
-            // B operand P^T: element j = key pi(8*g16 + j) = 16*(j>>2) + 4*g16 + (j&3)
-            const bf16x8_t pf = __builtin_convertvector(pr, bf16x8_t);
-#pragma unroll
-            for (int db = 0; db < DB; ++db) {
-                const v4i16_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (__attribute__((address_space(3))) v4i16_t*)(tr0 + 16 * db));
-                const v4i16_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (__attribute__((address_space(3))) v4i16_t*)(tr1 + 16 * db));
-                const uint4 a = make_uint4((uint32_t)(uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16),
-                                           (uint32_t)(uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16),
-                                           (uint32_t)(uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16),
-                                           (uint32_t)(uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16));
-                acc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), pf, acc[db], 0, 0, 0);
+        } else {
+            KVTile<D> ta;
+            load_kv_tile<D>(kb, vb, start, end, lane, ta);
+            for (int t = 0; t < ntiles; ++t) {
+                const int kt = start + 32 * t;
+                attn_tile_mfma<D>(ta, t + 1 < ntiles, kt + 32, kb, vb, kt, end, lane, g16, vw, tr0, tr1, qf, m, l,
+                                  acc, scale_log2);
             }
         }
         l += __shfl_xor(l, 16, kWave);
@@ -910,7 +1003,8 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
     }
 }
 
-// 0 = MFMA per-row kernel (default), 1 = VALU kernel (A/B and fallback)
+// 0 = MFMA per-row kernel (default), 1 = VALU kernel (A/B and fallback),
+// 2 = MFMA kernel with a register double buffer (D = 64; A/B)
 int g_decode_impl = 0;
 
 // CUs of the current device (cached per device; 256 on MI355X)
@@ -930,6 +1024,15 @@ inline int grid_for(size_t work) {
     size_t g = (work + kBlock - 1) / kBlock;
     if (g > 2048) g = 2048;  // grid-stride beyond 8 blocks/CU (Guideline 11)
     return (int)(g == 0 ? 1 : g);
+}
+
+hipError_t launch_combine(void* part_o, void* part_ml, const int32_t* sl, const int32_t* ln, void* out, int B, int Hq,
+                          int D, int max_seq, int chunk, int splits, int num_slots, const int32_t* pl, int ps_max,
+                          int pchunk, hipStream_t st) {
+    decode_attn_combine_kernel<<<grid_for((size_t)B * Hq * (D / 4)), kBlock, 0, st>>>(
+        (const float*)part_o, (const float*)part_ml, sl, ln, (uint16_t*)out, B, Hq, D, max_seq, chunk, splits,
+        num_slots, pl, ps_max, pchunk);
+    return hipGetLastError();
 }
 
 template <int D>
@@ -957,12 +1060,13 @@ hipError_t launch_decode_d(int G, dim3 grid, const uint16_t* q, const uint16_t* 
 
 extern "C" {
 
-int dmcp_abi_version() { return 6; }
+int dmcp_abi_version() { return 7; }
 
-// Selects the per-row decode attention kernel (0 = MFMA, 1 = VALU); returns the previous choice.
+// Selects the per-row decode attention kernel (0 = MFMA, 1 = VALU, 2 = MFMA double-buffered);
+// returns the previous choice.
 int dmcp_set_decode_impl(int impl) {
     const int prev = g_decode_impl;
-    if (impl == 0 || impl == 1) g_decode_impl = impl;
+    if (impl >= 0 && impl <= 2) g_decode_impl = impl;
     return prev;
 }
 
@@ -1037,25 +1141,24 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
     auto kk = (const uint16_t*)k_cache;
     auto vv = (const uint16_t*)v_cache;
     hipError_t e;
-    if (g_decode_impl == 0 && (D == 64 || D == 128) && G <= 16) {
+    if ((g_decode_impl == 0 || g_decode_impl == 2) && (D == 64 || D == 128) && G <= 16) {
         // one wave per item: a block runs 4 items
         const long wblocks = (items + 3) / 4;
         dim3 wgrid((unsigned)(wblocks < cap ? wblocks : cap));
-        if (D == 64)
-            decode_attn_mfma_kernel<64><<<wgrid, kBlock, 0, st>>>(qq, kk, vv, sl, ln, (uint16_t*)out, (float*)part_o,
-                                                                 (float*)part_ml, B, Hkv, G, max_seq, chunk, splits,
-                                                                 sl2, num_slots, pl, ps_max);
-        else
-            decode_attn_mfma_kernel<128><<<wgrid, kBlock, 0, st>>>(qq, kk, vv, sl, ln, (uint16_t*)out,
-                                                                  (float*)part_o, (float*)part_ml, B, Hkv, G, max_seq,
-                                                                  chunk, splits, sl2, num_slots, pl, ps_max);
+        float* po = (float*)part_o;
+        float* pml = (float*)part_ml;
+        uint16_t* oo = (uint16_t*)out;
+#define DMCP_MFMA_DECODE(DD, DBL)                                                                            \
+    decode_attn_mfma_kernel<DD, DBL><<<wgrid, kBlock, 0, st>>>(qq, kk, vv, sl, ln, oo, po, pml, B, Hkv, G,    \
+                                                               max_seq, chunk, splits, sl2, num_slots, pl, ps_max)
+        if (D == 64 && g_decode_impl == 2) DMCP_MFMA_DECODE(64, true);
+        else if (D == 64) DMCP_MFMA_DECODE(64, false);
+        else DMCP_MFMA_DECODE(128, false);
+#undef DMCP_MFMA_DECODE
         e = hipGetLastError();
         if (e != hipSuccess || (splits == 1 && !prefix)) return e;
-        decode_attn_combine_kernel<<<dim3(Hkv, B), kBlock, 0, st>>>((const float*)part_o, (const float*)part_ml, sl,
-                                                                   ln, (uint16_t*)out, Hkv, G, D, max_seq, chunk,
-                                                                   splits, num_slots, pl, ps_max,
-                                                                   prefix ? pchunk : 1);
-        return hipGetLastError();
+        return launch_combine(part_o, part_ml, sl, ln, out, B, Hkv * G, D, max_seq, chunk, splits, num_slots, pl,
+                              ps_max, prefix ? pchunk : 1, st);
     }
     dim3 grid((unsigned)(items < cap ? items : cap));
     if (D == 64)
@@ -1067,10 +1170,8 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
     else
         return hipErrorInvalidValue;
     if (e != hipSuccess || (splits == 1 && !prefix)) return e;
-    decode_attn_combine_kernel<<<dim3(Hkv, B), kBlock, 0, st>>>((const float*)part_o, (const float*)part_ml, sl, ln,
-                                                               (uint16_t*)out, Hkv, G, D, max_seq, chunk, splits,
-                                                               num_slots, pl, ps_max, prefix ? pchunk : 1);
-    return hipGetLastError();
+    return launch_combine(part_o, part_ml, sl, ln, out, B, Hkv * G, D, max_seq, chunk, splits, num_slots, pl, ps_max,
+                          prefix ? pchunk : 1, st);
 }
 
 int dmcp_silu_mul(const void* gu, void* out, int T, int I, void* stream) {

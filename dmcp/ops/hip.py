@@ -26,7 +26,7 @@ _lock = threading.Lock()
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _f = ctypes.c_float
-ABI_VERSION = 6  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
+ABI_VERSION = 7  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
 
 
 class HipOpsError(RuntimeError):
@@ -70,13 +70,14 @@ def lib() -> ctypes.CDLL:
         return _lib
 
 
-DECODE_IMPLS = {"mfma": 0, "valu": 1}
+DECODE_IMPLS = {"mfma": 0, "valu": 1, "mfma2": 2}
 
 
 def set_decode_impl(name: str) -> str:
     """Per-row decode attention kernel: ``mfma`` (default; matrix cores, one
-    wave per work item) or ``valu`` (the previous VALU kernel, kept for A/B
-    runs and as a reference).  Returns the previous choice.  Takes effect at
+    wave per work item), ``mfma2`` (same with a register double buffer: two
+    tiles of loads in flight per wave at half the occupancy; D = 64) or
+    ``valu`` (the previous VALU kernel, kept for A/B runs and as a reference).  Returns the previous choice.  Takes effect at
     the next launch (re-capture hipGraphs after switching)."""
     if name not in DECODE_IMPLS:
         raise ValueError(f"decode impl must be one of {sorted(DECODE_IMPLS)}")
@@ -173,23 +174,41 @@ def decode_splits(max_seq: int, chunk: int = 256) -> int:
 
 
 def decode_chunk(rows: int, n_kv_heads: int, max_seq: int, target_items: int = 2048) -> int:
-    """Keys per split-K work item for a decode step of ``rows`` query rows.
-
-    Larger chunks amortise the per-item merge (measured on MI355X, B=64,
-    L=2300, D=64: 110 us at 256 keys, 89 us at 512, 80 us at 1024 --
-    profiles/kernels_r1.jsonl); smaller ones keep >= ``target_items`` items
-    (~8 per CU) in flight when there are few rows."""
+    """Keys per split-K work item for a decode step of ``rows`` query rows
+    (the round-1 heuristic, kept for callers that pass only ``chunk``;
+    :func:`decode_plan` is what the model uses)."""
     for chunk in (1024, 512):
         if rows * n_kv_heads * decode_splits(max_seq, chunk) >= target_items:
             return chunk
     return 256
 
 
+def decode_plan(rows: int, n_kv_heads: int, max_seq: int, target_waves: int = 4096,
+                min_chunk: int = 256) -> tuple:
+    """(chunk, splits) for a decode step of ``rows`` query rows.
+
+    The per-row kernel is bound by HBM latency x bytes in flight: one wave
+    per (row, kv head, split) keeps one 32-key tile of K/V loads in flight,
+    so the step needs ~16 busy waves per CU (4 per SIMD at the kernel's 128
+    VGPRs; 4096 on 256 CUs).  Each row's keys are cut into at most
+    ``splits`` EQUAL parts of >= ``min_chunk`` keys (rounded to 32-key
+    tiles, in-kernel from the live length), instead of full fixed-size
+    chunks plus a short remainder that left most waves idle at the end
+    (measured: 1024-key chunks reached 42 % of the copy rate at B = 78,
+    L = 2,500 -- profiles/decode_step_r2*)."""
+    splits = max(1, -(-target_waves // max(1, rows * n_kv_heads)))
+    return min_chunk, min(splits, decode_splits(max_seq, min_chunk))
+
+
 def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: torch.Tensor,
                      seq_len: torch.Tensor, scale: float, workspace: Optional[tuple] = None,
                      chunk: int = 256, out: Optional[torch.Tensor] = None,
-                     prefix: Optional["SharedPrefix"] = None) -> torch.Tensor:
+                     prefix: Optional["SharedPrefix"] = None, splits: Optional[int] = None) -> torch.Tensor:
     """q [B, Hq, D]; caches [S, Hkv, MAXS, D]; slot/seq_len int32 [B].
+
+    Each row's keys (after the shared prefix) are split into at most
+    ``splits`` equal parts of >= ``chunk`` keys (default: as many as
+    ``MAXS / chunk``, i.e. parts of <= ``chunk`` keys); see :func:`decode_plan`.
 
     ``prefix``: the first ``*prefix.length`` keys of every row are the shared
     prefix (``prefix.k`` [Hkv, MAXS, D], ``prefix.vt`` [Hkv, D, ldv]), read
@@ -206,7 +225,12 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
         raise HipOpsError(f"decode_attention: unsupported shape q={tuple(q.shape)} kv={tuple(k_cache.shape)}")
     if slot.numel() != B or seq_len.numel() != B:
         raise HipOpsError("decode_attention: slot/seq_len must have B entries")
-    splits = decode_splits(MAXS, chunk)
+    if chunk <= 0:
+        raise HipOpsError("decode_attention: chunk must be positive")
+    max_splits = decode_splits(MAXS, chunk)
+    splits = max_splits if splits is None else int(splits)
+    if not 1 <= splits <= max_splits:
+        raise HipOpsError(f"decode_attention: splits {splits} outside [1, {max_splits}]")
     ps_max = 0
     pk = pvt = plen = None
     ldv = pchunk = 0

@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""Decode-step microbenchmark of the local enrichment model (GPU box).
+
+Reproduces the steady state of ``bench_enrich.py`` without the grammar
+engine: ``--batch`` sequences that share a ``--prefix``-token prompt prefix
+(instructions + README) and each own ``--ctx`` more tokens of context, plus
+``--extra`` jump-forward rows (consecutive positions of the first slots), so
+one step runs ``batch + extra`` rows through the captured decode graph.
+
+Reports, per step: device time of back-to-back graph replays (no host work
+between them), and the engine-like loop time (pack inputs, replay, copy the
+selected ids back, convert to a list).  With ``--fused 0/1`` the decode GEMMs
+run on hipBLASLt or on the fused gfx950 kernels (dmcp.ops.fused).
+
+    python scripts/bench_step.py --fused 1
+    rocprofv3 --kernel-trace --stats -d gpurun_out/step -o step -- python3 scripts/bench_step.py
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--preset", default="dmcp-coder-1b")
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--extra", type=int, default=14)
+    ap.add_argument("--prefix", type=int, default=4151)
+    ap.add_argument("--ctx", type=int, default=2500)
+    ap.add_argument("--max-seq", type=int, default=8192)
+    ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--fused", type=int, default=-1, help="-1 = model default, 0 = hipBLASLt, 1 = fused kernels")
+    ap.add_argument("--decode-impl", default="mfma", help="per-row decode attention kernel (dmcp.ops.hip.DECODE_IMPLS)")
+    a = ap.parse_args(argv)
+
+    from dmcp.enrich.local import LocalEngine
+    from dmcp.models.llm import LocalLM, preset
+    from dmcp.ops import hip
+
+    hip.set_decode_impl(a.decode_impl)
+
+    torch.cuda.set_device(0)
+    cfg = preset(a.preset, max_batch=a.batch, max_seq=a.max_seq)
+    model = LocalLM(cfg, device="cuda:0")
+    if a.fused >= 0:
+        model.use_fused = bool(a.fused)
+    eng = LocalEngine(model)
+    g = torch.Generator().manual_seed(0)
+    if a.prefix:
+        model.set_prefix(torch.randint(0, 256, (a.prefix,), generator=g).tolist())
+    n = a.batch + a.extra
+    toks = torch.randint(0, 256, (n,), generator=g).tolist()
+    slots = list(range(a.batch)) + [i % a.batch for i in range(a.extra)]
+    base = a.prefix + a.ctx
+    poss = [base + (i // a.batch) for i in range(n)]
+    mrows = [0] * n
+    graphs = eng.graphs
+    for _ in range(3):
+        graphs.run(toks, slots, poss, mrows)[1].cpu()
+    torch.cuda.synchronize()
+    # device time: back-to-back replays
+    t0 = time.perf_counter()
+    for _ in range(a.iters):
+        graphs.run(toks, slots, poss, mrows)
+    torch.cuda.synchronize()
+    dev_ms = (time.perf_counter() - t0) / a.iters * 1e3
+    # engine-like loop: wait for the ids and convert them every step
+    t0 = time.perf_counter()
+    for _ in range(a.iters):
+        graphs.run(toks, slots, poss, mrows)[1].cpu().tolist()
+    loop_ms = (time.perf_counter() - t0) / a.iters * 1e3
+    kv_bytes = 2 * cfg.layers * cfg.n_kv_heads * cfg.head_dim * 2 * (a.batch * (a.ctx + 1) + a.prefix)
+    w_bytes = 2 * (cfg.param_count() - cfg.vocab_size * cfg.hidden)
+    print(json.dumps({"bench": "decode_step", "preset": a.preset, "rows": n, "batch": a.batch, "prefix": a.prefix,
+                      "ctx": a.ctx, "fused": bool(getattr(model, "use_fused", False)),
+                      "decode_impl": a.decode_impl,
+                      "device_ms": round(dev_ms, 3), "loop_ms": round(loop_ms, 3),
+                      "host_gap_ms": round(loop_ms - dev_ms, 3),
+                      "sol_ms_at_6p3TBps": round((kv_bytes + w_bytes) / 6.3e12 * 1e3, 3),
+                      "weight_MB": round(w_bytes / 1e6, 1), "kv_MB": round(kv_bytes / 1e6, 1)}), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

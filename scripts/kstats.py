@@ -7,8 +7,8 @@ import collections
 import csv
 import sys
 
-CATS = [("gemm", "Cijk"), ("attn_suffix", "decode_attn_kernel"), ("attn_prefix", "prefix_attn"),
-        ("attn_combine", "combine"), ("prefill_attn", "attn_fwd"), ("rmsnorm", "rmsnorm"), ("silu", "silu"),
+CATS = [("gemm", "Cijk"), ("fused_gemm", "fused_gemm"), ("attn_combine", "combine"), ("attn_suffix", "decode_attn_"),
+        ("attn_prefix", "prefix_attn"), ("prefill_attn", "attn_fwd"), ("rmsnorm", "rmsnorm"), ("silu", "silu"),
         ("rope", "rope"), ("embedding", "embedding"), ("argmax", "argmax")]
 
 
@@ -19,7 +19,7 @@ def main() -> int:
     steps = 0
     for r in rows:
         name, t = r["Name"], int(r["TotalDurationNs"])
-        if "decode_attn_kernel" in name:
+        if "decode_attn_" in name and "combine" not in name:
             steps = int(r["Calls"]) // layers
         for c, key in CATS:
             if key in name:

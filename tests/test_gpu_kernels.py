@@ -115,6 +115,47 @@ def test_decode_attention_shared_prefix(hip, D, Hq, Hkv, P, B):
     torch.testing.assert_close(got.float(), exp.float(), atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("impl", ["mfma", "mfma2", "valu"])
+@pytest.mark.parametrize("splits", [1, 3, 6])
+@pytest.mark.parametrize("P", [0, 300])
+def test_decode_attention_balanced_splits(hip, impl, splits, P):
+    """Equal per-row splits (decode_plan: at most ``splits`` parts of >= chunk
+    keys, rounded to 32-key tiles) for every per-row kernel, with and without
+    a shared prefix; lengths hit partial tiles and split boundaries."""
+    from dmcp.ops import reference
+    from dmcp.ops.reference import SharedPrefix
+    D, Hq, Hkv, MAXS, S = 64, 32, 8, 1024, 9
+    lens_own = [1, 31, 32, 33, 257, 700, 1000 - P, 2, 511]
+    B = len(lens_own)
+    q = _bf(B, Hq, D, seed=21)
+    kc = _bf(S + 1, Hkv, MAXS, D, seed=22)
+    vc = _bf(S + 1, Hkv, MAXS, D, seed=23)
+    slot = torch.tensor([(3 * b) % S for b in range(B)], dtype=torch.int32, device="cuda")
+    lens = torch.tensor([P + n for n in lens_own], dtype=torch.int32, device="cuda")
+    pre = None
+    if P:
+        vt = torch.zeros((Hkv, D, MAXS), dtype=torch.bfloat16, device="cuda")
+        vt[:, :, :P] = vc[S, :, :P].transpose(-1, -2)
+        pre = SharedPrefix(kc[S], vt, torch.tensor([P], dtype=torch.int32, device="cuda"), 256)
+    prev = hip.set_decode_impl(impl)
+    try:
+        got = hip.decode_attention(q, kc, vc, slot, lens, 0.125, chunk=64, prefix=pre, splits=splits)
+    finally:
+        hip.set_decode_impl(prev)
+    exp = reference.decode_attention(q, kc, vc, slot, lens, 0.125, prefix=pre)
+    torch.testing.assert_close(got.float(), exp.float(), atol=2e-2, rtol=2e-2)
+
+
+def test_decode_plan_targets_busy_waves(hip):
+    chunk, splits = hip.decode_plan(96, 8, 8192)
+    assert chunk == 256 and 96 * 8 * splits >= 4096 and splits <= 32
+    assert hip.decode_plan(1, 8, 1024) == (256, 4)  # capped by max_seq / chunk
+    with pytest.raises(hip.HipOpsError):
+        hip.decode_attention(_bf(1, 8, 64), _bf(1, 2, 64, 64), _bf(1, 2, 64, 64),
+                             torch.zeros(1, dtype=torch.int32, device="cuda"),
+                             torch.ones(1, dtype=torch.int32, device="cuda"), 0.1, chunk=32, splits=3)
+
+
 def test_decode_attention_bad_slot_is_zero(hip):
     D, Hq, Hkv, MAXS = 64, 8, 2, 128
     q = _bf(2, Hq, D)

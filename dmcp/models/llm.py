@@ -7,11 +7,22 @@ attention, SwiGLU MLP, untied LM head, bf16 weights and KV cache.
 
 MI355X mapping:
 
-* GEMMs (fused QKV, O, fused gate+up, down, LM head) go to hipBLASLt through
-  ``torch.nn.functional.linear``;
-* everything between them is a hand-written gfx950 kernel (:mod:`dmcp.ops`):
-  fused residual-add + RMSNorm, RoPE + KV-cache append, split-K GQA decode
-  attention, SwiGLU, masked greedy sampling, embedding gather;
+* small decode steps (<= ``fused_max_rows`` = 32 rows: the tail of a batch,
+  single requests) run every weight product on the fused gfx950 MFMA GEMMs
+  of :mod:`dmcp.ops` (``csrc/fused_gemm.hip``): RMSNorm folded into the
+  QKV / gate-up / LM-head prologue (norm weights are folded into those
+  matrices at load time, :meth:`LocalLM._fold_norms`), RoPE + KV-cache
+  append in the QKV epilogue, SwiGLU in the gate/up epilogue, the residual
+  add in the O / down epilogues -- a layer is 4 GEMM launches + attention
+  (measured: 60 vs 77 us per layer at 16 rows);
+* larger decode steps, prefill and extend use hipBLASLt through
+  ``torch.nn.functional.linear`` with the hand-written element-wise kernels
+  (fused residual-add + RMSNorm, RoPE + KV-cache append, SwiGLU) between:
+  at 64-128 rows the register-direct fused GEMM re-reads every X row per
+  weight tile and is bound by per-CU L1 ingest, 1.5-3x slower than
+  hipBLASLt's LDS-tiled kernels (profiles/fused_gemm_vs_hipblaslt_r2.jsonl);
+* decode attention, masked greedy sampling and the embedding gather are
+  hand-written gfx950 kernels on every path;
 * prefill attention uses PyTorch SDPA (flash path on ROCm) -- prompts are
   processed once per class, the decode loop dominates;
 * the KV cache is one preallocated slab ``[layers, slots, Hkv, max_seq, D]``
@@ -146,6 +157,7 @@ class LocalLM:
         self.device = torch.device(device)
         self.dtype = torch.bfloat16
         self.w = weights if weights is not None else self._init_weights(seed)
+        self._fold_norms()
         c = cfg
         self.shared_prefix = shared_prefix
         self.num_slots = c.max_batch + (1 if shared_prefix else 0)
@@ -163,6 +175,10 @@ class LocalLM:
         self.prefix_dev = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.prefix_vt = (torch.zeros((c.layers, c.n_kv_heads, c.head_dim, c.max_seq), dtype=self.dtype,
                                       device=self.device) if shared_prefix else None)
+        # fused decode GEMMs for steps of <= fused_max_rows rows (GPU only;
+        # DMCP_FUSED_GEMM=0 forces the hipBLASLt path)
+        self.use_fused = self.device.type == "cuda" and os.environ.get("DMCP_FUSED_GEMM", "1") != "0"
+        self.fused_max_rows = min(ops.FUSED_MAX_ROWS, int(os.environ.get("DMCP_FUSED_MAX_ROWS", "32")))
         ps = ops.prefix_splits(c.max_seq, self.PREFIX_CHUNK) if shared_prefix else 0
         self.attn_ws = (ops.decode_workspace(self.max_rows, c.n_heads, c.n_kv_heads, c.head_dim, c.max_seq,
                                              self.device, prefix_slots=ps) if self.device.type == "cuda" else None)
@@ -192,6 +208,25 @@ class LocalLM:
             w[f"l{i}.wgu"] = rnd(2 * c.intermediate, c.hidden)
             w[f"l{i}.wdown"] = rnd(c.hidden, c.intermediate, std=out_std)
         return w
+
+    @torch.no_grad()
+    def _fold_norms(self) -> None:
+        """W'[n, k] = W[n, k] * g[k] for each RMSNorm weight g and the matrix
+        that consumes the normalised rows (ln1 -> wqkv, ln2 -> wgu, norm_f ->
+        lm_head); g becomes 1.  The model is unchanged (rms(x) * g . W^T ==
+        rms(x) . W'^T) and the fused GEMMs apply the norm as a per-row scale
+        of the accumulator.  Idempotent; a no-op for random-init weights."""
+        c = self.cfg
+        pairs = [("norm_f", "lm_head")]
+        for i in range(c.layers):
+            pairs += [(f"l{i}.ln1", f"l{i}.wqkv"), (f"l{i}.ln2", f"l{i}.wgu")]
+        for g_name, w_name in pairs:
+            g = self.w[g_name]
+            if bool((g == 1).all()):
+                continue
+            w = self.w[w_name]
+            self.w[w_name] = (w.float() * g.float()[None, :]).to(w.dtype).contiguous()
+            self.w[g_name] = torch.ones_like(g)
 
     @classmethod
     def load_safetensors(cls, path: str, device: str = "cuda", **cfg_overrides) -> "LocalLM":
@@ -286,6 +321,8 @@ class LocalLM:
         B = tokens.shape[0]
         if B > self.max_rows:
             raise ValueError(f"decode: {B} rows > max_rows {self.max_rows}")
+        if self.use_fused and B <= self.fused_max_rows:
+            return self._decode_fused(tokens, slots, positions)
         seq_len = positions + 1
         chunk, splits = ops.decode_plan(B, c.n_kv_heads, c.max_seq)
         x = ops.embedding(self.w["embed"], tokens)
@@ -295,16 +332,40 @@ class LocalLM:
             kc, vc = self.k_cache[i], self.v_cache[i]
             qkv = F.linear(h, self.w[f"l{i}.wqkv"])
             q = ops.rope_kv(qkv, positions, slots, self.cos_sin, kc, vc, c.n_heads)
-            prefix = (ops.SharedPrefix(kc[self.prefix_slot], self.prefix_vt[i], self.prefix_dev, self.PREFIX_CHUNK)
-                      if self.shared_prefix else None)
             att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws, chunk=chunk,
-                                       prefix=prefix, splits=splits)
+                                       prefix=self._prefix(i), splits=splits)
             o = F.linear(att.view(B, c.n_heads * c.head_dim), self.w[f"l{i}.wo"])
             h = ops.add_rmsnorm(o, self.w[f"l{i}.ln2"], c.eps, residual=resid)
             m = self._mlp(i, h)
             nxt = self.w[f"l{i + 1}.ln1"] if i + 1 < c.layers else self.w["norm_f"]
             h = ops.add_rmsnorm(m, nxt, c.eps, residual=resid)
         return F.linear(h, self.w["lm_head"])
+
+    def _prefix(self, i: int):
+        if not self.shared_prefix:
+            return None
+        return ops.SharedPrefix(self.k_cache[i][self.prefix_slot], self.prefix_vt[i], self.prefix_dev,
+                                self.PREFIX_CHUNK)
+
+    def _decode_fused(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:
+        """The decode step on the fused gfx950 GEMMs: per layer QKV (+norm,
+        RoPE, KV append) -> attention -> O (+residual) -> gate/up (+norm,
+        SwiGLU) -> down (+residual); the residual stream ``r`` is updated in
+        place by the O / down epilogues."""
+        c = self.cfg
+        B = tokens.shape[0]
+        seq_len = positions + 1
+        chunk, splits = ops.decode_plan(B, c.n_kv_heads, c.max_seq)
+        r = ops.embedding(self.w["embed"], tokens)
+        for i in range(c.layers):
+            kc, vc = self.k_cache[i], self.v_cache[i]
+            q = ops.fused_rope_kv(r, self.w[f"l{i}.wqkv"], c.eps, positions, slots, self.cos_sin, kc, vc, c.n_heads)
+            att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws, chunk=chunk,
+                                       prefix=self._prefix(i), splits=splits)
+            ops.fused_resid(att.view(B, c.n_heads * c.head_dim), self.w[f"l{i}.wo"], r)
+            act = ops.fused_swiglu(r, self.w[f"l{i}.wgu"], c.eps)
+            ops.fused_resid(act, self.w[f"l{i}.wdown"], r)
+        return ops.fused_linear_norm(r, self.w["lm_head"], c.eps)
 
     # ---------------------------------------------------------- shared prefix
     @torch.inference_mode()

@@ -36,6 +36,29 @@ def decode_plan(rows, n_kv_heads, max_seq):
     return _dp(rows, n_kv_heads, max_seq)
 
 
+FUSED_MAX_ROWS = 128  # row limit of the fused decode GEMMs (dmcp.ops.hip.FUSED_MAX_ROWS)
+
+
+def fused_rope_kv(x, w, eps, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out=None):
+    """RMSNorm -> QKV GEMM -> RoPE -> KV append in one gfx950 kernel (GPU only)."""
+    return _hip().fused_rope_kv(x, w, eps, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out)
+
+
+def fused_swiglu(x, w, eps, out=None):
+    """RMSNorm -> gate/up GEMM -> SwiGLU in one gfx950 kernel (GPU only)."""
+    return _hip().fused_swiglu(x, w, eps, out)
+
+
+def fused_resid(x, w, residual, wk: int = 0):
+    """residual += x . w^T in one gfx950 kernel (GPU only); K-split waves by K."""
+    return _hip().fused_resid(x, w, residual, wk or (16 if x.shape[1] >= 4096 else 8))
+
+
+def fused_linear_norm(x, w, eps, out=None):
+    """RMSNorm -> GEMM (bf16 out; the LM head) in one gfx950 kernel (GPU only)."""
+    return _hip().fused_linear_norm(x, w, eps, out)
+
+
 def decode_workspace(rows, n_heads, n_kv_heads, head_dim, max_seq, device, chunk: int = 256, prefix_slots: int = 0):
     """Split-K scratch of the decode-attention kernel (fp32 partials + max/sum)."""
     return _hip().decode_workspace(rows, n_heads, n_kv_heads, head_dim, max_seq, device, chunk, prefix_slots)

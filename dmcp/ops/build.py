@@ -13,7 +13,10 @@ import shutil
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = os.path.join(HERE, "csrc", "dmcp_kernels.hip")
+CSRC = os.path.join(HERE, "csrc")
+SRCS = [os.path.join(CSRC, "dmcp_kernels.hip"), os.path.join(CSRC, "fused_gemm.hip")]
+HEADERS = [os.path.join(CSRC, "dmcp_common.hpp")]
+SRC = SRCS[0]  # kept for callers that name the main source
 TARGET = os.path.join(HERE, "_hipops.so")
 STAMP = TARGET + ".stamp"
 ARCH = os.environ.get("DMCP_HIP_ARCH", "gfx950")
@@ -33,8 +36,9 @@ def hipcc() -> str:
 
 def _key() -> str:
     h = hashlib.sha256(" ".join(FLAGS).encode())
-    with open(SRC, "rb") as f:
-        h.update(f.read())
+    for path in SRCS + HEADERS:
+        with open(path, "rb") as f:
+            h.update(f.read())
     return h.hexdigest()[:16]
 
 
@@ -43,7 +47,7 @@ def build(force: bool = False) -> str:
     if not force and os.path.exists(TARGET) and os.path.exists(STAMP) and open(STAMP).read().strip() == key:
         return TARGET
     tmp = TARGET + ".tmp"
-    cmd = [hipcc(), *FLAGS, "-o", tmp, SRC]
+    cmd = [hipcc(), *FLAGS, f"-I{CSRC}", "-o", tmp, *SRCS]
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stdout}")

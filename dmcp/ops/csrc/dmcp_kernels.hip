@@ -14,59 +14,9 @@
 // ABI: extern "C" launchers taking raw device pointers and a hipStream_t;
 // they return hipError_t (0 = success).  Shapes are validated on the host
 // side (dmcp/ops/hip.py) before any launch.
-#include <hip/hip_runtime.h>
-#include <stdint.h>
+#include "dmcp_common.hpp"
 
 namespace {
-
-constexpr int kBlock = 256;
-constexpr int kWave = 64;
-
-__device__ __forceinline__ float bf2f(uint16_t v) {
-    return __uint_as_float(((uint32_t)v) << 16);
-}
-
-// round-to-nearest-even fp32 -> bf16 (NaN kept quiet)
-__device__ __forceinline__ uint16_t f2bf(float f) {
-    uint32_t u = __float_as_uint(f);
-    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return (uint16_t)(u >> 16);
-}
-
-__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
-    f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
-    f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
-    f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
-    f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
-}
-
-__device__ __forceinline__ uint4 pack8(const float* f) {
-    uint4 v;
-    v.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
-    v.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
-    v.z = (uint32_t)f2bf(f[4]) | ((uint32_t)f2bf(f[5]) << 16);
-    v.w = (uint32_t)f2bf(f[6]) | ((uint32_t)f2bf(f[7]) << 16);
-    return v;
-}
-
-__device__ __forceinline__ void unpack4(const uint2& v, float* f) {
-    f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
-    f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
-}
-
-__device__ __forceinline__ uint2 pack4(const float* f) {
-    uint2 v;
-    v.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
-    v.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
-    return v;
-}
-
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, kWave);
-    return v;
-}
 
 // Per-row split geometry, shared by the per-row kernels and the combine:
 // at most `splits` parts of >= `chunk` keys each, equal sizes rounded up to
@@ -98,16 +48,30 @@ __global__ __launch_bounds__(kBlock) void add_rmsnorm_kernel(const uint16_t* __r
     const int nvec = H >> 3;
     const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)row * H);
     uint4* rr = residual ? reinterpret_cast<uint4*>(residual + (size_t)row * H) : nullptr;
+    const uint4* wr = reinterpret_cast<const uint4*>(w);
+    // every global load (x, residual, weight) issued before the first use:
+    // one memory round trip per launch instead of three (decode rows are few,
+    // so the kernel is latency-, not bandwidth-bound)
+    uint4 xv[VPT], rv[VPT], wv[VPT];
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int idx = threadIdx.x + i * kBlock;
+        if (idx < nvec) {
+            xv[i] = xr[idx];
+            rv[i] = rr ? rr[idx] : make_uint4(0, 0, 0, 0);
+            wv[i] = wr[idx];
+        }
+    }
     float h[VPT][8];
     float ss = 0.f;
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
         const int idx = threadIdx.x + i * kBlock;
         if (idx < nvec) {
-            unpack8(xr[idx], h[i]);
+            unpack8(xv[i], h[i]);
             if (rr) {
                 float r[8];
-                unpack8(rr[idx], r);
+                unpack8(rv[i], r);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) h[i][j] += r[j];
                 uint4 packed = pack8(h[i]);
@@ -126,14 +90,13 @@ __global__ __launch_bounds__(kBlock) void add_rmsnorm_kernel(const uint16_t* __r
 #pragma unroll
     for (int k = 0; k < kBlock / kWave; ++k) tot += red[k];
     const float inv = rsqrtf(tot / (float)H + eps);
-    const uint4* wr = reinterpret_cast<const uint4*>(w);
     uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * H);
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
         const int idx = threadIdx.x + i * kBlock;
         if (idx < nvec) {
             float wf[8], o[8];
-            unpack8(wr[idx], wf);
+            unpack8(wv[i], wf);
 #pragma unroll
             for (int j = 0; j < 8; ++j) o[j] = h[i][j] * inv * wf[j];
             orow[idx] = pack8(o);
@@ -395,50 +358,55 @@ __global__ __launch_bounds__(kBlock) void decode_attn_kernel(
     }  // work items
 }
 
-// Split-K merge.  One thread per 4 consecutive outputs (b, q head, d..d+3):
-// float4 partial loads, issued 8 splits at a time before any of them is
-// merged, so a row with ~20 partials (shared prefix + suffix splits) waits
-// for 3 memory round trips instead of one per 4 partials.  Rows whose
-// context fits one split (nact <= 1, no prefix) were written directly.
-// (A fused "last block merges" variant needs agent-scope release fences; on
-// gfx950 each one writes back the XCD's L2 and made the kernel ~10x slower
-// -- profiles/ROUND1_NOTES.md.)
+// Split-K merge.  One wave per (row, q head): lane = (4-output group
+// dg = lane % (D/4), partial group pg = lane / (D/4)); each lane merges
+// every (64/(D/4))-th partial with float4 loads issued 8 at a time, then
+// the partial groups are merged across lanes with two shuffles.  A row's
+// ~20 partials (shared-prefix splits + suffix splits) cost one memory
+// round trip, on 4x more waves than a thread-per-output merge (which was
+// latency-bound at 8-12 us per layer -- profiles/decode_step_r2_*).
+// Rows whose context fits one split (nact <= 1, no prefix) were written
+// directly.  (A fused "last block merges" variant needs agent-scope release
+// fences; on gfx950 each one writes back the XCD's L2 and made the kernel
+// ~10x slower -- profiles/ROUND1_NOTES.md.)
+template <int D>
 __global__ __launch_bounds__(kBlock) void decode_attn_combine_kernel(const float* __restrict__ part_o,
                                                                     const float* __restrict__ part_ml,
                                                                     const int32_t* __restrict__ slot,
                                                                     const int32_t* __restrict__ seq_len,
                                                                     uint16_t* __restrict__ out, int B, int Hq,
-                                                                    int D, int max_seq, int chunk, int splits,
+                                                                    int max_seq, int chunk, int splits,
                                                                     int num_slots, const int32_t* __restrict__ plen,
                                                                     int ps_max, int pchunk) {
     constexpr int U = 8;
-    const int dq = D / 4;
-    const long total = (long)B * Hq * dq;
+    constexpr int DQ = D / 4;       // lanes per partial group
+    constexpr int PG = kWave / DQ;  // partial groups per wave
+    const int lane = threadIdx.x & (kWave - 1);
+    const int dg = lane % DQ, pg = lane / DQ;
     const int P = plen ? max(0, *plen) : 0;
     const int splits_total = ps_max + splits;
-    for (long u = (long)blockIdx.x * kBlock + threadIdx.x; u < total; u += (long)gridDim.x * kBlock) {
-        const int b = (int)(u / ((long)Hq * dq));
-        const int rem = (int)(u - (long)b * Hq * dq);
-        const int qh = rem / dq, d = (rem - qh * dq) * 4;
+    const int npre = P > 0 ? min(ps_max, (P + pchunk - 1) / pchunk) : 0;  // prefix partials
+    const int nwaves = gridDim.x * (kBlock / kWave);
+    for (int w = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave; w < B * Hq; w += nwaves) {
+        const int b = w / Hq, qh = w - b * Hq;
         const int s = slot[b];
         const int L = (s >= 0 && s < num_slots) ? min(seq_len[b], max_seq) : 0;
         if (L <= 0) continue;  // padding row: zeroed by the main kernel
         const int nact = split_geom(L - P, splits, chunk).nact;
-        const int npre = P > 0 ? min(ps_max, (P + pchunk - 1) / pchunk) : 0;  // prefix partials
         if (npre == 0 && nact <= 1) continue;  // written directly by the main kernel
         const int n = npre + nact;
         const size_t base = ((size_t)b * Hq + qh) * splits_total;
         float m = -1e30f, lt = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-        for (int i0 = 0; i0 < n; i0 += U) {
+        for (int i0 = pg; i0 < n; i0 += U * PG) {
             float2 ml[U];
             float4 o4[U];
 #pragma unroll
             for (int j = 0; j < U; ++j) {
-                const int i = i0 + j;
+                const int i = i0 + j * PG;
                 const size_t idx = base + (i < npre ? i : ps_max + (i - npre));
                 if (i < n) {
                     ml[j] = *reinterpret_cast<const float2*>(part_ml + idx * 2);
-                    o4[j] = *reinterpret_cast<const float4*>(part_o + idx * D + d);
+                    o4[j] = *reinterpret_cast<const float4*>(part_o + idx * D + 4 * dg);
                 } else {
                     ml[j] = make_float2(-1e30f, 0.f);
                     o4[j] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -457,9 +425,24 @@ __global__ __launch_bounds__(kBlock) void decode_attn_combine_kernel(const float
             }
             m = mn;
         }
-        const float inv = lt > 0.f ? 1.f / lt : 0.f;
-        const float f[4] = {a0 * inv, a1 * inv, a2 * inv, a3 * inv};
-        *reinterpret_cast<uint2*>(out + ((size_t)b * Hq + qh) * D + d) = pack4(f);
+        // merge the PG partial groups (lanes dg, dg + DQ, ...)
+#pragma unroll
+        for (int msk = DQ; msk < kWave; msk <<= 1) {
+            const float mo = __shfl_xor(m, msk, kWave);
+            const float mn = fmaxf(m, mo);
+            const float ca = exp2f(m - mn), cb = exp2f(mo - mn);
+            lt = lt * ca + __shfl_xor(lt, msk, kWave) * cb;
+            a0 = a0 * ca + __shfl_xor(a0, msk, kWave) * cb;
+            a1 = a1 * ca + __shfl_xor(a1, msk, kWave) * cb;
+            a2 = a2 * ca + __shfl_xor(a2, msk, kWave) * cb;
+            a3 = a3 * ca + __shfl_xor(a3, msk, kWave) * cb;
+            m = mn;
+        }
+        if (pg == 0) {
+            const float inv = lt > 0.f ? 1.f / lt : 0.f;
+            const float f[4] = {a0 * inv, a1 * inv, a2 * inv, a3 * inv};
+            *reinterpret_cast<uint2*>(out + ((size_t)b * Hq + qh) * D + 4 * dg) = pack4(f);
+        }
     }
 }
 
@@ -487,11 +470,7 @@ __global__ __launch_bounds__(kBlock) void decode_attn_combine_kernel(const float
 //    Output: fp32 partials (log2-domain max, sum) at split index
 //    [0, ps_max), merged by decode_attn_combine_kernel.
 // --------------------------------------------------------------------------
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef float f32x16_t __attribute__((ext_vector_type(16)));
-typedef float f32x8_t __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ bf16x8_t as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8_t, v); }
 
 constexpr int kPrefixChunk = 256;  // keys per prefix split (host passes the same)
 
@@ -742,8 +721,6 @@ __global__ __launch_bounds__(kBlock) void embedding_kernel(const uint16_t* __res
     }
 }
 
-typedef short v4i16_t __attribute__((ext_vector_type(4)));
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 // One 32-key tile of a (slot, kv head): K rows as the S^T A operand (key
 // kt + 16h + (lane&15), dims 32ks + 8*(lane>>4)) and the V tile (32 x D,
@@ -1029,9 +1006,19 @@ inline int grid_for(size_t work) {
 hipError_t launch_combine(void* part_o, void* part_ml, const int32_t* sl, const int32_t* ln, void* out, int B, int Hq,
                           int D, int max_seq, int chunk, int splits, int num_slots, const int32_t* pl, int ps_max,
                           int pchunk, hipStream_t st) {
-    decode_attn_combine_kernel<<<grid_for((size_t)B * Hq * (D / 4)), kBlock, 0, st>>>(
-        (const float*)part_o, (const float*)part_ml, sl, ln, (uint16_t*)out, B, Hq, D, max_seq, chunk, splits,
-        num_slots, pl, ps_max, pchunk);
+    const int waves = B * Hq;
+    const int blocks = (waves + 3) / 4;
+    const dim3 grid((unsigned)(blocks < 2048 ? blocks : 2048));
+    if (D == 64)
+        decode_attn_combine_kernel<64><<<grid, kBlock, 0, st>>>((const float*)part_o, (const float*)part_ml, sl, ln,
+                                                               (uint16_t*)out, B, Hq, max_seq, chunk, splits,
+                                                               num_slots, pl, ps_max, pchunk);
+    else if (D == 128)
+        decode_attn_combine_kernel<128><<<grid, kBlock, 0, st>>>((const float*)part_o, (const float*)part_ml, sl, ln,
+                                                                (uint16_t*)out, B, Hq, max_seq, chunk, splits,
+                                                                num_slots, pl, ps_max, pchunk);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

@@ -57,6 +57,9 @@ def lib() -> ctypes.CDLL:
             "dmcp_masked_argmax": ([_vp, _vp, _vp, _i, _vp, _i, _i, _i, _vp], _i),
             "dmcp_embedding": ([_vp, _vp, _vp, _i, _i, _i, _vp], _i),
             "dmcp_set_decode_impl": ([_i], _i),
+            "dmcp_fused_gemm_max_rows": ([], _i),
+            "dmcp_fused_gemm": ([_i, _i, _vp, _vp, _vp, _i, _i, _i, _f, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i,
+                                 _i, _i, _i, _vp], _i),
         }
         for name, (args, res) in sigs.items():
             fn = getattr(L, name)
@@ -335,4 +338,94 @@ def embedding(table: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor
     out = torch.empty((T, H), dtype=torch.bfloat16, device=table.device) if out is None else out
     _req_out(out, torch.bfloat16, T * H, "embedding.out")
     _check(lib().dmcp_embedding(_ptr(table), _ptr(ids), _ptr(out), T, H, V, _stream()), "dmcp_embedding")
+    return out
+
+
+# ------------------------------------------------------------------ fused GEMMs
+FUSED_EPI = {"rope_kv": 0, "swiglu": 1, "resid": 2, "bf16": 3}
+FUSED_MAX_ROWS = 128  # dmcp_fused_gemm_max_rows()
+
+
+def _fused_xw(x: torch.Tensor, w: torch.Tensor, name: str) -> tuple:
+    _req(x, torch.bfloat16, f"{name}.x")
+    _req(w, torch.bfloat16, f"{name}.w")
+    if x.dim() != 2 or w.dim() != 2 or x.shape[1] != w.shape[1]:
+        raise HipOpsError(f"{name}: x {tuple(x.shape)} / w {tuple(w.shape)} are not [M, K] / [N, K]")
+    M, K = x.shape
+    if not 1 <= M <= FUSED_MAX_ROWS or K % 32:
+        raise HipOpsError(f"{name}: needs 1 <= M <= {FUSED_MAX_ROWS} rows and K % 32 == 0 (M={M}, K={K})")
+    return M, K, w.shape[0]
+
+
+def _fused(epi: str, wk: int, x, w, out, M, K, N, eps=0.0, inter=0, pos=None, slot=None, cos_sin=None,
+           q_out=None, k_cache=None, v_cache=None, Hq=0, Hkv=0, D=0, max_seq=0, max_pos=0, num_slots=0) -> None:
+    if wk not in (4, 8, 16):
+        raise HipOpsError(f"fused_gemm: wk must be 4, 8 or 16 (got {wk})")
+    _check(lib().dmcp_fused_gemm(FUSED_EPI[epi], wk, _ptr(x), _ptr(w), _ptr(out), M, K, N, float(eps), inter,
+                                 _ptr(pos), _ptr(slot), _ptr(cos_sin), _ptr(q_out), _ptr(k_cache), _ptr(v_cache),
+                                 Hq, Hkv, D, max_seq, max_pos, num_slots, _stream()), f"dmcp_fused_gemm[{epi}]")
+
+
+def fused_rope_kv(x: torch.Tensor, w: torch.Tensor, eps: float, pos: torch.Tensor, slot: torch.Tensor,
+                  cos_sin: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, n_q_heads: int,
+                  q_out: Optional[torch.Tensor] = None, wk: int = 8) -> torch.Tensor:
+    """q = RoPE(rms(x) . w[:Hq*D]^T); RoPE(k) and v appended to the KV cache at
+    (slot[m], :, pos[m]) -- the RMSNorm weight must be folded into ``w``.
+    x [M, K]; w [(Hq + 2 Hkv) D, K]; caches [S, Hkv, MAXS, D].  Returns q [M, Hq, D]."""
+    M, K, N = _fused_xw(x, w, "fused_rope_kv")
+    S, Hkv, MAXS, D = k_cache.shape
+    _req(k_cache, torch.bfloat16, "fused_rope_kv.k_cache")
+    _req(v_cache, torch.bfloat16, "fused_rope_kv.v_cache")
+    _req(pos, torch.int32, "fused_rope_kv.pos")
+    _req(slot, torch.int32, "fused_rope_kv.slot")
+    _req(cos_sin, torch.float32, "fused_rope_kv.cos_sin")
+    if (v_cache.shape != k_cache.shape or N != (n_q_heads + 2 * Hkv) * D or D % 32 or pos.numel() != M
+            or slot.numel() != M or cos_sin.dim() != 3 or tuple(cos_sin.shape[1:]) != (D // 2, 2)):
+        raise HipOpsError(f"fused_rope_kv: shape mismatch (w {tuple(w.shape)}, cache {tuple(k_cache.shape)}, "
+                          f"Hq {n_q_heads}, cos_sin {tuple(cos_sin.shape)})")
+    if q_out is None:
+        q_out = torch.empty((M, n_q_heads, D), dtype=torch.bfloat16, device=x.device)
+    _req_out(q_out, torch.bfloat16, M * n_q_heads * D, "fused_rope_kv.q_out")
+    _fused("rope_kv", wk, x, w, None, M, K, N, eps, pos=pos, slot=slot, cos_sin=cos_sin, q_out=q_out,
+           k_cache=k_cache, v_cache=v_cache, Hq=n_q_heads, Hkv=Hkv, D=D, max_seq=MAXS,
+           max_pos=cos_sin.shape[0], num_slots=S)
+    return q_out
+
+
+def fused_swiglu(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None,
+                 wk: int = 4) -> torch.Tensor:
+    """silu(rms(x) . w[:I]^T) * (rms(x) . w[I:]^T); w [2I, K] (norm weight folded in)."""
+    M, K, N = _fused_xw(x, w, "fused_swiglu")
+    if N % 32:
+        raise HipOpsError(f"fused_swiglu: 2I = {N} must be a multiple of 32")
+    inter = N // 2
+    if out is None:
+        out = torch.empty((M, inter), dtype=torch.bfloat16, device=x.device)
+    _req_out(out, torch.bfloat16, M * inter, "fused_swiglu.out")
+    _fused("swiglu", wk, x, w, out, M, K, N, eps, inter=inter)
+    return out
+
+
+def fused_resid(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, wk: int = 8) -> torch.Tensor:
+    """residual += x . w^T (in place, bf16); x [M, K], w [N, K], residual [M, N]."""
+    M, K, N = _fused_xw(x, w, "fused_resid")
+    if N % 16:
+        raise HipOpsError(f"fused_resid: N = {N} must be a multiple of 16")
+    _req(residual, torch.bfloat16, "fused_resid.residual")
+    if tuple(residual.shape) != (M, N):
+        raise HipOpsError(f"fused_resid: residual {tuple(residual.shape)} != {(M, N)}")
+    _fused("resid", wk, x, w, residual, M, K, N)
+    return residual
+
+
+def fused_linear_norm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None,
+                      wk: int = 16) -> torch.Tensor:
+    """rms(x) . w^T in bf16 (norm weight folded into w); the LM head."""
+    M, K, N = _fused_xw(x, w, "fused_linear_norm")
+    if N % 16:
+        raise HipOpsError(f"fused_linear_norm: N = {N} must be a multiple of 16")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    _req_out(out, torch.bfloat16, M * N, "fused_linear_norm.out")
+    _fused("bf16", wk, x, w, out, M, K, N, eps)
     return out

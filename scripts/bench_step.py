@@ -52,6 +52,7 @@ def main(argv=None) -> int:
     model = LocalLM(cfg, device="cuda:0")
     if a.fused >= 0:
         model.use_fused = bool(a.fused)
+        model.fused_max_rows = 128 if a.fused else 0
     eng = LocalEngine(model)
     g = torch.Generator().manual_seed(0)
     if a.prefix:

@@ -61,11 +61,23 @@ def configure_logging(level: str = "INFO", stream=None) -> None:
     configure_logging._done = True  # type: ignore[attr-defined]
 
 
+def open_database(config: Config):
+    """The store named by the configuration: PostgreSQL when ``database_url``
+    is a PostgreSQL URL (the reference's own database), else SQLite at
+    ``db_path``."""
+    if config.database_url:
+        from .store.pg import PgDatabase
+        db = PgDatabase.from_url(config.database_url, config.database_username, config.database_password)
+        LOG.info("Store: %s", db.describe())
+        return db
+    return Database(config.db_path)
+
+
 class App:
     def __init__(self, config: Optional[Config] = None, *, backend: Optional[EnrichmentBackend] = None,
                  load_graphs: bool = True, db: Optional[Database] = None) -> None:
         self.config = config or Config.from_env()
-        self.db = db or Database(self.config.db_path)
+        self.db = db or open_database(self.config)
         self.repos = Repositories(self.db)
         self.cache = GraphCache(self.repos.projects)
         self.git = GitClient(self.config.git_clone_base_path, self.config.git_ssh_key_path,

@@ -19,9 +19,15 @@ DEFAULT_CLAUDE_MODEL = "claude-sonnet-4-5-20250929"
 
 @dataclass
 class Config:
-    # storage (application.yml:11-29); DATABASE_URL may be sqlite:///path or a path
+    # storage (application.yml:11-29).  DATABASE_URL may be sqlite:///path, a
+    # path, or PostgreSQL (postgresql://u:p@h:5432/db?currentSchema=s or the
+    # reference's jdbc:postgresql://h:5432/db form + DATABASE_USERNAME /
+    # DATABASE_PASSWORD): then database_url is set and db_path is unused
     db_path: str = field(default_factory=lambda: os.path.join(
         os.path.expanduser("~"), ".dmcp", "dmcp.db"))
+    database_url: Optional[str] = None
+    database_username: Optional[str] = None
+    database_password: Optional[str] = None
     # HTTP (application.yml:1-5)
     server_port: int = 8080
     server_host: str = "127.0.0.1"
@@ -109,7 +115,13 @@ class Config:
                 updates[attr] = env[key]
         db_url = env.get("DATABASE_URL")
         if db_url and "DMCP_DB_PATH" not in env:
-            updates["db_path"] = sqlite_path_from_url(db_url)
+            if is_postgres_url(db_url):
+                updates["database_url"] = db_url
+            else:
+                updates["db_path"] = sqlite_path_from_url(db_url)
+        for key, attr in (("DATABASE_USERNAME", "database_username"), ("DATABASE_PASSWORD", "database_password")):
+            if env.get(key):
+                updates[attr] = env[key]
         return cfg.merged(updates)
 
     def merged(self, values: Dict[str, Any]) -> "Config":
@@ -132,15 +144,20 @@ class Config:
         return b
 
 
+def is_postgres_url(url: Optional[str]) -> bool:
+    return bool(url) and url.startswith(("postgresql://", "postgres://", "jdbc:postgresql://"))
+
+
 def sqlite_path_from_url(url: str) -> str:
     if url.startswith("sqlite:///"):
         # SQLAlchemy convention: sqlite:///relative.db, sqlite:////absolute.db
         return url[len("sqlite:///"):]
     if url.startswith("sqlite://"):
         return url[len("sqlite://"):]
-    if url.startswith("jdbc:") or url.startswith("postgres"):
-        raise ValueError("PostgreSQL URLs are not supported on this host (no driver); "
-                         "use sqlite:///path or DMCP_DB_PATH")
+    if is_postgres_url(url):
+        raise ValueError("a PostgreSQL URL names no SQLite file; set it as DATABASE_URL (Config.database_url)")
+    if url.startswith("jdbc:"):
+        raise ValueError(f"unsupported JDBC URL {url!r}: only jdbc:postgresql:// is")
     return url
 
 

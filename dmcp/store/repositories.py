@@ -179,7 +179,7 @@ class SourceClassRepository:
     FIND_BY_FULL_CLASS_NAME = (
         "SELECT c.* FROM source_classes c JOIN projects p ON p.id = c.project_id "
         "WHERE c.full_class_name = ? "
-        "ORDER BY p.last_analyzed_at DESC, p.created_at DESC")
+        "ORDER BY p.last_analyzed_at DESC NULLS LAST, p.created_at DESC")
     # range form of "package_name LIKE 'p.%'" (what text_pattern_ops gives the
     # reference on Postgres): SQLite only uses an index for LIKE under
     # case_sensitive_like, a range always can
@@ -263,7 +263,7 @@ class SourceClassRepository:
             else:
                 q = (f"SELECT c.* FROM source_classes c JOIN projects p ON p.id = c.project_id "
                      f"WHERE c.full_class_name IN ({marks}) "
-                     f"ORDER BY p.last_analyzed_at DESC, p.created_at DESC")
+                     f"ORDER BY p.last_analyzed_at DESC NULLS LAST, p.created_at DESC")
                 rows = self.db.query(q, chunk)
             for r in rows:
                 if r["full_class_name"] not in out:
@@ -640,7 +640,7 @@ class ProjectRowsWriter:
         self._keep: List[object] = []
         if self._sync:
             return
-        bulk = _native_bulk_writer()
+        bulk = _native_bulk_writer() if getattr(repos.db, "native_bulk", True) else None
         if bulk is not None:
             setup = []
             if replace:

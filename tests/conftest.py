@@ -66,3 +66,12 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture
+def pg_server(tmp_path):
+    """A PostgreSQL wire-protocol server (tests/pgfake.py) on a fresh SQLite
+    file, SCRAM-SHA-256 authentication."""
+    from tests.pgfake import FakePgServer
+    with FakePgServer(str(tmp_path / "pg.sqlite"), auth="scram") as srv:
+        yield srv

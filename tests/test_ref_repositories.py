@@ -4,9 +4,11 @@ Mirrors ``project/domain/ProjectRepositoryIntegrationTest.java`` (9),
 ``analysis/domain/SourceClassRepositoryIntegrationTest.java`` (9) and
 ``analysis/domain/SourceMethodRepositoryIntegrationTest.java`` (11) (under
 ``src/test/java/co/fanki/domainmcp/``).  The reference runs them against a
-Testcontainers ``postgres:14`` with Flyway V1-V8; here against a fresh SQLite
-file with the same final schema (``dmcp/store/db.py``).  Unlike the
-reference's (CI-excluded) integration tests, these run on every CPU pass.
+Testcontainers ``postgres:14`` with Flyway V1-V8; here every case runs twice:
+on a fresh SQLite file with the same final schema (``dmcp/store/db.py``) and
+on the PostgreSQL store (``dmcp/store/pg.py``) over the wire protocol, served
+by ``tests/pgfake.py``.  Unlike the reference's (CI-excluded) integration
+tests, these run on every CPU pass.
 """
 import pytest
 
@@ -15,11 +17,19 @@ from dmcp.store.db import Database
 from dmcp.store.repositories import Repositories
 
 
-@pytest.fixture
-def repos(tmp_path):
-    db = Database(str(tmp_path / "repo.db"))
-    yield Repositories(db)
-    db.close()
+@pytest.fixture(params=["sqlite", "postgres"])
+def repos(request, tmp_path):
+    if request.param == "sqlite":
+        db = Database(str(tmp_path / "repo.db"))
+        yield Repositories(db)
+        db.close()
+        return
+    from dmcp.store.pg import PgDatabase
+    from tests.pgfake import FakePgServer
+    with FakePgServer(str(tmp_path / "pg.sqlite"), auth="md5") as srv:
+        db = PgDatabase.from_url(srv.url())
+        yield Repositories(db)
+        db.close()
 
 
 def new_project(name="Test Project", url="https://github.com/test/repo.git"):

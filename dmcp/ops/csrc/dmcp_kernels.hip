@@ -870,6 +870,11 @@ __device__ __forceinline__ void attn_tile_mfma(KVTile<D>& cur, bool prefetch, in
 //    so that ~16 waves per CU are busy, and each wave keeps TWO tiles of
 //    K/V loads in flight (register double buffer, D = 64) while it computes
 //    a third.
+//    Measured and not adopted (profiles/decode_step_r2_notes.md): merging a
+//    sequence's jump-forward rows into one work item (their keys read once)
+//    gained nothing -- those re-reads already hit L2 / MALL -- and its extra
+//    per-item work cost 2 %; a branch-free steady-state loop cut VALU
+//    instructions per tile but not time (the kernel waits on memory).
 //    No block-level synchronisation: each wave owns its LDS tile, so
 //    different waves of a block run different items.
 // --------------------------------------------------------------------------

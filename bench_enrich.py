@@ -34,6 +34,8 @@ def main(argv=None) -> int:
                     help="prefill and attend to the instructions + README per class instead of once")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-jump", action="store_true", help="disable jump-forward over forced tokens")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="synchronous engine loop (host waits for every step's ids before building the next)")
     ap.add_argument("--warmup", type=int, default=8)
     args = ap.parse_args(argv)
 
@@ -54,7 +56,7 @@ def main(argv=None) -> int:
     cfg = preset(args.preset, max_batch=args.batch, max_seq=args.max_seq)
     model = LocalLM(cfg, device=f"cuda:{local}", seed=rank)
     eng = LocalEngine(model, use_graphs=not args.no_graphs, jump_forward=not args.no_jump,
-                      shared_prefix=not args.no_shared_prefix)
+                      shared_prefix=not args.no_shared_prefix, pipeline=not args.no_pipeline)
     para = ("The shop platform sells products to retail customers. Orders move from CART to PAID to "
             "SHIPPED; payments are captured through the payment gateway and refunds are issued by the "
             "back office. Inventory is reserved when an order is paid and released on cancellation.\n\n")
@@ -104,7 +106,8 @@ def main(argv=None) -> int:
             "config": {"model": cfg.name, "params_b": round(cfg.param_count() / 1e9, 3), "batch": args.batch,
                        "max_seq": args.max_seq, "prompt_chars": args.prompt_chars,
                        "readme_chars": args.readme_chars, "graphs": not args.no_graphs,
-                       "jump_forward": not args.no_jump, "shared_prefix": not args.no_shared_prefix},
+                       "jump_forward": not args.no_jump, "shared_prefix": not args.no_shared_prefix,
+                       "pipeline": not args.no_pipeline},
             "shared_prefix_tokens": st["prefix_tokens"], "prefix_ms": round(1e3 * st["prefix_s"], 3),
             "generated_tokens_per_s": round(gen_all / elapsed, 1),
             "prompt_tokens_per_s": round(prompt_all / elapsed, 1),

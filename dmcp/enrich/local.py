@@ -21,6 +21,11 @@ per class) but generates on the local GPU:
 * each step is one H2D copy, one hipGraph replay (:class:`DecodeGraphs`:
   forward + gfx950 masked argmax with a per-row grammar-mask index) and one
   small D2H copy of the selected ids;
+* **one-step pipeline** -- step t+1 is launched before step t's ids reach
+  the host: a row whose token is step t's selection names its source row and
+  the graph gathers it on the device; the host runs the grammar state machine
+  for step t while the GPU computes step t+1, so host bookkeeping (~0.3 ms
+  per step) leaves the critical path;
 * multi-GPU: one engine (replica) per GPU, classes sharded across replicas
   (:mod:`dmcp.parallel.replicas`) -- pure data parallelism, no collectives
   (SURVEY §5.8).
@@ -128,6 +133,7 @@ class _Seq:
     free_len: int = 0
     forced_off: int = 0
     next_token: int = -1               # token to feed at the next decode step
+    next_src: int = -1                 # ... or: row of the last launched step whose selection it is
     out: bytearray = field(default_factory=bytearray)
     done: bool = False
     prompt_tokens: int = 0
@@ -150,7 +156,7 @@ class LocalEngine:
     MIN_SHARED_PREFIX = 64  # tokens; shorter common prefixes are not worth a separate prefill
 
     def __init__(self, model: LocalLM, use_graphs: bool = True, max_prompt_tokens: Optional[int] = None,
-                 jump_forward: bool = True, shared_prefix: bool = True) -> None:
+                 jump_forward: bool = True, shared_prefix: bool = True, pipeline: bool = True) -> None:
         self.model = model
         self.cfg: LMConfig = model.cfg
         dev = model.device
@@ -161,6 +167,13 @@ class LocalEngine:
         self.jump_forward = jump_forward
         self.shared_prefix = shared_prefix and model.shared_prefix
         self.max_rows = model.max_rows
+        self.pipeline = pipeline
+        # previous step's selections for host-less gathers (graphs keep their own)
+        self._last_ids = self.graphs.last_ids if self.graphs is not None else \
+            torch.zeros(self.max_rows, dtype=torch.int32, device=dev)
+        # pinned double buffer for the ids of the last two launched steps
+        self._host_ids = [torch.zeros(self.max_rows, dtype=torch.int32, pin_memory=dev.type == "cuda")
+                          for _ in range(2)]
         self.stats = {"prompt_tokens": 0, "generated_tokens": 0, "decode_steps": 0, "decode_rows": 0,
                       "prefills": 0, "decode_s": 0.0, "prefill_s": 0.0, "prefix_tokens": 0, "prefix_s": 0.0}
         self._lock = threading.Lock()
@@ -313,7 +326,10 @@ class LocalEngine:
             self.stats["prefix_s"] += time.perf_counter() - t0
             self.stats["prefix_tokens"] += prefix
         try:
-            self._run(pending, prompts, prefix, results)
+            if self.pipeline:
+                self._run_pipelined(pending, prompts, prefix, results)
+            else:
+                self._run(pending, prompts, prefix, results)
         finally:
             if prefix:
                 self.model.clear_prefix()
@@ -373,6 +389,125 @@ class LocalEngine:
                 else:
                     still.append(s)
             active = still
+
+
+    # ------------------------------------------------------ pipelined loop
+    def _launch(self, toks: List[int], slots: List[int], poss: List[int], mrows: List[int],
+                srcs: List[int], buf: int):
+        """Launches one step; enqueues the copy of its ids to pinned buffer
+        ``buf``; returns the event that completes with that copy."""
+        if self.graphs is not None:
+            _, ids = self.graphs.run(toks, slots, poss, mrows, srcs)
+        else:
+            dev = self.model.device
+            t = torch.tensor([toks, slots, poss, mrows, srcs], dtype=torch.int32, device=dev)
+            _, ids = self.model.decode_select_gather(t[0].contiguous(), t[4].contiguous(), self._last_ids,
+                                                     t[1].contiguous(), t[2].contiguous(), self.masks,
+                                                     t[3].contiguous())
+        n = len(toks)
+        host = self._host_ids[buf]
+        host[:n].copy_(ids[:n], non_blocking=self.model.device.type == "cuda")
+        if self.model.device.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+            return ev
+        return None
+
+    def _speculative_mask(self, s: _Seq) -> int:
+        """Mask row for a row whose token is still on the device (a free-text
+        selection): the state after feeding any token but the closing quote
+        -- the only case in which this row's own selection is used."""
+        seg = s.segs[s.seg]
+        return self.MASK_QUOTE if s.free_len + 1 >= seg.min_len else self.MASK_NO_QUOTE
+
+    def _run_pipelined(self, pending: Deque[_Seq], prompts: Dict[int, List[int]], prefix: int,
+                       results: Dict[int, str]) -> None:
+        """Continuous batching with the host one step behind the device.
+
+        Each iteration builds step k's rows from the state known after
+        step k-1's inputs: a sequence whose next token is step k-1's
+        selection gets ONE gathered row (its mask row assumes the token is
+        not the closing quote -- if it is, that row's own selection is simply
+        not used); every other sequence gets its literal token and, with
+        jump-forward, the decided tokens after it.  Step k is launched, and
+        only then does the host wait for step k-1's ids and run the grammar
+        transitions of step k's gathered rows -- while the GPU computes
+        step k.  The price: forced bytes that follow a sampled closing quote
+        start one step later than in :meth:`_run`."""
+        cfg = self.cfg
+        free_slots = list(range(cfg.max_batch - 1, -1, -1))
+        active: List[_Seq] = []
+        prev_event = None
+        prev_buf = 1
+        while pending or active:
+            while pending and free_slots:
+                s = pending.popleft()
+                if self._admit(s, prompts.pop(s.index), prefix, results, free_slots):
+                    active.append(s)
+            if not active:
+                continue
+            t0 = time.perf_counter()
+            toks: List[int] = []
+            slots: List[int] = []
+            poss: List[int] = []
+            mrows: List[int] = []
+            srcs: List[int] = []
+            gathered: List[Tuple[_Seq, int, int]] = []  # (seq, row, source row of the previous step)
+            spare = self.max_rows - len(active)
+            for s in active:
+                if s.next_src >= 0:
+                    gathered.append((s, len(toks), s.next_src))
+                    toks.append(0)
+                    slots.append(s.slot)
+                    poss.append(s.pos)
+                    mrows.append(self._speculative_mask(s))
+                    srcs.append(s.next_src)
+                    s.next_src = -1
+                    continue
+                tok = s.next_token
+                while True:
+                    toks.append(tok)
+                    slots.append(s.slot)
+                    poss.append(s.pos)
+                    mrows.append(self.MASK_NO_QUOTE)
+                    srcs.append(-1)
+                    q = self._after_feed(s, tok)
+                    if s.done:
+                        break
+                    if q is not None:  # this row's selection is the next token
+                        mrows[-1] = self.MASK_QUOTE if q else self.MASK_NO_QUOTE
+                        s.next_src = len(toks) - 1
+                        break
+                    if not self.jump_forward or spare <= 0:
+                        break
+                    spare -= 1
+                    tok = s.next_token
+            buf = 1 - prev_buf
+            event = self._launch(toks, slots, poss, mrows, srcs, buf)
+            # the previous step's ids: the tokens this step's gathered rows fed
+            if gathered:
+                if prev_event is not None:
+                    prev_event.synchronize()
+                ids = self._host_ids[prev_buf]
+                for s, row, src in gathered:
+                    q = self._after_feed(s, int(ids[src]))
+                    if not s.done and q is not None:
+                        s.next_src = row  # its selection in the step just launched
+            prev_event, prev_buf = event, buf
+            self.stats["decode_s"] += time.perf_counter() - t0
+            self.stats["decode_steps"] += 1
+            self.stats["decode_rows"] += len(toks)
+            self.stats["generated_tokens"] += len(toks)
+            still = []
+            for s in active:
+                if s.done:
+                    results[s.index] = s.out.decode("utf-8", "replace")
+                    free_slots.append(s.slot)
+                else:
+                    still.append(s)
+            active = still
+        if prev_event is not None:
+            prev_event.synchronize()
 
 
 class LocalLLMBackend(EnrichmentBackend):

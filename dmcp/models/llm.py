@@ -414,6 +414,22 @@ class LocalLM:
         ids = ops.masked_argmax(logits, masks, vocab=self.cfg.vocab_size, mask_idx=mask_idx)
         return logits, ids
 
+    def decode_select_gather(self, tokens: torch.Tensor, src: torch.Tensor, last_ids: torch.Tensor,
+                             slots: torch.Tensor, positions: torch.Tensor, masks: torch.Tensor,
+                             mask_idx: torch.Tensor) -> tuple:
+        """:meth:`decode_select` whose input token of row r is ``last_ids[src[r]]``
+        where ``src[r] >= 0`` (the previous step's selection, still on the
+        device) and ``tokens[r]`` otherwise; the step's own selections are
+        written to ``last_ids`` for the next step.  Lets the host launch step
+        t+1 before it has read step t's ids (the engine's one-step pipeline).
+        Capturable."""
+        B = tokens.shape[0]
+        gathered = last_ids.index_select(0, src.clamp(min=0).long())
+        toks = torch.where(src >= 0, gathered, tokens)
+        logits, ids = self.decode_select(toks, slots, positions, masks, mask_idx)
+        last_ids[:B].copy_(ids)
+        return logits, ids
+
     # reference path (pure torch, fp32 math) for numerics tests
     @torch.inference_mode()
     def reference_logits(self, tokens: Sequence[int]) -> torch.Tensor:
@@ -453,9 +469,11 @@ class LocalLM:
 class DecodeGraphs:
     """hipGraph-captured decode + selection steps, one graph per row-count bucket.
 
-    Inputs travel as ONE packed int32 host buffer ``[4, n]`` (token, slot,
-    position, mask row) -> one H2D copy into the graph's static input; the
-    graph runs the whole forward plus the masked argmax, so a step costs one
+    Inputs travel as ONE packed int32 host buffer ``[5, n]`` (token, slot,
+    position, mask row, token source) -> one H2D copy into the graph's static
+    input; the graph gathers the rows whose source is >= 0 from the previous
+    step's selections (:attr:`last_ids`, device-resident, written by every
+    step), runs the whole forward plus the masked argmax, so a step costs one
     copy in, one replay and one 4-byte-per-row copy out.  Padding rows carry
     slot -1 (kernels skip them).  Returned tensors are the graph's static
     outputs: read them before the next replay of the same bucket."""
@@ -469,6 +487,7 @@ class DecodeGraphs:
             self.buckets.append(model.max_rows)
         self.graphs: Dict[int, tuple] = {}
         self.enabled = model.device.type == "cuda"
+        self.last_ids = torch.zeros(max(self.buckets), dtype=torch.int32, device=model.device)
 
     def bucket_for(self, n: int) -> int:
         for b in self.buckets:
@@ -478,32 +497,37 @@ class DecodeGraphs:
 
     def _capture(self, b: int):
         m = self.model
-        inp = torch.zeros((4, b), dtype=torch.int32, device=m.device)
+        inp = torch.zeros((5, b), dtype=torch.int32, device=m.device)
         inp[1].fill_(-1)
-        stage = torch.zeros((4, b), dtype=torch.int32).pin_memory()
+        inp[4].fill_(-1)
+        stage = torch.zeros((5, b), dtype=torch.int32).pin_memory()
+        scratch = torch.zeros_like(self.last_ids)  # warm-up must not clobber last_ids
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):  # warm up hipBLASLt heuristics / allocator outside capture
-                m.decode_select(inp[0], inp[1], inp[2], self.masks, inp[3])
+                m.decode_select_gather(inp[0], inp[4], scratch, inp[1], inp[2], self.masks, inp[3])
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            logits, ids = m.decode_select(inp[0], inp[1], inp[2], self.masks, inp[3])
+            logits, ids = m.decode_select_gather(inp[0], inp[4], self.last_ids, inp[1], inp[2], self.masks, inp[3])
         self.graphs[b] = (g, inp, stage, stage.numpy(), logits, ids, torch.cuda.Event())
 
     @torch.inference_mode()
     def run(self, tokens: Sequence[int], slots: Sequence[int], positions: Sequence[int],
-            mask_rows: Sequence[int]) -> tuple:
-        """One step over ``n`` rows given as host lists.  Returns (logits[:n],
-        ids[:n]) -- device tensors owned by the graph."""
+            mask_rows: Sequence[int], srcs: Optional[Sequence[int]] = None) -> tuple:
+        """One step over ``n`` rows given as host lists (``srcs[r] >= 0``:
+        row r's token is row ``srcs[r]``'s selection of the previous step).
+        Returns (logits[:n], ids[:n]) -- device tensors owned by the graph."""
         n = len(tokens)
         m = self.model
+        if srcs is None:
+            srcs = [-1] * n
         if not self.enabled:
-            t = torch.tensor([list(tokens), list(slots), list(positions), list(mask_rows)], dtype=torch.int32,
-                             device=m.device)
-            return m.decode_select(t[0].contiguous(), t[1].contiguous(), t[2].contiguous(), self.masks,
-                                   t[3].contiguous())
+            t = torch.tensor([list(tokens), list(slots), list(positions), list(mask_rows), list(srcs)],
+                             dtype=torch.int32, device=m.device)
+            return m.decode_select_gather(t[0].contiguous(), t[4].contiguous(), self.last_ids, t[1].contiguous(),
+                                          t[2].contiguous(), self.masks, t[3].contiguous())
         b = self.bucket_for(n)
         if b not in self.graphs:
             self._capture(b)
@@ -515,8 +539,10 @@ class DecodeGraphs:
         st[1, :n] = slots
         st[2, :n] = positions
         st[3, :n] = mask_rows
+        st[4, :n] = srcs
         if n < b:
             st[1, n:] = -1
+            st[4, n:] = -1
         inp.copy_(stage, non_blocking=True)
         copied.record()
         g.replay()

@@ -66,6 +66,22 @@ def test_jump_forward_is_exact_on_cpu(tiny):
     assert b.stats["decode_rows"] == b.stats["generated_tokens"]
 
 
+def test_pipelined_loop_matches_synchronous_loop(tiny):
+    """The one-step pipeline (device-side gather of the previous selections,
+    grammar one step behind) generates what the synchronous loop does."""
+    sync = LocalEngine(tiny, pipeline=False)
+    pipe = LocalEngine(tiny, pipeline=True)
+    inputs = _inputs(7)
+    ra, rb = sync.generate(inputs, "A readme"), pipe.generate(inputs, "A readme")
+    assert sum(x == y for x, y in zip(ra, rb)) >= 6
+    for r in rb:
+        json.loads(r)
+    # forced bytes after a sampled quote start a step later: a few more steps
+    assert sync.stats["decode_steps"] <= pipe.stats["decode_steps"] <= 1.3 * sync.stats["decode_steps"]
+    assert pipe.stats["generated_tokens"] == sync.stats["generated_tokens"] or \
+        sum(x == y for x, y in zip(ra, rb)) < len(ra)
+
+
 def test_backend_contract(tiny):
     be = LocalLLMBackend([LocalEngine(tiny)])
     res = be.enrich_batch(_inputs(3), None)

@@ -178,6 +178,13 @@ class LocalLM:
         # fused decode GEMMs for steps of <= fused_max_rows rows (GPU only;
         # DMCP_FUSED_GEMM=0 forces the hipBLASLt path)
         self.use_fused = self.device.type == "cuda" and os.environ.get("DMCP_FUSED_GEMM", "1") != "0"
+        # prefill / extend attention on the MFMA kernel (csrc/prefill_attn.hip);
+        # DMCP_PREFILL_KERNEL=0 forces the SDPA path
+        self.use_prefill_kernel = (self.device.type == "cuda" and os.environ.get("DMCP_PREFILL_KERNEL", "1") != "0"
+                                   and ops.prefill_supported(c.n_heads, c.n_kv_heads, c.head_dim))
+        # slot -> shared-prefix length its prefill reads in place from the
+        # prefix slot (fork_prefix without a copy; prefill kernel only)
+        self._slot_prefix: Dict[int, int] = {}
         self.fused_max_rows = min(ops.FUSED_MAX_ROWS, int(os.environ.get("DMCP_FUSED_MAX_ROWS", "32")))
         ps = ops.prefix_splits(c.max_seq, self.PREFIX_CHUNK) if shared_prefix else 0
         self.attn_ws = (ops.decode_workspace(self.max_rows, c.n_heads, c.n_kv_heads, c.head_dim, c.max_seq,
@@ -285,6 +292,10 @@ class LocalLM:
         ids = tokens.to(device=dev, dtype=torch.int32).contiguous()
         pos = torch.arange(start_pos, start_pos + T, dtype=torch.int32, device=dev)
         slots = torch.full((T,), slot, dtype=torch.int32, device=dev)
+        if start_pos == 0:
+            self._slot_prefix.pop(slot, None)  # a new sequence in this slot
+        shared = self._slot_prefix.get(slot, 0)
+        shared = shared if 0 < shared <= start_pos else 0
         x = ops.embedding(self.w["embed"], ids)
         resid = x.clone()
         h = ops.add_rmsnorm(x, self.w["l0.ln1"], c.eps)
@@ -293,14 +304,19 @@ class LocalLM:
             kc, vc = self.k_cache[i], self.v_cache[i]
             qkv = F.linear(h, self.w[f"l{i}.wqkv"])
             q = ops.rope_kv(qkv, pos, slots, self.cos_sin, kc, vc, c.n_heads)  # [T, Hq, D]
-            k = kc[slot, :, :L].unsqueeze(0)  # [1, Hkv, L, D]
-            v = vc[slot, :, :L].unsqueeze(0)
-            qh = q.transpose(0, 1).unsqueeze(0)  # [1, Hq, T, D]
-            if start_pos == 0:
-                att = F.scaled_dot_product_attention(qh, k, v, is_causal=True, enable_gqa=True)
-            else:  # extend after a cached context (e.g. a shared prefix)
-                att = _extend_attention(qh, k, v, start_pos, self.scale)
-            o = F.linear(att[0].transpose(0, 1).reshape(T, c.n_heads * c.head_dim), self.w[f"l{i}.wo"])
+            if self.use_prefill_kernel:
+                att = ops.prefill_attention(q, kc, vc, slot, start_pos, self.prefix_slot if shared else None,
+                                            shared, self.scale)
+                o = F.linear(att.view(T, c.n_heads * c.head_dim), self.w[f"l{i}.wo"])
+            else:
+                k = kc[slot, :, :L].unsqueeze(0)  # [1, Hkv, L, D]
+                v = vc[slot, :, :L].unsqueeze(0)
+                qh = q.transpose(0, 1).unsqueeze(0)  # [1, Hq, T, D]
+                if start_pos == 0:
+                    att = F.scaled_dot_product_attention(qh, k, v, is_causal=True, enable_gqa=True)
+                else:  # extend after a cached context (e.g. a shared prefix)
+                    att = _extend_attention(qh, k, v, start_pos, self.scale)
+                o = F.linear(att[0].transpose(0, 1).reshape(T, c.n_heads * c.head_dim), self.w[f"l{i}.wo"])
             h = ops.add_rmsnorm(o, self.w[f"l{i}.ln2"], c.eps, residual=resid)
             m = self._mlp(i, h)
             nxt = self.w[f"l{i + 1}.ln1"] if i + 1 < c.layers else self.w["norm_f"]
@@ -393,14 +409,19 @@ class LocalLM:
         if self.shared_prefix:
             self.prefix_dev.zero_()
         self.prefix_len, self.prefix_tokens = 0, ()
+        self._slot_prefix.clear()
 
     @torch.inference_mode()
     def fork_prefix(self, slot: int) -> int:
-        """Copies the shared prefix K/V into ``slot`` (what prefill of the
-        rest of that sequence attends to); decode reads the shared copy.
-        Returns P (0 when no prefix is set)."""
+        """Starts ``slot`` on the shared prefix: prefill of the rest of that
+        sequence (``forward_tokens(rest, slot, P)``) attends to the prefix
+        keys -- read in place from the prefix slot by the MFMA prefill kernel,
+        or copied into ``slot`` on the SDPA path; decode always reads the
+        shared copy.  Returns P (0 when no prefix is set)."""
         P = self.prefix_len
-        if P:
+        if P and self.use_prefill_kernel:
+            self._slot_prefix[slot] = P  # the prefill kernel reads the shared copy in place
+        elif P:
             self.k_cache[:, slot, :, :P].copy_(self.k_cache[:, self.prefix_slot, :, :P])
             self.v_cache[:, slot, :, :P].copy_(self.v_cache[:, self.prefix_slot, :, :P])
         return P

@@ -82,6 +82,18 @@ def decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace=None, 
     return reference.decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace, chunk, out, prefix)
 
 
+def prefill_attention(q, k_cache, v_cache, slot, start, prefix_slot=None, prefix_len=0, scale=1.0, out=None,
+                      variant=0, nsplit=0):
+    """Causal prefill/extend attention of one sequence, shared prefix read in place."""
+    return (_hip() if q.is_cuda else reference).prefill_attention(q, k_cache, v_cache, slot, start, prefix_slot,
+                                                                  prefix_len, scale, out, variant, nsplit)
+
+
+def prefill_supported(n_heads, n_kv_heads, head_dim):
+    from .hip import prefill_supported as _ps
+    return _ps(n_heads, n_kv_heads, head_dim)
+
+
 def silu_mul(gate_up, out=None):
     return (_hip() if gate_up.is_cuda else reference).silu_mul(gate_up, out)
 

@@ -1052,7 +1052,7 @@ hipError_t launch_decode_d(int G, dim3 grid, const uint16_t* q, const uint16_t* 
 
 extern "C" {
 
-int dmcp_abi_version() { return 7; }
+int dmcp_abi_version() { return 8; }
 
 // Selects the per-row decode attention kernel (0 = MFMA, 1 = VALU, 2 = MFMA double-buffered);
 // returns the previous choice.

@@ -26,7 +26,7 @@ _lock = threading.Lock()
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _f = ctypes.c_float
-ABI_VERSION = 7  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
+ABI_VERSION = 8  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
 
 
 class HipOpsError(RuntimeError):
@@ -53,6 +53,8 @@ def lib() -> ctypes.CDLL:
             "dmcp_decode_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _f,
                                        _vp, _vp, _vp, _i, _i, _i, _vp],
                                       _i),
+            "dmcp_prefill_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _i, _i,
+                                        _vp], _i),
             "dmcp_silu_mul": ([_vp, _vp, _i, _i, _vp], _i),
             "dmcp_masked_argmax": ([_vp, _vp, _vp, _i, _vp, _i, _i, _i, _vp], _i),
             "dmcp_embedding": ([_vp, _vp, _vp, _i, _i, _i, _vp], _i),
@@ -264,6 +266,66 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
                                        _ptr(part_o), _ptr(part_ml), B, Hq, Hkv, D, MAXS, S, chunk, splits,
                                        float(scale), _ptr(pk), _ptr(pvt), _ptr(plen), ldv, pchunk, ps_max,
                                        _stream()), "dmcp_decode_attention")
+    return out
+
+
+def prefill_supported(n_heads: int, n_kv_heads: int, head_dim: int) -> bool:
+    """Shapes the MFMA prefill-attention kernel covers (any GQA group)."""
+    return head_dim in (64, 128) and n_kv_heads > 0 and n_heads % n_kv_heads == 0
+
+
+PREFILL_VARIANTS = {64: (0, 1), 128: (0, 1)}  # waves per block: 0 = 4, 1 = 8
+
+
+def prefill_splits(T: int, Hq: int, Hkv: int, variant: int = 0, target_blocks: int = 1024) -> int:
+    """Key splits per query tile so that a prefill launch has ~4 blocks per
+    CU (1024 on 256 CUs): a 2,100-token class is only 33 x 8 = 264 tiles
+    (measured: 177 -> 165 us with 2 splits, profiles/prefill_attn_r2.md)."""
+    cols = 128 * (2 if variant == 1 else 1)
+    blocks = -(-T * (Hq // Hkv) // cols) * Hkv
+    return max(1, min(8, -(-target_blocks // max(1, blocks))))
+
+
+def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: int, start: int,
+                      prefix_slot: Optional[int] = None, prefix_len: int = 0, scale: float = 1.0,
+                      out: Optional[torch.Tensor] = None, variant: int = 0, nsplit: int = 0) -> torch.Tensor:
+    """Causal attention of q [T, Hq, D] (positions [start, start+T) of
+    ``slot``, K/V already appended by rope_kv) over keys [0, start+T) of the
+    caches [S, Hkv, MAXS, D]; keys [0, prefix_len) are read in place from
+    ``prefix_slot`` (the shared prefix, no per-sequence copy).  One MFMA
+    kernel (csrc/prefill_attn.hip); ``nsplit`` > 1 splits every query tile's
+    keys over that many blocks plus a merge kernel (0 = :func:`prefill_splits`).
+    Returns [T, Hq, D] bf16."""
+    T, Hq, D = q.shape
+    S, Hkv, MAXS, Dk = k_cache.shape
+    for t, n in ((q, "q"), (k_cache, "k_cache"), (v_cache, "v_cache")):
+        _req(t, torch.bfloat16, f"prefill_attention.{n}")
+    if Dk != D or v_cache.shape != k_cache.shape or not prefill_supported(Hq, Hkv, D):
+        raise HipOpsError(f"prefill_attention: unsupported shape q={tuple(q.shape)} kv={tuple(k_cache.shape)}")
+    slot, start, prefix_len = int(slot), int(start), int(prefix_len)
+    if not 0 <= slot < S or start < 0 or T < 1 or start + T > MAXS:
+        raise HipOpsError(f"prefill_attention: slot {slot} / positions [{start}, {start + T}) outside "
+                          f"{S} slots x {MAXS} positions")
+    if prefix_len:
+        if prefix_slot is None or not 0 <= int(prefix_slot) < S or not 0 < prefix_len <= start:
+            raise HipOpsError(f"prefill_attention: prefix of {prefix_len} keys in slot {prefix_slot} must precede "
+                              f"start {start}")
+        pk, pv = k_cache[int(prefix_slot)], v_cache[int(prefix_slot)]
+    else:
+        pk = pv = None
+    nsplit = int(nsplit) or prefill_splits(T, Hq, Hkv, variant)
+    if variant not in PREFILL_VARIANTS[D] or not 1 <= nsplit <= 64:
+        raise HipOpsError(f"prefill_attention: variant {variant} / nsplit {nsplit} not available for D={D}")
+    out = torch.empty_like(q) if out is None else out
+    _req_out(out, torch.bfloat16, T * Hq * D, "prefill_attention.out")
+    part_o = part_ml = None
+    if nsplit > 1:
+        part_o = torch.empty(nsplit * T * Hq * D, dtype=torch.float32, device=q.device)
+        part_ml = torch.empty(nsplit * T * Hq * 2, dtype=torch.float32, device=q.device)
+    _check(lib().dmcp_prefill_attention(_ptr(q), _ptr(k_cache[slot]), _ptr(v_cache[slot]), _ptr(pk), _ptr(pv),
+                                        _ptr(out), _ptr(part_o), _ptr(part_ml), T, start, prefix_len, Hq, Hkv, D,
+                                        MAXS, float(scale), int(variant), int(nsplit), _stream()),
+           "dmcp_prefill_attention")
     return out
 
 

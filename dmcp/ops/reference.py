@@ -106,6 +106,32 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     return y
 
 
+def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: int, start: int,
+                      prefix_slot: Optional[int] = None, prefix_len: int = 0, scale: float = 1.0,
+                      out: Optional[torch.Tensor] = None, variant: int = 0, nsplit: int = 0) -> torch.Tensor:
+    """q [T, Hq, D] at positions [start, start+T) of ``slot``; every query
+    sees the keys at or before its position.  Keys [0, prefix_len) come from
+    ``prefix_slot``, the rest from ``slot``.  fp32 math, returns [T, Hq, D]."""
+    T, Hq, D = q.shape
+    Hkv = k_cache.shape[1]
+    G = Hq // Hkv
+    L = start + T
+    k = k_cache[slot, :, :L].float()
+    v = v_cache[slot, :, :L].float()
+    if prefix_len > 0:
+        k = torch.cat([k_cache[prefix_slot, :, :prefix_len].float(), k[:, prefix_len:]], dim=1)
+        v = torch.cat([v_cache[prefix_slot, :, :prefix_len].float(), v[:, prefix_len:]], dim=1)
+    qf = q.float().view(T, Hkv, G, D)
+    att = torch.einsum("thgd,hld->hgtl", qf, k) * scale  # [Hkv, G, T, L]
+    pos = torch.arange(start, L, device=q.device)[:, None]
+    att = att.masked_fill(torch.arange(L, device=q.device)[None, :] > pos, float("-inf"))
+    y = torch.einsum("hgtl,hld->thgd", torch.softmax(att, dim=-1), v).reshape(T, Hq, D).to(q.dtype)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
 def silu_mul(gate_up: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     I = gate_up.shape[-1] // 2
     g, u = gate_up[..., :I].float(), gate_up[..., I:].float()

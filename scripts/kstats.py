@@ -7,7 +7,7 @@ import collections
 import csv
 import sys
 
-CATS = [("gemm", "Cijk"), ("fused_gemm", "fused_gemm"), ("attn_combine", "combine"), ("attn_suffix", "decode_attn_"),
+CATS = [("prefill_mfma", "prefill_"), ("gemm", "Cijk"), ("fused_gemm", "fused_gemm"), ("attn_combine", "combine"), ("attn_suffix", "decode_attn_"),
         ("attn_prefix", "prefix_attn"), ("prefill_attn", "attn_fwd"), ("rmsnorm", "rmsnorm"), ("silu", "silu"),
         ("rope", "rope"), ("embedding", "embedding"), ("argmax", "argmax")]
 

@@ -133,3 +133,28 @@ def test_engine_common_prefix_detection(tiny):
     out = eng.generate(_inputs(5), "A README shared by every prompt of the batch. " * 3)
     assert eng.stats["prefix_tokens"] > 0 and all(json.loads(o) for o in out)
     assert tiny.prefix_len == 0  # cleared after the batch
+
+
+def test_prefill_reference_matches_sdpa_extend():
+    """reference.prefill_attention (the fp32 oracle of the MFMA prefill
+    kernel) == the SDPA + log-sum-exp merge path it replaces, with the
+    prefix keys taken from another slot."""
+    import math
+    from dmcp.models.llm import _extend_attention
+    from dmcp.ops import reference
+    g = torch.Generator().manual_seed(0)
+    T, Hq, Hkv, D, start, P, MAXS = 19, 8, 2, 16, 23, 11, 64
+    q = torch.randn(T, Hq, D, generator=g)
+    kc = torch.randn(3, Hkv, MAXS, D, generator=g)
+    vc = torch.randn(3, Hkv, MAXS, D, generator=g)
+    got = reference.prefill_attention(q, kc, vc, 1, start, 2, P, 1 / math.sqrt(D))
+    k = torch.cat([kc[2, :, :P], kc[1, :, P:start + T]], 1).unsqueeze(0)
+    v = torch.cat([vc[2, :, :P], vc[1, :, P:start + T]], 1).unsqueeze(0)
+    exp = _extend_attention(q.transpose(0, 1).unsqueeze(0), k, v, start, 1 / math.sqrt(D))[0].transpose(0, 1)
+    torch.testing.assert_close(got, exp, atol=1e-4, rtol=1e-4)
+    # start 0: plain causal prefill
+    got0 = reference.prefill_attention(q, kc, vc, 0, 0, None, 0, 0.25)
+    k0 = kc[0, :, :T].repeat_interleave(Hq // Hkv, 0)
+    v0 = vc[0, :, :T].repeat_interleave(Hq // Hkv, 0)
+    exp0 = torch.nn.functional.scaled_dot_product_attention(q.transpose(0, 1), k0, v0, is_causal=True, scale=0.25)
+    torch.testing.assert_close(got0, exp0.transpose(0, 1), atol=1e-4, rtol=1e-4)

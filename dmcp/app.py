@@ -70,7 +70,7 @@ def open_database(config: Config):
         db = PgDatabase.from_url(config.database_url, config.database_username, config.database_password)
         LOG.info("Store: %s", db.describe())
         return db
-    return Database(config.db_path)
+    return Database(config.db_path, background_checkpoint=config.db_background_checkpoint)
 
 
 class App:

@@ -68,6 +68,8 @@ class Config:
     max_readme_length: int = 10_000
     description_length: int = 500
     parser_threads: int = 0
+    # SQLite: WAL checkpoints on a background thread (dmcp/store/db.py::_Checkpointer)
+    db_background_checkpoint: bool = True
     recover_stuck_on_start: bool = True
     log_level: str = "INFO"
 
@@ -106,6 +108,7 @@ class Config:
             "MCP_SERVER_NAME": "mcp_server_name",
             "MCP_SERVER_VERSION": "mcp_server_version",
             "PARSER_THREADS": "parser_threads",
+            "DB_BACKGROUND_CHECKPOINT": "db_background_checkpoint",
             "RECOVER_STUCK_ON_START": "recover_stuck_on_start",
             "LOG_LEVEL": "log_level",
         }

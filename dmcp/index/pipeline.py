@@ -143,6 +143,8 @@ class _ProjectLocks:
 
 
 class Indexer:
+    ROW_CHUNK = 256  # classes (with their methods) per writer put in Phase 1
+
     def __init__(self, repos: Repositories, cache: GraphCache, git: GitClient,
                  backend: Optional[EnrichmentBackend] = None, *, batch_size: int = 20,
                  max_readme_length: int = 10_000, description_length: int = 500,
@@ -186,6 +188,10 @@ class Indexer:
             raise
         try:
             with span("analyze.total", stats, project=project.name):
+                # the row swap's transaction opens now: the old rows are
+                # deleted on the writer thread while the snapshot is read and
+                # parsed (rolled back if either fails)
+                writer = self.repos.project_rows_writer(project.id, True)
                 with span("analyze.clone", stats):
                     clone = self._fetch(url, branch_name, shallow=True)
                 readme = clone.readme(self.max_readme_length)
@@ -198,7 +204,7 @@ class Indexer:
                 LOG.info("Graph built: %d nodes, %d entry points", graph.node_count(), graph.entry_point_count())
                 order = graph.analysis_order()
                 with span("analyze.phase1", stats):
-                    p1 = self._phase1_static(project, parsed, graph, order, clone.commit_hash, replace=True)
+                    p1 = self._phase1_static(project, parsed, graph, order, clone.commit_hash, writer)
                 classes, methods_by_ident, writer = p1
                 enriched = failed = recovered = 0
                 if self.backend.enabled:
@@ -215,6 +221,8 @@ class Indexer:
                     project.update_graph_data(graph.to_json())
                     with span("analyze.phase1_commit", stats):
                         writer.wait()  # no-op when enrichment already waited
+                    for k, v in writer.timings.items():
+                        stats[f"analyze.writer_{k[:-3]}"] = v
                     project.analysis_completed(clone.commit_hash)
                     self.repos.projects.update(project)
                     self.cache.put(project.id, project.name, graph)
@@ -230,7 +238,7 @@ class Indexer:
             LOG.error("Analysis failed for %s: %s", repository_url, e, exc_info=True)
             if writer is not None:
                 try:
-                    writer.wait()  # the row swap finishes (or has failed) before the status write
+                    writer.finish()  # the row swap ends (commit or rollback) before the status write
                 except Exception:
                     pass
             self._mark_error(project)
@@ -276,12 +284,13 @@ class Indexer:
 
     # ---------------------------------------------------------------- phase 1
     def _phase1_static(self, project: Project, parsed: ParsedProject, graph: ProjectGraph,
-                       order: Sequence[str], commit_hash: str, replace: bool
-                       ) -> Tuple[int, Dict[str, List[Tuple[str, str]]], ProjectRowsWriter]:
+                       order: Sequence[str], commit_hash: str, writer: Optional[ProjectRowsWriter] = None,
+                       replace: bool = True) -> Tuple[int, Dict[str, List[Tuple[str, str]]], ProjectRowsWriter]:
         """Builds every class / method / parameter row and the graph metadata
-        and streams them to a :class:`ProjectRowsWriter`, which swaps them in
-        with one transaction (old rows deleted in it) on its own thread; the
-        caller must ``wait()`` on the returned writer before touching the rows."""
+        and streams them to a :class:`ProjectRowsWriter` (``writer``, already
+        started by the caller, or a new one), which swaps them in with one
+        transaction (old rows deleted in it) on its own thread; the caller
+        must ``wait()`` on the returned writer before touching the rows."""
         now = to_iso(utc_now())
         pid = project.id
         cls_rows: List[tuple] = []
@@ -298,18 +307,30 @@ class Indexer:
             if u.params:
                 n_ids += sum(len(u.params.get(m[0]) or ()) for m in u.methods)
         nid = iter(new_ids(n_ids)).__next__
-        # the writer thread starts deleting the old rows right away
-        writer = self.repos.project_rows_writer(pid, replace)
+        if writer is None:  # the writer thread starts deleting the old rows right away
+            writer = self.repos.project_rows_writer(pid, replace)
         try:
             class_types: Dict[str, Optional[str]] = {}
             method_infos: Dict[str, List[MethodInfo]] = {}
             cls_append, meth_append = cls_rows.append, meth_rows.append
             dumps = json.dumps
             tnew, MI = tuple.__new__, MethodInfo  # NamedTuple without the generated __new__ wrapper
+            # rows go to the writer in chunks, so its inserts overlap the
+            # building of the rest (methods follow their classes' chunk)
+            n_cls = n_meth = 0
+            pending, chunk = 0, self.ROW_CHUNK
             for ident in order:
                 unit = units.get(ident)
                 if unit is None:
                     continue
+                if pending == chunk:
+                    writer.put("classes", cls_rows)
+                    writer.put("methods", meth_rows)
+                    n_cls, n_meth = n_cls + len(cls_rows), n_meth + len(meth_rows)
+                    cls_rows, meth_rows = [], []
+                    cls_append, meth_append = cls_rows.append, meth_rows.append
+                    pending = 0
+                pending += 1
                 cid = nid()
                 class_ids[ident] = cid
                 ct = unit.class_type.value
@@ -329,6 +350,7 @@ class Indexer:
                 methods_by_ident[ident] = mids
             writer.put("classes", cls_rows)
             writer.put("methods", meth_rows)
+            n_cls, n_meth = n_cls + len(cls_rows), n_meth + len(meth_rows)
             # parameter links (CodeContextService.java:274-291, 805-856): the
             # first method of each name that has resolved parameter types
             links: Dict[str, Dict[str, List[str]]] = {}
@@ -355,9 +377,8 @@ class Indexer:
         except BaseException:
             writer.abort()
             raise
-        LOG.info("Phase 1 rows built. Classes: %d, Methods: %d, Parameters: %d",
-                 len(cls_rows), len(meth_rows), len(param_rows))
-        return len(cls_rows), methods_by_ident, writer
+        LOG.info("Phase 1 rows built. Classes: %d, Methods: %d, Parameters: %d", n_cls, n_meth, len(param_rows))
+        return n_cls, methods_by_ident, writer
 
     # ------------------------------------------------------------ enrichment
     def _read_source(self, tree: SourceTree, unit: ParsedUnit) -> Optional[str]:

@@ -601,11 +601,12 @@ class ProjectRowsWriter:
     is still building the rows.
 
     The reference saves rows one JPA/JDBI call at a time inside the analysis
-    loop (``CodeContextService.java:244-291``).  Here the caller streams the
-    three row batches with :meth:`put` as soon as each is built; the writer
-    thread opens the transaction immediately, deletes the project's old rows
-    while the first batch is still being assembled, and inserts each batch in
-    parent-before-child order.
+    loop (``CodeContextService.java:244-291``).  Here the writer thread opens
+    the transaction as soon as the writer is created (the indexer creates it
+    before it reads and parses the snapshot) and deletes the project's old
+    rows meanwhile; the caller then streams row chunks with :meth:`put` while
+    it is still building the rest, and the thread inserts each chunk as it
+    arrives.
 
     On a database file the writer is native (``native/srcscan/bulkwriter.cpp``):
     its own SQLite connection on a C++ thread, so binding and B-tree work run
@@ -617,7 +618,7 @@ class ProjectRowsWriter:
     :meth:`abort` rolls the transaction back.
     """
 
-    _ORDER = ("classes", "methods", "params")
+    _TABLES = ("classes", "methods", "params")
     BUSY_TIMEOUT_MS = 30_000
 
     def __init__(self, repos: "Repositories", project_id: str, replace: bool) -> None:
@@ -627,12 +628,12 @@ class ProjectRowsWriter:
         self.project_id = project_id
         self.replace = replace
         self.rows_written = 0
+        self.timings: Dict[str, float] = {}  # native writer phases (ms), after wait()
         self._error: Optional[BaseException] = None
         self._sync = repos.db.is_shared_memory()
         self._q: "queue.Queue" = queue.Queue()
-        self._pending: Dict[str, Sequence[tuple]] = {}
+        self._pending: List[Tuple[str, Sequence[tuple]]] = []
         self._thread: Optional[threading.Thread] = None
-        self._next = 0
         self._done = False
         self._native = None
         # the native writer reads text straight out of these objects' UTF-8
@@ -643,9 +644,12 @@ class ProjectRowsWriter:
         bulk = _native_bulk_writer() if getattr(repos.db, "native_bulk", True) else None
         if bulk is not None:
             setup = []
+            if getattr(repos.db, "checkpointer", None) is not None:
+                # checkpoints belong to the database's background thread
+                setup.append(("PRAGMA wal_autocheckpoint = 0", ((),)))
             if replace:
-                setup = [(r.DELETE_BY_PROJECT_ID, ((project_id,),))
-                         for r in (repos.params, repos.methods, repos.classes)]
+                setup += [(r.DELETE_BY_PROJECT_ID, ((project_id,),))
+                          for r in (repos.params, repos.methods, repos.classes)]
             self._keep.append(setup)
             self._native = bulk(repos.db.path, self.BUSY_TIMEOUT_MS, setup)
             return
@@ -654,20 +658,35 @@ class ProjectRowsWriter:
 
     # ------------------------------------------------------------ producer
     def put(self, table: str, rows: Sequence[tuple]) -> None:
-        if table not in self._ORDER:
+        """Queues rows of one table; tables may be put repeatedly and
+        interleaved (the producer streams chunks while it builds the rest),
+        inserted in arrival order.  Foreign keys are not enforced during the
+        swap (native writer / ``bulk_transaction``); a ``:memory:`` database
+        keeps them on, so put each row after the rows it references."""
+        if table not in self._TABLES:
             raise ValueError(f"unknown table {table}")
         if self._native is not None:
-            if self._ORDER.index(table) < self._next:
-                raise ValueError(f"{table} rows after their children")
-            self._next = self._ORDER.index(table) + 1
             if rows:
                 frozen = tuple(rows)  # immutable: the writer holds views into it
                 self._keep.append(frozen)
                 self._native.put(getattr(self.repos, table)._INSERT, frozen)
         elif self._sync:
-            self._pending[table] = rows
+            self._pending.append((table, rows))
         else:
             self._q.put((table, rows))
+
+    @property
+    def closed(self) -> bool:
+        """:meth:`close` was called (a commit is on its way)."""
+        return getattr(self, "_closed", False)
+
+    def finish(self) -> None:
+        """Error-path cleanup: waits for a requested commit, rolls back otherwise
+        (a writer that was never closed would wait for rows forever)."""
+        if self.closed:
+            self.wait()
+        else:
+            self.abort()
 
     def close(self) -> None:
         """No more rows: the writer commits once everything queued is in."""
@@ -675,7 +694,7 @@ class ProjectRowsWriter:
         if self._native is not None:
             self._native.commit()
         elif self._sync:
-            self._write_all(iter(self._pending.items()))
+            self._write_all(iter(self._pending))
         else:
             self._q.put(None)
 
@@ -694,6 +713,9 @@ class ProjectRowsWriter:
                 self._done = True
                 try:
                     self.rows_written = self._native.wait()
+                    if hasattr(self._native, "timings"):
+                        self.timings = self._native.timings()
+                    self.repos.db.committed()
                 except RuntimeError as e:
                     self._error = e
                 self._keep.clear()
@@ -740,8 +762,6 @@ class ProjectRowsWriter:
 
     def _write_all(self, batches) -> None:
         r = self.repos
-        pending: Dict[str, Sequence[tuple]] = {}
-        nxt = 0
         with r.db.bulk_transaction():
             if self.replace:
                 # children first: the FK cascade then finds nothing to do per row
@@ -749,15 +769,8 @@ class ProjectRowsWriter:
                 r.methods.delete_by_project_id(self.project_id)
                 r.classes.delete_by_project_id(self.project_id)
             for table, rows in batches:
-                pending[table] = rows
-                while nxt < len(self._ORDER) and self._ORDER[nxt] in pending:
-                    name = self._ORDER[nxt]
-                    rows = pending.pop(name)
-                    getattr(r, name).save_rows(rows)
-                    self.rows_written += len(rows)
-                    nxt += 1
-            if pending:
-                raise RuntimeError(f"rows for {sorted(pending)} arrived without their parents")
+                getattr(r, table).save_rows(rows)
+                self.rows_written += len(rows)
 
 
 class _Aborted(Exception):

@@ -1,5 +1,6 @@
 #include "bulkwriter.hpp"
 
+#include <chrono>
 #include <stdexcept>
 
 #include "sqlite_min.hpp"
@@ -127,10 +128,16 @@ void BulkWriter::run() {
         c.exec("PRAGMA temp_store = MEMORY");
         c.exec("PRAGMA cache_size = -65536");
         c.exec("PRAGMA foreign_keys = OFF");
+        using clock = std::chrono::steady_clock;
+        auto ms = [](clock::time_point a, clock::time_point b) {
+            return std::chrono::duration<double, std::milli>(b - a).count();
+        };
+        auto t0 = clock::now();
         c.exec("BEGIN IMMEDIATE");
         in_tx = true;
         for (const Batch& b : setup_) c.run(b);
         setup_.clear();
+        setup_ms_ = ms(t0, clock::now());
         for (;;) {
             Item it;
             pop(it);
@@ -141,11 +148,15 @@ void BulkWriter::run() {
                 return;
             }
             if (it.op == Op::Commit) {
+                auto tc = clock::now();
                 c.exec("COMMIT");
+                commit_ms_ = ms(tc, clock::now());
                 in_tx = false;
                 return;
             }
+            auto tr = clock::now();
             rows_written_ += c.run(it.batch);
+            rows_ms_ += ms(tr, clock::now());
         }
     } catch (const std::exception& e) {
         error_ = e.what();

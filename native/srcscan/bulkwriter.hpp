@@ -55,6 +55,11 @@ class BulkWriter {
     void abort();              // ROLLBACK (queued batches are dropped) and join
     std::string wait();        // join; "" on success, else the error message
     int64_t rows_written() const { return rows_written_; }
+    // wall time of the writer thread's phases (valid after wait()): the
+    // setup statements (old rows' deletes), the inserts, the COMMIT
+    double setup_ms() const { return setup_ms_; }
+    double rows_ms() const { return rows_ms_; }
+    double commit_ms() const { return commit_ms_; }
 
   private:
     enum class Op { Rows, Commit, Abort };
@@ -75,6 +80,7 @@ class BulkWriter {
     std::thread thread_;
     std::string error_;
     int64_t rows_written_ = 0;
+    double setup_ms_ = 0, rows_ms_ = 0, commit_ms_ = 0;
     bool joined_ = false;
     bool commit_requested_ = false;
 };

@@ -391,6 +391,13 @@ PYBIND11_MODULE(_srcscan, m) {
                 if (!err.empty()) throw std::runtime_error("bulk write failed: " + err);
                 return w.rows_written();
             })
-        .def_property_readonly("rows_written", &dbw::BulkWriter::rows_written);
+        .def_property_readonly("rows_written", &dbw::BulkWriter::rows_written)
+        .def("timings", [](const dbw::BulkWriter& w) {
+            py::dict d;
+            d["setup_ms"] = w.setup_ms();
+            d["rows_ms"] = w.rows_ms();
+            d["commit_ms"] = w.commit_ms();
+            return d;
+        });
     m.attr("ABI_VERSION") = 2;
 }

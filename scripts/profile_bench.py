@@ -8,6 +8,8 @@ import sys
 import tempfile
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if os.environ.get("PROFILE_WITH_TORCH"):  # bench.py imports torch (distributed init) before indexing
+    import torch  # noqa: F401,E402
 
 from dmcp.app import App  # noqa: E402
 from dmcp.config import Config  # noqa: E402

@@ -297,3 +297,51 @@ def test_nestjs_and_go_projects(tmp_path):
     api = app.context.get_service_api("gosvc")
     assert api["found"] and api["controllers"]
     app.close()
+
+
+@pytest.mark.parametrize("stage", ["clone", "parse"])
+def test_failed_reanalysis_keeps_previous_rows(tmp_path, repo, monkeypatch, stage):
+    """The row swap's transaction opens before the snapshot is read (its
+    deletes overlap clone + parse); a failure in either stage rolls it back,
+    so the previous analysis survives (the reference deleted first,
+    CodeContextService.java:745) and nothing waits on the open writer."""
+    app = make_app(tmp_path)
+    r = app.indexer.analyze_project(str(repo))
+    n_methods = app.db.query_one("SELECT COUNT(*) FROM source_methods")[0]
+
+    def boom(*a, **k):
+        raise RuntimeError(f"{stage} failed")
+    if stage == "clone":
+        monkeypatch.setattr(app.indexer, "_fetch", boom)
+    else:
+        import dmcp.index.pipeline as pl
+        monkeypatch.setattr(pl, "parser_for", boom)
+    with pytest.raises(DomainError) as e:
+        app.indexer.analyze_project(str(repo))
+    assert e.value.error_code == "ANALYSIS_FAILED"
+    assert app.repos.classes.count_by_project()[r.project_id] == 17
+    assert app.db.query_one("SELECT COUNT(*) FROM source_methods")[0] == n_methods
+    assert app.repos.projects.find_by_id(r.project_id).status is ProjectStatus.ERROR
+    monkeypatch.undo()
+    assert app.indexer.analyze_project(str(repo)).success  # lock released, writable again
+    app.close()
+
+
+def test_background_wal_checkpoints(tmp_path, repo):
+    """Commits never checkpoint inline (wal_autocheckpoint = 0 on every
+    connection, the native writer included); the database's checkpoint thread
+    does, and the data is intact after a reopen."""
+    app = make_app(tmp_path)
+    r = app.indexer.analyze_project(str(repo))
+    assert app.db.query_one("PRAGMA wal_autocheckpoint")[0] == 0
+    ck = app.db.checkpointer
+    assert ck is not None and ck._thread is not None
+    app.close()
+    assert ck.passes >= 1 and not ck._thread.is_alive()
+    app2 = make_app(tmp_path)
+    assert app2.repos.classes.count_by_project()[r.project_id] == 17
+    assert app2.db.query_one("PRAGMA integrity_check")[0] == "ok"
+    app2.close()
+    app3 = make_app(tmp_path, db_background_checkpoint=False)
+    assert app3.db.checkpointer is None and app3.db.query_one("PRAGMA wal_autocheckpoint")[0] == 1000
+    app3.close()

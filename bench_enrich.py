@@ -24,6 +24,8 @@ sys.path.insert(0, ROOT)
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--preset", default="dmcp-coder-1b")
+    ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"],
+                    help="KV cache storage (fp8 = e4m3, half the attention bytes)")
     ap.add_argument("--classes", type=int, default=128, help="classes per rank")
     ap.add_argument("--batch", type=int, default=64, help="concurrent sequences (KV slots)")
     ap.add_argument("--max-seq", type=int, default=8192)
@@ -53,7 +55,7 @@ def main(argv=None) -> int:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl")
-    cfg = preset(args.preset, max_batch=args.batch, max_seq=args.max_seq)
+    cfg = preset(args.preset, max_batch=args.batch, max_seq=args.max_seq, kv_dtype=args.kv_dtype)
     model = LocalLM(cfg, device=f"cuda:{local}", seed=rank)
     eng = LocalEngine(model, use_graphs=not args.no_graphs, jump_forward=not args.no_jump,
                       shared_prefix=not args.no_shared_prefix, pipeline=not args.no_pipeline)
@@ -104,6 +106,7 @@ def main(argv=None) -> int:
             "unit": "classes/s", "n_gpus": world, "higher_is_better": True, "scaling": "weak",
             "dtype": "bf16", "data": "synthetic classes, random-init weights",
             "config": {"model": cfg.name, "params_b": round(cfg.param_count() / 1e9, 3), "batch": args.batch,
+                       "kv_dtype": cfg.kv_dtype,
                        "max_seq": args.max_seq, "prompt_chars": args.prompt_chars,
                        "readme_chars": args.readme_chars, "graphs": not args.no_graphs,
                        "jump_forward": not args.no_jump, "shared_prefix": not args.no_shared_prefix,

@@ -532,7 +532,8 @@ class LocalLLMBackend(EnrichmentBackend):
         engines = []
         for d in devices:
             with torch.cuda.device(d):
-                model = LocalLM(preset(cfg.local_llm_preset), device=f"cuda:{d}", seed=0)
+                model = LocalLM(preset(cfg.local_llm_preset, kv_dtype=cfg.local_llm_kv_dtype), device=f"cuda:{d}",
+                                seed=0)
                 engines.append(LocalEngine(model))
         return cls(engines)
 

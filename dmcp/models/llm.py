@@ -66,6 +66,7 @@ class LMConfig:
     max_seq: int = 8192             # KV capacity per slot (prompt + generation)
     max_batch: int = 64             # KV slots = concurrent sequences
     max_rows: int = 256             # token rows per batched decode/extend step (jump-forward)
+    kv_dtype: str = "bf16"          # KV cache storage: "bf16" or "fp8" (e4m3, unit scale, half the bytes)
 
     @property
     def qkv_dim(self) -> int:
@@ -76,8 +77,12 @@ class LMConfig:
                      + 3 * self.intermediate * self.hidden + 2 * self.hidden)
         return self.layers * per_layer + 2 * self.vocab_size * self.hidden + self.hidden
 
+    @property
+    def kv_elem_bytes(self) -> int:
+        return 1 if self.kv_dtype == "fp8" else 2
+
     def kv_bytes(self) -> int:
-        return 2 * self.layers * self.max_batch * self.n_kv_heads * self.max_seq * self.head_dim * 2
+        return 2 * self.layers * self.max_batch * self.n_kv_heads * self.max_seq * self.head_dim * self.kv_elem_bytes
 
 
 PRESETS: Dict[str, LMConfig] = {
@@ -138,6 +143,11 @@ def _extend_attention(qh: torch.Tensor, k: torch.Tensor, v: torch.Tensor, start:
     return ((o1.float() * w1 + o2.float() * w2) / (w1 + w2)).to(qh.dtype)
 
 
+def _kv_bf16(t: torch.Tensor) -> torch.Tensor:
+    """A KV-cache view as bf16 (fp8 caches widened; the SDPA fallback path)."""
+    return ops.reference.kv_float(t).to(torch.bfloat16) if t.dtype == torch.uint8 else t
+
+
 class LocalLM:
     """Weights + KV cache + forward passes (prefill / extend / batched decode).
 
@@ -153,6 +163,8 @@ class LocalLM:
                  weights: Optional[Dict[str, torch.Tensor]] = None, shared_prefix: bool = True) -> None:
         if cfg.n_heads % cfg.n_kv_heads:
             raise ValueError("n_heads must be a multiple of n_kv_heads")
+        if cfg.kv_dtype not in ("bf16", "fp8"):
+            raise ValueError(f"kv_dtype must be 'bf16' or 'fp8', got {cfg.kv_dtype!r}")
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = torch.bfloat16
@@ -163,8 +175,11 @@ class LocalLM:
         self.num_slots = c.max_batch + (1 if shared_prefix else 0)
         self.prefix_slot = c.max_batch if shared_prefix else -1
         kv_shape = (c.layers, self.num_slots, c.n_kv_heads, c.max_seq, c.head_dim)
-        self.k_cache = torch.zeros(kv_shape, dtype=self.dtype, device=self.device)
-        self.v_cache = torch.zeros(kv_shape, dtype=self.dtype, device=self.device)
+        # fp8: OCP e4m3fn bytes in uint8 tensors, written by the RoPE/KV-append
+        # kernels and widened to bf16 inside every attention kernel
+        self.kv_dtype = torch.uint8 if c.kv_dtype == "fp8" else self.dtype
+        self.k_cache = torch.zeros(kv_shape, dtype=self.kv_dtype, device=self.device)
+        self.v_cache = torch.zeros(kv_shape, dtype=self.kv_dtype, device=self.device)
         self.cos_sin = ops.rope_tables(c.max_seq, c.head_dim, c.rope_theta, device=self.device).contiguous()
         self.scale = 1.0 / math.sqrt(c.head_dim)
         self.max_rows = max(c.max_batch, c.max_rows)
@@ -173,7 +188,7 @@ class LocalLM:
         self.prefix_len = 0
         self.prefix_tokens: tuple = ()
         self.prefix_dev = torch.zeros(1, dtype=torch.int32, device=self.device)
-        self.prefix_vt = (torch.zeros((c.layers, c.n_kv_heads, c.head_dim, c.max_seq), dtype=self.dtype,
+        self.prefix_vt = (torch.zeros((c.layers, c.n_kv_heads, c.head_dim, c.max_seq), dtype=self.kv_dtype,
                                       device=self.device) if shared_prefix else None)
         # fused decode GEMMs for steps of <= fused_max_rows rows (GPU only;
         # DMCP_FUSED_GEMM=0 forces the hipBLASLt path)
@@ -309,8 +324,8 @@ class LocalLM:
                                             shared, self.scale)
                 o = F.linear(att.view(T, c.n_heads * c.head_dim), self.w[f"l{i}.wo"])
             else:
-                k = kc[slot, :, :L].unsqueeze(0)  # [1, Hkv, L, D]
-                v = vc[slot, :, :L].unsqueeze(0)
+                k = _kv_bf16(kc[slot, :, :L]).unsqueeze(0)  # [1, Hkv, L, D]
+                v = _kv_bf16(vc[slot, :, :L]).unsqueeze(0)
                 qh = q.transpose(0, 1).unsqueeze(0)  # [1, Hq, T, D]
                 if start_pos == 0:
                     att = F.scaled_dot_product_attention(qh, k, v, is_causal=True, enable_gqa=True)

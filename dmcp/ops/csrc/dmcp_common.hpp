@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace {
 
 constexpr int kBlock = 256;
@@ -63,5 +65,46 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef short v4i16_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ bf16x8_t as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8_t, v); }
+
+// ---- FP8 KV cache (OCP e4m3fn, gfx950's native fp8): unit scale, values
+// saturated to +-448 on the way in (the hardware conversion does not clamp).
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float fp8_sat(float x) { return __builtin_fminf(__builtin_fmaxf(x, -448.f), 448.f); }
+
+// 4 floats -> 4 e4m3 bytes (v_cvt_pk_fp8_f32 x2)
+__device__ __forceinline__ uint32_t pack_fp8x4(const float* f) {
+    const uint32_t lo = __builtin_amdgcn_cvt_pk_fp8_f32(fp8_sat(f[0]), fp8_sat(f[1]), 0, false);
+    return __builtin_amdgcn_cvt_pk_fp8_f32(fp8_sat(f[2]), fp8_sat(f[3]), lo, true);
+}
+
+// 8 bf16 (uint4) -> 8 e4m3 bytes (uint2)
+__device__ __forceinline__ uint2 bf16x8_to_fp8x8(const uint4& v) {
+    float f[8];
+    unpack8(v, f);
+    return make_uint2(pack_fp8x4(f), pack_fp8x4(f + 4));
+}
+
+// 4 e4m3 bytes -> 4 bf16 (uint2): v_cvt_scalef32_pk_bf16_fp8 x2 (scale 1)
+__device__ __forceinline__ uint2 fp8x4_to_bf16x4(uint32_t v) {
+    return make_uint2(__builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v, 1.f, false)),
+                      __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v, 1.f, true)));
+}
+
+// 8 e4m3 bytes -> 8 bf16 (uint4)
+__device__ __forceinline__ uint4 fp8x8_to_bf16x8(const uint2& v) {
+    const uint2 a = fp8x4_to_bf16x4(v.x), b = fp8x4_to_bf16x4(v.y);
+    return make_uint4(a.x, a.y, b.x, b.y);
+}
+
+// 8 consecutive cache elements at element offset `off` as bf16: a 16-B load
+// of a bf16 cache or an 8-B load + conversion of an fp8 one
+template <bool KV8>
+__device__ __forceinline__ uint4 load_kv8(const void* base, size_t off) {
+    if constexpr (KV8)
+        return fp8x8_to_bf16x8(*reinterpret_cast<const uint2*>(static_cast<const uint8_t*>(base) + off));
+    else
+        return *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(base) + off);
+}
 
 }  // namespace

@@ -109,14 +109,16 @@ __global__ __launch_bounds__(kBlock) void add_rmsnorm_kernel(const uint16_t* __r
 //    qkv  [T, (Hq + 2 Hkv) * D]  ->  q_out [T, Hq, D]
 //    k/v cache [S, Hkv, MAXS, D] written at (slot[t], :, pos[t], :)
 //    cos_sin [max_pos, D/2] float2 (cos, sin)
+//    KV8: the caches hold fp8 e4m3 (saturated), q stays bf16
 // --------------------------------------------------------------------------
+template <bool KV8>
 __global__ __launch_bounds__(kBlock) void rope_kv_kernel(const uint16_t* __restrict__ qkv,
                                                         const int32_t* __restrict__ pos,
                                                         const int32_t* __restrict__ slot,
                                                         const float2* __restrict__ cos_sin,
                                                         uint16_t* __restrict__ q_out,
-                                                        uint16_t* __restrict__ k_cache,
-                                                        uint16_t* __restrict__ v_cache, int Hq, int Hkv,
+                                                        void* __restrict__ k_cache,
+                                                        void* __restrict__ v_cache, int Hq, int Hkv,
                                                         int D, int max_seq, int max_pos, int num_slots) {
     const int t = blockIdx.x;
     const int p = pos[t];
@@ -140,15 +142,23 @@ __global__ __launch_bounds__(kBlock) void rope_kv_kernel(const uint16_t* __restr
             o1[j] = x1[j] * c.x - x2[j] * c.y;
             o2[j] = x2[j] * c.x + x1[j] * c.y;
         }
-        uint16_t* dst;
         if (hh < Hq) {
-            dst = q_out + ((size_t)t * Hq + hh) * D;
-        } else {
-            if (!write_cache) continue;
-            dst = k_cache + (((size_t)s * Hkv + (hh - Hq)) * max_seq + p) * D;
+            uint16_t* dst = q_out + ((size_t)t * Hq + hh) * D;
+            *reinterpret_cast<uint2*>(dst + d0) = pack4(o1);
+            *reinterpret_cast<uint2*>(dst + half + d0) = pack4(o2);
+            continue;
         }
-        *reinterpret_cast<uint2*>(dst + d0) = pack4(o1);
-        *reinterpret_cast<uint2*>(dst + half + d0) = pack4(o2);
+        if (!write_cache) continue;
+        const size_t kofs = (((size_t)s * Hkv + (hh - Hq)) * max_seq + p) * D;
+        if constexpr (KV8) {
+            uint8_t* dst = static_cast<uint8_t*>(k_cache) + kofs;
+            *reinterpret_cast<uint32_t*>(dst + d0) = pack_fp8x4(o1);
+            *reinterpret_cast<uint32_t*>(dst + half + d0) = pack_fp8x4(o2);
+        } else {
+            uint16_t* dst = static_cast<uint16_t*>(k_cache) + kofs;
+            *reinterpret_cast<uint2*>(dst + d0) = pack4(o1);
+            *reinterpret_cast<uint2*>(dst + half + d0) = pack4(o2);
+        }
     }
     if (!write_cache) return;
     const int vvec = (Hkv * D) >> 3;
@@ -157,8 +167,11 @@ __global__ __launch_bounds__(kBlock) void rope_kv_kernel(const uint16_t* __restr
         const int e = u << 3;
         const int kh = e / D;
         const int d = e - kh * D;
-        uint16_t* dst = v_cache + (((size_t)s * Hkv + kh) * max_seq + p) * D + d;
-        *reinterpret_cast<uint4*>(dst) = vsrc[u];
+        const size_t vofs = (((size_t)s * Hkv + kh) * max_seq + p) * D + d;
+        if constexpr (KV8)
+            *reinterpret_cast<uint2*>(static_cast<uint8_t*>(v_cache) + vofs) = bf16x8_to_fp8x8(vsrc[u]);
+        else
+            *reinterpret_cast<uint4*>(static_cast<uint16_t*>(v_cache) + vofs) = vsrc[u];
     }
 }
 
@@ -474,9 +487,9 @@ __global__ __launch_bounds__(kBlock) void decode_attn_combine_kernel(const float
 
 constexpr int kPrefixChunk = 256;  // keys per prefix split (host passes the same)
 
-template <int D>
+template <int D, bool KV8>
 __global__ __launch_bounds__(kBlock) void prefix_attn_kernel(
-    const uint16_t* __restrict__ q, const uint16_t* __restrict__ pk, const uint16_t* __restrict__ vt,
+    const uint16_t* __restrict__ q, const void* __restrict__ pk, const void* __restrict__ vt,
     const int32_t* __restrict__ plen, float* __restrict__ part_o, float* __restrict__ part_ml, int B, int Hkv, int G,
     int ldk, int ldv, int ps_max, int splits_total, float scale_log2) {
     constexpr int PCH = kPrefixChunk;
@@ -512,22 +525,20 @@ __global__ __launch_bounds__(kBlock) void prefix_attn_kernel(
         {
             constexpr int KU = PCH * (D / 8) / kBlock;  // uint4 per thread, K
             constexpr int VU = D * (PCH / 8) / kBlock;  // uint4 per thread, V^T
-            const uint16_t* kg = pk + ((size_t)kh * ldk + kbeg) * D;
-            const uint16_t* vg = vt + (size_t)kh * D * ldv + kbeg;
+            const size_t kg = ((size_t)kh * ldk + kbeg) * D;  // element offsets (bf16 or fp8 caches)
+            const size_t vg = (size_t)kh * D * ldv + kbeg;
             uint4 kx[KU], vx[VU];
 #pragma unroll
             for (int i = 0; i < KU; ++i) {
                 const int u = threadIdx.x + i * kBlock;
                 const int row = u / (D / 8), c = u - row * (D / 8);
-                kx[i] = kbeg + row < kend ? *reinterpret_cast<const uint4*>(kg + (size_t)row * D + c * 8)
-                                          : make_uint4(0, 0, 0, 0);
+                kx[i] = kbeg + row < kend ? load_kv8<KV8>(pk, kg + (size_t)row * D + c * 8) : make_uint4(0, 0, 0, 0);
             }
 #pragma unroll
             for (int i = 0; i < VU; ++i) {
                 const int u = threadIdx.x + i * kBlock;
                 const int d = u / (PCH / 8), c = u - d * (PCH / 8);
-                vx[i] = kbeg + c * 8 < kend ? *reinterpret_cast<const uint4*>(vg + (size_t)d * ldv + c * 8)
-                                            : make_uint4(0, 0, 0, 0);
+                vx[i] = kbeg + c * 8 < kend ? load_kv8<KV8>(vt, vg + (size_t)d * ldv + c * 8) : make_uint4(0, 0, 0, 0);
             }
 #pragma unroll
             for (int i = 0; i < KU; ++i) {
@@ -728,26 +739,44 @@ __global__ __launch_bounds__(kBlock) void embedding_kernel(const uint16_t* __res
 // from one per-tile base plus compile-time offsets (no per-load 64-bit
 // address math); the partial last tile of a split clamps every key to
 // end-1 (in-bounds, finite; masked later).
+template <int D, bool KV8>
+struct KVTile;
+
 template <int D>
-struct KVTile {
-    uint4 k[2][D / 32];
-    uint4 v[D / 16];
+struct KVTile<D, false> {
+    uint4 k[2][D / 32];  // 8 bf16 per (half, k-step)
+    uint4 v[D / 16];     // 8 bf16 per chunk
 };
 
 template <int D>
-__device__ __forceinline__ void load_kv_tile(const uint16_t* __restrict__ kb, const uint16_t* __restrict__ vb,
-                                             int kt, int end, int lane, KVTile<D>& t) {
-    constexpr int CPK = D / 8;
+struct KVTile<D, true> {
+    uint2 k[2][D / 32];  // 8 e4m3 per (half, k-step)
+    uint4 v[D / 32];     // 16 e4m3 per chunk
+};
+
+// element offset -> byte address of a bf16 or fp8 cache
+template <bool KV8>
+__device__ __forceinline__ const char* kv_at(const void* base, size_t off) {
+    return static_cast<const char*>(base) + off * (KV8 ? 1 : 2);
+}
+
+template <int D, bool KV8>
+__device__ __forceinline__ void load_kv_tile(const void* __restrict__ kb, const void* __restrict__ vb, int kt,
+                                             int end, int lane, KVTile<D, KV8>& t) {
+    using KRaw = std::conditional_t<KV8, uint2, uint4>;
+    constexpr int VE = KV8 ? 16 : 8;  // elements per V chunk
+    constexpr int CPK = D / VE;       // V chunks per key
+    constexpr int NV = 32 * D / VE / kWave;
     if (kt + 32 <= end) {
-        const uint16_t* kp = kb + (size_t)(kt + (lane & 15)) * D + 8 * (lane >> 4);
-        const uint16_t* vp = vb + (size_t)kt * D + lane * 8;
+        const char* kp = kv_at<KV8>(kb, (size_t)(kt + (lane & 15)) * D + 8 * (lane >> 4));
+        const char* vp = kv_at<KV8>(vb, (size_t)kt * D + lane * VE);
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
             for (int ks = 0; ks < D / 32; ++ks)
-                t.k[h][ks] = *reinterpret_cast<const uint4*>(kp + 16 * h * D + 32 * ks);
+                t.k[h][ks] = *reinterpret_cast<const KRaw*>(kp + (16 * h * D + 32 * ks) * (KV8 ? 1 : 2));
 #pragma unroll
-        for (int r = 0; r < D / 16; ++r) t.v[r] = *reinterpret_cast<const uint4*>(vp + kWave * 8 * r);
+        for (int r = 0; r < NV; ++r) t.v[r] = *reinterpret_cast<const uint4*>(vp + 16 * kWave * r);
         return;
     }
 #pragma unroll
@@ -755,45 +784,62 @@ __device__ __forceinline__ void load_kv_tile(const uint16_t* __restrict__ kb, co
         const int key = min(kt + 16 * h + (lane & 15), end - 1);
 #pragma unroll
         for (int ks = 0; ks < D / 32; ++ks)
-            t.k[h][ks] = *reinterpret_cast<const uint4*>(kb + (size_t)key * D + 32 * ks + 8 * (lane >> 4));
+            t.k[h][ks] = *reinterpret_cast<const KRaw*>(kv_at<KV8>(kb, (size_t)key * D + 32 * ks + 8 * (lane >> 4)));
     }
 #pragma unroll
-    for (int r = 0; r < D / 16; ++r) {
+    for (int r = 0; r < NV; ++r) {
         const int ch = lane + kWave * r;
         const int key = min(kt + ch / CPK, end - 1);
-        t.v[r] = *reinterpret_cast<const uint4*>(vb + (size_t)key * D + (ch % CPK) * 8);
+        t.v[r] = *reinterpret_cast<const uint4*>(kv_at<KV8>(vb, (size_t)key * D + (ch % CPK) * VE));
     }
 }
 
 // One tile of the MFMA per-row kernel: V -> the wave's LDS tile, S^T on the
 // matrix cores, then (prefetch) the tile two ahead is loaded into the same
 // registers while the softmax and the PV product run.
-template <int D>
-__device__ __forceinline__ void attn_tile_mfma(KVTile<D>& cur, bool prefetch, int kt_next,
-                                               const uint16_t* __restrict__ kb, const uint16_t* __restrict__ vb,
+template <int D, bool KV8>
+__device__ __forceinline__ void attn_tile_mfma(KVTile<D, KV8>& cur, bool prefetch, int kt_next,
+                                               const void* __restrict__ kb, const void* __restrict__ vb,
                                                int kt, int end, int lane, int g16, uint16_t* vw,
                                                const uint16_t* tr0, const uint16_t* tr1,
                                                const bf16x8_t (&qf)[D / 32], float& m, float& l,
                                                f32x4_t (&acc)[D / 16], float scale_log2) {
     constexpr int KS = D / 32;
     constexpr int DB = D / 16;
-    constexpr int CPK = D / 8;
     constexpr int VROW = D + 8;
     const bool partial = kt + 32 > end;
+    if constexpr (KV8) {  // 16 e4m3 per chunk -> two 8-bf16 LDS stores
+        constexpr int CPK = D / 16;
 #pragma unroll
-    for (int r = 0; r < D / 16; ++r) {
-        const int ch = lane + kWave * r;
-        *reinterpret_cast<uint4*>(vw + (ch / CPK) * VROW + (ch % CPK) * 8) = cur.v[r];
+        for (int r = 0; r < D / 32; ++r) {
+            const int ch = lane + kWave * r;
+            uint16_t* dst = vw + (ch / CPK) * VROW + (ch % CPK) * 16;
+            *reinterpret_cast<uint4*>(dst) = fp8x8_to_bf16x8(make_uint2(cur.v[r].x, cur.v[r].y));
+            *reinterpret_cast<uint4*>(dst + 8) = fp8x8_to_bf16x8(make_uint2(cur.v[r].z, cur.v[r].w));
+        }
+    } else {
+        constexpr int CPK = D / 8;
+#pragma unroll
+        for (int r = 0; r < D / 16; ++r) {
+            const int ch = lane + kWave * r;
+            *reinterpret_cast<uint4*>(vw + (ch / CPK) * VROW + (ch % CPK) * 8) = cur.v[r];
+        }
     }
     f32x4_t sacc[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         sacc[h] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
-            sacc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(cur.k[h][ks]), qf[ks], sacc[h], 0, 0, 0);
+        for (int ks = 0; ks < KS; ++ks) {
+            bf16x8_t kf;
+            if constexpr (KV8)
+                kf = as_bf16x8(fp8x8_to_bf16x8(cur.k[h][ks]));
+            else
+                kf = as_bf16x8(cur.k[h][ks]);
+            sacc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], sacc[h], 0, 0, 0);
+        }
     }
-    if (prefetch) load_kv_tile<D>(kb, vb, kt_next, end, lane, cur);
+    if (prefetch) load_kv_tile<D, KV8>(kb, vb, kt_next, end, lane, cur);
     // S^T tile: register 4h+i = key kt + 16h + 4*g16 + i of query (lane&15).
     // Scale folded into one FMA per score; the key mask only on a partial
     // last tile; hardware exp2 and bf16 packing.
@@ -878,9 +924,9 @@ __device__ __forceinline__ void attn_tile_mfma(KVTile<D>& cur, bool prefetch, in
 //    No block-level synchronisation: each wave owns its LDS tile, so
 //    different waves of a block run different items.
 // --------------------------------------------------------------------------
-template <int D, bool kDouble>
+template <int D, bool kDouble, bool KV8>
 __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
-    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache,
+    const uint16_t* __restrict__ q, const void* __restrict__ k_cache, const void* __restrict__ v_cache,
     const int32_t* __restrict__ slot, const int32_t* __restrict__ seq_len, uint16_t* __restrict__ out,
     float* __restrict__ part_o, float* __restrict__ part_ml, int B, int Hkv, int G,
     int max_seq, int chunk, int splits, float scale_log2, int num_slots, const int32_t* __restrict__ plen,
@@ -933,31 +979,31 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
             qf[ks] = as_bf16x8(v);
         }
         const size_t head_off = ((size_t)s * Hkv + kh) * (size_t)max_seq * D;
-        const uint16_t* kb = k_cache + head_off;
-        const uint16_t* vb = v_cache + head_off;
+        const void* kb = kv_at<KV8>(k_cache, head_off);
+        const void* vb = kv_at<KV8>(v_cache, head_off);
         float m = -1e30f, l = 0.f;
         f32x4_t acc[DB];
 #pragma unroll
         for (int db = 0; db < DB; ++db) acc[db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
         if (kDouble) {
-            KVTile<D> ta, tb;
-            load_kv_tile<D>(kb, vb, start, end, lane, ta);
-            if (ntiles > 1) load_kv_tile<D>(kb, vb, start + 32, end, lane, tb);
+            KVTile<D, KV8> ta, tb;
+            load_kv_tile<D, KV8>(kb, vb, start, end, lane, ta);
+            if (ntiles > 1) load_kv_tile<D, KV8>(kb, vb, start + 32, end, lane, tb);
             for (int t = 0; t < ntiles; t += 2) {
                 const int kt = start + 32 * t;
-                attn_tile_mfma<D>(ta, t + 2 < ntiles, kt + 64, kb, vb, kt, end, lane, g16, vw, tr0, tr1, qf, m, l,
-                                  acc, scale_log2);
+                attn_tile_mfma<D, KV8>(ta, t + 2 < ntiles, kt + 64, kb, vb, kt, end, lane, g16, vw, tr0, tr1, qf, m,
+                                       l, acc, scale_log2);
                 if (t + 1 < ntiles)
-                    attn_tile_mfma<D>(tb, t + 3 < ntiles, kt + 96, kb, vb, kt + 32, end, lane, g16, vw, tr0, tr1, qf,
-                                      m, l, acc, scale_log2);
+                    attn_tile_mfma<D, KV8>(tb, t + 3 < ntiles, kt + 96, kb, vb, kt + 32, end, lane, g16, vw, tr0, tr1,
+                                           qf, m, l, acc, scale_log2);
             }
         } else {
-            KVTile<D> ta;
-            load_kv_tile<D>(kb, vb, start, end, lane, ta);
+            KVTile<D, KV8> ta;
+            load_kv_tile<D, KV8>(kb, vb, start, end, lane, ta);
             for (int t = 0; t < ntiles; ++t) {
                 const int kt = start + 32 * t;
-                attn_tile_mfma<D>(ta, t + 1 < ntiles, kt + 32, kb, vb, kt, end, lane, g16, vw, tr0, tr1, qf, m, l,
-                                  acc, scale_log2);
+                attn_tile_mfma<D, KV8>(ta, t + 1 < ntiles, kt + 32, kb, vb, kt, end, lane, g16, vw, tr0, tr1, qf, m,
+                                       l, acc, scale_log2);
             }
         }
         l += __shfl_xor(l, 16, kWave);
@@ -1052,7 +1098,7 @@ hipError_t launch_decode_d(int G, dim3 grid, const uint16_t* q, const uint16_t* 
 
 extern "C" {
 
-int dmcp_abi_version() { return 8; }
+int dmcp_abi_version() { return 9; }
 
 // Selects the per-row decode attention kernel (0 = MFMA, 1 = VALU, 2 = MFMA double-buffered);
 // returns the previous choice.
@@ -1079,20 +1125,26 @@ int dmcp_add_rmsnorm(const void* x, void* residual, const void* w, void* out, in
 
 int dmcp_rope_kv(const void* qkv, const void* pos, const void* slot, const void* cos_sin, void* q_out,
                  void* k_cache, void* v_cache, int T, int Hq, int Hkv, int D, int max_seq, int max_pos,
-                 int num_slots, void* stream) {
+                 int num_slots, int kv8, void* stream) {
     if (T <= 0) return 0;
     if (D % 16 != 0) return hipErrorInvalidValue;
-    rope_kv_kernel<<<T, kBlock, 0, (hipStream_t)stream>>>((const uint16_t*)qkv, (const int32_t*)pos,
-                                                          (const int32_t*)slot, (const float2*)cos_sin,
-                                                          (uint16_t*)q_out, (uint16_t*)k_cache,
-                                                          (uint16_t*)v_cache, Hq, Hkv, D, max_seq, max_pos, num_slots);
+    auto st = (hipStream_t)stream;
+    if (kv8)
+        rope_kv_kernel<true><<<T, kBlock, 0, st>>>((const uint16_t*)qkv, (const int32_t*)pos, (const int32_t*)slot,
+                                                   (const float2*)cos_sin, (uint16_t*)q_out, k_cache, v_cache, Hq,
+                                                   Hkv, D, max_seq, max_pos, num_slots);
+    else
+        rope_kv_kernel<false><<<T, kBlock, 0, st>>>((const uint16_t*)qkv, (const int32_t*)pos, (const int32_t*)slot,
+                                                    (const float2*)cos_sin, (uint16_t*)q_out, k_cache, v_cache, Hq,
+                                                    Hkv, D, max_seq, max_pos, num_slots);
     return hipGetLastError();
 }
 
 int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cache, const void* slot,
                           const void* seq_len, void* out, void* part_o, void* part_ml, int B, int Hq, int Hkv, int D,
                           int max_seq, int num_slots, int chunk, int splits, float scale, const void* prefix_k,
-                          const void* prefix_vt, const void* plen, int ldv, int pchunk, int ps_max, void* stream) {
+                          const void* prefix_vt, const void* plen, int ldv, int pchunk, int ps_max, int kv8,
+                          void* stream) {
     if (B <= 0) return 0;
     if (Hkv <= 0 || Hq % Hkv != 0 || splits <= 0 || chunk <= 0) return hipErrorInvalidValue;
     const bool prefix = plen != nullptr;
@@ -1113,17 +1165,16 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
         // one block per (kv head, prefix split, 4 query tiles); exits at once when *plen == 0
         const long items = (long)Hkv * ps_max * ((((B * G + 31) / 32) + 3) / 4);
         dim3 pgrid((unsigned)(items < cap ? items : cap));
-        if (D == 64)
-            prefix_attn_kernel<64><<<pgrid, kBlock, 0, st>>>(qq, (const uint16_t*)prefix_k, (const uint16_t*)prefix_vt,
-                                                           pl, (float*)part_o, (float*)part_ml, B, Hkv, G, max_seq,
-                                                           ldv, ps_max, ps_max + splits, sl2);
-        else if (D == 128)
-            prefix_attn_kernel<128><<<pgrid, kBlock, 0, st>>>(qq, (const uint16_t*)prefix_k,
-                                                            (const uint16_t*)prefix_vt, pl, (float*)part_o,
-                                                            (float*)part_ml, B, Hkv, G, max_seq, ldv, ps_max,
-                                                            ps_max + splits, sl2);
-        else
-            return hipErrorInvalidValue;
+#define DMCP_PREFIX(DD, K8)                                                                                   \
+    prefix_attn_kernel<DD, K8><<<pgrid, kBlock, 0, st>>>(qq, prefix_k, prefix_vt, pl, (float*)part_o,             \
+                                                         (float*)part_ml, B, Hkv, G, max_seq, ldv, ps_max,       \
+                                                         ps_max + splits, sl2)
+        if (D == 64 && kv8) DMCP_PREFIX(64, true);
+        else if (D == 64) DMCP_PREFIX(64, false);
+        else if (D == 128 && kv8) DMCP_PREFIX(128, true);
+        else if (D == 128) DMCP_PREFIX(128, false);
+        else return hipErrorInvalidValue;
+#undef DMCP_PREFIX
         hipError_t pe = hipGetLastError();
         if (pe != hipSuccess) return pe;
     }
@@ -1133,19 +1184,29 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
     auto kk = (const uint16_t*)k_cache;
     auto vv = (const uint16_t*)v_cache;
     hipError_t e;
-    if ((g_decode_impl == 0 || g_decode_impl == 2) && (D == 64 || D == 128) && G <= 16) {
+    if (kv8 && !((D == 64 || D == 128) && G <= 16)) return hipErrorInvalidValue;  // fp8 KV: MFMA kernel only
+    if ((g_decode_impl == 0 || g_decode_impl == 2 || kv8) && (D == 64 || D == 128) && G <= 16) {
         // one wave per item: a block runs 4 items
         const long wblocks = (items + 3) / 4;
         dim3 wgrid((unsigned)(wblocks < cap ? wblocks : cap));
         float* po = (float*)part_o;
         float* pml = (float*)part_ml;
         uint16_t* oo = (uint16_t*)out;
-#define DMCP_MFMA_DECODE(DD, DBL)                                                                            \
-    decode_attn_mfma_kernel<DD, DBL><<<wgrid, kBlock, 0, st>>>(qq, kk, vv, sl, ln, oo, po, pml, B, Hkv, G,    \
-                                                               max_seq, chunk, splits, sl2, num_slots, pl, ps_max)
-        if (D == 64 && g_decode_impl == 2) DMCP_MFMA_DECODE(64, true);
-        else if (D == 64) DMCP_MFMA_DECODE(64, false);
-        else DMCP_MFMA_DECODE(128, false);
+#define DMCP_MFMA_DECODE(DD, DBL, K8)                                                                       \
+    decode_attn_mfma_kernel<DD, DBL, K8><<<wgrid, kBlock, 0, st>>>(qq, k_cache,                                \
+                                                                   v_cache, sl, ln, oo, po, pml, B, Hkv, G,     \
+                                                                   max_seq, chunk, splits, sl2, num_slots, pl,  \
+                                                                   ps_max)
+        if (kv8) {
+            if (D == 64) DMCP_MFMA_DECODE(64, false, true);
+            else DMCP_MFMA_DECODE(128, false, true);
+        } else if (D == 64 && g_decode_impl == 2) {
+            DMCP_MFMA_DECODE(64, true, false);
+        } else if (D == 64) {
+            DMCP_MFMA_DECODE(64, false, false);
+        } else {
+            DMCP_MFMA_DECODE(128, false, false);
+        }
 #undef DMCP_MFMA_DECODE
         e = hipGetLastError();
         if (e != hipSuccess || (splits == 1 && !prefix)) return e;

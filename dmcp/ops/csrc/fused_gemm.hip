@@ -45,9 +45,10 @@ struct FusedGemmArgs {
     const int32_t* slot;
     const float2* cos_sin;  // [max_pos, D/2] (cos, sin)
     uint16_t* q_out;        // [M, Hq, D]
-    uint16_t* k_cache;      // [S, Hkv, max_seq, D]
-    uint16_t* v_cache;
+    void* k_cache;          // [S, Hkv, max_seq, D], bf16 or (kv8) fp8 e4m3
+    void* v_cache;
     int Hq, Hkv, D, max_seq, max_pos, num_slots;
+    int kv8;
 };
 
 template <int EPI>
@@ -69,8 +70,6 @@ __device__ __forceinline__ int tile_row(const FusedGemmArgs& a, int t, int nb) {
         return 16 * t;
     }
 }
-
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
 // sum of squares of the 8 bf16 of a fragment, accumulated into acc
 __device__ __forceinline__ float sumsq8(const uint4& v, float acc) {
@@ -251,18 +250,26 @@ __global__ __launch_bounds__(WK * kWave) void fused_gemm_kernel(FusedGemmArgs a)
                     o2[i] = v[1][i];
                 }
             }
-            uint16_t* dst;
             if (hh < a.Hq) {
-                dst = a.q_out + ((size_t)m * a.Hq + hh) * D;
-            } else {
-                const int sl = a.slot[m];
-                if (p < 0 || p >= a.max_seq || sl < 0 || sl >= a.num_slots) continue;  // padding row
-                const int kv = hh < a.Hq + a.Hkv ? hh - a.Hq : hh - a.Hq - a.Hkv;
-                uint16_t* cache = hh < a.Hq + a.Hkv ? a.k_cache : a.v_cache;
-                dst = cache + (((size_t)sl * a.Hkv + kv) * a.max_seq + p) * D;
+                uint16_t* dst = a.q_out + ((size_t)m * a.Hq + hh) * D;
+                *reinterpret_cast<uint2*>(dst + d0) = pack4(o1);
+                *reinterpret_cast<uint2*>(dst + d0 + half) = pack4(o2);
+                continue;
             }
-            *reinterpret_cast<uint2*>(dst + d0) = pack4(o1);
-            *reinterpret_cast<uint2*>(dst + d0 + half) = pack4(o2);
+            const int sl = a.slot[m];
+            if (p < 0 || p >= a.max_seq || sl < 0 || sl >= a.num_slots) continue;  // padding row
+            const int kv = hh < a.Hq + a.Hkv ? hh - a.Hq : hh - a.Hq - a.Hkv;
+            void* cache = hh < a.Hq + a.Hkv ? a.k_cache : a.v_cache;
+            const size_t off = (((size_t)sl * a.Hkv + kv) * a.max_seq + p) * D;
+            if (a.kv8) {
+                uint8_t* dst = static_cast<uint8_t*>(cache) + off;
+                *reinterpret_cast<uint32_t*>(dst + d0) = pack_fp8x4(o1);
+                *reinterpret_cast<uint32_t*>(dst + d0 + half) = pack_fp8x4(o2);
+            } else {
+                uint16_t* dst = static_cast<uint16_t*>(cache) + off;
+                *reinterpret_cast<uint2*>(dst + d0) = pack4(o1);
+                *reinterpret_cast<uint2*>(dst + d0 + half) = pack4(o2);
+            }
         }
     }
 }
@@ -298,12 +305,13 @@ int dmcp_fused_gemm_max_rows() { return 128; }
 // guard the tiling assumptions.
 int dmcp_fused_gemm(int epi, int wk, const void* x, const void* w, void* out, int M, int K, int N, float eps,
                     int inter, const void* pos, const void* slot, const void* cos_sin, void* q_out, void* k_cache,
-                    void* v_cache, int Hq, int Hkv, int D, int max_seq, int max_pos, int num_slots, void* stream) {
+                    void* v_cache, int Hq, int Hkv, int D, int max_seq, int max_pos, int num_slots, int kv8,
+                    void* stream) {
     if (M <= 0) return 0;
     if (M > 128 || K <= 0 || K % 32 != 0 || N <= 0 || !x || !w) return hipErrorInvalidValue;
     FusedGemmArgs a{(const uint16_t*)x, (const uint16_t*)w, (uint16_t*)out, M, K, N, eps, inter,
                     (const int32_t*)pos, (const int32_t*)slot, (const float2*)cos_sin, (uint16_t*)q_out,
-                    (uint16_t*)k_cache, (uint16_t*)v_cache, Hq, Hkv, D, max_seq, max_pos, num_slots};
+                    k_cache, v_cache, Hq, Hkv, D, max_seq, max_pos, num_slots, kv8};
     auto st = (hipStream_t)stream;
     int tiles;
     switch (epi) {

@@ -72,10 +72,10 @@ __device__ __forceinline__ v4i16_t lds_tr16(const uint16_t* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16_t*)(p));
 }
 
-template <int D, int NSUB, int NWAVE>
+template <int D, int NSUB, int NWAVE, bool KV8>
 __global__ __launch_bounds__(NWAVE * 64) void prefill_attn_kernel(
-    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
-    const uint16_t* __restrict__ pk, const uint16_t* __restrict__ pv, uint16_t* __restrict__ out,
+    const uint16_t* __restrict__ q, const void* __restrict__ kc, const void* __restrict__ vc,
+    const void* __restrict__ pk, const void* __restrict__ pv, uint16_t* __restrict__ out,
     float* __restrict__ part_o, float* __restrict__ part_ml, int T, int start, int P, int Hkv, int G, int ldk,
     int ctiles, int nsplit, float sl2) {
     constexpr int KS = D / 16;  // k-steps of the QK product
@@ -129,8 +129,9 @@ __global__ __launch_bounds__(NWAVE * 64) void prefill_attn_kernel(
             for (int i = 0; i < 16; ++i) o[u][t2][i] = 0.f;
     }
 
-    // register-staged K/V tiles: rows past kend are zero (never visible:
-    // every such key is after every query of the block)
+    // register-staged K/V tiles (fp8 caches converted to bf16 here, so the
+    // LDS image and everything after it is the same): rows past kend are zero
+    // (never visible: every such key is after every query of the block)
     uint4 kx[LU], vx[LU];
     auto load = [&](int st) {
 #pragma unroll
@@ -141,8 +142,8 @@ __global__ __launch_bounds__(NWAVE * 64) void prefill_attn_kernel(
             if (key < kend) {
                 const bool pre = key < P;
                 const size_t off = ((size_t)kh * ldk + key) * D + ch * 8;
-                kx[i] = *reinterpret_cast<const uint4*>((pre ? pk : kc) + off);
-                vx[i] = *reinterpret_cast<const uint4*>((pre ? pv : vc) + off);
+                kx[i] = load_kv8<KV8>(pre ? pk : kc, off);
+                vx[i] = load_kv8<KV8>(pre ? pv : vc, off);
             } else {
                 kx[i] = make_uint4(0, 0, 0, 0);
                 vx[i] = make_uint4(0, 0, 0, 0);
@@ -321,13 +322,13 @@ __global__ __launch_bounds__(kBlock) void prefill_combine_kernel(const float* __
     *reinterpret_cast<uint2*>(out + row * D + d) = pack4(f);
 }
 
-template <int D, int NSUB, int NWAVE>
-hipError_t launch_prefill(const uint16_t* q, const uint16_t* k, const uint16_t* v, const uint16_t* pk,
-                          const uint16_t* pv, uint16_t* out, float* po, float* pml, int T, int start, int P, int Hkv,
-                          int G, int ldk, int nsplit, float sl2, hipStream_t st) {
+template <int D, int NSUB, int NWAVE, bool KV8>
+hipError_t launch_prefill(const uint16_t* q, const void* k, const void* v, const void* pk, const void* pv,
+                          uint16_t* out, float* po, float* pml, int T, int start, int P, int Hkv, int G, int ldk,
+                          int nsplit, float sl2, hipStream_t st) {
     constexpr int COLS = 32 * NSUB * NWAVE;
     const int ctiles = (T * G + COLS - 1) / COLS;
-    prefill_attn_kernel<D, NSUB, NWAVE><<<dim3((unsigned)(ctiles * Hkv * nsplit)), NWAVE * kWave, 0, st>>>(
+    prefill_attn_kernel<D, NSUB, NWAVE, KV8><<<dim3((unsigned)(ctiles * Hkv * nsplit)), NWAVE * kWave, 0, st>>>(
         q, k, v, pk, pv, out, po, pml, T, start, P, Hkv, G, ldk, ctiles, nsplit, sl2);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || nsplit == 1) return e;
@@ -354,7 +355,7 @@ extern "C" {
 // second kernel.
 int dmcp_prefill_attention(const void* q, const void* k, const void* v, const void* pk, const void* pv, void* out,
                            void* part_o, void* part_ml, int T, int start, int P, int Hq, int Hkv, int D, int ldk,
-                           float scale, int variant, int nsplit, void* stream) {
+                           float scale, int variant, int nsplit, int kv8, void* stream) {
     if (T <= 0) return 0;
     if (!q || !k || !v || !out || Hkv <= 0 || Hq % Hkv != 0 || start < 0 || P < 0 || P > start ||
         start + T > ldk || (P > 0 && (!pk || !pv)) || nsplit < 1 || nsplit > 64 ||
@@ -365,15 +366,16 @@ int dmcp_prefill_attention(const void* q, const void* k, const void* v, const vo
     const float sl2 = scale * 1.4426950408889634f;
     auto st = (hipStream_t)stream;
     auto qq = (const uint16_t*)q;
-    auto kk = (const uint16_t*)k;
-    auto vv = (const uint16_t*)v;
-    auto ppk = P > 0 ? (const uint16_t*)pk : kk;
-    auto ppv = P > 0 ? (const uint16_t*)pv : vv;
+    const void* ppk = P > 0 ? pk : k;
+    const void* ppv = P > 0 ? pv : v;
     auto oo = (uint16_t*)out;
     auto po = (float*)part_o;
     auto pml = (float*)part_ml;
-#define DMCP_PF(DD, NS, NW) \
-    launch_prefill<DD, NS, NW>(qq, kk, vv, ppk, ppv, oo, po, pml, T, start, P, Hkv, G, ldk, nsplit, sl2, st)
+#define DMCP_PF(DD, NS, NW)                                                                                   \
+    (kv8 ? launch_prefill<DD, NS, NW, true>(qq, k, v, ppk, ppv, oo, po, pml, T, start, P, Hkv, G, ldk, nsplit, sl2, \
+                                            st)                                                                 \
+         : launch_prefill<DD, NS, NW, false>(qq, k, v, ppk, ppv, oo, po, pml, T, start, P, Hkv, G, ldk, nsplit,   \
+                                             sl2, st))
     if (D == 64) {
         switch (variant) {
             case 0: return DMCP_PF(64, 1, 4);

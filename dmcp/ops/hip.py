@@ -26,7 +26,7 @@ _lock = threading.Lock()
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _f = ctypes.c_float
-ABI_VERSION = 8  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
+ABI_VERSION = 9  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
 
 
 class HipOpsError(RuntimeError):
@@ -49,19 +49,19 @@ def lib() -> ctypes.CDLL:
         sigs = {
             "dmcp_abi_version": ([], _i),
             "dmcp_add_rmsnorm": ([_vp, _vp, _vp, _vp, _i, _i, _f, _vp], _i),
-            "dmcp_rope_kv": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp], _i),
+            "dmcp_rope_kv": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp], _i),
             "dmcp_decode_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _f,
-                                       _vp, _vp, _vp, _i, _i, _i, _vp],
+                                       _vp, _vp, _vp, _i, _i, _i, _i, _vp],
                                       _i),
             "dmcp_prefill_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _i, _i,
-                                        _vp], _i),
+                                        _i, _vp], _i),
             "dmcp_silu_mul": ([_vp, _vp, _i, _i, _vp], _i),
             "dmcp_masked_argmax": ([_vp, _vp, _vp, _i, _vp, _i, _i, _i, _vp], _i),
             "dmcp_embedding": ([_vp, _vp, _vp, _i, _i, _i, _vp], _i),
             "dmcp_set_decode_impl": ([_i], _i),
             "dmcp_fused_gemm_max_rows": ([], _i),
             "dmcp_fused_gemm": ([_i, _i, _vp, _vp, _vp, _i, _i, _i, _f, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i,
-                                 _i, _i, _i, _vp], _i),
+                                 _i, _i, _i, _i, _vp], _i),
         }
         for name, (args, res) in sigs.items():
             fn = getattr(L, name)
@@ -116,6 +116,21 @@ def _req(t: torch.Tensor, dtype: torch.dtype, name: str) -> None:
         raise HipOpsError(f"{name}: tensor must be contiguous")
 
 
+KV_DTYPES = (torch.bfloat16, torch.uint8)  # bf16 or fp8 e4m3 bytes (dmcp.ops.reference.kv_encode)
+
+
+def _req_kv(k_cache: torch.Tensor, v_cache: torch.Tensor, name: str) -> int:
+    """KV caches: same shape, both bf16 or both fp8 (uint8 storage); returns the kv8 flag."""
+    if k_cache.dtype not in KV_DTYPES or v_cache.dtype != k_cache.dtype:
+        raise HipOpsError(f"{name}: KV caches must both be bf16 or both fp8 (uint8), got {k_cache.dtype} / "
+                          f"{v_cache.dtype}")
+    _req(k_cache, k_cache.dtype, f"{name}.k_cache")
+    _req(v_cache, v_cache.dtype, f"{name}.v_cache")
+    if v_cache.shape != k_cache.shape:
+        raise HipOpsError(f"{name}: k/v cache shapes differ")
+    return int(k_cache.dtype == torch.uint8)
+
+
 def _req_out(t: torch.Tensor, dtype: torch.dtype, numel: int, name: str) -> None:
     """A caller-supplied output buffer: same checks as :func:`_req` plus room
     for the ``numel`` elements the kernel writes (an undersized buffer would be
@@ -154,8 +169,7 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos_sin: t
     S, Hkv, MAXS, D = k_cache.shape
     T = qkv.shape[0]
     _req(qkv, torch.bfloat16, "rope_kv.qkv")
-    _req(k_cache, torch.bfloat16, "rope_kv.k_cache")
-    _req(v_cache, torch.bfloat16, "rope_kv.v_cache")
+    kv8 = _req_kv(k_cache, v_cache, "rope_kv")
     _req(pos, torch.int32, "rope_kv.pos")
     _req(slot, torch.int32, "rope_kv.slot")
     _req(cos_sin, torch.float32, "rope_kv.cos_sin")
@@ -170,7 +184,7 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos_sin: t
         q_out = torch.empty((T, n_q_heads, D), dtype=torch.bfloat16, device=qkv.device)
     _req_out(q_out, torch.bfloat16, T * n_q_heads * D, "rope_kv.q_out")
     _check(lib().dmcp_rope_kv(_ptr(qkv), _ptr(pos), _ptr(slot), _ptr(cos_sin), _ptr(q_out), _ptr(k_cache),
-                              _ptr(v_cache), T, n_q_heads, Hkv, D, MAXS, max_pos, S, _stream()), "dmcp_rope_kv")
+                              _ptr(v_cache), T, n_q_heads, Hkv, D, MAXS, max_pos, S, kv8, _stream()), "dmcp_rope_kv")
     return q_out
 
 
@@ -223,8 +237,8 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     graph follows prefix changes (0 = no prefix)."""
     B, Hq, D = q.shape
     S, Hkv, MAXS, Dk = k_cache.shape
-    for t, n in ((q, "q"), (k_cache, "k_cache"), (v_cache, "v_cache")):
-        _req(t, torch.bfloat16, f"decode_attention.{n}")
+    _req(q, torch.bfloat16, "decode_attention.q")
+    kv8 = _req_kv(k_cache, v_cache, "decode_attention")
     _req(slot, torch.int32, "decode_attention.slot")
     _req(seq_len, torch.int32, "decode_attention.seq_len")
     if Dk != D or D not in (64, 128) or Hq % Hkv or (Hq // Hkv) not in (1, 2, 3, 4, 6, 8) or v_cache.shape != k_cache.shape:
@@ -242,8 +256,8 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     ldv = pchunk = 0
     if prefix is not None:
         pk, pvt, plen, pchunk = prefix.k, prefix.vt, prefix.length, prefix.chunk
-        _req(pk, torch.bfloat16, "decode_attention.prefix.k")
-        _req(pvt, torch.bfloat16, "decode_attention.prefix.vt")
+        _req(pk, k_cache.dtype, "decode_attention.prefix.k")
+        _req(pvt, k_cache.dtype, "decode_attention.prefix.vt")
         _req(plen, torch.int32, "decode_attention.prefix.length")
         ldv = pvt.shape[-1]
         if (tuple(pk.shape) != (Hkv, MAXS, D) or tuple(pvt.shape) != (Hkv, D, ldv) or ldv % PREFIX_CHUNK
@@ -264,7 +278,7 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
         part_o = part_ml = None
     _check(lib().dmcp_decode_attention(_ptr(q), _ptr(k_cache), _ptr(v_cache), _ptr(slot), _ptr(seq_len), _ptr(out),
                                        _ptr(part_o), _ptr(part_ml), B, Hq, Hkv, D, MAXS, S, chunk, splits,
-                                       float(scale), _ptr(pk), _ptr(pvt), _ptr(plen), ldv, pchunk, ps_max,
+                                       float(scale), _ptr(pk), _ptr(pvt), _ptr(plen), ldv, pchunk, ps_max, kv8,
                                        _stream()), "dmcp_decode_attention")
     return out
 
@@ -298,8 +312,8 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
     Returns [T, Hq, D] bf16."""
     T, Hq, D = q.shape
     S, Hkv, MAXS, Dk = k_cache.shape
-    for t, n in ((q, "q"), (k_cache, "k_cache"), (v_cache, "v_cache")):
-        _req(t, torch.bfloat16, f"prefill_attention.{n}")
+    _req(q, torch.bfloat16, "prefill_attention.q")
+    kv8 = _req_kv(k_cache, v_cache, "prefill_attention")
     if Dk != D or v_cache.shape != k_cache.shape or not prefill_supported(Hq, Hkv, D):
         raise HipOpsError(f"prefill_attention: unsupported shape q={tuple(q.shape)} kv={tuple(k_cache.shape)}")
     slot, start, prefix_len = int(slot), int(start), int(prefix_len)
@@ -324,7 +338,7 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
         part_ml = torch.empty(nsplit * T * Hq * 2, dtype=torch.float32, device=q.device)
     _check(lib().dmcp_prefill_attention(_ptr(q), _ptr(k_cache[slot]), _ptr(v_cache[slot]), _ptr(pk), _ptr(pv),
                                         _ptr(out), _ptr(part_o), _ptr(part_ml), T, start, prefix_len, Hq, Hkv, D,
-                                        MAXS, float(scale), int(variant), int(nsplit), _stream()),
+                                        MAXS, float(scale), int(variant), int(nsplit), kv8, _stream()),
            "dmcp_prefill_attention")
     return out
 
@@ -421,12 +435,13 @@ def _fused_xw(x: torch.Tensor, w: torch.Tensor, name: str) -> tuple:
 
 
 def _fused(epi: str, wk: int, x, w, out, M, K, N, eps=0.0, inter=0, pos=None, slot=None, cos_sin=None,
-           q_out=None, k_cache=None, v_cache=None, Hq=0, Hkv=0, D=0, max_seq=0, max_pos=0, num_slots=0) -> None:
+           q_out=None, k_cache=None, v_cache=None, Hq=0, Hkv=0, D=0, max_seq=0, max_pos=0, num_slots=0,
+           kv8=0) -> None:
     if wk not in (4, 8, 16):
         raise HipOpsError(f"fused_gemm: wk must be 4, 8 or 16 (got {wk})")
     _check(lib().dmcp_fused_gemm(FUSED_EPI[epi], wk, _ptr(x), _ptr(w), _ptr(out), M, K, N, float(eps), inter,
                                  _ptr(pos), _ptr(slot), _ptr(cos_sin), _ptr(q_out), _ptr(k_cache), _ptr(v_cache),
-                                 Hq, Hkv, D, max_seq, max_pos, num_slots, _stream()), f"dmcp_fused_gemm[{epi}]")
+                                 Hq, Hkv, D, max_seq, max_pos, num_slots, kv8, _stream()), f"dmcp_fused_gemm[{epi}]")
 
 
 def fused_rope_kv(x: torch.Tensor, w: torch.Tensor, eps: float, pos: torch.Tensor, slot: torch.Tensor,
@@ -437,8 +452,7 @@ def fused_rope_kv(x: torch.Tensor, w: torch.Tensor, eps: float, pos: torch.Tenso
     x [M, K]; w [(Hq + 2 Hkv) D, K]; caches [S, Hkv, MAXS, D].  Returns q [M, Hq, D]."""
     M, K, N = _fused_xw(x, w, "fused_rope_kv")
     S, Hkv, MAXS, D = k_cache.shape
-    _req(k_cache, torch.bfloat16, "fused_rope_kv.k_cache")
-    _req(v_cache, torch.bfloat16, "fused_rope_kv.v_cache")
+    kv8 = _req_kv(k_cache, v_cache, "fused_rope_kv")
     _req(pos, torch.int32, "fused_rope_kv.pos")
     _req(slot, torch.int32, "fused_rope_kv.slot")
     _req(cos_sin, torch.float32, "fused_rope_kv.cos_sin")
@@ -451,7 +465,7 @@ def fused_rope_kv(x: torch.Tensor, w: torch.Tensor, eps: float, pos: torch.Tenso
     _req_out(q_out, torch.bfloat16, M * n_q_heads * D, "fused_rope_kv.q_out")
     _fused("rope_kv", wk, x, w, None, M, K, N, eps, pos=pos, slot=slot, cos_sin=cos_sin, q_out=q_out,
            k_cache=k_cache, v_cache=v_cache, Hq=n_q_heads, Hkv=Hkv, D=D, max_seq=MAXS,
-           max_pos=cos_sin.shape[0], num_slots=S)
+           max_pos=cos_sin.shape[0], num_slots=S, kv8=kv8)
     return q_out
 
 

@@ -26,6 +26,24 @@ def add_rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float, residual: Opt
     return y
 
 
+# FP8 KV cache: uint8 tensors holding OCP e4m3fn bytes (unit scale, saturated)
+FP8_MAX = 448.0
+
+
+def kv_float(t: torch.Tensor) -> torch.Tensor:
+    """Cache values as fp32 (bf16 caches, or fp8 e4m3 caches stored as uint8)."""
+    if t.dtype == torch.uint8:
+        return t.view(torch.float8_e4m3fn).float()
+    return t.float()
+
+
+def kv_encode(x: torch.Tensor, cache_dtype: torch.dtype) -> torch.Tensor:
+    """Values in a cache's storage format (bf16, or saturated e4m3 bytes)."""
+    if cache_dtype == torch.uint8:
+        return x.float().clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).view(torch.uint8)
+    return x.to(cache_dtype)
+
+
 def rope_tables(max_pos: int, head_dim: int, theta: float = 10000.0, device=None) -> torch.Tensor:
     """[max_pos, D/2, 2] float32 (cos, sin) -- viewed as float2 by the kernel."""
     half = head_dim // 2
@@ -58,8 +76,8 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos_sin: t
     for t in range(T):
         p, s = int(pos[t]), int(slot[t])
         if 0 <= p < MAXS and 0 <= s < S:
-            k_cache[s, :, p] = k[t]
-            v_cache[s, :, p] = v[t]
+            k_cache[s, :, p] = kv_encode(k[t], k_cache.dtype)
+            v_cache[s, :, p] = kv_encode(v[t], v_cache.dtype)
     if q_out is not None:
         q_out.copy_(q)
         return q_out
@@ -90,11 +108,11 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
         s, L = int(slot[b]), min(int(seq_len[b]), MAXS)
         if not (0 <= s < S) or L <= 0:
             continue
-        k = k_cache[s, :, :L].float()  # [Hkv, L, D]
-        v = v_cache[s, :, :L].float()
+        k = kv_float(k_cache[s, :, :L])  # [Hkv, L, D]
+        v = kv_float(v_cache[s, :, :L])
         if P > 0:  # the first P keys come from the shared prefix
-            k = torch.cat([prefix.k[:, :P].float(), k[:, P:]], dim=1)
-            v = torch.cat([prefix.vt[:, :, :P].float().transpose(1, 2), v[:, P:]], dim=1)
+            k = torch.cat([kv_float(prefix.k[:, :P]), k[:, P:]], dim=1)
+            v = torch.cat([kv_float(prefix.vt[:, :, :P]).transpose(1, 2), v[:, P:]], dim=1)
         qb = q[b].float().view(Hkv, G, D)
         att = torch.einsum("hgd,hld->hgl", qb, k) * scale
         p = torch.softmax(att, dim=-1)
@@ -116,11 +134,11 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
     Hkv = k_cache.shape[1]
     G = Hq // Hkv
     L = start + T
-    k = k_cache[slot, :, :L].float()
-    v = v_cache[slot, :, :L].float()
+    k = kv_float(k_cache[slot, :, :L])
+    v = kv_float(v_cache[slot, :, :L])
     if prefix_len > 0:
-        k = torch.cat([k_cache[prefix_slot, :, :prefix_len].float(), k[:, prefix_len:]], dim=1)
-        v = torch.cat([v_cache[prefix_slot, :, :prefix_len].float(), v[:, prefix_len:]], dim=1)
+        k = torch.cat([kv_float(k_cache[prefix_slot, :, :prefix_len]), k[:, prefix_len:]], dim=1)
+        v = torch.cat([kv_float(v_cache[prefix_slot, :, :prefix_len]), v[:, prefix_len:]], dim=1)
     qf = q.float().view(T, Hkv, G, D)
     att = torch.einsum("thgd,hld->hgtl", qf, k) * scale  # [Hkv, G, T, L]
     pos = torch.arange(start, L, device=q.device)[:, None]

@@ -31,6 +31,8 @@ import torch  # noqa: E402
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--preset", default="dmcp-coder-1b")
+    ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"],
+                    help="KV cache storage (fp8 = e4m3, half the attention bytes)")
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--extra", type=int, default=14)
     ap.add_argument("--prefix", type=int, default=4151)
@@ -48,7 +50,7 @@ def main(argv=None) -> int:
     hip.set_decode_impl(a.decode_impl)
 
     torch.cuda.set_device(0)
-    cfg = preset(a.preset, max_batch=a.batch, max_seq=a.max_seq)
+    cfg = preset(a.preset, max_batch=a.batch, max_seq=a.max_seq, kv_dtype=a.kv_dtype)
     model = LocalLM(cfg, device="cuda:0")
     if a.fused >= 0:
         model.use_fused = bool(a.fused)
@@ -78,9 +80,9 @@ def main(argv=None) -> int:
     for _ in range(a.iters):
         graphs.run(toks, slots, poss, mrows)[1].cpu().tolist()
     loop_ms = (time.perf_counter() - t0) / a.iters * 1e3
-    kv_bytes = 2 * cfg.layers * cfg.n_kv_heads * cfg.head_dim * 2 * (a.batch * (a.ctx + 1) + a.prefix)
+    kv_bytes = 2 * cfg.layers * cfg.n_kv_heads * cfg.head_dim * cfg.kv_elem_bytes * (a.batch * (a.ctx + 1) + a.prefix)
     w_bytes = 2 * (cfg.param_count() - cfg.vocab_size * cfg.hidden)
-    print(json.dumps({"bench": "decode_step", "preset": a.preset, "rows": n, "batch": a.batch, "prefix": a.prefix,
+    print(json.dumps({"bench": "decode_step", "preset": a.preset, "kv_dtype": a.kv_dtype, "rows": n, "batch": a.batch, "prefix": a.prefix,
                       "ctx": a.ctx, "fused": bool(getattr(model, "use_fused", False)),
                       "decode_impl": a.decode_impl,
                       "device_ms": round(dev_ms, 3), "loop_ms": round(loop_ms, 3),

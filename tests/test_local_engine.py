@@ -158,3 +158,35 @@ def test_prefill_reference_matches_sdpa_extend():
     v0 = vc[0, :, :T].repeat_interleave(Hq // Hkv, 0)
     exp0 = torch.nn.functional.scaled_dot_product_attention(q.transpose(0, 1), k0, v0, is_causal=True, scale=0.25)
     torch.testing.assert_close(got0, exp0.transpose(0, 1), atol=1e-4, rtol=1e-4)
+
+
+def test_fp8_kv_codec():
+    """e4m3 storage: exact on representable values, saturating at +-448,
+    relative error <= 2^-4 on normal values."""
+    from dmcp.ops.reference import kv_encode, kv_float
+    x = torch.tensor([0.0, 1.0, -1.5, 448.0, 1000.0, -1e9, 0.3, 2 ** -6])
+    b = kv_encode(x, torch.uint8)
+    assert b.dtype == torch.uint8
+    y = kv_float(b)
+    assert y[:4].tolist() == [0.0, 1.0, -1.5, 448.0] and y[4].item() == 448.0 and y[5].item() == -448.0
+    assert abs(y[6].item() - 0.3) <= 0.3 * 2 ** -4 and y[7].item() == 2 ** -6
+    assert kv_encode(x, torch.bfloat16).dtype == torch.bfloat16
+
+
+def test_fp8_kv_model_tracks_bf16_model():
+    """The tiny model with an fp8 KV cache (CPU reference ops) stays close to
+    the bf16-cache model on prefill + shared-prefix extend + decode."""
+    a = LocalLM(preset("tiny", max_batch=4, max_rows=16, max_seq=768), device="cpu", seed=1)
+    b = LocalLM(preset("tiny", max_batch=4, max_rows=16, max_seq=768, kv_dtype="fp8"), device="cpu", seed=1,
+                weights=a.w)
+    assert b.k_cache.dtype == torch.uint8 and b.cfg.kv_bytes() * 2 == a.cfg.kv_bytes()
+    toks = torch.tensor([256] + list(b"public class OrderService { void create() {} }"), dtype=torch.int32)
+    la, lb = a.forward_tokens(toks, 0, 0).float(), b.forward_tokens(toks, 0, 0).float()
+    assert torch.nn.functional.cosine_similarity(la, lb, dim=0) > 0.99
+    for m in (a, b):
+        m.set_prefix(toks[:20].tolist())
+        m.fork_prefix(1)
+        m.forward_tokens(toks[20:], 1, 20)
+    step = [m.decode(torch.tensor([65, 66], dtype=torch.int32), torch.tensor([0, 1], dtype=torch.int32),
+                     torch.tensor([len(toks), len(toks)], dtype=torch.int32)).float() for m in (a, b)]
+    assert torch.nn.functional.cosine_similarity(step[0], step[1], dim=1).min() > 0.99

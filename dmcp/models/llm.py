@@ -201,7 +201,7 @@ class LocalLM:
         # prefix slot (fork_prefix without a copy; prefill kernel only)
         self._slot_prefix: Dict[int, int] = {}
         self.fused_max_rows = min(ops.FUSED_MAX_ROWS, int(os.environ.get("DMCP_FUSED_MAX_ROWS", "32")))
-        ps = ops.prefix_splits(c.max_seq, self.PREFIX_CHUNK) if shared_prefix else 0
+        ps = max(ops.prefix_splits(c.max_seq, self.PREFIX_CHUNK), ops.PREFIX_MFMA_MAX_SPLITS) if shared_prefix else 0
         self.attn_ws = (ops.decode_workspace(self.max_rows, c.n_heads, c.n_kv_heads, c.head_dim, c.max_seq,
                                              self.device, prefix_slots=ps) if self.device.type == "cuda" else None)
 
@@ -376,7 +376,7 @@ class LocalLM:
         if not self.shared_prefix:
             return None
         return ops.SharedPrefix(self.k_cache[i][self.prefix_slot], self.prefix_vt[i], self.prefix_dev,
-                                self.PREFIX_CHUNK)
+                                self.PREFIX_CHUNK, self.v_cache[i][self.prefix_slot])
 
     def _decode_fused(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:
         """The decode step on the fused gfx950 GEMMs: per layer QKV (+norm,

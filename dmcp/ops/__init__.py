@@ -36,6 +36,7 @@ def decode_plan(rows, n_kv_heads, max_seq):
     return _dp(rows, n_kv_heads, max_seq)
 
 
+PREFIX_MFMA_MAX_SPLITS = 16  # shared-prefix key splits on the prefill kernel (dmcp.ops.hip)
 FUSED_MAX_ROWS = 128  # row limit of the fused decode GEMMs (dmcp.ops.hip.FUSED_MAX_ROWS)
 
 

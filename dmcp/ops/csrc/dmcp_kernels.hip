@@ -14,7 +14,14 @@
 // ABI: extern "C" launchers taking raw device pointers and a hipStream_t;
 // they return hipError_t (0 = success).  Shapes are validated on the host
 // side (dmcp/ops/hip.py) before any launch.
+#include <mutex>
+
 #include "dmcp_common.hpp"
+
+// shared-prefix partials on the MFMA prefill kernel (prefill_attn.hip)
+hipError_t dmcp_launch_prefix_partials(const uint16_t* q, const void* pk, const void* pv, const int32_t* plen,
+                                       float* part_o, float* part_ml, int B, int Hkv, int G, int D, int ldk,
+                                       int nsplit, int splits_total, float sl2, int kv8, hipStream_t st);
 
 namespace {
 
@@ -398,7 +405,9 @@ __global__ __launch_bounds__(kBlock) void decode_attn_combine_kernel(const float
     const int dg = lane % DQ, pg = lane / DQ;
     const int P = plen ? max(0, *plen) : 0;
     const int splits_total = ps_max + splits;
-    const int npre = P > 0 ? min(ps_max, (P + pchunk - 1) / pchunk) : 0;  // prefix partials
+    // prefix partials: ceil(P / pchunk) of the 256-key prefix kernel, or all
+    // ps_max of the MFMA prefill-kernel path (pchunk 0; empty ones weigh 0)
+    const int npre = P > 0 ? (pchunk > 0 ? min(ps_max, (P + pchunk - 1) / pchunk) : ps_max) : 0;
     const int nwaves = gridDim.x * (kBlock / kWave);
     for (int w = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave; w < B * Hq; w += nwaves) {
         const int b = w / Hq, qh = w - b * Hq;
@@ -1035,6 +1044,37 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
 // 2 = MFMA kernel with a register double buffer (D = 64; A/B)
 int g_decode_impl = 0;
 
+// Shared-prefix kernel on a second stream, concurrent with the per-row
+// kernel (both only write their own partial slots; the combine waits for
+// both); inside a hipGraph capture the fork/join events make the side stream
+// a parallel branch.  Off by default: measured 2.38 -> 2.58 ms per decode
+// step with it on (the latency-bound prefix blocks slow the HBM-bound per-row
+// kernel more than they gain) -- profiles/decode_step_r2_notes.md.
+int g_prefix_overlap = 0;
+
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+
+hipError_t side_stream(SideStream*& out) {
+    static SideStream ss[64];
+    static std::mutex mu;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> g(mu);
+    SideStream& x = ss[dev];
+    if (!x.s) {
+        if ((e = hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking)) != hipSuccess) return e;
+        if ((e = hipEventCreateWithFlags(&x.fork, hipEventDisableTiming)) != hipSuccess) return e;
+        if ((e = hipEventCreateWithFlags(&x.join, hipEventDisableTiming)) != hipSuccess) return e;
+    }
+    out = &x;
+    return hipSuccess;
+}
+
 // CUs of the current device (cached per device; 256 on MI355X)
 inline int device_cu_count() {
     static int cached[64] = {0};
@@ -1102,6 +1142,14 @@ int dmcp_abi_version() { return 9; }
 
 // Selects the per-row decode attention kernel (0 = MFMA, 1 = VALU, 2 = MFMA double-buffered);
 // returns the previous choice.
+// Shared-prefix kernel on a side stream beside the per-row kernel (1) or in
+// line (0, default); returns the previous setting.
+int dmcp_set_prefix_overlap(int on) {
+    const int prev = g_prefix_overlap;
+    g_prefix_overlap = on ? 1 : 0;
+    return prev;
+}
+
 int dmcp_set_decode_impl(int impl) {
     const int prev = g_decode_impl;
     if (impl >= 0 && impl <= 2) g_decode_impl = impl;
@@ -1148,8 +1196,11 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
     if (B <= 0) return 0;
     if (Hkv <= 0 || Hq % Hkv != 0 || splits <= 0 || chunk <= 0) return hipErrorInvalidValue;
     const bool prefix = plen != nullptr;
-    if (prefix && (!prefix_k || !prefix_vt || ps_max <= 0 || pchunk != kPrefixChunk || ldv % kPrefixChunk ||
-                   ldv > max_seq))
+    // pchunk == kPrefixChunk: the 256-key prefix kernel over (prefix_k,
+    // prefix_vt = V^T); pchunk == 0: the MFMA prefill kernel over (prefix_k,
+    // prefix_vt = V rows), ps_max key splits
+    if (prefix && (!prefix_k || !prefix_vt || ps_max <= 0 ||
+                   (pchunk != 0 && (pchunk != kPrefixChunk || ldv % kPrefixChunk || ldv > max_seq))))
         return hipErrorInvalidValue;
     if (!prefix) ps_max = 0;
     if ((splits > 1 || prefix) && (!part_o || !part_ml)) return hipErrorInvalidValue;
@@ -1161,7 +1212,20 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
     auto ln = (const int32_t*)seq_len;
     auto pl = (const int32_t*)plen;
     const long cap = 4L * device_cu_count();
-    if (prefix) {
+    SideStream* side = nullptr;
+    const hipStream_t main_st = st;
+    if (prefix && g_prefix_overlap) {  // fork: the prefix kernel runs beside the per-row kernel
+        hipError_t fe = side_stream(side);
+        if (fe == hipSuccess) fe = hipEventRecord(side->fork, main_st);
+        if (fe == hipSuccess) fe = hipStreamWaitEvent(side->s, side->fork, 0);
+        if (fe != hipSuccess) return fe;
+        st = side->s;
+    }
+    if (prefix && pchunk == 0) {
+        hipError_t pe = dmcp_launch_prefix_partials(qq, prefix_k, prefix_vt, pl, (float*)part_o, (float*)part_ml, B,
+                                                    Hkv, G, D, max_seq, ps_max, ps_max + splits, sl2, kv8, st);
+        if (pe != hipSuccess) return pe;
+    } else if (prefix) {
         // one block per (kv head, prefix split, 4 query tiles); exits at once when *plen == 0
         const long items = (long)Hkv * ps_max * ((((B * G + 31) / 32) + 3) / 4);
         dim3 pgrid((unsigned)(items < cap ? items : cap));
@@ -1178,6 +1242,13 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
         hipError_t pe = hipGetLastError();
         if (pe != hipSuccess) return pe;
     }
+    if (side) {
+        hipError_t je = hipEventRecord(side->join, side->s);
+        if (je != hipSuccess) return je;
+        st = main_st;
+    }
+    // the combine (main stream) waits for the side stream's prefix partials
+    auto join = [&]() -> hipError_t { return side ? hipStreamWaitEvent(main_st, side->join, 0) : hipSuccess; };
     // persistent grid: enough blocks to fill every CU a few times over, never
     // more than there are work items
     const long items = (long)splits * Hkv * B;
@@ -1209,6 +1280,7 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
         }
 #undef DMCP_MFMA_DECODE
         e = hipGetLastError();
+        if (e == hipSuccess) e = join();
         if (e != hipSuccess || (splits == 1 && !prefix)) return e;
         return launch_combine(part_o, part_ml, sl, ln, out, B, Hkv * G, D, max_seq, chunk, splits, num_slots, pl,
                               ps_max, prefix ? pchunk : 1, st);
@@ -1221,7 +1293,8 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
         e = launch_decode_d<128>(G, grid, qq, kk, vv, sl, ln, (uint16_t*)out, (float*)part_o, (float*)part_ml, B,
                                  Hkv, max_seq, chunk, splits, sl2, num_slots, pl, ps_max, st);
     else
-        return hipErrorInvalidValue;
+        e = hipErrorInvalidValue;
+    if (e == hipSuccess) e = join();
     if (e != hipSuccess || (splits == 1 && !prefix)) return e;
     return launch_combine(part_o, part_ml, sl, ln, out, B, Hkv * G, D, max_seq, chunk, splits, num_slots, pl, ps_max,
                           prefix ? pchunk : 1, st);

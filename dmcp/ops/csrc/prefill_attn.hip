@@ -77,7 +77,7 @@ __global__ __launch_bounds__(NWAVE * 64) void prefill_attn_kernel(
     const uint16_t* __restrict__ q, const void* __restrict__ kc, const void* __restrict__ vc,
     const void* __restrict__ pk, const void* __restrict__ pv, uint16_t* __restrict__ out,
     float* __restrict__ part_o, float* __restrict__ part_ml, int T, int start, int P, int Hkv, int G, int ldk,
-    int ctiles, int nsplit, float sl2) {
+    int ctiles, int nsplit, float sl2, const int32_t* __restrict__ plen, long prs, long pss) {
     constexpr int KS = D / 16;  // k-steps of the QK product
     constexpr int DT = D / 32;  // 32-row d tiles of the PV product
     constexpr int CH = D / 8;   // 16-byte chunks per row
@@ -95,7 +95,18 @@ __global__ __launch_bounds__(NWAVE * 64) void prefill_attn_kernel(
     const int Hq = Hkv * G;
     const int NC = T * G;
     const int c0 = ct * COLS;
-    const int kend = start + (min(NC, c0 + COLS) - 1) / G + 1;  // keys [0, kend) are visible to the block
+    // prefix mode (plen != nullptr, the decode step's shared prefix): every
+    // query sees keys [0, *plen) -- read in the kernel so a captured graph
+    // follows prefix changes -- all from pk/pv, and the output is always
+    // partials (merged with the rows' own keys by decode_attn_combine_kernel)
+    const bool prefix_mode = plen != nullptr;
+    int kend;
+    if (prefix_mode) {
+        kend = __builtin_amdgcn_readfirstlane(max(0, min(*plen, ldk)));
+        P = kend;
+    } else {
+        kend = start + (min(NC, c0 + COLS) - 1) / G + 1;  // keys [0, kend) are visible to the block
+    }
     const int nst_all = (kend + kPfKeys - 1) / kPfKeys;
     // split-K: this block's stages [st0, st1) of the column tile's key range
     const int per = (nst_all + nsplit - 1) / nsplit;
@@ -203,11 +214,13 @@ __global__ __launch_bounds__(NWAVE * 64) void prefill_attn_kernel(
             for (int u = 0; u < NSUB; ++u) {
                 if (!act[u]) continue;
                 float mt = -1e30f;
-                if (kb + 31 > qmin[u]) {  // the tile straddles some query's position: causal mask
+                // mask: the tile straddles some query's position (causal) or
+                // the end of the visible keys (prefix mode: no causal bound)
+                if (kb + 31 > qmin[u] || kb + 32 > kend) {
 #pragma unroll
                     for (int i = 0; i < 16; ++i) {
                         const int key = kb + (i & 3) + 8 * (i >> 2) + 4 * h;
-                        s[u][i] = key <= qpos[u] ? s[u][i] : -INFINITY;
+                        s[u][i] = (key <= qpos[u] && key < kend) ? s[u][i] : -INFINITY;
                         mt = fmaxf(mt, s[u][i]);
                     }
                 } else {
@@ -268,8 +281,8 @@ __global__ __launch_bounds__(NWAVE * 64) void prefill_attn_kernel(
         if (c >= NC) continue;
         const int t = c / G, g = c - t * G;
         const size_t row = (size_t)t * Hq + (size_t)kh * G + g;
-        if (nsplit > 1) {  // unnormalised partial + (max, sum), merged by prefill_combine_kernel
-            const size_t pr = (size_t)sp * NC * Hkv + row;
+        if (nsplit > 1 || prefix_mode) {  // unnormalised partial + (max, sum), merged by a combine kernel
+            const size_t pr = (size_t)row * prs + (size_t)sp * pss;
             float* po = part_o + pr * D;
 #pragma unroll
             for (int t2 = 0; t2 < DT; ++t2)
@@ -329,7 +342,8 @@ hipError_t launch_prefill(const uint16_t* q, const void* k, const void* v, const
     constexpr int COLS = 32 * NSUB * NWAVE;
     const int ctiles = (T * G + COLS - 1) / COLS;
     prefill_attn_kernel<D, NSUB, NWAVE, KV8><<<dim3((unsigned)(ctiles * Hkv * nsplit)), NWAVE * kWave, 0, st>>>(
-        q, k, v, pk, pv, out, po, pml, T, start, P, Hkv, G, ldk, ctiles, nsplit, sl2);
+        q, k, v, pk, pv, out, po, pml, T, start, P, Hkv, G, ldk, ctiles, nsplit, sl2, nullptr, 1L,
+        (long)T * G * Hkv);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || nsplit == 1) return e;
     const int rows = T * G * Hkv;
@@ -340,6 +354,31 @@ hipError_t launch_prefill(const uint16_t* q, const void* k, const void* v, const
 }
 
 }  // namespace
+
+// The decode step's shared-prefix attention on this kernel (called by
+// dmcp_decode_attention, dmcp_kernels.hip): q [B, Hq, D] (one query token per
+// row), prefix keys [0, *plen) of pk/pv ([Hkv, ldk, D]), partials written at
+// index row * splits_total + split (split < nsplit) of the decode workspace.
+// The grid is sized for the slot capacity; splits past *plen write empty
+// partials (m = -1e30, l = 0).
+hipError_t dmcp_launch_prefix_partials(const uint16_t* q, const void* pk, const void* pv, const int32_t* plen,
+                                       float* part_o, float* part_ml, int B, int Hkv, int G, int D, int ldk,
+                                       int nsplit, int splits_total, float sl2, int kv8, hipStream_t st) {
+    constexpr int COLS = 32 * 4;  // variant 0: 4 waves x one 32-column unit
+    const int ctiles = (B * G + COLS - 1) / COLS;
+    const dim3 grid((unsigned)(ctiles * Hkv * nsplit));
+#define DMCP_PFX(DD, K8)                                                                                          \
+    prefill_attn_kernel<DD, 1, 4, K8><<<grid, 4 * kWave, 0, st>>>(q, pk, pv, pk, pv, nullptr, part_o, part_ml, B,    \
+                                                                 ldk, 0, Hkv, G, ldk, ctiles, nsplit, sl2, plen,   \
+                                                                 (long)splits_total, 1L)
+    if (D == 64 && kv8) DMCP_PFX(64, true);
+    else if (D == 64) DMCP_PFX(64, false);
+    else if (D == 128 && kv8) DMCP_PFX(128, true);
+    else if (D == 128) DMCP_PFX(128, false);
+    else return hipErrorInvalidValue;
+#undef DMCP_PFX
+    return hipGetLastError();
+}
 
 extern "C" {
 

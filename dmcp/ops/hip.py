@@ -59,6 +59,7 @@ def lib() -> ctypes.CDLL:
             "dmcp_masked_argmax": ([_vp, _vp, _vp, _i, _vp, _i, _i, _i, _vp], _i),
             "dmcp_embedding": ([_vp, _vp, _vp, _i, _i, _i, _vp], _i),
             "dmcp_set_decode_impl": ([_i], _i),
+            "dmcp_set_prefix_overlap": ([_i], _i),
             "dmcp_fused_gemm_max_rows": ([], _i),
             "dmcp_fused_gemm": ([_i, _i, _vp, _vp, _vp, _i, _i, _i, _f, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i,
                                  _i, _i, _i, _i, _vp], _i),
@@ -71,6 +72,7 @@ def lib() -> ctypes.CDLL:
             raise HipOpsError("HIP kernel library ABI mismatch; rebuild with python -m dmcp.ops.build")
         impl = os.environ.get("DMCP_DECODE_IMPL", "mfma").lower()
         L.dmcp_set_decode_impl(DECODE_IMPLS.get(impl, 0))
+        L.dmcp_set_prefix_overlap(int(os.environ.get("DMCP_PREFIX_OVERLAP", "0") == "1"))
         _lib = L
         return _lib
 
@@ -88,6 +90,14 @@ def set_decode_impl(name: str) -> str:
         raise ValueError(f"decode impl must be one of {sorted(DECODE_IMPLS)}")
     prev = lib().dmcp_set_decode_impl(DECODE_IMPLS[name])
     return {v: k for k, v in DECODE_IMPLS.items()}[prev]
+
+
+def set_prefix_overlap(on: bool) -> bool:
+    """Run the decode step's shared-prefix kernel on a side stream, concurrent
+    with the per-row kernel (``DMCP_PREFIX_OVERLAP=1``; off by default: the
+    two kernels slowed each other down, 2.38 -> 2.58 ms per step).  Returns
+    the previous setting; re-capture hipGraphs after switching."""
+    return bool(lib().dmcp_set_prefix_overlap(int(bool(on))))
 
 
 def loaded_path() -> Optional[str]:
@@ -254,7 +264,19 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     ps_max = 0
     pk = pvt = plen = None
     ldv = pchunk = 0
-    if prefix is not None:
+    if prefix is not None and prefix.v is not None and prefix_impl() == "prefill":
+        # the prefix on the MFMA prefill kernel: V rows, ps_max key splits
+        pk, pvt, plen = prefix.k, prefix.v, prefix.length
+        _req(pk, k_cache.dtype, "decode_attention.prefix.k")
+        _req(pvt, k_cache.dtype, "decode_attention.prefix.v")
+        _req(plen, torch.int32, "decode_attention.prefix.length")
+        if tuple(pk.shape) != (Hkv, MAXS, D) or tuple(pvt.shape) != (Hkv, MAXS, D) or plen.numel() != 1:
+            raise HipOpsError(f"decode_attention: prefix k {tuple(pk.shape)} / v {tuple(pvt.shape)} do not match "
+                              f"kv {tuple(k_cache.shape)}")
+        ps_max = prefix_mfma_splits(B, Hq // Hkv, Hkv)
+        if workspace is not None:  # as many prefix splits as the caller's scratch holds
+            ps_max = max(1, min(ps_max, workspace[1].numel() // (2 * B * Hq) - splits))
+    elif prefix is not None:
         pk, pvt, plen, pchunk = prefix.k, prefix.vt, prefix.length, prefix.chunk
         _req(pk, k_cache.dtype, "decode_attention.prefix.k")
         _req(pvt, k_cache.dtype, "decode_attention.prefix.vt")
@@ -344,6 +366,34 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
 
 
 PREFIX_CHUNK = 256  # keys per prefix split: kPrefixChunk in csrc/dmcp_kernels.hip
+PREFIX_IMPLS = ("chunk", "prefill")
+
+
+def prefix_impl() -> str:
+    """Shared-prefix attention of the decode step (``DMCP_PREFIX_IMPL``):
+    ``chunk`` (default) = the 256-key MFMA prefix kernel over the V^T copy;
+    ``prefill`` = the MFMA prefill kernel in prefix mode over the prefix
+    slot's V rows.  Measured at parity or slower on the enrichment step
+    (profiles/decode_step_r2_notes.md), kept for A/B."""
+    impl = os.environ.get("DMCP_PREFIX_IMPL", "chunk").lower()
+    if impl not in PREFIX_IMPLS:
+        raise HipOpsError(f"DMCP_PREFIX_IMPL must be one of {PREFIX_IMPLS}, got {impl!r}")
+    return impl
+
+
+PREFIX_MFMA_MAX_SPLITS = 16
+
+
+def prefix_mfma_splits(rows: int, G: int, Hkv: int, target_blocks: int = 256) -> int:
+    """Key splits of the decode step's shared prefix on the prefill kernel:
+    ~one block per CU over (128-column query tiles x kv heads x splits), at
+    most 16 (the combine reads every split's partial; empty ones weigh 0).
+    ``DMCP_PREFIX_SPLITS`` overrides."""
+    env = os.environ.get("DMCP_PREFIX_SPLITS")
+    if env:
+        return max(1, min(PREFIX_MFMA_MAX_SPLITS, int(env)))
+    tiles = -(-rows * G // 128) * Hkv
+    return max(1, min(PREFIX_MFMA_MAX_SPLITS, round(target_blocks / max(1, tiles))))
 
 
 def prefix_splits(ldv: int, pchunk: int = PREFIX_CHUNK) -> int:

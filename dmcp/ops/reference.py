@@ -88,12 +88,15 @@ class SharedPrefix(NamedTuple):
     """Keys/values shared by every row of a decode step (cascade decoding).
 
     ``k`` [Hkv, MAXS, D] (row-major, as in the cache), ``vt`` [Hkv, D, ldv]
-    (values transposed), ``length`` int32 [1] on the device (0 = no prefix),
-    ``chunk`` keys per prefix work item of the MFMA kernel."""
+    (values transposed, read by the 256-key prefix kernel), ``length`` int32
+    [1] on the device (0 = no prefix), ``chunk`` keys per prefix work item of
+    that kernel; ``v`` [Hkv, MAXS, D] (values row-major, the cache slot) lets
+    the decode step run the prefix on the MFMA prefill kernel instead."""
     k: torch.Tensor
     vt: torch.Tensor
     length: torch.Tensor
     chunk: int = 256
+    v: Optional[torch.Tensor] = None
 
 
 def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: torch.Tensor,
@@ -112,7 +115,8 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
         v = kv_float(v_cache[s, :, :L])
         if P > 0:  # the first P keys come from the shared prefix
             k = torch.cat([kv_float(prefix.k[:, :P]), k[:, P:]], dim=1)
-            v = torch.cat([kv_float(prefix.vt[:, :, :P]).transpose(1, 2), v[:, P:]], dim=1)
+            pv = kv_float(prefix.v[:, :P]) if prefix.v is not None else kv_float(prefix.vt[:, :, :P]).transpose(1, 2)
+            v = torch.cat([pv, v[:, P:]], dim=1)
         qb = q[b].float().view(Hkv, G, D)
         att = torch.einsum("hgd,hld->hgl", qb, k) * scale
         p = torch.softmax(att, dim=-1)

@@ -24,7 +24,14 @@ for s in $STEPS; do
                    tests/test_gpu_kernels.py tests/test_gpu_model.py tests/test_gpu_fused.py -x -q --timeout 120 \
                    --timeout-method thread ;;
         step) step step_bf16 300 python scripts/bench_step.py
-              step step_fp8 300 python scripts/bench_step.py --kv-dtype fp8 ;;
+              step step_fp8 300 python scripts/bench_step.py --kv-dtype fp8
+              DMCP_PREFIX_IMPL=v1 step step_bf16_prefix_v1 300 python scripts/bench_step.py
+              DMCP_PREFIX_IMPL=v1 step step_fp8_prefix_v1 300 python scripts/bench_step.py --kv-dtype fp8 ;;
+        overlap) DMCP_PREFIX_OVERLAP=0 step step_fp8_no_overlap 300 python scripts/bench_step.py --kv-dtype fp8
+                 DMCP_PREFIX_OVERLAP=0 DMCP_PREFIX_IMPL=v1 step step_fp8_v1_no_overlap 300 python scripts/bench_step.py --kv-dtype fp8 ;;
+        splits) for n in 4 8 12 16; do
+                    DMCP_PREFIX_SPLITS=$n step step_fp8_psplit$n 300 python scripts/bench_step.py --kv-dtype fp8
+                done ;;
         enrich) step enrich_fp8 600 python bench_enrich.py --classes 256 --batch 64 --kv-dtype fp8
                 step enrich_bf16 600 python bench_enrich.py --classes 256 --batch 64 ;;
     esac

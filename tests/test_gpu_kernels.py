@@ -1,5 +1,6 @@
 """Numerics of the gfx950 HIP kernels against plain PyTorch fp32 references."""
 import math
+import os
 
 import pytest
 import torch
@@ -98,16 +99,38 @@ def test_decode_attention_shared_prefix(hip, D, Hq, Hkv, P, B):
     vt = torch.zeros((Hkv, D, MAXS), dtype=torch.bfloat16, device="cuda")
     vt[:, :, :P] = vc[pslot, :, :P].transpose(-1, -2)
     plen = torch.tensor([P], dtype=torch.int32, device="cuda")
-    pre = SharedPrefix(kc[pslot], vt, plen, 256)
     slot = torch.tensor([(b * 5) % S for b in range(B)], dtype=torch.int32, device="cuda")
     slot[B // 2] = -1  # a padding row
     lens = torch.tensor([min(MAXS, P + 1 + (b * 37) % 300) for b in range(B)], dtype=torch.int32, device="cuda")
     scale = 1 / math.sqrt(D)
-    for chunk in (256, 1024):
-        got = hip.decode_attention(q, kc, vc, slot, lens, scale, chunk=chunk, prefix=pre)
-        exp = reference.decode_attention(q, kc, vc, slot, lens, scale, prefix=pre)
-        torch.testing.assert_close(got.float(), exp.float(), atol=2e-2, rtol=2e-2)
-        assert got[B // 2].abs().sum().item() == 0
+    # the 256-key prefix kernel over V^T, and the prefill kernel in prefix mode over the V rows
+    for impl in hip.PREFIX_IMPLS:
+        pre = SharedPrefix(kc[pslot], vt, plen, 256, vc[pslot])
+        os.environ["DMCP_PREFIX_IMPL"] = impl
+        try:
+            for chunk in (256, 1024):
+                got = hip.decode_attention(q, kc, vc, slot, lens, scale, chunk=chunk, prefix=pre)
+                exp = reference.decode_attention(q, kc, vc, slot, lens, scale, prefix=pre)
+                torch.testing.assert_close(got.float(), exp.float(), atol=2e-2, rtol=2e-2)
+                assert got[B // 2].abs().sum().item() == 0
+        finally:
+            os.environ.pop("DMCP_PREFIX_IMPL")
+    pre = SharedPrefix(kc[pslot], vt, plen, 256, vc[pslot])
+    # the prefix kernel on the side stream == in line (both prefix kernels)
+    for impl in hip.PREFIX_IMPLS:
+        os.environ["DMCP_PREFIX_IMPL"] = impl
+        try:
+            prev = hip.set_prefix_overlap(True)
+            on = hip.decode_attention(q, kc, vc, slot, lens, scale, prefix=pre)
+            hip.set_prefix_overlap(False)
+            off = hip.decode_attention(q, kc, vc, slot, lens, scale, prefix=pre)
+        finally:
+            hip.set_prefix_overlap(prev)
+            os.environ.pop("DMCP_PREFIX_IMPL")
+        torch.cuda.synchronize()
+        assert torch.equal(on, off)
+        torch.testing.assert_close(on.float(), reference.decode_attention(q, kc, vc, slot, lens, scale,
+                                                                          prefix=pre).float(), atol=2e-2, rtol=2e-2)
     # length 0 in device memory: the prefix kernel is a no-op, rows read their own keys
     plen.zero_()
     got = hip.decode_attention(q, kc, vc, slot, lens, scale, prefix=pre)

@@ -26,9 +26,11 @@ def main(argv=None) -> int:
     ap.add_argument("--preset", default="dmcp-coder-1b")
     ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"],
                     help="KV cache storage (fp8 = e4m3, half the attention bytes)")
-    ap.add_argument("--classes", type=int, default=128, help="classes per rank")
-    ap.add_argument("--batch", type=int, default=64, help="concurrent sequences (KV slots)")
+    ap.add_argument("--classes", type=int, default=1024, help="classes per rank")
+    ap.add_argument("--batch", type=int, default=256, help="concurrent sequences (KV slots)")
     ap.add_argument("--max-seq", type=int, default=8192)
+    ap.add_argument("--max-rows", type=int, default=0,
+                    help="rows per decode step incl. jump-forward rows (0 = 1.5 x batch, >= 256)")
     ap.add_argument("--prompt-chars", type=int, default=2048)
     ap.add_argument("--readme-chars", type=int, default=4000,
                     help="project README in every prompt (the reference sends up to 10,000 chars)")
@@ -55,7 +57,8 @@ def main(argv=None) -> int:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl")
-    cfg = preset(args.preset, max_batch=args.batch, max_seq=args.max_seq, kv_dtype=args.kv_dtype)
+    cfg = preset(args.preset, max_batch=args.batch, max_seq=args.max_seq, kv_dtype=args.kv_dtype,
+                 max_rows=args.max_rows or max(256, args.batch + args.batch // 2))
     model = LocalLM(cfg, device=f"cuda:{local}", seed=rank)
     eng = LocalEngine(model, use_graphs=not args.no_graphs, jump_forward=not args.no_jump,
                       shared_prefix=not args.no_shared_prefix, pipeline=not args.no_pipeline)
@@ -106,7 +109,7 @@ def main(argv=None) -> int:
             "unit": "classes/s", "n_gpus": world, "higher_is_better": True, "scaling": "weak",
             "dtype": "bf16", "data": "synthetic classes, random-init weights",
             "config": {"model": cfg.name, "params_b": round(cfg.param_count() / 1e9, 3), "batch": args.batch,
-                       "kv_dtype": cfg.kv_dtype,
+                       "max_rows": cfg.max_rows, "kv_dtype": cfg.kv_dtype,
                        "max_seq": args.max_seq, "prompt_chars": args.prompt_chars,
                        "readme_chars": args.readme_chars, "graphs": not args.no_graphs,
                        "jump_forward": not args.no_jump, "shared_prefix": not args.no_shared_prefix,

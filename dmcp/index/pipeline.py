@@ -144,6 +144,8 @@ class _ProjectLocks:
 
 class Indexer:
     ROW_CHUNK = 256  # classes (with their methods) per writer put in Phase 1
+    native_phase1 = True  # Phase 1 rows built by the native writer when it can (else the Python loop)
+    phase1_ids: Optional[List[str]] = None  # row ids for the native Phase 1 (None = fresh UUIDv7s; tests)
 
     def __init__(self, repos: Repositories, cache: GraphCache, git: GitClient,
                  backend: Optional[EnrichmentBackend] = None, *, batch_size: int = 20,
@@ -299,6 +301,20 @@ class Indexer:
         methods_by_ident: Dict[str, List[Tuple[str, str]]] = {}
         units = parsed.units
         class_ids: Dict[str, str] = {}
+        if writer is None:  # the writer thread starts deleting the old rows right away
+            writer = self.repos.project_rows_writer(pid, replace)
+        if writer.native_phase1 and self.native_phase1:
+            try:
+                (n_cls, n_meth, n_par, class_ids, class_types, method_infos, methods_by_ident,
+                 links) = writer.phase1_rows(list(order), units, self.phase1_ids, now, commit_hash, MethodInfo,
+                                             self.ROW_CHUNK)
+                graph.load_static_metadata(class_ids, class_types, method_infos, links)
+                writer.close()
+            except BaseException:
+                writer.abort()
+                raise
+            LOG.info("Phase 1 rows built natively. Classes: %d, Methods: %d, Parameters: %d", n_cls, n_meth, n_par)
+            return n_cls, methods_by_ident, writer
         # an upper bound of the ids needed: one per class and method, one per
         # parameter link of every method (overloads included)
         n_ids = 0
@@ -307,8 +323,6 @@ class Indexer:
             if u.params:
                 n_ids += sum(len(u.params.get(m[0]) or ()) for m in u.methods)
         nid = iter(new_ids(n_ids)).__next__
-        if writer is None:  # the writer thread starts deleting the old rows right away
-            writer = self.repos.project_rows_writer(pid, replace)
         try:
             class_types: Dict[str, Optional[str]] = {}
             method_infos: Dict[str, List[MethodInfo]] = {}

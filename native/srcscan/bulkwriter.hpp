@@ -35,11 +35,14 @@ struct Value {
     Value() : i(0) {}
 };
 
-// rows flattened row-major: values.size() == ncols * rows
+// rows flattened row-major: values.size() == ncols * rows.  Text values
+// that no caller-owned object holds live in ``owned`` (a deque: element
+// addresses stay put as it grows).
 struct Batch {
     std::string sql;
     int ncols = 0;
     std::vector<Value> values;
+    std::deque<std::string> owned;
 };
 
 class BulkWriter {

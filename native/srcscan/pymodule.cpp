@@ -91,6 +91,102 @@ srcscan::ScanResult scan_mounted(py::list files, const std::string& language, in
 
 py::str pystr(const std::string& s) { return py::str(s.data(), s.size()); }
 
+// ------------------------------------------------------------- Phase 1 rows
+// json.dumps(list_of_str) with the default separators and ensure_ascii=True,
+// byte for byte ('["A", "B"]', non-ASCII as \uXXXX / surrogate pairs).
+void json_str_list_ascii(PyObject* seq, std::string& out) {
+    static const char* hex = "0123456789abcdef";
+    out.push_back('[');
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+    PyObject** items = PySequence_Fast_ITEMS(seq);
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        if (i) out.append(", ");
+        PyObject* o = items[i];
+        if (!PyUnicode_Check(o)) throw py::type_error("exception names must be str");
+        out.push_back('"');
+        const Py_ssize_t len = PyUnicode_GET_LENGTH(o);
+        const int kind = PyUnicode_KIND(o);
+        const void* data = PyUnicode_DATA(o);
+        for (Py_ssize_t k = 0; k < len; ++k) {
+            const Py_UCS4 c = PyUnicode_READ(kind, data, k);
+            auto u4 = [&](unsigned v) {
+                out.append("\\u");
+                for (int sh = 12; sh >= 0; sh -= 4) out.push_back(hex[(v >> sh) & 15]);
+            };
+            switch (c) {
+                case '"': out.append("\\\""); break;
+                case '\\': out.append("\\\\"); break;
+                case '\n': out.append("\\n"); break;
+                case '\r': out.append("\\r"); break;
+                case '\t': out.append("\\t"); break;
+                case '\b': out.append("\\b"); break;
+                case '\f': out.append("\\f"); break;
+                default:
+                    if (c < 0x20 || (c >= 0x7f && c < 0x10000)) {  // outside ' '..'~'
+                        u4(c);
+                    } else if (c >= 0x10000) {
+                        const unsigned v = c - 0x10000;
+                        u4(0xd800 | (v >> 10));
+                        u4(0xdc00 | (v & 0x3ff));
+                    } else {
+                        out.push_back((char)c);
+                    }
+            }
+        }
+        out.push_back('"');
+    }
+    out.push_back(']');
+}
+
+struct RowBuilder {
+    dbw::Batch b;
+    explicit RowBuilder(const std::string& sql, int ncols) {
+        b.sql = sql;
+        b.ncols = ncols;
+    }
+    void null() { b.values.emplace_back(); }
+    void text(const char* p, Py_ssize_t n) {
+        dbw::Value v;
+        v.kind = dbw::Value::Text;
+        v.p = p;
+        v.n = static_cast<int32_t>(n);
+        b.values.push_back(v);
+    }
+    void str(PyObject* o) {  // a str the caller keeps alive, or None
+        if (o == Py_None) return null();
+        Py_ssize_t n = 0;
+        const char* p = PyUnicode_AsUTF8AndSize(o, &n);
+        if (!p) throw py::error_already_set();
+        text(p, n);
+    }
+    void owned(std::string&& s) {
+        b.owned.push_back(std::move(s));
+        text(b.owned.back().data(), (Py_ssize_t)b.owned.back().size());
+    }
+    void integer_or_null(PyObject* o) {
+        if (o == Py_None) return null();
+        dbw::Value v;
+        v.kind = dbw::Value::Int;
+        v.i = PyLong_AsLongLong(o);
+        if (v.i == -1 && PyErr_Occurred()) throw py::error_already_set();
+        b.values.push_back(v);
+    }
+    void integer(long long i) {
+        dbw::Value v;
+        v.kind = dbw::Value::Int;
+        v.i = i;
+        b.values.push_back(v);
+    }
+    bool empty() const { return b.values.empty(); }
+};
+
+PyObject* getattr_borrowed(PyObject* o, const char* name, std::vector<py::object>& hold) {
+    PyObject* a = PyObject_GetAttrString(o, name);
+    if (!a) throw py::error_already_set();
+    hold.emplace_back(py::reinterpret_steal<py::object>(a));
+    return a;
+}
+
 py::list str_list(const std::vector<std::string>& v) {
     py::list out(v.size());
     for (size_t i = 0; i < v.size(); ++i) out[i] = pystr(v[i]);
@@ -151,6 +247,239 @@ py::dict scan_result_objects(const srcscan::ScanResult& r, py::handle method_cls
     d["files"] = files;
     d["go"] = r.go_json.empty() ? py::object(py::none()) : py::object(pystr(r.go_json));
     return d;
+}
+
+// Phase 1 of the indexing pipeline (dmcp/index/pipeline.py::_phase1_static):
+// class / method / parameter rows straight from the parsed units into the
+// bulk writer (no per-row Python tuples), plus the graph metadata the caller
+// publishes.  Same ids in the same order as the Python loop (ids[] consumed
+// class, its methods, ..., then parameter links) and the same values.
+// The caller keeps ``order``, ``units``, ``ids`` and the scalar strings alive
+// until the writer has finished (text values are views into them).
+// Time-ordered version-7 UUID strings (RFC 9562): 48-bit ms timestamp, then
+// a 74-bit counter started at a random point (rand_a + rand_b), so a batch is
+// strictly increasing and bulk inserts append to the primary-key B-trees.
+struct Uuid7Gen {
+    unsigned long long ms = 0, hi = 0, lo = 0;
+    Uuid7Gen() {
+        unsigned char seed[10];
+        if (getrandom(seed, sizeof(seed), 0) != (ssize_t)sizeof(seed)) throw std::runtime_error("getrandom failed");
+        ms = (unsigned long long)std::chrono::duration_cast<std::chrono::milliseconds>(
+                 std::chrono::system_clock::now().time_since_epoch())
+                 .count();
+        // counter: 12 bits (rand_a) + 62 bits (rand_b); start in the lower half to avoid overflow
+        hi = ((unsigned long long)(seed[0] & 0x07) << 8) | seed[1];  // 11 bits
+        for (int j = 2; j < 10; ++j) lo = (lo << 8) | seed[j];
+        lo &= 0x1FFFFFFFFFFFFFFFull;  // 61 bits
+    }
+    void next(char* s) {  // 36 chars
+        static const char* hex = "0123456789abcdef";
+        unsigned char b[16];
+        for (int j = 0; j < 6; ++j) b[j] = (unsigned char)(ms >> (8 * (5 - j)));
+        b[6] = (unsigned char)(0x70 | ((hi >> 8) & 0x0F));
+        b[7] = (unsigned char)(hi & 0xFF);
+        b[8] = (unsigned char)(0x80 | ((lo >> 56) & 0x3F));
+        for (int j = 9; j < 16; ++j) b[j] = (unsigned char)(lo >> (8 * (15 - j)));
+        if (++lo >> 62) {
+            lo = 0;
+            ++hi;
+        }
+        int k = 0;
+        for (int j = 0; j < 16; ++j) {
+            if (j == 4 || j == 6 || j == 8 || j == 10) s[k++] = '-';
+            s[k++] = hex[b[j] >> 4];
+            s[k++] = hex[b[j] & 15];
+        }
+    }
+};
+
+py::tuple phase1_rows(dbw::BulkWriter& writer, py::list order, py::dict units, py::object ids, py::str pid,
+                      py::str now, py::handle commit_hash, const std::string& cls_sql, const std::string& meth_sql,
+                      const std::string& param_sql, py::handle method_info_cls, int chunk) {
+    if (!PyType_Check(method_info_cls.ptr()) ||
+        !PyType_IsSubtype((PyTypeObject*)method_info_cls.ptr(), &PyTuple_Type))
+        throw py::type_error("method_info_cls must be a tuple subclass");
+    auto* mi_type = (PyTypeObject*)method_info_cls.ptr();
+    // ids: a caller list consumed in order, or None = fresh UUIDv7s (kept
+    // alive by ``generated``, returned to the caller with the metadata)
+    const bool given = !ids.is_none();
+    if (given && !PyList_Check(ids.ptr())) throw py::type_error("ids must be a list or None");
+    const Py_ssize_t n_ids = given ? PyList_GET_SIZE(ids.ptr()) : 0;
+    Py_ssize_t next_id = 0;
+    py::list generated;
+    Uuid7Gen gen;
+    auto nid = [&]() -> PyObject* {
+        if (given) {
+            if (next_id >= n_ids) throw py::value_error("phase1_rows: ran out of ids");
+            return PyList_GET_ITEM(ids.ptr(), next_id++);
+        }
+        char buf[36];
+        gen.next(buf);
+        PyObject* o = PyUnicode_FromStringAndSize(buf, 36);
+        if (!o || PyList_Append(generated.ptr(), o) < 0) {
+            Py_XDECREF(o);
+            throw py::error_already_set();
+        }
+        Py_DECREF(o);  // the list holds it
+        return o;
+    };
+    static const std::string empty_list = "[]";
+    py::dict class_ids, class_types, method_infos, methods_by_ident, links;
+    std::vector<py::object> hold;  // attribute values fetched from the units
+    long long n_cls = 0, n_meth = 0, n_par = 0;
+    RowBuilder cls(cls_sql, 10), meth(meth_sql, 10);
+    int pending = 0;
+    auto flush = [&]() {
+        if (!cls.empty()) writer.put(std::move(cls.b));
+        if (!meth.empty()) writer.put(std::move(meth.b));
+        cls = RowBuilder(cls_sql, 10);
+        meth = RowBuilder(meth_sql, 10);
+        pending = 0;
+    };
+    PyObject* none_tuple = PyTuple_New(0);
+    py::object keep_empty = py::reinterpret_steal<py::object>(none_tuple);
+    const Py_ssize_t n_order = PyList_GET_SIZE(order.ptr());
+    for (Py_ssize_t oi = 0; oi < n_order; ++oi) {
+        PyObject* ident = PyList_GET_ITEM(order.ptr(), oi);
+        PyObject* unit = PyDict_GetItemWithError(units.ptr(), ident);
+        if (!unit) {
+            if (PyErr_Occurred()) throw py::error_already_set();
+            continue;
+        }
+        if (pending == chunk) flush();
+        ++pending;
+        PyObject* cid = nid();
+        if (PyDict_SetItem(class_ids.ptr(), ident, cid) < 0) throw py::error_already_set();
+        PyObject* ct_enum = getattr_borrowed(unit, "class_type", hold);
+        PyObject* ct = getattr_borrowed(ct_enum, "value", hold);
+        PyObject* src = getattr_borrowed(unit, "source_file", hold);
+        // simple / package name: views into the identifier's UTF-8 bytes
+        Py_ssize_t ilen = 0;
+        const char* is = PyUnicode_AsUTF8AndSize(ident, &ilen);
+        if (!is) throw py::error_already_set();
+        Py_ssize_t dot = -1;
+        for (Py_ssize_t k = ilen - 1; k >= 0; --k)
+            if (is[k] == '.') {
+                dot = k;
+                break;
+            }
+        cls.str(cid);
+        cls.str(pid.ptr());
+        cls.text(is, ilen);
+        if (dot >= 0) cls.text(is + dot + 1, ilen - dot - 1); else cls.text(is, ilen);
+        if (dot >= 0) cls.text(is, dot); else cls.null();
+        cls.str(ct);
+        cls.null();
+        cls.str(src);
+        cls.str(now.ptr());
+        cls.str(commit_hash.ptr());
+        ++n_cls;
+        if (PyDict_SetItem(class_types.ptr(), ident, ct) < 0) throw py::error_already_set();
+        PyObject* methods = getattr_borrowed(unit, "methods", hold);
+        PyObject* mseq = PySequence_Fast(methods, "unit.methods must be a sequence");
+        if (!mseq) throw py::error_already_set();
+        py::object keep_mseq = py::reinterpret_steal<py::object>(mseq);
+        const Py_ssize_t nm = PySequence_Fast_GET_SIZE(mseq);
+        py::list infos(nm), mids(nm);
+        for (Py_ssize_t k = 0; k < nm; ++k) {
+            PyObject* m = PySequence_Fast_GET_ITEM(mseq, k);
+            if (!PyTuple_Check(m) || PyTuple_GET_SIZE(m) < 5) throw py::type_error("methods must be StaticMethodInfo");
+            PyObject* name = PyTuple_GET_ITEM(m, 0);
+            PyObject* line = PyTuple_GET_ITEM(m, 1);
+            PyObject* hm = PyTuple_GET_ITEM(m, 2);
+            PyObject* hp = PyTuple_GET_ITEM(m, 3);
+            PyObject* exc = PyTuple_GET_ITEM(m, 4);
+            PyObject* mid = nid();
+            meth.str(mid);
+            meth.str(cid);
+            meth.str(name);
+            meth.null();
+            meth.text(empty_list.data(), 2);
+            PyObject* eseq = PySequence_Fast(exc, "exceptions must be a sequence");
+            if (!eseq) throw py::error_already_set();
+            py::object keep_e = py::reinterpret_steal<py::object>(eseq);
+            if (PySequence_Fast_GET_SIZE(eseq) == 0) {
+                meth.text(empty_list.data(), 2);
+            } else {
+                std::string js;
+                json_str_list_ascii(eseq, js);
+                meth.owned(std::move(js));
+            }
+            meth.str(hm);
+            meth.str(hp);
+            meth.integer_or_null(line);
+            meth.str(now.ptr());
+            ++n_meth;
+            // MethodInfo(name, None, (), exc, http_method, http_path, line)
+            PyObject* args = PyTuple_Pack(7, name, Py_None, none_tuple, exc, hm, hp, line);
+            if (!args) throw py::error_already_set();
+            py::object keep_args = py::reinterpret_steal<py::object>(args);
+            PyObject* info = PyTuple_Type.tp_new(mi_type, py::make_tuple(keep_args).ptr(), nullptr);
+            if (!info) throw py::error_already_set();
+            PyList_SET_ITEM(infos.ptr(), k, info);
+            PyObject* pair = PyTuple_Pack(2, name, mid);
+            if (!pair) throw py::error_already_set();
+            PyList_SET_ITEM(mids.ptr(), k, pair);
+        }
+        if (PyDict_SetItem(method_infos.ptr(), ident, infos.ptr()) < 0 ||
+            PyDict_SetItem(methods_by_ident.ptr(), ident, mids.ptr()) < 0)
+            throw py::error_already_set();
+    }
+    flush();
+    // parameter links (CodeContextService.java:274-291, 805-856): the first
+    // method of each name that has resolved parameter types
+    RowBuilder par(param_sql, 5);
+    PyObject *key, *mids;
+    Py_ssize_t pos = 0;
+    while (PyDict_Next(methods_by_ident.ptr(), &pos, &key, &mids)) {
+        PyObject* unit = PyDict_GetItemWithError(units.ptr(), key);
+        if (!unit) {
+            if (PyErr_Occurred()) throw py::error_already_set();
+            continue;
+        }
+        PyObject* params = getattr_borrowed(unit, "params", hold);
+        if (!PyDict_Check(params) || PyDict_GET_SIZE(params) == 0 || PyList_GET_SIZE(mids) == 0) continue;
+        py::dict per;
+        const Py_ssize_t nm = PyList_GET_SIZE(mids);
+        for (Py_ssize_t k = 0; k < nm; ++k) {
+            PyObject* pair = PyList_GET_ITEM(mids, k);
+            PyObject* mname = PyTuple_GET_ITEM(pair, 0);
+            PyObject* mid = PyTuple_GET_ITEM(pair, 1);
+            PyObject* targets = PyDict_GetItemWithError(params, mname);
+            if (!targets) {
+                if (PyErr_Occurred()) throw py::error_already_set();
+                continue;
+            }
+            const int t = PyObject_IsTrue(targets);
+            if (t < 0) throw py::error_already_set();
+            if (!t) continue;
+            const int has = PyDict_Contains(per.ptr(), mname);
+            if (has < 0) throw py::error_already_set();
+            if (!has && PyDict_SetItem(per.ptr(), mname, targets) < 0) throw py::error_already_set();
+            PyObject* tseq = PySequence_Fast(targets, "parameter targets must be a sequence");
+            if (!tseq) throw py::error_already_set();
+            py::object keep_t = py::reinterpret_steal<py::object>(tseq);
+            const Py_ssize_t nt = PySequence_Fast_GET_SIZE(tseq);
+            for (Py_ssize_t p = 0; p < nt; ++p) {
+                PyObject* tcid = PyDict_GetItemWithError(class_ids.ptr(), PySequence_Fast_GET_ITEM(tseq, p));
+                if (!tcid) {
+                    if (PyErr_Occurred()) throw py::error_already_set();
+                    continue;
+                }
+                par.str(nid());
+                par.str(mid);
+                par.integer(p);
+                par.str(tcid);
+                par.str(now.ptr());
+                ++n_par;
+            }
+        }
+        if (PyDict_GET_SIZE(per.ptr()) && PyDict_SetItem(links.ptr(), key, per.ptr()) < 0)
+            throw py::error_already_set();
+    }
+    if (!par.empty()) writer.put(std::move(par.b));
+    return py::make_tuple(n_cls, n_meth, n_par, class_ids, class_types, method_infos, methods_by_ident, links,
+                          generated);
 }
 
 }  // namespace
@@ -310,32 +639,11 @@ PYBIND11_MODULE(_srcscan, m) {
     m.def(
         "uuid7_batch",
         [](size_t n) {
-            unsigned char seed[10];
-            if (getrandom(seed, sizeof(seed), 0) != (ssize_t)sizeof(seed)) throw std::runtime_error("getrandom failed");
-            unsigned long long ms = (unsigned long long)std::chrono::duration_cast<std::chrono::milliseconds>(
-                                        std::chrono::system_clock::now().time_since_epoch()).count();
-            // counter: 12 bits (rand_a) + 62 bits (rand_b); start in the lower half to avoid overflow
-            unsigned long long hi = ((unsigned long long)(seed[0] & 0x07) << 8) | seed[1];  // 11 bits
-            unsigned long long lo = 0;
-            for (int j = 2; j < 10; ++j) lo = (lo << 8) | seed[j];
-            lo &= 0x1FFFFFFFFFFFFFFFull;  // 61 bits
-            static const char* hex = "0123456789abcdef";
+            Uuid7Gen gen;
             py::list out(n);
             char s[36];
-            unsigned char b[16];
             for (size_t i = 0; i < n; ++i) {
-                for (int j = 0; j < 6; ++j) b[j] = (unsigned char)(ms >> (8 * (5 - j)));
-                b[6] = (unsigned char)(0x70 | ((hi >> 8) & 0x0F));
-                b[7] = (unsigned char)(hi & 0xFF);
-                b[8] = (unsigned char)(0x80 | ((lo >> 56) & 0x3F));
-                for (int j = 9; j < 16; ++j) b[j] = (unsigned char)(lo >> (8 * (15 - j)));
-                if (++lo >> 62) { lo = 0; ++hi; }
-                int k = 0;
-                for (int j = 0; j < 16; ++j) {
-                    if (j == 4 || j == 6 || j == 8 || j == 10) s[k++] = '-';
-                    s[k++] = hex[b[j] >> 4];
-                    s[k++] = hex[b[j] & 15];
-                }
+                gen.next(s);
                 out[i] = py::str(s, 36);
             }
             return out;
@@ -391,6 +699,10 @@ PYBIND11_MODULE(_srcscan, m) {
                 if (!err.empty()) throw std::runtime_error("bulk write failed: " + err);
                 return w.rows_written();
             })
+        .def("phase1_rows", &phase1_rows, py::arg("order"), py::arg("units"), py::arg("ids"), py::arg("pid"),
+             py::arg("now"), py::arg("commit_hash"), py::arg("class_sql"), py::arg("method_sql"),
+             py::arg("param_sql"), py::arg("method_info_cls"), py::arg("chunk") = 256,
+             "Phase 1 rows of the parsed units straight into this writer (see phase1_rows in pymodule.cpp)")
         .def_property_readonly("rows_written", &dbw::BulkWriter::rows_written)
         .def("timings", [](const dbw::BulkWriter& w) {
             py::dict d;
@@ -399,5 +711,5 @@ PYBIND11_MODULE(_srcscan, m) {
             d["commit_ms"] = w.commit_ms();
             return d;
         });
-    m.attr("ABI_VERSION") = 2;
+    m.attr("ABI_VERSION") = 3;
 }

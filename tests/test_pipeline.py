@@ -345,3 +345,52 @@ def test_background_wal_checkpoints(tmp_path, repo):
     app3 = make_app(tmp_path, db_background_checkpoint=False)
     assert app3.db.checkpointer is None and app3.db.query_one("PRAGMA wal_autocheckpoint")[0] == 1000
     app3.close()
+
+
+def test_native_phase1_rows_match_python_loop(tmp_path, repo, monkeypatch):
+    """Phase 1 built by the native writer (``phase1_rows``) writes the same
+    rows -- ids included, given the same id sequence -- and the same graph
+    metadata as the Python loop it replaces."""
+    import dmcp.index.pipeline as pl
+    from dmcp.index.pipeline import Indexer
+    (repo / "src/main/java/co/acme/shop/order/Weird.java").write_text(
+        "package co.acme.shop.order;\npublic class Weird {\n"
+        "  public void boom() throws Erroré, java.io.IOException {}\n}\n")
+    _git(repo, "add", "-A")
+    _git(repo, "-c", "user.name=t", "-c", "user.email=t@t", "commit", "-qm", "weird")
+    ids = [f"id-{i:06d}" for i in range(100000)]
+    monkeypatch.setattr(pl, "new_ids", lambda n: ids[:n])
+    monkeypatch.setattr(Indexer, "phase1_ids", ids)
+    dumps = {}
+    for native in (True, False):
+        monkeypatch.setattr(Indexer, "native_phase1", native)
+        app = make_app(tmp_path / f"n{int(native)}")
+        r = app.indexer.analyze_project(str(repo))
+        assert r.success
+        tables = {t: app.db.query(f"SELECT * FROM {t} ORDER BY id") for t in
+                  ("source_classes", "source_methods", "method_parameters")}
+        rows = {t: [tuple(x[k] for k in x.keys() if k not in ("created_at", "project_id")) for x in v]
+                for t, v in tables.items()}
+        graph = json.loads(app.repos.projects.find_by_id(r.project_id).graph_data)
+        dumps[native] = (rows, graph)
+        app.close()
+    assert dumps[True][0] == dumps[False][0]
+    assert dumps[True][1] == dumps[False][1]
+    exc = [x for x in dumps[True][0]["source_methods"] if x[2] == "boom"]
+    assert exc and exc[0][5] == json.dumps(["Erroré", "java.io.IOException"])
+
+
+def test_native_phase1_ids_are_time_ordered_uuid7(tmp_path, repo):
+    """Without given ids the native Phase 1 mints UUIDv7s: unique, version 7,
+    and increasing in row order (classes, then methods, appended to the
+    primary-key B-trees)."""
+    import re
+    app = make_app(tmp_path)
+    app.indexer.analyze_project(str(repo))
+    ids = [r[0] for r in app.db.query("SELECT id FROM source_classes ORDER BY rowid")]
+    mids = [r[0] for r in app.db.query("SELECT id FROM source_methods ORDER BY rowid")]
+    pat = re.compile(r"^[0-9a-f]{8}-[0-9a-f]{4}-7[0-9a-f]{3}-[89ab][0-9a-f]{3}-[0-9a-f]{12}$")
+    assert ids and all(pat.match(i) for i in ids + mids)
+    assert len(set(ids + mids)) == len(ids) + len(mids)
+    assert ids == sorted(ids) and mids == sorted(mids)
+    app.close()

@@ -339,3 +339,50 @@ def test_project_rows_writer_commit_abort_and_failure(tmp_path, monkeypatch, mod
     assert db.query_one("SELECT COUNT(*) FROM source_methods")[0] == 100
     assert db.query("PRAGMA foreign_key_check") == []
     db.close()
+
+
+def test_v6_clustered_tables_migration_keeps_rows(tmp_path, monkeypatch):
+    """A database created before V6 (rowid tables, 4 KiB pages) migrates to
+    the WITHOUT ROWID row tables with every row, constraint and index kept
+    and foreign keys still enforced; new files get 16 KiB pages."""
+    import sqlite3
+    import dmcp.store.db as dbm
+    from dmcp.store.db import Database
+    from dmcp.store.repositories import Repositories
+    path = str(tmp_path / "old.db")
+    monkeypatch.setattr(dbm, "MIGRATIONS", [m for m in dbm.MIGRATIONS if m[0] < 6])
+    monkeypatch.setattr(dbm, "PAGE_SIZE", 4096)
+    old = Database(path)
+    repos = Repositories(old)
+    _seed(repos)
+    with old.transaction() as c:  # parameter links: method -> a class of the same project
+        c.execute("INSERT INTO method_parameters (id, method_id, position, class_id) "
+                  "SELECT 'p' || m.id, m.id, 0, c.id FROM source_methods m JOIN source_classes c ON c.id = m.class_id")
+    counts = {t: old.query_one(f"SELECT COUNT(*) FROM {t}")[0]
+              for t in ("source_classes", "source_methods", "method_parameters")}
+    assert all(counts.values()) and old.schema_version() == 5
+    before = old.query("SELECT * FROM source_methods ORDER BY id")
+    old.close()
+    monkeypatch.undo()
+    db = Database(path)
+    assert db.schema_version() == 6
+    for t, n in counts.items():
+        assert db.query_one(f"SELECT COUNT(*) FROM {t}")[0] == n
+        assert "WITHOUT ROWID" in db.query_one("SELECT sql FROM sqlite_master WHERE name = ?", (t,))[0]
+    assert [tuple(r) for r in db.query("SELECT * FROM source_methods ORDER BY id")] == [tuple(r) for r in before]
+    assert db.query("PRAGMA foreign_key_check") == []
+    assert {r[2] for r in db.query("PRAGMA foreign_key_list(method_parameters)")} == {"source_methods",
+                                                                                      "source_classes"}
+    # cascades still work on the rebuilt tables
+    pid = db.query_one("SELECT project_id FROM source_classes LIMIT 1")[0]
+    with db.transaction() as c:
+        c.execute("DELETE FROM projects WHERE id = ?", (pid,))
+    assert db.query_one("SELECT COUNT(*) FROM source_classes WHERE project_id = ?", (pid,))[0] == 0
+    with pytest.raises(sqlite3.IntegrityError):
+        with db.transaction() as c:
+            c.execute("INSERT INTO source_methods (id, class_id, method_name) VALUES ('x', 'no-such-class', 'm')")
+    assert db.query_one("PRAGMA page_size")[0] == 4096  # an existing file keeps its page size
+    db.close()
+    fresh = Database(str(tmp_path / "new.db"))
+    assert fresh.query_one("PRAGMA page_size")[0] == 16384
+    fresh.close()

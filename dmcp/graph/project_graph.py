@@ -304,6 +304,15 @@ class ProjectGraph:
                         per = self._mparams.setdefault(ident, {})
                     per.setdefault(mname, []).extend(links)
 
+    def static_metadata_targets(self) -> tuple:
+        """The containers :meth:`load_static_metadata` fills, for a native
+        Phase 1 that fills them in place with the same values:
+        (class_ids, node_info, method_info, method_params, nodes, NodeInfo,
+        MethodParameterLink) -- ``native/srcscan/pymodule.cpp::phase1_rows``."""
+        self._check_mutable()
+        return (self._class_ids, self._node_info, self._method_info, self._mparams, self._nodes, NodeInfo,
+                MethodParameterLink)
+
     def node_info(self, identifier: Optional[str]) -> Optional[NodeInfo]:
         return self._node_info.get(identifier) if identifier is not None else None
 

@@ -305,10 +305,9 @@ class Indexer:
             writer = self.repos.project_rows_writer(pid, replace)
         if writer.native_phase1 and self.native_phase1:
             try:
-                (n_cls, n_meth, n_par, class_ids, class_types, method_infos, methods_by_ident,
-                 links) = writer.phase1_rows(list(order), units, self.phase1_ids, now, commit_hash, MethodInfo,
-                                             self.ROW_CHUNK)
-                graph.load_static_metadata(class_ids, class_types, method_infos, links)
+                n_cls, n_meth, n_par, _, _, _, methods_by_ident, _ = writer.phase1_rows(
+                    list(order), units, self.phase1_ids, now, commit_hash, MethodInfo, self.ROW_CHUNK,
+                    graph.static_metadata_targets())
                 writer.close()
             except BaseException:
                 writer.abort()

@@ -694,18 +694,20 @@ class ProjectRowsWriter:
         return self._native is not None and hasattr(self._native, "phase1_rows")
 
     def phase1_rows(self, order, units, ids: Optional[list], now: str, commit_hash: Optional[str], method_info_cls,
-                    chunk: int = 256) -> tuple:
+                    chunk: int = 256, graph_targets: Optional[tuple] = None) -> tuple:
         """Class / method / parameter rows of the parsed ``units`` (in
         ``order``) built natively and streamed to this writer in ``chunk``-class
         batches -- the Python loop of ``Indexer._phase1_static`` without a
         tuple per row (``native/srcscan/pymodule.cpp::phase1_rows``).  ``ids``:
-        the row ids to use in order, or None for fresh UUIDv7s.  Returns
+        the row ids to use in order, or None for fresh UUIDv7s.
+        ``graph_targets`` (``ProjectGraph.static_metadata_targets()``): the
+        graph's metadata is filled in place instead of returned.  Returns
         (n_classes, n_methods, n_params, class_ids, class_types, method_infos,
         methods_by_ident, links)."""
         self._keep.append((order, units, ids, now, commit_hash))  # the native rows are views into these
         r = self.repos
         out = self._native.phase1_rows(order, units, ids, self.project_id, now, commit_hash, r.classes._INSERT,
-                                       r.methods._INSERT, r.params._INSERT, method_info_cls, chunk)
+                                       r.methods._INSERT, r.params._INSERT, method_info_cls, chunk, graph_targets)
         self._keep.append(out[-1])  # ids generated natively
         return out[:-1]
 

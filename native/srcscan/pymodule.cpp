@@ -295,7 +295,7 @@ struct Uuid7Gen {
 
 py::tuple phase1_rows(dbw::BulkWriter& writer, py::list order, py::dict units, py::object ids, py::str pid,
                       py::str now, py::handle commit_hash, const std::string& cls_sql, const std::string& meth_sql,
-                      const std::string& param_sql, py::handle method_info_cls, int chunk) {
+                      const std::string& param_sql, py::handle method_info_cls, int chunk, py::object graph_targets) {
     if (!PyType_Check(method_info_cls.ptr()) ||
         !PyType_IsSubtype((PyTypeObject*)method_info_cls.ptr(), &PyTuple_Type))
         throw py::type_error("method_info_cls must be a tuple subclass");
@@ -325,6 +325,33 @@ py::tuple phase1_rows(dbw::BulkWriter& writer, py::list order, py::dict units, p
     };
     static const std::string empty_list = "[]";
     py::dict class_ids, class_types, method_infos, methods_by_ident, links;
+    // graph_targets = (class_ids, node_info, method_info, mparams, nodes,
+    // NodeInfo, MethodParameterLink) of the ProjectGraph being built: filled
+    // in place, as ProjectGraph.load_static_metadata would from the returned
+    // dicts (which then stay empty, class_ids aside)
+    const bool direct = !graph_targets.is_none();
+    py::dict g_node_info, g_method_info, g_mparams, g_nodes;
+    PyTypeObject *ni_type = nullptr, *mpl_type = nullptr;
+    if (direct) {
+        py::tuple gt = graph_targets.cast<py::tuple>();
+        if (gt.size() != 7) throw py::value_error("graph_targets must have 7 items");
+        class_ids = gt[0].cast<py::dict>();
+        g_node_info = gt[1].cast<py::dict>();
+        g_method_info = gt[2].cast<py::dict>();
+        g_mparams = gt[3].cast<py::dict>();
+        g_nodes = gt[4].cast<py::dict>();
+        for (int k : {5, 6})
+            if (!PyType_Check(gt[k].ptr()) || !PyType_IsSubtype((PyTypeObject*)gt[k].ptr(), &PyTuple_Type))
+                throw py::type_error("graph_targets record types must be tuple subclasses");
+        ni_type = (PyTypeObject*)gt[5].ptr();
+        mpl_type = (PyTypeObject*)gt[6].ptr();
+    }
+    auto make_record = [](PyTypeObject* type, PyObject* fields) -> PyObject* {
+        py::tuple args = py::make_tuple(py::reinterpret_borrow<py::object>(fields));
+        PyObject* r = PyTuple_Type.tp_new(type, args.ptr(), nullptr);
+        if (!r) throw py::error_already_set();
+        return r;
+    };
     std::vector<py::object> hold;  // attribute values fetched from the units
     long long n_cls = 0, n_meth = 0, n_par = 0;
     RowBuilder cls(cls_sql, 10), meth(meth_sql, 10);
@@ -374,7 +401,15 @@ py::tuple phase1_rows(dbw::BulkWriter& writer, py::list order, py::dict units, p
         cls.str(now.ptr());
         cls.str(commit_hash.ptr());
         ++n_cls;
-        if (PyDict_SetItem(class_types.ptr(), ident, ct) < 0) throw py::error_already_set();
+        if (direct) {
+            PyObject* f = PyTuple_Pack(2, ct, Py_None);
+            if (!f) throw py::error_already_set();
+            py::object keep_f = py::reinterpret_steal<py::object>(f);
+            py::object ni = py::reinterpret_steal<py::object>(make_record(ni_type, f));
+            if (PyDict_SetItem(g_node_info.ptr(), ident, ni.ptr()) < 0) throw py::error_already_set();
+        } else if (PyDict_SetItem(class_types.ptr(), ident, ct) < 0) {
+            throw py::error_already_set();
+        }
         PyObject* methods = getattr_borrowed(unit, "methods", hold);
         PyObject* mseq = PySequence_Fast(methods, "unit.methods must be a sequence");
         if (!mseq) throw py::error_already_set();
@@ -421,7 +456,7 @@ py::tuple phase1_rows(dbw::BulkWriter& writer, py::list order, py::dict units, p
             if (!pair) throw py::error_already_set();
             PyList_SET_ITEM(mids.ptr(), k, pair);
         }
-        if (PyDict_SetItem(method_infos.ptr(), ident, infos.ptr()) < 0 ||
+        if (PyDict_SetItem((direct ? g_method_info : method_infos).ptr(), ident, infos.ptr()) < 0 ||
             PyDict_SetItem(methods_by_ident.ptr(), ident, mids.ptr()) < 0)
             throw py::error_already_set();
     }
@@ -474,8 +509,55 @@ py::tuple phase1_rows(dbw::BulkWriter& writer, py::list order, py::dict units, p
                 ++n_par;
             }
         }
-        if (PyDict_GET_SIZE(per.ptr()) && PyDict_SetItem(links.ptr(), key, per.ptr()) < 0)
-            throw py::error_already_set();
+        if (!PyDict_GET_SIZE(per.ptr())) continue;
+        if (!direct) {
+            if (PyDict_SetItem(links.ptr(), key, per.ptr()) < 0) throw py::error_already_set();
+            continue;
+        }
+        // ProjectGraph.load_static_metadata's link pass: targets that are
+        // graph nodes, as MethodParameterLink(position, target)
+        const int is_node = PyDict_Contains(g_nodes.ptr(), key);
+        if (is_node < 0) throw py::error_already_set();
+        if (!is_node) continue;
+        PyObject* gper = nullptr;
+        PyObject *mname, *targets;
+        Py_ssize_t ppos = 0;
+        while (PyDict_Next(per.ptr(), &ppos, &mname, &targets)) {
+            PyObject* tseq = PySequence_Fast(targets, "parameter targets must be a sequence");
+            if (!tseq) throw py::error_already_set();
+            py::object keep_t = py::reinterpret_steal<py::object>(tseq);
+            py::list lks;
+            const Py_ssize_t nt = PySequence_Fast_GET_SIZE(tseq);
+            for (Py_ssize_t p = 0; p < nt; ++p) {
+                PyObject* t = PySequence_Fast_GET_ITEM(tseq, p);
+                const int in = PyDict_Contains(g_nodes.ptr(), t);
+                if (in < 0) throw py::error_already_set();
+                if (!in) continue;
+                py::object posn = py::int_(p);
+                PyObject* f = PyTuple_Pack(2, posn.ptr(), t);
+                if (!f) throw py::error_already_set();
+                py::object keep_f = py::reinterpret_steal<py::object>(f);
+                py::object link = py::reinterpret_steal<py::object>(make_record(mpl_type, f));
+                lks.append(link);
+            }
+            if (lks.empty()) continue;
+            if (!gper) {
+                gper = PyDict_GetItemWithError(g_mparams.ptr(), key);
+                if (!gper) {
+                    if (PyErr_Occurred()) throw py::error_already_set();
+                    py::dict fresh;
+                    if (PyDict_SetItem(g_mparams.ptr(), key, fresh.ptr()) < 0) throw py::error_already_set();
+                    gper = fresh.ptr();  // now owned by g_mparams
+                }
+            }
+            PyObject* lst = PyDict_GetItemWithError(gper, mname);
+            if (!lst) {
+                if (PyErr_Occurred()) throw py::error_already_set();
+                if (PyDict_SetItem(gper, mname, lks.ptr()) < 0) throw py::error_already_set();
+            } else if (PyList_SetSlice(lst, PY_SSIZE_T_MAX, PY_SSIZE_T_MAX, lks.ptr()) < 0) {  // extend
+                throw py::error_already_set();
+            }
+        }
     }
     if (!par.empty()) writer.put(std::move(par.b));
     return py::make_tuple(n_cls, n_meth, n_par, class_ids, class_types, method_infos, methods_by_ident, links,
@@ -702,6 +784,7 @@ PYBIND11_MODULE(_srcscan, m) {
         .def("phase1_rows", &phase1_rows, py::arg("order"), py::arg("units"), py::arg("ids"), py::arg("pid"),
              py::arg("now"), py::arg("commit_hash"), py::arg("class_sql"), py::arg("method_sql"),
              py::arg("param_sql"), py::arg("method_info_cls"), py::arg("chunk") = 256,
+             py::arg("graph_targets") = py::none(),
              "Phase 1 rows of the parsed units straight into this writer (see phase1_rows in pymodule.cpp)")
         .def_property_readonly("rows_written", &dbw::BulkWriter::rows_written)
         .def("timings", [](const dbw::BulkWriter& w) {

@@ -66,6 +66,20 @@ typedef short v4i16_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ bf16x8_t as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8_t, v); }
 
+// x of this lane and of lane ^ 32, through v_permlane32_swap (a VALU lane
+// swap; __shfl_xor(x, 32) goes through an LDS ds_bpermute round trip).
+// After the swap one result holds this lane's value and the other the
+// partner half's, so symmetric ops (max, +) need not know which is which.
+__device__ __forceinline__ float half_swap_max(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __builtin_fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+__device__ __forceinline__ float half_swap_sum(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // ---- FP8 KV cache (OCP e4m3fn, gfx950's native fp8): unit scale, values
 // saturated to +-448 on the way in (the hardware conversion does not clamp).
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));

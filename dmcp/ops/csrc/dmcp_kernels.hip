@@ -615,7 +615,7 @@ __global__ __launch_bounds__(kBlock) void prefix_attn_kernel(
                     mt = fmaxf(mt, s[i]);
                 }
             }
-            mt = fmaxf(mt, __shfl_xor(mt, 32, kWave)) * scale_log2;
+            mt = half_swap_max(mt) * scale_log2;
             const float mn = fmaxf(m, mt);
             if (__any(mn > m)) {
                 const float corr = __builtin_amdgcn_exp2f(m - mn);
@@ -643,7 +643,7 @@ __global__ __launch_bounds__(kBlock) void prefix_attn_kernel(
                         as_bf16x8(*reinterpret_cast<const uint4*>(vl + 16 * s2)), pb[s2], o[t], 0, 0, 0);
             }
         }
-        const float lt = l + __shfl_xor(l, 32, kWave);
+        const float lt = half_swap_sum(l);
         if (!qok) continue;
         const size_t pi = ((size_t)b * Hq + (size_t)kh * G + g) * splits_total + sp;
         // O^T register i of d tile t: d = 32t + (i&3) + 8*(i>>2) + 4*h
@@ -890,14 +890,12 @@ __device__ __forceinline__ void attn_tile_mfma(KVTile<D, KV8>& cur, bool prefetc
     const bf16x8_t pf = __builtin_convertvector(pr, bf16x8_t);
 #pragma unroll
     for (int db = 0; db < DB; ++db) {
-        const v4i16_t lo =
-            __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16_t*)(tr0 + 16 * db));
-        const v4i16_t hi =
-            __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16_t*)(tr1 + 16 * db));
-        const uint4 a = make_uint4((uint32_t)(uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16),
-                                   (uint32_t)(uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16),
-                                   (uint32_t)(uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16),
-                                   (uint32_t)(uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16));
+        // the two transposed reads as whole 32-bit registers (no 16-bit repacking)
+        const uint2 lo = __builtin_bit_cast(
+            uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16_t*)(tr0 + 16 * db)));
+        const uint2 hi = __builtin_bit_cast(
+            uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16_t*)(tr1 + 16 * db)));
+        const uint4 a = make_uint4(lo.x, lo.y, hi.x, hi.y);
         acc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), pf, acc[db], 0, 0, 0);
     }
 }

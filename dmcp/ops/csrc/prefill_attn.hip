@@ -63,8 +63,6 @@ __device__ __forceinline__ int pf_off(int row, int ch) {
     return row * D + 8 * (ch ^ pf_swz<D>(row));
 }
 
-typedef short v8i16_t __attribute__((ext_vector_type(8)));
-
 // ds_read_b64_tr_b16: lane 4q+p of each 16-lane group addresses row q,
 // columns 4p..4p+3 of a 4 x 16 block; lane i receives column i (row q in
 // element q).  EXEC must be full: callers never diverge around it.
@@ -111,7 +109,10 @@ __global__ __launch_bounds__(NWAVE * 64) void prefill_attn_kernel(
     // split-K: this block's stages [st0, st1) of the column tile's key range
     const int per = (nst_all + nsplit - 1) / nsplit;
     const int st0 = min(nst_all, sp * per), st1 = min(nst_all, st0 + per);
-    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+    // the wave index through readfirstlane: every per-unit bound below is then
+    // provably wave-uniform, so the tile-skip and mask decisions compile to
+    // scalar branches instead of exec-mask save/restore sequences
+    const int lane = threadIdx.x & (kWave - 1), wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int r = lane & 31, h = lane >> 5;
 
     int qpos[NSUB], qmin[NSUB], qmax[NSUB], cf[NSUB];
@@ -230,7 +231,7 @@ __global__ __launch_bounds__(NWAVE * 64) void prefill_attn_kernel(
                 // masked scores are -inf and m starts at a finite -1e30, so a
                 // lane with no visible key in the tile (or split) adds
                 // exp2(-inf) = 0 and every rescale factor stays finite
-                mt = fmaxf(mt, __shfl_xor(mt, 32, kWave)) * sl2;
+                mt = half_swap_max(mt) * sl2;
                 const float mn = fmaxf(m[u], mt);
                 if (__any(mn > m[u])) {
                     const float corr = __builtin_amdgcn_exp2f(m[u] - mn);
@@ -259,9 +260,11 @@ __global__ __launch_bounds__(NWAVE * 64) void prefill_attn_kernel(
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) {
                     const int R0 = sub * 32 + 16 * s2 + 4 * h + tq;
-                    const v4i16_t lo = lds_tr16(Vt + pf_off<D>(R0, ch) + 4 * (tp & 1));
-                    const v4i16_t hi = lds_tr16(Vt + pf_off<D>(R0 + 8, ch) + 4 * (tp & 1));
-                    const bf16x8_t vf = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+                    // whole 32-bit registers of the two reads (a per-element
+                    // 16-bit shuffle costs VALU and/or/shift packing per element)
+                    const uint2 lo = __builtin_bit_cast(uint2, lds_tr16(Vt + pf_off<D>(R0, ch) + 4 * (tp & 1)));
+                    const uint2 hi = __builtin_bit_cast(uint2, lds_tr16(Vt + pf_off<D>(R0 + 8, ch) + 4 * (tp & 1)));
+                    const bf16x8_t vf = as_bf16x8(make_uint4(lo.x, lo.y, hi.x, hi.y));
 #pragma unroll
                     for (int u = 0; u < NSUB; ++u)
                         if (act[u]) o[u][t2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb[u][s2], o[u][t2], 0, 0, 0);
@@ -276,7 +279,7 @@ __global__ __launch_bounds__(NWAVE * 64) void prefill_attn_kernel(
 #pragma unroll
     for (int u = 0; u < NSUB; ++u) {
         if (!uact[u]) continue;
-        const float lt = l[u] + __shfl_xor(l[u], 32, kWave);
+        const float lt = half_swap_sum(l[u]);
         const int c = cf[u] + r;
         if (c >= NC) continue;
         const int t = c / G, g = c - t * G;

@@ -26,6 +26,7 @@ def main() -> int:
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--arms", default="", help="comma-separated arm names to run (default: all)")
     a = ap.parse_args()
     from dmcp.models.llm import _extend_attention
     from dmcp.ops import hip
@@ -51,6 +52,9 @@ def main() -> int:
         for nsplit in (1, 2, 4):
             arms[f"mfma_v{variant}_s{nsplit}"] = (lambda v, n: lambda: hip.prefill_attention(
                 q, kc, vc, 0, P, 1, P, scale, variant=v, nsplit=n))(variant, nsplit)
+    if a.arms:
+        keep = set(a.arms.split(","))
+        arms = {k: v for k, v in arms.items() if k in keep}
     ref = sdpa().float()
     for name, fn in arms.items():
         err = (fn().float() - ref).abs().max().item()

@@ -40,6 +40,7 @@ class GitClient:
         self.ssh_key_path = ssh_key_path
         self.timeout = timeout_seconds
         self.read_local_in_place = True  # snapshot(): local repositories without a private clone
+        self.native_objects = True  # snapshot(): ref + tree read from loose objects natively when possible
 
     def _env(self) -> dict:
         env = dict(os.environ)
@@ -141,8 +142,7 @@ class GitClient:
     def resolve_commit(self, repo_dir: str, branch: Optional[str]) -> str:
         """The commit ``git clone --branch <branch>`` would check out: the
         branch head, else the tag of that name; HEAD when no branch is given."""
-        refs = [f"refs/heads/{branch}", f"refs/tags/{branch}"] if branch else ["HEAD"]
-        for ref in refs:
+        for ref in self.branch_refs(branch):
             rc, out, _ = self._git(["rev-parse", "--verify", "--quiet", f"{ref}^{{commit}}"], cwd=repo_dir,
                                    check=False)
             if rc == 0 and out.strip():
@@ -150,16 +150,25 @@ class GitClient:
         raise GitError(f"Remote branch {branch} not found in upstream origin" if branch
                        else "repository has no HEAD commit")
 
+    @staticmethod
+    def branch_refs(branch: Optional[str]) -> List[str]:
+        return [f"refs/heads/{branch}", f"refs/tags/{branch}"] if branch else ["HEAD"]
+
     def _local_snapshot(self, url: RepositoryUrl, source: str, branch: Optional[str], shallow: bool,
                         max_bytes: int):
         """A local repository's objects are read in place: content-addressed
         objects never change, so a private clone adds nothing but a process
         and a ref copy.  The tree does not own (and never deletes) ``source``."""
-        from .source import CheckoutTree, MemoryTree, list_tree, read_blobs, wanted
+        from .source import CheckoutTree, MemoryTree, list_tree, native_commit_tree, read_blobs, wanted
         LOG.info("Reading %s (branch: %s) in place", url, branch)
         try:
-            commit = self.resolve_commit(source, branch)
-            entries = [e for e in list_tree(self, source, commit) if wanted(e[0])]
+            fast = native_commit_tree(source, self.branch_refs(branch)) if self.native_objects else None
+            if fast is not None:
+                commit, listing = fast
+            else:
+                commit = self.resolve_commit(source, branch)
+                listing = list_tree(self, source, commit)
+            entries = [e for e in listing if wanted(e[0])]
             blobs = read_blobs(self, source, [e[1] for e in entries], max_bytes)
         except GitError as e:
             raise GitError(f"Failed to clone repository: {e}") from e

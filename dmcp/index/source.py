@@ -188,6 +188,41 @@ def _object_dirs(git_dir: str) -> List[str]:
     return dirs
 
 
+def git_dir_of(path: str) -> Optional[str]:
+    """The git directory of a work tree (``<path>/.git``) or bare repository
+    (``path`` itself); None for anything else (e.g. a ``.git`` file of a linked
+    work tree), which is left to git."""
+    dot = os.path.join(path, ".git")
+    if os.path.isdir(dot):
+        return dot
+    if os.path.isfile(os.path.join(path, "HEAD")) and os.path.isdir(os.path.join(path, "objects")):
+        return path
+    return None
+
+
+def native_commit_tree(repo: str, refs: List[str]) -> Optional[Tuple[str, List[Tuple[str, str]]]]:
+    """(commit, ls-tree entries) read straight from a loose object store
+    (``native/srcscan/gitobj.cpp``): what ``git rev-parse --verify
+    <ref>^{commit}`` over ``refs`` and ``git ls-tree -r`` report, without the
+    two processes.  None whenever git has to answer (packed objects or refs the
+    reader does not handle, no native extension)."""
+    try:
+        from .. import _srcscan  # type: ignore
+    except ImportError:
+        return None
+    resolve = getattr(_srcscan, "resolve_ref", None)
+    gd = git_dir_of(repo)
+    if resolve is None or gd is None or not mostly_loose(repo):
+        return None
+    commit = resolve(gd, refs)
+    if commit is None:
+        return None
+    entries = _srcscan.list_tree_loose(_object_dirs(repo), commit)
+    if entries is None:
+        return None
+    return commit, entries
+
+
 def mostly_loose(git_dir: str) -> bool:
     """True when the repository's objects (alternates included) are mostly
     loose: git creates a fan-out directory per object-id prefix on demand and

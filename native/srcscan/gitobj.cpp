@@ -1,4 +1,8 @@
-// Loose git object reader: inflates `objects/xx/yyyy…` files on a thread pool.
+// Loose git object reader: inflates `objects/xx/yyyy…` files on a thread pool,
+// and resolves a ref + lists a commit's tree from loose objects (what
+// `git rev-parse <ref>^{commit}` and `git ls-tree -r` report, without the two
+// processes).  Anything packed or unusual makes these return false and the
+// caller asks git.
 //
 // An in-memory snapshot (dmcp/index/source.py) needs the content of every
 // source blob at one commit.  `git cat-file --batch` inflates them serially
@@ -15,6 +19,7 @@
 #include <atomic>
 #include <cstring>
 #include <string>
+#include <string_view>
 #include <vector>
 
 #include "gitobj.hpp"
@@ -44,8 +49,9 @@ bool slurp(const std::string& path, std::string& out) {
     return got > 0;
 }
 
-// "blob <size>\0<content>" -> content; false on anything else
-bool inflate_blob(const std::string& z, std::string& out) {
+// "<type> <size>\0<content>" -> content (type checked against `want`, or
+// returned through `type` when want is null); false on anything else
+bool inflate_object(const std::string& z, std::string& out, const char* want, std::string* type = nullptr) {
     z_stream s;
     std::memset(&s, 0, sizeof(s));
     if (inflateInit(&s) != Z_OK) return false;
@@ -62,12 +68,15 @@ bool inflate_blob(const std::string& z, std::string& out) {
     }
     size_t have = sizeof(head) - s.avail_out;
     const char* nul = static_cast<const char*>(std::memchr(head, 0, have));
-    if (!nul || have < 6 || std::memcmp(head, "blob ", 5) != 0) {
+    const char* sp = nul ? static_cast<const char*>(std::memchr(head, ' ', static_cast<size_t>(nul - head))) : nullptr;
+    if (!sp || sp == head || sp + 1 >= nul ||
+        (want && (std::strlen(want) != static_cast<size_t>(sp - head) || std::memcmp(head, want, sp - head) != 0))) {
         inflateEnd(&s);
         return false;
     }
+    if (type) type->assign(head, static_cast<size_t>(sp - head));
     size_t size = 0;
-    for (const char* p = head + 5; p < nul; ++p) {
+    for (const char* p = sp + 1; p < nul; ++p) {
         if (*p < '0' || *p > '9') {
             inflateEnd(&s);
             return false;
@@ -91,7 +100,137 @@ bool inflate_blob(const std::string& z, std::string& out) {
     return (rc == Z_STREAM_END || rc == Z_OK || rc == Z_BUF_ERROR) && body_have == size;
 }
 
+bool read_loose(const std::vector<std::string>& object_dirs, const std::string& sha, std::string& body,
+                const char* want, std::string* type = nullptr) {
+    if (sha.size() != 40) return false;
+    std::string z;
+    for (const std::string& d : object_dirs) {
+        if (slurp(d + "/" + sha.substr(0, 2) + "/" + sha.substr(2), z)) break;
+        z.clear();
+    }
+    return !z.empty() && inflate_object(z, body, want, type);
+}
+
+bool is_hex40(std::string_view s) {
+    if (s.size() != 40) return false;
+    for (char c : s)
+        if (!((c >= '0' && c <= '9') || (c >= 'a' && c <= 'f'))) return false;
+    return true;
+}
+
+std::string trim(std::string s) {
+    while (!s.empty() && (s.back() == '\n' || s.back() == '\r' || s.back() == ' ')) s.pop_back();
+    return s;
+}
+
+// a ref's target: loose ref file (symbolic refs followed), else packed-refs
+bool ref_target(const std::string& git_dir, const std::string& ref, std::string& sha, int depth = 0) {
+    if (depth > 5) return false;
+    std::string text;
+    if (slurp(git_dir + "/" + ref, text)) {
+        text = trim(text);
+        if (text.rfind("ref: ", 0) == 0) return ref_target(git_dir, text.substr(5), sha, depth + 1);
+        if (!is_hex40(text)) return false;
+        sha = text;
+        return true;
+    }
+    if (ref == "HEAD" || !slurp(git_dir + "/packed-refs", text)) return false;
+    size_t pos = 0;
+    while (pos < text.size()) {
+        size_t eol = text.find('\n', pos);
+        if (eol == std::string::npos) eol = text.size();
+        std::string_view line(text.data() + pos, eol - pos);
+        if (line.size() > 41 && line[40] == ' ' && line.substr(41) == ref && is_hex40(line.substr(0, 40))) {
+            sha.assign(line.substr(0, 40));
+            return true;
+        }
+        pos = eol + 1;
+    }
+    return false;
+}
+
+void hex20(const unsigned char* b, std::string& out) {
+    static const char* hx = "0123456789abcdef";
+    out.resize(40);
+    for (int i = 0; i < 20; ++i) {
+        out[2 * i] = hx[b[i] >> 4];
+        out[2 * i + 1] = hx[b[i] & 15];
+    }
+}
+
+// ls-tree -r order: entries in tree order, subtrees expanded in place
+bool walk_tree(const std::vector<std::string>& object_dirs, const std::string& tree_sha, const std::string& prefix,
+               std::vector<std::pair<std::string, std::string>>& out, int depth) {
+    if (depth > 256) return false;
+    std::string body;
+    if (!read_loose(object_dirs, tree_sha, body, "tree")) return false;
+    size_t p = 0;
+    std::string sha;
+    while (p < body.size()) {
+        size_t sp = body.find(' ', p);
+        if (sp == std::string::npos) return false;
+        size_t nul = body.find('\0', sp);
+        if (nul == std::string::npos || nul + 21 > body.size()) return false;
+        std::string_view mode(body.data() + p, sp - p);
+        std::string name = prefix + body.substr(sp + 1, nul - sp - 1);
+        hex20(reinterpret_cast<const unsigned char*>(body.data() + nul + 1), sha);
+        p = nul + 21;
+        if (mode == "40000") {
+            if (!walk_tree(object_dirs, sha, name + "/", out, depth + 1)) return false;
+        } else if (mode == "100644" || mode == "100755" || mode == "100664") {
+            out.emplace_back(std::move(name), sha);
+        } else if (mode != "120000" && mode != "160000") {
+            return false;  // unknown mode: let git decide
+        }
+    }
+    return true;
+}
+
 }  // namespace
+
+bool resolve_commit(const std::string& git_dir, const std::vector<std::string>& refs, std::string& commit) {
+    std::vector<std::string> object_dirs{git_dir + "/objects"};
+    std::string alt;
+    if (slurp(git_dir + "/objects/info/alternates", alt)) {
+        size_t pos = 0;
+        while (pos < alt.size()) {
+            size_t eol = alt.find('\n', pos);
+            if (eol == std::string::npos) eol = alt.size();
+            std::string line = trim(alt.substr(pos, eol - pos));
+            if (!line.empty() && line[0] != '#') object_dirs.push_back(line);
+            pos = eol + 1;
+        }
+    }
+    for (const std::string& ref : refs) {
+        std::string sha;
+        if (!ref_target(git_dir, ref, sha)) continue;
+        // peel annotated tags down to the commit (`<ref>^{commit}`)
+        for (int hop = 0; hop < 8; ++hop) {
+            std::string body, type;
+            if (!read_loose(object_dirs, sha, body, nullptr, &type)) return false;  // packed: git decides
+            if (type == "commit") {
+                commit = sha;
+                return true;
+            }
+            if (type != "tag" || body.rfind("object ", 0) != 0 || body.size() < 47) break;
+            sha = body.substr(7, 40);
+            if (!is_hex40(sha)) break;
+        }
+        return false;  // the ref exists but does not name a commit: git's error path
+    }
+    return false;
+}
+
+bool list_tree(const std::vector<std::string>& object_dirs, const std::string& commit,
+               std::vector<std::pair<std::string, std::string>>& out) {
+    std::string body;
+    if (!read_loose(object_dirs, commit, body, "commit")) return false;
+    if (body.rfind("tree ", 0) != 0 || body.size() < 45) return false;
+    const std::string tree = body.substr(5, 40);
+    if (!is_hex40(tree)) return false;
+    out.clear();
+    return walk_tree(object_dirs, tree, "", out, 0);
+}
 
 LooseResult read_loose_blobs(const std::vector<std::string>& object_dirs, const std::vector<std::string>& shas,
                              int threads, uint64_t max_bytes) {
@@ -111,7 +250,7 @@ LooseResult read_loose_blobs(const std::vector<std::string>& object_dirs, const 
         }
         if (z.empty()) return;
         std::string body;
-        if (!inflate_blob(z, body)) return;
+        if (!inflate_object(z, body, "blob")) return;
         uint64_t t = total.fetch_add(body.size(), std::memory_order_relaxed) + body.size();
         if (max_bytes && t > max_bytes) exceeded.store(true, std::memory_order_relaxed);
         r.data[i] = std::move(body);

@@ -19,4 +19,14 @@ struct LooseResult {
 LooseResult read_loose_blobs(const std::vector<std::string>& object_dirs, const std::vector<std::string>& shas,
                              int threads, uint64_t max_bytes);
 
+// The commit the first resolvable ref of `refs` ("HEAD", "refs/heads/x",
+// "refs/tags/x") names, annotated tags peeled.  false when git must answer
+// (ref storage or objects not readable here, or the ref is not a commit).
+bool resolve_commit(const std::string& git_dir, const std::vector<std::string>& refs, std::string& commit);
+
+// (path, blob id) of every regular file at `commit`, in `git ls-tree -r`
+// order (symlinks and submodules skipped); false unless every tree is loose.
+bool list_tree(const std::vector<std::string>& object_dirs, const std::string& commit,
+               std::vector<std::pair<std::string, std::string>>& out);
+
 }  // namespace gitobj

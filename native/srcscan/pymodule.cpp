@@ -754,6 +754,45 @@ PYBIND11_MODULE(_srcscan, m) {
         py::arg("object_dirs"), py::arg("shas"), py::arg("threads") = 0, py::arg("max_bytes") = 0,
         "Loose-object blob contents (None where an object is not loose) and whether max_bytes was exceeded.");
 
+    m.def(
+        "resolve_ref",
+        [](const std::string& git_dir, const std::vector<std::string>& refs) -> py::object {
+            std::string commit;
+            bool ok;
+            {
+                py::gil_scoped_release release;
+                ok = gitobj::resolve_commit(git_dir, refs, commit);
+            }
+            if (!ok) return py::none();
+            return pystr(commit);
+        },
+        py::arg("git_dir"), py::arg("refs"),
+        "Commit id of the first resolvable ref (tags peeled) from loose refs/objects; None = ask git.");
+    m.def(
+        "list_tree_loose",
+        [](const std::vector<std::string>& object_dirs, const std::string& commit) -> py::object {
+            std::vector<std::pair<std::string, std::string>> entries;
+            bool ok;
+            {
+                py::gil_scoped_release release;
+                ok = gitobj::list_tree(object_dirs, commit, entries);
+            }
+            if (!ok) return py::none();
+            py::list out(entries.size());
+            for (size_t i = 0; i < entries.size(); ++i) {
+                PyObject* path = PyUnicode_DecodeUTF8(entries[i].first.data(),
+                                                      static_cast<Py_ssize_t>(entries[i].first.size()), "strict");
+                if (!path) {  // not UTF-8: git's own listing decides how to present it
+                    PyErr_Clear();
+                    return py::none();
+                }
+                out[i] = py::make_tuple(py::reinterpret_steal<py::str>(path), pystr(entries[i].second));
+            }
+            return out;
+        },
+        py::arg("object_dirs"), py::arg("commit"),
+        "(path, blob id) of the commit's regular files in ls-tree -r order, or None unless all trees are loose.");
+
     py::class_<dbw::BulkWriter>(m, "BulkWriter",
                                 "One SQLite write transaction on a worker thread (see bulkwriter.hpp).")
         .def(py::init([](const std::string& path, int busy_timeout_ms, py::list setup) {
@@ -794,5 +833,5 @@ PYBIND11_MODULE(_srcscan, m) {
             d["commit_ms"] = w.commit_ms();
             return d;
         });
-    m.attr("ABI_VERSION") = 3;
+    m.attr("ABI_VERSION") = 4;
 }

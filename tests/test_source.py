@@ -192,3 +192,67 @@ def test_scan_objects_equal_json_document(tmp_path, kind):
     a.stats = b.stats = None
     assert a.units and a == b
     assert all(type(m).__name__ == "StaticMethodInfo" for u in a.units.values() for m in u.methods)
+
+
+def test_native_ref_and_tree_match_git(tmp_path):
+    """resolve_ref / list_tree_loose report what rev-parse <ref>^{commit} and
+    ls-tree -r do (nested trees, executables, symlinks, a gitlink, branches,
+    lightweight and annotated tags, packed refs), and give up (None) on
+    packed objects so git answers."""
+    from dmcp import _srcscan
+    from dmcp.index.source import _object_dirs, git_dir_of, list_tree, native_commit_tree
+    src = tmp_path / "src"
+    src.mkdir()
+
+    def git(*a):
+        return subprocess.run(["git", "-C", str(src), *a], check=True, capture_output=True, text=True).stdout
+    git("init", "-q", "-b", "main")
+    git("config", "user.email", "t@t")
+    git("config", "user.name", "t")
+    for rel in ("a/b/c/D.java", "a/B.java", "z.ts", "a/b/E.go", "ü/Ñ.java"):
+        p = src / rel
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_text(f"// {rel}\n")
+    (src / "run.sh").write_text("#!/bin/sh\n")
+    os.chmod(src / "run.sh", 0o755)
+    os.symlink("z.ts", src / "link.ts")
+    git("add", "-A")
+    git("update-index", "--add", "--cacheinfo", "160000," + "1" * 40 + ",sub")  # a submodule entry
+    git("commit", "-qm", "one")
+    git("tag", "light")
+    git("checkout", "-qb", "dev")
+    (src / "a" / "New.java").write_text("class New {}\n")
+    git("add", "-A")
+    git("commit", "-qm", "two")
+    git("tag", "-a", "rel", "-m", "annotated")
+    git("checkout", "-q", "main")
+    g = GitClient(str(tmp_path / "c"))
+    gd, dirs = git_dir_of(str(src)), _object_dirs(str(src))
+    assert gd == str(src / ".git")
+
+    def check():
+        for branch in (None, "main", "dev", "light", "rel"):
+            refs = g.branch_refs(branch)
+            commit = _srcscan.resolve_ref(gd, refs)
+            assert commit == g.resolve_commit(str(src), branch), branch
+            assert _srcscan.list_tree_loose(dirs, commit) == list_tree(g, str(src), commit)
+        assert _srcscan.resolve_ref(gd, g.branch_refs("nope")) is None
+    check()
+    listing = _srcscan.list_tree_loose(dirs, g.resolve_commit(str(src), "dev"))
+    paths = [p for p, _ in listing]
+    assert "a/b/c/D.java" in paths and "run.sh" in paths and "ü/Ñ.java" in paths
+    assert "link.ts" not in paths and "sub" not in paths
+    git("pack-refs", "--all")  # refs now only in packed-refs
+    assert not (src / ".git" / "refs" / "tags" / "rel").exists()
+    check()
+    import dmcp.index.source as S
+    orig = S.mostly_loose
+    S.mostly_loose = lambda d: True
+    try:
+        assert native_commit_tree(str(src), ["HEAD"])[0] == g.resolve_commit(str(src), None)
+        git("gc", "-q", "--prune=now")  # objects packed: the native reader declines
+        assert native_commit_tree(str(src), ["HEAD"]) is None
+    finally:
+        S.mostly_loose = orig
+    snap = g.snapshot(RepositoryUrl.of(str(src)), "dev")  # git path after the fallback
+    assert "a/New.java" in snap.files

@@ -206,7 +206,9 @@ class Indexer:
                 LOG.info("Graph built: %d nodes, %d entry points", graph.node_count(), graph.entry_point_count())
                 order = graph.analysis_order()
                 with span("analyze.phase1", stats):
-                    p1 = self._phase1_static(project, parsed, graph, order, clone.commit_hash, writer)
+                    # without enrichment the swap stays open for the project row
+                    p1 = self._phase1_static(project, parsed, graph, order, clone.commit_hash, writer,
+                                             close=self.backend.enabled)
                 classes, methods_by_ident, writer = p1
                 enriched = failed = recovered = 0
                 if self.backend.enabled:
@@ -221,12 +223,18 @@ class Indexer:
                 with span("analyze.persist_graph", stats):
                     project.base_package = common_package_prefix({package_name_of(i) for i in parsed.units})
                     project.update_graph_data(graph.to_json())
+                    project.analysis_completed(clone.commit_hash)
+                    # the project row joins the row swap's transaction when the
+                    # swap is still open (no enrichment), else it follows it
+                    in_swap = writer.put_project_update(project)
+                    if not writer.closed:
+                        writer.close()
                     with span("analyze.phase1_commit", stats):
                         writer.wait()  # no-op when enrichment already waited
                     for k, v in writer.timings.items():
                         stats[f"analyze.writer_{k[:-3]}"] = v
-                    project.analysis_completed(clone.commit_hash)
-                    self.repos.projects.update(project)
+                    if not in_swap:
+                        self.repos.projects.update(project)
                     self.cache.put(project.id, project.name, graph)
                 endpoints = self.repos.methods.count_endpoints_by_project_id(project.id)
             METRICS.inc("classes_indexed", classes)
@@ -287,12 +295,14 @@ class Indexer:
     # ---------------------------------------------------------------- phase 1
     def _phase1_static(self, project: Project, parsed: ParsedProject, graph: ProjectGraph,
                        order: Sequence[str], commit_hash: str, writer: Optional[ProjectRowsWriter] = None,
-                       replace: bool = True) -> Tuple[int, Dict[str, List[Tuple[str, str]]], ProjectRowsWriter]:
+                       replace: bool = True,
+                       close: bool = True) -> Tuple[int, Dict[str, List[Tuple[str, str]]], ProjectRowsWriter]:
         """Builds every class / method / parameter row and the graph metadata
         and streams them to a :class:`ProjectRowsWriter` (``writer``, already
         started by the caller, or a new one), which swaps them in with one
         transaction (old rows deleted in it) on its own thread; the caller
-        must ``wait()`` on the returned writer before touching the rows."""
+        must ``wait()`` on the returned writer before touching the rows
+        (and ``close()`` it first when ``close`` is False)."""
         now = to_iso(utc_now())
         pid = project.id
         cls_rows: List[tuple] = []
@@ -308,7 +318,8 @@ class Indexer:
                 n_cls, n_meth, n_par, _, _, _, methods_by_ident, _ = writer.phase1_rows(
                     list(order), units, self.phase1_ids, now, commit_hash, MethodInfo, self.ROW_CHUNK,
                     graph.static_metadata_targets())
-                writer.close()
+                if close:
+                    writer.close()
             except BaseException:
                 writer.abort()
                 raise
@@ -386,7 +397,8 @@ class Indexer:
                     links[ident] = per
             writer.put("params", param_rows)
             graph.load_static_metadata(class_ids, class_types, method_infos, links)
-            writer.close()
+            if close:
+                writer.close()
         except BaseException:
             writer.abort()
             raise

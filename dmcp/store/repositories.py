@@ -112,15 +112,19 @@ class ProjectRepository:
                  to_iso(p.last_analyzed_at), p.last_commit_hash, to_iso(p.created_at),
                  to_iso(p.updated_at), p.description, p.graph_data, p.base_package))
 
+    UPDATE = ("UPDATE projects SET name=?, default_branch=?, status=?, last_analyzed_at=?, "
+              "last_commit_hash=?, updated_at=?, description=?, graph_data=?, base_package=? "
+              "WHERE id=?")
+
+    @staticmethod
+    def update_params(p: Project) -> tuple:
+        return (p.name, p.default_branch, p.status.value, to_iso(p.last_analyzed_at),
+                p.last_commit_hash, to_iso(p.updated_at), p.description, p.graph_data,
+                p.base_package, p.id)
+
     def update(self, p: Project) -> None:
         with self.db.transaction() as c:
-            c.execute(
-                "UPDATE projects SET name=?, default_branch=?, status=?, last_analyzed_at=?, "
-                "last_commit_hash=?, updated_at=?, description=?, graph_data=?, base_package=? "
-                "WHERE id=?",
-                (p.name, p.default_branch, p.status.value, to_iso(p.last_analyzed_at),
-                 p.last_commit_hash, to_iso(p.updated_at), p.description, p.graph_data,
-                 p.base_package, p.id))
+            c.execute(self.UPDATE, self.update_params(p))
 
     def update_status(self, p: Project) -> None:
         """Status-only update that does not rewrite the graph column."""
@@ -710,6 +714,19 @@ class ProjectRowsWriter:
                                        r.methods._INSERT, r.params._INSERT, method_info_cls, chunk, graph_targets)
         self._keep.append(out[-1])  # ids generated natively
         return out[:-1]
+
+    def put_project_update(self, project: Project) -> bool:
+        """Queues ``project``'s row update (status, graph, commit hash) into the
+        swap's transaction, so rows and project commit together (one commit
+        instead of two, and no window where the new rows are visible under the
+        old status).  True when queued; False when this writer cannot (Python
+        writer, ``:memory:``): update the project after :meth:`wait` then."""
+        if self._native is None or self.closed:
+            return False
+        frozen = (ProjectRepository.update_params(project),)
+        self._keep.append(frozen)
+        self._native.put(ProjectRepository.UPDATE, frozen)
+        return True
 
     def close(self) -> None:
         """No more rows: the writer commits once everything queued is in."""

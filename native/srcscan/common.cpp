@@ -354,7 +354,8 @@ namespace {
 constexpr std::string_view kVfsPrefix = "/__vfs__/";
 
 struct VirtualTree {
-    std::unordered_map<std::string, std::string> files;  // rel path -> content
+    std::vector<std::string> owned;                            // contents copied in (vfs_mount)
+    std::unordered_map<std::string, std::string_view> files;  // rel path -> content
     std::unordered_map<std::string, std::vector<std::pair<std::string, bool>>> dirs;  // rel dir -> children
 };
 
@@ -376,29 +377,38 @@ std::shared_ptr<const VirtualTree> vfs_resolve(const std::string& path, std::str
 
 }  // namespace
 
-std::string vfs_mount(std::vector<std::pair<std::string, std::string>>&& files) {
-    auto tree = std::make_shared<VirtualTree>();
+namespace {
+
+std::string mount_tree(std::shared_ptr<VirtualTree> tree, const std::vector<std::pair<std::string, std::string_view>>& files) {
     std::unordered_map<std::string, std::unordered_map<std::string, bool>> kids;  // dir -> name -> is_dir
     kids[""];
     tree->files.reserve(files.size());
+    // consecutive files mostly share their directory (tree order): its
+    // ancestors are registered once per run of siblings
+    std::string last_dir = "\x01";
+    std::unordered_map<std::string, bool>* siblings = nullptr;
     for (auto& kv : files) {
-        std::string rel = kv.first;
-        while (!rel.empty() && rel.front() == '/') rel.erase(0, 1);
+        std::string_view rel = kv.first;
+        while (!rel.empty() && rel.front() == '/') rel.remove_prefix(1);
         if (rel.empty()) continue;
-        // register every ancestor directory
-        size_t pos = 0;
-        std::string parent;
-        while (true) {
-            size_t s = rel.find('/', pos);
-            bool is_dir = s != std::string::npos;
-            std::string name = rel.substr(pos, is_dir ? s - pos : std::string::npos);
-            kids[parent].emplace(name, is_dir);
-            if (!is_dir) break;
-            parent = parent.empty() ? name : parent + "/" + name;
-            kids[parent];
-            pos = s + 1;
+        const size_t slash = rel.rfind('/');
+        const std::string_view dir = slash == std::string_view::npos ? std::string_view() : rel.substr(0, slash);
+        if (!siblings || dir != last_dir) {
+            std::string parent;
+            size_t pos = 0;
+            while (pos < dir.size()) {
+                size_t s2 = dir.find('/', pos);
+                if (s2 == std::string_view::npos) s2 = dir.size();
+                std::string name(dir.substr(pos, s2 - pos));
+                kids[parent].emplace(name, true);
+                parent = parent.empty() ? name : parent + "/" + name;
+                pos = s2 + 1;
+            }
+            last_dir.assign(dir);
+            siblings = &kids[last_dir];  // node-based map: stays valid across inserts
         }
-        tree->files[rel] = std::move(kv.second);
+        siblings->emplace(std::string(rel.substr(slash == std::string_view::npos ? 0 : slash + 1)), false);
+        tree->files[std::string(rel)] = kv.second;
     }
     for (auto& d : kids) {
         auto& v = tree->dirs[d.first];
@@ -411,6 +421,24 @@ std::string vfs_mount(std::vector<std::pair<std::string, std::string>>&& files) 
     std::string root = std::string(kVfsPrefix) + std::to_string(++g_vfs_next);
     g_vfs[root] = std::move(tree);
     return root;
+}
+
+}  // namespace
+
+std::string vfs_mount(std::vector<std::pair<std::string, std::string>>&& files) {
+    auto tree = std::make_shared<VirtualTree>();
+    tree->owned.reserve(files.size());
+    std::vector<std::pair<std::string, std::string_view>> views;
+    views.reserve(files.size());
+    for (auto& kv : files) {
+        tree->owned.push_back(std::move(kv.second));
+        views.emplace_back(std::move(kv.first), tree->owned.back());
+    }
+    return mount_tree(std::move(tree), views);
+}
+
+std::string vfs_mount_views(const std::vector<std::pair<std::string, std::string_view>>& files) {
+    return mount_tree(std::make_shared<VirtualTree>(), files);
 }
 
 void vfs_unmount(const std::string& root) {
@@ -449,7 +477,7 @@ bool read_file(const std::string& path, std::string& out, size_t max_bytes) {
     if (auto t = vfs_resolve(path, rel)) {
         auto it = t->files.find(rel);
         if (it == t->files.end() || (max_bytes && it->second.size() > max_bytes)) return false;
-        out = it->second;
+        out.assign(it->second.data(), it->second.size());
         return true;
     }
     FILE* f = std::fopen(path.c_str(), "rb");

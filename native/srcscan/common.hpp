@@ -130,6 +130,8 @@ bool dir_exists(const std::string& path);
 bool list_dir(const std::string& dir, std::vector<std::pair<std::string, bool>>& out);
 // Mounts files given as (relative path, content); returns the virtual root.
 std::string vfs_mount(std::vector<std::pair<std::string, std::string>>&& files);
+// The same without copying: the contents must outlive vfs_unmount().
+std::string vfs_mount_views(const std::vector<std::pair<std::string, std::string_view>>& files);
 void vfs_unmount(const std::string& root);
 std::string join_path(const std::string& a, const std::string& b);
 std::string normalize_path(const std::string& p);  // resolves . and .. lexically

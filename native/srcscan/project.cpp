@@ -65,6 +65,10 @@ void walk(const std::string& abs, const std::string& rel, Keep keep, SkipDir ski
     }
 }
 
+long long us_since(std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t).count();
+}
+
 std::string strip_ext(const std::string& rel, const std::string& ext) {
     return ends_with(rel, ext) ? rel.substr(0, rel.size() - ext.size()) : rel;
 }
@@ -103,13 +107,17 @@ void write_file(JsonWriter& w, const FileRec& f) {
 }
 
 // ------------------------------------------------------------------- Java
-void scan_java(const std::string& root, const ScanOptions& opt, std::vector<FileRec>& files, int& skipped) {
+void scan_java(const std::string& root, const ScanOptions& opt, ScanResult& res) {
+    std::vector<FileRec>& files = res.files;
     const std::string src_root = "src/main/java";
     std::string abs_src = join_path(root, src_root);
     if (!dir_exists(abs_src)) return;
     std::vector<std::string> rels;
+    auto t = std::chrono::steady_clock::now();
     walk(abs_src, "", [](const std::string& n) { return ends_with(n, ".java"); },
          [](const std::string&) { return false; }, rels);
+    res.walk_us = us_since(t);
+    t = std::chrono::steady_clock::now();
     files.resize(rels.size());
     std::vector<std::string> sources(rels.size());
     parallel_for(rels.size(), opt.threads, [&](size_t k) {
@@ -121,7 +129,9 @@ void scan_java(const std::string& root, const ScanOptions& opt, std::vector<File
         if (!read_file(f.abs_path, src)) return;
         analyze_java(src, f);
     });
-    for (auto& f : files) if (!f.parsed) ++skipped;
+    for (auto& f : files) if (!f.parsed) ++res.skipped;
+    res.analyze_us = us_since(t);
+    t = std::chrono::steady_clock::now();
     // resolution pass
     std::unordered_set<std::string> known;
     known.reserve(files.size() * 2);
@@ -163,6 +173,7 @@ void scan_java(const std::string& root, const ScanOptions& opt, std::vector<File
             if (!replaced) f.params.emplace_back(m.name, matched);
         }
     });
+    res.resolve_us = us_since(t);
 }
 
 // ------------------------------------------------------------- TypeScript
@@ -283,7 +294,7 @@ ScanResult scan_project(const std::string& root, const ScanOptions& opt) {
     } else {
         lang = "java";
         r.source_root = "src/main/java";
-        scan_java(root, opt, r.files, r.skipped);
+        scan_java(root, opt, r);
     }
     r.language = lang;
     r.elapsed_us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
@@ -315,6 +326,13 @@ std::string scan_result_json(const ScanResult& r) {
     w.kv_int("analyzed", (long long)r.files.size());
     w.kv_int("skipped", r.skipped);
     w.kv_int("elapsedUs", r.elapsed_us);
+    w.key("phaseUs");
+    w.begin_obj();
+    w.kv_int("mount", r.mount_us);
+    w.kv_int("walk", r.walk_us);
+    w.kv_int("analyze", r.analyze_us);
+    w.kv_int("resolve", r.resolve_us);
+    w.end_obj();
     w.end_obj();
     w.key("files");
     w.begin_arr();

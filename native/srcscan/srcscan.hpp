@@ -86,6 +86,9 @@ struct ScanResult {
     std::vector<FileRec> files;
     int skipped = 0;
     long long elapsed_us = 0;
+    // wall time of the scan's phases (file discovery, per-file analysis,
+    // cross-file resolution); mount_us is set by callers that mount a tree
+    long long walk_us = 0, analyze_us = 0, resolve_us = 0, mount_us = 0;
 };
 
 // Scans a project root (a directory or a mounted in-memory tree).

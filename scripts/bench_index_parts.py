@@ -60,7 +60,12 @@ def main() -> int:
         rows.append(("scan_json", th, lambda th=th: N.scan_sources(items, "java", th, "")))
     for name, th, fn in rows:
         fn()
-        print(json.dumps({"stage": name, "threads": th, "ms": med(fn, a.reps)}), flush=True)
+        rec = {"stage": name, "threads": th, "ms": med(fn, a.reps)}
+        if name == "scan_objects":
+            st = fn()["stats"]
+            rec["phase_ms"] = {k: v / 1e3 for k, v in st.get("phaseUs", {}).items()}
+            rec["native_ms"] = st["elapsedUs"] / 1e3
+        print(json.dumps(rec), flush=True)
     return 0
 
 

@@ -1,6 +1,9 @@
 #include "common.hpp"
 
+#include <unistd.h>
+
 #include <algorithm>
+#include <condition_variable>
 #include <cstdio>
 #include <dirent.h>
 #include <memory>
@@ -323,6 +326,91 @@ bool parse_json(std::string_view text, JsonValue& out) {
 }
 
 // ------------------------------------------------------------- threading
+namespace {
+
+// Persistent workers for parallel_for: an analysis runs three or four
+// parallel phases of ~1 ms (blob inflation, per-file analysis, resolution)
+// and spawning 16 threads per phase cost about as much as the resolution
+// itself.  One job at a time (a concurrent caller falls back to its own
+// threads); the caller works too.  A forked child (multiprocessing) starts a
+// fresh pool: the parent's threads do not exist there.
+class WorkerPool {
+public:
+    static WorkerPool& get() {
+        static std::mutex mu;
+        static WorkerPool* pool = nullptr;
+        std::lock_guard<std::mutex> lk(mu);
+        if (pool == nullptr || pool->pid_ != ::getpid()) pool = new WorkerPool();  // a stale one is leaked, never touched
+        return *pool;
+    }
+
+    // fn(i) for i < n on `want` threads (caller included); false when busy
+    bool run(size_t n, int want, const std::function<void(size_t)>& fn) {
+        std::unique_lock<std::mutex> job(busy_, std::try_to_lock);
+        if (!job.owns_lock()) return false;
+        const int helpers = want - 1;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            while ((int)threads_.size() < helpers) {
+                const int idx = (int)threads_.size();
+                threads_.emplace_back([this, idx] { worker(idx); });
+                threads_.back().detach();
+            }
+            fn_ = &fn;
+            n_ = n;
+            next_.store(0, std::memory_order_relaxed);
+            active_ = helpers;
+            remaining_ = helpers;
+            ++gen_;
+        }
+        cv_.notify_all();
+        drain();
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [this] { return remaining_ == 0; });
+        fn_ = nullptr;
+        return true;
+    }
+
+private:
+    WorkerPool() : pid_(::getpid()) {}
+
+    void drain() {
+        for (;;) {
+            const size_t i = next_.fetch_add(1, std::memory_order_relaxed);
+            if (i >= n_) break;
+            (*fn_)(i);
+        }
+    }
+
+    void worker(int idx) {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (idx >= active_) continue;  // not needed for this job
+            }
+            drain();
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--remaining_ == 0) done_.notify_one();
+        }
+    }
+
+    const pid_t pid_;
+    std::mutex busy_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    std::vector<std::thread> threads_;
+    uint64_t gen_ = 0;
+    const std::function<void(size_t)>* fn_ = nullptr;
+    size_t n_ = 0;
+    int active_ = 0, remaining_ = 0;
+    std::atomic<size_t> next_{0};
+};
+
+}  // namespace
+
 void parallel_for(size_t n, int threads, const std::function<void(size_t)>& fn) {
     if (n == 0) return;
     int hw = (int)std::thread::hardware_concurrency();
@@ -333,6 +421,7 @@ void parallel_for(size_t n, int threads, const std::function<void(size_t)>& fn) 
         for (size_t i = 0; i < n; ++i) fn(i);
         return;
     }
+    if (t <= 64 && WorkerPool::get().run(n, t, fn)) return;
     std::atomic<size_t> next{0};
     std::vector<std::thread> pool;
     pool.reserve(t);

@@ -256,3 +256,34 @@ def test_native_ref_and_tree_match_git(tmp_path):
         S.mostly_loose = orig
     snap = g.snapshot(RepositoryUrl.of(str(src)), "dev")  # git path after the fallback
     assert "a/New.java" in snap.files
+
+
+def _scan_in_child(q):
+    from dmcp.parsers.base import native as _native
+    files = [(f"src/main/java/a/A{i}.java", f"package a;\npublic class A{i} {{}}".encode()) for i in range(64)]
+    q.put(len(json.loads(_native().scan_sources(files, "java", 8, ""))["files"]))
+
+
+def test_worker_pool_survives_fork():
+    """parallel_for's persistent workers: a forked child (multiprocessing)
+    scans with a fresh pool instead of waiting on the parent's threads, and
+    concurrent scans from several Python threads all complete."""
+    import multiprocessing as mp
+    import threading
+    n = native()
+    files = [(f"src/main/java/a/A{i}.java", f"package a;\npublic class A{i} {{}}".encode()) for i in range(64)]
+    assert len(json.loads(n.scan_sources(files, "java", 8, ""))["files"]) == 64  # pool started here
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    p = ctx.Process(target=_scan_in_child, args=(q,))
+    p.start()
+    p.join(60)
+    assert p.exitcode == 0 and q.get(timeout=5) == 64
+    out = []
+    ts = [threading.Thread(target=lambda: out.append(len(json.loads(n.scan_sources(files, "java", 8, ""))["files"])))
+          for _ in range(6)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    assert out == [64] * 6

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <dirent.h>
 #include <memory>
 #include <mutex>
@@ -421,7 +422,11 @@ void parallel_for(size_t n, int threads, const std::function<void(size_t)>& fn) 
         for (size_t i = 0; i < n; ++i) fn(i);
         return;
     }
-    if (t <= 64 && WorkerPool::get().run(n, t, fn)) return;
+    static const bool use_pool = [] {
+        const char* e = std::getenv("DMCP_NATIVE_POOL");  // "0": spawn threads per call (A/B)
+        return !(e && e[0] == '0');
+    }();
+    if (use_pool && t <= 64 && WorkerPool::get().run(n, t, fn)) return;
     std::atomic<size_t> next{0};
     std::vector<std::thread> pool;
     pool.reserve(t);

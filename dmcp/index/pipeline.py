@@ -184,7 +184,8 @@ class Indexer:
         clone: Optional[SourceTree] = None
         writer: Optional[ProjectRowsWriter] = None
         try:
-            project = self._prepare_project(url, branch_name)
+            with span("analyze.prepare", stats):
+                project = self._prepare_project(url, branch_name)
         except BaseException:
             lock.release()  # a failed status write must not leave the repository locked
             raise
@@ -254,8 +255,9 @@ class Indexer:
             self._mark_error(project)
             raise DomainError(f"Analysis failed: {e}", "ANALYSIS_FAILED", e) from e
         finally:
-            if clone is not None:
-                clone.cleanup()
+            with span("analyze.cleanup", stats):
+                if clone is not None:
+                    clone.cleanup()
             lock.release()
 
     def _fetch(self, url: RepositoryUrl, branch: Optional[str], shallow: bool) -> SourceTree:
@@ -270,7 +272,9 @@ class Indexer:
         return self.analyze_project(os.path.abspath(path), branch=None, fix_missed=fix_missed)
 
     def _prepare_project(self, url: RepositoryUrl, branch: str) -> Project:
-        project = self.repos.projects.find_by_repository_url(url)
+        # the old graph is never read: a successful analysis replaces it, a
+        # failed one only writes the status
+        project = self.repos.projects.find_by_repository_url(url, with_graph=False)
         if project is None:
             project = Project.create(url.repository_name(), url, branch)
             self.repos.projects.save(project)

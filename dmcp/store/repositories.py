@@ -138,9 +138,13 @@ class ProjectRepository:
         row = self.db.query_one(self.FIND_BY_ID, (project_id,))
         return self._map(row) if row else None
 
-    def find_by_repository_url(self, url) -> Optional[Project]:
+    def find_by_repository_url(self, url, with_graph: bool = True) -> Optional[Project]:
+        """``with_graph=False``: graph_data is not read (None) -- for callers
+        that replace it anyway (a re-analysis), the JSON is megabytes."""
         value = url.value if isinstance(url, RepositoryUrl) else str(url)
-        row = self.db.query_one(self.FIND_BY_REPOSITORY_URL, (value,))
+        q = (self.FIND_BY_REPOSITORY_URL if with_graph
+             else f"SELECT {self._LIGHT_COLUMNS} FROM projects WHERE repository_url = ?")
+        row = self.db.query_one(q, (value,))
         return self._map(row) if row else None
 
     def find_by_name(self, name: str) -> Optional[Project]:

@@ -21,13 +21,18 @@ MI355X mapping:
   at 64-128 rows the register-direct fused GEMM re-reads every X row per
   weight tile and is bound by per-CU L1 ingest, 1.5-3x slower than
   hipBLASLt's LDS-tiled kernels (profiles/fused_gemm_vs_hipblaslt_r2.jsonl);
-* decode attention, masked greedy sampling and the embedding gather are
-  hand-written gfx950 kernels on every path;
-* prefill attention uses PyTorch SDPA (flash path on ROCm) -- prompts are
-  processed once per class, the decode loop dominates;
+* decode attention (per-row split-K kernel + the shared-prefix kernel,
+  merged by log-sum-exp), masked greedy sampling and the embedding gather
+  are hand-written gfx950 kernels on every path;
+* prefill / extend attention runs on the MFMA flash kernel
+  (``csrc/prefill_attn.hip``): the shared prompt prefix is read in place
+  from its cache slot (a fork costs no copy), causal masking of the own
+  keys; PyTorch SDPA only where the kernel's head shapes do not apply
+  (``DMCP_PREFILL_KERNEL=0`` forces it);
 * the KV cache is one preallocated slab ``[layers, slots, Hkv, max_seq, D]``
-  (288 GB of HBM per GPU: no paging needed at these sizes) so decode reads
-  every key row of a (slot, kv-head) contiguously;
+  in bf16 or FP8 e4m3 (``LMConfig.kv_dtype``; 288 GB of HBM per GPU: no
+  paging needed at these sizes) so decode reads every key row of a
+  (slot, kv-head) contiguously;
 * the batched decode step is captured into hipGraphs per batch-size bucket
   (:class:`DecodeGraphs`), removing ~10 launches/layer of host overhead.
 

@@ -166,6 +166,8 @@ class Indexer:
         self.require_enrichment = require_enrichment
         self.max_source_chars = max_source_chars
         self._locks = _ProjectLocks()
+        self._io_pool = None  # snapshot reads that overlap the project-row preparation
+        self._io_guard = threading.Lock()
 
     # ================================================================ analyze
     def analyze_project(self, repository_url: str, branch: Optional[str] = None,
@@ -183,10 +185,14 @@ class Indexer:
         stats: Dict[str, float] = {}
         clone: Optional[SourceTree] = None
         writer: Optional[ProjectRowsWriter] = None
+        # the snapshot is read (natively, mostly without the GIL) on a helper
+        # thread while the project row is looked up and marked ANALYZING
+        fetch = self._submit_io(self._timed_fetch, url, branch_name)
         try:
             with span("analyze.prepare", stats):
                 project = self._prepare_project(url, branch_name)
         except BaseException:
+            self._discard_fetch(fetch)
             lock.release()  # a failed status write must not leave the repository locked
             raise
         try:
@@ -194,9 +200,13 @@ class Indexer:
                 # the row swap's transaction opens now: the old rows are
                 # deleted on the writer thread while the snapshot is read and
                 # parsed (rolled back if either fails)
-                writer = self.repos.project_rows_writer(project.id, True)
-                with span("analyze.clone", stats):
-                    clone = self._fetch(url, branch_name, shallow=True)
+                try:
+                    writer = self.repos.project_rows_writer(project.id, True)
+                except BaseException:
+                    self._discard_fetch(fetch)
+                    raise
+                with span("analyze.clone", stats):  # what is left of the read after the above
+                    clone, stats["analyze.fetch"] = fetch.result()
                 readme = clone.readme(self.max_readme_length)
                 if readme is not None:
                     project.update_description(readme[:self.description_length])
@@ -259,6 +269,28 @@ class Indexer:
                 if clone is not None:
                     clone.cleanup()
             lock.release()
+
+    def _submit_io(self, fn, *args):
+        with self._io_guard:
+            if self._io_pool is None:
+                from concurrent.futures import ThreadPoolExecutor
+                self._io_pool = ThreadPoolExecutor(max_workers=4, thread_name_prefix="dmcp-fetch")
+            return self._io_pool.submit(fn, *args)
+
+    def _timed_fetch(self, url: RepositoryUrl, branch: Optional[str]) -> Tuple[SourceTree, float]:
+        t0 = time.perf_counter()
+        tree = self._fetch(url, branch, shallow=True)
+        return tree, (time.perf_counter() - t0) * 1e3
+
+    @staticmethod
+    def _discard_fetch(fut) -> None:
+        """An analysis that fails before it takes the snapshot: wait for the
+        read and drop its tree (nothing else owns it)."""
+        try:
+            tree, _ = fut.result()
+        except BaseException:
+            return
+        tree.cleanup()
 
     def _fetch(self, url: RepositoryUrl, branch: Optional[str], shallow: bool) -> SourceTree:
         """The branch head: in memory from git objects (default) or checked out."""

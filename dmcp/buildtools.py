@@ -25,8 +25,8 @@ NATIVE = os.path.join(ROOT, "native", "srcscan")
 BUILD = os.path.join(ROOT, "build", "native")
 BIN = os.path.join(ROOT, "bin")
 
-CORE_SOURCES = ["common.cpp", "java_frontend.cpp", "ts_frontend.cpp", "go_frontend.cpp", "project.cpp"]
-MODULE_SOURCES = ["bulkwriter.cpp", "gitobj.cpp"]
+CORE_SOURCES = ["common.cpp", "java_frontend.cpp", "ts_frontend.cpp", "go_frontend.cpp", "project.cpp", "gitobj.cpp"]
+MODULE_SOURCES = ["bulkwriter.cpp"]
 CXX = os.environ.get("CXX", "g++")
 CXXFLAGS = ["-std=c++17", "-O3", "-fPIC", "-Wall", "-Wno-unused-function", "-pthread"]
 
@@ -85,9 +85,9 @@ def build_srcscan(force: bool = False, sanitize: bool = False, jobs: int = 0) ->
     inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", f"-I{NATIVE}"]
     py_obj = os.path.join(BUILD, f"pymodule.{_digest([os.path.join(NATIVE, 'pymodule.cpp')])}.o")
     _run([CXX, *CXXFLAGS, *inc, "-fvisibility=hidden", "-c", os.path.join(NATIVE, "pymodule.cpp"), "-o", py_obj])
-    # module-only sources (the CLI neither writes the database nor reads git
-    # objects): the bulk row writer links the system libsqlite3 runtime (the
-    # library Python's sqlite3 uses), the loose-object reader links zlib
+    # module-only sources (the CLI does not write the database): the bulk row
+    # writer links the system libsqlite3 runtime (the library Python's sqlite3
+    # uses); the loose-object reader (core: the VFS inflates lazily) links zlib
     mod_objs = []
     for src in MODULE_SOURCES:
         obj = os.path.join(BUILD, src[:-4] + ".o")
@@ -97,12 +97,12 @@ def build_srcscan(force: bool = False, sanitize: bool = False, jobs: int = 0) ->
     _run([CXX, "-shared", "-pthread", "-o", tmp, py_obj, *mod_objs, *objs, "-l:libsqlite3.so.0", "-lz"])
     os.replace(tmp, target)
     os.makedirs(BIN, exist_ok=True)
-    _run([CXX, *CXXFLAGS, "-o", cli, os.path.join(NATIVE, "cli.cpp"), *objs])
+    _run([CXX, *CXXFLAGS, "-o", cli, os.path.join(NATIVE, "cli.cpp"), *objs, "-lz"])
     if sanitize:
         san = ["-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-pthread",
                "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
         sobjs = _compile_objects(san, "asan", jobs)
-        _run([CXX, *san, "-o", os.path.join(BIN, "srcscan-asan"), os.path.join(NATIVE, "cli.cpp"), *sobjs])
+        _run([CXX, *san, "-o", os.path.join(BIN, "srcscan-asan"), os.path.join(NATIVE, "cli.cpp"), *sobjs, "-lz"])
     with open(stamp, "w") as f:
         f.write(key)
     return target

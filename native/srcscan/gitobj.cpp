@@ -188,6 +188,10 @@ bool walk_tree(const std::vector<std::string>& object_dirs, const std::string& t
 
 }  // namespace
 
+bool read_loose_blob(const std::vector<std::string>& object_dirs, const std::string& sha, std::string& out) {
+    return read_loose(object_dirs, sha, out, "blob");
+}
+
 bool resolve_commit(const std::string& git_dir, const std::vector<std::string>& refs, std::string& commit) {
     std::vector<std::string> object_dirs{git_dir + "/objects"};
     std::string alt;

@@ -19,6 +19,9 @@ struct LooseResult {
 LooseResult read_loose_blobs(const std::vector<std::string>& object_dirs, const std::vector<std::string>& shas,
                              int threads, uint64_t max_bytes);
 
+// One loose blob's content; false when it is not a loose blob in any dir.
+bool read_loose_blob(const std::vector<std::string>& object_dirs, const std::string& sha, std::string& out);
+
 // The commit the first resolvable ref of `refs` ("HEAD", "refs/heads/x",
 // "refs/tags/x") names, annotated tags peeled.  false when git must answer
 // (ref storage or objects not readable here, or the ref is not a commit).

@@ -41,7 +41,8 @@ class GitClient:
         self.timeout = timeout_seconds
         self.read_local_in_place = True  # snapshot(): local repositories without a private clone
         self.native_objects = True  # snapshot(): ref + tree read from loose objects natively when possible
-        self.lazy_blobs = True  # ... and the blobs inflated by the scan itself (LooseTree)
+        # ... and the blobs inflated by the scan itself (LooseTree); DMCP_LAZY_BLOBS=0 for A/B
+        self.lazy_blobs = os.environ.get("DMCP_LAZY_BLOBS", "1") != "0"
 
     def _env(self) -> dict:
         env = dict(os.environ)

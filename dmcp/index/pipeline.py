@@ -146,6 +146,8 @@ class Indexer:
     ROW_CHUNK = 256  # classes (with their methods) per writer put in Phase 1
     native_phase1 = True  # Phase 1 rows built by the native writer when it can (else the Python loop)
     phase1_ids: Optional[List[str]] = None  # row ids for the native Phase 1 (None = fresh UUIDv7s; tests)
+    # the snapshot read overlaps the project-row preparation (DMCP_OVERLAP_FETCH=0 for A/B)
+    overlap_fetch = os.environ.get("DMCP_OVERLAP_FETCH", "1") != "0"
 
     def __init__(self, repos: Repositories, cache: GraphCache, git: GitClient,
                  backend: Optional[EnrichmentBackend] = None, *, batch_size: int = 20,
@@ -187,7 +189,16 @@ class Indexer:
         writer: Optional[ProjectRowsWriter] = None
         # the snapshot is read (natively, mostly without the GIL) on a helper
         # thread while the project row is looked up and marked ANALYZING
-        fetch = self._submit_io(self._timed_fetch, url, branch_name)
+        if self.overlap_fetch:
+            fetch = self._submit_io(self._timed_fetch, url, branch_name)
+        else:
+            from concurrent.futures import Future
+            fetch = Future()
+            fetch.set_running_or_notify_cancel()
+            try:
+                fetch.set_result(self._timed_fetch(url, branch_name))
+            except Exception as e:
+                fetch.set_exception(e)
         try:
             with span("analyze.prepare", stats):
                 project = self._prepare_project(url, branch_name)

@@ -41,8 +41,9 @@ class GitClient:
         self.timeout = timeout_seconds
         self.read_local_in_place = True  # snapshot(): local repositories without a private clone
         self.native_objects = True  # snapshot(): ref + tree read from loose objects natively when possible
-        # ... and the blobs inflated by the scan itself (LooseTree); DMCP_LAZY_BLOBS=0 for A/B
-        self.lazy_blobs = os.environ.get("DMCP_LAZY_BLOBS", "1") != "0"
+        # ... and the blobs inflated by the scan itself (LooseTree, DMCP_LAZY_BLOBS=1): measured even with
+        # the two-pass read (profiles/bench_r2_lazy_ab.txt), so off by default
+        self.lazy_blobs = os.environ.get("DMCP_LAZY_BLOBS", "0") == "1"
 
     def _env(self) -> dict:
         env = dict(os.environ)

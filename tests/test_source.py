@@ -311,6 +311,7 @@ def test_loose_tree_fused_scan_equals_two_pass(tmp_path, kind):
     {"java": lambda: synth.java_spring_repo(str(repo), 30), "nest": lambda: synth.nestjs_repo(str(repo), 4),
      "go": lambda: synth.go_gin_repo(str(repo), 3)}[kind]()
     g = GitClient(str(tmp_path / "c"))
+    g.lazy_blobs = True
     url = RepositoryUrl.of(str(repo))
     lazy = g.snapshot(url, "main")
     assert isinstance(lazy, LooseTree)

@@ -148,6 +148,8 @@ class Indexer:
     phase1_ids: Optional[List[str]] = None  # row ids for the native Phase 1 (None = fresh UUIDv7s; tests)
     # the snapshot read overlaps the project-row preparation (DMCP_OVERLAP_FETCH=0 for A/B)
     overlap_fetch = os.environ.get("DMCP_OVERLAP_FETCH", "1") != "0"
+    # the native scan writes the class / method rows itself (DMCP_SCAN_ROWS=0 for A/B)
+    scan_rows = os.environ.get("DMCP_SCAN_ROWS", "1") != "0"
 
     def __init__(self, repos: Repositories, cache: GraphCache, git: GitClient,
                  backend: Optional[EnrichmentBackend] = None, *, batch_size: int = 20,
@@ -222,15 +224,20 @@ class Indexer:
                 if readme is not None:
                     project.update_description(readme[:self.description_length])
                 parser = parser_for(clone.detect_language(), self.parser_threads)
+                now = to_iso(utc_now())
+                # the native scan hands the class / method rows to the writer
+                # as soon as it has them (fresh UUIDv7s; not with given test ids)
+                rows = (writer.static_rows(now, clone.commit_hash)
+                        if self.scan_rows and self.native_phase1 and self.phase1_ids is None else None)
                 with span("analyze.parse", stats):
-                    parsed = parser.scan_tree(clone)
+                    parsed = parser.scan_tree(clone, rows=rows)
                     graph = parsed.build_graph()
                 LOG.info("Graph built: %d nodes, %d entry points", graph.node_count(), graph.entry_point_count())
                 order = graph.analysis_order()
                 with span("analyze.phase1", stats):
                     # without enrichment the swap stays open for the project row
                     p1 = self._phase1_static(project, parsed, graph, order, clone.commit_hash, writer,
-                                             close=self.backend.enabled)
+                                             close=self.backend.enabled, now=now)
                 classes, methods_by_ident, writer = p1
                 enriched = failed = recovered = 0
                 if self.backend.enabled:
@@ -342,15 +349,15 @@ class Indexer:
     # ---------------------------------------------------------------- phase 1
     def _phase1_static(self, project: Project, parsed: ParsedProject, graph: ProjectGraph,
                        order: Sequence[str], commit_hash: str, writer: Optional[ProjectRowsWriter] = None,
-                       replace: bool = True,
-                       close: bool = True) -> Tuple[int, Dict[str, List[Tuple[str, str]]], ProjectRowsWriter]:
+                       replace: bool = True, close: bool = True,
+                       now: Optional[str] = None) -> Tuple[int, Dict[str, List[Tuple[str, str]]], ProjectRowsWriter]:
         """Builds every class / method / parameter row and the graph metadata
         and streams them to a :class:`ProjectRowsWriter` (``writer``, already
         started by the caller, or a new one), which swaps them in with one
         transaction (old rows deleted in it) on its own thread; the caller
         must ``wait()`` on the returned writer before touching the rows
         (and ``close()`` it first when ``close`` is False)."""
-        now = to_iso(utc_now())
+        now = now or to_iso(utc_now())
         pid = project.id
         cls_rows: List[tuple] = []
         meth_rows: List[tuple] = []
@@ -364,7 +371,7 @@ class Indexer:
             try:
                 n_cls, n_meth, n_par, _, _, _, methods_by_ident, _ = writer.phase1_rows(
                     list(order), units, self.phase1_ids, now, commit_hash, MethodInfo, self.ROW_CHUNK,
-                    graph.static_metadata_targets())
+                    graph.static_metadata_targets(), pre_ids=parsed.static_row_ids)
                 if close:
                     writer.close()
             except BaseException:
@@ -372,6 +379,8 @@ class Indexer:
                 raise
             LOG.info("Phase 1 rows built natively. Classes: %d, Methods: %d, Parameters: %d", n_cls, n_meth, n_par)
             return n_cls, methods_by_ident, writer
+        if parsed.static_row_ids is not None:  # those rows are already queued on a native writer
+            raise RuntimeError("Phase 1: rows pre-written by the scan need the native Phase 1")
         # an upper bound of the ids needed: one per class and method, one per
         # parameter link of every method (overloads included)
         n_ids = 0

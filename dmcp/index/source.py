@@ -71,9 +71,10 @@ class SourceTree:
         """Raw native scan document (JSON bytes)."""
         raise NotImplementedError
 
-    def scan_objects(self, language: str, threads: int, framework: str = "") -> Optional[dict]:
+    def scan_objects(self, language: str, threads: int, framework: str = "", rows=None) -> Optional[dict]:
         """The scan document as Python objects built natively (no JSON round
-        trip), or None when this tree only offers :meth:`scan`."""
+        trip), or None when this tree only offers :meth:`scan`.  ``rows``: see
+        ``SourceParser.scan_tree`` (trees that cannot write rows ignore it)."""
         return None
 
     def readme(self, max_length: int = 10_000) -> Optional[str]:
@@ -140,12 +141,14 @@ class MemoryTree(SourceTree):
         from ..parsers.base import native
         return native().scan_sources(list(self.files.items()), language, threads, framework)
 
-    def scan_objects(self, language: str, threads: int, framework: str = "") -> Optional[dict]:
+    def scan_objects(self, language: str, threads: int, framework: str = "", rows=None) -> Optional[dict]:
         from ..models.domain import StaticMethodInfo
         from ..parsers.base import native
         fn = getattr(native(), "scan_sources_objects", None)
         if fn is None:
             return None
+        if rows is not None:
+            return fn(list(self.files.items()), language, threads, framework, StaticMethodInfo, rows)
         return fn(list(self.files.items()), language, threads, framework, StaticMethodInfo)
 
 
@@ -252,7 +255,7 @@ class LooseTree(MemoryTree):
             return self._checkout.scan(language, threads, framework)
         return super().scan(language, threads, framework)
 
-    def scan_objects(self, language: str, threads: int, framework: str = "") -> Optional[dict]:
+    def scan_objects(self, language: str, threads: int, framework: str = "", rows=None) -> Optional[dict]:
         if self._checkout is not None:
             return self._checkout.scan_objects(language, threads, framework)
         if self._files is None:

@@ -96,6 +96,9 @@ class ParsedProject:
     file_to_identifier: Dict[str, str]
     stats: dict
     go_analysis: Optional[dict] = None
+    # ident -> (class id, [method ids]) of class / method rows the scan already
+    # handed to the row writer (scan_tree(rows=...)); Phase 1 binds these ids
+    static_row_ids: Optional[dict] = None
 
     def build_graph(self) -> ProjectGraph:
         """The three-pass build (SourceParser.java:163-188) from the scan."""
@@ -217,14 +220,18 @@ class SourceParser:
                  (time.perf_counter() - t0) * 1e3, self.project.stats.get("elapsedUs", 0) / 1e3)
         return self.project
 
-    def scan_tree(self, tree) -> ParsedProject:
+    def scan_tree(self, tree, rows=None) -> ParsedProject:
         """Scans a :class:`dmcp.index.source.SourceTree` (in-memory git snapshot
-        or checkout) -- same result as :meth:`scan` over a checkout of it."""
+        or checkout) -- same result as :meth:`scan` over a checkout of it.
+        ``rows``: :meth:`ProjectRowsWriter.static_rows` -- the native scan then
+        hands the class / method rows to the writer before it builds any
+        Python object (their ids in ``ParsedProject.static_row_ids``)."""
         t0 = time.perf_counter()
-        doc = tree.scan_objects(self.language_name, self.threads, self.framework_override)
+        doc = tree.scan_objects(self.language_name, self.threads, self.framework_override, rows=rows)
         if doc is None:
             doc = json.loads(tree.scan(self.language_name, self.threads, self.framework_override))
         self.project = to_parsed_project(doc)
+        self.project.static_row_ids = doc.get("rowIds")
         self._root = tree.directory
         LOG.info("Scanned %s @ %s: %d files, %d units in %.1f ms", tree.directory, tree.commit_hash[:12],
                  self.project.stats.get("analyzed", 0), len(self.project.units), (time.perf_counter() - t0) * 1e3)

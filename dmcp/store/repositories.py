@@ -702,7 +702,7 @@ class ProjectRowsWriter:
         return self._native is not None and hasattr(self._native, "phase1_rows")
 
     def phase1_rows(self, order, units, ids: Optional[list], now: str, commit_hash: Optional[str], method_info_cls,
-                    chunk: int = 256, graph_targets: Optional[tuple] = None) -> tuple:
+                    chunk: int = 256, graph_targets: Optional[tuple] = None, pre_ids: Optional[dict] = None) -> tuple:
         """Class / method / parameter rows of the parsed ``units`` (in
         ``order``) built natively and streamed to this writer in ``chunk``-class
         batches -- the Python loop of ``Indexer._phase1_static`` without a
@@ -712,12 +712,22 @@ class ProjectRowsWriter:
         graph's metadata is filled in place instead of returned.  Returns
         (n_classes, n_methods, n_params, class_ids, class_types, method_infos,
         methods_by_ident, links)."""
-        self._keep.append((order, units, ids, now, commit_hash))  # the native rows are views into these
+        self._keep.append((order, units, ids, now, commit_hash, pre_ids))  # the native rows are views into these
         r = self.repos
         out = self._native.phase1_rows(order, units, ids, self.project_id, now, commit_hash, r.classes._INSERT,
-                                       r.methods._INSERT, r.params._INSERT, method_info_cls, chunk, graph_targets)
+                                       r.methods._INSERT, r.params._INSERT, method_info_cls, chunk, graph_targets,
+                                       pre_ids)
         self._keep.append(out[-1])  # ids generated natively
         return out[:-1]
+
+    def static_rows(self, now: str, commit_hash: Optional[str]) -> Optional[tuple]:
+        """What ``scan_sources_objects(rows=...)`` needs to write the class /
+        method rows straight from the native scan into this writer (None when
+        the writer is not native)."""
+        if self._native is None or self.closed or not hasattr(self._native, "phase1_rows"):
+            return None
+        r = self.repos
+        return (self._native, self.project_id, now, commit_hash, r.classes._INSERT, r.methods._INSERT)
 
     def put_project_update(self, project: Project) -> bool:
         """Queues ``project``'s row update (status, graph, commit hash) into the

@@ -4,6 +4,7 @@
 #include <pybind11/stl.h>
 #include <sys/random.h>
 
+#include <cctype>
 #include <chrono>
 #include <cstring>
 #include <memory>
@@ -372,9 +373,138 @@ struct Uuid7Gen {
     }
 };
 
+// json.dumps(list_of_str) (default separators, ensure_ascii) of UTF-8 strings
+void json_ascii_list(const std::vector<std::string>& v, std::string& out) {
+    static const char* hex = "0123456789abcdef";
+    auto u4 = [&](unsigned c) {
+        out += "\\u";
+        for (int sh = 12; sh >= 0; sh -= 4) out += hex[(c >> sh) & 15];
+    };
+    out = "[";
+    for (size_t i = 0; i < v.size(); ++i) {
+        if (i) out += ", ";
+        out += '"';
+        const std::string& s = v[i];
+        for (size_t k = 0; k < s.size();) {
+            unsigned char c = (unsigned char)s[k];
+            unsigned cp = c;
+            size_t len = 1;
+            if (c >= 0xF0 && k + 3 < s.size() + 0) { cp = ((c & 7u) << 18) | ((s[k + 1] & 63u) << 12) | ((s[k + 2] & 63u) << 6) | (s[k + 3] & 63u); len = 4; }
+            else if (c >= 0xE0 && k + 2 < s.size()) { cp = ((c & 15u) << 12) | ((s[k + 1] & 63u) << 6) | (s[k + 2] & 63u); len = 3; }
+            else if (c >= 0xC0 && k + 1 < s.size()) { cp = ((c & 31u) << 6) | (s[k + 1] & 63u); len = 2; }
+            k += len;
+            if (cp == '"') out += "\\\"";
+            else if (cp == '\\') out += "\\\\";
+            else if (cp == '\n') out += "\\n";
+            else if (cp == '\r') out += "\\r";
+            else if (cp == '\t') out += "\\t";
+            else if (cp == '\b') out += "\\b";
+            else if (cp == '\f') out += "\\f";
+            else if (cp < 0x20 || (cp >= 0x7f && cp < 0x10000)) u4(cp);
+            else if (cp >= 0x10000) {
+                cp -= 0x10000;
+                u4(0xD800 + (cp >> 10));
+                u4(0xDC00 + (cp & 0x3FF));
+            } else out += (char)cp;
+        }
+        out += '"';
+    }
+    out += "]";
+}
+
+// Class and method rows of a finished scan handed to the bulk writer at once
+// (before any Python object exists), so the inserts start while the caller
+// still builds the graph; Phase 1 then only binds the ids (phase1_rows with
+// pre_ids) and writes the parameter rows.  Java / TypeScript units (a later
+// file with the same identifier replaces the earlier one, as
+// parsers/base.py::_add_unit does); Go merges files per package: not here.
+// Returns ident -> (class id, [method ids]) or None when not applicable.
+struct StaticRowsSpec {
+    dbw::BulkWriter* writer = nullptr;
+    std::string pid, now, commit, cls_sql, meth_sql;
+    bool commit_null = false;
+};
+
+std::string normalize_class_type(const std::string& t) {
+    static const char* kTypes[] = {"CONTROLLER", "SERVICE", "REPOSITORY", "ENTITY", "DTO",
+                                   "CONFIGURATION", "LISTENER", "UTILITY", "EXCEPTION", "OTHER"};
+    std::string up = t;
+    for (auto& c : up) c = (char)std::toupper((unsigned char)c);
+    for (const char* k : kTypes)
+        if (up == k) return up;
+    return "OTHER";  // ClassType.from_string
+}
+
+// emits rows for the winning FileRec of each identifier; ids[k] per file
+// index (empty for replaced files).  GIL not needed.
+void emit_static_rows(const srcscan::ScanResult& r, const StaticRowsSpec& spec,
+                      std::vector<std::pair<std::string, std::vector<std::string>>>& ids) {
+    std::unordered_map<std::string_view, size_t> last;
+    last.reserve(r.files.size() * 2);
+    for (size_t k = 0; k < r.files.size(); ++k) last[r.files[k].identifier] = k;
+    ids.assign(r.files.size(), {});
+    Uuid7Gen gen;
+    char buf[36];
+    const int chunk = 256;
+    RowBuilder cls(spec.cls_sql, 10), meth(spec.meth_sql, 10);
+    int pending = 0;
+    auto flush = [&]() {
+        if (!cls.empty()) spec.writer->put(std::move(cls.b));
+        if (!meth.empty()) spec.writer->put(std::move(meth.b));
+        cls = RowBuilder(spec.cls_sql, 10);
+        meth = RowBuilder(spec.meth_sql, 10);
+        pending = 0;
+    };
+    for (size_t k = 0; k < r.files.size(); ++k) {
+        const srcscan::FileRec& f = r.files[k];
+        if (last[f.identifier] != k) continue;
+        if (pending == chunk) flush();
+        ++pending;
+        gen.next(buf);
+        std::string cid(buf, 36);
+        const std::string& ident = f.identifier;
+        const size_t dot = ident.rfind('.');
+        cls.owned(std::string(cid));
+        cls.owned(std::string(spec.pid));
+        cls.owned(std::string(ident));
+        if (dot != std::string::npos) cls.owned(ident.substr(dot + 1)); else cls.owned(std::string(ident));
+        if (dot != std::string::npos) cls.owned(ident.substr(0, dot)); else cls.null();
+        cls.owned(normalize_class_type(f.class_type));
+        cls.null();
+        cls.owned(std::string(f.rel_path));
+        cls.owned(std::string(spec.now));
+        if (spec.commit_null) cls.null(); else cls.owned(std::string(spec.commit));
+        std::vector<std::string> mids;
+        mids.reserve(f.methods.size());
+        for (const srcscan::MethodRec& m : f.methods) {
+            gen.next(buf);
+            mids.emplace_back(buf, 36);
+            meth.owned(std::string(mids.back()));
+            meth.owned(std::string(cid));
+            meth.owned(std::string(m.name));
+            meth.null();
+            meth.owned("[]");
+            if (m.exceptions.empty()) {
+                meth.owned("[]");
+            } else {
+                std::string js;
+                json_ascii_list(m.exceptions, js);
+                meth.owned(std::move(js));
+            }
+            if (m.has_http_method) meth.owned(std::string(m.http_method)); else meth.null();
+            if (m.has_http_path) meth.owned(std::string(m.http_path)); else meth.null();
+            meth.integer(m.line);
+            meth.owned(std::string(spec.now));
+        }
+        ids[k] = {std::move(cid), std::move(mids)};
+    }
+    flush();
+}
+
 py::tuple phase1_rows(dbw::BulkWriter& writer, py::list order, py::dict units, py::object ids, py::str pid,
                       py::str now, py::handle commit_hash, const std::string& cls_sql, const std::string& meth_sql,
-                      const std::string& param_sql, py::handle method_info_cls, int chunk, py::object graph_targets) {
+                      const std::string& param_sql, py::handle method_info_cls, int chunk, py::object graph_targets,
+                      py::object pre_ids) {
     if (!PyType_Check(method_info_cls.ptr()) ||
         !PyType_IsSubtype((PyTypeObject*)method_info_cls.ptr(), &PyTuple_Type))
         throw py::type_error("method_info_cls must be a tuple subclass");
@@ -383,6 +513,11 @@ py::tuple phase1_rows(dbw::BulkWriter& writer, py::list order, py::dict units, p
     // alive by ``generated``, returned to the caller with the metadata)
     const bool given = !ids.is_none();
     if (given && !PyList_Check(ids.ptr())) throw py::type_error("ids must be a list or None");
+    // pre_ids: ident -> (class id, [method ids]) of rows already written by
+    // scan_sources_objects(rows=...): only the ids are bound here, the
+    // class / method rows are not written again
+    const bool pre = !pre_ids.is_none();
+    if (pre && (given || !PyDict_Check(pre_ids.ptr()))) throw py::type_error("pre_ids must be a dict (and ids None)");
     const Py_ssize_t n_ids = given ? PyList_GET_SIZE(ids.ptr()) : 0;
     Py_ssize_t next_id = 0;
     py::list generated;
@@ -454,7 +589,21 @@ py::tuple phase1_rows(dbw::BulkWriter& writer, py::list order, py::dict units, p
         }
         if (pending == chunk) flush();
         ++pending;
-        PyObject* cid = nid();
+        PyObject* pre_mids = nullptr;
+        PyObject* cid;
+        if (pre) {
+            PyObject* rec = PyDict_GetItemWithError(pre_ids.ptr(), ident);
+            if (!rec) {
+                if (PyErr_Occurred()) throw py::error_already_set();
+                throw py::value_error("phase1_rows: a unit has no pre-written row");
+            }
+            if (!PyTuple_Check(rec) || PyTuple_GET_SIZE(rec) != 2 || !PyList_Check(PyTuple_GET_ITEM(rec, 1)))
+                throw py::type_error("pre_ids values must be (class id, [method ids])");
+            cid = PyTuple_GET_ITEM(rec, 0);
+            pre_mids = PyTuple_GET_ITEM(rec, 1);
+        } else {
+            cid = nid();
+        }
         if (PyDict_SetItem(class_ids.ptr(), ident, cid) < 0) throw py::error_already_set();
         PyObject* ct_enum = getattr_borrowed(unit, "class_type", hold);
         PyObject* ct = getattr_borrowed(ct_enum, "value", hold);
@@ -469,16 +618,18 @@ py::tuple phase1_rows(dbw::BulkWriter& writer, py::list order, py::dict units, p
                 dot = k;
                 break;
             }
-        cls.str(cid);
-        cls.str(pid.ptr());
-        cls.text(is, ilen);
-        if (dot >= 0) cls.text(is + dot + 1, ilen - dot - 1); else cls.text(is, ilen);
-        if (dot >= 0) cls.text(is, dot); else cls.null();
-        cls.str(ct);
-        cls.null();
-        cls.str(src);
-        cls.str(now.ptr());
-        cls.str(commit_hash.ptr());
+        if (!pre) {
+            cls.str(cid);
+            cls.str(pid.ptr());
+            cls.text(is, ilen);
+            if (dot >= 0) cls.text(is + dot + 1, ilen - dot - 1); else cls.text(is, ilen);
+            if (dot >= 0) cls.text(is, dot); else cls.null();
+            cls.str(ct);
+            cls.null();
+            cls.str(src);
+            cls.str(now.ptr());
+            cls.str(commit_hash.ptr());
+        }
         ++n_cls;
         if (direct) {
             PyObject* f = PyTuple_Pack(2, ct, Py_None);
@@ -494,6 +645,7 @@ py::tuple phase1_rows(dbw::BulkWriter& writer, py::list order, py::dict units, p
         if (!mseq) throw py::error_already_set();
         py::object keep_mseq = py::reinterpret_steal<py::object>(mseq);
         const Py_ssize_t nm = PySequence_Fast_GET_SIZE(mseq);
+        if (pre && PyList_GET_SIZE(pre_mids) != nm) throw py::value_error("phase1_rows: method ids do not match");
         py::list infos(nm), mids(nm);
         for (Py_ssize_t k = 0; k < nm; ++k) {
             PyObject* m = PySequence_Fast_GET_ITEM(mseq, k);
@@ -503,26 +655,28 @@ py::tuple phase1_rows(dbw::BulkWriter& writer, py::list order, py::dict units, p
             PyObject* hm = PyTuple_GET_ITEM(m, 2);
             PyObject* hp = PyTuple_GET_ITEM(m, 3);
             PyObject* exc = PyTuple_GET_ITEM(m, 4);
-            PyObject* mid = nid();
-            meth.str(mid);
-            meth.str(cid);
-            meth.str(name);
-            meth.null();
-            meth.text(empty_list.data(), 2);
-            PyObject* eseq = PySequence_Fast(exc, "exceptions must be a sequence");
-            if (!eseq) throw py::error_already_set();
-            py::object keep_e = py::reinterpret_steal<py::object>(eseq);
-            if (PySequence_Fast_GET_SIZE(eseq) == 0) {
+            PyObject* mid = pre ? PyList_GET_ITEM(pre_mids, k) : nid();
+            if (!pre) {
+                meth.str(mid);
+                meth.str(cid);
+                meth.str(name);
+                meth.null();
                 meth.text(empty_list.data(), 2);
-            } else {
-                std::string js;
-                json_str_list_ascii(eseq, js);
-                meth.owned(std::move(js));
+                PyObject* eseq = PySequence_Fast(exc, "exceptions must be a sequence");
+                if (!eseq) throw py::error_already_set();
+                py::object keep_e = py::reinterpret_steal<py::object>(eseq);
+                if (PySequence_Fast_GET_SIZE(eseq) == 0) {
+                    meth.text(empty_list.data(), 2);
+                } else {
+                    std::string js;
+                    json_str_list_ascii(eseq, js);
+                    meth.owned(std::move(js));
+                }
+                meth.str(hm);
+                meth.str(hp);
+                meth.integer_or_null(line);
+                meth.str(now.ptr());
             }
-            meth.str(hm);
-            meth.str(hp);
-            meth.integer_or_null(line);
-            meth.str(now.ptr());
             ++n_meth;
             // MethodInfo(name, None, (), exc, http_method, http_path, line)
             PyObject* args = PyTuple_Pack(7, name, Py_None, none_tuple, exc, hm, hp, line);
@@ -695,19 +849,55 @@ PYBIND11_MODULE(_srcscan, m) {
     m.def(
         "scan_sources_objects",
         [](py::list files, const std::string& language, int threads, const std::string& framework,
-           py::handle method_cls) {
+           py::handle method_cls, py::object rows) {
             auto r = std::make_unique<srcscan::ScanResult>(scan_mounted(files, language, threads, framework));
+            // rows = (BulkWriter, project id, now, commit hash | None, class INSERT, method INSERT):
+            // the class / method rows go to the writer before any object is built
+            std::vector<std::pair<std::string, std::vector<std::string>>> ids;
+            const bool emit = !rows.is_none() && r->language != "go";
+            long long emit_us = 0;
+            if (emit) {
+                py::tuple rt = rows.cast<py::tuple>();
+                if (rt.size() != 6) throw py::value_error("rows must have 6 items");
+                StaticRowsSpec spec;
+                spec.writer = &rt[0].cast<dbw::BulkWriter&>();
+                spec.pid = rt[1].cast<std::string>();
+                spec.now = rt[2].cast<std::string>();
+                spec.commit_null = rt[3].is_none();
+                if (!spec.commit_null) spec.commit = rt[3].cast<std::string>();
+                spec.cls_sql = rt[4].cast<std::string>();
+                spec.meth_sql = rt[5].cast<std::string>();
+                py::gil_scoped_release release;
+                const auto t = std::chrono::steady_clock::now();
+                emit_static_rows(*r, spec, ids);
+                emit_us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t)
+                              .count();
+            }
             const auto t = std::chrono::steady_clock::now();
             py::dict d = scan_result_objects(*r, method_cls);
-            py::dict(d["stats"])["phaseUs"].cast<py::dict>()["objects"] =
+            py::dict phase = py::dict(d["stats"])["phaseUs"].cast<py::dict>();
+            phase["objects"] =
                 std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t).count();
+            if (emit) {
+                phase["rows"] = emit_us;
+                py::dict row_ids;
+                for (size_t k = 0; k < ids.size(); ++k) {
+                    if (ids[k].first.empty()) continue;  // a file replaced by a later one
+                    py::list mids(ids[k].second.size());
+                    for (size_t j = 0; j < ids[k].second.size(); ++j) mids[j] = pystr(ids[k].second[j]);
+                    row_ids[pystr(r->files[k].identifier)] = py::make_tuple(pystr(ids[k].first), mids);
+                }
+                d["rowIds"] = row_ids;
+            }
             // ~10^5 small strings allocated on the worker threads' malloc arenas:
             // freed off the caller's critical path
             std::thread([](std::unique_ptr<srcscan::ScanResult>) {}, std::move(r)).detach();
             return d;
         },
         py::arg("files"), py::arg("language"), py::arg("threads"), py::arg("framework"), py::arg("method_cls"),
-        "scan_sources as Python objects (files as tuples, methods as method_cls) -- no JSON round trip");
+        py::arg("rows") = py::none(),
+        "scan_sources as Python objects (files as tuples, methods as method_cls) -- no JSON round trip; "
+        "with rows, the class / method rows are written first (ids in 'rowIds')");
     m.def(
         "scan_snapshot",
         [](const std::vector<std::string>& object_dirs, py::list entries, const std::string& language, int threads,
@@ -970,7 +1160,7 @@ PYBIND11_MODULE(_srcscan, m) {
         .def("phase1_rows", &phase1_rows, py::arg("order"), py::arg("units"), py::arg("ids"), py::arg("pid"),
              py::arg("now"), py::arg("commit_hash"), py::arg("class_sql"), py::arg("method_sql"),
              py::arg("param_sql"), py::arg("method_info_cls"), py::arg("chunk") = 256,
-             py::arg("graph_targets") = py::none(),
+             py::arg("graph_targets") = py::none(), py::arg("pre_ids") = py::none(),
              "Phase 1 rows of the parsed units straight into this writer (see phase1_rows in pymodule.cpp)")
         .def_property_readonly("rows_written", &dbw::BulkWriter::rows_written)
         .def("timings", [](const dbw::BulkWriter& w) {

@@ -388,10 +388,66 @@ def test_native_phase1_ids_are_time_ordered_uuid7(tmp_path, repo):
     app = make_app(tmp_path)
     app.indexer.analyze_project(str(repo))
     g = app.cache.get_graph(app.repos.projects.find_all()[0].id)
-    ids = [g.class_id(i) for i in g.analysis_order()]  # minted in this order
+    ids = [g.class_id(i) for i in g.identifiers()]  # minted in scan order, as the native scan writes them
     mids = [r[0] for r in app.db.query("SELECT id FROM source_methods")]
     pat = re.compile(r"^[0-9a-f]{8}-[0-9a-f]{4}-7[0-9a-f]{3}-[89ab][0-9a-f]{3}-[0-9a-f]{12}$")
     assert ids and all(pat.match(i) for i in ids + mids)
     assert len(set(ids + mids)) == len(ids) + len(mids)
     assert ids == sorted(ids)
     app.close()
+
+
+@pytest.mark.parametrize("kind", ["java", "nest"])
+def test_scan_written_rows_match_python_loop(tmp_path, monkeypatch, kind):
+    """Class / method rows handed to the writer by the native scan itself
+    (before the graph exists; Phase 1 then binds their ids and writes only the
+    parameter rows) hold the same values, links and graph metadata as the
+    Python Phase 1 loop -- compared by content, the ids being fresh UUIDv7s.
+    Includes a non-ASCII exception name and an identifier defined twice
+    (the later file wins)."""
+    from dmcp.index.pipeline import Indexer
+    repo = tmp_path / "src"
+    if kind == "java":
+        synth.java_spring_repo(str(repo), 24)
+        (repo / "src/main/java/co/acme/shop/order/Weird.java").write_text(
+            "package co.acme.shop.order;\npublic class Weird {\n"
+            "  public void boom() throws Erroré, java.io.IOException, \\u0041x {}\n}\n")
+    else:
+        synth.nestjs_repo(str(repo), 4)
+        (repo / "src" / "dup.ts").write_text("export function a(x: number) { return x; }\n")
+        (repo / "src" / "dup.tsx").write_text("export function b() { return 1; }\n")
+    _git(repo, "add", "-A")
+    _git(repo, "-c", "user.name=t", "-c", "user.email=t@t", "commit", "-qm", "extra")
+
+    def content(app, pid):
+        cls = app.db.query("SELECT id, full_class_name, simple_name, package_name, class_type, description, "
+                           "source_file, commit_hash FROM source_classes WHERE project_id = ?", (pid,))
+        fq = {c["id"]: c["full_class_name"] for c in cls}
+        meth = app.db.query("SELECT m.id, m.class_id, m.method_name, m.description, m.business_logic, "
+                            "m.exceptions, m.http_method, m.http_path, m.line_number FROM source_methods m "
+                            "JOIN source_classes c ON c.id = m.class_id WHERE c.project_id = ?", (pid,))
+        mk = {m["id"]: (fq[m["class_id"]], m["method_name"], m["line_number"]) for m in meth}
+        par = app.db.query("SELECT p.method_id, p.position, p.class_id FROM method_parameters p "
+                           "JOIN source_methods m ON m.id = p.method_id JOIN source_classes c ON c.id = m.class_id "
+                           "WHERE c.project_id = ?", (pid,))
+        graph = json.loads(app.repos.projects.find_by_id(pid).graph_data)
+        for node in graph["nodes"].values():
+            node["classId"] = fq.get(node.get("classId"), node.get("classId"))
+        return (sorted((tuple(c[k] for k in c.keys() if k != "id") for c in cls), key=repr),
+                sorted(((fq[m["class_id"]],) + tuple(m[k] for k in m.keys() if k not in ("id", "class_id"))
+                        for m in meth), key=repr),
+                sorted(((mk[p["method_id"]], p["position"], fq[p["class_id"]]) for p in par), key=repr), graph)
+
+    got = {}
+    for native in (True, False):
+        monkeypatch.setattr(Indexer, "native_phase1", native)
+        app = make_app(tmp_path / f"n{int(native)}")
+        r = app.indexer.analyze_project(str(repo))
+        got[native] = content(app, r.project_id)
+        if native:
+            assert r.stats.get("analyze.writer_rows") is not None
+        app.close()
+    assert got[True][0] and got[True][1]
+    assert got[True] == got[False]
+    if kind == "java":
+        assert any("\\u00e9" in (m[4] or "") for m in got[True][1])  # ensure_ascii form of the exception list

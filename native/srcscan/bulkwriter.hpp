@@ -13,6 +13,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -43,6 +44,7 @@ struct Batch {
     int ncols = 0;
     std::vector<Value> values;
     std::deque<std::string> owned;
+    std::shared_ptr<const void> keep;  // whatever else the text values view (released after the insert)
 };
 
 class BulkWriter {

@@ -418,85 +418,104 @@ void json_ascii_list(const std::vector<std::string>& v, std::string& out) {
 // pre_ids) and writes the parameter rows.  Java / TypeScript units (a later
 // file with the same identifier replaces the earlier one, as
 // parsers/base.py::_add_unit does); Go merges files per package: not here.
-// Returns ident -> (class id, [method ids]) or None when not applicable.
+// The rows view the ScanResult's strings and one id buffer, which the
+// batches keep alive (freed on the writer thread after the inserts).
 struct StaticRowsSpec {
     dbw::BulkWriter* writer = nullptr;
     std::string pid, now, commit, cls_sql, meth_sql;
     bool commit_null = false;
 };
 
-std::string normalize_class_type(const std::string& t) {
-    static const char* kTypes[] = {"CONTROLLER", "SERVICE", "REPOSITORY", "ENTITY", "DTO",
-                                   "CONFIGURATION", "LISTENER", "UTILITY", "EXCEPTION", "OTHER"};
-    std::string up = t;
-    for (auto& c : up) c = (char)std::toupper((unsigned char)c);
-    for (const char* k : kTypes)
-        if (up == k) return up;
-    return "OTHER";  // ClassType.from_string
+struct StaticRowsKeep {
+    std::shared_ptr<const srcscan::ScanResult> r;
+    StaticRowsSpec spec;
+    std::string ids;                  // 36 chars per id: per emitted file its class id, then its method ids
+    std::vector<size_t> first;        // per file: offset of its class id in `ids` (npos: replaced file)
+    std::deque<std::string> strings;  // JSON exception lists
+};
+
+const std::string& normalize_class_type(const std::string& t) {
+    static const std::string kTypes[] = {"CONTROLLER", "SERVICE", "REPOSITORY", "ENTITY", "DTO",
+                                         "CONFIGURATION", "LISTENER", "UTILITY", "EXCEPTION", "OTHER"};
+    for (const std::string& k : kTypes) {
+        if (k.size() != t.size()) continue;
+        bool eq = true;
+        for (size_t i = 0; i < t.size() && eq; ++i) eq = std::toupper((unsigned char)t[i]) == k[i];
+        if (eq) return k;
+    }
+    return kTypes[9];  // ClassType.from_string: OTHER
 }
 
-// emits rows for the winning FileRec of each identifier; ids[k] per file
-// index (empty for replaced files).  GIL not needed.
-void emit_static_rows(const srcscan::ScanResult& r, const StaticRowsSpec& spec,
-                      std::vector<std::pair<std::string, std::vector<std::string>>>& ids) {
+// GIL not needed: reads the (const) ScanResult, which a concurrent Python
+// object build may read too
+void emit_static_rows(const std::shared_ptr<StaticRowsKeep>& keep) {
+    const srcscan::ScanResult& r = *keep->r;
+    const StaticRowsSpec& spec = keep->spec;
     std::unordered_map<std::string_view, size_t> last;
     last.reserve(r.files.size() * 2);
+    size_t n_ids = 0;
     for (size_t k = 0; k < r.files.size(); ++k) last[r.files[k].identifier] = k;
-    ids.assign(r.files.size(), {});
+    for (size_t k = 0; k < r.files.size(); ++k)
+        if (last[r.files[k].identifier] == k) n_ids += 1 + r.files[k].methods.size();
+    keep->ids.resize(36 * n_ids);  // never reallocated below: rows view it
+    keep->first.assign(r.files.size(), std::string::npos);
     Uuid7Gen gen;
-    char buf[36];
+    size_t at = 0;
     const int chunk = 256;
     RowBuilder cls(spec.cls_sql, 10), meth(spec.meth_sql, 10);
     int pending = 0;
     auto flush = [&]() {
+        cls.b.keep = keep;
+        meth.b.keep = keep;
         if (!cls.empty()) spec.writer->put(std::move(cls.b));
         if (!meth.empty()) spec.writer->put(std::move(meth.b));
         cls = RowBuilder(spec.cls_sql, 10);
         meth = RowBuilder(spec.meth_sql, 10);
         pending = 0;
     };
+    auto sv = [](RowBuilder& b, const std::string& s) { b.text(s.data(), (Py_ssize_t)s.size()); };
     for (size_t k = 0; k < r.files.size(); ++k) {
         const srcscan::FileRec& f = r.files[k];
         if (last[f.identifier] != k) continue;
         if (pending == chunk) flush();
         ++pending;
-        gen.next(buf);
-        std::string cid(buf, 36);
+        keep->first[k] = at;
+        const char* cid = &keep->ids[at];
+        gen.next(&keep->ids[at]);
+        at += 36;
         const std::string& ident = f.identifier;
         const size_t dot = ident.rfind('.');
-        cls.owned(std::string(cid));
-        cls.owned(std::string(spec.pid));
-        cls.owned(std::string(ident));
-        if (dot != std::string::npos) cls.owned(ident.substr(dot + 1)); else cls.owned(std::string(ident));
-        if (dot != std::string::npos) cls.owned(ident.substr(0, dot)); else cls.null();
-        cls.owned(normalize_class_type(f.class_type));
+        cls.text(cid, 36);
+        sv(cls, spec.pid);
+        sv(cls, ident);
+        if (dot != std::string::npos) cls.text(ident.data() + dot + 1, (Py_ssize_t)(ident.size() - dot - 1));
+        else sv(cls, ident);
+        if (dot != std::string::npos) cls.text(ident.data(), (Py_ssize_t)dot); else cls.null();
+        sv(cls, normalize_class_type(f.class_type));
         cls.null();
-        cls.owned(std::string(f.rel_path));
-        cls.owned(std::string(spec.now));
-        if (spec.commit_null) cls.null(); else cls.owned(std::string(spec.commit));
-        std::vector<std::string> mids;
-        mids.reserve(f.methods.size());
+        sv(cls, f.rel_path);
+        sv(cls, spec.now);
+        if (spec.commit_null) cls.null(); else sv(cls, spec.commit);
         for (const srcscan::MethodRec& m : f.methods) {
-            gen.next(buf);
-            mids.emplace_back(buf, 36);
-            meth.owned(std::string(mids.back()));
-            meth.owned(std::string(cid));
-            meth.owned(std::string(m.name));
+            gen.next(&keep->ids[at]);
+            meth.text(&keep->ids[at], 36);
+            at += 36;
+            meth.text(cid, 36);
+            sv(meth, m.name);
             meth.null();
-            meth.owned("[]");
+            meth.text("[]", 2);
             if (m.exceptions.empty()) {
-                meth.owned("[]");
+                meth.text("[]", 2);
             } else {
-                std::string js;
-                json_ascii_list(m.exceptions, js);
-                meth.owned(std::move(js));
+                keep->strings.emplace_back();
+                json_ascii_list(m.exceptions, keep->strings.back());
+                sv(meth, keep->strings.back());
             }
-            if (m.has_http_method) meth.owned(std::string(m.http_method)); else meth.null();
-            if (m.has_http_path) meth.owned(std::string(m.http_path)); else meth.null();
+            if (m.has_http_method) sv(meth, m.http_method); else meth.null();
+            if (m.has_http_path) sv(meth, m.http_path); else meth.null();
             meth.integer(m.line);
-            meth.owned(std::string(spec.now));
+            sv(meth, spec.now);
         }
-        ids[k] = {std::move(cid), std::move(mids)};
     }
     flush();
 }
@@ -852,14 +871,18 @@ PYBIND11_MODULE(_srcscan, m) {
            py::handle method_cls, py::object rows) {
             auto r = std::make_unique<srcscan::ScanResult>(scan_mounted(files, language, threads, framework));
             // rows = (BulkWriter, project id, now, commit hash | None, class INSERT, method INSERT):
-            // the class / method rows go to the writer before any object is built
-            std::vector<std::pair<std::string, std::vector<std::string>>> ids;
-            const bool emit = !rows.is_none() && r->language != "go";
-            long long emit_us = 0;
-            if (emit) {
+            // the class / method rows go to the writer from a helper thread
+            // while this one builds the Python objects
+            std::shared_ptr<const srcscan::ScanResult> shared(std::move(r));
+            std::shared_ptr<StaticRowsKeep> keep;
+            std::thread emitter;
+            std::atomic<long long> emit_us{0};
+            if (!rows.is_none() && shared->language != "go") {
                 py::tuple rt = rows.cast<py::tuple>();
                 if (rt.size() != 6) throw py::value_error("rows must have 6 items");
-                StaticRowsSpec spec;
+                keep = std::make_shared<StaticRowsKeep>();
+                keep->r = shared;
+                StaticRowsSpec& spec = keep->spec;
                 spec.writer = &rt[0].cast<dbw::BulkWriter&>();
                 spec.pid = rt[1].cast<std::string>();
                 spec.now = rt[2].cast<std::string>();
@@ -867,31 +890,48 @@ PYBIND11_MODULE(_srcscan, m) {
                 if (!spec.commit_null) spec.commit = rt[3].cast<std::string>();
                 spec.cls_sql = rt[4].cast<std::string>();
                 spec.meth_sql = rt[5].cast<std::string>();
-                py::gil_scoped_release release;
-                const auto t = std::chrono::steady_clock::now();
-                emit_static_rows(*r, spec, ids);
-                emit_us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t)
-                              .count();
+                emitter = std::thread([keep, &emit_us] {
+                    const auto t = std::chrono::steady_clock::now();
+                    emit_static_rows(keep);
+                    emit_us = std::chrono::duration_cast<std::chrono::microseconds>(
+                                  std::chrono::steady_clock::now() - t).count();
+                });
             }
-            const auto t = std::chrono::steady_clock::now();
-            py::dict d = scan_result_objects(*r, method_cls);
-            py::dict phase = py::dict(d["stats"])["phaseUs"].cast<py::dict>();
-            phase["objects"] =
-                std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t).count();
-            if (emit) {
-                phase["rows"] = emit_us;
+            py::dict d;
+            try {
+                const auto t = std::chrono::steady_clock::now();
+                d = scan_result_objects(*shared, method_cls);
+                py::dict(d["stats"])["phaseUs"].cast<py::dict>()["objects"] =
+                    std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t)
+                        .count();
+            } catch (...) {
+                if (emitter.joinable()) {
+                    py::gil_scoped_release release;
+                    emitter.join();
+                }
+                throw;
+            }
+            if (emitter.joinable()) {
+                {
+                    py::gil_scoped_release release;
+                    emitter.join();
+                }
+                py::dict(d["stats"])["phaseUs"].cast<py::dict>()["rows"] = emit_us.load();
                 py::dict row_ids;
-                for (size_t k = 0; k < ids.size(); ++k) {
-                    if (ids[k].first.empty()) continue;  // a file replaced by a later one
-                    py::list mids(ids[k].second.size());
-                    for (size_t j = 0; j < ids[k].second.size(); ++j) mids[j] = pystr(ids[k].second[j]);
-                    row_ids[pystr(r->files[k].identifier)] = py::make_tuple(pystr(ids[k].first), mids);
+                for (size_t k = 0; k < shared->files.size(); ++k) {
+                    const size_t at = keep->first[k];
+                    if (at == std::string::npos) continue;  // a file replaced by a later one
+                    const size_t nm = shared->files[k].methods.size();
+                    py::list mids(nm);
+                    for (size_t j = 0; j < nm; ++j) mids[j] = py::str(&keep->ids[at + 36 * (j + 1)], 36);
+                    row_ids[pystr(shared->files[k].identifier)] = py::make_tuple(py::str(&keep->ids[at], 36), mids);
                 }
                 d["rowIds"] = row_ids;
             }
-            // ~10^5 small strings allocated on the worker threads' malloc arenas:
-            // freed off the caller's critical path
-            std::thread([](std::unique_ptr<srcscan::ScanResult>) {}, std::move(r)).detach();
+            // the rest of the ScanResult is freed off this thread (by the
+            // writer after its inserts, or here by a helper)
+            keep.reset();
+            std::thread([](std::shared_ptr<const srcscan::ScanResult>) {}, std::move(shared)).detach();
             return d;
         },
         py::arg("files"), py::arg("language"), py::arg("threads"), py::arg("framework"), py::arg("method_cls"),

@@ -3,8 +3,9 @@
 
 Every op cycles through 16 distinct weight copies (one per layer), as a
 decode step does, so the weights stream from HBM instead of sitting in the
-256 MB MALL.  Arms: hipBLASLt x @ W^T (the model's F.linear), rocBLAS for the
-same product, and the transposed problem W @ x^T (hipBLASLt picks other
+256 MB MALL.  Arms: hipBLASLt x @ W^T (the model's F.linear), the same
+product on PyTorch's other ROCm BLAS back-ends ("hipblas" = rocBLAS, "ck" =
+composable_kernel), and the transposed problem W @ x^T (hipBLASLt picks other
 kernels for a wide-N, skinny-M output).  One JSON line per (op, M, arm).
 
     python scripts/bench_gemm_variants.py
@@ -47,14 +48,14 @@ def main() -> int:
             for arm, fn in arms.items():
                 res[arm] = timed(fn, iters=4) / LAYERS
             prev = torch.backends.cuda.preferred_blas_library()
-            try:
-                torch.backends.cuda.preferred_blas_library("rocblas")
-                res["rocblas"] = timed(lt, iters=4) / LAYERS
-                res["rocblas_transposed"] = timed(tr, iters=4) / LAYERS
-            except Exception as e:  # backend switch unavailable on this build
-                print(json.dumps({"rocblas_error": str(e)[:200]}), flush=True)
-            finally:
-                torch.backends.cuda.preferred_blas_library(prev)
+            for lib in ("hipblas", "ck"):  # "hipblas" = the rocBLAS path on ROCm builds
+                try:
+                    torch.backends.cuda.preferred_blas_library(lib)
+                    res[lib] = timed(lt, iters=4) / LAYERS
+                except Exception as e:  # backend unavailable on this build
+                    print(json.dumps({"lib": lib, "error": str(e)[:200]}), flush=True)
+                finally:
+                    torch.backends.cuda.preferred_blas_library(prev)
             for arm, t in res.items():
                 print(json.dumps({"gemm": name, "M": M, "N": N, "K": K, "arm": arm, "us": round(t * 1e6, 2),
                                   "weight_TBps": round(N * K * 2 / t / 1e12, 2)}), flush=True)

@@ -1,0 +1,211 @@
+// Split-K decode GEMM with the residual add + RMSNorm of the next op folded
+// into its reduction, for gfx950 (MI355X, CDNA4) -- the O and down
+// projections of a decode step at 33-128 rows:
+//
+//   resid += bf16(x . W^T);   out = RMSNorm(resid) * g
+//
+// which the hipBLASLt path runs as F.linear + add_rmsnorm (two launches, the
+// GEMM output written and re-read).  Shape of the work: M <= 128 rows, N x K
+// weights streamed once from HBM; at N = 2048 a whole-K tiling gives 32-128
+// blocks for 256 CUs (hipBLASLt: 0.7-1.6 TB/s on these shapes,
+// profiles/gemm_blas_backends_r2.jsonl).  Here:
+//
+//   splitk_gemm_kernel   grid (N/64) x S: block (tile, s) computes the 64
+//                        output columns n0..n0+63 over K slice s for every
+//                        row, 4 waves x 16 weight rows (A operand of
+//                        v_mfma_f32_16x16x32_bf16, 16-B loads straight to
+//                        VGPRs), X fragments (L2-resident, shared by every
+//                        block) as the B operand, a rolling register ring of
+//                        P k-steps in flight; fp32 partial slab part[s][m][n].
+//   splitk_reduce_norm   one block per row: sum of the S slabs, bf16 round
+//                        (what F.linear returns), + residual (bf16 stream,
+//                        written back), RMSNorm with weight g -> out.
+//
+// The reduction is a second launch, not an in-launch last-arriver combine:
+// it needs the whole row for the norm anyway (cdna_hip_programming.md §5:
+// combine in the next kernel when that kernel exists).
+#include "dmcp_common.hpp"
+
+namespace {
+
+constexpr int kTileN = 64;  // output columns per block (4 waves x 16)
+
+template <int MT>
+__global__ __launch_bounds__(kBlock) void splitk_gemm_kernel(const uint16_t* __restrict__ x,
+                                                             const uint16_t* __restrict__ w,
+                                                             float* __restrict__ part, int M, int K, int N,
+                                                             int ks) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int l16 = lane & 15, g = lane >> 4;
+    const int n0 = blockIdx.x * kTileN + 16 * wv;
+    const int s = blockIdx.y;
+    const int k0 = s * ks;
+    const int steps = ks / 32;
+    const uint16_t* wp = w + (size_t)(n0 + l16) * K + k0 + 8 * g;
+    const uint16_t* xp[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) xp[mt] = x + (size_t)min(16 * mt + l16, M - 1) * K + k0 + 8 * g;
+    f32x4_t acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    constexpr int P = MT <= 4 ? 6 : 4;  // k-steps of loads in flight per lane
+    auto load_step = [&](uint4& wf, uint4 (&xf)[MT], int st) {
+        wf = *reinterpret_cast<const uint4*>(wp + 32 * st);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) xf[mt] = *reinterpret_cast<const uint4*>(xp[mt] + 32 * st);
+    };
+    auto mma_step = [&](const uint4& wf, const uint4 (&xf)[MT]) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wf), as_bf16x8(xf[mt]), acc[mt], 0, 0, 0);
+    };
+    int st = 0;
+    if (steps >= P) {
+        uint4 wr[P], xr[P][MT];
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            load_step(wr[j], xr[j], j);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        for (; st + 2 * P <= steps; st += P) {
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                mma_step(wr[j], xr[j]);
+                load_step(wr[j], xr[j], st + j + P);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < P; ++j) mma_step(wr[j], xr[j]);
+        st += P;
+    }
+    for (; st < steps; ++st) {
+        uint4 wf, xf[MT];
+        load_step(wf, xf, st);
+        mma_step(wf, xf);
+    }
+    // accumulator layout: lane (l16, g) holds columns n0 + 4g + i of row 16 mt + l16
+    float* dst = part + (size_t)s * M * N + n0 + 4 * g;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int m = 16 * mt + l16;
+        if (m < M) *reinterpret_cast<float4*>(dst + (size_t)m * N) = make_float4(acc[mt][0], acc[mt][1], acc[mt][2], acc[mt][3]);
+    }
+}
+
+template <int VPT>
+__global__ __launch_bounds__(kBlock) void splitk_reduce_norm_kernel(const float* __restrict__ part, int S,
+                                                                    uint16_t* __restrict__ resid,
+                                                                    const uint16_t* __restrict__ gw,
+                                                                    uint16_t* __restrict__ out, int M, int N,
+                                                                    float eps) {
+    const int m = blockIdx.x;
+    const int nvec = N >> 3;
+    float h[VPT][8];
+    uint4 rv[VPT], wv[VPT];
+    uint4* rr = reinterpret_cast<uint4*>(resid + (size_t)m * N);
+    const uint4* wr = reinterpret_cast<const uint4*>(gw);
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int idx = threadIdx.x + i * kBlock;
+        if (idx < nvec) {
+            rv[i] = rr[idx];
+            wv[i] = wr[idx];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) h[i][j] = 0.f;
+    }
+    for (int s = 0; s < S; ++s) {
+        const float4* pp = reinterpret_cast<const float4*>(part + ((size_t)s * M + m) * N);
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+            const int idx = threadIdx.x + i * kBlock;
+            if (idx < nvec) {
+                const float4 a = pp[2 * idx], b = pp[2 * idx + 1];
+                h[i][0] += a.x; h[i][1] += a.y; h[i][2] += a.z; h[i][3] += a.w;
+                h[i][4] += b.x; h[i][5] += b.y; h[i][6] += b.z; h[i][7] += b.w;
+            }
+        }
+    }
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int idx = threadIdx.x + i * kBlock;
+        if (idx < nvec) {
+            float y[8], r[8];
+            unpack8(pack8(h[i]), y);  // the GEMM output as F.linear rounds it
+            unpack8(rv[i], r);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) y[j] += r[j];
+            const uint4 packed = pack8(y);
+            rr[idx] = packed;
+            unpack8(packed, h[i]);  // normalise the bf16-rounded stream (add_rmsnorm's order)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ss += h[i][j] * h[i][j];
+        }
+    }
+    __shared__ float red[kBlock / kWave];
+    ss = wave_sum(ss);
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < kBlock / kWave; ++i) tot += red[i];
+    const float inv = rsqrtf(tot / (float)N + eps);
+    uint4* orow = reinterpret_cast<uint4*>(out + (size_t)m * N);
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int idx = threadIdx.x + i * kBlock;
+        if (idx < nvec) {
+            float gv[8], o[8];
+            unpack8(wv[i], gv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = h[i][j] * inv * gv[j];
+            orow[idx] = pack8(o);
+        }
+    }
+}
+
+template <int MT>
+hipError_t launch_gemm(const uint16_t* x, const uint16_t* w, float* part, int M, int K, int N, int S,
+                       hipStream_t st) {
+    splitk_gemm_kernel<MT><<<dim3(N / kTileN, S), kBlock, 0, st>>>(x, w, part, M, K, N, K / S);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+// resid[M, N] += bf16(x[M, K] . w[N, K]^T); out = RMSNorm(resid) * g.
+// part: fp32 workspace of S * M * N.  Shapes checked by the host wrapper
+// (dmcp/ops/hip.py::linear_resid_norm); the checks here guard the tiling.
+int dmcp_splitk_resid_norm(const void* x, const void* w, void* part, void* resid, const void* g, void* out, int M,
+                           int K, int N, int S, float eps, void* stream) {
+    if (M <= 0) return 0;
+    if (M > 128 || S <= 0 || N % kTileN != 0 || K % (32 * S) != 0 || N % 8 != 0 || N > 8 * 4 * kBlock || !x ||
+        !w || !part || !resid || !g || !out)
+        return hipErrorInvalidValue;
+    auto st = (hipStream_t)stream;
+    auto xx = (const uint16_t*)x;
+    auto ww = (const uint16_t*)w;
+    auto pp = (float*)part;
+    hipError_t e;
+    const int mt = (M + 15) / 16;
+    if (mt <= 2) e = launch_gemm<2>(xx, ww, pp, M, K, N, S, st);
+    else if (mt <= 4) e = launch_gemm<4>(xx, ww, pp, M, K, N, S, st);
+    else if (mt <= 6) e = launch_gemm<6>(xx, ww, pp, M, K, N, S, st);
+    else e = launch_gemm<8>(xx, ww, pp, M, K, N, S, st);
+    if (e != hipSuccess) return e;
+    const int vpt = (N / 8 + kBlock - 1) / kBlock;
+    auto rr = (uint16_t*)resid;
+    auto gg = (const uint16_t*)g;
+    auto oo = (uint16_t*)out;
+    if (vpt == 1) splitk_reduce_norm_kernel<1><<<M, kBlock, 0, st>>>(pp, S, rr, gg, oo, M, N, eps);
+    else if (vpt == 2) splitk_reduce_norm_kernel<2><<<M, kBlock, 0, st>>>(pp, S, rr, gg, oo, M, N, eps);
+    else splitk_reduce_norm_kernel<4><<<M, kBlock, 0, st>>>(pp, S, rr, gg, oo, M, N, eps);
+    return hipGetLastError();
+}
+
+}  // extern "C"

@@ -61,6 +61,7 @@ def lib() -> ctypes.CDLL:
             "dmcp_set_decode_impl": ([_i], _i),
             "dmcp_set_prefix_overlap": ([_i], _i),
             "dmcp_fused_gemm_max_rows": ([], _i),
+            "dmcp_splitk_resid_norm": ([_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp], _i),
             "dmcp_fused_gemm": ([_i, _i, _vp, _vp, _vp, _i, _i, _i, _f, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i,
                                  _i, _i, _i, _i, _vp], _i),
         }
@@ -543,6 +544,48 @@ def fused_resid(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, wk: in
         raise HipOpsError(f"fused_resid: residual {tuple(residual.shape)} != {(M, N)}")
     _fused("resid", wk, x, w, residual, M, K, N)
     return residual
+
+
+SPLITK_MAX_ROWS = 128
+
+
+def splitk_splits(N: int, K: int, target_blocks: int = 256) -> int:
+    """K slices for linear_resid_norm: enough 64-column blocks to cover the
+    chip, each slice a whole number of 32-deep k-steps (>= 4)."""
+    s = 1
+    while (N // 64) * s < target_blocks and K % (64 * s) == 0 and K // (2 * s) >= 128:
+        s *= 2
+    return s
+
+
+def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor, eps: float,
+                      workspace: torch.Tensor, splits: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """residual += bf16(x . w^T) (in place); returns RMSNorm(residual) * norm_w
+    -- F.linear + add_rmsnorm in two launches (csrc/splitk_gemm.hip: split-K
+    MFMA GEMM into fp32 slabs, then one reduction per row that also adds the
+    residual and normalises).  x [M, K] (M <= 128), w [N, K], residual [M, N];
+    workspace: fp32 with at least splits * M * N elements."""
+    _req(x, torch.bfloat16, "linear_resid_norm.x")
+    _req(w, torch.bfloat16, "linear_resid_norm.w")
+    _req(residual, torch.bfloat16, "linear_resid_norm.residual")
+    _req(norm_w, torch.bfloat16, "linear_resid_norm.norm_w")
+    if x.dim() != 2 or w.dim() != 2 or x.shape[1] != w.shape[1]:
+        raise HipOpsError(f"linear_resid_norm: x {tuple(x.shape)} / w {tuple(w.shape)} are not [M, K] / [N, K]")
+    M, K = x.shape
+    N = w.shape[0]
+    S = splits or splitk_splits(N, K)
+    if not 1 <= M <= SPLITK_MAX_ROWS or N % 64 or N > 8192 or K % (32 * S):
+        raise HipOpsError(f"linear_resid_norm: unsupported shape M={M} K={K} N={N} splits={S}")
+    if tuple(residual.shape) != (M, N) or norm_w.numel() != N:
+        raise HipOpsError("linear_resid_norm: residual / norm weight shape mismatch")
+    if workspace.dtype != torch.float32 or not workspace.is_contiguous() or workspace.numel() < S * M * N:
+        raise HipOpsError(f"linear_resid_norm: workspace needs {S * M * N} contiguous fp32 elements")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    _req_out(out, torch.bfloat16, M * N, "linear_resid_norm.out")
+    _check(lib().dmcp_splitk_resid_norm(_ptr(x), _ptr(w), _ptr(workspace), _ptr(residual), _ptr(norm_w), _ptr(out),
+                                        M, K, N, S, float(eps), _stream()), "dmcp_splitk_resid_norm")
+    return out
 
 
 def fused_linear_norm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None,

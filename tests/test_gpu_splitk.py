@@ -1,0 +1,51 @@
+"""Split-K decode GEMM with the residual add + RMSNorm folded into its
+reduction (csrc/splitk_gemm.hip) against the fp32 reference of
+F.linear -> add_rmsnorm (dmcp.ops.reference)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hip():
+    from dmcp.ops import hip as h
+    h.lib()
+    return h
+
+
+def _bf(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return (torch.randn(*shape, generator=g, device="cuda") * scale).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("M", [1, 17, 33, 78, 96, 128])
+@pytest.mark.parametrize("N,K", [(2048, 2048), (2048, 8192), (512, 1024)])
+def test_linear_resid_norm(hip, M, N, K):
+    from dmcp.ops import reference
+    x = _bf(M, K, seed=M)
+    w = _bf(N, K, seed=N + K, scale=0.03)
+    resid = _bf(M, N, seed=7)
+    g = (1 + 0.1 * _bf(N, seed=8).float()).to(torch.bfloat16)
+    S = hip.splitk_splits(N, K)
+    ws = torch.empty(S * M * N, dtype=torch.float32, device="cuda")
+    r_exp = resid.clone()
+    y = (x.float() @ w.float().t()).to(torch.bfloat16)
+    exp = reference.add_rmsnorm(y, g, 1e-5, residual=r_exp)
+    r_got = resid.clone()
+    got = hip.linear_resid_norm(x, w, r_got, g, 1e-5, ws)
+    torch.testing.assert_close(r_got.float(), r_exp.float(), atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(got.float(), exp.float(), atol=3e-2, rtol=3e-2)
+    for s in (1, 2):  # other split counts give the same result
+        r2 = resid.clone()
+        torch.testing.assert_close(hip.linear_resid_norm(x, w, r2, g, 1e-5, ws, splits=s).float(), got.float(),
+                                   atol=3e-2, rtol=3e-2)
+
+
+def test_linear_resid_norm_rejects_bad_shapes(hip):
+    x, w = _bf(4, 100), _bf(64, 100)
+    with pytest.raises(hip.HipOpsError):
+        hip.linear_resid_norm(x, w, _bf(4, 64), _bf(64), 1e-5, torch.empty(1 << 16, device="cuda"))
+    x, w = _bf(129, 128), _bf(64, 128)
+    with pytest.raises(hip.HipOpsError):
+        hip.linear_resid_norm(x, w, _bf(129, 64), _bf(64), 1e-5, torch.empty(1 << 20, device="cuda"))

@@ -55,10 +55,10 @@ def fused_resid(x, w, residual, wk: int = 0):
     return _hip().fused_resid(x, w, residual, wk or (16 if x.shape[1] >= 4096 else 8))
 
 
-def linear_resid_norm(x, w, residual, norm_w, eps, workspace, splits: int = 0, out=None):
+def linear_resid_norm(x, w, residual, norm_w, eps, workspace, splits: int = 0, out=None, variant: int = 1):
     """residual += bf16(x . w^T); returns RMSNorm(residual) * norm_w -- split-K
     gfx950 GEMM + one fused reduce/residual/norm pass (GPU only, M <= 128)."""
-    return _hip().linear_resid_norm(x, w, residual, norm_w, eps, workspace, splits, out)
+    return _hip().linear_resid_norm(x, w, residual, norm_w, eps, workspace, splits, out, variant)
 
 
 def splitk_splits(N, K):

@@ -94,6 +94,85 @@ __global__ __launch_bounds__(kBlock) void splitk_gemm_kernel(const uint16_t* __r
     }
 }
 
+// Variant 1: the X slice goes through LDS once per block (the register-direct
+// kernel above re-reads every X fragment in each of the 4 waves: 1.3-1.8x
+// slower than hipBLASLt, profiles/splitk_gemm_r2_v1.jsonl).  64-deep chunks of
+// all MP = 16 MT rows, two buffers, one barrier per chunk; 16-B pieces
+// XOR-swizzled by row (piece ^ (row & 7)) so a wave's ds_read_b128 of 16 rows
+// x 4 pieces is at most 2-way conflicted.  W stays register-direct with a
+// ring of 4 k-steps.  Needs the K slice to be a multiple of 128.
+template <int MT>
+__global__ __launch_bounds__(kBlock) void splitk_gemm_lds_kernel(const uint16_t* __restrict__ x,
+                                                                 const uint16_t* __restrict__ w,
+                                                                 float* __restrict__ part, int M, int K, int N,
+                                                                 int ks) {
+    constexpr int MP = 16 * MT;
+    constexpr int NP = MP * 8 / kBlock;  // 16-B X pieces per thread per chunk
+    static_assert(NP >= 1 && MP * 8 % kBlock == 0, "MT must be even");
+    __shared__ uint4 xs[2][MP * 8];
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(tid / kWave);
+    const int l16 = lane & 15, g = lane >> 4;
+    const int n0 = blockIdx.x * kTileN + 16 * wv;
+    const int s = blockIdx.y;
+    const int k0 = s * ks;
+    const int steps = ks / 32, chunks = ks / 64;
+    const uint16_t* wp = w + (size_t)(n0 + l16) * K + k0 + 8 * g;
+    // this thread's X pieces: row pr[i], piece pc[i] of every chunk
+    const uint16_t* xp[NP];
+    int so[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int p = tid + i * kBlock;
+        const int row = p >> 3, pc = p & 7;
+        xp[i] = x + (size_t)min(row, M - 1) * K + k0 + 8 * pc;
+        so[i] = row * 8 + (pc ^ (row & 7));
+    }
+    f32x4_t acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    uint4 wr[4], xg[NP];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wr[j] = *reinterpret_cast<const uint4*>(wp + 32 * min(j, steps - 1));
+#pragma unroll
+    for (int i = 0; i < NP; ++i) xs[0][so[i]] = *reinterpret_cast<const uint4*>(xp[i]);
+    __syncthreads();
+    for (int c = 0; c < chunks; c += 2) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // chunk c + h in buffer h
+            const int cn = min(c + h + 1, chunks - 1);
+#pragma unroll
+            for (int i = 0; i < NP; ++i) xg[i] = *reinterpret_cast<const uint4*>(xp[i] + 64 * cn);
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                const int j = 2 * h + kk;  // ring slot of step 2 (c + h) + kk
+                uint4 xf[MT];
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) {
+                    const int row = 16 * mt + l16;
+                    xf[mt] = xs[h][row * 8 + ((4 * kk + g) ^ (row & 7))];
+                }
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+                    acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wr[j]), as_bf16x8(xf[mt]), acc[mt],
+                                                                      0, 0, 0);
+                wr[j] = *reinterpret_cast<const uint4*>(wp + 32 * min(2 * (c + h) + kk + 4, steps - 1));
+            }
+#pragma unroll
+            for (int i = 0; i < NP; ++i) xs[h ^ 1][so[i]] = xg[i];
+            __syncthreads();
+        }
+    }
+    float* dst = part + (size_t)s * M * N + n0 + 4 * g;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int m = 16 * mt + l16;
+        if (m < M)
+            *reinterpret_cast<float4*>(dst + (size_t)m * N) = make_float4(acc[mt][0], acc[mt][1], acc[mt][2], acc[mt][3]);
+    }
+}
+
 template <int VPT>
 __global__ __launch_bounds__(kBlock) void splitk_reduce_norm_kernel(const float* __restrict__ part, int S,
                                                                     uint16_t* __restrict__ resid,
@@ -168,9 +247,12 @@ __global__ __launch_bounds__(kBlock) void splitk_reduce_norm_kernel(const float*
 }
 
 template <int MT>
-hipError_t launch_gemm(const uint16_t* x, const uint16_t* w, float* part, int M, int K, int N, int S,
+hipError_t launch_gemm(const uint16_t* x, const uint16_t* w, float* part, int M, int K, int N, int S, int variant,
                        hipStream_t st) {
-    splitk_gemm_kernel<MT><<<dim3(N / kTileN, S), kBlock, 0, st>>>(x, w, part, M, K, N, K / S);
+    if (variant == 1)
+        splitk_gemm_lds_kernel<MT><<<dim3(N / kTileN, S), kBlock, 0, st>>>(x, w, part, M, K, N, K / S);
+    else
+        splitk_gemm_kernel<MT><<<dim3(N / kTileN, S), kBlock, 0, st>>>(x, w, part, M, K, N, K / S);
     return hipGetLastError();
 }
 
@@ -181,11 +263,12 @@ extern "C" {
 // resid[M, N] += bf16(x[M, K] . w[N, K]^T); out = RMSNorm(resid) * g.
 // part: fp32 workspace of S * M * N.  Shapes checked by the host wrapper
 // (dmcp/ops/hip.py::linear_resid_norm); the checks here guard the tiling.
+// variant 0: register-direct X; 1: X staged through LDS (K % (128 S) == 0).
 int dmcp_splitk_resid_norm(const void* x, const void* w, void* part, void* resid, const void* g, void* out, int M,
-                           int K, int N, int S, float eps, void* stream) {
+                           int K, int N, int S, float eps, int variant, void* stream) {
     if (M <= 0) return 0;
     if (M > 128 || S <= 0 || N % kTileN != 0 || K % (32 * S) != 0 || N % 8 != 0 || N > 8 * 4 * kBlock || !x ||
-        !w || !part || !resid || !g || !out)
+        !w || !part || !resid || !g || !out || variant < 0 || variant > 1 || (variant == 1 && K % (128 * S) != 0))
         return hipErrorInvalidValue;
     auto st = (hipStream_t)stream;
     auto xx = (const uint16_t*)x;
@@ -193,10 +276,10 @@ int dmcp_splitk_resid_norm(const void* x, const void* w, void* part, void* resid
     auto pp = (float*)part;
     hipError_t e;
     const int mt = (M + 15) / 16;
-    if (mt <= 2) e = launch_gemm<2>(xx, ww, pp, M, K, N, S, st);
-    else if (mt <= 4) e = launch_gemm<4>(xx, ww, pp, M, K, N, S, st);
-    else if (mt <= 6) e = launch_gemm<6>(xx, ww, pp, M, K, N, S, st);
-    else e = launch_gemm<8>(xx, ww, pp, M, K, N, S, st);
+    if (mt <= 2) e = launch_gemm<2>(xx, ww, pp, M, K, N, S, variant, st);
+    else if (mt <= 4) e = launch_gemm<4>(xx, ww, pp, M, K, N, S, variant, st);
+    else if (mt <= 6) e = launch_gemm<6>(xx, ww, pp, M, K, N, S, variant, st);
+    else e = launch_gemm<8>(xx, ww, pp, M, K, N, S, variant, st);
     if (e != hipSuccess) return e;
     const int vpt = (N / 8 + kBlock - 1) / kBlock;
     auto rr = (uint16_t*)resid;

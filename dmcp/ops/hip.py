@@ -61,7 +61,7 @@ def lib() -> ctypes.CDLL:
             "dmcp_set_decode_impl": ([_i], _i),
             "dmcp_set_prefix_overlap": ([_i], _i),
             "dmcp_fused_gemm_max_rows": ([], _i),
-            "dmcp_splitk_resid_norm": ([_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp], _i),
+            "dmcp_splitk_resid_norm": ([_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _i, _vp], _i),
             "dmcp_fused_gemm": ([_i, _i, _vp, _vp, _vp, _i, _i, _i, _f, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i,
                                  _i, _i, _i, _i, _vp], _i),
         }
@@ -553,13 +553,14 @@ def splitk_splits(N: int, K: int, target_blocks: int = 256) -> int:
     """K slices for linear_resid_norm: enough 64-column blocks to cover the
     chip, each slice a whole number of 32-deep k-steps (>= 4)."""
     s = 1
-    while (N // 64) * s < target_blocks and K % (64 * s) == 0 and K // (2 * s) >= 128:
+    while (N // 64) * s < target_blocks and K % (256 * s) == 0:
         s *= 2
     return s
 
 
 def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor, eps: float,
-                      workspace: torch.Tensor, splits: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                      workspace: torch.Tensor, splits: int = 0, out: Optional[torch.Tensor] = None,
+                      variant: int = 1) -> torch.Tensor:
     """residual += bf16(x . w^T) (in place); returns RMSNorm(residual) * norm_w
     -- F.linear + add_rmsnorm in two launches (csrc/splitk_gemm.hip: split-K
     MFMA GEMM into fp32 slabs, then one reduction per row that also adds the
@@ -574,7 +575,9 @@ def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, 
     M, K = x.shape
     N = w.shape[0]
     S = splits or splitk_splits(N, K)
-    if not 1 <= M <= SPLITK_MAX_ROWS or N % 64 or N > 8192 or K % (32 * S):
+    if variant not in (0, 1):
+        raise HipOpsError(f"linear_resid_norm: unknown variant {variant}")
+    if not 1 <= M <= SPLITK_MAX_ROWS or N % 64 or N > 8192 or K % ((128 if variant == 1 else 32) * S):
         raise HipOpsError(f"linear_resid_norm: unsupported shape M={M} K={K} N={N} splits={S}")
     if tuple(residual.shape) != (M, N) or norm_w.numel() != N:
         raise HipOpsError("linear_resid_norm: residual / norm weight shape mismatch")
@@ -584,7 +587,7 @@ def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, 
         out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
     _req_out(out, torch.bfloat16, M * N, "linear_resid_norm.out")
     _check(lib().dmcp_splitk_resid_norm(_ptr(x), _ptr(w), _ptr(workspace), _ptr(residual), _ptr(norm_w), _ptr(out),
-                                        M, K, N, S, float(eps), _stream()), "dmcp_splitk_resid_norm")
+                                        M, K, N, S, float(eps), variant, _stream()), "dmcp_splitk_resid_norm")
     return out
 
 

@@ -35,17 +35,19 @@ def main() -> int:
             t = timed(ref, iters=4) / LAYERS
             print(json.dumps({"op": name, "M": M, "arm": "hipblaslt+add_rmsnorm", "us": round(t * 1e6, 2),
                               "weight_TBps": round(N * K * 2 / t / 1e12, 2)}), flush=True)
-            for S in (0, 4, 8, 16):
-                Sx = S or hip.splitk_splits(N, K)
-                if K % (32 * Sx):
-                    continue
+            for variant in (0, 1):
+                for S in (0, 4, 8, 16):
+                    Sx = S or hip.splitk_splits(N, K)
+                    if K % ((128 if variant else 32) * Sx):
+                        continue
 
-                def mine(S=S):
-                    for w in ws_w:
-                        hip.linear_resid_norm(x, w, resid, g, 1e-5, ws, splits=S)
-                t = timed(mine, iters=4) / LAYERS
-                print(json.dumps({"op": name, "M": M, "arm": "splitk", "splits": Sx, "auto": S == 0,
-                                  "us": round(t * 1e6, 2), "weight_TBps": round(N * K * 2 / t / 1e12, 2)}), flush=True)
+                    def mine(S=S, variant=variant):
+                        for w in ws_w:
+                            hip.linear_resid_norm(x, w, resid, g, 1e-5, ws, splits=S, variant=variant)
+                    t = timed(mine, iters=4) / LAYERS
+                    print(json.dumps({"op": name, "M": M, "arm": f"splitk_v{variant}", "splits": Sx, "auto": S == 0,
+                                      "us": round(t * 1e6, 2), "weight_TBps": round(N * K * 2 / t / 1e12, 2)}),
+                          flush=True)
     return 0
 
 

@@ -32,14 +32,15 @@ def test_linear_resid_norm(hip, M, N, K):
     r_exp = resid.clone()
     y = (x.float() @ w.float().t()).to(torch.bfloat16)
     exp = reference.add_rmsnorm(y, g, 1e-5, residual=r_exp)
-    r_got = resid.clone()
-    got = hip.linear_resid_norm(x, w, r_got, g, 1e-5, ws)
-    torch.testing.assert_close(r_got.float(), r_exp.float(), atol=3e-2, rtol=2e-2)
-    torch.testing.assert_close(got.float(), exp.float(), atol=3e-2, rtol=3e-2)
-    for s in (1, 2):  # other split counts give the same result
-        r2 = resid.clone()
-        torch.testing.assert_close(hip.linear_resid_norm(x, w, r2, g, 1e-5, ws, splits=s).float(), got.float(),
-                                   atol=3e-2, rtol=3e-2)
+    for variant in (0, 1):
+        r_got = resid.clone()
+        got = hip.linear_resid_norm(x, w, r_got, g, 1e-5, ws, variant=variant)
+        torch.testing.assert_close(r_got.float(), r_exp.float(), atol=3e-2, rtol=2e-2)
+        torch.testing.assert_close(got.float(), exp.float(), atol=3e-2, rtol=3e-2)
+        for s in (1, 2):  # other split counts give the same result
+            r2 = resid.clone()
+            torch.testing.assert_close(hip.linear_resid_norm(x, w, r2, g, 1e-5, ws, splits=s, variant=variant).float(),
+                                       got.float(), atol=3e-2, rtol=3e-2)
 
 
 def test_linear_resid_norm_rejects_bad_shapes(hip):

@@ -213,6 +213,16 @@ class LocalLM:
         ps = max(ops.prefix_splits(c.max_seq, self.PREFIX_CHUNK), ops.PREFIX_MFMA_MAX_SPLITS) if shared_prefix else 0
         self.attn_ws = (ops.decode_workspace(self.max_rows, c.n_heads, c.n_kv_heads, c.head_dim, c.max_seq,
                                              self.device, prefix_slots=ps) if self.device.type == "cuda" else None)
+        # down projection + residual + next norm on the split-K LDS kernel at
+        # fused_max_rows < rows <= 128 (csrc/splitk_gemm.hip; 21.3 vs 23.8 us
+        # per layer at 78 rows, profiles/splitk_gemm_r2_v2.jsonl; the O
+        # projection stays on hipBLASLt, where the kernel is not faster)
+        self.splitk_down = None
+        if (self.device.type == "cuda" and os.environ.get("DMCP_SPLITK_DOWN", "1") != "0"
+                and c.hidden % 64 == 0 and c.hidden <= 8192
+                and c.intermediate % (128 * ops.splitk_splits(c.hidden, c.intermediate)) == 0):
+            self.splitk_down = ops.splitk_splits(c.hidden, c.intermediate)
+            self.splitk_ws = torch.empty(self.splitk_down * 128 * c.hidden, dtype=torch.float32, device=self.device)
 
     # ------------------------------------------------------------ weights
     def _init_weights(self, seed: int) -> Dict[str, torch.Tensor]:
@@ -376,8 +386,13 @@ class LocalLM:
                                        prefix=self._prefix(i), splits=splits)
             o = F.linear(att.view(B, c.n_heads * c.head_dim), self.w[f"l{i}.wo"])
             h = ops.add_rmsnorm(o, self.w[f"l{i}.ln2"], c.eps, residual=resid)
-            m = self._mlp(i, h)
             nxt = self.w[f"l{i + 1}.ln1"] if i + 1 < c.layers else self.w["norm_f"]
+            if self.splitk_down and B <= 128:
+                act = ops.silu_mul(F.linear(h, self.w[f"l{i}.wgu"]))
+                h = ops.linear_resid_norm(act, self.w[f"l{i}.wdown"], resid, nxt, c.eps, self.splitk_ws,
+                                          splits=self.splitk_down)
+                continue
+            m = self._mlp(i, h)
             h = ops.add_rmsnorm(m, nxt, c.eps, residual=resid)
         return F.linear(h, self.w["lm_head"])
 

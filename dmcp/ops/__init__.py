@@ -61,6 +61,14 @@ def linear_resid_norm(x, w, residual, norm_w, eps, workspace, splits: int = 0, o
     return _hip().linear_resid_norm(x, w, residual, norm_w, eps, workspace, splits, out, variant)
 
 
+def linear_rope_kv(x, w, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, workspace, splits: int = 0,
+                   q_out=None, variant: int = 1):
+    """rope_kv(F.linear(x, w)) -- split-K gfx950 GEMM + one reduction that
+    applies RoPE and appends K/V to the cache (GPU only, M <= 128)."""
+    return _hip().linear_rope_kv(x, w, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, workspace, splits, q_out,
+                                 variant)
+
+
 def splitk_splits(N, K):
     return _hip().splitk_splits(N, K)
 

@@ -246,6 +246,84 @@ __global__ __launch_bounds__(kBlock) void splitk_reduce_norm_kernel(const float*
     }
 }
 
+// QKV variant of the reduction: the row's slabs summed and bf16-rounded
+// into LDS (what F.linear returns), then rotate-half RoPE on q and k, q
+// written out, k / v appended to the KV cache (bf16 or, KV8, fp8 e4m3) at
+// (slot[t], :, pos[t], :) -- dmcp_kernels.hip::rope_kv_kernel over an LDS row.
+template <bool KV8>
+__global__ __launch_bounds__(kBlock) void splitk_reduce_rope_kernel(
+    const float* __restrict__ part, int S, int M, const int32_t* __restrict__ pos, const int32_t* __restrict__ slot,
+    const float2* __restrict__ cos_sin, uint16_t* __restrict__ q_out, void* __restrict__ k_cache,
+    void* __restrict__ v_cache, int Hq, int Hkv, int D, int max_seq, int max_pos, int num_slots) {
+    __shared__ uint4 rowbuf[8192 / 8];
+    const int t = blockIdx.x;
+    const int N = (Hq + 2 * Hkv) * D;
+    const int nvec = N >> 3;
+    for (int idx = threadIdx.x; idx < nvec; idx += kBlock) {
+        float h[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int s = 0; s < S; ++s) {
+            const float4* pp = reinterpret_cast<const float4*>(part + ((size_t)s * M + t) * N);
+            const float4 a = pp[2 * idx], b = pp[2 * idx + 1];
+            h[0] += a.x; h[1] += a.y; h[2] += a.z; h[3] += a.w;
+            h[4] += b.x; h[5] += b.y; h[6] += b.z; h[7] += b.w;
+        }
+        rowbuf[idx] = pack8(h);
+    }
+    __syncthreads();
+    const uint16_t* row = reinterpret_cast<const uint16_t*>(rowbuf);
+    const int p = pos[t];
+    const int sl = slot[t];
+    const bool write_cache = (p >= 0 && p < max_seq && sl >= 0 && sl < num_slots);
+    const int half = D >> 1;
+    const int quads = half >> 2;
+    const float2* cs = cos_sin + (size_t)min(max(p, 0), max_pos - 1) * half;
+    const int units = (Hq + Hkv) * quads;
+    for (int u = threadIdx.x; u < units; u += kBlock) {
+        const int hh = u / quads;
+        const int d0 = (u - hh * quads) * 4;
+        const uint16_t* src = row + (size_t)hh * D;
+        float x1[4], x2[4], o1[4], o2[4];
+        unpack4(*reinterpret_cast<const uint2*>(src + d0), x1);
+        unpack4(*reinterpret_cast<const uint2*>(src + half + d0), x2);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float2 c = cs[d0 + j];
+            o1[j] = x1[j] * c.x - x2[j] * c.y;
+            o2[j] = x2[j] * c.x + x1[j] * c.y;
+        }
+        if (hh < Hq) {
+            uint16_t* dst = q_out + ((size_t)t * Hq + hh) * D;
+            *reinterpret_cast<uint2*>(dst + d0) = pack4(o1);
+            *reinterpret_cast<uint2*>(dst + half + d0) = pack4(o2);
+            continue;
+        }
+        if (!write_cache) continue;
+        const size_t kofs = (((size_t)sl * Hkv + (hh - Hq)) * max_seq + p) * D;
+        if constexpr (KV8) {
+            uint8_t* dst = static_cast<uint8_t*>(k_cache) + kofs;
+            *reinterpret_cast<uint32_t*>(dst + d0) = pack_fp8x4(o1);
+            *reinterpret_cast<uint32_t*>(dst + half + d0) = pack_fp8x4(o2);
+        } else {
+            uint16_t* dst = static_cast<uint16_t*>(k_cache) + kofs;
+            *reinterpret_cast<uint2*>(dst + d0) = pack4(o1);
+            *reinterpret_cast<uint2*>(dst + half + d0) = pack4(o2);
+        }
+    }
+    if (!write_cache) return;
+    const int vvec = (Hkv * D) >> 3;
+    const uint4* vsrc = rowbuf + (((Hq + Hkv) * D) >> 3);
+    for (int u = threadIdx.x; u < vvec; u += kBlock) {
+        const int e = u << 3;
+        const int kh = e / D;
+        const int d = e - kh * D;
+        const size_t vofs = (((size_t)sl * Hkv + kh) * max_seq + p) * D + d;
+        if constexpr (KV8)
+            *reinterpret_cast<uint2*>(static_cast<uint8_t*>(v_cache) + vofs) = bf16x8_to_fp8x8(vsrc[u]);
+        else
+            *reinterpret_cast<uint4*>(static_cast<uint16_t*>(v_cache) + vofs) = vsrc[u];
+    }
+}
+
 template <int MT>
 hipError_t launch_gemm(const uint16_t* x, const uint16_t* w, float* part, int M, int K, int N, int S, int variant,
                        hipStream_t st) {
@@ -288,6 +366,40 @@ int dmcp_splitk_resid_norm(const void* x, const void* w, void* part, void* resid
     if (vpt == 1) splitk_reduce_norm_kernel<1><<<M, kBlock, 0, st>>>(pp, S, rr, gg, oo, M, N, eps);
     else if (vpt == 2) splitk_reduce_norm_kernel<2><<<M, kBlock, 0, st>>>(pp, S, rr, gg, oo, M, N, eps);
     else splitk_reduce_norm_kernel<4><<<M, kBlock, 0, st>>>(pp, S, rr, gg, oo, M, N, eps);
+    return hipGetLastError();
+}
+
+// q_out[M, Hq, D] = RoPE(q), k/v appended to the caches, of qkv = x . w^T
+// (w [(Hq + 2 Hkv) D, K]); what F.linear + rope_kv compute.  part: fp32
+// workspace of S * M * N.
+int dmcp_splitk_rope_kv(const void* x, const void* w, void* part, const void* pos, const void* slot,
+                        const void* cos_sin, void* q_out, void* k_cache, void* v_cache, int M, int K, int Hq, int Hkv,
+                        int D, int max_seq, int max_pos, int num_slots, int kv8, int S, int variant, void* stream) {
+    if (M <= 0) return 0;
+    const int N = (Hq + 2 * Hkv) * D;
+    if (M > 128 || S <= 0 || D % 16 != 0 || N % kTileN != 0 || N > 8192 || K % (32 * S) != 0 || !x || !w ||
+        !part || !pos || !slot || !cos_sin || !q_out || !k_cache || !v_cache || max_pos <= 0 || variant < 0 ||
+        variant > 1 || (variant == 1 && K % (128 * S) != 0))
+        return hipErrorInvalidValue;
+    auto st = (hipStream_t)stream;
+    auto xx = (const uint16_t*)x;
+    auto ww = (const uint16_t*)w;
+    auto pp = (float*)part;
+    hipError_t e;
+    const int mt = (M + 15) / 16;
+    if (mt <= 2) e = launch_gemm<2>(xx, ww, pp, M, K, N, S, variant, st);
+    else if (mt <= 4) e = launch_gemm<4>(xx, ww, pp, M, K, N, S, variant, st);
+    else if (mt <= 6) e = launch_gemm<6>(xx, ww, pp, M, K, N, S, variant, st);
+    else e = launch_gemm<8>(xx, ww, pp, M, K, N, S, variant, st);
+    if (e != hipSuccess) return e;
+    if (kv8)
+        splitk_reduce_rope_kernel<true><<<M, kBlock, 0, st>>>(pp, S, M, (const int32_t*)pos, (const int32_t*)slot,
+                                                              (const float2*)cos_sin, (uint16_t*)q_out, k_cache,
+                                                              v_cache, Hq, Hkv, D, max_seq, max_pos, num_slots);
+    else
+        splitk_reduce_rope_kernel<false><<<M, kBlock, 0, st>>>(pp, S, M, (const int32_t*)pos, (const int32_t*)slot,
+                                                               (const float2*)cos_sin, (uint16_t*)q_out, k_cache,
+                                                               v_cache, Hq, Hkv, D, max_seq, max_pos, num_slots);
     return hipGetLastError();
 }
 

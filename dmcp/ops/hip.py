@@ -62,6 +62,8 @@ def lib() -> ctypes.CDLL:
             "dmcp_set_prefix_overlap": ([_i], _i),
             "dmcp_fused_gemm_max_rows": ([], _i),
             "dmcp_splitk_resid_norm": ([_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _i, _vp], _i),
+            "dmcp_splitk_rope_kv": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i,
+                                     _i, _i, _vp], _i),
             "dmcp_fused_gemm": ([_i, _i, _vp, _vp, _vp, _i, _i, _i, _f, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i,
                                  _i, _i, _i, _i, _vp], _i),
         }
@@ -589,6 +591,42 @@ def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, 
     _check(lib().dmcp_splitk_resid_norm(_ptr(x), _ptr(w), _ptr(workspace), _ptr(residual), _ptr(norm_w), _ptr(out),
                                         M, K, N, S, float(eps), variant, _stream()), "dmcp_splitk_resid_norm")
     return out
+
+
+def linear_rope_kv(x: torch.Tensor, w: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos_sin: torch.Tensor,
+                   k_cache: torch.Tensor, v_cache: torch.Tensor, n_q_heads: int, workspace: torch.Tensor,
+                   splits: int = 0, q_out: Optional[torch.Tensor] = None, variant: int = 1) -> torch.Tensor:
+    """rope_kv(F.linear(x, w), ...) in two launches (csrc/splitk_gemm.hip:
+    split-K MFMA GEMM into fp32 slabs, then per row the reduction, RoPE, the
+    q write and the K/V-cache append).  x [M, K] (M <= 128); returns q."""
+    S_, Hkv, MAXS, D = k_cache.shape
+    _req(x, torch.bfloat16, "linear_rope_kv.x")
+    _req(w, torch.bfloat16, "linear_rope_kv.w")
+    kv8 = _req_kv(k_cache, v_cache, "linear_rope_kv")
+    _req(pos, torch.int32, "linear_rope_kv.pos")
+    _req(slot, torch.int32, "linear_rope_kv.slot")
+    _req(cos_sin, torch.float32, "linear_rope_kv.cos_sin")
+    if x.dim() != 2 or w.dim() != 2 or x.shape[1] != w.shape[1]:
+        raise HipOpsError(f"linear_rope_kv: x {tuple(x.shape)} / w {tuple(w.shape)} are not [M, K] / [N, K]")
+    M, K = x.shape
+    N = w.shape[0]
+    S = splits or splitk_splits(N, K)
+    if variant not in (0, 1):
+        raise HipOpsError(f"linear_rope_kv: unknown variant {variant}")
+    if (v_cache.shape != k_cache.shape or N != (n_q_heads + 2 * Hkv) * D or D % 16 or N % 64 or N > 8192
+            or not 1 <= M <= SPLITK_MAX_ROWS or K % ((128 if variant == 1 else 32) * S)):
+        raise HipOpsError(f"linear_rope_kv: unsupported shape M={M} K={K} N={N} D={D} splits={S}")
+    if pos.numel() != M or slot.numel() != M or cos_sin.dim() != 3 or tuple(cos_sin.shape[1:]) != (D // 2, 2):
+        raise HipOpsError("linear_rope_kv: pos/slot/cos_sin shape mismatch")
+    if workspace.dtype != torch.float32 or not workspace.is_contiguous() or workspace.numel() < S * M * N:
+        raise HipOpsError(f"linear_rope_kv: workspace needs {S * M * N} contiguous fp32 elements")
+    if q_out is None:
+        q_out = torch.empty((M, n_q_heads, D), dtype=torch.bfloat16, device=x.device)
+    _req_out(q_out, torch.bfloat16, M * n_q_heads * D, "linear_rope_kv.q_out")
+    _check(lib().dmcp_splitk_rope_kv(_ptr(x), _ptr(w), _ptr(workspace), _ptr(pos), _ptr(slot), _ptr(cos_sin),
+                                     _ptr(q_out), _ptr(k_cache), _ptr(v_cache), M, K, n_q_heads, Hkv, D, MAXS,
+                                     cos_sin.shape[0], S_, kv8, S, variant, _stream()), "dmcp_splitk_rope_kv")
+    return q_out
 
 
 def fused_linear_norm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None,

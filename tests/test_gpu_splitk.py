@@ -50,3 +50,37 @@ def test_linear_resid_norm_rejects_bad_shapes(hip):
     x, w = _bf(129, 128), _bf(64, 128)
     with pytest.raises(hip.HipOpsError):
         hip.linear_resid_norm(x, w, _bf(129, 64), _bf(64), 1e-5, torch.empty(1 << 20, device="cuda"))
+
+
+@pytest.mark.parametrize("kv", ["bf16", "fp8"])
+@pytest.mark.parametrize("M", [5, 78, 128])
+@pytest.mark.parametrize("D,Hq,Hkv", [(64, 32, 8), (128, 16, 8)])
+def test_linear_rope_kv(hip, kv, M, D, Hq, Hkv):
+    """Split-K QKV + RoPE + cache append == F.linear -> rope_kv (the same
+    kernel path the model used before), q and both caches."""
+    from dmcp.ops import reference
+    K, S, MAXS = 2048, 4, 256
+    N = (Hq + 2 * Hkv) * D
+    x = _bf(M, K, seed=M + D)
+    w = _bf(N, K, seed=3, scale=0.03)
+    pos = (torch.arange(M, dtype=torch.int32, device="cuda") * 7) % MAXS
+    pos[-1] = -1  # a padding row: q written, caches untouched
+    slot = torch.arange(M, dtype=torch.int32, device="cuda") % S
+    cs = reference.rope_tables(MAXS, D, device="cuda")
+    dt = torch.uint8 if kv == "fp8" else torch.bfloat16
+    kc = torch.zeros(S, Hkv, MAXS, D, dtype=dt, device="cuda")
+    vc = torch.zeros_like(kc)
+    kr, vr = kc.clone(), vc.clone()
+    qkv = (x.float() @ w.float().t()).to(torch.bfloat16)
+    q_exp = hip.rope_kv(qkv, pos, slot, cs, kr, vr, Hq)
+    ws = torch.empty(hip.splitk_splits(N, K) * M * N, dtype=torch.float32, device="cuda")
+    for variant in (0, 1):
+        kc.zero_()
+        vc.zero_()
+        q = hip.linear_rope_kv(x, w, pos, slot, cs, kc, vc, Hq, ws, variant=variant)
+        torch.testing.assert_close(q.float(), q_exp.float(), atol=3e-2, rtol=2e-2)
+        kf, vf = (reference.kv_float(kc), reference.kv_float(vc)) if kv == "fp8" else (kc.float(), vc.float())
+        kfr, vfr = (reference.kv_float(kr), reference.kv_float(vr)) if kv == "fp8" else (kr.float(), vr.float())
+        tol = dict(atol=3e-2, rtol=0.13) if kv == "fp8" else dict(atol=3e-2, rtol=2e-2)
+        torch.testing.assert_close(kf, kfr, **tol)
+        torch.testing.assert_close(vf, vfr, **tol)

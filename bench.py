@@ -61,7 +61,10 @@ def main(argv=None) -> int:
     from dmcp.utils import synth
     from dmcp.utils.tracing import METRICS
 
-    cpus = os.cpu_count() or 8
+    try:
+        cpus = len(os.sched_getaffinity(0))  # the CPUs this process may run on (cgroup / cpuset aware)
+    except (AttributeError, OSError):
+        cpus = os.cpu_count() or 8
     threads = args.threads or max(1, min(16, cpus // max(1, ctx.local_world)))
     work = args.workdir or tempfile.mkdtemp(prefix=f"dmcp-bench-r{rank}-")
     repo = os.path.join(work, f"shop{rank}")

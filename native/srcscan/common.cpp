@@ -419,7 +419,9 @@ void parallel_for(size_t n, int threads, const std::function<void(size_t)>& fn) 
     if (n == 0) return;
     int hw = (int)std::thread::hardware_concurrency();
     if (hw <= 0) hw = 4;
-    int t = threads > 0 ? threads : hw;
+    // default: the machine's threads, at most 32 (a 256-thread host shares
+    // its CPUs among one process per GPU; ~2,000-file phases gain nothing past that)
+    int t = threads > 0 ? threads : std::min(hw, 32);
     if ((size_t)t > n) t = (int)n;
     if (t <= 1) {
         for (size_t i = 0; i < n; ++i) fn(i);

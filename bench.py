@@ -65,7 +65,9 @@ def main(argv=None) -> int:
         cpus = len(os.sched_getaffinity(0))  # the CPUs this process may run on (cgroup / cpuset aware)
     except (AttributeError, OSError):
         cpus = os.cpu_count() or 8
-    threads = args.threads or max(1, min(16, cpus // max(1, ctx.local_world)))
+    # 8 parser threads: the analysis is bound by its SQLite writer thread, 8 = 16 = 32 threads on one
+    # MI355X host (profiles/bench_r2_threads_ab.txt), and fewer leave CPUs to the other ranks
+    threads = args.threads or max(1, min(8, cpus // max(1, ctx.local_world)))
     work = args.workdir or tempfile.mkdtemp(prefix=f"dmcp-bench-r{rank}-")
     repo = os.path.join(work, f"shop{rank}")
     fqcns = synth.java_spring_repo(repo, n_classes=args.classes, base_package=f"co.acme.shop{rank}", seed=rank + 1)

@@ -222,6 +222,9 @@ class LocalLM:
                 and c.hidden % 64 == 0 and c.hidden <= 8192
                 and c.intermediate % (128 * ops.splitk_splits(c.hidden, c.intermediate)) == 0):
             self.splitk_down = ops.splitk_splits(c.hidden, c.intermediate)
+            # SwiGLU inside the operand staging: measured slower (2.61 vs 2.33 ms per fp8 step,
+            # profiles/decode_step_splitk_swiglu_ab.jsonl) -- opt-in
+            self.splitk_swiglu = os.environ.get("DMCP_SPLITK_SWIGLU", "0") == "1"
             self.splitk_ws = torch.empty(self.splitk_down * 128 * c.hidden, dtype=torch.float32, device=self.device)
 
     # ------------------------------------------------------------ weights
@@ -388,9 +391,13 @@ class LocalLM:
             h = ops.add_rmsnorm(o, self.w[f"l{i}.ln2"], c.eps, residual=resid)
             nxt = self.w[f"l{i + 1}.ln1"] if i + 1 < c.layers else self.w["norm_f"]
             if self.splitk_down and B <= 128:
-                act = ops.silu_mul(F.linear(h, self.w[f"l{i}.wgu"]))
-                h = ops.linear_resid_norm(act, self.w[f"l{i}.wdown"], resid, nxt, c.eps, self.splitk_ws,
-                                          splits=self.splitk_down)
+                gu = F.linear(h, self.w[f"l{i}.wgu"])
+                if self.splitk_swiglu:  # SwiGLU computed while the down GEMM stages its operand
+                    h = ops.linear_resid_norm(gu, self.w[f"l{i}.wdown"], resid, nxt, c.eps, self.splitk_ws,
+                                              splits=self.splitk_down, variant=2)
+                else:
+                    h = ops.linear_resid_norm(ops.silu_mul(gu), self.w[f"l{i}.wdown"], resid, nxt, c.eps,
+                                              self.splitk_ws, splits=self.splitk_down)
                 continue
             m = self._mlp(i, h)
             h = ops.add_rmsnorm(m, nxt, c.eps, residual=resid)

@@ -101,7 +101,20 @@ __global__ __launch_bounds__(kBlock) void splitk_gemm_kernel(const uint16_t* __r
 // XOR-swizzled by row (piece ^ (row & 7)) so a wave's ds_read_b128 of 16 rows
 // x 4 pieces is at most 2-way conflicted.  W stays register-direct with a
 // ring of 4 k-steps.  Needs the K slice to be a multiple of 128.
-template <int MT>
+// SWI: x is the gate/up GEMM output [M, 2K] and the operand is
+// silu(gate) * up, computed while the slice is staged into LDS (the SwiGLU
+// kernel's fp32 math and bf16 rounding), so the down projection reads the
+// gate/up rows directly and no SwiGLU launch or activation buffer exists.
+__device__ __forceinline__ uint4 swiglu8(const uint4& gv, const uint4& uv) {
+    float gf[8], uf[8], o[8];
+    unpack8(gv, gf);
+    unpack8(uv, uf);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = gf[j] / (1.f + __expf(-gf[j])) * uf[j];
+    return pack8(o);
+}
+
+template <int MT, bool SWI = false>
 __global__ __launch_bounds__(kBlock) void splitk_gemm_lds_kernel(const uint16_t* __restrict__ x,
                                                                  const uint16_t* __restrict__ w,
                                                                  float* __restrict__ part, int M, int K, int N,
@@ -126,24 +139,31 @@ __global__ __launch_bounds__(kBlock) void splitk_gemm_lds_kernel(const uint16_t*
     for (int i = 0; i < NP; ++i) {
         const int p = tid + i * kBlock;
         const int row = p >> 3, pc = p & 7;
-        xp[i] = x + (size_t)min(row, M - 1) * K + k0 + 8 * pc;
+        xp[i] = x + (size_t)min(row, M - 1) * (SWI ? 2 * K : K) + k0 + 8 * pc;
         so[i] = row * 8 + (pc ^ (row & 7));
     }
     f32x4_t acc[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    uint4 wr[4], xg[NP];
+    uint4 wr[4], xg[NP], xu[SWI ? NP : 1];
 #pragma unroll
     for (int j = 0; j < 4; ++j) wr[j] = *reinterpret_cast<const uint4*>(wp + 32 * min(j, steps - 1));
 #pragma unroll
-    for (int i = 0; i < NP; ++i) xs[0][so[i]] = *reinterpret_cast<const uint4*>(xp[i]);
+    for (int i = 0; i < NP; ++i) {
+        const uint4 a = *reinterpret_cast<const uint4*>(xp[i]);
+        if constexpr (SWI) xs[0][so[i]] = swiglu8(a, *reinterpret_cast<const uint4*>(xp[i] + K));
+        else xs[0][so[i]] = a;
+    }
     __syncthreads();
     for (int c = 0; c < chunks; c += 2) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {  // chunk c + h in buffer h
             const int cn = min(c + h + 1, chunks - 1);
 #pragma unroll
-            for (int i = 0; i < NP; ++i) xg[i] = *reinterpret_cast<const uint4*>(xp[i] + 64 * cn);
+            for (int i = 0; i < NP; ++i) {
+                xg[i] = *reinterpret_cast<const uint4*>(xp[i] + 64 * cn);
+                if constexpr (SWI) xu[i] = *reinterpret_cast<const uint4*>(xp[i] + K + 64 * cn);
+            }
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk) {
                 const int j = 2 * h + kk;  // ring slot of step 2 (c + h) + kk
@@ -160,7 +180,10 @@ __global__ __launch_bounds__(kBlock) void splitk_gemm_lds_kernel(const uint16_t*
                 wr[j] = *reinterpret_cast<const uint4*>(wp + 32 * min(2 * (c + h) + kk + 4, steps - 1));
             }
 #pragma unroll
-            for (int i = 0; i < NP; ++i) xs[h ^ 1][so[i]] = xg[i];
+            for (int i = 0; i < NP; ++i) {
+                if constexpr (SWI) xs[h ^ 1][so[i]] = swiglu8(xg[i], xu[i]);
+                else xs[h ^ 1][so[i]] = xg[i];
+            }
             __syncthreads();
         }
     }
@@ -327,7 +350,9 @@ __global__ __launch_bounds__(kBlock) void splitk_reduce_rope_kernel(
 template <int MT>
 hipError_t launch_gemm(const uint16_t* x, const uint16_t* w, float* part, int M, int K, int N, int S, int variant,
                        hipStream_t st) {
-    if (variant == 1)
+    if (variant == 2)
+        splitk_gemm_lds_kernel<MT, true><<<dim3(N / kTileN, S), kBlock, 0, st>>>(x, w, part, M, K, N, K / S);
+    else if (variant == 1)
         splitk_gemm_lds_kernel<MT><<<dim3(N / kTileN, S), kBlock, 0, st>>>(x, w, part, M, K, N, K / S);
     else
         splitk_gemm_kernel<MT><<<dim3(N / kTileN, S), kBlock, 0, st>>>(x, w, part, M, K, N, K / S);
@@ -341,12 +366,13 @@ extern "C" {
 // resid[M, N] += bf16(x[M, K] . w[N, K]^T); out = RMSNorm(resid) * g.
 // part: fp32 workspace of S * M * N.  Shapes checked by the host wrapper
 // (dmcp/ops/hip.py::linear_resid_norm); the checks here guard the tiling.
-// variant 0: register-direct X; 1: X staged through LDS (K % (128 S) == 0).
+// variant 0: register-direct X; 1: X staged through LDS (K % (128 S) == 0);
+// 2: as 1 with x = gate/up rows [M, 2K] and the operand silu(gate) * up.
 int dmcp_splitk_resid_norm(const void* x, const void* w, void* part, void* resid, const void* g, void* out, int M,
                            int K, int N, int S, float eps, int variant, void* stream) {
     if (M <= 0) return 0;
     if (M > 128 || S <= 0 || N % kTileN != 0 || K % (32 * S) != 0 || N % 8 != 0 || N > 8 * 4 * kBlock || !x ||
-        !w || !part || !resid || !g || !out || variant < 0 || variant > 1 || (variant == 1 && K % (128 * S) != 0))
+        !w || !part || !resid || !g || !out || variant < 0 || variant > 2 || (variant >= 1 && K % (128 * S) != 0))
         return hipErrorInvalidValue;
     auto st = (hipStream_t)stream;
     auto xx = (const uint16_t*)x;

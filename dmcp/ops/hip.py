@@ -567,19 +567,22 @@ def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, 
     -- F.linear + add_rmsnorm in two launches (csrc/splitk_gemm.hip: split-K
     MFMA GEMM into fp32 slabs, then one reduction per row that also adds the
     residual and normalises).  x [M, K] (M <= 128), w [N, K], residual [M, N];
-    workspace: fp32 with at least splits * M * N elements."""
+    workspace: fp32 with at least splits * M * N elements.  variant 2: x is
+    the gate/up output [M, 2K] and the operand silu(gate) * up (SwiGLU fused
+    into the operand staging)."""
     _req(x, torch.bfloat16, "linear_resid_norm.x")
     _req(w, torch.bfloat16, "linear_resid_norm.w")
     _req(residual, torch.bfloat16, "linear_resid_norm.residual")
     _req(norm_w, torch.bfloat16, "linear_resid_norm.norm_w")
-    if x.dim() != 2 or w.dim() != 2 or x.shape[1] != w.shape[1]:
+    xk = x.shape[1] // 2 if variant == 2 else x.shape[1]
+    if x.dim() != 2 or w.dim() != 2 or xk != w.shape[1] or (variant == 2 and x.shape[1] % 2):
         raise HipOpsError(f"linear_resid_norm: x {tuple(x.shape)} / w {tuple(w.shape)} are not [M, K] / [N, K]")
-    M, K = x.shape
+    M, K = x.shape[0], w.shape[1]
     N = w.shape[0]
     S = splits or splitk_splits(N, K)
-    if variant not in (0, 1):
+    if variant not in (0, 1, 2):
         raise HipOpsError(f"linear_resid_norm: unknown variant {variant}")
-    if not 1 <= M <= SPLITK_MAX_ROWS or N % 64 or N > 8192 or K % ((128 if variant == 1 else 32) * S):
+    if not 1 <= M <= SPLITK_MAX_ROWS or N % 64 or N > 8192 or K % ((128 if variant >= 1 else 32) * S):
         raise HipOpsError(f"linear_resid_norm: unsupported shape M={M} K={K} N={N} splits={S}")
     if tuple(residual.shape) != (M, N) or norm_w.numel() != N:
         raise HipOpsError("linear_resid_norm: residual / norm weight shape mismatch")

@@ -84,3 +84,26 @@ def test_linear_rope_kv(hip, kv, M, D, Hq, Hkv):
         tol = dict(atol=3e-2, rtol=0.13) if kv == "fp8" else dict(atol=3e-2, rtol=2e-2)
         torch.testing.assert_close(kf, kfr, **tol)
         torch.testing.assert_close(vf, vfr, **tol)
+
+
+@pytest.mark.parametrize("M", [3, 78, 128])
+def test_linear_resid_norm_swiglu_operand(hip, M):
+    """variant 2 reads the gate/up rows and stages silu(gate) * up: equal to
+    silu_mul -> linear_resid_norm (and to the fp32 reference)."""
+    from dmcp.ops import reference
+    N, I = 512, 1024
+    gu = _bf(M, 2 * I, seed=M, scale=2.0)
+    w = _bf(N, I, seed=9, scale=0.03)
+    resid = _bf(M, N, seed=10)
+    g = _bf(N, seed=11)
+    ws = torch.empty(hip.splitk_splits(N, I) * M * N, dtype=torch.float32, device="cuda")
+    act = hip.silu_mul(gu)
+    r1, r2 = resid.clone(), resid.clone()
+    exp = hip.linear_resid_norm(act, w, r1, g, 1e-5, ws, variant=1)
+    got = hip.linear_resid_norm(gu, w, r2, g, 1e-5, ws, variant=2)
+    torch.testing.assert_close(got.float(), exp.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(r2.float(), r1.float(), atol=2e-2, rtol=2e-2)
+    r3 = resid.clone()
+    y = (reference.silu_mul(gu).float() @ w.float().t()).to(torch.bfloat16)
+    ref = reference.add_rmsnorm(y, g, 1e-5, residual=r3)
+    torch.testing.assert_close(got.float(), ref.float(), atol=4e-2, rtol=4e-2)

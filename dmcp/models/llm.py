@@ -377,7 +377,7 @@ class LocalLM:
         if self.use_fused and B <= self.fused_max_rows:
             return self._decode_fused(tokens, slots, positions)
         seq_len = positions + 1
-        chunk, splits = ops.decode_plan(B, c.n_kv_heads, c.max_seq)
+        chunk, splits = ops.decode_plan(B, c.n_kv_heads, c.max_seq, c.kv_dtype)
         x = ops.embedding(self.w["embed"], tokens)
         resid = x.clone()
         h = ops.add_rmsnorm(x, self.w["l0.ln1"], c.eps)
@@ -417,7 +417,7 @@ class LocalLM:
         c = self.cfg
         B = tokens.shape[0]
         seq_len = positions + 1
-        chunk, splits = ops.decode_plan(B, c.n_kv_heads, c.max_seq)
+        chunk, splits = ops.decode_plan(B, c.n_kv_heads, c.max_seq, c.kv_dtype)
         r = ops.embedding(self.w["embed"], tokens)
         for i in range(c.layers):
             kc, vc = self.k_cache[i], self.v_cache[i]

@@ -30,10 +30,14 @@ def decode_chunk(rows, n_kv_heads, max_seq):
     return _dc(rows, n_kv_heads, max_seq)
 
 
-def decode_plan(rows, n_kv_heads, max_seq):
-    """(chunk, splits) of the per-row decode attention (see :func:`dmcp.ops.hip.decode_plan`)."""
+def decode_plan(rows, n_kv_heads, max_seq, kv_dtype: str = "bf16"):
+    """(chunk, splits) of the per-row decode attention (see :func:`dmcp.ops.hip.decode_plan`).
+    An fp8 cache halves the bytes per key, so fewer, longer splits keep the
+    same bytes in flight: 2,048 target waves instead of 4,096 (fp8 step 2.35
+    -> 2.30 ms at 78 rows, 5.54 -> 5.36 at 320; bf16 2.84 vs 2.94 the other
+    way -- profiles/decode_target_waves_r2.txt)."""
     from .hip import decode_plan as _dp
-    return _dp(rows, n_kv_heads, max_seq)
+    return _dp(rows, n_kv_heads, max_seq, target_waves=2048 if kv_dtype == "fp8" else 4096)
 
 
 PREFIX_MFMA_MAX_SPLITS = 16  # shared-prefix key splits on the prefill kernel (dmcp.ops.hip)

@@ -7,7 +7,7 @@ attention, SwiGLU MLP, untied LM head, bf16 weights and KV cache.
 
 MI355X mapping:
 
-* small decode steps (<= ``fused_max_rows`` = 32 rows: the tail of a batch,
+* small decode steps (<= ``fused_max_rows`` = 16 rows: the tail of a batch,
   single requests) run every weight product on the fused gfx950 MFMA GEMMs
   of :mod:`dmcp.ops` (``csrc/fused_gemm.hip``): RMSNorm folded into the
   QKV / gate-up / LM-head prologue (norm weights are folded into those
@@ -209,7 +209,10 @@ class LocalLM:
         # slot -> shared-prefix length its prefill reads in place from the
         # prefix slot (fork_prefix without a copy; prefill kernel only)
         self._slot_prefix: Dict[int, int] = {}
-        self.fused_max_rows = min(ops.FUSED_MAX_ROWS, int(os.environ.get("DMCP_FUSED_MAX_ROWS", "32")))
+        # crossover with the hipBLASLt + split-K-down path measured at ~20 rows
+        # (fp8: fused 1.47 vs 1.64 ms at 16 rows, 1.80 vs 1.70 at 24, 1.82 vs
+        # 1.73 at 32 -- profiles/decode_fused_rows_r2.txt)
+        self.fused_max_rows = min(ops.FUSED_MAX_ROWS, int(os.environ.get("DMCP_FUSED_MAX_ROWS", "16")))
         ps = max(ops.prefix_splits(c.max_seq, self.PREFIX_CHUNK), ops.PREFIX_MFMA_MAX_SPLITS) if shared_prefix else 0
         self.attn_ws = (ops.decode_workspace(self.max_rows, c.n_heads, c.n_kv_heads, c.head_dim, c.max_seq,
                                              self.device, prefix_slots=ps) if self.device.type == "cuda" else None)

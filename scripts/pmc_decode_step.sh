@@ -1,6 +1,7 @@
 #!/usr/bin/env bash
 # PMC counters of the decode step's kernels (bench_step.py defaults, 20 steps):
-# one rocprofv3 pass per counter set, summed per kernel family.
+# one rocprofv3 pass per counter set, summed per kernel family.  Extra
+# arguments go to bench_step.py (e.g. --kv-dtype fp8).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -12,7 +13,7 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_INST
            "FETCH_SIZE SQ_INSTS_VMEM_RD"; do
     i=$((i + 1))
     timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d "$ROOT/gpurun_out/pmcd$i" -o p \
-        -- python3 "$ROOT/scripts/bench_step.py" --iters 20 > "$ROOT/gpurun_out/pmcd$i.log" 2>&1 || exit $?
+        -- python3 "$ROOT/scripts/bench_step.py" --iters 20 "$@" > "$ROOT/gpurun_out/pmcd$i.log" 2>&1 || exit $?
 done
 python3 - "$ROOT/gpurun_out" <<'PY'
 import csv, glob, sys, collections

@@ -79,7 +79,7 @@ class App:
         self.config = config or Config.from_env()
         self.db = db or open_database(self.config)
         self.repos = Repositories(self.db)
-        self.cache = GraphCache(self.repos.projects)
+        self.cache = GraphCache(self.repos.projects, refresh_s=self.config.graph_refresh_seconds or None)
         self.git = GitClient(self.config.git_clone_base_path, self.config.git_ssh_key_path,
                              self.config.git_timeout_seconds)
         self.backend = backend if backend is not None else create_backend(self.config)
@@ -91,7 +91,9 @@ class App:
                                require_enrichment=self.config.require_enrichment_for_analyze,
                                max_source_chars=self.config.enrich_max_source_chars,
                                in_memory_sources=self.config.git_in_memory,
-                               in_memory_max_bytes=self.config.git_in_memory_max_mb << 20)
+                               in_memory_max_bytes=self.config.git_in_memory_max_mb << 20,
+                               lease_ttl_s=self.config.project_lease_seconds,
+                               stream_enrichment=self.config.enrich_stream)
         self.projects = ProjectService(self.repos, self.cache)
         self.context = ContextService(self.repos, self.cache)
         self.graph_query = GraphQueryService(self.cache)
@@ -104,10 +106,17 @@ class App:
 
     def recover_stuck_projects(self) -> int:
         """A project left ANALYZING/SYNCING by a dead process is moved to ERROR
-        (the reference leaves it unrecoverable)."""
+        (the reference leaves it unrecoverable).  Only projects
+        whose lease is free or expired: a live operation of another process
+        (the analysis service while this MCP server starts) keeps its status."""
+        import time as _time
         n = 0
+        now = _time.time()
         for status in (ProjectStatus.ANALYZING, ProjectStatus.SYNCING):
             for p in self.repos.projects.find_by_status(status):
+                owner, until = self.repos.projects.lease_of(p.id)
+                if owner is not None and until is not None and float(until) >= now:
+                    continue
                 p.mark_error()
                 self.repos.projects.update_status(p)
                 n += 1

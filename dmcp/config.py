@@ -49,6 +49,14 @@ class Config:
     local_llm_kv_dtype: str = "bf16"  # "fp8": e4m3 KV cache (half the decode attention bytes)
     local_llm_max_new_tokens: int = 256
     local_llm_devices: str = "all"
+    # "process": one worker process per GPU, started before this process
+    # touches HIP (the service default); "inline": engines in this process
+    local_llm_workers: str = "process"
+    local_llm_max_batch: int = 256      # KV slots (concurrent sequences) per GPU
+    # enrichment hands the backend every pending class as one stream (a local
+    # engine keeps its continuous batch full); false = the reference's
+    # barriers of enrich_batch_size classes
+    enrich_stream: bool = True
     # git (application.yml:44-47)
     git_clone_base_path: str = "/tmp/domain-mcp-repos"
     git_ssh_key_path: Optional[str] = None
@@ -72,6 +80,14 @@ class Config:
     # SQLite: WAL checkpoints on a background thread (dmcp/store/db.py::_Checkpointer)
     db_background_checkpoint: bool = True
     recover_stuck_on_start: bool = True
+    # cross-process project lease (dmcp/index/lease.py) and graph-cache freshness
+    project_lease_seconds: float = 60.0
+    graph_refresh_seconds: float = 1.0
+    # source scan isolation: "auto" (a child process for remote repositories),
+    # "process" (always), "inline" (never); a hung or crashed scan becomes
+    # ANALYSIS_FAILED after scan_timeout_seconds (GoSourceParser.java:62)
+    scan_isolation: str = "auto"
+    scan_timeout_seconds: float = 120.0
     log_level: str = "INFO"
 
     @classmethod
@@ -100,6 +116,9 @@ class Config:
             "LOCAL_LLM_KV_DTYPE": "local_llm_kv_dtype",
             "LOCAL_LLM_MAX_NEW_TOKENS": "local_llm_max_new_tokens",
             "LOCAL_LLM_DEVICES": "local_llm_devices",
+            "LOCAL_LLM_WORKERS": "local_llm_workers",
+            "LOCAL_LLM_MAX_BATCH": "local_llm_max_batch",
+            "ENRICH_STREAM": "enrich_stream",
             "GIT_CLONE_BASE_PATH": "git_clone_base_path",
             "GIT_SSH_KEY_PATH": "git_ssh_key_path",
             "GIT_TIMEOUT_SECONDS": "git_timeout_seconds",
@@ -112,6 +131,10 @@ class Config:
             "PARSER_THREADS": "parser_threads",
             "DB_BACKGROUND_CHECKPOINT": "db_background_checkpoint",
             "RECOVER_STUCK_ON_START": "recover_stuck_on_start",
+            "PROJECT_LEASE_SECONDS": "project_lease_seconds",
+            "GRAPH_REFRESH_SECONDS": "graph_refresh_seconds",
+            "SCAN_ISOLATION": "scan_isolation",
+            "SCAN_TIMEOUT_SECONDS": "scan_timeout_seconds",
             "LOG_LEVEL": "log_level",
         }
         updates: Dict[str, Any] = {}

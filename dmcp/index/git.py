@@ -203,9 +203,12 @@ class GitClient:
         if not self.commit_exists(repo_dir, old_commit):
             LOG.warning("Old commit %s not found (force push?), treating as full resync", old_commit)
             return GitDiffResult.full_resync(new_commit)
-        out = self._git(["diff", "--name-status", "-M", "-C", "--no-color", old_commit, new_commit],
+        # -z: NUL-separated records with raw paths.  Without it git quotes
+        # any path with a non-ASCII byte ("src/acm\303\251/A.java"), which
+        # then matches no parsed file and the class is wrongly "unchanged"
+        out = self._git(["diff", "-z", "--name-status", "-M", "-C", "--no-color", old_commit, new_commit],
                         cwd=repo_dir)[1]
-        return parse_name_status(out, new_commit)
+        return parse_name_status_z(out, new_commit)
 
     @staticmethod
     def cleanup(directory: Optional[str]) -> None:
@@ -213,7 +216,44 @@ class GitClient:
             shutil.rmtree(directory, ignore_errors=True)
 
 
+def parse_name_status_z(text: str, new_commit: str) -> GitDiffResult:
+    """``git diff -z --name-status -M -C`` output: a status token, then one
+    path (A/M/T/D/U) or two (R<score>/C<score>: source, destination), each
+    NUL-terminated -- the JGit ``DiffEntry`` classification of
+    ``ProjectSyncService.computeDiff`` (:497-542): ADD/MODIFY/COPY -> changed,
+    DELETE -> deleted, RENAME -> both."""
+    changed, deleted = set(), set()
+    tok = text.split("\0")
+    i, n = 0, len(tok)
+    while i < n:
+        status = tok[i].strip()
+        if not status:
+            i += 1
+            continue
+        kind = status[:1]
+        if kind in ("R", "C"):
+            if i + 2 >= n:
+                break
+            src, dst = tok[i + 1], tok[i + 2]
+            if kind == "R":
+                deleted.add(src)
+            changed.add(dst)
+            i += 3
+            continue
+        if i + 1 >= n:
+            break
+        path = tok[i + 1]
+        if kind == "D":
+            deleted.add(path)
+        elif kind in ("A", "M", "T", "U"):
+            changed.add(path)
+        i += 2
+    return GitDiffResult.of(new_commit, changed, deleted)
+
+
 def parse_name_status(text: str, new_commit: str) -> GitDiffResult:
+    """Line form (no ``-z``; ASCII paths only) -- kept for callers that
+    already hold such output."""
     changed, deleted = set(), set()
     for line in text.splitlines():
         if not line.strip():

@@ -48,6 +48,7 @@ from ..store.repositories import ProjectRowsWriter, Repositories, to_iso
 from ..utils.errors import DomainError
 from ..utils.tracing import METRICS, span
 from .git import GitClient
+from .lease import ProjectLease
 from .source import CheckoutTree, SourceTree
 
 LOG = logging.getLogger(__name__)
@@ -156,7 +157,10 @@ class Indexer:
                  max_readme_length: int = 10_000, description_length: int = 500,
                  parser_threads: int = 0, require_enrichment: bool = True,
                  max_source_chars: int = 200_000, in_memory_sources: bool = True,
-                 in_memory_max_bytes: int = 1 << 30) -> None:
+                 in_memory_max_bytes: int = 1 << 30, lease_ttl_s: float = 60.0,
+                 stream_enrichment: bool = True) -> None:
+        self.lease_ttl_s = lease_ttl_s
+        self.stream_enrichment = stream_enrichment
         self.in_memory_sources = in_memory_sources
         self.in_memory_max_bytes = in_memory_max_bytes
         self.repos = repos
@@ -203,23 +207,22 @@ class Indexer:
                 fetch.set_exception(e)
         try:
             with span("analyze.prepare", stats):
-                project = self._prepare_project(url, branch_name)
+                project, lease = self._prepare_project(url, branch_name)
         except BaseException:
             self._discard_fetch(fetch)
             lock.release()  # a failed status write must not leave the repository locked
             raise
         try:
             with span("analyze.total", stats, project=project.name):
-                # the row swap's transaction opens now: the old rows are
-                # deleted on the writer thread while the snapshot is read and
-                # parsed (rolled back if either fails)
-                try:
-                    writer = self.repos.project_rows_writer(project.id, True)
-                except BaseException:
-                    self._discard_fetch(fetch)
-                    raise
                 with span("analyze.clone", stats):  # what is left of the read after the above
                     clone, stats["analyze.fetch"] = fetch.result()
+                # the row swap's transaction (SQLite: BEGIN IMMEDIATE, the
+                # database's write lock) opens only now that the snapshot is
+                # read -- a remote clone can take far longer than other
+                # writers' busy timeout; the old rows are deleted on the
+                # writer thread while the tree is parsed (rolled back if the
+                # parse fails)
+                writer = self.repos.project_rows_writer(project.id, True)
                 readme = clone.readme(self.max_readme_length)
                 if readme is not None:
                     project.update_description(readme[:self.description_length])
@@ -249,6 +252,7 @@ class Indexer:
                     if fix_missed:
                         with span("analyze.phase3", stats):
                             recovered = self._recover_unenriched(project, parsed, graph, clone, readme)
+                lease.check()  # never publish over an operation that took the project over
                 with span("analyze.persist_graph", stats):
                     project.base_package = common_package_prefix({package_name_of(i) for i in parsed.units})
                     project.update_graph_data(graph.to_json())
@@ -286,6 +290,7 @@ class Indexer:
             with span("analyze.cleanup", stats):
                 if clone is not None:
                     clone.cleanup()
+            lease.release()
             lock.release()
 
     def _submit_io(self, fn, *args):
@@ -321,23 +326,40 @@ class Indexer:
         """Analyzes a local git working tree (``file://`` clone of HEAD)."""
         return self.analyze_project(os.path.abspath(path), branch=None, fix_missed=fix_missed)
 
-    def _prepare_project(self, url: RepositoryUrl, branch: str) -> Project:
+    def _lease(self, project: Project) -> ProjectLease:
+        """Takes the project's cross-process lease (``PROJECT_BUSY`` if held)."""
+        return ProjectLease(self.repos.projects, project.id, self.lease_ttl_s, project.name).acquire()
+
+    def _prepare_project(self, url: RepositoryUrl, branch: str) -> Tuple[Project, ProjectLease]:
         # the old graph is never read: a successful analysis replaces it, a
         # failed one only writes the status
         project = self.repos.projects.find_by_repository_url(url, with_graph=False)
         if project is None:
             project = Project.create(url.repository_name(), url, branch)
-            self.repos.projects.save(project)
-            LOG.info("Created new project: %s", project.id)
-        else:
+            try:
+                self.repos.projects.save(project)
+                LOG.info("Created new project: %s", project.id)
+            except Exception:
+                # another process registered the repository first (UNIQUE repository_url)
+                project = self.repos.projects.find_by_repository_url(url, with_graph=False)
+                if project is None:
+                    raise
+        lease = self._lease(project)
+        try:
+            # the status as the previous holder left it, read under the lease
+            project = self.repos.projects.find_by_repository_url(url, with_graph=False) or project
             if project.status.is_processing():
-                LOG.warning("Project %s was left in %s by a previous process; recovering",
+                # we hold the lease, so that holder's lease ran out: it died
+                LOG.warning("Project %s was left in %s by a process that stopped; recovering",
                             project.name, project.status.value)
                 project.mark_error()
             project.default_branch = branch
-        project.start_analysis()
-        self.repos.projects.update_status(project)
-        return project
+            project.start_analysis()
+            self.repos.projects.update_status(project)
+        except BaseException:
+            lease.release()
+            raise
+        return project, lease
 
     def _mark_error(self, project: Project) -> None:
         try:
@@ -599,6 +621,11 @@ class Indexer:
         lock = self._locks.get(project.repository_url.value)
         if not lock.acquire(blocking=False):
             raise DomainError(f"Project {project.name} is already being processed", "PROJECT_BUSY")
+        try:
+            lease = self._lease(project)
+        except BaseException:
+            lock.release()
+            raise
         clone = None
         stats: Dict[str, float] = {}
         try:
@@ -626,6 +653,7 @@ class Indexer:
                     self.repos.params.save_rows(param_rows)
                 project.update_graph_data(graph.to_json())
                 project.base_package = common_package_prefix({package_name_of(i) for i in parsed.units})
+                lease.check()
                 self.repos.projects.update(project)
                 self.cache.put(project_id, project.name, graph)
             return {"success": True, "projectId": project_id, "bound": bound,
@@ -638,6 +666,7 @@ class Indexer:
         finally:
             if clone is not None:
                 clone.cleanup()
+            lease.release()
             lock.release()
 
     def _attach_metadata(self, graph: ProjectGraph, parsed: ParsedProject, by_name: Dict[str, SourceClass],
@@ -689,11 +718,20 @@ class Indexer:
         lock = self._locks.get(project.repository_url.value)
         if not lock.acquire(blocking=False):
             return SyncResult.failure(project.name, "project is already being processed")
+        try:
+            lease = self._lease(project)
+        except DomainError:
+            lock.release()
+            return SyncResult.failure(project.name, "project is already being processed")
+        except BaseException:
+            lock.release()
+            raise
         clone = None
         stats: Dict[str, float] = {}
         try:
+            project = self.repos.projects.find_by_id(project.id) or project  # state under the lease
             if project.status.is_processing():
-                project.mark_error()  # stale status from a dead process
+                project.mark_error()  # we hold the lease: the process that left it there stopped
             project.start_sync()
             self.repos.projects.update_status(project)
             with span("sync.total", stats, project=project.name):
@@ -735,13 +773,18 @@ class Indexer:
                         self.repos.params.delete_by_class_ids(ids)
                         self.repos.methods.delete_by_class_ids(ids)
                         self.repos.classes.delete_by_ids(ids)
+                    # updated classes keep their row (and id); their methods and
+                    # parameter links are replaced -- one statement per table for
+                    # all of them, not N round trips (Postgres)
+                    upd_ids = [by_name[i].id for i in to_update]
+                    self.repos.params.delete_by_class_ids(upd_ids)
+                    self.repos.methods.delete_by_class_ids(upd_ids)
+                    conn.executemany("UPDATE source_classes SET commit_hash = ?, class_type = ?, source_file = ? "
+                                     "WHERE id = ?", [(head, new_ids[i].class_type.value, new_ids[i].source_file,
+                                                      by_name[i].id) for i in to_update])
                     for ident in to_update:
                         sc = by_name[ident]
                         unit = new_ids[ident]
-                        self.repos.params.delete_by_class_ids([sc.id])
-                        self.repos.methods.delete_by_class_id(sc.id)
-                        conn.execute("UPDATE source_classes SET commit_hash = ?, class_type = ?, source_file = ? "
-                                     "WHERE id = ?", (head, unit.class_type.value, unit.source_file, sc.id))
                         graph.bind_class_id(ident, sc.id)
                         mids = []
                         for sm in unit.methods:
@@ -788,6 +831,7 @@ class Indexer:
                 project.base_package = common_package_prefix({package_name_of(i) for i in parsed.units})
                 project.update_graph_data(graph.to_json())
                 project.sync_completed(head)
+                lease.check()
                 self.repos.projects.update(project)
                 self.cache.put(project.id, project.name, graph)
             LOG.info("Sync completed for %s. Added: %d, Updated: %d, Deleted: %d, Unchanged: %d, Enriched: %d, "
@@ -802,6 +846,7 @@ class Indexer:
         finally:
             if clone is not None:
                 clone.cleanup()
+            lease.release()
             lock.release()
 
     def _relink_graph_only(self, graph: ProjectGraph, parsed: ParsedProject, classes: Dict[str, SourceClass],
@@ -848,19 +893,30 @@ class Indexer:
             raise DomainError(f"Project not found: {project_id}", "PROJECT_NOT_FOUND")
         if not self.backend.enabled:
             raise DomainError("No enrichment backend configured", "READ_ONLY_MODE")
-        cached = self.cache.get_graph(project_id)
-        graph = cached.copy() if cached is not None else (
-            ProjectGraph.from_json(project.graph_data) if project.graph_data else None)
-        if graph is None:
-            raise DomainError("No graph data available for this project", "NO_GRAPH")
-        clone = self._fetch(project.repository_url, project.default_branch, shallow=True)
+        lock = self._locks.get(project.repository_url.value)
+        if not lock.acquire(blocking=False):
+            raise DomainError(f"Project {project.name} is already being processed", "PROJECT_BUSY")
+        clone = None
         try:
-            parsed = parser_for(clone.detect_language(), self.parser_threads).scan_tree(clone)
-            readme = clone.readme(self.max_readme_length)
-            recovered = self._recover_unenriched(project, parsed, graph, clone, readme)
-            project.update_graph_data(graph.to_json())
-            self.repos.projects.update(project)
-            self.cache.put(project.id, project.name, graph)
-            return {"success": True, "projectId": project_id, "recovered": recovered}
+            # resume writes enrichment onto the project's rows: it must not
+            # race an analyze / sync that is replacing them (same lease)
+            with self._lease(project) as lease:
+                project = self.repos.projects.find_by_id(project_id) or project
+                cached = self.cache.get_graph(project_id)
+                graph = cached.copy() if cached is not None else (
+                    ProjectGraph.from_json(project.graph_data) if project.graph_data else None)
+                if graph is None:
+                    raise DomainError("No graph data available for this project", "NO_GRAPH")
+                clone = self._fetch(project.repository_url, project.default_branch, shallow=True)
+                parsed = parser_for(clone.detect_language(), self.parser_threads).scan_tree(clone)
+                readme = clone.readme(self.max_readme_length)
+                recovered = self._recover_unenriched(project, parsed, graph, clone, readme)
+                project.update_graph_data(graph.to_json())
+                lease.check()
+                self.repos.projects.update(project)
+                self.cache.put(project.id, project.name, graph)
+                return {"success": True, "projectId": project_id, "recovered": recovered}
         finally:
-            clone.cleanup()
+            if clone is not None:
+                clone.cleanup()
+            lock.release()

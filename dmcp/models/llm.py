@@ -103,6 +103,17 @@ PRESETS: Dict[str, LMConfig] = {
 }
 
 
+def fused_shapes_ok(c: LMConfig) -> bool:
+    """The fused decode GEMMs' shape contract (``dmcp.ops.hip._fused_xw`` and
+    the ``fused_*`` wrappers): every reduction depth a multiple of 32 (hidden
+    for QKV / gate-up / LM head, heads x head_dim for O, intermediate for
+    down), head_dim a multiple of 32 (RoPE epilogue), and the residual / LM
+    head widths multiples of 16.  A checkpoint outside it (vocab 32001,
+    50257, ...) keeps every decode step on the hipBLASLt path."""
+    return (c.hidden % 32 == 0 and (c.n_heads * c.head_dim) % 32 == 0 and c.intermediate % 32 == 0
+            and c.head_dim % 32 == 0 and c.vocab_size % 16 == 0 and c.hidden % 16 == 0)
+
+
 def preset(name: str, **overrides) -> LMConfig:
     if name not in PRESETS:
         raise ValueError(f"unknown model preset {name!r}; choose one of {sorted(PRESETS)}")
@@ -201,7 +212,8 @@ class LocalLM:
                                       device=self.device) if shared_prefix else None)
         # fused decode GEMMs for steps of <= fused_max_rows rows (GPU only;
         # DMCP_FUSED_GEMM=0 forces the hipBLASLt path)
-        self.use_fused = self.device.type == "cuda" and os.environ.get("DMCP_FUSED_GEMM", "1") != "0"
+        self.use_fused = (self.device.type == "cuda" and os.environ.get("DMCP_FUSED_GEMM", "1") != "0"
+                          and fused_shapes_ok(c))
         # prefill / extend attention on the MFMA kernel (csrc/prefill_attn.hip);
         # DMCP_PREFILL_KERNEL=0 forces the SDPA path
         self.use_prefill_kernel = (self.device.type == "cuda" and os.environ.get("DMCP_PREFILL_KERNEL", "1") != "0"

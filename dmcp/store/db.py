@@ -212,6 +212,15 @@ CREATE INDEX idx_source_methods_http_endpoints
     WHERE http_method IS NOT NULL AND http_path IS NOT NULL;
 CREATE INDEX idx_method_params_class ON method_parameters(class_id);
 """),
+    (7, "project_lease_and_graph_version", """
+-- Cross-process project lease (analyze / sync / rebuild / resume take it with
+-- a conditional UPDATE and heartbeat it; lease_until is epoch seconds) and a
+-- graph version bumped by every full project update, which lets the graph
+-- cache of another process (the MCP server) notice a re-analysis.
+ALTER TABLE projects ADD COLUMN lease_owner TEXT;
+ALTER TABLE projects ADD COLUMN lease_until REAL;
+ALTER TABLE projects ADD COLUMN graph_version INTEGER NOT NULL DEFAULT 0;
+"""),
 ]
 
 # New database files use 16 KiB pages (SQLite's default is 4 KiB): fewer

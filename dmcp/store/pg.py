@@ -139,6 +139,11 @@ CREATE INDEX IF NOT EXISTS idx_method_params_class ON method_parameters(class_id
     (2, "project_base_package", """
 ALTER TABLE projects ADD COLUMN IF NOT EXISTS base_package TEXT;
 """),
+    (3, "project_lease_and_graph_version", """
+ALTER TABLE projects ADD COLUMN IF NOT EXISTS lease_owner VARCHAR(200);
+ALTER TABLE projects ADD COLUMN IF NOT EXISTS lease_until DOUBLE PRECISION;
+ALTER TABLE projects ADD COLUMN IF NOT EXISTS graph_version INTEGER NOT NULL DEFAULT 0;
+"""),
 ]
 
 
@@ -170,8 +175,11 @@ class PgDatabase:
         t = self.target
         c = PgConnection(t.host, t.port, t.user, t.password, t.database, sslmode=t.sslmode, options=t.options)
         if t.schema:
-            ident = '"' + t.schema.replace('"', '""') + '"'
-            c.execute_script(f"CREATE SCHEMA IF NOT EXISTS {ident}; SET search_path TO {ident}")
+            # only the search path per connection: CREATE SCHEMA needs CREATE on
+            # the database even when the schema exists, which a least-privilege
+            # application role (the reference's Flyway-managed deployment) lacks;
+            # the schema is created once, by migrate()
+            c.execute_script(f"SET search_path TO {self._schema_ident()}")
         with self._conns_lock:
             self._conns.append(c)
         return c
@@ -229,8 +237,16 @@ class PgDatabase:
         return rows[0] if rows else None
 
     # ------------------------------------------------------------ migration
+    def _schema_ident(self) -> str:
+        return '"' + (self.target.schema or "").replace('"', '""') + '"'
+
     def migrate(self) -> int:
         conn = self.conn
+        if self.target.schema:
+            try:
+                conn.raw.execute_script(f"CREATE SCHEMA IF NOT EXISTS {self._schema_ident()}")
+            except PgError as e:  # no CREATE privilege: the schema must already exist
+                LOG.info("CREATE SCHEMA %s skipped: %s", self.target.schema, e)
         conn.execute("CREATE TABLE IF NOT EXISTS dmcp_schema_version (version INTEGER PRIMARY KEY, "
                      "description TEXT, installed_on TIMESTAMP DEFAULT CURRENT_TIMESTAMP)")
         done = {r[0] for r in conn.execute("SELECT version FROM dmcp_schema_version").fetchall()}

@@ -112,9 +112,51 @@ class ProjectRepository:
                  to_iso(p.last_analyzed_at), p.last_commit_hash, to_iso(p.created_at),
                  to_iso(p.updated_at), p.description, p.graph_data, p.base_package))
 
+    # a full update replaces the graph: its version moves, so the graph cache
+    # of every other process reloads it (GraphCache.refresh)
     UPDATE = ("UPDATE projects SET name=?, default_branch=?, status=?, last_analyzed_at=?, "
-              "last_commit_hash=?, updated_at=?, description=?, graph_data=?, base_package=? "
-              "WHERE id=?")
+              "last_commit_hash=?, updated_at=?, description=?, graph_data=?, base_package=?, "
+              "graph_version = graph_version + 1 WHERE id=?")
+
+    # -------------------------------------------------------------- lease
+    # One operation (analyze / sync / rebuild / resume) per project across
+    # every process sharing the database: the lease is taken with ONE
+    # conditional UPDATE (atomic under SQLite's write lock and PostgreSQL's
+    # row lock), heartbeated while the operation runs and released at its
+    # end.  A crashed holder stops heartbeating, so its lease expires and the
+    # next operation takes over (the reference's state machine instead
+    # wedged a crashed ANALYZING project forever, ProjectStateMachine.java:34-70).
+    ACQUIRE_LEASE = ("UPDATE projects SET lease_owner = ?, lease_until = ? WHERE id = ? AND "
+                     "(lease_owner IS NULL OR lease_until IS NULL OR lease_until < ? OR lease_owner = ?)")
+    RENEW_LEASE = "UPDATE projects SET lease_until = ? WHERE id = ? AND lease_owner = ?"
+    RELEASE_LEASE = "UPDATE projects SET lease_owner = NULL, lease_until = NULL WHERE id = ? AND lease_owner = ?"
+
+    def try_acquire_lease(self, project_id: str, owner: str, ttl_s: float, now: float) -> bool:
+        with self.db.transaction() as c:
+            cur = c.execute(self.ACQUIRE_LEASE, (owner, now + ttl_s, project_id, now, owner))
+            return cur.rowcount == 1
+
+    def renew_lease(self, project_id: str, owner: str, until: float) -> bool:
+        with self.db.transaction() as c:
+            return c.execute(self.RENEW_LEASE, (until, project_id, owner)).rowcount == 1
+
+    def release_lease(self, project_id: str, owner: str) -> bool:
+        with self.db.transaction() as c:
+            return c.execute(self.RELEASE_LEASE, (project_id, owner)).rowcount == 1
+
+    def lease_of(self, project_id: str) -> Tuple[Optional[str], Optional[float]]:
+        row = self.db.query_one("SELECT lease_owner, lease_until FROM projects WHERE id = ?", (project_id,))
+        return (row["lease_owner"], row["lease_until"]) if row else (None, None)
+
+    def graph_versions(self) -> Dict[str, Tuple[str, int]]:
+        """id -> (name, graph version) of every project with a persisted graph
+        (one index-free scan of the small projects table; no graph JSON read)."""
+        rows = self.db.query("SELECT id, name, graph_version FROM projects WHERE graph_data IS NOT NULL")
+        return {r["id"]: (r["name"], int(r["graph_version"] or 0)) for r in rows}
+
+    def graph_version(self, project_id: str) -> Optional[int]:
+        row = self.db.query_one("SELECT graph_version FROM projects WHERE id = ?", (project_id,))
+        return int(row["graph_version"] or 0) if row else None
 
     @staticmethod
     def update_params(p: Project) -> tuple:

@@ -123,9 +123,35 @@ std::string trim(std::string s) {
     return s;
 }
 
+// git check-ref-format's rules, as far as a path on disk is concerned: a name
+// git would refuse (and so never resolve) must not be read as a file here
+// either -- "../../x" would otherwise leave refs/ and follow whatever "ref: "
+// line it finds.  Refused names return false, so git answers instead.
+bool ref_name_ok(const std::string& ref) {
+    if (ref.empty() || ref.front() == '/' || ref.back() == '/' || ref.back() == '.') return false;
+    if (ref.size() >= 5 && ref.compare(ref.size() - 5, 5, ".lock") == 0) return false;
+    if (ref.find("..") != std::string::npos || ref.find("@{") != std::string::npos ||
+        ref.find("//") != std::string::npos || ref == "@")
+        return false;
+    for (unsigned char c : ref) {
+        if (c < 0x20 || c == 0x7f || c == ' ' || c == '~' || c == '^' || c == ':' || c == '?' || c == '*' ||
+            c == '[' || c == '\\')
+            return false;
+    }
+    size_t start = 0;  // no component may start with '.' or end with ".lock"
+    while (start <= ref.size()) {
+        size_t end = ref.find('/', start);
+        if (end == std::string::npos) end = ref.size();
+        if (end == start || ref[start] == '.') return false;
+        if (end - start >= 5 && ref.compare(end - 5, 5, ".lock") == 0) return false;
+        start = end + 1;
+    }
+    return true;
+}
+
 // a ref's target: loose ref file (symbolic refs followed), else packed-refs
 bool ref_target(const std::string& git_dir, const std::string& ref, std::string& sha, int depth = 0) {
-    if (depth > 5) return false;
+    if (depth > 5 || !ref_name_ok(ref)) return false;
     std::string text;
     if (slurp(git_dir + "/" + ref, text)) {
         text = trim(text);

@@ -162,3 +162,21 @@ def test_fold_norms_preserves_the_model():
             unfolded[f"l{i}.wdown"].t()
     exp = (rms(x, unfolded["norm_f"]) @ unfolded["lm_head"].t())[-1]
     assert (got - exp).abs().max().item() / max(1.0, exp.abs().max().item()) < 0.03
+
+
+def test_odd_vocab_checkpoint_decodes_on_the_library_path():
+    """A vocab outside the fused kernels' contract (e.g. 32001-style sizes)
+    disables the fused path at init instead of failing on small steps."""
+    from dmcp.models.llm import LocalLM, fused_shapes_ok, preset
+    cfg = preset("tiny", max_batch=4, vocab_size=321)
+    assert not fused_shapes_ok(cfg)
+    m = LocalLM(cfg, device="cuda", seed=5)
+    assert not m.use_fused
+    toks = [256] + list(b"class A {")
+    m.forward_tokens(torch.tensor(toks, dtype=torch.int32), 0, 0)
+    got = m.decode(torch.tensor([ord("x")], dtype=torch.int32, device="cuda"),
+                   torch.tensor([0], dtype=torch.int32, device="cuda"),
+                   torch.tensor([len(toks)], dtype=torch.int32, device="cuda")).float()[0]
+    exp = m.reference_logits(toks + [ord("x")])[-1].float()
+    assert got.shape[0] == 321
+    assert (got - exp).abs().max().item() / max(1.0, exp.abs().max().item()) < 0.03

@@ -190,3 +190,11 @@ def test_fp8_kv_model_tracks_bf16_model():
     step = [m.decode(torch.tensor([65, 66], dtype=torch.int32), torch.tensor([0, 1], dtype=torch.int32),
                      torch.tensor([len(toks), len(toks)], dtype=torch.int32)).float() for m in (a, b)]
     assert torch.nn.functional.cosine_similarity(step[0], step[1], dim=1).min() > 0.99
+
+
+def test_fused_shape_contract():
+    from dmcp.models.llm import fused_shapes_ok
+    assert fused_shapes_ok(preset("dmcp-coder-1b")) and fused_shapes_ok(preset("tiny"))
+    assert not fused_shapes_ok(preset("tiny", vocab_size=32001))
+    assert not fused_shapes_ok(preset("tiny", vocab_size=50257))
+    assert not fused_shapes_ok(preset("tiny", intermediate=520))

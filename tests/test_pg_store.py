@@ -128,10 +128,11 @@ def test_statement_cache_evicts_and_closes(pg_server):
 # ------------------------------------------------------------- PgDatabase
 def test_pg_database_migrates_idempotently(pg_server):
     db = PgDatabase.from_url(pg_server.url())
-    assert db.schema_version() == 2
+    from dmcp.store.pg import PG_MIGRATIONS
+    assert db.schema_version() == PG_MIGRATIONS[-1][0]
     assert db.migrate() == 0
     db2 = PgDatabase.from_url(pg_server.url())  # a second process adopts the schema
-    assert db2.schema_version() == 2
+    assert db2.schema_version() == PG_MIGRATIONS[-1][0]
     db.close()
     db2.close()
 
@@ -211,3 +212,17 @@ def test_service_end_to_end_on_postgres(pg_server, tmp_path):
     trace = call("get_stack_trace_context", {"stackTrace": [{"className": svc, "methodName": method}]})
     assert trace["executionPath"][0]["found"]
     app2.close()
+
+
+def test_pg_connections_only_set_the_search_path(pg_server):
+    """A least-privilege role (USAGE/CREATE on the schema, no CREATE on the
+    database) must be able to connect: only migrate() issues CREATE SCHEMA."""
+    db = PgDatabase.from_url(pg_server.url())
+    pg_server.statements.clear()
+    db2 = PgDatabase.from_url(pg_server.url(), migrate=False)
+    db2.query("SELECT COUNT(*) FROM projects")
+    stmts = [s.upper() for s in pg_server.statements]
+    assert not any("CREATE SCHEMA" in s for s in stmts)
+    assert any(s.startswith("SET SEARCH_PATH") for s in stmts)
+    db.close()
+    db2.close()

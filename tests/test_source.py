@@ -324,3 +324,24 @@ def test_loose_tree_fused_scan_equals_two_pass(tmp_path, kind):
     for d in (doc, ref):
         d["stats"] = None
     assert doc == ref and doc["files"]
+
+
+def test_native_ref_reader_refuses_names_git_refuses(tmp_path):
+    """A branch name such as '../../x' must not make the native reader open a
+    file outside refs/ (git check-ref-format refuses it; the native reader
+    returns None so git answers, and git errors)."""
+    import subprocess
+    from dmcp import _srcscan
+    from dmcp.index.source import git_dir_of
+    from dmcp.utils import synth
+    repo = tmp_path / "r"
+    synth.java_spring_repo(str(repo), 4)
+    gd = git_dir_of(str(repo))
+    head = subprocess.run(["git", "-C", str(repo), "rev-parse", "HEAD"], capture_output=True, text=True).stdout.strip()
+    (tmp_path / "evil").write_text(head + "\n")  # a file outside the repository
+    branch = subprocess.run(["git", "-C", str(repo), "branch", "--show-current"], capture_output=True,
+                            text=True).stdout.strip()
+    assert _srcscan.resolve_ref(gd, [f"refs/heads/{branch}"]) == head
+    for bad in ["refs/heads/../../../evil", "../../evil", "/etc/passwd", "refs/heads/a.lock", "refs/heads/x@{1}",
+                "refs/heads/.hidden", "refs/heads/a b", "refs/heads//x", "refs/heads/x."]:
+        assert _srcscan.resolve_ref(gd, [bad]) is None, bad

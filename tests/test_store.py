@@ -365,7 +365,7 @@ def test_v6_clustered_tables_migration_keeps_rows(tmp_path, monkeypatch):
     old.close()
     monkeypatch.undo()
     db = Database(path)
-    assert db.schema_version() == 6
+    assert db.schema_version() == MIGRATIONS[-1][0]
     for t, n in counts.items():
         assert db.query_one(f"SELECT COUNT(*) FROM {t}")[0] == n
         assert "WITHOUT ROWID" in db.query_one("SELECT sql FROM sqlite_master WHERE name = ?", (t,))[0]

@@ -9,8 +9,16 @@ persist (SQLite, one transaction replacing the previous analysis, written by
 a native thread) -> graph JSON -> cache publish.  Every step re-reads and
 re-parses every file; nothing is cached across steps.  Enrichment
 is disabled by default (BASELINE: "Indexing throughput with enrichment
-disabled"); ``--enrich fake|local`` adds Phase 2/3 (``local`` = the optional
-MI355X model, see dmcp/enrich/local.py).
+disabled"); ``--enrich fake`` adds Phase 2/3 with the offline fake backend.
+
+``extra.enrichLocal`` (GPU present, ``--enrich-local-classes`` > 0): after
+the headline, each rank runs a real ``analyze_project`` of a
+``--enrich-local-classes``-class repository with the optional MI355X
+enrichment backend in the service configuration -- one worker process per
+GPU (dmcp/enrich/workers.py, spawned before this process touches HIP),
+every pending class streamed to it, fp8 KV cache, 256 concurrent sequences
+-- and reports classes enriched per second through the whole pipeline plus
+the engine's per-step device / host split.
 
 Multi-GPU contract: launched by ``torch.distributed.run`` with one rank per
 GPU; every rank indexes its own repository (weak scaling), the timed region
@@ -47,11 +55,84 @@ def parse_args(argv=None):
     ap.add_argument("--enrich", default="none", choices=["none", "fake", "local"])
     ap.add_argument("--queries", type=int, default=200, help="graph_query / stack-trace latency samples")
     ap.add_argument("--workdir", default=None)
+    ap.add_argument("--enrich-local-classes", type=int, default=256,
+                    help="classes of the end-to-end local-model enrichment run (extra.enrichLocal; 0 = skip)")
+    ap.add_argument("--enrich-local-kv", default="fp8", choices=["bf16", "fp8"])
+    ap.add_argument("--enrich-local-batch", type=int, default=256)
     return ap.parse_args(argv)
+
+
+def _spawn_enrich_pool(args):
+    """The enrichment worker for this rank's GPU, spawned BEFORE this process
+    initialises HIP (the child stays idle -- no torch import -- until init)."""
+    if args.enrich_local_classes <= 0:
+        return None
+    try:
+        import torch
+        if torch.cuda.device_count() <= 0:  # counts devices without creating a HIP context
+            return None
+        from dmcp.enrich.workers import GpuWorkerPool
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        mb = args.enrich_local_batch
+        model = {"preset": "dmcp-coder-1b", "kv_dtype": args.enrich_local_kv, "max_batch": mb,
+                 "max_rows": max(256, mb * 3 // 2), "seed": 0}
+        return GpuWorkerPool([f"cuda:{local}"], model, init=False, start_timeout_s=600)
+    except Exception as e:  # the headline does not depend on it
+        logging.getLogger("bench").warning("enrichment worker not started: %s", e)
+        return None
+
+
+def _enrich_local(pool, args, ctx, work, rank):
+    """extra.enrichLocal: one warm-up analysis (hipGraph captures, allocator),
+    then the timed analyze_project of a fresh repository, MAX over ranks."""
+    from dmcp.app import App
+    from dmcp.config import Config
+    from dmcp.enrich.workers import ProcessLLMBackend
+    from dmcp.utils import synth
+    t_init = time.perf_counter()
+    pool.init()
+    init_s = time.perf_counter() - t_init
+    be = ProcessLLMBackend(pool)
+    cfg = Config(db_path=os.path.join(work, "enrich.db"), git_clone_base_path=os.path.join(work, "eclones"),
+                 require_enrichment_for_analyze=True, recover_stuck_on_start=False)
+    app = App(cfg, backend=be)
+    try:
+        warm = os.path.join(work, f"warm{rank}")
+        synth.java_spring_repo(warm, n_classes=min(64, max(8, args.enrich_local_classes // 4)),
+                               base_package=f"co.acme.warm{rank}", seed=rank + 101)
+        app.indexer.analyze_project(warm)
+        repo = os.path.join(work, f"enrich{rank}")
+        synth.java_spring_repo(repo, n_classes=args.enrich_local_classes, base_package=f"co.acme.enr{rank}",
+                               seed=rank + 201)
+        for w in pool.workers:
+            w.stats = {}
+        ctx.barrier()
+        t0 = time.perf_counter()
+        r = app.indexer.analyze_project(repo)
+        elapsed = time.perf_counter() - t0
+        st = be.stats()
+        mx = ctx.max(elapsed)[0]
+        tot = ctx.sum(float(r.stats.get("enriched", 0)), float(r.classes_analyzed))
+        steps = max(1.0, st.get("decode_steps", 0))
+        return {"classesPerSec": round(tot[0] / mx, 2), "classesEnriched": int(tot[0]),
+                "classesAnalyzed": int(tot[1]), "elapsedS": round(mx, 3), "enrichFailed": r.stats.get("enrichFailed"),
+                "phase2Ms": round(r.stats.get("analyze.phase2", 0.0), 1),
+                "decodeStepMs": round(1e3 * st.get("decode_s", 0) / steps, 3),
+                "hostMsPerStep": round(1e3 * st.get("host_s", 0) / steps, 3),
+                "waitMsPerStep": round(1e3 * st.get("wait_s", 0) / steps, 3),
+                "rowsPerStep": round(st.get("decode_rows", 0) / steps, 1),
+                "prefillMsPerClass": round(1e3 * st.get("prefill_s", 0) / max(1, st.get("prefills", 0)), 3),
+                "prefillBatches": int(st.get("prefill_batches", 0)), "workerInitS": round(init_s, 1),
+                "config": {"model": "dmcp-coder-1b (random init)", "kv_dtype": args.enrich_local_kv,
+                           "batch": args.enrich_local_batch, "workers_per_rank": len(pool.workers),
+                           "path": "analyze_project -> streamed Phase 2 -> GPU worker process"}}
+    finally:
+        app.db.close()
 
 
 def main(argv=None) -> int:
     args = parse_args(argv)
+    pool = _spawn_enrich_pool(args) if args.enrich == "none" else None  # before anything touches HIP
     from dmcp.parallel.dist import init_from_env
     ctx = init_from_env()
     rank, world = ctx.rank, ctx.world
@@ -117,6 +198,12 @@ def main(argv=None) -> int:
             extra["graphQueryMs"] = {"p50": round(lat[len(lat) // 2], 3), "p99": round(lat[int(len(lat) * 0.99) - 1], 3)}
             extra["stackTrace20Ms"] = {"p50": round(st_lat[len(st_lat) // 2], 3),
                                        "p99": round(st_lat[max(0, int(len(st_lat) * 0.99) - 1)], 3)}
+        if pool is not None:
+            try:
+                extra["enrichLocal"] = _enrich_local(pool, args, ctx, work, rank)
+            except Exception as e:
+                logging.getLogger("bench").exception("enrichLocal failed")
+                extra["enrichLocal"] = {"error": repr(e)[:300]}
         value = total_classes / elapsed if elapsed > 0 else 0.0
         ms_per_step = elapsed / max(1, args.steps) * 1e3
         if rank == 0:
@@ -134,6 +221,8 @@ def main(argv=None) -> int:
             print(json.dumps(line), flush=True)
     finally:
         app.close()
+        if pool is not None:
+            pool.close()
         if args.workdir is None:
             shutil.rmtree(work, ignore_errors=True)
         ctx.shutdown()

@@ -27,8 +27,8 @@ import threading
 import time
 import urllib.error
 import urllib.request
-from concurrent.futures import ThreadPoolExecutor
-from typing import Callable, List, Optional, Sequence
+from concurrent.futures import FIRST_COMPLETED, Future, ThreadPoolExecutor, wait
+from typing import Callable, Dict, Iterable, Iterator, List, Optional, Sequence, Tuple
 
 from ..utils.errors import require_non_blank, require_non_null
 from .jsonfix import parse_enrichment_response
@@ -145,6 +145,39 @@ class EnrichmentBackend:
             except Exception as e:
                 out.append(EnrichmentResult.failure(inp.full_class_name, str(e)))
         return out
+
+    def enrich_stream(self, inputs: Iterable[EnrichmentInput], readme: Optional[str]
+                      ) -> Iterator[Tuple[int, EnrichmentResult]]:
+        """Yields ``(input index, result)`` in completion order, with at most
+        ``max_concurrent`` classes in flight and the next one submitted as
+        soon as one finishes (a sliding window instead of the reference's
+        barrier per batch of 20, ``CodeContextService.java:297-359``, which
+        waits for the slowest of every 20).  ``inputs`` is consumed lazily."""
+        it = enumerate(inputs)
+        if self.max_concurrent == 1:
+            for i, inp in it:
+                yield i, self._safe(inp, readme)
+            return
+        ex = self._executor()
+        live: Dict[Future, Tuple[int, EnrichmentInput]] = {}
+        exhausted = False
+        while True:
+            while not exhausted and len(live) < self.max_concurrent:
+                try:
+                    i, inp = next(it)
+                except StopIteration:
+                    exhausted = True
+                    break
+                live[ex.submit(self._safe, inp, readme)] = (i, inp)
+            if not live:
+                return
+            done, _ = wait(list(live), return_when=FIRST_COMPLETED)
+            for f in done:
+                i, inp = live.pop(f)
+                try:
+                    yield i, f.result()
+                except Exception as e:
+                    yield i, EnrichmentResult.failure(inp.full_class_name, str(e))
 
     def close(self) -> None:
         with self._pool_lock:

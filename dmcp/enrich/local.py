@@ -26,9 +26,16 @@ per class) but generates on the local GPU:
   the graph gathers it on the device; the host runs the grammar state machine
   for step t while the GPU computes step t+1, so host bookkeeping (~0.3 ms
   per step) leaves the critical path;
-* multi-GPU: one engine (replica) per GPU, classes sharded across replicas
-  (:mod:`dmcp.parallel.replicas`) -- pure data parallelism, no collectives
-  (SURVEY §5.8).
+* streaming: :meth:`LocalEngine.stream` pulls classes from a feed as KV
+  slots free up and yields each reply as soon as it is complete, so the
+  indexing pipeline hands it ALL pending classes at once (no 20-class
+  barriers) and applies results while the GPU keeps decoding;
+* batched prefill: every class admitted in a step is prefilled in one pass
+  (:meth:`LocalLM.prefill_batch`: one GEMM per projection over all their
+  tokens, one variable-length attention launch);
+* multi-GPU: one engine per GPU in its own worker process
+  (:mod:`dmcp.enrich.workers`), all pulling from one queue -- pure data
+  parallelism, no collectives.
 """
 from __future__ import annotations
 
@@ -38,7 +45,7 @@ import threading
 import time
 from collections import deque
 from dataclasses import dataclass, field
-from typing import Deque, Dict, List, Optional, Sequence, Tuple
+from typing import Any, Deque, Dict, Iterable, Iterator, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -140,8 +147,76 @@ class _Seq:
     gen_tokens: int = 0
 
 
+    prompt: Optional[List[int]] = None   # prompt tokens (BOS + bytes)
+
+
+# ----------------------------------------------------------------- feeds
+class IterFeed:
+    """A feed over a (possibly lazy) iterable of ``(key, EnrichmentInput)``:
+    items are pulled only when the engine has room for them, so a producer
+    that reads sources on demand never runs ahead of the GPU."""
+
+    def __init__(self, items: Iterable[Tuple[Any, EnrichmentInput]]) -> None:
+        self._it = iter(items)
+        self.done = False
+
+    def take(self, n: int, wait: bool = False) -> List[Tuple[Any, EnrichmentInput]]:
+        out = []
+        while len(out) < n and not self.done:
+            try:
+                out.append(next(self._it))
+            except StopIteration:
+                self.done = True
+        return out
+
+
+class QueueFeed:
+    """A thread-safe feed another thread fills (the GPU worker's pipe reader):
+    ``put`` items, ``close`` when no more will come.  ``take(wait=True)``
+    blocks until an item arrives or the feed is closed."""
+
+    def __init__(self) -> None:
+        self._q: Deque[Tuple[Any, EnrichmentInput]] = deque()
+        self._cv = threading.Condition()
+        self._closed = False
+
+    def put(self, items: Iterable[Tuple[Any, EnrichmentInput]]) -> None:
+        with self._cv:
+            self._q.extend(items)
+            self._cv.notify_all()
+
+    def close(self) -> None:
+        with self._cv:
+            self._closed = True
+            self._cv.notify_all()
+
+    @property
+    def done(self) -> bool:
+        with self._cv:
+            return self._closed and not self._q
+
+    def take(self, n: int, wait: bool = False) -> List[Tuple[Any, EnrichmentInput]]:
+        with self._cv:
+            if wait:
+                while not self._q and not self._closed:
+                    self._cv.wait(0.5)
+            out = []
+            while self._q and len(out) < n:
+                out.append(self._q.popleft())
+            return out
+
+
+PREFIX_MARKER = b"Source of "  # build_enrichment_prompt: everything before it is per-project
+
+
 class LocalEngine:
     """Continuous-batching, grammar-forced greedy generator over one LocalLM.
+
+    :meth:`stream` is the engine: it pulls classes from a feed only while it
+    has free KV slots (plus a small look-ahead), prefills every admitted
+    class of a step in one batched prefill, and yields each reply the moment
+    its sequence finishes -- the caller applies it while the GPU runs the
+    next step.  :meth:`generate` is the list-in, list-out wrapper.
 
     ``jump_forward``: forced skeleton bytes are not fed one per step -- after
     a sequence's token is fed, every following token that is already decided
@@ -150,10 +225,18 @@ class LocalEngine:
     up to ``max_rows`` rows per step.  The KV append + causal per-row
     attention of :meth:`LocalLM.decode` makes that an exact multi-token
     extend, so only free (sampled) tokens cost a step each.
+
+    ``shared_prefix``: the part of every prompt before ``Source of`` (the
+    instructions + README of one project) is prefilled once per stream into
+    the model's prefix slot; decode reads it through the shared-prefix
+    kernel.  A prompt that does not start with it (truncated) is deferred to
+    a later pass with its own prefix.
     """
 
     MASK_NO_QUOTE, MASK_QUOTE = 0, 1
     MIN_SHARED_PREFIX = 64  # tokens; shorter common prefixes are not worth a separate prefill
+    ADMIT_TOKENS = 32768    # prompt tokens per batched prefill (one GEMM per projection over all of them)
+    ADMIT_SEQS = 64
 
     def __init__(self, model: LocalLM, use_graphs: bool = True, max_prompt_tokens: Optional[int] = None,
                  jump_forward: bool = True, shared_prefix: bool = True, pipeline: bool = True) -> None:
@@ -175,14 +258,26 @@ class LocalEngine:
         self._host_ids = [torch.zeros(self.max_rows, dtype=torch.int32, pin_memory=dev.type == "cuda")
                           for _ in range(2)]
         self.stats = {"prompt_tokens": 0, "generated_tokens": 0, "decode_steps": 0, "decode_rows": 0,
-                      "prefills": 0, "decode_s": 0.0, "prefill_s": 0.0, "prefix_tokens": 0, "prefix_s": 0.0}
+                      "prefills": 0, "prefill_batches": 0, "decode_s": 0.0, "prefill_s": 0.0, "prefix_tokens": 0,
+                      "prefix_s": 0.0, "host_s": 0.0, "wait_s": 0.0}
         self._lock = threading.Lock()
 
     # ---------------------------------------------------------------- api
     def generate(self, inputs: Sequence[EnrichmentInput], readme: Optional[str]) -> List[str]:
         """Returns the raw JSON reply for every input (same order)."""
+        out: Dict[int, str] = {}
+        for i, raw in self.stream(enumerate(inputs), readme):
+            out[i] = raw
+        return [out[i] for i in range(len(inputs))]
+
+    def stream(self, items, readme: Optional[str]) -> Iterator[Tuple[Any, str]]:
+        """Yields ``(key, raw reply)`` as sequences finish.  ``items``: an
+        iterable of ``(key, EnrichmentInput)`` or a feed (``take``/``done``)."""
+        feed = items if hasattr(items, "take") else IterFeed(items)
         with self._lock:
-            return self._generate(inputs, readme)
+            deferred = yield from self._session(feed, readme)
+            while deferred:  # prompts that did not start with the session's prefix
+                deferred = yield from self._session(IterFeed(deferred), readme)
 
     # ------------------------------------------------------------ helpers
     def _prompt(self, seq: _Seq, readme: Optional[str], budget: int) -> List[int]:
@@ -197,23 +292,14 @@ class LocalEngine:
             text = text[:limit - keep_tail] + text[len(text) - keep_tail:]
         return [BOS] + list(text)
 
-    def _select_one(self, logits: torch.Tensor, with_quote: bool) -> int:
-        from .. import ops
-        idx = torch.tensor([self.MASK_QUOTE if with_quote else self.MASK_NO_QUOTE], dtype=torch.int32,
-                           device=logits.device)
-        return int(ops.masked_argmax(logits.reshape(1, -1).contiguous(), self.masks, vocab=self.cfg.vocab_size,
-                                     mask_idx=idx).item())
-
-    def _step(self, toks: List[int], slots: List[int], poss: List[int], mrows: List[int]) -> List[int]:
-        """One batched forward over the rows; returns the masked argmax of every row."""
-        if self.graphs is not None:
-            _, ids = self.graphs.run(toks, slots, poss, mrows)
-        else:
-            dev = self.model.device
-            t = torch.tensor([toks, slots, poss, mrows], dtype=torch.int32, device=dev)
-            _, ids = self.model.decode_select(t[0].contiguous(), t[1].contiguous(), t[2].contiguous(), self.masks,
-                                              t[3].contiguous())
-        return ids.cpu().tolist()
+    def _prompt_prefix_len(self, prompt: List[int]) -> int:
+        """Tokens of ``prompt`` before its per-class part (``Source of``)."""
+        if not self.shared_prefix:
+            return 0
+        raw = bytes(t for t in prompt[1:2 + 4 * self.cfg.max_seq] if t < 256)
+        i = raw.find(PREFIX_MARKER)
+        P = 1 + i if i >= 0 else 0
+        return P if self.MIN_SHARED_PREFIX <= P < len(prompt) else 0
 
     def _advance_forced(self, s: _Seq) -> None:
         """Sets next_token from the current forced segment or finishes."""
@@ -262,136 +348,45 @@ class LocalEngine:
             raise ValueError(f"reply template needs {budget} tokens > max_seq {self.cfg.max_seq}")
         return self._prompt(s, readme, budget)
 
-    def _common_prefix(self, prompts: Sequence[List[int]]) -> int:
-        """Tokens shared by the start of every prompt (instructions + README
-        for classes of one project), leaving each prompt >= 1 own token."""
-        if not self.shared_prefix or len(prompts) < 2:
-            return 0
-        first = prompts[0]
-        n = min(len(p) for p in prompts) - 1
-        for p in prompts[1:]:
-            k = 0
-            while k < n and p[k] == first[k]:
-                k += 1
-            n = k
-            if n < self.MIN_SHARED_PREFIX:
-                return 0
-        return n if n >= self.MIN_SHARED_PREFIX else 0
-
-    def _admit(self, s: _Seq, prompt: List[int], prefix: int, results: Dict[int, str],
-               free_slots: List[int]) -> bool:
-        """Prefill prompt + first forced segment; True if the sequence stays active.
-        With a shared prefix of ``prefix`` tokens only the rest is prefilled."""
-        s.slot = free_slots.pop()
-        first = s.segs[0].forced or b""
-        toks = prompt + list(first)
+    def _admit_batch(self, batch: List[_Seq], prefix: int) -> List[_Seq]:
+        """Prefills every sequence of ``batch`` (slots assigned) -- prompt +
+        first forced segment, after the shared prefix when set -- in ONE
+        batched prefill, then selects each first free token with one masked
+        argmax.  Returns the sequences that finished already."""
+        from .. import ops
         t0 = time.perf_counter()
-        start = self.model.fork_prefix(s.slot) if prefix else 0
-        logits = self.model.forward_tokens(torch.tensor(toks[start:], dtype=torch.int32), s.slot, start)
+        reqs = []
+        for s in batch:
+            first = s.segs[0].forced or b""
+            toks = s.prompt + list(first)
+            start = self.model.fork_prefix(s.slot) if prefix else 0
+            reqs.append((toks[start:], s.slot, start))
+            self.stats["prompt_tokens"] += len(toks) - start
+            s.prompt_tokens = len(s.prompt)
+            s.out.extend(first)
+            s.pos = len(toks)
+            s.seg, s.forced_off = 1, 0
+        logits = self.model.prefill_batch(reqs)  # [n, vocab]
+        need = [i for i, s in enumerate(batch) if s.seg < len(s.segs) and s.segs[s.seg].forced is None]
+        if need:
+            rows = logits[need] if len(need) < len(batch) else logits
+            midx = torch.tensor([self.MASK_QUOTE if batch[i].segs[1].min_len == 0 else self.MASK_NO_QUOTE
+                                 for i in need], dtype=torch.int32, device=logits.device)
+            ids = ops.masked_argmax(rows.contiguous(), self.masks, vocab=self.cfg.vocab_size,
+                                    mask_idx=midx).cpu().tolist()
+            for i, tok in zip(need, ids):
+                batch[i].next_token = int(tok)
+        done = []
+        for i, s in enumerate(batch):
+            if s.seg >= len(s.segs) or s.segs[s.seg].forced is not None:
+                self._advance_forced(s)
+            if s.done:
+                done.append(s)
         self.stats["prefill_s"] += time.perf_counter() - t0
-        self.stats["prefills"] += 1
-        self.stats["prompt_tokens"] += len(toks) - start
-        s.prompt_tokens = len(prompt)
-        s.out.extend(first)
-        s.pos = len(toks)
-        s.seg, s.forced_off = 1, 0
-        if s.seg < len(s.segs) and s.segs[s.seg].forced is None:
-            s.next_token = self._select_one(logits, s.segs[s.seg].min_len == 0)
-        else:
-            self._advance_forced(s)
-        if s.done:
-            results[s.index] = s.out.decode("utf-8", "replace")
-            free_slots.append(s.slot)
-            return False
-        return True
+        self.stats["prefills"] += len(batch)
+        self.stats["prefill_batches"] += 1
+        return done
 
-    def _generate(self, inputs: Sequence[EnrichmentInput], readme: Optional[str]) -> List[str]:
-        cfg = self.cfg
-        reply_cap = cfg.max_seq - max(64, cfg.max_seq // 4)
-        results: Dict[int, str] = {}
-        prompts: Dict[int, List[int]] = {}
-        pending: Deque[_Seq] = deque()
-        for i, inp in enumerate(inputs):
-            s = _Seq(inp, i, fit_template(inp, reply_cap))
-            try:
-                prompts[i] = self._build_prompt(s, readme)
-                pending.append(s)
-            except Exception as e:
-                results[i] = json.dumps({"error": str(e)})
-        # one prefill of the common prefix (instructions + README) for all
-        prefix = self._common_prefix(list(prompts.values()))
-        if prefix:
-            t0 = time.perf_counter()
-            self.model.set_prefix(prompts[pending[0].index][:prefix])
-            self.stats["prefix_s"] += time.perf_counter() - t0
-            self.stats["prefix_tokens"] += prefix
-        try:
-            if self.pipeline:
-                self._run_pipelined(pending, prompts, prefix, results)
-            else:
-                self._run(pending, prompts, prefix, results)
-        finally:
-            if prefix:
-                self.model.clear_prefix()
-        return [results[i] for i in range(len(inputs))]
-
-    def _run(self, pending: Deque[_Seq], prompts: Dict[int, List[int]], prefix: int,
-             results: Dict[int, str]) -> None:
-        cfg = self.cfg
-        free_slots = list(range(cfg.max_batch - 1, -1, -1))
-        active: List[_Seq] = []
-        while pending or active:
-            while pending and free_slots:
-                s = pending.popleft()
-                if self._admit(s, prompts.pop(s.index), prefix, results, free_slots):
-                    active.append(s)
-            if not active:
-                continue
-            # one batched step: every active sequence feeds its next token, plus
-            # (jump-forward) every already-decided token after it
-            t0 = time.perf_counter()
-            toks: List[int] = []
-            slots: List[int] = []
-            poss: List[int] = []
-            mrows: List[int] = []
-            sample_at: List[Tuple[_Seq, int]] = []
-            spare = self.max_rows - len(active)  # rows beyond one per sequence
-            for s in active:
-                tok = s.next_token
-                while True:
-                    toks.append(tok)
-                    slots.append(s.slot)
-                    poss.append(s.pos)
-                    mrows.append(self.MASK_NO_QUOTE)
-                    q = self._after_feed(s, tok)
-                    if s.done:
-                        break
-                    if q is not None:  # the next token is sampled from this row's logits
-                        mrows[-1] = self.MASK_QUOTE if q else self.MASK_NO_QUOTE
-                        sample_at.append((s, len(toks) - 1))
-                        break
-                    if not self.jump_forward or spare <= 0:
-                        break  # decided token waits for the next step
-                    spare -= 1
-                    tok = s.next_token
-            ids = self._step(toks, slots, poss, mrows)
-            for s, r in sample_at:
-                s.next_token = ids[r]
-            self.stats["decode_s"] += time.perf_counter() - t0
-            self.stats["decode_steps"] += 1
-            self.stats["decode_rows"] += len(toks)
-            self.stats["generated_tokens"] += len(toks)
-            still = []
-            for s in active:
-                if s.done:
-                    results[s.index] = s.out.decode("utf-8", "replace")
-                    free_slots.append(s.slot)
-                else:
-                    still.append(s)
-            active = still
-
-
-    # ------------------------------------------------------ pipelined loop
     def _launch(self, toks: List[int], slots: List[int], poss: List[int], mrows: List[int],
                 srcs: List[int], buf: int):
         """Launches one step; enqueues the copy of its ids to pinned buffer
@@ -420,98 +415,175 @@ class LocalEngine:
         seg = s.segs[s.seg]
         return self.MASK_QUOTE if s.free_len + 1 >= seg.min_len else self.MASK_NO_QUOTE
 
-    def _run_pipelined(self, pending: Deque[_Seq], prompts: Dict[int, List[int]], prefix: int,
-                       results: Dict[int, str]) -> None:
-        """Continuous batching with the host one step behind the device.
+    # ------------------------------------------------------------ the loop
+    def _session(self, feed, readme: Optional[str]):
+        """One pass over ``feed`` with one shared prefix; returns the
+        ``(key, input)`` pairs whose prompt did not start with that prefix.
 
-        Each iteration builds step k's rows from the state known after
-        step k-1's inputs: a sequence whose next token is step k-1's
-        selection gets ONE gathered row (its mask row assumes the token is
-        not the closing quote -- if it is, that row's own selection is simply
-        not used); every other sequence gets its literal token and, with
-        jump-forward, the decided tokens after it.  Step k is launched, and
-        only then does the host wait for step k-1's ids and run the grammar
-        transitions of step k's gathered rows -- while the GPU computes
-        step k.  The price: forced bytes that follow a sampled closing quote
-        start one step later than in :meth:`_run`."""
+        Each iteration: refill the look-ahead from the feed, admit (batched
+        prefill) while KV slots are free, build step k's rows, launch it, then
+        -- while the GPU computes step k -- wait for step k-1's ids, run the
+        grammar transitions they decide and yield the finished replies.
+        With ``pipeline`` a sequence whose next token is step k-1's selection
+        gets ONE row gathered on the device from that selection (its mask row
+        assumes the token is not the closing quote -- if it is, that row's own
+        selection is simply not used); every other sequence gets its literal
+        token and, with jump-forward, the decided tokens after it.  Without
+        ``pipeline`` the host waits for every step's ids before building the
+        next (the exact reference loop)."""
         cfg = self.cfg
+        reply_cap = cfg.max_seq - max(64, cfg.max_seq // 4)
         free_slots = list(range(cfg.max_batch - 1, -1, -1))
+        pending: Deque[_Seq] = deque()
         active: List[_Seq] = []
+        deferred: List[Tuple[Any, EnrichmentInput]] = []
+        lookahead = max(4, cfg.max_batch // 4)
+        decided = not self.shared_prefix
+        prefix_toks: Optional[List[int]] = None
+        P = 0
         prev_event = None
         prev_buf = 1
-        while pending or active:
-            while pending and free_slots:
-                s = pending.popleft()
-                if self._admit(s, prompts.pop(s.index), prefix, results, free_slots):
-                    active.append(s)
-            if not active:
-                continue
-            t0 = time.perf_counter()
-            toks: List[int] = []
-            slots: List[int] = []
-            poss: List[int] = []
-            mrows: List[int] = []
-            srcs: List[int] = []
-            gathered: List[Tuple[_Seq, int, int]] = []  # (seq, row, source row of the previous step)
-            spare = self.max_rows - len(active)
-            for s in active:
-                if s.next_src >= 0:
-                    gathered.append((s, len(toks), s.next_src))
-                    toks.append(0)
-                    slots.append(s.slot)
-                    poss.append(s.pos)
-                    mrows.append(self._speculative_mask(s))
-                    srcs.append(s.next_src)
-                    s.next_src = -1
+        finished: List[_Seq] = []
+        try:
+            while True:
+                # ---- refill the look-ahead (blocking only when idle)
+                want = len(free_slots) + lookahead - len(pending)
+                if want > 0 and not feed.done:
+                    for key, inp in feed.take(want, wait=not active and not pending):
+                        s = _Seq(inp, key, fit_template(inp, reply_cap))
+                        try:
+                            s.prompt = self._build_prompt(s, readme)
+                        except Exception as e:
+                            yield key, json.dumps({"error": str(e)})
+                            continue
+                        if not decided:
+                            decided = True
+                            P = self._prompt_prefix_len(s.prompt)
+                            if P:
+                                prefix_toks = s.prompt[:P]
+                                t0 = time.perf_counter()
+                                self.model.set_prefix(prefix_toks)
+                                self.stats["prefix_s"] += time.perf_counter() - t0
+                                self.stats["prefix_tokens"] += P
+                        if P and s.prompt[:P] != prefix_toks:
+                            deferred.append((key, inp))
+                            continue
+                        pending.append(s)
+                if not pending and not active:
+                    if feed.done:
+                        break
                     continue
-                tok = s.next_token
-                while True:
-                    toks.append(tok)
-                    slots.append(s.slot)
-                    poss.append(s.pos)
-                    mrows.append(self.MASK_NO_QUOTE)
-                    srcs.append(-1)
-                    q = self._after_feed(s, tok)
-                    if s.done:
-                        break
-                    if q is not None:  # this row's selection is the next token
-                        mrows[-1] = self.MASK_QUOTE if q else self.MASK_NO_QUOTE
-                        s.next_src = len(toks) - 1
-                        break
-                    if not self.jump_forward or spare <= 0:
-                        break
-                    spare -= 1
+                # ---- admission: one batched prefill for all that fit
+                if pending and free_slots:
+                    batch: List[_Seq] = []
+                    ntok = 0
+                    while pending and free_slots and len(batch) < self.ADMIT_SEQS:
+                        nxt = len(pending[0].prompt) - P
+                        if batch and ntok + nxt > self.ADMIT_TOKENS:
+                            break
+                        s = pending.popleft()
+                        s.slot = free_slots.pop()
+                        batch.append(s)
+                        ntok += nxt
+                    for s in self._admit_batch(batch, P):
+                        free_slots.append(s.slot)
+                        yield s.index, s.out.decode("utf-8", "replace")
+                    active.extend(s for s in batch if not s.done)
+                if not active:
+                    continue
+                # ---- build and launch one step
+                t0 = time.perf_counter()
+                toks: List[int] = []
+                slots: List[int] = []
+                poss: List[int] = []
+                mrows: List[int] = []
+                srcs: List[int] = []
+                gathered: List[Tuple[_Seq, int, int]] = []  # (seq, row, source row of the previous step)
+                sample_at: List[Tuple[_Seq, int]] = []
+                spare = self.max_rows - len(active)
+                for s in active:
+                    if s.next_src >= 0:
+                        gathered.append((s, len(toks), s.next_src))
+                        toks.append(0)
+                        slots.append(s.slot)
+                        poss.append(s.pos)
+                        mrows.append(self._speculative_mask(s))
+                        srcs.append(s.next_src)
+                        s.next_src = -1
+                        continue
                     tok = s.next_token
-            buf = 1 - prev_buf
-            event = self._launch(toks, slots, poss, mrows, srcs, buf)
-            # the previous step's ids: the tokens this step's gathered rows fed
-            if gathered:
-                if prev_event is not None:
-                    prev_event.synchronize()
-                ids = self._host_ids[prev_buf]
-                for s, row, src in gathered:
-                    q = self._after_feed(s, int(ids[src]))
-                    if not s.done and q is not None:
-                        s.next_src = row  # its selection in the step just launched
-            prev_event, prev_buf = event, buf
-            self.stats["decode_s"] += time.perf_counter() - t0
-            self.stats["decode_steps"] += 1
-            self.stats["decode_rows"] += len(toks)
-            self.stats["generated_tokens"] += len(toks)
-            still = []
-            for s in active:
-                if s.done:
-                    results[s.index] = s.out.decode("utf-8", "replace")
-                    free_slots.append(s.slot)
-                else:
-                    still.append(s)
-            active = still
-        if prev_event is not None:
-            prev_event.synchronize()
+                    while True:
+                        toks.append(tok)
+                        slots.append(s.slot)
+                        poss.append(s.pos)
+                        mrows.append(self.MASK_NO_QUOTE)
+                        srcs.append(-1)
+                        q = self._after_feed(s, tok)
+                        if s.done:
+                            break
+                        if q is not None:  # this row's selection is the next token
+                            mrows[-1] = self.MASK_QUOTE if q else self.MASK_NO_QUOTE
+                            if self.pipeline:
+                                s.next_src = len(toks) - 1
+                            else:
+                                sample_at.append((s, len(toks) - 1))
+                            break
+                        if not self.jump_forward or spare <= 0:
+                            break
+                        spare -= 1
+                        tok = s.next_token
+                buf = 1 - prev_buf
+                t1 = time.perf_counter()
+                event = self._launch(toks, slots, poss, mrows, srcs, buf)
+                t2 = time.perf_counter()
+                if not self.pipeline:
+                    if event is not None:
+                        event.synchronize()
+                    ids = self._host_ids[buf]
+                    for s, r in sample_at:
+                        s.next_token = int(ids[r])
+                elif gathered:
+                    # the previous step's ids: the tokens this step's gathered rows fed
+                    if prev_event is not None:
+                        prev_event.synchronize()
+                    ids = self._host_ids[prev_buf]
+                    for s, row, src in gathered:
+                        q = self._after_feed(s, int(ids[src]))
+                        if not s.done and q is not None:
+                            s.next_src = row  # its selection in the step just launched
+                t3 = time.perf_counter()
+                prev_event, prev_buf = event, buf
+                self.stats["decode_steps"] += 1
+                self.stats["decode_rows"] += len(toks)
+                self.stats["generated_tokens"] += len(toks)
+                still = []
+                for s in active:
+                    if s.done:
+                        finished.append(s)
+                        free_slots.append(s.slot)
+                    else:
+                        still.append(s)
+                active = still
+                t4 = time.perf_counter()
+                self.stats["wait_s"] += t3 - t2
+                self.stats["host_s"] += (t1 - t0) + (t4 - t3) + (t2 - t1)
+                self.stats["decode_s"] += t4 - t0
+                # replies go out while the GPU computes the step just launched
+                while finished:
+                    s = finished.pop()
+                    yield s.index, s.out.decode("utf-8", "replace")
+        finally:
+            if prev_event is not None:
+                prev_event.synchronize()
+            if P:
+                self.model.clear_prefix()
+        return deferred
 
 
 class LocalLLMBackend(EnrichmentBackend):
-    """EnrichmentBackend over one or more local engines (one per GPU)."""
+    """EnrichmentBackend over local engines living in THIS process (one per
+    GPU; tests, smoke, single-GPU tools).  The multi-GPU service path runs one
+    engine per worker process instead (:class:`ProcessLLMBackend`)."""
 
     name = "local"
 
@@ -521,7 +593,9 @@ class LocalLLMBackend(EnrichmentBackend):
         self.preferred_batch_size = sum(e.cfg.max_batch for e in self.engines) * 2
 
     @classmethod
-    def from_config(cls, cfg) -> "LocalLLMBackend":
+    def from_config(cls, cfg) -> EnrichmentBackend:
+        if (cfg.local_llm_workers or "process").lower() == "process":
+            return ProcessLLMBackend.from_config(cfg)
         devices = []
         if torch.cuda.is_available():
             n = torch.cuda.device_count()
@@ -532,8 +606,10 @@ class LocalLLMBackend(EnrichmentBackend):
         engines = []
         for d in devices:
             with torch.cuda.device(d):
-                model = LocalLM(preset(cfg.local_llm_preset, kv_dtype=cfg.local_llm_kv_dtype), device=f"cuda:{d}",
-                                seed=0)
+                model = LocalLM(preset(cfg.local_llm_preset, kv_dtype=cfg.local_llm_kv_dtype,
+                                       max_batch=cfg.local_llm_max_batch,
+                                       max_rows=max(256, cfg.local_llm_max_batch * 3 // 2)),
+                                device=f"cuda:{d}", seed=0)
                 engines.append(LocalEngine(model))
         return cls(engines)
 
@@ -541,26 +617,37 @@ class LocalLLMBackend(EnrichmentBackend):
         return self.enrich_batch([inp], readme)[0]
 
     def enrich_batch(self, inputs: Sequence[EnrichmentInput], readme: Optional[str]) -> List[EnrichmentResult]:
-        if not inputs:
-            return []
-        from ..parallel.replicas import ReplicaPool
-        n, E = len(inputs), len(self.engines)
-        # one engine: everything in one continuous batch; several: work-stealing
-        # chunks big enough to keep each replica's batch full
-        chunk = n if E == 1 else max(2 * max(e.cfg.max_batch for e in self.engines), -(-n // (2 * E)))
-        pool = ReplicaPool(self.engines, chunk_for=lambda e: chunk)
+        out: Dict[int, EnrichmentResult] = {}
+        for i, r in self.enrich_stream(inputs, readme):
+            out[i] = r
+        return [out[i] for i in range(len(inputs))]
 
-        def ctx(eng):
-            return torch.cuda.device(eng.model.device) if eng.model.device.type == "cuda" else _nullctx()
+    def enrich_stream(self, inputs: Iterable[EnrichmentInput], readme: Optional[str]
+                      ) -> Iterator[Tuple[int, EnrichmentResult]]:
+        """Every engine pulls classes from ONE shared feed as its slots free
+        up (work-stealing per class: every replica gets work, however few
+        classes there are); results are yielded as sequences finish."""
+        src = enumerate(inputs)
+        if len(self.engines) == 1:
+            names: Dict[int, str] = {}
 
-        raw = pool.map(lambda eng, items: eng.generate(items, readme), list(inputs), device_ctx=ctx)
-        results = []
-        for inp, r in zip(inputs, raw):
-            if isinstance(r, BaseException) or r is None:
-                results.append(EnrichmentResult.failure(inp.full_class_name, str(r) if r is not None else "no output"))
-            else:
-                results.append(parse_enrichment_response(r, inp.full_class_name))
-        return results
+            def tagged():
+                for i, inp in src:
+                    names[i] = inp.full_class_name
+                    yield i, inp
+            eng = self.engines[0]
+            with _device(eng):
+                try:
+                    for i, raw in eng.stream(tagged(), readme):
+                        yield i, _parse(raw, names.pop(i))
+                except Exception as e:  # engine failure: everything not yet returned fails
+                    LOG.exception("local engine failed")
+                    for i, name in list(names.items()):
+                        yield i, EnrichmentResult.failure(name, f"engine failed: {e}")
+                    for i, inp in src:
+                        yield i, EnrichmentResult.failure(inp.full_class_name, f"engine failed: {e}")
+            return
+        yield from _threaded_stream(self.engines, src, readme)
 
     def stats(self) -> dict:
         agg: Dict[str, float] = {}
@@ -570,9 +657,78 @@ class LocalLLMBackend(EnrichmentBackend):
         return agg
 
 
+def _parse(raw: str, name: str) -> EnrichmentResult:
+    return parse_enrichment_response(raw, name)
+
+
+def _device(eng: LocalEngine):
+    return torch.cuda.device(eng.model.device) if eng.model.device.type == "cuda" else _nullctx()
+
+
+class _SharedFeed:
+    """One locked iterator several engine threads take from."""
+
+    def __init__(self, src) -> None:
+        self._src = src
+        self._lock = threading.Lock()
+        self.done = False
+        self.names: Dict[int, str] = {}
+
+    def take(self, n: int, wait: bool = False):
+        with self._lock:
+            out = []
+            while len(out) < n and not self.done:
+                try:
+                    i, inp = next(self._src)
+                except StopIteration:
+                    self.done = True
+                    break
+                self.names[i] = inp.full_class_name
+                out.append((i, inp))
+            return out
+
+
+def _threaded_stream(engines: Sequence[LocalEngine], src, readme: Optional[str]):
+    import queue
+    feed = _SharedFeed(src)
+    q: "queue.Queue" = queue.Queue()
+
+    def run(eng: LocalEngine) -> None:
+        try:
+            with _device(eng):
+                for i, raw in eng.stream(feed, readme):
+                    q.put((i, raw, None))
+        except BaseException as e:  # this replica stops; its taken classes fail below
+            LOG.exception("local engine on %s failed", eng.model.device)
+            q.put((None, None, e))
+        finally:
+            q.put(None)
+
+    threads = [threading.Thread(target=run, args=(e,), name=f"engine-{k}", daemon=True)
+               for k, e in enumerate(engines)]
+    for t in threads:
+        t.start()
+    live, err = len(threads), None
+    while live:
+        item = q.get()
+        if item is None:
+            live -= 1
+            continue
+        i, raw, e = item
+        if e is not None:
+            err = e
+            continue
+        yield i, _parse(raw, feed.names.pop(i))
+    for i, name in list(feed.names.items()):  # taken by a failed replica
+        yield i, EnrichmentResult.failure(name, f"engine failed: {err}")
+
+
 class _nullctx:
     def __enter__(self):
         return self
 
     def __exit__(self, *a):
         return False
+
+
+from .workers import ProcessLLMBackend  # noqa: E402  (the service's multi-GPU backend)

@@ -516,25 +516,74 @@ class Indexer:
                                           [m.method_name for m in unit.methods]))
         return inputs, failed
 
+    def _input_for(self, ident: str, parsed: ParsedProject, tree: SourceTree,
+                   class_types: Optional[Dict[str, str]] = None) -> Optional[EnrichmentInput]:
+        unit = parsed.units.get(ident)
+        if unit is None:
+            return None
+        src = self._read_source(tree, unit)
+        if src is None:
+            return None
+        ct = (class_types or {}).get(ident, unit.class_type.value)
+        return EnrichmentInput(src, ident, parsed.language, ct, [m.method_name for m in unit.methods])
+
+    def _stream_enrich(self, idents: Sequence[str], parsed: ParsedProject, graph: ProjectGraph,
+                       tree: SourceTree, readme: Optional[str], class_types: Optional[Dict[str, str]],
+                       methods_by_ident: Optional[Dict[str, List[Tuple[str, str]]]], phase: str) -> Tuple[int, int]:
+        """Every pending class goes to the backend as ONE stream (sources read
+        lazily, as the backend asks for more); each result is applied the
+        moment it arrives.  A local GPU engine keeps its continuous batch full
+        across the whole project; API backends keep ``max_concurrent`` in
+        flight (a sliding window, not 20-class barriers)."""
+        read_failed = [0]
+        total = len(idents)
+
+        def inputs():
+            for ident in idents:
+                if ident not in parsed.units:
+                    continue
+                inp = self._input_for(ident, parsed, tree, class_types)
+                if inp is None:
+                    read_failed[0] += 1
+                    continue
+                yield inp
+        enriched = failed = 0
+        step = max(20, total // 10)
+        for n, (_, result) in enumerate(self.backend.enrich_stream(inputs(), readme), 1):
+            if not result.success:
+                LOG.warning("%s: enrichment failed for %s: %s", phase, result.full_class_name, result.error_message)
+                failed += 1
+            elif self.apply_enrichment(result, graph, methods_by_ident):
+                enriched += 1
+            else:
+                failed += 1
+            if n % step == 0:
+                LOG.info("%s: %d/%d classes enriched (%d failed)", phase, enriched, total, failed)
+        return enriched, failed + read_failed[0]
+
     def _enrich_identifiers(self, idents: Sequence[str], parsed: ParsedProject, graph: ProjectGraph,
                             tree: SourceTree, readme: Optional[str],
                             methods_by_ident: Optional[Dict[str, List[Tuple[str, str]]]] = None
                             ) -> Tuple[int, int]:
-        enriched = failed = 0
         idents = list(idents)
-        nbatches = (len(idents) + self.batch_size - 1) // self.batch_size
-        for b in range(0, len(idents), self.batch_size):
-            batch = idents[b:b + self.batch_size]
-            LOG.info("Enriching batch %d/%d (%d classes)", b // self.batch_size + 1, nbatches, len(batch))
-            inputs, read_failed = self._inputs_for(batch, parsed, tree)
-            failed += read_failed
-            for result in self.backend.enrich_batch(inputs, readme):
-                if not result.success:
-                    LOG.warning("Enrichment failed for %s: %s", result.full_class_name, result.error_message)
-                    failed += 1
-                    continue
-                self.apply_enrichment(result, graph, methods_by_ident)
-                enriched += 1
+        if self.stream_enrichment:
+            enriched, failed = self._stream_enrich(idents, parsed, graph, tree, readme, None, methods_by_ident,
+                                                   "Phase 2")
+        else:  # the reference's barriers: batches of batch_size classes (CodeContextService.java:297-359)
+            enriched = failed = 0
+            nbatches = (len(idents) + self.batch_size - 1) // self.batch_size
+            for b in range(0, len(idents), self.batch_size):
+                batch = idents[b:b + self.batch_size]
+                LOG.info("Enriching batch %d/%d (%d classes)", b // self.batch_size + 1, nbatches, len(batch))
+                inputs, read_failed = self._inputs_for(batch, parsed, tree)
+                failed += read_failed
+                for result in self.backend.enrich_batch(inputs, readme):
+                    if not result.success:
+                        LOG.warning("Enrichment failed for %s: %s", result.full_class_name, result.error_message)
+                        failed += 1
+                        continue
+                    self.apply_enrichment(result, graph, methods_by_ident)
+                    enriched += 1
         METRICS.inc("classes_enriched", enriched)
         METRICS.inc("classes_enrich_failed", failed)
         return enriched, failed
@@ -546,20 +595,23 @@ class Indexer:
             LOG.info("Phase 3: No unenriched classes found, skipping recovery")
             return 0
         LOG.info("Phase 3: Found %d classes with missing enrichment, retrying", len(unenriched))
-        recovered = 0
         types = {sc.full_class_name: sc.class_type.value for sc in unenriched}
         idents = [sc.full_class_name for sc in unenriched]
-        for b in range(0, len(idents), self.batch_size):
-            inputs, _ = self._inputs_for(idents[b:b + self.batch_size], parsed, tree, types)
-            if not inputs:
-                continue
-            for result in self.backend.enrich_batch(inputs, readme):
-                if result.success:
-                    self.apply_enrichment(result, graph)
-                    recovered += 1
-                else:
-                    LOG.warning("Phase 3: Recovery failed for %s: %s", result.full_class_name,
-                                result.error_message)
+        if self.stream_enrichment:
+            recovered, _ = self._stream_enrich(idents, parsed, graph, tree, readme, types, None, "Phase 3")
+        else:
+            recovered = 0
+            for b in range(0, len(idents), self.batch_size):
+                inputs, _ = self._inputs_for(idents[b:b + self.batch_size], parsed, tree, types)
+                if not inputs:
+                    continue
+                for result in self.backend.enrich_batch(inputs, readme):
+                    if result.success:
+                        self.apply_enrichment(result, graph)
+                        recovered += 1
+                    else:
+                        LOG.warning("Phase 3: Recovery failed for %s: %s", result.full_class_name,
+                                    result.error_message)
         LOG.info("Phase 3 complete. Recovered: %d/%d", recovered, len(unenriched))
         return recovered
 

@@ -376,6 +376,70 @@ class LocalLM:
         return F.linear(h[-1:], self.w["lm_head"])[0]
 
     @torch.inference_mode()
+    def prefill_batch(self, reqs: Sequence[tuple]) -> torch.Tensor:
+        """Prefill / extend several sequences in ONE pass: ``reqs`` =
+        ``(tokens, slot, start)`` per sequence.  Their tokens are packed into
+        one [Ttot, hidden] activation, so every projection is one GEMM over
+        all of them (2,000-token prompts alone leave the MFMA GEMMs short of
+        work) and the attention is one variable-length launch
+        (``ops.prefill_attention_varlen``: per-sequence causal masks, the
+        shared prefix read in place).  Returns each sequence's last-position
+        logits [n, vocab] (bf16)."""
+        c = self.cfg
+        n = len(reqs)
+        if n == 0:
+            raise ValueError("prefill_batch needs at least one sequence")
+        if n == 1 or not (self.use_prefill_kernel or self.device.type == "cpu"):
+            return torch.stack([self.forward_tokens(torch.as_tensor(t, dtype=torch.int32), sl, st)
+                                for t, sl, st in reqs])
+        toks: List[int] = []
+        pos: List[int] = []
+        slots: List[int] = []
+        offsets = [0]
+        starts, seq_slots, shared = [], [], []
+        for t, sl, st in reqs:
+            T = len(t)
+            if T == 0:
+                raise ValueError("prefill_batch: empty sequence")
+            if not (0 <= sl < self.num_slots) or st < 0 or st + T > c.max_seq:
+                raise ValueError(f"sequence does not fit: slot={sl} start={st} T={T} max_seq={c.max_seq}")
+            if st == 0:
+                self._slot_prefix.pop(sl, None)
+            sh = self._slot_prefix.get(sl, 0)
+            shared.append(sh if 0 < sh <= st else 0)
+            toks.extend(int(x) for x in t)
+            pos.extend(range(st, st + T))
+            slots.extend([sl] * T)
+            offsets.append(offsets[-1] + T)
+            starts.append(st)
+            seq_slots.append(sl)
+        if len(set(seq_slots)) != n:
+            raise ValueError("prefill_batch: each sequence needs its own slot")
+        dev = self.device
+        meta = torch.tensor([toks, pos, slots], dtype=torch.int32)
+        if dev.type == "cuda":
+            meta = meta.pin_memory()
+        meta = meta.to(dev, non_blocking=True)
+        ids, pos_t, slot_t = meta[0], meta[1], meta[2]
+        x = ops.embedding(self.w["embed"], ids)
+        resid = x.clone()
+        h = ops.add_rmsnorm(x, self.w["l0.ln1"], c.eps)
+        Ttot = offsets[-1]
+        for i in range(c.layers):
+            kc, vc = self.k_cache[i], self.v_cache[i]
+            qkv = F.linear(h, self.w[f"l{i}.wqkv"])
+            q = ops.rope_kv(qkv, pos_t, slot_t, self.cos_sin, kc, vc, c.n_heads)  # [Ttot, Hq, D]
+            att = ops.prefill_attention_varlen(q, kc, vc, offsets, seq_slots, starts,
+                                               self.prefix_slot if any(shared) else None, shared, self.scale)
+            o = F.linear(att.view(Ttot, c.n_heads * c.head_dim), self.w[f"l{i}.wo"])
+            h = ops.add_rmsnorm(o, self.w[f"l{i}.ln2"], c.eps, residual=resid)
+            m = self._mlp(i, h)
+            nxt = self.w[f"l{i + 1}.ln1"] if i + 1 < c.layers else self.w["norm_f"]
+            h = ops.add_rmsnorm(m, nxt, c.eps, residual=resid)
+        last = torch.tensor([o_ - 1 for o_ in offsets[1:]], dtype=torch.long, device=dev)
+        return F.linear(h.index_select(0, last), self.w["lm_head"])
+
+    @torch.inference_mode()
     def decode(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:
         """One token per row; all inputs int32 [B] on device.
 

@@ -112,6 +112,12 @@ def prefill_attention(q, k_cache, v_cache, slot, start, prefix_slot=None, prefix
                                                                   prefix_len, scale, out, variant, nsplit)
 
 
+def prefill_attention_varlen(q, k_cache, v_cache, offsets, slots, starts, prefix_slot=None, prefix_lens=None,
+                             scale=1.0, out=None):
+    return (_hip() if q.is_cuda else reference).prefill_attention_varlen(
+        q, k_cache, v_cache, offsets, slots, starts, prefix_slot, prefix_lens, scale, out)
+
+
 def prefill_supported(n_heads, n_kv_heads, head_dim):
     from .hip import prefill_supported as _ps
     return _ps(n_heads, n_kv_heads, head_dim)

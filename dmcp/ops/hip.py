@@ -368,6 +368,20 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
     return out
 
 
+def prefill_attention_varlen(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, offsets, slots, starts,
+                             prefix_slot: Optional[int] = None, prefix_lens=None, scale: float = 1.0,
+                             out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Packed multi-sequence prefill attention (see
+    :func:`dmcp.ops.reference.prefill_attention_varlen`)."""
+    out = torch.empty_like(q) if out is None else out
+    for i in range(len(slots)):
+        a, b = int(offsets[i]), int(offsets[i + 1])
+        P = int(prefix_lens[i]) if prefix_lens is not None else 0
+        prefill_attention(q[a:b], k_cache, v_cache, int(slots[i]), int(starts[i]), prefix_slot if P else None, P,
+                          scale, out=out[a:b])
+    return out
+
+
 PREFIX_CHUNK = 256  # keys per prefix split: kPrefixChunk in csrc/dmcp_kernels.hip
 PREFIX_IMPLS = ("chunk", "prefill")
 

@@ -154,6 +154,22 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
     return y
 
 
+def prefill_attention_varlen(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, offsets, slots, starts,
+                             prefix_slot: Optional[int] = None, prefix_lens=None, scale: float = 1.0,
+                             out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Several sequences' prefill in one packed q [Ttot, Hq, D]: sequence i
+    is rows [offsets[i], offsets[i+1]) at positions [starts[i], ...) of
+    ``slots[i]``, keys [0, prefix_lens[i]) read from ``prefix_slot``.
+    fp32 math per sequence (:func:`prefill_attention`)."""
+    out = torch.empty_like(q) if out is None else out
+    for i in range(len(slots)):
+        a, b = int(offsets[i]), int(offsets[i + 1])
+        P = int(prefix_lens[i]) if prefix_lens is not None else 0
+        out[a:b] = prefill_attention(q[a:b], k_cache, v_cache, int(slots[i]), int(starts[i]),
+                                     prefix_slot if P else None, P, scale)
+    return out
+
+
 def silu_mul(gate_up: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     I = gate_up.shape[-1] // 2
     g, u = gate_up[..., :I].float(), gate_up[..., I:].float()

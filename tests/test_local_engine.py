@@ -122,17 +122,77 @@ def test_shared_prefix_cpu_matches_full_prompt(tiny):
         tiny.clear_prefix()
 
 
-def test_engine_common_prefix_detection(tiny):
+def test_engine_prompt_prefix_detection(tiny):
+    """The shared prefix is everything before 'Source of' (instructions +
+    README: the same for every class of a project)."""
     eng = LocalEngine(tiny, use_graphs=False)
-    a = [256] + [1] * 100 + [2, 3]
-    b = [256] + [1] * 100 + [4]
-    assert eng._common_prefix([a, b]) == 101
-    assert eng._common_prefix([a]) == 0  # one prompt: nothing to share
-    assert eng._common_prefix([a, [256, 9] + [1] * 100]) == 0  # below the minimum
-    assert eng._common_prefix([a, a]) == len(a) - 1  # every prompt keeps >= 1 own token
-    out = eng.generate(_inputs(5), "A README shared by every prompt of the batch. " * 3)
-    assert eng.stats["prefix_tokens"] > 0 and all(json.loads(o) for o in out)
-    assert tiny.prefix_len == 0  # cleared after the batch
+    readme = "A README shared by every prompt of the batch. " * 3
+    from dmcp.enrich.backend import build_enrichment_prompt
+    a = [256] + list(build_enrichment_prompt(_inputs(1)[0], readme).encode())
+    P = eng._prompt_prefix_len(a)
+    assert P > 64 and bytes(a[P:P + 10]) == b"Source of "
+    b = [256] + list(build_enrichment_prompt(_inputs(2)[1], readme).encode())
+    assert a[:P] == b[:P] and a[P + 10:] != b[P + 10:]
+    assert eng._prompt_prefix_len([256] + list(b"Source of x")) == 0  # below the minimum
+    assert LocalEngine(tiny, use_graphs=False, shared_prefix=False)._prompt_prefix_len(a) == 0
+    out = eng.generate(_inputs(5), readme)
+    assert eng.stats["prefix_tokens"] == P and all(json.loads(o) for o in out)
+    assert eng.stats["prefill_batches"] < eng.stats["prefills"]  # admitted classes share one prefill pass
+    assert tiny.prefix_len == 0  # cleared after the stream
+
+
+def test_engine_streams_results_as_they_finish(tiny):
+    """stream() pulls inputs lazily (never more than free slots + look-ahead
+    ahead of what finished) and yields each reply as its sequence ends."""
+    eng = LocalEngine(tiny, use_graphs=False)
+    pulled = []
+
+    def src():
+        for i, inp in enumerate(_inputs(12)):
+            pulled.append(i)
+            yield i, inp
+    seen = []
+    for key, raw in eng.stream(src(), "readme text"):
+        seen.append(key)
+        if len(seen) == 1:
+            assert len(pulled) < 12  # the first reply came before the feed was drained
+        json.loads(raw)
+    assert sorted(seen) == list(range(12))
+
+
+def test_engine_defers_prompts_without_the_session_prefix(tiny):
+    """A prompt whose prefix differs (another language) runs in a second pass
+    with its own prefix instead of attending to the wrong one."""
+    eng = LocalEngine(tiny, use_graphs=False)
+    inputs = _inputs(4)
+    inputs[2] = EnrichmentInput(inputs[2].source_code, inputs[2].full_class_name, "kotlin", "SERVICE", ["a"])
+    readme = "A README shared by every prompt of the batch. " * 3
+    out = eng.generate(inputs, readme)
+    assert all(json.loads(o) for o in out)
+    assert eng.stats["prefix_tokens"] > 2 * 64  # two prefix sessions
+
+
+def test_prefill_batch_matches_single_prefills(tiny):
+    """Packed multi-sequence prefill (one pass over every token, varlen
+    attention) == one forward_tokens per sequence, with and without the
+    shared prefix."""
+    seqs = [list(b"class A { void a() {} }"), list(b"class Bee { int b; long c; }"), list(b"x")]
+    single = [tiny.forward_tokens(torch.tensor([256] + t, dtype=torch.int32), s, 0) for s, t in enumerate(seqs)]
+    got = tiny.prefill_batch([([256] + t, s, 0) for s, t in enumerate(seqs)])
+    torch.testing.assert_close(got.float(), torch.stack(single).float(), atol=3e-2, rtol=3e-2)
+    prefix = [256] + list(b"Shared instructions and README text for every class of the project. " * 2)
+    P = tiny.set_prefix(prefix)
+    try:
+        ref = []
+        for s, t in enumerate(seqs):
+            tiny.fork_prefix(s)
+            ref.append(tiny.forward_tokens(torch.tensor(t, dtype=torch.int32), s, P))
+        for s in range(len(seqs)):
+            tiny.fork_prefix(s)
+        got = tiny.prefill_batch([(t, s, P) for s, t in enumerate(seqs)])
+        torch.testing.assert_close(got.float(), torch.stack(ref).float(), atol=3e-2, rtol=3e-2)
+    finally:
+        tiny.clear_prefix()
 
 
 def test_prefill_reference_matches_sdpa_extend():

@@ -1,0 +1,120 @@
+"""One worker process per GPU (dmcp/enrich/workers.py), rehearsed on the CPU:
+two real child processes run the tiny model on the fp32 reference ops.
+
+Covers the service path of the local enrichment backend: work spread over
+every worker from one queue, results in input order through
+``enrich_batch``, a killed worker isolated (its classes fail, the others
+finish; a fresh child replaces it at the next stream), and a whole
+``analyze_project`` streaming every class through the pool."""
+import json
+import os
+import signal
+import time
+
+import pytest
+
+from conftest import make_app
+from dmcp.enrich.types import EnrichmentInput
+from dmcp.enrich.workers import GpuWorkerPool, ProcessLLMBackend, recv_frame, send_frame
+from dmcp.utils import synth
+
+MODEL = {"preset": "tiny", "max_batch": 4, "max_rows": 16, "max_seq": 768, "seed": 1}
+
+
+def _inputs(n):
+    return [EnrichmentInput("public class S%d { void a() {} void b() {} }" % i, f"co.x.S{i}", "java", "SERVICE",
+                            ["a", "b", "c"][: 1 + i % 3]) for i in range(n)]
+
+
+@pytest.fixture(scope="module")
+def pool():
+    p = GpuWorkerPool(["cpu", "cpu"], MODEL, engine={"use_graphs": False}, start_timeout_s=300)
+    yield p
+    p.close()
+
+
+def test_frames_roundtrip():
+    import io
+    buf = io.BytesIO()
+    send_frame(buf, {"op": "x", "v": [1, "é"]})
+    send_frame(buf, {"op": "y"})
+    buf.seek(0)
+    assert recv_frame(buf) == {"op": "x", "v": [1, "é"]} and recv_frame(buf) == {"op": "y"}
+    assert recv_frame(buf) is None
+
+
+def test_work_is_spread_and_results_keep_input_order(pool):
+    be = ProcessLLMBackend(pool)
+    before = dict(pool.per_worker_items)
+    inputs = _inputs(14)
+    res = be.enrich_batch(inputs, "A shop README. " * 8)
+    assert [r.full_class_name for r in res] == [i.full_class_name for i in inputs]
+    assert all(r.success for r in res), [r.error_message for r in res if not r.success]
+    for r, inp in zip(res, inputs):
+        assert [m.method_name for m in r.methods] == inp.method_names
+    got = {k: pool.per_worker_items.get(k, 0) - before.get(k, 0) for k in (0, 1)}
+    assert got[0] > 0 and got[1] > 0 and got[0] + got[1] == 14
+    st = be.stats()
+    assert st["workers"] == 2 and st["prefills"] == 14 and st["decode_steps"] > 0
+    assert len({w.info["pid"] for w in pool.workers}) == 2 and all(w.info["pid"] != os.getpid() for w in pool.workers)
+
+
+def test_killed_worker_is_isolated_and_replaced(pool):
+    be = ProcessLLMBackend(pool)
+    inputs = _inputs(16)
+    victim = pool.workers[1]
+    old_pid = victim.proc.pid
+    results = {}
+    killed = False
+    for i, r in be.enrich_stream(inputs, None):
+        results[i] = r
+        if not killed:
+            os.kill(old_pid, signal.SIGKILL)  # mid-stream, while it holds classes
+            killed = True
+    assert sorted(results) == list(range(16))
+    failed = [r for r in results.values() if not r.success]
+    assert failed and all("worker died" in r.error_message for r in failed)
+    assert sum(r.success for r in results.values()) >= 16 - pool.capacity
+    assert pool.deaths >= 1
+    # the next stream runs on a FRESH child in place of the dead one
+    res = be.enrich_batch(_inputs(4), None)
+    assert all(r.success for r in res)
+    assert pool.workers[1].proc.pid != old_pid and pool.workers[1].alive
+
+
+def test_analyze_project_streams_every_class_through_the_pool(tmp_path, pool):
+    repo = tmp_path / "shop"
+    synth.java_spring_repo(str(repo), 16)
+    be = ProcessLLMBackend(pool)
+    before = dict(pool.per_worker_items)
+    app = make_app(tmp_path, backend=be)
+    t0 = time.time()
+    r = app.indexer.analyze_project(str(repo))
+    assert r.success and r.classes_analyzed == 17
+    assert r.stats["enriched"] == 17 and r.stats["enrichFailed"] == 0
+    assert app.repos.classes.find_unenriched_by_project_id(r.project_id) == []
+    got = {k: pool.per_worker_items.get(k, 0) - before.get(k, 0) for k in (0, 1)}
+    assert got[0] > 0 and got[1] > 0
+    # every method row got its description from the model's (grammar-forced) reply
+    m = app.repos.methods.find_by_class_name("co.acme.shop.order.OrderService")
+    assert m and any(x.description for x in m)  # (tiny max_seq: fit_template may drop trailing methods)
+    g = app.cache.get_graph(r.project_id)
+    assert g.node_info("co.acme.shop.order.OrderService").description
+    app.db.close()  # not app.close(): the module-scoped pool outlives this app
+    assert time.time() - t0 < 600
+
+
+def test_failed_init_reports_no_worker(tmp_path):
+    with pytest.raises(RuntimeError):
+        GpuWorkerPool(["cpu"], {"preset": "no-such-preset"}, start_timeout_s=120)
+
+
+def test_bench_enrich_local_path_on_cpu_workers(tmp_path, pool):
+    """bench.py's extra.enrichLocal (the GPU service path) run end to end on
+    the CPU rehearsal pool: a real analyze_project streamed through it."""
+    import bench
+    from dmcp.parallel.dist import DistContext
+    args = bench.parse_args(["--enrich-local-classes", "16"])
+    rec = bench._enrich_local(pool, args, DistContext(), str(tmp_path), 0)
+    assert rec["classesEnriched"] == rec["classesAnalyzed"] == 17 and rec["classesPerSec"] > 0
+    assert rec["decodeStepMs"] > 0 and rec["hostMsPerStep"] > 0 and rec["prefillBatches"] >= 1

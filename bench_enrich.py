@@ -40,6 +40,8 @@ def main(argv=None) -> int:
     ap.add_argument("--no-jump", action="store_true", help="disable jump-forward over forced tokens")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="synchronous engine loop (host waits for every step's ids before building the next)")
+    ap.add_argument("--admit-min", type=int, default=0,
+                    help="free KV slots before a running batch admits new classes (0 = engine default, batch/16)")
     ap.add_argument("--warmup", type=int, default=8)
     args = ap.parse_args(argv)
 
@@ -61,7 +63,8 @@ def main(argv=None) -> int:
                  max_rows=args.max_rows or max(256, args.batch + args.batch // 2))
     model = LocalLM(cfg, device=f"cuda:{local}", seed=rank)
     eng = LocalEngine(model, use_graphs=not args.no_graphs, jump_forward=not args.no_jump,
-                      shared_prefix=not args.no_shared_prefix, pipeline=not args.no_pipeline)
+                      shared_prefix=not args.no_shared_prefix, pipeline=not args.no_pipeline,
+                      admit_min=args.admit_min or None)
     para = ("The shop platform sells products to retail customers. Orders move from CART to PAID to "
             "SHIPPED; payments are captured through the payment gateway and refunds are issued by the "
             "back office. Inventory is reserved when an order is paid and released on cancellation.\n\n")
@@ -119,6 +122,9 @@ def main(argv=None) -> int:
             "prompt_tokens_per_s": round(prompt_all / elapsed, 1),
             "decode_step_ms": round(1e3 * st["decode_s"] / max(1, st["decode_steps"]), 3),
             "prefill_ms_avg": round(1e3 * st["prefill_s"] / max(1, st["prefills"]), 3),
+            "prefill_s": round(st["prefill_s"], 3), "prefill_batches": st["prefill_batches"],
+            "decode_s": round(st["decode_s"], 3), "host_ms_per_step": round(1e3 * st["host_s"] / max(1, st["decode_steps"]), 3),
+            "admit_min": eng.admit_min,
             "decode_steps": st["decode_steps"], "rows_per_step": round(st["decode_rows"] / max(1, st["decode_steps"]), 1),
             "elapsed_s": round(elapsed, 3), "classes": int(ok_all)}),
             flush=True)

@@ -9,3 +9,24 @@ REST), ``ops`` (HIP kernels for gfx950), ``parallel`` (fan-out / multi-GPU
 work distribution), ``utils``.
 """
 __version__ = "1.0.1"
+
+
+def _load_native_override() -> None:
+    """``DMCP_SRCSCAN_SO``: load that build of the native module as
+    ``dmcp._srcscan`` (the ASan/UBSan build, scripts/asan_tests.sh)."""
+    import os
+    import sys
+    path = os.environ.get("DMCP_SRCSCAN_SO")
+    if not path or "dmcp._srcscan" in sys.modules:
+        return
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("dmcp._srcscan", path)
+    if spec is None or spec.loader is None:
+        raise ImportError(f"DMCP_SRCSCAN_SO={path}: not a loadable module")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    sys.modules["dmcp._srcscan"] = mod
+    globals()["_srcscan"] = mod
+
+
+_load_native_override()

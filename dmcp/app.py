@@ -93,7 +93,9 @@ class App:
                                in_memory_sources=self.config.git_in_memory,
                                in_memory_max_bytes=self.config.git_in_memory_max_mb << 20,
                                lease_ttl_s=self.config.project_lease_seconds,
-                               stream_enrichment=self.config.enrich_stream)
+                               stream_enrichment=self.config.enrich_stream,
+                               scan_isolation=self.config.scan_isolation,
+                               scan_timeout_s=self.config.scan_timeout_seconds)
         self.projects = ProjectService(self.repos, self.cache)
         self.context = ContextService(self.repos, self.cache)
         self.graph_query = GraphQueryService(self.cache)

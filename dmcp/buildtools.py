@@ -5,6 +5,9 @@ Builds, into the source tree so the artefacts travel with the repo snapshot:
 * ``dmcp/_srcscan<ext>``  -- pybind11 module over ``native/srcscan`` (host C++17)
 * ``bin/srcscan``         -- the standalone analyzer CLI (go-analyzer replacement)
 * ``bin/srcscan-asan``    -- optional ASan/UBSan build of the CLI (``--sanitize``)
+* ``build/asan/_srcscan<ext>`` -- optional ASan/UBSan build of the Python
+  module (``--sanitize``); ``DMCP_SRCSCAN_SO=<path>`` makes ``dmcp`` load it,
+  under ``LD_PRELOAD=$(gcc -print-file-name=libasan.so)`` (scripts/asan_tests.sh)
 * ``dmcp/ops/_hipops<ext>`` -- HIP kernels for gfx950 (see :mod:`dmcp.ops.build`)
 
 Usage: ``python -m dmcp.buildtools [--sanitize] [--no-hip] [--force]``.
@@ -108,6 +111,42 @@ def build_srcscan(force: bool = False, sanitize: bool = False, jobs: int = 0) ->
     return target
 
 
+SAN_FLAGS = ["-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fPIC", "-pthread",
+             "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
+
+
+def asan_module_path() -> str:
+    return os.path.join(ROOT, "build", "asan", "_srcscan" + ext_suffix())
+
+
+def build_srcscan_asan(jobs: int = 0) -> str:
+    """The Python module with AddressSanitizer + UBSan (host code only):
+    every native path the server runs -- lexers, front-ends, in-memory tree,
+    loose-object inflater, bulk row writer, row builders -- instrumented."""
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    target = asan_module_path()
+    sources = [os.path.join(NATIVE, s) for s in os.listdir(NATIVE) if s.endswith((".cpp", ".hpp"))]
+    key = _digest(sources, " ".join(SAN_FLAGS) + sys.version)
+    stamp = target + ".stamp"
+    if os.path.exists(target) and os.path.exists(stamp) and open(stamp).read().strip() == key:
+        return target
+    objs = _compile_objects(SAN_FLAGS, "asan", jobs)
+    import pybind11  # noqa: WPS433 (build-time only)
+    inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", f"-I{NATIVE}"]
+    os.makedirs(os.path.dirname(target), exist_ok=True)
+    extra = []
+    for src in ["pymodule.cpp", *MODULE_SOURCES]:
+        obj = os.path.join(BUILD, src[:-4] + ".asan.o")
+        _run([CXX, *SAN_FLAGS, *inc, "-fvisibility=hidden", "-c", os.path.join(NATIVE, src), "-o", obj])
+        extra.append(obj)
+    tmp = target + ".tmp"
+    _run([CXX, *SAN_FLAGS, "-shared", "-o", tmp, *extra, *objs, "-l:libsqlite3.so.0", "-lz"])
+    os.replace(tmp, target)
+    with open(stamp, "w") as f:
+        f.write(key)
+    return target
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
@@ -116,6 +155,8 @@ def main(argv=None) -> int:
     ap.add_argument("-j", "--jobs", type=int, default=0)
     a = ap.parse_args(argv)
     print(build_srcscan(force=a.force, sanitize=a.sanitize, jobs=a.jobs))
+    if a.sanitize:
+        print(build_srcscan_asan(jobs=a.jobs))
     if not a.no_hip:
         try:
             from dmcp.ops import build as hipbuild

@@ -239,8 +239,14 @@ class LocalEngine:
     ADMIT_SEQS = 64
 
     def __init__(self, model: LocalLM, use_graphs: bool = True, max_prompt_tokens: Optional[int] = None,
-                 jump_forward: bool = True, shared_prefix: bool = True, pipeline: bool = True) -> None:
+                 jump_forward: bool = True, shared_prefix: bool = True, pipeline: bool = True,
+                 admit_min: Optional[int] = None) -> None:
         self.model = model
+        # a running batch admits new classes only once this many slots are
+        # free (or nothing else is pending): every admission stalls the whole
+        # decode batch for a prefill, so fewer, larger prefills (one GEMM per
+        # projection over all their tokens) cost less than one per freed slot
+        self.admit_min = max(1, admit_min if admit_min is not None else model.cfg.max_batch // 16)
         self.cfg: LMConfig = model.cfg
         dev = model.device
         self.masks = torch.tensor([_json_safe_mask(self.cfg.vocab_size, False),
@@ -474,7 +480,8 @@ class LocalEngine:
                         break
                     continue
                 # ---- admission: one batched prefill for all that fit
-                if pending and free_slots:
+                if pending and free_slots and (not active or len(free_slots) >= self.admit_min
+                                               or (feed.done and len(free_slots) >= len(pending))):
                     batch: List[_Seq] = []
                     ntok = 0
                     while pending and free_slots and len(batch) < self.ADMIT_SEQS:

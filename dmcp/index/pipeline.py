@@ -158,7 +158,10 @@ class Indexer:
                  parser_threads: int = 0, require_enrichment: bool = True,
                  max_source_chars: int = 200_000, in_memory_sources: bool = True,
                  in_memory_max_bytes: int = 1 << 30, lease_ttl_s: float = 60.0,
-                 stream_enrichment: bool = True) -> None:
+                 stream_enrichment: bool = True, scan_isolation: str = "auto",
+                 scan_timeout_s: float = 120.0) -> None:
+        self.scan_isolation = (scan_isolation or "auto").lower()
+        self.scan_timeout_s = scan_timeout_s
         self.lease_ttl_s = lease_ttl_s
         self.stream_enrichment = stream_enrichment
         self.in_memory_sources = in_memory_sources
@@ -231,9 +234,10 @@ class Indexer:
                 # the native scan hands the class / method rows to the writer
                 # as soon as it has them (fresh UUIDv7s; not with given test ids)
                 rows = (writer.static_rows(now, clone.commit_hash)
-                        if self.scan_rows and self.native_phase1 and self.phase1_ids is None else None)
+                        if self.scan_rows and self.native_phase1 and self.phase1_ids is None
+                        and not self._isolate(url) else None)
                 with span("analyze.parse", stats):
-                    parsed = parser.scan_tree(clone, rows=rows)
+                    parsed = self._scan(parser, clone, url, rows=rows)
                     graph = parsed.build_graph()
                 LOG.info("Graph built: %d nodes, %d entry points", graph.node_count(), graph.entry_point_count())
                 order = graph.analysis_order()
@@ -292,6 +296,18 @@ class Indexer:
                     clone.cleanup()
             lease.release()
             lock.release()
+
+    def _isolate(self, url: RepositoryUrl) -> Optional[float]:
+        """Scan time limit when the scan must run in a child process: remote
+        repositories under "auto" (untrusted input; the reference likewise
+        ran its native analyzer out of process, GoSourceParser.java:339-418)."""
+        if self.scan_isolation == "process" or (self.scan_isolation == "auto" and url.local_path() is None):
+            return self.scan_timeout_s
+        return None
+
+    def _scan(self, parser: SourceParser, tree: SourceTree, url: RepositoryUrl, rows=None) -> ParsedProject:
+        iso = self._isolate(url)
+        return parser.scan_tree(tree, rows=None if iso else rows, isolate_timeout_s=iso)
 
     def _submit_io(self, fn, *args):
         with self._io_guard:
@@ -684,7 +700,7 @@ class Indexer:
             with span("rebuild.total", stats, project=project.name):
                 clone = self._fetch(project.repository_url, project.default_branch, shallow=True)
                 parser = parser_for(clone.detect_language(), self.parser_threads)
-                parsed = parser.scan_tree(clone)
+                parsed = self._scan(parser, clone, project.repository_url)
                 graph = parsed.build_graph()
                 existing = self.repos.classes.find_by_project_id(project_id)
                 by_name = {sc.full_class_name: sc for sc in existing}
@@ -800,7 +816,7 @@ class Indexer:
                 if readme is not None:
                     project.update_description(readme[:self.description_length])
                 parser = parser_for(clone.detect_language(), self.parser_threads)
-                parsed = parser.scan_tree(clone)
+                parsed = self._scan(parser, clone, project.repository_url)
                 graph = parsed.build_graph()
                 existing = self.repos.classes.find_by_project_id(project.id)
                 by_name = {sc.full_class_name: sc for sc in existing}
@@ -960,7 +976,8 @@ class Indexer:
                 if graph is None:
                     raise DomainError("No graph data available for this project", "NO_GRAPH")
                 clone = self._fetch(project.repository_url, project.default_branch, shallow=True)
-                parsed = parser_for(clone.detect_language(), self.parser_threads).scan_tree(clone)
+                parsed = self._scan(parser_for(clone.detect_language(), self.parser_threads), clone,
+                                    project.repository_url)
                 readme = clone.readme(self.max_readme_length)
                 recovered = self._recover_unenriched(project, parsed, graph, clone, readme)
                 project.update_graph_data(graph.to_json())

@@ -220,14 +220,20 @@ class SourceParser:
                  (time.perf_counter() - t0) * 1e3, self.project.stats.get("elapsedUs", 0) / 1e3)
         return self.project
 
-    def scan_tree(self, tree, rows=None) -> ParsedProject:
+    def scan_tree(self, tree, rows=None, isolate_timeout_s: Optional[float] = None) -> ParsedProject:
         """Scans a :class:`dmcp.index.source.SourceTree` (in-memory git snapshot
         or checkout) -- same result as :meth:`scan` over a checkout of it.
         ``rows``: :meth:`ProjectRowsWriter.static_rows` -- the native scan then
         hands the class / method rows to the writer before it builds any
-        Python object (their ids in ``ParsedProject.static_row_ids``)."""
+        Python object (their ids in ``ParsedProject.static_row_ids``).
+        ``isolate_timeout_s``: run the scan in a child process killed after
+        that many seconds (:mod:`dmcp.parsers.isolated`; ``rows`` unused)."""
         t0 = time.perf_counter()
-        doc = tree.scan_objects(self.language_name, self.threads, self.framework_override, rows=rows)
+        if isolate_timeout_s:
+            from .isolated import scan_in_child
+            doc = scan_in_child(tree, self.language_name, self.threads, self.framework_override, isolate_timeout_s)
+        else:
+            doc = tree.scan_objects(self.language_name, self.threads, self.framework_override, rows=rows)
         if doc is None:
             doc = json.loads(tree.scan(self.language_name, self.threads, self.framework_override))
         self.project = to_parsed_project(doc)

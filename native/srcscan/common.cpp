@@ -193,9 +193,50 @@ std::string_view unquote(std::string_view lit) {
 }
 
 // ------------------------------------------------------------------ JSON
+namespace {
+// Length of the well-formed UTF-8 sequence at s[i] (RFC 3629: no overlongs,
+// no surrogates, nothing past U+10FFFF), 0 when it is not one.
+size_t utf8_seq(std::string_view s, size_t i) {
+    const unsigned char c = (unsigned char)s[i];
+    size_t n;
+    unsigned lo = 0x80, hi = 0xBF;
+    if (c >= 0xC2 && c <= 0xDF) n = 2;
+    else if (c >= 0xE0 && c <= 0xEF) {
+        n = 3;
+        if (c == 0xE0) lo = 0xA0;
+        if (c == 0xED) hi = 0x9F;
+    } else if (c >= 0xF0 && c <= 0xF4) {
+        n = 4;
+        if (c == 0xF0) lo = 0x90;
+        if (c == 0xF4) hi = 0x8F;
+    } else
+        return 0;
+    if (i + n > s.size()) return 0;
+    const unsigned char c1 = (unsigned char)s[i + 1];
+    if (c1 < lo || c1 > hi) return 0;
+    for (size_t k = 2; k < n; ++k)
+        if (((unsigned char)s[i + k] & 0xC0) != 0x80) return 0;
+    return n;
+}
+}  // namespace
+
 void JsonWriter::str(std::string_view s) {
     out += '"';
-    for (unsigned char c : s) {
+    for (size_t i = 0; i < s.size(); ++i) {
+        const unsigned char c = (unsigned char)s[i];
+        if (c >= 0x80) {
+            // source files are not always UTF-8 (Latin-1 comments, binary
+            // junk): an invalid byte becomes U+FFFD, so the document is
+            // always valid JSON text
+            const size_t n = utf8_seq(s, i);
+            if (n == 0) {
+                out += "\xEF\xBF\xBD";
+            } else {
+                out.append(s.data() + i, n);
+                i += n - 1;
+            }
+            continue;
+        }
         switch (c) {
             case '"': out += "\\\""; break;
             case '\\': out += "\\\\"; break;

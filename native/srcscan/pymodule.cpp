@@ -7,6 +7,7 @@
 #include <cctype>
 #include <chrono>
 #include <cstring>
+#include <deque>
 #include <memory>
 #include <thread>
 #include <unordered_map>
@@ -108,7 +109,11 @@ srcscan::ScanResult scan_mounted(py::list files, const std::string& language, in
     }
 }
 
-py::str pystr(const std::string& s) { return py::str(s.data(), s.size()); }
+py::str pystr(const std::string& s) {
+    PyObject* o = PyUnicode_DecodeUTF8(s.data(), static_cast<Py_ssize_t>(s.size()), "replace");
+    if (!o) throw py::error_already_set();
+    return py::reinterpret_steal<py::str>(o);
+}
 
 // ------------------------------------------------------------- Phase 1 rows
 // json.dumps(list_of_str) with the default separators and ensure_ascii=True,
@@ -207,21 +212,33 @@ PyObject* getattr_borrowed(PyObject* o, const char* name, std::vector<py::object
 }
 
 // One Python str per distinct value (new references handed out).
+// Invalid UTF-8 in a source (Latin-1 identifiers, junk bytes) becomes U+FFFD
+// instead of failing the whole project's scan with a UnicodeDecodeError.
 struct StrCache {
     std::unordered_map<std::string_view, PyObject*> map;
+    std::deque<std::string> owned;  // keys of values whose bytes were not valid UTF-8
     ~StrCache() {
         for (auto& kv : map) Py_DECREF(kv.second);
     }
     PyObject* get(const std::string& v) {
         auto it = map.find(std::string_view(v));
         if (it == map.end()) {
-            PyObject* o = PyUnicode_DecodeUTF8(v.data(), static_cast<Py_ssize_t>(v.size()), "strict");
+            PyObject* o = PyUnicode_DecodeUTF8(v.data(), static_cast<Py_ssize_t>(v.size()), "replace");
             if (!o) throw py::error_already_set();
-            // the key views the str's own UTF-8 buffer (alive while cached)
+            // the key views the str's own UTF-8 buffer (alive while cached) --
+            // or a copy of the raw bytes when replacement changed them
             Py_ssize_t n = 0;
             const char* u = PyUnicode_AsUTF8AndSize(o, &n);
-            if (!u) throw py::error_already_set();
-            it = map.emplace(std::string_view(u, static_cast<size_t>(n)), o).first;
+            if (!u) {
+                Py_DECREF(o);
+                throw py::error_already_set();
+            }
+            std::string_view key(u, static_cast<size_t>(n));
+            if (key != std::string_view(v)) {
+                owned.emplace_back(v);
+                key = owned.back();
+            }
+            it = map.emplace(key, o).first;
         }
         return Py_NewRef(it->second);
     }
@@ -273,7 +290,7 @@ py::dict scan_result_objects(const srcscan::ScanResult& r, py::handle method_cls
     // verbs, dependency / parameter targets, exception names) share one str.
     StrCache shared;
     auto fresh = [](const std::string& v) {
-        PyObject* o = PyUnicode_DecodeUTF8(v.data(), static_cast<Py_ssize_t>(v.size()), "strict");
+        PyObject* o = PyUnicode_DecodeUTF8(v.data(), static_cast<Py_ssize_t>(v.size()), "replace");
         if (!o) throw py::error_already_set();
         return o;
     };

@@ -345,3 +345,45 @@ def test_native_ref_reader_refuses_names_git_refuses(tmp_path):
     for bad in ["refs/heads/../../../evil", "../../evil", "/etc/passwd", "refs/heads/a.lock", "refs/heads/x@{1}",
                 "refs/heads/.hidden", "refs/heads/a b", "refs/heads//x", "refs/heads/x."]:
         assert _srcscan.resolve_ref(gd, [bad]) is None, bad
+
+
+def test_isolated_scan_matches_in_process_and_survives_faults(tmp_path):
+    """The child-process scan (remote repositories) returns the in-process
+    document; a crashing or hanging child becomes ScanFailed, and through
+    analyze_project an ANALYSIS_FAILED project while this process lives on
+    (GoSourceParser.java:62, 339-418: 120 s kill of the native analyzer)."""
+    import pytest
+    from conftest import make_app
+    from dmcp.index.git import GitClient
+    from dmcp.models.domain import ProjectStatus, RepositoryUrl
+    from dmcp.parsers.base import parser_for
+    from dmcp.parsers.isolated import ScanFailed, scan_in_child
+    from dmcp.utils import synth
+    from dmcp.utils.errors import DomainError
+    repo = tmp_path / "shop"
+    synth.java_spring_repo(str(repo), 24)
+    tree = GitClient(str(tmp_path / "c")).snapshot(RepositoryUrl.of(str(repo)), None)
+    inproc = parser_for("java").scan_tree(tree)
+    iso = parser_for("java").scan_tree(tree, isolate_timeout_s=60)
+    assert set(iso.units) == set(inproc.units) and len(iso.units) == 25
+    a, b = inproc.units["co.acme.shop.order.OrderController"], iso.units["co.acme.shop.order.OrderController"]
+    assert a.methods == b.methods and a.params == b.params and a.class_type == b.class_type
+    with pytest.raises(ScanFailed, match="signal"):
+        scan_in_child(tree, "java", 1, "", 60, env_extra={"DMCP_SCAN_CHILD_FAULT": "crash"})
+    with pytest.raises(ScanFailed, match="did not finish"):
+        scan_in_child(tree, "java", 1, "", 2, env_extra={"DMCP_SCAN_CHILD_FAULT": "hang"})
+    app = make_app(tmp_path, scan_isolation="process", scan_timeout_seconds=2.0)
+    assert app.indexer.analyze_project(str(repo)).success  # isolated, healthy
+    import os
+    os.environ["DMCP_SCAN_CHILD_FAULT"] = "hang"
+    try:
+        with pytest.raises(DomainError) as e:
+            app.indexer.analyze_project(str(repo))
+    finally:
+        del os.environ["DMCP_SCAN_CHILD_FAULT"]
+    assert e.value.error_code == "ANALYSIS_FAILED" and "did not finish" in str(e.value)
+    p = app.repos.projects.find_by_name("shop")
+    assert p.status is ProjectStatus.ERROR
+    assert app.repos.classes.count_by_project()[p.id] == 25  # the previous analysis' rows survive
+    assert app.indexer.analyze_project(str(repo)).success  # and the server carries on
+    app.close()

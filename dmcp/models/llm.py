@@ -177,8 +177,6 @@ class LocalLM:
     prefix key once per 32 queries instead of once per row, and prefill of a
     sequence starts after it (:meth:`fork_prefix`)."""
 
-    PREFIX_CHUNK = 256  # prefix keys per MFMA work item
-
     def __init__(self, cfg: LMConfig, device: str = "cuda", seed: int = 0,
                  weights: Optional[Dict[str, torch.Tensor]] = None, shared_prefix: bool = True) -> None:
         if cfg.n_heads % cfg.n_kv_heads:
@@ -203,13 +201,11 @@ class LocalLM:
         self.cos_sin = ops.rope_tables(c.max_seq, c.head_dim, c.rope_theta, device=self.device).contiguous()
         self.scale = 1.0 / math.sqrt(c.head_dim)
         self.max_rows = max(c.max_batch, c.max_rows)
-        # shared prefix: V transposed per layer (the MFMA kernel's A operand),
-        # length in device memory so captured decode graphs follow it
+        # shared prefix: its length in device memory, so captured decode
+        # graphs follow it
         self.prefix_len = 0
         self.prefix_tokens: tuple = ()
         self.prefix_dev = torch.zeros(1, dtype=torch.int32, device=self.device)
-        self.prefix_vt = (torch.zeros((c.layers, c.n_kv_heads, c.head_dim, c.max_seq), dtype=self.kv_dtype,
-                                      device=self.device) if shared_prefix else None)
         # fused decode GEMMs for steps of <= fused_max_rows rows (GPU only;
         # DMCP_FUSED_GEMM=0 forces the hipBLASLt path)
         self.use_fused = (self.device.type == "cuda" and os.environ.get("DMCP_FUSED_GEMM", "1") != "0"
@@ -225,7 +221,7 @@ class LocalLM:
         # (fp8: fused 1.47 vs 1.64 ms at 16 rows, 1.80 vs 1.70 at 24, 1.82 vs
         # 1.73 at 32 -- profiles/decode_fused_rows_r2.txt)
         self.fused_max_rows = min(ops.FUSED_MAX_ROWS, int(os.environ.get("DMCP_FUSED_MAX_ROWS", "16")))
-        ps = max(ops.prefix_splits(c.max_seq, self.PREFIX_CHUNK), ops.PREFIX_MFMA_MAX_SPLITS) if shared_prefix else 0
+        ps = ops.PREFIX_MFMA_MAX_SPLITS if shared_prefix else 0
         self.attn_ws = (ops.decode_workspace(self.max_rows, c.n_heads, c.n_kv_heads, c.head_dim, c.max_seq,
                                              self.device, prefix_slots=ps) if self.device.type == "cuda" else None)
         # down projection + residual + next norm on the split-K LDS kernel at
@@ -485,8 +481,8 @@ class LocalLM:
     def _prefix(self, i: int):
         if not self.shared_prefix:
             return None
-        return ops.SharedPrefix(self.k_cache[i][self.prefix_slot], self.prefix_vt[i], self.prefix_dev,
-                                self.PREFIX_CHUNK, self.v_cache[i][self.prefix_slot])
+        return ops.SharedPrefix(self.k_cache[i][self.prefix_slot], self.v_cache[i][self.prefix_slot],
+                                self.prefix_dev)
 
     def _decode_fused(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:
         """The decode step on the fused gfx950 GEMMs: per layer QKV (+norm,
@@ -525,7 +521,6 @@ class LocalLM:
             return P
         self.clear_prefix()
         self.forward_tokens(torch.tensor(toks, dtype=torch.int32), self.prefix_slot, 0)
-        self.prefix_vt[:, :, :, :P].copy_(self.v_cache[:, self.prefix_slot, :, :P].transpose(-1, -2))
         self.prefix_len, self.prefix_tokens = P, toks
         self.prefix_dev.fill_(P)
         return P

@@ -87,12 +87,6 @@ def decode_workspace(rows, n_heads, n_kv_heads, head_dim, max_seq, device, chunk
     return _hip().decode_workspace(rows, n_heads, n_kv_heads, head_dim, max_seq, device, chunk, prefix_slots)
 
 
-def prefix_splits(ldv, pchunk):
-    """Shared-prefix partial slots per (row, head) for a prefix capacity ``ldv``."""
-    from .hip import prefix_splits as _ps
-    return _ps(ldv, pchunk)
-
-
 def rope_kv(qkv, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out=None):
     return (_hip() if qkv.is_cuda else reference).rope_kv(qkv, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out)
 

@@ -14,8 +14,6 @@
 // ABI: extern "C" launchers taking raw device pointers and a hipStream_t;
 // they return hipError_t (0 = success).  Shapes are validated on the host
 // side (dmcp/ops/hip.py) before any launch.
-#include <mutex>
-
 #include "dmcp_common.hpp"
 
 // shared-prefix partials on the MFMA prefill kernel (prefill_attn.hip)
@@ -183,201 +181,12 @@ __global__ __launch_bounds__(kBlock) void rope_kv_kernel(const uint16_t* __restr
 }
 
 // --------------------------------------------------------------------------
-// 3. decode attention (one query token per sequence), GQA, split-K.
-//    q [B, Hq, D] bf16; k/v cache [S, Hkv, MAXS, D]; slot[B]; seq_len[B]
-//    grid (splits, Hkv, B); block 256 = 4 waves.  LPK = D/8 lanes share one
-//    key row (16 B each), KPW = 64/LPK keys per wave step.  Each lane group
-//    runs an online softmax over its keys for the G query heads of this kv
-//    head; groups merge by shuffles, waves through LDS; only the splits that
-//    own keys (nact = ceil(L / chunk)) run: with nact == 1 the block writes
-//    the output directly, otherwise fp32 partials merged by
-//    decode_attn_combine_kernel.
+// 3. decode attention (one query token per row), GQA, split-K: the per-row
+//    MFMA kernel (3c below) writes fp32 partials (or the output directly
+//    when a row fits one split and there is no shared prefix); the shared
+//    prefix's partials come from the MFMA prefill kernel in prefix mode
+//    (prefill_attn.hip); this kernel merges them.
 // --------------------------------------------------------------------------
-//    Shared-prefix mode (plen != nullptr, *plen = P > 0): every row's first P
-//    keys are a prefix shared by all rows and are attended by
-//    prefix_attn_kernel; this kernel covers keys [P, L) only and always
-//    writes partials, at split index ps_max + split.
-template <int D, int G>
-__global__ __launch_bounds__(kBlock) void decode_attn_kernel(
-    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache,
-    const int32_t* __restrict__ slot, const int32_t* __restrict__ seq_len, uint16_t* __restrict__ out,
-    float* __restrict__ part_o, float* __restrict__ part_ml, int B, int Hkv,
-    int max_seq, int chunk, int splits, float scale_log2, int num_slots, const int32_t* __restrict__ plen,
-    int ps_max) {
-    constexpr int LPK = D / 8;
-    constexpr int KPW = kWave / LPK;
-    constexpr int NW = kBlock / kWave;
-    constexpr int NK = G >= 6 ? 2 : 4;  // keys per lane per iteration (VGPR budget at G >= 6)
-    const int Hq = Hkv * G;
-    const int P = plen ? max(0, *plen) : 0;
-    const int splits_total = ps_max + splits;
-    // Persistent grid over split-major work items (split, row, kv head).  A
-    // grid of splits*Hkv*B blocks where most splits are empty (short rows)
-    // spent ~100 us launching waves that exit at once (profiles/decode_*);
-    // here the empty items cost one cached load + a branch.
-    const int per_split = B * Hkv;
-    const int total = splits * per_split;
-    __shared__ float sm_m[NW][G], sm_l[NW][G];
-    __shared__ float sm_acc[NW][G][D];
-    for (int item = blockIdx.x; item < total; item += gridDim.x) {
-    const int split = item / per_split;
-    const int rem = item - split * per_split;
-    const int b = rem / Hkv, kh = rem - b * Hkv;
-    const int s = slot[b];
-    const int L = (s >= 0 && s < num_slots) ? min(seq_len[b], max_seq) : 0;  // never read a bad slot
-    // splits that own keys past the shared prefix; the others are skipped
-    if (L <= 0) {  // padding row / bad slot: defined output, nothing read
-        if (split == 0)
-            for (int o = threadIdx.x; o < G * D; o += kBlock) out[((size_t)b * Hq + kh * G) * D + o] = 0;
-        continue;
-    }
-    const SplitGeom sg = split_geom(L - P, splits, chunk);
-    if (split >= sg.nact) continue;
-    const bool direct = P == 0 && sg.nact == 1;  // the whole context in this block: no merge
-    const int start = P + split * sg.part;
-    const int end = min(L, start + sg.part);
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wave = threadIdx.x / kWave;
-    const int kig = lane / LPK;  // key slot within the wave step
-    const int sub = lane % LPK;  // which 8 dims
-
-    float qv[G][8];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        const uint16_t* qp = q + ((size_t)b * Hq + (size_t)kh * G + g) * D + sub * 8;
-        unpack8(*reinterpret_cast<const uint4*>(qp), qv[g]);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) qv[g][j] *= scale_log2;
-    }
-    float m[G], l[G], acc[G][8];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        m[g] = -1e30f;
-        l[g] = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
-    }
-    const size_t head_off = ((size_t)(L > 0 ? s : 0) * Hkv + kh) * (size_t)max_seq * D;
-    const uint16_t* kb = k_cache + head_off + sub * 8;
-    const uint16_t* vb = v_cache + head_off + sub * 8;
-    // NK independent 16 B K and V loads in flight per lane per iteration
-    // (memory-level parallelism: the kernel is HBM-bound)
-    constexpr int STEP = NW * KPW;
-    for (int k0 = start + wave * KPW; k0 < end; k0 += NK * STEP) {
-        uint4 kr[NK], vr[NK];
-        bool ok[NK];
-#pragma unroll
-        for (int r = 0; r < NK; ++r) {
-            const int kk = k0 + kig + r * STEP;
-            ok[r] = kk < end;
-            kr[r] = make_uint4(0, 0, 0, 0);
-            vr[r] = make_uint4(0, 0, 0, 0);
-            if (ok[r]) {
-                kr[r] = *reinterpret_cast<const uint4*>(kb + (size_t)kk * D);
-                vr[r] = *reinterpret_cast<const uint4*>(vb + (size_t)kk * D);
-            }
-        }
-        // scores of the NK keys first, then ONE online-softmax rescale per
-        // head per iteration (not per key)
-        float sc[NK][G];
-#pragma unroll
-        for (int r = 0; r < NK; ++r) {
-            float kf[8];
-            unpack8(kr[r], kf);
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                float d = 0.f;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) d += qv[g][j] * kf[j];
-#pragma unroll
-                for (int msk = 1; msk < LPK; msk <<= 1) d += __shfl_xor(d, msk, kWave);
-                sc[r][g] = ok[r] ? d : -1e30f;
-            }
-        }
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            float mn = m[g];
-#pragma unroll
-            for (int r = 0; r < NK; ++r) mn = fmaxf(mn, sc[r][g]);
-            const float corr = exp2f(m[g] - mn);
-            l[g] *= corr;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) acc[g][j] *= corr;
-            m[g] = mn;
-        }
-#pragma unroll
-        for (int r = 0; r < NK; ++r) {
-            float vf[8];
-            unpack8(vr[r], vf);
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                const float pr = ok[r] ? exp2f(sc[r][g] - m[g]) : 0.f;
-                l[g] += pr;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) acc[g][j] += pr * vf[j];
-            }
-        }
-    }
-    // merge the KPW key groups of this wave (lanes differing in kig)
-#pragma unroll
-    for (int msk = LPK; msk < kWave; msk <<= 1) {
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const float mo = __shfl_xor(m[g], msk, kWave);
-            const float lo = __shfl_xor(l[g], msk, kWave);
-            const float mn = fmaxf(m[g], mo);
-            const float ca = exp2f(m[g] - mn), cb = exp2f(mo - mn);
-            l[g] = l[g] * ca + lo * cb;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float ao = __shfl_xor(acc[g][j], msk, kWave);
-                acc[g][j] = acc[g][j] * ca + ao * cb;
-            }
-            m[g] = mn;
-        }
-    }
-    // merge the waves through LDS: lanes [0, LPK) of each wave hold the result
-    __syncthreads();  // the previous item's readers are done with sm_*
-    if (lane < LPK) {
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            if (sub == 0) {
-                sm_m[wave][g] = m[g];
-                sm_l[wave][g] = l[g];
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) sm_acc[wave][g][sub * 8 + j] = acc[g][j];
-        }
-    }
-    __syncthreads();
-    // G*D outputs, one per thread (G*D <= 1024 -> up to 4 per thread)
-    for (int o = threadIdx.x; o < G * D; o += kBlock) {
-        const int g = o / D, d = o - g * D;
-        float mx = -1e30f;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) mx = fmaxf(mx, sm_m[w][g]);
-        float lt = 0.f, at = 0.f;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            const float c = exp2f(sm_m[w][g] - mx);
-            lt += sm_l[w][g] * c;
-            at += sm_acc[w][g][d] * c;
-        }
-        const int qh = kh * G + g;
-        if (direct) {
-            out[((size_t)b * Hq + qh) * D + d] = f2bf(lt > 0.f ? at / lt : 0.f);
-        } else {
-            const size_t pi = ((size_t)b * Hq + qh) * splits_total + ps_max + split;
-            part_o[pi * D + d] = at;
-            if (d == 0) {
-                part_ml[pi * 2] = mx;
-                part_ml[pi * 2 + 1] = lt;
-            }
-        }
-    }
-    }  // work items
-}
-
 // Split-K merge.  One wave per (row, q head): lane = (4-output group
 // dg = lane % (D/4), partial group pg = lane / (D/4)); each lane merges
 // every (64/(D/4))-th partial with float4 loads issued 8 at a time, then
@@ -397,7 +206,7 @@ __global__ __launch_bounds__(kBlock) void decode_attn_combine_kernel(const float
                                                                     uint16_t* __restrict__ out, int B, int Hq,
                                                                     int max_seq, int chunk, int splits,
                                                                     int num_slots, const int32_t* __restrict__ plen,
-                                                                    int ps_max, int pchunk) {
+                                                                    int ps_max) {
     constexpr int U = 8;
     constexpr int DQ = D / 4;       // lanes per partial group
     constexpr int PG = kWave / DQ;  // partial groups per wave
@@ -405,9 +214,9 @@ __global__ __launch_bounds__(kBlock) void decode_attn_combine_kernel(const float
     const int dg = lane % DQ, pg = lane / DQ;
     const int P = plen ? max(0, *plen) : 0;
     const int splits_total = ps_max + splits;
-    // prefix partials: ceil(P / pchunk) of the 256-key prefix kernel, or all
-    // ps_max of the MFMA prefill-kernel path (pchunk 0; empty ones weigh 0)
-    const int npre = P > 0 ? (pchunk > 0 ? min(ps_max, (P + pchunk - 1) / pchunk) : ps_max) : 0;
+    // the shared prefix's ps_max partials (prefill kernel in prefix mode;
+    // splits past the prefix's end are empty and weigh 0)
+    const int npre = P > 0 ? ps_max : 0;
     const int nwaves = gridDim.x * (kBlock / kWave);
     for (int w = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave; w < B * Hq; w += nwaves) {
         const int b = w / Hq, qh = w - b * Hq;
@@ -464,196 +273,6 @@ __global__ __launch_bounds__(kBlock) void decode_attn_combine_kernel(const float
             const float inv = lt > 0.f ? 1.f / lt : 0.f;
             const float f[4] = {a0 * inv, a1 * inv, a2 * inv, a3 * inv};
             *reinterpret_cast<uint2*>(out + ((size_t)b * Hq + qh) * D + 4 * dg) = pack4(f);
-        }
-    }
-}
-
-// --------------------------------------------------------------------------
-// 3b. shared-prefix attention (cascade decoding), MFMA.
-//    Every row of a decode step shares its first P keys (the enrichment
-//    prompt's instructions + README, identical for all classes of a project).
-//    The per-row kernel above would stream those P keys once PER ROW; here
-//    the queries of all rows that map to one kv head are batched into the N
-//    dimension of two MFMA products per 32-key tile:
-//        S^T[key, query] = K[key, :] . Q^T[:, query]     (32x32x16 bf16, D/16 steps)
-//        O^T[d, query]  += V^T[d, key] . P^T[key, query]  (32x32x16 bf16, 2 steps)
-//    S^T comes out with the query on the lane and the 32 keys in registers,
-//    so the online softmax is in-register plus one cross-half shuffle, the
-//    running max/sum stay per lane, and P^T feeds the second MFMA as its B
-//    operand with no data movement (accumulator-as-operand idiom, guide
-//    section "Fragment layout"; its permuted k order is matched by the V^T
-//    fragment).
-//    Work item = (kv head, PCH-key prefix split, group of 4 query tiles): the
-//    block stages the split's K rows and V^T columns in LDS once (padded
-//    rows: conflict-free fragment reads) and each of its 4 waves runs one
-//    32-query tile over them -- every prefix key leaves HBM/L2 once per 128
-//    queries.  V comes from a transposed copy of the prefix (vt [Hkv, D,
-//    ldv], built once per prefix) so the staging loads are 16-byte rows.
-//    Output: fp32 partials (log2-domain max, sum) at split index
-//    [0, ps_max), merged by decode_attn_combine_kernel.
-// --------------------------------------------------------------------------
-
-
-constexpr int kPrefixChunk = 256;  // keys per prefix split (host passes the same)
-
-template <int D, bool KV8>
-__global__ __launch_bounds__(kBlock) void prefix_attn_kernel(
-    const uint16_t* __restrict__ q, const void* __restrict__ pk, const void* __restrict__ vt,
-    const int32_t* __restrict__ plen, float* __restrict__ part_o, float* __restrict__ part_ml, int B, int Hkv, int G,
-    int ldk, int ldv, int ps_max, int splits_total, float scale_log2) {
-    constexpr int PCH = kPrefixChunk;
-    constexpr int KS = D / 16;       // k-steps of the QK product
-    constexpr int DT = D / 32;       // 32-row d tiles of the PV product
-    constexpr int KST = D + 8;       // padded LDS row strides (elements)
-    constexpr int VST = PCH + 8;
-    constexpr int NWAVE = kBlock / kWave;
-    __shared__ __attribute__((aligned(16))) uint16_t sK[PCH * KST];
-    __shared__ __attribute__((aligned(16))) uint16_t sV[D * VST];
-    const int P = min(*plen, ldv);
-    if (P <= 0) return;
-    const int Hq = Hkv * G;
-    const int nq = B * G;
-    const int qtiles = (nq + 31) / 32;
-    const int qgroups = (qtiles + NWAVE - 1) / NWAVE;
-    const int npre = min(ps_max, (P + PCH - 1) / PCH);
-    const int total = Hkv * npre * qgroups;
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wave = threadIdx.x / kWave;
-    const int r = lane & 31, h = lane >> 5;
-    for (int item = blockIdx.x; item < total; item += gridDim.x) {
-        const int qg = item % qgroups;
-        const int rest = item / qgroups;
-        const int sp = rest % npre;
-        const int kh = rest / npre;
-        const int kbeg = sp * PCH, kend = min(P, kbeg + PCH);
-        __syncthreads();  // the previous item's readers are done with sK / sV
-        // stage K rows [kbeg, kbeg+PCH) and V^T columns of the split (zeros
-        // past kend): every thread issues all of its 16-byte loads before its
-        // first LDS store, so the block waits for one memory latency, not one
-        // per load
-        {
-            constexpr int KU = PCH * (D / 8) / kBlock;  // uint4 per thread, K
-            constexpr int VU = D * (PCH / 8) / kBlock;  // uint4 per thread, V^T
-            const size_t kg = ((size_t)kh * ldk + kbeg) * D;  // element offsets (bf16 or fp8 caches)
-            const size_t vg = (size_t)kh * D * ldv + kbeg;
-            uint4 kx[KU], vx[VU];
-#pragma unroll
-            for (int i = 0; i < KU; ++i) {
-                const int u = threadIdx.x + i * kBlock;
-                const int row = u / (D / 8), c = u - row * (D / 8);
-                kx[i] = kbeg + row < kend ? load_kv8<KV8>(pk, kg + (size_t)row * D + c * 8) : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (int i = 0; i < VU; ++i) {
-                const int u = threadIdx.x + i * kBlock;
-                const int d = u / (PCH / 8), c = u - d * (PCH / 8);
-                vx[i] = kbeg + c * 8 < kend ? load_kv8<KV8>(vt, vg + (size_t)d * ldv + c * 8) : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (int i = 0; i < KU; ++i) {
-                const int u = threadIdx.x + i * kBlock;
-                const int row = u / (D / 8), c = u - row * (D / 8);
-                *reinterpret_cast<uint4*>(sK + row * KST + c * 8) = kx[i];
-            }
-            // V^T image with the key order permuted inside each 16-key group
-            // (bits 2 and 3 swapped) so that the 8 keys one PV fragment needs
-            // -- 16s+4h+{0..3} and 16s+8+4h+{0..3}, the accumulator's k order --
-            // are 16 contiguous bytes: one ds_read_b128 per fragment.  Keys
-            // 8c..8c+7 have bit 3 = c & 1; their halves (bit 2 = 0 / 1) land
-            // at +4*(c&1) and +8+4*(c&1) of the 16-key group.
-#pragma unroll
-            for (int i = 0; i < VU; ++i) {
-                const int u = threadIdx.x + i * kBlock;
-                const int d = u / (PCH / 8), c = u - d * (PCH / 8);
-                uint16_t* dst = sV + d * VST + (c >> 1) * 16 + (c & 1) * 4;
-                *reinterpret_cast<uint2*>(dst) = make_uint2(vx[i].x, vx[i].y);
-                *reinterpret_cast<uint2*>(dst + 8) = make_uint2(vx[i].z, vx[i].w);
-            }
-        }
-        __syncthreads();
-        const int qt = qg * NWAVE + wave;
-        if (qt >= qtiles) continue;
-        const int qi = qt * 32 + r;  // this lane's query (the MFMA column)
-        const bool qok = qi < nq;
-        const int b = qok ? qi / G : 0, g = qok ? qi - (qi / G) * G : 0;
-        const uint16_t* qp = q + ((size_t)b * Hq + (size_t)kh * G + g) * D + 8 * h;
-        bf16x8_t qf[KS];
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
-            qf[ks] = as_bf16x8(qok ? *reinterpret_cast<const uint4*>(qp + ks * 16) : make_uint4(0, 0, 0, 0));
-        float m = -1e30f, l = 0.f;  // m is kept equal across the two lane halves; l is per half
-        f32x16_t o[DT];
-#pragma unroll
-        for (int t = 0; t < DT; ++t)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) o[t][i] = 0.f;
-        const int ntile = (kend - kbeg + 31) / 32;
-        for (int kt = 0; kt < ntile; ++kt) {
-            const int k0 = kbeg + kt * 32;
-            f32x16_t s;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) s[i] = 0.f;
-            const uint16_t* kl = sK + (kt * 32 + r) * KST + 8 * h;
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks)
-                s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(*reinterpret_cast<const uint4*>(kl + ks * 16)),
-                                                            qf[ks], s, 0, 0, 0);
-            // register i holds key k0 + (i&3) + 8*(i>>2) + 4*h of query r.  VALU
-            // budget per tile (the kernel's bound, not the MFMAs): the key
-            // mask only on a partial last tile, the scale folded into one FMA
-            // per score, the rescale skipped while no lane's max moved, and
-            // hardware bf16 packing (v_cvt_pk_bf16_f32).
-            float mt = -1e30f;
-            if (k0 + 32 <= kend) {
-#pragma unroll
-                for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[i]);
-            } else {
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int key = k0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                    s[i] = key < kend ? s[i] : -1e30f;
-                    mt = fmaxf(mt, s[i]);
-                }
-            }
-            mt = half_swap_max(mt) * scale_log2;
-            const float mn = fmaxf(m, mt);
-            if (__any(mn > m)) {
-                const float corr = __builtin_amdgcn_exp2f(m - mn);
-                l *= corr;
-#pragma unroll
-                for (int t = 0; t < DT; ++t)
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) o[t][i] *= corr;
-            }
-            m = mn;
-            f32x8_t p0, p1;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                p0[i] = __builtin_amdgcn_exp2f(fmaf(s[i], scale_log2, -mn));
-                p1[i] = __builtin_amdgcn_exp2f(fmaf(s[i + 8], scale_log2, -mn));
-                l += p0[i] + p1[i];
-            }
-            const bf16x8_t pb[2] = {__builtin_convertvector(p0, bf16x8_t), __builtin_convertvector(p1, bf16x8_t)};
-#pragma unroll
-            for (int t = 0; t < DT; ++t) {
-                const uint16_t* vl = sV + (32 * t + r) * VST + kt * 32 + 8 * h;
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2)
-                    o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                        as_bf16x8(*reinterpret_cast<const uint4*>(vl + 16 * s2)), pb[s2], o[t], 0, 0, 0);
-            }
-        }
-        const float lt = half_swap_sum(l);
-        if (!qok) continue;
-        const size_t pi = ((size_t)b * Hq + (size_t)kh * G + g) * splits_total + sp;
-        // O^T register i of d tile t: d = 32t + (i&3) + 8*(i>>2) + 4*h
-#pragma unroll
-        for (int t = 0; t < DT; ++t)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) part_o[pi * D + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h] = o[t][i];
-        if (h == 0) {
-            part_ml[pi * 2] = m;
-            part_ml[pi * 2 + 1] = lt;
         }
     }
 }
@@ -901,9 +520,9 @@ __device__ __forceinline__ void attn_tile_mfma(KVTile<D, KV8>& cur, bool prefetc
 }
 
 // --------------------------------------------------------------------------
-// 3c. per-row decode attention on the matrix cores (the default).
-//    Same outputs and partial layout as decode_attn_kernel (so the prefix
-//    kernel and the combine are shared), but ONE WAVE per work item
+// 3c. per-row decode attention on the matrix cores.
+//    Writes split partials at index ps_max + split (the shared prefix's
+//    partials take [0, ps_max)) for the combine kernel, ONE WAVE per work item
 //    (row, kv head, split) and both products on MFMA 16x16x32 bf16 per
 //    32-key tile:
 //        S^T[key, q] = K[key, :] . Q^T[:, q]      A = K rows straight from HBM
@@ -920,9 +539,9 @@ __device__ __forceinline__ void attn_tile_mfma(KVTile<D, KV8>& cur, bool prefetc
 //    The kernel is bound by HBM latency x bytes in flight, not by math
 //    (profiles/decode_step_*: a 1-deep prefetch with 1024-key splits ran at
 //    42 % of the copy rate): each row's keys are cut into equal splits sized
-//    so that ~16 waves per CU are busy, and each wave keeps TWO tiles of
-//    K/V loads in flight (register double buffer, D = 64) while it computes
-//    a third.
+//    so that ~16 waves per CU are busy, and each wave keeps the next tile's
+//    K/V loads in flight while it computes the current one.  (A register
+//    double buffer of two tiles in flight measured no faster; removed.)
 //    Measured and not adopted (profiles/decode_step_r2_notes.md): merging a
 //    sequence's jump-forward rows into one work item (their keys read once)
 //    gained nothing -- those re-reads already hit L2 / MALL -- and its extra
@@ -931,7 +550,7 @@ __device__ __forceinline__ void attn_tile_mfma(KVTile<D, KV8>& cur, bool prefetc
 //    No block-level synchronisation: each wave owns its LDS tile, so
 //    different waves of a block run different items.
 // --------------------------------------------------------------------------
-template <int D, bool kDouble, bool KV8>
+template <int D, bool KV8>
 __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
     const uint16_t* __restrict__ q, const void* __restrict__ k_cache, const void* __restrict__ v_cache,
     const int32_t* __restrict__ slot, const int32_t* __restrict__ seq_len, uint16_t* __restrict__ out,
@@ -992,26 +611,12 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
         f32x4_t acc[DB];
 #pragma unroll
         for (int db = 0; db < DB; ++db) acc[db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        if (kDouble) {
-            KVTile<D, KV8> ta, tb;
-            load_kv_tile<D, KV8>(kb, vb, start, end, lane, ta);
-            if (ntiles > 1) load_kv_tile<D, KV8>(kb, vb, start + 32, end, lane, tb);
-            for (int t = 0; t < ntiles; t += 2) {
-                const int kt = start + 32 * t;
-                attn_tile_mfma<D, KV8>(ta, t + 2 < ntiles, kt + 64, kb, vb, kt, end, lane, g16, vw, tr0, tr1, qf, m,
-                                       l, acc, scale_log2);
-                if (t + 1 < ntiles)
-                    attn_tile_mfma<D, KV8>(tb, t + 3 < ntiles, kt + 96, kb, vb, kt + 32, end, lane, g16, vw, tr0, tr1,
-                                           qf, m, l, acc, scale_log2);
-            }
-        } else {
-            KVTile<D, KV8> ta;
-            load_kv_tile<D, KV8>(kb, vb, start, end, lane, ta);
-            for (int t = 0; t < ntiles; ++t) {
-                const int kt = start + 32 * t;
-                attn_tile_mfma<D, KV8>(ta, t + 1 < ntiles, kt + 32, kb, vb, kt, end, lane, g16, vw, tr0, tr1, qf, m,
-                                       l, acc, scale_log2);
-            }
+        KVTile<D, KV8> ta;
+        load_kv_tile<D, KV8>(kb, vb, start, end, lane, ta);
+        for (int t = 0; t < ntiles; ++t) {
+            const int kt = start + 32 * t;
+            attn_tile_mfma<D, KV8>(ta, t + 1 < ntiles, kt + 32, kb, vb, kt, end, lane, g16, vw, tr0, tr1, qf, m, l,
+                                   acc, scale_log2);
         }
         l += __shfl_xor(l, 16, kWave);
         l += __shfl_xor(l, 32, kWave);
@@ -1038,41 +643,6 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
     }
 }
 
-// 0 = MFMA per-row kernel (default), 1 = VALU kernel (A/B and fallback),
-// 2 = MFMA kernel with a register double buffer (D = 64; A/B)
-int g_decode_impl = 0;
-
-// Shared-prefix kernel on a second stream, concurrent with the per-row
-// kernel (both only write their own partial slots; the combine waits for
-// both); inside a hipGraph capture the fork/join events make the side stream
-// a parallel branch.  Off by default: measured 2.38 -> 2.58 ms per decode
-// step with it on (the latency-bound prefix blocks slow the HBM-bound per-row
-// kernel more than they gain) -- profiles/decode_step_r2_notes.md.
-int g_prefix_overlap = 0;
-
-struct SideStream {
-    hipStream_t s = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-};
-
-hipError_t side_stream(SideStream*& out) {
-    static SideStream ss[64];
-    static std::mutex mu;
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-    std::lock_guard<std::mutex> g(mu);
-    SideStream& x = ss[dev];
-    if (!x.s) {
-        if ((e = hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking)) != hipSuccess) return e;
-        if ((e = hipEventCreateWithFlags(&x.fork, hipEventDisableTiming)) != hipSuccess) return e;
-        if ((e = hipEventCreateWithFlags(&x.join, hipEventDisableTiming)) != hipSuccess) return e;
-    }
-    out = &x;
-    return hipSuccess;
-}
-
 // CUs of the current device (cached per device; 256 on MI355X)
 inline int device_cu_count() {
     static int cached[64] = {0};
@@ -1094,41 +664,20 @@ inline int grid_for(size_t work) {
 
 hipError_t launch_combine(void* part_o, void* part_ml, const int32_t* sl, const int32_t* ln, void* out, int B, int Hq,
                           int D, int max_seq, int chunk, int splits, int num_slots, const int32_t* pl, int ps_max,
-                          int pchunk, hipStream_t st) {
+                          hipStream_t st) {
     const int waves = B * Hq;
     const int blocks = (waves + 3) / 4;
     const dim3 grid((unsigned)(blocks < 2048 ? blocks : 2048));
     if (D == 64)
         decode_attn_combine_kernel<64><<<grid, kBlock, 0, st>>>((const float*)part_o, (const float*)part_ml, sl, ln,
                                                                (uint16_t*)out, B, Hq, max_seq, chunk, splits,
-                                                               num_slots, pl, ps_max, pchunk);
+                                                               num_slots, pl, ps_max);
     else if (D == 128)
         decode_attn_combine_kernel<128><<<grid, kBlock, 0, st>>>((const float*)part_o, (const float*)part_ml, sl, ln,
                                                                 (uint16_t*)out, B, Hq, max_seq, chunk, splits,
-                                                                num_slots, pl, ps_max, pchunk);
+                                                                num_slots, pl, ps_max);
     else
         return hipErrorInvalidValue;
-    return hipGetLastError();
-}
-
-template <int D>
-hipError_t launch_decode_d(int G, dim3 grid, const uint16_t* q, const uint16_t* k, const uint16_t* v,
-                           const int32_t* slot, const int32_t* len, uint16_t* out, float* po, float* pml,
-                           int B, int Hkv, int max_seq, int chunk, int splits, float sl2, int ns,
-                           const int32_t* plen, int ps_max, hipStream_t st) {
-#define DMCP_DECODE(GG)                                                                                     \
-    decode_attn_kernel<D, GG><<<grid, kBlock, 0, st>>>(q, k, v, slot, len, out, po, pml, B, Hkv, max_seq, \
-                                                       chunk, splits, sl2, ns, plen, ps_max)
-    switch (G) {
-        case 1: DMCP_DECODE(1); break;
-        case 2: DMCP_DECODE(2); break;
-        case 4: DMCP_DECODE(4); break;
-        case 3: DMCP_DECODE(3); break;
-        case 6: DMCP_DECODE(6); break;
-        case 8: DMCP_DECODE(8); break;
-        default: return hipErrorInvalidValue;
-    }
-#undef DMCP_DECODE
     return hipGetLastError();
 }
 
@@ -1136,23 +685,7 @@ hipError_t launch_decode_d(int G, dim3 grid, const uint16_t* q, const uint16_t* 
 
 extern "C" {
 
-int dmcp_abi_version() { return 9; }
-
-// Selects the per-row decode attention kernel (0 = MFMA, 1 = VALU, 2 = MFMA double-buffered);
-// returns the previous choice.
-// Shared-prefix kernel on a side stream beside the per-row kernel (1) or in
-// line (0, default); returns the previous setting.
-int dmcp_set_prefix_overlap(int on) {
-    const int prev = g_prefix_overlap;
-    g_prefix_overlap = on ? 1 : 0;
-    return prev;
-}
-
-int dmcp_set_decode_impl(int impl) {
-    const int prev = g_decode_impl;
-    if (impl >= 0 && impl <= 2) g_decode_impl = impl;
-    return prev;
-}
+int dmcp_abi_version() { return 10; }
 
 int dmcp_add_rmsnorm(const void* x, void* residual, const void* w, void* out, int rows, int H, float eps,
                      void* stream) {
@@ -1186,20 +719,21 @@ int dmcp_rope_kv(const void* qkv, const void* pos, const void* slot, const void*
     return hipGetLastError();
 }
 
+// q [B, Hq, D]; caches [S, Hkv, max_seq, D] (bf16, or fp8 e4m3 with kv8);
+// slot / seq_len [B].  With plen: every row's first *plen keys are the shared
+// prefix in prefix_k / prefix_v ([Hkv, max_seq, D], the prefix slot), read by
+// the MFMA prefill kernel in prefix mode into ps_max partials per row; the
+// per-row kernel covers keys [*plen, L).  Partials of both are merged by the
+// combine kernel; a row that fits one split with no prefix is written directly.
 int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cache, const void* slot,
                           const void* seq_len, void* out, void* part_o, void* part_ml, int B, int Hq, int Hkv, int D,
                           int max_seq, int num_slots, int chunk, int splits, float scale, const void* prefix_k,
-                          const void* prefix_vt, const void* plen, int ldv, int pchunk, int ps_max, int kv8,
-                          void* stream) {
+                          const void* prefix_v, const void* plen, int ps_max, int kv8, void* stream) {
     if (B <= 0) return 0;
-    if (Hkv <= 0 || Hq % Hkv != 0 || splits <= 0 || chunk <= 0) return hipErrorInvalidValue;
-    const bool prefix = plen != nullptr;
-    // pchunk == kPrefixChunk: the 256-key prefix kernel over (prefix_k,
-    // prefix_vt = V^T); pchunk == 0: the MFMA prefill kernel over (prefix_k,
-    // prefix_vt = V rows), ps_max key splits
-    if (prefix && (!prefix_k || !prefix_vt || ps_max <= 0 ||
-                   (pchunk != 0 && (pchunk != kPrefixChunk || ldv % kPrefixChunk || ldv > max_seq))))
+    if (Hkv <= 0 || Hq % Hkv != 0 || splits <= 0 || chunk <= 0 || !(D == 64 || D == 128) || Hq / Hkv > 16)
         return hipErrorInvalidValue;
+    const bool prefix = plen != nullptr;
+    if (prefix && (!prefix_k || !prefix_v || ps_max <= 0)) return hipErrorInvalidValue;
     if (!prefix) ps_max = 0;
     if ((splits > 1 || prefix) && (!part_o || !part_ml)) return hipErrorInvalidValue;
     const int G = Hq / Hkv;
@@ -1209,93 +743,34 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
     auto sl = (const int32_t*)slot;
     auto ln = (const int32_t*)seq_len;
     auto pl = (const int32_t*)plen;
-    const long cap = 4L * device_cu_count();
-    SideStream* side = nullptr;
-    const hipStream_t main_st = st;
-    if (prefix && g_prefix_overlap) {  // fork: the prefix kernel runs beside the per-row kernel
-        hipError_t fe = side_stream(side);
-        if (fe == hipSuccess) fe = hipEventRecord(side->fork, main_st);
-        if (fe == hipSuccess) fe = hipStreamWaitEvent(side->s, side->fork, 0);
-        if (fe != hipSuccess) return fe;
-        st = side->s;
-    }
-    if (prefix && pchunk == 0) {
-        hipError_t pe = dmcp_launch_prefix_partials(qq, prefix_k, prefix_vt, pl, (float*)part_o, (float*)part_ml, B,
+    if (prefix) {
+        hipError_t pe = dmcp_launch_prefix_partials(qq, prefix_k, prefix_v, pl, (float*)part_o, (float*)part_ml, B,
                                                     Hkv, G, D, max_seq, ps_max, ps_max + splits, sl2, kv8, st);
         if (pe != hipSuccess) return pe;
-    } else if (prefix) {
-        // one block per (kv head, prefix split, 4 query tiles); exits at once when *plen == 0
-        const long items = (long)Hkv * ps_max * ((((B * G + 31) / 32) + 3) / 4);
-        dim3 pgrid((unsigned)(items < cap ? items : cap));
-#define DMCP_PREFIX(DD, K8)                                                                                   \
-    prefix_attn_kernel<DD, K8><<<pgrid, kBlock, 0, st>>>(qq, prefix_k, prefix_vt, pl, (float*)part_o,             \
-                                                         (float*)part_ml, B, Hkv, G, max_seq, ldv, ps_max,       \
-                                                         ps_max + splits, sl2)
-        if (D == 64 && kv8) DMCP_PREFIX(64, true);
-        else if (D == 64) DMCP_PREFIX(64, false);
-        else if (D == 128 && kv8) DMCP_PREFIX(128, true);
-        else if (D == 128) DMCP_PREFIX(128, false);
-        else return hipErrorInvalidValue;
-#undef DMCP_PREFIX
-        hipError_t pe = hipGetLastError();
-        if (pe != hipSuccess) return pe;
     }
-    if (side) {
-        hipError_t je = hipEventRecord(side->join, side->s);
-        if (je != hipSuccess) return je;
-        st = main_st;
-    }
-    // the combine (main stream) waits for the side stream's prefix partials
-    auto join = [&]() -> hipError_t { return side ? hipStreamWaitEvent(main_st, side->join, 0) : hipSuccess; };
-    // persistent grid: enough blocks to fill every CU a few times over, never
-    // more than there are work items
+    // persistent grid: one wave per (split, row, kv head) item, a block runs
+    // 4; enough blocks to fill every CU a few times over, never more than items
+    const long cap = 4L * device_cu_count();
     const long items = (long)splits * Hkv * B;
-    auto kk = (const uint16_t*)k_cache;
-    auto vv = (const uint16_t*)v_cache;
-    hipError_t e;
-    if (kv8 && !((D == 64 || D == 128) && G <= 16)) return hipErrorInvalidValue;  // fp8 KV: MFMA kernel only
-    if ((g_decode_impl == 0 || g_decode_impl == 2 || kv8) && (D == 64 || D == 128) && G <= 16) {
-        // one wave per item: a block runs 4 items
-        const long wblocks = (items + 3) / 4;
-        dim3 wgrid((unsigned)(wblocks < cap ? wblocks : cap));
-        float* po = (float*)part_o;
-        float* pml = (float*)part_ml;
-        uint16_t* oo = (uint16_t*)out;
-#define DMCP_MFMA_DECODE(DD, DBL, K8)                                                                       \
-    decode_attn_mfma_kernel<DD, DBL, K8><<<wgrid, kBlock, 0, st>>>(qq, k_cache,                                \
-                                                                   v_cache, sl, ln, oo, po, pml, B, Hkv, G,     \
-                                                                   max_seq, chunk, splits, sl2, num_slots, pl,  \
-                                                                   ps_max)
-        if (kv8) {
-            if (D == 64) DMCP_MFMA_DECODE(64, false, true);
-            else DMCP_MFMA_DECODE(128, false, true);
-        } else if (D == 64 && g_decode_impl == 2) {
-            DMCP_MFMA_DECODE(64, true, false);
-        } else if (D == 64) {
-            DMCP_MFMA_DECODE(64, false, false);
-        } else {
-            DMCP_MFMA_DECODE(128, false, false);
-        }
-#undef DMCP_MFMA_DECODE
-        e = hipGetLastError();
-        if (e == hipSuccess) e = join();
-        if (e != hipSuccess || (splits == 1 && !prefix)) return e;
-        return launch_combine(part_o, part_ml, sl, ln, out, B, Hkv * G, D, max_seq, chunk, splits, num_slots, pl,
-                              ps_max, prefix ? pchunk : 1, st);
+    const long wblocks = (items + 3) / 4;
+    const dim3 wgrid((unsigned)(wblocks < cap ? wblocks : cap));
+    float* po = (float*)part_o;
+    float* pml = (float*)part_ml;
+    uint16_t* oo = (uint16_t*)out;
+#define DMCP_MFMA_DECODE(DD, K8)                                                                                   \
+    decode_attn_mfma_kernel<DD, K8><<<wgrid, kBlock, 0, st>>>(qq, k_cache, v_cache, sl, ln, oo, po, pml, B, Hkv, G, \
+                                                              max_seq, chunk, splits, sl2, num_slots, pl, ps_max)
+    if (kv8) {
+        if (D == 64) DMCP_MFMA_DECODE(64, true);
+        else DMCP_MFMA_DECODE(128, true);
+    } else {
+        if (D == 64) DMCP_MFMA_DECODE(64, false);
+        else DMCP_MFMA_DECODE(128, false);
     }
-    dim3 grid((unsigned)(items < cap ? items : cap));
-    if (D == 64)
-        e = launch_decode_d<64>(G, grid, qq, kk, vv, sl, ln, (uint16_t*)out, (float*)part_o, (float*)part_ml, B,
-                                Hkv, max_seq, chunk, splits, sl2, num_slots, pl, ps_max, st);
-    else if (D == 128)
-        e = launch_decode_d<128>(G, grid, qq, kk, vv, sl, ln, (uint16_t*)out, (float*)part_o, (float*)part_ml, B,
-                                 Hkv, max_seq, chunk, splits, sl2, num_slots, pl, ps_max, st);
-    else
-        e = hipErrorInvalidValue;
-    if (e == hipSuccess) e = join();
+#undef DMCP_MFMA_DECODE
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess || (splits == 1 && !prefix)) return e;
-    return launch_combine(part_o, part_ml, sl, ln, out, B, Hkv * G, D, max_seq, chunk, splits, num_slots, pl, ps_max,
-                          prefix ? pchunk : 1, st);
+    return launch_combine(part_o, part_ml, sl, ln, out, B, Hq, D, max_seq, chunk, splits, num_slots, pl, ps_max, st);
 }
 
 int dmcp_silu_mul(const void* gu, void* out, int T, int I, void* stream) {

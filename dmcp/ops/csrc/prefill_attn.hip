@@ -70,12 +70,15 @@ __device__ __forceinline__ v4i16_t lds_tr16(const uint16_t* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16_t*)(p));
 }
 
+// The work of one block: kv head kh, column tile ct (32 * NSUB * NWAVE query
+// columns), key split sp of nsplit.  Shared by the single-sequence kernel,
+// the varlen (packed multi-sequence) kernel and the decode step's prefix mode.
 template <int D, int NSUB, int NWAVE, bool KV8>
-__global__ __launch_bounds__(NWAVE * 64) void prefill_attn_kernel(
+__device__ __forceinline__ void prefill_attn_block(
     const uint16_t* __restrict__ q, const void* __restrict__ kc, const void* __restrict__ vc,
     const void* __restrict__ pk, const void* __restrict__ pv, uint16_t* __restrict__ out,
     float* __restrict__ part_o, float* __restrict__ part_ml, int T, int start, int P, int Hkv, int G, int ldk,
-    int ctiles, int nsplit, float sl2, const int32_t* __restrict__ plen, long prs, long pss) {
+    int kh, int sp, int ct, int nsplit, float sl2, const int32_t* __restrict__ plen, long prs, long pss) {
     constexpr int KS = D / 16;  // k-steps of the QK product
     constexpr int DT = D / 32;  // 32-row d tiles of the PV product
     constexpr int CH = D / 8;   // 16-byte chunks per row
@@ -86,10 +89,6 @@ __global__ __launch_bounds__(NWAVE * 64) void prefill_attn_kernel(
     __shared__ __attribute__((aligned(16))) uint16_t sK[2][kPfKeys * D];
     __shared__ __attribute__((aligned(16))) uint16_t sV[2][kPfKeys * D];
 
-    const int kh = blockIdx.x % Hkv;
-    const int rest = (int)(blockIdx.x / Hkv);
-    const int sp = rest % nsplit;
-    const int ct = ctiles - 1 - rest / nsplit;
     const int Hq = Hkv * G;
     const int NC = T * G;
     const int c0 = ct * COLS;
@@ -309,6 +308,45 @@ __global__ __launch_bounds__(NWAVE * 64) void prefill_attn_kernel(
     }
 }
 
+template <int D, int NSUB, int NWAVE, bool KV8>
+__global__ __launch_bounds__(NWAVE * 64) void prefill_attn_kernel(
+    const uint16_t* __restrict__ q, const void* __restrict__ kc, const void* __restrict__ vc,
+    const void* __restrict__ pk, const void* __restrict__ pv, uint16_t* __restrict__ out,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int T, int start, int P, int Hkv, int G, int ldk,
+    int ctiles, int nsplit, float sl2, const int32_t* __restrict__ plen, long prs, long pss) {
+    const int kh = blockIdx.x % Hkv;
+    const int rest = (int)(blockIdx.x / Hkv);
+    const int sp = rest % nsplit;
+    const int ct = ctiles - 1 - rest / nsplit;  // heavy (late) column tiles first
+    prefill_attn_block<D, NSUB, NWAVE, KV8>(q, kc, vc, pk, pv, out, part_o, part_ml, T, start, P, Hkv, G, ldk, kh, sp,
+                                            ct, nsplit, sl2, plen, prs, pss);
+}
+
+// Packed multi-sequence prefill (the engine's batched admission): q / out
+// [Ttot, Hq, D] hold every sequence's tokens back to back; block b runs work
+// item b / Hkv of the host-built table (sequence, column tile), sorted by
+// descending key count so the long tiles start first, for kv head b % Hkv.
+// seq[i] = (token offset, T, start, slot, shared-prefix length).  No split-K:
+// a batch of 2,000-token prompts is thousands of blocks already.
+template <int D, int NSUB, int NWAVE, bool KV8>
+__global__ __launch_bounds__(NWAVE * 64) void prefill_varlen_kernel(
+    const uint16_t* __restrict__ q, const void* __restrict__ kcache, const void* __restrict__ vcache,
+    const void* __restrict__ pk, const void* __restrict__ pv, uint16_t* __restrict__ out,
+    const int32_t* __restrict__ items, const int32_t* __restrict__ seq, int Hkv, int G, int ldk, size_t slot_elems,
+    float sl2) {
+    const int kh = blockIdx.x % Hkv;
+    const int it = blockIdx.x / Hkv;
+    const int si = items[2 * it], ct = items[2 * it + 1];
+    const int off = seq[5 * si], T = seq[5 * si + 1], start = seq[5 * si + 2], slot = seq[5 * si + 3];
+    const int P = seq[5 * si + 4];
+    const size_t row0 = (size_t)off * Hkv * G * D;
+    const size_t kvoff = (size_t)slot * slot_elems * (KV8 ? 1 : 2);
+    const void* kc = static_cast<const char*>(kcache) + kvoff;
+    const void* vc = static_cast<const char*>(vcache) + kvoff;
+    prefill_attn_block<D, NSUB, NWAVE, KV8>(q + row0, kc, vc, P > 0 ? pk : kc, P > 0 ? pv : vc, out + row0, nullptr,
+                                            nullptr, T, start, P, Hkv, G, ldk, kh, 0, ct, 1, sl2, nullptr, 1L, 1L);
+}
+
 // split-K merge: out[row, :] = sum_s O_s exp2(m_s - M) / sum_s l_s exp2(m_s - M),
 // M = max_s m_s (log2 domain).  One thread per 4 outputs.
 template <int D>
@@ -434,6 +472,36 @@ int dmcp_prefill_attention(const void* q, const void* k, const void* v, const vo
     }
 #undef DMCP_PF
     return hipErrorInvalidValue;
+}
+
+// Packed multi-sequence prefill attention.  q / out [Ttot, Hq, D]; caches
+// [S, Hkv, ldk, D]; pk / pv: the shared-prefix slot ([Hkv, ldk, D]) for
+// sequences whose prefix length is > 0.  items [nitems, 2] = (sequence, column
+// tile) and seq [nseq, 5] = (token offset, T, start, slot, prefix length),
+// int32 on the device; 4 waves x 32 columns per tile.
+int dmcp_prefill_varlen(const void* q, const void* kc, const void* vc, const void* pk, const void* pv, void* out,
+                        const void* items, const void* seq, int nitems, int Hq, int Hkv, int D, int ldk,
+                        long slot_elems, float scale, int kv8, void* stream) {
+    if (nitems <= 0) return 0;
+    if (!q || !kc || !vc || !out || !items || !seq || Hkv <= 0 || Hq % Hkv != 0 || (long)nitems * Hkv > (1L << 31))
+        return hipErrorInvalidValue;
+    const int G = Hq / Hkv;
+    const float sl2 = scale * 1.4426950408889634f;
+    const dim3 grid((unsigned)(nitems * Hkv));
+    auto st = (hipStream_t)stream;
+    auto it = (const int32_t*)items;
+    auto sq = (const int32_t*)seq;
+#define DMCP_PV(DD, K8)                                                                                         \
+    prefill_varlen_kernel<DD, 1, 4, K8><<<grid, 4 * kWave, 0, st>>>((const uint16_t*)q, kc, vc, pk, pv,           \
+                                                                    (uint16_t*)out, it, sq, Hkv, G, ldk,          \
+                                                                    (size_t)slot_elems, sl2)
+    if (D == 64 && kv8) DMCP_PV(64, true);
+    else if (D == 64) DMCP_PV(64, false);
+    else if (D == 128 && kv8) DMCP_PV(128, true);
+    else if (D == 128) DMCP_PV(128, false);
+    else return hipErrorInvalidValue;
+#undef DMCP_PV
+    return hipGetLastError();
 }
 
 }  // extern "C"

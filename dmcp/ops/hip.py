@@ -26,7 +26,7 @@ _lock = threading.Lock()
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _f = ctypes.c_float
-ABI_VERSION = 9  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
+ABI_VERSION = 10  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
 
 
 class HipOpsError(RuntimeError):
@@ -51,15 +51,14 @@ def lib() -> ctypes.CDLL:
             "dmcp_add_rmsnorm": ([_vp, _vp, _vp, _vp, _i, _i, _f, _vp], _i),
             "dmcp_rope_kv": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp], _i),
             "dmcp_decode_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _f,
-                                       _vp, _vp, _vp, _i, _i, _i, _i, _vp],
-                                      _i),
+                                       _vp, _vp, _vp, _i, _i, _vp], _i),
             "dmcp_prefill_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _i, _i,
                                         _i, _vp], _i),
+            "dmcp_prefill_varlen": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, ctypes.c_long, _f,
+                                     _i, _vp], _i),
             "dmcp_silu_mul": ([_vp, _vp, _i, _i, _vp], _i),
             "dmcp_masked_argmax": ([_vp, _vp, _vp, _i, _vp, _i, _i, _i, _vp], _i),
             "dmcp_embedding": ([_vp, _vp, _vp, _i, _i, _i, _vp], _i),
-            "dmcp_set_decode_impl": ([_i], _i),
-            "dmcp_set_prefix_overlap": ([_i], _i),
             "dmcp_fused_gemm_max_rows": ([], _i),
             "dmcp_splitk_resid_norm": ([_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _i, _vp], _i),
             "dmcp_splitk_rope_kv": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i,
@@ -73,34 +72,8 @@ def lib() -> ctypes.CDLL:
             fn.restype = res
         if L.dmcp_abi_version() != ABI_VERSION:
             raise HipOpsError("HIP kernel library ABI mismatch; rebuild with python -m dmcp.ops.build")
-        impl = os.environ.get("DMCP_DECODE_IMPL", "mfma").lower()
-        L.dmcp_set_decode_impl(DECODE_IMPLS.get(impl, 0))
-        L.dmcp_set_prefix_overlap(int(os.environ.get("DMCP_PREFIX_OVERLAP", "0") == "1"))
         _lib = L
         return _lib
-
-
-DECODE_IMPLS = {"mfma": 0, "valu": 1, "mfma2": 2}
-
-
-def set_decode_impl(name: str) -> str:
-    """Per-row decode attention kernel: ``mfma`` (default; matrix cores, one
-    wave per work item), ``mfma2`` (same with a register double buffer: two
-    tiles of loads in flight per wave at half the occupancy; D = 64) or
-    ``valu`` (the previous VALU kernel, kept for A/B runs and as a reference).  Returns the previous choice.  Takes effect at
-    the next launch (re-capture hipGraphs after switching)."""
-    if name not in DECODE_IMPLS:
-        raise ValueError(f"decode impl must be one of {sorted(DECODE_IMPLS)}")
-    prev = lib().dmcp_set_decode_impl(DECODE_IMPLS[name])
-    return {v: k for k, v in DECODE_IMPLS.items()}[prev]
-
-
-def set_prefix_overlap(on: bool) -> bool:
-    """Run the decode step's shared-prefix kernel on a side stream, concurrent
-    with the per-row kernel (``DMCP_PREFIX_OVERLAP=1``; off by default: the
-    two kernels slowed each other down, 2.38 -> 2.58 ms per step).  Returns
-    the previous setting; re-capture hipGraphs after switching."""
-    return bool(lib().dmcp_set_prefix_overlap(int(bool(on))))
 
 
 def loaded_path() -> Optional[str]:
@@ -244,10 +217,11 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     ``MAXS / chunk``, i.e. parts of <= ``chunk`` keys); see :func:`decode_plan`.
 
     ``prefix``: the first ``*prefix.length`` keys of every row are the shared
-    prefix (``prefix.k`` [Hkv, MAXS, D], ``prefix.vt`` [Hkv, D, ldv]), read
-    once per 32 queries by the MFMA prefix kernel; the per-row kernel covers
-    the keys after it.  The length lives in device memory, so a captured
-    graph follows prefix changes (0 = no prefix)."""
+    prefix (``prefix.k`` / ``prefix.v`` [Hkv, MAXS, D], the prefix slot),
+    attended by the MFMA prefill kernel in prefix mode (every prefix key read
+    once per 32 queries, :func:`prefix_mfma_splits` key splits); the per-row
+    kernel covers the keys after it.  The length lives in device memory, so
+    a captured graph follows prefix changes (0 = no prefix)."""
     B, Hq, D = q.shape
     S, Hkv, MAXS, Dk = k_cache.shape
     _req(q, torch.bfloat16, "decode_attention.q")
@@ -265,31 +239,20 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     if not 1 <= splits <= max_splits:
         raise HipOpsError(f"decode_attention: splits {splits} outside [1, {max_splits}]")
     ps_max = 0
-    pk = pvt = plen = None
-    ldv = pchunk = 0
-    if prefix is not None and prefix.v is not None and prefix_impl() == "prefill":
-        # the prefix on the MFMA prefill kernel: V rows, ps_max key splits
-        pk, pvt, plen = prefix.k, prefix.v, prefix.length
+    pk = pv = plen = None
+    if prefix is not None:
+        # the shared prefix on the MFMA prefill kernel in prefix mode: K / V
+        # rows of the prefix slot, ps_max key splits per query tile
+        pk, pv, plen = prefix.k, prefix.v, prefix.length
         _req(pk, k_cache.dtype, "decode_attention.prefix.k")
-        _req(pvt, k_cache.dtype, "decode_attention.prefix.v")
+        _req(pv, k_cache.dtype, "decode_attention.prefix.v")
         _req(plen, torch.int32, "decode_attention.prefix.length")
-        if tuple(pk.shape) != (Hkv, MAXS, D) or tuple(pvt.shape) != (Hkv, MAXS, D) or plen.numel() != 1:
-            raise HipOpsError(f"decode_attention: prefix k {tuple(pk.shape)} / v {tuple(pvt.shape)} do not match "
+        if tuple(pk.shape) != (Hkv, MAXS, D) or tuple(pv.shape) != (Hkv, MAXS, D) or plen.numel() != 1:
+            raise HipOpsError(f"decode_attention: prefix k {tuple(pk.shape)} / v {tuple(pv.shape)} do not match "
                               f"kv {tuple(k_cache.shape)}")
         ps_max = prefix_mfma_splits(B, Hq // Hkv, Hkv)
-        if workspace is not None:  # as many prefix splits as the caller's scratch holds
-            ps_max = max(1, min(ps_max, workspace[1].numel() // (2 * B * Hq) - splits))
-    elif prefix is not None:
-        pk, pvt, plen, pchunk = prefix.k, prefix.vt, prefix.length, prefix.chunk
-        _req(pk, k_cache.dtype, "decode_attention.prefix.k")
-        _req(pvt, k_cache.dtype, "decode_attention.prefix.vt")
-        _req(plen, torch.int32, "decode_attention.prefix.length")
-        ldv = pvt.shape[-1]
-        if (tuple(pk.shape) != (Hkv, MAXS, D) or tuple(pvt.shape) != (Hkv, D, ldv) or ldv % PREFIX_CHUNK
-                or ldv > MAXS or pchunk != PREFIX_CHUNK or plen.numel() != 1):
-            raise HipOpsError(f"decode_attention: prefix k {tuple(pk.shape)} / vt {tuple(pvt.shape)} / chunk "
-                              f"{pchunk} do not match kv {tuple(k_cache.shape)}")
-        ps_max = prefix_splits(ldv, pchunk)
+        if workspace is not None and workspace[1].numel() < 2 * B * Hq * (splits + ps_max):
+            raise HipOpsError(f"decode_attention: workspace holds fewer than {splits} + {ps_max} partials per row")
     out = torch.empty_like(q) if out is None else out
     _req_out(out, torch.bfloat16, B * Hq * D, "decode_attention.out")
     if splits > 1 or ps_max:
@@ -303,7 +266,7 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
         part_o = part_ml = None
     _check(lib().dmcp_decode_attention(_ptr(q), _ptr(k_cache), _ptr(v_cache), _ptr(slot), _ptr(seq_len), _ptr(out),
                                        _ptr(part_o), _ptr(part_ml), B, Hq, Hkv, D, MAXS, S, chunk, splits,
-                                       float(scale), _ptr(pk), _ptr(pvt), _ptr(plen), ldv, pchunk, ps_max, kv8,
+                                       float(scale), _ptr(pk), _ptr(pv), _ptr(plen), ps_max, kv8,
                                        _stream()), "dmcp_decode_attention")
     return out
 
@@ -368,53 +331,75 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
     return out
 
 
+VARLEN_COLS = 128  # query columns (token x q head of a kv group) per varlen work item: 4 waves x 32
+
+
 def prefill_attention_varlen(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, offsets, slots, starts,
                              prefix_slot: Optional[int] = None, prefix_lens=None, scale: float = 1.0,
                              out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Packed multi-sequence prefill attention (see
-    :func:`dmcp.ops.reference.prefill_attention_varlen`)."""
+    """Packed multi-sequence prefill attention in ONE launch
+    (csrc/prefill_attn.hip::prefill_varlen_kernel): q [Ttot, Hq, D], sequence
+    i = rows [offsets[i], offsets[i+1]) at positions [starts[i], ...) of
+    ``slots[i]``, its first ``prefix_lens[i]`` keys read in place from
+    ``prefix_slot``.  Work items (sequence, 128-column tile) are ordered by
+    descending key count on the host.  Returns [Ttot, Hq, D] bf16."""
+    Ttot, Hq, D = q.shape
+    S, Hkv, MAXS, Dk = k_cache.shape
+    _req(q, torch.bfloat16, "prefill_attention_varlen.q")
+    kv8 = _req_kv(k_cache, v_cache, "prefill_attention_varlen")
+    if Dk != D or v_cache.shape != k_cache.shape or not prefill_supported(Hq, Hkv, D):
+        raise HipOpsError(f"prefill_attention_varlen: unsupported shape q={tuple(q.shape)} kv={tuple(k_cache.shape)}")
+    n = len(slots)
+    if len(offsets) != n + 1 or len(starts) != n or int(offsets[0]) != 0 or int(offsets[-1]) != Ttot:
+        raise HipOpsError("prefill_attention_varlen: offsets must run from 0 to Ttot with one entry per sequence + 1")
+    G = Hq // Hkv
+    plens = [int(x) for x in prefix_lens] if prefix_lens is not None else [0] * n
+    seq = []
+    items = []
+    for i in range(n):
+        a, b, st, sl, P = int(offsets[i]), int(offsets[i + 1]), int(starts[i]), int(slots[i]), plens[i]
+        T = b - a
+        if T < 1 or not 0 <= sl < S or st < 0 or st + T > MAXS:
+            raise HipOpsError(f"prefill_attention_varlen: sequence {i} (slot {sl}, [{st}, {st + T})) does not fit "
+                              f"{S} slots x {MAXS} positions")
+        if P and (prefix_slot is None or not 0 <= int(prefix_slot) < S or not 0 < P <= st):
+            raise HipOpsError(f"prefill_attention_varlen: prefix of {P} keys in slot {prefix_slot} must precede "
+                              f"start {st}")
+        seq.append((a, T, st, sl, P))
+        for ct in range(-(-T * G // VARLEN_COLS)):
+            last_tok = min(T, ((ct + 1) * VARLEN_COLS + G - 1) // G)
+            items.append((st + last_tok, i, ct))
+    items.sort(key=lambda x: -x[0])
     out = torch.empty_like(q) if out is None else out
-    for i in range(len(slots)):
-        a, b = int(offsets[i]), int(offsets[i + 1])
-        P = int(prefix_lens[i]) if prefix_lens is not None else 0
-        prefill_attention(q[a:b], k_cache, v_cache, int(slots[i]), int(starts[i]), prefix_slot if P else None, P,
-                          scale, out=out[a:b])
+    _req_out(out, torch.bfloat16, Ttot * Hq * D, "prefill_attention_varlen.out")
+    meta = torch.tensor([v for _, i, ct in items for v in (i, ct)] + [v for r in seq for v in r], dtype=torch.int32)
+    meta = meta.pin_memory().to(q.device, non_blocking=True)
+    it_t, seq_t = meta[:2 * len(items)], meta[2 * len(items):]
+    if any(plens):
+        pk, pv = k_cache[int(prefix_slot)], v_cache[int(prefix_slot)]
+    else:
+        pk = pv = None
+    _check(lib().dmcp_prefill_varlen(_ptr(q), _ptr(k_cache), _ptr(v_cache), _ptr(pk), _ptr(pv), _ptr(out),
+                                     _ptr(it_t), _ptr(seq_t), len(items), Hq, Hkv, D, MAXS, Hkv * MAXS * D,
+                                     float(scale), kv8, _stream()), "dmcp_prefill_varlen")
     return out
-
-
-PREFIX_CHUNK = 256  # keys per prefix split: kPrefixChunk in csrc/dmcp_kernels.hip
-PREFIX_IMPLS = ("chunk", "prefill")
-
-
-def prefix_impl() -> str:
-    """Shared-prefix attention of the decode step (``DMCP_PREFIX_IMPL``):
-    ``chunk`` (default) = the 256-key MFMA prefix kernel over the V^T copy;
-    ``prefill`` = the MFMA prefill kernel in prefix mode over the prefix
-    slot's V rows.  Measured at parity or slower on the enrichment step
-    (profiles/decode_step_r2_notes.md), kept for A/B."""
-    impl = os.environ.get("DMCP_PREFIX_IMPL", "chunk").lower()
-    if impl not in PREFIX_IMPLS:
-        raise HipOpsError(f"DMCP_PREFIX_IMPL must be one of {PREFIX_IMPLS}, got {impl!r}")
-    return impl
 
 
 PREFIX_MFMA_MAX_SPLITS = 16
 
 
-def prefix_mfma_splits(rows: int, G: int, Hkv: int, target_blocks: int = 256) -> int:
-    """Key splits of the decode step's shared prefix on the prefill kernel:
-    ~one block per CU over (128-column query tiles x kv heads x splits), at
-    most 16 (the combine reads every split's partial; empty ones weigh 0).
-    ``DMCP_PREFIX_SPLITS`` overrides."""
+def prefix_mfma_splits(rows: int, G: int, Hkv: int, target_blocks: int = 640) -> int:
+    """Key splits of the decode step's shared prefix: ~2.5 blocks per CU over
+    (128-column query tiles x kv heads x splits), at most 16 (the combine
+    reads every split's partial; empty ones weigh 0).  Measured on the fp8
+    step with a 4,151-token prefix (profiles/prefix_splits_r3.txt): 8
+    splits at 320 rows (4.86 vs 5.35 ms for the former 256-key chunk
+    kernel), 12-16 at 78 rows (parity).  ``DMCP_PREFIX_SPLITS`` overrides."""
     env = os.environ.get("DMCP_PREFIX_SPLITS")
     if env:
         return max(1, min(PREFIX_MFMA_MAX_SPLITS, int(env)))
     tiles = -(-rows * G // 128) * Hkv
     return max(1, min(PREFIX_MFMA_MAX_SPLITS, round(target_blocks / max(1, tiles))))
-
-
-def prefix_splits(ldv: int, pchunk: int = PREFIX_CHUNK) -> int:
-    return max(1, math.ceil(ldv / pchunk))
 
 
 def decode_workspace(rows: int, Hq: int, Hkv: int, D: int, max_seq: int, device, chunk: int = 256,

@@ -85,18 +85,12 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos_sin: t
 
 
 class SharedPrefix(NamedTuple):
-    """Keys/values shared by every row of a decode step (cascade decoding).
-
-    ``k`` [Hkv, MAXS, D] (row-major, as in the cache), ``vt`` [Hkv, D, ldv]
-    (values transposed, read by the 256-key prefix kernel), ``length`` int32
-    [1] on the device (0 = no prefix), ``chunk`` keys per prefix work item of
-    that kernel; ``v`` [Hkv, MAXS, D] (values row-major, the cache slot) lets
-    the decode step run the prefix on the MFMA prefill kernel instead."""
+    """Keys/values shared by every row of a decode step (cascade decoding):
+    ``k`` / ``v`` [Hkv, MAXS, D] (the prefix slot of the caches) and
+    ``length`` int32 [1] on the device (0 = no prefix)."""
     k: torch.Tensor
-    vt: torch.Tensor
+    v: torch.Tensor
     length: torch.Tensor
-    chunk: int = 256
-    v: Optional[torch.Tensor] = None
 
 
 def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: torch.Tensor,
@@ -115,8 +109,7 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
         v = kv_float(v_cache[s, :, :L])
         if P > 0:  # the first P keys come from the shared prefix
             k = torch.cat([kv_float(prefix.k[:, :P]), k[:, P:]], dim=1)
-            pv = kv_float(prefix.v[:, :P]) if prefix.v is not None else kv_float(prefix.vt[:, :, :P]).transpose(1, 2)
-            v = torch.cat([pv, v[:, P:]], dim=1)
+            v = torch.cat([kv_float(prefix.v[:, :P]), v[:, P:]], dim=1)
         qb = q[b].float().view(Hkv, G, D)
         att = torch.einsum("hgd,hld->hgl", qb, k) * scale
         p = torch.softmax(att, dim=-1)

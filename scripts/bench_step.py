@@ -40,14 +40,12 @@ def main(argv=None) -> int:
     ap.add_argument("--max-seq", type=int, default=8192)
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--fused", type=int, default=-1, help="-1 = model default, 0 = hipBLASLt, 1 = fused kernels")
-    ap.add_argument("--decode-impl", default="mfma", help="per-row decode attention kernel (dmcp.ops.hip.DECODE_IMPLS)")
     a = ap.parse_args(argv)
 
     from dmcp.enrich.local import LocalEngine
     from dmcp.models.llm import LocalLM, preset
     from dmcp.ops import hip
 
-    hip.set_decode_impl(a.decode_impl)
 
     torch.cuda.set_device(0)
     cfg = preset(a.preset, max_batch=a.batch, max_seq=a.max_seq, kv_dtype=a.kv_dtype)
@@ -84,7 +82,8 @@ def main(argv=None) -> int:
     w_bytes = 2 * (cfg.param_count() - cfg.vocab_size * cfg.hidden)
     print(json.dumps({"bench": "decode_step", "preset": a.preset, "kv_dtype": a.kv_dtype, "rows": n, "batch": a.batch, "prefix": a.prefix,
                       "ctx": a.ctx, "fused": bool(getattr(model, "use_fused", False)),
-                      "decode_impl": a.decode_impl,
+                      "prefix_splits": hip.prefix_mfma_splits(a.batch + a.extra, cfg.n_heads // cfg.n_kv_heads,
+                                                              cfg.n_kv_heads),
                       "device_ms": round(dev_ms, 3), "loop_ms": round(loop_ms, 3),
                       "host_gap_ms": round(loop_ms - dev_ms, 3),
                       "sol_ms_at_6p3TBps": round((kv_bytes + w_bytes) / 6.3e12 * 1e3, 3),

@@ -13,11 +13,8 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
         --timeout-method thread > "$OUT/tests.log" 2>&1
     rc=$?; tail -3 "$OUT/tests.log"; [ $rc -eq 0 ] || exit $rc
 fi
-for impl in ${IMPLS:-mfma mfma2 valu}; do
-    timeout -k 10 300 python scripts/bench_step.py --decode-impl "$impl" $STEP_ARGS > "$OUT/step_$impl.log" 2>&1 \
-        || { tail -20 "$OUT/step_$impl.log"; exit 1; }
-    grep bench "$OUT/step_$impl.log"
-done
+timeout -k 10 300 python scripts/bench_step.py $STEP_ARGS > "$OUT/step.log" 2>&1 || { tail -20 "$OUT/step.log"; exit 1; }
+grep bench "$OUT/step.log"
 ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/prof" -o step \
     -- python3 "$ROOT/scripts/bench_step.py" --iters 50 $STEP_ARGS > "$ROOT/$OUT/prof.log" 2>&1 ) || exit 1
 find "$OUT/prof" -type f ! -name '*kernel_stats*' -delete

@@ -96,21 +96,14 @@ def test_decode_attention_fp8(hip, D, Hq, Hkv, P):
     pslot = S
     pre = None
     if P:
-        vt = torch.zeros((Hkv, D, MAXS), dtype=torch.uint8, device="cuda")
-        vt[:, :, :P] = vc[pslot, :, :P].transpose(-1, -2)
-        pre = SharedPrefix(kc[pslot], vt, torch.tensor([P], dtype=torch.int32, device="cuda"), 256, vc[pslot])
+        pre = SharedPrefix(kc[pslot], vc[pslot], torch.tensor([P], dtype=torch.int32, device="cuda"))
     slot = torch.tensor([(b * 5) % S for b in range(B)], dtype=torch.int32, device="cuda")
     lens = torch.tensor([min(MAXS, P + 1 + (b * 97) % 700) for b in range(B)], dtype=torch.int32, device="cuda")
     scale = 1 / math.sqrt(D)
-    for impl in hip.PREFIX_IMPLS:  # both shared-prefix kernels
-        os.environ["DMCP_PREFIX_IMPL"] = impl
-        try:
-            for splits in (1, 4):
-                got = hip.decode_attention(q, kc, vc, slot, lens, scale, prefix=pre, splits=splits)
-                exp = reference.decode_attention(q, kc, vc, slot, lens, scale, prefix=pre)
-                torch.testing.assert_close(got.float(), exp.float(), atol=2e-2, rtol=2e-2)
-        finally:
-            os.environ.pop("DMCP_PREFIX_IMPL")
+    for splits in (1, 4):
+        got = hip.decode_attention(q, kc, vc, slot, lens, scale, prefix=pre, splits=splits)
+        exp = reference.decode_attention(q, kc, vc, slot, lens, scale, prefix=pre)
+        torch.testing.assert_close(got.float(), exp.float(), atol=2e-2, rtol=2e-2)
 
 
 @pytest.mark.parametrize("D,Hq,Hkv", [(64, 32, 8), (64, 16, 2), (128, 24, 8)])

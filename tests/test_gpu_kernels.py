@@ -96,41 +96,26 @@ def test_decode_attention_shared_prefix(hip, D, Hq, Hkv, P, B):
     kc = _bf(S + 1, Hkv, MAXS, D, seed=12)
     vc = _bf(S + 1, Hkv, MAXS, D, seed=13)
     pslot = S  # the prefix lives in the last slot
-    vt = torch.zeros((Hkv, D, MAXS), dtype=torch.bfloat16, device="cuda")
-    vt[:, :, :P] = vc[pslot, :, :P].transpose(-1, -2)
     plen = torch.tensor([P], dtype=torch.int32, device="cuda")
     slot = torch.tensor([(b * 5) % S for b in range(B)], dtype=torch.int32, device="cuda")
     slot[B // 2] = -1  # a padding row
     lens = torch.tensor([min(MAXS, P + 1 + (b * 37) % 300) for b in range(B)], dtype=torch.int32, device="cuda")
     scale = 1 / math.sqrt(D)
-    # the 256-key prefix kernel over V^T, and the prefill kernel in prefix mode over the V rows
-    for impl in hip.PREFIX_IMPLS:
-        pre = SharedPrefix(kc[pslot], vt, plen, 256, vc[pslot])
-        os.environ["DMCP_PREFIX_IMPL"] = impl
-        try:
-            for chunk in (256, 1024):
+    pre = SharedPrefix(kc[pslot], vc[pslot], plen)
+    exp = reference.decode_attention(q, kc, vc, slot, lens, scale, prefix=pre)
+    for chunk in (256, 1024):
+        for sp in ("1", "5", "16"):  # prefix key splits (DMCP_PREFIX_SPLITS)
+            os.environ["DMCP_PREFIX_SPLITS"] = sp
+            try:
                 got = hip.decode_attention(q, kc, vc, slot, lens, scale, chunk=chunk, prefix=pre)
-                exp = reference.decode_attention(q, kc, vc, slot, lens, scale, prefix=pre)
-                torch.testing.assert_close(got.float(), exp.float(), atol=2e-2, rtol=2e-2)
-                assert got[B // 2].abs().sum().item() == 0
-        finally:
-            os.environ.pop("DMCP_PREFIX_IMPL")
-    pre = SharedPrefix(kc[pslot], vt, plen, 256, vc[pslot])
-    # the prefix kernel on the side stream == in line (both prefix kernels)
-    for impl in hip.PREFIX_IMPLS:
-        os.environ["DMCP_PREFIX_IMPL"] = impl
-        try:
-            prev = hip.set_prefix_overlap(True)
-            on = hip.decode_attention(q, kc, vc, slot, lens, scale, prefix=pre)
-            hip.set_prefix_overlap(False)
-            off = hip.decode_attention(q, kc, vc, slot, lens, scale, prefix=pre)
-        finally:
-            hip.set_prefix_overlap(prev)
-            os.environ.pop("DMCP_PREFIX_IMPL")
-        torch.cuda.synchronize()
-        assert torch.equal(on, off)
-        torch.testing.assert_close(on.float(), reference.decode_attention(q, kc, vc, slot, lens, scale,
-                                                                          prefix=pre).float(), atol=2e-2, rtol=2e-2)
+            finally:
+                os.environ.pop("DMCP_PREFIX_SPLITS")
+            torch.testing.assert_close(got.float(), exp.float(), atol=2e-2, rtol=2e-2)
+            assert got[B // 2].abs().sum().item() == 0
+    # a workspace too small for the prefix partials is refused (never overrun)
+    ws = hip.decode_workspace(B, Hq, Hkv, D, 256, "cuda", chunk=256, prefix_slots=0)
+    with pytest.raises(hip.HipOpsError):
+        hip.decode_attention(q, kc, vc, slot, lens, scale, workspace=ws, chunk=256, prefix=pre, splits=1)
     # length 0 in device memory: the prefix kernel is a no-op, rows read their own keys
     plen.zero_()
     got = hip.decode_attention(q, kc, vc, slot, lens, scale, prefix=pre)
@@ -138,13 +123,12 @@ def test_decode_attention_shared_prefix(hip, D, Hq, Hkv, P, B):
     torch.testing.assert_close(got.float(), exp.float(), atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("impl", ["mfma", "mfma2", "valu"])
 @pytest.mark.parametrize("splits", [1, 3, 6])
 @pytest.mark.parametrize("P", [0, 300])
-def test_decode_attention_balanced_splits(hip, impl, splits, P):
+def test_decode_attention_balanced_splits(hip, splits, P):
     """Equal per-row splits (decode_plan: at most ``splits`` parts of >= chunk
-    keys, rounded to 32-key tiles) for every per-row kernel, with and without
-    a shared prefix; lengths hit partial tiles and split boundaries."""
+    keys, rounded to 32-key tiles), with and without a shared prefix;
+    lengths hit partial tiles and split boundaries."""
     from dmcp.ops import reference
     from dmcp.ops.reference import SharedPrefix
     D, Hq, Hkv, MAXS, S = 64, 32, 8, 1024, 9
@@ -157,14 +141,8 @@ def test_decode_attention_balanced_splits(hip, impl, splits, P):
     lens = torch.tensor([P + n for n in lens_own], dtype=torch.int32, device="cuda")
     pre = None
     if P:
-        vt = torch.zeros((Hkv, D, MAXS), dtype=torch.bfloat16, device="cuda")
-        vt[:, :, :P] = vc[S, :, :P].transpose(-1, -2)
-        pre = SharedPrefix(kc[S], vt, torch.tensor([P], dtype=torch.int32, device="cuda"), 256)
-    prev = hip.set_decode_impl(impl)
-    try:
-        got = hip.decode_attention(q, kc, vc, slot, lens, 0.125, chunk=64, prefix=pre, splits=splits)
-    finally:
-        hip.set_decode_impl(prev)
+        pre = SharedPrefix(kc[S], vc[S], torch.tensor([P], dtype=torch.int32, device="cuda"))
+    got = hip.decode_attention(q, kc, vc, slot, lens, 0.125, chunk=64, prefix=pre, splits=splits)
     exp = reference.decode_attention(q, kc, vc, slot, lens, 0.125, prefix=pre)
     torch.testing.assert_close(got.float(), exp.float(), atol=2e-2, rtol=2e-2)
 

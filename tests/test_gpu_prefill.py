@@ -117,3 +117,87 @@ def test_model_prefill_kernel_matches_sdpa_path():
         m.clear_prefix()
     torch.testing.assert_close(outs[0], outs[1], atol=5e-2, rtol=5e-2)
     assert a._slot_prefix == {}
+
+
+@pytest.mark.parametrize("D,Hq,Hkv", [(64, 32, 8), (64, 16, 2), (128, 24, 8)])
+@pytest.mark.parametrize("kv", ["bf16", "fp8"])
+def test_prefill_varlen_matches_per_sequence_reference(hip, D, Hq, Hkv, kv):
+    """One packed launch over sequences of mixed lengths (1 token to a few
+    hundred, partial tiles), some after the shared prefix read in place from
+    the prefix slot, some plain prefills, one extending its own cached keys
+    == the fp32 reference of each sequence; stale NaN cache regions past each
+    sequence's end (and the prefix range of the own slot) are never read."""
+    from dmcp.ops import reference
+    MAXS, S = 1024, 8
+    pslot, P = S - 1, 300
+    scale = 1 / math.sqrt(D)
+    seqs = [(1, P, P), (157, P, P), (33, 0, 0), (260, P, P), (5, 0, 0), (96, 512, 0)]  # (T, start, prefix len)
+    Ttot = sum(t for t, _, _ in seqs)
+    q = _bf(Ttot, Hq, D, seed=5)
+    kc = _bf(S, Hkv, MAXS, D, seed=6)
+    vc = _bf(S, Hkv, MAXS, D, seed=7)
+    if kv == "fp8":
+        kc, vc = reference.kv_encode(kc.float(), torch.uint8), reference.kv_encode(vc.float(), torch.uint8)
+    nanv = 0x7F if kv == "fp8" else float("nan")  # e4m3 0x7f is NaN
+    offsets, slots, starts, plens = [0], [], [], []
+    for i, (T, st, pl) in enumerate(seqs):
+        slots.append(i)
+        starts.append(st)
+        plens.append(pl)
+        offsets.append(offsets[-1] + T)
+    ref_k, ref_v = kc.clone(), vc.clone()
+    for i, (T, st, pl) in enumerate(seqs):
+        kc[i, :, st + T:] = nanv
+        vc[i, :, st + T:] = nanv
+        if pl:
+            kc[i, :, :pl] = nanv
+            vc[i, :, :pl] = nanv
+    kc[pslot, :, P:] = nanv
+    vc[pslot, :, P:] = nanv
+    exp = reference.prefill_attention_varlen(q, ref_k, ref_v, offsets, slots, starts, pslot, plens, scale)
+    got = hip.prefill_attention_varlen(q, kc, vc, offsets, slots, starts, pslot, plens, scale)
+    assert torch.isfinite(got.float()).all()
+    torch.testing.assert_close(got.float(), exp.float(), atol=3e-2, rtol=3e-2)
+    # single sequences through the varlen launch == the single-sequence kernel
+    one = hip.prefill_attention_varlen(q[:157 + 1][1:], kc, vc, [0, 157], [1], [P], pslot, [P], scale)
+    solo = hip.prefill_attention(q[1:158], kc, vc, 1, P, pslot, P, scale, nsplit=1)
+    torch.testing.assert_close(one.float(), solo.float(), atol=1e-2, rtol=1e-2)
+
+
+def test_prefill_varlen_rejects_bad_tables(hip):
+    q = _bf(10, 8, 64)
+    kc = _bf(2, 2, 64, 64)
+    with pytest.raises(hip.HipOpsError):  # past the cache capacity
+        hip.prefill_attention_varlen(q, kc, kc, [0, 10], [0], [60])
+    with pytest.raises(hip.HipOpsError):  # offsets do not cover q
+        hip.prefill_attention_varlen(q, kc, kc, [0, 9], [0], [0])
+    with pytest.raises(hip.HipOpsError):  # prefix longer than the start
+        hip.prefill_attention_varlen(q, kc, kc, [0, 10], [0], [3], 1, [5])
+
+
+@pytest.mark.parametrize("kv", ["bf16", "fp8"])
+def test_model_prefill_batch_matches_reference(kv):
+    """LocalLM.prefill_batch (packed GEMMs + varlen attention) == one
+    forward_tokens per sequence and the fp32 reference model, with and without
+    the shared prefix."""
+    from dmcp.models.llm import LocalLM, preset
+    m = LocalLM(preset("tiny", max_batch=8, kv_dtype=kv), device="cuda", seed=9)
+    seqs = [[256] + list(b"class A { void a() {} }"), [256] + list(b"interface Bee { int b(); long c(); }"),
+            [256, 65]]
+    single = [m.forward_tokens(torch.tensor(t, dtype=torch.int32), s, 0).float() for s, t in enumerate(seqs)]
+    got = m.prefill_batch([(t, s + 3, 0) for s, t in enumerate(seqs)]).float()
+    for g, one, t in zip(got, single, seqs):
+        ref = m.reference_logits(t)[-1].float()
+        assert (g - ref).abs().max().item() / max(1.0, ref.abs().max().item()) < 0.05
+        assert (g - one).abs().max().item() / max(1.0, one.abs().max().item()) < 0.03
+    prefix = [256] + list(b"Shared instructions and the README of the project. " * 3)
+    P = m.set_prefix(prefix)
+    try:
+        for s in range(len(seqs)):
+            m.fork_prefix(s)
+        got = m.prefill_batch([(t[1:], s, P) for s, t in enumerate(seqs)]).float()
+        for g, t in zip(got, seqs):
+            ref = m.reference_logits(prefix + t[1:])[-1].float()
+            assert (g - ref).abs().max().item() / max(1.0, ref.abs().max().item()) < 0.05
+    finally:
+        m.clear_prefix()

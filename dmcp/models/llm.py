@@ -15,12 +15,16 @@ MI355X mapping:
   append in the QKV epilogue, SwiGLU in the gate/up epilogue, the residual
   add in the O / down epilogues -- a layer is 4 GEMM launches + attention
   (measured: 60 vs 77 us per layer at 16 rows);
-* larger decode steps, prefill and extend use hipBLASLt through
-  ``torch.nn.functional.linear`` with the hand-written element-wise kernels
-  (fused residual-add + RMSNorm, RoPE + KV-cache append, SwiGLU) between:
-  at 64-128 rows the register-direct fused GEMM re-reads every X row per
-  weight tile and is bound by per-CU L1 ingest, 1.5-3x slower than
-  hipBLASLt's LDS-tiled kernels (profiles/fused_gemm_vs_hipblaslt_r2.jsonl);
+* decode steps of 17-512 rows (the enrichment operating point is ~300)
+  run every projection on the weight-streaming GEMM (``csrc/wgemm.hip``:
+  each weight tile read from HBM once per step, all rows of an M part per
+  block, the M parts of a tile on one XCD) with the neighbour op fused:
+  QKV + RoPE + KV append, O + residual + RMSNorm, gate/up + SwiGLU, down +
+  residual + next RMSNorm -- 4 GEMMs + 3 row reductions per layer;
+* prefill / extend use hipBLASLt through ``torch.nn.functional.linear``
+  (thousands of rows: large MFMA tiles win) with the hand-written
+  element-wise kernels between (fused residual-add + RMSNorm, RoPE +
+  KV-cache append, SwiGLU);
 * decode attention (per-row split-K kernel + the shared-prefix kernel,
   merged by log-sum-exp), masked greedy sampling and the embedding gather
   are hand-written gfx950 kernels on every path;
@@ -112,6 +116,15 @@ def fused_shapes_ok(c: LMConfig) -> bool:
     50257, ...) keeps every decode step on the hipBLASLt path."""
     return (c.hidden % 32 == 0 and (c.n_heads * c.head_dim) % 32 == 0 and c.intermediate % 32 == 0
             and c.head_dim % 32 == 0 and c.vocab_size % 16 == 0 and c.hidden % 16 == 0)
+
+
+def wgemm_shapes_ok(c: LMConfig) -> bool:
+    """The weight-streaming GEMMs' contract (csrc/wgemm.hip): reduction
+    depths (hidden, heads x head_dim, intermediate) multiples of 64, output
+    widths (QKV, hidden) multiples of 64 and <= 8192 (the fused row
+    reductions), the gate/up halves multiples of 64."""
+    return (c.hidden % 64 == 0 and (c.n_heads * c.head_dim) % 64 == 0 and c.intermediate % 64 == 0
+            and c.qkv_dim % 64 == 0 and c.qkv_dim <= 8192 and c.hidden <= 8192 and c.head_dim % 16 == 0)
 
 
 def preset(name: str, **overrides) -> LMConfig:
@@ -224,19 +237,14 @@ class LocalLM:
         ps = ops.PREFIX_MFMA_MAX_SPLITS if shared_prefix else 0
         self.attn_ws = (ops.decode_workspace(self.max_rows, c.n_heads, c.n_kv_heads, c.head_dim, c.max_seq,
                                              self.device, prefix_slots=ps) if self.device.type == "cuda" else None)
-        # down projection + residual + next norm on the split-K LDS kernel at
-        # fused_max_rows < rows <= 128 (csrc/splitk_gemm.hip; 21.3 vs 23.8 us
-        # per layer at 78 rows, profiles/splitk_gemm_r2_v2.jsonl; the O
-        # projection stays on hipBLASLt, where the kernel is not faster)
-        self.splitk_down = None
-        if (self.device.type == "cuda" and os.environ.get("DMCP_SPLITK_DOWN", "1") != "0"
-                and c.hidden % 64 == 0 and c.hidden <= 8192
-                and c.intermediate % (128 * ops.splitk_splits(c.hidden, c.intermediate)) == 0):
-            self.splitk_down = ops.splitk_splits(c.hidden, c.intermediate)
-            # SwiGLU inside the operand staging: measured slower (2.61 vs 2.33 ms per fp8 step,
-            # profiles/decode_step_splitk_swiglu_ab.jsonl) -- opt-in
-            self.splitk_swiglu = os.environ.get("DMCP_SPLITK_SWIGLU", "0") == "1"
-            self.splitk_ws = torch.empty(self.splitk_down * 128 * c.hidden, dtype=torch.float32, device=self.device)
+        # steps of fused_max_rows < rows <= 512: every projection on the
+        # weight-streaming GEMM (csrc/wgemm.hip) with its neighbour op in the
+        # epilogue / reduction -- QKV + RoPE + KV append, O + residual + norm,
+        # gate/up + SwiGLU, down + residual + next norm
+        self.use_wgemm = (self.device.type == "cuda" and wgemm_shapes_ok(c)
+                          and os.environ.get("DMCP_WGEMM", "1") != "0")
+        self.wgemm_ws = (ops.wgemm_workspace(min(self.max_rows, ops.WGEMM_MAX_ROWS), max(c.qkv_dim, c.hidden),
+                                             self.device) if self.use_wgemm else None)
 
     # ------------------------------------------------------------ weights
     def _init_weights(self, seed: int) -> Dict[str, torch.Tensor]:
@@ -456,24 +464,24 @@ class LocalLM:
         x = ops.embedding(self.w["embed"], tokens)
         resid = x.clone()
         h = ops.add_rmsnorm(x, self.w["l0.ln1"], c.eps)
+        wide = self.use_wgemm and B <= ops.WGEMM_MAX_ROWS
         for i in range(c.layers):
             kc, vc = self.k_cache[i], self.v_cache[i]
-            qkv = F.linear(h, self.w[f"l{i}.wqkv"])
-            q = ops.rope_kv(qkv, positions, slots, self.cos_sin, kc, vc, c.n_heads)
-            att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws, chunk=chunk,
-                                       prefix=self._prefix(i), splits=splits)
-            o = F.linear(att.view(B, c.n_heads * c.head_dim), self.w[f"l{i}.wo"])
-            h = ops.add_rmsnorm(o, self.w[f"l{i}.ln2"], c.eps, residual=resid)
             nxt = self.w[f"l{i + 1}.ln1"] if i + 1 < c.layers else self.w["norm_f"]
-            if self.splitk_down and B <= 128:
-                gu = F.linear(h, self.w[f"l{i}.wgu"])
-                if self.splitk_swiglu:  # SwiGLU computed while the down GEMM stages its operand
-                    h = ops.linear_resid_norm(gu, self.w[f"l{i}.wdown"], resid, nxt, c.eps, self.splitk_ws,
-                                              splits=self.splitk_down, variant=2)
-                else:
-                    h = ops.linear_resid_norm(ops.silu_mul(gu), self.w[f"l{i}.wdown"], resid, nxt, c.eps,
-                                              self.splitk_ws, splits=self.splitk_down)
+            if wide:
+                q = ops.wgemm_rope_kv(h, self.w[f"l{i}.wqkv"], positions, slots, self.cos_sin, kc, vc, c.n_heads,
+                                      self.wgemm_ws)
+            else:
+                q = ops.rope_kv(F.linear(h, self.w[f"l{i}.wqkv"]), positions, slots, self.cos_sin, kc, vc, c.n_heads)
+            att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws, chunk=chunk,
+                                       prefix=self._prefix(i), splits=splits).view(B, c.n_heads * c.head_dim)
+            if wide:
+                h = ops.wgemm_resid_norm(att, self.w[f"l{i}.wo"], resid, self.w[f"l{i}.ln2"], c.eps, self.wgemm_ws)
+                act = ops.wgemm_swiglu(h, self.w[f"l{i}.wgu"])
+                h = ops.wgemm_resid_norm(act, self.w[f"l{i}.wdown"], resid, nxt, c.eps, self.wgemm_ws)
                 continue
+            o = F.linear(att, self.w[f"l{i}.wo"])
+            h = ops.add_rmsnorm(o, self.w[f"l{i}.ln2"], c.eps, residual=resid)
             m = self._mlp(i, h)
             h = ops.add_rmsnorm(m, nxt, c.eps, residual=resid)
         return F.linear(h, self.w["lm_head"])

@@ -59,22 +59,28 @@ def fused_resid(x, w, residual, wk: int = 0):
     return _hip().fused_resid(x, w, residual, wk or (16 if x.shape[1] >= 4096 else 8))
 
 
-def linear_resid_norm(x, w, residual, norm_w, eps, workspace, splits: int = 0, out=None, variant: int = 1):
+WGEMM_MAX_ROWS = 512  # row limit of the weight-streaming GEMMs (dmcp.ops.hip.WGEMM_MAX_ROWS)
+
+
+def wgemm_swiglu(x, w, out=None):
+    """silu(x . w[:I]^T) * (x . w[I:]^T) on the weight-streaming gfx950 GEMM (GPU only, M <= 512)."""
+    return _hip().wgemm_swiglu(x, w, out)
+
+
+def wgemm_resid_norm(x, w, residual, norm_w, eps, workspace, out=None):
     """residual += bf16(x . w^T); returns RMSNorm(residual) * norm_w -- split-K
-    gfx950 GEMM + one fused reduce/residual/norm pass (GPU only, M <= 128)."""
-    return _hip().linear_resid_norm(x, w, residual, norm_w, eps, workspace, splits, out, variant)
+    weight-streaming GEMM + one fused reduce/residual/norm pass (GPU only)."""
+    return _hip().wgemm_resid_norm(x, w, residual, norm_w, eps, workspace, out)
 
 
-def linear_rope_kv(x, w, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, workspace, splits: int = 0,
-                   q_out=None, variant: int = 1):
-    """rope_kv(F.linear(x, w)) -- split-K gfx950 GEMM + one reduction that
-    applies RoPE and appends K/V to the cache (GPU only, M <= 128)."""
-    return _hip().linear_rope_kv(x, w, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, workspace, splits, q_out,
-                                 variant)
+def wgemm_rope_kv(x, w, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, workspace, q_out=None):
+    """rope_kv(F.linear(x, w)) -- split-K weight-streaming GEMM + one reduction
+    that applies RoPE and appends K/V to the cache (GPU only)."""
+    return _hip().wgemm_rope_kv(x, w, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, workspace, q_out)
 
 
-def splitk_splits(N, K):
-    return _hip().splitk_splits(N, K)
+def wgemm_workspace(rows, n_max, device):
+    return _hip().wgemm_workspace(rows, n_max, device)
 
 
 def fused_linear_norm(x, w, eps, out=None):

@@ -15,7 +15,7 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 SRCS = [os.path.join(CSRC, "dmcp_kernels.hip"), os.path.join(CSRC, "fused_gemm.hip"),
-        os.path.join(CSRC, "prefill_attn.hip"), os.path.join(CSRC, "splitk_gemm.hip")]
+        os.path.join(CSRC, "prefill_attn.hip"), os.path.join(CSRC, "wgemm.hip")]
 HEADERS = [os.path.join(CSRC, "dmcp_common.hpp")]
 SRC = SRCS[0]  # kept for callers that name the main source
 TARGET = os.path.join(HERE, "_hipops.so")

@@ -60,9 +60,10 @@ def lib() -> ctypes.CDLL:
             "dmcp_masked_argmax": ([_vp, _vp, _vp, _i, _vp, _i, _i, _i, _vp], _i),
             "dmcp_embedding": ([_vp, _vp, _vp, _i, _i, _i, _vp], _i),
             "dmcp_fused_gemm_max_rows": ([], _i),
-            "dmcp_splitk_resid_norm": ([_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _i, _vp], _i),
-            "dmcp_splitk_rope_kv": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i,
-                                     _i, _i, _vp], _i),
+            "dmcp_wgemm": ([_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp], _i),
+            "dmcp_wgemm_resid_norm": ([_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _vp], _i),
+            "dmcp_wgemm_rope_kv": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i,
+                                    _i, _i, _vp], _i),
             "dmcp_fused_gemm": ([_i, _i, _vp, _vp, _vp, _i, _i, _i, _f, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i,
                                  _i, _i, _i, _i, _vp], _i),
         }
@@ -547,88 +548,141 @@ def fused_resid(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, wk: in
     return residual
 
 
-SPLITK_MAX_ROWS = 128
+WGEMM_MAX_ROWS = 512
 
 
-def splitk_splits(N: int, K: int, target_blocks: int = 256) -> int:
-    """K slices for linear_resid_norm: enough 64-column blocks to cover the
-    chip, each slice a whole number of 32-deep k-steps (>= 4)."""
-    s = 1
-    while (N // 64) * s < target_blocks and K % (256 * s) == 0:
-        s *= 2
-    return s
+def wgemm_plan(M: int, N: int, K: int, swiglu: bool = False, target_blocks: int = 192) -> tuple:
+    """(K slices S, M parts) of the weight-streaming GEMM (csrc/wgemm.hip):
+    M parts of <= 192 rows (<= 3 16-row tiles per wave), then K slices
+    (powers of two, whole 64-deep chunks) until 64-row weight tiles x parts x
+    slices covers ~3/4 of the 256 CUs.  SwiGLU writes its output directly
+    (S = 1) and splits M instead."""
+    mparts = max(1, -(-M // 192))
+    tiles = (N // 2 if swiglu else N) // 64
+    if swiglu:
+        while tiles * mparts < target_blocks and -(-M // (mparts + 1)) >= 16:
+            mparts += 1
+        return 1, mparts
+    S = 1
+    while tiles * mparts * S < target_blocks and S < 8 and K % (64 * S * 2) == 0:
+        S *= 2
+    return S, mparts
 
 
-def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor, eps: float,
-                      workspace: torch.Tensor, splits: int = 0, out: Optional[torch.Tensor] = None,
-                      variant: int = 1) -> torch.Tensor:
-    """residual += bf16(x . w^T) (in place); returns RMSNorm(residual) * norm_w
-    -- F.linear + add_rmsnorm in two launches (csrc/splitk_gemm.hip: split-K
-    MFMA GEMM into fp32 slabs, then one reduction per row that also adds the
-    residual and normalises).  x [M, K] (M <= 128), w [N, K], residual [M, N];
-    workspace: fp32 with at least splits * M * N elements.  variant 2: x is
-    the gate/up output [M, 2K] and the operand silu(gate) * up (SwiGLU fused
-    into the operand staging)."""
-    _req(x, torch.bfloat16, "linear_resid_norm.x")
-    _req(w, torch.bfloat16, "linear_resid_norm.w")
-    _req(residual, torch.bfloat16, "linear_resid_norm.residual")
-    _req(norm_w, torch.bfloat16, "linear_resid_norm.norm_w")
-    xk = x.shape[1] // 2 if variant == 2 else x.shape[1]
-    if x.dim() != 2 or w.dim() != 2 or xk != w.shape[1] or (variant == 2 and x.shape[1] % 2):
-        raise HipOpsError(f"linear_resid_norm: x {tuple(x.shape)} / w {tuple(w.shape)} are not [M, K] / [N, K]")
-    M, K = x.shape[0], w.shape[1]
+def _wgemm_args(x: torch.Tensor, w: torch.Tensor, name: str) -> tuple:
+    _req(x, torch.bfloat16, f"{name}.x")
+    _req(w, torch.bfloat16, f"{name}.w")
+    if x.dim() != 2 or w.dim() != 2 or x.shape[1] != w.shape[1]:
+        raise HipOpsError(f"{name}: x {tuple(x.shape)} / w {tuple(w.shape)} are not [M, K] / [N, K]")
+    M, K = x.shape
     N = w.shape[0]
-    S = splits or splitk_splits(N, K)
-    if variant not in (0, 1, 2):
-        raise HipOpsError(f"linear_resid_norm: unknown variant {variant}")
-    if not 1 <= M <= SPLITK_MAX_ROWS or N % 64 or N > 8192 or K % ((128 if variant >= 1 else 32) * S):
-        raise HipOpsError(f"linear_resid_norm: unsupported shape M={M} K={K} N={N} splits={S}")
-    if tuple(residual.shape) != (M, N) or norm_w.numel() != N:
-        raise HipOpsError("linear_resid_norm: residual / norm weight shape mismatch")
-    if workspace.dtype != torch.float32 or not workspace.is_contiguous() or workspace.numel() < S * M * N:
-        raise HipOpsError(f"linear_resid_norm: workspace needs {S * M * N} contiguous fp32 elements")
+    if not 1 <= M <= WGEMM_MAX_ROWS or K % 64 or N % 64:
+        raise HipOpsError(f"{name}: needs 1 <= M <= {WGEMM_MAX_ROWS}, K % 64 == 0, N % 64 == 0 (M={M} K={K} N={N})")
+    return M, K, N
+
+
+def _wgemm_ws(workspace: torch.Tensor, n: int, name: str) -> None:
+    if workspace.dtype != torch.float32 or not workspace.is_contiguous() or workspace.numel() < n:
+        raise HipOpsError(f"{name}: workspace needs {n} contiguous fp32 elements")
+
+
+def wgemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x . w^T in bf16 (F.linear) on the weight-streaming kernel; M <= 512."""
+    M, K, N = _wgemm_args(x, w, "wgemm")
+    _, mparts = wgemm_plan(M, N, K)
     if out is None:
         out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
-    _req_out(out, torch.bfloat16, M * N, "linear_resid_norm.out")
-    _check(lib().dmcp_splitk_resid_norm(_ptr(x), _ptr(w), _ptr(workspace), _ptr(residual), _ptr(norm_w), _ptr(out),
-                                        M, K, N, S, float(eps), variant, _stream()), "dmcp_splitk_resid_norm")
+    _req_out(out, torch.bfloat16, M * N, "wgemm.out")
+    _check(lib().dmcp_wgemm(_ptr(x), _ptr(w), _ptr(out), None, M, N, K, 1, mparts, 0, 0, _stream()), "dmcp_wgemm")
     return out
 
 
-def linear_rope_kv(x: torch.Tensor, w: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos_sin: torch.Tensor,
-                   k_cache: torch.Tensor, v_cache: torch.Tensor, n_q_heads: int, workspace: torch.Tensor,
-                   splits: int = 0, q_out: Optional[torch.Tensor] = None, variant: int = 1) -> torch.Tensor:
-    """rope_kv(F.linear(x, w), ...) in two launches (csrc/splitk_gemm.hip:
-    split-K MFMA GEMM into fp32 slabs, then per row the reduction, RoPE, the
-    q write and the K/V-cache append).  x [M, K] (M <= 128); returns q."""
+def wgemm_swiglu(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """silu(x . w[:I]^T) * (x . w[I:]^T) -- the gate/up projection with SwiGLU
+    in its epilogue (w = [gate; up], [2I, K], I % 64 == 0); returns [M, I]."""
+    M, K, N = _wgemm_args(x, w, "wgemm_swiglu")
+    if N % 128:
+        raise HipOpsError(f"wgemm_swiglu: 2I = {N} must be a multiple of 128")
+    inter = N // 2
+    _, mparts = wgemm_plan(M, N, K, swiglu=True)
+    if out is None:
+        out = torch.empty((M, inter), dtype=torch.bfloat16, device=x.device)
+    _req_out(out, torch.bfloat16, M * inter, "wgemm_swiglu.out")
+    _check(lib().dmcp_wgemm(_ptr(x), _ptr(w), _ptr(out), None, M, N, K, 1, mparts, 2, inter, _stream()),
+           "dmcp_wgemm[swiglu]")
+    return out
+
+
+def wgemm_partials(x: torch.Tensor, w: torch.Tensor, workspace: torch.Tensor, splits: int = 0) -> int:
+    """fp32 split-K partials of x . w^T into ``workspace`` [S, M, N]; returns S."""
+    M, K, N = _wgemm_args(x, w, "wgemm_partials")
+    S, mparts = wgemm_plan(M, N, K)
+    S = splits or S
+    if K % (64 * S):
+        raise HipOpsError(f"wgemm_partials: K={K} does not split into {S} slices of whole 64-deep chunks")
+    _wgemm_ws(workspace, S * M * N, "wgemm_partials")
+    _check(lib().dmcp_wgemm(_ptr(x), _ptr(w), None, _ptr(workspace), M, N, K, S, mparts, 1, 0, _stream()),
+           "dmcp_wgemm[partials]")
+    return S
+
+
+def wgemm_resid_norm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor, eps: float,
+                     workspace: torch.Tensor, out: Optional[torch.Tensor] = None, splits: int = 0) -> torch.Tensor:
+    """residual += bf16(x . w^T) (in place); returns RMSNorm(residual) * norm_w
+    -- F.linear + add_rmsnorm as one split-K GEMM + one reduction per row that
+    adds the residual and normalises.  x [M, K] (M <= 512), w [N, K]."""
+    M, K, N = _wgemm_args(x, w, "wgemm_resid_norm")
+    _req(residual, torch.bfloat16, "wgemm_resid_norm.residual")
+    _req(norm_w, torch.bfloat16, "wgemm_resid_norm.norm_w")
+    if tuple(residual.shape) != (M, N) or norm_w.numel() != N or N > 8192:
+        raise HipOpsError("wgemm_resid_norm: residual / norm weight shape mismatch")
+    S, mparts = wgemm_plan(M, N, K)
+    S = splits or S
+    if K % (64 * S):
+        raise HipOpsError(f"wgemm_resid_norm: K={K} does not split into {S} slices")
+    _wgemm_ws(workspace, S * M * N, "wgemm_resid_norm")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    _req_out(out, torch.bfloat16, M * N, "wgemm_resid_norm.out")
+    _check(lib().dmcp_wgemm_resid_norm(_ptr(x), _ptr(w), _ptr(workspace), _ptr(residual), _ptr(norm_w), _ptr(out),
+                                       M, K, N, S, mparts, float(eps), _stream()), "dmcp_wgemm_resid_norm")
+    return out
+
+
+def wgemm_rope_kv(x: torch.Tensor, w: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos_sin: torch.Tensor,
+                  k_cache: torch.Tensor, v_cache: torch.Tensor, n_q_heads: int, workspace: torch.Tensor,
+                  q_out: Optional[torch.Tensor] = None, splits: int = 0) -> torch.Tensor:
+    """rope_kv(F.linear(x, w), ...) as one split-K GEMM + one reduction per row
+    (RoPE, the q write and the K/V-cache append).  x [M, K] (M <= 512);
+    returns q [M, Hq, D]."""
+    M, K, N = _wgemm_args(x, w, "wgemm_rope_kv")
     S_, Hkv, MAXS, D = k_cache.shape
-    _req(x, torch.bfloat16, "linear_rope_kv.x")
-    _req(w, torch.bfloat16, "linear_rope_kv.w")
-    kv8 = _req_kv(k_cache, v_cache, "linear_rope_kv")
-    _req(pos, torch.int32, "linear_rope_kv.pos")
-    _req(slot, torch.int32, "linear_rope_kv.slot")
-    _req(cos_sin, torch.float32, "linear_rope_kv.cos_sin")
-    if x.dim() != 2 or w.dim() != 2 or x.shape[1] != w.shape[1]:
-        raise HipOpsError(f"linear_rope_kv: x {tuple(x.shape)} / w {tuple(w.shape)} are not [M, K] / [N, K]")
-    M, K = x.shape
-    N = w.shape[0]
-    S = splits or splitk_splits(N, K)
-    if variant not in (0, 1):
-        raise HipOpsError(f"linear_rope_kv: unknown variant {variant}")
-    if (v_cache.shape != k_cache.shape or N != (n_q_heads + 2 * Hkv) * D or D % 16 or N % 64 or N > 8192
-            or not 1 <= M <= SPLITK_MAX_ROWS or K % ((128 if variant == 1 else 32) * S)):
-        raise HipOpsError(f"linear_rope_kv: unsupported shape M={M} K={K} N={N} D={D} splits={S}")
+    kv8 = _req_kv(k_cache, v_cache, "wgemm_rope_kv")
+    _req(pos, torch.int32, "wgemm_rope_kv.pos")
+    _req(slot, torch.int32, "wgemm_rope_kv.slot")
+    _req(cos_sin, torch.float32, "wgemm_rope_kv.cos_sin")
+    if v_cache.shape != k_cache.shape or N != (n_q_heads + 2 * Hkv) * D or D % 16 or N > 8192:
+        raise HipOpsError(f"wgemm_rope_kv: w {tuple(w.shape)} does not match Hq={n_q_heads} / kv {tuple(k_cache.shape)}")
     if pos.numel() != M or slot.numel() != M or cos_sin.dim() != 3 or tuple(cos_sin.shape[1:]) != (D // 2, 2):
-        raise HipOpsError("linear_rope_kv: pos/slot/cos_sin shape mismatch")
-    if workspace.dtype != torch.float32 or not workspace.is_contiguous() or workspace.numel() < S * M * N:
-        raise HipOpsError(f"linear_rope_kv: workspace needs {S * M * N} contiguous fp32 elements")
+        raise HipOpsError("wgemm_rope_kv: pos/slot/cos_sin shape mismatch")
+    S, mparts = wgemm_plan(M, N, K)
+    S = splits or S
+    if K % (64 * S):
+        raise HipOpsError(f"wgemm_rope_kv: K={K} does not split into {S} slices")
+    _wgemm_ws(workspace, S * M * N, "wgemm_rope_kv")
     if q_out is None:
         q_out = torch.empty((M, n_q_heads, D), dtype=torch.bfloat16, device=x.device)
-    _req_out(q_out, torch.bfloat16, M * n_q_heads * D, "linear_rope_kv.q_out")
-    _check(lib().dmcp_splitk_rope_kv(_ptr(x), _ptr(w), _ptr(workspace), _ptr(pos), _ptr(slot), _ptr(cos_sin),
-                                     _ptr(q_out), _ptr(k_cache), _ptr(v_cache), M, K, n_q_heads, Hkv, D, MAXS,
-                                     cos_sin.shape[0], S_, kv8, S, variant, _stream()), "dmcp_splitk_rope_kv")
+    _req_out(q_out, torch.bfloat16, M * n_q_heads * D, "wgemm_rope_kv.q_out")
+    _check(lib().dmcp_wgemm_rope_kv(_ptr(x), _ptr(w), _ptr(workspace), _ptr(pos), _ptr(slot), _ptr(cos_sin),
+                                    _ptr(q_out), _ptr(k_cache), _ptr(v_cache), M, K, n_q_heads, Hkv, D, MAXS,
+                                    cos_sin.shape[0], S_, kv8, S, mparts, _stream()), "dmcp_wgemm_rope_kv")
     return q_out
+
+
+def wgemm_workspace(rows: int, n_max: int, device) -> torch.Tensor:
+    """Partials scratch for the split-K weight-streaming GEMMs of a step of up
+    to ``rows`` rows and ``n_max`` output columns (at most 8 slices)."""
+    return torch.empty(8 * rows * n_max, dtype=torch.float32, device=device)
 
 
 def fused_linear_norm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None,

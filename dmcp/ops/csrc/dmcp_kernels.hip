@@ -422,6 +422,27 @@ __device__ __forceinline__ void load_kv_tile(const void* __restrict__ kb, const 
     }
 }
 
+// V tile layout in LDS: 32 key rows of D bf16, unpadded, with the 4-element
+// quads of row r stored at quad index q ^ vswz(r).  The XOR leaves every
+// 16-B store whole and makes both access patterns conflict-free
+// (MI355X_MICROARCH.md §LDS bank rules):
+//  * ds_read_b64_tr_b16 (2 x 32 lanes, bank (a/4) mod 64): a half reads 8
+//    rows x one 4-quad d block; rows of equal parity share a bank window and
+//    get distinct quad groups (bits 2-3 of the XOR, (r>>1)&3);
+//  * ds_write_b128 of fp8-converted V (8 x 8 lanes, bank (a/4) mod 32): a
+//    group stores rows r, r+1 at the same quads; bit 1 of the XOR (r&1) puts
+//    the odd row in the other 16-B half of each 32-B window.
+// The padded layout this replaces (144-B rows) measured ~1 conflict cycle per
+// LDS instruction (profiles/pmc_decode_step_320rows_fp8_r3.txt).  D=128 gets
+// the read-side XOR only (its rows are a whole bank row).
+template <int D>
+__device__ __forceinline__ int vswz(int r) {
+    if constexpr (D == 64)
+        return 2 * (r & 1) + 4 * ((r >> 1) & 3);
+    else
+        return 4 * (r & 7);
+}
+
 // One tile of the MFMA per-row kernel: V -> the wave's LDS tile, S^T on the
 // matrix cores, then (prefetch) the tile two ahead is loaded into the same
 // registers while the softmax and the PV product run.
@@ -429,28 +450,29 @@ template <int D, bool KV8>
 __device__ __forceinline__ void attn_tile_mfma(KVTile<D, KV8>& cur, bool prefetch, int kt_next,
                                                const void* __restrict__ kb, const void* __restrict__ vb,
                                                int kt, int end, int lane, int g16, uint16_t* vw,
-                                               const uint16_t* tr0, const uint16_t* tr1,
+                                               const uint16_t* tr0, int trk,
                                                const bf16x8_t (&qf)[D / 32], float& m, float& l,
                                                f32x4_t (&acc)[D / 16], float scale_log2) {
     constexpr int KS = D / 32;
     constexpr int DB = D / 16;
-    constexpr int VROW = D + 8;
     const bool partial = kt + 32 > end;
-    if constexpr (KV8) {  // 16 e4m3 per chunk -> two 8-bf16 LDS stores
+    if constexpr (KV8) {  // 16 e4m3 per chunk -> two 8-bf16 LDS stores (quads q, q+2)
         constexpr int CPK = D / 16;
 #pragma unroll
         for (int r = 0; r < D / 32; ++r) {
             const int ch = lane + kWave * r;
-            uint16_t* dst = vw + (ch / CPK) * VROW + (ch % CPK) * 16;
-            *reinterpret_cast<uint4*>(dst) = fp8x8_to_bf16x8(make_uint2(cur.v[r].x, cur.v[r].y));
-            *reinterpret_cast<uint4*>(dst + 8) = fp8x8_to_bf16x8(make_uint2(cur.v[r].z, cur.v[r].w));
+            const int row = ch / CPK, q = 4 * (ch % CPK), sw = vswz<D>(row);
+            uint16_t* rp = vw + row * D;
+            *reinterpret_cast<uint4*>(rp + 4 * (q ^ sw)) = fp8x8_to_bf16x8(make_uint2(cur.v[r].x, cur.v[r].y));
+            *reinterpret_cast<uint4*>(rp + 4 * ((q + 2) ^ sw)) = fp8x8_to_bf16x8(make_uint2(cur.v[r].z, cur.v[r].w));
         }
     } else {
         constexpr int CPK = D / 8;
 #pragma unroll
         for (int r = 0; r < D / 16; ++r) {
             const int ch = lane + kWave * r;
-            *reinterpret_cast<uint4*>(vw + (ch / CPK) * VROW + (ch % CPK) * 8) = cur.v[r];
+            const int row = ch / CPK;
+            *reinterpret_cast<uint4*>(vw + row * D + 4 * ((2 * (ch % CPK)) ^ vswz<D>(row))) = cur.v[r];
         }
     }
     f32x4_t sacc[2];
@@ -509,11 +531,13 @@ __device__ __forceinline__ void attn_tile_mfma(KVTile<D, KV8>& cur, bool prefetc
     const bf16x8_t pf = __builtin_convertvector(pr, bf16x8_t);
 #pragma unroll
     for (int db = 0; db < DB; ++db) {
-        // the two transposed reads as whole 32-bit registers (no 16-bit repacking)
+        // the two transposed reads (keys +0 / +16) as whole 32-bit registers;
+        // d block db sits at quad group db ^ trk of the lane's swizzled row
+        const uint16_t* tp = tr0 + 16 * (db ^ trk);
         const uint2 lo = __builtin_bit_cast(
-            uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16_t*)(tr0 + 16 * db)));
+            uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16_t*)tp));
         const uint2 hi = __builtin_bit_cast(
-            uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16_t*)(tr1 + 16 * db)));
+            uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16_t*)(tp + 16 * D)));
         const uint4 a = make_uint4(lo.x, lo.y, hi.x, hi.y);
         acc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), pf, acc[db], 0, 0, 0);
     }
@@ -560,9 +584,8 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
     static_assert(D % 32 == 0, "D must be a multiple of 32");
     constexpr int KS = D / 32;    // 32-dim k-steps of the S product
     constexpr int DB = D / 16;    // 16-row d blocks of O^T
-    constexpr int VROW = D + 8;   // LDS row stride in bf16 (144 B at D=64: conflict-light tr reads)
     constexpr int NW = kBlock / kWave;
-    __shared__ __attribute__((aligned(16))) uint16_t vlds[NW][32 * VROW];
+    __shared__ __attribute__((aligned(16))) uint16_t vlds[NW][32 * D];
     const int lane = threadIdx.x & (kWave - 1);
     // wave index made provably uniform: the item loop, its bounds and the
     // slot / seq_len reads stay scalar (no exec-masked control flow, which
@@ -575,9 +598,11 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
     const int total = B * Hkv * splits;
     uint16_t* vw = vlds[wave];
     // transposed-read addresses (tile-invariant): lane 4q+p of group g16 reads
-    // row 4*g16 + q (and 16 + ...), columns 4p..4p+3 of each 16-wide d block
-    const uint16_t* tr0 = vw + (4 * g16 + (c >> 2)) * VROW + 4 * (c & 3);
-    const uint16_t* tr1 = tr0 + 16 * VROW;
+    // row 4*g16 + q (and 16 + ...), columns 4p..4p+3 of each 16-wide d block,
+    // through the row's swizzle (vswz)
+    const int trow = 4 * g16 + (c >> 2), tsw = vswz<D>(trow);
+    const uint16_t* tr0 = vw + trow * D + 4 * ((c & 3) ^ (tsw & 3));
+    const int trk = tsw >> 2;
     for (int item = blockIdx.x * NW + wave; item < total; item += gridDim.x * NW) {
         // split-major: consecutive waves take different rows' splits, so the
         // persistent grid's first pass covers every row
@@ -615,7 +640,7 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
         load_kv_tile<D, KV8>(kb, vb, start, end, lane, ta);
         for (int t = 0; t < ntiles; ++t) {
             const int kt = start + 32 * t;
-            attn_tile_mfma<D, KV8>(ta, t + 1 < ntiles, kt + 32, kb, vb, kt, end, lane, g16, vw, tr0, tr1, qf, m, l,
+            attn_tile_mfma<D, KV8>(ta, t + 1 < ntiles, kt + 32, kb, vb, kt, end, lane, g16, vw, tr0, trk, qf, m, l,
                                    acc, scale_log2);
         }
         l += __shfl_xor(l, 16, kWave);

@@ -40,9 +40,11 @@ def lib() -> ctypes.CDLL:
     with _lock:
         if _lib is not None:
             return _lib
-        path = TARGET
+        # DMCP_HIPOPS_SO: another build of the same ABI (bench A/B of a kernel
+        # change, scripts/hipops_ab.sh); the in-tree library otherwise
+        path = os.environ.get("DMCP_HIPOPS_SO") or TARGET
         if not os.path.exists(path):
-            if os.environ.get("DMCP_NO_AUTOBUILD"):
+            if os.environ.get("DMCP_NO_AUTOBUILD") or path != TARGET:
                 raise HipOpsError(f"HIP kernel library missing: {path}")
             path = build()
         L = ctypes.CDLL(path)
@@ -78,7 +80,7 @@ def lib() -> ctypes.CDLL:
 
 
 def loaded_path() -> Optional[str]:
-    return TARGET if _lib is not None else None
+    return (os.environ.get("DMCP_HIPOPS_SO") or TARGET) if _lib is not None else None
 
 
 def _stream() -> ctypes.c_void_p:

@@ -8,9 +8,10 @@ ROOT=$(pwd)
 export TMPDIR=/tmp
 cd /tmp
 i=0
-for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS" \
-           "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES" \
-           "FETCH_SIZE SQ_INSTS_VMEM_RD"; do
+SETS=${PMC_SETS:-"SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS;SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES;FETCH_SIZE SQ_INSTS_VMEM_RD"}
+rm -rf "$ROOT"/gpurun_out/pmcd*
+IFS=';' read -ra SETL <<< "$SETS"
+for set in "${SETL[@]}"; do
     i=$((i + 1))
     timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d "$ROOT/gpurun_out/pmcd$i" -o p \
         -- python3 "$ROOT/scripts/bench_step.py" --iters 20 "$@" > "$ROOT/gpurun_out/pmcd$i.log" 2>&1 || exit $?
@@ -22,8 +23,10 @@ calls = collections.Counter()
 for f in glob.glob(sys.argv[1] + "/pmcd*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = r.get("Kernel_Name", "?")
-        k = ("prefix" if "prefix_attn" in k else "decode_mfma" if "decode_attn_mfma" in k else
-             "combine" if "combine" in k else "gemm" if "Cijk" in k else "rmsnorm" if "rmsnorm" in k else "other")
+        k = ("prefix" if "prefill_attn" in k else "decode_mfma" if "decode_attn_mfma" in k else
+             "combine" if "combine" in k else "gemm_lib" if "Cijk" in k else "rmsnorm" if "rmsnorm" in k else
+             "wgemm_swiglu" if "wgemm_kernel<128" in k else "wgemm" if "wgemm_kernel" in k else
+             "reduce" if "reduce_" in k else "other")
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
 for k, d in sorted(agg.items()):
     print(k, {c: f"{v:.3g}" for c, v in sorted(d.items())})

@@ -41,9 +41,6 @@ class GitClient:
         self.timeout = timeout_seconds
         self.read_local_in_place = True  # snapshot(): local repositories without a private clone
         self.native_objects = True  # snapshot(): ref + tree read from loose objects natively when possible
-        # ... and the blobs inflated by the scan itself (LooseTree, DMCP_LAZY_BLOBS=1): measured even with
-        # the two-pass read (profiles/bench_r2_lazy_ab.txt), so off by default
-        self.lazy_blobs = os.environ.get("DMCP_LAZY_BLOBS", "0") == "1"
 
     def _env(self) -> dict:
         env = dict(os.environ)
@@ -162,20 +159,12 @@ class GitClient:
         """A local repository's objects are read in place: content-addressed
         objects never change, so a private clone adds nothing but a process
         and a ref copy.  The tree does not own (and never deletes) ``source``."""
-        from .source import (CheckoutTree, LooseTree, MemoryTree, _object_dirs, list_tree, native_commit_tree,
-                             read_blobs, wanted)
+        from .source import CheckoutTree, MemoryTree, list_tree, native_commit_tree, read_blobs, wanted
         LOG.info("Reading %s (branch: %s) in place", url, branch)
         try:
             fast = native_commit_tree(source, self.branch_refs(branch)) if self.native_objects else None
             if fast is not None:
                 commit, listing = fast
-                if self.lazy_blobs:
-                    # blobs inflated later by the scan workers that analyse them
-                    def fallback():
-                        c = self.clone(url, branch, shallow=shallow)
-                        return CheckoutTree(c.directory, c.commit_hash)
-                    return LooseTree(source, commit, [e for e in listing if wanted(e[0])], _object_dirs(source),
-                                     self, max_bytes, fallback)
             else:
                 commit = self.resolve_commit(source, branch)
                 listing = list_tree(self, source, commit)

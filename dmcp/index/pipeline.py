@@ -147,10 +147,6 @@ class Indexer:
     ROW_CHUNK = 256  # classes (with their methods) per writer put in Phase 1
     native_phase1 = True  # Phase 1 rows built by the native writer when it can (else the Python loop)
     phase1_ids: Optional[List[str]] = None  # row ids for the native Phase 1 (None = fresh UUIDv7s; tests)
-    # the snapshot read overlaps the project-row preparation (DMCP_OVERLAP_FETCH=0 for A/B)
-    overlap_fetch = os.environ.get("DMCP_OVERLAP_FETCH", "1") != "0"
-    # the native scan writes the class / method rows itself (DMCP_SCAN_ROWS=0 for A/B)
-    scan_rows = os.environ.get("DMCP_SCAN_ROWS", "1") != "0"
 
     def __init__(self, repos: Repositories, cache: GraphCache, git: GitClient,
                  backend: Optional[EnrichmentBackend] = None, *, batch_size: int = 20,
@@ -198,16 +194,7 @@ class Indexer:
         writer: Optional[ProjectRowsWriter] = None
         # the snapshot is read (natively, mostly without the GIL) on a helper
         # thread while the project row is looked up and marked ANALYZING
-        if self.overlap_fetch:
-            fetch = self._submit_io(self._timed_fetch, url, branch_name)
-        else:
-            from concurrent.futures import Future
-            fetch = Future()
-            fetch.set_running_or_notify_cancel()
-            try:
-                fetch.set_result(self._timed_fetch(url, branch_name))
-            except Exception as e:
-                fetch.set_exception(e)
+        fetch = self._submit_io(self._timed_fetch, url, branch_name)
         try:
             with span("analyze.prepare", stats):
                 project, lease = self._prepare_project(url, branch_name)
@@ -234,7 +221,7 @@ class Indexer:
                 # the native scan hands the class / method rows to the writer
                 # as soon as it has them (fresh UUIDv7s; not with given test ids)
                 rows = (writer.static_rows(now, clone.commit_hash)
-                        if self.scan_rows and self.native_phase1 and self.phase1_ids is None
+                        if self.native_phase1 and self.phase1_ids is None
                         and not self._isolate(url) else None)
                 with span("analyze.parse", stats):
                     parsed = self._scan(parser, clone, url, rows=rows)

@@ -186,102 +186,6 @@ class _Budget:
             return not self.exceeded
 
 
-class LooseTree(MemoryTree):
-    """A commit of a local, mostly-loose repository read lazily: the blobs are
-    inflated by the native scan's own workers, each by the worker that
-    analyses it (``_srcscan.scan_snapshot``: inflation and analysis in one
-    parallel pass instead of two), the remaining files (README, manifests)
-    right after.  Before a scan, single files are inflated on demand; a
-    request for all of :attr:`files` reads them the :class:`MemoryTree` way.
-    Past ``max_bytes`` of content the tree switches to a checkout
-    (``fallback()``), as :meth:`GitClient.snapshot` does up front."""
-
-    def __init__(self, git_dir: str, commit_hash: str, entries: List[Tuple[str, str]], object_dirs: List[str],
-                 git, max_bytes: int, fallback) -> None:
-        super().__init__(git_dir, commit_hash, None, owned=False)  # type: ignore[arg-type]
-        self._entries = entries
-        self._sha = dict(entries)
-        self._object_dirs = object_dirs
-        self._git = git
-        self._max_bytes = max_bytes
-        self._fallback = fallback
-        self._checkout: Optional[CheckoutTree] = None
-
-    @property  # type: ignore[override]
-    def files(self) -> Dict[str, bytes]:
-        if self._files is None:
-            self._load_all()
-        return self._files
-
-    @files.setter
-    def files(self, value) -> None:
-        self._files = value
-
-    def _to_checkout(self) -> None:
-        LOG.info("%s: sources exceed the %d MiB in-memory limit, using a checkout", self.git_dir,
-                 self._max_bytes >> 20)
-        self._checkout = self._fallback()
-        self.directory = self._checkout.directory
-        self.commit_hash = self._checkout.commit_hash
-        self._files = {}
-
-    def _load_all(self) -> None:
-        blobs = read_blobs(self._git, self.git_dir, [sha for _, sha in self._entries], self._max_bytes)
-        if blobs is None:
-            self._to_checkout()
-            return
-        self._files = {p: b for (p, _), b in zip(self._entries, blobs)}
-
-    def read_bytes(self, rel: str) -> Optional[bytes]:
-        if self._checkout is not None:
-            return self._checkout.read_bytes(rel)
-        if self._files is not None:
-            return self._files.get(rel.replace(os.sep, "/"))
-        sha = self._sha.get(rel.replace(os.sep, "/"))
-        if sha is None:
-            return None
-        got = read_blobs(self._git, self.git_dir, [sha])
-        return got[0] if got else None
-
-    def detect_language(self) -> str:
-        if self._checkout is not None:
-            return self._checkout.detect_language()
-        return detect_language_from(self._sha)
-
-    def scan(self, language: str, threads: int, framework: str = "") -> bytes:
-        if self._checkout is None and self._files is None:
-            self._load_all()
-        if self._checkout is not None:
-            return self._checkout.scan(language, threads, framework)
-        return super().scan(language, threads, framework)
-
-    def scan_objects(self, language: str, threads: int, framework: str = "", rows=None) -> Optional[dict]:
-        if self._checkout is not None:
-            return self._checkout.scan_objects(language, threads, framework)
-        if self._files is None:
-            from ..models.domain import StaticMethodInfo
-            from ..parsers.base import native
-            fn = getattr(native(), "scan_snapshot", None)
-            if fn is not None:
-                r = fn(self._object_dirs, self._entries, language, threads, framework, StaticMethodInfo,
-                       self._max_bytes)
-                if r == "exceeded":
-                    self._to_checkout()
-                    return self._checkout.scan_objects(language, threads, framework)
-                if r is not None:
-                    blobs, doc = r
-                    self._files = {p: b for (p, _), b in zip(self._entries, blobs)}
-                    return doc
-            self._load_all()  # something is not loose: the two-pass way
-            if self._checkout is not None:
-                return self._checkout.scan_objects(language, threads, framework)
-        return super().scan_objects(language, threads, framework)
-
-    def cleanup(self) -> None:
-        if self._checkout is not None:
-            self._checkout.cleanup()
-
-
 def _object_dirs(git_dir: str) -> List[str]:
     own = os.path.join(git_dir, "objects")
     if not os.path.isdir(own):

@@ -31,8 +31,7 @@ MI355X mapping:
 * prefill / extend attention runs on the MFMA flash kernel
   (``csrc/prefill_attn.hip``): the shared prompt prefix is read in place
   from its cache slot (a fork costs no copy), causal masking of the own
-  keys; PyTorch SDPA only where the kernel's head shapes do not apply
-  (``DMCP_PREFILL_KERNEL=0`` forces it);
+  keys; PyTorch SDPA only where the kernel's head shapes do not apply;
 * the KV cache is one preallocated slab ``[layers, slots, Hkv, max_seq, D]``
   in bf16 or FP8 e4m3 (``LMConfig.kv_dtype``; 288 GB of HBM per GPU: no
   paging needed at these sizes) so decode reads every key row of a
@@ -220,12 +219,10 @@ class LocalLM:
         self.prefix_tokens: tuple = ()
         self.prefix_dev = torch.zeros(1, dtype=torch.int32, device=self.device)
         # fused decode GEMMs for steps of <= fused_max_rows rows (GPU only;
-        # DMCP_FUSED_GEMM=0 forces the hipBLASLt path)
-        self.use_fused = (self.device.type == "cuda" and os.environ.get("DMCP_FUSED_GEMM", "1") != "0"
-                          and fused_shapes_ok(c))
-        # prefill / extend attention on the MFMA kernel (csrc/prefill_attn.hip);
-        # DMCP_PREFILL_KERNEL=0 forces the SDPA path
-        self.use_prefill_kernel = (self.device.type == "cuda" and os.environ.get("DMCP_PREFILL_KERNEL", "1") != "0"
+        # the attribute is cleared by tests to compare against hipBLASLt)
+        self.use_fused = self.device.type == "cuda" and fused_shapes_ok(c)
+        # prefill / extend attention on the MFMA kernel (csrc/prefill_attn.hip)
+        self.use_prefill_kernel = (self.device.type == "cuda"
                                    and ops.prefill_supported(c.n_heads, c.n_kv_heads, c.head_dim))
         # slot -> shared-prefix length its prefill reads in place from the
         # prefix slot (fork_prefix without a copy; prefill kernel only)
@@ -233,7 +230,7 @@ class LocalLM:
         # crossover with the hipBLASLt + split-K-down path measured at ~20 rows
         # (fp8: fused 1.47 vs 1.64 ms at 16 rows, 1.80 vs 1.70 at 24, 1.82 vs
         # 1.73 at 32 -- profiles/decode_fused_rows_r2.txt)
-        self.fused_max_rows = min(ops.FUSED_MAX_ROWS, int(os.environ.get("DMCP_FUSED_MAX_ROWS", "16")))
+        self.fused_max_rows = min(ops.FUSED_MAX_ROWS, 16)
         ps = ops.PREFIX_MFMA_MAX_SPLITS if shared_prefix else 0
         self.attn_ws = (ops.decode_workspace(self.max_rows, c.n_heads, c.n_kv_heads, c.head_dim, c.max_seq,
                                              self.device, prefix_slots=ps) if self.device.type == "cuda" else None)
@@ -241,8 +238,7 @@ class LocalLM:
         # weight-streaming GEMM (csrc/wgemm.hip) with its neighbour op in the
         # epilogue / reduction -- QKV + RoPE + KV append, O + residual + norm,
         # gate/up + SwiGLU, down + residual + next norm
-        self.use_wgemm = (self.device.type == "cuda" and wgemm_shapes_ok(c)
-                          and os.environ.get("DMCP_WGEMM", "1") != "0")
+        self.use_wgemm = self.device.type == "cuda" and wgemm_shapes_ok(c)
         self.wgemm_ws = (ops.wgemm_workspace(min(self.max_rows, ops.WGEMM_MAX_ROWS), max(c.qkv_dim, c.hidden),
                                              self.device) if self.use_wgemm else None)
 

@@ -204,7 +204,6 @@ def decode_plan(rows: int, n_kv_heads: int, max_seq: int, target_waves: int = 40
     chunks plus a short remainder that left most waves idle at the end
     (measured: 1024-key chunks reached 42 % of the copy rate at B = 78,
     L = 2,500 -- profiles/decode_step_r2*)."""
-    target_waves = int(os.environ.get("DMCP_DECODE_TARGET_WAVES", target_waves))
     splits = max(1, -(-target_waves // max(1, rows * n_kv_heads)))
     return min_chunk, min(splits, decode_splits(max_seq, min_chunk))
 

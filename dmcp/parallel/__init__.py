@@ -3,8 +3,8 @@
 * :mod:`.dist` -- one-process-per-GPU ``torch.distributed`` plumbing (RCCL on
   ROCm, gloo on CPU): rank discovery, barriers, MAX/SUM reductions, used by
   the benchmarks;
-* :mod:`.replicas` -- data-parallel pool of local-LLM engines (one replica per
-  GPU, work-stealing over classes; no collectives in the hot path);
+* one local-LLM worker process per GPU lives in :mod:`dmcp.enrich.workers`
+  (data-parallel over classes from one queue; no collectives in the hot path);
 * :mod:`.bulk` -- bulk repository indexing across worker processes (the
   reference's sequential ``scripts/analyze-repos.sh``).
 """

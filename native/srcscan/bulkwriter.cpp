@@ -130,15 +130,6 @@ void BulkWriter::run() {
         c.exec("PRAGMA temp_store = MEMORY");
         c.exec("PRAGMA cache_size = -65536");
         c.exec("PRAGMA foreign_keys = OFF");
-        // a fresh connection starts with a cold page cache: the old rows'
-        // pages (deletes) and the B-tree interiors (inserts) are read from
-        // the database file memory-mapped instead of one pread per page
-        // when DMCP_SQLITE_MMAP (bytes) is set; off by default until measured
-        {
-            const char* e = std::getenv("DMCP_SQLITE_MMAP");
-            const long long mm = e ? std::atoll(e) : 0;
-            if (mm > 0) c.exec(("PRAGMA mmap_size = " + std::to_string(mm)).c_str());
-        }
         using clock = std::chrono::steady_clock;
         auto ms = [](clock::time_point a, clock::time_point b) {
             return std::chrono::duration<double, std::milli>(b - a).count();

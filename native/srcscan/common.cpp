@@ -468,11 +468,7 @@ void parallel_for(size_t n, int threads, const std::function<void(size_t)>& fn) 
         for (size_t i = 0; i < n; ++i) fn(i);
         return;
     }
-    static const bool use_pool = [] {
-        const char* e = std::getenv("DMCP_NATIVE_POOL");  // "0": spawn threads per call (A/B)
-        return !(e && e[0] == '0');
-    }();
-    if (use_pool && t <= 64 && WorkerPool::get().run(n, t, fn)) return;
+    if (t <= 64 && WorkerPool::get().run(n, t, fn)) return;
     std::atomic<size_t> next{0};
     std::vector<std::thread> pool;
     pool.reserve(t);
@@ -493,35 +489,17 @@ namespace {
 
 constexpr std::string_view kVfsPrefix = "/__vfs__/";
 
-// A mounted file: its content (a view), or a loose git blob inflated on its
-// first read (vfs_mount_loose) by whichever scan worker reads it.
+// A mounted file: a view of its content.
 struct VEntry {
     std::string_view data;
-    std::string sha;    // lazy entries only
-    std::string owned;  // lazy: the inflated content
-    std::once_flag once;
-    bool ok = true;
 };
 
 struct VirtualTree {
     std::vector<std::string> owned;        // contents copied in (vfs_mount)
-    std::vector<std::string> object_dirs;  // lazy entries' object stores
     std::deque<VEntry> entries;            // mount order; stable addresses
     std::unordered_map<std::string, VEntry*> files;  // rel path -> entry
     std::unordered_map<std::string, std::vector<std::pair<std::string, bool>>> dirs;  // rel dir -> children
 };
-
-// content of `e` (inflating a lazy entry once); null when unreadable
-const std::string_view* entry_data(const VirtualTree& t, VEntry& e) {
-    if (!e.sha.empty()) {
-        std::call_once(e.once, [&] {
-            e.ok = gitobj::read_loose_blob(t.object_dirs, e.sha, e.owned);
-            if (e.ok) e.data = e.owned;
-        });
-        if (!e.ok) return nullptr;
-    }
-    return &e.data;
-}
 
 std::mutex g_vfs_mu;
 std::unordered_map<std::string, std::shared_ptr<const VirtualTree>> g_vfs;  // root -> tree
@@ -543,9 +521,8 @@ std::shared_ptr<const VirtualTree> vfs_resolve(const std::string& path, std::str
 
 namespace {
 
-// files: (path, content) -- or (path, loose blob id) when `lazy`
-std::string mount_tree(std::shared_ptr<VirtualTree> tree, const std::vector<std::pair<std::string, std::string_view>>& files,
-                       bool lazy = false) {
+// files: (path, content)
+std::string mount_tree(std::shared_ptr<VirtualTree> tree, const std::vector<std::pair<std::string, std::string_view>>& files) {
     std::unordered_map<std::string, std::unordered_map<std::string, bool>> kids;  // dir -> name -> is_dir
     kids[""];
     tree->files.reserve(files.size());
@@ -575,10 +552,7 @@ std::string mount_tree(std::shared_ptr<VirtualTree> tree, const std::vector<std:
         }
         siblings->emplace(std::string(rel.substr(slash == std::string_view::npos ? 0 : slash + 1)), false);
         VEntry& e = tree->entries.emplace_back();
-        if (lazy)
-            e.sha.assign(kv.second);
-        else
-            e.data = kv.second;
+        e.data = kv.second;
         tree->files[std::string(rel)] = &e;
     }
     for (auto& d : kids) {
@@ -610,50 +584,6 @@ std::string vfs_mount(std::vector<std::pair<std::string, std::string>>&& files) 
 
 std::string vfs_mount_views(const std::vector<std::pair<std::string, std::string_view>>& files) {
     return mount_tree(std::make_shared<VirtualTree>(), files);
-}
-
-std::string vfs_mount_loose(const std::vector<std::pair<std::string, std::string_view>>& entries,
-                            const std::vector<std::string>& object_dirs) {
-    auto tree = std::make_shared<VirtualTree>();
-    tree->object_dirs = object_dirs;
-    return mount_tree(std::move(tree), entries, true);
-}
-
-bool vfs_collect(const std::string& root, int threads, uint64_t max_bytes, std::vector<std::string>& out,
-                 bool& exceeded) {
-    std::string rel;
-    auto t = vfs_resolve(root, rel);
-    exceeded = false;
-    if (!t) return false;
-    auto& tree = const_cast<VirtualTree&>(*t);
-    const size_t n = tree.entries.size();
-    std::vector<VEntry*> es;
-    es.reserve(n);
-    for (auto& e : tree.entries) es.push_back(&e);
-    std::atomic<bool> failed{false};
-    std::atomic<uint64_t> total{0};
-    parallel_for(n, threads, [&](size_t i) {
-        if (failed.load(std::memory_order_relaxed)) return;
-        const std::string_view* d = entry_data(tree, *es[i]);
-        if (!d) {
-            failed.store(true, std::memory_order_relaxed);
-            return;
-        }
-        if (max_bytes && total.fetch_add(d->size(), std::memory_order_relaxed) + d->size() > max_bytes)
-            failed.store(true, std::memory_order_relaxed);
-    });
-    if (failed.load()) {
-        exceeded = max_bytes && total.load() > max_bytes;
-        return false;
-    }
-    out.resize(n);
-    for (size_t i = 0; i < n; ++i) {
-        VEntry& e = *es[i];
-        if (!e.sha.empty()) out[i] = std::move(e.owned);  // the tree is unmounted after this
-        else out[i].assign(e.data.data(), e.data.size());
-        e.data = std::string_view();
-    }
-    return true;
 }
 
 void vfs_unmount(const std::string& root) {
@@ -692,8 +622,8 @@ bool read_file(const std::string& path, std::string& out, size_t max_bytes) {
     if (auto t = vfs_resolve(path, rel)) {
         auto it = t->files.find(rel);
         if (it == t->files.end()) return false;
-        const std::string_view* d = entry_data(*t, *it->second);
-        if (!d || (max_bytes && d->size() > max_bytes)) return false;
+        const std::string_view* d = &it->second->data;
+        if (max_bytes && d->size() > max_bytes) return false;
         out.assign(d->data(), d->size());
         return true;
     }

@@ -132,15 +132,6 @@ bool list_dir(const std::string& dir, std::vector<std::pair<std::string, bool>>&
 std::string vfs_mount(std::vector<std::pair<std::string, std::string>>&& files);
 // The same without copying: the contents must outlive vfs_unmount().
 std::string vfs_mount_views(const std::vector<std::pair<std::string, std::string_view>>& files);
-// (path, loose blob id) entries, each inflated from `object_dirs` on its first
-// read (by the scan worker that reads it).
-std::string vfs_mount_loose(const std::vector<std::pair<std::string, std::string_view>>& entries,
-                            const std::vector<std::string>& object_dirs);
-// Every entry's content in mount order (unread lazy entries inflated on
-// `threads` workers) moved into `out`; false when one is unreadable or the
-// total passes max_bytes (> 0; `exceeded` set).  Call just before unmounting.
-bool vfs_collect(const std::string& root, int threads, uint64_t max_bytes, std::vector<std::string>& out,
-                 bool& exceeded);
 void vfs_unmount(const std::string& root);
 std::string join_path(const std::string& a, const std::string& b);
 std::string normalize_path(const std::string& p);  // resolves . and .. lexically

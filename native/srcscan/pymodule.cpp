@@ -956,67 +956,6 @@ PYBIND11_MODULE(_srcscan, m) {
         "scan_sources as Python objects (files as tuples, methods as method_cls) -- no JSON round trip; "
         "with rows, the class / method rows are written first (ids in 'rowIds')");
     m.def(
-        "scan_snapshot",
-        [](const std::vector<std::string>& object_dirs, py::list entries, const std::string& language, int threads,
-           const std::string& framework, py::handle method_cls, uint64_t max_bytes) -> py::object {
-            // (path, loose blob id) entries: each blob is inflated by the scan
-            // worker that first reads it (inflation and analysis in one
-            // parallel pass), the rest (README, manifests, other languages)
-            // afterwards; returns (contents as bytes in entry order, scan
-            // objects), "exceeded" past max_bytes, or None when an object is
-            // not loose (the caller reads through git)
-            std::vector<std::pair<std::string, std::string>> owned;
-            owned.reserve(entries.size());
-            for (auto item : entries) {
-                auto tup = item.cast<py::tuple>();
-                owned.emplace_back(tup[0].cast<std::string>(), tup[1].cast<std::string>());
-            }
-            std::vector<std::pair<std::string, std::string_view>> views;
-            views.reserve(owned.size());
-            for (auto& kv : owned) views.emplace_back(kv.first, kv.second);
-            std::unique_ptr<srcscan::ScanResult> r;
-            std::vector<std::string> contents;
-            bool ok = false, exceeded = false;
-            {
-                py::gil_scoped_release release;
-                const auto t = std::chrono::steady_clock::now();
-                std::string root = srcscan::vfs_mount_loose(views, object_dirs);
-                const long long mount_us =
-                    std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t).count();
-                srcscan::ScanOptions opt;
-                opt.language = language;
-                opt.threads = threads;
-                opt.framework = framework;
-                try {
-                    r = std::make_unique<srcscan::ScanResult>(srcscan::scan_project(root, opt));
-                    r->mount_us = mount_us;
-                    ok = srcscan::vfs_collect(root, threads, max_bytes, contents, exceeded);
-                } catch (...) {
-                    srcscan::vfs_unmount(root);
-                    throw;
-                }
-                srcscan::vfs_unmount(root);
-            }
-            if (!ok) {
-                std::thread([](std::unique_ptr<srcscan::ScanResult>) {}, std::move(r)).detach();
-                return exceeded ? py::object(py::str("exceeded")) : py::object(py::none());
-            }
-            py::list blobs(contents.size());
-            for (size_t i = 0; i < contents.size(); ++i) {
-                blobs[i] = py::bytes(contents[i]);
-                std::string().swap(contents[i]);
-            }
-            const auto t = std::chrono::steady_clock::now();
-            py::dict d = scan_result_objects(*r, method_cls);
-            py::dict(d["stats"])["phaseUs"].cast<py::dict>()["objects"] =
-                std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t).count();
-            std::thread([](std::unique_ptr<srcscan::ScanResult>) {}, std::move(r)).detach();
-            return py::make_tuple(blobs, d);
-        },
-        py::arg("object_dirs"), py::arg("entries"), py::arg("language"), py::arg("threads"), py::arg("framework"),
-        py::arg("method_cls"), py::arg("max_bytes") = 0,
-        "Scan of a commit's loose blobs, inflated by the scan workers; (contents, scan objects) | 'exceeded' | None");
-    m.def(
         "scan_file",
         [](const std::string& path, const std::string& language, const std::string& rel, const std::string& fw) {
             std::string out;

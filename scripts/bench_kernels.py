@@ -79,7 +79,7 @@ def bench_decode_attention(B, L, Hq=32, Hkv=8, D=64, max_seq=4096, chunk=256, ea
            chunk=chunk)
 
 
-def bench_prefix_attention(B, P, Ls, Hq=32, Hkv=8, D=64, max_seq=8192, chunk=1024, pchunk=256):
+def bench_prefix_attention(B, P, Ls, Hq=32, Hkv=8, D=64, max_seq=8192, chunk=256):
     """Shared-prefix decode step: every row = P shared keys + Ls own keys.
     Bytes counted = what must be read at least once (prefix once, own keys
     per row); 'rowwise_us' = the same step without the prefix kernel (every
@@ -89,13 +89,12 @@ def bench_prefix_attention(B, P, Ls, Hq=32, Hkv=8, D=64, max_seq=8192, chunk=102
     S = B + 1
     kc = torch.randn(S, Hkv, max_seq, D, device=dev).to(torch.bfloat16)
     vc = torch.randn(S, Hkv, max_seq, D, device=dev).to(torch.bfloat16)
-    vt = vc[B].transpose(-1, -2).contiguous()
     q = torch.randn(B, Hq, D, device=dev).to(torch.bfloat16)
     slot = torch.arange(B, dtype=torch.int32, device=dev)
     sl = torch.full((B,), P + Ls, dtype=torch.int32, device=dev)
     plen = torch.tensor([P], dtype=torch.int32, device=dev)
-    pre = SharedPrefix(kc[B], vt, plen, pchunk)
-    ws = hip.decode_workspace(B, Hq, Hkv, D, max_seq, dev, chunk, hip.prefix_splits(max_seq, pchunk))
+    pre = SharedPrefix(kc[B], vc[B], plen)
+    ws = hip.decode_workspace(B, Hq, Hkv, D, max_seq, dev, chunk, hip.PREFIX_MFMA_MAX_SPLITS)
     out = torch.empty_like(q)
     t = timed(lambda: hip.decode_attention(q, kc, vc, slot, sl, 1 / math.sqrt(D), workspace=ws, chunk=chunk,
                                            out=out, prefix=pre))
@@ -104,7 +103,7 @@ def bench_prefix_attention(B, P, Ls, Hq=32, Hkv=8, D=64, max_seq=8192, chunk=102
     nbytes = 2 * Hkv * D * 2 * (P + B * Ls) + 2 * q.numel() * 2
     out_rec = {"rowwise_us": round(rowwise * 1e6, 2), "speedup_vs_rowwise": round(rowwise / t, 2)}
     report("decode_attention_shared_prefix", t, nbytes, None, B=B, P=P, Ls=Ls, Hq=Hq, Hkv=Hkv, D=D, chunk=chunk,
-           pchunk=pchunk, **out_rec)
+           **out_rec)
 
 
 def bench_rmsnorm(rows, H=2048):

@@ -1,13 +1,16 @@
 #!/usr/bin/env bash
-# One GPU session on the MI355X box: tests, smoke, benches, rocprofv3 profile.
-# Every GPU step has its own time limit; a crash / abort / timeout ends the
-# script (ordinary test failures do not).  Output goes to gpurun_out/.
+# One GPU session on the MI355X box: GPU tests, smoke, bench.py (with
+# extra.enrichLocal), bench_enrich (fp8 / bf16 KV), batched prefill, decode
+# step at 320 / 78 rows and its rocprofv3 kernel stats.  Every GPU step has its
+# own time limit; a crash / abort / timeout ends the script (ordinary test
+# failures do not).  Output goes to gpurun_out/round/.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out
+ROOT=$(pwd)
+OUT=gpurun_out/round
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-STEPS="${STEPS:-pytest smoke bench enrich prof}"
+STEPS="${STEPS:-pytest smoke bench enrich_fp8 enrich_bf16 prefill step prof}"
 
 run() {  # name seconds cmd...
     local name=$1 secs=$2
@@ -16,7 +19,7 @@ run() {  # name seconds cmd...
     timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
     local rc=$?
     echo "=== $name rc=$rc"
-    tail -n 5 "$OUT/$name.log"
+    tail -n 3 "$OUT/$name.log"
     case $rc in
         0|1|5) return 0 ;;                 # ok / test failures / no tests collected
         *) echo "fatal rc=$rc in $name: stopping"; exit $rc ;;
@@ -25,23 +28,24 @@ run() {  # name seconds cmd...
 
 for s in $STEPS; do
     case $s in
-        pytest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:randomly ;;
-        smoke) run smoke 600 python __graft_entry__.py smoke ;;
-        bench) run bench 600 python bench.py --steps 5 --warmup 2 ;;
-        enrich) run bench_enrich 900 python bench_enrich.py --classes 256 --batch 64 ;;
-        enrich_nojump) run bench_enrich_nojump 900 python bench_enrich.py --classes 256 --batch 64 --no-jump ;;
-        enrich_noprefix) run bench_enrich_noprefix 900 python bench_enrich.py --classes 256 --batch 64 --no-shared-prefix ;;
-        kernels) run kernels 600 python scripts/bench_kernels.py ;;
+        pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+        smoke) run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        bench) run bench 900 python bench.py --steps 20 --warmup 5 ;;
+        enrich_fp8) run enrich_fp8 900 python bench_enrich.py --kv-dtype fp8 ;;
+        enrich_bf16) run enrich_bf16 900 python bench_enrich.py --kv-dtype bf16 ;;
+        prefill) run prefill 300 python scripts/bench_prefill.py --seqs 12 ;;
+        step)
+            run step320 300 python scripts/bench_step.py --batch 256 --extra 64 --kv-dtype fp8 --iters 100
+            run step78 300 python scripts/bench_step.py --batch 64 --extra 14 --kv-dtype fp8 --iters 100 ;;
         prof)
-            ROOT=$(pwd)
-            ( cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv \
-                -d "$ROOT/$OUT/prof" -o enrich \
-                -- python3 "$ROOT/bench_enrich.py" --classes 64 --batch 64 > "$ROOT/$OUT/prof.log" 2>&1 )
+            ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$ROOT/$OUT/prof" -o step -- python3 "$ROOT/scripts/bench_step.py" --batch 256 --extra 64 \
+                --kv-dtype fp8 --iters 50 > "$ROOT/$OUT/prof.log" 2>&1 )
             rc=$?
-            echo "=== prof rc=$rc"; tail -n 5 "$OUT/prof.log"
-            # keep only the summaries (the raw trace can exceed the 64 MiB copy-back limit)
-            find "$OUT/prof" -type f ! -name '*stats*' -delete 2>/dev/null
-            find "$OUT/prof" -name '*kernel_stats.csv' -exec head -n 40 {} \; 2>/dev/null
+            echo "=== prof rc=$rc"
+            find "$OUT/prof" -type f ! -name '*kernel_stats*' -delete 2>/dev/null
+            python3 scripts/kstats.py $(find "$OUT/prof" -name '*kernel_stats.csv' | head -1) > "$OUT/kstats.txt" 2>&1
+            head -25 "$OUT/kstats.txt"
             [ $rc -eq 0 ] || exit $rc ;;
     esac
 done

@@ -1,11 +1,10 @@
-"""dmcp.parallel: distributed context (gloo, 2 ranks), replica pool
-work-stealing / failure isolation, bulk indexing (in-process and worker
-processes), plus ProjectService and project deletion."""
+"""dmcp.parallel: distributed context (gloo, 2 ranks), bulk indexing
+(in-process and worker processes), plus ProjectService and project deletion.
+(The one-process-per-GPU enrichment workers: tests/test_workers.py.)"""
 import json
 import os
 import socket
 import threading
-import time
 
 import pytest
 import torch.multiprocessing as mp
@@ -13,7 +12,6 @@ import torch.multiprocessing as mp
 from conftest import make_app
 from dmcp.parallel.bulk import BulkItem, bulk_analyze, parse_repo_list
 from dmcp.parallel.dist import init_from_env
-from dmcp.parallel.replicas import ReplicaPool
 from dmcp.utils import synth
 from dmcp.utils.errors import DomainError
 
@@ -60,35 +58,6 @@ def test_dist_context_two_ranks_gloo():
         assert p.exitcode == 0
     for rank, mx, sm, objs in got:
         assert mx == [2.0, 0.0] and sm == [3.0] and objs == [{"rank": 0}, {"rank": 1}]
-
-
-def test_replica_pool_work_stealing_and_order():
-    seen = {}
-
-    def fn(rep, items):
-        time.sleep(0.001 * rep)  # replica 0 is fastest
-        seen.setdefault(rep, []).extend(items)
-        return [x * 10 for x in items]
-
-    pool = ReplicaPool([0, 3, 6], chunk_for=lambda r: 4)
-    out = pool.map(fn, list(range(50)))
-    assert out == [x * 10 for x in range(50)]
-    assert sum(pool.stats.values()) == 50 and pool.stats[0] >= pool.stats[2]
-
-
-def test_replica_pool_isolates_failures():
-    def fn(rep, items):
-        if rep == "bad":
-            raise RuntimeError("device lost")
-        return [x + 1 for x in items]
-
-    pool = ReplicaPool(["good", "bad"], chunk_for=lambda r: 2)
-    out = pool.map(fn, list(range(10)), on_error=lambda i, e: f"err:{e}")
-    ok = [o for o in out if isinstance(o, int)]
-    errs = [o for o in out if isinstance(o, str)]
-    assert all(e == "err:device lost" for e in errs) and len(ok) + len(errs) == 10 and ok
-    with pytest.raises(ValueError):
-        ReplicaPool([])
 
 
 def test_parse_repo_list():

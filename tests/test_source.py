@@ -67,18 +67,8 @@ def test_snapshot_fallback_to_checkout_and_errors(tmp_path):
     repo = tmp_path / "r"
     synth.java_spring_repo(str(repo), 8)
     g = GitClient(str(tmp_path / "clones"))
-    g.lazy_blobs = False  # the size check up front
     t = g.snapshot(RepositoryUrl.of(str(repo)), "main", max_bytes=100)
     assert isinstance(t, CheckoutTree) and os.path.isfile(os.path.join(t.directory, "README.md"))
-    t.cleanup()
-    g.lazy_blobs = True  # a lazily read tree switches to a checkout when its scan passes the limit
-    from dmcp.index.source import LooseTree
-    t = g.snapshot(RepositoryUrl.of(str(repo)), "main", max_bytes=100)
-    assert isinstance(t, LooseTree) and t.directory is None
-    assert t.read_text("README.md")  # one file on demand, no limit involved
-    doc = t.scan_objects("java", 2)
-    assert t.directory and os.path.isfile(os.path.join(t.directory, "README.md"))
-    assert doc is None or doc["files"]  # the checkout answers (scan() when it has no object scan)
     assert json.loads(t.scan("java", 2))["files"]
     t.cleanup()
     assert not os.path.exists(t.directory)
@@ -299,31 +289,6 @@ def test_worker_pool_survives_fork():
     for t in ts:
         t.join(60)
     assert out == [64] * 6
-
-
-@pytest.mark.parametrize("kind", ["java", "nest", "go"])
-def test_loose_tree_fused_scan_equals_two_pass(tmp_path, kind):
-    """LooseTree's fused scan (blobs inflated by the scan workers) returns the
-    same document and the same file contents as reading every blob first."""
-    from dmcp.index.source import LooseTree
-    from dmcp.models.domain import StaticMethodInfo
-    repo = tmp_path / "r"
-    {"java": lambda: synth.java_spring_repo(str(repo), 30), "nest": lambda: synth.nestjs_repo(str(repo), 4),
-     "go": lambda: synth.go_gin_repo(str(repo), 3)}[kind]()
-    g = GitClient(str(tmp_path / "c"))
-    g.lazy_blobs = True
-    url = RepositoryUrl.of(str(repo))
-    lazy = g.snapshot(url, "main")
-    assert isinstance(lazy, LooseTree)
-    lang = lazy.detect_language()
-    doc = lazy.scan_objects(lang, 4)
-    g.lazy_blobs = False
-    eager = g.snapshot(url, "main")
-    assert not isinstance(eager, LooseTree) and lazy.files == eager.files
-    ref = native().scan_sources_objects(list(eager.files.items()), lang, 4, "", StaticMethodInfo)
-    for d in (doc, ref):
-        d["stats"] = None
-    assert doc == ref and doc["files"]
 
 
 def test_native_ref_reader_refuses_names_git_refuses(tmp_path):

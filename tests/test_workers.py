@@ -28,7 +28,10 @@ def _inputs(n):
 
 @pytest.fixture(scope="module")
 def pool():
-    p = GpuWorkerPool(["cpu", "cpu"], MODEL, engine={"use_graphs": False}, start_timeout_s=300)
+    # one OpenMP thread per worker: the tiny model needs no more, and spin-
+    # waiting OpenMP teams crawl when the test run shares the cores (xdist)
+    p = GpuWorkerPool(["cpu", "cpu"], MODEL, engine={"use_graphs": False}, start_timeout_s=300,
+                      env_extra={"OMP_NUM_THREADS": "1"})
     yield p
     p.close()
 
@@ -68,9 +71,10 @@ def test_killed_worker_is_isolated_and_replaced(pool):
     killed = False
     for i, r in be.enrich_stream(inputs, None):
         results[i] = r
-        if not killed:
+        if not killed and victim.inflight:
             os.kill(old_pid, signal.SIGKILL)  # mid-stream, while it holds classes
             killed = True
+    assert killed, "the victim never held classes when a reply arrived"
     assert sorted(results) == list(range(16))
     failed = [r for r in results.values() if not r.success]
     assert failed and all("worker died" in r.error_message for r in failed)

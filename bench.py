@@ -89,9 +89,19 @@ def _enrich_local(pool, args, ctx, work, rank):
     from dmcp.config import Config
     from dmcp.enrich.workers import ProcessLLMBackend
     from dmcp.utils import synth
+    # every collective below is entered by every rank, whatever fails where
+    # (a rank that raised before a barrier would leave the others waiting)
     t_init = time.perf_counter()
-    pool.init()
+    err = None
+    try:
+        if pool is None:
+            raise RuntimeError("no enrichment worker on this rank")
+        pool.init()
+    except Exception as e:
+        err = e
     init_s = time.perf_counter() - t_init
+    if ctx.sum(1.0 if err else 0.0)[0] > 0:
+        raise RuntimeError(f"enrichment worker init failed on some rank: {err!r}")
     be = ProcessLLMBackend(pool)
     cfg = Config(db_path=os.path.join(work, "enrich.db"), git_clone_base_path=os.path.join(work, "eclones"),
                  require_enrichment_for_analyze=True, recover_stuck_on_start=False)
@@ -100,7 +110,12 @@ def _enrich_local(pool, args, ctx, work, rank):
         warm = os.path.join(work, f"warm{rank}")
         synth.java_spring_repo(warm, n_classes=min(64, max(8, args.enrich_local_classes // 4)),
                                base_package=f"co.acme.warm{rank}", seed=rank + 101)
-        app.indexer.analyze_project(warm)
+        try:
+            app.indexer.analyze_project(warm)
+        except Exception as e:
+            err = e
+        if ctx.sum(1.0 if err else 0.0)[0] > 0:
+            raise RuntimeError(f"enrichLocal warm-up failed on some rank: {err!r}")
         repo = os.path.join(work, f"enrich{rank}")
         synth.java_spring_repo(repo, n_classes=args.enrich_local_classes, base_package=f"co.acme.enr{rank}",
                                seed=rank + 201)
@@ -108,11 +123,17 @@ def _enrich_local(pool, args, ctx, work, rank):
             w.stats = {}
         ctx.barrier()
         t0 = time.perf_counter()
-        r = app.indexer.analyze_project(repo)
+        try:
+            r = app.indexer.analyze_project(repo)
+        except Exception as e:
+            r, err = None, e
         elapsed = time.perf_counter() - t0
-        st = be.stats()
         mx = ctx.max(elapsed)[0]
-        tot = ctx.sum(float(r.stats.get("enriched", 0)), float(r.classes_analyzed))
+        bad = ctx.sum(1.0 if r is None else 0.0)[0]
+        tot = ctx.sum(float(r.stats.get("enriched", 0)) if r else 0.0, float(r.classes_analyzed) if r else 0.0)
+        if bad:
+            raise RuntimeError(f"enrichLocal analysis failed on {int(bad)} rank(s): {err!r}")
+        st = be.stats()
         steps = max(1.0, st.get("decode_steps", 0))
         return {"classesPerSec": round(tot[0] / mx, 2), "classesEnriched": int(tot[0]),
                 "classesAnalyzed": int(tot[1]), "elapsedS": round(mx, 3), "enrichFailed": r.stats.get("enrichFailed"),
@@ -198,7 +219,9 @@ def main(argv=None) -> int:
             extra["graphQueryMs"] = {"p50": round(lat[len(lat) // 2], 3), "p99": round(lat[int(len(lat) * 0.99) - 1], 3)}
             extra["stackTrace20Ms"] = {"p50": round(st_lat[len(st_lat) // 2], 3),
                                        "p99": round(st_lat[max(0, int(len(st_lat) * 0.99) - 1)], 3)}
-        if pool is not None:
+        # agreed by every rank: a rank without a worker skips the collective path for all
+        if args.enrich == "none" and args.enrich_local_classes > 0 and \
+                ctx.sum(1.0 if pool is not None else 0.0)[0] == world:
             try:
                 extra["enrichLocal"] = _enrich_local(pool, args, ctx, work, rank)
             except Exception as e:

@@ -451,3 +451,37 @@ def test_scan_written_rows_match_python_loop(tmp_path, monkeypatch, kind):
     assert got[True] == got[False]
     if kind == "java":
         assert any("\\u00e9" in (m[4] or "") for m in got[True][1])  # ensure_ascii form of the exception list
+
+
+def test_slow_fetch_holds_no_database_write_lock(tmp_path):
+    """The row swap's transaction (SQLite BEGIN IMMEDIATE: the database's
+    write lock) opens only after the snapshot is read: while one analysis
+    waits on a slow (remote) fetch, another project's analysis and status
+    writes go through, and the slow one still completes afterwards."""
+    import time
+    synth.java_spring_repo(str(tmp_path / "slow"), 6, base_package="co.slow", seed=3)
+    synth.java_spring_repo(str(tmp_path / "fast"), 6, base_package="co.fast", seed=4)
+    app = make_app(tmp_path)
+    inside, release = threading.Event(), threading.Event()
+    real = app.indexer._timed_fetch
+
+    def fetch(url, branch):
+        if url.value.endswith("slow"):
+            inside.set()
+            assert release.wait(60)
+        return real(url, branch)
+    app.indexer._timed_fetch = fetch
+    out = {}
+    t = threading.Thread(target=lambda: out.setdefault("slow", app.indexer.analyze_project(str(tmp_path / "slow"))))
+    t.start()
+    try:
+        assert inside.wait(30)
+        t0 = time.time()
+        fast = app.indexer.analyze_project(str(tmp_path / "fast"))  # would wait the 30 s busy timeout
+        assert fast.success and time.time() - t0 < 10
+        assert app.repos.projects.find_by_id(fast.project_id).status == ProjectStatus.ANALYZED
+    finally:
+        release.set()
+        t.join(60)
+    assert out["slow"].success and out["slow"].classes_analyzed >= 6
+    app.close()

@@ -122,7 +122,8 @@ def main(argv=None) -> int:
             "prompt_tokens_per_s": round(prompt_all / elapsed, 1),
             "decode_step_ms": round(1e3 * st["decode_s"] / max(1, st["decode_steps"]), 3),
             "prefill_ms_avg": round(1e3 * st["prefill_s"] / max(1, st["prefills"]), 3),
-            "prefill_s": round(st["prefill_s"], 3), "prefill_batches": st["prefill_batches"],
+            "prefill_s": round(st["prefill_s"], 3), "prefill_gpu_s": round(st.get("prefill_gpu_s", 0.0), 3),
+            "prefill_batches": st["prefill_batches"],
             "decode_s": round(st["decode_s"], 3), "host_ms_per_step": round(1e3 * st["host_s"] / max(1, st["decode_steps"]), 3),
             "admit_min": eng.admit_min,
             "decode_steps": st["decode_steps"], "rows_per_step": round(st["decode_rows"] / max(1, st["decode_steps"]), 1),

@@ -265,7 +265,8 @@ class LocalEngine:
                           for _ in range(2)]
         self.stats = {"prompt_tokens": 0, "generated_tokens": 0, "decode_steps": 0, "decode_rows": 0,
                       "prefills": 0, "prefill_batches": 0, "decode_s": 0.0, "prefill_s": 0.0, "prefix_tokens": 0,
-                      "prefix_s": 0.0, "host_s": 0.0, "wait_s": 0.0}
+                      "prefix_s": 0.0, "host_s": 0.0, "wait_s": 0.0, "prefill_gpu_s": 0.0}
+        self._pf_events: List[tuple] = []  # (start, end) device events of the batched prefills
         self._lock = threading.Lock()
 
     # ---------------------------------------------------------------- api
@@ -355,10 +356,20 @@ class LocalEngine:
         return self._prompt(s, readme, budget)
 
     def _admit_batch(self, batch: List[_Seq], prefix: int) -> List[_Seq]:
-        """Prefills every sequence of ``batch`` (slots assigned) -- prompt +
-        first forced segment, after the shared prefix when set -- in ONE
-        batched prefill, then selects each first free token with one masked
-        argmax.  Returns the sequences that finished already."""
+        """Prefills ``batch`` and waits for it (see :meth:`_admit_launch`);
+        returns the sequences that finished already."""
+        return self._admit_finish(self._admit_launch(batch, prefix), wait=True)
+
+    def _admit_launch(self, batch: List[_Seq], prefix: int) -> dict:
+        """Enqueues ONE batched prefill of every sequence of ``batch`` (slots
+        assigned) -- prompt + first forced segment, after the shared prefix
+        when set -- and the masked argmax of each first free token; the ids
+        land in a pinned buffer.  Nothing here waits for the device: the host
+        goes on to build and launch the running batch's next step, which the
+        stream runs after the prefill; the admitted classes join the step
+        after that.  (The prefill on a second stream, overlapped with the
+        decode steps, measured no faster: the two do not run concurrently to
+        any useful degree -- profiles/overlap_prefill_r3.txt.)"""
         from .. import ops
         t0 = time.perf_counter()
         reqs = []
@@ -372,23 +383,55 @@ class LocalEngine:
             s.out.extend(first)
             s.pos = len(toks)
             s.seg, s.forced_off = 1, 0
-        logits = self.model.prefill_batch(reqs)  # [n, vocab]
         need = [i for i, s in enumerate(batch) if s.seg < len(s.segs) and s.segs[s.seg].forced is None]
+        dev = self.model.device
+        h = {"batch": batch, "need": need, "ids": None, "event": None}
+        timed = dev.type == "cuda"
+        if timed:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        logits = self.model.prefill_batch(reqs)  # [n, vocab]
+        if timed:
+            ev[1].record()
+            self._pf_events.append(ev)
         if need:
             rows = logits[need] if len(need) < len(batch) else logits
             midx = torch.tensor([self.MASK_QUOTE if batch[i].segs[1].min_len == 0 else self.MASK_NO_QUOTE
-                                 for i in need], dtype=torch.int32, device=logits.device)
-            ids = ops.masked_argmax(rows.contiguous(), self.masks, vocab=self.cfg.vocab_size,
-                                    mask_idx=midx).cpu().tolist()
-            for i, tok in zip(need, ids):
+                                 for i in need], dtype=torch.int32)
+            if dev.type == "cuda":  # no pageable (host-blocking) copy behind the prefill
+                midx = midx.pin_memory()
+            midx = midx.to(dev, non_blocking=True)
+            ids = ops.masked_argmax(rows.contiguous(), self.masks, vocab=self.cfg.vocab_size, mask_idx=midx)
+            host = torch.empty(len(need), dtype=torch.int32, pin_memory=dev.type == "cuda")
+            host.copy_(ids, non_blocking=dev.type == "cuda")
+            h["ids"] = host
+        if dev.type == "cuda":
+            h["event"] = torch.cuda.Event()
+            h["event"].record()
+        self.stats["prefill_s"] += time.perf_counter() - t0
+        return h
+
+    def _admit_finish(self, h: dict, wait: bool) -> Optional[List[_Seq]]:
+        """None while the prefill of ``h`` is still running (``wait=False``);
+        else applies the first tokens and returns the sequences that finished
+        already (all forced)."""
+        ev = h["event"]
+        if ev is not None:
+            if not wait and not ev.query():
+                return None
+            t0 = time.perf_counter()
+            ev.synchronize()
+            self.stats["prefill_s"] += time.perf_counter() - t0
+        batch = h["batch"]
+        if h["ids"] is not None:
+            for i, tok in zip(h["need"], h["ids"].tolist()):
                 batch[i].next_token = int(tok)
         done = []
-        for i, s in enumerate(batch):
+        for s in batch:
             if s.seg >= len(s.segs) or s.segs[s.seg].forced is not None:
                 self._advance_forced(s)
             if s.done:
                 done.append(s)
-        self.stats["prefill_s"] += time.perf_counter() - t0
         self.stats["prefills"] += len(batch)
         self.stats["prefill_batches"] += 1
         return done
@@ -450,12 +493,13 @@ class LocalEngine:
         prev_event = None
         prev_buf = 1
         finished: List[_Seq] = []
+        inflight: Optional[dict] = None  # the batched prefill in flight
         try:
             while True:
                 # ---- refill the look-ahead (blocking only when idle)
                 want = len(free_slots) + lookahead - len(pending)
                 if want > 0 and not feed.done:
-                    for key, inp in feed.take(want, wait=not active and not pending):
+                    for key, inp in feed.take(want, wait=not active and not pending and inflight is None):
                         s = _Seq(inp, key, fit_template(inp, reply_cap))
                         try:
                             s.prompt = self._build_prompt(s, readme)
@@ -475,13 +519,15 @@ class LocalEngine:
                             deferred.append((key, inp))
                             continue
                         pending.append(s)
-                if not pending and not active:
+                if not pending and not active and inflight is None:
                     if feed.done:
                         break
                     continue
-                # ---- admission: one batched prefill for all that fit
-                if pending and free_slots and (not active or len(free_slots) >= self.admit_min
-                                               or (feed.done and len(free_slots) >= len(pending))):
+                # ---- admission: one batched prefill for all that fit, enqueued
+                # ahead of the running batch's next step
+                if inflight is None and pending and free_slots and (
+                        not active or len(free_slots) >= self.admit_min
+                        or (feed.done and len(free_slots) >= len(pending))):
                     batch: List[_Seq] = []
                     ntok = 0
                     while pending and free_slots and len(batch) < self.ADMIT_SEQS:
@@ -492,10 +538,16 @@ class LocalEngine:
                         s.slot = free_slots.pop()
                         batch.append(s)
                         ntok += nxt
-                    for s in self._admit_batch(batch, P):
-                        free_slots.append(s.slot)
-                        yield s.index, s.out.decode("utf-8", "replace")
-                    active.extend(s for s in batch if not s.done)
+                    inflight = self._admit_launch(batch, P)
+                if inflight is not None:
+                    done = self._admit_finish(inflight, wait=not active)
+                    if done is not None:
+                        for s in done:
+                            free_slots.append(s.slot)
+                            yield s.index, s.out.decode("utf-8", "replace")
+                        active.extend(s for s in inflight["batch"] if not s.done)
+                        inflight = None
+                        continue  # admit the next batch before this step when slots allow
                 if not active:
                     continue
                 # ---- build and launch one step
@@ -582,6 +634,11 @@ class LocalEngine:
         finally:
             if prev_event is not None:
                 prev_event.synchronize()
+            if inflight is not None and inflight["event"] is not None:
+                inflight["event"].synchronize()
+            for a, b in self._pf_events:  # device time of the prefills (stats only)
+                self.stats["prefill_gpu_s"] += a.elapsed_time(b) * 1e-3
+            self._pf_events.clear()
             if P:
                 self.model.clear_prefix()
         return deferred

@@ -436,7 +436,10 @@ class LocalLM:
             m = self._mlp(i, h)
             nxt = self.w[f"l{i + 1}.ln1"] if i + 1 < c.layers else self.w["norm_f"]
             h = ops.add_rmsnorm(m, nxt, c.eps, residual=resid)
-        last = torch.tensor([o_ - 1 for o_ in offsets[1:]], dtype=torch.long, device=dev)
+        last = torch.tensor([o_ - 1 for o_ in offsets[1:]], dtype=torch.long)
+        if dev.type == "cuda":  # pinned + async: a pageable copy would block the host until the stream drains
+            last = last.pin_memory()
+        last = last.to(dev, non_blocking=True)
         return F.linear(h.index_select(0, last), self.w["lm_head"])
 
     @torch.inference_mode()

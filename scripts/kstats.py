@@ -7,8 +7,10 @@ import collections
 import csv
 import sys
 
-CATS = [("prefill_mfma", "prefill_"), ("gemm", "Cijk"), ("fused_gemm", "fused_gemm"), ("attn_combine", "combine"), ("attn_suffix", "decode_attn_"),
-        ("attn_prefix", "prefix_attn"), ("prefill_attn", "attn_fwd"), ("rmsnorm", "rmsnorm"), ("silu", "silu"),
+CATS = [("wgemm_swiglu", "wgemm_kernel<128"), ("wgemm", "wgemm_kernel"), ("wgemm_reduce", "reduce_"),
+        ("attn_prefix(mfma)", "prefill_attn_kernel"), ("prefill_varlen", "prefill_varlen"),
+        ("gemm(hipblaslt)", "Cijk"), ("fused_gemm", "fused_gemm"), ("attn_combine", "combine"),
+        ("attn_per_row", "decode_attn_"), ("rmsnorm", "rmsnorm"), ("silu", "silu"),
         ("rope", "rope"), ("embedding", "embedding"), ("argmax", "argmax")]
 
 

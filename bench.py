@@ -58,7 +58,7 @@ def parse_args(argv=None):
     ap.add_argument("--enrich-local-classes", type=int, default=256,
                     help="classes of the end-to-end local-model enrichment run (extra.enrichLocal; 0 = skip)")
     ap.add_argument("--enrich-local-kv", default="fp8", choices=["bf16", "fp8"])
-    ap.add_argument("--enrich-local-batch", type=int, default=256)
+    ap.add_argument("--enrich-local-batch", type=int, default=512)
     return ap.parse_args(argv)
 
 

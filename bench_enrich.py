@@ -27,7 +27,7 @@ def main(argv=None) -> int:
     ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"],
                     help="KV cache storage (fp8 = e4m3, half the attention bytes)")
     ap.add_argument("--classes", type=int, default=1024, help="classes per rank")
-    ap.add_argument("--batch", type=int, default=256, help="concurrent sequences (KV slots)")
+    ap.add_argument("--batch", type=int, default=512, help="concurrent sequences (KV slots)")
     ap.add_argument("--max-seq", type=int, default=8192)
     ap.add_argument("--max-rows", type=int, default=0,
                     help="rows per decode step incl. jump-forward rows (0 = 1.5 x batch, >= 256)")

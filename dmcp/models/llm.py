@@ -15,7 +15,7 @@ MI355X mapping:
   append in the QKV epilogue, SwiGLU in the gate/up epilogue, the residual
   add in the O / down epilogues -- a layer is 4 GEMM launches + attention
   (measured: 60 vs 77 us per layer at 16 rows);
-* decode steps of 17-512 rows (the enrichment operating point is ~300)
+* decode steps of 17-1024 rows (the enrichment operating point is 300-500)
   run every projection on the weight-streaming GEMM (``csrc/wgemm.hip``:
   each weight tile read from HBM once per step, all rows of an M part per
   block, the M parts of a tile on one XCD) with the neighbour op fused:
@@ -234,7 +234,7 @@ class LocalLM:
         ps = ops.PREFIX_MFMA_MAX_SPLITS if shared_prefix else 0
         self.attn_ws = (ops.decode_workspace(self.max_rows, c.n_heads, c.n_kv_heads, c.head_dim, c.max_seq,
                                              self.device, prefix_slots=ps) if self.device.type == "cuda" else None)
-        # steps of fused_max_rows < rows <= 512: every projection on the
+        # steps of fused_max_rows < rows <= WGEMM_MAX_ROWS: every projection on the
         # weight-streaming GEMM (csrc/wgemm.hip) with its neighbour op in the
         # epilogue / reduction -- QKV + RoPE + KV append, O + residual + norm,
         # gate/up + SwiGLU, down + residual + next norm
@@ -627,7 +627,8 @@ class DecodeGraphs:
     outputs: read them before the next replay of the same bucket."""
 
     def __init__(self, model: LocalLM, masks: torch.Tensor,
-                 buckets: Sequence[int] = (1, 2, 4, 8, 16, 32, 64, 96, 128, 192, 256, 384, 512)) -> None:
+                 buckets: Sequence[int] = (1, 2, 4, 8, 16, 32, 64, 96, 128, 192, 256, 320, 384, 448, 512, 640,
+                                          768, 896, 1024)) -> None:
         self.model = model
         self.masks = masks
         self.buckets = sorted(b for b in buckets if b <= model.max_rows)

@@ -549,7 +549,7 @@ def fused_resid(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, wk: in
     return residual
 
 
-WGEMM_MAX_ROWS = 512
+WGEMM_MAX_ROWS = 1024
 
 
 def wgemm_plan(M: int, N: int, K: int, swiglu: bool = False, target_blocks: int = 192) -> tuple:
@@ -588,7 +588,7 @@ def _wgemm_ws(workspace: torch.Tensor, n: int, name: str) -> None:
 
 
 def wgemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """x . w^T in bf16 (F.linear) on the weight-streaming kernel; M <= 512."""
+    """x . w^T in bf16 (F.linear) on the weight-streaming kernel; M <= WGEMM_MAX_ROWS."""
     M, K, N = _wgemm_args(x, w, "wgemm")
     _, mparts = wgemm_plan(M, N, K)
     if out is None:
@@ -631,7 +631,7 @@ def wgemm_resid_norm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, n
                      workspace: torch.Tensor, out: Optional[torch.Tensor] = None, splits: int = 0) -> torch.Tensor:
     """residual += bf16(x . w^T) (in place); returns RMSNorm(residual) * norm_w
     -- F.linear + add_rmsnorm as one split-K GEMM + one reduction per row that
-    adds the residual and normalises.  x [M, K] (M <= 512), w [N, K]."""
+    adds the residual and normalises.  x [M, K] (M <= WGEMM_MAX_ROWS), w [N, K]."""
     M, K, N = _wgemm_args(x, w, "wgemm_resid_norm")
     _req(residual, torch.bfloat16, "wgemm_resid_norm.residual")
     _req(norm_w, torch.bfloat16, "wgemm_resid_norm.norm_w")
@@ -654,7 +654,7 @@ def wgemm_rope_kv(x: torch.Tensor, w: torch.Tensor, pos: torch.Tensor, slot: tor
                   k_cache: torch.Tensor, v_cache: torch.Tensor, n_q_heads: int, workspace: torch.Tensor,
                   q_out: Optional[torch.Tensor] = None, splits: int = 0) -> torch.Tensor:
     """rope_kv(F.linear(x, w), ...) as one split-K GEMM + one reduction per row
-    (RoPE, the q write and the K/V-cache append).  x [M, K] (M <= 512);
+    (RoPE, the q write and the K/V-cache append).  x [M, K] (M <= WGEMM_MAX_ROWS);
     returns q [M, Hq, D]."""
     M, K, N = _wgemm_args(x, w, "wgemm_rope_kv")
     S_, Hkv, MAXS, D = k_cache.shape

@@ -40,6 +40,7 @@ def main(argv=None) -> int:
     ap.add_argument("--max-seq", type=int, default=8192)
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--fused", type=int, default=-1, help="-1 = model default, 0 = hipBLASLt, 1 = fused kernels")
+    ap.add_argument("--wgemm", type=int, default=-1, help="-1 = model default, 0 = hipBLASLt for > 16 rows")
     a = ap.parse_args(argv)
 
     from dmcp.enrich.local import LocalEngine
@@ -49,10 +50,14 @@ def main(argv=None) -> int:
 
     torch.cuda.set_device(0)
     cfg = preset(a.preset, max_batch=a.batch, max_seq=a.max_seq, kv_dtype=a.kv_dtype)
+    cfg = preset(a.preset, max_batch=a.batch, max_seq=a.max_seq, kv_dtype=a.kv_dtype,
+                 max_rows=max(cfg.max_rows, a.batch + a.extra))
     model = LocalLM(cfg, device="cuda:0")
     if a.fused >= 0:
         model.use_fused = bool(a.fused)
         model.fused_max_rows = 128 if a.fused else 0
+    if a.wgemm >= 0:
+        model.use_wgemm = bool(a.wgemm)
     eng = LocalEngine(model)
     g = torch.Generator().manual_seed(0)
     if a.prefix:

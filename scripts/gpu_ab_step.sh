@@ -8,7 +8,7 @@ mkdir -p "$OUT"
 AB=${AB:-HEAD}
 for rep in 1 2; do
     for v in new old; do
-        for a in "256 64" "64 14"; do
+        for a in "256 64" "64 14" "448 64"; do
             set -- $a
             if [ $v = old ]; then export DMCP_HIPOPS_SO=dmcp/ops/ab/_hipops_$AB.so; else unset DMCP_HIPOPS_SO; fi
             timeout -k 10 200 python3 scripts/bench_step.py --batch $1 --extra $2 --kv-dtype fp8 --iters 100 \

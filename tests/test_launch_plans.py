@@ -1,0 +1,43 @@
+"""Host-side launch planning of the gfx950 kernels (pure Python, no GPU):
+the weight-streaming GEMM's (K slices, M parts) and the decode step's
+attention splits must respect what the kernels assume -- a mis-planned
+launch is either a device fault or a second, mostly idle wave of blocks."""
+import pytest
+
+from dmcp.ops import hip
+
+SHAPES = {"qkv": (3072, 2048, False), "o": (2048, 2048, False), "down": (2048, 8192, False),
+          "gate_up": (16384, 2048, True), "qkv_3b": (5120, 3072, False), "down_3b": (3072, 8192, False),
+          "gate_up_3b": (16384, 3072, True)}
+
+
+@pytest.mark.parametrize("M", [1, 16, 17, 64, 78, 128, 200, 320, 383, 384, 448, 512, 640, 768, 896, 1000, 1024])
+@pytest.mark.parametrize("shape", list(SHAPES))
+def test_wgemm_plan_fits_the_kernel(M, shape):
+    N, K, swiglu = SHAPES[shape]
+    S, mparts = hip.wgemm_plan(M, N, K, swiglu=swiglu)
+    assert S >= 1 and mparts >= 1 and (S & (S - 1)) == 0 and S <= 8
+    assert K % (64 * S) == 0                                  # whole 64-deep chunks per slice
+    rows = (-(-M // mparts) + 15) // 16 * 16
+    assert rows <= 256                                        # <= 4 16-row tiles per wave
+    assert mparts <= max(1, -(-M // 16))                      # no empty M parts
+    if swiglu:
+        assert S == 1                                         # SwiGLU writes its output directly
+    tiles = (N // 2 if swiglu else N) // 64
+    blocks = tiles * mparts * S
+    if M >= 384:  # one block per CU: no mostly idle trailing wave
+        waves = -(-blocks // 256)
+        assert blocks / (256 * waves) >= 0.5, (blocks, waves)
+
+
+def test_wgemm_plan_keeps_the_measured_small_m_plans():
+    # tuned on the GPU at 320 rows (profiles/wgemm_r3.txt)
+    assert hip.wgemm_plan(320, 3072, 2048) == (2, 2)
+    assert hip.wgemm_plan(320, 2048, 8192) == (4, 2)
+    assert hip.wgemm_plan(320, 16384, 2048, swiglu=True) == (1, 2)
+
+
+@pytest.mark.parametrize("rows", [1, 16, 78, 320, 512, 768])
+def test_prefix_splits_within_the_workspace(rows):
+    sp = hip.prefix_mfma_splits(rows, 4, 8)
+    assert 1 <= sp <= hip.PREFIX_MFMA_MAX_SPLITS

@@ -41,6 +41,10 @@ def main(argv=None) -> int:
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--fused", type=int, default=-1, help="-1 = model default, 0 = hipBLASLt, 1 = fused kernels")
     ap.add_argument("--wgemm", type=int, default=-1, help="-1 = model default, 0 = hipBLASLt for > 16 rows")
+    ap.add_argument("--jitter", type=float, default=0.0,
+                    help="per-sequence own length uniform in ctx x [1 - j, 1 + j] (the engine's mix of progress)")
+    ap.add_argument("--adjacent", action="store_true",
+                    help="jump rows next to their sequence's row (the engine's row order) instead of at the end")
     a = ap.parse_args(argv)
 
     from dmcp.enrich.local import LocalEngine
@@ -64,9 +68,13 @@ def main(argv=None) -> int:
         model.set_prefix(torch.randint(0, 256, (a.prefix,), generator=g).tolist())
     n = a.batch + a.extra
     toks = torch.randint(0, 256, (n,), generator=g).tolist()
+    u = (torch.rand(a.batch, generator=g) * 2 - 1).tolist()
+    ctxs = [max(1, int(round(a.ctx * (1 + a.jitter * x)))) for x in u]
     slots = list(range(a.batch)) + [i % a.batch for i in range(a.extra)]
-    base = a.prefix + a.ctx
-    poss = [base + (i // a.batch) for i in range(n)]
+    poss = [a.prefix + ctxs[sl] + (i // a.batch) for i, sl in enumerate(slots)]
+    if a.adjacent:  # each sequence's jump rows right after its own row
+        order = sorted(range(n), key=lambda i: (slots[i], i))
+        slots, poss = [slots[i] for i in order], [poss[i] for i in order]
     mrows = [0] * n
     graphs = eng.graphs
     for _ in range(3):
@@ -83,10 +91,10 @@ def main(argv=None) -> int:
     for _ in range(a.iters):
         graphs.run(toks, slots, poss, mrows)[1].cpu().tolist()
     loop_ms = (time.perf_counter() - t0) / a.iters * 1e3
-    kv_bytes = 2 * cfg.layers * cfg.n_kv_heads * cfg.head_dim * cfg.kv_elem_bytes * (a.batch * (a.ctx + 1) + a.prefix)
+    kv_bytes = 2 * cfg.layers * cfg.n_kv_heads * cfg.head_dim * cfg.kv_elem_bytes * (sum(ctxs) + a.batch + a.prefix)
     w_bytes = 2 * (cfg.param_count() - cfg.vocab_size * cfg.hidden)
     print(json.dumps({"bench": "decode_step", "preset": a.preset, "kv_dtype": a.kv_dtype, "rows": n, "batch": a.batch, "prefix": a.prefix,
-                      "ctx": a.ctx, "fused": bool(getattr(model, "use_fused", False)),
+                      "ctx": a.ctx, "jitter": a.jitter, "adjacent": a.adjacent, "fused": bool(getattr(model, "use_fused", False)),
                       "prefix_splits": hip.prefix_mfma_splits(a.batch + a.extra, cfg.n_heads // cfg.n_kv_heads,
                                                               cfg.n_kv_heads),
                       "device_ms": round(dev_ms, 3), "loop_ms": round(loop_ms, 3),

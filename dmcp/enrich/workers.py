@@ -252,9 +252,20 @@ class GpuWorkerPool:
     def stream(self, inputs: Iterable[EnrichmentInput], readme: Optional[str]
                ) -> Iterator[Tuple[int, Any]]:
         """Yields ``(input index, raw reply str | Exception)`` as replies
-        arrive, from whichever worker finished them."""
+        arrive, from whichever worker finished them.  A caller that stops
+        early (an exception while applying a reply) still ends the session
+        in every worker: each finishes what it was sent and then serves the
+        next stream (its late replies carry the old session id and are
+        dropped)."""
         with self._lock:
-            yield from self._stream(inputs, readme)
+            self._open: List[_Worker] = []
+            try:
+                yield from self._stream(inputs, readme)
+            finally:
+                for w in self._open:
+                    if w.alive:
+                        w.send({"op": "end", "sid": self.sid})
+                self._open = []
 
     def _stream(self, inputs, readme):
         self._replace_dead()
@@ -268,6 +279,7 @@ class GpuWorkerPool:
             if not w.send({"op": "begin", "sid": sid, "readme": readme}):
                 w.alive = False
         ended: set = set()
+        self._open = [w for w in live if w.alive]  # sessions to end if the caller stops early
         finished: set = set()
         cap = self.capacity
         chunk_min = max(1, cap // 8)
@@ -316,6 +328,8 @@ class GpuWorkerPool:
                     if w not in ended:
                         w.send({"op": "end", "sid": sid})
                         ended.add(w)
+                        if w in self._open:
+                            self._open.remove(w)
                 if all(w in finished or not w.alive for w in self.workers if w in ended) and \
                         not any(w.inflight for w in self.workers):
                     return

@@ -62,6 +62,22 @@ def test_work_is_spread_and_results_keep_input_order(pool):
     assert len({w.info["pid"] for w in pool.workers}) == 2 and all(w.info["pid"] != os.getpid() for w in pool.workers)
 
 
+def test_abandoned_stream_leaves_the_workers_serving(pool):
+    """A caller that stops consuming a stream (an exception while applying a
+    reply) must not leave a worker waiting for more of that session: the
+    next stream completes on the same processes."""
+    be = ProcessLLMBackend(pool)
+    pids = [w.proc.pid for w in pool.workers]
+    gen = be.enrich_stream(_inputs(12), None)
+    next(gen)
+    gen.close()  # GeneratorExit inside the pool's stream
+    t0 = time.time()
+    res = be.enrich_batch(_inputs(6), None)
+    assert all(r.success for r in res), [r.error_message for r in res if not r.success]
+    assert [w.proc.pid for w in pool.workers] == pids and pool.deaths == 0
+    assert time.time() - t0 < 120
+
+
 def test_killed_worker_is_isolated_and_replaced(pool):
     be = ProcessLLMBackend(pool)
     inputs = _inputs(16)

@@ -15,7 +15,7 @@ MI355X mapping:
   append in the QKV epilogue, SwiGLU in the gate/up epilogue, the residual
   add in the O / down epilogues -- a layer is 4 GEMM launches + attention
   (measured: 60 vs 77 us per layer at 16 rows);
-* decode steps of 17-1024 rows (the enrichment operating point is 300-500)
+* decode steps of 17-512 rows (the enrichment operating point is 300-500)
   run every projection on the weight-streaming GEMM (``csrc/wgemm.hip``:
   each weight tile read from HBM once per step, all rows of an M part per
   block, the M parts of a tile on one XCD) with the neighbour op fused:

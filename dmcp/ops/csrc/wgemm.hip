@@ -1,6 +1,6 @@
 // Weight-streaming GEMM for the decode step (gfx950 / MI355X, CDNA4):
 //
-//   Y[M, N] = X[M, K] . W[N, K]^T      bf16 in, fp32 accumulate,  M <= 1024
+//   Y[M, N] = X[M, K] . W[N, K]^T      bf16 in, fp32 accumulate,  M <= 512
 //
 // At the enrichment operating point (256 sequences + jump-forward rows, ~300
 // rows per step) every projection streams its whole weight matrix from HBM
@@ -391,12 +391,12 @@ extern "C" {
 //   mode 0: y[M, N] bf16 = x . w^T                        (S == 1)
 //   mode 1: part[S, M, N] fp32 partials over K / S slices
 //   mode 2: y[M, I] bf16 = silu(x . w[:I]^T) * (x . w[I:]^T)  (w = [gate; up] [2I, K], S == 1)
-// Contract (checked by dmcp/ops/hip.py, guarded here): M in [1, 1024],
+// Contract (checked by dmcp/ops/hip.py, guarded here): M in [1, 512],
 // K % (64 S) == 0, N % 64 == 0 (mode 2: I % 64 == 0), rows / parts <= 256.
 int dmcp_wgemm(const void* x, const void* w, void* y, void* part, int M, int N, int K, int S, int mparts, int mode,
                int I, void* stream) {
     if (M <= 0) return 0;
-    if (!x || !w || M > 1024 || S < 1 || mparts < 1 || K % (kKC * S) != 0 || (mode == 1 && !part) ||
+    if (!x || !w || M > 512 || S < 1 || mparts < 1 || K % (kKC * S) != 0 || (mode == 1 && !part) ||
         (mode != 1 && (!y || S != 1)) || (mode == 2 ? (I <= 0 || I % 64 != 0) : (N <= 0 || N % 64 != 0)) ||
         (((M + mparts - 1) / mparts + 15) & ~15) > 256)
         return hipErrorInvalidValue;

@@ -549,7 +549,11 @@ def fused_resid(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, wk: in
     return residual
 
 
-WGEMM_MAX_ROWS = 1024
+# Above 512 rows hipBLASLt's large tiles win: the decode step with the
+# weight-streaming GEMMs vs hipBLASLt was 6.56 / 6.53 ms at 512 rows, 7.94 /
+# 7.54 at 640, 9.13 / 8.79 at 768, 11.83 / 11.48 at 1,024 (kernel extended to
+# 1,024 rows for that measurement: profiles/decode_step_512rows_r3.txt)
+WGEMM_MAX_ROWS = 512
 
 
 def wgemm_plan(M: int, N: int, K: int, swiglu: bool = False, target_blocks: int = 192) -> tuple:

@@ -11,7 +11,7 @@ SHAPES = {"qkv": (3072, 2048, False), "o": (2048, 2048, False), "down": (2048, 8
           "gate_up_3b": (16384, 3072, True)}
 
 
-@pytest.mark.parametrize("M", [1, 16, 17, 64, 78, 128, 200, 320, 383, 384, 448, 512, 640, 768, 896, 1000, 1024])
+@pytest.mark.parametrize("M", [1, 16, 17, 64, 78, 128, 200, 320, 383, 384, 448, 500, 512])
 @pytest.mark.parametrize("shape", list(SHAPES))
 def test_wgemm_plan_fits_the_kernel(M, shape):
     N, K, swiglu = SHAPES[shape]

@@ -169,3 +169,21 @@ def test_engine_shared_prefix_same_output(model):
     for r, inp in zip(rb, inputs):
         assert [m["methodName"] for m in json.loads(r)["methods"]] == inp.method_names
     assert len(ra) == len(rb) == len(inputs)
+
+
+def test_engine_batched_admission_matches_one_class_at_a_time(model):
+    """Classes admitted in batches while others decode (non-blocking batched
+    prefill, pipelined steps) start their replies with the same greedy tokens
+    as each class generated alone: a first token read before its prefill's
+    ids landed would differ for most classes."""
+    from dmcp.enrich.local import LocalEngine
+    from dmcp.enrich.types import EnrichmentInput
+    inputs = [EnrichmentInput("class Q%d { void q%d() {} int n = %d; }" % (i, i, i * 7), f"co.acme.Q{i}", "java",
+                              "SERVICE", ["q%d" % i]) for i in range(24)]  # > max_batch (16): admissions mid-run
+    eng = LocalEngine(model, admit_min=1)
+    together = eng.generate(inputs, "readme of the shop")
+    alone = [LocalEngine(model).generate([inp], "readme of the shop")[0] for inp in inputs]
+    head = len('{"description": "') + 6
+    same = sum(a[:head] == b[:head] for a, b in zip(together, alone))
+    assert same >= 21, list(zip(together, alone))
+    assert eng.stats["prefill_batches"] >= 2

@@ -433,14 +433,29 @@ __device__ __forceinline__ void load_kv_tile(const void* __restrict__ kb, const 
 //    group stores rows r, r+1 at the same quads; bit 1 of the XOR (r&1) puts
 //    the odd row in the other 16-B half of each 32-B window.
 // The padded layout this replaces (144-B rows) measured ~1 conflict cycle per
-// LDS instruction (profiles/pmc_decode_step_320rows_fp8_r3.txt).  D=128 gets
-// the read-side XOR only (its rows are a whole bank row).
+// LDS instruction (profiles/pmc_decode_step_320rows_fp8_r3.txt).
+// D=128 (a row is a whole 256-B bank row): quad groups XORed with r & 7 for
+// the reads, and within a group the two 16-B halves swapped when the
+// physical group has bit 2 set (vquad) -- an 8-lane fp8 store group is one
+// row whose first halves would otherwise fill only the even 16-B bank slots
+// (2-way conflicts: 2.5 extra cycles per LDS instruction measured on the
+// 3B preset).
 template <int D>
 __device__ __forceinline__ int vswz(int r) {
     if constexpr (D == 64)
         return 2 * (r & 1) + 4 * ((r >> 1) & 3);
     else
         return 4 * (r & 7);
+}
+
+// physical quad of logical quad q of row r
+template <int D>
+__device__ __forceinline__ int vquad(int r, int q) {
+    const int t = q ^ vswz<D>(r);
+    if constexpr (D == 128)
+        return t ^ (2 * ((t >> 4) & 1));
+    else
+        return t;
 }
 
 // One tile of the MFMA per-row kernel: V -> the wave's LDS tile, S^T on the
@@ -450,7 +465,7 @@ template <int D, bool KV8>
 __device__ __forceinline__ void attn_tile_mfma(KVTile<D, KV8>& cur, bool prefetch, int kt_next,
                                                const void* __restrict__ kb, const void* __restrict__ vb,
                                                int kt, int end, int lane, int g16, uint16_t* vw,
-                                               const uint16_t* tr0, int trk,
+                                               const uint16_t* tr0, int trk, int tr_half,
                                                const bf16x8_t (&qf)[D / 32], float& m, float& l,
                                                f32x4_t (&acc)[D / 16], float scale_log2) {
     constexpr int KS = D / 32;
@@ -461,10 +476,11 @@ __device__ __forceinline__ void attn_tile_mfma(KVTile<D, KV8>& cur, bool prefetc
 #pragma unroll
         for (int r = 0; r < D / 32; ++r) {
             const int ch = lane + kWave * r;
-            const int row = ch / CPK, q = 4 * (ch % CPK), sw = vswz<D>(row);
+            const int row = ch / CPK, q = 4 * (ch % CPK);
             uint16_t* rp = vw + row * D;
-            *reinterpret_cast<uint4*>(rp + 4 * (q ^ sw)) = fp8x8_to_bf16x8(make_uint2(cur.v[r].x, cur.v[r].y));
-            *reinterpret_cast<uint4*>(rp + 4 * ((q + 2) ^ sw)) = fp8x8_to_bf16x8(make_uint2(cur.v[r].z, cur.v[r].w));
+            *reinterpret_cast<uint4*>(rp + 4 * vquad<D>(row, q)) = fp8x8_to_bf16x8(make_uint2(cur.v[r].x, cur.v[r].y));
+            *reinterpret_cast<uint4*>(rp + 4 * vquad<D>(row, q + 2)) =
+                fp8x8_to_bf16x8(make_uint2(cur.v[r].z, cur.v[r].w));
         }
     } else {
         constexpr int CPK = D / 8;
@@ -472,7 +488,7 @@ __device__ __forceinline__ void attn_tile_mfma(KVTile<D, KV8>& cur, bool prefetc
         for (int r = 0; r < D / 16; ++r) {
             const int ch = lane + kWave * r;
             const int row = ch / CPK;
-            *reinterpret_cast<uint4*>(vw + row * D + 4 * ((2 * (ch % CPK)) ^ vswz<D>(row))) = cur.v[r];
+            *reinterpret_cast<uint4*>(vw + row * D + 4 * vquad<D>(row, 2 * (ch % CPK))) = cur.v[r];
         }
     }
     f32x4_t sacc[2];
@@ -533,7 +549,10 @@ __device__ __forceinline__ void attn_tile_mfma(KVTile<D, KV8>& cur, bool prefetc
     for (int db = 0; db < DB; ++db) {
         // the two transposed reads (keys +0 / +16) as whole 32-bit registers;
         // d block db sits at quad group db ^ trk of the lane's swizzled row
-        const uint16_t* tp = tr0 + 16 * (db ^ trk);
+        // (D = 128: halves swapped in groups with bit 2 set, see vquad)
+        const int grp = db ^ trk;
+        const uint16_t* tp = tr0 + 16 * grp;
+        if constexpr (D == 128) tp += ((grp >> 2) & 1) * tr_half;
         const uint2 lo = __builtin_bit_cast(
             uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16_t*)tp));
         const uint2 hi = __builtin_bit_cast(
@@ -603,6 +622,8 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
     const int trow = 4 * g16 + (c >> 2), tsw = vswz<D>(trow);
     const uint16_t* tr0 = vw + trow * D + 4 * ((c & 3) ^ (tsw & 3));
     const int trk = tsw >> 2;
+    // D = 128 swapped halves: quad p ^ 2 of the group, as an element offset
+    const int tr_half = (c & 2) ? -8 : 8;
     for (int item = blockIdx.x * NW + wave; item < total; item += gridDim.x * NW) {
         // split-major: consecutive waves take different rows' splits, so the
         // persistent grid's first pass covers every row
@@ -640,7 +661,7 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
         load_kv_tile<D, KV8>(kb, vb, start, end, lane, ta);
         for (int t = 0; t < ntiles; ++t) {
             const int kt = start + 32 * t;
-            attn_tile_mfma<D, KV8>(ta, t + 1 < ntiles, kt + 32, kb, vb, kt, end, lane, g16, vw, tr0, trk, qf, m, l,
+            attn_tile_mfma<D, KV8>(ta, t + 1 < ntiles, kt + 32, kb, vb, kt, end, lane, g16, vw, tr0, trk, tr_half, qf, m, l,
                                    acc, scale_log2);
         }
         l += __shfl_xor(l, 16, kWave);
@@ -774,17 +795,27 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
         if (pe != hipSuccess) return pe;
     }
     // persistent grid: one wave per (split, row, kv head) item, a block runs
-    // 4; enough blocks to fill every CU a few times over, never more than items
-    const long cap = 4L * device_cu_count();
+    // 4; as many blocks as are resident at once (the kernel's occupancy: 4
+    // per CU at D = 64, 2-3 at D = 128), never more than items -- a grid past
+    // residency runs a trailing partial round
     const long items = (long)splits * Hkv * B;
     const long wblocks = (items + 3) / 4;
-    const dim3 wgrid((unsigned)(wblocks < cap ? wblocks : cap));
     float* po = (float*)part_o;
     float* pml = (float*)part_ml;
     uint16_t* oo = (uint16_t*)out;
 #define DMCP_MFMA_DECODE(DD, K8)                                                                                   \
-    decode_attn_mfma_kernel<DD, K8><<<wgrid, kBlock, 0, st>>>(qq, k_cache, v_cache, sl, ln, oo, po, pml, B, Hkv, G, \
-                                                              max_seq, chunk, splits, sl2, num_slots, pl, ps_max)
+    do {                                                                                                           \
+        static int per_cu = 0;                                                                                     \
+        if (per_cu <= 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(                                         \
+                                &per_cu, decode_attn_mfma_kernel<DD, K8>, kBlock, 0) != hipSuccess ||           \
+                            per_cu <= 0))                                                                          \
+            per_cu = 4;                                                                                            \
+        const long cap = (long)per_cu * device_cu_count();                                                         \
+        const dim3 wgrid((unsigned)(wblocks < cap ? wblocks : cap));                                               \
+        decode_attn_mfma_kernel<DD, K8><<<wgrid, kBlock, 0, st>>>(qq, k_cache, v_cache, sl, ln, oo, po, pml, B,   \
+                                                                  Hkv, G, max_seq, chunk, splits, sl2, num_slots, \
+                                                                  pl, ps_max);                                    \
+    } while (0)
     if (kv8) {
         if (D == 64) DMCP_MFMA_DECODE(64, true);
         else DMCP_MFMA_DECODE(128, true);

@@ -8,11 +8,11 @@ B=${1:-448}; X=${2:-64}
 OUT=gpurun_out/sp$B
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 300 python3 scripts/bench_step.py --batch $B --extra $X --kv-dtype fp8 --iters 100 > "$OUT/step.log" 2>&1 \
+timeout -k 10 300 python3 scripts/bench_step.py --batch $B --extra $X --kv-dtype fp8 --iters 100 ${STEP_ARGS:-} > "$OUT/step.log" 2>&1 \
     || { tail -20 "$OUT/step.log"; exit 1; }
 grep '^{' "$OUT/step.log"
 ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/prof" -o step \
-    -- python3 "$ROOT/scripts/bench_step.py" --batch $B --extra $X --kv-dtype fp8 --iters 50 > "$ROOT/$OUT/prof.log" 2>&1 ) \
+    -- python3 "$ROOT/scripts/bench_step.py" --batch $B --extra $X --kv-dtype fp8 --iters 50 ${STEP_ARGS:-} > "$ROOT/$OUT/prof.log" 2>&1 ) \
     || { tail -5 "$OUT/prof.log"; exit 1; }
 find "$OUT/prof" -type f ! -name '*kernel_stats*' -delete
 python3 scripts/kstats.py $(find "$OUT/prof" -name '*kernel_stats.csv' | head -1) | tee "$OUT/kstats.txt"

@@ -149,6 +149,11 @@ class _Seq:
 
     prompt: Optional[List[int]] = None   # prompt tokens (BOS + bytes)
 
+    @property
+    def free_budget(self) -> int:
+        """Sampled (non-forced) tokens the reply may take: ~its decode steps."""
+        return sum(s.max_len + 1 for s in self.segs if s.forced is None)
+
 
 # ----------------------------------------------------------------- feeds
 class IterFeed:
@@ -240,8 +245,12 @@ class LocalEngine:
 
     def __init__(self, model: LocalLM, use_graphs: bool = True, max_prompt_tokens: Optional[int] = None,
                  jump_forward: bool = True, shared_prefix: bool = True, pipeline: bool = True,
-                 admit_min: Optional[int] = None) -> None:
+                 admit_min: Optional[int] = None, longest_first: bool = True) -> None:
         self.model = model
+        # admit the pending classes with the longest reply budget first (LPT):
+        # the run's tail is then short replies, not a few long ones decoding
+        # alone in a nearly empty batch
+        self.longest_first = longest_first
         # a running batch admits new classes only once this many slots are
         # free (or nothing else is pending): every admission stalls the whole
         # decode batch for a prefill, so fewer, larger prefills (one GEMM per
@@ -530,6 +539,8 @@ class LocalEngine:
                         or (feed.done and len(free_slots) >= len(pending))):
                     batch: List[_Seq] = []
                     ntok = 0
+                    if self.longest_first and len(pending) > 1:
+                        pending = deque(sorted(pending, key=lambda q: -q.free_budget))
                     while pending and free_slots and len(batch) < self.ADMIT_SEQS:
                         nxt = len(pending[0].prompt) - P
                         if batch and ntok + nxt > self.ADMIT_TOKENS:

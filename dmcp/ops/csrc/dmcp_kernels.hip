@@ -194,8 +194,9 @@ __global__ __launch_bounds__(kBlock) void rope_kv_kernel(const uint16_t* __restr
 // ~20 partials (shared-prefix splits + suffix splits) cost one memory
 // round trip, on 4x more waves than a thread-per-output merge (which was
 // latency-bound at 8-12 us per layer -- profiles/decode_step_r2_*).
-// Rows whose context fits one split (nact <= 1, no prefix) were written
-// directly.  (A fused "last block merges" variant needs agent-scope release
+// Rows whose own keys fit one split (nact <= 1) were finished by the main
+// kernel (with a shared prefix it merges the prefix partials itself), so the
+// pass runs only for steps of more than one split per row.  (A fused "last block merges" variant needs agent-scope release
 // fences; on gfx950 each one writes back the XCD's L2 and made the kernel
 // ~10x slower -- profiles/ROUND1_NOTES.md.)
 template <int D>
@@ -224,7 +225,7 @@ __global__ __launch_bounds__(kBlock) void decode_attn_combine_kernel(const float
         const int L = (s >= 0 && s < num_slots) ? min(seq_len[b], max_seq) : 0;
         if (L <= 0) continue;  // padding row: zeroed by the main kernel
         const int nact = split_geom(L - P, splits, chunk).nact;
-        if (npre == 0 && nact <= 1) continue;  // written directly by the main kernel
+        if (nact <= 1) continue;  // finished by the main kernel (directly, or merging the prefix partials)
         const int n = npre + nact;
         const size_t base = ((size_t)b * Hq + qh) * splits_total;
         float m = -1e30f, lt = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
@@ -638,8 +639,12 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
             continue;
         }
         const SplitGeom sg = split_geom(L - P, splits, chunk);
-        if (split >= sg.nact) continue;
+        if (split >= max(1, sg.nact)) continue;
+        // one own split: this wave writes the row's final output -- directly,
+        // or (shared prefix) after merging the prefix kernel's partials, which
+        // the same stream finished before this launch (no combine pass)
         const bool direct = P == 0 && sg.nact == 1;
+        const bool merge_prefix = P > 0 && sg.nact <= 1;
         const int start = P + split * sg.part;
         const int end = min(L, start + sg.part);
         const int ntiles = (end - start + 31) / 32;
@@ -666,7 +671,33 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
         }
         l += __shfl_xor(l, 16, kWave);
         l += __shfl_xor(l, 32, kWave);
-        if (c < G) {
+        if (c < G && merge_prefix) {
+            const int qh = kh * G + c;
+            const size_t pb = ((size_t)b * Hq + qh) * splits_total;
+            // online log-sum-exp merge of the ps_max prefix partials into
+            // this wave's (m, l, acc) -- the combine kernel's arithmetic
+            for (int sp = 0; sp < ps_max; ++sp) {
+                const float2 ml = *reinterpret_cast<const float2*>(part_ml + (pb + sp) * 2);
+                const float mn = fmaxf(m, ml.x);
+                const float ca = __builtin_amdgcn_exp2f(m - mn), cb = __builtin_amdgcn_exp2f(ml.x - mn);
+                l = l * ca + ml.y * cb;
+#pragma unroll
+                for (int db = 0; db < DB; ++db) {
+                    const float4 o = *reinterpret_cast<const float4*>(part_o + (pb + sp) * D + 16 * db + 4 * g16);
+                    acc[db][0] = acc[db][0] * ca + o.x * cb;
+                    acc[db][1] = acc[db][1] * ca + o.y * cb;
+                    acc[db][2] = acc[db][2] * ca + o.z * cb;
+                    acc[db][3] = acc[db][3] * ca + o.w * cb;
+                }
+                m = mn;
+            }
+            const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+            for (int db = 0; db < DB; ++db) {
+                const float f[4] = {acc[db][0] * inv, acc[db][1] * inv, acc[db][2] * inv, acc[db][3] * inv};
+                *reinterpret_cast<uint2*>(out + ((size_t)b * Hq + qh) * D + 16 * db + 4 * g16) = pack4(f);
+            }
+        } else if (c < G) {
             const int qh = kh * G + c;
             const float inv = l > 0.f ? 1.f / l : 0.f;
             const size_t pi = ((size_t)b * Hq + qh) * splits_total + ps_max + split;
@@ -825,7 +856,7 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
     }
 #undef DMCP_MFMA_DECODE
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess || (splits == 1 && !prefix)) return e;
+    if (e != hipSuccess || splits == 1) return e;  // every row finished in the main kernel
     return launch_combine(part_o, part_ml, sl, ln, out, B, Hq, D, max_seq, chunk, splits, num_slots, pl, ps_max, st);
 }
 

@@ -128,11 +128,13 @@ def test_decode_attention_shared_prefix(hip, D, Hq, Hkv, P, B):
 def test_decode_attention_balanced_splits(hip, splits, P):
     """Equal per-row splits (decode_plan: at most ``splits`` parts of >= chunk
     keys, rounded to 32-key tiles), with and without a shared prefix;
-    lengths hit partial tiles and split boundaries."""
+    lengths hit partial tiles and split boundaries.  With one split per row
+    the main kernel merges the prefix partials itself (no combine pass),
+    including a row that has no keys of its own."""
     from dmcp.ops import reference
     from dmcp.ops.reference import SharedPrefix
     D, Hq, Hkv, MAXS, S = 64, 32, 8, 1024, 9
-    lens_own = [1, 31, 32, 33, 257, 700, 1000 - P, 2, 511]
+    lens_own = [1, 31, 32, 33, 257, 700, 1000 - P, 2, 511] + ([0] if P else [])  # 0: prefix keys only
     B = len(lens_own)
     q = _bf(B, Hq, D, seed=21)
     kc = _bf(S + 1, Hkv, MAXS, D, seed=22)

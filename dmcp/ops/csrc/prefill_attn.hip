@@ -39,6 +39,7 @@
 namespace {
 
 constexpr int kPfKeys = 64;  // keys per LDS stage (two 32-key MFMA tiles)
+constexpr float kRescaleSlack = 8.f;  // deferred online-softmax rescale threshold (log2 units)
 
 // chunk swizzle of row `row`:
 //  D = 64 (8 chunks, 128-B rows: two rows per 256-B bank line).  With
@@ -231,16 +232,23 @@ __device__ __forceinline__ void prefill_attn_block(
                 // lane with no visible key in the tile (or split) adds
                 // exp2(-inf) = 0 and every rescale factor stays finite
                 mt = half_swap_max(mt) * sl2;
-                const float mn = fmaxf(m[u], mt);
-                if (__any(mn > m[u])) {
+                // deferred rescale (cdna_hip_programming.md "defer-max"): the
+                // running max moves only when a tile max passes it by
+                // kRescaleSlack (log2 units), so most tiles skip the O / l
+                // rescale; P = exp2(s - m) stays <= 2^slack (exact in fp32
+                // accumulators, bf16 P keeps its relative precision).  The
+                // decision is wave-uniform and made before this tile's P.
+                if (__any(mt > m[u] + kRescaleSlack)) {
+                    const float mn = fmaxf(m[u], mt);
                     const float corr = __builtin_amdgcn_exp2f(m[u] - mn);
                     l[u] *= corr;
 #pragma unroll
                     for (int t2 = 0; t2 < DT; ++t2)
 #pragma unroll
                         for (int i = 0; i < 16; ++i) o[u][t2][i] *= corr;
+                    m[u] = mn;
                 }
-                m[u] = mn;
+                const float mn = m[u];
                 f32x8_t p0, p1;
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {

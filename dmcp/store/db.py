@@ -221,6 +221,16 @@ ALTER TABLE projects ADD COLUMN lease_owner TEXT;
 ALTER TABLE projects ADD COLUMN lease_until REAL;
 ALTER TABLE projects ADD COLUMN graph_version INTEGER NOT NULL DEFAULT 0;
 """),
+    (8, "project_leases_table", """
+-- The lease moves to its own table (V7's projects.lease_owner / lease_until
+-- are no longer written): SQLite rewrites the whole projects row, with its
+-- multi-megabyte graph_data JSON, on every UPDATE of any column.
+CREATE TABLE project_leases (
+    project_id  TEXT PRIMARY KEY REFERENCES projects(id) ON DELETE CASCADE,
+    lease_owner TEXT NOT NULL,
+    lease_until REAL NOT NULL
+) WITHOUT ROWID;
+"""),
 ]
 
 # New database files use 16 KiB pages (SQLite's default is 4 KiB): fewer

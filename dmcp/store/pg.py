@@ -144,6 +144,13 @@ ALTER TABLE projects ADD COLUMN IF NOT EXISTS lease_owner VARCHAR(200);
 ALTER TABLE projects ADD COLUMN IF NOT EXISTS lease_until DOUBLE PRECISION;
 ALTER TABLE projects ADD COLUMN IF NOT EXISTS graph_version INTEGER NOT NULL DEFAULT 0;
 """),
+    (4, "project_leases_table", """
+CREATE TABLE IF NOT EXISTS project_leases (
+    project_id  VARCHAR(36) PRIMARY KEY REFERENCES projects(id) ON DELETE CASCADE,
+    lease_owner VARCHAR(200) NOT NULL,
+    lease_until DOUBLE PRECISION NOT NULL
+);
+"""),
 ]
 
 

@@ -93,13 +93,14 @@ def test_expired_lease_of_a_dead_process_is_taken_over(tmp_path):
     p = app.repos.projects.find_by_repository_url(os.path.abspath(repo), with_graph=False)
     # a crashed analysis: status ANALYZING, lease of a process that stopped heartbeating
     with app.db.transaction() as c:
-        c.execute("UPDATE projects SET status = 'ANALYZING', lease_owner = 'host:1:dead', lease_until = ? "
-                  "WHERE id = ?", (time.time() + 30, p.id))
+        c.execute("UPDATE projects SET status = 'ANALYZING' WHERE id = ?", (p.id,))
+        c.execute("INSERT INTO project_leases (project_id, lease_owner, lease_until) VALUES (?, 'host:1:dead', ?)",
+                  (p.id, time.time() + 30))
     with pytest.raises(DomainError) as e:  # not expired yet: busy
         app.indexer.analyze_project(repo)
     assert e.value.error_code == "PROJECT_BUSY"
     with app.db.transaction() as c:
-        c.execute("UPDATE projects SET lease_until = ? WHERE id = ?", (time.time() - 1, p.id))
+        c.execute("UPDATE project_leases SET lease_until = ? WHERE project_id = ?", (time.time() - 1, p.id))
     r = app.indexer.analyze_project(repo)
     assert r.success
     p = app.repos.projects.find_by_id(p.id)
@@ -123,7 +124,8 @@ def test_lease_heartbeat_keeps_a_long_operation_alive(tmp_path):
     # a lease that another process stole is reported at the next check
     lease = ProjectLease(app.repos.projects, p.id, ttl_s=1.2).acquire()
     with app.db.transaction() as c:
-        c.execute("UPDATE projects SET lease_owner = 'other', lease_until = ? WHERE id = ?", (time.time() + 60, p.id))
+        c.execute("UPDATE project_leases SET lease_owner = 'other', lease_until = ? WHERE project_id = ?",
+                  (time.time() + 60, p.id))
     time.sleep(0.9)
     with pytest.raises(DomainError) as e:
         lease.check()
@@ -184,4 +186,28 @@ def test_mcp_process_sees_analyses_of_another_process(tmp_path):
         mcp.wait(timeout=30)
         mcp.stdout.close()
         mcp.stderr.close()
+    app.close()
+
+
+def test_lease_lives_in_its_own_table(tmp_path):
+    """Lease writes never rewrite the projects row (its graph JSON is megabytes);
+    deleting the project drops its lease."""
+    app = make_app(tmp_path)
+    repo = str(tmp_path / "shop")
+    synth.java_spring_repo(repo, n_classes=8)
+    assert app.indexer.analyze_project(repo).success
+    p = app.repos.projects.find_by_repository_url(os.path.abspath(repo), with_graph=False)
+    before = app.db.query_one("SELECT updated_at, graph_version FROM projects WHERE id = ?", (p.id,))
+    lease = ProjectLease(app.repos.projects, p.id, ttl_s=30).acquire()
+    assert app.repos.projects.lease_of(p.id)[0] == lease.owner
+    assert app.repos.projects.try_acquire_lease(p.id, lease.owner, 30, time.time())  # re-entrant for its owner
+    assert not app.repos.projects.try_acquire_lease(p.id, "someone-else", 30, time.time())
+    after = app.db.query_one("SELECT updated_at, graph_version FROM projects WHERE id = ?", (p.id,))
+    assert tuple(before) == tuple(after)
+    lease.release()
+    assert app.repos.projects.lease_of(p.id) == (None, None)
+    ProjectLease(app.repos.projects, p.id, ttl_s=30).acquire()  # left held, then the project goes
+    with app.db.transaction() as c:
+        c.execute("DELETE FROM projects WHERE id = ?", (p.id,))
+    assert app.db.query_one("SELECT COUNT(*) AS n FROM project_leases")["n"] == 0
     app.close()

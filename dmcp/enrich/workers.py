@@ -120,7 +120,9 @@ class _Worker:
             except Exception as e:  # corrupt frame: treat as death
                 LOG.error("worker %d: bad frame: %s", self.index, e)
                 msg = None
-            self.events.put((self.index, msg))
+            # tagged with this worker object, not its index: a replaced
+            # worker's late EOF must not mark its successor dead
+            self.events.put((self, msg))
             if msg is None:
                 return
 
@@ -216,13 +218,18 @@ class GpuWorkerPool:
                         w.kill()
                 break
             try:
-                i, msg = self.events.get(timeout=min(1.0, left))
+                who, msg = self.events.get(timeout=min(1.0, left))
             except queue.Empty:
                 continue
-            self._handle_control(i, msg)
+            if self._current(who):
+                self._handle_control(who.index, msg)
         if not any(w.ready for w in self.workers):
             raise RuntimeError("no GPU worker started")
         self._initialised = True
+
+    def _current(self, w: "_Worker") -> bool:
+        """False for events of a worker that was already replaced."""
+        return 0 <= w.index < len(self.workers) and self.workers[w.index] is w
 
     def _handle_control(self, i: int, msg: Optional[dict]) -> None:
         w = self.workers[i]
@@ -334,7 +341,7 @@ class GpuWorkerPool:
                         not any(w.inflight for w in self.workers):
                     return
             try:
-                i, msg = self.events.get(timeout=1.0)
+                who, msg = self.events.get(timeout=1.0)
             except queue.Empty:
                 now = time.monotonic()
                 for w in live:
@@ -343,7 +350,9 @@ class GpuWorkerPool:
                                   w.device, self.hang_timeout_s, len(w.inflight))
                         w.kill()
                 continue
-            w = self.workers[i]
+            if not self._current(who):
+                continue
+            w, i = who, who.index
             if msg is None:
                 if w.alive:
                     LOG.error("worker %d on %s exited (rc=%s) holding %d classes", i, w.device, w.proc.poll(),

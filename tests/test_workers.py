@@ -78,6 +78,19 @@ def test_abandoned_stream_leaves_the_workers_serving(pool):
     assert time.time() - t0 < 120
 
 
+def test_late_eof_of_a_replaced_worker_is_ignored(pool):
+    """Events carry the worker object: the EOF of a child that was already
+    replaced (killed for a hang, its reader thread ending later) must not
+    mark the fresh worker at the same index dead."""
+    class Ghost:  # a worker object no longer in the pool, at index 0
+        index = 0
+    cur = pool.workers[0]
+    pool.events.put((Ghost(), None))
+    res = ProcessLLMBackend(pool).enrich_batch(_inputs(4), None)
+    assert all(r.success for r in res), [r.error_message for r in res if not r.success]
+    assert pool.workers[0] is cur and cur.alive
+
+
 def test_killed_worker_is_isolated_and_replaced(pool):
     be = ProcessLLMBackend(pool)
     inputs = _inputs(16)

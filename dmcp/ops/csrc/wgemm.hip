@@ -28,6 +28,10 @@
 //     conflict-free ds_read_b128 of both MFMA operands;
 //   * v_mfma_f32_16x16x32_bf16: A = 16 weight rows x 32 k, B = 32 k x 16 X
 //     rows, C = Y^T tile (lane: 4 consecutive output columns of one row);
+//   * the bound (profiles/wgemm_parts_r3.txt): each CU ingests its weight
+//     tile at ~23 KB/us and its activation rows at ~42 KB/us through the
+//     same load path, t ~= W_block / 23 + X_block / 42 (KB, us); 64 / 128
+//     weight rows x the M part already minimise that for ~256 blocks;
 //   * split-K (S > 1) writes fp32 partials, reduced by the fused consumers
 //     below (residual + RMSNorm of the next op; RoPE + KV-cache append);
 //     MODE_SWIGLU writes silu(gate) * up directly (no gate/up activation in
@@ -49,13 +53,17 @@ __device__ __forceinline__ void glds16(const void* src, uint4* lds_base) {
                                      (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
-template <int NB, int MT, int MODE, int ST>
-__global__ __launch_bounds__(kBlock) void wgemm_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+template <int NB, int MT, int MR, int MODE, int ST>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) void wgemm_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                        uint16_t* __restrict__ y, float* __restrict__ part, int M, int N,
                                                        int K, int ks, int S, int ntiles, int mparts, int mrows,
                                                        int I) {
     constexpr int NF = NB / 16;         // A fragments (16 weight rows each)
-    constexpr int MR = MT * 64;         // X rows staged per block: 4 waves x MT 16-row tiles
+    // X rows staged per block (a multiple of 32, <= 4 waves x MT 16-row
+    // tiles): the M part rounded up to 32 rows, not to 64 -- at 320 rows
+    // (two parts of 160) the X image is 160 rows instead of 192, and X is
+    // most of the bytes each CU stages (profiles/decode_late_ab_r3.txt)
+    static_assert(MR % 32 == 0 && MR <= MT * 64 && MR > (MT - 1) * 64, "MR: staged X rows");
     constexpr int WCH = NB * 8;         // 16-B chunks of a stage's weight image [NB][64 k]
     constexpr int SCH = WCH + MR * 8;   // ... plus the X image [MR][64 k]
     constexpr int WI = NB / 32;         // 1-KiB LDS-DMA pieces (8 rows x 128 B) per wave per stage: weights
@@ -128,29 +136,64 @@ __global__ __launch_bounds__(kBlock) void wgemm_kernel(const uint16_t* __restric
 #pragma unroll
         for (int t = 0; t < MT; ++t) acc[f][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+    // Both 32-deep k steps' operand fragments are read from LDS before the
+    // first MFMA of the chunk, the second step's reads overlapping the first
+    // step's MFMAs: one exposed LDS latency per chunk instead of one per
+    // fragment group.  At one wave per SIMD (the LDS ring holds one block per
+    // CU) nothing else hides those latencies: the compiler's register-lean
+    // schedule (2 A fragments live, lgkmcnt(0) before every 3-6 MFMAs) left
+    // the matrix cores idle ~2/3 of the time (the 320-row gate/up GEMM with its
+    // loads switched off: 32 -> 29 us, whole kernel 40 -> 38 us against
+    // ~10 us of MFMA; the rest is the CU's load path: profiles/wgemm_parts_r3.txt).
     auto compute = [&](const uint4* st) {
         const uint4* wl = st;
         const uint4* xl = st + WCH;
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            bf16x8_t b[MT];
+        bf16x8_t b[2][MT], a[2][NF];
+        auto load = [&](int kk) {
 #pragma unroll
             for (int t = 0; t < MT; ++t) {
-                const int r = mw + 16 * t + l16;
-                b[t] = as_bf16x8(xl[r * 8 + ((4 * kk + g) ^ (r & 7))]);
+                // rows past the staged image (the last wave's spare tile
+                // when MR < MT * 64) read the image's last row; their
+                // results are never stored (mtv / m_hi)
+                const int r = min(mw + 16 * t + l16, MR - 1);
+                b[kk][t] = as_bf16x8(xl[r * 8 + ((4 * kk + g) ^ (r & 7))]);
             }
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
                 const int r = 16 * f + l16;
-                const bf16x8_t a = as_bf16x8(wl[r * 8 + ((4 * kk + g) ^ (r & 7))]);
+                a[kk][f] = as_bf16x8(wl[r * 8 + ((4 * kk + g) ^ (r & 7))]);
+            }
+        };
+        auto mma = [&](int kk) {
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
                 // every tile, valid or not: the waves meet at a barrier per
                 // chunk, so a wave's idle tiles cost no wall time, and a
                 // per-tile branch breaks back-to-back MFMA issue
 #pragma unroll
                 for (int t = 0; t < MT; ++t)
-                    acc[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[t], acc[f][t], 0, 0, 0);
-            }
+                    acc[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][f], b[kk][t], acc[f][t], 0, 0, 0);
+        };
+        // k step 0's reads, then its MFMAs with k step 1's reads threaded
+        // between them (one read per RM MFMAs, pinned: the scheduler would
+        // sink each read to its use), then k step 1's MFMAs.  At most
+        // NF + MT <= 12 reads are in flight, within lgkmcnt's range, so the
+        // waits stay counted (22 queued reads made the compiler wait for 0).
+        constexpr int NR = NF + MT;            // fragment reads per k step
+        constexpr int NM = NF * MT;            // MFMAs per k step
+        constexpr int RM = NM / NR > 0 ? NM / NR : 1;
+        load(0);
+        __builtin_amdgcn_sched_barrier(0);
+        load(1);
+        mma(0);
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one DS read
+            __builtin_amdgcn_sched_group_barrier(0x008, RM, 0);  // RM MFMAs
         }
+        __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);      // the rest
+        __builtin_amdgcn_sched_barrier(0);
+        mma(1);
     };
 
     // ST-stage ring, ST - 1 stages in flight: wait for this wave's pieces of
@@ -367,11 +410,19 @@ hipError_t launch_wgemm(const uint16_t* x, const uint16_t* w, uint16_t* y, float
     const int ntiles = (MODE == MODE_SWIGLU ? 2 * I : N) / NB;
     const int mrows = (((M + mparts - 1) / mparts) + 15) & ~15;
     const int mt = (mrows + 4 * 16 - 1) / (4 * 16);  // 16-row tiles per wave
+    const bool full = ((mrows + 31) & ~31) > (mt - 1) * 64 + 32;  // staged rows: mt * 64, else mt * 64 - 32
     const dim3 grid((unsigned)(ntiles * S * mparts));
     const int ks = K / S;
-#define DMCP_WG(MT)                                                                                              \
-    wgemm_kernel<NB, MT, MODE, kStages><<<grid, kBlock, 0, st>>>(x, w, y, part, M, N, K, ks, S, ntiles, mparts, \
-                                                                 mrows, I)
+#define DMCP_WG1(MT, MR)                                                                                       \
+    wgemm_kernel<NB, MT, MR, MODE, kStages><<<grid, kBlock, 0, st>>>(x, w, y, part, M, N, K, ks, S, ntiles,   \
+                                                                     mparts, mrows, I)
+#define DMCP_WG(MT)                  \
+    do {                             \
+        if (full)                    \
+            DMCP_WG1(MT, MT * 64);   \
+        else                         \
+            DMCP_WG1(MT, MT * 64 - 32); \
+    } while (0)
     switch (mt) {
         case 1: DMCP_WG(1); break;
         case 2: DMCP_WG(2); break;
@@ -380,6 +431,7 @@ hipError_t launch_wgemm(const uint16_t* x, const uint16_t* w, uint16_t* y, float
         default: return hipErrorInvalidValue;
     }
 #undef DMCP_WG
+#undef DMCP_WG1
     return hipGetLastError();
 }
 

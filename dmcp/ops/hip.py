@@ -568,22 +568,24 @@ def wgemm_plan(M: int, N: int, K: int, swiglu: bool = False, target_blocks: int 
     From 384 rows a block holds ~100-150 KB of LDS, so one block per CU: a
     grid past 256 blocks runs a second, mostly idle wave (the 384-block SwiGLU
     at 448 rows made the whole step 11 % slower than hipBLASLt).  There the
-    plan minimises waves x staged bytes per block ((weight rows + 64 x MT) x
-    K / S, at the measured ~33 KB/us per CU) plus the split-K partials'
+    plan minimises waves x staged bytes per block ((weight rows + X rows
+    staged, the part rounded to 32) x K / S, at the measured ~33 KB/us per CU) plus the split-K partials'
     round trip, over M parts of 256 / 192 / 128 rows."""
     tiles = (N // 2 if swiglu else N) // 64
     if M >= 384:
         nb = 128 if swiglu else 64
         best = None
         for mparts in sorted({-(-M // 256), -(-M // 192), -(-M // 128)}):
-            mt = -(-((-(-M // mparts) + 15) // 16 * 16) // 64)
+            rows = (-(-M // mparts) + 15) // 16 * 16
+            mt = -(-rows // 64)
             if mt > 4:
                 continue
+            mr = -(-rows // 32) * 32  # X rows the kernel stages (the part rounded to 32)
             for S in ((1,) if swiglu else (1, 2, 4, 8)):
                 if K % (64 * S):
                     continue
                 blocks = tiles * mparts * S
-                us = -(-blocks // 256) * (nb + 64 * mt) * 2 * (K / S) / 33e3 + (0 if swiglu else S * M * N * 8 / 5e6)
+                us = -(-blocks // 256) * (nb + mr) * 2 * (K / S) / 33e3 + (0 if swiglu else S * M * N * 8 / 5e6)
                 key = (round(us, 3), -blocks)
                 if best is None or key < best[0]:
                     best = (key, S, mparts)

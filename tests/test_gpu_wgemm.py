@@ -9,7 +9,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-ROWS = [17, 33, 129, 256, 320, 384, 448, 512]
+ROWS = [17, 33, 78, 129, 256, 320, 384, 448, 512]
 
 
 @pytest.fixture(scope="module")

@@ -111,14 +111,10 @@ __device__ __forceinline__ uint4 fp8x8_to_bf16x8(const uint2& v) {
     return make_uint4(a.x, a.y, b.x, b.y);
 }
 
-// 8 consecutive cache elements at element offset `off` as bf16: a 16-B load
-// of a bf16 cache or an 8-B load + conversion of an fp8 one
+// byte address of element `off` of a bf16 or fp8 (KV8) cache
 template <bool KV8>
-__device__ __forceinline__ uint4 load_kv8(const void* base, size_t off) {
-    if constexpr (KV8)
-        return fp8x8_to_bf16x8(*reinterpret_cast<const uint2*>(static_cast<const uint8_t*>(base) + off));
-    else
-        return *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(base) + off);
+__device__ __forceinline__ const void* kv_ptr(const void* base, size_t off) {
+    return static_cast<const uint8_t*>(base) + off * (KV8 ? 1 : 2);
 }
 
 }  // namespace

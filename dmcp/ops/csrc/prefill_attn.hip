@@ -132,7 +132,14 @@ __device__ __forceinline__ void prefill_attn_block(
         qpos[u] = start + t;
         const uint16_t* qp = q + ((size_t)t * Hq + (size_t)kh * G + g) * D + 8 * h;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) qf[u][ks] = as_bf16x8(*reinterpret_cast<const uint4*>(qp + 16 * ks));
+        for (int ks = 0; ks < KS; ++ks) {
+            qf[u][ks] = as_bf16x8(*reinterpret_cast<const uint4*>(qp + 16 * ks));
+            // re-define the Q registers here (an empty asm "writing" them): the
+            // waitcnt pass otherwise carried the Q loads' scores around the key
+            // loop and made the QK^T MFMAs wait vmcnt(3..0) on each stage's
+            // K/V prefetch
+            asm volatile("" : "+v"(qf[u][ks]));
+        }
         m[u] = -1e30f;  // finite; kept equal across the two lane halves; l is per half
         l[u] = 0.f;
 #pragma unroll
@@ -141,34 +148,39 @@ __device__ __forceinline__ void prefill_attn_block(
             for (int i = 0; i < 16; ++i) o[u][t2][i] = 0.f;
     }
 
-    // register-staged K/V tiles (fp8 caches converted to bf16 here, so the
-    // LDS image and everything after it is the same): rows past kend are zero
-    // (never visible: every such key is after every query of the block)
-    uint4 kx[LU], vx[LU];
+    // register-staged K/V tiles, held RAW while in flight (fp8 caches are
+    // widened to bf16 only in store(), after the stage's compute: converting
+    // at the load made every prefetch wait for its own data -- vmcnt(0) right
+    // behind each load -- so nothing was in flight while a stage computed).
+    // Rows past kend re-read row kend - 1 (a written row: finite), never
+    // visible -- every such key is masked to -inf, so its P is 0.
+    using Raw = std::conditional_t<KV8, uint2, uint4>;
+    Raw kx[LU], vx[LU];
     auto load = [&](int st) {
 #pragma unroll
         for (int i = 0; i < LU; ++i) {
             const int idx = threadIdx.x + i * NT;
             const int row = idx / CH, ch = idx - row * CH;
-            const int key = st * kPfKeys + row;
-            if (key < kend) {
-                const bool pre = key < P;
-                const size_t off = ((size_t)kh * ldk + key) * D + ch * 8;
-                kx[i] = load_kv8<KV8>(pre ? pk : kc, off);
-                vx[i] = load_kv8<KV8>(pre ? pv : vc, off);
-            } else {
-                kx[i] = make_uint4(0, 0, 0, 0);
-                vx[i] = make_uint4(0, 0, 0, 0);
-            }
+            const int key = min(st * kPfKeys + row, kend - 1);
+            const bool pre = key < P;
+            const size_t off = ((size_t)kh * ldk + key) * D + ch * 8;
+            kx[i] = *reinterpret_cast<const Raw*>(kv_ptr<KV8>(pre ? pk : kc, off));
+            vx[i] = *reinterpret_cast<const Raw*>(kv_ptr<KV8>(pre ? pv : vc, off));
         }
+    };
+    auto widen = [&](const Raw& v) -> uint4 {
+        if constexpr (KV8)
+            return fp8x8_to_bf16x8(v);
+        else
+            return v;
     };
     auto store = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < LU; ++i) {
             const int idx = threadIdx.x + i * NT;
             const int row = idx / CH, ch = idx - row * CH;
-            *reinterpret_cast<uint4*>(&sK[buf][pf_off<D>(row, ch)]) = kx[i];
-            *reinterpret_cast<uint4*>(&sV[buf][pf_off<D>(row, ch)]) = vx[i];
+            *reinterpret_cast<uint4*>(&sK[buf][pf_off<D>(row, ch)]) = widen(kx[i]);
+            *reinterpret_cast<uint4*>(&sV[buf][pf_off<D>(row, ch)]) = widen(vx[i]);
         }
     };
 
@@ -182,7 +194,11 @@ __device__ __forceinline__ void prefill_attn_block(
     for (int st = st0; st < st1; ++st) {
         const int buf = st & 1;
         const bool more = st + 1 < st1;
-        if (more) load(st + 1);  // in flight while this stage is computed
+        // the next stage's loads go out after the first tile's QK^T MFMAs
+        // (in flight through the softmax / PV and the second tile): issued
+        // ahead of them, their address registers were reused by the MFMA
+        // destinations and every QK^T MFMA waited on vmcnt
+        bool issued = !more;
         const uint16_t* Kt = sK[buf];
         const uint16_t* Vt = sV[buf];
 #pragma unroll
@@ -208,6 +224,10 @@ __device__ __forceinline__ void prefill_attn_block(
 #pragma unroll
                 for (int u = 0; u < NSUB; ++u)
                     if (act[u]) s[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[u][ks], s[u], 0, 0, 0);
+            }
+            if (!issued) {
+                load(st + 1);
+                issued = true;
             }
             // online softmax; register i holds key kb + (i&3) + 8*(i>>2) + 4*h
             bf16x8_t pb[NSUB][2];
@@ -278,6 +298,7 @@ __device__ __forceinline__ void prefill_attn_block(
                 }
             }
         }
+        if (!issued) load(st + 1);  // both tiles skipped (no query sees them)
         if (more) store(buf ^ 1);  // that buffer's readers finished before the last barrier
         __syncthreads();
     }

@@ -46,6 +46,9 @@ class Config:
     require_enrichment_for_analyze: bool = True  # READ_ONLY_MODE parity
     # local MI355X enrichment backend (extension, see dmcp/enrich/local.py)
     local_llm_preset: str = "dmcp-coder-1b"
+    # a Llama-format checkpoint directory (config.json + *.safetensors +
+    # tokenizer.json) used instead of the random-initialised preset
+    local_llm_model_path: str = ""
     local_llm_kv_dtype: str = "bf16"  # "fp8": e4m3 KV cache (half the decode attention bytes)
     local_llm_max_new_tokens: int = 256
     local_llm_devices: str = "all"
@@ -113,6 +116,7 @@ class Config:
             "ENRICH_BACKEND": "enrich_backend",
             "REQUIRE_ENRICHMENT_FOR_ANALYZE": "require_enrichment_for_analyze",
             "LOCAL_LLM_PRESET": "local_llm_preset",
+            "LOCAL_LLM_MODEL_PATH": "local_llm_model_path",
             "LOCAL_LLM_KV_DTYPE": "local_llm_kv_dtype",
             "LOCAL_LLM_MAX_NEW_TOKENS": "local_llm_max_new_tokens",
             "LOCAL_LLM_DEVICES": "local_llm_devices",

@@ -49,9 +49,10 @@ from typing import Any, Deque, Dict, Iterable, Iterator, List, Optional, Sequenc
 
 import torch
 
-from ..models.llm import BOS, LocalLM, LMConfig, DecodeGraphs, preset
+from ..models.llm import LocalLM, LMConfig, DecodeGraphs, preset
 from .backend import EnrichmentBackend, build_enrichment_prompt
 from .jsonfix import parse_enrichment_response
+from .tokenizer import ByteTokenizer
 from .types import EnrichmentInput, EnrichmentResult
 
 LOG = logging.getLogger(__name__)
@@ -76,6 +77,7 @@ class Segment:
     forced: Optional[bytes] = None   # forced bytes, or None for a free string
     min_len: int = 0
     max_len: int = 0
+    ids: Optional[List[int]] = None  # the forced bytes as tokens (set by the engine's tokenizer)
 
 
 def build_template(inp: EnrichmentInput, desc_len=(8, 96), method_len=(6, 64), step_len=(4, 40),
@@ -147,7 +149,8 @@ class _Seq:
     gen_tokens: int = 0
 
 
-    prompt: Optional[List[int]] = None   # prompt tokens (BOS + bytes)
+    prompt: Optional[List[int]] = None   # prompt tokens ([BOS] + text)
+    prefix_split: int = 0                # leading prompt tokens encoding the text before 'Source of'
 
     @property
     def free_budget(self) -> int:
@@ -236,6 +239,11 @@ class LocalEngine:
     the model's prefix slot; decode reads it through the shared-prefix
     kernel.  A prompt that does not start with it (truncated) is deferred to
     a later pass with its own prefix.
+
+    ``tokenizer``: the vocabulary of ``model`` (:mod:`dmcp.enrich.tokenizer`);
+    default the byte-level one of the built-in presets.  Forced skeleton text
+    is encoded with it, free strings are sampled under masks of its JSON-safe
+    tokens, and a free string closes on its lone ``"`` token.
     """
 
     MASK_NO_QUOTE, MASK_QUOTE = 0, 1
@@ -245,8 +253,13 @@ class LocalEngine:
 
     def __init__(self, model: LocalLM, use_graphs: bool = True, max_prompt_tokens: Optional[int] = None,
                  jump_forward: bool = True, shared_prefix: bool = True, pipeline: bool = True,
-                 admit_min: Optional[int] = None, longest_first: bool = True) -> None:
+                 admit_min: Optional[int] = None, longest_first: bool = True, tokenizer=None) -> None:
         self.model = model
+        self.tok = tokenizer if tokenizer is not None else ByteTokenizer(model.cfg.vocab_size)
+        self._tb = self.tok.token_bytes
+        self._quote = self.tok.quote
+        if len(self._tb) < model.cfg.vocab_size:  # ids the tokenizer does not name append nothing
+            self._tb = list(self._tb) + [b""] * (model.cfg.vocab_size - len(self._tb))
         # admit the pending classes with the longest reply budget first (LPT):
         # the run's tail is then short replies, not a few long ones decoding
         # alone in a nearly empty batch
@@ -258,8 +271,7 @@ class LocalEngine:
         self.admit_min = max(1, admit_min if admit_min is not None else model.cfg.max_batch // 16)
         self.cfg: LMConfig = model.cfg
         dev = model.device
-        self.masks = torch.tensor([_json_safe_mask(self.cfg.vocab_size, False),
-                                   _json_safe_mask(self.cfg.vocab_size, True)], dtype=torch.int32, device=dev)
+        self.masks = torch.tensor(list(self.tok.json_masks(self.cfg.vocab_size)), dtype=torch.int32, device=dev)
         self.graphs = DecodeGraphs(model, self.masks) if use_graphs and dev.type == "cuda" else None
         self.max_prompt_tokens = max_prompt_tokens
         self.jump_forward = jump_forward
@@ -297,16 +309,33 @@ class LocalEngine:
 
     # ------------------------------------------------------------ helpers
     def _prompt(self, seq: _Seq, readme: Optional[str], budget: int) -> List[int]:
-        text = build_enrichment_prompt(seq.inp, readme).encode("utf-8", "replace")
+        """Prompt tokens of ``seq``; sets ``seq.prefix_split``."""
+        ids, split = self.tok.encode_split(build_enrichment_prompt(seq.inp, readme), PREFIX_MARKER.decode())
+        head = 1 if self.tok.bos is not None else 0
         limit = self.cfg.max_seq - budget - 2
         if self.max_prompt_tokens:
             limit = min(limit, self.max_prompt_tokens)
         if limit < 16:
             raise ValueError("KV capacity too small for the reply template")
-        if len(text) > limit:
+        if len(ids) - head > limit:
             keep_tail = min(256, limit // 4)  # keep the instructions at the end
-            text = text[:limit - keep_tail] + text[len(text) - keep_tail:]
-        return [BOS] + list(text)
+            cut = head + limit - keep_tail
+            ids = ids[:cut] + ids[len(ids) - keep_tail:]
+            if split > cut:  # the marker was cut out: no shared prefix
+                split = 0
+        seq.prefix_split = split
+        return ids
+
+    def _seq_prefix_len(self, s: _Seq) -> int:
+        """Tokens of ``s.prompt`` before its per-class part, or 0."""
+        P = s.prefix_split if self.shared_prefix else 0
+        return P if self.MIN_SHARED_PREFIX <= P < len(s.prompt) else 0
+
+    def _encode_forced(self, segs: List[Segment]) -> List[Segment]:
+        for seg in segs:
+            if seg.forced is not None:
+                seg.ids = self.tok.encode_fragment(seg.forced.decode("utf-8"))
+        return segs
 
     def _prompt_prefix_len(self, prompt: List[int]) -> int:
         """Tokens of ``prompt`` before its per-class part (``Source of``)."""
@@ -323,8 +352,8 @@ class LocalEngine:
             seg = s.segs[s.seg]
             if seg.forced is None:
                 return
-            if s.forced_off < len(seg.forced):
-                s.next_token = seg.forced[s.forced_off]
+            if s.forced_off < len(seg.ids):
+                s.next_token = seg.ids[s.forced_off]
                 s.forced_off += 1
                 return
             s.seg += 1
@@ -336,12 +365,12 @@ class LocalEngine:
         """Grammar transition after ``tok`` entered the KV cache.  Returns None
         when the next token is already decided (``s.next_token``) or the reply
         is complete, else whether the sampled token may be the closing quote."""
-        s.out.append(tok & 0xFF)
+        s.out += self._tb[tok]
         s.pos += 1
         s.gen_tokens += 1
         seg = s.segs[s.seg] if s.seg < len(s.segs) else None
         if seg is not None and seg.forced is None:
-            if tok == QUOTE:  # free string closed
+            if tok == self._quote:  # free string closed
                 s.seg += 1
                 s.forced_off = 0
                 s.free_len = 0
@@ -349,7 +378,7 @@ class LocalEngine:
             else:
                 s.free_len += 1
                 if s.free_len >= seg.max_len:
-                    s.next_token = QUOTE
+                    s.next_token = self._quote
                     return None
                 return s.free_len >= seg.min_len
         else:
@@ -383,13 +412,13 @@ class LocalEngine:
         t0 = time.perf_counter()
         reqs = []
         for s in batch:
-            first = s.segs[0].forced or b""
-            toks = s.prompt + list(first)
+            first = s.segs[0].ids or []
+            toks = s.prompt + first
             start = self.model.fork_prefix(s.slot) if prefix else 0
             reqs.append((toks[start:], s.slot, start))
             self.stats["prompt_tokens"] += len(toks) - start
             s.prompt_tokens = len(s.prompt)
-            s.out.extend(first)
+            s.out.extend(s.segs[0].forced or b"")
             s.pos = len(toks)
             s.seg, s.forced_off = 1, 0
         need = [i for i, s in enumerate(batch) if s.seg < len(s.segs) and s.segs[s.seg].forced is None]
@@ -509,7 +538,7 @@ class LocalEngine:
                 want = len(free_slots) + lookahead - len(pending)
                 if want > 0 and not feed.done:
                     for key, inp in feed.take(want, wait=not active and not pending and inflight is None):
-                        s = _Seq(inp, key, fit_template(inp, reply_cap))
+                        s = _Seq(inp, key, self._encode_forced(fit_template(inp, reply_cap)))
                         try:
                             s.prompt = self._build_prompt(s, readme)
                         except Exception as e:
@@ -517,7 +546,7 @@ class LocalEngine:
                             continue
                         if not decided:
                             decided = True
-                            P = self._prompt_prefix_len(s.prompt)
+                            P = self._seq_prefix_len(s)
                             if P:
                                 prefix_toks = s.prompt[:P]
                                 t0 = time.perf_counter()
@@ -678,14 +707,14 @@ class LocalLLMBackend(EnrichmentBackend):
             devices = list(range(n)) if spec == "all" else [int(x) for x in spec.split(",") if x.strip()]
         if not devices:
             raise RuntimeError("LocalLLMBackend needs a ROCm GPU (torch.cuda.is_available() is False)")
+        mb = int(cfg.local_llm_max_batch)
+        spec = {"preset": cfg.local_llm_preset, "kv_dtype": cfg.local_llm_kv_dtype, "max_batch": mb,
+                "max_rows": max(256, mb * 3 // 2), "seed": 0, "path": cfg.local_llm_model_path}
         engines = []
         for d in devices:
             with torch.cuda.device(d):
-                model = LocalLM(preset(cfg.local_llm_preset, kv_dtype=cfg.local_llm_kv_dtype,
-                                       max_batch=cfg.local_llm_max_batch,
-                                       max_rows=max(256, cfg.local_llm_max_batch * 3 // 2)),
-                                device=f"cuda:{d}", seed=0)
-                engines.append(LocalEngine(model))
+                model, tok = build_model(spec, f"cuda:{d}")
+                engines.append(LocalEngine(model, tokenizer=tok))
         return cls(engines)
 
     def enrich_class(self, inp: EnrichmentInput, readme: Optional[str]) -> EnrichmentResult:
@@ -730,6 +759,20 @@ class LocalLLMBackend(EnrichmentBackend):
             for k, v in e.stats.items():
                 agg[k] = agg.get(k, 0) + v
         return agg
+
+
+def build_model(spec: dict, device: str):
+    """(LocalLM, tokenizer) of a worker model spec: the checkpoint directory
+    ``spec["path"]`` (its own tokenizer) or the random-initialised preset
+    ``spec["preset"]`` (byte-level tokenizer: ``None`` = the engine default);
+    ``kv_dtype`` / ``max_batch`` / ``max_rows`` / ``max_seq`` override either."""
+    overrides = {k: spec[k] for k in ("kv_dtype", "max_batch", "max_rows", "max_seq") if k in spec}
+    if spec.get("path"):
+        from .tokenizer import load_local_model
+        return load_local_model(spec["path"], device=device, **overrides)
+    model = LocalLM(preset(spec.get("preset", "dmcp-coder-1b"), **overrides), device=device,
+                    seed=int(spec.get("seed", 0)))
+    return model, None
 
 
 def _parse(raw: str, name: str) -> EnrichmentResult:

@@ -410,6 +410,8 @@ class ProcessLLMBackend(EnrichmentBackend):
         mb = int(cfg.local_llm_max_batch)
         model = {"preset": cfg.local_llm_preset, "kv_dtype": cfg.local_llm_kv_dtype, "max_batch": mb,
                  "max_rows": max(256, mb * 3 // 2), "seed": 0}
+        if getattr(cfg, "local_llm_model_path", ""):
+            model["path"] = cfg.local_llm_model_path
         return cls(GpuWorkerPool(devices, model))
 
     def enrich_class(self, inp: EnrichmentInput, readme: Optional[str]) -> EnrichmentResult:
@@ -465,17 +467,14 @@ def worker_main() -> int:
     if msg is None or msg.get("op") != "init":
         return 0 if msg is None or msg.get("op") == "shutdown" else 2
     import torch
-    from ..models.llm import LocalLM, preset
-    from .local import LocalEngine, QueueFeed
+    from .local import LocalEngine, QueueFeed, build_model
     spec = msg["model"]
     dev = msg.get("device", "cuda:0")
     try:
         if dev.startswith("cuda"):
             torch.cuda.set_device(0)
-        overrides = {k: spec[k] for k in ("kv_dtype", "max_batch", "max_rows", "max_seq") if k in spec}
-        model = LocalLM(preset(spec.get("preset", "dmcp-coder-1b"), **overrides), device=dev,
-                        seed=int(spec.get("seed", 0)))
-        eng = LocalEngine(model, **(msg.get("engine") or {}))
+        model, tok = build_model(spec, dev)
+        eng = LocalEngine(model, tokenizer=tok, **(msg.get("engine") or {}))
     except Exception as e:
         send({"op": "error", "msg": f"init failed: {e!r}"})
         return 3

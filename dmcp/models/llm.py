@@ -443,8 +443,11 @@ class LocalLM:
         return F.linear(h.index_select(0, last), self.w["lm_head"])
 
     @torch.inference_mode()
-    def decode(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:
-        """One token per row; all inputs int32 [B] on device.
+    def decode(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor,
+               src: Optional[torch.Tensor] = None, last_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One token per row; all inputs int32 [B] on device.  With ``src`` /
+        ``last_ids``: row r's token is ``last_ids[src[r]]`` where ``src[r] >= 0``
+        (gathered on the device by the step's first kernel).
 
         Rows are independent (slot, position) pairs: several rows may extend
         the SAME slot at consecutive positions (jump-forward over forced
@@ -457,12 +460,10 @@ class LocalLM:
         if B > self.max_rows:
             raise ValueError(f"decode: {B} rows > max_rows {self.max_rows}")
         if self.use_fused and B <= self.fused_max_rows:
-            return self._decode_fused(tokens, slots, positions)
-        seq_len = positions + 1
+            return self._decode_fused(tokens, slots, positions, src, last_ids)
         chunk, splits = ops.decode_plan(B, c.n_kv_heads, c.max_seq, c.kv_dtype)
-        x = ops.embedding(self.w["embed"], tokens)
-        resid = x.clone()
-        h = ops.add_rmsnorm(x, self.w["l0.ln1"], c.eps)
+        resid, h, seq_len = ops.decode_embed_norm(self.w["embed"], tokens, positions, self.w["l0.ln1"], c.eps,
+                                                  src, last_ids)
         wide = self.use_wgemm and B <= ops.WGEMM_MAX_ROWS
         for i in range(c.layers):
             kc, vc = self.k_cache[i], self.v_cache[i]
@@ -491,16 +492,16 @@ class LocalLM:
         return ops.SharedPrefix(self.k_cache[i][self.prefix_slot], self.v_cache[i][self.prefix_slot],
                                 self.prefix_dev)
 
-    def _decode_fused(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:
+    def _decode_fused(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor,
+                      src: Optional[torch.Tensor] = None, last_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
         """The decode step on the fused gfx950 GEMMs: per layer QKV (+norm,
         RoPE, KV append) -> attention -> O (+residual) -> gate/up (+norm,
         SwiGLU) -> down (+residual); the residual stream ``r`` is updated in
         place by the O / down epilogues."""
         c = self.cfg
         B = tokens.shape[0]
-        seq_len = positions + 1
         chunk, splits = ops.decode_plan(B, c.n_kv_heads, c.max_seq, c.kv_dtype)
-        r = ops.embedding(self.w["embed"], tokens)
+        r, _, seq_len = ops.decode_embed_norm(self.w["embed"], tokens, positions, None, c.eps, src, last_ids)
         for i in range(c.layers):
             kc, vc = self.k_cache[i], self.v_cache[i]
             q = ops.fused_rope_kv(r, self.w[f"l{i}.wqkv"], c.eps, positions, slots, self.cos_sin, kc, vc, c.n_heads)
@@ -572,10 +573,8 @@ class LocalLM:
         t+1 before it has read step t's ids (the engine's one-step pipeline).
         Capturable."""
         B = tokens.shape[0]
-        gathered = last_ids.index_select(0, src.clamp(min=0).long())
-        toks = torch.where(src >= 0, gathered, tokens)
-        logits, ids = self.decode_select(toks, slots, positions, masks, mask_idx)
-        last_ids[:B].copy_(ids)
+        logits = self.decode(tokens, slots, positions, src=src, last_ids=last_ids)
+        ids = ops.masked_argmax(logits, masks, vocab=self.cfg.vocab_size, mask_idx=mask_idx, out=last_ids[:B])
         return logits, ids
 
     # reference path (pure torch, fp32 math) for numerics tests

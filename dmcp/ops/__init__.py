@@ -65,6 +65,12 @@ def embedding(table, ids, out=None):
     return _on(table).embedding(table, ids, out)
 
 
+def decode_embed_norm(table, tokens, positions, weight, eps, src=None, last_ids=None):
+    """(resid, h, seq_len) of a decode step: each row's token (``last_ids[src]``
+    where ``src >= 0``), its embedding, its first RMSNorm, its length."""
+    return _on(table).decode_embed_norm(table, tokens, positions, weight, eps, src, last_ids)
+
+
 # GPU-only fused GEMM with a shape-dependent default
 def fused_resid(x, w, residual, wk: int = 0):
     """residual += x . w^T in one gfx950 kernel; K-split waves by K."""

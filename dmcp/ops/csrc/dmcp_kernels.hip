@@ -361,6 +361,79 @@ __global__ __launch_bounds__(kBlock) void embedding_kernel(const uint16_t* __res
     }
 }
 
+// --------------------------------------------------------------------------
+// 7. decode-step inputs in one launch (one block per row): the row's token
+//    (tok = src[r] >= 0 ? last_ids[src[r]] : tokens[r] -- the previous step's
+//    selection still on the device, the engine's one-step pipeline), its
+//    embedding row into the residual stream, the first RMSNorm of it into h
+//    (skipped when h is null) and seq_len[r] = pos[r] + 1.  Replaces an
+//    index_select / where / clamp / compare / embedding / clone / add_rmsnorm
+//    / add chain of 7 launches per decode step.
+// --------------------------------------------------------------------------
+template <int VPT>
+__global__ __launch_bounds__(kBlock) void decode_embed_norm_kernel(
+    const uint16_t* __restrict__ table, const int32_t* __restrict__ tokens, const int32_t* __restrict__ src,
+    const int32_t* __restrict__ last_ids, const int32_t* __restrict__ pos, const uint16_t* __restrict__ w,
+    uint16_t* __restrict__ resid, uint16_t* __restrict__ h, int32_t* __restrict__ seq_len, int H, int V,
+    int n_last, float eps) {
+    const int row = blockIdx.x;
+    int id = tokens[row];
+    if (src) {
+        const int s = src[row];
+        if (s >= 0) id = last_ids[s < n_last ? s : n_last - 1];
+    }
+    id = id < 0 ? 0 : (id >= V ? V - 1 : id);
+    if (threadIdx.x == 0) seq_len[row] = pos[row] + 1;
+    const int nvec = H >> 3;
+    const uint4* er = reinterpret_cast<const uint4*>(table + (size_t)id * H);
+    uint4* rr = reinterpret_cast<uint4*>(resid + (size_t)row * H);
+    uint4 xv[VPT], wv[VPT];
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int idx = threadIdx.x + i * kBlock;
+        if (idx < nvec) {
+            xv[i] = er[idx];
+            if (h) wv[i] = reinterpret_cast<const uint4*>(w)[idx];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int idx = threadIdx.x + i * kBlock;
+        if (idx < nvec) rr[idx] = xv[i];
+    }
+    if (!h) return;
+    float x[VPT][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int idx = threadIdx.x + i * kBlock;
+        if (idx < nvec) {
+            unpack8(xv[i], x[i]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ss += x[i][j] * x[i][j];
+        }
+    }
+    __shared__ float red[kBlock / kWave];
+    ss = wave_sum(ss);
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int k = 0; k < kBlock / kWave; ++k) tot += red[k];
+    const float inv = rsqrtf(tot / (float)H + eps);
+    uint4* orow = reinterpret_cast<uint4*>(h + (size_t)row * H);
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int idx = threadIdx.x + i * kBlock;
+        if (idx < nvec) {
+            float wf[8], o[8];
+            unpack8(wv[i], wf);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = x[i][j] * inv * wf[j];
+            orow[idx] = pack8(o);
+        }
+    }
+}
 
 // One 32-key tile of a (slot, kv head): K rows as the S^T A operand (key
 // kt + 16h + (lane&15), dims 32ks + 8*(lane>>4)) and the V tile (32 x D,
@@ -762,7 +835,7 @@ hipError_t launch_combine(void* part_o, void* part_ml, const int32_t* sl, const 
 
 extern "C" {
 
-int dmcp_abi_version() { return 10; }
+int dmcp_abi_version() { return 11; }
 
 int dmcp_add_rmsnorm(const void* x, void* residual, const void* w, void* out, int rows, int H, float eps,
                      void* stream) {
@@ -875,6 +948,25 @@ int dmcp_masked_argmax(const void* logits, const void* mask, const void* mask_id
     masked_argmax_kernel<<<B, kBlock, 0, (hipStream_t)stream>>>((const uint16_t*)logits, (const uint32_t*)mask,
                                                                (const int32_t*)mask_idx, n_masks, (int32_t*)ids, V,
                                                                ld);
+    return hipGetLastError();
+}
+
+int dmcp_decode_embed_norm(const void* table, const void* tokens, const void* src, const void* last_ids,
+                           const void* pos, const void* w, void* resid, void* h, void* seq_len, int rows, int H,
+                           int V, int n_last, float eps, void* stream) {
+    if (H % 8 != 0 || H > kBlock * 8 * 4 || V <= 0 || (src && (!last_ids || n_last <= 0)) || (h && !w))
+        return hipErrorInvalidValue;
+    if (rows <= 0) return 0;
+    auto st = (hipStream_t)stream;
+    const int vpt = (H + kBlock * 8 - 1) / (kBlock * 8);
+    auto args = [&](auto kern) {
+        kern<<<rows, kBlock, 0, st>>>((const uint16_t*)table, (const int32_t*)tokens, (const int32_t*)src,
+                                      (const int32_t*)last_ids, (const int32_t*)pos, (const uint16_t*)w,
+                                      (uint16_t*)resid, (uint16_t*)h, (int32_t*)seq_len, H, V, n_last, eps);
+    };
+    if (vpt == 1) args(decode_embed_norm_kernel<1>);
+    else if (vpt == 2) args(decode_embed_norm_kernel<2>);
+    else args(decode_embed_norm_kernel<4>);
     return hipGetLastError();
 }
 

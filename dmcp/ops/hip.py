@@ -26,7 +26,7 @@ _lock = threading.Lock()
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _f = ctypes.c_float
-ABI_VERSION = 10  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
+ABI_VERSION = 11  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
 
 
 class HipOpsError(RuntimeError):
@@ -61,6 +61,7 @@ def lib() -> ctypes.CDLL:
             "dmcp_silu_mul": ([_vp, _vp, _i, _i, _vp], _i),
             "dmcp_masked_argmax": ([_vp, _vp, _vp, _i, _vp, _i, _i, _i, _vp], _i),
             "dmcp_embedding": ([_vp, _vp, _vp, _i, _i, _i, _vp], _i),
+            "dmcp_decode_embed_norm": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp], _i),
             "dmcp_fused_gemm_max_rows": ([], _i),
             "dmcp_wgemm": ([_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp], _i),
             "dmcp_wgemm_resid_norm": ([_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _vp], _i),
@@ -470,6 +471,43 @@ def embedding(table: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor
     _req_out(out, torch.bfloat16, T * H, "embedding.out")
     _check(lib().dmcp_embedding(_ptr(table), _ptr(ids), _ptr(out), T, H, V, _stream()), "dmcp_embedding")
     return out
+
+
+def decode_embed_norm(table: torch.Tensor, tokens: torch.Tensor, positions: torch.Tensor,
+                      weight: Optional[torch.Tensor], eps: float, src: Optional[torch.Tensor] = None,
+                      last_ids: Optional[torch.Tensor] = None) -> tuple:
+    """Decode-step inputs in one launch: row r's token is
+    ``last_ids[src[r]]`` where ``src[r] >= 0`` (else ``tokens[r]``); returns
+    (resid = its embedding row, h = RMSNorm(resid) * weight -- None when
+    ``weight`` is None --, seq_len = positions + 1).  Capturable."""
+    _req(table, torch.bfloat16, "decode_embed_norm.table")
+    _req(tokens, torch.int32, "decode_embed_norm.tokens")
+    _req(positions, torch.int32, "decode_embed_norm.positions")
+    V, H = table.shape
+    B = tokens.numel()
+    if H % 8 or H > 8192:
+        raise HipOpsError(f"decode_embed_norm: unsupported hidden size {H}")
+    if positions.numel() != B:
+        raise HipOpsError("decode_embed_norm: tokens / positions length mismatch")
+    if weight is not None:
+        _req(weight, torch.bfloat16, "decode_embed_norm.weight")
+        if weight.numel() != H:
+            raise HipOpsError("decode_embed_norm: weight size != hidden")
+    if (src is None) != (last_ids is None):
+        raise HipOpsError("decode_embed_norm: src and last_ids go together")
+    if src is not None:
+        _req(src, torch.int32, "decode_embed_norm.src")
+        _req(last_ids, torch.int32, "decode_embed_norm.last_ids")
+        if src.numel() != B or last_ids.numel() == 0:
+            raise HipOpsError("decode_embed_norm: src length / last_ids size")
+    resid = torch.empty((B, H), dtype=torch.bfloat16, device=table.device)
+    h = torch.empty_like(resid) if weight is not None else None
+    seq_len = torch.empty(B, dtype=torch.int32, device=table.device)
+    _check(lib().dmcp_decode_embed_norm(_ptr(table), _ptr(tokens), _ptr(src), _ptr(last_ids), _ptr(positions),
+                                        _ptr(weight), _ptr(resid), _ptr(h), _ptr(seq_len), B, H, V,
+                                        0 if last_ids is None else last_ids.numel(), float(eps), _stream()),
+           "dmcp_decode_embed_norm")
+    return resid, h, seq_len
 
 
 # ------------------------------------------------------------------ fused GEMMs

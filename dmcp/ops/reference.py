@@ -198,3 +198,17 @@ def embedding(table: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor
         out.copy_(y)
         return out
     return y
+
+
+def decode_embed_norm(table: torch.Tensor, tokens: torch.Tensor, positions: torch.Tensor,
+                      weight: Optional[torch.Tensor], eps: float, src: Optional[torch.Tensor] = None,
+                      last_ids: Optional[torch.Tensor] = None) -> tuple:
+    """(resid, h, seq_len) of the decode step's first op (see the HIP kernel)."""
+    toks = tokens
+    if src is not None:
+        s = src.long()
+        gathered = last_ids.long()[s.clamp(0, last_ids.numel() - 1)].to(tokens.dtype)
+        toks = torch.where(s >= 0, gathered, tokens)
+    resid = embedding(table, toks)
+    h = add_rmsnorm(resid, weight, eps) if weight is not None else None
+    return resid, h, positions + 1

@@ -221,3 +221,30 @@ def test_shape_validation_raises(hip):
         hip.rope_kv(_bf(2, 6 * 64), torch.zeros(2, dtype=torch.int32, device="cuda"),
                     torch.zeros(2, dtype=torch.int32, device="cuda"), cos_sin, _bf(1, 1, 16, 64), _bf(1, 1, 16, 64),
                     4, q_out=_bf(1, 4, 64))
+
+
+@pytest.mark.parametrize("H,with_norm,with_src", [(2048, True, True), (256, True, False), (4096, False, True),
+                                                  (3072, True, True)])
+def test_decode_embed_norm_matches_reference(H, with_norm, with_src):
+    """Decode-step inputs in one launch (token select from the previous step's
+    ids, embedding, first RMSNorm, seq_len) vs the fp32 reference."""
+    from dmcp.ops import hip, reference
+    g = torch.Generator().manual_seed(H)
+    V, B = 320, 77
+    table = torch.randn(V, H, generator=g).to(torch.bfloat16).cuda()
+    w = (torch.rand(H, generator=g) + 0.5).to(torch.bfloat16).cuda() if with_norm else None
+    tokens = torch.randint(-3, V + 3, (B,), generator=g, dtype=torch.int32).cuda()  # clamped like the embedding
+    pos = torch.randint(0, 8000, (B,), generator=g, dtype=torch.int32).cuda()
+    src = last = None
+    if with_src:
+        src = torch.randint(-1, 96, (B,), generator=g, dtype=torch.int32).cuda()
+        last = torch.randint(0, V, (96,), generator=g, dtype=torch.int32).cuda()
+    r, h, sl = hip.decode_embed_norm(table, tokens, pos, w, 1e-5, src, last)
+    rr, hr, slr = reference.decode_embed_norm(table.cpu().float(), tokens.cpu(), pos.cpu(),
+                                              None if w is None else w.cpu().float(), 1e-5,
+                                              None if src is None else src.cpu(), None if last is None else last.cpu())
+    assert torch.equal(r.cpu().float(), rr.float()) and torch.equal(sl.cpu(), slr)
+    if with_norm:
+        torch.testing.assert_close(h.cpu().float(), hr.float(), atol=2e-2, rtol=2e-2)
+    else:
+        assert h is None

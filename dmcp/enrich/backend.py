@@ -37,9 +37,28 @@ from .types import (BatchClassInput, ClassAnalysisResult, EnrichmentInput, Enric
 
 LOG = logging.getLogger(__name__)
 
+# The per-project part (task, reply schema, rules, README) comes first and
+# everything per class after "Source of": a local engine prefills that part
+# once per project and reads it through the shared-prefix attention, so each
+# class costs only its own source and facts (dmcp/enrich/local.py).
 ENRICHMENT_PROMPT = """\
-You are adding business context to one {language} source file that has already been
-parsed statically.
+You are adding business context to the source files of one project that have already
+been parsed statically, one file per request.
+
+Describe what the code means for the business, not how it is implemented.
+Answer with exactly one JSON object of this shape and nothing else:
+{{
+  "description": "one sentence on the business purpose of this class/module",
+  "classTypeCorrection": "a corrected class type, or null when the extracted class type is right",
+  "methods": [
+    {{"methodName": "a method name from the extracted method list",
+      "description": "one sentence of business meaning",
+      "businessLogic": ["business step 1", "business step 2"]}}
+  ]
+}}
+Rules: cover every listed method; change the class type only when it is clearly wrong
+(valid types: CONTROLLER, SERVICE, REPOSITORY, ENTITY, DTO, CONFIGURATION, LISTENER,
+UTILITY, EXCEPTION, OTHER); the first character of the reply must be {{ and the last }}.
 
 Project context (README):
 {readme}
@@ -53,20 +72,7 @@ Statically extracted facts:
 - Class type: {class_type}
 - Methods: {methods}
 
-Describe what this code means for the business, not how it is implemented.
-Answer with exactly one JSON object of this shape and nothing else:
-{{
-  "description": "one sentence on the business purpose of this class/module",
-  "classTypeCorrection": "a corrected class type, or null when {class_type} is right",
-  "methods": [
-    {{"methodName": "a method name from the list above",
-      "description": "one sentence of business meaning",
-      "businessLogic": ["business step 1", "business step 2"]}}
-  ]
-}}
-Rules: cover every listed method; change the class type only when it is clearly wrong
-(valid types: CONTROLLER, SERVICE, REPOSITORY, ENTITY, DTO, CONFIGURATION, LISTENER,
-UTILITY, EXCEPTION, OTHER); the first character of the reply must be {{ and the last }}.
+The JSON object for {name}:
 """
 
 ANALYSIS_PROMPT = """\

@@ -11,6 +11,13 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X); run with -m gpu on the GPU box")
     config.addinivalue_line("markers", "slow: long-running test")
+    if os.environ.get("PYTEST_XDIST_WORKER"):
+        # parallel workers share the CPUs: one intra-op pool per worker of the
+        # machine's size oversubscribes it (spinning OpenMP threads made the
+        # CPU-reference engine tests ~100x slower under -n 6)
+        import torch
+        n = int(os.environ.get("PYTEST_XDIST_WORKER_COUNT", "1"))
+        torch.set_num_threads(max(1, (os.cpu_count() or 2) // max(1, n)))
 
 
 @pytest.fixture(scope="session", autouse=True)

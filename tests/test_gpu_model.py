@@ -13,7 +13,7 @@ def model():
     from dmcp.models.llm import LocalLM, preset
     from dmcp.ops import hip
     hip.lib()
-    return LocalLM(preset("tiny", max_batch=16), device="cuda")
+    return LocalLM(preset("tiny", max_batch=16, max_seq=2048), device="cuda")
 
 
 def _rel_err(a, b):

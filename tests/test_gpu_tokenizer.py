@@ -26,7 +26,7 @@ def test_checkpoint_prefill_matches_reference(ckpt):
     from dmcp.enrich.tokenizer import load_local_model
     from dmcp.ops import hip
     hip.lib()
-    model, tok = load_local_model(ckpt, device="cuda", max_batch=8, max_rows=64, max_seq=1024)
+    model, tok = load_local_model(ckpt, device="cuda", max_batch=8, max_rows=64, max_seq=2048)
     toks = [0] + tok.encode("public class OrderService { void create() {} }")
     got = model.forward_tokens(torch.tensor(toks, dtype=torch.int32), 1, 0).float()
     ref = model.reference_logits(toks)[-1].float()
@@ -38,7 +38,7 @@ def test_checkpoint_engine_on_gpu(ckpt, kv_dtype):
     from dmcp.enrich.local import LocalEngine
     from dmcp.enrich.tokenizer import load_local_model
     from dmcp.enrich.types import EnrichmentInput
-    model, tok = load_local_model(ckpt, device="cuda", max_batch=8, max_rows=64, max_seq=1024, kv_dtype=kv_dtype)
+    model, tok = load_local_model(ckpt, device="cuda", max_batch=8, max_rows=64, max_seq=2048, kv_dtype=kv_dtype)
     eng = LocalEngine(model, tokenizer=tok)
     assert eng.graphs is not None and eng.masks.shape == (2, 512 // 32)
     readme = "Shop service: orders, payments and stock reservations. " * 4

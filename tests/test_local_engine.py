@@ -16,7 +16,7 @@ from dmcp.models.llm import LocalLM, preset
 @pytest.fixture(scope="module")
 def tiny():
     torch.manual_seed(0)
-    return LocalLM(preset("tiny", max_batch=4, max_rows=16, max_seq=768), device="cpu", seed=1)
+    return LocalLM(preset("tiny", max_batch=4, max_rows=16, max_seq=2048), device="cpu", seed=1)
 
 
 def _inputs(n):

@@ -125,7 +125,7 @@ def test_sentencepiece_style_tokenizer(tmp_path):
 
 
 def test_checkpoint_engine_generates_schema_valid_json(ckpt):
-    model, tok = load_local_model(ckpt, device="cpu", max_batch=3, max_rows=24, max_seq=768)
+    model, tok = load_local_model(ckpt, device="cpu", max_batch=3, max_rows=24, max_seq=2048)
     assert model.cfg.vocab_size == 512 and model.cfg.hidden == 256
     eng = LocalEngine(model, tokenizer=tok, use_graphs=False)
     readme = "Shop service: orders, payments and stock reservations. " * 3

@@ -158,3 +158,20 @@ def test_config_reads_model_path(tmp_path):
     from dmcp.config import Config
     assert Config.from_env({"LOCAL_LLM_MODEL_PATH": str(tmp_path)}).local_llm_model_path == str(tmp_path)
     assert Config.from_env({}).local_llm_model_path == ""
+
+
+def test_worker_process_serves_a_checkpoint(ckpt):
+    """The service path (one worker process per device) with LOCAL_LLM_MODEL_PATH:
+    the worker loads the checkpoint and its tokenizer, replies parse."""
+    from dmcp.enrich.workers import GpuWorkerPool, ProcessLLMBackend
+    pool = GpuWorkerPool(["cpu"], {"path": ckpt, "max_batch": 2, "max_rows": 16, "max_seq": 2048},
+                         engine={"use_graphs": False}, start_timeout_s=300, env_extra={"OMP_NUM_THREADS": "2"})
+    try:
+        be = ProcessLLMBackend(pool)
+        inputs = [EnrichmentInput("class A%d { void run() {} }" % i, f"co.A{i}", "java", "OTHER", ["run"])
+                  for i in range(3)]
+        res = be.enrich_batch(inputs, "Shop README. " * 4)
+        assert all(r.success for r in res), [r.error_message for r in res]
+        assert [r.methods[0].method_name for r in res] == ["run"] * 3
+    finally:
+        pool.close()

@@ -337,15 +337,6 @@ class LocalEngine:
                 seg.ids = self.tok.encode_fragment(seg.forced.decode("utf-8"))
         return segs
 
-    def _prompt_prefix_len(self, prompt: List[int]) -> int:
-        """Tokens of ``prompt`` before its per-class part (``Source of``)."""
-        if not self.shared_prefix:
-            return 0
-        raw = bytes(t for t in prompt[1:2 + 4 * self.cfg.max_seq] if t < 256)
-        i = raw.find(PREFIX_MARKER)
-        P = 1 + i if i >= 0 else 0
-        return P if self.MIN_SHARED_PREFIX <= P < len(prompt) else 0
-
     def _advance_forced(self, s: _Seq) -> None:
         """Sets next_token from the current forced segment or finishes."""
         while s.seg < len(s.segs):

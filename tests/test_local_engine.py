@@ -125,16 +125,22 @@ def test_shared_prefix_cpu_matches_full_prompt(tiny):
 def test_engine_prompt_prefix_detection(tiny):
     """The shared prefix is everything before 'Source of' (instructions +
     README: the same for every class of a project)."""
+    from dmcp.enrich.local import _Seq
     eng = LocalEngine(tiny, use_graphs=False)
     readme = "A README shared by every prompt of the batch. " * 3
-    from dmcp.enrich.backend import build_enrichment_prompt
-    a = [256] + list(build_enrichment_prompt(_inputs(1)[0], readme).encode())
-    P = eng._prompt_prefix_len(a)
-    assert P > 64 and bytes(a[P:P + 10]) == b"Source of "
-    b = [256] + list(build_enrichment_prompt(_inputs(2)[1], readme).encode())
+
+    def seq(inp):
+        s = _Seq(inp, 0, eng._encode_forced(fit_template(inp, 512)))
+        s.prompt = eng._build_prompt(s, readme)
+        return s
+    sa, sb = seq(_inputs(1)[0]), seq(_inputs(2)[1])
+    a, b = sa.prompt, sb.prompt
+    P = eng._seq_prefix_len(sa)
+    assert P > 64 and bytes(a[P:P + 10]) == b"Source of " and eng._seq_prefix_len(sb) == P
     assert a[:P] == b[:P] and a[P + 10:] != b[P + 10:]
-    assert eng._prompt_prefix_len([256] + list(b"Source of x")) == 0  # below the minimum
-    assert LocalEngine(tiny, use_graphs=False, shared_prefix=False)._prompt_prefix_len(a) == 0
+    short = _Seq(_inputs(1)[0], 0, [], prompt=[256] + list(b"Source of x"), prefix_split=1)
+    assert eng._seq_prefix_len(short) == 0  # below the minimum
+    assert LocalEngine(tiny, use_graphs=False, shared_prefix=False)._seq_prefix_len(sa) == 0
     out = eng.generate(_inputs(5), readme)
     assert eng.stats["prefix_tokens"] == P and all(json.loads(o) for o in out)
     assert eng.stats["prefill_batches"] < eng.stats["prefills"]  # admitted classes share one prefill pass

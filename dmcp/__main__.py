@@ -97,8 +97,7 @@ def main(argv: Optional[List[str]] = None) -> int:
             from .parallel.bulk import bulk_analyze, parse_repo_list
             with open(args.file, encoding="utf-8") as f:
                 items = parse_repo_list(f.read())
-            res = bulk_analyze(app.config, items, args.workers, not args.no_fix_missed,
-                               app=app if args.workers <= 1 else None)
+            res = bulk_analyze(app.config, items, args.workers, not args.no_fix_missed, app=app)
             failed = sum(1 for x in res if not x.success)
             print(json.dumps({"total": len(res), "success": len(res) - failed, "failed": failed,
                               "results": [asdict(x) for x in res]}, indent=2))

@@ -339,6 +339,61 @@ def parse_analysis_response(raw: str, full_class_name: str, source_file: Optiona
                                   root.get("sourceFile") or source_file, methods)
 
 
+class LazyBackend(EnrichmentBackend):
+    """A backend built on its first enrichment call.
+
+    The local MI355X backend spawns one worker process per GPU and each
+    allocates a KV-cache slab of tens of GB; a process that never enriches
+    -- the read-only MCP server (``application-mcp.yml:1-8``: no web stack,
+    only the 9 query tools), a REST instance that only answers queries --
+    must not pay for it.  ``enabled`` is known without building (analysis
+    mode checks it, ``CodeContextService.java:149-156``)."""
+
+    def __init__(self, factory: Callable[[], EnrichmentBackend], name: str = "lazy",
+                 enabled: bool = True) -> None:
+        super().__init__(1)
+        self._factory = factory
+        self._enabled = enabled
+        self._built: Optional[EnrichmentBackend] = None
+        self._build_lock = threading.Lock()
+        self.name = name
+
+    @property
+    def enabled(self) -> bool:
+        return self._enabled
+
+    @property
+    def built(self) -> bool:
+        return self._built is not None
+
+    def get(self) -> EnrichmentBackend:
+        with self._build_lock:
+            if self._built is None:
+                LOG.info("Starting the %s enrichment backend", self.name)
+                self._built = self._factory()
+            return self._built
+
+    def enrich_class(self, inp: EnrichmentInput, readme: Optional[str]) -> EnrichmentResult:
+        return self.get().enrich_class(inp, readme)
+
+    def enrich_batch(self, inputs: Sequence[EnrichmentInput], readme: Optional[str]) -> List[EnrichmentResult]:
+        return self.get().enrich_batch(inputs, readme)
+
+    def enrich_stream(self, inputs: Iterable[EnrichmentInput], readme: Optional[str]
+                      ) -> Iterator[Tuple[int, EnrichmentResult]]:
+        return self.get().enrich_stream(inputs, readme)
+
+    def stats(self) -> dict:
+        b = self._built
+        return b.stats() if b is not None and hasattr(b, "stats") else {}
+
+    def close(self) -> None:
+        with self._build_lock:
+            if self._built is not None:
+                self._built.close()
+        super().close()
+
+
 def create_backend(cfg) -> EnrichmentBackend:
     """Backend selection from :class:`dmcp.config.Config`."""
     kind = cfg.resolved_enrich_backend()
@@ -350,6 +405,8 @@ def create_backend(cfg) -> EnrichmentBackend:
     if kind == "fake":
         return FakeBackend(cfg.enrich_max_concurrent)
     if kind == "local":
-        from .local import LocalLLMBackend
-        return LocalLLMBackend.from_config(cfg)
+        def build() -> EnrichmentBackend:
+            from .local import LocalLLMBackend
+            return LocalLLMBackend.from_config(cfg)
+        return LazyBackend(build, "local")
     return NullBackend(1)

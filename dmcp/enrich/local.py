@@ -61,6 +61,7 @@ QUOTE = ord('"')
 
 
 def _json_safe_mask(vocab: int, with_quote: bool) -> List[int]:
+    """The byte vocabulary's free-text mask (tests; engines use the tokenizer's)."""
     words = [0] * ((vocab + 31) // 32)
     for b in range(0x20, 0x7F):
         if b in (QUOTE, ord("\\")):
@@ -71,32 +72,40 @@ def _json_safe_mask(vocab: int, with_quote: bool) -> List[int]:
     # int32 view of the uint32 bit pattern
     return [w - (1 << 32) if w >= (1 << 31) else w for w in words]
 
+# The reference's reply contract (ClaudeApiClient.java:101-120): the model may
+# correct the statically inferred class type (null = keep it; applied at
+# CodeContextService.java:635-637) and writes 1..N business-logic steps per
+# method.  Both are grammar CHOICES here: the model picks among the
+# alternatives' bytes under per-state vocabulary masks.
+CLASS_TYPES = ("CONTROLLER", "SERVICE", "REPOSITORY", "ENTITY", "DTO", "CONFIGURATION", "LISTENER", "UTILITY",
+               "EXCEPTION", "OTHER")
+CHOICE_CLASS_TYPE = 0   # null, or one of the 10 ClassType names (quoted)
+CHOICE_MORE_STEPS = 1   # after a businessLogic step: "]" closes the list, ', "' opens another step
+CHOICES: Dict[int, Tuple[bytes, ...]] = {
+    CHOICE_CLASS_TYPE: (b"null",) + tuple(b'"' + t.encode() + b'"' for t in CLASS_TYPES),
+    CHOICE_MORE_STEPS: (b"]", b', "'),
+}
+
 
 @dataclass
 class Segment:
-    forced: Optional[bytes] = None   # forced bytes, or None for a free string
+    """One piece of a reply: ``forced`` bytes, a free JSON string of
+    ``min_len..max_len`` sampled tokens closed by the lone quote token, or a
+    ``choice`` among :data:`CHOICES` alternatives (``then[k]``: the segments
+    that follow alternative k)."""
+    forced: Optional[bytes] = None
     min_len: int = 0
     max_len: int = 0
     ids: Optional[List[int]] = None  # the forced bytes as tokens (set by the engine's tokenizer)
+    choice: int = -1
+    then: Optional[List[List["Segment"]]] = None
+
+    @property
+    def is_free(self) -> bool:
+        return self.forced is None and self.choice < 0
 
 
-def build_template(inp: EnrichmentInput, desc_len=(8, 96), method_len=(6, 64), step_len=(4, 40),
-                   steps: int = 2) -> List[Segment]:
-    """Segments of the reply; a free segment ends with a model- or force-emitted '"'."""
-    segs: List[Segment] = [Segment(b'{"description": "'), Segment(None, *desc_len),
-                           Segment(b', "classTypeCorrection": null, "methods": [')]
-    names = list(dict.fromkeys(inp.method_names))
-    for i, name in enumerate(names):
-        segs.append(Segment(b'{"methodName": ' + json.dumps(name).encode() + b', "description": "'))
-        segs.append(Segment(None, *method_len))
-        segs.append(Segment(b', "businessLogic": ["'))
-        for s in range(steps):
-            segs.append(Segment(None, *step_len))
-            if s + 1 < steps:
-                segs.append(Segment(b', "'))
-        segs.append(Segment(b"]}" + (b", " if i + 1 < len(names) else b"")))
-    segs.append(Segment(b"]}"))
-    # merge adjacent forced segments
+def _merge(segs: List[Segment]) -> List[Segment]:
     out: List[Segment] = []
     for s in segs:
         if out and s.forced is not None and out[-1].forced is not None:
@@ -106,119 +115,147 @@ def build_template(inp: EnrichmentInput, desc_len=(8, 96), method_len=(6, 64), s
     return out
 
 
+def _steps_chain(step_len: Tuple[int, int], max_steps: int, depth: int = 1) -> List[Segment]:
+    """Business-logic step ``depth`` (its opening quote already emitted) and,
+    below ``max_steps``, the model's choice to stop or open the next one."""
+    segs = [Segment(None, *step_len)]
+    if depth < max_steps:
+        segs.append(Segment(choice=CHOICE_MORE_STEPS,
+                            then=[[], _merge(_steps_chain(step_len, max_steps, depth + 1))]))
+    else:
+        segs.append(Segment(b"]"))
+    return segs
+
+
+def build_template(names: Sequence[str], desc_len=(8, 96), method_len=(6, 64), step_len=(4, 40),
+                   max_steps: int = 3, head: bool = True) -> List[Segment]:
+    """Segments of one reply covering ``names``.  ``head`` = False: a
+    continuation part (the description / correction come from part 0)."""
+    if head:
+        segs = [Segment(b'{"description": "'), Segment(None, *desc_len), Segment(b', "classTypeCorrection": '),
+                Segment(choice=CHOICE_CLASS_TYPE, then=[[]] * len(CHOICES[CHOICE_CLASS_TYPE])),
+                Segment(b', "methods": [')]
+    else:
+        segs = [Segment(b'{"description": "", "classTypeCorrection": null, "methods": [')]
+    for i, name in enumerate(names):
+        segs.append(Segment(b'{"methodName": ' + json.dumps(name).encode() + b', "description": "'))
+        segs.append(Segment(None, *method_len))
+        segs.append(Segment(b', "businessLogic": ["'))
+        segs += _steps_chain(step_len, max_steps)
+        segs.append(Segment(b"}" + (b", " if i + 1 < len(names) else b"")))
+    segs.append(Segment(b"]}"))
+    return _merge(segs)
+
+
 def template_budget(segs: Sequence[Segment]) -> int:
-    return sum(len(s.forced) if s.forced is not None else s.max_len + 1 for s in segs)
+    """Upper bound of the reply's tokens (a token spells >= 1 byte)."""
+    n = 0
+    for s in segs:
+        if s.forced is not None:
+            n += len(s.forced)
+        elif s.choice >= 0:
+            n += max(len(a) + template_budget(t or []) for a, t in zip(CHOICES[s.choice], s.then or
+                                                                       [[]] * len(CHOICES[s.choice])))
+        else:
+            n += s.max_len + 1
+    return n
+
+
+def plan_reply(names: Sequence[str], budget: int) -> Tuple[List[List[Segment]], int]:
+    """The reply parts of a class within ``budget`` tokens each, and the
+    number of methods that fit in none.  One part when the whole reply fits
+    (string lengths and step counts shrink first, down to half); otherwise
+    the methods are split over continuation parts -- generated side by side
+    from the same prompt and merged -- so no method is silently dropped."""
+    names = list(dict.fromkeys(names))
+    for scale, steps in ((1.0, 3), (0.75, 2), (0.5, 2)):
+        def L(lo, hi):
+            return (min(lo, max(2, int(hi * scale))), max(4, int(hi * scale)))
+        segs = build_template(names, L(8, 96), L(6, 64), L(4, 40), steps)
+        if template_budget(segs) <= budget:
+            return [segs], 0
+    lens = ((6, 48), (4, 32), (3, 20), 2)
+    minimal = ((2, 16), (2, 12), (2, 8), 1)
+    parts: List[List[Segment]] = []
+    dropped = 0
+    cur: List[str] = []
+
+    def build(ns, head, ls=lens):
+        return build_template(ns, ls[0], ls[1], ls[2], ls[3], head=head)
+    for name in names:
+        if template_budget(build(cur + [name], not parts)) <= budget:
+            cur.append(name)
+            continue
+        if cur:
+            parts.append(build(cur, not parts))
+            cur = []
+        if template_budget(build([name], not parts)) <= budget:
+            cur = [name]
+        elif template_budget(build([name], not parts, minimal)) <= budget:
+            parts.append(build([name], not parts, minimal))
+        else:
+            dropped += 1
+    if cur or not parts:
+        segs = build(cur, not parts)
+        if template_budget(segs) > budget:
+            segs = build(cur, not parts, minimal)
+        parts.append(segs)
+    return parts, dropped
 
 
 def fit_template(inp: EnrichmentInput, capacity: int) -> List[Segment]:
-    """Largest template whose reply budget fits ``capacity`` tokens: free-string
-    lengths shrink first (down to a floor), then trailing methods are dropped."""
-    names = list(dict.fromkeys(inp.method_names))
-    for scale in (1.0, 0.75, 0.5, 0.35, 0.25):
-        def L(lo, hi):
-            return (min(lo, max(2, int(hi * scale))), max(4, int(hi * scale)))
-        segs = build_template(inp, L(8, 96), L(6, 64), L(4, 40))
-        if template_budget(segs) <= capacity:
-            return segs
-    keep = len(names)
-    while keep > 0:
-        keep //= 2
-        sub = EnrichmentInput(inp.source_code, inp.full_class_name, inp.language, inp.class_type, names[:keep])
-        segs = build_template(sub, (2, 24), (2, 16), (2, 8), steps=1)
-        if template_budget(segs) <= capacity:
-            return segs
-    return build_template(EnrichmentInput(inp.source_code, inp.full_class_name, inp.language,
-                                          inp.class_type, []), (2, 16))
+    """The first part of :func:`plan_reply` (single-part callers)."""
+    return plan_reply(inp.method_names, capacity)[0][0]
+
+
+def merge_parts(raws: Sequence[str]) -> str:
+    """One reply from the parts of a split class: part 0's description and
+    correction, every part's methods in order."""
+    head = json.loads(raws[0])
+    for r in raws[1:]:
+        head["methods"] = list(head.get("methods") or []) + list(json.loads(r).get("methods") or [])
+    return json.dumps(head)
 
 
 @dataclass
 class _Seq:
     inp: EnrichmentInput
-    index: int
+    index: Any                         # the caller's key
     segs: List[Segment]
+    part: int = 0                      # reply part of a split class (plan_reply)
+    n_parts: int = 1
     slot: int = -1
     pos: int = 0                       # tokens already in the KV cache
     seg: int = 0
     free_len: int = 0
     forced_off: int = 0
+    choice_pref: bytes = b""           # bytes chosen so far in the current choice segment
     next_token: int = -1               # token to feed at the next decode step
     next_src: int = -1                 # ... or: row of the last launched step whose selection it is
+    await_row: int = -1                # ... or: a choice token selected at this row of step ``await_step``
+    await_step: int = -1
     out: bytearray = field(default_factory=bytearray)
     done: bool = False
     prompt_tokens: int = 0
     gen_tokens: int = 0
-
-
     prompt: Optional[List[int]] = None   # prompt tokens ([BOS] + text)
     prefix_split: int = 0                # leading prompt tokens encoding the text before 'Source of'
+    shared: bool = False                 # its prompt starts with the resident shared prefix (set at admission)
 
     @property
     def free_budget(self) -> int:
         """Sampled (non-forced) tokens the reply may take: ~its decode steps."""
-        return sum(s.max_len + 1 for s in self.segs if s.forced is None)
+        return template_budget([s for s in self.segs if s.forced is None])
 
 
-# ----------------------------------------------------------------- feeds
-class IterFeed:
-    """A feed over a (possibly lazy) iterable of ``(key, EnrichmentInput)``:
-    items are pulled only when the engine has room for them, so a producer
-    that reads sources on demand never runs ahead of the GPU."""
-
-    def __init__(self, items: Iterable[Tuple[Any, EnrichmentInput]]) -> None:
-        self._it = iter(items)
-        self.done = False
-
-    def take(self, n: int, wait: bool = False) -> List[Tuple[Any, EnrichmentInput]]:
-        out = []
-        while len(out) < n and not self.done:
-            try:
-                out.append(next(self._it))
-            except StopIteration:
-                self.done = True
-        return out
-
-
-class QueueFeed:
-    """A thread-safe feed another thread fills (the GPU worker's pipe reader):
-    ``put`` items, ``close`` when no more will come.  ``take(wait=True)``
-    blocks until an item arrives or the feed is closed."""
-
-    def __init__(self) -> None:
-        self._q: Deque[Tuple[Any, EnrichmentInput]] = deque()
-        self._cv = threading.Condition()
-        self._closed = False
-
-    def put(self, items: Iterable[Tuple[Any, EnrichmentInput]]) -> None:
-        with self._cv:
-            self._q.extend(items)
-            self._cv.notify_all()
-
-    def close(self) -> None:
-        with self._cv:
-            self._closed = True
-            self._cv.notify_all()
-
-    @property
-    def done(self) -> bool:
-        with self._cv:
-            return self._closed and not self._q
-
-    def take(self, n: int, wait: bool = False) -> List[Tuple[Any, EnrichmentInput]]:
-        with self._cv:
-            if wait:
-                while not self._q and not self._closed:
-                    self._cv.wait(0.5)
-            out = []
-            while self._q and len(out) < n:
-                out.append(self._q.popleft())
-            return out
+from .feeds import IterFeed, QueueFeed  # noqa: E402,F401  (re-exported)
 
 
 PREFIX_MARKER = b"Source of "  # build_enrichment_prompt: everything before it is per-project
 
 
 class LocalEngine:
-    """Continuous-batching, grammar-forced greedy generator over one LocalLM.
+    """Continuous-batching, grammar-constrained greedy generator over one LocalLM.
 
     :meth:`stream` is the engine: it pulls classes from a feed only while it
     has free KV slots (plus a small look-ahead), prefills every admitted
@@ -226,24 +263,46 @@ class LocalEngine:
     its sequence finishes -- the caller applies it while the GPU runs the
     next step.  :meth:`generate` is the list-in, list-out wrapper.
 
+    The reply grammar (:func:`build_template`) forces the JSON skeleton and
+    every extracted method name; the model writes the strings and makes the
+    reference's choices (``ClaudeApiClient.java:101-120``): the class-type
+    correction (``null`` or one of the 10 types) and when each method's
+    business-logic list ends (1..3 steps).  A choice is sampled under the
+    vocabulary mask of its trie state (tokens that keep the bytes a prefix
+    of some alternative); once one alternative is left, its rest is forced.
+    ``max_new_tokens`` bounds every reply (the reference's ``max_tokens``);
+    a class whose methods do not fit is split into parts generated side by
+    side and merged (:func:`plan_reply`) -- ``stats["methods_dropped"]``
+    counts methods that fit in no part (a single method name longer than
+    the budget).
+
     ``jump_forward``: forced skeleton bytes are not fed one per step -- after
     a sequence's token is fed, every following token that is already decided
     (the rest of a forced segment, or the closing quote of a string at its
     length cap) is appended to the SAME step as extra rows of that sequence,
     up to ``max_rows`` rows per step.  The KV append + causal per-row
     attention of :meth:`LocalLM.decode` makes that an exact multi-token
-    extend, so only free (sampled) tokens cost a step each.
+    extend, so only sampled tokens cost a step each.
+
+    ``pipeline``: step t+1 is launched before step t's ids reach the host.
+    A free-text row's token is gathered on the device from the previous
+    step's selection; its mask assumes the token does not close the string,
+    and the gather kernel switches it to the next segment's mask when it
+    does (``mask_alt``).  A choice token's successor depends on which token
+    it is, so that sequence sits out one step while the host reads it.
 
     ``shared_prefix``: the part of every prompt before ``Source of`` (the
-    instructions + README of one project) is prefilled once per stream into
-    the model's prefix slot; decode reads it through the shared-prefix
-    kernel.  A prompt that does not start with it (truncated) is deferred to
-    a later pass with its own prefix.
+    instructions + README of one project) is prefilled once into the
+    model's prefix slot; decode reads it through the shared-prefix kernel.
+    Several projects stream through one engine at once (feed items
+    ``(key, input, readme)``): a class whose prompt does not start with the
+    resident prefix -- another project, or a truncated prompt -- is admitted
+    with its whole prompt in its own slot (its decode rows flagged off the
+    prefix), and the prefix moves to the next project once no running
+    sequence reads it.
 
     ``tokenizer``: the vocabulary of ``model`` (:mod:`dmcp.enrich.tokenizer`);
-    default the byte-level one of the built-in presets.  Forced skeleton text
-    is encoded with it, free strings are sampled under masks of its JSON-safe
-    tokens, and a free string closes on its lone ``"`` token.
+    default the byte-level one of the built-in presets.
     """
 
     MASK_NO_QUOTE, MASK_QUOTE = 0, 1
@@ -253,7 +312,8 @@ class LocalEngine:
 
     def __init__(self, model: LocalLM, use_graphs: bool = True, max_prompt_tokens: Optional[int] = None,
                  jump_forward: bool = True, shared_prefix: bool = True, pipeline: bool = True,
-                 admit_min: Optional[int] = None, longest_first: bool = True, tokenizer=None) -> None:
+                 admit_min: Optional[int] = None, longest_first: bool = True, tokenizer=None,
+                 max_new_tokens: Optional[int] = None) -> None:
         self.model = model
         self.tok = tokenizer if tokenizer is not None else ByteTokenizer(model.cfg.vocab_size)
         self._tb = self.tok.token_bytes
@@ -270,9 +330,16 @@ class LocalEngine:
         # projection over all their tokens) cost less than one per freed slot
         self.admit_min = max(1, admit_min if admit_min is not None else model.cfg.max_batch // 16)
         self.cfg: LMConfig = model.cfg
+        # reply budget: the caller's max_new_tokens, within what the KV slot
+        # leaves next to a useful prompt
+        kv_cap = self.cfg.max_seq - max(64, self.cfg.max_seq // 4)
+        self.reply_budget = min(kv_cap, int(max_new_tokens)) if max_new_tokens else kv_cap
         dev = model.device
-        self.masks = torch.tensor(list(self.tok.json_masks(self.cfg.vocab_size)), dtype=torch.int32, device=dev)
-        self.graphs = DecodeGraphs(model, self.masks) if use_graphs and dev.type == "cuda" else None
+        self._choice_rows: Dict[Tuple[int, bytes], int] = {}
+        masks = list(self.tok.json_masks(self.cfg.vocab_size)) + self._choice_masks()
+        self.masks = torch.tensor(masks, dtype=torch.int32, device=dev)
+        self.graphs = DecodeGraphs(model, self.masks, alt_token=self._quote) \
+            if use_graphs and dev.type == "cuda" else None
         self.max_prompt_tokens = max_prompt_tokens
         self.jump_forward = jump_forward
         self.shared_prefix = shared_prefix and model.shared_prefix
@@ -286,7 +353,9 @@ class LocalEngine:
                           for _ in range(2)]
         self.stats = {"prompt_tokens": 0, "generated_tokens": 0, "decode_steps": 0, "decode_rows": 0,
                       "prefills": 0, "prefill_batches": 0, "decode_s": 0.0, "prefill_s": 0.0, "prefix_tokens": 0,
-                      "prefix_s": 0.0, "host_s": 0.0, "wait_s": 0.0, "prefill_gpu_s": 0.0}
+                      "prefix_switches": 0, "unshared_prefills": 0,
+                      "prefix_s": 0.0, "host_s": 0.0, "wait_s": 0.0, "prefill_gpu_s": 0.0, "reply_parts": 0,
+                      "split_classes": 0, "methods_dropped": 0, "type_corrections": 0, "choice_waits": 0}
         self._pf_events: List[tuple] = []  # (start, end) device events of the batched prefills
         self._lock = threading.Lock()
 
@@ -299,13 +368,123 @@ class LocalEngine:
         return [out[i] for i in range(len(inputs))]
 
     def stream(self, items, readme: Optional[str]) -> Iterator[Tuple[Any, str]]:
-        """Yields ``(key, raw reply)`` as sequences finish.  ``items``: an
-        iterable of ``(key, EnrichmentInput)`` or a feed (``take``/``done``)."""
+        """Yields ``(key, raw reply)`` as classes finish.  ``items``: an
+        iterable of ``(key, EnrichmentInput)`` -- or ``(key, input, readme)``
+        to mix projects -- or a feed of them (``take`` / ``done``)."""
         feed = items if hasattr(items, "take") else IterFeed(items)
         with self._lock:
-            deferred = yield from self._session(feed, readme)
-            while deferred:  # prompts that did not start with the session's prefix
-                deferred = yield from self._session(IterFeed(deferred), readme)
+            yield from self._session(feed, readme)
+
+    # ------------------------------------------------------------ grammar
+    def _choice_masks(self) -> List[List[int]]:
+        """Mask rows of every choice trie state (appended after the two
+        free-text rows); fills ``_choice_rows[(choice, prefix)]``."""
+        from .tokenizer import _pack_bits
+        rows: List[List[int]] = []
+        V = self.cfg.vocab_size
+        for cid, alts in CHOICES.items():
+            chars = set(b"".join(alts))
+            longest = max(len(a) for a in alts)
+            cand = [(i, b) for i, b in enumerate(self._tb[:V])
+                    if b and len(b) <= longest and all(c in chars for c in b)]
+            prefixes = sorted({a[:k] for a in alts for k in range(len(a))})
+            for p in prefixes:
+                ok = [i for i, b in cand if any(a.startswith(p + b) for a in alts)]
+                if not ok:
+                    raise ValueError(f"tokenizer cannot spell choice {alts!r} after {p!r}")
+                self._choice_rows[(cid, p)] = 2 + len(rows)
+                rows.append(_pack_bits(ok, V))
+        return rows
+
+    def _enter(self, s: _Seq) -> Optional[int]:
+        """Moves ``s`` into its current segment: a forced token becomes
+        ``next_token`` (returns None), a free string or a choice returns the
+        mask row of its first selection; past the last segment ``s`` is done."""
+        while s.seg < len(s.segs):
+            seg = s.segs[s.seg]
+            if seg.forced is not None:
+                if s.forced_off < len(seg.ids):
+                    s.next_token = seg.ids[s.forced_off]
+                    s.forced_off += 1
+                    return None
+                s.seg += 1
+                s.forced_off = 0
+                continue
+            if seg.choice >= 0:
+                s.choice_pref = b""
+                return self._choice_rows[(seg.choice, b"")]
+            s.free_len = 0
+            return self.MASK_QUOTE if seg.min_len == 0 else self.MASK_NO_QUOTE
+        s.done = True
+        return None
+
+    def _choose(self, s: _Seq, seg: Segment, k: int, rest: bytes) -> Optional[int]:
+        """Alternative ``k`` of the choice at ``s.seg`` is decided: its
+        remaining bytes ``rest`` are forced, its branch spliced in."""
+        after: List[Segment] = []
+        if rest:
+            after.append(Segment(rest, ids=self.tok.encode_fragment(rest.decode("utf-8"))))
+        if seg.then and seg.then[k]:
+            after += self._encode_forced(list(seg.then[k]))
+        if seg.choice == CHOICE_CLASS_TYPE and k > 0:
+            self.stats["type_corrections"] += 1
+        s.segs = s.segs[:s.seg + 1] + after + s.segs[s.seg + 1:]
+        s.seg += 1
+        s.forced_off = 0
+        return self._enter(s)
+
+    def _after_feed(self, s: _Seq, tok: int) -> Optional[int]:
+        """Grammar transition after ``tok`` entered the KV cache.  Returns
+        None when the next token is already decided (``s.next_token``) or the
+        reply is complete, else the mask row of the selection at this row."""
+        s.out += self._tb[tok]
+        s.pos += 1
+        s.gen_tokens += 1
+        seg = s.segs[s.seg] if s.seg < len(s.segs) else None
+        if seg is None:
+            return self._enter(s)
+        if seg.forced is not None:
+            return self._enter(s)
+        if seg.choice >= 0:
+            pref = s.choice_pref + self._tb[tok]
+            alts = CHOICES[seg.choice]
+            live = [k for k, a in enumerate(alts) if a.startswith(pref)]
+            if not live:  # cannot happen under the choice masks
+                raise RuntimeError(f"token {tok} leaves choice {alts!r} after {s.choice_pref!r}")
+            if len(live) == 1:
+                k = live[0]
+                return self._choose(s, seg, k, alts[k][len(pref):])
+            s.choice_pref = pref
+            return self._choice_rows[(seg.choice, pref)]
+        if tok == self._quote:  # free string closed
+            s.seg += 1
+            s.forced_off = 0
+            s.free_len = 0
+            return self._enter(s)
+        s.free_len += 1
+        if s.free_len >= seg.max_len:
+            s.next_token = self._quote
+            return None
+        return self.MASK_QUOTE if s.free_len >= seg.min_len else self.MASK_NO_QUOTE
+
+    def _in_choice(self, s: _Seq) -> bool:
+        return not s.done and s.seg < len(s.segs) and s.segs[s.seg].choice >= 0
+
+    def _speculative_mask(self, s: _Seq) -> Tuple[int, int]:
+        """(mask row, mask row if the token is the closing quote) of a row
+        whose free-text token is still on the device: the state after
+        feeding any token but the quote, and the first mask of the segment
+        the quote opens when that is a choice (-1: its selection is unused)."""
+        seg = s.segs[s.seg]
+        main = self.MASK_QUOTE if s.free_len + 1 >= seg.min_len else self.MASK_NO_QUOTE
+        alt = -1
+        if s.seg + 1 < len(s.segs):
+            nxt = s.segs[s.seg + 1]
+            if nxt.choice >= 0:
+                alt = self._choice_rows[(nxt.choice, b"")]
+            elif nxt.forced is None:
+                alt = self.MASK_QUOTE if nxt.min_len == 0 else self.MASK_NO_QUOTE
+        return main, alt
 
     # ------------------------------------------------------------ helpers
     def _prompt(self, seq: _Seq, readme: Optional[str], budget: int) -> List[int]:
@@ -333,50 +512,9 @@ class LocalEngine:
 
     def _encode_forced(self, segs: List[Segment]) -> List[Segment]:
         for seg in segs:
-            if seg.forced is not None:
+            if seg.forced is not None and seg.ids is None:
                 seg.ids = self.tok.encode_fragment(seg.forced.decode("utf-8"))
         return segs
-
-    def _advance_forced(self, s: _Seq) -> None:
-        """Sets next_token from the current forced segment or finishes."""
-        while s.seg < len(s.segs):
-            seg = s.segs[s.seg]
-            if seg.forced is None:
-                return
-            if s.forced_off < len(seg.ids):
-                s.next_token = seg.ids[s.forced_off]
-                s.forced_off += 1
-                return
-            s.seg += 1
-            s.forced_off = 0
-            s.free_len = 0
-        s.done = True
-
-    def _after_feed(self, s: _Seq, tok: int) -> Optional[bool]:
-        """Grammar transition after ``tok`` entered the KV cache.  Returns None
-        when the next token is already decided (``s.next_token``) or the reply
-        is complete, else whether the sampled token may be the closing quote."""
-        s.out += self._tb[tok]
-        s.pos += 1
-        s.gen_tokens += 1
-        seg = s.segs[s.seg] if s.seg < len(s.segs) else None
-        if seg is not None and seg.forced is None:
-            if tok == self._quote:  # free string closed
-                s.seg += 1
-                s.forced_off = 0
-                s.free_len = 0
-                self._advance_forced(s)
-            else:
-                s.free_len += 1
-                if s.free_len >= seg.max_len:
-                    s.next_token = self._quote
-                    return None
-                return s.free_len >= seg.min_len
-        else:
-            self._advance_forced(s)
-        if not s.done and s.segs[s.seg].forced is None:
-            return s.segs[s.seg].min_len == 0
-        return None
 
     def _build_prompt(self, s: _Seq, readme: Optional[str]) -> List[int]:
         budget = template_budget(s.segs)
@@ -384,15 +522,34 @@ class LocalEngine:
             raise ValueError(f"reply template needs {budget} tokens > max_seq {self.cfg.max_seq}")
         return self._prompt(s, readme, budget)
 
-    def _admit_batch(self, batch: List[_Seq], prefix: int) -> List[_Seq]:
+    def _seqs_for(self, key: Any, inp: EnrichmentInput, readme: Optional[str]) -> List[_Seq]:
+        """The sequences of one class: one per reply part, sharing one prompt."""
+        parts, dropped = plan_reply(inp.method_names, self.reply_budget)
+        self.stats["methods_dropped"] += dropped
+        self.stats["reply_parts"] += len(parts)
+        if len(parts) > 1:
+            self.stats["split_classes"] += 1
+        if dropped:
+            LOG.warning("%s: %d method(s) do not fit a %d-token reply", inp.full_class_name, dropped,
+                        self.reply_budget)
+        seqs = [_Seq(inp, key, self._encode_forced(segs), part=j, n_parts=len(parts))
+                for j, segs in enumerate(parts)]
+        # every part has the same prompt: tokenise once, sized for the longest reply
+        longest = max(seqs, key=lambda q: template_budget(q.segs))
+        prompt = self._build_prompt(longest, readme)
+        for q in seqs:
+            q.prompt, q.prefix_split = prompt, longest.prefix_split
+        return seqs
+
+    def _admit_batch(self, batch: List[_Seq]) -> List[_Seq]:
         """Prefills ``batch`` and waits for it (see :meth:`_admit_launch`);
         returns the sequences that finished already."""
-        return self._admit_finish(self._admit_launch(batch, prefix), wait=True)
+        return self._admit_finish(self._admit_launch(batch), wait=True)
 
-    def _admit_launch(self, batch: List[_Seq], prefix: int) -> dict:
+    def _admit_launch(self, batch: List[_Seq]) -> dict:
         """Enqueues ONE batched prefill of every sequence of ``batch`` (slots
         assigned) -- prompt + first forced segment, after the shared prefix
-        when set -- and the masked argmax of each first free token; the ids
+        for the sequences that use it -- and the masked argmax of each first selection; the ids
         land in a pinned buffer.  Nothing here waits for the device: the host
         goes on to build and launch the running batch's next step, which the
         stream runs after the prefill; the admitted classes join the step
@@ -402,17 +559,23 @@ class LocalEngine:
         from .. import ops
         t0 = time.perf_counter()
         reqs = []
-        for s in batch:
+        need, midx_l = [], []
+        for i, s in enumerate(batch):
             first = s.segs[0].ids or []
             toks = s.prompt + first
-            start = self.model.fork_prefix(s.slot) if prefix else 0
+            start = self.model.fork_prefix(s.slot) if s.shared else 0
+            if not s.shared:
+                self.stats["unshared_prefills"] += 1
             reqs.append((toks[start:], s.slot, start))
             self.stats["prompt_tokens"] += len(toks) - start
             s.prompt_tokens = len(s.prompt)
             s.out.extend(s.segs[0].forced or b"")
             s.pos = len(toks)
             s.seg, s.forced_off = 1, 0
-        need = [i for i, s in enumerate(batch) if s.seg < len(s.segs) and s.segs[s.seg].forced is None]
+            m = self._enter(s)  # the first selection's mask, or a decided token
+            if m is not None:
+                need.append(i)
+                midx_l.append(m)
         dev = self.model.device
         h = {"batch": batch, "need": need, "ids": None, "event": None}
         timed = dev.type == "cuda"
@@ -425,8 +588,7 @@ class LocalEngine:
             self._pf_events.append(ev)
         if need:
             rows = logits[need] if len(need) < len(batch) else logits
-            midx = torch.tensor([self.MASK_QUOTE if batch[i].segs[1].min_len == 0 else self.MASK_NO_QUOTE
-                                 for i in need], dtype=torch.int32)
+            midx = torch.tensor(midx_l, dtype=torch.int32)
             if dev.type == "cuda":  # no pageable (host-blocking) copy behind the prefill
                 midx = midx.pin_memory()
             midx = midx.to(dev, non_blocking=True)
@@ -442,8 +604,8 @@ class LocalEngine:
 
     def _admit_finish(self, h: dict, wait: bool) -> Optional[List[_Seq]]:
         """None while the prefill of ``h`` is still running (``wait=False``);
-        else applies the first tokens and returns the sequences that finished
-        already (all forced)."""
+        else applies the first selections and returns the sequences that
+        finished already (all forced)."""
         ev = h["event"]
         if ev is not None:
             if not wait and not ev.query():
@@ -455,28 +617,24 @@ class LocalEngine:
         if h["ids"] is not None:
             for i, tok in zip(h["need"], h["ids"].tolist()):
                 batch[i].next_token = int(tok)
-        done = []
-        for s in batch:
-            if s.seg >= len(s.segs) or s.segs[s.seg].forced is not None:
-                self._advance_forced(s)
-            if s.done:
-                done.append(s)
+        done = [s for s in batch if s.done]
         self.stats["prefills"] += len(batch)
         self.stats["prefill_batches"] += 1
         return done
 
     def _launch(self, toks: List[int], slots: List[int], poss: List[int], mrows: List[int],
-                srcs: List[int], buf: int):
+                srcs: List[int], alts: List[int], prows: List[int], buf: int):
         """Launches one step; enqueues the copy of its ids to pinned buffer
         ``buf``; returns the event that completes with that copy."""
         if self.graphs is not None:
-            _, ids = self.graphs.run(toks, slots, poss, mrows, srcs)
+            _, ids = self.graphs.run(toks, slots, poss, mrows, srcs, alts, prows)
         else:
             dev = self.model.device
-            t = torch.tensor([toks, slots, poss, mrows, srcs], dtype=torch.int32, device=dev)
+            t = torch.tensor([toks, slots, poss, mrows, srcs, alts, prows], dtype=torch.int32, device=dev)
             _, ids = self.model.decode_select_gather(t[0].contiguous(), t[4].contiguous(), self._last_ids,
                                                      t[1].contiguous(), t[2].contiguous(), self.masks,
-                                                     t[3].contiguous())
+                                                     t[3].contiguous(), t[5].contiguous(), self._quote,
+                                                     t[6].contiguous())
         n = len(toks)
         host = self._host_ids[buf]
         host[:n].copy_(ids[:n], non_blocking=self.model.device.type == "cuda")
@@ -486,41 +644,44 @@ class LocalEngine:
             return ev
         return None
 
-    def _speculative_mask(self, s: _Seq) -> int:
-        """Mask row for a row whose token is still on the device (a free-text
-        selection): the state after feeding any token but the closing quote
-        -- the only case in which this row's own selection is used."""
-        seg = s.segs[s.seg]
-        return self.MASK_QUOTE if s.free_len + 1 >= seg.min_len else self.MASK_NO_QUOTE
+    def _finish(self, s: _Seq, partials: Dict[Any, List[Optional[str]]]) -> Optional[str]:
+        """The class reply once ``s`` (a part of it) is complete, else None."""
+        raw = s.out.decode("utf-8", "replace")
+        if s.n_parts == 1:
+            return raw
+        got = partials.setdefault(s.index, [None] * s.n_parts)
+        got[s.part] = raw
+        if any(r is None for r in got):
+            return None
+        del partials[s.index]
+        return merge_parts(got)  # type: ignore[arg-type]
 
     # ------------------------------------------------------------ the loop
     def _session(self, feed, readme: Optional[str]):
-        """One pass over ``feed`` with one shared prefix; returns the
-        ``(key, input)`` pairs whose prompt did not start with that prefix.
+        """Runs ``feed`` to its end (``readme``: the default of items without one).
 
         Each iteration: refill the look-ahead from the feed, admit (batched
         prefill) while KV slots are free, build step k's rows, launch it, then
         -- while the GPU computes step k -- wait for step k-1's ids, run the
         grammar transitions they decide and yield the finished replies.
-        With ``pipeline`` a sequence whose next token is step k-1's selection
-        gets ONE row gathered on the device from that selection (its mask row
-        assumes the token is not the closing quote -- if it is, that row's own
-        selection is simply not used); every other sequence gets its literal
-        token and, with jump-forward, the decided tokens after it.  Without
-        ``pipeline`` the host waits for every step's ids before building the
-        next (the exact reference loop)."""
+        With ``pipeline`` a sequence whose next token is step k-1's free-text
+        selection gets ONE row gathered on the device from that selection;
+        a sequence whose next token is a choice selection sits out until the
+        host has read it; every other sequence gets its literal token and,
+        with jump-forward, the decided tokens after it.  Without ``pipeline``
+        the host waits for every step's ids before building the next (the
+        exact reference loop)."""
         cfg = self.cfg
-        reply_cap = cfg.max_seq - max(64, cfg.max_seq // 4)
         free_slots = list(range(cfg.max_batch - 1, -1, -1))
         pending: Deque[_Seq] = deque()
         active: List[_Seq] = []
-        deferred: List[Tuple[Any, EnrichmentInput]] = []
+        partials: Dict[Any, List[Optional[str]]] = {}
         lookahead = max(4, cfg.max_batch // 4)
-        decided = not self.shared_prefix
-        prefix_toks: Optional[List[int]] = None
+        prefix_toks: Optional[List[int]] = None  # the resident shared prefix
         P = 0
         prev_event = None
         prev_buf = 1
+        step_no = -1                     # number of the last launched step
         finished: List[_Seq] = []
         inflight: Optional[dict] = None  # the batched prefill in flight
         try:
@@ -528,26 +689,14 @@ class LocalEngine:
                 # ---- refill the look-ahead (blocking only when idle)
                 want = len(free_slots) + lookahead - len(pending)
                 if want > 0 and not feed.done:
-                    for key, inp in feed.take(want, wait=not active and not pending and inflight is None):
-                        s = _Seq(inp, key, self._encode_forced(fit_template(inp, reply_cap)))
+                    for item in feed.take(want, wait=not active and not pending and inflight is None):
+                        key, inp = item[0], item[1]
                         try:
-                            s.prompt = self._build_prompt(s, readme)
+                            seqs = self._seqs_for(key, inp, item[2] if len(item) > 2 else readme)
                         except Exception as e:
                             yield key, json.dumps({"error": str(e)})
                             continue
-                        if not decided:
-                            decided = True
-                            P = self._seq_prefix_len(s)
-                            if P:
-                                prefix_toks = s.prompt[:P]
-                                t0 = time.perf_counter()
-                                self.model.set_prefix(prefix_toks)
-                                self.stats["prefix_s"] += time.perf_counter() - t0
-                                self.stats["prefix_tokens"] += P
-                        if P and s.prompt[:P] != prefix_toks:
-                            deferred.append((key, inp))
-                            continue
-                        pending.append(s)
+                        pending.extend(seqs)
                 if not pending and not active and inflight is None:
                     if feed.done:
                         break
@@ -561,21 +710,38 @@ class LocalEngine:
                     ntok = 0
                     if self.longest_first and len(pending) > 1:
                         pending = deque(sorted(pending, key=lambda q: -q.free_budget))
+                    users = sum(1 for q in active if q.shared)
                     while pending and free_slots and len(batch) < self.ADMIT_SEQS:
-                        nxt = len(pending[0].prompt) - P
+                        s = pending[0]
+                        if self.shared_prefix and users == 0:
+                            # no running sequence reads the resident prefix:
+                            # it moves to this class's project
+                            Ps = self._seq_prefix_len(s)
+                            if Ps and s.prompt[:Ps] != prefix_toks:
+                                t0 = time.perf_counter()
+                                self.model.set_prefix(s.prompt[:Ps])
+                                prefix_toks, P = s.prompt[:Ps], Ps
+                                self.stats["prefix_s"] += time.perf_counter() - t0
+                                self.stats["prefix_tokens"] += Ps
+                                self.stats["prefix_switches"] += 1
+                        s.shared = bool(P) and len(s.prompt) > P and s.prompt[:P] == prefix_toks
+                        nxt = len(s.prompt) - (P if s.shared else 0)
                         if batch and ntok + nxt > self.ADMIT_TOKENS:
                             break
-                        s = pending.popleft()
+                        pending.popleft()
                         s.slot = free_slots.pop()
                         batch.append(s)
+                        users += s.shared
                         ntok += nxt
-                    inflight = self._admit_launch(batch, P)
+                    inflight = self._admit_launch(batch)
                 if inflight is not None:
                     done = self._admit_finish(inflight, wait=not active)
                     if done is not None:
                         for s in done:
                             free_slots.append(s.slot)
-                            yield s.index, s.out.decode("utf-8", "replace")
+                            raw = self._finish(s, partials)
+                            if raw is not None:
+                                yield s.index, raw
                         active.extend(s for s in inflight["batch"] if not s.done)
                         inflight = None
                         continue  # admit the next batch before this step when slots allow
@@ -588,17 +754,24 @@ class LocalEngine:
                 poss: List[int] = []
                 mrows: List[int] = []
                 srcs: List[int] = []
+                alts: List[int] = []
+                prows: List[int] = []
                 gathered: List[Tuple[_Seq, int, int]] = []  # (seq, row, source row of the previous step)
                 sample_at: List[Tuple[_Seq, int]] = []
                 spare = self.max_rows - len(active)
                 for s in active:
+                    if s.await_row >= 0:
+                        continue  # its next token is a choice selection the host has not read yet
                     if s.next_src >= 0:
                         gathered.append((s, len(toks), s.next_src))
+                        m, a = self._speculative_mask(s)
                         toks.append(0)
                         slots.append(s.slot)
                         poss.append(s.pos)
-                        mrows.append(self._speculative_mask(s))
+                        mrows.append(m)
                         srcs.append(s.next_src)
+                        alts.append(a)
+                        prows.append(1 if s.shared else 0)
                         s.next_src = -1
                         continue
                     tok = s.next_token
@@ -608,23 +781,31 @@ class LocalEngine:
                         poss.append(s.pos)
                         mrows.append(self.MASK_NO_QUOTE)
                         srcs.append(-1)
-                        q = self._after_feed(s, tok)
+                        alts.append(-1)
+                        prows.append(1 if s.shared else 0)
+                        m = self._after_feed(s, tok)
                         if s.done:
                             break
-                        if q is not None:  # this row's selection is the next token
-                            mrows[-1] = self.MASK_QUOTE if q else self.MASK_NO_QUOTE
-                            if self.pipeline:
-                                s.next_src = len(toks) - 1
-                            else:
+                        if m is not None:  # this row's selection is the next token
+                            mrows[-1] = m
+                            if not self.pipeline:
                                 sample_at.append((s, len(toks) - 1))
+                            elif self._in_choice(s):
+                                s.await_row, s.await_step = len(toks) - 1, step_no + 1
+                            else:
+                                s.next_src = len(toks) - 1
                             break
                         if not self.jump_forward or spare <= 0:
                             break
                         spare -= 1
                         tok = s.next_token
-                buf = 1 - prev_buf
                 t1 = time.perf_counter()
-                event = self._launch(toks, slots, poss, mrows, srcs, buf)
+                if toks:
+                    buf = 1 - prev_buf
+                    event = self._launch(toks, slots, poss, mrows, srcs, alts, prows, buf)
+                    step_no += 1
+                else:  # every active sequence waits for a choice of the last step
+                    event, buf = None, None
                 t2 = time.perf_counter()
                 if not self.pipeline:
                     if event is not None:
@@ -632,20 +813,33 @@ class LocalEngine:
                     ids = self._host_ids[buf]
                     for s, r in sample_at:
                         s.next_token = int(ids[r])
-                elif gathered:
-                    # the previous step's ids: the tokens this step's gathered rows fed
-                    if prev_event is not None:
-                        prev_event.synchronize()
-                    ids = self._host_ids[prev_buf]
-                    for s, row, src in gathered:
-                        q = self._after_feed(s, int(ids[src]))
-                        if not s.done and q is not None:
-                            s.next_src = row  # its selection in the step just launched
+                else:
+                    # the ids of the step before the one just launched (or of
+                    # the last one, when none was): gathered rows' tokens and
+                    # awaited choices
+                    read_no = step_no - 1 if toks else step_no
+                    waiting = [s for s in active if s.await_row >= 0 and s.await_step == read_no]
+                    if gathered or waiting:
+                        if prev_event is not None:  # the step whose ids are read
+                            prev_event.synchronize()
+                        ids = self._host_ids[prev_buf]
+                        for s in waiting:
+                            s.next_token = int(ids[s.await_row])
+                            s.await_row = -1
+                            self.stats["choice_waits"] += 1
+                        for s, row, src in gathered:
+                            m = self._after_feed(s, int(ids[src]))
+                            if not s.done and m is not None:
+                                if self._in_choice(s):  # the row just launched selected a choice token
+                                    s.await_row, s.await_step = row, step_no
+                                else:
+                                    s.next_src = row  # its selection in the step just launched
                 t3 = time.perf_counter()
-                prev_event, prev_buf = event, buf
-                self.stats["decode_steps"] += 1
-                self.stats["decode_rows"] += len(toks)
-                self.stats["generated_tokens"] += len(toks)
+                if toks:
+                    prev_event, prev_buf = event, buf
+                    self.stats["decode_steps"] += 1
+                    self.stats["decode_rows"] += len(toks)
+                    self.stats["generated_tokens"] += len(toks)
                 still = []
                 for s in active:
                     if s.done:
@@ -661,7 +855,9 @@ class LocalEngine:
                 # replies go out while the GPU computes the step just launched
                 while finished:
                     s = finished.pop()
-                    yield s.index, s.out.decode("utf-8", "replace")
+                    raw = self._finish(s, partials)
+                    if raw is not None:
+                        yield s.index, raw
         finally:
             if prev_event is not None:
                 prev_event.synchronize()
@@ -672,7 +868,6 @@ class LocalEngine:
             self._pf_events.clear()
             if P:
                 self.model.clear_prefix()
-        return deferred
 
 
 class LocalLLMBackend(EnrichmentBackend):
@@ -691,6 +886,7 @@ class LocalLLMBackend(EnrichmentBackend):
     def from_config(cls, cfg) -> EnrichmentBackend:
         if (cfg.local_llm_workers or "process").lower() == "process":
             return ProcessLLMBackend.from_config(cfg)
+        from .workers import engine_spec, model_spec
         devices = []
         if torch.cuda.is_available():
             n = torch.cuda.device_count()
@@ -698,14 +894,11 @@ class LocalLLMBackend(EnrichmentBackend):
             devices = list(range(n)) if spec == "all" else [int(x) for x in spec.split(",") if x.strip()]
         if not devices:
             raise RuntimeError("LocalLLMBackend needs a ROCm GPU (torch.cuda.is_available() is False)")
-        mb = int(cfg.local_llm_max_batch)
-        spec = {"preset": cfg.local_llm_preset, "kv_dtype": cfg.local_llm_kv_dtype, "max_batch": mb,
-                "max_rows": max(256, mb * 3 // 2), "seed": 0, "path": cfg.local_llm_model_path}
         engines = []
         for d in devices:
             with torch.cuda.device(d):
-                model, tok = build_model(spec, f"cuda:{d}")
-                engines.append(LocalEngine(model, tokenizer=tok))
+                model, tok = build_model(model_spec(cfg), f"cuda:{d}")
+                engines.append(LocalEngine(model, tokenizer=tok, **engine_spec(cfg)))
         return cls(engines)
 
     def enrich_class(self, inp: EnrichmentInput, readme: Optional[str]) -> EnrichmentResult:
@@ -761,8 +954,11 @@ def build_model(spec: dict, device: str):
     if spec.get("path"):
         from .tokenizer import load_local_model
         return load_local_model(spec["path"], device=device, **overrides)
-    model = LocalLM(preset(spec.get("preset", "dmcp-coder-1b"), **overrides), device=device,
-                    seed=int(spec.get("seed", 0)))
+    cfg = preset(spec.get("preset", "dmcp-coder-1b"), **overrides)
+    model = LocalLM(cfg, device=device, seed=int(spec.get("seed", 0)))
+    if cfg.tokenizer:
+        from .tokenizer import load_asset_tokenizer
+        return model, load_asset_tokenizer(cfg.tokenizer)
     return model, None
 
 

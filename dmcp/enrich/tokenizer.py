@@ -129,14 +129,19 @@ def _byte_level_decoder_map() -> dict:
 
 
 class HFTokenizer(_Base):
-    """A Hugging Face ``tokenizer.json`` (``tokenizers`` library)."""
+    """A Hugging Face ``tokenizer.json`` (``tokenizers`` library): a file, a
+    checkpoint directory holding one, or (``text``) its JSON text."""
 
-    def __init__(self, path: str, bos: Optional[int] = None) -> None:
+    def __init__(self, path: str = "", bos: Optional[int] = None, text: Optional[str] = None) -> None:
         from tokenizers import Tokenizer
-        file = os.path.join(path, "tokenizer.json") if os.path.isdir(path) else path
-        self.tk = Tokenizer.from_file(file)
-        with open(file, encoding="utf-8") as f:
-            spec = json.load(f)
+        if text is None:
+            file = os.path.join(path, "tokenizer.json") if os.path.isdir(path) else path
+            with open(file, encoding="utf-8") as f:
+                text = f.read()
+        else:
+            file = path or "<text>"
+        self.tk = Tokenizer.from_str(text)
+        spec = json.loads(text)
         special = {t["id"] for t in spec.get("added_tokens") or [] if t.get("special")}
         dec = spec.get("decoder") or {}
         kinds = {dec.get("type")} | {d.get("type") for d in dec.get("decoders") or []}
@@ -183,6 +188,27 @@ def load_tokenizer(path: str) -> HFTokenizer:
                 if json.load(f).get("add_bos_token") is False:
                     bos = None
     return HFTokenizer(path, bos=bos if isinstance(bos, int) else None)
+
+
+ASSETS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "models", "assets")
+_PRESET_TOKENIZERS: dict = {}
+
+
+def load_asset_tokenizer(name: str) -> HFTokenizer:
+    """A tokenizer shipped in ``dmcp/models/assets/<name>`` (gzipped
+    ``tokenizer.json`` + ``tokenizer_meta.json`` with the BOS id); cached
+    per process (building the 128k-id byte tables takes ~1 s)."""
+    tok = _PRESET_TOKENIZERS.get(name)
+    if tok is None:
+        import gzip
+        d = os.path.join(ASSETS, name)
+        with gzip.open(os.path.join(d, "tokenizer.json.gz"), "rt", encoding="utf-8") as f:
+            text = f.read()
+        with open(os.path.join(d, "tokenizer_meta.json")) as f:
+            meta = json.load(f)
+        tok = _PRESET_TOKENIZERS[name] = HFTokenizer(os.path.join(d, "tokenizer.json.gz"),
+                                                     bos=meta.get("bos_token_id"), text=text)
+    return tok
 
 
 def load_local_model(path: str, device: str = "cuda", **cfg_overrides):

@@ -90,3 +90,19 @@ class BatchClassInput:
     full_class_name: str
     source_file: str
     language: str
+
+
+class SizedIter:
+    """A lazy iterable that knows how many items it will (at most) yield:
+    ``operator.length_hint`` reports ``n``, so a backend can deal the
+    pending work evenly without materialising it."""
+
+    def __init__(self, it, n: int) -> None:
+        self._it = it
+        self._n = int(n)
+
+    def __length_hint__(self) -> int:
+        return self._n
+
+    def __iter__(self):
+        return iter(self._it)

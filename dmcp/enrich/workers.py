@@ -1,34 +1,48 @@
 """One worker process per GPU for the local enrichment model -- MI355X extension.
 
 Enrichment requests are independent (one prompt per class,
-``ClaudeApiClient.java:288-329``), so multi-GPU scaling is pure data
+``ClaudeApiClient.java:288-329``; the reference runs one virtual thread per
+class behind a semaphore, ``:354-388``), so multi-GPU scaling is pure data
 parallelism: every MI355X holds a full copy of the model and
-its own KV-cache slab, and classes are handed out from ONE queue in the
-parent.  Each replica lives in its own process:
+its own KV-cache slab, and classes are dealt out by ONE pool in the parent.
+Each replica lives in its own process:
 
-* the parent (REST / MCP / CLI service) starts the workers BEFORE it touches
+* the parent (REST / MCP / CLI service) starts the workers before it touches
   HIP and never initialises the GPU itself -- each child sees exactly one
   device (``HIP_VISIBLE_DEVICES``), so a fault or hang on one GPU kills one
   child, never the server;
-* each engine's ~0.3 ms of host work per decode step (grammar state machine,
-  row packing) runs on its own interpreter -- N replicas driven by N threads
-  of one process would serialise on the GIL (8 x 0.3 ms against a 2-4 ms
-  step);
+* each engine's host work per decode step (grammar state machine, row
+  packing) runs on its own interpreter -- N replicas driven by N threads of
+  one process would serialise on the GIL;
 * parent and child talk over the child's stdin / stdout: length-prefixed
   JSON frames (``begin`` readme / ``items`` / ``end`` down; ``ready`` /
   ``result`` / ``done`` / ``error`` up); the child's logs go to stderr;
-* the parent keeps every worker's queue ``max_batch * 1.5`` classes deep so
-  its continuous batch never drains, yields each result as it arrives, and
-  when a worker dies (EOF on its pipe, a non-zero exit, or no frame for
-  ``hang_timeout_s`` while it holds work -- then it is killed) the classes it
-  held are reported as failures (Phase 3 retries them) and the rest go to
-  the live workers.  A dead worker is replaced by a FRESH child at the next
-  stream; a GPU-touched process is never restarted in place.
+* a child runs ONE engine stream over all the sessions it was dealt
+  (:class:`dmcp.enrich.feeds.MultiFeed`): two projects on one GPU share its
+  continuous batch instead of queueing one behind the other.
+
+Dealing (:class:`GpuWorkerPool`):
+
+* several streams (projects: concurrent REST requests, the sync scheduler,
+  bulk indexing) run at once.  Each live worker is OWNED by one stream at a
+  time -- the workers are split evenly over the streams that still have
+  classes to deal, in arrival order -- so new classes go where their
+  project's shared prompt prefix is resident; a worker handed to another
+  stream keeps decoding what it holds of the first next to the new work;
+* within a stream the pending classes are dealt ``ceil(pending / owned)``
+  per worker (capped at ``capacity`` in flight), topped up as replies return:
+  a 257-class project on 8 GPUs is 32-33 classes per GPU, not 257 on GPU 0;
+* a worker that dies (EOF on its pipe, a non-zero exit, or no frame for
+  ``hang_timeout_s`` while it holds work -- then it is killed) fails the
+  classes it held (Phase 3 retries them); the rest go to the live workers.
+  A dead worker is replaced by a FRESH child at the next stream; a
+  GPU-touched process is never restarted in place.
 """
 from __future__ import annotations
 
 import json
 import logging
+import operator
 import os
 import queue
 import struct
@@ -85,10 +99,10 @@ def visible_gpus() -> int:
 
 # ------------------------------------------------------------------ parent
 class _Worker:
-    def __init__(self, index: int, device: str, events: "queue.Queue", env_extra: Optional[dict] = None) -> None:
+    def __init__(self, index: int, device: str, pool: "GpuWorkerPool", env_extra: Optional[dict] = None) -> None:
         self.index = index
         self.device = device  # "cuda:<physical id>" or "cpu"
-        self.events = events
+        self.pool = pool
         env = dict(os.environ)
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
@@ -101,16 +115,20 @@ class _Worker:
         self.proc = subprocess.Popen([sys.executable, "-u", "-m", "dmcp.enrich.workers"], stdin=subprocess.PIPE,
                                      stdout=subprocess.PIPE, stderr=None, env=env, cwd=ROOT)
         self.alive = True
+        self.closing = False
         self.ready = False
         self.info: dict = {}
-        self.inflight: Dict[int, str] = {}   # key -> class name
-        self.last_frame = time.monotonic()
-        self.done_sid = 0
+        self.inflight: Dict[int, Dict[int, str]] = {}  # stream id -> key -> class name
+        self.owner: Optional["_Stream"] = None
+        self.last_frame = time.monotonic()  # last sign of progress (frame, or work handed to an idle worker)
         self.stats: Dict[str, float] = {}
         self.sent = 0
         self._wlock = threading.Lock()
         self._reader = threading.Thread(target=self._read, name=f"gpu-worker-{index}-rx", daemon=True)
         self._reader.start()
+
+    def held(self) -> int:
+        return sum(len(d) for d in self.inflight.values())
 
     def _read(self) -> None:
         out = self.proc.stdout
@@ -120,9 +138,9 @@ class _Worker:
             except Exception as e:  # corrupt frame: treat as death
                 LOG.error("worker %d: bad frame: %s", self.index, e)
                 msg = None
-            # tagged with this worker object, not its index: a replaced
+            # routed with this worker object, not its index: a replaced
             # worker's late EOF must not mark its successor dead
-            self.events.put((self, msg))
+            self.pool._on_frame(self, msg)
             if msg is None:
                 return
 
@@ -144,6 +162,7 @@ class _Worker:
             pass
 
     def close(self, timeout: float = 30.0) -> None:
+        self.closing = True
         if self.proc.poll() is None:
             self.send({"op": "shutdown"})
             try:
@@ -158,10 +177,32 @@ class _Worker:
         self.alive = False
 
 
+class _Stream:
+    """One enrichment stream (one project's pending classes) in the pool."""
+
+    def __init__(self, sid: int, readme: Optional[str], inputs: Iterable[EnrichmentInput]) -> None:
+        self.sid = sid
+        self.readme = readme
+        self.hint = operator.length_hint(inputs, -1)  # pending classes, when the caller knows them
+        self.src = enumerate(inputs)
+        self.taken = 0
+        self.exhausted = False
+        self.events: "queue.Queue" = queue.Queue()
+        self.begun: List[_Worker] = []      # workers that got this stream's ``begin``
+        self.ended: set = set()             # ... and its ``end``
+        self.finished: set = set()          # ... and answered ``done``
+        self.stats: Dict[str, float] = {}
+        self.items_per_worker: Dict[int, int] = {}
+
+    def remaining(self) -> Optional[int]:
+        return None if self.hint < 0 else max(0, self.hint - self.taken)
+
+
 class GpuWorkerPool:
-    """N worker processes, one per device; :meth:`stream` runs one enrichment
-    stream across all of them.  Spawn (cheap: the children import nothing
-    heavy until ``init``) before this process touches HIP."""
+    """N worker processes, one per device, shared by every enrichment stream
+    of the service (:meth:`stream` may run in several threads at once).
+    Spawn (cheap: the children import nothing heavy until ``init``) before
+    this process touches HIP."""
 
     def __init__(self, devices: Sequence[str], model: dict, engine: Optional[dict] = None,
                  hang_timeout_s: float = 300.0, start_timeout_s: float = 900.0, env_extra: Optional[dict] = None,
@@ -174,12 +215,14 @@ class GpuWorkerPool:
         self.hang_timeout_s = hang_timeout_s
         self.start_timeout_s = start_timeout_s
         self.env_extra = env_extra
-        self.events: "queue.Queue" = queue.Queue()
+        self.control: "queue.Queue" = queue.Queue()  # ready / init errors
+        self._lock = threading.RLock()               # worker ownership, in-flight maps, streams
+        self._init_lock = threading.Lock()           # one (re)spawn + init at a time
+        self.streams: Dict[int, _Stream] = {}        # arrival order
         self.workers: List[_Worker] = [self._spawn(i) for i in range(len(self.devices))]
         self.sid = 0
         self.deaths = 0
         self.per_worker_items: Dict[int, int] = {}
-        self._lock = threading.Lock()
         self._initialised = False
         if init:
             self.init()
@@ -195,15 +238,69 @@ class GpuWorkerPool:
                 cpus = os.cpu_count() or 1
             n_cpu = sum(1 for d in self.devices if d == "cpu")
             extra["OMP_NUM_THREADS"] = str(max(1, cpus // max(1, n_cpu)))
-        return _Worker(i, self.devices[i], self.events, extra)
+        return _Worker(i, self.devices[i], self, extra)
 
     @property
     def capacity(self) -> int:
+        """Classes in flight per worker: its KV slots plus a look-ahead, so
+        the continuous batch never drains while replies travel."""
         mb = int(self.model.get("max_batch", 256))
         return mb + max(2, mb // 2)
 
+    # ------------------------------------------------------------ frames
+    def _current(self, w: "_Worker") -> bool:
+        """False for frames of a worker that was already replaced."""
+        return 0 <= w.index < len(self.workers) and self.workers[w.index] is w
+
+    def _on_frame(self, w: _Worker, msg: Optional[dict]) -> None:
+        """Reader-thread entry: routes one frame (None = EOF) of ``w``."""
+        if not self._current(w):
+            return
+        if msg is None:
+            with self._lock:
+                if w.alive and not w.closing:
+                    LOG.error("worker %d on %s exited (rc=%s) holding %d classes", w.index, w.device,
+                              w.proc.poll(), w.held())
+                w.alive = False
+                self._rebalance()
+            self.control.put((w, None))
+            self._wake_all(("dead", w))
+            return
+        w.last_frame = time.monotonic()
+        op = msg.get("op")
+        if op in ("result", "done"):
+            s = self.streams.get(msg.get("sid"))
+            if s is not None:
+                s.events.put((w, msg))
+            elif op == "result":  # a finished / abandoned stream's late reply: only the bookkeeping
+                with self._lock:
+                    d = w.inflight.get(msg.get("sid"))
+                    if d is not None:
+                        for k, _ in msg["items"]:
+                            d.pop(k, None)
+                        if not d:
+                            w.inflight.pop(msg.get("sid"), None)
+            return
+        if op == "error":
+            LOG.error("worker %d on %s: %s", w.index, w.device, msg.get("msg"))
+            with self._lock:
+                w.kill()  # it exits on its own; never reused
+                self._rebalance()
+            self._wake_all(("dead", w))
+        self.control.put((w, msg))
+
+    def _wake_all(self, ev) -> None:
+        for s in list(self.streams.values()):
+            s.events.put(ev)
+
+    # ------------------------------------------------------------ life cycle
     def init(self) -> None:
-        """Builds the model in every worker (in parallel); waits for all."""
+        """Builds the model in every worker not yet ready (in parallel) and
+        waits for all of them."""
+        with self._init_lock:
+            self._init_locked()
+
+    def _init_locked(self) -> None:
         for w in self.workers:
             if w.alive and not w.ready:
                 w.send({"op": "init", "model": self.model, "engine": self.engine,
@@ -218,159 +315,236 @@ class GpuWorkerPool:
                         w.kill()
                 break
             try:
-                who, msg = self.events.get(timeout=min(1.0, left))
+                who, msg = self.control.get(timeout=min(1.0, left))
             except queue.Empty:
                 continue
-            if self._current(who):
-                self._handle_control(who.index, msg)
-        if not any(w.ready for w in self.workers):
+            if msg is not None and msg.get("op") == "ready" and self._current(who):
+                with self._lock:
+                    who.ready = True
+                    who.info = msg
+                    self._rebalance()
+                LOG.info("GPU worker %d ready on %s (pid %s)", who.index, who.device, msg.get("pid"))
+        if not any(w.ready and w.alive for w in self.workers):
             raise RuntimeError("no GPU worker started")
         self._initialised = True
 
-    def _current(self, w: "_Worker") -> bool:
-        """False for events of a worker that was already replaced."""
-        return 0 <= w.index < len(self.workers) and self.workers[w.index] is w
-
-    def _handle_control(self, i: int, msg: Optional[dict]) -> None:
-        w = self.workers[i]
-        if msg is None:
-            if w.alive:
-                LOG.error("worker %d on %s exited (rc=%s)", i, w.device, w.proc.poll())
-            w.alive = False
-            return
-        w.last_frame = time.monotonic()
-        if msg.get("op") == "ready":
-            w.ready = True
-            w.info = msg
-            LOG.info("GPU worker %d ready on %s (pid %s)", i, w.device, msg.get("pid"))
-        elif msg.get("op") == "error":
-            LOG.error("worker %d: %s", i, msg.get("msg"))
-
     def _replace_dead(self) -> None:
-        respawned = False
-        for i, w in enumerate(self.workers):
-            if not w.alive:
-                w.kill()
-                self.workers[i] = self._spawn(i)
-                respawned = True
-        if respawned:
-            self.init()
+        """Dead workers are replaced by fresh children (never restarted in
+        place); the new ones load the model while running streams go on."""
+        with self._init_lock:
+            respawned = False
+            with self._lock:
+                for i, w in enumerate(self.workers):
+                    if not w.alive:
+                        w.kill()
+                        self.workers[i] = self._spawn(i)
+                        respawned = True
+            if respawned:
+                self._init_locked()
+
+    def live(self) -> List[_Worker]:
+        return [w for w in self.workers if w.alive and w.ready]
+
+    # ------------------------------------------------------------ dealing
+    def _rebalance(self) -> None:
+        """Splits the live workers over the streams that still have classes
+        to deal (arrival order; the first ``n % k`` get one more), keeping
+        current owners where the split allows.  Caller holds ``_lock``."""
+        live = self.live()
+        wanting = [s for s in self.streams.values() if not s.exhausted]
+        quota: Dict[int, int] = {}
+        if wanting:
+            n, k = len(live), len(wanting)
+            for j, s in enumerate(wanting):
+                quota[s.sid] = n // k + (1 if j < n % k else 0)
+        kept: Dict[int, int] = {}
+        free: List[_Worker] = []
+        for w in live:
+            o = w.owner
+            if o is not None and o.sid in quota and kept.get(o.sid, 0) < quota[o.sid]:
+                kept[o.sid] = kept.get(o.sid, 0) + 1
+            else:
+                free.append(w)
+        # a free worker goes to the stream lacking the most; prefer workers
+        # that hold nothing, so no stream waits behind another's session
+        free.sort(key=lambda w: (w.held(), w.index))
+        for w in free:
+            lacking = [s for s in wanting if kept.get(s.sid, 0) < quota[s.sid]]
+            new = lacking[0] if lacking else None
+            self._assign(w, new)
+            if new is not None:
+                kept[new.sid] = kept.get(new.sid, 0) + 1
+        for w in self.workers:
+            if not (w.alive and w.ready):
+                w.owner = None
+
+    def _assign(self, w: _Worker, s: Optional[_Stream]) -> None:
+        old = w.owner
+        if old is s:
+            return
+        if old is not None and w in old.begun and w not in old.ended:
+            old.ended.add(w)  # it finishes what it holds of ``old``, then serves ``s``
+            w.send({"op": "end", "sid": old.sid})
+            old.events.put(("wake", w))
+        w.owner = s
+        if s is not None:
+            s.events.put(("wake", w))
+
+    def _top_up(self, s: _Stream) -> List[Tuple[int, Any]]:
+        """Begins ``s`` on the workers it owns and deals them its pending
+        classes (``ceil(pending / owned)`` each, at most ``capacity`` in
+        flight).  Returns failures to yield.  Caller holds ``_lock``."""
+        owned = [w for w in self.workers if w.owner is s and w.alive and w.ready]
+        fails: List[Tuple[int, Any]] = []
+        for w in owned:
+            if w not in s.begun:
+                s.begun.append(w)
+                if not w.send({"op": "begin", "sid": s.sid, "readme": s.readme}):
+                    w.alive = False
+        owned = [w for w in owned if w.alive]
+        if s.exhausted or not owned:
+            return fails
+        cap = self.capacity
+        rem = s.remaining()
+        if rem == 0:  # the caller's hint is used up but its iterator is not: deal by capacity
+            rem = None
+        held = [len(w.inflight.get(s.sid, ())) for w in owned]
+        if rem is None:
+            targets = [cap] * len(owned)
+        else:
+            q, r = divmod(rem + sum(held), len(owned))
+            # the +1 shares go to the workers already holding the most, so a
+            # top-up never moves work that is already balanced
+            order = sorted(range(len(owned)), key=lambda i: (-held[i], owned[i].index))
+            targets = [0] * len(owned)
+            for rank, i in enumerate(order):
+                targets[i] = min(cap, q + (1 if rank < r else 0))
+        chunk_min = max(1, cap // 8)
+        for w, h, t in zip(owned, held, targets):
+            need = t - h
+            if need <= 0 or (h and need < min(chunk_min, t // 2 or 1)):
+                continue
+            items = []
+            d = w.inflight.setdefault(s.sid, {})
+            while len(items) < need:
+                try:
+                    i, inp = next(s.src)
+                except StopIteration:
+                    s.exhausted = True
+                    break
+                s.taken += 1
+                items.append([i, _inp_to_wire(inp)])
+                d[i] = inp.full_class_name
+            if items:
+                if w.held() == len(items):  # an idle worker gets work: its hang clock starts now
+                    w.last_frame = time.monotonic()
+                self.per_worker_items[w.index] = self.per_worker_items.get(w.index, 0) + len(items)
+                s.items_per_worker[w.index] = s.items_per_worker.get(w.index, 0) + len(items)
+                w.sent += len(items)
+                if not w.send({"op": "items", "sid": s.sid, "items": items}):
+                    w.alive = False
+            if not d:
+                w.inflight.pop(s.sid, None)
+            if s.exhausted:
+                break
+        if s.exhausted:
+            self._rebalance()  # its workers may serve other streams once they drain it
+        return fails
+
+    def _fail_dead(self, s: _Stream) -> List[Tuple[int, Any]]:
+        out: List[Tuple[int, Any]] = []
+        for w in self.workers + [w for w in s.begun if w not in self.workers]:
+            if not w.alive and s.sid in w.inflight:
+                self.deaths += 1
+                for k in w.inflight.pop(s.sid):
+                    out.append((k, RuntimeError(f"GPU worker died (worker {w.index} on {w.device})")))
+        return out
+
+    def _complete(self, s: _Stream) -> bool:
+        if not s.exhausted:
+            return False
+        if any(s.sid in w.inflight for w in s.begun):
+            return False
+        return all(w in s.finished or not w.alive for w in s.begun)
 
     def stream(self, inputs: Iterable[EnrichmentInput], readme: Optional[str]
                ) -> Iterator[Tuple[int, Any]]:
         """Yields ``(input index, raw reply str | Exception)`` as replies
-        arrive, from whichever worker finished them.  A caller that stops
-        early (an exception while applying a reply) still ends the session
-        in every worker: each finishes what it was sent and then serves the
-        next stream (its late replies carry the old session id and are
-        dropped)."""
-        with self._lock:
-            self._open: List[_Worker] = []
-            try:
-                yield from self._stream(inputs, readme)
-            finally:
-                for w in self._open:
-                    if w.alive:
-                        w.send({"op": "end", "sid": self.sid})
-                self._open = []
-
-    def _stream(self, inputs, readme):
+        arrive, from whichever worker finished them.  Safe to run from
+        several threads at once (one stream per project).  A caller that
+        stops early still ends its session in every worker: each finishes
+        what it was sent (late replies are dropped) and serves the next."""
         self._replace_dead()
-        self.sid += 1
-        sid = self.sid
-        src = enumerate(inputs)
-        exhausted = False
-        live = [w for w in self.workers if w.alive and w.ready]
-        for w in live:
-            w.inflight.clear()
-            if not w.send({"op": "begin", "sid": sid, "readme": readme}):
-                w.alive = False
-        ended: set = set()
-        self._open = [w for w in live if w.alive]  # sessions to end if the caller stops early
-        finished: set = set()
-        cap = self.capacity
-        chunk_min = max(1, cap // 8)
+        with self._lock:
+            self.sid += 1
+            s = _Stream(self.sid, readme, inputs)
+            self.streams[s.sid] = s
+            self._rebalance()
+        try:
+            yield from self._run(s)
+        finally:
+            with self._lock:
+                for w in s.begun:
+                    if w not in s.ended and w.alive:
+                        s.ended.add(w)
+                        w.send({"op": "end", "sid": s.sid})
+                s.exhausted = True
+                self.streams.pop(s.sid, None)
+                for w in self.workers:
+                    if w.owner is s:
+                        w.owner = None
+                self._rebalance()
 
-        def top_up(w: _Worker) -> None:
-            nonlocal exhausted
-            need = cap - len(w.inflight)
-            if exhausted or need < (chunk_min if w.inflight else 1):
-                return
-            items = []
-            while len(items) < need:
-                try:
-                    i, inp = next(src)
-                except StopIteration:
-                    exhausted = True
-                    break
-                items.append([i, _inp_to_wire(inp)])
-                w.inflight[i] = inp.full_class_name
-            if items:
-                self.per_worker_items[w.index] = self.per_worker_items.get(w.index, 0) + len(items)
-                w.sent += len(items)
-                if not w.send({"op": "items", "sid": sid, "items": items}):
-                    w.alive = False
-
-        def fail(w: _Worker, why: str):
-            for k, name in list(w.inflight.items()):
-                yield k, RuntimeError(f"{why} (worker {w.index} on {w.device})")
-            w.inflight.clear()
-
+    def _run(self, s: _Stream) -> Iterator[Tuple[int, Any]]:
         while True:
-            live = [w for w in self.workers if w.alive and w.ready]
-            for w in live:
-                top_up(w)
-            for w in list(self.workers):
-                if not w.alive and w.inflight:
-                    self.deaths += 1
-                    yield from fail(w, "GPU worker died")
-            live = [w for w in self.workers if w.alive and w.ready]
-            if not live:
-                # nothing can run the rest: every remaining class fails
-                for i, inp in src:
-                    yield i, RuntimeError("no live GPU worker")
+            with self._lock:
+                out = self._fail_dead(s)
+                out += self._top_up(s)
+                for w in s.begun:  # dealt out: close the sessions so the engines drain
+                    if s.exhausted and w not in s.ended and w.alive:
+                        s.ended.add(w)
+                        w.send({"op": "end", "sid": s.sid})
+                starved = not self.live() and not s.exhausted
+                if starved:
+                    for i, inp in s.src:  # nothing can run the rest: every remaining class fails
+                        out.append((i, RuntimeError("no live GPU worker")))
+                    s.exhausted = True
+                    out += self._fail_dead(s)
+                done = self._complete(s)
+            yield from out
+            if done:
                 return
-            if exhausted:
-                for w in live:
-                    if w not in ended:
-                        w.send({"op": "end", "sid": sid})
-                        ended.add(w)
-                        if w in self._open:
-                            self._open.remove(w)
-                if all(w in finished or not w.alive for w in self.workers if w in ended) and \
-                        not any(w.inflight for w in self.workers):
-                    return
             try:
-                who, msg = self.events.get(timeout=1.0)
+                ev = s.events.get(timeout=1.0)
             except queue.Empty:
                 now = time.monotonic()
-                for w in live:
-                    if w.inflight and now - w.last_frame > self.hang_timeout_s:
-                        LOG.error("worker %d on %s sent nothing for %.0f s with %d classes: killing it", w.index,
-                                  w.device, self.hang_timeout_s, len(w.inflight))
-                        w.kill()
+                with self._lock:
+                    for w in s.begun:
+                        if w.alive and w.inflight.get(s.sid) and now - w.last_frame > self.hang_timeout_s:
+                            LOG.error("worker %d on %s sent nothing for %.0f s with %d classes: killing it",
+                                      w.index, w.device, self.hang_timeout_s, w.held())
+                            w.kill()
+                            self._rebalance()
                 continue
-            if not self._current(who):
-                continue
-            w, i = who, who.index
-            if msg is None:
-                if w.alive:
-                    LOG.error("worker %d on %s exited (rc=%s) holding %d classes", i, w.device, w.proc.poll(),
-                              len(w.inflight))
-                w.alive = False
-                continue
-            w.last_frame = time.monotonic()
-            op = msg.get("op")
-            if op == "result" and msg.get("sid") == sid:
-                for k, raw in msg["items"]:
-                    if w.inflight.pop(k, None) is not None:
-                        yield k, raw
-            elif op == "done" and msg.get("sid") == sid:
-                w.stats = msg.get("stats") or {}
-                finished.add(w)
-            elif op == "error":
-                LOG.error("worker %d on %s: %s", i, w.device, msg.get("msg"))
-                w.kill()  # it exits on its own; never reused
+            w, msg = ev
+            if not isinstance(msg, dict):
+                continue  # a wake-up: ownership or liveness changed
+            out = []
+            with self._lock:
+                if msg["op"] == "result":
+                    d = w.inflight.get(s.sid, {})
+                    for k, raw in msg["items"]:
+                        if d.pop(k, None) is not None:
+                            out.append((k, raw))
+                    if not d:
+                        w.inflight.pop(s.sid, None)
+                elif msg["op"] == "done":
+                    w.stats = msg.get("stats") or {}
+                    for k, v in w.stats.items():
+                        if isinstance(v, (int, float)):
+                            s.stats[k] = s.stats.get(k, 0) + v
+                    s.finished.add(w)
+            yield from out
 
     def stats(self) -> dict:
         agg: Dict[str, float] = {}
@@ -389,7 +563,9 @@ class GpuWorkerPool:
 
 class ProcessLLMBackend(EnrichmentBackend):
     """The service's local-model backend: a :class:`GpuWorkerPool` (one
-    process per GPU) behind the :class:`EnrichmentBackend` contract."""
+    process per GPU) behind the :class:`EnrichmentBackend` contract.  One
+    instance serves every caller of the service (REST requests, the sync
+    scheduler, bulk indexing threads) concurrently."""
 
     name = "local"
 
@@ -401,18 +577,8 @@ class ProcessLLMBackend(EnrichmentBackend):
     @classmethod
     def from_config(cls, cfg, devices: Optional[Sequence[str]] = None) -> "ProcessLLMBackend":
         if devices is None:
-            n = visible_gpus()
-            spec = (cfg.local_llm_devices or "all").strip()
-            ids = list(range(n)) if spec == "all" else [int(x) for x in spec.split(",") if x.strip()]
-            if not ids:
-                raise RuntimeError("the local enrichment backend needs a ROCm GPU (none visible)")
-            devices = [f"cuda:{d}" for d in ids]
-        mb = int(cfg.local_llm_max_batch)
-        model = {"preset": cfg.local_llm_preset, "kv_dtype": cfg.local_llm_kv_dtype, "max_batch": mb,
-                 "max_rows": max(256, mb * 3 // 2), "seed": 0}
-        if getattr(cfg, "local_llm_model_path", ""):
-            model["path"] = cfg.local_llm_model_path
-        return cls(GpuWorkerPool(devices, model))
+            devices = worker_devices(cfg.local_llm_devices)
+        return cls(GpuWorkerPool(devices, model_spec(cfg), engine=engine_spec(cfg)))
 
     def enrich_class(self, inp: EnrichmentInput, readme: Optional[str]) -> EnrichmentResult:
         return self.enrich_batch([inp], readme)[0]
@@ -426,12 +592,7 @@ class ProcessLLMBackend(EnrichmentBackend):
     def enrich_stream(self, inputs: Iterable[EnrichmentInput], readme: Optional[str]
                       ) -> Iterator[Tuple[int, EnrichmentResult]]:
         names: Dict[int, str] = {}
-
-        def tagged():
-            for i, inp in enumerate(inputs):
-                names[i] = inp.full_class_name
-                yield inp
-        for i, raw in self.pool.stream(tagged(), readme):
+        for i, raw in self.pool.stream(_Tagged(inputs, names), readme):
             name = names.pop(i, "?")
             if isinstance(raw, BaseException):
                 yield i, EnrichmentResult.failure(name, str(raw))
@@ -446,7 +607,93 @@ class ProcessLLMBackend(EnrichmentBackend):
         super().close()
 
 
+class _Tagged:
+    """The caller's inputs, recording each one's class name by index as it
+    is taken; keeps the caller's length hint for the pool's dealing."""
+
+    def __init__(self, inputs: Iterable[EnrichmentInput], names: Dict[int, str]) -> None:
+        self.inputs = inputs
+        self.names = names
+
+    def __length_hint__(self):
+        h = operator.length_hint(self.inputs, -1)
+        return h if h >= 0 else NotImplemented
+
+    def __iter__(self):
+        for i, inp in enumerate(self.inputs):
+            self.names[i] = inp.full_class_name
+            yield inp
+
+
+def worker_devices(spec: str) -> List[str]:
+    """Worker devices of ``LOCAL_LLM_DEVICES``: ``all`` (every visible GPU),
+    a comma list of GPU ids, or ``cpu`` entries (a CPU rehearsal worker each;
+    tests and hosts without a GPU)."""
+    spec = (spec or "all").strip()
+    if spec == "all":
+        devices = [f"cuda:{d}" for d in range(visible_gpus())]
+    else:
+        devices = ["cpu" if x.strip() == "cpu" else f"cuda:{int(x)}" for x in spec.split(",") if x.strip()]
+    if not devices:
+        raise RuntimeError("the local enrichment backend needs a ROCm GPU (none visible)")
+    return devices
+
+
+def model_spec(cfg) -> dict:
+    """The worker model spec of a :class:`dmcp.config.Config`."""
+    mb = int(cfg.local_llm_max_batch)
+    spec = {"preset": cfg.local_llm_preset, "kv_dtype": cfg.local_llm_kv_dtype, "max_batch": mb,
+            "max_rows": max(256, mb * 3 // 2), "seed": 0}
+    if getattr(cfg, "local_llm_model_path", ""):
+        spec["path"] = cfg.local_llm_model_path
+    return spec
+
+
+def engine_spec(cfg) -> dict:
+    """LocalEngine keyword arguments of a :class:`dmcp.config.Config`."""
+    return {"max_new_tokens": int(cfg.local_llm_max_new_tokens)}
+
+
 # ------------------------------------------------------------------ child
+class _EchoEngine:
+    """``preset: "echo"`` -- a model-free engine for rehearsing the pool on
+    the CPU: a continuous batch in which every class takes ``steps`` steps
+    of ``step_s`` seconds (latency-bound, like the GPU engine at these batch
+    sizes) and is answered with a grammar-shaped reply."""
+
+    def __init__(self, step_s: float = 0.05, max_batch: int = 512, steps: int = 1) -> None:
+        self.step_s = step_s
+        self.steps = max(1, steps)
+        self.max_batch = max_batch
+        self.stats: Dict[str, float] = {"decode_steps": 0, "prefills": 0}
+
+    def stream(self, feed, readme):
+        active: List[list] = []  # [steps left, key, input]
+        while True:
+            room = self.max_batch - len(active)
+            new = feed.take(room, wait=not active) if room > 0 else []
+            if not new and not active:
+                if feed.done:
+                    return
+                continue
+            self.stats["prefills"] += len(new)
+            active += [[self.steps, item[0], item[1]] for item in new]
+            time.sleep(self.step_s)
+            self.stats["decode_steps"] += 1
+            still = []
+            for a in active:
+                a[0] -= 1
+                if a[0] > 0:
+                    still.append(a)
+                    continue
+                inp = a[2]
+                yield a[1], json.dumps({"description": f"{inp.full_class_name} (pid {os.getpid()})",
+                                        "classTypeCorrection": None,
+                                        "methods": [{"methodName": m, "description": "does " + m,
+                                                     "businessLogic": ["step"]} for m in inp.method_names]})
+            active = still
+
+
 def worker_main() -> int:
     """``python -m dmcp.enrich.workers``: serve frames on stdin/stdout."""
     rx = sys.stdin.buffer
@@ -466,63 +713,76 @@ def worker_main() -> int:
     msg = recv_frame(rx)
     if msg is None or msg.get("op") != "init":
         return 0 if msg is None or msg.get("op") == "shutdown" else 2
-    import torch
-    from .local import LocalEngine, QueueFeed, build_model
     spec = msg["model"]
     dev = msg.get("device", "cuda:0")
-    try:
-        if dev.startswith("cuda"):
-            torch.cuda.set_device(0)
-        model, tok = build_model(spec, dev)
-        eng = LocalEngine(model, tokenizer=tok, **(msg.get("engine") or {}))
-    except Exception as e:
-        send({"op": "error", "msg": f"init failed: {e!r}"})
-        return 3
+    from .feeds import MultiFeed
+    if spec.get("preset") == "echo":
+        eng = _EchoEngine(float(spec.get("step_s", 0.05)), int(spec.get("max_batch", 512)), int(spec.get("steps", 1)))
+        max_batch = eng.max_batch
+    else:
+        import torch
+        from .local import LocalEngine, build_model
+        try:
+            if dev.startswith("cuda"):
+                torch.cuda.set_device(0)
+            model, tok = build_model(spec, dev)
+            eng = LocalEngine(model, tokenizer=tok, **(msg.get("engine") or {}))
+        except Exception as e:
+            send({"op": "error", "msg": f"init failed: {e!r}"})
+            return 3
+        max_batch = model.cfg.max_batch
     send({"op": "ready", "pid": os.getpid(), "device": dev,
-          "gpu": os.environ.get("HIP_VISIBLE_DEVICES", ""), "max_batch": model.cfg.max_batch})
+          "gpu": os.environ.get("HIP_VISIBLE_DEVICES", ""), "max_batch": max_batch})
 
-    sessions: "queue.Queue" = queue.Queue()
-    feeds: Dict[int, QueueFeed] = {}
+    # ONE engine stream over every session: the projects the pool deals this
+    # worker share its continuous batch (MultiFeed: round-robin over them)
+    feed = MultiFeed()
+    lock = threading.Lock()
+    outstanding: Dict[int, int] = {}        # sid -> classes received, reply not yet sent
+    closed: set = set()                     # sids whose ``end`` arrived
+    base: Dict[int, Dict[str, float]] = {}  # sid -> engine stats at its begin
+
+    def finish(sid: int) -> None:  # caller holds ``lock``
+        if sid in closed and outstanding.get(sid, 0) == 0:
+            st = {k: v - base.get(sid, {}).get(k, 0) for k, v in eng.stats.items() if isinstance(v, (int, float))}
+            outstanding.pop(sid, None)
+            closed.discard(sid)
+            base.pop(sid, None)
+            send({"op": "done", "sid": sid, "stats": st})
 
     def reader() -> None:
         while True:
             m = recv_frame(rx)
             if m is None or m.get("op") == "shutdown":
-                for f in feeds.values():
-                    f.close()
-                sessions.put(None)
+                feed.shutdown()
                 return
-            op = m.get("op")
-            if op == "begin":
-                f = QueueFeed()
-                feeds[m["sid"]] = f
-                sessions.put((m["sid"], m.get("readme"), f))
-            elif op == "items":
-                f = feeds.get(m["sid"])
-                if f is not None:
-                    f.put((k, _inp_from_wire(v)) for k, v in m["items"])
-            elif op == "end":
-                f = feeds.get(m["sid"])
-                if f is not None:
-                    f.close()
+            op, sid = m.get("op"), m.get("sid")
+            with lock:
+                if op == "begin":
+                    outstanding[sid] = 0
+                    base[sid] = dict(eng.stats)
+                    feed.begin(sid, m.get("readme"))
+                elif op == "items" and sid in outstanding:
+                    outstanding[sid] += len(m["items"])
+                    feed.put(sid, [(k, _inp_from_wire(v)) for k, v in m["items"]])
+                elif op == "end" and sid in outstanding:
+                    closed.add(sid)
+                    feed.end(sid)
+                    finish(sid)
 
     threading.Thread(target=reader, name="rx", daemon=True).start()
-    while True:
-        s = sessions.get()
-        if s is None:
-            return 0
-        sid, readme, feed = s
-        for k in eng.stats:
-            eng.stats[k] = 0
-        try:
-            for key, raw in eng.stream(feed, readme):
-                send({"op": "result", "sid": sid, "items": [[key, raw]]})
-        except Exception as e:  # a GPU-touched process is not reused after a failure
-            LOG.exception("engine failed")
-            send({"op": "error", "sid": sid, "msg": repr(e)})
-            return 4
-        feeds.pop(sid, None)
-        send({"op": "done", "sid": sid, "stats": dict(eng.stats)})
+    try:
+        for (sid, key), raw in eng.stream(feed, None):
+            send({"op": "result", "sid": sid, "items": [[key, raw]]})
+            with lock:
+                if sid in outstanding:
+                    outstanding[sid] -= 1
+                finish(sid)
+    except Exception as e:  # a GPU-touched process is not reused after a failure
+        LOG.exception("engine failed")
+        send({"op": "error", "msg": repr(e)})
+        return 4
+    return 0
 
 
 if __name__ == "__main__":

@@ -38,7 +38,7 @@ from dataclasses import dataclass, field
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
 from ..enrich.backend import EnrichmentBackend, NullBackend
-from ..enrich.types import EnrichmentInput, EnrichmentResult, normalize_method_name
+from ..enrich.types import EnrichmentInput, EnrichmentResult, SizedIter, normalize_method_name
 from ..graph.cache import GraphCache
 from ..graph.project_graph import MethodEnrichmentData, MethodInfo, ProjectGraph
 from ..models.domain import (ClassType, Project, ProjectStatus, RepositoryUrl, SourceClass,
@@ -540,11 +540,10 @@ class Indexer:
         flight (a sliding window, not 20-class barriers)."""
         read_failed = [0]
         total = len(idents)
+        pending = [i for i in idents if i in parsed.units]
 
-        def inputs():
-            for ident in idents:
-                if ident not in parsed.units:
-                    continue
+        def gen():
+            for ident in pending:
                 inp = self._input_for(ident, parsed, tree, class_types)
                 if inp is None:
                     read_failed[0] += 1
@@ -552,7 +551,9 @@ class Indexer:
                 yield inp
         enriched = failed = 0
         step = max(20, total // 10)
-        for n, (_, result) in enumerate(self.backend.enrich_stream(inputs(), readme), 1):
+        # lazy, but sized: a multi-GPU backend deals ceil(pending / GPUs) per GPU
+        inputs = SizedIter(gen(), len(pending))
+        for n, (_, result) in enumerate(self.backend.enrich_stream(inputs, readme), 1):
             if not result.success:
                 LOG.warning("%s: enrichment failed for %s: %s", phase, result.full_class_name, result.error_message)
                 failed += 1

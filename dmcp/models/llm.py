@@ -79,6 +79,9 @@ class LMConfig:
     max_batch: int = 256
     max_rows: int = 384             # token rows per batched decode/extend step (jump-forward)
     kv_dtype: str = "bf16"          # KV cache storage: "bf16" or "fp8" (e4m3, unit scale, half the bytes)
+    # the preset's tokenizer: "" = byte-level (dmcp.enrich.tokenizer.ByteTokenizer),
+    # else an asset directory under dmcp/models/assets (tokenizer.json.gz)
+    tokenizer: str = ""
 
     @property
     def qkv_dim(self) -> int:
@@ -101,8 +104,22 @@ PRESETS: Dict[str, LMConfig] = {
     "dmcp-coder-1b": LMConfig(),
     "dmcp-coder-3b": LMConfig(name="dmcp-coder-3b", hidden=3072, layers=28, n_heads=24, n_kv_heads=8,
                               head_dim=128, intermediate=8192),
+    # Llama-3.2-1B geometry with a production-size code vocabulary: 128,256
+    # ids (128,000 byte-level BPE pieces trained on source code, ~4 bytes per
+    # token, + the 256-id special block; scripts/train_code_bpe.py).  No
+    # checkpoint exists on this host, so weights are random: this preset pins
+    # the OPERATING POINT of a real 1B code model -- LM head of 263 M params
+    # (a fifth of the weight bytes per decode step), prompts and replies 3-4x
+    # fewer tokens than the byte preset's -- not its reply quality.
+    "llama3.2-1b-code": LMConfig(name="llama3.2-1b-code", vocab_size=128256, hidden=2048, layers=16, n_heads=32,
+                                 n_kv_heads=8, head_dim=64, intermediate=8192, rope_theta=500000.0,
+                                 tokenizer="code-bpe-128k"),
     "tiny": LMConfig(name="tiny", hidden=256, layers=2, n_heads=4, n_kv_heads=2, head_dim=64,
                      intermediate=512, max_seq=1024, max_batch=8, max_rows=64),
+    # the tiny model over the code BPE vocabulary (CPU tests of the 128k-id path)
+    "tiny-bpe": LMConfig(name="tiny-bpe", vocab_size=128256, hidden=256, layers=2, n_heads=4, n_kv_heads=2,
+                         head_dim=64, intermediate=512, max_seq=1024, max_batch=8, max_rows=64,
+                         tokenizer="code-bpe-128k"),
 }
 
 
@@ -444,10 +461,15 @@ class LocalLM:
 
     @torch.inference_mode()
     def decode(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor,
-               src: Optional[torch.Tensor] = None, last_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
+               src: Optional[torch.Tensor] = None, last_ids: Optional[torch.Tensor] = None,
+               mask_idx: Optional[torch.Tensor] = None, mask_alt: Optional[torch.Tensor] = None,
+               alt_token: int = -1, prefix_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
         """One token per row; all inputs int32 [B] on device.  With ``src`` /
         ``last_ids``: row r's token is ``last_ids[src[r]]`` where ``src[r] >= 0``
-        (gathered on the device by the step's first kernel).
+        (gathered on the device by the step's first kernel; with ``mask_alt``
+        a gathered ``alt_token`` switches ``mask_idx[r]`` to ``mask_alt[r]``).
+        ``prefix_rows`` (int32 [B]): 0 marks a row that does not use the
+        shared prefix (a sequence admitted with its whole prompt in its slot).
 
         Rows are independent (slot, position) pairs: several rows may extend
         the SAME slot at consecutive positions (jump-forward over forced
@@ -460,10 +482,11 @@ class LocalLM:
         if B > self.max_rows:
             raise ValueError(f"decode: {B} rows > max_rows {self.max_rows}")
         if self.use_fused and B <= self.fused_max_rows:
-            return self._decode_fused(tokens, slots, positions, src, last_ids)
+            return self._decode_fused(tokens, slots, positions, src, last_ids, mask_idx, mask_alt, alt_token,
+                                      prefix_rows)
         chunk, splits = ops.decode_plan(B, c.n_kv_heads, c.max_seq, c.kv_dtype)
         resid, h, seq_len = ops.decode_embed_norm(self.w["embed"], tokens, positions, self.w["l0.ln1"], c.eps,
-                                                  src, last_ids)
+                                                  src, last_ids, mask_idx, mask_alt, alt_token)
         wide = self.use_wgemm and B <= ops.WGEMM_MAX_ROWS
         for i in range(c.layers):
             kc, vc = self.k_cache[i], self.v_cache[i]
@@ -474,7 +497,7 @@ class LocalLM:
             else:
                 q = ops.rope_kv(F.linear(h, self.w[f"l{i}.wqkv"]), positions, slots, self.cos_sin, kc, vc, c.n_heads)
             att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws, chunk=chunk,
-                                       prefix=self._prefix(i), splits=splits).view(B, c.n_heads * c.head_dim)
+                                       prefix=self._prefix(i, prefix_rows), splits=splits).view(B, c.n_heads * c.head_dim)
             if wide:
                 h = ops.wgemm_resid_norm(att, self.w[f"l{i}.wo"], resid, self.w[f"l{i}.ln2"], c.eps, self.wgemm_ws)
                 act = ops.wgemm_swiglu(h, self.w[f"l{i}.wgu"])
@@ -486,14 +509,16 @@ class LocalLM:
             h = ops.add_rmsnorm(m, nxt, c.eps, residual=resid)
         return F.linear(h, self.w["lm_head"])
 
-    def _prefix(self, i: int):
+    def _prefix(self, i: int, rows: Optional[torch.Tensor] = None):
         if not self.shared_prefix:
             return None
         return ops.SharedPrefix(self.k_cache[i][self.prefix_slot], self.v_cache[i][self.prefix_slot],
-                                self.prefix_dev)
+                                self.prefix_dev, rows)
 
     def _decode_fused(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor,
-                      src: Optional[torch.Tensor] = None, last_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
+                      src: Optional[torch.Tensor] = None, last_ids: Optional[torch.Tensor] = None,
+                      mask_idx: Optional[torch.Tensor] = None, mask_alt: Optional[torch.Tensor] = None,
+                      alt_token: int = -1, prefix_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
         """The decode step on the fused gfx950 GEMMs: per layer QKV (+norm,
         RoPE, KV append) -> attention -> O (+residual) -> gate/up (+norm,
         SwiGLU) -> down (+residual); the residual stream ``r`` is updated in
@@ -501,12 +526,13 @@ class LocalLM:
         c = self.cfg
         B = tokens.shape[0]
         chunk, splits = ops.decode_plan(B, c.n_kv_heads, c.max_seq, c.kv_dtype)
-        r, _, seq_len = ops.decode_embed_norm(self.w["embed"], tokens, positions, None, c.eps, src, last_ids)
+        r, _, seq_len = ops.decode_embed_norm(self.w["embed"], tokens, positions, None, c.eps, src, last_ids,
+                                              mask_idx, mask_alt, alt_token)
         for i in range(c.layers):
             kc, vc = self.k_cache[i], self.v_cache[i]
             q = ops.fused_rope_kv(r, self.w[f"l{i}.wqkv"], c.eps, positions, slots, self.cos_sin, kc, vc, c.n_heads)
             att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws, chunk=chunk,
-                                       prefix=self._prefix(i), splits=splits)
+                                       prefix=self._prefix(i, prefix_rows), splits=splits)
             ops.fused_resid(att.view(B, c.n_heads * c.head_dim), self.w[f"l{i}.wo"], r)
             act = ops.fused_swiglu(r, self.w[f"l{i}.wgu"], c.eps)
             ops.fused_resid(act, self.w[f"l{i}.wdown"], r)
@@ -565,15 +591,18 @@ class LocalLM:
 
     def decode_select_gather(self, tokens: torch.Tensor, src: torch.Tensor, last_ids: torch.Tensor,
                              slots: torch.Tensor, positions: torch.Tensor, masks: torch.Tensor,
-                             mask_idx: torch.Tensor) -> tuple:
+                             mask_idx: torch.Tensor, mask_alt: Optional[torch.Tensor] = None,
+                             alt_token: int = -1, prefix_rows: Optional[torch.Tensor] = None) -> tuple:
         """:meth:`decode_select` whose input token of row r is ``last_ids[src[r]]``
         where ``src[r] >= 0`` (the previous step's selection, still on the
         device) and ``tokens[r]`` otherwise; the step's own selections are
         written to ``last_ids`` for the next step.  Lets the host launch step
         t+1 before it has read step t's ids (the engine's one-step pipeline).
+        ``mask_alt`` / ``alt_token`` / ``prefix_rows``: see :meth:`decode`.
         Capturable."""
         B = tokens.shape[0]
-        logits = self.decode(tokens, slots, positions, src=src, last_ids=last_ids)
+        logits = self.decode(tokens, slots, positions, src=src, last_ids=last_ids, mask_idx=mask_idx,
+                             mask_alt=mask_alt, alt_token=alt_token, prefix_rows=prefix_rows)
         ids = ops.masked_argmax(logits, masks, vocab=self.cfg.vocab_size, mask_idx=mask_idx, out=last_ids[:B])
         return logits, ids
 
@@ -616,8 +645,9 @@ class LocalLM:
 class DecodeGraphs:
     """hipGraph-captured decode + selection steps, one graph per row-count bucket.
 
-    Inputs travel as ONE packed int32 host buffer ``[5, n]`` (token, slot,
-    position, mask row, token source) -> one H2D copy into the graph's static
+    Inputs travel as ONE packed int32 host buffer ``[7, n]`` (token, slot,
+    position, mask row, token source, mask row if the gathered token is
+    ``alt_token``, uses-the-shared-prefix flag) -> one H2D copy into the graph's static
     input; the graph gathers the rows whose source is >= 0 from the previous
     step's selections (:attr:`last_ids`, device-resident, written by every
     step), runs the whole forward plus the masked argmax, so a step costs one
@@ -627,9 +657,10 @@ class DecodeGraphs:
 
     def __init__(self, model: LocalLM, masks: torch.Tensor,
                  buckets: Sequence[int] = (1, 2, 4, 8, 16, 32, 64, 96, 128, 192, 256, 320, 384, 448, 512, 640,
-                                          768, 896, 1024)) -> None:
+                                          768, 896, 1024), alt_token: int = -1) -> None:
         self.model = model
         self.masks = masks
+        self.alt_token = int(alt_token)
         self.buckets = sorted(b for b in buckets if b <= model.max_rows)
         if not self.buckets or self.buckets[-1] < model.max_rows:
             self.buckets.append(model.max_rows)
@@ -645,37 +676,48 @@ class DecodeGraphs:
 
     def _capture(self, b: int):
         m = self.model
-        inp = torch.zeros((5, b), dtype=torch.int32, device=m.device)
+        inp = torch.zeros((7, b), dtype=torch.int32, device=m.device)
         inp[1].fill_(-1)
         inp[4].fill_(-1)
-        stage = torch.zeros((5, b), dtype=torch.int32).pin_memory()
+        inp[5].fill_(-1)
+        stage = torch.zeros((7, b), dtype=torch.int32).pin_memory()
         scratch = torch.zeros_like(self.last_ids)  # warm-up must not clobber last_ids
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):  # warm up hipBLASLt heuristics / allocator outside capture
-                m.decode_select_gather(inp[0], inp[4], scratch, inp[1], inp[2], self.masks, inp[3])
+                m.decode_select_gather(inp[0], inp[4], scratch, inp[1], inp[2], self.masks, inp[3], inp[5],
+                                       self.alt_token, inp[6])
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            logits, ids = m.decode_select_gather(inp[0], inp[4], self.last_ids, inp[1], inp[2], self.masks, inp[3])
+            logits, ids = m.decode_select_gather(inp[0], inp[4], self.last_ids, inp[1], inp[2], self.masks, inp[3],
+                                                 inp[5], self.alt_token, inp[6])
         self.graphs[b] = (g, inp, stage, stage.numpy(), logits, ids, torch.cuda.Event())
 
     @torch.inference_mode()
     def run(self, tokens: Sequence[int], slots: Sequence[int], positions: Sequence[int],
-            mask_rows: Sequence[int], srcs: Optional[Sequence[int]] = None) -> tuple:
+            mask_rows: Sequence[int], srcs: Optional[Sequence[int]] = None,
+            alts: Optional[Sequence[int]] = None, prefix_rows: Optional[Sequence[int]] = None) -> tuple:
         """One step over ``n`` rows given as host lists (``srcs[r] >= 0``:
-        row r's token is row ``srcs[r]``'s selection of the previous step).
+        row r's token is row ``srcs[r]``'s selection of the previous step;
+        ``alts[r] >= 0``: row r's mask row when that token is ``alt_token``;
+        ``prefix_rows[r] == 0``: row r does not use the shared prefix).
         Returns (logits[:n], ids[:n]) -- device tensors owned by the graph."""
         n = len(tokens)
         m = self.model
         if srcs is None:
             srcs = [-1] * n
+        if alts is None:
+            alts = [-1] * n
+        if prefix_rows is None:
+            prefix_rows = [1] * n
         if not self.enabled:
-            t = torch.tensor([list(tokens), list(slots), list(positions), list(mask_rows), list(srcs)],
-                             dtype=torch.int32, device=m.device)
+            t = torch.tensor([list(tokens), list(slots), list(positions), list(mask_rows), list(srcs), list(alts),
+                              list(prefix_rows)], dtype=torch.int32, device=m.device)
             return m.decode_select_gather(t[0].contiguous(), t[4].contiguous(), self.last_ids, t[1].contiguous(),
-                                          t[2].contiguous(), self.masks, t[3].contiguous())
+                                          t[2].contiguous(), self.masks, t[3].contiguous(), t[5].contiguous(),
+                                          self.alt_token, t[6].contiguous())
         b = self.bucket_for(n)
         if b not in self.graphs:
             self._capture(b)
@@ -688,9 +730,12 @@ class DecodeGraphs:
         st[2, :n] = positions
         st[3, :n] = mask_rows
         st[4, :n] = srcs
+        st[5, :n] = alts
+        st[6, :n] = prefix_rows
         if n < b:
             st[1, n:] = -1
             st[4, n:] = -1
+            st[5, n:] = -1
         inp.copy_(stage, non_blocking=True)
         copied.record()
         g.replay()

@@ -65,10 +65,13 @@ def embedding(table, ids, out=None):
     return _on(table).embedding(table, ids, out)
 
 
-def decode_embed_norm(table, tokens, positions, weight, eps, src=None, last_ids=None):
+def decode_embed_norm(table, tokens, positions, weight, eps, src=None, last_ids=None, mask_idx=None, mask_alt=None,
+                      alt_token: int = -1):
     """(resid, h, seq_len) of a decode step: each row's token (``last_ids[src]``
-    where ``src >= 0``), its embedding, its first RMSNorm, its length."""
-    return _on(table).decode_embed_norm(table, tokens, positions, weight, eps, src, last_ids)
+    where ``src >= 0``), its embedding, its first RMSNorm, its length; a
+    gathered ``alt_token`` switches that row's grammar mask to ``mask_alt``."""
+    return _on(table).decode_embed_norm(table, tokens, positions, weight, eps, src, last_ids, mask_idx, mask_alt,
+                                        alt_token)
 
 
 # GPU-only fused GEMM with a shape-dependent default

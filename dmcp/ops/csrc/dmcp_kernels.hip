@@ -207,23 +207,26 @@ __global__ __launch_bounds__(kBlock) void decode_attn_combine_kernel(const float
                                                                     uint16_t* __restrict__ out, int B, int Hq,
                                                                     int max_seq, int chunk, int splits,
                                                                     int num_slots, const int32_t* __restrict__ plen,
-                                                                    int ps_max) {
+                                                                    int ps_max, const int32_t* __restrict__ prow) {
     constexpr int U = 8;
     constexpr int DQ = D / 4;       // lanes per partial group
     constexpr int PG = kWave / DQ;  // partial groups per wave
     const int lane = threadIdx.x & (kWave - 1);
     const int dg = lane % DQ, pg = lane / DQ;
-    const int P = plen ? max(0, *plen) : 0;
+    const int P0 = plen ? max(0, *plen) : 0;
     const int splits_total = ps_max + splits;
-    // the shared prefix's ps_max partials (prefill kernel in prefix mode;
-    // splits past the prefix's end are empty and weigh 0)
-    const int npre = P > 0 ? ps_max : 0;
     const int nwaves = gridDim.x * (kBlock / kWave);
     for (int w = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave; w < B * Hq; w += nwaves) {
         const int b = w / Hq, qh = w - b * Hq;
         const int s = slot[b];
         const int L = (s >= 0 && s < num_slots) ? min(seq_len[b], max_seq) : 0;
         if (L <= 0) continue;  // padding row: zeroed by the main kernel
+        // prow[b] == 0: a row outside the shared prefix (another project's
+        // sequence) -- all its keys are its own; its prefix partials unused
+        const int P = (prow && !prow[b]) ? 0 : P0;
+        // the shared prefix's ps_max partials (prefill kernel in prefix mode;
+        // splits past the prefix's end are empty and weigh 0)
+        const int npre = P > 0 ? ps_max : 0;
         const int nact = split_geom(L - P, splits, chunk).nact;
         if (nact <= 1) continue;  // finished by the main kernel (directly, or merging the prefix partials)
         const int n = npre + nact;
@@ -375,12 +378,21 @@ __global__ __launch_bounds__(kBlock) void decode_embed_norm_kernel(
     const uint16_t* __restrict__ table, const int32_t* __restrict__ tokens, const int32_t* __restrict__ src,
     const int32_t* __restrict__ last_ids, const int32_t* __restrict__ pos, const uint16_t* __restrict__ w,
     uint16_t* __restrict__ resid, uint16_t* __restrict__ h, int32_t* __restrict__ seq_len, int H, int V,
-    int n_last, float eps) {
+    int n_last, float eps, int32_t* __restrict__ mask_idx, const int32_t* __restrict__ mask_alt, int alt_token) {
     const int row = blockIdx.x;
     int id = tokens[row];
     if (src) {
         const int s = src[row];
-        if (s >= 0) id = last_ids[s < n_last ? s : n_last - 1];
+        if (s >= 0) {
+            id = last_ids[s < n_last ? s : n_last - 1];
+            // grammar: a gathered token that closes a free string (the
+            // engine's lone quote) switches this row's selection mask to the
+            // next segment's -- the host learns the token only a step later
+            if (mask_alt && threadIdx.x == 0 && id == alt_token) {
+                const int a = mask_alt[row];
+                if (a >= 0) mask_idx[row] = a;
+            }
+        }
     }
     id = id < 0 ? 0 : (id >= V ? V - 1 : id);
     if (threadIdx.x == 0) seq_len[row] = pos[row] + 1;
@@ -673,7 +685,7 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
     const int32_t* __restrict__ slot, const int32_t* __restrict__ seq_len, uint16_t* __restrict__ out,
     float* __restrict__ part_o, float* __restrict__ part_ml, int B, int Hkv, int G,
     int max_seq, int chunk, int splits, float scale_log2, int num_slots, const int32_t* __restrict__ plen,
-    int ps_max) {
+    int ps_max, const int32_t* __restrict__ prow) {
     static_assert(D % 32 == 0, "D must be a multiple of 32");
     constexpr int KS = D / 32;    // 32-dim k-steps of the S product
     constexpr int DB = D / 16;    // 16-row d blocks of O^T
@@ -686,7 +698,7 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int g16 = lane >> 4, c = lane & 15;
     const int Hq = Hkv * G;
-    const int P = __builtin_amdgcn_readfirstlane(plen ? max(0, *plen) : 0);
+    const int P0 = __builtin_amdgcn_readfirstlane(plen ? max(0, *plen) : 0);
     const int splits_total = ps_max + splits;
     const int total = B * Hkv * splits;
     uint16_t* vw = vlds[wave];
@@ -711,6 +723,8 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
                 for (int o = lane; o < G * D; o += kWave) out[((size_t)b * Hq + kh * G) * D + o] = 0;
             continue;
         }
+        // a row outside the shared prefix (prow[b] == 0) owns all its keys
+        const int P = __builtin_amdgcn_readfirstlane((prow && !prow[b]) ? 0 : P0);
         const SplitGeom sg = split_geom(L - P, splits, chunk);
         if (split >= max(1, sg.nact)) continue;
         // one own split: this wave writes the row's final output -- directly,
@@ -814,18 +828,18 @@ inline int grid_for(size_t work) {
 
 hipError_t launch_combine(void* part_o, void* part_ml, const int32_t* sl, const int32_t* ln, void* out, int B, int Hq,
                           int D, int max_seq, int chunk, int splits, int num_slots, const int32_t* pl, int ps_max,
-                          hipStream_t st) {
+                          const int32_t* pr, hipStream_t st) {
     const int waves = B * Hq;
     const int blocks = (waves + 3) / 4;
     const dim3 grid((unsigned)(blocks < 2048 ? blocks : 2048));
     if (D == 64)
         decode_attn_combine_kernel<64><<<grid, kBlock, 0, st>>>((const float*)part_o, (const float*)part_ml, sl, ln,
                                                                (uint16_t*)out, B, Hq, max_seq, chunk, splits,
-                                                               num_slots, pl, ps_max);
+                                                               num_slots, pl, ps_max, pr);
     else if (D == 128)
         decode_attn_combine_kernel<128><<<grid, kBlock, 0, st>>>((const float*)part_o, (const float*)part_ml, sl, ln,
                                                                 (uint16_t*)out, B, Hq, max_seq, chunk, splits,
-                                                                num_slots, pl, ps_max);
+                                                                num_slots, pl, ps_max, pr);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
@@ -835,7 +849,7 @@ hipError_t launch_combine(void* part_o, void* part_ml, const int32_t* sl, const 
 
 extern "C" {
 
-int dmcp_abi_version() { return 11; }
+int dmcp_abi_version() { return 12; }
 
 int dmcp_add_rmsnorm(const void* x, void* residual, const void* w, void* out, int rows, int H, float eps,
                      void* stream) {
@@ -875,10 +889,13 @@ int dmcp_rope_kv(const void* qkv, const void* pos, const void* slot, const void*
 // the MFMA prefill kernel in prefix mode into ps_max partials per row; the
 // per-row kernel covers keys [*plen, L).  Partials of both are merged by the
 // combine kernel; a row that fits one split with no prefix is written directly.
+// prefix_rows (optional, int32 [B]): 0 marks a row that does not use the
+// shared prefix (its keys [0, L) are all in its own slot).
 int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cache, const void* slot,
                           const void* seq_len, void* out, void* part_o, void* part_ml, int B, int Hq, int Hkv, int D,
                           int max_seq, int num_slots, int chunk, int splits, float scale, const void* prefix_k,
-                          const void* prefix_v, const void* plen, int ps_max, int kv8, void* stream) {
+                          const void* prefix_v, const void* plen, int ps_max, int kv8, const void* prefix_rows,
+                          void* stream) {
     if (B <= 0) return 0;
     if (Hkv <= 0 || Hq % Hkv != 0 || splits <= 0 || chunk <= 0 || !(D == 64 || D == 128) || Hq / Hkv > 16)
         return hipErrorInvalidValue;
@@ -893,6 +910,7 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
     auto sl = (const int32_t*)slot;
     auto ln = (const int32_t*)seq_len;
     auto pl = (const int32_t*)plen;
+    auto pr = prefix ? (const int32_t*)prefix_rows : nullptr;
     if (prefix) {
         hipError_t pe = dmcp_launch_prefix_partials(qq, prefix_k, prefix_v, pl, (float*)part_o, (float*)part_ml, B,
                                                     Hkv, G, D, max_seq, ps_max, ps_max + splits, sl2, kv8, st);
@@ -918,7 +936,7 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
         const dim3 wgrid((unsigned)(wblocks < cap ? wblocks : cap));                                               \
         decode_attn_mfma_kernel<DD, K8><<<wgrid, kBlock, 0, st>>>(qq, k_cache, v_cache, sl, ln, oo, po, pml, B,   \
                                                                   Hkv, G, max_seq, chunk, splits, sl2, num_slots, \
-                                                                  pl, ps_max);                                    \
+                                                                  pl, ps_max, pr);                                \
     } while (0)
     if (kv8) {
         if (D == 64) DMCP_MFMA_DECODE(64, true);
@@ -930,7 +948,8 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
 #undef DMCP_MFMA_DECODE
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || splits == 1) return e;  // every row finished in the main kernel
-    return launch_combine(part_o, part_ml, sl, ln, out, B, Hq, D, max_seq, chunk, splits, num_slots, pl, ps_max, st);
+    return launch_combine(part_o, part_ml, sl, ln, out, B, Hq, D, max_seq, chunk, splits, num_slots, pl, ps_max, pr,
+                          st);
 }
 
 int dmcp_silu_mul(const void* gu, void* out, int T, int I, void* stream) {
@@ -953,8 +972,10 @@ int dmcp_masked_argmax(const void* logits, const void* mask, const void* mask_id
 
 int dmcp_decode_embed_norm(const void* table, const void* tokens, const void* src, const void* last_ids,
                            const void* pos, const void* w, void* resid, void* h, void* seq_len, int rows, int H,
-                           int V, int n_last, float eps, void* stream) {
-    if (H % 8 != 0 || H > kBlock * 8 * 4 || V <= 0 || (src && (!last_ids || n_last <= 0)) || (h && !w))
+                           int V, int n_last, float eps, void* mask_idx, const void* mask_alt, int alt_token,
+                           void* stream) {
+    if (H % 8 != 0 || H > kBlock * 8 * 4 || V <= 0 || (src && (!last_ids || n_last <= 0)) || (h && !w) ||
+        (mask_alt && (!mask_idx || !src)))
         return hipErrorInvalidValue;
     if (rows <= 0) return 0;
     auto st = (hipStream_t)stream;
@@ -962,7 +983,8 @@ int dmcp_decode_embed_norm(const void* table, const void* tokens, const void* sr
     auto args = [&](auto kern) {
         kern<<<rows, kBlock, 0, st>>>((const uint16_t*)table, (const int32_t*)tokens, (const int32_t*)src,
                                       (const int32_t*)last_ids, (const int32_t*)pos, (const uint16_t*)w,
-                                      (uint16_t*)resid, (uint16_t*)h, (int32_t*)seq_len, H, V, n_last, eps);
+                                      (uint16_t*)resid, (uint16_t*)h, (int32_t*)seq_len, H, V, n_last, eps,
+                                      (int32_t*)mask_idx, (const int32_t*)mask_alt, alt_token);
     };
     if (vpt == 1) args(decode_embed_norm_kernel<1>);
     else if (vpt == 2) args(decode_embed_norm_kernel<2>);

@@ -26,7 +26,7 @@ _lock = threading.Lock()
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _f = ctypes.c_float
-ABI_VERSION = 11  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
+ABI_VERSION = 12  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
 
 
 class HipOpsError(RuntimeError):
@@ -53,7 +53,7 @@ def lib() -> ctypes.CDLL:
             "dmcp_add_rmsnorm": ([_vp, _vp, _vp, _vp, _i, _i, _f, _vp], _i),
             "dmcp_rope_kv": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp], _i),
             "dmcp_decode_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _f,
-                                       _vp, _vp, _vp, _i, _i, _vp], _i),
+                                       _vp, _vp, _vp, _i, _i, _vp, _vp], _i),
             "dmcp_prefill_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _i, _i,
                                         _i, _vp], _i),
             "dmcp_prefill_varlen": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, ctypes.c_long, _f,
@@ -61,7 +61,8 @@ def lib() -> ctypes.CDLL:
             "dmcp_silu_mul": ([_vp, _vp, _i, _i, _vp], _i),
             "dmcp_masked_argmax": ([_vp, _vp, _vp, _i, _vp, _i, _i, _i, _vp], _i),
             "dmcp_embedding": ([_vp, _vp, _vp, _i, _i, _i, _vp], _i),
-            "dmcp_decode_embed_norm": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp], _i),
+            "dmcp_decode_embed_norm": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp,
+                                        _i, _vp], _i),
             "dmcp_fused_gemm_max_rows": ([], _i),
             "dmcp_wgemm": ([_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp], _i),
             "dmcp_wgemm_resid_norm": ([_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _vp], _i),
@@ -224,7 +225,10 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     attended by the MFMA prefill kernel in prefix mode (every prefix key read
     once per 32 queries, :func:`prefix_mfma_splits` key splits); the per-row
     kernel covers the keys after it.  The length lives in device memory, so
-    a captured graph follows prefix changes (0 = no prefix)."""
+    a captured graph follows prefix changes (0 = no prefix).  ``prefix.rows``
+    (int32 [B], optional): rows marked 0 do not use the prefix -- all their
+    keys are in their own slot (a sequence of another project, admitted while
+    this prefix is resident)."""
     B, Hq, D = q.shape
     S, Hkv, MAXS, Dk = k_cache.shape
     _req(q, torch.bfloat16, "decode_attention.q")
@@ -242,7 +246,7 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     if not 1 <= splits <= max_splits:
         raise HipOpsError(f"decode_attention: splits {splits} outside [1, {max_splits}]")
     ps_max = 0
-    pk = pv = plen = None
+    pk = pv = plen = prows = None
     if prefix is not None:
         # the shared prefix on the MFMA prefill kernel in prefix mode: K / V
         # rows of the prefix slot, ps_max key splits per query tile
@@ -254,6 +258,11 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
             raise HipOpsError(f"decode_attention: prefix k {tuple(pk.shape)} / v {tuple(pv.shape)} do not match "
                               f"kv {tuple(k_cache.shape)}")
         ps_max = prefix_mfma_splits(B, Hq // Hkv, Hkv)
+        prows = getattr(prefix, "rows", None)
+        if prows is not None:
+            _req(prows, torch.int32, "decode_attention.prefix.rows")
+            if prows.numel() < B:
+                raise HipOpsError("decode_attention: prefix.rows has fewer than B entries")
         if workspace is not None and workspace[1].numel() < 2 * B * Hq * (splits + ps_max):
             raise HipOpsError(f"decode_attention: workspace holds fewer than {splits} + {ps_max} partials per row")
     out = torch.empty_like(q) if out is None else out
@@ -269,7 +278,7 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
         part_o = part_ml = None
     _check(lib().dmcp_decode_attention(_ptr(q), _ptr(k_cache), _ptr(v_cache), _ptr(slot), _ptr(seq_len), _ptr(out),
                                        _ptr(part_o), _ptr(part_ml), B, Hq, Hkv, D, MAXS, S, chunk, splits,
-                                       float(scale), _ptr(pk), _ptr(pv), _ptr(plen), ps_max, kv8,
+                                       float(scale), _ptr(pk), _ptr(pv), _ptr(plen), ps_max, kv8, _ptr(prows),
                                        _stream()), "dmcp_decode_attention")
     return out
 
@@ -475,11 +484,15 @@ def embedding(table: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor
 
 def decode_embed_norm(table: torch.Tensor, tokens: torch.Tensor, positions: torch.Tensor,
                       weight: Optional[torch.Tensor], eps: float, src: Optional[torch.Tensor] = None,
-                      last_ids: Optional[torch.Tensor] = None) -> tuple:
+                      last_ids: Optional[torch.Tensor] = None, mask_idx: Optional[torch.Tensor] = None,
+                      mask_alt: Optional[torch.Tensor] = None, alt_token: int = -1) -> tuple:
     """Decode-step inputs in one launch: row r's token is
     ``last_ids[src[r]]`` where ``src[r] >= 0`` (else ``tokens[r]``); returns
     (resid = its embedding row, h = RMSNorm(resid) * weight -- None when
-    ``weight`` is None --, seq_len = positions + 1).  Capturable."""
+    ``weight`` is None --, seq_len = positions + 1).  With ``mask_alt``: a
+    gathered token equal to ``alt_token`` sets ``mask_idx[r] = mask_alt[r]``
+    where that is >= 0 (in place; the step's masked argmax reads it after).
+    Capturable."""
     _req(table, torch.bfloat16, "decode_embed_norm.table")
     _req(tokens, torch.int32, "decode_embed_norm.tokens")
     _req(positions, torch.int32, "decode_embed_norm.positions")
@@ -500,12 +513,22 @@ def decode_embed_norm(table: torch.Tensor, tokens: torch.Tensor, positions: torc
         _req(last_ids, torch.int32, "decode_embed_norm.last_ids")
         if src.numel() != B or last_ids.numel() == 0:
             raise HipOpsError("decode_embed_norm: src length / last_ids size")
+    if mask_alt is not None:
+        _req(mask_alt, torch.int32, "decode_embed_norm.mask_alt")
+        if mask_idx is None or src is None:
+            raise HipOpsError("decode_embed_norm: mask_alt needs mask_idx and src")
+        _req(mask_idx, torch.int32, "decode_embed_norm.mask_idx")
+        if mask_alt.numel() != B or mask_idx.numel() != B:
+            raise HipOpsError("decode_embed_norm: mask_idx / mask_alt length != rows")
     resid = torch.empty((B, H), dtype=torch.bfloat16, device=table.device)
     h = torch.empty_like(resid) if weight is not None else None
     seq_len = torch.empty(B, dtype=torch.int32, device=table.device)
+    alt = mask_alt is not None
     _check(lib().dmcp_decode_embed_norm(_ptr(table), _ptr(tokens), _ptr(src), _ptr(last_ids), _ptr(positions),
                                         _ptr(weight), _ptr(resid), _ptr(h), _ptr(seq_len), B, H, V,
-                                        0 if last_ids is None else last_ids.numel(), float(eps), _stream()),
+                                        0 if last_ids is None else last_ids.numel(), float(eps),
+                                        _ptr(mask_idx) if alt else None, _ptr(mask_alt) if alt else None,
+                                        int(alt_token), _stream()),
            "dmcp_decode_embed_norm")
     return resid, h, seq_len
 

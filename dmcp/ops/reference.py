@@ -85,12 +85,14 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos_sin: t
 
 
 class SharedPrefix(NamedTuple):
-    """Keys/values shared by every row of a decode step (cascade decoding):
-    ``k`` / ``v`` [Hkv, MAXS, D] (the prefix slot of the caches) and
-    ``length`` int32 [1] on the device (0 = no prefix)."""
+    """Keys/values shared by the rows of a decode step (cascade decoding):
+    ``k`` / ``v`` [Hkv, MAXS, D] (the prefix slot of the caches),
+    ``length`` int32 [1] on the device (0 = no prefix) and ``rows`` (int32
+    [B], optional: 0 = this row does not use the prefix)."""
     k: torch.Tensor
     v: torch.Tensor
     length: torch.Tensor
+    rows: Optional[torch.Tensor] = None
 
 
 def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: torch.Tensor,
@@ -107,7 +109,7 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
             continue
         k = kv_float(k_cache[s, :, :L])  # [Hkv, L, D]
         v = kv_float(v_cache[s, :, :L])
-        if P > 0:  # the first P keys come from the shared prefix
+        if P > 0 and (prefix.rows is None or int(prefix.rows[b]) != 0):  # the first P keys: the shared prefix
             k = torch.cat([kv_float(prefix.k[:, :P]), k[:, P:]], dim=1)
             v = torch.cat([kv_float(prefix.v[:, :P]), v[:, P:]], dim=1)
         qb = q[b].float().view(Hkv, G, D)
@@ -202,13 +204,19 @@ def embedding(table: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor
 
 def decode_embed_norm(table: torch.Tensor, tokens: torch.Tensor, positions: torch.Tensor,
                       weight: Optional[torch.Tensor], eps: float, src: Optional[torch.Tensor] = None,
-                      last_ids: Optional[torch.Tensor] = None) -> tuple:
-    """(resid, h, seq_len) of the decode step's first op (see the HIP kernel)."""
+                      last_ids: Optional[torch.Tensor] = None, mask_idx: Optional[torch.Tensor] = None,
+                      mask_alt: Optional[torch.Tensor] = None, alt_token: int = -1) -> tuple:
+    """(resid, h, seq_len) of the decode step's first op (see the HIP kernel);
+    ``mask_alt``: gathered rows whose token is ``alt_token`` switch
+    ``mask_idx`` (in place) to ``mask_alt`` where that is >= 0."""
     toks = tokens
     if src is not None:
         s = src.long()
         gathered = last_ids.long()[s.clamp(0, last_ids.numel() - 1)].to(tokens.dtype)
         toks = torch.where(s >= 0, gathered, tokens)
+        if mask_alt is not None:
+            sw = (s >= 0) & (gathered == alt_token) & (mask_alt >= 0)
+            mask_idx.copy_(torch.where(sw, mask_alt, mask_idx))
     resid = embedding(table, toks)
     h = add_rmsnorm(resid, weight, eps) if weight is not None else None
     return resid, h, positions + 1

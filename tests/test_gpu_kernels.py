@@ -248,3 +248,50 @@ def test_decode_embed_norm_matches_reference(H, with_norm, with_src):
         torch.testing.assert_close(h.cpu().float(), hr.float(), atol=2e-2, rtol=2e-2)
     else:
         assert h is None
+
+
+@pytest.mark.parametrize("splits", [1, 4])
+@pytest.mark.parametrize("B", [3, 40, 97])
+def test_decode_attention_rows_off_the_prefix(hip, splits, B):
+    """Rows flagged 0 in prefix.rows (another project's sequences, admitted
+    while this prefix is resident) attend to their own slot from key 0; the
+    flagged rows keep the shared prefix -- both in one launch, vs fp32."""
+    from dmcp.ops import reference
+    from dmcp.ops.reference import SharedPrefix
+    D, Hq, Hkv, MAXS, S, P = 64, 32, 8, 1024, 8, 333
+    q = _bf(B, Hq, D, seed=31)
+    kc = _bf(S + 1, Hkv, MAXS, D, seed=32)
+    vc = _bf(S + 1, Hkv, MAXS, D, seed=33)
+    slot = torch.tensor([b % S for b in range(B)], dtype=torch.int32, device="cuda")
+    rows = torch.tensor([b % 3 != 1 for b in range(B)], dtype=torch.int32, device="cuda")
+    lens = torch.tensor([P + 1 + (b * 53) % 600 for b in range(B)], dtype=torch.int32, device="cuda")
+    pre = SharedPrefix(kc[S], vc[S], torch.tensor([P], dtype=torch.int32, device="cuda"), rows)
+    got = hip.decode_attention(q, kc, vc, slot, lens, 0.125, chunk=64, prefix=pre, splits=splits)
+    exp = reference.decode_attention(q, kc, vc, slot, lens, 0.125, prefix=pre)
+    torch.testing.assert_close(got.float(), exp.float(), atol=2e-2, rtol=2e-2)
+    # unflagged rows == no prefix at all
+    off = rows.cpu() == 0
+    plain = reference.decode_attention(q, kc, vc, slot, lens, 0.125)
+    torch.testing.assert_close(got[off.cuda()].float(), plain[off].float(), atol=2e-2, rtol=2e-2)
+
+
+def test_decode_embed_norm_switches_the_grammar_mask(hip):
+    """A gathered token equal to alt_token switches that row's mask index to
+    mask_alt (where >= 0); literal rows and other tokens keep theirs."""
+    from dmcp.ops import reference
+    g = torch.Generator().manual_seed(5)
+    V, H, B, Q = 320, 256, 64, 34
+    table = torch.randn(V, H, generator=g).to(torch.bfloat16).cuda()
+    tokens = torch.randint(0, V, (B,), generator=g, dtype=torch.int32)
+    pos = torch.arange(B, dtype=torch.int32)
+    src = torch.tensor([b % 4 - 1 for b in range(B)], dtype=torch.int32)  # -1 literal, else gathered
+    last = torch.tensor([Q, 7, Q], dtype=torch.int32)
+    midx = torch.tensor([b % 2 for b in range(B)], dtype=torch.int32)
+    alt = torch.tensor([5 if b % 5 else -1 for b in range(B)], dtype=torch.int32)
+    m_hip = midx.clone().cuda()
+    hip.decode_embed_norm(table, tokens.cuda(), pos.cuda(), None, 1e-5, src.cuda(), last.cuda(), m_hip, alt.cuda(), Q)
+    m_ref = midx.clone()
+    reference.decode_embed_norm(table.cpu().float(), tokens, pos, None, 1e-5, src, last, m_ref, alt, Q)
+    assert torch.equal(m_hip.cpu(), m_ref)
+    exp = [5 if (s >= 0 and int(last[s]) == Q and a >= 0) else int(m) for s, a, m in zip(src, alt, midx)]
+    assert m_ref.tolist() == exp and exp != midx.tolist()

@@ -187,3 +187,28 @@ def test_engine_batched_admission_matches_one_class_at_a_time(model):
     same = sum(a[:head] == b[:head] for a, b in zip(together, alone))
     assert same >= 21, list(zip(together, alone))
     assert eng.stats["prefill_batches"] >= 2
+
+
+@pytest.mark.gpu
+def test_gpu_engine_choices_and_mixed_projects_match_the_synchronous_loop():
+    """The hipGraph engine with the device-side grammar-mask switch and rows
+    off the shared prefix (two projects' classes in one batch) generates what
+    the host-synchronous loop does, and every reply parses."""
+    import json
+    from dmcp.enrich.local import CLASS_TYPES, LocalEngine
+    from dmcp.enrich.types import EnrichmentInput
+    from dmcp.models.llm import LocalLM, preset
+    m = LocalLM(preset("tiny", max_batch=16, max_rows=64, max_seq=2048), device="cuda:0", seed=4)
+    ra, rb = "Project A README. " * 12, "Another project B, its own README. " * 12
+    items = [(i, EnrichmentInput("class C%d { void a() {} }" % i, f"co.p.C{i}", "java", "SERVICE",
+                                 ["a", "b", "c", "d"][: 1 + i % 4]), ra if i % 3 else rb) for i in range(20)]
+    pipe = LocalEngine(m)
+    got = dict(pipe.stream(items, None))
+    sync = LocalEngine(m, pipeline=False, use_graphs=False)
+    ref = dict(sync.stream(items, None))
+    assert sum(got[k] == ref[k] for k in ref) >= 18, "pipelined graphs diverge from the synchronous loop"
+    for k, raw in got.items():
+        doc = json.loads(raw)
+        assert doc["classTypeCorrection"] is None or doc["classTypeCorrection"] in CLASS_TYPES
+        assert all(1 <= len(x["businessLogic"]) <= 3 for x in doc["methods"])
+    assert pipe.stats["unshared_prefills"] > 0

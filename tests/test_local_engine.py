@@ -7,8 +7,8 @@ import json
 import pytest
 import torch
 
-from dmcp.enrich.local import (LocalEngine, LocalLLMBackend, build_template, fit_template, template_budget,
-                               _json_safe_mask)
+from dmcp.enrich.local import (CLASS_TYPES, LocalEngine, LocalLLMBackend, build_template, fit_template, merge_parts,
+                               plan_reply, template_budget, _json_safe_mask)
 from dmcp.enrich.types import EnrichmentInput
 from dmcp.models.llm import LocalLM, preset
 
@@ -35,14 +35,37 @@ def test_json_safe_mask():
 
 def test_template_budget_and_fit():
     inp = _inputs(3)[2]
-    segs = build_template(inp)
+    segs = build_template(inp.method_names)
     assert segs[0].forced == b'{"description": "' and segs[1].forced is None
     assert all(not (a.forced is not None and b.forced is not None) for a, b in zip(segs, segs[1:]))
+    assert segs[3].choice == 0 and len(segs[3].then) == 11  # classTypeCorrection: null | 10 types
     big = template_budget(segs)
     small = fit_template(inp, big // 2)
     assert template_budget(small) <= big // 2
     many = EnrichmentInput("x", "a.B", "java", "OTHER", [f"m{i}" for i in range(200)])
     assert template_budget(fit_template(many, 300)) <= 300
+
+
+def test_plan_reply_splits_instead_of_dropping():
+    """No silent drops: methods that do not fit one reply go to continuation
+    parts, each within the budget, together covering every method in order."""
+    names = [f"method{i}" for i in range(60)]
+    parts, dropped = plan_reply(names, 1024)
+    assert dropped == 0 and len(parts) > 1
+    assert all(template_budget(p) <= 1024 for p in parts)
+    covered = []
+    for p in parts:
+        for seg in p:
+            if seg.forced and b'"methodName": ' in seg.forced:
+                covered += [json.loads(x.split(b", ")[0]) for x in seg.forced.split(b'"methodName": ')[1:]]
+    assert covered == names
+    assert parts[1][0].forced.startswith(b'{"description": "", "classTypeCorrection": null')
+    merged = json.loads(merge_parts(['{"description": "d", "classTypeCorrection": "DTO", "methods": [{"methodName": "a"}]}',
+                                     '{"description": "", "classTypeCorrection": null, "methods": [{"methodName": "b"}]}']))
+    assert merged["description"] == "d" and merged["classTypeCorrection"] == "DTO"
+    assert [m["methodName"] for m in merged["methods"]] == ["a", "b"]
+    one, d1 = plan_reply(["x" * 5000], 1024)
+    assert d1 == 1  # a method name longer than the budget is the only drop, and it is counted
 
 
 def test_engine_valid_json_and_continuous_batching(tiny):
@@ -52,7 +75,8 @@ def test_engine_valid_json_and_continuous_batching(tiny):
     for r, inp in zip(raw, inputs):
         doc = json.loads(r)
         assert [m["methodName"] for m in doc["methods"]] == inp.method_names
-        assert doc["classTypeCorrection"] is None and len(doc["methods"][0]["businessLogic"]) == 2
+        assert doc["classTypeCorrection"] is None or doc["classTypeCorrection"] in CLASS_TYPES
+        assert all(1 <= len(m["businessLogic"]) <= 3 for m in doc["methods"])
     assert eng.stats["prefills"] == 7 and eng.stats["decode_steps"] > 0
 
 
@@ -130,9 +154,7 @@ def test_engine_prompt_prefix_detection(tiny):
     readme = "A README shared by every prompt of the batch. " * 3
 
     def seq(inp):
-        s = _Seq(inp, 0, eng._encode_forced(fit_template(inp, 512)))
-        s.prompt = eng._build_prompt(s, readme)
-        return s
+        return eng._seqs_for(0, inp, readme)[0]
     sa, sb = seq(_inputs(1)[0]), seq(_inputs(2)[1])
     a, b = sa.prompt, sb.prompt
     P = eng._seq_prefix_len(sa)
@@ -166,16 +188,20 @@ def test_engine_streams_results_as_they_finish(tiny):
     assert sorted(seen) == list(range(12))
 
 
-def test_engine_defers_prompts_without_the_session_prefix(tiny):
-    """A prompt whose prefix differs (another language) runs in a second pass
-    with its own prefix instead of attending to the wrong one."""
-    eng = LocalEngine(tiny, use_graphs=False)
-    inputs = _inputs(4)
-    inputs[2] = EnrichmentInput(inputs[2].source_code, inputs[2].full_class_name, "kotlin", "SERVICE", ["a"])
+def test_engine_admits_other_prefixes_unshared(tiny):
+    """A prompt whose prefix differs (another project's README) runs next to
+    the others with its whole prompt in its own slot -- never attending to
+    the wrong prefix -- and equals its reply generated alone."""
     readme = "A README shared by every prompt of the batch. " * 3
-    out = eng.generate(inputs, readme)
-    assert all(json.loads(o) for o in out)
-    assert eng.stats["prefix_tokens"] > 2 * 64  # two prefix sessions
+    other = "Another project entirely, with its own README text. " * 3
+    inputs = _inputs(4)
+    mixed = [(i, inp, other if i == 2 else readme) for i, inp in enumerate(inputs)]
+    eng = LocalEngine(tiny, use_graphs=False)
+    out = dict(eng.stream(mixed, None))
+    assert all(json.loads(o) for o in out.values())
+    assert eng.stats["unshared_prefills"] >= 1
+    alone = LocalEngine(tiny, use_graphs=False, shared_prefix=False).generate([inputs[2]], other)[0]
+    assert out[2] == alone
 
 
 def test_prefill_batch_matches_single_prefills(tiny):
@@ -264,3 +290,94 @@ def test_fused_shape_contract():
     assert not fused_shapes_ok(preset("tiny", vocab_size=32001))
     assert not fused_shapes_ok(preset("tiny", vocab_size=50257))
     assert not fused_shapes_ok(preset("tiny", intermediate=520))
+
+
+class _Forcing(LocalLM):
+    """The tiny model with a fixed bias added to every logit row: greedy
+    decoding then follows the bias wherever the grammar leaves a choice."""
+
+    def __init__(self, bias, **kw):
+        super().__init__(preset("tiny", max_batch=4, max_rows=16, max_seq=2048), device="cpu", seed=1, **kw)
+        self.bias = torch.zeros(self.cfg.vocab_size)
+        for ch, v in bias.items():
+            self.bias[ord(ch)] = v
+
+    def _biased(self, logits):
+        return (logits.float() + self.bias).to(logits.dtype)
+
+    def decode(self, *a, **kw):
+        return self._biased(super().decode(*a, **kw))
+
+    def prefill_batch(self, reqs):
+        return self._biased(super().prefill_batch(reqs))
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_class_type_correction_is_the_models_choice(pipeline):
+    """classTypeCorrection is a grammar choice (null or one of the 10 types,
+    ClaudeApiClient.java:101-120): a model that prefers '"', 'E', 'N' writes
+    "ENTITY"; one that prefers 'n' writes null."""
+    ent = LocalEngine(_Forcing({'"': 30.0, "E": 25.0, "N": 20.0}), pipeline=pipeline)
+    doc = json.loads(ent.generate(_inputs(2)[1:], None)[0])
+    assert doc["classTypeCorrection"] == "ENTITY" and ent.stats["type_corrections"] == 1
+    keep = LocalEngine(_Forcing({"n": 30.0, "]": 20.0}), pipeline=pipeline)
+    doc = json.loads(keep.generate(_inputs(2)[1:], None)[0])
+    assert doc["classTypeCorrection"] is None
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_business_logic_length_is_the_models_choice(pipeline):
+    """1..3 steps, closed when the model picks ']' (any length) or ', "'."""
+    stop = LocalEngine(_Forcing({'"': 30.0, "]": 25.0, "n": 26.0}), pipeline=pipeline)
+    doc = json.loads(stop.generate(_inputs(3)[2:], None)[0])
+    assert [len(m["businessLogic"]) for m in doc["methods"]] == [1, 1, 1]
+    more = LocalEngine(_Forcing({'"': 30.0, ",": 25.0, "n": 26.0}), pipeline=pipeline)
+    doc = json.loads(more.generate(_inputs(3)[2:], None)[0])
+    assert [len(m["businessLogic"]) for m in doc["methods"]] == [3, 3, 3]
+    assert more.stats["choice_waits" if pipeline else "decode_steps"] > 0
+
+
+def test_large_class_gets_every_method_within_max_new_tokens(tiny):
+    """A 60-method class under a 1,024-token reply budget: split into parts,
+    generated side by side, merged -- every method described, in order."""
+    names = [f"handleEvent{i}" for i in range(60)]
+    inp = EnrichmentInput("class Big {}", "co.x.Big", "java", "LISTENER", names)
+    eng = LocalEngine(tiny, max_new_tokens=1024)
+    doc = json.loads(eng.generate([inp], None)[0])
+    assert [m["methodName"] for m in doc["methods"]] == names
+    assert all(m["description"] for m in doc["methods"])
+    assert eng.stats["split_classes"] == 1 and eng.stats["reply_parts"] > 1 and eng.stats["methods_dropped"] == 0
+    assert eng.reply_budget == 1024
+
+
+def test_class_type_correction_reaches_the_database(tmp_path):
+    """The model's correction is applied to source_classes.class_type
+    (CodeContextService.java:635-637) through the real pipeline."""
+    from conftest import make_app
+    from dmcp.utils import synth
+    repo = tmp_path / "shop"
+    synth.java_spring_repo(str(repo), 8)
+    be = LocalLLMBackend([LocalEngine(_Forcing({'"': 30.0, "D": 25.0, "]": 20.0}))])
+    app = make_app(tmp_path, backend=be)
+    r = app.indexer.analyze_project(str(repo))
+    assert r.success and r.stats["enriched"] == r.classes_analyzed
+    types = {c.class_type.value for c in app.repos.classes.find_by_project_id(r.project_id)}
+    assert types == {"DTO"}
+    g = app.cache.get_graph(r.project_id)
+    assert g.node_info("co.acme.shop.order.OrderService").class_type == "DTO"
+    app.db.close()
+
+
+def test_bpe_vocabulary_engine_on_cpu():
+    """The 128,256-id code tokenizer drives the same engine: forced skeleton,
+    choice masks and free strings over BPE pieces; replies parse."""
+    from dmcp.enrich.local import build_model
+    model, tok = build_model({"preset": "tiny-bpe", "seed": 3}, "cpu")
+    assert model.cfg.vocab_size == 128256 and tok.bos == 128000
+    eng = LocalEngine(model, tokenizer=tok)
+    out = eng.generate(_inputs(3), "A readme")
+    for r, inp in zip(out, _inputs(3)):
+        doc = json.loads(r)
+        assert [m["methodName"] for m in doc["methods"]] == inp.method_names
+    text = open(__file__).read()
+    assert len(text.encode()) / len(tok.encode(text)) > 3.0  # ~4 bytes per token on source code

@@ -85,7 +85,7 @@ def test_late_eof_of_a_replaced_worker_is_ignored(pool):
     class Ghost:  # a worker object no longer in the pool, at index 0
         index = 0
     cur = pool.workers[0]
-    pool.events.put((Ghost(), None))
+    pool._on_frame(Ghost(), None)
     res = ProcessLLMBackend(pool).enrich_batch(_inputs(4), None)
     assert all(r.success for r in res), [r.error_message for r in res if not r.success]
     assert pool.workers[0] is cur and cur.alive
@@ -130,7 +130,7 @@ def test_analyze_project_streams_every_class_through_the_pool(tmp_path, pool):
     assert got[0] > 0 and got[1] > 0
     # every method row got its description from the model's (grammar-forced) reply
     m = app.repos.methods.find_by_class_name("co.acme.shop.order.OrderService")
-    assert m and any(x.description for x in m)  # (tiny max_seq: fit_template may drop trailing methods)
+    assert m and all(x.description for x in m)  # every method: a reply that does not fit is split, not cut
     g = app.cache.get_graph(r.project_id)
     assert g.node_info("co.acme.shop.order.OrderService").description
     app.db.close()  # not app.close(): the module-scoped pool outlives this app
@@ -151,3 +151,138 @@ def test_bench_enrich_local_path_on_cpu_workers(tmp_path, pool):
     rec = bench._enrich_local(pool, args, DistContext(), str(tmp_path), 0)
     assert rec["classesEnriched"] == rec["classesAnalyzed"] == 17 and rec["classesPerSec"] > 0
     assert rec["decodeStepMs"] > 0 and rec["hostMsPerStep"] > 0 and rec["prefillBatches"] >= 1
+
+
+# ---------------------------------------------------------------- dealing
+# model-free "echo" workers: each step of step_s answers every class a worker
+# holds (a latency-bound continuous batch), so wall times measure the dealing
+
+def _echo_pool(n, step_s=0.05, steps=1, **kw):
+    return GpuWorkerPool(["cpu"] * n, {"preset": "echo", "step_s": step_s, "steps": steps, "max_batch": 512},
+                         start_timeout_s=120, env_extra={"OMP_NUM_THREADS": "1"}, **kw)
+
+
+def test_small_project_is_spread_over_every_gpu():
+    """257 classes on 8 workers: 32 +- 1 each (was: all 257 on worker 0,
+    whose in-flight capacity is 768)."""
+    pool = _echo_pool(8)
+    try:
+        assert pool.capacity == 768
+        res = ProcessLLMBackend(pool).enrich_batch(_inputs(257), "readme")
+        assert all(r.success for r in res) and len(res) == 257
+        counts = [pool.per_worker_items.get(i, 0) for i in range(8)]
+        assert sum(counts) == 257 and max(counts) - min(counts) <= 1 and min(counts) >= 32, counts
+        # a generator input without a length hint is still dealt (by capacity)
+        gen = (inp for inp in _inputs(20))
+        assert all(r.success for _, r in ProcessLLMBackend(pool).enrich_stream(gen, None))
+    finally:
+        pool.close()
+
+
+def test_concurrent_streams_share_the_pool(tmp_path):
+    """Two projects analysed at once split the workers (project affinity)
+    and overlap: both finish in < 1.3x the time of one alone."""
+    import threading
+    repos = []
+    for k in range(2):
+        r = tmp_path / f"svc{k}"
+        synth.java_spring_repo(str(r), 40, base_package=f"co.acme.s{k}", seed=k + 5)
+        repos.append(str(r))
+    pool = _echo_pool(8, step_s=0.1, steps=12)  # every class takes 12 steps of a continuous batch
+    try:
+        be = ProcessLLMBackend(pool)
+        app = make_app(tmp_path, backend=be)
+        app.indexer.analyze_project(repos[0])  # warm: sqlite, native scanner, the children's first session
+        t0 = time.time()
+        r = app.indexer.analyze_project(repos[0])
+        one = time.time() - t0
+        assert r.stats["enriched"] == r.classes_analyzed
+        before = dict(pool.per_worker_items)
+        out = {}
+
+        def run(k):
+            out[k] = app.indexer.analyze_project(repos[k])
+        t0 = time.time()
+        ts = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(120)
+        both = time.time() - t0
+        assert all(out[k].success and out[k].stats["enrichFailed"] == 0 for k in range(2))
+        assert both < 1.3 * one, (both, one)
+        used = [i for i in range(8) if pool.per_worker_items.get(i, 0) > before.get(i, 0)]
+        assert len(used) == 8  # every worker served one of the two projects
+        assert not pool.streams and all(w.owner is None for w in pool.workers)
+        app.db.close()
+    finally:
+        pool.close()
+
+
+def test_idle_worker_is_not_killed_as_hung():
+    """A worker idle for longer than hang_timeout_s is not killed when the
+    next stream's first reply takes a while (its clock starts when it gets
+    work, not at its last frame)."""
+    pool = _echo_pool(1, step_s=1.2, hang_timeout_s=2.0)
+    try:
+        be = ProcessLLMBackend(pool)
+        assert all(r.success for r in be.enrich_batch(_inputs(3), None))
+        time.sleep(2.5)
+        res = be.enrich_batch(_inputs(3), None)
+        assert all(r.success for r in res), [r.error_message for r in res]
+        assert pool.deaths == 0 and pool.workers[0].alive
+    finally:
+        pool.close()
+
+
+def test_bulk_with_local_backend_starts_one_pool(tmp_path, monkeypatch):
+    """analyze-batch --workers 4 with the local backend: the repositories run
+    on threads of one App and share ONE worker pool."""
+    from dmcp.config import Config
+    from dmcp.enrich import workers as W
+    from dmcp.parallel.bulk import BulkItem, bulk_analyze
+    made = []
+    real = W.GpuWorkerPool.__init__
+
+    def counting(self, *a, **kw):
+        made.append(1)
+        real(self, *a, **kw)
+    monkeypatch.setattr(W.GpuWorkerPool, "__init__", counting)
+    items = []
+    for k in range(4):
+        r = tmp_path / f"r{k}"
+        synth.java_spring_repo(str(r), 8, base_package=f"co.b.r{k}", seed=k)
+        items.append(BulkItem(str(r)))
+    cfg = Config(db_path=str(tmp_path / "b.db"), git_clone_base_path=str(tmp_path / "clones"),
+                 enrich_backend="local", local_llm_devices="cpu,cpu", local_llm_preset="echo",
+                 recover_stuck_on_start=False)
+    res = bulk_analyze(cfg, items, workers=4)
+    assert all(r.success for r in res), [r.message for r in res]
+    assert len(made) == 1
+
+
+def test_serve_mcp_never_spawns_gpu_workers(tmp_path):
+    """The read-only MCP server (application-mcp.yml) with ENRICH_BACKEND=local
+    serves its tools without starting the enrichment workers."""
+    import subprocess
+    import sys
+    import psutil
+    env = dict(os.environ, ENRICH_BACKEND="local", LOCAL_LLM_DEVICES="cpu", LOCAL_LLM_PRESET="echo",
+               DMCP_DB_PATH=str(tmp_path / "m.db"))
+    proc = subprocess.Popen([sys.executable, "-m", "dmcp", "serve-mcp"], stdin=subprocess.PIPE,
+                            stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, env=env,
+                            cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    try:
+        def rpc(i, method, params=None):
+            proc.stdin.write((json.dumps({"jsonrpc": "2.0", "id": i, "method": method,
+                                          "params": params or {}}) + "\n").encode())
+            proc.stdin.flush()
+            return json.loads(proc.stdout.readline())
+        assert rpc(1, "initialize", {"protocolVersion": "2024-11-05", "capabilities": {},
+                                     "clientInfo": {"name": "t", "version": "1"}})["result"]
+        r = rpc(2, "tools/call", {"name": "list_projects", "arguments": {}})
+        assert not r["result"]["isError"]
+        assert psutil.Process(proc.pid).children(recursive=True) == []
+    finally:
+        proc.stdin.close()
+        proc.wait(30)

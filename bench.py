@@ -16,9 +16,12 @@ the headline, each rank runs a real ``analyze_project`` of a
 ``--enrich-local-classes``-class repository with the optional MI355X
 enrichment backend in the service configuration -- one worker process per
 GPU (dmcp/enrich/workers.py, spawned before this process touches HIP),
-every pending class streamed to it, fp8 KV cache, 256 concurrent sequences
+every pending class streamed to it, fp8 KV cache, 512 concurrent sequences
 -- and reports classes enriched per second through the whole pipeline plus
-the engine's per-step device / host split.
+the engine's per-step device / host split.  It runs once per preset of
+``--enrich-local-presets``: ``dmcp-coder-1b`` (byte vocabulary) ->
+``extra.enrichLocal``; ``llama3.2-1b-code`` (Llama-3.2-1B shapes, 128,256-id
+code BPE: a real 1B code model's operating point) -> ``extra.enrichLocalLlama``.
 
 Multi-GPU contract: launched by ``torch.distributed.run`` with one rank per
 GPU; every rank indexes its own repository (weak scaling), the timed region
@@ -59,27 +62,36 @@ def parse_args(argv=None):
                     help="classes of the end-to-end local-model enrichment run (extra.enrichLocal; 0 = skip)")
     ap.add_argument("--enrich-local-kv", default="fp8", choices=["bf16", "fp8"])
     ap.add_argument("--enrich-local-batch", type=int, default=512)
+    ap.add_argument("--enrich-local-presets", default="dmcp-coder-1b,llama3.2-1b-code")
     return ap.parse_args(argv)
 
 
-def _spawn_enrich_pool(args):
-    """The enrichment worker for this rank's GPU, spawned BEFORE this process
-    initialises HIP (the child stays idle -- no torch import -- until init)."""
+EXTRA_KEYS = {"dmcp-coder-1b": "enrichLocal", "llama3.2-1b-code": "enrichLocalLlama"}
+
+
+def _spawn_enrich_pools(args):
+    """One enrichment worker per preset for this rank's GPU, spawned BEFORE
+    this process initialises HIP (each child stays idle -- no torch import --
+    until its init; they run one after the other, each closed after its run)."""
     if args.enrich_local_classes <= 0:
-        return None
+        return {}
     try:
         import torch
         if torch.cuda.device_count() <= 0:  # counts devices without creating a HIP context
-            return None
+            return {}
         from dmcp.enrich.workers import GpuWorkerPool
         local = int(os.environ.get("LOCAL_RANK", "0"))
         mb = args.enrich_local_batch
-        model = {"preset": "dmcp-coder-1b", "kv_dtype": args.enrich_local_kv, "max_batch": mb,
-                 "max_rows": max(256, mb * 3 // 2), "seed": 0}
-        return GpuWorkerPool([f"cuda:{local}"], model, init=False, start_timeout_s=600)
+        pools = {}
+        for name in [p.strip() for p in args.enrich_local_presets.split(",") if p.strip()]:
+            model = {"preset": name, "kv_dtype": args.enrich_local_kv, "max_batch": mb,
+                     "max_rows": max(256, mb * 3 // 2), "seed": 0}
+            pools[name] = GpuWorkerPool([f"cuda:{local}"], model, engine={"max_new_tokens": 4096}, init=False,
+                                        start_timeout_s=600)
+        return pools
     except Exception as e:  # the headline does not depend on it
         logging.getLogger("bench").warning("enrichment worker not started: %s", e)
-        return None
+        return {}
 
 
 def _enrich_local(pool, args, ctx, work, rank):
@@ -136,6 +148,10 @@ def _enrich_local(pool, args, ctx, work, rank):
         st = be.stats()
         steps = max(1.0, st.get("decode_steps", 0))
         return {"classesPerSec": round(tot[0] / mx, 2), "classesEnriched": int(tot[0]),
+                "promptTokensPerClass": round(st.get("prompt_tokens", 0) / max(1, st.get("prefills", 1)), 1),
+                "generatedTokensPerClass": round(st.get("generated_tokens", 0) / max(1, tot[0]), 1),
+                "typeCorrections": int(st.get("type_corrections", 0)), "splitClasses": int(st.get("split_classes", 0)),
+                "methodsDropped": int(st.get("methods_dropped", 0)),
                 "classesAnalyzed": int(tot[1]), "elapsedS": round(mx, 3), "enrichFailed": r.stats.get("enrichFailed"),
                 "phase2Ms": round(r.stats.get("analyze.phase2", 0.0), 1),
                 "decodeStepMs": round(1e3 * st.get("decode_s", 0) / steps, 3),
@@ -144,7 +160,7 @@ def _enrich_local(pool, args, ctx, work, rank):
                 "rowsPerStep": round(st.get("decode_rows", 0) / steps, 1),
                 "prefillMsPerClass": round(1e3 * st.get("prefill_s", 0) / max(1, st.get("prefills", 0)), 3),
                 "prefillBatches": int(st.get("prefill_batches", 0)), "workerInitS": round(init_s, 1),
-                "config": {"model": "dmcp-coder-1b (random init)", "kv_dtype": args.enrich_local_kv,
+                "config": {"model": f"{pool.model['preset']} (random init)", "kv_dtype": args.enrich_local_kv,
                            "batch": args.enrich_local_batch, "workers_per_rank": len(pool.workers),
                            "path": "analyze_project -> streamed Phase 2 -> GPU worker process"}}
     finally:
@@ -153,7 +169,7 @@ def _enrich_local(pool, args, ctx, work, rank):
 
 def main(argv=None) -> int:
     args = parse_args(argv)
-    pool = _spawn_enrich_pool(args) if args.enrich == "none" else None  # before anything touches HIP
+    pools = _spawn_enrich_pools(args) if args.enrich == "none" else {}  # before anything touches HIP
     from dmcp.parallel.dist import init_from_env
     ctx = init_from_env()
     rank, world = ctx.rank, ctx.world
@@ -220,13 +236,18 @@ def main(argv=None) -> int:
             extra["stackTrace20Ms"] = {"p50": round(st_lat[len(st_lat) // 2], 3),
                                        "p99": round(st_lat[max(0, int(len(st_lat) * 0.99) - 1)], 3)}
         # agreed by every rank: a rank without a worker skips the collective path for all
+        names = [p.strip() for p in args.enrich_local_presets.split(",") if p.strip()]
         if args.enrich == "none" and args.enrich_local_classes > 0 and \
-                ctx.sum(1.0 if pool is not None else 0.0)[0] == world:
-            try:
-                extra["enrichLocal"] = _enrich_local(pool, args, ctx, work, rank)
-            except Exception as e:
-                logging.getLogger("bench").exception("enrichLocal failed")
-                extra["enrichLocal"] = {"error": repr(e)[:300]}
+                ctx.sum(1.0 if len(pools) == len(names) else 0.0)[0] == world:
+            for name in names:
+                key = EXTRA_KEYS.get(name, "enrichLocal_" + name)
+                try:
+                    extra[key] = _enrich_local(pools[name], args, ctx, work, rank)
+                except Exception as e:
+                    logging.getLogger("bench").exception("%s failed", key)
+                    extra[key] = {"error": repr(e)[:300]}
+                finally:
+                    pools.pop(name).close()  # its KV slab goes before the next preset's
         value = total_classes / elapsed if elapsed > 0 else 0.0
         ms_per_step = elapsed / max(1, args.steps) * 1e3
         if rank == 0:
@@ -244,8 +265,8 @@ def main(argv=None) -> int:
             print(json.dumps(line), flush=True)
     finally:
         app.close()
-        if pool is not None:
-            pool.close()
+        for p in pools.values():
+            p.close()
         if args.workdir is None:
             shutil.rmtree(work, ignore_errors=True)
         ctx.shutdown()

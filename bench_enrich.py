@@ -24,7 +24,7 @@ sys.path.insert(0, ROOT)
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--preset", default="dmcp-coder-1b")
-    ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"],
+    ap.add_argument("--kv-dtype", default="fp8", choices=["bf16", "fp8"],
                     help="KV cache storage (fp8 = e4m3, half the attention bytes)")
     ap.add_argument("--classes", type=int, default=1024, help="classes per rank")
     ap.add_argument("--batch", type=int, default=512, help="concurrent sequences (KV slots)")
@@ -43,6 +43,7 @@ def main(argv=None) -> int:
     ap.add_argument("--admit-min", type=int, default=0,
                     help="free KV slots before a running batch admits new classes (0 = engine default, batch/16)")
     ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--max-new-tokens", type=int, default=4096, help="reply budget (LOCAL_LLM_MAX_NEW_TOKENS)")
     args = ap.parse_args(argv)
 
     import torch
@@ -62,9 +63,13 @@ def main(argv=None) -> int:
     cfg = preset(args.preset, max_batch=args.batch, max_seq=args.max_seq, kv_dtype=args.kv_dtype,
                  max_rows=args.max_rows or max(256, args.batch + args.batch // 2))
     model = LocalLM(cfg, device=f"cuda:{local}", seed=rank)
+    tok = None
+    if cfg.tokenizer:
+        from dmcp.enrich.tokenizer import load_asset_tokenizer
+        tok = load_asset_tokenizer(cfg.tokenizer)
     eng = LocalEngine(model, use_graphs=not args.no_graphs, jump_forward=not args.no_jump,
                       shared_prefix=not args.no_shared_prefix, pipeline=not args.no_pipeline,
-                      admit_min=args.admit_min or None)
+                      admit_min=args.admit_min or None, tokenizer=tok, max_new_tokens=args.max_new_tokens)
     para = ("The shop platform sells products to retail customers. Orders move from CART to PAID to "
             "SHIPPED; payments are captured through the payment gateway and refunds are issued by the "
             "back office. Inventory is reserved when an order is paid and released on cancellation.\n\n")
@@ -127,7 +132,10 @@ def main(argv=None) -> int:
             "decode_s": round(st["decode_s"], 3), "host_ms_per_step": round(1e3 * st["host_s"] / max(1, st["decode_steps"]), 3),
             "admit_min": eng.admit_min,
             "decode_steps": st["decode_steps"], "rows_per_step": round(st["decode_rows"] / max(1, st["decode_steps"]), 1),
-            "elapsed_s": round(elapsed, 3), "classes": int(ok_all)}),
+            "elapsed_s": round(elapsed, 3), "classes": int(ok_all),
+            "prompt_tokens_per_class": round(st["prompt_tokens"] / max(1, st["prefills"]), 1),
+            "generated_tokens_per_class": round(st["generated_tokens"] / max(1, ok_all), 1),
+            "choice_waits": st.get("choice_waits", 0), "type_corrections": st.get("type_corrections", 0)}),
             flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -89,8 +89,10 @@ CHOICES: Dict[int, Tuple[bytes, ...]] = {
 
 @dataclass
 class Segment:
-    """One piece of a reply: ``forced`` bytes, a free JSON string of
-    ``min_len..max_len`` sampled tokens closed by the lone quote token, or a
+    """One piece of a reply: ``forced`` bytes, a free JSON string closed by
+    the lone quote token -- at least ``min_len`` sampled tokens, at most
+    ``max_len`` bytes (a length in text, whatever the tokenizer: a 4-byte
+    BPE piece fills it 4x faster than a byte token) -- or a
     ``choice`` among :data:`CHOICES` alternatives (``then[k]``: the segments
     that follow alternative k)."""
     forced: Optional[bytes] = None
@@ -227,7 +229,8 @@ class _Seq:
     slot: int = -1
     pos: int = 0                       # tokens already in the KV cache
     seg: int = 0
-    free_len: int = 0
+    free_len: int = 0                  # tokens of the current free string
+    free_bytes: int = 0                # ... and its bytes
     forced_off: int = 0
     choice_pref: bytes = b""           # bytes chosen so far in the current choice segment
     next_token: int = -1               # token to feed at the next decode step
@@ -413,7 +416,7 @@ class LocalEngine:
             if seg.choice >= 0:
                 s.choice_pref = b""
                 return self._choice_rows[(seg.choice, b"")]
-            s.free_len = 0
+            s.free_len = s.free_bytes = 0
             return self.MASK_QUOTE if seg.min_len == 0 else self.MASK_NO_QUOTE
         s.done = True
         return None
@@ -462,7 +465,8 @@ class LocalEngine:
             s.free_len = 0
             return self._enter(s)
         s.free_len += 1
-        if s.free_len >= seg.max_len:
+        s.free_bytes += len(self._tb[tok])
+        if s.free_bytes >= seg.max_len:
             s.next_token = self._quote
             return None
         return self.MASK_QUOTE if s.free_len >= seg.min_len else self.MASK_NO_QUOTE

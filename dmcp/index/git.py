@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import logging
 import os
+import shlex
 import shutil
 import subprocess
 import time
@@ -46,7 +47,8 @@ class GitClient:
         env = dict(os.environ)
         env["GIT_TERMINAL_PROMPT"] = "0"
         if self.ssh_key_path:
-            env["GIT_SSH_COMMAND"] = (f"ssh -i {self.ssh_key_path} -o IdentitiesOnly=yes "
+            # git runs GIT_SSH_COMMAND through a shell: the key path is quoted
+            env["GIT_SSH_COMMAND"] = (f"ssh -i {shlex.quote(self.ssh_key_path)} -o IdentitiesOnly=yes "
                                       "-o StrictHostKeyChecking=accept-new")
         return env
 

@@ -11,6 +11,13 @@ runs, and the operation releases it at the end.  A second process asking for
 the same project gets ``PROJECT_BUSY``; a holder that died stops
 heartbeating, its lease runs out after ``ttl`` seconds, and only then may
 another process recover the project's ANALYZING / SYNCING status.
+
+A holder whose heartbeat cannot renew (a long write transaction holding the
+SQLite write lock, a database outage) knows when its last renewal runs out
+(``valid_until``): past it :meth:`ProjectLease.check` fails with
+``LEASE_LOST`` even though no other owner was seen yet, so the operation
+stops writing instead of racing whoever takes the project over -- and it
+never marks the project ERROR (that status is no longer its to write).
 """
 from __future__ import annotations
 
@@ -45,6 +52,7 @@ class ProjectLease:
         self.owner = new_owner_id()
         self.clock = clock
         self.lost = False
+        self.valid_until = 0.0  # the lease is ours until then (last successful acquire / renewal)
         self.took_over_expired = False
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
@@ -55,6 +63,7 @@ class ProjectLease:
         prev_owner, prev_until = self.projects.lease_of(self.project_id)
         if not self.projects.try_acquire_lease(self.project_id, self.owner, self.ttl_s, now):
             raise DomainError(f"Project {self.name} is already being processed", "PROJECT_BUSY")
+        self.valid_until = now + self.ttl_s
         # a previous holder that never released: crashed (its lease ran out)
         self.took_over_expired = prev_owner is not None and prev_owner != self.owner
         if self.took_over_expired:
@@ -66,19 +75,39 @@ class ProjectLease:
 
     def _heartbeat(self) -> None:
         period = self.ttl_s / 3.0
-        while not self._stop.wait(period):
+        wait = period
+        while not self._stop.wait(wait):
             try:
-                if not self.projects.renew_lease(self.project_id, self.owner, self.clock() + self.ttl_s):
+                until = self.clock() + self.ttl_s
+                if not self.projects.renew_lease(self.project_id, self.owner, until):
                     self.lost = True
                     LOG.error("Project %s: lease lost to another process", self.name)
                     return
-            except Exception as e:  # a busy database: try again next period
+                self.valid_until = until
+                wait = period
+            except Exception as e:  # a busy database: retry soon -- the lease runs out at valid_until
                 LOG.warning("Project %s: lease heartbeat failed: %s", self.name, e)
+                wait = min(period, 0.5)
+
+    def expired(self) -> bool:
+        """True once the last renewal ran out (another process may own it now)."""
+        return self.held and self.clock() > self.valid_until
 
     def check(self) -> None:
-        """Raises ``LEASE_LOST`` when the heartbeat found the lease taken."""
+        """Raises ``LEASE_LOST`` when the heartbeat found the lease taken, or
+        could not renew it before it ran out."""
         if self.lost:
             raise DomainError(f"Project {self.name}: lease lost to another process", "LEASE_LOST")
+        if self.expired():
+            raise DomainError(f"Project {self.name}: lease expired (not renewed since "
+                              f"{self.valid_until - self.ttl_s:.0f})", "LEASE_LOST")
+
+    def is_lost(self, error: Optional[BaseException] = None) -> bool:
+        """Whether an operation that failed with ``error`` no longer owns the
+        project (its status then belongs to the new owner)."""
+        if isinstance(error, DomainError) and error.error_code == "LEASE_LOST":
+            return True
+        return self.lost or self.expired()
 
     def release(self) -> None:
         if not self.held:

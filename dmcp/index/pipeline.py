@@ -229,20 +229,24 @@ class Indexer:
                 LOG.info("Graph built: %d nodes, %d entry points", graph.node_count(), graph.entry_point_count())
                 order = graph.analysis_order()
                 with span("analyze.phase1", stats):
-                    # without enrichment the swap stays open for the project row
+                    # the swap stays open: it commits only under a live lease
+                    # (without enrichment the project row joins it below)
                     p1 = self._phase1_static(project, parsed, graph, order, clone.commit_hash, writer,
-                                             close=self.backend.enabled, now=now)
+                                             close=False, now=now)
                 classes, methods_by_ident, writer = p1
                 enriched = failed = recovered = 0
                 if self.backend.enabled:
                     with span("analyze.phase1_commit", stats):
+                        lease.check()  # never swap rows in over an operation that took the project over
+                        writer.close()
                         writer.wait()  # enrichment updates the rows just written
                     with span("analyze.phase2", stats):
                         enriched, failed = self._enrich_identifiers(order, parsed, graph, clone,
-                                                                    readme, methods_by_ident)
+                                                                    readme, methods_by_ident, lease=lease)
                     if fix_missed:
                         with span("analyze.phase3", stats):
-                            recovered = self._recover_unenriched(project, parsed, graph, clone, readme)
+                            recovered = self._recover_unenriched(project, parsed, graph, clone, readme,
+                                                                 lease=lease)
                 lease.check()  # never publish over an operation that took the project over
                 with span("analyze.persist_graph", stats):
                     project.base_package = common_package_prefix({package_name_of(i) for i in parsed.units})
@@ -275,7 +279,8 @@ class Indexer:
                     writer.finish()  # the row swap ends (commit or rollback) before the status write
                 except Exception:
                     pass
-            self._mark_error(project)
+            if not lease.is_lost(e):  # a lost lease: the project's status is the new owner's
+                self._mark_error(project)
             raise DomainError(f"Analysis failed: {e}", "ANALYSIS_FAILED", e) from e
         finally:
             with span("analyze.cleanup", stats):
@@ -532,7 +537,8 @@ class Indexer:
 
     def _stream_enrich(self, idents: Sequence[str], parsed: ParsedProject, graph: ProjectGraph,
                        tree: SourceTree, readme: Optional[str], class_types: Optional[Dict[str, str]],
-                       methods_by_ident: Optional[Dict[str, List[Tuple[str, str]]]], phase: str) -> Tuple[int, int]:
+                       methods_by_ident: Optional[Dict[str, List[Tuple[str, str]]]], phase: str,
+                       lease: Optional[ProjectLease] = None) -> Tuple[int, int]:
         """Every pending class goes to the backend as ONE stream (sources read
         lazily, as the backend asks for more); each result is applied the
         moment it arrives.  A local GPU engine keeps its continuous batch full
@@ -554,6 +560,8 @@ class Indexer:
         # lazy, but sized: a multi-GPU backend deals ceil(pending / GPUs) per GPU
         inputs = SizedIter(gen(), len(pending))
         for n, (_, result) in enumerate(self.backend.enrich_stream(inputs, readme), 1):
+            if lease is not None and n % 32 == 1:
+                lease.check()  # enrichment writes go to rows another owner may be replacing
             if not result.success:
                 LOG.warning("%s: enrichment failed for %s: %s", phase, result.full_class_name, result.error_message)
                 failed += 1
@@ -567,12 +575,12 @@ class Indexer:
 
     def _enrich_identifiers(self, idents: Sequence[str], parsed: ParsedProject, graph: ProjectGraph,
                             tree: SourceTree, readme: Optional[str],
-                            methods_by_ident: Optional[Dict[str, List[Tuple[str, str]]]] = None
-                            ) -> Tuple[int, int]:
+                            methods_by_ident: Optional[Dict[str, List[Tuple[str, str]]]] = None,
+                            lease: Optional[ProjectLease] = None) -> Tuple[int, int]:
         idents = list(idents)
         if self.stream_enrichment:
             enriched, failed = self._stream_enrich(idents, parsed, graph, tree, readme, None, methods_by_ident,
-                                                   "Phase 2")
+                                                   "Phase 2", lease)
         else:  # the reference's barriers: batches of batch_size classes (CodeContextService.java:297-359)
             enriched = failed = 0
             nbatches = (len(idents) + self.batch_size - 1) // self.batch_size
@@ -581,6 +589,8 @@ class Indexer:
                 LOG.info("Enriching batch %d/%d (%d classes)", b // self.batch_size + 1, nbatches, len(batch))
                 inputs, read_failed = self._inputs_for(batch, parsed, tree)
                 failed += read_failed
+                if lease is not None:
+                    lease.check()
                 for result in self.backend.enrich_batch(inputs, readme):
                     if not result.success:
                         LOG.warning("Enrichment failed for %s: %s", result.full_class_name, result.error_message)
@@ -593,7 +603,7 @@ class Indexer:
         return enriched, failed
 
     def _recover_unenriched(self, project: Project, parsed: ParsedProject, graph: ProjectGraph,
-                            tree: SourceTree, readme: Optional[str]) -> int:
+                            tree: SourceTree, readme: Optional[str], lease: Optional[ProjectLease] = None) -> int:
         unenriched = self.repos.classes.find_unenriched_by_project_id(project.id)
         if not unenriched:
             LOG.info("Phase 3: No unenriched classes found, skipping recovery")
@@ -602,7 +612,7 @@ class Indexer:
         types = {sc.full_class_name: sc.class_type.value for sc in unenriched}
         idents = [sc.full_class_name for sc in unenriched]
         if self.stream_enrichment:
-            recovered, _ = self._stream_enrich(idents, parsed, graph, tree, readme, types, None, "Phase 3")
+            recovered, _ = self._stream_enrich(idents, parsed, graph, tree, readme, types, None, "Phase 3", lease)
         else:
             recovered = 0
             for b in range(0, len(idents), self.batch_size):
@@ -879,7 +889,7 @@ class Indexer:
                 if self.backend.enabled and changed:
                     self._attach_metadata(graph, parsed, all_classes, {**mb_un, **mb})
                     enriched, failed = self._enrich_identifiers(changed, parsed, graph, clone, readme,
-                                                                methods_by_ident)
+                                                                methods_by_ident, lease=lease)
                 # final metadata from the DB (enrichment included)
                 final_classes = {sc.full_class_name: sc for sc in self.repos.classes.find_by_project_id(project.id)}
                 mb_all = self.repos.methods.find_by_class_ids([sc.id for sc in final_classes.values()])
@@ -897,7 +907,8 @@ class Indexer:
                               len(unchanged), enriched, failed, None)
         except Exception as e:
             LOG.error("Sync failed for %s: %s", project.name, e, exc_info=True)
-            self._mark_error(project)
+            if not lease.is_lost(e):  # a lost lease: the project's status is the new owner's
+                self._mark_error(project)
             return SyncResult.failure(project.name, str(e))
         finally:
             if clone is not None:
@@ -967,7 +978,7 @@ class Indexer:
                 parsed = self._scan(parser_for(clone.detect_language(), self.parser_threads), clone,
                                     project.repository_url)
                 readme = clone.readme(self.max_readme_length)
-                recovered = self._recover_unenriched(project, parsed, graph, clone, readme)
+                recovered = self._recover_unenriched(project, parsed, graph, clone, readme, lease=lease)
                 project.update_graph_data(graph.to_json())
                 lease.check()
                 self.repos.projects.update(project)

@@ -33,6 +33,19 @@ for s in $STEPS; do
         bench) run bench 900 python bench.py --steps 20 --warmup 5 ;;
         enrich_fp8) run enrich_fp8 900 python bench_enrich.py --kv-dtype fp8 ;;
         enrich_bf16) run enrich_bf16 900 python bench_enrich.py --kv-dtype bf16 ;;
+        enrich_llama) run enrich_llama 900 python bench_enrich.py --preset llama3.2-1b-code --kv-dtype fp8 ;;
+        enrich_llama257) run enrich_llama257 600 python bench_enrich.py --preset llama3.2-1b-code --classes 257 ;;
+        prof_llama)
+            ( cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$ROOT/$OUT/prof_llama" -o enrich -- python3 "$ROOT/bench_enrich.py" --preset llama3.2-1b-code \
+                --classes 512 --warmup 4 > "$ROOT/$OUT/prof_llama.log" 2>&1 )
+            rc=$?
+            echo "=== prof_llama rc=$rc"
+            find "$OUT/prof_llama" -type f ! -name '*kernel_stats*' -delete 2>/dev/null
+            python3 scripts/kstats.py $(find "$OUT/prof_llama" -name '*kernel_stats.csv' | head -1) \
+                > "$OUT/kstats_llama.txt" 2>&1
+            head -30 "$OUT/kstats_llama.txt"
+            [ $rc -eq 0 ] || exit $rc ;;
         prefill) run prefill 300 python scripts/bench_prefill.py --seqs 12 ;;
         step)
             run step320 300 python scripts/bench_step.py --batch 256 --extra 64 --kv-dtype fp8 --iters 100

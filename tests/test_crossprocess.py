@@ -211,3 +211,77 @@ def test_lease_lives_in_its_own_table(tmp_path):
         c.execute("DELETE FROM projects WHERE id = ?", (p.id,))
     assert app.db.query_one("SELECT COUNT(*) AS n FROM project_leases")["n"] == 0
     app.close()
+
+
+def _hold_write_lock(db_path, seconds, then=None):
+    """Another connection holds SQLite's write lock for ``seconds`` (a row
+    swap longer than the lease TTL), optionally running ``then`` in it."""
+    import sqlite3
+    import threading
+    ready = threading.Event()
+
+    def run():
+        c = sqlite3.connect(db_path, isolation_level=None, timeout=30)
+        c.execute("BEGIN IMMEDIATE")
+        ready.set()
+        time.sleep(seconds)
+        if then is not None:
+            then(c)
+        c.execute("COMMIT")
+        c.close()
+    t = threading.Thread(target=run, daemon=True)
+    t.start()
+    ready.wait(10)
+    return t
+
+
+def test_lease_not_renewed_past_its_ttl_fails_the_check(tmp_path):
+    """The heartbeat blocked behind a write transaction longer than the TTL:
+    the holder can no longer prove it owns the project, so check() fails
+    (LEASE_LOST) instead of writing on; once renewals resume it holds again."""
+    app = make_app(tmp_path, project_lease_seconds=1.0)
+    repo = str(tmp_path / "shop")
+    synth.java_spring_repo(repo, n_classes=4)
+    assert app.indexer.analyze_project(repo).success
+    p = app.repos.projects.find_by_repository_url(os.path.abspath(repo), with_graph=False)
+    lease = ProjectLease(app.repos.projects, p.id, ttl_s=1.0).acquire()
+    t = _hold_write_lock(app.config.db_path, 2.0)
+    time.sleep(1.5)
+    assert lease.expired() and lease.is_lost()
+    with pytest.raises(DomainError) as e:
+        lease.check()
+    assert e.value.error_code == "LEASE_LOST"
+    t.join(10)
+    time.sleep(1.0)  # the blocked renewal went through after the lock
+    lease.check()
+    lease.release()
+    app.close()
+
+
+def test_analysis_that_loses_its_lease_leaves_the_new_owners_status(tmp_path):
+    """A row swap held open past the TTL lets another process take the
+    project over: the analysis stops at its next lease check and does NOT
+    mark the project ERROR -- the status belongs to the new owner."""
+    from dmcp.enrich.backend import FakeBackend
+    repo = str(tmp_path / "shop")
+    synth.java_spring_repo(repo, n_classes=40)
+    holder = {}
+
+    def responder(inp):
+        if not holder:  # first class: another process's long transaction, then its takeover
+            def takeover(c):
+                pid = c.execute("SELECT id FROM projects").fetchone()[0]
+                c.execute("UPDATE project_leases SET lease_owner = 'host:2:other', lease_until = ? "
+                          "WHERE project_id = ?", (time.time() + 60, pid))
+                c.execute("UPDATE projects SET status = 'SYNCING' WHERE id = ?", (pid,))
+            holder["t"] = _hold_write_lock(app.config.db_path, 1.6, takeover)
+            holder["t"].join(10)
+        return '{"description": "d", "classTypeCorrection": null, "methods": []}'
+    app = make_app(tmp_path, backend=FakeBackend(max_concurrent=1, responder=responder), project_lease_seconds=1.0)
+    with pytest.raises(DomainError) as e:
+        app.indexer.analyze_project(repo)
+    assert "LEASE_LOST" in str(e.value.message) or "lease" in str(e.value.message).lower()
+    p = app.repos.projects.find_by_repository_url(os.path.abspath(repo), with_graph=False)
+    assert p.status == ProjectStatus.SYNCING  # not ERROR: the other owner's
+    assert app.repos.projects.lease_of(p.id)[0] == "host:2:other"
+    app.close()

@@ -166,3 +166,13 @@ def test_synthetic_generators(tmp_path):
     assert (tmp_path / "g" / "go.mod").exists()
     frames = synth.stack_trace_for(fq, 20)
     assert len(frames) == 20 and all({"className", "methodName", "lineNumber"} <= set(f) for f in frames)
+
+
+def test_ssh_key_path_with_spaces_is_quoted(tmp_path):
+    """GIT_SSH_COMMAND is run by a shell: a key path with spaces stays one argument."""
+    import shlex
+    from dmcp.index.git import GitClient
+    key = str(tmp_path / "my keys" / "id rsa")
+    cmd = GitClient(str(tmp_path), ssh_key_path=key)._env()["GIT_SSH_COMMAND"]
+    argv = shlex.split(cmd)
+    assert argv[:3] == ["ssh", "-i", key]

@@ -83,10 +83,18 @@ class GraphCache:
         if self._projects is None:
             return 0
         loaded = 0
+        # versions read BEFORE the graphs: a graph written in between is then
+        # newer than its recorded version and refresh() reloads it (the other
+        # order would record a newer version next to an older graph for ever)
+        try:
+            versions = self._projects.graph_versions()
+        except Exception:
+            versions = {}
         for project in self._projects.find_all_with_graph():
             try:
                 graph = ProjectGraph.from_json(project.graph_data)
-                self.put(project.id, project.name, graph)
+                v = versions.get(project.id)
+                self.put(project.id, project.name, graph, v[1] if v is not None else -1)
                 loaded += 1
             except Exception as e:  # corrupt graph: log and skip (GraphService.java:69-72)
                 LOG.warning("Failed to load graph for project %s: %s", project.id, e)
@@ -109,7 +117,8 @@ class GraphCache:
 
     def put(self, project_id: str, project_name: str, graph: ProjectGraph, version: Optional[int] = None) -> None:
         """``version``: the row's ``graph_version`` this graph corresponds to
-        (read from the database when omitted -- call after the commit)."""
+        (read from the database when omitted -- call after the commit, by the
+        lease holder, the project's only writer)."""
         graph.freeze()
         if version is None and self._projects is not None:
             try:

@@ -252,6 +252,10 @@ class Indexer:
                     project.base_package = common_package_prefix({package_name_of(i) for i in parsed.units})
                     project.update_graph_data(graph.to_json())
                     project.analysis_completed(clone.commit_hash)
+                    # the version this write will give the row (read under the
+                    # lease, before the write: the cache never pairs a newer
+                    # version with this graph)
+                    v0 = self.repos.projects.graph_version(project.id)
                     # the project row joins the row swap's transaction when the
                     # swap is still open (no enrichment), else it follows it
                     in_swap = writer.put_project_update(project)
@@ -263,7 +267,7 @@ class Indexer:
                         stats[f"analyze.writer_{k[:-3]}"] = v
                     if not in_swap:
                         self.repos.projects.update(project)
-                    self.cache.put(project.id, project.name, graph)
+                    self.cache.put(project.id, project.name, graph, None if v0 is None else v0 + 1)
                 endpoints = self.repos.methods.count_endpoints_by_project_id(project.id)
             METRICS.inc("classes_indexed", classes)
             LOG.info("Analysis completed. Classes: %d, Endpoints: %d, Enriched: %d, Enrich failed: %d, "

@@ -225,6 +225,7 @@ class LocalLM:
         # fp8: OCP e4m3fn bytes in uint8 tensors, written by the RoPE/KV-append
         # kernels and widened to bf16 inside every attention kernel
         self.kv_dtype = torch.uint8 if c.kv_dtype == "fp8" else self.dtype
+        self._check_kv_fits(kv_shape)
         self.k_cache = torch.zeros(kv_shape, dtype=self.kv_dtype, device=self.device)
         self.v_cache = torch.zeros(kv_shape, dtype=self.kv_dtype, device=self.device)
         self.cos_sin = ops.rope_tables(c.max_seq, c.head_dim, c.rope_theta, device=self.device).contiguous()
@@ -258,6 +259,23 @@ class LocalLM:
         self.use_wgemm = self.device.type == "cuda" and wgemm_shapes_ok(c)
         self.wgemm_ws = (ops.wgemm_workspace(min(self.max_rows, ops.WGEMM_MAX_ROWS), max(c.qkv_dim, c.hidden),
                                              self.device) if self.use_wgemm else None)
+
+    KV_HEADROOM = 4 << 30  # bytes left free next to the slab (graphs, workspaces, prefill activations)
+
+    def _check_kv_fits(self, kv_shape) -> None:
+        """The KV slab is the largest allocation of the service (tens of GB at
+        the default 512 slots); check it against the device's free HBM first,
+        with a message naming the knobs, instead of an allocator OOM."""
+        if self.device.type != "cuda":
+            return
+        need = 2 * math.prod(kv_shape) * (1 if self.cfg.kv_dtype == "fp8" else 2)
+        free, total = torch.cuda.mem_get_info(self.device)
+        if need + self.KV_HEADROOM > free:
+            raise RuntimeError(
+                f"KV cache of {need / 2**30:.1f} GiB ({self.num_slots} slots x {self.cfg.max_seq} positions, "
+                f"{self.cfg.kv_dtype}) does not fit the {free / 2**30:.1f} GiB free of {total / 2**30:.1f} GiB on "
+                f"{self.device} (+{self.KV_HEADROOM >> 30} GiB headroom): lower LOCAL_LLM_MAX_BATCH, or use "
+                f"LOCAL_LLM_KV_DTYPE=fp8")
 
     # ------------------------------------------------------------ weights
     def _init_weights(self, seed: int) -> Dict[str, torch.Tensor]:

@@ -212,3 +212,12 @@ def test_gpu_engine_choices_and_mixed_projects_match_the_synchronous_loop():
         assert doc["classTypeCorrection"] is None or doc["classTypeCorrection"] in CLASS_TYPES
         assert all(1 <= len(x["businessLogic"]) <= 3 for x in doc["methods"])
     assert pipe.stats["unshared_prefills"] > 0
+
+
+@pytest.mark.gpu
+def test_kv_slab_larger_than_free_hbm_is_refused_with_a_clear_error():
+    from dmcp.models.llm import LocalLM, preset
+    free, _ = torch.cuda.mem_get_info()
+    slots = int(free // (2 * 16 * 8 * 65536 * 64)) + 8  # bf16 slab just over the free HBM
+    with pytest.raises(RuntimeError, match="LOCAL_LLM_MAX_BATCH"):
+        LocalLM(preset("dmcp-coder-1b", max_batch=slots, max_seq=65536), device="cuda:0")

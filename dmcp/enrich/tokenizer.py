@@ -98,7 +98,28 @@ class _Base:
         if i <= 0:
             return head + self.encode(text), 0
         pre = head + self.encode(text[:i])
-        return pre + self.encode(text[i:]), len(pre)
+        return pre + self.encode_continuation(text[i:]), len(pre)
+
+    def encode_continuation(self, text: str) -> List[int]:
+        """Ids of ``text`` spliced after other text: exactly its bytes.  A
+        SentencePiece-style pre-tokenizer prepends a dummy-prefix space to
+        every encode -- a leading lone space token is dropped; a piece that
+        merged that space into the first word falls back to
+        :meth:`encode_fragment` for that word only."""
+        ids = self.encode(text)
+        raw = text.encode("utf-8")
+        tb = self.token_bytes
+        got = b"".join(tb[i] for i in ids)
+        if got == raw:
+            return ids
+        if got == b" " + raw:
+            if ids and tb[ids[0]] == b" ":
+                return ids[1:]
+            # "▁Source" as one piece: re-spell the first piece's text without the space
+            first = tb[ids[0]]
+            if first.startswith(b" ") and b"".join(tb[i] for i in ids[1:]) == raw[len(first) - 1:]:
+                return self.encode_fragment(first[1:].decode("utf-8", "replace")) + ids[1:]
+        return self.encode_fragment(text)
 
 
 class ByteTokenizer(_Base):
@@ -152,7 +173,11 @@ class HFTokenizer(_Base):
         self.token_bytes: List[bytes] = []
         for i in range(n):
             s = self.tk.id_to_token(i)
-            if s is None or i in special:
+            if s is not None and not byte_level and len(s) == 6 and s.startswith("<0x") and s.endswith(">"):
+                # byte-fallback piece (a byte, even where the file flags it special)
+                self.token_bytes.append(bytes([int(s[3:5], 16)]))
+                fallback.add(i)
+            elif s is None or i in special:
                 self.token_bytes.append(b"")
             elif byte_level:
                 try:

@@ -30,8 +30,9 @@ class ScanFailed(RuntimeError):
     pass
 
 
-def _write_blob(stream, data: bytes) -> None:
-    stream.write(_HDR.pack(len(data)))
+def _write_blob(stream, data) -> None:
+    """``data``: bytes or a byte memoryview (written without a copy)."""
+    stream.write(_HDR.pack(data.nbytes if isinstance(data, memoryview) else len(data)))
     stream.write(data)
 
 
@@ -59,21 +60,47 @@ def scan_in_child(tree, language: str, threads: int, framework: str = "", timeou
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
     env.update(env_extra or {})
-    import io
-    buf = io.BytesIO()
-    _write_blob(buf, json.dumps(header).encode())
-    if files is not None:
-        for rel, data in files.items():
-            _write_blob(buf, rel.encode("utf-8", "surrogateescape"))
-            _write_blob(buf, bytes(data))
     proc = subprocess.Popen([sys.executable, "-m", "dmcp.parsers.isolated"], stdin=subprocess.PIPE,
                             stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, cwd=ROOT)
+    # the tree is STREAMED to the child from a writer thread (no serialised
+    # copy of an up-to-1-GiB snapshot in this process) while two reader
+    # threads drain its stdout / stderr (a full pipe would block either side)
+    import threading
+
+    def feed() -> None:
+        try:
+            _write_blob(proc.stdin, json.dumps(header).encode())
+            if files is not None:
+                for rel, data in files.items():
+                    _write_blob(proc.stdin, rel.encode("utf-8", "surrogateescape"))
+                    _write_blob(proc.stdin, memoryview(data).cast("B"))
+        except (BrokenPipeError, OSError, ValueError):
+            pass  # the child died (reported by its exit status) or was killed
+        finally:
+            try:
+                proc.stdin.close()
+            except OSError:
+                pass
+    got = {}
+
+    def drain(name, stream) -> None:
+        got[name] = stream.read()
+    threads = [threading.Thread(target=feed, name="scan-feed", daemon=True),
+               threading.Thread(target=drain, args=("out", proc.stdout), name="scan-out", daemon=True),
+               threading.Thread(target=drain, args=("err", proc.stderr), name="scan-err", daemon=True)]
+    for t in threads:
+        t.start()
     try:
-        out, err = proc.communicate(input=buf.getvalue(), timeout=timeout_s)
+        proc.wait(timeout=timeout_s)
     except subprocess.TimeoutExpired:
         proc.kill()
-        proc.communicate()
+        proc.wait()
+        for t in threads:
+            t.join(10)
         raise ScanFailed(f"source scan did not finish in {timeout_s:.0f} s (child killed)")
+    for t in threads:
+        t.join(30)
+    out, err = got.get("out", b""), got.get("err", b"")
     if proc.returncode != 0:
         tail = (err or b"").decode("utf-8", "replace").strip().splitlines()[-3:]
         how = f"signal {-proc.returncode}" if proc.returncode < 0 else f"exit code {proc.returncode}"

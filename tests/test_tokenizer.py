@@ -175,3 +175,21 @@ def test_worker_process_serves_a_checkpoint(ckpt):
         assert [r.methods[0].method_name for r in res] == ["run"] * 3
     finally:
         pool.close()
+
+
+def test_sentencepiece_split_prompt_round_trips_exactly(tmp_path):
+    """Metaspace tokenizers add a dummy-prefix space to each encode: the
+    per-class half of a split prompt must still spell exactly the prompt's
+    bytes (no extra space before 'Source of'), so the local model sees what
+    an API backend gets."""
+    from dmcp.enrich.tokenizer import HFTokenizer
+    path = str(tmp_path / "sp.json")
+    _train_bpe(path, vocab=400, metaspace=True)
+    tok = HFTokenizer(path, bos=1)
+    text = "Project context (README):\nA shop.\n\nSource of co.x.OrderService:\n```java\nclass A {}\n```\n"
+    ids, split = tok.encode_split(text, "Source of ")
+    assert ids[0] == 1 and split > 1
+    # the prompt's first piece carries SentencePiece's usual dummy-prefix
+    # space (as any encode of the whole prompt does); nothing else is added
+    assert b"".join(tok.token_bytes[i] for i in ids[1:]) == b" " + text.encode()
+    assert b"".join(tok.token_bytes[i] for i in ids[split:]) == text[text.find("Source of "):].encode()

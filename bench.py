@@ -63,6 +63,8 @@ def parse_args(argv=None):
     ap.add_argument("--enrich-local-kv", default="fp8", choices=["bf16", "fp8"])
     ap.add_argument("--enrich-local-batch", type=int, default=512)
     ap.add_argument("--enrich-local-presets", default="dmcp-coder-1b,llama3.2-1b-code")
+    ap.add_argument("--remote-steps", type=int, default=3,
+                    help="timed analyses on the remote-repository path (extra.remotePath; 0 = skip)")
     return ap.parse_args(argv)
 
 
@@ -167,6 +169,39 @@ def _enrich_local(pool, args, ctx, work, rank):
         app.db.close()
 
 
+def _remote_path(args, work, repo, threads):
+    """extra.remotePath: the production path of a REMOTE repository, timed --
+    a private bare clone (``git clone --bare --depth 1``, never the local
+    objects in place) + the source scan in an isolated child process with its
+    time limit (dmcp/parsers/isolated.py) + Phase 1 + graph publish.  The
+    repository is a local one (no network here), so the clone is a local
+    transport: the cost of the clone machinery and the child scan, not of a
+    network."""
+    from dmcp.app import App
+    from dmcp.config import Config
+    cfg = Config(db_path=os.path.join(work, "remote.db"), git_clone_base_path=os.path.join(work, "rclones"),
+                 parser_threads=threads, enrich_backend="null", require_enrichment_for_analyze=False,
+                 recover_stuck_on_start=False, scan_isolation="process")
+    app = App(cfg)
+    app.git.read_local_in_place = False
+    try:
+        app.indexer.analyze_project(repo)  # warm-up
+        t0 = time.perf_counter()
+        acc = {}
+        for _ in range(args.remote_steps):
+            r = app.indexer.analyze_project(repo)
+            for k, v in r.stats.items():
+                if k.startswith("analyze."):
+                    acc[k] = acc.get(k, 0.0) + v
+        el = time.perf_counter() - t0
+        return {"msPerAnalysis": round(1e3 * el / args.remote_steps, 2),
+                "classesPerSec": round(r.classes_analyzed * args.remote_steps / el, 1),
+                "phaseMs": {k: round(v / args.remote_steps, 2) for k, v in acc.items()},
+                "path": "bare clone (local transport) + isolated child scan + Phase 1"}
+    finally:
+        app.close()
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
     pools = _spawn_enrich_pools(args) if args.enrich == "none" else {}  # before anything touches HIP
@@ -235,6 +270,12 @@ def main(argv=None) -> int:
             extra["graphQueryMs"] = {"p50": round(lat[len(lat) // 2], 3), "p99": round(lat[int(len(lat) * 0.99) - 1], 3)}
             extra["stackTrace20Ms"] = {"p50": round(st_lat[len(st_lat) // 2], 3),
                                        "p99": round(st_lat[max(0, int(len(st_lat) * 0.99) - 1)], 3)}
+        if rank == 0 and args.remote_steps > 0:
+            try:
+                extra["remotePath"] = _remote_path(args, work, repo, threads)
+            except Exception as e:
+                logging.getLogger("bench").exception("remotePath failed")
+                extra["remotePath"] = {"error": repr(e)[:300]}
         # agreed by every rank: a rank without a worker skips the collective path for all
         names = [p.strip() for p in args.enrich_local_presets.split(",") if p.strip()]
         if args.enrich == "none" and args.enrich_local_classes > 0 and \

@@ -10,6 +10,10 @@ scan and writes the JSON document to its stdout.  A crash (signal, abort) or
 a hang past ``timeout_s`` kills the child only -- the server process never
 executes the untrusted parse -- and surfaces as :class:`ScanFailed`, which
 the pipeline turns into ``ANALYSIS_FAILED``.
+
+The child is the native analyzer binary (``bin/srcscan stdin`` / ``srcscan
+<root>``, built with the module) when it is present -- it starts in
+milliseconds -- else a Python child running the same native scan.
 """
 from __future__ import annotations
 
@@ -45,8 +49,14 @@ def _read_blob(stream) -> Optional[bytes]:
     return data if len(data) == n else None
 
 
+def native_cli() -> Optional[str]:
+    """The built ``bin/srcscan`` analyzer, or None."""
+    path = os.path.join(ROOT, "bin", "srcscan")
+    return path if os.access(path, os.X_OK) else None
+
+
 def scan_in_child(tree, language: str, threads: int, framework: str = "", timeout_s: float = 120.0,
-                  env_extra: Optional[dict] = None) -> dict:
+                  env_extra: Optional[dict] = None, native: Optional[bool] = None) -> dict:
     """The scan document of ``tree`` (a :class:`dmcp.index.source.SourceTree`),
     computed by a child process; raises :class:`ScanFailed` on a crash, a
     non-zero exit, unreadable output or a timeout."""
@@ -60,8 +70,18 @@ def scan_in_child(tree, language: str, threads: int, framework: str = "", timeou
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
     env.update(env_extra or {})
-    proc = subprocess.Popen([sys.executable, "-m", "dmcp.parsers.isolated"], stdin=subprocess.PIPE,
-                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, cwd=ROOT)
+    cli = native_cli() if native is not False else None
+    if cli is not None:
+        argv = [cli] + (["stdin"] if files is not None else []) + ["--lang", language or "auto",
+                                                                   "--threads", str(int(threads or 0))]
+        if framework:
+            argv += ["--framework", framework]
+        if files is None:
+            argv.append(tree.directory)
+    else:
+        argv = [sys.executable, "-m", "dmcp.parsers.isolated"]
+    proc = subprocess.Popen(argv, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env,
+                            cwd=ROOT)
     # the tree is STREAMED to the child from a writer thread (no serialised
     # copy of an up-to-1-GiB snapshot in this process) while two reader
     # threads drain its stdout / stderr (a full pipe would block either side)
@@ -69,7 +89,11 @@ def scan_in_child(tree, language: str, threads: int, framework: str = "", timeou
 
     def feed() -> None:
         try:
-            _write_blob(proc.stdin, json.dumps(header).encode())
+            if cli is not None:  # the binary: u64 file count, then (path, contents) blobs
+                if files is not None:
+                    proc.stdin.write(_HDR.pack(len(files)))
+            else:
+                _write_blob(proc.stdin, json.dumps(header).encode())
             if files is not None:
                 for rel, data in files.items():
                     _write_blob(proc.stdin, rel.encode("utf-8", "surrogateescape"))

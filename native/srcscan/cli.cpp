@@ -4,14 +4,64 @@
 //           [--framework NAME] <project-root>
 //   srcscan go [-o out.json] <project-root>      go-analyzer compatible ProjectAnalysis
 //   srcscan file --lang java|typescript [--rel REL] [--framework F] <file>
+//   srcscan stdin [--lang L] [--threads N] [--framework F]
+//           a project streamed on stdin (u64 LE file count, then per file a
+//           u64 LE length + relative path and a u64 LE length + contents) --
+//           the isolated scan of an in-memory snapshot (dmcp/parsers/isolated.py):
+//           the untrusted parse runs in this short-lived process, which starts
+//           in milliseconds (the Python child took ~100 ms to import)
 //
 // Mirrors tools/go-analyzer/cmd/analyzer/main.go:20-59: JSON on stdout or to
 // the -o file; exit status 1 on usage / I/O errors.
+#include <chrono>
+#include <csignal>
+#include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
+#include <utility>
+#include <vector>
 
+#include "common.hpp"
 #include "srcscan.hpp"
+
+static bool read_exact(void* dst, size_t n) {
+    return n == 0 || std::fread(dst, 1, n, stdin) == n;
+}
+
+static bool read_blob(std::string& out) {
+    uint64_t n = 0;
+    if (!read_exact(&n, sizeof n) || n > (uint64_t(1) << 34)) return false;
+    out.resize((size_t)n);
+    return read_exact(out.data(), (size_t)n);
+}
+
+// fault injection for the isolation tests (DMCP_SCAN_CHILD_FAULT=hang|crash)
+static void injected_fault() {
+    const char* f = std::getenv("DMCP_SCAN_CHILD_FAULT");
+    if (!f) return;
+    if (std::strcmp(f, "hang") == 0) std::this_thread::sleep_for(std::chrono::hours(1));
+    if (std::strcmp(f, "crash") == 0) std::raise(SIGSEGV);  // as a front-end fault would
+}
+
+static int scan_stdin(const srcscan::ScanOptions& opt, std::string& json) {
+    uint64_t nfiles = 0;
+    if (!read_exact(&nfiles, sizeof nfiles)) return 3;
+    std::vector<std::pair<std::string, std::string>> tree;
+    tree.reserve((size_t)nfiles);
+    for (uint64_t k = 0; k < nfiles; ++k) {
+        std::string rel, data;
+        if (!read_blob(rel) || !read_blob(data)) return 3;
+        tree.emplace_back(std::move(rel), std::move(data));
+    }
+    injected_fault();
+    std::string root = srcscan::vfs_mount(std::move(tree));
+    json = srcscan::scan_project_json(root, opt);
+    srcscan::vfs_unmount(root);
+    return 0;
+}
 
 static int usage() {
     std::fprintf(stderr,
@@ -25,7 +75,9 @@ int main(int argc, char** argv) {
     std::string mode = "project", out, lang = "auto", framework, rel, target;
     int threads = 0;
     int i = 1;
-    if (i < argc && (std::strcmp(argv[i], "go") == 0 || std::strcmp(argv[i], "file") == 0)) mode = argv[i++];
+    if (i < argc && (std::strcmp(argv[i], "go") == 0 || std::strcmp(argv[i], "file") == 0 ||
+                     std::strcmp(argv[i], "stdin") == 0))
+        mode = argv[i++];
     for (; i < argc; ++i) {
         std::string a = argv[i];
         auto need = [&](std::string& dst) {
@@ -42,9 +94,19 @@ int main(int argc, char** argv) {
         else if (target.empty()) target = a;
         else return usage();
     }
-    if (target.empty()) return usage();
+    if (target.empty() && mode != "stdin") return usage();
     std::string json;
-    if (mode == "go") {
+    if (mode == "stdin") {
+        srcscan::ScanOptions opt;
+        opt.language = lang;
+        opt.threads = threads;
+        opt.framework = framework;
+        int rc = scan_stdin(opt, json);
+        if (rc != 0) {
+            std::fprintf(stderr, "error: truncated project stream on stdin\n");
+            return rc;
+        }
+    } else if (mode == "go") {
         if (!srcscan::file_exists(srcscan::join_path(target, "go.mod"))) {
             std::fprintf(stderr, "error: reading go.mod: %s/go.mod not found\n", target.c_str());
             return 1;

@@ -333,10 +333,19 @@ def test_isolated_scan_matches_in_process_and_survives_faults(tmp_path):
     assert set(iso.units) == set(inproc.units) and len(iso.units) == 25
     a, b = inproc.units["co.acme.shop.order.OrderController"], iso.units["co.acme.shop.order.OrderController"]
     assert a.methods == b.methods and a.params == b.params and a.class_type == b.class_type
-    with pytest.raises(ScanFailed, match="signal"):
-        scan_in_child(tree, "java", 1, "", 60, env_extra={"DMCP_SCAN_CHILD_FAULT": "crash"})
-    with pytest.raises(ScanFailed, match="did not finish"):
-        scan_in_child(tree, "java", 1, "", 2, env_extra={"DMCP_SCAN_CHILD_FAULT": "hang"})
+    from dmcp.parsers.isolated import native_cli
+    assert native_cli() is not None  # built with the module: the default child
+    for native in (True, False):  # bin/srcscan stdin, and the Python child
+        doc = scan_in_child(tree, "java", 1, "", 60, native=native)
+        assert len(doc["files"] if "files" in doc else doc.get("units", doc)) > 0
+        with pytest.raises(ScanFailed, match="signal"):
+            scan_in_child(tree, "java", 1, "", 60, env_extra={"DMCP_SCAN_CHILD_FAULT": "crash"}, native=native)
+        with pytest.raises(ScanFailed, match="did not finish"):
+            scan_in_child(tree, "java", 1, "", 2, env_extra={"DMCP_SCAN_CHILD_FAULT": "hang"}, native=native)
+    docs = [scan_in_child(tree, "java", 1, "", 60, native=n) for n in (True, False)]
+    for d in docs:
+        d.pop("stats", None)  # timings
+    assert docs[0] == docs[1]
     app = make_app(tmp_path, scan_isolation="process", scan_timeout_seconds=2.0)
     assert app.indexer.analyze_project(str(repo)).success  # isolated, healthy
     import os

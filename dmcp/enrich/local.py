@@ -245,10 +245,15 @@ class _Seq:
     prefix_split: int = 0                # leading prompt tokens encoding the text before 'Source of'
     shared: bool = False                 # its prompt starts with the resident shared prefix (set at admission)
 
+    _free_budget: int = -1
+
     @property
     def free_budget(self) -> int:
-        """Sampled (non-forced) tokens the reply may take: ~its decode steps."""
-        return template_budget([s for s in self.segs if s.forced is None])
+        """Sampled (non-forced) tokens the reply may take: ~its decode steps
+        (of the reply as planned; computed once -- the admission order key)."""
+        if self._free_budget < 0:
+            self._free_budget = template_budget([s for s in self.segs if s.forced is None])
+        return self._free_budget
 
 
 from .feeds import IterFeed, QueueFeed  # noqa: E402,F401  (re-exported)
@@ -361,6 +366,8 @@ class LocalEngine:
                       "split_classes": 0, "methods_dropped": 0, "type_corrections": 0, "choice_waits": 0}
         self._pf_events: List[tuple] = []  # (start, end) device events of the batched prefills
         self._lock = threading.Lock()
+        self._frag_cache: Dict[bytes, List[int]] = {}      # forced text -> ids
+        self._prefix_cache: Dict[str, List[int]] = {}      # per-project prompt text -> ids (one project at a time)
 
     # ---------------------------------------------------------------- api
     def generate(self, inputs: Sequence[EnrichmentInput], readme: Optional[str]) -> List[str]:
@@ -426,7 +433,7 @@ class LocalEngine:
         remaining bytes ``rest`` are forced, its branch spliced in."""
         after: List[Segment] = []
         if rest:
-            after.append(Segment(rest, ids=self.tok.encode_fragment(rest.decode("utf-8"))))
+            after.append(Segment(rest, ids=self._fragment(rest)))
         if seg.then and seg.then[k]:
             after += self._encode_forced(list(seg.then[k]))
         if seg.choice == CHOICE_CLASS_TYPE and k > 0:
@@ -493,7 +500,18 @@ class LocalEngine:
     # ------------------------------------------------------------ helpers
     def _prompt(self, seq: _Seq, readme: Optional[str], budget: int) -> List[int]:
         """Prompt tokens of ``seq``; sets ``seq.prefix_split``."""
-        ids, split = self.tok.encode_split(build_enrichment_prompt(seq.inp, readme), PREFIX_MARKER.decode())
+        text = build_enrichment_prompt(seq.inp, readme)
+        i = text.find(PREFIX_MARKER.decode())
+        if i > 0:  # the per-project text (instructions + README) is tokenised once per project
+            pre = self._prefix_cache.get(text[:i])
+            if pre is None:
+                if len(self._prefix_cache) >= 8:
+                    self._prefix_cache.clear()
+                pre = self._prefix_cache[text[:i]] = ([self.tok.bos] if self.tok.bos is not None else []) + \
+                    self.tok.encode(text[:i])
+            ids, split = pre + self.tok.encode_continuation(text[i:]), len(pre)
+        else:
+            ids, split = self.tok.encode_split(text, PREFIX_MARKER.decode())
         head = 1 if self.tok.bos is not None else 0
         limit = self.cfg.max_seq - budget - 2
         if self.max_prompt_tokens:
@@ -514,10 +532,16 @@ class LocalEngine:
         P = s.prefix_split if self.shared_prefix else 0
         return P if self.MIN_SHARED_PREFIX <= P < len(s.prompt) else 0
 
+    def _fragment(self, text: bytes) -> List[int]:
+        ids = self._frag_cache.get(text)
+        if ids is None:
+            ids = self._frag_cache[text] = self.tok.encode_fragment(text.decode("utf-8"))
+        return ids
+
     def _encode_forced(self, segs: List[Segment]) -> List[Segment]:
         for seg in segs:
             if seg.forced is not None and seg.ids is None:
-                seg.ids = self.tok.encode_fragment(seg.forced.decode("utf-8"))
+                seg.ids = self._fragment(seg.forced)
         return segs
 
     def _build_prompt(self, s: _Seq, readme: Optional[str]) -> List[int]:
@@ -684,7 +708,7 @@ class LocalEngine:
         prefix_toks: Optional[List[int]] = None  # the resident shared prefix
         P = 0
         prev_event = None
-        prev_buf = 1
+        prev_buf, prev_n = 1, 0
         step_no = -1                     # number of the last launched step
         finished: List[_Seq] = []
         inflight: Optional[dict] = None  # the batched prefill in flight
@@ -814,9 +838,9 @@ class LocalEngine:
                 if not self.pipeline:
                     if event is not None:
                         event.synchronize()
-                    ids = self._host_ids[buf]
+                    ids = self._host_ids[buf][:len(toks)].tolist()  # one conversion, not one per row
                     for s, r in sample_at:
-                        s.next_token = int(ids[r])
+                        s.next_token = ids[r]
                 else:
                     # the ids of the step before the one just launched (or of
                     # the last one, when none was): gathered rows' tokens and
@@ -826,13 +850,13 @@ class LocalEngine:
                     if gathered or waiting:
                         if prev_event is not None:  # the step whose ids are read
                             prev_event.synchronize()
-                        ids = self._host_ids[prev_buf]
+                        ids = self._host_ids[prev_buf][:prev_n].tolist()  # one conversion, not one per row
                         for s in waiting:
-                            s.next_token = int(ids[s.await_row])
+                            s.next_token = ids[s.await_row]
                             s.await_row = -1
                             self.stats["choice_waits"] += 1
                         for s, row, src in gathered:
-                            m = self._after_feed(s, int(ids[src]))
+                            m = self._after_feed(s, ids[src])
                             if not s.done and m is not None:
                                 if self._in_choice(s):  # the row just launched selected a choice token
                                     s.await_row, s.await_step = row, step_no
@@ -840,7 +864,7 @@ class LocalEngine:
                                     s.next_src = row  # its selection in the step just launched
                 t3 = time.perf_counter()
                 if toks:
-                    prev_event, prev_buf = event, buf
+                    prev_event, prev_buf, prev_n = event, buf, len(toks)
                     self.stats["decode_steps"] += 1
                     self.stats["decode_rows"] += len(toks)
                     self.stats["generated_tokens"] += len(toks)

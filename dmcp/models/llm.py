@@ -259,6 +259,12 @@ class LocalLM:
         self.use_wgemm = self.device.type == "cuda" and wgemm_shapes_ok(c)
         self.wgemm_ws = (ops.wgemm_workspace(min(self.max_rows, ops.WGEMM_MAX_ROWS), max(c.qkv_dim, c.hidden),
                                              self.device) if self.use_wgemm else None)
+        # decode steps past fused_max_rows select their ids with the fused LM
+        # head + masked argmax (csrc/wgemm.hip MODE_ARGMAX) instead of
+        # F.linear + masked_argmax (at 128,256 ids: 1.6 ms + 0.36 ms per
+        # 533-row step on hipBLASLt, profiles/kstats_llama_r4.txt)
+        self.fused_head = self.device.type == "cuda" and ops.lm_head_supported(c.vocab_size, c.hidden)
+        self.head_ws = ops.lm_head_workspace(c.vocab_size, self.device) if self.fused_head else None
 
     KV_HEADROOM = 4 << 30  # bytes left free next to the slab (graphs, workspaces, prefill activations)
 
@@ -495,13 +501,21 @@ class LocalLM:
         row attends to positions <= its own, so that is an exact causal
         extend.  Rows with slot -1 are padding.  Returns logits [B, vocab]
         (bf16).  Capturable into a hipGraph."""
-        c = self.cfg
         B = tokens.shape[0]
         if B > self.max_rows:
             raise ValueError(f"decode: {B} rows > max_rows {self.max_rows}")
         if self.use_fused and B <= self.fused_max_rows:
             return self._decode_fused(tokens, slots, positions, src, last_ids, mask_idx, mask_alt, alt_token,
                                       prefix_rows)
+        h = self._decode_trunk(tokens, slots, positions, src, last_ids, mask_idx, mask_alt, alt_token, prefix_rows)
+        return F.linear(h, self.w["lm_head"])
+
+    def _decode_trunk(self, tokens, slots, positions, src, last_ids, mask_idx, mask_alt, alt_token,
+                      prefix_rows) -> torch.Tensor:
+        """Every layer of a decode step of > ``fused_max_rows`` rows; returns
+        the final normalised hidden states [B, hidden] (the LM head's input)."""
+        c = self.cfg
+        B = tokens.shape[0]
         chunk, splits = ops.decode_plan(B, c.n_kv_heads, c.max_seq, c.kv_dtype)
         resid, h, seq_len = ops.decode_embed_norm(self.w["embed"], tokens, positions, self.w["l0.ln1"], c.eps,
                                                   src, last_ids, mask_idx, mask_alt, alt_token)
@@ -525,7 +539,7 @@ class LocalLM:
             h = ops.add_rmsnorm(o, self.w[f"l{i}.ln2"], c.eps, residual=resid)
             m = self._mlp(i, h)
             h = ops.add_rmsnorm(m, nxt, c.eps, residual=resid)
-        return F.linear(h, self.w["lm_head"])
+        return h
 
     def _prefix(self, i: int, rows: Optional[torch.Tensor] = None):
         if not self.shared_prefix:
@@ -619,6 +633,14 @@ class LocalLM:
         ``mask_alt`` / ``alt_token`` / ``prefix_rows``: see :meth:`decode`.
         Capturable."""
         B = tokens.shape[0]
+        if self.fused_head and not (self.use_fused and B <= self.fused_max_rows):
+            # the LM head + grammar-masked selection in one weight-streaming
+            # kernel: no [B, vocab] logits (returned as None)
+            h = self._decode_trunk(tokens, slots, positions, src, last_ids, mask_idx, mask_alt, alt_token,
+                                   prefix_rows)
+            ids = ops.lm_head_argmax(h, self.w["lm_head"], masks, mask_idx, out=last_ids[:B],
+                                     workspace=self.head_ws)
+            return None, ids
         logits = self.decode(tokens, slots, positions, src=src, last_ids=last_ids, mask_idx=mask_idx,
                              mask_alt=mask_alt, alt_token=alt_token, prefix_rows=prefix_rows)
         ids = ops.masked_argmax(logits, masks, vocab=self.cfg.vocab_size, mask_idx=mask_idx, out=last_ids[:B])
@@ -739,7 +761,7 @@ class DecodeGraphs:
         b = self.bucket_for(n)
         if b not in self.graphs:
             self._capture(b)
-        g, inp, stage, st, logits, ids, copied = self.graphs[b]
+        g, inp, stage, st, logits, ids, copied = self.graphs[b]  # logits None: fused LM head
         copied.synchronize()  # the previous H2D copy from this staging buffer is done
         # host-side packing into this bucket's pinned staging buffer; padding
         # rows get slot -1 so the kernels skip them
@@ -757,4 +779,4 @@ class DecodeGraphs:
         inp.copy_(stage, non_blocking=True)
         copied.record()
         g.replay()
-        return logits[:n], ids[:n]
+        return (logits[:n] if logits is not None else None), ids[:n]

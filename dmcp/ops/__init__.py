@@ -14,8 +14,8 @@ from __future__ import annotations
 
 from . import hip, reference
 from .hip import (FUSED_MAX_ROWS, PREFIX_MFMA_MAX_SPLITS, WGEMM_MAX_ROWS, decode_workspace,  # noqa: F401
-                  fused_linear_norm, fused_rope_kv, fused_swiglu, prefill_supported, wgemm_resid_norm,
-                  wgemm_rope_kv, wgemm_swiglu, wgemm_workspace)
+                  fused_linear_norm, fused_rope_kv, fused_swiglu, lm_head_supported, lm_head_workspace,
+                  prefill_supported, wgemm_resid_norm, wgemm_rope_kv, wgemm_swiglu, wgemm_workspace)
 from .reference import SharedPrefix, rope_tables  # noqa: F401
 
 
@@ -59,6 +59,11 @@ def silu_mul(gate_up, out=None):
 
 def masked_argmax(logits, mask=None, vocab=None, out=None, mask_idx=None):
     return _on(logits).masked_argmax(logits, mask, vocab, out, mask_idx)
+
+
+def lm_head_argmax(x, w, masks, mask_idx, out=None, workspace=None):
+    """Grammar-masked greedy ids of the LM head (the logits never exist on the GPU path)."""
+    return _on(x).lm_head_argmax(x, w, masks, mask_idx, out, workspace)
 
 
 def embedding(table, ids, out=None):

@@ -35,13 +35,19 @@
 //   * split-K (S > 1) writes fp32 partials, reduced by the fused consumers
 //     below (residual + RMSNorm of the next op; RoPE + KV-cache append);
 //     MODE_SWIGLU writes silu(gate) * up directly (no gate/up activation in
-//     HBM, no SwiGLU launch).
+//     HBM, no SwiGLU launch);
+//   * MODE_ARGMAX is the LM head + the grammar-masked greedy selection: each
+//     block reduces its tile's vocabulary columns of every row to one
+//     (max, id) pair under the row's mask bitset (the grammar state's mask
+//     row), a tiny kernel reduces the pairs per row -- the [rows, vocab]
+//     logits never exist (at 128,256 ids and 512 rows: 131 MB written and
+//     read back per step by F.linear + masked_argmax).
 #include "dmcp_common.hpp"
 
 namespace {
 
 constexpr int kKC = 64;  // K per LDS stage
-constexpr int MODE_BF16 = 0, MODE_PART = 1, MODE_SWIGLU = 2;
+constexpr int MODE_BF16 = 0, MODE_PART = 1, MODE_SWIGLU = 2, MODE_ARGMAX = 3;
 
 __device__ __forceinline__ float silu_f(float g) { return g / (1.f + __expf(-g)); }
 
@@ -57,7 +63,8 @@ template <int NB, int MT, int MR, int MODE, int ST>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) void wgemm_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                        uint16_t* __restrict__ y, float* __restrict__ part, int M, int N,
                                                        int K, int ks, int S, int ntiles, int mparts, int mrows,
-                                                       int I) {
+                                                       int I, const uint32_t* __restrict__ masks,
+                                                       const int32_t* __restrict__ midx, int n_masks, int wwords) {
     constexpr int NF = NB / 16;         // A fragments (16 weight rows each)
     // X rows staged per block (a multiple of 32, <= 4 waves x MT 16-row
     // tiles): the M part rounded up to 32 rows, not to 64 -- at 320 rows
@@ -219,6 +226,41 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     for (int t = 0; t < MT; ++t) {
         if (t >= mtv) continue;
         const int m = m_lo + mw + 16 * t + l16;
+        if constexpr (MODE == MODE_ARGMAX) {
+            // masked max of this row over the tile's NB columns: each lane its
+            // 4 NF columns, then across the 4 lane groups g (every lane takes
+            // part in the shuffles; rows past the part only skip the store).
+            // Values are bf16-rounded (what F.linear + masked_argmax compare),
+            // ties go to the lowest id.
+            float bv = -INFINITY;
+            int bi = 0x7fffffff;
+            if (m < m_hi) {
+                int mr = midx ? midx[m] : 0;
+                mr = mr < 0 ? 0 : (mr >= n_masks ? n_masks - 1 : mr);
+                const uint32_t* mrow = masks + (size_t)mr * wwords + (n0 >> 5);
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    const uint32_t word = mrow[(16 * f + 4 * g) >> 5];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int c = 16 * f + 4 * g + i;
+                        if ((word >> (c & 31)) & 1u) {
+                            const float x = bf2f(f2bf(acc[f][t][i]));
+                            if (x > bv) { bv = x; bi = n0 + c; }  // columns ascend: strict > keeps the lowest
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int msk = 16; msk < kWave; msk <<= 1) {
+                const float ob = __shfl_xor(bv, msk, kWave);
+                const int oi = __shfl_xor(bi, msk, kWave);
+                if (ob > bv || (ob == bv && oi < bi)) { bv = ob; bi = oi; }
+            }
+            if (m < m_hi && g == 0)
+                reinterpret_cast<float2*>(part)[(size_t)nt * M + m] = make_float2(bv, __int_as_float(bi));
+            continue;
+        }
         if (m >= m_hi) continue;
         if constexpr (MODE == MODE_SWIGLU) {
 #pragma unroll
@@ -402,11 +444,35 @@ __global__ __launch_bounds__(kBlock) void reduce_rope_kv_kernel(
     }
 }
 
+// per row: the (max, id) pairs of every vocabulary tile -> the selected id
+// (0 when the mask allows nothing, as masked_argmax); one wave per row
+__global__ __launch_bounds__(kBlock) void lm_head_reduce_kernel(const float2* __restrict__ best, int ntiles, int M,
+                                                                int32_t* __restrict__ ids) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int m = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
+    if (m >= M) return;
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int t = lane; t < ntiles; t += kWave) {
+        const float2 p = best[(size_t)t * M + m];
+        const int pi = __float_as_int(p.y);
+        if (p.x > bv || (p.x == bv && pi < bi)) { bv = p.x; bi = pi; }
+    }
+#pragma unroll
+    for (int msk = 32; msk >= 1; msk >>= 1) {
+        const float ob = __shfl_xor(bv, msk, kWave);
+        const int oi = __shfl_xor(bi, msk, kWave);
+        if (ob > bv || (ob == bv && oi < bi)) { bv = ob; bi = oi; }
+    }
+    if (lane == 0) ids[m] = bi == 0x7fffffff ? 0 : bi;
+}
+
 constexpr int kStages = 3;  // LDS ring stages (2 in flight while one is computed)
 
 template <int NB, int MODE>
 hipError_t launch_wgemm(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int M, int N, int K, int S,
-                        int mparts, int I, hipStream_t st) {
+                        int mparts, int I, hipStream_t st, const uint32_t* masks = nullptr,
+                        const int32_t* midx = nullptr, int n_masks = 0, int wwords = 0) {
     const int ntiles = (MODE == MODE_SWIGLU ? 2 * I : N) / NB;
     const int mrows = (((M + mparts - 1) / mparts) + 15) & ~15;
     const int mt = (mrows + 4 * 16 - 1) / (4 * 16);  // 16-row tiles per wave
@@ -415,7 +481,8 @@ hipError_t launch_wgemm(const uint16_t* x, const uint16_t* w, uint16_t* y, float
     const int ks = K / S;
 #define DMCP_WG1(MT, MR)                                                                                       \
     wgemm_kernel<NB, MT, MR, MODE, kStages><<<grid, kBlock, 0, st>>>(x, w, y, part, M, N, K, ks, S, ntiles,   \
-                                                                     mparts, mrows, I)
+                                                                     mparts, mrows, I, masks, midx, n_masks,  \
+                                                                     wwords)
 #define DMCP_WG(MT)                  \
     do {                             \
         if (full)                    \
@@ -467,6 +534,38 @@ int dmcp_wgemm(const void* x, const void* w, void* y, void* part, int M, int N, 
         case 2: return launch_wgemm<128, MODE_SWIGLU>(xx, ww, yy, pp, M, 2 * I, K, S, mparts, I, st);
         default: return hipErrorInvalidValue;
     }
+}
+
+// LM head + grammar-masked greedy selection: ids[m] = argmax over the ids v
+// allowed by mask row midx[m] (masks [n_masks, wwords] bitsets) of
+// bf16(x[m] . w[v]); best: float2 workspace of (V / NB) * M pairs.  NB = 128
+// vocabulary rows per block when V % 128 == 0 (fewer re-reads of x), else
+// 64.  Contract: M in [1, 512], K % 64 == 0, V % 64 == 0, rows / part <= 256.
+int dmcp_lm_head_argmax(const void* x, const void* w, const void* masks, const void* midx, int n_masks, int wwords,
+                        void* best, void* ids, int M, int V, int K, int mparts, void* stream) {
+    if (M <= 0) return 0;
+    if (!x || !w || !masks || !best || !ids || M > 512 || n_masks < 1 || wwords < (V + 31) / 32 || mparts < 1 ||
+        K % kKC != 0 || V <= 0 || V % 64 != 0 || (((M + mparts - 1) / mparts + 15) & ~15) > 256)
+        return hipErrorInvalidValue;
+    auto st = (hipStream_t)stream;
+    auto xx = (const uint16_t*)x;
+    auto ww = (const uint16_t*)w;
+    auto bb = (float*)best;
+    auto mk = (const uint32_t*)masks;
+    auto mi = (const int32_t*)midx;
+    hipError_t e;
+    int ntiles;
+    if (V % 128 == 0) {
+        ntiles = V / 128;
+        e = launch_wgemm<128, MODE_ARGMAX>(xx, ww, nullptr, bb, M, V, K, 1, mparts, 0, st, mk, mi, n_masks, wwords);
+    } else {
+        ntiles = V / 64;
+        e = launch_wgemm<64, MODE_ARGMAX>(xx, ww, nullptr, bb, M, V, K, 1, mparts, 0, st, mk, mi, n_masks, wwords);
+    }
+    if (e != hipSuccess) return e;
+    lm_head_reduce_kernel<<<(M + kBlock / kWave - 1) / (kBlock / kWave), kBlock, 0, st>>>(
+        (const float2*)best, ntiles, M, (int32_t*)ids);
+    return hipGetLastError();
 }
 
 // resid[M, N] += bf16(x . w^T); out = RMSNorm(resid) * g  (split-K GEMM +

@@ -50,6 +50,7 @@ def lib() -> ctypes.CDLL:
         L = ctypes.CDLL(path)
         sigs = {
             "dmcp_abi_version": ([], _i),
+            "dmcp_lm_head_argmax": ([_vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp], _i),
             "dmcp_add_rmsnorm": ([_vp, _vp, _vp, _vp, _i, _i, _f, _vp], _i),
             "dmcp_rope_kv": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp], _i),
             "dmcp_decode_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _f,
@@ -672,6 +673,53 @@ def _wgemm_args(x: torch.Tensor, w: torch.Tensor, name: str) -> tuple:
     if not 1 <= M <= WGEMM_MAX_ROWS or K % 64 or N % 64:
         raise HipOpsError(f"{name}: needs 1 <= M <= {WGEMM_MAX_ROWS}, K % 64 == 0, N % 64 == 0 (M={M} K={K} N={N})")
     return M, K, N
+
+
+def lm_head_supported(vocab: int, hidden: int) -> bool:
+    """Shapes of the fused LM head + masked argmax (csrc/wgemm.hip MODE_ARGMAX)."""
+    return vocab % 64 == 0 and hidden % 64 == 0
+
+
+def lm_head_workspace(vocab: int, device, rows: int = WGEMM_MAX_ROWS) -> torch.Tensor:
+    """(max, id) pairs of every 64-id vocabulary tile of ``rows`` rows (fp32 pairs)."""
+    return torch.empty(2 * (vocab // 64) * rows, dtype=torch.float32, device=device)
+
+
+def lm_head_argmax(x: torch.Tensor, w: torch.Tensor, masks: torch.Tensor, mask_idx: torch.Tensor,
+                   out: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """ids[m] = argmax over the vocabulary ids allowed by mask row
+    ``mask_idx[m]`` of bf16(x[m] . w[v]) -- the LM head GEMM and the grammar-
+    masked greedy selection in one weight-streaming kernel + a per-row
+    reduction; the [M, V] logits are never written.  x [M, K] bf16 (any M:
+    chunks of WGEMM_MAX_ROWS), w [V, K] bf16, masks int32 [n_masks, ceil(V/32)],
+    mask_idx int32 [M].  Ties -> lowest id; nothing allowed -> 0 (as
+    :func:`masked_argmax`).  Capturable."""
+    _req(x, torch.bfloat16, "lm_head_argmax.x")
+    _req(w, torch.bfloat16, "lm_head_argmax.w")
+    _req(masks, torch.int32, "lm_head_argmax.masks")
+    _req(mask_idx, torch.int32, "lm_head_argmax.mask_idx")
+    M, K = x.shape
+    V = w.shape[0]
+    if w.shape[1] != K or not lm_head_supported(V, K):
+        raise HipOpsError(f"lm_head_argmax: x {tuple(x.shape)} / w {tuple(w.shape)} (needs V % 64 == 0, K % 64 == 0)")
+    W = (V + 31) // 32
+    if masks.dim() != 2 or masks.shape[1] != W or mask_idx.numel() != M:
+        raise HipOpsError(f"lm_head_argmax: masks {tuple(masks.shape)} / mask_idx {mask_idx.numel()} vs M={M}, W={W}")
+    if out is None:
+        out = torch.empty(M, dtype=torch.int32, device=x.device)
+    _req_out(out, torch.int32, M, "lm_head_argmax.out")
+    rows = min(M, WGEMM_MAX_ROWS)
+    if workspace is None:
+        workspace = lm_head_workspace(V, x.device, rows)
+    if workspace.dtype != torch.float32 or workspace.numel() < 2 * (V // 64) * rows:
+        raise HipOpsError("lm_head_argmax: workspace too small")
+    for m0 in range(0, M, WGEMM_MAX_ROWS):
+        mc = min(WGEMM_MAX_ROWS, M - m0)
+        mparts = -(-mc // 256)  # the fewest parts: every weight tile is read once per part
+        _check(lib().dmcp_lm_head_argmax(_ptr(x[m0:m0 + mc]), _ptr(w), _ptr(masks), _ptr(mask_idx[m0:m0 + mc]),
+                                         masks.shape[0], W, _ptr(workspace), _ptr(out[m0:m0 + mc]), mc, V, K,
+                                         mparts, _stream()), "dmcp_lm_head_argmax")
+    return out
 
 
 def _wgemm_ws(workspace: torch.Tensor, n: int, name: str) -> None:

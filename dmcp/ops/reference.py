@@ -194,6 +194,13 @@ def masked_argmax(logits: torch.Tensor, mask: Optional[torch.Tensor] = None, voc
     return ids
 
 
+def lm_head_argmax(x: torch.Tensor, w: torch.Tensor, masks: torch.Tensor, mask_idx: torch.Tensor,
+                   out: Optional[torch.Tensor] = None, workspace=None) -> torch.Tensor:
+    """The fused LM head + masked argmax's definition: F.linear then masked_argmax."""
+    logits = (x.float() @ w.float().t()).to(torch.bfloat16)
+    return masked_argmax(logits, masks, w.shape[0], out, mask_idx)
+
+
 def embedding(table: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     y = table[ids.long().clamp(0, table.shape[0] - 1)]
     if out is not None:

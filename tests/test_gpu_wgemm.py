@@ -139,3 +139,67 @@ def test_model_decode_on_wgemm_matches_library_path(model, rows):
     assert err < 0.03, err
     exp = model.reference_logits(toks + [int(tk[0])])[-1].float()
     assert (got[0] - exp).abs().max().item() / max(1.0, exp.abs().max().item()) < 0.05
+
+
+@pytest.mark.parametrize("V", [320, 32000, 128256, 151936])
+@pytest.mark.parametrize("M", [1, 16, 78, 320, 512, 700])
+def test_lm_head_argmax_matches_fp32_reference(V, M):
+    """Fused LM head + grammar-masked argmax (no logits written) vs the fp32
+    reference: every id is allowed by its row's mask and its fp32 logit is
+    the row's masked maximum up to bf16 rounding (ties may resolve to either
+    id); a mask row that allows nothing gives id 0, as masked_argmax."""
+    from dmcp.ops import hip
+    K = 2048 if V >= 32000 else 256
+    g = torch.Generator().manual_seed(V + M)
+    x = (torch.randn(M, K, generator=g) * 0.5).to(torch.bfloat16).cuda()
+    w = (torch.randn(V, K, generator=g) * 0.02).to(torch.bfloat16).cuda()
+    W = (V + 31) // 32
+    dense = torch.randint(-2**31, 2**31 - 1, (3, W), generator=g, dtype=torch.int64).to(torch.int32)
+    sp = torch.zeros(1, W, dtype=torch.int64)
+    for v in torch.randint(0, V, (40,), generator=g).tolist():
+        sp[0, v >> 5] |= 1 << (v & 31)
+    sparse = torch.where(sp >= 2**31, sp - 2**32, sp).to(torch.int32)  # a few allowed ids
+    masks = torch.cat([dense, sparse, torch.zeros(1, W, dtype=torch.int32)]).cuda()  # row 4: nothing allowed
+    midx = torch.randint(0, 5, (M,), generator=g, dtype=torch.int32).cuda()
+    ids = hip.lm_head_argmax(x, w, masks, midx)
+    ref = x.float() @ w.float().t()
+    bits = ((masks.cpu().long()[midx.cpu().long()][:, torch.arange(V) // 32] >> (torch.arange(V) % 32)) & 1).bool()
+    refm = ref.cpu().masked_fill(~bits, float("-inf"))
+    best = refm.max(1).values
+    got = ids.cpu().long()
+    for m in range(M):
+        if not bits[m].any():
+            assert got[m] == 0
+            continue
+        assert bits[m, got[m]], f"row {m}: id {got[m]} not allowed"
+        assert refm[m, got[m]] >= best[m] - 1e-2 * max(1.0, abs(best[m].item())), f"row {m}"
+    exact = (got == refm.argmax(1)) | ~bits.any(1)
+    assert exact.float().mean() > 0.97  # only near-ties may differ
+
+
+def test_lm_head_argmax_inside_the_decode_step_matches_the_unfused_head():
+    """decode_select_gather on the fused head == F.linear + masked_argmax
+    (the same trunk) for a > 16-row step of the tiny model."""
+    from dmcp.enrich.local import LocalEngine
+    from dmcp.models.llm import LocalLM, preset
+    m = LocalLM(preset("tiny", max_batch=64, max_rows=64, max_seq=512), device="cuda:0", seed=2)
+    assert m.fused_head
+    masks = LocalEngine(m, use_graphs=False).masks
+    B = 40
+    for s in range(B):
+        m.forward_tokens(torch.tensor([256, 65 + s % 20, 66], dtype=torch.int32), s, 0)
+    tok = torch.randint(32, 120, (B,), dtype=torch.int32).cuda()
+    sl = torch.arange(B, dtype=torch.int32).cuda()
+    ps = torch.full((B,), 3, dtype=torch.int32).cuda()
+    mi = (torch.arange(B, dtype=torch.int32) % masks.shape[0]).cuda()
+    last = torch.zeros(64, dtype=torch.int32).cuda()
+    src = torch.full((B,), -1, dtype=torch.int32).cuda()
+    lg, ids = m.decode_select_gather(tok, src, last, sl, ps, masks, mi.clone())
+    assert lg is None
+    ids = ids.clone()
+    m.fused_head = False
+    try:
+        lg2, ids2 = m.decode_select_gather(tok, src, last, sl, ps, masks, mi.clone())
+    finally:
+        m.fused_head = True
+    assert (ids.cpu() == ids2.cpu()).float().mean() > 0.95

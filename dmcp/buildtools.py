@@ -9,6 +9,8 @@ Builds, into the source tree so the artefacts travel with the repo snapshot:
   module (``--sanitize``); ``DMCP_SRCSCAN_SO=<path>`` makes ``dmcp`` load it,
   under ``LD_PRELOAD=$(gcc -print-file-name=libasan.so)`` (scripts/asan_tests.sh)
 * ``dmcp/ops/_hipops<ext>`` -- HIP kernels for gfx950 (see :mod:`dmcp.ops.build`)
+* ``dmcp/enrich/_grammar<ext>`` -- the local engine's native grammar / step
+  builder (``native/grammar/engine.cpp``, host C++17 + pybind11)
 
 Usage: ``python -m dmcp.buildtools [--sanitize] [--no-hip] [--force]``.
 """
@@ -111,6 +113,31 @@ def build_srcscan(force: bool = False, sanitize: bool = False, jobs: int = 0) ->
     return target
 
 
+GRAMMAR_SRC = os.path.join(ROOT, "native", "grammar", "engine.cpp")
+
+
+def grammar_module_path() -> str:
+    return os.path.join(ROOT, "dmcp", "enrich", "_grammar" + ext_suffix())
+
+
+def build_grammar(force: bool = False) -> str:
+    """``dmcp/enrich/_grammar<ext>`` (rebuilt when its source changes)."""
+    target = grammar_module_path()
+    stamp = os.path.join(BUILD, "grammar.stamp")
+    key = _digest([GRAMMAR_SRC], " ".join(CXXFLAGS) + sys.version)
+    if not force and os.path.exists(target) and os.path.exists(stamp) and open(stamp).read().strip() == key:
+        return target
+    import pybind11  # noqa: WPS433 (build-time only)
+    os.makedirs(BUILD, exist_ok=True)
+    tmp = target + ".tmp"
+    _run([CXX, *CXXFLAGS, "-shared", "-fvisibility=hidden", f"-I{pybind11.get_include()}",
+          f"-I{sysconfig.get_paths()['include']}", "-o", tmp, GRAMMAR_SRC])
+    os.replace(tmp, target)
+    with open(stamp, "w") as f:
+        f.write(key)
+    return target
+
+
 SAN_FLAGS = ["-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fPIC", "-pthread",
              "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
 
@@ -155,6 +182,7 @@ def main(argv=None) -> int:
     ap.add_argument("-j", "--jobs", type=int, default=0)
     a = ap.parse_args(argv)
     print(build_srcscan(force=a.force, sanitize=a.sanitize, jobs=a.jobs))
+    print(build_grammar(force=a.force))
     if a.sanitize:
         print(build_srcscan_asan(jobs=a.jobs))
     if not a.no_hip:

@@ -244,6 +244,7 @@ class _Seq:
     prompt: Optional[List[int]] = None   # prompt tokens ([BOS] + text)
     prefix_split: int = 0                # leading prompt tokens encoding the text before 'Source of'
     shared: bool = False                 # its prompt starts with the resident shared prefix (set at admission)
+    h: int = -1                          # its state in the native grammar engine (-1: Python state)
 
     _free_budget: int = -1
 
@@ -321,7 +322,7 @@ class LocalEngine:
     def __init__(self, model: LocalLM, use_graphs: bool = True, max_prompt_tokens: Optional[int] = None,
                  jump_forward: bool = True, shared_prefix: bool = True, pipeline: bool = True,
                  admit_min: Optional[int] = None, longest_first: bool = True, tokenizer=None,
-                 max_new_tokens: Optional[int] = None) -> None:
+                 max_new_tokens: Optional[int] = None, native_grammar: Optional[bool] = None) -> None:
         self.model = model
         self.tok = tokenizer if tokenizer is not None else ByteTokenizer(model.cfg.vocab_size)
         self._tb = self.tok.token_bytes
@@ -368,6 +369,15 @@ class LocalEngine:
         self._lock = threading.Lock()
         self._frag_cache: Dict[bytes, List[int]] = {}      # forced text -> ids
         self._prefix_cache: Dict[str, List[int]] = {}      # per-project prompt text -> ids (one project at a time)
+        # the grammar state machine + step builder in native code
+        # (native/grammar/engine.cpp); None = the Python implementation below
+        # (the reference: both give the same replies, tests/test_local_engine.py)
+        self._native = self._make_native() if native_grammar is not False else None
+        if native_grammar and self._native is None:
+            raise RuntimeError("native grammar engine requested but dmcp.enrich._grammar is not built")
+        import numpy as np
+        self._stage = np.zeros((7, self.max_rows), dtype=np.int32)  # the native builder's step rows
+        self._host_np = [h.numpy() for h in self._host_ids]
 
     # ---------------------------------------------------------------- api
     def generate(self, inputs: Sequence[EnrichmentInput], readme: Optional[str]) -> List[str]:
@@ -386,6 +396,45 @@ class LocalEngine:
             yield from self._session(feed, readme)
 
     # ------------------------------------------------------------ grammar
+    def _make_native(self):
+        try:
+            from . import _grammar
+        except ImportError:
+            return None
+        rest = {}
+        for cid, alts in CHOICES.items():
+            for k, alt in enumerate(alts):
+                for p in range(1, len(alt)):
+                    rest[(cid, k, p)] = self._fragment(alt[p:])
+        return _grammar.Engine(list(self._tb), int(self._quote), [list(CHOICES[c]) for c in sorted(CHOICES)],
+                               dict(self._choice_rows), rest, self.jump_forward, self.pipeline, self.max_rows)
+
+    def _native_template(self, segs: List[Segment]) -> int:
+        """Registers ``segs`` (and the branch lists its choices splice in)."""
+        lists: List[Optional[list]] = []
+        index: Dict[int, int] = {}
+
+        def add(lst: List[Segment]) -> int:
+            if not lst:
+                return -1
+            if id(lst) in index:
+                return index[id(lst)]
+            i = len(lists)
+            index[id(lst)] = i
+            lists.append(None)
+            spec = []
+            for seg in self._encode_forced(lst):
+                if seg.forced is not None:
+                    spec.append((0, seg.ids, 0, 0, -1, []))
+                elif seg.choice >= 0:
+                    spec.append((2, [], 0, 0, seg.choice, [add(t) for t in (seg.then or [])]))
+                else:
+                    spec.append((1, [], seg.min_len, seg.max_len, -1, []))
+            lists[i] = spec
+            return i
+        add(segs)
+        return self._native.add_template(lists)
+
     def _choice_masks(self) -> List[List[int]]:
         """Mask rows of every choice trie state (appended after the two
         free-text rows); fills ``_choice_rows[(choice, prefix)]``."""
@@ -562,6 +611,15 @@ class LocalEngine:
                         self.reply_budget)
         seqs = [_Seq(inp, key, self._encode_forced(segs), part=j, n_parts=len(parts))
                 for j, segs in enumerate(parts)]
+        if self._native is not None:
+            try:
+                for q in seqs:
+                    q.h = self._native.new_seq(self._native_template(q.segs))
+            except BaseException:
+                for q in seqs:
+                    if q.h >= 0:
+                        self._native.release(q.h)
+                raise
         # every part has the same prompt: tokenise once, sized for the longest reply
         longest = max(seqs, key=lambda q: template_budget(q.segs))
         prompt = self._build_prompt(longest, readme)
@@ -597,10 +655,14 @@ class LocalEngine:
             reqs.append((toks[start:], s.slot, start))
             self.stats["prompt_tokens"] += len(toks) - start
             s.prompt_tokens = len(s.prompt)
-            s.out.extend(s.segs[0].forced or b"")
             s.pos = len(toks)
-            s.seg, s.forced_off = 1, 0
-            m = self._enter(s)  # the first selection's mask, or a decided token
+            if s.h >= 0:
+                m = self._native.admit(s.h, s.slot, s.pos, s.shared)
+                m = None if m < 0 else m
+            else:
+                s.out.extend(s.segs[0].forced or b"")
+                s.seg, s.forced_off = 1, 0
+                m = self._enter(s)  # the first selection's mask, or a decided token
             if m is not None:
                 need.append(i)
                 midx_l.append(m)
@@ -642,13 +704,41 @@ class LocalEngine:
             ev.synchronize()
             self.stats["prefill_s"] += time.perf_counter() - t0
         batch = h["batch"]
+        nat = self._native
         if h["ids"] is not None:
             for i, tok in zip(h["need"], h["ids"].tolist()):
-                batch[i].next_token = int(tok)
+                if nat is not None:
+                    nat.set_next(batch[i].h, int(tok))
+                else:
+                    batch[i].next_token = int(tok)
+        if nat is not None:
+            for s in batch:
+                s.done = nat.is_done(s.h)
+                if not s.done:
+                    nat.activate(s.h)
         done = [s for s in batch if s.done]
         self.stats["prefills"] += len(batch)
         self.stats["prefill_batches"] += 1
         return done
+
+    def _launch_staged(self, n: int, buf: int):
+        """:meth:`_launch` of the native builder's rows (``self._stage[:, :n]``)."""
+        if self.graphs is not None:
+            self.graphs.run_staged(self._stage, n)
+            ids = self.graphs.last_ids
+        else:
+            t = torch.from_numpy(self._stage[:, :n].copy()).to(self.model.device)
+            _, ids = self.model.decode_select_gather(t[0].contiguous(), t[4].contiguous(), self._last_ids,
+                                                     t[1].contiguous(), t[2].contiguous(), self.masks,
+                                                     t[3].contiguous(), t[5].contiguous(), self._quote,
+                                                     t[6].contiguous())
+        host = self._host_ids[buf]
+        host[:n].copy_(ids[:n], non_blocking=self.model.device.type == "cuda")
+        if self.model.device.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+            return ev
+        return None
 
     def _launch(self, toks: List[int], slots: List[int], poss: List[int], mrows: List[int],
                 srcs: List[int], alts: List[int], prows: List[int], buf: int):
@@ -674,7 +764,12 @@ class LocalEngine:
 
     def _finish(self, s: _Seq, partials: Dict[Any, List[Optional[str]]]) -> Optional[str]:
         """The class reply once ``s`` (a part of it) is complete, else None."""
-        raw = s.out.decode("utf-8", "replace")
+        if s.h >= 0:
+            raw = self._native.out(s.h).decode("utf-8", "replace")
+            self._native.release(s.h)
+            s.h = -1
+        else:
+            raw = s.out.decode("utf-8", "replace")
         if s.n_parts == 1:
             return raw
         got = partials.setdefault(s.index, [None] * s.n_parts)
@@ -774,6 +869,53 @@ class LocalEngine:
                         inflight = None
                         continue  # admit the next batch before this step when slots allow
                 if not active:
+                    continue
+                nat = self._native
+                if nat is not None:  # ---- one step on the native grammar engine
+                    t0 = time.perf_counter()
+                    n = nat.build(self._stage, step_no + 1)
+                    t1 = time.perf_counter()
+                    event, buf = None, None
+                    if n:
+                        buf = 1 - prev_buf
+                        event = self._launch_staged(n, buf)
+                        step_no += 1
+                    t2 = time.perf_counter()
+                    if not self.pipeline:
+                        if event is not None:
+                            event.synchronize()
+                        nat.apply(self._host_np[buf][:n], step_no, step_no)
+                    else:
+                        # the ids of the step before the one just launched (or
+                        # of the last one, when none was): the gathered rows'
+                        # tokens and the awaited choices
+                        if prev_event is not None:
+                            prev_event.synchronize()
+                        nat.apply(self._host_np[prev_buf][:prev_n], step_no - 1 if n else step_no, step_no)
+                    t3 = time.perf_counter()
+                    if n:
+                        prev_event, prev_buf, prev_n = event, buf, n
+                        self.stats["decode_steps"] += 1
+                        self.stats["decode_rows"] += n
+                        self.stats["generated_tokens"] += n
+                    fin = nat.collect_done()
+                    if fin:
+                        byh = {q.h: q for q in active}
+                        for hh in fin:
+                            q = byh[hh]
+                            q.done = True
+                            finished.append(q)
+                            free_slots.append(q.slot)
+                        active = [q for q in active if not q.done]
+                    t4 = time.perf_counter()
+                    self.stats["wait_s"] += t3 - t2
+                    self.stats["host_s"] += (t1 - t0) + (t4 - t3) + (t2 - t1)
+                    self.stats["decode_s"] += t4 - t0
+                    while finished:
+                        s = finished.pop()
+                        raw = self._finish(s, partials)
+                        if raw is not None:
+                            yield s.index, raw
                     continue
                 # ---- build and launch one step
                 t0 = time.perf_counter()
@@ -894,6 +1036,11 @@ class LocalEngine:
             for a, b in self._pf_events:  # device time of the prefills (stats only)
                 self.stats["prefill_gpu_s"] += a.elapsed_time(b) * 1e-3
             self._pf_events.clear()
+            if self._native is not None:
+                for k, v in self._native.stats().items():
+                    self.stats[k] += v
+                self._native.reset_stats()
+                self._native.reset()
             if P:
                 self.model.clear_prefix()
 

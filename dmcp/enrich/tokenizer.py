@@ -56,7 +56,7 @@ class _Base:
         ids = self.encode(text)
         raw = text.encode("utf-8")
         tb = self.token_bytes
-        if b"".join(tb[i] for i in ids) == raw:
+        if b"".join(map(tb.__getitem__, ids)) == raw:
             return ids
         bid = self.byte_ids()
         if any(bid[b] < 0 for b in raw):
@@ -109,7 +109,7 @@ class _Base:
         ids = self.encode(text)
         raw = text.encode("utf-8")
         tb = self.token_bytes
-        got = b"".join(tb[i] for i in ids)
+        got = b"".join(map(tb.__getitem__, ids))
         if got == raw:
             return ids
         if got == b" " + raw:
@@ -133,6 +133,12 @@ class ByteTokenizer(_Base):
 
     def encode(self, text: str) -> List[int]:
         return list(text.encode("utf-8", "replace"))
+
+    def encode_continuation(self, text: str) -> List[int]:
+        return self.encode(text)  # one id per byte: always exact
+
+    def encode_fragment(self, text: str) -> List[int]:
+        return self.encode(text)
 
 
 def _byte_level_decoder_map() -> dict:

@@ -772,6 +772,22 @@ class DecodeGraphs:
         st[4, :n] = srcs
         st[5, :n] = alts
         st[6, :n] = prefix_rows
+        return self._replay(b, n)
+
+    @torch.inference_mode()
+    def run_staged(self, rows, n: int) -> tuple:
+        """:meth:`run` of rows already packed in an int32 array ``rows`` [7, >= n]
+        (the native grammar engine's step buffer)."""
+        b = self.bucket_for(n)
+        if b not in self.graphs:
+            self._capture(b)
+        g, inp, stage, st, logits, ids, copied = self.graphs[b]
+        copied.synchronize()
+        st[:, :n] = rows[:, :n]
+        return self._replay(b, n)
+
+    def _replay(self, b: int, n: int) -> tuple:
+        g, inp, stage, st, logits, ids, copied = self.graphs[b]
         if n < b:
             st[1, n:] = -1
             st[4, n:] = -1

@@ -1,0 +1,447 @@
+// Grammar engine of the local enrichment model's decode loop -- host C++.
+//
+// The per-step host work of dmcp/enrich/local.py::LocalEngine (the reply
+// grammar's state machine and the packing of a step's rows) in native code:
+// at the enrichment operating point a step carries 500-770 rows, and the
+// Python loop spent ~6 us per row (3.6 ms per step on the MI355X host, more
+// than the device's step -- VERDICT r3 weak #5).  The Python engine keeps
+// admission, prefill, feeds and results; this module owns every admitted
+// sequence's grammar state:
+//
+//   * segments: forced token ids, a free JSON string (>= min_len sampled
+//     tokens, <= max_len bytes, closed by the lone quote token), or a choice
+//     among alternatives (class-type correction, "more business-logic
+//     steps?") whose remaining bytes are forced once one alternative is left
+//     and whose branch segments are spliced in after it;
+//   * build(): one step's rows, straight into the caller's int32 [7, cap]
+//     buffer (token, slot, position, mask row, token source, mask row if the
+//     gathered token is the quote, uses-the-shared-prefix) -- literal rows
+//     with jump-forward over decided tokens, one device-gathered row per
+//     pending free-text selection, nothing for a pending choice selection;
+//   * apply(): the previous step's ids into the grammar (gathered rows,
+//     awaited choices) -- or, without the one-step pipeline, this step's.
+//
+// Semantics are those of the Python reference implementation in local.py
+// (LocalEngine._enter / _after_feed / _speculative_mask / the build loop);
+// tests/test_local_engine.py checks both produce the same replies.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstdint>
+#include <map>
+#include <unordered_map>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace py = pybind11;
+
+namespace {
+
+enum Kind : int { FORCED = 0, FREE = 1, CHOICE = 2 };
+
+struct Seg {
+    int kind = FORCED;
+    std::vector<int32_t> ids;  // forced tokens
+    int min_len = 0, max_len = 0;
+    int choice = -1;
+    std::vector<int> then;     // per alternative: a list of the sequence's template (-1 = none)
+};
+
+// the reply structure of one sequence: lists[0] its segments, the others the
+// branches its choices splice in; freed with the last sequence using it
+struct Template {
+    std::vector<std::vector<Seg>> lists;
+    int refs = 0;
+};
+
+struct Seq {
+    int tid = -1;
+    std::vector<Seg> segs;     // its own copy: splices never touch the template
+    int slot = -1, pos = 0, seg = 0, free_len = 0, free_bytes = 0, forced_off = 0;
+    std::string choice_pref;
+    int next_token = -1, next_src = -1, await_row = -1;
+    long long await_step = -1;
+    bool done = false, shared = false, active = false;
+    std::string out;
+    long long gen_tokens = 0;
+};
+
+constexpr int ROWS = 7;
+
+class Engine {
+  public:
+    Engine(std::vector<py::bytes> token_bytes, int quote, std::vector<std::vector<py::bytes>> choices,
+           std::map<std::pair<int, py::bytes>, int> choice_rows,
+           std::map<std::tuple<int, int, int>, std::vector<int32_t>> rest_ids, bool jump_forward, bool pipeline,
+           int max_rows)
+        : quote_(quote), jump_(jump_forward), pipeline_(pipeline), max_rows_(max_rows) {
+        tb_.reserve(token_bytes.size());
+        for (auto& b : token_bytes) tb_.emplace_back(std::string(b));
+        for (auto& alts : choices) {
+            std::vector<std::string> a;
+            for (auto& x : alts) a.emplace_back(std::string(x));
+            alts_.push_back(std::move(a));
+        }
+        for (auto& kv : choice_rows) rows_[{kv.first.first, std::string(kv.first.second)}] = kv.second;
+        rest_ = std::move(rest_ids);
+    }
+
+    using SegSpec = std::tuple<int, std::vector<int32_t>, int, int, int, std::vector<int>>;
+
+    // a template: lists of segments (kind, forced ids, min_len, max_len,
+    // choice, then = list index per alternative); list 0 is the reply
+    int add_template(const std::vector<std::vector<SegSpec>>& lists) {
+        if (lists.empty()) throw std::invalid_argument("a template needs its main list");
+        Template t;
+        for (auto& spec : lists) {
+            std::vector<Seg> l;
+            l.reserve(spec.size());
+            for (auto& x : spec) {
+                Seg s;
+                s.kind = std::get<0>(x);
+                s.ids = std::get<1>(x);
+                s.min_len = std::get<2>(x);
+                s.max_len = std::get<3>(x);
+                s.choice = std::get<4>(x);
+                s.then = std::get<5>(x);
+                if (s.kind == CHOICE && (s.choice < 0 || s.choice >= (int)alts_.size()))
+                    throw std::invalid_argument("choice id out of range");
+                for (int li : s.then)
+                    if (li >= (int)lists.size()) throw std::invalid_argument("branch list out of range");
+                l.push_back(std::move(s));
+            }
+            t.lists.push_back(std::move(l));
+        }
+        const int tid = next_tid_++;
+        templates_.emplace(tid, std::move(t));
+        return tid;
+    }
+
+    int new_seq(int tid) {
+        Template& t = templates_.at(tid);
+        Seq q;
+        q.tid = tid;
+        q.segs = t.lists[0];
+        ++t.refs;
+        int h;
+        if (!free_handles_.empty()) {
+            h = free_handles_.back();
+            free_handles_.pop_back();
+            seqs_[h] = std::move(q);
+        } else {
+            h = (int)seqs_.size();
+            seqs_.push_back(std::move(q));
+        }
+        return h;
+    }
+
+    void release(int h) {
+        Seq& q = seqs_.at(h);
+        if (q.active) throw std::logic_error("release of an active sequence");
+        auto it = templates_.find(q.tid);
+        if (it != templates_.end() && --it->second.refs <= 0) templates_.erase(it);
+        q = Seq();
+        free_handles_.push_back(h);
+    }
+
+    // after its prefill (prompt + the first forced segment): returns the
+    // mask row of the first selection, or -1 (decided / done)
+    int admit(int h, int slot, int pos, bool shared) {
+        Seq& q = seqs_.at(h);
+        q.slot = slot;
+        q.pos = pos;
+        q.shared = shared;
+        if (!q.segs.empty())
+            for (int t : q.segs[0].ids) q.out += tb_.at(t);
+        q.seg = 1;
+        q.forced_off = 0;
+        return enter(q);
+    }
+
+    void set_next(int h, int tok) { seqs_.at(h).next_token = tok; }
+    void activate(int h) {
+        Seq& q = seqs_.at(h);
+        if (!q.active && !q.done) {
+            q.active = true;
+            active_.push_back(h);
+        }
+    }
+    bool is_done(int h) const { return seqs_.at(h).done; }
+    py::bytes out(int h) const { return py::bytes(seqs_.at(h).out); }
+    int slot(int h) const { return seqs_.at(h).slot; }
+
+    // one step's rows into buf [7, cap]; returns the row count
+    int build(py::array_t<int32_t, py::array::c_style> buf, long long step_no) {
+        auto b = buf.mutable_unchecked<2>();
+        if (b.shape(0) < ROWS) throw std::invalid_argument("buffer needs 7 rows");
+        const int cap = (int)b.shape(1);
+        gathered_.clear();
+        sample_at_.clear();
+        int n = 0;
+        int spare = max_rows_ - (int)active_.size();
+        auto push = [&](int tok, const Seq& q, int mrow, int src, int alt) {
+            if (n >= cap) throw std::length_error("step rows exceed the buffer");
+            b(0, n) = tok;
+            b(1, n) = q.slot;
+            b(2, n) = q.pos;
+            b(3, n) = mrow;
+            b(4, n) = src;
+            b(5, n) = alt;
+            b(6, n) = q.shared ? 1 : 0;
+            ++n;
+        };
+        for (int h : active_) {
+            Seq& q = seqs_[h];
+            if (q.await_row >= 0) continue;  // a choice selection the host has not read yet
+            if (q.next_src >= 0) {
+                int main_m, alt_m;
+                speculative(q, main_m, alt_m);
+                gathered_.push_back({h, n, q.next_src});
+                push(0, q, main_m, q.next_src, alt_m);
+                q.next_src = -1;
+                continue;
+            }
+            int tok = q.next_token;
+            for (;;) {
+                push(tok, q, MASK_NO_QUOTE, -1, -1);
+                const int m = after_feed(q, tok);
+                if (q.done) break;
+                if (m >= 0) {
+                    b(3, n - 1) = m;
+                    if (!pipeline_) sample_at_.push_back({h, n - 1});
+                    else if (in_choice(q)) { q.await_row = n - 1; q.await_step = step_no; }
+                    else q.next_src = n - 1;
+                    break;
+                }
+                if (!jump_ || spare <= 0) break;
+                --spare;
+                tok = q.next_token;
+            }
+        }
+        last_n_ = n;
+        return n;
+    }
+
+    // ids: the selections of step ``read_no`` (pipeline: the step before the
+    // one just launched -- or the last one when none was; else this step's)
+    void apply(py::array_t<int32_t, py::array::c_style> ids_arr, long long read_no, long long launched_no) {
+        auto ids = ids_arr.unchecked<1>();
+        const long long nid = ids.shape(0);
+        auto at = [&](int r) -> int {
+            if (r < 0 || r >= nid) throw std::out_of_range("selection row outside the step");
+            return ids(r);
+        };
+        if (!pipeline_) {
+            for (auto& p : sample_at_) seqs_[p.first].next_token = at(p.second);
+            return;
+        }
+        for (int h : active_) {
+            Seq& q = seqs_[h];
+            if (q.await_row >= 0 && q.await_step == read_no) {
+                q.next_token = at(q.await_row);
+                q.await_row = -1;
+                ++choice_waits_;
+            }
+        }
+        for (auto& g : gathered_) {
+            Seq& q = seqs_[g.h];
+            const int m = after_feed(q, at(g.src));
+            if (!q.done && m >= 0) {
+                if (in_choice(q)) { q.await_row = g.row; q.await_step = launched_no; }
+                else q.next_src = g.row;
+            }
+        }
+        gathered_.clear();
+    }
+
+    // finished sequences leave the active set (in order)
+    std::vector<int> collect_done() {
+        std::vector<int> fin, keep;
+        keep.reserve(active_.size());
+        for (int h : active_) {
+            if (seqs_[h].done) { seqs_[h].active = false; fin.push_back(h); }
+            else keep.push_back(h);
+        }
+        active_.swap(keep);
+        return fin;
+    }
+
+    int n_active() const { return (int)active_.size(); }
+    int n_templates() const { return (int)templates_.size(); }
+    int users() const {  // active sequences reading the shared prefix
+        int u = 0;
+        for (int h : active_) u += seqs_[h].shared ? 1 : 0;
+        return u;
+    }
+    py::dict stats() const {
+        py::dict d;
+        d["choice_waits"] = choice_waits_;
+        d["type_corrections"] = type_corrections_;
+        return d;
+    }
+    void reset_stats() { choice_waits_ = type_corrections_ = 0; }
+    // end of a stream: every sequence and template goes (an abandoned stream
+    // leaves none behind for the next)
+    void reset() {
+        seqs_.clear();
+        free_handles_.clear();
+        active_.clear();
+        templates_.clear();
+        gathered_.clear();
+        sample_at_.clear();
+    }
+
+  private:
+    static constexpr int MASK_NO_QUOTE = 0, MASK_QUOTE = 1, CLASS_TYPE = 0;
+    struct Gathered { int h, row, src; };
+
+    int choice_row(int cid, const std::string& pref) const {
+        auto it = rows_.find({cid, pref});
+        if (it == rows_.end()) throw std::logic_error("no mask row for a choice state");
+        return it->second;
+    }
+
+    int enter(Seq& q) {
+        while (q.seg < (int)q.segs.size()) {
+            const Seg& s = q.segs[q.seg];
+            if (s.kind == FORCED) {
+                if (q.forced_off < (int)s.ids.size()) {
+                    q.next_token = s.ids[q.forced_off++];
+                    return -1;
+                }
+                ++q.seg;
+                q.forced_off = 0;
+                continue;
+            }
+            if (s.kind == CHOICE) {
+                q.choice_pref.clear();
+                return choice_row(s.choice, q.choice_pref);
+            }
+            q.free_len = q.free_bytes = 0;
+            return s.min_len == 0 ? MASK_QUOTE : MASK_NO_QUOTE;
+        }
+        q.done = true;
+        return -1;
+    }
+
+    int choose(Seq& q, int k, int consumed) {
+        const int cid = q.segs[q.seg].choice;
+        const int branch = k < (int)q.segs[q.seg].then.size() ? q.segs[q.seg].then[k] : -1;
+        const std::string& alt = alts_[cid][k];
+        std::vector<Seg> after;
+        if (consumed < (int)alt.size()) {
+            auto it = rest_.find({cid, k, consumed});
+            if (it == rest_.end()) throw std::logic_error("no ids for a choice's rest");
+            Seg r;
+            r.kind = FORCED;
+            r.ids = it->second;
+            after.push_back(std::move(r));
+        }
+        if (branch >= 0) {
+            const auto& l = templates_.at(q.tid).lists.at(branch);
+            after.insert(after.end(), l.begin(), l.end());
+        }
+        if (cid == CLASS_TYPE && k > 0) ++type_corrections_;
+        q.segs.insert(q.segs.begin() + q.seg + 1, std::make_move_iterator(after.begin()),
+                      std::make_move_iterator(after.end()));
+        ++q.seg;
+        q.forced_off = 0;
+        return enter(q);
+    }
+
+    int after_feed(Seq& q, int tok) {
+        const std::string& tbv = tb_.at(tok);
+        q.out += tbv;
+        ++q.pos;
+        ++q.gen_tokens;
+        if (q.seg >= (int)q.segs.size()) return enter(q);
+        const Seg& s = q.segs[q.seg];
+        if (s.kind == FORCED) return enter(q);
+        if (s.kind == CHOICE) {
+            std::string pref = q.choice_pref + tbv;
+            const auto& alts = alts_[s.choice];
+            int live = -1, nlive = 0;
+            for (int k = 0; k < (int)alts.size(); ++k)
+                if (alts[k].size() >= pref.size() && alts[k].compare(0, pref.size(), pref) == 0) { live = k; ++nlive; }
+            if (nlive == 0) throw std::runtime_error("a token left the choice's alternatives");
+            if (nlive == 1) return choose(q, live, (int)pref.size());
+            q.choice_pref = std::move(pref);
+            return choice_row(s.choice, q.choice_pref);
+        }
+        if (tok == quote_) {  // free string closed
+            ++q.seg;
+            q.forced_off = 0;
+            q.free_len = 0;
+            return enter(q);
+        }
+        ++q.free_len;
+        q.free_bytes += (int)tbv.size();
+        if (q.free_bytes >= s.max_len) {
+            q.next_token = quote_;
+            return -1;
+        }
+        return q.free_len >= s.min_len ? MASK_QUOTE : MASK_NO_QUOTE;
+    }
+
+    bool in_choice(const Seq& q) const {
+        return !q.done && q.seg < (int)q.segs.size() && q.segs[q.seg].kind == CHOICE;
+    }
+
+    void speculative(const Seq& q, int& main_m, int& alt_m) const {
+        const Seg& s = q.segs[q.seg];
+        main_m = q.free_len + 1 >= s.min_len ? MASK_QUOTE : MASK_NO_QUOTE;
+        alt_m = -1;
+        if (q.seg + 1 < (int)q.segs.size()) {
+            const Seg& nx = q.segs[q.seg + 1];
+            if (nx.kind == CHOICE) alt_m = choice_row(nx.choice, std::string());
+            else if (nx.kind == FREE) alt_m = nx.min_len == 0 ? MASK_QUOTE : MASK_NO_QUOTE;
+        }
+    }
+
+    std::vector<std::string> tb_;
+    int quote_;
+    bool jump_, pipeline_;
+    int max_rows_;
+    std::vector<std::vector<std::string>> alts_;
+    std::map<std::pair<int, std::string>, int> rows_;
+    std::map<std::tuple<int, int, int>, std::vector<int32_t>> rest_;
+    std::unordered_map<int, Template> templates_;
+    int next_tid_ = 0;
+    std::vector<Seq> seqs_;
+    std::vector<int> free_handles_, active_;
+    std::vector<Gathered> gathered_;
+    std::vector<std::pair<int, int>> sample_at_;
+    int last_n_ = 0;
+    long long choice_waits_ = 0, type_corrections_ = 0;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_grammar, m) {
+    m.doc() = "Native grammar engine of the local enrichment decode loop (see native/grammar/engine.cpp)";
+    py::class_<Engine>(m, "Engine")
+        .def(py::init<std::vector<py::bytes>, int, std::vector<std::vector<py::bytes>>,
+                      std::map<std::pair<int, py::bytes>, int>,
+                      std::map<std::tuple<int, int, int>, std::vector<int32_t>>, bool, bool, int>())
+        .def("add_template", &Engine::add_template)
+        .def("n_templates", [](const Engine& e) { return e.n_templates(); })
+        .def("new_seq", &Engine::new_seq)
+        .def("release", &Engine::release)
+        .def("admit", &Engine::admit)
+        .def("set_next", &Engine::set_next)
+        .def("activate", &Engine::activate)
+        .def("is_done", &Engine::is_done)
+        .def("out", &Engine::out)
+        .def("slot", &Engine::slot)
+        .def("build", &Engine::build)
+        .def("apply", &Engine::apply)
+        .def("collect_done", &Engine::collect_done)
+        .def("n_active", &Engine::n_active)
+        .def("users", &Engine::users)
+        .def("stats", &Engine::stats)
+        .def("reset_stats", &Engine::reset_stats)
+        .def("reset", &Engine::reset);
+}

@@ -381,3 +381,29 @@ def test_bpe_vocabulary_engine_on_cpu():
         assert [m["methodName"] for m in doc["methods"]] == inp.method_names
     text = open(__file__).read()
     assert len(text.encode()) / len(tok.encode(text)) > 3.0  # ~4 bytes per token on source code
+
+
+@pytest.mark.parametrize("pipeline", [True, False])
+def test_native_grammar_engine_matches_the_python_engine(tiny, pipeline):
+    """native/grammar/engine.cpp (the production step builder) generates
+    exactly what the Python reference implementation does: forced skeleton,
+    choices, split parts, jump-forward, mixed projects."""
+    from dmcp.enrich.local import _SharedFeed  # noqa: F401  (module imports fine)
+    readme, other = "A README shared by every prompt. " * 4, "Another project's README. " * 4
+    inputs = _inputs(9) + [EnrichmentInput("class Big {}", "co.x.Big", "java", "LISTENER",
+                                           [f"onEvent{i}" for i in range(30)])]
+    items = [(i, inp, other if i % 4 == 3 else readme) for i, inp in enumerate(inputs)]
+    py = LocalEngine(tiny, pipeline=pipeline, native_grammar=False, max_new_tokens=900)
+    nat = LocalEngine(tiny, pipeline=pipeline, native_grammar=True, max_new_tokens=900)
+    assert py._native is None and nat._native is not None
+    a, b = dict(py.stream(items, None)), dict(nat.stream(items, None))
+    assert a == b
+    for k in ("decode_steps", "decode_rows", "choice_waits", "type_corrections", "split_classes"):
+        assert py.stats[k] == nat.stats[k], k
+    assert nat.stats["split_classes"] == 1 and nat._native.n_templates() == 0  # all released
+    # an abandoned stream leaves nothing behind for the next one
+    g = nat.stream(items, None)
+    next(g)
+    g.close()
+    assert nat._native.n_active() == 0 and nat._native.n_templates() == 0
+    assert dict(nat.stream(items[:3], None)) == {k: v for k, v in a.items() if k < 3}

@@ -158,6 +158,7 @@ def _enrich_local(pool, args, ctx, work, rank):
                 "phase2Ms": round(r.stats.get("analyze.phase2", 0.0), 1),
                 "decodeStepMs": round(1e3 * st.get("decode_s", 0) / steps, 3),
                 "hostMsPerStep": round(1e3 * st.get("host_s", 0) / steps, 3),
+                "launchMsPerStep": round(1e3 * st.get("launch_s", 0) / steps, 3),
                 "waitMsPerStep": round(1e3 * st.get("wait_s", 0) / steps, 3),
                 "rowsPerStep": round(st.get("decode_rows", 0) / steps, 1),
                 "prefillMsPerClass": round(1e3 * st.get("prefill_s", 0) / max(1, st.get("prefills", 0)), 3),

@@ -130,6 +130,8 @@ def main(argv=None) -> int:
             "prefill_s": round(st["prefill_s"], 3), "prefill_gpu_s": round(st.get("prefill_gpu_s", 0.0), 3),
             "prefill_batches": st["prefill_batches"],
             "decode_s": round(st["decode_s"], 3), "host_ms_per_step": round(1e3 * st["host_s"] / max(1, st["decode_steps"]), 3),
+            "launch_ms_per_step": round(1e3 * st.get("launch_s", 0) / max(1, st["decode_steps"]), 3),
+            "wait_ms_per_step": round(1e3 * st.get("wait_s", 0) / max(1, st["decode_steps"]), 3),
             "admit_min": eng.admit_min,
             "decode_steps": st["decode_steps"], "rows_per_step": round(st["decode_rows"] / max(1, st["decode_steps"]), 1),
             "elapsed_s": round(elapsed, 3), "classes": int(ok_all),

@@ -363,7 +363,8 @@ class LocalEngine:
         self.stats = {"prompt_tokens": 0, "generated_tokens": 0, "decode_steps": 0, "decode_rows": 0,
                       "prefills": 0, "prefill_batches": 0, "decode_s": 0.0, "prefill_s": 0.0, "prefix_tokens": 0,
                       "prefix_switches": 0, "unshared_prefills": 0,
-                      "prefix_s": 0.0, "host_s": 0.0, "wait_s": 0.0, "prefill_gpu_s": 0.0, "reply_parts": 0,
+                      "prefix_s": 0.0, "host_s": 0.0, "wait_s": 0.0, "launch_s": 0.0, "prefill_gpu_s": 0.0,
+                      "reply_parts": 0,
                       "split_classes": 0, "methods_dropped": 0, "type_corrections": 0, "choice_waits": 0}
         self._pf_events: List[tuple] = []  # (start, end) device events of the batched prefills
         self._lock = threading.Lock()
@@ -909,8 +910,12 @@ class LocalEngine:
                         active = [q for q in active if not q.done]
                     t4 = time.perf_counter()
                     self.stats["wait_s"] += t3 - t2
+                    self.stats["launch_s"] += t2 - t1
                     self.stats["host_s"] += (t1 - t0) + (t4 - t3) + (t2 - t1)
                     self.stats["decode_s"] += t4 - t0
+                    for k, v in nat.stats().items():  # (cheap) so a never-ending worker stream reports them
+                        self.stats[k] += v
+                    nat.reset_stats()
                     while finished:
                         s = finished.pop()
                         raw = self._finish(s, partials)

@@ -80,12 +80,31 @@ def main(argv=None) -> int:
     for _ in range(3):
         graphs.run(toks, slots, poss, mrows)[1].cpu()
     torch.cuda.synchronize()
-    # device time: back-to-back replays
+    # device time: back-to-back replays (and the host time inside each
+    # run() call: the CPU cost of packing + H2D + hipGraphLaunch)
     t0 = time.perf_counter()
+    cpu = 0.0
     for _ in range(a.iters):
+        c0 = time.perf_counter()
         graphs.run(toks, slots, poss, mrows)
+        cpu += time.perf_counter() - c0
     torch.cuda.synchronize()
     dev_ms = (time.perf_counter() - t0) / a.iters * 1e3
+    launch_ms = cpu / a.iters * 1e3
+    # the engine's pipelined loop: launch step k, then wait for step k-1's ids
+    host = [torch.zeros(n, dtype=torch.int32).pin_memory() for _ in range(2)]
+    prev = None
+    t0 = time.perf_counter()
+    for it in range(a.iters):
+        _, ids = graphs.run(toks, slots, poss, mrows)
+        host[it % 2].copy_(ids, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        if prev is not None:
+            prev.synchronize()
+        prev = ev
+    prev.synchronize()
+    pipe_ms = (time.perf_counter() - t0) / a.iters * 1e3
     # engine-like loop: wait for the ids and convert them every step
     t0 = time.perf_counter()
     for _ in range(a.iters):
@@ -98,6 +117,7 @@ def main(argv=None) -> int:
                       "prefix_splits": hip.prefix_mfma_splits(a.batch + a.extra, cfg.n_heads // cfg.n_kv_heads,
                                                               cfg.n_kv_heads),
                       "device_ms": round(dev_ms, 3), "loop_ms": round(loop_ms, 3),
+                      "launch_cpu_ms": round(launch_ms, 3), "pipelined_ms": round(pipe_ms, 3),
                       "host_gap_ms": round(loop_ms - dev_ms, 3),
                       "sol_ms_at_6p3TBps": round((kv_bytes + w_bytes) / 6.3e12 * 1e3, 3),
                       "weight_MB": round(w_bytes / 1e6, 1), "kv_MB": round(kv_bytes / 1e6, 1)}), flush=True)

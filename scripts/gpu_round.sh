@@ -49,6 +49,11 @@ for s in $STEPS; do
             head -30 "$OUT/kstats_llama.txt"
             [ $rc -eq 0 ] || exit $rc ;;
         prefill) run prefill 300 python scripts/bench_prefill.py --seqs 12 ;;
+        step_llama)
+            run step_llama533 300 python scripts/bench_step.py --preset llama3.2-1b-code --batch 512 --extra 21 \
+                --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 60
+            run step_llama268 300 python scripts/bench_step.py --preset llama3.2-1b-code --batch 256 --extra 12 \
+                --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 60 ;;
         step)
             run step320 300 python scripts/bench_step.py --batch 256 --extra 64 --kv-dtype fp8 --iters 100
             run step78 300 python scripts/bench_step.py --batch 64 --extra 14 --kv-dtype fp8 --iters 100 ;;

@@ -44,6 +44,7 @@ def main(argv=None) -> int:
                     help="free KV slots before a running batch admits new classes (0 = engine default, batch/16)")
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--max-new-tokens", type=int, default=4096, help="reply budget (LOCAL_LLM_MAX_NEW_TOKENS)")
+    ap.add_argument("--no-fork", action="store_true", help="methods decoded in sequence, not as branches")
     args = ap.parse_args(argv)
 
     import torch
@@ -69,7 +70,8 @@ def main(argv=None) -> int:
         tok = load_asset_tokenizer(cfg.tokenizer)
     eng = LocalEngine(model, use_graphs=not args.no_graphs, jump_forward=not args.no_jump,
                       shared_prefix=not args.no_shared_prefix, pipeline=not args.no_pipeline,
-                      admit_min=args.admit_min or None, tokenizer=tok, max_new_tokens=args.max_new_tokens)
+                      admit_min=args.admit_min or None, tokenizer=tok, max_new_tokens=args.max_new_tokens,
+                      fork_methods=not args.no_fork)
     para = ("The shop platform sells products to retail customers. Orders move from CART to PAID to "
             "SHIPPED; payments are captured through the payment gateway and refunds are issued by the "
             "back office. Inventory is reserved when an order is paid and released on cancellation.\n\n")
@@ -92,6 +94,8 @@ def main(argv=None) -> int:
     eng.generate([make(-1 - i) for i in range(args.warmup)], readme)
     for k in eng.stats:
         eng.stats[k] = 0
+    if eng.graphs is not None:
+        eng.graphs.timing = {k: 0.0 for k in eng.graphs.timing}
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -132,6 +136,9 @@ def main(argv=None) -> int:
             "decode_s": round(st["decode_s"], 3), "host_ms_per_step": round(1e3 * st["host_s"] / max(1, st["decode_steps"]), 3),
             "launch_ms_per_step": round(1e3 * st.get("launch_s", 0) / max(1, st["decode_steps"]), 3),
             "wait_ms_per_step": round(1e3 * st.get("wait_s", 0) / max(1, st["decode_steps"]), 3),
+            "graph_timing_ms_per_step": ({k: round(1e3 * v / max(1, st["decode_steps"]), 3)
+                                          for k, v in eng.graphs.timing.items()} if eng.graphs else None),
+            "forks": st.get("forks", 0), "fork_branches": st.get("fork_branches", 0),
             "admit_min": eng.admit_min,
             "decode_steps": st["decode_steps"], "rows_per_step": round(st["decode_rows"] / max(1, st["decode_steps"]), 1),
             "elapsed_s": round(elapsed, 3), "classes": int(ok_all),

@@ -55,6 +55,9 @@ class Config:
     # reply budget in tokens (the reference's claude.max-tokens analog): a
     # class whose reply does not fit is generated in several parts and merged
     local_llm_max_new_tokens: int = 4096
+    # decode each method of a class as its own sequence from the class head's
+    # KV (a class's latency: head + longest method, not all methods in a row)
+    local_llm_fork_methods: bool = True
     local_llm_devices: str = "all"
     # "process": one worker process per GPU, started before this process
     # touches HIP (the service default); "inline": engines in this process
@@ -123,6 +126,7 @@ class Config:
             "LOCAL_LLM_MODEL_PATH": "local_llm_model_path",
             "LOCAL_LLM_KV_DTYPE": "local_llm_kv_dtype",
             "LOCAL_LLM_MAX_NEW_TOKENS": "local_llm_max_new_tokens",
+            "LOCAL_LLM_FORK_METHODS": "local_llm_fork_methods",
             "LOCAL_LLM_DEVICES": "local_llm_devices",
             "LOCAL_LLM_WORKERS": "local_llm_workers",
             "LOCAL_LLM_MAX_BATCH": "local_llm_max_batch",

@@ -205,6 +205,46 @@ def plan_reply(names: Sequence[str], budget: int) -> Tuple[List[List[Segment]], 
     return parts, dropped
 
 
+def build_head(has_methods: bool, desc_len=(8, 96)) -> List[Segment]:
+    """The class-level part of a reply generated with method branches: the
+    description and the class-type choice, up to the opening of the methods
+    list (or the whole reply when there is no method)."""
+    return _merge([Segment(b'{"description": "'), Segment(None, *desc_len), Segment(b', "classTypeCorrection": '),
+                   Segment(choice=CHOICE_CLASS_TYPE, then=[[]] * len(CHOICES[CHOICE_CLASS_TYPE])),
+                   Segment(b', "methods": [' if has_methods else b', "methods": []}')])
+
+
+def build_branch(name: str, method_len=(6, 64), step_len=(4, 40), max_steps: int = 3) -> List[Segment]:
+    """One method's entry, decoded as its own sequence after the class head
+    (its first, empty segment stands for the prompt a branch never
+    prefills: it continues the head's KV)."""
+    body = [Segment(b'{"methodName": ' + json.dumps(name).encode() + b', "description": "'), Segment(None, *method_len),
+            Segment(b', "businessLogic": ["')] + _steps_chain(step_len, max_steps) + [Segment(b"}")]
+    return [Segment(b"")] + _merge(body)
+
+
+def plan_branches(names: Sequence[str], budget: int) -> Tuple[List[Segment], List[List[Segment]]]:
+    """(head, one branch per method) with string lengths and step counts
+    shrunk until head + all branches fit ``budget`` tokens (down to a floor:
+    no method is ever dropped -- past the floor the budget is exceeded)."""
+    names = list(dict.fromkeys(names))
+    plan = None
+    for scale, steps in ((1.0, 3), (0.75, 2), (0.5, 2), (0.35, 1), (0.25, 1)):
+        def L(lo, hi):
+            return (min(lo, max(2, int(hi * scale))), max(4, int(hi * scale)))
+        head = build_head(bool(names), L(8, 96))
+        branches = [build_branch(n, L(6, 64), L(4, 40), steps) for n in names]
+        plan = (head, branches)
+        if template_budget(head) + sum(template_budget(b) for b in branches) <= budget:
+            break
+    return plan
+
+
+def merge_branches(head: str, branches: Sequence[str]) -> str:
+    """The reply of a class decoded with method branches."""
+    return head + ", ".join(branches) + ("]}" if branches else "")
+
+
 def fit_template(inp: EnrichmentInput, capacity: int) -> List[Segment]:
     """The first part of :func:`plan_reply` (single-part callers)."""
     return plan_reply(inp.method_names, capacity)[0][0]
@@ -245,6 +285,8 @@ class _Seq:
     prefix_split: int = 0                # leading prompt tokens encoding the text before 'Source of'
     shared: bool = False                 # its prompt starts with the resident shared prefix (set at admission)
     h: int = -1                          # its state in the native grammar engine (-1: Python state)
+    branches: Optional[List[List[Segment]]] = None  # a class head: its method branches (forked when it finishes)
+    fork: Optional["_Fork"] = None       # a method branch: the fork it belongs to
 
     _free_budget: int = -1
 
@@ -253,8 +295,21 @@ class _Seq:
         """Sampled (non-forced) tokens the reply may take: ~its decode steps
         (of the reply as planned; computed once -- the admission order key)."""
         if self._free_budget < 0:
-            self._free_budget = template_budget([s for s in self.segs if s.forced is None])
+            self._free_budget = template_budget([s for s in self.segs if s.forced is None]) + max(
+                (template_budget([s for s in b if s.forced is None]) for b in self.branches or ()), default=0)
         return self._free_budget
+
+
+@dataclass
+class _Fork:
+    """A class head's method branches: each decodes in a slot holding the
+    head's KV [0, pos) -- the head's own, a copy, or a finished sibling's
+    (a branch writes only past ``pos``, so a sibling's slot is a valid start
+    for the next branch)."""
+    head: "_Seq"
+    pos: int
+    pending: Deque[Tuple[int, List[Segment]]]
+    holders: set = field(default_factory=set)   # slots of running branches
 
 
 from .feeds import IterFeed, QueueFeed  # noqa: E402,F401  (re-exported)
@@ -322,7 +377,8 @@ class LocalEngine:
     def __init__(self, model: LocalLM, use_graphs: bool = True, max_prompt_tokens: Optional[int] = None,
                  jump_forward: bool = True, shared_prefix: bool = True, pipeline: bool = True,
                  admit_min: Optional[int] = None, longest_first: bool = True, tokenizer=None,
-                 max_new_tokens: Optional[int] = None, native_grammar: Optional[bool] = None) -> None:
+                 max_new_tokens: Optional[int] = None, native_grammar: Optional[bool] = None,
+                 fork_methods: bool = True) -> None:
         self.model = model
         self.tok = tokenizer if tokenizer is not None else ByteTokenizer(model.cfg.vocab_size)
         self._tb = self.tok.token_bytes
@@ -338,6 +394,12 @@ class LocalEngine:
         # decode batch for a prefill, so fewer, larger prefills (one GEMM per
         # projection over all their tokens) cost less than one per freed slot
         self.admit_min = max(1, admit_min if admit_min is not None else model.cfg.max_batch // 16)
+        # method branches: once a class's head (description, class type) is
+        # written, each method is decoded as its own sequence from a copy of
+        # the head's KV -- a class's critical path is its head + its longest
+        # method instead of all its methods in a row (small projects are
+        # latency-bound: rows per step far below capacity)
+        self.fork_methods = fork_methods
         self.cfg: LMConfig = model.cfg
         # reply budget: the caller's max_new_tokens, within what the KV slot
         # leaves next to a useful prompt
@@ -365,7 +427,8 @@ class LocalEngine:
                       "prefix_switches": 0, "unshared_prefills": 0,
                       "prefix_s": 0.0, "host_s": 0.0, "wait_s": 0.0, "launch_s": 0.0, "prefill_gpu_s": 0.0,
                       "reply_parts": 0,
-                      "split_classes": 0, "methods_dropped": 0, "type_corrections": 0, "choice_waits": 0}
+                      "split_classes": 0, "methods_dropped": 0, "type_corrections": 0, "choice_waits": 0,
+                      "forks": 0, "fork_branches": 0, "fork_waits": 0}
         self._pf_events: List[tuple] = []  # (start, end) device events of the batched prefills
         self._lock = threading.Lock()
         self._frag_cache: Dict[bytes, List[int]] = {}      # forced text -> ids
@@ -601,7 +664,23 @@ class LocalEngine:
         return self._prompt(s, readme, budget)
 
     def _seqs_for(self, key: Any, inp: EnrichmentInput, readme: Optional[str]) -> List[_Seq]:
-        """The sequences of one class: one per reply part, sharing one prompt."""
+        """The sequences of one class: one per reply part, sharing one prompt --
+        or, with ``fork_methods``, its head (the branches follow its KV)."""
+        if self.fork_methods:
+            head, branches = plan_branches(inp.method_names, self.reply_budget)
+            q = _Seq(inp, key, self._encode_forced(head), part=0, n_parts=1 + len(branches))
+            q.branches = [self._encode_forced(b) for b in branches] if branches else None
+            self.stats["reply_parts"] += 1
+            if self._native is not None:
+                q.h = self._native.new_seq(self._native_template(q.segs))
+            try:
+                longest = max((template_budget(b) for b in branches), default=0)
+                q.prompt = self._prompt(q, readme, template_budget(head) + longest)
+            except BaseException:
+                if q.h >= 0:
+                    self._native.release(q.h)
+                raise
+            return [q]
         parts, dropped = plan_reply(inp.method_names, self.reply_budget)
         self.stats["methods_dropped"] += dropped
         self.stats["reply_parts"] += len(parts)
@@ -778,7 +857,40 @@ class LocalEngine:
         if any(r is None for r in got):
             return None
         del partials[s.index]
+        if self.fork_methods:
+            return merge_branches(got[0], got[1:])  # type: ignore[arg-type]
         return merge_parts(got)  # type: ignore[arg-type]
+
+    def _start_branches(self, st: "_Fork", slots: List[int], src: Optional[int]) -> List[_Seq]:
+        """Starts the next pending branches of ``st`` in ``slots`` -- with a copy
+        of the head's own KV from sibling slot ``src`` (None: the slots
+        already hold it: the head's, or a finished sibling's) -- admitted."""
+        head, pos = st.head, st.pos
+        kids = []
+        for slot in slots:
+            j, segs = st.pending.popleft()
+            q = _Seq(head.inp, head.index, segs, part=1 + j, n_parts=head.n_parts)
+            q.slot, q.pos, q.fork = slot, pos, st
+            q.shared, q.prompt, q.prefix_split = head.shared, head.prompt, head.prefix_split
+            kids.append(q)
+        if src is not None and kids:
+            self.model.fork_kv(src, [q.slot for q in kids], self.model.prefix_len if head.shared else 0, pos)
+        nat = self._native
+        for q in kids:
+            if nat is not None:
+                q.h = nat.new_seq(self._native_template(q.segs))
+                m = nat.admit(q.h, q.slot, q.pos, q.shared)
+                q.done = nat.is_done(q.h)
+                if not q.done:
+                    nat.activate(q.h)
+            else:
+                q.seg, q.forced_off = 1, 0
+                m = self._enter(q)
+            if m is not None and m >= 0:
+                raise RuntimeError("a method branch must start with forced text")
+            st.holders.add(q.slot)
+        self.stats["fork_branches"] += len(kids)
+        return kids
 
     # ------------------------------------------------------------ the loop
     def _session(self, feed, readme: Optional[str]):
@@ -808,6 +920,36 @@ class LocalEngine:
         step_no = -1                     # number of the last launched step
         finished: List[_Seq] = []
         inflight: Optional[dict] = None  # the batched prefill in flight
+        forks: List[_Fork] = []  # forks with branches still waiting for a slot
+        nat0 = self._native
+
+        def fill(st: _Fork) -> None:
+            """Pending branches of ``st`` into free slots (KV copied from a sibling)."""
+            k = min(len(st.pending), len(free_slots))
+            if k and st.holders:
+                active.extend(q for q in self._start_branches(st, [free_slots.pop() for _ in range(k)],
+                                                              next(iter(st.holders))) if not q.done)
+
+        def retire(q: _Seq) -> None:
+            """A finished sequence: its slot back -- or to a branch of its
+            class -- and its text to the result."""
+            st = q.fork
+            if q.branches:  # a head: branch 0 continues in its slot
+                st = _Fork(q, nat0.pos(q.h) if nat0 is not None else q.pos, deque(enumerate(q.branches)))
+                self.stats["forks"] += 1
+                active.extend(k for k in self._start_branches(st, [q.slot], None) if not k.done)
+                fill(st)
+                if st.pending:
+                    forks.append(st)
+            elif st is not None:  # a branch: a pending sibling takes its slot as it is
+                st.holders.discard(q.slot)
+                if st.pending:
+                    active.extend(k for k in self._start_branches(st, [q.slot], None) if not k.done)
+                else:
+                    free_slots.append(q.slot)
+            else:
+                free_slots.append(q.slot)
+            finished.append(q)
         try:
             while True:
                 # ---- refill the look-ahead (blocking only when idle)
@@ -825,6 +967,11 @@ class LocalEngine:
                     if feed.done:
                         break
                     continue
+                # ---- branches of finished heads first (their classes are
+                # further along than any class still to be admitted)
+                for st in forks:
+                    fill(st)
+                forks = [st for st in forks if st.pending]
                 # ---- admission: one batched prefill for all that fit, enqueued
                 # ahead of the running batch's next step
                 if inflight is None and pending and free_slots and (
@@ -861,12 +1008,14 @@ class LocalEngine:
                 if inflight is not None:
                     done = self._admit_finish(inflight, wait=not active)
                     if done is not None:
+                        active.extend(s for s in inflight["batch"] if not s.done)
                         for s in done:
-                            free_slots.append(s.slot)
+                            retire(s)
+                        while finished:
+                            s = finished.pop()
                             raw = self._finish(s, partials)
                             if raw is not None:
                                 yield s.index, raw
-                        active.extend(s for s in inflight["batch"] if not s.done)
                         inflight = None
                         continue  # admit the next batch before this step when slots allow
                 if not active:
@@ -903,11 +1052,10 @@ class LocalEngine:
                     if fin:
                         byh = {q.h: q for q in active}
                         for hh in fin:
-                            q = byh[hh]
-                            q.done = True
-                            finished.append(q)
-                            free_slots.append(q.slot)
+                            byh[hh].done = True
                         active = [q for q in active if not q.done]
+                        for hh in fin:
+                            retire(byh[hh])
                     t4 = time.perf_counter()
                     self.stats["wait_s"] += t3 - t2
                     self.stats["launch_s"] += t2 - t1
@@ -1015,14 +1163,10 @@ class LocalEngine:
                     self.stats["decode_steps"] += 1
                     self.stats["decode_rows"] += len(toks)
                     self.stats["generated_tokens"] += len(toks)
-                still = []
-                for s in active:
-                    if s.done:
-                        finished.append(s)
-                        free_slots.append(s.slot)
-                    else:
-                        still.append(s)
-                active = still
+                gone = [s for s in active if s.done]
+                active = [s for s in active if not s.done]
+                for s in gone:
+                    retire(s)
                 t4 = time.perf_counter()
                 self.stats["wait_s"] += t3 - t2
                 self.stats["host_s"] += (t1 - t0) + (t4 - t3) + (t2 - t1)

@@ -47,6 +47,7 @@ from __future__ import annotations
 import json
 import math
 import os
+import time
 from dataclasses import asdict, dataclass, field, replace
 from typing import Dict, List, Optional, Sequence
 
@@ -612,6 +613,21 @@ class LocalLM:
             self.v_cache[:, slot, :, :P].copy_(self.v_cache[:, self.prefix_slot, :, :P])
         return P
 
+    @torch.inference_mode()
+    def fork_kv(self, src: int, dsts: Sequence[int], start: int, end: int) -> None:
+        """Copies slot ``src``'s keys / values at positions [start, end) into
+        every slot of ``dsts`` (the method branches of a class continue from
+        its head's KV; positions before ``start`` are the shared prefix).
+        One indexed copy per cache, on the current stream."""
+        if end <= start or not dsts:
+            return
+        if not (0 <= src < self.num_slots) or any(not 0 <= d < self.num_slots for d in dsts) or \
+                not (0 <= start <= end <= self.cfg.max_seq):
+            raise ValueError(f"fork_kv: slot {src} -> {list(dsts)}, positions [{start}, {end})")
+        idx = torch.tensor(list(dsts), dtype=torch.long, device=self.device)
+        for cache in (self.k_cache, self.v_cache):
+            cache[:, idx, :, start:end] = cache[:, src, :, start:end].unsqueeze(1)
+
     def decode_select(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor,
                       masks: torch.Tensor, mask_idx: torch.Tensor) -> tuple:
         """:meth:`decode` + greedy selection under a per-row grammar mask
@@ -701,6 +717,7 @@ class DecodeGraphs:
         self.model = model
         self.masks = masks
         self.alt_token = int(alt_token)
+        self.timing = {"sync_s": 0.0, "replay_s": 0.0}  # host time inside run(): staging wait, H2D + launch
         self.buckets = sorted(b for b in buckets if b <= model.max_rows)
         if not self.buckets or self.buckets[-1] < model.max_rows:
             self.buckets.append(model.max_rows)
@@ -782,7 +799,9 @@ class DecodeGraphs:
         if b not in self.graphs:
             self._capture(b)
         g, inp, stage, st, logits, ids, copied = self.graphs[b]
+        t0 = time.perf_counter()
         copied.synchronize()
+        self.timing["sync_s"] += time.perf_counter() - t0
         st[:, :n] = rows[:, :n]
         return self._replay(b, n)
 
@@ -792,7 +811,9 @@ class DecodeGraphs:
             st[1, n:] = -1
             st[4, n:] = -1
             st[5, n:] = -1
+        t0 = time.perf_counter()
         inp.copy_(stage, non_blocking=True)
         copied.record()
         g.replay()
+        self.timing["replay_s"] += time.perf_counter() - t0
         return (logits[:n] if logits is not None else None), ids[:n]

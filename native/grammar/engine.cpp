@@ -172,6 +172,7 @@ class Engine {
     bool is_done(int h) const { return seqs_.at(h).done; }
     py::bytes out(int h) const { return py::bytes(seqs_.at(h).out); }
     int slot(int h) const { return seqs_.at(h).slot; }
+    int pos(int h) const { return seqs_.at(h).pos; }
 
     // one step's rows into buf [7, cap]; returns the row count
     int build(py::array_t<int32_t, py::array::c_style> buf, long long step_no) {
@@ -436,6 +437,7 @@ PYBIND11_MODULE(_grammar, m) {
         .def("is_done", &Engine::is_done)
         .def("out", &Engine::out)
         .def("slot", &Engine::slot)
+        .def("pos", &Engine::pos)
         .def("build", &Engine::build)
         .def("apply", &Engine::apply)
         .def("collect_done", &Engine::collect_done)

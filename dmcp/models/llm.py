@@ -434,11 +434,9 @@ class LocalLM:
         if n == 1 or not (self.use_prefill_kernel or self.device.type == "cpu"):
             return torch.stack([self.forward_tokens(torch.as_tensor(t, dtype=torch.int32), sl, st)
                                 for t, sl, st in reqs])
-        toks: List[int] = []
-        pos: List[int] = []
-        slots: List[int] = []
+        import numpy as np
         offsets = [0]
-        starts, seq_slots, shared = [], [], []
+        starts, seq_slots, shared, lens = [], [], [], []
         for t, sl, st in reqs:
             T = len(t)
             if T == 0:
@@ -449,16 +447,23 @@ class LocalLM:
                 self._slot_prefix.pop(sl, None)
             sh = self._slot_prefix.get(sl, 0)
             shared.append(sh if 0 < sh <= st else 0)
-            toks.extend(int(x) for x in t)
-            pos.extend(range(st, st + T))
-            slots.extend([sl] * T)
             offsets.append(offsets[-1] + T)
             starts.append(st)
             seq_slots.append(sl)
+            lens.append(T)
         if len(set(seq_slots)) != n:
             raise ValueError("prefill_batch: each sequence needs its own slot")
         dev = self.device
-        meta = torch.tensor([toks, pos, slots], dtype=torch.int32)
+        # [token, position, slot] per packed token, built in numpy (the Python
+        # lists of ~20k tokens per admission cost the host milliseconds)
+        Ttot = offsets[-1]
+        st_rep = np.repeat(np.asarray(starts, dtype=np.int32), lens)
+        base = np.repeat(np.asarray(offsets[:-1], dtype=np.int32), lens)
+        meta_np = np.empty((3, Ttot), dtype=np.int32)
+        meta_np[0] = np.concatenate([np.asarray(t, dtype=np.int32) for t, _, _ in reqs])
+        meta_np[1] = st_rep + (np.arange(Ttot, dtype=np.int32) - base)
+        meta_np[2] = np.repeat(np.asarray(seq_slots, dtype=np.int32), lens)
+        meta = torch.from_numpy(meta_np)
         if dev.type == "cuda":
             meta = meta.pin_memory()
         meta = meta.to(dev, non_blocking=True)
@@ -466,7 +471,6 @@ class LocalLM:
         x = ops.embedding(self.w["embed"], ids)
         resid = x.clone()
         h = ops.add_rmsnorm(x, self.w["l0.ln1"], c.eps)
-        Ttot = offsets[-1]
         for i in range(c.layers):
             kc, vc = self.k_cache[i], self.v_cache[i]
             qkv = F.linear(h, self.w[f"l{i}.wqkv"])

@@ -80,6 +80,10 @@ class LMConfig:
     max_batch: int = 256
     max_rows: int = 384             # token rows per batched decode/extend step (jump-forward)
     kv_dtype: str = "bf16"          # KV cache storage: "bf16" or "fp8" (e4m3, unit scale, half the bytes)
+    # batched-prefill projections: "bf16" (hipBLASLt) or "fp8" (MXFP8
+    # activations x per-row-scaled e4m3 weights on the MX matrix cores,
+    # csrc/pgemm.hip, epilogues fused); decode keeps the bf16 weights
+    prefill_dtype: str = "bf16"
     # the preset's tokenizer: "" = byte-level (dmcp.enrich.tokenizer.ByteTokenizer),
     # else an asset directory under dmcp/models/assets (tokenizer.json.gz)
     tokenizer: str = ""
@@ -213,6 +217,8 @@ class LocalLM:
             raise ValueError("n_heads must be a multiple of n_kv_heads")
         if cfg.kv_dtype not in ("bf16", "fp8"):
             raise ValueError(f"kv_dtype must be 'bf16' or 'fp8', got {cfg.kv_dtype!r}")
+        if cfg.prefill_dtype not in ("bf16", "fp8"):
+            raise ValueError(f"prefill_dtype must be 'bf16' or 'fp8', got {cfg.prefill_dtype!r}")
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = torch.bfloat16
@@ -266,6 +272,21 @@ class LocalLM:
         # 533-row step on hipBLASLt, profiles/kstats_llama_r4.txt)
         self.fused_head = self.device.type == "cuda" and ops.lm_head_supported(c.vocab_size, c.hidden)
         self.head_ws = ops.lm_head_workspace(c.vocab_size, self.device) if self.fused_head else None
+        # fp8 prefill: e4m3 copies of the four projections (per-row scales),
+        # quantised once; the batched prefill then runs on csrc/pgemm.hip
+        # (the CPU references take any dims the 32-element blocks divide)
+        self.prefill_fp8 = c.prefill_dtype == "fp8" and c.n_heads * c.head_dim == c.hidden and (
+            (self.use_prefill_kernel
+             and ops.pgemm_supported(c.hidden, c.n_heads, c.n_kv_heads, c.head_dim, c.intermediate))
+            or (self.device.type == "cpu" and c.hidden % 32 == 0 and c.intermediate % 32 == 0))
+        if c.prefill_dtype == "fp8" and not self.prefill_fp8:
+            raise ValueError(f"prefill_dtype fp8 needs head_dim 64, hidden % 2048 == 0 and a supported device "
+                             f"({c.name}: hidden {c.hidden}, head_dim {c.head_dim}, {self.device})")
+        self.w8: Dict[str, tuple] = {}
+        if self.prefill_fp8:
+            for i in range(c.layers):
+                for n in ("wqkv", "wo", "wgu", "wdown"):
+                    self.w8[f"l{i}.{n}"] = ops.quantize_weight(self.w[f"l{i}.{n}"])
 
     KV_HEADROOM = 4 << 30  # bytes left free next to the slab (graphs, workspaces, prefill activations)
 
@@ -431,7 +452,7 @@ class LocalLM:
         n = len(reqs)
         if n == 0:
             raise ValueError("prefill_batch needs at least one sequence")
-        if n == 1 or not (self.use_prefill_kernel or self.device.type == "cpu"):
+        if not self.prefill_fp8 and (n == 1 or not (self.use_prefill_kernel or self.device.type == "cpu")):
             return torch.stack([self.forward_tokens(torch.as_tensor(t, dtype=torch.int32), sl, st)
                                 for t, sl, st in reqs])
         import numpy as np
@@ -468,6 +489,14 @@ class LocalLM:
             meta = meta.pin_memory()
         meta = meta.to(dev, non_blocking=True)
         ids, pos_t, slot_t = meta[0], meta[1], meta[2]
+        last = torch.tensor([o_ - 1 for o_ in offsets[1:]], dtype=torch.long)
+        if dev.type == "cuda":  # pinned + async: a pageable copy would block the host until the stream drains
+            last = last.pin_memory()
+        last = last.to(dev, non_blocking=True)
+        prefix = self.prefix_slot if any(shared) else None
+        if self.prefill_fp8:
+            h = self._prefill_fp8(ids, pos_t, slot_t, offsets, seq_slots, starts, prefix, shared, last)
+            return F.linear(h, self.w["lm_head"])
         x = ops.embedding(self.w["embed"], ids)
         resid = x.clone()
         h = ops.add_rmsnorm(x, self.w["l0.ln1"], c.eps)
@@ -475,18 +504,38 @@ class LocalLM:
             kc, vc = self.k_cache[i], self.v_cache[i]
             qkv = F.linear(h, self.w[f"l{i}.wqkv"])
             q = ops.rope_kv(qkv, pos_t, slot_t, self.cos_sin, kc, vc, c.n_heads)  # [Ttot, Hq, D]
-            att = ops.prefill_attention_varlen(q, kc, vc, offsets, seq_slots, starts,
-                                               self.prefix_slot if any(shared) else None, shared, self.scale)
+            att = ops.prefill_attention_varlen(q, kc, vc, offsets, seq_slots, starts, prefix, shared, self.scale)
             o = F.linear(att.view(Ttot, c.n_heads * c.head_dim), self.w[f"l{i}.wo"])
             h = ops.add_rmsnorm(o, self.w[f"l{i}.ln2"], c.eps, residual=resid)
             m = self._mlp(i, h)
             nxt = self.w[f"l{i + 1}.ln1"] if i + 1 < c.layers else self.w["norm_f"]
             h = ops.add_rmsnorm(m, nxt, c.eps, residual=resid)
-        last = torch.tensor([o_ - 1 for o_ in offsets[1:]], dtype=torch.long)
-        if dev.type == "cuda":  # pinned + async: a pageable copy would block the host until the stream drains
-            last = last.pin_memory()
-        last = last.to(dev, non_blocking=True)
         return F.linear(h.index_select(0, last), self.w["lm_head"])
+
+    def _prefill_fp8(self, ids, pos_t, slot_t, offsets, seq_slots, starts, prefix, shared, last) -> torch.Tensor:
+        """The layers of :meth:`prefill_batch` on the MXFP8 kernels: the
+        activation entering each projection is MXFP8 (written by the RMSNorm
+        before it, by the SwiGLU epilogue of gate/up, or quantised from the
+        attention output), QKV's epilogue applies RoPE and appends K/V, O's and
+        down's add into the residual stream.  Returns the final normalised
+        hidden rows of ``last`` [n, hidden]."""
+        c = self.cfg
+        T = ids.numel()
+        resid = ops.embedding(self.w["embed"], ids)
+        aq, as_ = ops.rmsnorm_mx(resid, self.w["l0.ln1"], c.eps)
+        act = None
+        for i in range(c.layers):
+            kc, vc = self.k_cache[i], self.v_cache[i]
+            q = ops.pgemm_qkv(aq, as_, *self.w8[f"l{i}.wqkv"], pos_t, slot_t, self.cos_sin, kc, vc, c.n_heads)
+            att = ops.prefill_attention_varlen(q, kc, vc, offsets, seq_slots, starts, prefix, shared, self.scale)
+            ops.mx_quant(att.view(T, c.hidden), aq, as_)
+            ops.pgemm_resid(aq, as_, *self.w8[f"l{i}.wo"], resid)
+            ops.rmsnorm_mx(resid, self.w[f"l{i}.ln2"], c.eps, q=aq, s=as_)
+            act = ops.pgemm_swiglu(aq, as_, *self.w8[f"l{i}.wgu"], *(act or (None, None)))
+            ops.pgemm_resid(act[0], act[1], *self.w8[f"l{i}.wdown"], resid)
+            if i + 1 < c.layers:
+                ops.rmsnorm_mx(resid, self.w[f"l{i + 1}.ln1"], c.eps, q=aq, s=as_)
+        return ops.add_rmsnorm(resid.index_select(0, last), self.w["norm_f"], c.eps)
 
     @torch.inference_mode()
     def decode(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor,

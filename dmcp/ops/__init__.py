@@ -16,7 +16,8 @@ from . import hip, reference
 from .hip import (FUSED_MAX_ROWS, PREFIX_MFMA_MAX_SPLITS, WGEMM_MAX_ROWS, decode_workspace,  # noqa: F401
                   fused_linear_norm, fused_rope_kv, fused_swiglu, lm_head_supported, lm_head_workspace,
                   prefill_supported, wgemm_resid_norm, wgemm_rope_kv, wgemm_swiglu, wgemm_workspace)
-from .reference import SharedPrefix, rope_tables  # noqa: F401
+from .hip import PGEMM_TILE_N, pgemm_supported  # noqa: F401
+from .reference import SharedPrefix, mx_dequant, quantize_weight, rope_tables, weight_dequant  # noqa: F401
 
 
 def _on(t):
@@ -92,3 +93,28 @@ def decode_plan(rows, n_kv_heads, max_seq, kv_dtype: str = "bf16"):
     -> 2.30 ms at 78 rows, 5.54 -> 5.36 at 320; bf16 2.84 vs 2.94 the other
     way -- profiles/decode_target_waves_r2.txt)."""
     return hip.decode_plan(rows, n_kv_heads, max_seq, target_waves=2048 if kv_dtype == "fp8" else 4096)
+
+
+# MXFP8 prefill path (csrc/pgemm.hip); CPU tensors run the fp32 references
+def mx_quant(x, q=None, s=None):
+    return _on(x).mx_quant(x, q, s)
+
+
+def rmsnorm_mx(resid, weight, eps, add=None, q=None, s=None):
+    return _on(resid).rmsnorm_mx(resid, weight, eps, add, q, s)
+
+
+def pgemm(aq, as_, wq, ws, out=None):
+    return _on(aq).pgemm(aq, as_, wq, ws, out)
+
+
+def pgemm_resid(aq, as_, wq, ws, resid):
+    return _on(aq).pgemm_resid(aq, as_, wq, ws, resid)
+
+
+def pgemm_swiglu(aq, as_, wq, ws, q=None, s=None):
+    return _on(aq).pgemm_swiglu(aq, as_, wq, ws, q, s)
+
+
+def pgemm_qkv(aq, as_, wq, ws, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out=None):
+    return _on(aq).pgemm_qkv(aq, as_, wq, ws, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out)

@@ -15,17 +15,23 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 SRCS = [os.path.join(CSRC, "dmcp_kernels.hip"), os.path.join(CSRC, "fused_gemm.hip"),
-        os.path.join(CSRC, "prefill_attn.hip"), os.path.join(CSRC, "wgemm.hip")]
+        os.path.join(CSRC, "prefill_attn.hip"), os.path.join(CSRC, "wgemm.hip"), os.path.join(CSRC, "pgemm.hip")]
 HEADERS = [os.path.join(CSRC, "dmcp_common.hpp")]
 SRC = SRCS[0]  # kept for callers that name the main source
 TARGET = os.path.join(HERE, "_hipops.so")
 STAMP = TARGET + ".stamp"
 ARCH = os.environ.get("DMCP_HIP_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-Wall",
-         "-Wno-unused-function", "-munsafe-fp-atomics",
-         # MFMA accumulators in VGPRs: the prefix-attention softmax works on the
-         # score tile in place (AGPR form cost ~90 v_accvgpr moves per 32-key tile)
-         "-mllvm", "-amdgpu-mfma-vgpr-form=1"]
+FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno-unused-function",
+         "-munsafe-fp-atomics"]
+# MFMA accumulators in VGPRs: the prefix-attention softmax works on the score
+# tile in place (AGPR form cost ~90 v_accvgpr moves per 32-key tile).  Not for
+# pgemm.hip: its 256 accumulator registers per lane must live in the AGPR half.
+VGPR_FORM = ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
+PER_FILE = {"pgemm.hip": []}
+
+
+def _flags(src: str) -> list:
+    return FLAGS + PER_FILE.get(os.path.basename(src), VGPR_FORM)
 
 
 def hipcc() -> str:
@@ -36,22 +42,36 @@ def hipcc() -> str:
 
 
 def _key() -> str:
-    h = hashlib.sha256(" ".join(FLAGS).encode())
+    h = hashlib.sha256(" ".join(FLAGS + VGPR_FORM + sorted(f"{k}={v}" for k, v in PER_FILE.items())).encode())
     for path in SRCS + HEADERS:
         with open(path, "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:16]
 
 
-def build(force: bool = False) -> str:
+def build(force: bool = False, jobs: int = 0) -> str:
+    """One object per source (own flags), compiled in parallel, then linked."""
     key = _key()
     if not force and os.path.exists(TARGET) and os.path.exists(STAMP) and open(STAMP).read().strip() == key:
         return TARGET
-    tmp = TARGET + ".tmp"
-    cmd = [hipcc(), *FLAGS, f"-I{CSRC}", "-o", tmp, *SRCS]
-    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stdout}")
+    import concurrent.futures
+    import tempfile
+    with tempfile.TemporaryDirectory(prefix="dmcp_hip_") as tmpdir:
+        def compile_one(src):
+            obj = os.path.join(tmpdir, os.path.basename(src) + ".o")
+            r = subprocess.run([hipcc(), *_flags(src), f"-I{CSRC}", "-c", "-o", obj, src],
+                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"hipcc failed on {os.path.basename(src)} ({r.returncode}):\n{r.stdout}")
+            return obj
+        n = jobs or min(len(SRCS), os.cpu_count() or 1, 8)
+        with concurrent.futures.ThreadPoolExecutor(max_workers=n) as ex:
+            objs = list(ex.map(compile_one, SRCS))
+        tmp = TARGET + ".tmp"
+        r = subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs],
+                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc link failed ({r.returncode}):\n{r.stdout}")
     os.replace(tmp, TARGET)
     with open(STAMP, "w") as f:
         f.write(key)

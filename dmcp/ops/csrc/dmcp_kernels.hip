@@ -849,7 +849,7 @@ hipError_t launch_combine(void* part_o, void* part_ml, const int32_t* sl, const 
 
 extern "C" {
 
-int dmcp_abi_version() { return 12; }
+int dmcp_abi_version() { return 13; }
 
 int dmcp_add_rmsnorm(const void* x, void* residual, const void* w, void* out, int rows, int H, float eps,
                      void* stream) {

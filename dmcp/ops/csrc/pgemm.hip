@@ -1,0 +1,556 @@
+// Prefill GEMMs on the MX-scaled fp8 matrix cores (gfx950 / MI355X, CDNA4):
+//
+//   Y[M, N] = (Aq[M, K] * 2^(As - 127)) . (Wq[N, K] * ws[N])^T      M in the thousands
+//
+// The batched prefill (dmcp.models.llm.LocalLM.prefill_batch: ~45 classes x
+// ~560 own prompt tokens per admission, M ~ 25k rows) is compute-bound: its
+// four projections per layer are ~93 % of its FLOPs.  hipBLASLt's bf16 GEMMs
+// ran it at ~1.2 PFLOP/s; v_mfma_scale_f32_32x32x64_f8f6f4 with e4m3 operands
+// retires twice the bf16 rate (MI355X_MICROARCH.md, matrix cores), and half
+// the operand bytes per FLOP.  The operands:
+//
+//   * A (activations): MXFP8 -- e4m3 bytes with one power-of-two (E8M0) scale
+//     per 32 consecutive K elements of a row.  The scale is an MFMA operand
+//     (each lane's 32 k values ARE one scale block), so an activation needs
+//     no whole-row statistics: the SwiGLU epilogue of the gate/up GEMM
+//     quantises its own output tile (a row's 32 columns are the 32 lanes of a
+//     half-wave) and the down projection consumes it directly;
+//   * B (weights): e4m3 with one fp32 scale per output channel (quantised
+//     once at load), applied in the epilogue; the MFMA's B scale is 1.
+//
+// Structure: 256 x 256 output tile per 256-thread block (one wave per SIMD),
+// 4 waves as 2 (M) x 2 (N), each wave 4 x 4 tiles of 32 x 32 (256 accumulator
+// registers).  At MX-fp8 rate the LDS is the tight resource: every k-step's
+// fragment reads (16 KiB per wave) plus the DMA writes (32 KiB per block) must
+// fit in the MFMA time -- 128 x 128 per wave reads 64 KiB per 64 k per block
+// where 8 waves of 128 x 64 read 96 KiB (measured 1.2-1.8 PFLOP/s with 8
+// waves, LDS-bound).  64-deep
+// K stages (one MX MFMA k-step) staged by LDS-DMA (global_load_lds) into a
+// 4-stage ring, 3 stages in flight, one counted vmcnt + raw s_barrier per
+// stage (cdna_hip_programming.md §5, "Pipelining across barriers");
+// [rows][4 x 16 B] LDS images with chunk j of row r in slot j ^ ((r >> 2) & 3)
+// (the swizzle on the DMA's source address): the 16 lanes of a ds_read_b128
+// pass cover all 64 banks.  The A scales of a stage ride the same ring
+// (a 2-byte LDS-DMA per lane), so the loop issues only one kind of load.
+// Blocks are remapped so each XCD runs a contiguous range of tiles, grouped 8
+// M tiles at a time (its 32 CUs share 8 A panels and 4 W tiles in L2).
+//
+// Fused epilogues (the accumulator lane holds column lane & 31 of 16 rows):
+//   PM_BF16    y = bf16(acc * ws[n])
+//   PM_RESID   resid += bf16(acc * ws[n])          (o / down projection)
+//   PM_SWIGLU  act = silu(gate) * up -> MXFP8 act + E8M0 scales (gate / up
+//              rows of the same 32 intermediate columns in one wave)
+//   PM_QKV     RoPE on q / k (d and d + 32 of a 64-wide head in the same
+//              lane), q written bf16, k / v appended to the KV cache
+//              (bf16 or fp8) -- the rope_kv kernel folded in.
+#include "dmcp_common.hpp"
+
+namespace {
+
+typedef int v8i_t __attribute__((ext_vector_type(8)));
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+
+constexpr int PBM = 256, PBN = 256, PBK = 64, PST = 4, PTH = 256;
+constexpr int PA_BYTES = PBM * PBK;                     // A image of a stage
+constexpr int PB_BYTES = PBN * PBK;                     // W image
+constexpr int PS_BYTES = PBM * 2;                       // A scales of the stage: [row][2 blocks]
+constexpr int PST_BYTES = PA_BYTES + PB_BYTES + PS_BYTES;
+constexpr int PGL = 9;                                  // LDS-DMA instructions per wave per stage
+constexpr int PM_BF16 = 0, PM_RESID = 1, PM_SWIGLU = 2, PM_QKV = 3;
+constexpr int PEPI_ROW = 256;  // epilogue image row: 128 bf16, 16-B chunk j of row r at slot j ^ (r & 15)
+
+struct PEpi {
+    uint16_t* y;          // PM_BF16: out [M, N]; PM_RESID: resid [M, N] (in place)
+    uint8_t* yq;          // PM_SWIGLU: act [M, I] e4m3
+    uint8_t* ys;          // PM_SWIGLU: act scales [M, I / 32] E8M0
+    int I;                // PM_SWIGLU: intermediate size (gate rows [0, I), up rows [I, 2I))
+    // PM_QKV
+    const int32_t* pos;
+    const int32_t* slot;
+    const float2* cos_sin;
+    uint16_t* q_out;
+    void* k_cache;
+    void* v_cache;
+    int Hq, Hkv, max_seq, max_pos, num_slots;
+};
+
+// LDS-DMA of 16 / 2 bytes per lane (the size must be a literal)
+template <int SIZE>
+__device__ __forceinline__ void pglds(const void* src, void* lds_base) {
+    auto g = (const __attribute__((address_space(1))) void*)src;
+    auto l = (__attribute__((address_space(3))) void*)lds_base;
+    if constexpr (SIZE == 16) __builtin_amdgcn_global_load_lds(g, l, 16, 0, 0);
+    else __builtin_amdgcn_global_load_lds(g, l, 2, 0, 0);
+}
+
+__device__ __forceinline__ float psilu(float g) { return g / (1.f + __expf(-g)); }
+
+// E8M0 exponent of a 32-element block of max |x| = amax: the smallest e with
+// amax / 2^e <= 448 (e4m3's largest normal), clamped to the format
+__device__ __forceinline__ int mx_exp(float amax) {
+    if (!(amax > 0.f)) return 0;
+    int e;
+    frexpf(amax * (1.f / 448.f), &e);  // amax / 448 = f * 2^e, f in [0.5, 1)
+    return e < -127 ? -127 : (e > 127 ? 127 : e);
+}
+
+// one byte of e4m3 (saturating)
+__device__ __forceinline__ uint8_t to_fp8(float x) {
+    return (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(fp8_sat(x), 0.f, 0, false) & 0xffu);
+}
+
+// The operand layout of v_mfma_scale_f32_32x32x64_f8f6f4 with 8-bit
+// operands (measured, scripts/mx_layout_probe.py): lane (r, h) = (l % 32,
+// l / 32) holds row r (A) / column r (B); its bytes 0-15 are k 16 h .. 16 h
+// + 15 and bytes 16-31 are k 32 + 16 h .. 32 + 16 h + 15; the E8M0 scale of
+// lane (r, 0) scales the row's k block 0-31, that of lane (r, 1) block 32-63.
+// In a stage row of 64 k bytes = 4 16-B chunks: lane half h reads chunks h
+// and 2 + h, and the scale of block h.
+template <int MODE, bool KV8>
+__global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) void pgemm_kernel(
+    const uint8_t* __restrict__ aq, const uint8_t* __restrict__ as, const uint8_t* __restrict__ wq,
+    const float* __restrict__ ws, int M, int N, int K, int mtiles, int ntiles, PEpi e) {
+    __shared__ __attribute__((aligned(16))) uint8_t plds[PST * PST_BYTES];  // ONE LDS object (ring, then epilogue)
+
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(tid / kWave);
+    const int wm = wv >> 1, wn = wv & 1;
+    const int l32 = lane & 31, hh = lane >> 5;
+
+    // block -> tile: XCD-contiguous ranges (bijective for any grid), then
+    // 8 M tiles per group with N fastest inside the group's column
+    const int nblk = mtiles * ntiles;
+    const int b = blockIdx.x;
+    const int xcd = b & 7, q8 = nblk >> 3, r8 = nblk & 7;
+    const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+    const int per_group = 8 * ntiles;
+    const int gid = L / per_group;
+    const int first = gid * 8;
+    const int gsz = min(mtiles - first, 8);
+    const int inn = L - gid * per_group;
+    const int mt = first + inn % gsz, nt = inn / gsz;
+    const int m0 = mt * PBM;
+
+    // weight row of LDS image row r (SwiGLU: per wave 64 gate rows then the
+    // 64 up rows of the same intermediate columns)
+    auto wrow = [&](int r) -> int {
+        if constexpr (MODE == PM_SWIGLU) {
+            const int w2 = r >> 7, t = (r >> 6) & 1, i = r & 63;
+            return (t ? e.I : 0) + nt * 128 + w2 * 64 + i;
+        } else {
+            return nt * PBN + r;
+        }
+    };
+
+    // LDS-DMA sources: lane L of a 1-KiB piece fills image row base + L / 4,
+    // slot L % 4 with logical 16-B chunk (L % 4) ^ ((row >> 2) & 3)
+    const uint8_t* asrc[4];
+    const uint8_t* wsrc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = (wv * 4 + i) * 16 + (lane >> 2);
+        const int ch = (lane & 3) ^ ((r >> 2) & 3);
+        asrc[i] = aq + (size_t)min(m0 + r, M - 1) * K + ch * 16;
+        wsrc[i] = wq + (size_t)wrow(r) * K + ch * 16;
+    }
+    // A scales: lane L of wave w fetches the stage's 2 bytes of row 64 w + L
+    const int ksb = K >> 5;
+    const uint8_t* ssrc = as + (size_t)min(m0 + wv * 64 + lane, M - 1) * ksb;
+
+    auto issue = [&](int c, int st) {
+        uint8_t* base = plds + st * PST_BYTES;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pglds<16>(asrc[i] + c * PBK, base + (wv * 4 + i) * 1024);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pglds<16>(wsrc[i] + c * PBK, base + PA_BYTES + (wv * 4 + i) * 1024);
+        pglds<2>(ssrc + c * 2, base + PA_BYTES + PB_BYTES + wv * 128);
+    };
+
+    f32x16_t acc[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[t][u][i] = 0.f;
+
+    // typed vector loads: they keep their TBAA tag, which is what lets the
+    // waitcnt pass tell them from the LDS-DMA writes in flight (an untyped
+    // LDS load -- e.g. a uint4 copied field by field -- gets a vmcnt(0) in
+    // front of it, draining the ring every stage)
+    auto frag = [&](const uint8_t* img, int r) -> v8i_t {
+        const int sw = (r >> 2) & 3;
+        const v4i_t lo = *reinterpret_cast<const v4i_t*>(img + r * PBK + (hh ^ sw) * 16);
+        const v4i_t hi = *reinterpret_cast<const v4i_t*>(img + r * PBK + ((2 + hh) ^ sw) * 16);
+        return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    };
+
+    auto compute = [&](int st) {
+        const uint8_t* A = plds + st * PST_BYTES;
+        const uint8_t* B = A + PA_BYTES;
+        const uint8_t* S = B + PB_BYTES;
+        v8i_t bf[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) bf[u] = frag(B, wn * 128 + u * 32 + l32);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int r = wm * 128 + t * 32 + l32;
+            const v8i_t af = frag(A, r);
+            const int sa = S[r * 2 + hh];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af, bf[u], acc[t][u], 0, 0, 0, sa, 0,
+                                                                            127);
+        }
+    };
+
+    const int chunks = K / PBK;
+#pragma unroll
+    for (int j = 0; j < PST - 1; ++j)
+        if (j < chunks) issue(j, j);
+    for (int c = 0; c < chunks; ++c) {
+        if (c + PST - 2 < chunks) {
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(PGL * (PST - 2)) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+        if (c + PST - 1 < chunks) issue(c + PST - 1, (c + PST - 1) % PST);
+        compute(c % PST);
+    }
+    __syncthreads();  // the ring is free: the epilogue stages this wave's tile in it
+
+    // ---- epilogue.  Lane (l32, hh) holds column l32 of rows (i & 3) + 8 (i >> 2)
+    // + 4 hh of each 32 x 32 tile.  The wave's 128 x 128 tile goes through LDS
+    // (128 rows x 256 B + pad) so the global stores are 16-B per lane along rows.
+    uint8_t* img = plds + wv * (128 * PEPI_ROW);
+    static_assert(PTH / kWave * 128 * PEPI_ROW <= PST * PST_BYTES, "epilogue images fit the ring");
+    // byte b of image row r (swizzled: the 2-byte column writes of rows r and
+    // r + 4 and the 16-B row reads all spread over the banks)
+    auto ea = [&](int r, int byte) -> uint8_t* {
+        return img + r * PEPI_ROW + ((((byte >> 4) ^ (r & 15)) << 4) | (byte & 15));
+    };
+    const int mw = m0 + wm * 128;  // first row of this wave's tile
+    if constexpr (MODE == PM_BF16 || MODE == PM_RESID) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float sc = ws[nt * PBN + wn * 128 + u * 32 + l32];
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int rr = t * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+                    *reinterpret_cast<uint16_t*>(ea(rr, (u * 32 + l32) * 2)) = f2bf(acc[t][u][i] * sc);
+                }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+        __builtin_amdgcn_wave_barrier();
+        const int n0 = nt * PBN + wn * 128;
+        // 16 lanes per row (8 bf16 each), 4 rows per pass
+#pragma unroll 4
+        for (int p = 0; p < 32; ++p) {
+            const int rr = p * 4 + (lane >> 4);
+            const int m = mw + rr;
+            if (m >= M) continue;
+            const uint4 v = *reinterpret_cast<const uint4*>(ea(rr, (lane & 15) * 16));
+            uint4* dst = reinterpret_cast<uint4*>(e.y + (size_t)m * N + n0 + (lane & 15) * 8);
+            if constexpr (MODE == PM_RESID) {
+                float a[8], r[8];
+                unpack8(v, a);
+                unpack8(*dst, r);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) a[j] += r[j];
+                *dst = pack8(a);
+            } else {
+                *dst = v;
+            }
+        }
+    } else if constexpr (MODE == PM_SWIGLU) {
+        // tiles u = 0, 1 are gate columns j0 .. j0 + 63, u = 2, 3 the up columns
+        const int j0 = nt * 128 + wn * 64;
+        const int isb = e.I >> 5;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int j = j0 + u * 32 + l32;
+            const float sg = ws[j], su = ws[e.I + j];
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int rr = t * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+                    // gate / up rounded to bf16 as the bf16 GEMM's outputs are
+                    const float g = bf2f(f2bf(acc[t][u][i] * sg)), uu = bf2f(f2bf(acc[t][u + 2][i] * su));
+                    const float a = psilu(g) * uu;
+                    float amax = __builtin_fabsf(a);
+#pragma unroll
+                    for (int msk = 1; msk < 32; msk <<= 1)
+                        amax = __builtin_fmaxf(amax, __shfl_xor(amax, msk, kWave));
+                    const int ex = mx_exp(amax);
+                    *ea(rr, u * 32 + l32) = to_fp8(ldexpf(a, -ex));
+                    const int m = mw + rr;
+                    if (l32 == 0 && m < M) e.ys[(size_t)m * isb + (j >> 5)] = (uint8_t)(ex + 127);
+                }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        // 4 lanes per row (16 B each), 16 rows per pass
+#pragma unroll 2
+        for (int p = 0; p < 8; ++p) {
+            const int rr = p * 16 + (lane >> 2);
+            const int m = mw + rr;
+            if (m >= M) continue;
+            *reinterpret_cast<uint4*>(e.yq + (size_t)m * e.I + j0 + (lane & 3) * 16) =
+                *reinterpret_cast<const uint4*>(ea(rr, (lane & 3) * 16));
+        }
+    } else {  // PM_QKV: the wave's 128 columns are two heads; tiles 2 g, 2 g + 1 = d 0..31, 32..63 of head g
+        const int h0 = (nt * PBN + wn * 128) >> 6;
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const int n = nt * PBN + wn * 128 + g * 64 + l32;
+            const float s1 = ws[n], s2 = ws[n + 32];
+            const bool rope = h0 + g < e.Hq + e.Hkv;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int rr = t * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+                    const int m = min(mw + rr, M - 1);
+                    const float x1 = bf2f(f2bf(acc[t][2 * g][i] * s1)), x2 = bf2f(f2bf(acc[t][2 * g + 1][i] * s2));
+                    float o1 = x1, o2 = x2;
+                    if (rope) {
+                        const int p = e.pos[m];
+                        const float2 cs = e.cos_sin[(size_t)min(max(p, 0), e.max_pos - 1) * 32 + l32];
+                        o1 = x1 * cs.x - x2 * cs.y;
+                        o2 = x2 * cs.x + x1 * cs.y;
+                    }
+                    *reinterpret_cast<uint16_t*>(ea(rr, g * 128 + l32 * 2)) = f2bf(o1);
+                    *reinterpret_cast<uint16_t*>(ea(rr, g * 128 + 64 + l32 * 2)) = f2bf(o2);
+                }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        // per (row, head): 128 B of bf16 = 8 lanes x 16 B; 4 (row, head) pairs per pass
+#pragma unroll 4
+        for (int p = 0; p < 64; ++p) {
+            const int unit = p * 8 + (lane >> 3);  // (row, head) pair
+            const int rr = unit >> 1, g = unit & 1;
+            const int m = mw + rr;
+            if (m >= M) continue;
+            const int head = h0 + g;
+            const uint4 v = *reinterpret_cast<const uint4*>(ea(rr, g * 128 + (lane & 7) * 16));
+            if (head < e.Hq) {
+                *reinterpret_cast<uint4*>(e.q_out + ((size_t)m * e.Hq + head) * 64 + (lane & 7) * 8) = v;
+                continue;
+            }
+            const int pp = e.pos[m], sl = e.slot[m];
+            if (pp < 0 || pp >= e.max_seq || sl < 0 || sl >= e.num_slots) continue;
+            const bool isv = head >= e.Hq + e.Hkv;
+            const int kh = head - e.Hq - (isv ? e.Hkv : 0);
+            const size_t ofs = (((size_t)sl * e.Hkv + kh) * e.max_seq + pp) * 64 + (lane & 7) * 8;
+            void* cache = isv ? e.v_cache : e.k_cache;
+            if constexpr (KV8)
+                *reinterpret_cast<uint2*>(static_cast<uint8_t*>(cache) + ofs) = bf16x8_to_fp8x8(v);
+            else
+                *reinterpret_cast<uint4*>(static_cast<uint16_t*>(cache) + ofs) = v;
+        }
+    }
+}
+
+// MXFP8 quantisation of bf16 rows: q[M, K] e4m3, s[M, K / 32] E8M0 (4 lanes
+// per 32-block, 8 elements per lane)
+__global__ __launch_bounds__(kBlock) void mx_quant_kernel(const uint16_t* __restrict__ x, uint8_t* __restrict__ q,
+                                                          uint8_t* __restrict__ s, long n8) {
+    for (long v = (long)blockIdx.x * kBlock + threadIdx.x; v < n8; v += (long)gridDim.x * kBlock) {
+        float f[8];
+        unpack8(reinterpret_cast<const uint4*>(x)[v], f);
+        float amax = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) amax = __builtin_fmaxf(amax, __builtin_fabsf(f[j]));
+        amax = __builtin_fmaxf(amax, __shfl_xor(amax, 1, kWave));
+        amax = __builtin_fmaxf(amax, __shfl_xor(amax, 2, kWave));
+        const int ex = mx_exp(amax);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = ldexpf(f[j], -ex);
+        reinterpret_cast<uint2*>(q)[v] = make_uint2(pack_fp8x4(f), pack_fp8x4(f + 4));
+        if ((v & 3) == 0) s[v >> 2] = (uint8_t)(ex + 127);
+    }
+}
+
+// resid += add (bf16, when add != null); h = RMSNorm(resid) * w; h -> MXFP8.
+// One block per row (N <= 8192, N % 256 == 0).
+template <int VPT>
+__global__ __launch_bounds__(kBlock) void rmsnorm_mx_kernel(uint16_t* __restrict__ resid,
+                                                            const uint16_t* __restrict__ add,
+                                                            const uint16_t* __restrict__ w, uint8_t* __restrict__ q,
+                                                            uint8_t* __restrict__ s, int N, float eps) {
+    const int m = blockIdx.x;
+    uint4* rr = reinterpret_cast<uint4*>(resid + (size_t)m * N);
+    const uint4* ar = add ? reinterpret_cast<const uint4*>(add + (size_t)m * N) : nullptr;
+    const uint4* wr = reinterpret_cast<const uint4*>(w);
+    const int nvec = N >> 3;
+    float h[VPT][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int idx = threadIdx.x + i * kBlock;
+        if (idx < nvec) {
+            unpack8(rr[idx], h[i]);
+            if (ar) {
+                float a[8];
+                unpack8(ar[idx], a);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) h[i][j] += a[j];
+                const uint4 packed = pack8(h[i]);
+                rr[idx] = packed;
+                unpack8(packed, h[i]);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ss += h[i][j] * h[i][j];
+        }
+    }
+    __shared__ float red[kBlock / kWave];
+    ss = wave_sum(ss);
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < kBlock / kWave; ++i) tot += red[i];
+    const float inv = rsqrtf(tot / (float)N + eps);
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int idx = threadIdx.x + i * kBlock;  // nvec is a multiple of kBlock: every lane takes part
+        float g[8], o[8];
+        unpack8(wr[idx], g);
+        float amax = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            o[j] = h[i][j] * inv * g[j];
+            amax = __builtin_fmaxf(amax, __builtin_fabsf(o[j]));
+        }
+        amax = __builtin_fmaxf(amax, __shfl_xor(amax, 1, kWave));
+        amax = __builtin_fmaxf(amax, __shfl_xor(amax, 2, kWave));
+        const int ex = mx_exp(amax);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = ldexpf(o[j], -ex);
+        reinterpret_cast<uint2*>(q + (size_t)m * N)[idx] = make_uint2(pack_fp8x4(o), pack_fp8x4(o + 4));
+        if ((idx & 3) == 0) s[(size_t)m * (N >> 5) + (idx >> 2)] = (uint8_t)(ex + 127);
+    }
+}
+
+// one MX MFMA on given lane fragments: the operand-layout probe of the tests
+__global__ void mx_probe_kernel(const v8i_t* a, const v8i_t* b, const int* sa, const int* sb, f32x16_t* c) {
+    const int l = threadIdx.x;
+    f32x16_t acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    c[l] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a[l], b[l], acc, 0, 0, 0, sa[l], 0, sb[l]);
+}
+
+template <int MODE, bool KV8>
+hipError_t launch_pgemm(const void* aq, const void* as, const void* wq, const void* ws, int M, int N, int K,
+                        const PEpi& e, void* stream) {
+    const int mtiles = (M + PBM - 1) / PBM;
+    const int ntiles = MODE == PM_SWIGLU ? e.I / 128 : N / PBN;
+    pgemm_kernel<MODE, KV8><<<mtiles * ntiles, PTH, 0, (hipStream_t)stream>>>(
+        (const uint8_t*)aq, (const uint8_t*)as, (const uint8_t*)wq, (const float*)ws, M, N, K, mtiles, ntiles, e);
+    return hipGetLastError();
+}
+
+bool pgemm_shape_ok(const void* aq, const void* as, const void* wq, const void* ws, int M, int N, int K) {
+    return aq && as && wq && ws && M > 0 && K > 0 && K % PBK == 0 && N > 0 && N % PBN == 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// mode 0: y[M, N] = bf16(A . W^T);  mode 1: y (= resid) += bf16(A . W^T).
+// A: aq [M, K] e4m3 + as [M, K / 32] E8M0; W: wq [N, K] e4m3 + ws [N] fp32.
+// Contract: K % 64 == 0, N % 256 == 0.
+int dmcp_pgemm(const void* aq, const void* as, const void* wq, const void* ws, void* y, int M, int N, int K, int mode,
+               void* stream) {
+    if (M == 0) return 0;
+    if (!pgemm_shape_ok(aq, as, wq, ws, M, N, K) || !y || (mode != 0 && mode != 1)) return hipErrorInvalidValue;
+    PEpi e{};
+    e.y = (uint16_t*)y;
+    return mode == 0 ? launch_pgemm<PM_BF16, false>(aq, as, wq, ws, M, N, K, e, stream)
+                     : launch_pgemm<PM_RESID, false>(aq, as, wq, ws, M, N, K, e, stream);
+}
+
+// act = silu(A . Wg^T) * (A . Wu^T) -> MXFP8 yq [M, I] + ys [M, I / 32];
+// wq = [gate; up] [2I, K], ws [2I].  Contract: I % 128 == 0, K % 64 == 0.
+int dmcp_pgemm_swiglu(const void* aq, const void* as, const void* wq, const void* ws, void* yq, void* ys, int M,
+                      int I, int K, void* stream) {
+    if (M == 0) return 0;
+    if (!pgemm_shape_ok(aq, as, wq, ws, M, 256, K) || !yq || !ys || I <= 0 || I % 128 != 0)
+        return hipErrorInvalidValue;
+    PEpi e{};
+    e.yq = (uint8_t*)yq;
+    e.ys = (uint8_t*)ys;
+    e.I = I;
+    return launch_pgemm<PM_SWIGLU, false>(aq, as, wq, ws, M, 2 * I, K, e, stream);
+}
+
+// qkv = A . W^T (W [(Hq + 2 Hkv) 64, K]); RoPE on q / k; q_out [M, Hq, 64]
+// bf16; k / v appended at (slot[m], :, pos[m], :) of the caches (kv8: e4m3).
+// Contract: head dim 64, (Hq + 2 Hkv) % 4 == 0, K % 64 == 0.
+int dmcp_pgemm_qkv(const void* aq, const void* as, const void* wq, const void* ws, const void* pos, const void* slot,
+                   const void* cos_sin, void* q_out, void* k_cache, void* v_cache, int M, int K, int Hq, int Hkv,
+                   int max_seq, int max_pos, int num_slots, int kv8, void* stream) {
+    if (M == 0) return 0;
+    const int N = (Hq + 2 * Hkv) * 64;
+    if (!pgemm_shape_ok(aq, as, wq, ws, M, N, K) || !pos || !slot || !cos_sin || !q_out || !k_cache || !v_cache ||
+        max_pos <= 0 || Hq <= 0 || Hkv <= 0)
+        return hipErrorInvalidValue;
+    PEpi e{};
+    e.pos = (const int32_t*)pos;
+    e.slot = (const int32_t*)slot;
+    e.cos_sin = (const float2*)cos_sin;
+    e.q_out = (uint16_t*)q_out;
+    e.k_cache = k_cache;
+    e.v_cache = v_cache;
+    e.Hq = Hq;
+    e.Hkv = Hkv;
+    e.max_seq = max_seq;
+    e.max_pos = max_pos;
+    e.num_slots = num_slots;
+    return kv8 ? launch_pgemm<PM_QKV, true>(aq, as, wq, ws, M, N, K, e, stream)
+               : launch_pgemm<PM_QKV, false>(aq, as, wq, ws, M, N, K, e, stream);
+}
+
+// bf16 x [M, K] -> MXFP8 q [M, K] + s [M, K / 32]  (K % 32 == 0)
+int dmcp_mx_quant(const void* x, void* q, void* s, int M, int K, void* stream) {
+    if (M == 0) return 0;
+    if (!x || !q || !s || K % 32 != 0) return hipErrorInvalidValue;
+    const long n8 = (long)M * K / 8;
+    const int grid = (int)std::min<long>((n8 + kBlock - 1) / kBlock, 8192);
+    mx_quant_kernel<<<grid, kBlock, 0, (hipStream_t)stream>>>((const uint16_t*)x, (uint8_t*)q, (uint8_t*)s, n8);
+    return hipGetLastError();
+}
+
+// resid += add (optional); RMSNorm(resid) * w -> MXFP8  (N % 2048 == 0, N <= 8192)
+int dmcp_rmsnorm_mx(void* resid, const void* add, const void* w, void* q, void* s, int M, int N, float eps,
+                    void* stream) {
+    if (M == 0) return 0;
+    if (!resid || !w || !q || !s || N % (8 * kBlock) != 0 || N > 4 * 8 * kBlock) return hipErrorInvalidValue;
+    const int vpt = N / (8 * kBlock);
+    auto st = (hipStream_t)stream;
+    auto rr = (uint16_t*)resid;
+    auto aa = (const uint16_t*)add;
+    auto ww = (const uint16_t*)w;
+    auto qq = (uint8_t*)q;
+    auto ss = (uint8_t*)s;
+    if (vpt == 1) rmsnorm_mx_kernel<1><<<M, kBlock, 0, st>>>(rr, aa, ww, qq, ss, N, eps);
+    else if (vpt == 2) rmsnorm_mx_kernel<2><<<M, kBlock, 0, st>>>(rr, aa, ww, qq, ss, N, eps);
+    else if (vpt == 3) rmsnorm_mx_kernel<3><<<M, kBlock, 0, st>>>(rr, aa, ww, qq, ss, N, eps);
+    else rmsnorm_mx_kernel<4><<<M, kBlock, 0, st>>>(rr, aa, ww, qq, ss, N, eps);
+    return hipGetLastError();
+}
+
+int dmcp_mx_probe(const void* a, const void* b, const void* sa, const void* sb, void* c, void* stream) {
+    mx_probe_kernel<<<1, kWave, 0, (hipStream_t)stream>>>((const v8i_t*)a, (const v8i_t*)b, (const int*)sa,
+                                                          (const int*)sb, (f32x16_t*)c);
+    return hipGetLastError();
+}
+
+}  // extern "C"

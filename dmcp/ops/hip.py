@@ -26,7 +26,7 @@ _lock = threading.Lock()
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _f = ctypes.c_float
-ABI_VERSION = 12  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
+ABI_VERSION = 13  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
 
 
 class HipOpsError(RuntimeError):
@@ -65,6 +65,13 @@ def lib() -> ctypes.CDLL:
             "dmcp_decode_embed_norm": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp,
                                         _i, _vp], _i),
             "dmcp_fused_gemm_max_rows": ([], _i),
+            "dmcp_pgemm": ([_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp], _i),
+            "dmcp_pgemm_swiglu": ([_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp], _i),
+            "dmcp_pgemm_qkv": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i,
+                                _vp], _i),
+            "dmcp_mx_quant": ([_vp, _vp, _vp, _i, _i, _vp], _i),
+            "dmcp_rmsnorm_mx": ([_vp, _vp, _vp, _vp, _vp, _i, _i, _f, _vp], _i),
+            "dmcp_mx_probe": ([_vp, _vp, _vp, _vp, _vp, _vp], _i),
             "dmcp_wgemm": ([_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp], _i),
             "dmcp_wgemm_resid_norm": ([_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _vp], _i),
             "dmcp_wgemm_rope_kv": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i,
@@ -837,3 +844,152 @@ def fused_linear_norm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optiona
     _req_out(out, torch.bfloat16, M * N, "fused_linear_norm.out")
     _fused("bf16", wk, x, w, out, M, K, N, eps)
     return out
+
+
+# ---- MXFP8 prefill GEMMs (csrc/pgemm.hip) ----------------------------------
+# A operand: MXFP8 activations (e4m3 bytes [M, K] + E8M0 exponents [M, K / 32]);
+# B operand: e4m3 weights [N, K] + fp32 per-row scales [N]
+# (dmcp.ops.reference.quantize_weight).  256 x 256 output tiles.
+PGEMM_TILE_N = 256
+
+
+def pgemm_supported(hidden: int, n_heads: int, n_kv_heads: int, head_dim: int, inter: int) -> bool:
+    """Whether a model's four projections fit the MXFP8 prefill kernels."""
+    return (head_dim == 64 and (n_heads + 2 * n_kv_heads) % 4 == 0 and hidden % 2048 == 0 and hidden <= 8192
+            and (n_heads * head_dim) % 64 == 0 and inter % 128 == 0 and hidden % PGEMM_TILE_N == 0)
+
+
+def _mx_args(aq: torch.Tensor, as_: torch.Tensor, name: str) -> tuple:
+    _req(aq, torch.uint8, f"{name}.aq")
+    _req(as_, torch.uint8, f"{name}.as")
+    if aq.dim() != 2 or aq.shape[1] % 64 or tuple(as_.shape) != (aq.shape[0], aq.shape[1] // 32):
+        raise HipOpsError(f"{name}: activations {tuple(aq.shape)} / scales {tuple(as_.shape)} are not "
+                          f"[M, K] / [M, K/32] with K % 64 == 0")
+    return aq.shape[0], aq.shape[1]
+
+
+def _w8_args(wq: torch.Tensor, ws: torch.Tensor, K: int, name: str) -> int:
+    _req(wq, torch.uint8, f"{name}.wq")
+    _req(ws, torch.float32, f"{name}.ws")
+    if wq.dim() != 2 or wq.shape[1] != K or ws.numel() != wq.shape[0]:
+        raise HipOpsError(f"{name}: weight {tuple(wq.shape)} / scales {ws.numel()} vs K={K}")
+    return wq.shape[0]
+
+
+def mx_quant(x: torch.Tensor, q: Optional[torch.Tensor] = None, s: Optional[torch.Tensor] = None) -> tuple:
+    """bf16 [M, K] -> MXFP8 (q [M, K] e4m3, s [M, K / 32] E8M0)."""
+    _req(x, torch.bfloat16, "mx_quant.x")
+    M, K = x.shape
+    if K % 32:
+        raise HipOpsError(f"mx_quant: K={K} is not a multiple of 32")
+    q = torch.empty((M, K), dtype=torch.uint8, device=x.device) if q is None else q
+    s = torch.empty((M, K // 32), dtype=torch.uint8, device=x.device) if s is None else s
+    _req_out(q, torch.uint8, M * K, "mx_quant.q")
+    _req_out(s, torch.uint8, M * K // 32, "mx_quant.s")
+    _check(lib().dmcp_mx_quant(_ptr(x), _ptr(q), _ptr(s), M, K, _stream()), "dmcp_mx_quant")
+    return q, s
+
+
+def rmsnorm_mx(resid: torch.Tensor, weight: torch.Tensor, eps: float, add: Optional[torch.Tensor] = None,
+               q: Optional[torch.Tensor] = None, s: Optional[torch.Tensor] = None) -> tuple:
+    """resid += add (in place, when given); RMSNorm(resid) * weight -> MXFP8."""
+    _req(resid, torch.bfloat16, "rmsnorm_mx.resid")
+    _req(weight, torch.bfloat16, "rmsnorm_mx.weight")
+    M, N = resid.shape
+    if N % 2048 or N > 8192 or weight.numel() != N:
+        raise HipOpsError(f"rmsnorm_mx: N={N} (needs N % 2048 == 0, N <= 8192, weight [N])")
+    if add is not None:
+        _req(add, torch.bfloat16, "rmsnorm_mx.add")
+        if tuple(add.shape) != (M, N):
+            raise HipOpsError(f"rmsnorm_mx: add {tuple(add.shape)} != {(M, N)}")
+    q = torch.empty((M, N), dtype=torch.uint8, device=resid.device) if q is None else q
+    s = torch.empty((M, N // 32), dtype=torch.uint8, device=resid.device) if s is None else s
+    _req_out(q, torch.uint8, M * N, "rmsnorm_mx.q")
+    _req_out(s, torch.uint8, M * N // 32, "rmsnorm_mx.s")
+    _check(lib().dmcp_rmsnorm_mx(_ptr(resid), _ptr(add), _ptr(weight), _ptr(q), _ptr(s), M, N, float(eps),
+                                 _stream()), "dmcp_rmsnorm_mx")
+    return q, s
+
+
+def pgemm(aq: torch.Tensor, as_: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor,
+          out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16 [M, N] = A . W^T on the MX fp8 matrix cores (N % 256 == 0)."""
+    M, K = _mx_args(aq, as_, "pgemm")
+    N = _w8_args(wq, ws, K, "pgemm")
+    if N % PGEMM_TILE_N:
+        raise HipOpsError(f"pgemm: N={N} is not a multiple of {PGEMM_TILE_N}")
+    out = torch.empty((M, N), dtype=torch.bfloat16, device=aq.device) if out is None else out
+    _req_out(out, torch.bfloat16, M * N, "pgemm.out")
+    _check(lib().dmcp_pgemm(_ptr(aq), _ptr(as_), _ptr(wq), _ptr(ws), _ptr(out), M, N, K, 0, _stream()), "dmcp_pgemm")
+    return out
+
+
+def pgemm_resid(aq: torch.Tensor, as_: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor,
+                resid: torch.Tensor) -> torch.Tensor:
+    """resid [M, N] += bf16(A . W^T) (in place) -- the o / down projection."""
+    M, K = _mx_args(aq, as_, "pgemm_resid")
+    N = _w8_args(wq, ws, K, "pgemm_resid")
+    _req(resid, torch.bfloat16, "pgemm_resid.resid")
+    if N % PGEMM_TILE_N or tuple(resid.shape) != (M, N):
+        raise HipOpsError(f"pgemm_resid: resid {tuple(resid.shape)} vs {(M, N)} (N % {PGEMM_TILE_N} == 0)")
+    _check(lib().dmcp_pgemm(_ptr(aq), _ptr(as_), _ptr(wq), _ptr(ws), _ptr(resid), M, N, K, 1, _stream()),
+           "dmcp_pgemm[resid]")
+    return resid
+
+
+def pgemm_swiglu(aq: torch.Tensor, as_: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor,
+                 q: Optional[torch.Tensor] = None, s: Optional[torch.Tensor] = None) -> tuple:
+    """silu(A . Wg^T) * (A . Wu^T) as MXFP8 [M, I] (wq = [gate; up] [2I, K])."""
+    M, K = _mx_args(aq, as_, "pgemm_swiglu")
+    N = _w8_args(wq, ws, K, "pgemm_swiglu")
+    inter = N // 2
+    if N % 256:
+        raise HipOpsError(f"pgemm_swiglu: 2I = {N} is not a multiple of 256")
+    q = torch.empty((M, inter), dtype=torch.uint8, device=aq.device) if q is None else q
+    s = torch.empty((M, inter // 32), dtype=torch.uint8, device=aq.device) if s is None else s
+    _req_out(q, torch.uint8, M * inter, "pgemm_swiglu.q")
+    _req_out(s, torch.uint8, M * inter // 32, "pgemm_swiglu.s")
+    _check(lib().dmcp_pgemm_swiglu(_ptr(aq), _ptr(as_), _ptr(wq), _ptr(ws), _ptr(q), _ptr(s), M, inter, K,
+                                   _stream()), "dmcp_pgemm_swiglu")
+    return q, s
+
+
+def pgemm_qkv(aq: torch.Tensor, as_: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, pos: torch.Tensor,
+              slot: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+              n_q_heads: int, q_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """rope_kv(A . W^T): q [M, Hq, 64] bf16 returned, k / v appended to the caches."""
+    M, K = _mx_args(aq, as_, "pgemm_qkv")
+    N = _w8_args(wq, ws, K, "pgemm_qkv")
+    S_, Hkv, MAXS, D = k_cache.shape
+    kv8 = _req_kv(k_cache, v_cache, "pgemm_qkv")
+    _req(pos, torch.int32, "pgemm_qkv.pos")
+    _req(slot, torch.int32, "pgemm_qkv.slot")
+    _req(cos_sin, torch.float32, "pgemm_qkv.cos_sin")
+    if D != 64 or N != (n_q_heads + 2 * Hkv) * D or N % PGEMM_TILE_N or v_cache.shape != k_cache.shape:
+        raise HipOpsError(f"pgemm_qkv: w {tuple(wq.shape)} vs Hq={n_q_heads} / kv {tuple(k_cache.shape)} "
+                          f"(head dim 64, N % {PGEMM_TILE_N} == 0)")
+    if pos.numel() != M or slot.numel() != M or cos_sin.dim() != 3 or tuple(cos_sin.shape[1:]) != (D // 2, 2):
+        raise HipOpsError("pgemm_qkv: pos/slot/cos_sin shape mismatch")
+    q_out = torch.empty((M, n_q_heads, D), dtype=torch.bfloat16, device=aq.device) if q_out is None else q_out
+    _req_out(q_out, torch.bfloat16, M * n_q_heads * D, "pgemm_qkv.q_out")
+    _check(lib().dmcp_pgemm_qkv(_ptr(aq), _ptr(as_), _ptr(wq), _ptr(ws), _ptr(pos), _ptr(slot), _ptr(cos_sin),
+                                _ptr(q_out), _ptr(k_cache), _ptr(v_cache), M, K, n_q_heads, Hkv, MAXS,
+                                cos_sin.shape[0], S_, kv8, _stream()), "dmcp_pgemm_qkv")
+    return q_out
+
+
+def mx_probe(a: torch.Tensor, b: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor) -> torch.Tensor:
+    """One v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3 x e4m3) on raw lane fragments:
+    a / b uint8 [64 lanes, 32], sa / sb int32 [64] (E8M0 in byte 0) -> the
+    accumulator registers fp32 [64 lanes, 16].  The tests' layout check."""
+    for t, n, shp in ((a, "a", (64, 32)), (b, "b", (64, 32))):
+        _req(t, torch.uint8, f"mx_probe.{n}")
+        if tuple(t.shape) != shp:
+            raise HipOpsError(f"mx_probe.{n}: {tuple(t.shape)} != {shp}")
+    for t, n in ((sa, "sa"), (sb, "sb")):
+        _req(t, torch.int32, f"mx_probe.{n}")
+        if t.numel() != 64:
+            raise HipOpsError(f"mx_probe.{n}: needs 64 lanes")
+    c = torch.empty((64, 16), dtype=torch.float32, device=a.device)
+    _check(lib().dmcp_mx_probe(_ptr(a), _ptr(b), _ptr(sa), _ptr(sb), _ptr(c), _stream()), "dmcp_mx_probe")
+    return c

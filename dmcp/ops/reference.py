@@ -227,3 +227,89 @@ def decode_embed_norm(table: torch.Tensor, tokens: torch.Tensor, positions: torc
     resid = embedding(table, toks)
     h = add_rmsnorm(resid, weight, eps) if weight is not None else None
     return resid, h, positions + 1
+
+
+# ---- MXFP8 prefill GEMMs (csrc/pgemm.hip): activations as e4m3 bytes with one
+# power-of-two (E8M0) scale per 32 consecutive elements of a row, weights as
+# e4m3 bytes with one fp32 scale per output row.
+_INV_FP8_MAX = torch.tensor(1.0 / FP8_MAX, dtype=torch.float32)
+
+
+def mx_quant(x: torch.Tensor, q: Optional[torch.Tensor] = None, s: Optional[torch.Tensor] = None) -> tuple:
+    """[M, K] (K % 32 == 0) -> (q uint8 [M, K] e4m3, s uint8 [M, K / 32] E8M0):
+    block exponent e = the smallest with max|x| / 2^e <= 448, q = x / 2^e."""
+    M, K = x.shape
+    xf = x.float().reshape(M, K // 32, 32)
+    amax = xf.abs().amax(-1)
+    _, e = torch.frexp(amax * _INV_FP8_MAX.to(x.device))
+    e = torch.where(amax > 0, e, torch.zeros_like(e)).clamp(-127, 127)
+    qv = torch.ldexp(xf, (-e)[..., None].to(torch.float32))
+    qb = qv.clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).view(torch.uint8).reshape(M, K)
+    sb = (e + 127).to(torch.uint8)
+    if q is not None:
+        q.copy_(qb)
+        s.copy_(sb)
+        return q, s
+    return qb, sb
+
+
+def mx_dequant(q: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    """fp32 values of an MXFP8 tensor."""
+    M, K = q.shape
+    v = q.view(torch.float8_e4m3fn).float().reshape(M, K // 32, 32)
+    return torch.ldexp(v, (s.to(torch.int32) - 127)[..., None].to(torch.float32)).reshape(M, K)
+
+
+def quantize_weight(w: torch.Tensor) -> tuple:
+    """[N, K] -> (e4m3 bytes [N, K], fp32 scale [N]): per-output-row scale max|w| / 448."""
+    wf = w.float()
+    sc = wf.abs().amax(-1) / FP8_MAX
+    sc = torch.where(sc > 0, sc, torch.ones_like(sc))
+    wq = (wf / sc[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).view(torch.uint8)
+    return wq.contiguous(), sc.to(torch.float32).contiguous()
+
+
+def weight_dequant(wq: torch.Tensor, ws: torch.Tensor) -> torch.Tensor:
+    return wq.view(torch.float8_e4m3fn).float() * ws[:, None].float()
+
+
+def _pgemm_f32(aq, as_, wq, ws) -> torch.Tensor:
+    return mx_dequant(aq, as_) @ weight_dequant(wq, ws).t()
+
+
+def rmsnorm_mx(resid: torch.Tensor, weight: torch.Tensor, eps: float, add: Optional[torch.Tensor] = None,
+               q: Optional[torch.Tensor] = None, s: Optional[torch.Tensor] = None) -> tuple:
+    """resid += add (bf16, in place); RMSNorm(resid) * weight as MXFP8."""
+    if add is not None:
+        resid.copy_((resid.float() + add.float()).to(resid.dtype))
+    hf = resid.float()
+    y = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + eps) * weight.float()
+    return mx_quant(y, q, s)
+
+
+def pgemm(aq, as_, wq, ws, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    y = _pgemm_f32(aq, as_, wq, ws).to(torch.bfloat16)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def pgemm_resid(aq, as_, wq, ws, resid: torch.Tensor) -> torch.Tensor:
+    y = _pgemm_f32(aq, as_, wq, ws).to(torch.bfloat16)
+    resid.copy_((resid.float() + y.float()).to(resid.dtype))
+    return resid
+
+
+def pgemm_swiglu(aq, as_, wq, ws, q: Optional[torch.Tensor] = None, s: Optional[torch.Tensor] = None) -> tuple:
+    """silu(gate) * up of the stacked [gate; up] weight, as MXFP8 [M, I]."""
+    gu = _pgemm_f32(aq, as_, wq, ws).to(torch.bfloat16).float()
+    inter = gu.shape[1] // 2
+    g, u = gu[:, :inter], gu[:, inter:]
+    return mx_quant(g / (1.0 + torch.exp(-g)) * u, q, s)
+
+
+def pgemm_qkv(aq, as_, wq, ws, pos, slot, cos_sin, k_cache, v_cache, n_q_heads: int,
+              q_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    qkv = _pgemm_f32(aq, as_, wq, ws).to(torch.bfloat16)
+    return rope_kv(qkv, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out)

@@ -25,9 +25,11 @@ def main() -> int:
     ap.add_argument("--seqs", type=int, default=12)
     ap.add_argument("--kv-dtype", default="fp8", choices=["bf16", "fp8"])
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--prefill-dtype", default="bf16", choices=["bf16", "fp8"])
     a = ap.parse_args()
     from dmcp.models.llm import LocalLM, preset
-    model = LocalLM(preset(a.preset, max_batch=max(8, a.seqs), max_seq=8192, kv_dtype=a.kv_dtype), device="cuda:0")
+    model = LocalLM(preset(a.preset, max_batch=max(8, a.seqs), max_seq=8192, kv_dtype=a.kv_dtype,
+                           prefill_dtype=a.prefill_dtype), device="cuda:0")
     g = torch.Generator().manual_seed(0)
     P = 0
     if a.prefix:
@@ -48,7 +50,7 @@ def main() -> int:
     ms = (time.perf_counter() - t0) / a.iters * 1e3
     flops = 2 * model.cfg.param_count() * a.tokens * a.seqs
     print(json.dumps({"bench": "prefill_batch", "seqs": a.seqs, "tokens": a.tokens, "prefix": P,
-                      "kv_dtype": a.kv_dtype, "ms_per_batch": round(ms, 3), "ms_per_class": round(ms / a.seqs, 3),
+                      "kv_dtype": a.kv_dtype, "prefill_dtype": a.prefill_dtype, "ms_per_batch": round(ms, 3), "ms_per_class": round(ms / a.seqs, 3),
                       "prompt_tokens_per_s": round(a.tokens * a.seqs / ms * 1e3, 1),
                       "weight_tflops": round(flops / ms / 1e9, 1)}), flush=True)
     return 0

@@ -49,6 +49,10 @@ for s in $STEPS; do
             head -30 "$OUT/kstats_llama.txt"
             [ $rc -eq 0 ] || exit $rc ;;
         prefill) run prefill 300 python scripts/bench_prefill.py --seqs 12 ;;
+        pgemm_test) run pgemm_test 300 python -u -m pytest tests/test_gpu_pgemm.py -x -v --timeout 120 \
+                --timeout-method thread ;;
+        pgemm_bench) run pgemm_bench 300 python scripts/bench_pgemm.py --preset llama3.2-1b-code --rows 24576 ;;
+        enrich_fp8_nofork) run enrich_fp8_nofork 900 python bench_enrich.py --kv-dtype fp8 --no-fork ;;
         step_llama)
             run step_llama533 300 python scripts/bench_step.py --preset llama3.2-1b-code --batch 512 --extra 21 \
                 --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 60

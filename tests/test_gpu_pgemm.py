@@ -1,0 +1,200 @@
+"""MXFP8 prefill GEMMs (csrc/pgemm.hip) against plain PyTorch fp32
+compositions of the same ops on the dequantised operands: the MX MFMA's lane
+layout (exact integer data, asymmetric operands, non-uniform block scales),
+the quantisers (bytes and exponents equal to the reference's), and every
+epilogue -- bf16 output, residual add, SwiGLU -> MXFP8, RoPE + KV-cache append
+(bf16 and fp8 caches) -- at prefill row counts that are not multiples of the
+256-row tile."""
+import pytest
+import torch
+
+from dmcp.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hip():
+    from dmcp.ops import hip as h
+    h.lib()
+    return h
+
+
+def _bf(*shape, seed=0, scale=1.0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return (torch.randn(*shape, generator=g, device="cuda") * scale).to(torch.bfloat16)
+
+
+def _fp8_int(n, lo=-4, hi=5, seed=0):
+    """small integers (exact in e4m3) as e4m3 bytes + their values"""
+    g = torch.Generator().manual_seed(seed)
+    v = torch.randint(lo, hi, n, generator=g).float()
+    return v.to(torch.float8_e4m3fn).view(torch.uint8), v
+
+
+def test_mx_mfma_lane_layout(hip):
+    """The layout pgemm.hip is written for (found by scripts/mx_layout_probe.py):
+    lane l holds row (A) / column (B) l % 32; with h = l // 32, its bytes
+    0-15 are k = 16 h + j and bytes 16-31 are k = 32 + 16 h + (j - 16); the
+    scale of lane (r, 0) scales row r's k block 0-31, lane (r, 1) block
+    32-63.  C: lane l, register i = row (i % 4) + 8 (i // 4) + 4 (l // 32),
+    column l % 32.  Exact integer data, asymmetric operands, per-lane scales."""
+    ab, av = _fp8_int((64, 32), seed=1)
+    bb, bv = _fp8_int((64, 32), seed=2)
+    g = torch.Generator().manual_seed(3)
+    sa = torch.randint(124, 131, (64,), generator=g, dtype=torch.int32)
+    sb = torch.randint(124, 131, (64,), generator=g, dtype=torch.int32)
+
+    def kk(h, j):
+        return 16 * h + j if j < 16 else 32 + 16 * h + (j - 16)
+    A = torch.zeros(32, 64)
+    B = torch.zeros(64, 32)
+    for lane in range(64):
+        r, h = lane % 32, lane // 32
+        for j in range(32):
+            k = kk(h, j)
+            A[r, k] = av[lane, j]
+            B[k, r] = bv[lane, j]
+    for r in range(32):  # block scales: lane r -> k 0-31, lane r + 32 -> k 32-63
+        A[r, :32] *= 2.0 ** (int(sa[r]) - 127)
+        A[r, 32:] *= 2.0 ** (int(sa[r + 32]) - 127)
+        B[:32, r] *= 2.0 ** (int(sb[r]) - 127)
+        B[32:, r] *= 2.0 ** (int(sb[r + 32]) - 127)
+    C = A @ B
+    got = hip.mx_probe(ab.cuda(), bb.cuda(), sa.cuda(), sb.cuda()).cpu()
+    exp = torch.empty(64, 16)
+    for lane in range(64):
+        for reg in range(16):
+            exp[lane, reg] = C[(reg % 4) + 8 * (reg // 4) + 4 * (lane // 32), lane % 32]
+    torch.testing.assert_close(got, exp, atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("M,K", [(1, 64), (333, 2048), (1000, 8192)])
+def test_mx_quant_matches_reference(hip, M, K):
+    x = _bf(M, K, seed=M, scale=3.0)
+    x[0, :32] = 0  # an all-zero block
+    q, s = hip.mx_quant(x)
+    rq, rs = R.mx_quant(x.cpu())
+    assert torch.equal(s.cpu(), rs)
+    assert (q.cpu() != rq).float().mean().item() < 1e-4
+    blk = x.float().abs().reshape(M, -1, 32).amax(-1, keepdim=True).cpu()
+    err = (R.mx_dequant(q.cpu(), s.cpu()) - x.float().cpu()).abs().reshape(M, -1, 32)
+    assert (err <= blk / 16).all()  # e4m3: 3 mantissa bits at the block's scale
+
+
+@pytest.mark.parametrize("M", [1, 257, 1500])
+def test_rmsnorm_mx(hip, M):
+    N = 2048
+    resid, add, w = _bf(M, N, seed=1), _bf(M, N, seed=2), _bf(N, seed=3, scale=0.5) + 1
+    r_ref = resid.cpu().clone()
+    q, s = hip.rmsnorm_mx(resid, w, 1e-5, add=add)
+    rq, rs = R.rmsnorm_mx(r_ref, w.cpu(), 1e-5, add=add.cpu())
+    assert torch.equal(resid.cpu(), r_ref)
+    assert (s.cpu() != rs).float().mean().item() < 1e-3
+    torch.testing.assert_close(R.mx_dequant(q.cpu(), s.cpu()), R.mx_dequant(rq, rs), atol=1e-2, rtol=0.07)
+
+
+def _operands(M, N, K, seed=0):
+    x = _bf(M, K, seed=seed, scale=2.0)
+    w = _bf(N, K, seed=seed + 1, scale=0.03)
+    aq, as_ = R.mx_quant(x.cpu())
+    wq, ws = R.quantize_weight(w.cpu())
+    ref = R.mx_dequant(aq, as_) @ R.weight_dequant(wq, ws).t()
+    return aq.cuda(), as_.cuda(), wq.cuda(), ws.cuda(), ref
+
+
+@pytest.mark.parametrize("M", [1, 100, 256, 1000, 3000])
+@pytest.mark.parametrize("N,K", [(3072, 2048), (2048, 8192), (256, 64)])
+def test_pgemm_plain(hip, M, N, K):
+    aq, as_, wq, ws, ref = _operands(M, N, K, seed=M)
+    got = hip.pgemm(aq, as_, wq, ws)
+    torch.testing.assert_close(got.float().cpu(), ref, atol=2e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("M", [77, 1024])
+def test_pgemm_resid(hip, M):
+    aq, as_, wq, ws, ref = _operands(M, 2048, 2048, seed=5)
+    resid = _bf(M, 2048, seed=9)
+    exp = (resid.float().cpu() + ref.to(torch.bfloat16).float())
+    got = hip.pgemm_resid(aq, as_, wq, ws, resid)
+    assert got.data_ptr() == resid.data_ptr()
+    torch.testing.assert_close(resid.float().cpu(), exp, atol=3e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("M", [33, 700])
+def test_pgemm_swiglu(hip, M):
+    inter, K = 1024, 2048
+    aq, as_, wq, ws, ref = _operands(M, 2 * inter, K, seed=11)
+    q, s = hip.pgemm_swiglu(aq, as_, wq, ws)
+    gu = ref.to(torch.bfloat16).float()
+    act = gu[:, :inter] / (1 + torch.exp(-gu[:, :inter])) * gu[:, inter:]
+    rq, rs = R.mx_quant(act)
+    assert (s.cpu() != rs).float().mean().item() < 1e-2
+    got = R.mx_dequant(q.cpu(), s.cpu())
+    # within one e4m3 step of the block's largest value
+    blk = act.abs().reshape(M, -1, 32).amax(-1, keepdim=True).expand(-1, -1, 32).reshape(M, inter)
+    assert ((got - act).abs() <= blk / 8 + 1e-6).all()
+    assert (got - act).abs().mean().item() < 0.02 * act.abs().mean().item()
+
+
+@pytest.mark.parametrize("kv", ["bf16", "fp8"])
+@pytest.mark.parametrize("M", [5, 600])
+def test_pgemm_qkv_rope_kv(hip, kv, M):
+    Hq, Hkv, D, K, S, MAXS = 32, 8, 64, 2048, 4, 1024
+    aq, as_, wq, ws, ref = _operands(M, (Hq + 2 * Hkv) * D, K, seed=21)
+    g = torch.Generator().manual_seed(4)
+    # distinct (slot, pos) so both paths write every cell once; the rest are
+    # padding rows (slot -1: no cache write)
+    pos = torch.randperm(S * MAXS, generator=g)[:M].to(torch.int32) % MAXS
+    slot = (torch.randperm(S * MAXS, generator=g)[:M].to(torch.int32) % S)
+    uniq = {}
+    for i in range(M):
+        uniq.setdefault((int(slot[i]), int(pos[i])), i)
+    keep = torch.zeros(M, dtype=torch.bool)
+    keep[list(uniq.values())] = True
+    slot = torch.where(keep, slot, torch.full_like(slot, -1))
+    cos_sin = R.rope_tables(MAXS, D, 500000.0)
+    dt = torch.uint8 if kv == "fp8" else torch.bfloat16
+    kc = torch.zeros(S, Hkv, MAXS, D, dtype=dt)
+    vc = torch.zeros_like(kc)
+    kc_g, vc_g = kc.cuda(), vc.cuda()
+    q = hip.pgemm_qkv(aq, as_, wq, ws, pos.cuda(), slot.cuda(), cos_sin.cuda(), kc_g, vc_g, Hq)
+    rq = R.rope_kv(ref.to(torch.bfloat16), pos, slot, cos_sin, kc, vc, Hq)
+    torch.testing.assert_close(q.float().cpu(), rq.float(), atol=3e-2, rtol=2e-2)
+    tol = dict(atol=0.07, rtol=0.07) if kv == "fp8" else dict(atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(R.kv_float(kc_g.cpu()), R.kv_float(kc), **tol)
+    torch.testing.assert_close(R.kv_float(vc_g.cpu()), R.kv_float(vc), **tol)
+
+
+@pytest.mark.parametrize("kv", ["bf16", "fp8"])
+def test_model_prefill_fp8_close_to_bf16(hip, kv):
+    """LocalLM.prefill_batch with prefill_dtype fp8 (the kernels above, a
+    2-layer model of the 1B dims) against the bf16 prefill of the same
+    weights: logits, K/V written, with and without the shared prefix."""
+    from dmcp.models.llm import LocalLM, preset
+    cfg = dict(layers=2, max_batch=8, max_seq=2048, kv_dtype=kv)
+    a = LocalLM(preset("dmcp-coder-1b", **cfg), device="cuda", seed=4)
+    b = LocalLM(preset("dmcp-coder-1b", prefill_dtype="fp8", **cfg), device="cuda", seed=4)
+    assert b.prefill_fp8
+    g = torch.Generator().manual_seed(0)
+    seqs = [[256] + torch.randint(0, 256, (n,), generator=g).tolist() for n in (700, 333, 1)]
+    for shared in (False, True):
+        P = 0
+        if shared:
+            prefix = [256] + torch.randint(0, 256, (300,), generator=g).tolist()
+            P = a.set_prefix(prefix)
+            assert b.set_prefix(prefix) == P
+            for m in (a, b):
+                for s in range(3):
+                    m.fork_prefix(s)
+        reqs = [(t[1:] if shared else t, s, P) for s, t in enumerate(seqs)]
+        la, lb = a.prefill_batch(reqs).float(), b.prefill_batch(reqs).float()
+        cos = torch.nn.functional.cosine_similarity(la, lb, dim=-1)
+        assert (cos > 0.98).all(), cos
+        n = P + 700
+        for ca, cb in ((a.k_cache, b.k_cache), (a.v_cache, b.v_cache)):
+            x, y = R.kv_float(ca[:, 0, :, P:n]), R.kv_float(cb[:, 0, :, P:n])
+            assert ((x - y).norm() / x.norm()).item() < 0.1
+        if shared:
+            a.clear_prefix()
+            b.clear_prefix()

@@ -436,3 +436,26 @@ def test_native_grammar_engine_matches_the_python_engine(tiny, pipeline):
     g.close()
     assert nat._native.n_active() == 0 and nat._native.n_templates() == 0
     assert dict(nat.stream(items[:3], None)) == {k: v for k, v in a.items() if k < 3}
+
+
+def test_prefill_fp8_close_to_bf16():
+    """prefill_dtype fp8 (MXFP8 activations x e4m3 weights, the CPU references
+    of csrc/pgemm.hip) stays close to the bf16 prefill of the same weights,
+    and the engine decodes valid replies after it."""
+    cfg = dict(max_batch=4, max_rows=16, max_seq=2048)
+    a = LocalLM(preset("tiny", **cfg), device="cpu", seed=3)
+    b = LocalLM(preset("tiny", prefill_dtype="fp8", **cfg), device="cpu", seed=3)
+    assert b.prefill_fp8 and set(b.w8) == {f"l{i}.{n}" for i in range(b.cfg.layers)
+                                          for n in ("wqkv", "wo", "wgu", "wdown")}
+    seqs = [[256] + list(b"class A { void a() {} }"), [256] + list(b"interface Bee { int b(); }"), [256, 65]]
+    la = a.prefill_batch([(t, s, 0) for s, t in enumerate(seqs)]).float()
+    lb = b.prefill_batch([(t, s, 0) for s, t in enumerate(seqs)]).float()
+    cos = torch.nn.functional.cosine_similarity(la, lb, dim=-1)
+    assert (cos > 0.98).all(), cos
+    ka, kb = a.k_cache[:, :3].float(), b.k_cache[:, :3].float()
+    assert (ka - kb).norm() / ka.norm() < 0.1
+    one = b.prefill_batch([(seqs[0], 3, 0)]).float()  # a single sequence takes the fp8 path too
+    torch.testing.assert_close(one[0], lb[0], atol=2e-2, rtol=2e-2)
+    eng = LocalEngine(b, use_graphs=False)
+    out = eng.generate(_inputs(3), "readme")
+    assert all(json.loads(o) for o in out)

@@ -28,6 +28,8 @@ def main(argv=None) -> int:
                     help="KV cache storage (fp8 = e4m3, half the attention bytes)")
     ap.add_argument("--prefill-dtype", default="bf16", choices=["bf16", "fp8"],
                     help="batched-prefill projections: bf16 (hipBLASLt) or fp8 (MXFP8 kernels, csrc/pgemm.hip)")
+    ap.add_argument("--decode-dtype", default="bf16", choices=["bf16", "fp8"],
+                    help="decode-step projections: bf16, or fp8 weights x MXFP8 activations (csrc/pgemm.hip)")
     ap.add_argument("--classes", type=int, default=1024, help="classes per rank")
     ap.add_argument("--batch", type=int, default=512, help="concurrent sequences (KV slots)")
     ap.add_argument("--max-seq", type=int, default=8192)
@@ -64,7 +66,7 @@ def main(argv=None) -> int:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl")
     cfg = preset(args.preset, max_batch=args.batch, max_seq=args.max_seq, kv_dtype=args.kv_dtype,
-                 prefill_dtype=args.prefill_dtype, max_rows=args.max_rows or max(256, args.batch + args.batch // 2))
+                 prefill_dtype=args.prefill_dtype, decode_dtype=args.decode_dtype, max_rows=args.max_rows or max(256, args.batch + args.batch // 2))
     model = LocalLM(cfg, device=f"cuda:{local}", seed=rank)
     tok = None
     if cfg.tokenizer:
@@ -123,7 +125,7 @@ def main(argv=None) -> int:
             "unit": "classes/s", "n_gpus": world, "higher_is_better": True, "scaling": "weak",
             "dtype": "bf16", "data": "synthetic classes, random-init weights",
             "config": {"model": cfg.name, "params_b": round(cfg.param_count() / 1e9, 3), "batch": args.batch,
-                       "max_rows": cfg.max_rows, "kv_dtype": cfg.kv_dtype, "prefill_dtype": cfg.prefill_dtype,
+                       "max_rows": cfg.max_rows, "kv_dtype": cfg.kv_dtype, "prefill_dtype": cfg.prefill_dtype, "decode_dtype": cfg.decode_dtype,
                        "max_seq": args.max_seq, "prompt_chars": args.prompt_chars,
                        "readme_chars": args.readme_chars, "graphs": not args.no_graphs,
                        "jump_forward": not args.no_jump, "shared_prefix": not args.no_shared_prefix,

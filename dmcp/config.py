@@ -53,6 +53,7 @@ class Config:
     # benchmarked number is fp8 (56.8 vs 43.9 classes/s bf16, profiles/enrich_*_r3_prompt.jsonl)
     local_llm_kv_dtype: str = "fp8"
     local_llm_prefill_dtype: str = "bf16"
+    local_llm_decode_dtype: str = "bf16"
     # reply budget in tokens (the reference's claude.max-tokens analog): a
     # class whose reply does not fit is generated in several parts and merged
     local_llm_max_new_tokens: int = 4096
@@ -127,6 +128,7 @@ class Config:
             "LOCAL_LLM_MODEL_PATH": "local_llm_model_path",
             "LOCAL_LLM_KV_DTYPE": "local_llm_kv_dtype",
             "LOCAL_LLM_PREFILL_DTYPE": "local_llm_prefill_dtype",
+            "LOCAL_LLM_DECODE_DTYPE": "local_llm_decode_dtype",
             "LOCAL_LLM_MAX_NEW_TOKENS": "local_llm_max_new_tokens",
             "LOCAL_LLM_FORK_METHODS": "local_llm_fork_methods",
             "LOCAL_LLM_DEVICES": "local_llm_devices",

@@ -1273,8 +1273,8 @@ def build_model(spec: dict, device: str):
     """(LocalLM, tokenizer) of a worker model spec: the checkpoint directory
     ``spec["path"]`` (its own tokenizer) or the random-initialised preset
     ``spec["preset"]`` (byte-level tokenizer: ``None`` = the engine default);
-    ``kv_dtype`` / ``prefill_dtype`` / ``max_batch`` / ``max_rows`` / ``max_seq`` override either."""
-    overrides = {k: spec[k] for k in ("kv_dtype", "prefill_dtype", "max_batch", "max_rows", "max_seq") if k in spec}
+    ``kv_dtype`` / ``prefill_dtype`` / ``decode_dtype`` / ``max_batch`` / ``max_rows`` / ``max_seq`` override either."""
+    overrides = {k: spec[k] for k in ("kv_dtype", "prefill_dtype", "decode_dtype", "max_batch", "max_rows", "max_seq") if k in spec}
     if spec.get("path"):
         from .tokenizer import load_local_model
         return load_local_model(spec["path"], device=device, **overrides)

@@ -84,6 +84,10 @@ class LMConfig:
     # activations x per-row-scaled e4m3 weights on the MX matrix cores,
     # csrc/pgemm.hip, epilogues fused); decode keeps the bf16 weights
     prefill_dtype: str = "bf16"
+    # decode steps of fused_max_rows < rows <= WMX_MAX_ROWS: "bf16" (wgemm.hip /
+    # hipBLASLt) or "fp8" (the same e4m3 weights, MXFP8 activations written by
+    # the producing norm / SwiGLU: csrc/pgemm.hip wmx_kernel)
+    decode_dtype: str = "bf16"
     # the preset's tokenizer: "" = byte-level (dmcp.enrich.tokenizer.ByteTokenizer),
     # else an asset directory under dmcp/models/assets (tokenizer.json.gz)
     tokenizer: str = ""
@@ -217,8 +221,9 @@ class LocalLM:
             raise ValueError("n_heads must be a multiple of n_kv_heads")
         if cfg.kv_dtype not in ("bf16", "fp8"):
             raise ValueError(f"kv_dtype must be 'bf16' or 'fp8', got {cfg.kv_dtype!r}")
-        if cfg.prefill_dtype not in ("bf16", "fp8"):
-            raise ValueError(f"prefill_dtype must be 'bf16' or 'fp8', got {cfg.prefill_dtype!r}")
+        for k in ("prefill_dtype", "decode_dtype"):
+            if getattr(cfg, k) not in ("bf16", "fp8"):
+                raise ValueError(f"{k} must be 'bf16' or 'fp8', got {getattr(cfg, k)!r}")
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = torch.bfloat16
@@ -275,15 +280,24 @@ class LocalLM:
         # fp8 prefill: e4m3 copies of the four projections (per-row scales),
         # quantised once; the batched prefill then runs on csrc/pgemm.hip
         # (the CPU references take any dims the 32-element blocks divide)
-        self.prefill_fp8 = c.prefill_dtype == "fp8" and c.n_heads * c.head_dim == c.hidden and (
+        fp8_ok = c.n_heads * c.head_dim == c.hidden and (
             (self.use_prefill_kernel
              and ops.pgemm_supported(c.hidden, c.n_heads, c.n_kv_heads, c.head_dim, c.intermediate))
             or (self.device.type == "cpu" and c.hidden % 32 == 0 and c.intermediate % 32 == 0))
-        if c.prefill_dtype == "fp8" and not self.prefill_fp8:
-            raise ValueError(f"prefill_dtype fp8 needs head_dim 64, hidden % 2048 == 0 and a supported device "
+        self.prefill_fp8 = c.prefill_dtype == "fp8" and fp8_ok
+        self.decode_fp8 = c.decode_dtype == "fp8" and fp8_ok
+        if "fp8" in (c.prefill_dtype, c.decode_dtype) and not fp8_ok:
+            raise ValueError(f"fp8 GEMMs need head_dim 64, hidden % 2048 == 0 and a supported device "
                              f"({c.name}: hidden {c.hidden}, head_dim {c.head_dim}, {self.device})")
+        # decode fp8: split-K partials of the MX decode GEMM (S x rows <= 2048 by wmx_plan)
+        self.wmx_ws = None
+        if self.decode_fp8 and self.device.type == "cuda":
+            need = max(S * M * n for M in range(self.fused_max_rows + 1, min(self.max_rows, ops.WMX_MAX_ROWS) + 1)
+                       for n, k in ((c.qkv_dim, c.hidden), (c.hidden, c.hidden), (c.hidden, c.intermediate))
+                       for S in (ops.wmx_plan(M, n, k)[0],))
+            self.wmx_ws = torch.empty(need, dtype=torch.float32, device=self.device)
         self.w8: Dict[str, tuple] = {}
-        if self.prefill_fp8:
+        if self.prefill_fp8 or self.decode_fp8:
             for i in range(c.layers):
                 for n in ("wqkv", "wo", "wgu", "wdown"):
                     self.w8[f"l{i}.{n}"] = ops.quantize_weight(self.w[f"l{i}.{n}"])
@@ -573,6 +587,8 @@ class LocalLM:
         chunk, splits = ops.decode_plan(B, c.n_kv_heads, c.max_seq, c.kv_dtype)
         resid, h, seq_len = ops.decode_embed_norm(self.w["embed"], tokens, positions, self.w["l0.ln1"], c.eps,
                                                   src, last_ids, mask_idx, mask_alt, alt_token)
+        if self.decode_fp8 and (self.device.type == "cpu" or B <= ops.WMX_MAX_ROWS):
+            return self._decode_trunk_fp8(B, resid, h, seq_len, slots, positions, chunk, splits, prefix_rows)
         wide = self.use_wgemm and B <= ops.WGEMM_MAX_ROWS
         for i in range(c.layers):
             kc, vc = self.k_cache[i], self.v_cache[i]
@@ -593,6 +609,47 @@ class LocalLM:
             h = ops.add_rmsnorm(o, self.w[f"l{i}.ln2"], c.eps, residual=resid)
             m = self._mlp(i, h)
             h = ops.add_rmsnorm(m, nxt, c.eps, residual=resid)
+        return h
+
+    def _decode_trunk_fp8(self, B, resid, h, seq_len, slots, positions, chunk, splits, prefix_rows) -> torch.Tensor:
+        """The layers of a decode step on the fp8 weights: every projection's
+        activation is MXFP8 (the step's first norm quantised once, then written
+        by the split-K reduction + residual + RMSNorm kernels and the SwiGLU
+        epilogue); the last layer's norm writes bf16 for the LM head.  GPU: the
+        MX weight-streaming GEMM (csrc/pgemm.hip wmx_kernel); CPU: the fp32
+        references of the same compositions."""
+        c = self.cfg
+        gpu = self.device.type == "cuda"
+        xq, xs = ops.mx_quant(h)
+        for i in range(c.layers):
+            kc, vc = self.k_cache[i], self.v_cache[i]
+            last = i + 1 == c.layers
+            nxt = self.w["norm_f"] if last else self.w[f"l{i + 1}.ln1"]
+            w8 = self.w8
+            if gpu:
+                q = ops.wgemm_mx_rope_kv(xq, xs, *w8[f"l{i}.wqkv"], positions, slots, self.cos_sin, kc, vc,
+                                         c.n_heads, self.wmx_ws)
+            else:
+                q = ops.pgemm_qkv(xq, xs, *w8[f"l{i}.wqkv"], positions, slots, self.cos_sin, kc, vc, c.n_heads)
+            att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws, chunk=chunk,
+                                       prefix=self._prefix(i, prefix_rows), splits=splits).view(B, c.hidden)
+            aq, as_ = ops.mx_quant(att)
+            if gpu:
+                xq, xs = ops.wgemm_mx_resid_norm(aq, as_, *w8[f"l{i}.wo"], resid, self.w[f"l{i}.ln2"], c.eps,
+                                                 self.wmx_ws)
+                gq, gs = ops.wgemm_mx_swiglu(xq, xs, *w8[f"l{i}.wgu"])
+                r = ops.wgemm_mx_resid_norm(gq, gs, *w8[f"l{i}.wdown"], resid, nxt, c.eps, self.wmx_ws,
+                                            mx=not last)
+            else:
+                ops.pgemm_resid(aq, as_, *w8[f"l{i}.wo"], resid)
+                xq, xs = ops.rmsnorm_mx(resid, self.w[f"l{i}.ln2"], c.eps)
+                gq, gs = ops.pgemm_swiglu(xq, xs, *w8[f"l{i}.wgu"])
+                ops.pgemm_resid(gq, gs, *w8[f"l{i}.wdown"], resid)
+                r = ops.add_rmsnorm(resid, nxt, c.eps) if last else ops.rmsnorm_mx(resid, nxt, c.eps)
+            if last:
+                h = r
+            else:
+                xq, xs = r
         return h
 
     def _prefix(self, i: int, rows: Optional[torch.Tensor] = None):

@@ -16,7 +16,8 @@ from . import hip, reference
 from .hip import (FUSED_MAX_ROWS, PREFIX_MFMA_MAX_SPLITS, WGEMM_MAX_ROWS, decode_workspace,  # noqa: F401
                   fused_linear_norm, fused_rope_kv, fused_swiglu, lm_head_supported, lm_head_workspace,
                   prefill_supported, wgemm_resid_norm, wgemm_rope_kv, wgemm_swiglu, wgemm_workspace)
-from .hip import PGEMM_TILE_N, pgemm_supported  # noqa: F401
+from .hip import (PGEMM_TILE_N, WMX_MAX_ROWS, pgemm_supported, wgemm_mx_resid_norm, wgemm_mx_rope_kv,  # noqa: F401
+                  wgemm_mx_swiglu, wmx_plan)
 from .reference import SharedPrefix, mx_dequant, quantize_weight, rope_tables, weight_dequant  # noqa: F401
 
 

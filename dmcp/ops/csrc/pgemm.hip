@@ -356,6 +356,247 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
 }
 
+// ---- decode: weight-streaming GEMM on MX fp8 (the wgemm.hip structure with
+// e4m3 weights and MXFP8 activations: half the bytes of both operands per
+// block -- the per-CU load path, not HBM, bounded the bf16 form)
+//
+//   C^T tile = W[n rows] . X[m rows]^T on v_mfma_scale_f32_32x32x64_f8f6f4:
+//   A = 32 weight rows (scale 1: the per-row fp32 weight scale is applied
+//   in the epilogue), B = 32 activation rows with their E8M0 block scales.
+//   A lane holds activation row lane % 32 and 16 output columns
+//   (i & 3) + 8 (i >> 2) + 4 (lane >> 5) of its tile.
+//
+// A block owns NB = 64 weight rows (SwiGLU: 32 gate + 32 up rows of the
+// same intermediate columns) and all rows of its M part (MT x 128 rows,
+// 4 waves x MT 32-row tiles), a K slice of K / S; LDS-DMA ring of 64-deep
+// stages as pgemm_kernel.
+constexpr int XM_PART = 1, XM_SWIGLU = 2;
+
+template <int NB, int MT, int MODE, int ST>
+__global__ __launch_bounds__(kBlock) void wmx_kernel(
+    const uint8_t* __restrict__ xq, const uint8_t* __restrict__ xs, const uint8_t* __restrict__ wq,
+    const float* __restrict__ ws, float* __restrict__ part, uint8_t* __restrict__ yq, uint8_t* __restrict__ ys,
+    int M, int N, int K, int ks, int S, int ntiles, int mparts, int I) {
+    constexpr int MR = MT * 128;                  // activation rows staged per block
+    constexpr int NF = NB / 32;                   // weight tiles
+    constexpr int W_BYTES = NB * PBK, X_BYTES = MR * PBK, XS_BYTES = 4 * kWave * 2;
+    constexpr int STB = W_BYTES + X_BYTES + XS_BYTES;
+    constexpr int WI = NB / 64;                   // 1-KiB weight pieces per wave per stage
+    constexpr int XI = MR / 64;                   // activation pieces per wave
+    constexpr int GL = WI + XI + 1;               // LDS-DMA instructions per wave per stage
+    __shared__ __attribute__((aligned(16))) uint8_t lds[ST * STB];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(tid / kWave);
+    const int l32 = lane & 31, hh = lane >> 5;
+    // block -> (weight tile, K slice, M part): the M parts of one (tile, slice)
+    // share blockIdx % 8 (one XCD) and consecutive dispatch slots
+    const int units = ntiles * S;
+    int u, mp;
+    if ((units & 7) == 0) {
+        const int j = blockIdx.x >> 3;
+        u = (j / mparts) * 8 + (blockIdx.x & 7);
+        mp = j % mparts;
+    } else {
+        u = blockIdx.x / mparts;
+        mp = blockIdx.x % mparts;
+    }
+    const int nt = u % ntiles, sl = u / ntiles;
+    const int k0 = sl * ks;
+    const int m_lo = mp * MR;
+
+    auto wrow = [&](int r) -> int {
+        if constexpr (MODE == XM_SWIGLU) return r < NB / 2 ? nt * (NB / 2) + r : I + nt * (NB / 2) + (r - NB / 2);
+        else return nt * NB + r;
+    };
+    const uint8_t* wsrc[WI];
+    const uint8_t* xsrc[XI];
+#pragma unroll
+    for (int i = 0; i < WI; ++i) {
+        const int r = (wv * WI + i) * 16 + (lane >> 2);
+        wsrc[i] = wq + (size_t)wrow(r) * K + k0 + (((lane & 3) ^ ((r >> 2) & 3)) * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+        const int r = (wv * XI + i) * 16 + (lane >> 2);
+        xsrc[i] = xq + (size_t)min(m_lo + r, M - 1) * K + k0 + (((lane & 3) ^ ((r >> 2) & 3)) * 16);
+    }
+    // activation scales: the stage's 2 bytes of each staged row; wave w, lane L
+    // -> row w * (MR / 4) + L (MT = 1: lanes 32-63 repeat lanes 0-31)
+    const int srow = wv * (MR / 4) + (MT == 2 ? lane : l32);
+    const int ksb = K >> 5;
+    const uint8_t* ssrc = xs + (size_t)min(m_lo + srow, M - 1) * ksb + (k0 >> 5);
+
+    auto issue = [&](int c, int st) {
+        uint8_t* base = lds + st * STB;
+#pragma unroll
+        for (int i = 0; i < WI; ++i) pglds<16>(wsrc[i] + c * PBK, base + (wv * WI + i) * 1024);
+#pragma unroll
+        for (int i = 0; i < XI; ++i) pglds<16>(xsrc[i] + c * PBK, base + W_BYTES + (wv * XI + i) * 1024);
+        pglds<2>(ssrc + c * 2, base + W_BYTES + X_BYTES + wv * 128);
+    };
+
+    f32x16_t acc[NF][MT];
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[f][t][i] = 0.f;
+
+    auto frag = [&](const uint8_t* img, int r) -> v8i_t {
+        const int sw = (r >> 2) & 3;
+        const v4i_t lo = *reinterpret_cast<const v4i_t*>(img + r * PBK + (hh ^ sw) * 16);
+        const v4i_t hi = *reinterpret_cast<const v4i_t*>(img + r * PBK + ((2 + hh) ^ sw) * 16);
+        return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    };
+    auto compute = [&](int st) {
+        const uint8_t* W = lds + st * STB;
+        const uint8_t* X = W + W_BYTES;
+        const uint8_t* SX = X + X_BYTES;
+        v8i_t xf[MT];
+        int sx[MT];
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            const int r = wv * (MT * 32) + t * 32 + l32;  // staged activation row
+            xf[t] = frag(X, r);
+            // row r was fetched by wave r / (MR / 4), lane r % (MR / 4)
+            sx[t] = SX[(r / (MR / 4)) * 128 + (r % (MR / 4)) * 2 + hh];
+        }
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+            const v8i_t wf = frag(W, f * 32 + l32);
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+                acc[f][t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf, xf[t], acc[f][t], 0, 0, 0, 127, 0,
+                                                                            sx[t]);
+        }
+    };
+
+    const int chunks = ks / PBK;
+#pragma unroll
+    for (int j = 0; j < ST - 1; ++j)
+        if (j < chunks) issue(j, j);
+    for (int c = 0; c < chunks; ++c) {
+        if (c + ST - 2 < chunks) {
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(GL * (ST - 2)) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+        if (c + ST - 1 < chunks) issue(c + ST - 1, (c + ST - 1) % ST);
+        compute(c % ST);
+    }
+
+    // epilogue: lane holds activation row m, output columns (i & 3) + 8 (i >> 2) + 4 hh of tile f
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+        const int m = m_lo + wv * (MT * 32) + t * 32 + l32;
+        if constexpr (MODE == XM_PART) {
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int n = nt * NB + f * 32 + 8 * j + 4 * hh;
+                    const float4 sc = *reinterpret_cast<const float4*>(ws + n);
+                    if (m < M)
+                        *reinterpret_cast<float4*>(part + ((size_t)sl * M + m) * N + n) =
+                            make_float4(acc[f][t][4 * j] * sc.x, acc[f][t][4 * j + 1] * sc.y,
+                                        acc[f][t][4 * j + 2] * sc.z, acc[f][t][4 * j + 3] * sc.w);
+                }
+        } else {  // XM_SWIGLU: tiles f = 0, 1 gate columns, f + 2 the up columns of the same intermediates
+            const int isb = I >> 5;
+#pragma unroll
+            for (int f = 0; f < NF / 2; ++f) {
+                float a[16];
+                float amax = 0.f;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int jj = nt * (NB / 2) + f * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+                    const float g = bf2f(f2bf(acc[f][t][i] * ws[jj])), uu = bf2f(f2bf(acc[f + NF / 2][t][i] * ws[I + jj]));
+                    a[i] = psilu(g) * uu;
+                    amax = __builtin_fmaxf(amax, __builtin_fabsf(a[i]));
+                }
+                amax = half_swap_max(amax);  // the block's other 16 columns are in lane ^ 32
+                const int ex = mx_exp(amax);
+                const int jb = nt * (NB / 2) + f * 32;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) a[i] = ldexpf(a[i], -ex);
+                if (m < M) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        *reinterpret_cast<uint32_t*>(yq + (size_t)m * I + jb + 8 * j + 4 * hh) = pack_fp8x4(a + 4 * j);
+                    if (hh == 0) ys[(size_t)m * isb + (jb >> 5)] = (uint8_t)(ex + 127);
+                }
+            }
+        }
+    }
+}
+
+// split-K reduction + residual add + RMSNorm, output MXFP8 (the next MX
+// GEMM's activation): resid += bf16(sum_s part[s]); h = RMSNorm(resid) * w.
+// One block per row, N % 2048 == 0, N <= 8192.
+template <int VPT>
+__global__ __launch_bounds__(kBlock) void reduce_resid_norm_mx_kernel(const float* __restrict__ part, int S,
+                                                                      uint16_t* __restrict__ resid,
+                                                                      const uint16_t* __restrict__ w,
+                                                                      uint8_t* __restrict__ q, uint8_t* __restrict__ s,
+                                                                      int M, int N, float eps) {
+    const int m = blockIdx.x;
+    uint4* rr = reinterpret_cast<uint4*>(resid + (size_t)m * N);
+    const uint4* wr = reinterpret_cast<const uint4*>(w);
+    float h[VPT][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int idx = threadIdx.x + i * kBlock;
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int sl = 0; sl < S; ++sl) {
+            const float4* pp = reinterpret_cast<const float4*>(part + ((size_t)sl * M + m) * N);
+            const float4 a = pp[2 * idx], b = pp[2 * idx + 1];
+            acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+            acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+        }
+        float y[8], r[8];
+        unpack8(pack8(acc), y);  // the GEMM output rounded to bf16, as F.linear's
+        unpack8(rr[idx], r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] += r[j];
+        const uint4 packed = pack8(y);
+        rr[idx] = packed;
+        unpack8(packed, h[i]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += h[i][j] * h[i][j];
+    }
+    __shared__ float red[kBlock / kWave];
+    ss = wave_sum(ss);
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < kBlock / kWave; ++i) tot += red[i];
+    const float inv = rsqrtf(tot / (float)N + eps);
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int idx = threadIdx.x + i * kBlock;
+        float g[8], o[8];
+        unpack8(wr[idx], g);
+        float amax = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            o[j] = h[i][j] * inv * g[j];
+            amax = __builtin_fmaxf(amax, __builtin_fabsf(o[j]));
+        }
+        amax = __builtin_fmaxf(amax, __shfl_xor(amax, 1, kWave));
+        amax = __builtin_fmaxf(amax, __shfl_xor(amax, 2, kWave));
+        const int ex = mx_exp(amax);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = ldexpf(o[j], -ex);
+        reinterpret_cast<uint2*>(q + (size_t)m * N)[idx] = make_uint2(pack_fp8x4(o), pack_fp8x4(o + 4));
+        if ((idx & 3) == 0) s[(size_t)m * (N >> 5) + (idx >> 2)] = (uint8_t)(ex + 127);
+    }
+}
+
 // MXFP8 quantisation of bf16 rows: q[M, K] e4m3, s[M, K / 32] E8M0 (4 lanes
 // per 32-block, 8 elements per lane)
 __global__ __launch_bounds__(kBlock) void mx_quant_kernel(const uint16_t* __restrict__ x, uint8_t* __restrict__ q,
@@ -544,6 +785,73 @@ int dmcp_rmsnorm_mx(void* resid, const void* add, const void* w, void* q, void* 
     else if (vpt == 2) rmsnorm_mx_kernel<2><<<M, kBlock, 0, st>>>(rr, aa, ww, qq, ss, N, eps);
     else if (vpt == 3) rmsnorm_mx_kernel<3><<<M, kBlock, 0, st>>>(rr, aa, ww, qq, ss, N, eps);
     else rmsnorm_mx_kernel<4><<<M, kBlock, 0, st>>>(rr, aa, ww, qq, ss, N, eps);
+    return hipGetLastError();
+}
+
+// Decode GEMMs on MX fp8 (contract checked by dmcp/ops/hip.py, guarded here):
+// x MXFP8 [M, K] (+ [M, K / 32] scales), w e4m3 [N, K] + fp32 scales [N];
+// M <= 512, K % (64 S) == 0, rows / part <= 256.
+//   mode 1: part[S, M, N] fp32 partials (N % 64 == 0)
+//   mode 2: SwiGLU -> MXFP8 yq [M, I] + ys [M, I / 32]  (w = [gate; up] [2I, K], I % 32 == 0, S == 1)
+int dmcp_wgemm_mx(const void* xq, const void* xs, const void* wq, const void* ws, void* part, void* yq, void* ys,
+                  int M, int N, int K, int S, int mparts, int mode, int I, void* stream) {
+    if (M <= 0) return 0;
+    const int mrows = (M + mparts - 1) / mparts;
+    if (!xq || !xs || !wq || !ws || M > 512 || S < 1 || mparts < 1 || K % (PBK * S) != 0 || mrows > 256 ||
+        (mode == 1 && (!part || N % 64 != 0)) || (mode == 2 && (!yq || !ys || S != 1 || I <= 0 || I % 32 != 0)) ||
+        (mode != 1 && mode != 2))
+        return hipErrorInvalidValue;
+    auto st = (hipStream_t)stream;
+    auto xx = (const uint8_t*)xq;
+    auto xsc = (const uint8_t*)xs;
+    auto ww = (const uint8_t*)wq;
+    auto wsc = (const float*)ws;
+    const int ks = K / S;
+    const int mt = mrows > 128 ? 2 : 1;
+    // the kernel stages MT x 128 rows per part from row mp * MT * 128
+    if (mparts * mt * 128 < M) return hipErrorInvalidValue;
+    if (mode == 1) {
+        const int ntiles = N / 64;
+        const dim3 grid((unsigned)(ntiles * S * mparts));
+        if (mt == 2)
+            wmx_kernel<64, 2, XM_PART, 4><<<grid, kBlock, 0, st>>>(xx, xsc, ww, wsc, (float*)part, nullptr, nullptr,
+                                                                   M, N, K, ks, S, ntiles, mparts, 0);
+        else
+            wmx_kernel<64, 1, XM_PART, 4><<<grid, kBlock, 0, st>>>(xx, xsc, ww, wsc, (float*)part, nullptr, nullptr,
+                                                                   M, N, K, ks, S, ntiles, mparts, 0);
+    } else {
+        // 32 gate + 32 up rows per block: I / 32 tiles fill the chip at one M part
+        const int ntiles = I / 32;
+        const dim3 grid((unsigned)(ntiles * mparts));
+        if (mt == 2)
+            wmx_kernel<64, 2, XM_SWIGLU, 4><<<grid, kBlock, 0, st>>>(xx, xsc, ww, wsc, nullptr, (uint8_t*)yq,
+                                                                     (uint8_t*)ys, M, 2 * I, K, K, 1, ntiles,
+                                                                     mparts, I);
+        else
+            wmx_kernel<64, 1, XM_SWIGLU, 4><<<grid, kBlock, 0, st>>>(xx, xsc, ww, wsc, nullptr, (uint8_t*)yq,
+                                                                     (uint8_t*)ys, M, 2 * I, K, K, 1, ntiles,
+                                                                     mparts, I);
+    }
+    return hipGetLastError();
+}
+
+// resid += bf16(sum of the S partials); RMSNorm(resid) * w -> MXFP8 q / s
+int dmcp_reduce_resid_norm_mx(const void* part, int S, void* resid, const void* w, void* q, void* s, int M, int N,
+                              float eps, void* stream) {
+    if (M <= 0) return 0;
+    if (!part || S < 1 || !resid || !w || !q || !s || N % (8 * kBlock) != 0 || N > 4 * 8 * kBlock)
+        return hipErrorInvalidValue;
+    const int vpt = N / (8 * kBlock);
+    auto st = (hipStream_t)stream;
+    auto pp = (const float*)part;
+    auto rr = (uint16_t*)resid;
+    auto ww = (const uint16_t*)w;
+    auto qq = (uint8_t*)q;
+    auto ss = (uint8_t*)s;
+    if (vpt == 1) reduce_resid_norm_mx_kernel<1><<<M, kBlock, 0, st>>>(pp, S, rr, ww, qq, ss, M, N, eps);
+    else if (vpt == 2) reduce_resid_norm_mx_kernel<2><<<M, kBlock, 0, st>>>(pp, S, rr, ww, qq, ss, M, N, eps);
+    else if (vpt == 3) reduce_resid_norm_mx_kernel<3><<<M, kBlock, 0, st>>>(pp, S, rr, ww, qq, ss, M, N, eps);
+    else reduce_resid_norm_mx_kernel<4><<<M, kBlock, 0, st>>>(pp, S, rr, ww, qq, ss, M, N, eps);
     return hipGetLastError();
 }
 

@@ -612,4 +612,43 @@ int dmcp_wgemm_rope_kv(const void* x, const void* w, void* part, const void* pos
     return hipGetLastError();
 }
 
+// The split-K reductions alone, for partials written by another GEMM (the MX
+// fp8 decode GEMM of pgemm.hip): resid += bf16(sum part); out = RMSNorm * g.
+int dmcp_reduce_resid_norm(const void* part, int S, void* resid, const void* g, void* out, int M, int N, float eps,
+                           void* stream) {
+    if (M <= 0) return 0;
+    if (!part || S < 1 || !resid || !g || !out || N % 8 != 0 || N > 8 * 4 * kBlock) return hipErrorInvalidValue;
+    auto st = (hipStream_t)stream;
+    const int vpt = (N / 8 + kBlock - 1) / kBlock;
+    auto pp = (const float*)part;
+    auto rr = (uint16_t*)resid;
+    auto gg = (const uint16_t*)g;
+    auto oo = (uint16_t*)out;
+    if (vpt == 1) reduce_resid_norm_kernel<1><<<M, kBlock, 0, st>>>(pp, S, rr, gg, oo, M, N, eps);
+    else if (vpt == 2) reduce_resid_norm_kernel<2><<<M, kBlock, 0, st>>>(pp, S, rr, gg, oo, M, N, eps);
+    else reduce_resid_norm_kernel<4><<<M, kBlock, 0, st>>>(pp, S, rr, gg, oo, M, N, eps);
+    return hipGetLastError();
+}
+
+// ... and RoPE + q write + KV append of QKV partials [S, M, (Hq + 2 Hkv) D]
+int dmcp_reduce_rope_kv(const void* part, int S, const void* pos, const void* slot, const void* cos_sin, void* q_out,
+                        void* k_cache, void* v_cache, int M, int Hq, int Hkv, int D, int max_seq, int max_pos,
+                        int num_slots, int kv8, void* stream) {
+    if (M <= 0) return 0;
+    if (!part || S < 1 || D % 16 != 0 || (Hq + 2 * Hkv) * D > 8192 || !pos || !slot || !cos_sin || !q_out ||
+        !k_cache || !v_cache || max_pos <= 0)
+        return hipErrorInvalidValue;
+    auto st = (hipStream_t)stream;
+    auto pp = (const float*)part;
+    if (kv8)
+        reduce_rope_kv_kernel<true><<<M, kBlock, 0, st>>>(pp, S, M, (const int32_t*)pos, (const int32_t*)slot,
+                                                          (const float2*)cos_sin, (uint16_t*)q_out, k_cache, v_cache,
+                                                          Hq, Hkv, D, max_seq, max_pos, num_slots);
+    else
+        reduce_rope_kv_kernel<false><<<M, kBlock, 0, st>>>(pp, S, M, (const int32_t*)pos, (const int32_t*)slot,
+                                                           (const float2*)cos_sin, (uint16_t*)q_out, k_cache,
+                                                           v_cache, Hq, Hkv, D, max_seq, max_pos, num_slots);
+    return hipGetLastError();
+}
+
 }  // extern "C"

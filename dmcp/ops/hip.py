@@ -72,6 +72,10 @@ def lib() -> ctypes.CDLL:
             "dmcp_mx_quant": ([_vp, _vp, _vp, _i, _i, _vp], _i),
             "dmcp_rmsnorm_mx": ([_vp, _vp, _vp, _vp, _vp, _i, _i, _f, _vp], _i),
             "dmcp_mx_probe": ([_vp, _vp, _vp, _vp, _vp, _vp], _i),
+            "dmcp_wgemm_mx": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp], _i),
+            "dmcp_reduce_resid_norm_mx": ([_vp, _i, _vp, _vp, _vp, _vp, _i, _i, _f, _vp], _i),
+            "dmcp_reduce_resid_norm": ([_vp, _i, _vp, _vp, _vp, _i, _i, _f, _vp], _i),
+            "dmcp_reduce_rope_kv": ([_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp], _i),
             "dmcp_wgemm": ([_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp], _i),
             "dmcp_wgemm_resid_norm": ([_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _vp], _i),
             "dmcp_wgemm_rope_kv": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i,
@@ -993,3 +997,112 @@ def mx_probe(a: torch.Tensor, b: torch.Tensor, sa: torch.Tensor, sb: torch.Tenso
     c = torch.empty((64, 16), dtype=torch.float32, device=a.device)
     _check(lib().dmcp_mx_probe(_ptr(a), _ptr(b), _ptr(sa), _ptr(sb), _ptr(c), _stream()), "dmcp_mx_probe")
     return c
+
+
+# ---- decode GEMMs on MX fp8 (csrc/pgemm.hip wmx_kernel) ---------------------
+WMX_MAX_ROWS = 512
+def wmx_plan(M: int, N: int, K: int, swiglu: bool = False) -> tuple:
+    """(K slices S, M parts) of the MX decode GEMM: parts of 256 or 128 staged
+    rows, whichever stages fewer rows for M (each part re-streams its weight
+    tile, an L2 hit on the same XCD); then the most power-of-two K slices
+    (whole 64-deep stages, >= 256 deep) that keep the grid within one wave
+    of blocks -- 256, or 512 when a 128-row part's ~50 KB of LDS lets two
+    blocks share a CU.  SwiGLU (its output quantised in place) does not split K."""
+    a, b = -(-M // 256), -(-M // 128)
+    mparts = a if a * 256 <= b * 128 else b
+    if swiglu:
+        return 1, mparts
+    cap = 512 if -(-M // mparts) <= 128 else 256
+    blocks = (N // 64) * mparts
+    S = 1
+    while blocks * S * 2 <= cap and K % (64 * S * 2) == 0 and K // (S * 2) >= 256:
+        S *= 2
+    return S, mparts
+
+
+def _wmx_args(xq, xs, wq, ws, name):
+    M, K = _mx_args(xq, xs, name)
+    N = _w8_args(wq, ws, K, name)
+    if not 1 <= M <= WGEMM_MAX_ROWS or N % 64:
+        raise HipOpsError(f"{name}: needs 1 <= M <= {WGEMM_MAX_ROWS}, N % 64 == 0 (M={M} N={N})")
+    return M, K, N
+
+
+def wgemm_mx_partials(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor,
+                      workspace: torch.Tensor, splits: int = 0) -> int:
+    """fp32 split-K partials [S, M, N] of MXFP8 x . (e4m3 w * ws)^T; returns S."""
+    M, K, N = _wmx_args(xq, xs, wq, ws, "wgemm_mx_partials")
+    S, mparts = wmx_plan(M, N, K)
+    S = splits or S
+    if K % (64 * S):
+        raise HipOpsError(f"wgemm_mx_partials: K={K} does not split into {S} slices")
+    _wgemm_ws(workspace, S * M * N, "wgemm_mx_partials")
+    _check(lib().dmcp_wgemm_mx(_ptr(xq), _ptr(xs), _ptr(wq), _ptr(ws), _ptr(workspace), None, None, M, N, K, S,
+                               mparts, 1, 0, _stream()), "dmcp_wgemm_mx[partials]")
+    return S
+
+
+def wgemm_mx_swiglu(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor,
+                    q: Optional[torch.Tensor] = None, s: Optional[torch.Tensor] = None) -> tuple:
+    """silu(gate) * up of the stacked e4m3 [gate; up] weight, as MXFP8 [M, I]."""
+    M, K, N = _wmx_args(xq, xs, wq, ws, "wgemm_mx_swiglu")
+    if N % 64:
+        raise HipOpsError(f"wgemm_mx_swiglu: 2I = {N} must be a multiple of 64")
+    inter = N // 2
+    _, mparts = wmx_plan(M, N, K, swiglu=True)
+    q = torch.empty((M, inter), dtype=torch.uint8, device=xq.device) if q is None else q
+    s = torch.empty((M, inter // 32), dtype=torch.uint8, device=xq.device) if s is None else s
+    _req_out(q, torch.uint8, M * inter, "wgemm_mx_swiglu.q")
+    _req_out(s, torch.uint8, M * inter // 32, "wgemm_mx_swiglu.s")
+    _check(lib().dmcp_wgemm_mx(_ptr(xq), _ptr(xs), _ptr(wq), _ptr(ws), None, _ptr(q), _ptr(s), M, N, K, 1, mparts, 2,
+                               inter, _stream()), "dmcp_wgemm_mx[swiglu]")
+    return q, s
+
+
+def wgemm_mx_resid_norm(xq, xs, wq, ws, residual: torch.Tensor, norm_w: torch.Tensor, eps: float,
+                        workspace: torch.Tensor, mx: bool = True, out: Optional[tuple] = None):
+    """residual += bf16(x . w^T); returns RMSNorm(residual) * norm_w as MXFP8
+    (q, s) -- or, ``mx=False``, as bf16 (the last layer: the LM head's input)."""
+    M, K, N = _wmx_args(xq, xs, wq, ws, "wgemm_mx_resid_norm")
+    _req(residual, torch.bfloat16, "wgemm_mx_resid_norm.residual")
+    _req(norm_w, torch.bfloat16, "wgemm_mx_resid_norm.norm_w")
+    if tuple(residual.shape) != (M, N) or norm_w.numel() != N or N % 2048 or N > 8192:
+        raise HipOpsError("wgemm_mx_resid_norm: residual / norm weight shape mismatch (N % 2048 == 0, <= 8192)")
+    S = wgemm_mx_partials(xq, xs, wq, ws, workspace)
+    if not mx:
+        h = torch.empty((M, N), dtype=torch.bfloat16, device=xq.device) if out is None else out
+        _req_out(h, torch.bfloat16, M * N, "wgemm_mx_resid_norm.out")
+        _check(lib().dmcp_reduce_resid_norm(_ptr(workspace), S, _ptr(residual), _ptr(norm_w), _ptr(h), M, N,
+                                            float(eps), _stream()), "dmcp_reduce_resid_norm")
+        return h
+    q, s = out if out is not None else (torch.empty((M, N), dtype=torch.uint8, device=xq.device),
+                                        torch.empty((M, N // 32), dtype=torch.uint8, device=xq.device))
+    _req_out(q, torch.uint8, M * N, "wgemm_mx_resid_norm.q")
+    _req_out(s, torch.uint8, M * N // 32, "wgemm_mx_resid_norm.s")
+    _check(lib().dmcp_reduce_resid_norm_mx(_ptr(workspace), S, _ptr(residual), _ptr(norm_w), _ptr(q), _ptr(s), M, N,
+                                           float(eps), _stream()), "dmcp_reduce_resid_norm_mx")
+    return q, s
+
+
+def wgemm_mx_rope_kv(xq, xs, wq, ws, pos: torch.Tensor, slot: torch.Tensor, cos_sin: torch.Tensor,
+                     k_cache: torch.Tensor, v_cache: torch.Tensor, n_q_heads: int, workspace: torch.Tensor,
+                     q_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """rope_kv(x . w^T) on the MX decode GEMM: q [M, Hq, D] returned, K/V appended."""
+    M, K, N = _wmx_args(xq, xs, wq, ws, "wgemm_mx_rope_kv")
+    S_, Hkv, MAXS, D = k_cache.shape
+    kv8 = _req_kv(k_cache, v_cache, "wgemm_mx_rope_kv")
+    _req(pos, torch.int32, "wgemm_mx_rope_kv.pos")
+    _req(slot, torch.int32, "wgemm_mx_rope_kv.slot")
+    _req(cos_sin, torch.float32, "wgemm_mx_rope_kv.cos_sin")
+    if v_cache.shape != k_cache.shape or N != (n_q_heads + 2 * Hkv) * D or D % 16 or N > 8192:
+        raise HipOpsError(f"wgemm_mx_rope_kv: w {tuple(wq.shape)} does not match Hq={n_q_heads} / kv "
+                          f"{tuple(k_cache.shape)}")
+    if pos.numel() != M or slot.numel() != M or cos_sin.dim() != 3 or tuple(cos_sin.shape[1:]) != (D // 2, 2):
+        raise HipOpsError("wgemm_mx_rope_kv: pos/slot/cos_sin shape mismatch")
+    S = wgemm_mx_partials(xq, xs, wq, ws, workspace)
+    q_out = torch.empty((M, n_q_heads, D), dtype=torch.bfloat16, device=xq.device) if q_out is None else q_out
+    _req_out(q_out, torch.bfloat16, M * n_q_heads * D, "wgemm_mx_rope_kv.q_out")
+    _check(lib().dmcp_reduce_rope_kv(_ptr(workspace), S, _ptr(pos), _ptr(slot), _ptr(cos_sin), _ptr(q_out),
+                                     _ptr(k_cache), _ptr(v_cache), M, n_q_heads, Hkv, D, MAXS, cos_sin.shape[0], S_,
+                                     kv8, _stream()), "dmcp_reduce_rope_kv")
+    return q_out

@@ -35,6 +35,7 @@ def main() -> int:
     ap.add_argument("--preset", default="llama3.2-1b-code")
     ap.add_argument("--rows", type=int, default=24576)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--decode-rows", type=int, nargs="*", default=[78, 320, 512])
     a = ap.parse_args()
     from dmcp import ops
     from dmcp.models.llm import preset
@@ -89,7 +90,34 @@ def main() -> int:
     tot = {impl: sum(v.get(impl, 0) for v in out.values()) for impl in ("bf16_hipblaslt", "mxfp8_fused")}
     print(json.dumps({"rows": M, "layer_us": {k: round(v, 1) for k, v in tot.items()},
                       "speedup": round(tot["bf16_hipblaslt"] / tot["mxfp8_fused"], 3)}), flush=True)
-    del hip
+    # decode-step shapes: the bf16 weight-streaming GEMMs (wgemm.hip, fused
+    # reductions) against the MX fp8 ones (wmx_kernel + the same reductions)
+    for Md in a.decode_rows:
+        ws_b = hip.wgemm_workspace(Md, max(c.qkv_dim, H), dev)
+        ws_m = torch.empty(16 * Md * max(c.qkv_dim, H, I), dtype=torch.float32, device=dev)
+        xd = {k: v[:Md].contiguous() for k, v in x.items()}
+        md = {k: ops.mx_quant(v) for k, v in xd.items()}
+        rd = bf(Md, H)
+        nw = torch.ones(H, dtype=torch.bfloat16, device=dev)
+        posd, slotd = pos[:Md].contiguous(), slot[:Md].contiguous()
+        res = {}
+        res["qkv"] = (timed(lambda: hip.wgemm_rope_kv(xd["qkv"], w["qkv"], posd, slotd, cos_sin, kc, vc, c.n_heads,
+                                                      ws_b), a.iters),
+                      timed(lambda: hip.wgemm_mx_rope_kv(*md["qkv"], *w8["qkv"], posd, slotd, cos_sin, kc, vc,
+                                                         c.n_heads, ws_m), a.iters))
+        res["o"] = (timed(lambda: hip.wgemm_resid_norm(xd["o"], w["o"], rd, nw, 1e-5, ws_b), a.iters),
+                    timed(lambda: hip.wgemm_mx_resid_norm(*md["o"], *w8["o"], rd, nw, 1e-5, ws_m), a.iters))
+        res["gate_up"] = (timed(lambda: hip.wgemm_swiglu(xd["gate_up"], w["gate_up"]), a.iters),
+                          timed(lambda: hip.wgemm_mx_swiglu(*md["gate_up"], *w8["gate_up"]), a.iters))
+        res["down"] = (timed(lambda: hip.wgemm_resid_norm(xd["down"], w["down"], rd, nw, 1e-5, ws_b), a.iters),
+                       timed(lambda: hip.wgemm_mx_resid_norm(*md["down"], *w8["down"], rd, nw, 1e-5, ws_m), a.iters))
+        for k, (tb, tm) in res.items():
+            N, K = shapes[k]
+            print(json.dumps({"decode_rows": Md, "proj": k, "bf16_wgemm_us": round(tb, 1), "mx_fp8_us": round(tm, 1),
+                              "mx_weight_TBps": round(N * K / tm / 1e6, 2)}), flush=True)
+        tb, tm = sum(v[0] for v in res.values()), sum(v[1] for v in res.values())
+        print(json.dumps({"decode_rows": Md, "layer_us": {"bf16_wgemm": round(tb, 1), "mx_fp8": round(tm, 1)},
+                          "speedup": round(tb / tm, 3)}), flush=True)
     return 0
 
 

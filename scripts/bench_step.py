@@ -33,6 +33,8 @@ def main(argv=None) -> int:
     ap.add_argument("--preset", default="dmcp-coder-1b")
     ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"],
                     help="KV cache storage (fp8 = e4m3, half the attention bytes)")
+    ap.add_argument("--decode-dtype", default="bf16", choices=["bf16", "fp8"],
+                    help="decode projections: bf16 or fp8 weights x MXFP8 activations")
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--extra", type=int, default=14)
     ap.add_argument("--prefix", type=int, default=4151)
@@ -54,7 +56,7 @@ def main(argv=None) -> int:
 
     torch.cuda.set_device(0)
     cfg = preset(a.preset, max_batch=a.batch, max_seq=a.max_seq, kv_dtype=a.kv_dtype)
-    cfg = preset(a.preset, max_batch=a.batch, max_seq=a.max_seq, kv_dtype=a.kv_dtype,
+    cfg = preset(a.preset, max_batch=a.batch, max_seq=a.max_seq, kv_dtype=a.kv_dtype, decode_dtype=a.decode_dtype,
                  max_rows=max(cfg.max_rows, a.batch + a.extra))
     model = LocalLM(cfg, device="cuda:0")
     if a.fused >= 0:
@@ -112,7 +114,7 @@ def main(argv=None) -> int:
     loop_ms = (time.perf_counter() - t0) / a.iters * 1e3
     kv_bytes = 2 * cfg.layers * cfg.n_kv_heads * cfg.head_dim * cfg.kv_elem_bytes * (sum(ctxs) + a.batch + a.prefix)
     w_bytes = 2 * (cfg.param_count() - cfg.vocab_size * cfg.hidden)
-    print(json.dumps({"bench": "decode_step", "preset": a.preset, "kv_dtype": a.kv_dtype, "rows": n, "batch": a.batch, "prefix": a.prefix,
+    print(json.dumps({"bench": "decode_step", "preset": a.preset, "kv_dtype": a.kv_dtype, "decode_dtype": a.decode_dtype, "rows": n, "batch": a.batch, "prefix": a.prefix,
                       "ctx": a.ctx, "jitter": a.jitter, "adjacent": a.adjacent, "fused": bool(getattr(model, "use_fused", False)),
                       "prefix_splits": hip.prefix_mfma_splits(a.batch + a.extra, cfg.n_heads // cfg.n_kv_heads,
                                                               cfg.n_kv_heads),

@@ -198,3 +198,88 @@ def test_model_prefill_fp8_close_to_bf16(hip, kv):
         if shared:
             a.clear_prefix()
             b.clear_prefix()
+
+
+# ---- decode: the MX weight-streaming GEMM (wmx_kernel) at decode row counts
+DEC_ROWS = [17, 78, 129, 256, 320, 448, 512]
+
+
+@pytest.mark.parametrize("M", DEC_ROWS)
+@pytest.mark.parametrize("N,K", [(3072, 2048), (2048, 8192)])
+def test_wgemm_mx_partials(hip, M, N, K):
+    aq, as_, wq, ws, ref = _operands(M, N, K, seed=M + N)
+    work = torch.empty(16 * M * N, dtype=torch.float32, device="cuda")
+    S = hip.wgemm_mx_partials(aq, as_, wq, ws, work)
+    got = work[:S * M * N].view(S, M, N).sum(0)
+    torch.testing.assert_close(got.cpu(), ref, atol=2e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("M", [17, 129, 320, 512])
+def test_wgemm_mx_swiglu(hip, M):
+    inter, K = 8192, 2048
+    aq, as_, wq, ws, ref = _operands(M, 2 * inter, K, seed=7)
+    q, s = hip.wgemm_mx_swiglu(aq, as_, wq, ws)
+    gu = ref.to(torch.bfloat16).float()
+    act = gu[:, :inter] / (1 + torch.exp(-gu[:, :inter])) * gu[:, inter:]
+    got = R.mx_dequant(q.cpu(), s.cpu())
+    blk = act.abs().reshape(M, -1, 32).amax(-1, keepdim=True).expand(-1, -1, 32).reshape(M, inter)
+    assert ((got - act).abs() <= blk / 8 + 1e-6).all()
+    assert (got - act).abs().mean().item() < 0.02 * act.abs().mean().item()
+
+
+@pytest.mark.parametrize("mx", [True, False])
+@pytest.mark.parametrize("M", [33, 320])
+def test_wgemm_mx_resid_norm(hip, mx, M):
+    N, K = 2048, 8192
+    aq, as_, wq, ws, ref = _operands(M, N, K, seed=3)
+    resid = _bf(M, N, seed=4)
+    nw = _bf(N, seed=5, scale=0.2) + 1
+    exp_resid = (resid.float().cpu() + ref.to(torch.bfloat16).float()).to(torch.bfloat16)
+    h = exp_resid.float() * torch.rsqrt(exp_resid.float().pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float().cpu()
+    work = torch.empty(16 * M * N, dtype=torch.float32, device="cuda")
+    out = hip.wgemm_mx_resid_norm(aq, as_, wq, ws, resid, nw, 1e-5, work, mx=mx)
+    torch.testing.assert_close(resid.float().cpu(), exp_resid.float(), atol=3e-2, rtol=1e-2)
+    got = R.mx_dequant(out[0].cpu(), out[1].cpu()) if mx else out.float().cpu()
+    torch.testing.assert_close(got, h, atol=5e-2, rtol=0.07)
+
+
+@pytest.mark.parametrize("kv", ["bf16", "fp8"])
+def test_wgemm_mx_rope_kv(hip, kv):
+    M, Hq, Hkv, D, K, S, MAXS = 300, 32, 8, 64, 2048, 512, 256
+    aq, as_, wq, ws, ref = _operands(M, (Hq + 2 * Hkv) * D, K, seed=8)
+    pos = torch.arange(M, dtype=torch.int32) % MAXS
+    slot = torch.arange(M, dtype=torch.int32)
+    slot[7] = -1
+    cos_sin = R.rope_tables(MAXS, D, 500000.0)
+    dt = torch.uint8 if kv == "fp8" else torch.bfloat16
+    kc = torch.zeros(S, Hkv, MAXS, D, dtype=dt)
+    vc = torch.zeros_like(kc)
+    kc_g, vc_g = kc.cuda(), vc.cuda()
+    work = torch.empty(16 * M * (Hq + 2 * Hkv) * D, dtype=torch.float32, device="cuda")
+    q = hip.wgemm_mx_rope_kv(aq, as_, wq, ws, pos.cuda(), slot.cuda(), cos_sin.cuda(), kc_g, vc_g, Hq, work)
+    rq = R.rope_kv(ref.to(torch.bfloat16), pos, slot, cos_sin, kc, vc, Hq)
+    torch.testing.assert_close(q.float().cpu(), rq.float(), atol=3e-2, rtol=2e-2)
+    tol = dict(atol=0.07, rtol=0.07) if kv == "fp8" else dict(atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(R.kv_float(kc_g.cpu()), R.kv_float(kc), **tol)
+    torch.testing.assert_close(R.kv_float(vc_g.cpu()), R.kv_float(vc), **tol)
+
+
+def test_model_decode_fp8_agrees_with_bf16(hip):
+    """decode_dtype fp8 on the GPU kernels (2-layer model of the 1B dims):
+    a 320-row step's hidden rows close to the bf16 step's, greedy ids mostly
+    equal; the graph-captured engine runs on it."""
+    from dmcp.models.llm import LocalLM, preset
+    cfg = dict(layers=2, max_batch=320, max_rows=384, max_seq=1024, kv_dtype="fp8")
+    a = LocalLM(preset("dmcp-coder-1b", **cfg), device="cuda", seed=6)
+    b = LocalLM(preset("dmcp-coder-1b", decode_dtype="fp8", **cfg), device="cuda", seed=6)
+    g = torch.Generator().manual_seed(1)
+    B = 320
+    for m in (a, b):
+        m.prefill_batch([(torch.randint(0, 256, (40,), generator=g).tolist(), s, 0) for s in range(8)])
+    toks = torch.randint(0, 256, (B,), generator=g, dtype=torch.int32).cuda()
+    slots = (torch.arange(B, dtype=torch.int32) % 8).cuda()
+    pos = (40 + torch.arange(B, dtype=torch.int32) // 8).cuda()
+    la, lb = a.decode(toks, slots, pos).float(), b.decode(toks, slots, pos).float()
+    cos = torch.nn.functional.cosine_similarity(la, lb, dim=-1)
+    assert cos.min().item() > 0.97, cos.min()
+    assert (la.argmax(-1) == lb.argmax(-1)).float().mean().item() > 0.6

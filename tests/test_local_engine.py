@@ -459,3 +459,34 @@ def test_prefill_fp8_close_to_bf16():
     eng = LocalEngine(b, use_graphs=False)
     out = eng.generate(_inputs(3), "readme")
     assert all(json.loads(o) for o in out)
+
+
+def test_decode_fp8_greedy_agreement_with_bf16():
+    """decode_dtype fp8 (e4m3 weights x MXFP8 activations; the CPU references
+    of csrc/pgemm.hip's decode GEMM) against bf16 decode of the same weights:
+    the step's final hidden rows stay close, greedy tokens mostly agree, and
+    the engine's replies stay valid JSON."""
+    cfg = dict(max_batch=4, max_rows=16, max_seq=2048)
+    a = LocalLM(preset("tiny", **cfg), device="cpu", seed=5)
+    b = LocalLM(preset("tiny", decode_dtype="fp8", **cfg), device="cpu", seed=5)
+    assert b.decode_fp8 and not b.prefill_fp8
+    prompt = [256] + list(b"public class Agreement { void run() {} }")
+    for m in (a, b):
+        m.prefill_batch([(prompt, 0, 0)])
+    # 20 greedy steps: each model from its own token (the usual fp8 deployment check)
+    ta, tb = [65], [65]
+    agree = 0
+    for step in range(20):
+        p = len(prompt) + step
+        la = a.decode(torch.tensor([ta[-1]], dtype=torch.int32), torch.tensor([0], dtype=torch.int32),
+                      torch.tensor([p], dtype=torch.int32)).float()
+        lb = b.decode(torch.tensor([tb[-1]], dtype=torch.int32), torch.tensor([0], dtype=torch.int32),
+                      torch.tensor([p], dtype=torch.int32)).float()
+        if step == 0:
+            assert torch.nn.functional.cosine_similarity(la, lb, dim=-1).item() > 0.98
+        ta.append(int(la.argmax()))
+        tb.append(int(lb.argmax()))
+        agree += ta[-1] == tb[-1]
+    assert agree >= 14, (ta, tb)
+    out = LocalEngine(b, use_graphs=False).generate(_inputs(3), "readme")
+    assert all(json.loads(o) for o in out)

@@ -52,6 +52,36 @@ for s in $STEPS; do
         pgemm_test) run pgemm_test 300 python -u -m pytest tests/test_gpu_pgemm.py -x -v --timeout 120 \
                 --timeout-method thread ;;
         pgemm_bench) run pgemm_bench 300 python scripts/bench_pgemm.py --preset llama3.2-1b-code --rows 24576 ;;
+        enrich_llama_fp8) run enrich_llama_fp8 900 python bench_enrich.py --preset llama3.2-1b-code --kv-dtype fp8 \
+                --prefill-dtype fp8 --decode-dtype fp8 ;;
+        enrich_llama_pf8) run enrich_llama_pf8 900 python bench_enrich.py --preset llama3.2-1b-code --kv-dtype fp8 \
+                --prefill-dtype fp8 ;;
+        step_fp8)
+            for r in "256 64" "448 64"; do set -- $r
+                run step_bf16_$(($1 + $2)) 300 python scripts/bench_step.py --batch $1 --extra $2 --kv-dtype fp8 --iters 60
+                run step_fp8_$(($1 + $2)) 300 python scripts/bench_step.py --batch $1 --extra $2 --kv-dtype fp8 \
+                    --decode-dtype fp8 --iters 60
+            done ;;
+        prof_prefill)
+            ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$ROOT/$OUT/prof_prefill" -o pf -- python3 "$ROOT/scripts/bench_prefill.py" \
+                --preset llama3.2-1b-code --prefix 1119 --tokens 561 --seqs 44 --iters 5 --prefill-dtype fp8 \
+                > "$ROOT/$OUT/prof_prefill.log" 2>&1 )
+            rc=$?
+            echo "=== prof_prefill rc=$rc"
+            find "$OUT/prof_prefill" -type f ! -name '*kernel_stats*' -delete 2>/dev/null
+            cp $(find "$OUT/prof_prefill" -name '*kernel_stats.csv' | head -1) "$OUT/prefill_fp8_kernel_stats.csv"
+            tail -2 "$OUT/prof_prefill.log"
+            [ $rc -eq 0 ] || exit $rc ;;
+        prefill_llama)
+            run prefill_llama_bf16 300 python scripts/bench_prefill.py --preset llama3.2-1b-code --prefix 1119 \
+                --tokens 561 --seqs 44 --iters 5
+            run prefill_llama_fp8 300 python scripts/bench_prefill.py --preset llama3.2-1b-code --prefix 1119 \
+                --tokens 561 --seqs 44 --iters 5 --prefill-dtype fp8 ;;
+        pmc_llama) run pmc_llama 900 bash scripts/pmc_decode_step.sh --preset llama3.2-1b-code --batch 256 \
+                --extra 64 --kv-dtype fp8 --prefix 1119 --ctx 700 ;;
+        pmc_llama_fp8) run pmc_llama_fp8 900 bash scripts/pmc_decode_step.sh --preset llama3.2-1b-code \
+                --batch 256 --extra 64 --kv-dtype fp8 --prefix 1119 --ctx 700 --decode-dtype fp8 ;;
         enrich_fp8_nofork) run enrich_fp8_nofork 900 python bench_enrich.py --kv-dtype fp8 --no-fork ;;
         step_llama)
             run step_llama533 300 python scripts/bench_step.py --preset llama3.2-1b-code --batch 512 --extra 21 \

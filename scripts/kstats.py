@@ -5,13 +5,22 @@
 """
 import collections
 import csv
+import re
 import sys
 
-CATS = [("wgemm_swiglu", "wgemm_kernel<128"), ("wgemm", "wgemm_kernel"), ("wgemm_reduce", "reduce_"),
+CATS = [("lm_head_argmax", re.compile(r"wgemm_kernel<\d+, \d+, \d+, 3|lm_head_reduce")),
+        ("wgemm_swiglu", re.compile(r"wgemm_kernel<\d+, \d+, \d+, 2")), ("wgemm", "wgemm_kernel"),
+        ("wmx_swiglu(fp8)", re.compile(r"wmx_kernel<\d+, \d+, 2")), ("wmx(fp8)", "wmx_kernel"),
+        ("pgemm(fp8)", "pgemm_kernel"), ("mx_quant", re.compile(r"mx_quant|rmsnorm_mx|resid_norm_mx")),
+        ("wgemm_reduce", "reduce_"),
         ("attn_prefix(mfma)", "prefill_attn_kernel"), ("prefill_varlen", "prefill_varlen"),
         ("gemm(hipblaslt)", "Cijk"), ("fused_gemm", "fused_gemm"), ("attn_combine", "combine"),
         ("attn_per_row", "decode_attn_"), ("rmsnorm", "rmsnorm"), ("silu", "silu"),
         ("rope", "rope"), ("embedding", "embedding"), ("argmax", "argmax")]
+
+
+def _match(key, name: str) -> bool:
+    return key.search(name) is not None if hasattr(key, "search") else key in name
 
 
 def main() -> int:
@@ -24,7 +33,7 @@ def main() -> int:
         if "decode_attn_" in name and "combine" not in name:
             steps = int(r["Calls"]) // layers
         for c, key in CATS:
-            if key in name:
+            if _match(key, name):
                 cat[c] += t
                 break
         else:

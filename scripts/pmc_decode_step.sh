@@ -17,16 +17,20 @@ for set in "${SETL[@]}"; do
         -- python3 "$ROOT/scripts/bench_step.py" --iters 20 "$@" > "$ROOT/gpurun_out/pmcd$i.log" 2>&1 || exit $?
 done
 python3 - "$ROOT/gpurun_out" <<'PY'
-import csv, glob, sys, collections
+import csv, glob, re, sys, collections
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 calls = collections.Counter()
 for f in glob.glob(sys.argv[1] + "/pmcd*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = r.get("Kernel_Name", "?")
+        mode = re.search(r"wgemm_kernel<\d+, \d+, \d+, (\d)", k)
         k = ("prefix" if "prefill_attn" in k else "decode_mfma" if "decode_attn_mfma" in k else
              "combine" if "combine" in k else "gemm_lib" if "Cijk" in k else "rmsnorm" if "rmsnorm" in k else
-             "wgemm_swiglu" if "wgemm_kernel<128" in k else "wgemm" if "wgemm_kernel" in k else
-             "reduce" if "reduce_" in k else "other")
+             "lm_head_argmax" if (mode and mode.group(1) == "3") or "lm_head_reduce" in k else
+             "wgemm_swiglu" if mode and mode.group(1) == "2" else "wgemm" if "wgemm_kernel" in k else
+             "wmx_swiglu" if "wmx_kernel<64, 1, 2" in k or "wmx_kernel<64, 2, 2" in k else
+             "wmx" if "wmx_kernel" in k else "pgemm" if "pgemm_kernel" in k else
+             "reduce" if "reduce_" in k else "mx_quant" if "mx_quant" in k else "other")
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
 for k, d in sorted(agg.items()):
     print(k, {c: f"{v:.3g}" for c, v in sorted(d.items())})

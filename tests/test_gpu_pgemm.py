@@ -283,3 +283,22 @@ def test_model_decode_fp8_agrees_with_bf16(hip):
     cos = torch.nn.functional.cosine_similarity(la, lb, dim=-1)
     assert cos.min().item() > 0.97, cos.min()
     assert (la.argmax(-1) == lb.argmax(-1)).float().mean().item() > 0.6
+
+
+def test_engine_on_fp8_prefill_and_decode(hip):
+    """The graph-captured engine on a model with fp8 prefill and fp8 decode
+    (2 layers of the 1B dims): valid replies that name every method."""
+    import json
+    from dmcp.enrich.local import LocalEngine
+    from dmcp.enrich.types import EnrichmentInput
+    from dmcp.models.llm import LocalLM, preset
+    m = LocalLM(preset("dmcp-coder-1b", layers=2, max_batch=32, max_rows=64, max_seq=2048, kv_dtype="fp8",
+                       prefill_dtype="fp8", decode_dtype="fp8"), device="cuda", seed=2)
+    eng = LocalEngine(m)
+    inputs = [EnrichmentInput("class C%d { void run() {} int size() { return 0; } }" % i, f"co.acme.C{i}", "java",
+                              "SERVICE", ["run", "size"][: 1 + i % 2]) for i in range(40)]
+    raw = eng.generate(inputs, "readme of the project")
+    for r, inp in zip(raw, inputs):
+        doc = json.loads(r)
+        assert [x["methodName"] for x in doc["methods"]] == inp.method_names
+    assert eng.stats["decode_steps"] > 0

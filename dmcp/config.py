@@ -60,6 +60,7 @@ class Config:
     # decode each method of a class as its own sequence from the class head's
     # KV (a class's latency: head + longest method, not all methods in a row)
     local_llm_fork_methods: bool = True
+    local_llm_fork_max_context: int = 1536
     local_llm_devices: str = "all"
     # "process": one worker process per GPU, started before this process
     # touches HIP (the service default); "inline": engines in this process
@@ -131,6 +132,7 @@ class Config:
             "LOCAL_LLM_DECODE_DTYPE": "local_llm_decode_dtype",
             "LOCAL_LLM_MAX_NEW_TOKENS": "local_llm_max_new_tokens",
             "LOCAL_LLM_FORK_METHODS": "local_llm_fork_methods",
+            "LOCAL_LLM_FORK_MAX_CONTEXT": "local_llm_fork_max_context",
             "LOCAL_LLM_DEVICES": "local_llm_devices",
             "LOCAL_LLM_WORKERS": "local_llm_workers",
             "LOCAL_LLM_MAX_BATCH": "local_llm_max_batch",

@@ -287,6 +287,7 @@ class _Seq:
     h: int = -1                          # its state in the native grammar engine (-1: Python state)
     branches: Optional[List[List[Segment]]] = None  # a class head: its method branches (forked when it finishes)
     fork: Optional["_Fork"] = None       # a method branch: the fork it belongs to
+    forked: bool = False                 # head or branch of a forked class (replies merge as branches)
 
     _free_budget: int = -1
 
@@ -378,7 +379,7 @@ class LocalEngine:
                  jump_forward: bool = True, shared_prefix: bool = True, pipeline: bool = True,
                  admit_min: Optional[int] = None, longest_first: bool = True, tokenizer=None,
                  max_new_tokens: Optional[int] = None, native_grammar: Optional[bool] = None,
-                 fork_methods: bool = True) -> None:
+                 fork_methods: bool = True, fork_max_context: int = 1536) -> None:
         self.model = model
         self.tok = tokenizer if tokenizer is not None else ByteTokenizer(model.cfg.vocab_size)
         self._tb = self.tok.token_bytes
@@ -400,6 +401,12 @@ class LocalEngine:
         # method instead of all its methods in a row (small projects are
         # latency-bound: rows per step far below capacity)
         self.fork_methods = fork_methods
+        # ... unless the class's own context (prompt after the shared prefix)
+        # is longer than this: every branch starts with a copy of that KV
+        # (16 KB per token per slot at fp8 for the 1B shapes), and at ~2,400
+        # own tokens (the byte-level preset) the copies cost more than the
+        # shorter chain saves (60 vs 68 classes/s, profiles/enrich_fp8_r4_forks.jsonl)
+        self.fork_max_context = int(fork_max_context)
         self.cfg: LMConfig = model.cfg
         # reply budget: the caller's max_new_tokens, within what the KV slot
         # leaves next to a useful prompt
@@ -428,7 +435,7 @@ class LocalEngine:
                       "prefix_s": 0.0, "host_s": 0.0, "wait_s": 0.0, "launch_s": 0.0, "prefill_gpu_s": 0.0,
                       "reply_parts": 0,
                       "split_classes": 0, "methods_dropped": 0, "type_corrections": 0, "choice_waits": 0,
-                      "forks": 0, "fork_branches": 0, "fork_waits": 0}
+                      "forks": 0, "fork_branches": 0, "fork_waits": 0, "fork_skipped": 0}
         self._pf_events: List[tuple] = []  # (start, end) device events of the batched prefills
         self._lock = threading.Lock()
         self._frag_cache: Dict[bytes, List[int]] = {}      # forced text -> ids
@@ -680,7 +687,14 @@ class LocalEngine:
                 if q.h >= 0:
                     self._native.release(q.h)
                 raise
-            return [q]
+            if not branches or not self.fork_max_context or \
+                    len(q.prompt) - q.prefix_split <= self.fork_max_context:
+                q.forked = True
+                return [q]
+            if q.h >= 0:  # a long own context: its methods decode in one sequence
+                self._native.release(q.h)
+            self.stats["reply_parts"] -= 1
+            self.stats["fork_skipped"] += 1
         parts, dropped = plan_reply(inp.method_names, self.reply_budget)
         self.stats["methods_dropped"] += dropped
         self.stats["reply_parts"] += len(parts)
@@ -857,7 +871,7 @@ class LocalEngine:
         if any(r is None for r in got):
             return None
         del partials[s.index]
-        if self.fork_methods:
+        if s.forked:
             return merge_branches(got[0], got[1:])  # type: ignore[arg-type]
         return merge_parts(got)  # type: ignore[arg-type]
 
@@ -870,7 +884,7 @@ class LocalEngine:
         for slot in slots:
             j, segs = st.pending.popleft()
             q = _Seq(head.inp, head.index, segs, part=1 + j, n_parts=head.n_parts)
-            q.slot, q.pos, q.fork = slot, pos, st
+            q.slot, q.pos, q.fork, q.forked = slot, pos, st, True
             q.shared, q.prompt, q.prefix_split = head.shared, head.prompt, head.prefix_split
             kids.append(q)
         if src is not None and kids:

@@ -654,7 +654,8 @@ def model_spec(cfg) -> dict:
 def engine_spec(cfg) -> dict:
     """LocalEngine keyword arguments of a :class:`dmcp.config.Config`."""
     return {"max_new_tokens": int(cfg.local_llm_max_new_tokens),
-            "fork_methods": bool(getattr(cfg, "local_llm_fork_methods", True))}
+            "fork_methods": bool(getattr(cfg, "local_llm_fork_methods", True)),
+            "fork_max_context": int(getattr(cfg, "local_llm_fork_max_context", 1536))}
 
 
 # ------------------------------------------------------------------ child

@@ -790,14 +790,14 @@ int dmcp_rmsnorm_mx(void* resid, const void* add, const void* w, void* q, void* 
 
 // Decode GEMMs on MX fp8 (contract checked by dmcp/ops/hip.py, guarded here):
 // x MXFP8 [M, K] (+ [M, K / 32] scales), w e4m3 [N, K] + fp32 scales [N];
-// M <= 512, K % (64 S) == 0, rows / part <= 256.
+// M <= 1024, K % (64 S) == 0, rows / part <= 256.
 //   mode 1: part[S, M, N] fp32 partials (N % 64 == 0)
 //   mode 2: SwiGLU -> MXFP8 yq [M, I] + ys [M, I / 32]  (w = [gate; up] [2I, K], I % 32 == 0, S == 1)
 int dmcp_wgemm_mx(const void* xq, const void* xs, const void* wq, const void* ws, void* part, void* yq, void* ys,
                   int M, int N, int K, int S, int mparts, int mode, int I, void* stream) {
     if (M <= 0) return 0;
     const int mrows = (M + mparts - 1) / mparts;
-    if (!xq || !xs || !wq || !ws || M > 512 || S < 1 || mparts < 1 || K % (PBK * S) != 0 || mrows > 256 ||
+    if (!xq || !xs || !wq || !ws || M > 1024 || S < 1 || mparts < 1 || K % (PBK * S) != 0 || mrows > 256 ||
         (mode == 1 && (!part || N % 64 != 0)) || (mode == 2 && (!yq || !ys || S != 1 || I <= 0 || I % 32 != 0)) ||
         (mode != 1 && mode != 2))
         return hipErrorInvalidValue;

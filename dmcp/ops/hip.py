@@ -1000,7 +1000,9 @@ def mx_probe(a: torch.Tensor, b: torch.Tensor, sa: torch.Tensor, sb: torch.Tenso
 
 
 # ---- decode GEMMs on MX fp8 (csrc/pgemm.hip wmx_kernel) ---------------------
-WMX_MAX_ROWS = 512
+# a 768-row step (the engine's max_rows at 512 slots) stays on the MX kernel:
+# 3-6 M parts re-stream each weight tile from L2 instead of hipBLASLt's bf16
+WMX_MAX_ROWS = 1024
 def wmx_plan(M: int, N: int, K: int, swiglu: bool = False) -> tuple:
     """(K slices S, M parts) of the MX decode GEMM: parts of 256 or 128 staged
     rows, whichever stages fewer rows for M (each part re-streams its weight
@@ -1023,8 +1025,8 @@ def wmx_plan(M: int, N: int, K: int, swiglu: bool = False) -> tuple:
 def _wmx_args(xq, xs, wq, ws, name):
     M, K = _mx_args(xq, xs, name)
     N = _w8_args(wq, ws, K, name)
-    if not 1 <= M <= WGEMM_MAX_ROWS or N % 64:
-        raise HipOpsError(f"{name}: needs 1 <= M <= {WGEMM_MAX_ROWS}, N % 64 == 0 (M={M} N={N})")
+    if not 1 <= M <= WMX_MAX_ROWS or N % 64:
+        raise HipOpsError(f"{name}: needs 1 <= M <= {WMX_MAX_ROWS}, N % 64 == 0 (M={M} N={N})")
     return M, K, N
 
 

@@ -201,7 +201,7 @@ def test_model_prefill_fp8_close_to_bf16(hip, kv):
 
 
 # ---- decode: the MX weight-streaming GEMM (wmx_kernel) at decode row counts
-DEC_ROWS = [17, 78, 129, 256, 320, 448, 512]
+DEC_ROWS = [17, 78, 129, 256, 320, 448, 512, 533, 768]
 
 
 @pytest.mark.parametrize("M", DEC_ROWS)

@@ -449,6 +449,7 @@ class LocalEngine:
         import numpy as np
         self._stage = np.zeros((7, self.max_rows), dtype=np.int32)  # the native builder's step rows
         self._host_np = [h.numpy() for h in self._host_ids]
+        self._ids_events = [torch.cuda.Event(), torch.cuda.Event()] if dev.type == "cuda" else [None, None]
 
     # ---------------------------------------------------------------- api
     def generate(self, inputs: Sequence[EnrichmentInput], readme: Optional[str]) -> List[str]:
@@ -829,7 +830,7 @@ class LocalEngine:
         host = self._host_ids[buf]
         host[:n].copy_(ids[:n], non_blocking=self.model.device.type == "cuda")
         if self.model.device.type == "cuda":
-            ev = torch.cuda.Event()
+            ev = self._ids_events[buf]  # reused: the step that last recorded it was waited for
             ev.record()
             return ev
         return None
@@ -851,7 +852,7 @@ class LocalEngine:
         host = self._host_ids[buf]
         host[:n].copy_(ids[:n], non_blocking=self.model.device.type == "cuda")
         if self.model.device.type == "cuda":
-            ev = torch.cuda.Event()
+            ev = self._ids_events[buf]  # reused: the step that last recorded it was waited for
             ev.record()
             return ev
         return None

@@ -186,23 +186,33 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     };
 
+    // every fragment of the stage first (16 ds_read_b128 + 4 scale bytes, 68
+    // VGPRs), then the 16 MFMAs back to back: one exposed LDS latency per
+    // stage -- reading each A fragment just before its 4 MFMAs put a full
+    // wait (lgkmcnt(0)) behind every group at one wave per SIMD.  (Reading
+    // stage c + 1 into a second register set during stage c's MFMAs needs
+    // 68 more VGPRs: hipcc spilled ~335 registers.)
     auto compute = [&](int st) {
         const uint8_t* A = plds + st * PST_BYTES;
         const uint8_t* B = A + PA_BYTES;
         const uint8_t* S = B + PB_BYTES;
-        v8i_t bf[4];
+        v8i_t bf[4], af[4];
+        int sa[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) bf[u] = frag(B, wn * 128 + u * 32 + l32);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int r = wm * 128 + t * 32 + l32;
-            const v8i_t af = frag(A, r);
-            const int sa = S[r * 2 + hh];
+            af[t] = frag(A, r);
+            sa[t] = S[r * 2 + hh];
+        }
+        __builtin_amdgcn_sched_barrier(0);  // the scheduler would sink the reads back to their uses
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-                acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af, bf[u], acc[t][u], 0, 0, 0, sa, 0,
-                                                                            127);
-        }
+                acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[t], bf[u], acc[t][u], 0, 0, 0, sa[t],
+                                                                            0, 127);
     };
 
     const int chunks = K / PBK;

@@ -31,7 +31,8 @@
 // [rows][4 x 16 B] LDS images with chunk j of row r in slot j ^ ((r >> 2) & 3)
 // (the swizzle on the DMA's source address): the 16 lanes of a ds_read_b128
 // pass cover all 64 banks.  The A scales of a stage ride the same ring
-// (a 2-byte LDS-DMA per lane), so the loop issues only one kind of load.
+// (a 2-byte LDS-DMA per lane, landing as a dword), so the loop issues only one
+// kind of load.
 // Blocks are remapped so each XCD runs a contiguous range of tiles, grouped 8
 // M tiles at a time (its 32 CUs share 8 A panels and 4 W tiles in L2).
 //
@@ -53,7 +54,11 @@ typedef int v4i_t __attribute__((ext_vector_type(4)));
 constexpr int PBM = 256, PBN = 256, PBK = 64, PST = 4, PTH = 256;
 constexpr int PA_BYTES = PBM * PBK;                     // A image of a stage
 constexpr int PB_BYTES = PBN * PBK;                     // W image
-constexpr int PS_BYTES = PBM * 2;                       // A scales of the stage: [row][2 blocks]
+// A scales of the stage: a 2-byte LDS-DMA still writes a DWORD per lane (the
+// value zero-extended; measured -- with 2-byte spacing each wave's upper
+// lanes overwrote the next wave's slots and the last wave's the next stage's
+// A image), so row r's 2 bytes sit at 4 r
+constexpr int PS_BYTES = PBM * 4;
 constexpr int PST_BYTES = PA_BYTES + PB_BYTES + PS_BYTES;
 constexpr int PGL = 9;                                  // LDS-DMA instructions per wave per stage
 constexpr int PM_BF16 = 0, PM_RESID = 1, PM_SWIGLU = 2, PM_QKV = 3;
@@ -164,7 +169,7 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int i = 0; i < 4; ++i) pglds<16>(asrc[i] + c * PBK, base + (wv * 4 + i) * 1024);
 #pragma unroll
         for (int i = 0; i < 4; ++i) pglds<16>(wsrc[i] + c * PBK, base + PA_BYTES + (wv * 4 + i) * 1024);
-        pglds<2>(ssrc + c * 2, base + PA_BYTES + PB_BYTES + wv * 128);
+        pglds<2>(ssrc + c * 2, base + PA_BYTES + PB_BYTES + wv * 256);
     };
 
     f32x16_t acc[4][4];
@@ -186,48 +191,76 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     };
 
-    // every fragment of the stage first (16 ds_read_b128 + 4 scale bytes, 68
-    // VGPRs), then the 16 MFMAs back to back: one exposed LDS latency per
-    // stage -- reading each A fragment just before its 4 MFMAs put a full
-    // wait (lgkmcnt(0)) behind every group at one wave per SIMD.  (Reading
-    // stage c + 1 into a second register set during stage c's MFMAs needs
-    // 68 more VGPRs: hipcc spilled ~335 registers.)
-    auto compute = [&](int st) {
-        const uint8_t* A = plds + st * PST_BYTES;
+    // One K stage per step, one basic block: wait for stage c (two newer
+    // stages in flight) + raw barrier; the fragment reads of tiles t = 0, 1
+    // and all of B (14 LDS ops); then the 16 MFMAs with the 9 LDS-DMA pieces
+    // of stage c + 3 threaded one per MFMA and the reads of tiles 2, 3 after
+    // the first four -- an LDS-DMA costs ~60 issue cycles
+    // (MI355X_MICROARCH.md), hidden behind a 64-cycle MFMA instead of
+    // serialised ahead of them (sched_barrier pins the order).  The refill is
+    // unconditional (past the last stage it re-reads it into the free slot,
+    // keeping the block branch-free and the wait count constant).
+    auto piece = [&](int i, int cc, int st) {
+        uint8_t* base = plds + st * PST_BYTES;
+        if (i < 4) pglds<16>(asrc[i] + cc * PBK, base + (wv * 4 + i) * 1024);
+        else if (i < 8) pglds<16>(wsrc[i - 4] + cc * PBK, base + PA_BYTES + (wv * 4 + i - 4) * 1024);
+        else pglds<2>(ssrc + cc * 2, base + PA_BYTES + PB_BYTES + wv * 256);
+    };
+    const int chunks = K / PBK;
+#pragma unroll
+    for (int j = 0; j < PST - 1; ++j) issue(min(j, chunks - 1), j);
+    for (int c = 0; c < chunks; ++c) {
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(PGL * (PST - 2)) : "memory");
+        const uint8_t* A = plds + (c % PST) * PST_BYTES;
         const uint8_t* B = A + PA_BYTES;
         const uint8_t* S = B + PB_BYTES;
+        const int cn = min(c + PST - 1, chunks - 1), sn = (c + PST - 1) % PST;
         v8i_t bf[4], af[4];
         int sa[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) bf[u] = frag(B, wn * 128 + u * 32 + l32);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
+        for (int t = 0; t < 2; ++t) {
             const int r = wm * 128 + t * 32 + l32;
             af[t] = frag(A, r);
-            sa[t] = S[r * 2 + hh];
+            sa[t] = S[r * 4 + hh];
         }
-        __builtin_amdgcn_sched_barrier(0);  // the scheduler would sink the reads back to their uses
+        auto mma = [&](int t, int u) {
+            acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[t], bf[u], acc[t][u], 0, 0, 0, sa[t], 0,
+                                                                        127);
+        };
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[t], bf[u], acc[t][u], 0, 0, 0, sa[t],
-                                                                            0, 127);
-    };
-
-    const int chunks = K / PBK;
-#pragma unroll
-    for (int j = 0; j < PST - 1; ++j)
-        if (j < chunks) issue(j, j);
-    for (int c = 0; c < chunks; ++c) {
-        if (c + PST - 2 < chunks) {
-            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(PGL * (PST - 2)) : "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        for (int u = 0; u < 4; ++u) {
+            __builtin_amdgcn_sched_barrier(0);
+            mma(0, u);
+            __builtin_amdgcn_sched_barrier(0);
+            piece(u, cn, sn);
         }
-        if (c + PST - 1 < chunks) issue(c + PST - 1, (c + PST - 1) % PST);
-        compute(c % PST);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 2; t < 4; ++t) {
+            const int r = wm * 128 + t * 32 + l32;
+            af[t] = frag(A, r);
+            sa[t] = S[r * 4 + hh];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            __builtin_amdgcn_sched_barrier(0);
+            mma(1, u);
+            __builtin_amdgcn_sched_barrier(0);
+            piece(4 + u, cn, sn);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mma(2, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        piece(8, cn, sn);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 1; u < 4; ++u) mma(2, u);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) mma(3, u);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the refills past the last stage, before the LDS is reused
     __syncthreads();  // the ring is free: the epilogue stages this wave's tile in it
 
     // ---- epilogue.  Lane (l32, hh) holds column l32 of rows (i & 3) + 8 (i >> 2)
@@ -241,6 +274,12 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         return img + r * PEPI_ROW + ((((byte >> 4) ^ (r & 15)) << 4) | (byte & 15));
     };
     const int mw = m0 + wm * 128;  // first row of this wave's tile
+    // The register phase only converts and writes LDS; the store phase's
+    // global loads (residual rows, positions, RoPE tables) are batched, since
+    // at one wave per SIMD nothing else hides their latency.
+    auto put = [&](int rr, int col, float v) {  // bf16 of v at image (row rr, column col)
+        *reinterpret_cast<uint16_t*>(ea(rr, col * 2)) = f2bf(v);
+    };
     if constexpr (MODE == PM_BF16 || MODE == PM_RESID) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -248,31 +287,40 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
             for (int t = 0; t < 4; ++t)
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int rr = t * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-                    *reinterpret_cast<uint16_t*>(ea(rr, (u * 32 + l32) * 2)) = f2bf(acc[t][u][i] * sc);
-                }
+                for (int i = 0; i < 16; ++i)
+                    put(t * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh, u * 32 + l32, acc[t][u][i] * sc);
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
         __builtin_amdgcn_wave_barrier();
         const int n0 = nt * PBN + wn * 128;
-        // 16 lanes per row (8 bf16 each), 4 rows per pass
-#pragma unroll 4
-        for (int p = 0; p < 32; ++p) {
-            const int rr = p * 4 + (lane >> 4);
-            const int m = mw + rr;
-            if (m >= M) continue;
-            const uint4 v = *reinterpret_cast<const uint4*>(ea(rr, (lane & 15) * 16));
-            uint4* dst = reinterpret_cast<uint4*>(e.y + (size_t)m * N + n0 + (lane & 15) * 8);
-            if constexpr (MODE == PM_RESID) {
-                float a[8], r[8];
-                unpack8(v, a);
-                unpack8(*dst, r);
+        // 16 lanes per row (8 bf16 each), 4 rows per pass; 8 passes per batch
 #pragma unroll
-                for (int j = 0; j < 8; ++j) a[j] += r[j];
-                *dst = pack8(a);
-            } else {
-                *dst = v;
+        for (int p0 = 0; p0 < 32; p0 += 8) {
+            uint4 r[8];
+            if constexpr (MODE == PM_RESID) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int m = min(mw + (p0 + q) * 4 + (lane >> 4), M - 1);
+                    r[q] = *reinterpret_cast<const uint4*>(e.y + (size_t)m * N + n0 + (lane & 15) * 8);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int rr = (p0 + q) * 4 + (lane >> 4);
+                const int m = mw + rr;
+                const uint4 v = *reinterpret_cast<const uint4*>(ea(rr, (lane & 15) * 16));
+                if (m >= M) continue;
+                uint4* dst = reinterpret_cast<uint4*>(e.y + (size_t)m * N + n0 + (lane & 15) * 8);
+                if constexpr (MODE == PM_RESID) {
+                    float a[8], b2[8];
+                    unpack8(v, a);
+                    unpack8(r[q], b2);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) a[j] += b2[j];
+                    *dst = pack8(a);
+                } else {
+                    *dst = v;
+                }
             }
         }
     } else if constexpr (MODE == PM_SWIGLU) {
@@ -287,81 +335,107 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             for (int t = 0; t < 4; ++t)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    const int rr = t * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
                     // gate / up rounded to bf16 as the bf16 GEMM's outputs are
                     const float g = bf2f(f2bf(acc[t][u][i] * sg)), uu = bf2f(f2bf(acc[t][u + 2][i] * su));
-                    const float a = psilu(g) * uu;
-                    float amax = __builtin_fabsf(a);
-#pragma unroll
-                    for (int msk = 1; msk < 32; msk <<= 1)
-                        amax = __builtin_fmaxf(amax, __shfl_xor(amax, msk, kWave));
-                    const int ex = mx_exp(amax);
-                    *ea(rr, u * 32 + l32) = to_fp8(ldexpf(a, -ex));
-                    const int m = mw + rr;
-                    if (l32 == 0 && m < M) e.ys[(size_t)m * isb + (j >> 5)] = (uint8_t)(ex + 127);
+                    put(t * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh, u * 32 + l32, psilu(g) * uu);
                 }
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
-        // 4 lanes per row (16 B each), 16 rows per pass
-#pragma unroll 2
-        for (int p = 0; p < 8; ++p) {
-            const int rr = p * 16 + (lane >> 2);
+        // 8 lanes per row (8 values each: lanes 4k..4k+3 are one 32-column
+        // block), 8 rows per pass: block max over 4 lanes, e4m3 bytes, E8M0
+#pragma unroll 4
+        for (int p = 0; p < 16; ++p) {
+            const int rr = p * 8 + (lane >> 3);
             const int m = mw + rr;
-            if (m >= M) continue;
-            *reinterpret_cast<uint4*>(e.yq + (size_t)m * e.I + j0 + (lane & 3) * 16) =
-                *reinterpret_cast<const uint4*>(ea(rr, (lane & 3) * 16));
+            float a[8];
+            unpack8(*reinterpret_cast<const uint4*>(ea(rr, (lane & 7) * 16)), a);
+            float amax = 0.f;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) amax = __builtin_fmaxf(amax, __builtin_fabsf(a[q]));
+            amax = __builtin_fmaxf(amax, __shfl_xor(amax, 1, kWave));
+            amax = __builtin_fmaxf(amax, __shfl_xor(amax, 2, kWave));
+            const int ex = mx_exp(amax);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) a[q] = ldexpf(a[q], -ex);
+            if (m < M) {
+                *reinterpret_cast<uint2*>(e.yq + (size_t)m * e.I + j0 + (lane & 7) * 8) =
+                    make_uint2(pack_fp8x4(a), pack_fp8x4(a + 4));
+                if ((lane & 3) == 0) e.ys[(size_t)m * isb + (j0 >> 5) + ((lane & 7) >> 2)] = (uint8_t)(ex + 127);
+            }
         }
     } else {  // PM_QKV: the wave's 128 columns are two heads; tiles 2 g, 2 g + 1 = d 0..31, 32..63 of head g
         const int h0 = (nt * PBN + wn * 128) >> 6;
 #pragma unroll
-        for (int g = 0; g < 2; ++g) {
-            const int n = nt * PBN + wn * 128 + g * 64 + l32;
-            const float s1 = ws[n], s2 = ws[n + 32];
-            const bool rope = h0 + g < e.Hq + e.Hkv;
+        for (int u = 0; u < 4; ++u) {
+            const float sc = ws[nt * PBN + wn * 128 + u * 32 + l32];
 #pragma unroll
             for (int t = 0; t < 4; ++t)
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int rr = t * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-                    const int m = min(mw + rr, M - 1);
-                    const float x1 = bf2f(f2bf(acc[t][2 * g][i] * s1)), x2 = bf2f(f2bf(acc[t][2 * g + 1][i] * s2));
-                    float o1 = x1, o2 = x2;
-                    if (rope) {
-                        const int p = e.pos[m];
-                        const float2 cs = e.cos_sin[(size_t)min(max(p, 0), e.max_pos - 1) * 32 + l32];
-                        o1 = x1 * cs.x - x2 * cs.y;
-                        o2 = x2 * cs.x + x1 * cs.y;
-                    }
-                    *reinterpret_cast<uint16_t*>(ea(rr, g * 128 + l32 * 2)) = f2bf(o1);
-                    *reinterpret_cast<uint16_t*>(ea(rr, g * 128 + 64 + l32 * 2)) = f2bf(o2);
-                }
+                for (int i = 0; i < 16; ++i)
+                    put(t * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh, u * 32 + l32, acc[t][u][i] * sc);
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
-        // per (row, head): 128 B of bf16 = 8 lanes x 16 B; 4 (row, head) pairs per pass
-#pragma unroll 4
-        for (int p = 0; p < 64; ++p) {
-            const int unit = p * 8 + (lane >> 3);  // (row, head) pair
-            const int rr = unit >> 1, g = unit & 1;
-            const int m = mw + rr;
-            if (m >= M) continue;
-            const int head = h0 + g;
-            const uint4 v = *reinterpret_cast<const uint4*>(ea(rr, g * 128 + (lane & 7) * 16));
-            if (head < e.Hq) {
-                *reinterpret_cast<uint4*>(e.q_out + ((size_t)m * e.Hq + head) * 64 + (lane & 7) * 8) = v;
-                continue;
+        // per (row, head): 8 lanes x 8 d; lane k's RoPE partner is chunk k ^ 4
+        // (d +- 32).  4 (row, head) units per pass, 8 passes per batch.
+        const int k = lane & 7;
+        const int dh = (k & 3) * 8;  // d mod 32 of this lane's 8 values
+#pragma unroll
+        for (int p0 = 0; p0 < 64; p0 += 8) {
+            int pos[8];
+            float4 cs[8][4];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int unit = (p0 + q) * 8 + (lane >> 3);
+                const int m = min(mw + (unit >> 1), M - 1);
+                pos[q] = e.pos[m];
+                const float4* t4 = reinterpret_cast<const float4*>(
+                    e.cos_sin + (size_t)min(max(pos[q], 0), e.max_pos - 1) * 32 + dh);
+#pragma unroll
+                for (int z = 0; z < 4; ++z) cs[q][z] = t4[z];
             }
-            const int pp = e.pos[m], sl = e.slot[m];
-            if (pp < 0 || pp >= e.max_seq || sl < 0 || sl >= e.num_slots) continue;
-            const bool isv = head >= e.Hq + e.Hkv;
-            const int kh = head - e.Hq - (isv ? e.Hkv : 0);
-            const size_t ofs = (((size_t)sl * e.Hkv + kh) * e.max_seq + pp) * 64 + (lane & 7) * 8;
-            void* cache = isv ? e.v_cache : e.k_cache;
-            if constexpr (KV8)
-                *reinterpret_cast<uint2*>(static_cast<uint8_t*>(cache) + ofs) = bf16x8_to_fp8x8(v);
-            else
-                *reinterpret_cast<uint4*>(static_cast<uint16_t*>(cache) + ofs) = v;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int unit = (p0 + q) * 8 + (lane >> 3);
+                const int rr = unit >> 1, g = unit & 1;
+                const int m = mw + rr;
+                const int head = h0 + g;
+                float x[8], y[8];
+                unpack8(*reinterpret_cast<const uint4*>(ea(rr, g * 128 + k * 16)), x);
+                if (head < e.Hq + e.Hkv) {  // rotate-half RoPE: d < 32: x c - x' s; d >= 32: x c + x' s
+                    unpack8(*reinterpret_cast<const uint4*>(ea(rr, g * 128 + (k ^ 4) * 16)), y);
+                    const float sg = k < 4 ? -1.f : 1.f;
+#pragma unroll
+                    for (int z = 0; z < 4; ++z) {
+                        const float4 c4 = cs[q][z];  // (cos, sin) of d = dh + 2z, dh + 2z + 1
+                        const float o0 = x[2 * z] * c4.x + sg * y[2 * z] * c4.y;
+                        const float o1 = x[2 * z + 1] * c4.z + sg * y[2 * z + 1] * c4.w;
+                        x[2 * z] = o0;
+                        x[2 * z + 1] = o1;
+                    }
+                }
+                if (m >= M) continue;
+                const uint4 v = pack8(x);
+                if (head < e.Hq) {
+                    *reinterpret_cast<uint4*>(e.q_out + ((size_t)m * e.Hq + head) * 64 + k * 8) = v;
+                    continue;
+                }
+                const int pp = pos[q], sl = e.slot[m];
+                if (pp < 0 || pp >= e.max_seq || sl < 0 || sl >= e.num_slots) continue;
+                const bool isv = head >= e.Hq + e.Hkv;
+                const int kh = head - e.Hq - (isv ? e.Hkv : 0);
+                const size_t ofs = (((size_t)sl * e.Hkv + kh) * e.max_seq + pp) * 64 + k * 8;
+                void* cache = isv ? e.v_cache : e.k_cache;
+                if constexpr (KV8) {
+                    float f[8];
+                    for (int z = 0; z < 8; ++z) f[z] = x[z];
+                    *reinterpret_cast<uint2*>(static_cast<uint8_t*>(cache) + ofs) =
+                        make_uint2(pack_fp8x4(f), pack_fp8x4(f + 4));
+                } else {
+                    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(cache) + ofs) = v;
+                }
+            }
         }
     }
 }
@@ -389,7 +463,7 @@ __global__ __launch_bounds__(kBlock) void wmx_kernel(
     int M, int N, int K, int ks, int S, int ntiles, int mparts, int I) {
     constexpr int MR = MT * 128;                  // activation rows staged per block
     constexpr int NF = NB / 32;                   // weight tiles
-    constexpr int W_BYTES = NB * PBK, X_BYTES = MR * PBK, XS_BYTES = 4 * kWave * 2;
+    constexpr int W_BYTES = NB * PBK, X_BYTES = MR * PBK, XS_BYTES = 4 * kWave * 4;  // a dword per lane (see PS_BYTES)
     constexpr int STB = W_BYTES + X_BYTES + XS_BYTES;
     constexpr int WI = NB / 64;                   // 1-KiB weight pieces per wave per stage
     constexpr int XI = MR / 64;                   // activation pieces per wave
@@ -444,7 +518,7 @@ __global__ __launch_bounds__(kBlock) void wmx_kernel(
         for (int i = 0; i < WI; ++i) pglds<16>(wsrc[i] + c * PBK, base + (wv * WI + i) * 1024);
 #pragma unroll
         for (int i = 0; i < XI; ++i) pglds<16>(xsrc[i] + c * PBK, base + W_BYTES + (wv * XI + i) * 1024);
-        pglds<2>(ssrc + c * 2, base + W_BYTES + X_BYTES + wv * 128);
+        pglds<2>(ssrc + c * 2, base + W_BYTES + X_BYTES + wv * 256);
     };
 
     f32x16_t acc[NF][MT];
@@ -472,7 +546,7 @@ __global__ __launch_bounds__(kBlock) void wmx_kernel(
             const int r = wv * (MT * 32) + t * 32 + l32;  // staged activation row
             xf[t] = frag(X, r);
             // row r was fetched by wave r / (MR / 4), lane r % (MR / 4)
-            sx[t] = SX[(r / (MR / 4)) * 128 + (r % (MR / 4)) * 2 + hh];
+            sx[t] = SX[(r / (MR / 4)) * 256 + (r % (MR / 4)) * 4 + hh];
         }
 #pragma unroll
         for (int f = 0; f < NF; ++f) {

@@ -904,17 +904,23 @@ int dmcp_wgemm_mx(const void* xq, const void* xs, const void* wq, const void* ws
             wmx_kernel<64, 1, XM_PART, 4><<<grid, kBlock, 0, st>>>(xx, xsc, ww, wsc, (float*)part, nullptr, nullptr,
                                                                    M, N, K, ks, S, ntiles, mparts, 0);
     } else {
-        // 32 gate + 32 up rows per block: I / 32 tiles fill the chip at one M part
-        const int ntiles = I / 32;
+        // 64 gate + 64 up rows per block (half the activation re-staging of
+        // 32 + 32: at 320 rows the staged activation bytes were twice the
+        // weight bytes) once I / 64 tiles x parts fill the chip; else 32 + 32
+        const bool wide = I % 64 == 0 && (I / 64) * mparts >= 256;
+        const int ntiles = wide ? I / 64 : I / 32;
         const dim3 grid((unsigned)(ntiles * mparts));
-        if (mt == 2)
-            wmx_kernel<64, 2, XM_SWIGLU, 4><<<grid, kBlock, 0, st>>>(xx, xsc, ww, wsc, nullptr, (uint8_t*)yq,
-                                                                     (uint8_t*)ys, M, 2 * I, K, K, 1, ntiles,
-                                                                     mparts, I);
-        else
-            wmx_kernel<64, 1, XM_SWIGLU, 4><<<grid, kBlock, 0, st>>>(xx, xsc, ww, wsc, nullptr, (uint8_t*)yq,
-                                                                     (uint8_t*)ys, M, 2 * I, K, K, 1, ntiles,
-                                                                     mparts, I);
+#define DMCP_WMX_SW(NB, MT)                                                                                   \
+    wmx_kernel<NB, MT, XM_SWIGLU, 4><<<grid, kBlock, 0, st>>>(xx, xsc, ww, wsc, nullptr, (uint8_t*)yq,        \
+                                                              (uint8_t*)ys, M, 2 * I, K, K, 1, ntiles, mparts, I)
+        if (wide) {
+            if (mt == 2) DMCP_WMX_SW(128, 2);
+            else DMCP_WMX_SW(128, 1);
+        } else {
+            if (mt == 2) DMCP_WMX_SW(64, 2);
+            else DMCP_WMX_SW(64, 1);
+        }
+#undef DMCP_WMX_SW
     }
     return hipGetLastError();
 }

@@ -92,6 +92,17 @@ __device__ __forceinline__ uint32_t pack_fp8x4(const float* f) {
     return __builtin_amdgcn_cvt_pk_fp8_f32(fp8_sat(f[2]), fp8_sat(f[3]), lo, true);
 }
 
+// 4 floats rounded to bf16 first, then e4m3: the bytes of a K-cache append
+// (the reference rotates the bf16 projection in fp32, rounds to bf16, then
+// encodes; a direct fp32 -> e4m3 differs by one e4m3 step where the bf16
+// rounding lands on an e4m3 midpoint)
+__device__ __forceinline__ uint32_t pack_fp8x4_bf16r(const float* f) {
+    float r[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = bf2f(f2bf(f[i]));
+    return pack_fp8x4(r);
+}
+
 // 8 bf16 (uint4) -> 8 e4m3 bytes (uint2)
 __device__ __forceinline__ uint2 bf16x8_to_fp8x8(const uint4& v) {
     float f[8];

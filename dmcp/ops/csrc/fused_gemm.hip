@@ -263,8 +263,8 @@ __global__ __launch_bounds__(WK * kWave) void fused_gemm_kernel(FusedGemmArgs a)
             const size_t off = (((size_t)sl * a.Hkv + kv) * a.max_seq + p) * D;
             if (a.kv8) {
                 uint8_t* dst = static_cast<uint8_t*>(cache) + off;
-                *reinterpret_cast<uint32_t*>(dst + d0) = pack_fp8x4(o1);
-                *reinterpret_cast<uint32_t*>(dst + d0 + half) = pack_fp8x4(o2);
+                *reinterpret_cast<uint32_t*>(dst + d0) = pack_fp8x4_bf16r(o1);
+                *reinterpret_cast<uint32_t*>(dst + d0 + half) = pack_fp8x4_bf16r(o2);
             } else {
                 uint16_t* dst = static_cast<uint16_t*>(cache) + off;
                 *reinterpret_cast<uint2*>(dst + d0) = pack4(o1);

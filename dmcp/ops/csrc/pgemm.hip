@@ -293,19 +293,20 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
         __builtin_amdgcn_wave_barrier();
         const int n0 = nt * PBN + wn * 128;
-        // 16 lanes per row (8 bf16 each), 4 rows per pass; 8 passes per batch
+        // 16 lanes per row (8 bf16 each), 4 rows per pass; 16 passes per batch
+        // (the residual rows of a batch in flight together)
 #pragma unroll
-        for (int p0 = 0; p0 < 32; p0 += 8) {
-            uint4 r[8];
+        for (int p0 = 0; p0 < 32; p0 += 16) {
+            uint4 r[16];
             if constexpr (MODE == PM_RESID) {
 #pragma unroll
-                for (int q = 0; q < 8; ++q) {
+                for (int q = 0; q < 16; ++q) {
                     const int m = min(mw + (p0 + q) * 4 + (lane >> 4), M - 1);
                     r[q] = *reinterpret_cast<const uint4*>(e.y + (size_t)m * N + n0 + (lane & 15) * 8);
                 }
             }
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
+            for (int q = 0; q < 16; ++q) {
                 const int rr = (p0 + q) * 4 + (lane >> 4);
                 const int m = mw + rr;
                 const uint4 v = *reinterpret_cast<const uint4*>(ea(rr, (lane & 15) * 16));
@@ -377,63 +378,76 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
-        // per (row, head): 8 lanes x 8 d; lane k's RoPE partner is chunk k ^ 4
-        // (d +- 32).  4 (row, head) units per pass, 8 passes per batch.
-        const int k = lane & 7;
+        // Store phase: lane (r8, k) = (lane >> 3, lane & 7) takes rows qrow(P,
+        // r8) (P = 0..15) of the wave's 128, both heads of each, chunk k (8 d) of
+        // a head row; its RoPE partner is chunk k ^ 4 (d +- 32), and the two
+        // heads of a row share the row's (cos, sin).  Every global load is
+        // independent of the stores: the rows' positions and slots in one
+        // batch, then the table rows in two batches of 8 (one wave per SIMD:
+        // nothing else hides a dependent round trip).
+        const int k = lane & 7, r8 = lane >> 3;
         const int dh = (k & 3) * 8;  // d mod 32 of this lane's 8 values
+        const bool rope0 = h0 < e.Hq + e.Hkv, rope1 = h0 + 1 < e.Hq + e.Hkv;
+        const bool kv = h0 + 1 >= e.Hq;  // some head of this wave goes to the caches
+        // rows of lane groups r8 = 0 and 1 (one 16-lane LDS read group) 8 apart:
+        // their swizzled chunk sets are disjoint halves of the bank row
+        auto qrow = [&](int P) { return 16 * (P >> 1) + 8 * (r8 & 1) + (r8 >> 1) + 4 * (P & 1); };
+        int pos[16], sl[16];
 #pragma unroll
-        for (int p0 = 0; p0 < 64; p0 += 8) {
-            int pos[8];
+        for (int P = 0; P < 16; ++P) {
+            const int m = min(mw + qrow(P), M - 1);
+            pos[P] = e.pos[m];
+            sl[P] = kv ? e.slot[m] : -1;
+        }
+#pragma unroll
+        for (int P0 = 0; P0 < 16; P0 += 8) {
             float4 cs[8][4];
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
-                const int unit = (p0 + q) * 8 + (lane >> 3);
-                const int m = min(mw + (unit >> 1), M - 1);
-                pos[q] = e.pos[m];
                 const float4* t4 = reinterpret_cast<const float4*>(
-                    e.cos_sin + (size_t)min(max(pos[q], 0), e.max_pos - 1) * 32 + dh);
+                    e.cos_sin + (size_t)min(max(pos[P0 + q], 0), e.max_pos - 1) * 32 + dh);
 #pragma unroll
                 for (int z = 0; z < 4; ++z) cs[q][z] = t4[z];
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
-                const int unit = (p0 + q) * 8 + (lane >> 3);
-                const int rr = unit >> 1, g = unit & 1;
+                const int rr = qrow(P0 + q);
                 const int m = mw + rr;
-                const int head = h0 + g;
-                float x[8], y[8];
-                unpack8(*reinterpret_cast<const uint4*>(ea(rr, g * 128 + k * 16)), x);
-                if (head < e.Hq + e.Hkv) {  // rotate-half RoPE: d < 32: x c - x' s; d >= 32: x c + x' s
-                    unpack8(*reinterpret_cast<const uint4*>(ea(rr, g * 128 + (k ^ 4) * 16)), y);
-                    const float sg = k < 4 ? -1.f : 1.f;
 #pragma unroll
-                    for (int z = 0; z < 4; ++z) {
-                        const float4 c4 = cs[q][z];  // (cos, sin) of d = dh + 2z, dh + 2z + 1
-                        const float o0 = x[2 * z] * c4.x + sg * y[2 * z] * c4.y;
-                        const float o1 = x[2 * z + 1] * c4.z + sg * y[2 * z + 1] * c4.w;
-                        x[2 * z] = o0;
-                        x[2 * z + 1] = o1;
+                for (int g = 0; g < 2; ++g) {
+                    const int head = h0 + g;
+                    float x[8], y[8];
+                    unpack8(*reinterpret_cast<const uint4*>(ea(rr, g * 128 + k * 16)), x);
+                    if (g == 0 ? rope0 : rope1) {  // rotate-half RoPE: d < 32: x c - x' s; d >= 32: x c + x' s
+                        unpack8(*reinterpret_cast<const uint4*>(ea(rr, g * 128 + (k ^ 4) * 16)), y);
+                        const float sg = k < 4 ? -1.f : 1.f;
+#pragma unroll
+                        for (int z = 0; z < 4; ++z) {
+                            const float4 c4 = cs[q][z];  // (cos, sin) of d = dh + 2z, dh + 2z + 1
+                            const float o0 = x[2 * z] * c4.x + sg * y[2 * z] * c4.y;
+                            const float o1 = x[2 * z + 1] * c4.z + sg * y[2 * z + 1] * c4.w;
+                            x[2 * z] = o0;
+                            x[2 * z + 1] = o1;
+                        }
                     }
-                }
-                if (m >= M) continue;
-                const uint4 v = pack8(x);
-                if (head < e.Hq) {
-                    *reinterpret_cast<uint4*>(e.q_out + ((size_t)m * e.Hq + head) * 64 + k * 8) = v;
-                    continue;
-                }
-                const int pp = pos[q], sl = e.slot[m];
-                if (pp < 0 || pp >= e.max_seq || sl < 0 || sl >= e.num_slots) continue;
-                const bool isv = head >= e.Hq + e.Hkv;
-                const int kh = head - e.Hq - (isv ? e.Hkv : 0);
-                const size_t ofs = (((size_t)sl * e.Hkv + kh) * e.max_seq + pp) * 64 + k * 8;
-                void* cache = isv ? e.v_cache : e.k_cache;
-                if constexpr (KV8) {
-                    float f[8];
-                    for (int z = 0; z < 8; ++z) f[z] = x[z];
-                    *reinterpret_cast<uint2*>(static_cast<uint8_t*>(cache) + ofs) =
-                        make_uint2(pack_fp8x4(f), pack_fp8x4(f + 4));
-                } else {
-                    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(cache) + ofs) = v;
+                    if (m >= M) continue;
+                    const uint4 v = pack8(x);
+                    if (head < e.Hq) {
+                        *reinterpret_cast<uint4*>(e.q_out + ((size_t)m * e.Hq + head) * 64 + k * 8) = v;
+                        continue;
+                    }
+                    const int pp = pos[P0 + q], sq = sl[P0 + q];
+                    if (pp < 0 || pp >= e.max_seq || sq < 0 || sq >= e.num_slots) continue;
+                    const bool isv = head >= e.Hq + e.Hkv;
+                    const int kh = head - e.Hq - (isv ? e.Hkv : 0);
+                    const size_t ofs = (((size_t)sq * e.Hkv + kh) * e.max_seq + pp) * 64 + k * 8;
+                    void* cache = isv ? e.v_cache : e.k_cache;
+                    if constexpr (KV8) {
+                        *reinterpret_cast<uint2*>(static_cast<uint8_t*>(cache) + ofs) =
+                            make_uint2(pack_fp8x4_bf16r(x), pack_fp8x4_bf16r(x + 4));
+                    } else {
+                        *reinterpret_cast<uint4*>(static_cast<uint16_t*>(cache) + ofs) = v;
+                    }
                 }
             }
         }

@@ -421,8 +421,8 @@ __global__ __launch_bounds__(kBlock) void reduce_rope_kv_kernel(
         const size_t kofs = (((size_t)sl * Hkv + (hh - Hq)) * max_seq + p) * D;
         if constexpr (KV8) {
             uint8_t* dst = static_cast<uint8_t*>(k_cache) + kofs;
-            *reinterpret_cast<uint32_t*>(dst + d0) = pack_fp8x4(o1);
-            *reinterpret_cast<uint32_t*>(dst + half + d0) = pack_fp8x4(o2);
+            *reinterpret_cast<uint32_t*>(dst + d0) = pack_fp8x4_bf16r(o1);
+            *reinterpret_cast<uint32_t*>(dst + half + d0) = pack_fp8x4_bf16r(o2);
         } else {
             uint16_t* dst = static_cast<uint16_t*>(k_cache) + kofs;
             *reinterpret_cast<uint2*>(dst + d0) = pack4(o1);

@@ -20,6 +20,11 @@ def hip():
     return h
 
 
+# fp8 KV: one e4m3 step (12.5 %): the kernel's fp32 RoPE (fused multiply-adds)
+# and torch's can straddle a bf16 / e4m3 rounding boundary
+FP8_KV_TOL = dict(atol=0.07, rtol=0.13)
+
+
 def _bf(*shape, seed=0, scale=1.0):
     g = torch.Generator(device="cuda").manual_seed(seed)
     return (torch.randn(*shape, generator=g, device="cuda") * scale).to(torch.bfloat16)
@@ -121,6 +126,15 @@ def test_pgemm_resid(hip, M):
     torch.testing.assert_close(resid.float().cpu(), exp, atol=3e-2, rtol=1e-2)
 
 
+def _mx_error_like_reference(got, act):
+    """the kernel's MXFP8 output is as close to the fp32 activation as the
+    reference quantiser's own (e4m3 over a 32-block scale: ~2.3 % mean error
+    on these Gaussian operands)"""
+    rq, rs = R.mx_quant(act)
+    own = (R.mx_dequant(rq, rs) - act).abs().mean().item()
+    assert (got - act).abs().mean().item() <= 1.1 * own + 1e-3 * act.abs().mean().item()
+
+
 @pytest.mark.parametrize("M", [33, 700])
 def test_pgemm_swiglu(hip, M):
     inter, K = 1024, 2048
@@ -134,7 +148,7 @@ def test_pgemm_swiglu(hip, M):
     # within one e4m3 step of the block's largest value
     blk = act.abs().reshape(M, -1, 32).amax(-1, keepdim=True).expand(-1, -1, 32).reshape(M, inter)
     assert ((got - act).abs() <= blk / 8 + 1e-6).all()
-    assert (got - act).abs().mean().item() < 0.02 * act.abs().mean().item()
+    _mx_error_like_reference(got, act)
 
 
 @pytest.mark.parametrize("kv", ["bf16", "fp8"])
@@ -161,7 +175,7 @@ def test_pgemm_qkv_rope_kv(hip, kv, M):
     q = hip.pgemm_qkv(aq, as_, wq, ws, pos.cuda(), slot.cuda(), cos_sin.cuda(), kc_g, vc_g, Hq)
     rq = R.rope_kv(ref.to(torch.bfloat16), pos, slot, cos_sin, kc, vc, Hq)
     torch.testing.assert_close(q.float().cpu(), rq.float(), atol=3e-2, rtol=2e-2)
-    tol = dict(atol=0.07, rtol=0.07) if kv == "fp8" else dict(atol=3e-2, rtol=2e-2)
+    tol = FP8_KV_TOL if kv == "fp8" else dict(atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(R.kv_float(kc_g.cpu()), R.kv_float(kc), **tol)
     torch.testing.assert_close(R.kv_float(vc_g.cpu()), R.kv_float(vc), **tol)
 
@@ -224,7 +238,7 @@ def test_wgemm_mx_swiglu(hip, M):
     got = R.mx_dequant(q.cpu(), s.cpu())
     blk = act.abs().reshape(M, -1, 32).amax(-1, keepdim=True).expand(-1, -1, 32).reshape(M, inter)
     assert ((got - act).abs() <= blk / 8 + 1e-6).all()
-    assert (got - act).abs().mean().item() < 0.02 * act.abs().mean().item()
+    _mx_error_like_reference(got, act)
 
 
 @pytest.mark.parametrize("mx", [True, False])
@@ -238,7 +252,9 @@ def test_wgemm_mx_resid_norm(hip, mx, M):
     h = exp_resid.float() * torch.rsqrt(exp_resid.float().pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float().cpu()
     work = torch.empty(16 * M * N, dtype=torch.float32, device="cuda")
     out = hip.wgemm_mx_resid_norm(aq, as_, wq, ws, resid, nw, 1e-5, work, mx=mx)
-    torch.testing.assert_close(resid.float().cpu(), exp_resid.float(), atol=3e-2, rtol=1e-2)
+    # split-K sums in another order: bf16(sum) may differ by an ulp, and the
+    # residual add rounds again (up to ~2 bf16 ulps)
+    torch.testing.assert_close(resid.float().cpu(), exp_resid.float(), atol=3e-2, rtol=2e-2)
     got = R.mx_dequant(out[0].cpu(), out[1].cpu()) if mx else out.float().cpu()
     torch.testing.assert_close(got, h, atol=5e-2, rtol=0.07)
 
@@ -259,7 +275,7 @@ def test_wgemm_mx_rope_kv(hip, kv):
     q = hip.wgemm_mx_rope_kv(aq, as_, wq, ws, pos.cuda(), slot.cuda(), cos_sin.cuda(), kc_g, vc_g, Hq, work)
     rq = R.rope_kv(ref.to(torch.bfloat16), pos, slot, cos_sin, kc, vc, Hq)
     torch.testing.assert_close(q.float().cpu(), rq.float(), atol=3e-2, rtol=2e-2)
-    tol = dict(atol=0.07, rtol=0.07) if kv == "fp8" else dict(atol=3e-2, rtol=2e-2)
+    tol = FP8_KV_TOL if kv == "fp8" else dict(atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(R.kv_float(kc_g.cpu()), R.kv_float(kc), **tol)
     torch.testing.assert_close(R.kv_float(vc_g.cpu()), R.kv_float(vc), **tol)
 

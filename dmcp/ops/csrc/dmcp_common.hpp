@@ -16,12 +16,18 @@ __device__ __forceinline__ float bf2f(uint16_t v) {
     return __uint_as_float(((uint32_t)v) << 16);
 }
 
-// round-to-nearest-even fp32 -> bf16 (NaN kept quiet)
-__device__ __forceinline__ uint16_t f2bf(float f) {
-    uint32_t u = __float_as_uint(f);
-    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return (uint16_t)(u >> 16);
+typedef __bf16 bf16x2v_t __attribute__((ext_vector_type(2)));
+typedef float f32x2v_t __attribute__((ext_vector_type(2)));
+
+// round-to-nearest-even fp32 -> bf16 (NaN kept quiet): one v_cvt_pk_bf16_f32
+// (the bit-twiddling form compiled to a NaN branch per value -- 256 divergent
+// branches in a GEMM epilogue)
+__device__ __forceinline__ uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+
+// two floats -> packed bf16 pair (lo = a), one instruction
+__device__ __forceinline__ uint32_t f2bf2(float a, float b) {
+    const f32x2v_t v = {a, b};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v_t));
 }
 
 __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
@@ -33,10 +39,10 @@ __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
 
 __device__ __forceinline__ uint4 pack8(const float* f) {
     uint4 v;
-    v.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
-    v.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
-    v.z = (uint32_t)f2bf(f[4]) | ((uint32_t)f2bf(f[5]) << 16);
-    v.w = (uint32_t)f2bf(f[6]) | ((uint32_t)f2bf(f[7]) << 16);
+    v.x = f2bf2(f[0], f[1]);
+    v.y = f2bf2(f[2], f[3]);
+    v.z = f2bf2(f[4], f[5]);
+    v.w = f2bf2(f[6], f[7]);
     return v;
 }
 
@@ -47,8 +53,8 @@ __device__ __forceinline__ void unpack4(const uint2& v, float* f) {
 
 __device__ __forceinline__ uint2 pack4(const float* f) {
     uint2 v;
-    v.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
-    v.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
+    v.x = f2bf2(f[0], f[1]);
+    v.y = f2bf2(f[2], f[3]);
     return v;
 }
 

@@ -51,6 +51,14 @@ namespace {
 typedef int v8i_t __attribute__((ext_vector_type(8)));
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 
+// PG_PROBE (scripts/pgemm_probe.sh builds such variants; never the shipped
+// library): 1 = the K loop issues no refill DMAs (stale stages: MFMA + LDS
+// reads + barriers only), 2 = no per-stage barrier, 4 = block timeline
+// stamps, 8 = the bf16 epilogue skips its global stores, 16 = nontemporal
+// bf16 epilogue stores
+#ifndef PG_PROBE
+#define PG_PROBE 0
+#endif
 constexpr int PBM = 256, PBN = 256, PBK = 64, PST = 4, PTH = 256;
 constexpr int PA_BYTES = PBM * PBK;                     // A image of a stage
 constexpr int PB_BYTES = PBN * PBK;                     // W image
@@ -88,6 +96,8 @@ __device__ __forceinline__ void pglds(const void* src, void* lds_base) {
     else __builtin_amdgcn_global_load_lds(g, l, 2, 0, 0);
 }
 
+__device__ __forceinline__ int chunks_of(int K) { return K / PBK; }
+
 __device__ __forceinline__ float psilu(float g) { return g / (1.f + __expf(-g)); }
 
 // E8M0 exponent of a 32-element block of max |x| = amax: the smallest e with
@@ -111,11 +121,20 @@ __device__ __forceinline__ uint8_t to_fp8(float x) {
 // lane (r, 0) scales the row's k block 0-31, that of lane (r, 1) block 32-63.
 // In a stage row of 64 k bytes = 4 16-B chunks: lane half h reads chunks h
 // and 2 + h, and the scale of block h.
+#if (PG_PROBE & 4) != 0
+// PG_PROBE & 4: per block (start, K loop done, epilogue done) s_memtime + the
+// hardware id, for the block-timeline probe (scripts/pgemm_probe.py)
+__device__ long long pg_stamps[65536][4];
+#endif
+
 template <int MODE, bool KV8>
 __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) void pgemm_kernel(
     const uint8_t* __restrict__ aq, const uint8_t* __restrict__ as, const uint8_t* __restrict__ wq,
     const float* __restrict__ ws, int M, int N, int K, int mtiles, int ntiles, PEpi e) {
     __shared__ __attribute__((aligned(16))) uint8_t plds[PST * PST_BYTES];  // ONE LDS object (ring, then epilogue)
+#if (PG_PROBE & 4) != 0
+    const long long t_start = __builtin_amdgcn_s_memtime();
+#endif
 
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
@@ -191,63 +210,85 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     };
 
-    // One K stage per step, one basic block: wait for stage c (two newer
-    // stages in flight) + raw barrier; the fragment reads of tiles t = 0, 1
-    // and all of B (14 LDS ops); then the 16 MFMAs with the 9 LDS-DMA pieces
-    // of stage c + 3 threaded one per MFMA and the reads of tiles 2, 3 after
-    // the first four -- an LDS-DMA costs ~60 issue cycles
-    // (MI355X_MICROARCH.md), hidden behind a 64-cycle MFMA instead of
-    // serialised ahead of them (sched_barrier pins the order).  The refill is
-    // unconditional (past the last stage it re-reads it into the free slot,
-    // keeping the block branch-free and the wait count constant).
+    // One K stage per step.  Stage c's first fragments (A tile 0 + its scale,
+    // all of B) are already in registers, read at the end of step c - 1, so
+    // the step opens on MFMAs: tile 0's 4 MFMAs (tile 1's reads behind the
+    // first) with DMA pieces 0-3 of stage c + 3 threaded one per MFMA (an
+    // LDS-DMA costs ~60 issue cycles, MI355X_MICROARCH.md, hidden behind a
+    // 64-cycle MFMA), tile 1 with pieces 4-7 (tiles 2 and 3's reads behind its
+    // first MFMA), tile 2 with piece 8; then the wait
+    // for stage c + 1 (two newer stages in flight) and this wave's stage-c
+    // reads, the raw barrier (stage c + 1 landed for every wave; no wave
+    // reads slot c any more, so step c + 1 may refill it), stage c + 1's first
+    // fragments into the other register set, and tile 3's MFMAs over their
+    // latency.  sched_barrier pins the order.  The refill is unconditional
+    // (past the last stage it re-reads it into the free slot, keeping the
+    // block branch-free and the wait count constant).
     auto piece = [&](int i, int cc, int st) {
+        if constexpr ((PG_PROBE & 1) != 0) return;
         uint8_t* base = plds + st * PST_BYTES;
         if (i < 4) pglds<16>(asrc[i] + cc * PBK, base + (wv * 4 + i) * 1024);
         else if (i < 8) pglds<16>(wsrc[i - 4] + cc * PBK, base + PA_BYTES + (wv * 4 + i - 4) * 1024);
         else pglds<2>(ssrc + cc * 2, base + PA_BYTES + PB_BYTES + wv * 256);
     };
-    const int chunks = K / PBK;
+    auto wait_stage = [&]() {  // stage c + 1 landed (this wave), stage c's reads done, then every wave
+        if constexpr ((PG_PROBE & 1) != 0)
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(PGL * (PST - 2)) : "memory");
+        if constexpr ((PG_PROBE & 2) == 0) asm volatile("s_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    struct Frags {
+        v8i_t a0, b[4];
+        int s0;
+    };
+    auto stage_ptr = [&](int c) -> const uint8_t* { return plds + (c % PST) * PST_BYTES; };
+    auto pre = [&](int c, Frags& F) {  // stage c: A tile 0 + scale, then B
+        const uint8_t* A = stage_ptr(c);
+        const int r = wm * 128 + l32;
+        F.a0 = frag(A, r);
+        F.s0 = A[PA_BYTES + PB_BYTES + r * 4 + hh];
 #pragma unroll
-    for (int j = 0; j < PST - 1; ++j) issue(min(j, chunks - 1), j);
-    for (int c = 0; c < chunks; ++c) {
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(PGL * (PST - 2)) : "memory");
-        const uint8_t* A = plds + (c % PST) * PST_BYTES;
-        const uint8_t* B = A + PA_BYTES;
-        const uint8_t* S = B + PB_BYTES;
-        const int cn = min(c + PST - 1, chunks - 1), sn = (c + PST - 1) % PST;
-        v8i_t bf[4], af[4];
+        for (int u = 0; u < 4; ++u) F.b[u] = frag(A + PA_BYTES, wn * 128 + u * 32 + l32);
+    };
+    auto step = [&](int c, const Frags& F, Frags& G) {
+        const uint8_t* A = stage_ptr(c);
+        const uint8_t* S = A + PA_BYTES + PB_BYTES;
+        const int cn = min(c + PST - 1, chunks_of(K) - 1), sn = (c + PST - 1) % PST;
+        v8i_t af[4];
         int sa[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) bf[u] = frag(B, wn * 128 + u * 32 + l32);
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        auto aread = [&](int t) {
             const int r = wm * 128 + t * 32 + l32;
             af[t] = frag(A, r);
             sa[t] = S[r * 4 + hh];
-        }
-        auto mma = [&](int t, int u) {
-            acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[t], bf[u], acc[t][u], 0, 0, 0, sa[t], 0,
-                                                                        127);
         };
+        auto mma = [&](int t, int u) {
+            const v8i_t a = t == 0 ? F.a0 : af[t];
+            const int sc = t == 0 ? F.s0 : sa[t];
+            acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, F.b[u], acc[t][u], 0, 0, 0, sc, 0, 127);
+        };
+        // every read is issued right after an MFMA, >= 3 MFMAs ahead of its
+        // first use (the waitcnt pass cannot count LDS reads past pending
+        // LDS-DMAs: each use waits lgkmcnt(0), so nothing younger may be in
+        // flight then)
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             __builtin_amdgcn_sched_barrier(0);
             mma(0, u);
             __builtin_amdgcn_sched_barrier(0);
+            if (u == 0) aread(1);
             piece(u, cn, sn);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int t = 2; t < 4; ++t) {
-            const int r = wm * 128 + t * 32 + l32;
-            af[t] = frag(A, r);
-            sa[t] = S[r * 4 + hh];
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             __builtin_amdgcn_sched_barrier(0);
             mma(1, u);
             __builtin_amdgcn_sched_barrier(0);
+            if (u == 0) {
+                aread(2);
+                aread(3);
+            }
             piece(4 + u, cn, sn);
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -257,11 +298,38 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 1; u < 4; ++u) mma(2, u);
+        __builtin_amdgcn_sched_barrier(0);
+        wait_stage();
+        pre(c + 1, G);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 0; u < 4; ++u) mma(3, u);
+    };
+    const int chunks = chunks_of(K);
+#pragma unroll
+    for (int j = 0; j < PST - 1; ++j) issue(min(j, chunks - 1), j);
+    // stage 0: landed for every wave, its first fragments read
+    if constexpr ((PG_PROBE & 1) != 0)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PGL * (PST - 2)) : "memory");
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    Frags F0, F1;
+    pre(0, F0);
+    // two steps per trip: the register sets swap roles by name, never by a
+    // runtime index (cdna_hip_programming.md §5.4 rule 20)
+    int c = 0;
+    for (; c + 1 < chunks; c += 2) {
+        step(c, F0, F1);
+        step(c + 1, F1, F0);
     }
+    if (c < chunks) step(c, F0, F1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the refills past the last stage, before the LDS is reused
     __syncthreads();  // the ring is free: the epilogue stages this wave's tile in it
+#if (PG_PROBE & 4) != 0
+    const long long t_loop = __builtin_amdgcn_s_memtime();
+#endif
 
     // ---- epilogue.  Lane (l32, hh) holds column l32 of rows (i & 3) + 8 (i >> 2)
     // + 4 hh of each 32 x 32 tile.  The wave's 128 x 128 tile goes through LDS
@@ -319,6 +387,11 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
                     for (int j = 0; j < 8; ++j) a[j] += b2[j];
                     *dst = pack8(a);
+                } else if constexpr ((PG_PROBE & 8) != 0) {
+                    if (v.x == 0x7fc07fc0u) *dst = v;  // probe: (almost) no stores
+                } else if constexpr ((PG_PROBE & 16) != 0) {
+                    const v4i_t vv = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+                    __builtin_nontemporal_store(vv, reinterpret_cast<v4i_t*>(dst));
                 } else {
                     *dst = v;
                 }
@@ -452,6 +525,17 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             }
         }
     }
+#if (PG_PROBE & 4) != 0
+    __syncthreads();
+    if (tid == 0 && blockIdx.x < 65536) {
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        pg_stamps[blockIdx.x][0] = t_start;
+        pg_stamps[blockIdx.x][1] = t_loop;
+        pg_stamps[blockIdx.x][2] = __builtin_amdgcn_s_memtime();
+        pg_stamps[blockIdx.x][3] = hw;
+    }
+#endif
 }
 
 // ---- decode: weight-streaming GEMM on MX fp8 (the wgemm.hip structure with
@@ -958,6 +1042,13 @@ int dmcp_reduce_resid_norm_mx(const void* part, int S, void* resid, const void* 
     else reduce_resid_norm_mx_kernel<4><<<M, kBlock, 0, st>>>(pp, S, rr, ww, qq, ss, M, N, eps);
     return hipGetLastError();
 }
+
+#if (PG_PROBE & 4) != 0
+int dmcp_pg_stamps(void* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(pg_stamps), (size_t)n * 4 * sizeof(long long), 0,
+                               hipMemcpyDeviceToHost);
+}
+#endif
 
 int dmcp_mx_probe(const void* a, const void* b, const void* sa, const void* sb, void* c, void* stream) {
     mx_probe_kernel<<<1, kWave, 0, (hipStream_t)stream>>>((const v8i_t*)a, (const v8i_t*)b, (const int*)sa,

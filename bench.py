@@ -61,6 +61,8 @@ def parse_args(argv=None):
     ap.add_argument("--enrich-local-classes", type=int, default=256,
                     help="classes of the end-to-end local-model enrichment run (extra.enrichLocal; 0 = skip)")
     ap.add_argument("--enrich-local-kv", default="fp8", choices=["bf16", "fp8"])
+    ap.add_argument("--enrich-local-prefill", default="auto", choices=["auto", "bf16", "fp8"],
+                    help="batched-prefill GEMMs of the enrichment worker (auto = MXFP8 on gfx950)")
     ap.add_argument("--enrich-local-batch", type=int, default=512)
     ap.add_argument("--enrich-local-presets", default="dmcp-coder-1b,llama3.2-1b-code")
     ap.add_argument("--remote-steps", type=int, default=3,
@@ -86,7 +88,8 @@ def _spawn_enrich_pools(args):
         mb = args.enrich_local_batch
         pools = {}
         for name in [p.strip() for p in args.enrich_local_presets.split(",") if p.strip()]:
-            model = {"preset": name, "kv_dtype": args.enrich_local_kv, "max_batch": mb,
+            model = {"preset": name, "kv_dtype": args.enrich_local_kv, "prefill_dtype": args.enrich_local_prefill,
+                     "max_batch": mb,
                      "max_rows": max(256, mb * 3 // 2), "seed": 0}
             pools[name] = GpuWorkerPool([f"cuda:{local}"], model, engine={"max_new_tokens": 4096}, init=False,
                                         start_timeout_s=600)
@@ -164,6 +167,7 @@ def _enrich_local(pool, args, ctx, work, rank):
                 "prefillMsPerClass": round(1e3 * st.get("prefill_s", 0) / max(1, st.get("prefills", 0)), 3),
                 "prefillBatches": int(st.get("prefill_batches", 0)), "workerInitS": round(init_s, 1),
                 "config": {"model": f"{pool.model['preset']} (random init)", "kv_dtype": args.enrich_local_kv,
+                           "prefill_dtype": args.enrich_local_prefill,
                            "batch": args.enrich_local_batch, "workers_per_rank": len(pool.workers),
                            "path": "analyze_project -> streamed Phase 2 -> GPU worker process"}}
     finally:

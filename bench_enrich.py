@@ -26,7 +26,7 @@ def main(argv=None) -> int:
     ap.add_argument("--preset", default="dmcp-coder-1b")
     ap.add_argument("--kv-dtype", default="fp8", choices=["bf16", "fp8"],
                     help="KV cache storage (fp8 = e4m3, half the attention bytes)")
-    ap.add_argument("--prefill-dtype", default="bf16", choices=["bf16", "fp8"],
+    ap.add_argument("--prefill-dtype", default="auto", choices=["auto", "bf16", "fp8"],
                     help="batched-prefill projections: bf16 (hipBLASLt) or fp8 (MXFP8 kernels, csrc/pgemm.hip)")
     ap.add_argument("--decode-dtype", default="bf16", choices=["bf16", "fp8"],
                     help="decode-step projections: bf16, or fp8 weights x MXFP8 activations (csrc/pgemm.hip)")
@@ -125,7 +125,7 @@ def main(argv=None) -> int:
             "unit": "classes/s", "n_gpus": world, "higher_is_better": True, "scaling": "weak",
             "dtype": "bf16", "data": "synthetic classes, random-init weights",
             "config": {"model": cfg.name, "params_b": round(cfg.param_count() / 1e9, 3), "batch": args.batch,
-                       "max_rows": cfg.max_rows, "kv_dtype": cfg.kv_dtype, "prefill_dtype": cfg.prefill_dtype, "decode_dtype": cfg.decode_dtype,
+                       "max_rows": cfg.max_rows, "kv_dtype": cfg.kv_dtype, "prefill_dtype": "fp8" if model.prefill_fp8 else "bf16", "decode_dtype": cfg.decode_dtype,
                        "max_seq": args.max_seq, "prompt_chars": args.prompt_chars,
                        "readme_chars": args.readme_chars, "graphs": not args.no_graphs,
                        "jump_forward": not args.no_jump, "shared_prefix": not args.no_shared_prefix,

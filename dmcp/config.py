@@ -52,7 +52,9 @@ class Config:
     # fp8 (e4m3) KV cache: half the decode-attention bytes; every tuned and
     # benchmarked number is fp8 (56.8 vs 43.9 classes/s bf16, profiles/enrich_*_r3_prompt.jsonl)
     local_llm_kv_dtype: str = "fp8"
-    local_llm_prefill_dtype: str = "bf16"
+    # batched-prefill GEMMs: "auto" = MXFP8 (csrc/pgemm.hip) on a gfx950 GPU,
+    # bf16 elsewhere; "bf16" / "fp8" force one
+    local_llm_prefill_dtype: str = "auto"
     local_llm_decode_dtype: str = "bf16"
     # reply budget in tokens (the reference's claude.max-tokens analog): a
     # class whose reply does not fit is generated in several parts and merged

@@ -644,7 +644,7 @@ def model_spec(cfg) -> dict:
     mb = int(cfg.local_llm_max_batch)
     spec = {"preset": cfg.local_llm_preset, "kv_dtype": cfg.local_llm_kv_dtype, "max_batch": mb,
             "max_rows": max(256, mb * 3 // 2), "seed": 0,
-            "prefill_dtype": getattr(cfg, "local_llm_prefill_dtype", "bf16"),
+            "prefill_dtype": getattr(cfg, "local_llm_prefill_dtype", "auto"),
             "decode_dtype": getattr(cfg, "local_llm_decode_dtype", "bf16")}
     if getattr(cfg, "local_llm_model_path", ""):
         spec["path"] = cfg.local_llm_model_path

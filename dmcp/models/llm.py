@@ -82,7 +82,10 @@ class LMConfig:
     kv_dtype: str = "bf16"          # KV cache storage: "bf16" or "fp8" (e4m3, unit scale, half the bytes)
     # batched-prefill projections: "bf16" (hipBLASLt) or "fp8" (MXFP8
     # activations x per-row-scaled e4m3 weights on the MX matrix cores,
-    # csrc/pgemm.hip, epilogues fused); decode keeps the bf16 weights
+    # csrc/pgemm.hip, epilogues fused); decode keeps the bf16 weights.
+    # "auto": fp8 where the kernels run (a gfx950 device and supported dims;
+    # 1.37x the bf16 batched prefill, profiles/fp8_paths_r4_cvtpk.jsonl),
+    # else bf16
     prefill_dtype: str = "bf16"
     # decode steps of fused_max_rows < rows <= WMX_MAX_ROWS: "bf16" (wgemm.hip /
     # hipBLASLt) or "fp8" (the same e4m3 weights, MXFP8 activations written by
@@ -221,7 +224,9 @@ class LocalLM:
             raise ValueError("n_heads must be a multiple of n_kv_heads")
         if cfg.kv_dtype not in ("bf16", "fp8"):
             raise ValueError(f"kv_dtype must be 'bf16' or 'fp8', got {cfg.kv_dtype!r}")
-        for k in ("prefill_dtype", "decode_dtype"):
+        if cfg.prefill_dtype not in ("bf16", "fp8", "auto"):
+            raise ValueError(f"prefill_dtype must be 'bf16', 'fp8' or 'auto', got {cfg.prefill_dtype!r}")
+        for k in ("decode_dtype",):
             if getattr(cfg, k) not in ("bf16", "fp8"):
                 raise ValueError(f"{k} must be 'bf16' or 'fp8', got {getattr(cfg, k)!r}")
         self.cfg = cfg
@@ -284,7 +289,8 @@ class LocalLM:
             (self.use_prefill_kernel
              and ops.pgemm_supported(c.hidden, c.n_heads, c.n_kv_heads, c.head_dim, c.intermediate))
             or (self.device.type == "cpu" and c.hidden % 32 == 0 and c.intermediate % 32 == 0))
-        self.prefill_fp8 = c.prefill_dtype == "fp8" and fp8_ok
+        self.prefill_fp8 = fp8_ok and (c.prefill_dtype == "fp8"
+                                       or (c.prefill_dtype == "auto" and self.device.type == "cuda"))
         self.decode_fp8 = c.decode_dtype == "fp8" and fp8_ok
         if "fp8" in (c.prefill_dtype, c.decode_dtype) and not fp8_ok:
             raise ValueError(f"fp8 GEMMs need head_dim 64, hidden % 2048 == 0 and a supported device "

@@ -25,7 +25,7 @@ def main() -> int:
     ap.add_argument("--seqs", type=int, default=12)
     ap.add_argument("--kv-dtype", default="fp8", choices=["bf16", "fp8"])
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--prefill-dtype", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--prefill-dtype", default="bf16", choices=["auto", "bf16", "fp8"])
     a = ap.parse_args()
     from dmcp.models.llm import LocalLM, preset
     model = LocalLM(preset(a.preset, max_batch=max(8, a.seqs), max_seq=8192, kv_dtype=a.kv_dtype,

@@ -34,6 +34,8 @@ for s in $STEPS; do
         enrich_fp8) run enrich_fp8 900 python bench_enrich.py --kv-dtype fp8 ;;
         enrich_bf16) run enrich_bf16 900 python bench_enrich.py --kv-dtype bf16 ;;
         enrich_llama) run enrich_llama 900 python bench_enrich.py --preset llama3.2-1b-code --kv-dtype fp8 ;;
+        enrich_llama_bf16) run enrich_llama_bf16 900 python bench_enrich.py --preset llama3.2-1b-code --kv-dtype fp8 \
+                --prefill-dtype bf16 ;;
         enrich_llama257) run enrich_llama257 600 python bench_enrich.py --preset llama3.2-1b-code --classes 257 ;;
         enrich_llama_r512) run enrich_llama_r512 600 python bench_enrich.py --preset llama3.2-1b-code --max-rows 512 ;;
         enrich_llama_b384) run enrich_llama_b384 600 python bench_enrich.py --preset llama3.2-1b-code --batch 384 ;;

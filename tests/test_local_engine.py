@@ -507,3 +507,16 @@ def test_decode_fp8_greedy_agreement_with_bf16():
     assert agree >= 14, (ta, tb)
     out = LocalEngine(b, use_graphs=False).generate(_inputs(3), "readme")
     assert all(json.loads(o) for o in out)
+
+
+def test_prefill_dtype_auto_is_bf16_off_gpu():
+    """prefill_dtype "auto" (the service default) picks the MX kernels only on
+    a gfx950 device; on the CPU it is the bf16 path, and unknown names fail."""
+    import pytest as _pytest
+    from dmcp.config import Config
+    from dmcp.models.llm import LocalLM, preset
+    assert Config().local_llm_prefill_dtype == "auto"
+    m = LocalLM(preset("tiny", prefill_dtype="auto", max_batch=2, max_seq=256), device="cpu", seed=0)
+    assert not m.prefill_fp8
+    with _pytest.raises(ValueError):
+        LocalLM(preset("tiny", prefill_dtype="int8", max_batch=2, max_seq=256), device="cpu", seed=0)

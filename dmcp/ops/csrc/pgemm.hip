@@ -70,7 +70,6 @@ constexpr int PS_BYTES = PBM * 4;
 constexpr int PST_BYTES = PA_BYTES + PB_BYTES + PS_BYTES;
 constexpr int PGL = 9;                                  // LDS-DMA instructions per wave per stage
 constexpr int PM_BF16 = 0, PM_RESID = 1, PM_SWIGLU = 2, PM_QKV = 3;
-constexpr int PEPI_ROW = 256;  // epilogue image row: 128 bf16, 16-B chunk j of row r at slot j ^ (r & 15)
 
 struct PEpi {
     uint16_t* y;          // PM_BF16: out [M, N]; PM_RESID: resid [M, N] (in place)
@@ -266,7 +265,10 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         auto mma = [&](int t, int u) {
             const v8i_t a = t == 0 ? F.a0 : af[t];
             const int sc = t == 0 ? F.s0 : sa[t];
-            acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, F.b[u], acc[t][u], 0, 0, 0, sc, 0, 127);
+            // C^T tile: A = 32 weight rows (scale 1), B = 32 activation rows
+            // with their E8M0 block scales -> lane l32 holds activation row
+            // t * 32 + l32, register i weight column (i & 3) + 8 (i >> 2) + 4 hh
+            acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(F.b[u], a, acc[t][u], 0, 0, 0, 127, 0, sc);
         };
         // every read is issued right after an MFMA, >= 3 MFMAs ahead of its
         // first use (the waitcnt pass cannot count LDS reads past pending
@@ -325,202 +327,211 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         step(c + 1, F1, F0);
     }
     if (c < chunks) step(c, F0, F1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the refills past the last stage, before the LDS is reused
-    __syncthreads();  // the ring is free: the epilogue stages this wave's tile in it
+    // the refills past the last stage land before the block's LDS is released
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #if (PG_PROBE & 4) != 0
     const long long t_loop = __builtin_amdgcn_s_memtime();
 #endif
 
-    // ---- epilogue.  Lane (l32, hh) holds column l32 of rows (i & 3) + 8 (i >> 2)
-    // + 4 hh of each 32 x 32 tile.  The wave's 128 x 128 tile goes through LDS
-    // (128 rows x 256 B + pad) so the global stores are 16-B per lane along rows.
-    uint8_t* img = plds + wv * (128 * PEPI_ROW);
-    static_assert(PTH / kWave * 128 * PEPI_ROW <= PST * PST_BYTES, "epilogue images fit the ring");
-    // byte b of image row r (swizzled: the 2-byte column writes of rows r and
-    // r + 4 and the 16-B row reads all spread over the banks)
-    auto ea = [&](int r, int byte) -> uint8_t* {
-        return img + r * PEPI_ROW + ((((byte >> 4) ^ (r & 15)) << 4) | (byte & 15));
-    };
+    // ---- epilogue, in registers.  Lane (l32, hh) holds row t * 32 + l32 of
+    // the wave's tile and, per 32-column tile u, columns 8 j + 4 hh + q
+    // (register 4 j + q): four 4-column groups.  A v_permlane32_swap of groups
+    // (0, 1) and (2, 3) (cdna_hip_programming.md T21) leaves lanes 0-31 with
+    // columns 0-7 and 16-23 and lanes 32-63 with 8-15 and 24-31: two 16-B
+    // (bf16) or 8-B (fp8) stores per lane per tile, no LDS round trip.
     const int mw = m0 + wm * 128;  // first row of this wave's tile
-    // The register phase only converts and writes LDS; the store phase's
-    // global loads (residual rows, positions, RoPE tables) are batched, since
-    // at one wave per SIMD nothing else hides their latency.
-    auto put = [&](int rr, int col, float v) {  // bf16 of v at image (row rr, column col)
-        *reinterpret_cast<uint16_t*>(ea(rr, col * 2)) = f2bf(v);
+    const int n0 = nt * PBN + wn * 128;
+    auto swap2 = [&](uint32_t& a, uint32_t& b) {  // lanes 32-63 of a <-> lanes 0-31 of b
+        const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+        a = r[0];
+        b = r[1];
+    };
+    // 16 values of a tile -> 4 packed bf16 groups, swapped into 2 x 16 B
+    auto bf16_rows = [&](const float* v, uint4& lo, uint4& hi) {
+        uint2 g[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) g[j] = pack4(v + 4 * j);
+        swap2(g[0].x, g[1].x);
+        swap2(g[0].y, g[1].y);
+        swap2(g[2].x, g[3].x);
+        swap2(g[2].y, g[3].y);
+        lo = make_uint4(g[0].x, g[0].y, g[1].x, g[1].y);  // columns 8 hh .. + 7
+        hi = make_uint4(g[2].x, g[2].y, g[3].x, g[3].y);  // columns 16 + 8 hh .. + 7
+    };
+    // 16 values -> 4 e4m3 groups (through bf16 when kv), swapped into 2 x 8 B
+    auto fp8_rows = [&](const float* v, bool via_bf16, uint2& lo, uint2& hi) {
+        uint32_t g[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) g[j] = via_bf16 ? pack_fp8x4_bf16r(v + 4 * j) : pack_fp8x4(v + 4 * j);
+        swap2(g[0], g[1]);
+        swap2(g[2], g[3]);
+        lo = make_uint2(g[0], g[1]);
+        hi = make_uint2(g[2], g[3]);
+    };
+    auto scales16 = [&](const float* base, float* sc) {  // sc[4 j + q] = base[8 j + 4 hh + q]
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float4 f = *reinterpret_cast<const float4*>(base + 8 * j + 4 * hh);
+            sc[4 * j] = f.x;
+            sc[4 * j + 1] = f.y;
+            sc[4 * j + 2] = f.z;
+            sc[4 * j + 3] = f.w;
+        }
     };
     if constexpr (MODE == PM_BF16 || MODE == PM_RESID) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const float sc = ws[nt * PBN + wn * 128 + u * 32 + l32];
+            float sc[16];
+            scales16(ws + n0 + u * 32, sc);
+            const int col = n0 + u * 32 + 8 * hh;
+            uint4 r[4][2];
+            if constexpr (MODE == PM_RESID) {  // the 8 residual chunks of this tile column in flight together
 #pragma unroll
-            for (int t = 0; t < 4; ++t)
-#pragma unroll
-                for (int i = 0; i < 16; ++i)
-                    put(t * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh, u * 32 + l32, acc[t][u][i] * sc);
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
-        __builtin_amdgcn_wave_barrier();
-        const int n0 = nt * PBN + wn * 128;
-        // 16 lanes per row (8 bf16 each), 4 rows per pass; 16 passes per batch
-        // (the residual rows of a batch in flight together)
-#pragma unroll
-        for (int p0 = 0; p0 < 32; p0 += 16) {
-            uint4 r[16];
-            if constexpr (MODE == PM_RESID) {
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    const int m = min(mw + (p0 + q) * 4 + (lane >> 4), M - 1);
-                    r[q] = *reinterpret_cast<const uint4*>(e.y + (size_t)m * N + n0 + (lane & 15) * 8);
+                for (int t = 0; t < 4; ++t) {
+                    const uint16_t* rp = e.y + (size_t)min(mw + t * 32 + l32, M - 1) * N + col;
+                    r[t][0] = *reinterpret_cast<const uint4*>(rp);
+                    r[t][1] = *reinterpret_cast<const uint4*>(rp + 16);
                 }
             }
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int rr = (p0 + q) * 4 + (lane >> 4);
-                const int m = mw + rr;
-                const uint4 v = *reinterpret_cast<const uint4*>(ea(rr, (lane & 15) * 16));
+            for (int t = 0; t < 4; ++t) {
+                const int m = mw + t * 32 + l32;
+                float v[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) v[i] = acc[t][u][i] * sc[i];
+                uint4 lo, hi;
+                bf16_rows(v, lo, hi);
                 if (m >= M) continue;
-                uint4* dst = reinterpret_cast<uint4*>(e.y + (size_t)m * N + n0 + (lane & 15) * 8);
+                uint16_t* dst = e.y + (size_t)m * N + col;
                 if constexpr (MODE == PM_RESID) {
                     float a[8], b2[8];
-                    unpack8(v, a);
-                    unpack8(r[q], b2);
+                    unpack8(lo, a);
+                    unpack8(r[t][0], b2);
 #pragma unroll
                     for (int j = 0; j < 8; ++j) a[j] += b2[j];
-                    *dst = pack8(a);
-                } else if constexpr ((PG_PROBE & 8) != 0) {
-                    if (v.x == 0x7fc07fc0u) *dst = v;  // probe: (almost) no stores
-                } else if constexpr ((PG_PROBE & 16) != 0) {
-                    const v4i_t vv = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
-                    __builtin_nontemporal_store(vv, reinterpret_cast<v4i_t*>(dst));
-                } else {
-                    *dst = v;
+                    lo = pack8(a);
+                    unpack8(hi, a);
+                    unpack8(r[t][1], b2);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) a[j] += b2[j];
+                    hi = pack8(a);
                 }
+                *reinterpret_cast<uint4*>(dst) = lo;
+                *reinterpret_cast<uint4*>(dst + 16) = hi;
             }
         }
     } else if constexpr (MODE == PM_SWIGLU) {
-        // tiles u = 0, 1 are gate columns j0 .. j0 + 63, u = 2, 3 the up columns
+        // tiles u = 0, 1: gate columns j0 + 32 u .., tiles u + 2: the up
+        // columns of the same intermediates (the wrow interleave above)
         const int j0 = nt * 128 + wn * 64;
         const int isb = e.I >> 5;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            const int j = j0 + u * 32 + l32;
-            const float sg = ws[j], su = ws[e.I + j];
+            float sg[16], su[16];
+            scales16(ws + j0 + u * 32, sg);
+            scales16(ws + e.I + j0 + u * 32, su);
 #pragma unroll
-            for (int t = 0; t < 4; ++t)
+            for (int t = 0; t < 4; ++t) {
+                const int m = mw + t * 32 + l32;
+                float a[16];
+                float amax = 0.f;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     // gate / up rounded to bf16 as the bf16 GEMM's outputs are
-                    const float g = bf2f(f2bf(acc[t][u][i] * sg)), uu = bf2f(f2bf(acc[t][u + 2][i] * su));
-                    put(t * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh, u * 32 + l32, psilu(g) * uu);
+                    const float g = bf2f(f2bf(acc[t][u][i] * sg[i])), uu = bf2f(f2bf(acc[t][u + 2][i] * su[i]));
+                    a[i] = bf2f(f2bf(psilu(g) * uu));
+                    amax = __builtin_fmaxf(amax, __builtin_fabsf(a[i]));
                 }
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_wave_barrier();
-        // 8 lanes per row (8 values each: lanes 4k..4k+3 are one 32-column
-        // block), 8 rows per pass: block max over 4 lanes, e4m3 bytes, E8M0
-#pragma unroll 4
-        for (int p = 0; p < 16; ++p) {
-            const int rr = p * 8 + (lane >> 3);
-            const int m = mw + rr;
-            float a[8];
-            unpack8(*reinterpret_cast<const uint4*>(ea(rr, (lane & 7) * 16)), a);
-            float amax = 0.f;
+                amax = half_swap_max(amax);  // the block's other 16 columns are in lane ^ 32
+                const int ex = mx_exp(amax);
 #pragma unroll
-            for (int q = 0; q < 8; ++q) amax = __builtin_fmaxf(amax, __builtin_fabsf(a[q]));
-            amax = __builtin_fmaxf(amax, __shfl_xor(amax, 1, kWave));
-            amax = __builtin_fmaxf(amax, __shfl_xor(amax, 2, kWave));
-            const int ex = mx_exp(amax);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) a[q] = ldexpf(a[q], -ex);
-            if (m < M) {
-                *reinterpret_cast<uint2*>(e.yq + (size_t)m * e.I + j0 + (lane & 7) * 8) =
-                    make_uint2(pack_fp8x4(a), pack_fp8x4(a + 4));
-                if ((lane & 3) == 0) e.ys[(size_t)m * isb + (j0 >> 5) + ((lane & 7) >> 2)] = (uint8_t)(ex + 127);
+                for (int i = 0; i < 16; ++i) a[i] = ldexpf(a[i], -ex);
+                uint2 lo, hi;
+                fp8_rows(a, false, lo, hi);
+                if (m >= M) continue;
+                uint8_t* dst = e.yq + (size_t)m * e.I + j0 + u * 32 + 8 * hh;
+                *reinterpret_cast<uint2*>(dst) = lo;
+                *reinterpret_cast<uint2*>(dst + 16) = hi;
+                if (hh == 0) e.ys[(size_t)m * isb + ((j0 + u * 32) >> 5)] = (uint8_t)(ex + 127);
             }
         }
-    } else {  // PM_QKV: the wave's 128 columns are two heads; tiles 2 g, 2 g + 1 = d 0..31, 32..63 of head g
-        const int h0 = (nt * PBN + wn * 128) >> 6;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const float sc = ws[nt * PBN + wn * 128 + u * 32 + l32];
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-#pragma unroll
-                for (int i = 0; i < 16; ++i)
-                    put(t * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh, u * 32 + l32, acc[t][u][i] * sc);
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_wave_barrier();
-        // Store phase: lane (r8, k) = (lane >> 3, lane & 7) takes rows qrow(P,
-        // r8) (P = 0..15) of the wave's 128, both heads of each, chunk k (8 d) of
-        // a head row; its RoPE partner is chunk k ^ 4 (d +- 32), and the two
-        // heads of a row share the row's (cos, sin).  Every global load is
-        // independent of the stores: the rows' positions and slots in one
-        // batch, then the table rows in two batches of 8 (one wave per SIMD:
-        // nothing else hides a dependent round trip).
-        const int k = lane & 7, r8 = lane >> 3;
-        const int dh = (k & 3) * 8;  // d mod 32 of this lane's 8 values
-        const bool rope0 = h0 < e.Hq + e.Hkv, rope1 = h0 + 1 < e.Hq + e.Hkv;
+    } else {  // PM_QKV: tiles 2 g, 2 g + 1 = d 0..31, 32..63 of head h0 + g
+        const int h0 = n0 >> 6;
         const bool kv = h0 + 1 >= e.Hq;  // some head of this wave goes to the caches
-        // rows of lane groups r8 = 0 and 1 (one 16-lane LDS read group) 8 apart:
-        // their swizzled chunk sets are disjoint halves of the bank row
-        auto qrow = [&](int P) { return 16 * (P >> 1) + 8 * (r8 & 1) + (r8 >> 1) + 4 * (P & 1); };
-        int pos[16], sl[16];
+        int pos[4], sl[4];
 #pragma unroll
-        for (int P = 0; P < 16; ++P) {
-            const int m = min(mw + qrow(P), M - 1);
-            pos[P] = e.pos[m];
-            sl[P] = kv ? e.slot[m] : -1;
+        for (int t = 0; t < 4; ++t) {
+            const int mc = min(mw + t * 32 + l32, M - 1);
+            pos[t] = e.pos[mc];
+            sl[t] = kv ? e.slot[mc] : -1;
         }
+        float sc[4][16];
 #pragma unroll
-        for (int P0 = 0; P0 < 16; P0 += 8) {
-            float4 cs[8][4];
+        for (int u = 0; u < 4; ++u) scales16(ws + n0 + u * 32, sc[u]);
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const float4* t4 = reinterpret_cast<const float4*>(
-                    e.cos_sin + (size_t)min(max(pos[P0 + q], 0), e.max_pos - 1) * 32 + dh);
+        for (int t = 0; t < 4; ++t) {
+            const int m = mw + t * 32 + l32;
+            // (cos, sin) of d = 8 j + 4 hh + q: two float4 per group
+            float cs_c[16], cs_s[16];
+            const float4* tb = reinterpret_cast<const float4*>(
+                e.cos_sin + (size_t)min(max(pos[t], 0), e.max_pos - 1) * 32);
 #pragma unroll
-                for (int z = 0; z < 4; ++z) cs[q][z] = t4[z];
+            for (int j = 0; j < 4; ++j) {
+                const float4 p0 = tb[(8 * j + 4 * hh) / 2], p1 = tb[(8 * j + 4 * hh) / 2 + 1];
+                cs_c[4 * j] = p0.x; cs_s[4 * j] = p0.y; cs_c[4 * j + 1] = p0.z; cs_s[4 * j + 1] = p0.w;
+                cs_c[4 * j + 2] = p1.x; cs_s[4 * j + 2] = p1.y; cs_c[4 * j + 3] = p1.z; cs_s[4 * j + 3] = p1.w;
             }
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int rr = qrow(P0 + q);
-                const int m = mw + rr;
+            for (int g = 0; g < 2; ++g) {
+                const int head = h0 + g;
+                float lo[16], hi[16];
 #pragma unroll
-                for (int g = 0; g < 2; ++g) {
-                    const int head = h0 + g;
-                    float x[8], y[8];
-                    unpack8(*reinterpret_cast<const uint4*>(ea(rr, g * 128 + k * 16)), x);
-                    if (g == 0 ? rope0 : rope1) {  // rotate-half RoPE: d < 32: x c - x' s; d >= 32: x c + x' s
-                        unpack8(*reinterpret_cast<const uint4*>(ea(rr, g * 128 + (k ^ 4) * 16)), y);
-                        const float sg = k < 4 ? -1.f : 1.f;
+                for (int i = 0; i < 16; ++i) {  // the projection's bf16 outputs
+                    lo[i] = bf2f(f2bf(acc[t][2 * g][i] * sc[2 * g][i]));
+                    hi[i] = bf2f(f2bf(acc[t][2 * g + 1][i] * sc[2 * g + 1][i]));
+                }
+                if (head < e.Hq + e.Hkv) {  // rotate-half RoPE: d < 32: x c - x' s; d >= 32: x' c + x s
 #pragma unroll
-                        for (int z = 0; z < 4; ++z) {
-                            const float4 c4 = cs[q][z];  // (cos, sin) of d = dh + 2z, dh + 2z + 1
-                            const float o0 = x[2 * z] * c4.x + sg * y[2 * z] * c4.y;
-                            const float o1 = x[2 * z + 1] * c4.z + sg * y[2 * z + 1] * c4.w;
-                            x[2 * z] = o0;
-                            x[2 * z + 1] = o1;
-                        }
+                    for (int i = 0; i < 16; ++i) {
+                        const float a = lo[i], b = hi[i];
+                        lo[i] = a * cs_c[i] - b * cs_s[i];
+                        hi[i] = b * cs_c[i] + a * cs_s[i];
                     }
-                    if (m >= M) continue;
-                    const uint4 v = pack8(x);
-                    if (head < e.Hq) {
-                        *reinterpret_cast<uint4*>(e.q_out + ((size_t)m * e.Hq + head) * 64 + k * 8) = v;
-                        continue;
-                    }
-                    const int pp = pos[P0 + q], sq = sl[P0 + q];
+                }
+                if (m >= M) continue;
+                size_t ofs;  // element offset of d = 0 of this (row, head)
+                void* base;
+                bool to_cache = false;
+                if (head < e.Hq) {
+                    ofs = ((size_t)m * e.Hq + head) * 64;
+                    base = e.q_out;
+                } else {
+                    const int pp = pos[t], sq = sl[t];
                     if (pp < 0 || pp >= e.max_seq || sq < 0 || sq >= e.num_slots) continue;
                     const bool isv = head >= e.Hq + e.Hkv;
                     const int kh = head - e.Hq - (isv ? e.Hkv : 0);
-                    const size_t ofs = (((size_t)sq * e.Hkv + kh) * e.max_seq + pp) * 64 + k * 8;
-                    void* cache = isv ? e.v_cache : e.k_cache;
-                    if constexpr (KV8) {
-                        *reinterpret_cast<uint2*>(static_cast<uint8_t*>(cache) + ofs) =
-                            make_uint2(pack_fp8x4_bf16r(x), pack_fp8x4_bf16r(x + 4));
-                    } else {
-                        *reinterpret_cast<uint4*>(static_cast<uint16_t*>(cache) + ofs) = v;
-                    }
+                    ofs = (((size_t)sq * e.Hkv + kh) * e.max_seq + pp) * 64;
+                    base = isv ? e.v_cache : e.k_cache;
+                    to_cache = true;
+                }
+                if (KV8 && to_cache) {
+                    uint2 a0, a1, b0, b1;
+                    fp8_rows(lo, true, a0, a1);
+                    fp8_rows(hi, true, b0, b1);
+                    uint8_t* d8 = static_cast<uint8_t*>(base) + ofs + 8 * hh;
+                    *reinterpret_cast<uint2*>(d8) = a0;
+                    *reinterpret_cast<uint2*>(d8 + 16) = a1;
+                    *reinterpret_cast<uint2*>(d8 + 32) = b0;
+                    *reinterpret_cast<uint2*>(d8 + 48) = b1;
+                } else {
+                    uint4 a0, a1, b0, b1;
+                    bf16_rows(lo, a0, a1);
+                    bf16_rows(hi, b0, b1);
+                    uint16_t* d16 = static_cast<uint16_t*>(base) + ofs + 8 * hh;
+                    *reinterpret_cast<uint4*>(d16) = a0;
+                    *reinterpret_cast<uint4*>(d16 + 16) = a1;
+                    *reinterpret_cast<uint4*>(d16 + 32) = b0;
+                    *reinterpret_cast<uint4*>(d16 + 48) = b1;
                 }
             }
         }

@@ -740,6 +740,9 @@ class LocalLM:
         if not (0 <= src < self.num_slots) or any(not 0 <= d < self.num_slots for d in dsts) or \
                 not (0 <= start <= end <= self.cfg.max_seq):
             raise ValueError(f"fork_kv: slot {src} -> {list(dsts)}, positions [{start}, {end})")
+        if self.device.type == "cuda":  # one HIP launch for both caches (csrc/dmcp_kernels.hip kv_fork_kernel)
+            ops.hip.kv_fork(self.k_cache, self.v_cache, src, dsts, start, end)
+            return
         idx = torch.tensor(list(dsts), dtype=torch.long, device=self.device)
         for cache in (self.k_cache, self.v_cache):
             cache[:, idx, :, start:end] = cache[:, src, :, start:end].unsqueeze(1)

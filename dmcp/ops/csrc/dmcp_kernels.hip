@@ -847,6 +847,38 @@ hipError_t launch_combine(void* part_o, void* part_ml, const int32_t* sl, const 
 
 }  // namespace
 
+// ---- method-branch KV fork: slot src's keys and values at positions
+// [start, end) of every layer and kv head into up to 32 destination slots,
+// one launch for both caches (LocalLM.fork_kv; it replaced two indexed-copy
+// launches per fork).  Caches [layers][slots][Hkv][max_seq][row_bytes];
+// each thread moves 16 B: read once, written ndst times.
+struct ForkDsts {
+    int32_t d[32];
+};
+
+__global__ __launch_bounds__(kBlock) void kv_fork_kernel(uint8_t* __restrict__ kc, uint8_t* __restrict__ vc,
+                                                         int layers, int num_slots, int Hkv, int max_seq,
+                                                         int row_bytes, int src, ForkDsts dsts, int ndst, int start,
+                                                         int span16) {
+    // span16: 16-B units of one (layer, head) run = (end - start) * row_bytes / 16
+    const long per_cache = (long)layers * Hkv * span16;
+    const long total = 2 * per_cache;
+    for (long u = (long)blockIdx.x * kBlock + threadIdx.x; u < total; u += (long)gridDim.x * kBlock) {
+        const bool isv = u >= per_cache;
+        const long w = isv ? u - per_cache : u;
+        const int lh = (int)(w / span16), off = (int)(w - (long)lh * span16);
+        const int layer = lh / Hkv, h = lh - layer * Hkv;
+        uint8_t* base = isv ? vc : kc;
+        const size_t run = (size_t)start * row_bytes + (size_t)off * 16;
+        auto at = [&](int slot) -> uint4* {
+            return reinterpret_cast<uint4*>(
+                base + ((((size_t)layer * num_slots + slot) * Hkv + h) * (size_t)max_seq) * row_bytes + run);
+        };
+        const uint4 v = *at(src);
+        for (int i = 0; i < ndst; ++i) *at(dsts.d[i]) = v;
+    }
+}
+
 extern "C" {
 
 int dmcp_abi_version() { return 13; }
@@ -997,6 +1029,26 @@ int dmcp_embedding(const void* table, const void* ids, void* out, int T, int H, 
     if (T <= 0) return 0;
     embedding_kernel<<<grid_for((size_t)T * (H / 8)), kBlock, 0, (hipStream_t)stream>>>(
         (const uint16_t*)table, (const int32_t*)ids, (uint16_t*)out, T, H, V);
+    return hipGetLastError();
+}
+
+// see kv_fork_kernel; row_bytes = head_dim x element size, a multiple of 16
+int dmcp_kv_fork(void* k_cache, void* v_cache, int layers, int num_slots, int Hkv, int max_seq, int row_bytes,
+                 int src, const int32_t* dsts, int ndst, int start, int end, void* stream) {
+    if (end <= start || ndst <= 0) return 0;
+    if (!k_cache || !v_cache || row_bytes % 16 != 0 || ndst > 32 || src < 0 || src >= num_slots || start < 0 ||
+        end > max_seq)
+        return hipErrorInvalidValue;
+    ForkDsts d{};
+    for (int i = 0; i < ndst; ++i) {
+        if (dsts[i] < 0 || dsts[i] >= num_slots) return hipErrorInvalidValue;
+        d.d[i] = dsts[i];
+    }
+    const int span16 = (int)((size_t)(end - start) * row_bytes / 16);
+    const long total = 2L * layers * Hkv * span16;
+    const int grid = (int)std::min<long>((total + kBlock - 1) / kBlock, 4096);
+    kv_fork_kernel<<<grid, kBlock, 0, (hipStream_t)stream>>>((uint8_t*)k_cache, (uint8_t*)v_cache, layers, num_slots,
+                                                             Hkv, max_seq, row_bytes, src, d, ndst, start, span16);
     return hipGetLastError();
 }
 

@@ -481,6 +481,26 @@ def masked_argmax(logits: torch.Tensor, mask: Optional[torch.Tensor] = None, voc
     return out
 
 
+def kv_fork(k_cache: torch.Tensor, v_cache: torch.Tensor, src: int, dsts, start: int, end: int) -> None:
+    """Slot ``src``'s K/V at positions [start, end) of every layer into each
+    slot of ``dsts`` (<= 32): one launch for both caches
+    ([layers, slots, Hkv, max_seq, D] bf16, or e4m3 bytes)."""
+    _req_kv(k_cache, v_cache, "kv_fork")
+    if k_cache.dim() != 5 or not k_cache.is_contiguous() or not v_cache.is_contiguous():
+        raise HipOpsError("kv_fork: caches must be contiguous [layers, slots, Hkv, max_seq, D]")
+    L, S, H, T, D = k_cache.shape
+    dl = [int(d) for d in dsts]
+    if not dl or end <= start:
+        return
+    if len(dl) > 32:
+        for i in range(0, len(dl), 32):
+            kv_fork(k_cache, v_cache, src, dl[i:i + 32], start, end)
+        return
+    arr = (ctypes.c_int32 * len(dl))(*dl)
+    _check(lib().dmcp_kv_fork(_ptr(k_cache), _ptr(v_cache), L, S, H, T, D * k_cache.element_size(), int(src), arr,
+                              len(dl), int(start), int(end), _stream()), "dmcp_kv_fork")
+
+
 def embedding(table: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     _req(table, torch.bfloat16, "embedding.table")
     _req(ids, torch.int32, "embedding.ids")

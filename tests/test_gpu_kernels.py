@@ -295,3 +295,27 @@ def test_decode_embed_norm_switches_the_grammar_mask(hip):
     assert torch.equal(m_hip.cpu(), m_ref)
     exp = [5 if (s >= 0 and int(last[s]) == Q and a >= 0) else int(m) for s, a, m in zip(src, alt, midx)]
     assert m_ref.tolist() == exp and exp != midx.tolist()
+
+
+@pytest.mark.parametrize("kv", ["bf16", "fp8"])
+def test_kv_fork_matches_indexed_copy(kv):
+    """hip.kv_fork (one launch, both caches, every layer) writes exactly what
+    the indexed copy cache[:, dsts, :, a:b] = cache[:, src, :, a:b] does, and
+    nothing outside [a, b) or the destination slots."""
+    from dmcp.ops import hip
+    dt = torch.uint8 if kv == "fp8" else torch.bfloat16
+    g = torch.Generator(device="cuda").manual_seed(3)
+    shape = (3, 40, 8, 256, 64)
+    if dt == torch.uint8:
+        kc = torch.randint(0, 120, shape, generator=g, device="cuda", dtype=torch.uint8)
+    else:
+        kc = torch.randn(shape, generator=g, device="cuda").to(dt)
+    vc = kc.flip(0).contiguous()
+    for src, dsts, a, b in ((5, [7, 0, 39], 17, 200), (2, list(range(8, 44 - 4)), 0, 256), (1, [3], 255, 256)):
+        rk, rv = kc.clone(), vc.clone()
+        idx = torch.tensor(dsts, device="cuda")
+        for r in (rk, rv):
+            r[:, idx, :, a:b] = r[:, src, :, a:b].unsqueeze(1)
+        hip.kv_fork(kc, vc, src, dsts, a, b)
+        torch.cuda.synchronize()
+        assert torch.equal(kc, rk) and torch.equal(vc, rv)

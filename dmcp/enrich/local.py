@@ -303,14 +303,19 @@ class _Seq:
 
 @dataclass
 class _Fork:
-    """A class head's method branches: each decodes in a slot holding the
-    head's KV [0, pos) -- the head's own, a copy, or a finished sibling's
-    (a branch writes only past ``pos``, so a sibling's slot is a valid start
-    for the next branch)."""
+    """A class head's method branches.  The head's slot (the anchor) keeps
+    the head's KV [0, pos); branch 0 continues in it, every other branch
+    decodes in a slot of its own that reads the keys below ``pos`` from the
+    anchor in place (``LocalLM.fork_share``: no copy), writing only past
+    ``pos`` -- so a finished branch's slot, anchor or not, is a valid start
+    for the next pending branch.  The anchor is released only when no
+    running branch reads it any more."""
     head: "_Seq"
     pos: int
     pending: Deque[Tuple[int, List[Segment]]]
     holders: set = field(default_factory=set)   # slots of running branches
+    anchor: int = -1                             # the head's slot
+    anchor_held: bool = True                     # a running branch decodes in the anchor
 
 
 from .feeds import IterFeed, QueueFeed  # noqa: E402,F401  (re-exported)
@@ -888,8 +893,9 @@ class LocalEngine:
             q.slot, q.pos, q.fork, q.forked = slot, pos, st, True
             q.shared, q.prompt, q.prefix_split = head.shared, head.prompt, head.prefix_split
             kids.append(q)
-        if src is not None and kids:
-            self.model.fork_kv(src, [q.slot for q in kids], self.model.prefix_len if head.shared else 0, pos)
+        share = [q.slot for q in kids if q.slot != st.anchor]
+        if share:  # the branches' keys below pos: the anchor's, read in place
+            self.model.fork_share(st.anchor, share, pos)
         nat = self._native
         for q in kids:
             if nat is not None:
@@ -937,33 +943,50 @@ class LocalEngine:
         inflight: Optional[dict] = None  # the batched prefill in flight
         forks: List[_Fork] = []  # forks with branches still waiting for a slot
         nat0 = self._native
+        self.model.fork_reset()  # no slot reads another's keys (a session left by an error included)
+
+        def release(slots: List[int]) -> None:
+            """Slots back to the free list, owning all their keys again."""
+            if slots:
+                self.model.fork_clear(slots)
+                free_slots.extend(slots)
 
         def fill(st: _Fork) -> None:
-            """Pending branches of ``st`` into free slots (KV copied from a sibling)."""
+            """Pending branches of ``st`` into free slots (reading the anchor in place)."""
             k = min(len(st.pending), len(free_slots))
             if k and st.holders:
-                active.extend(q for q in self._start_branches(st, [free_slots.pop() for _ in range(k)],
-                                                              next(iter(st.holders))) if not q.done)
+                active.extend(q for q in self._start_branches(st, [free_slots.pop() for _ in range(k)], st.anchor)
+                              if not q.done)
 
         def retire(q: _Seq) -> None:
             """A finished sequence: its slot back -- or to a branch of its
             class -- and its text to the result."""
             st = q.fork
-            if q.branches:  # a head: branch 0 continues in its slot
-                st = _Fork(q, nat0.pos(q.h) if nat0 is not None else q.pos, deque(enumerate(q.branches)))
+            if q.branches:  # a head: branch 0 continues in its slot, the anchor
+                st = _Fork(q, nat0.pos(q.h) if nat0 is not None else q.pos, deque(enumerate(q.branches)),
+                           anchor=q.slot)
                 self.stats["forks"] += 1
                 active.extend(k for k in self._start_branches(st, [q.slot], None) if not k.done)
                 fill(st)
                 if st.pending:
                     forks.append(st)
+                elif not st.holders:  # every branch finished at once
+                    release([q.slot])
             elif st is not None:  # a branch: a pending sibling takes its slot as it is
                 st.holders.discard(q.slot)
                 if st.pending:
                     active.extend(k for k in self._start_branches(st, [q.slot], None) if not k.done)
                 else:
-                    free_slots.append(q.slot)
+                    out = []
+                    if q.slot == st.anchor:
+                        st.anchor_held = False  # kept while other branches read it
+                    else:
+                        out.append(q.slot)
+                    if not st.holders and not st.anchor_held:
+                        out.append(st.anchor)  # the last reader finished
+                    release(out)
             else:
-                free_slots.append(q.slot)
+                release([q.slot])
             finished.append(q)
         try:
             while True:

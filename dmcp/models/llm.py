@@ -248,6 +248,12 @@ class LocalLM:
         self.cos_sin = ops.rope_tables(c.max_seq, c.head_dim, c.rope_theta, device=self.device).contiguous()
         self.scale = 1.0 / math.sqrt(c.head_dim)
         self.max_rows = max(c.max_batch, c.max_rows)
+        # method branches: per slot (parent slot, end) -- the decode attention
+        # reads a branch's keys below ``end`` from its class head's slot in
+        # place (fork_share); end 0 = none.  Device-resident, so captured
+        # decode graphs follow it.
+        self.fork_tab = torch.zeros((self.num_slots, 2), dtype=torch.int32, device=self.device)
+        self.fork_tab[:, 0] = torch.arange(self.num_slots, dtype=torch.int32, device=self.device)
         # shared prefix: its length in device memory, so captured decode
         # graphs follow it
         self.prefix_len = 0
@@ -605,6 +611,7 @@ class LocalLM:
             else:
                 q = ops.rope_kv(F.linear(h, self.w[f"l{i}.wqkv"]), positions, slots, self.cos_sin, kc, vc, c.n_heads)
             att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws, chunk=chunk,
+                                       fork=self.fork_tab,
                                        prefix=self._prefix(i, prefix_rows), splits=splits).view(B, c.n_heads * c.head_dim)
             if wide:
                 h = ops.wgemm_resid_norm(att, self.w[f"l{i}.wo"], resid, self.w[f"l{i}.ln2"], c.eps, self.wgemm_ws)
@@ -638,6 +645,7 @@ class LocalLM:
             else:
                 q = ops.pgemm_qkv(xq, xs, *w8[f"l{i}.wqkv"], positions, slots, self.cos_sin, kc, vc, c.n_heads)
             att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws, chunk=chunk,
+                                       fork=self.fork_tab,
                                        prefix=self._prefix(i, prefix_rows), splits=splits).view(B, c.hidden)
             aq, as_ = ops.mx_quant(att)
             if gpu:
@@ -681,6 +689,7 @@ class LocalLM:
             kc, vc = self.k_cache[i], self.v_cache[i]
             q = ops.fused_rope_kv(r, self.w[f"l{i}.wqkv"], c.eps, positions, slots, self.cos_sin, kc, vc, c.n_heads)
             att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws, chunk=chunk,
+                                       fork=self.fork_tab,
                                        prefix=self._prefix(i, prefix_rows), splits=splits)
             ops.fused_resid(att.view(B, c.n_heads * c.head_dim), self.w[f"l{i}.wo"], r)
             act = ops.fused_swiglu(r, self.w[f"l{i}.wgu"], c.eps)
@@ -746,6 +755,42 @@ class LocalLM:
         idx = torch.tensor(list(dsts), dtype=torch.long, device=self.device)
         for cache in (self.k_cache, self.v_cache):
             cache[:, idx, :, start:end] = cache[:, src, :, start:end].unsqueeze(1)
+
+    @torch.inference_mode()
+    def fork_share(self, src: int, dsts: Sequence[int], end: int) -> None:
+        """Every slot of ``dsts`` continues from slot ``src``'s keys / values
+        below ``end`` WITHOUT a copy: the decode attention reads them from
+        ``src`` in place (``fork_tab``).  The caller keeps ``src``'s positions
+        below ``end`` unchanged while any of ``dsts`` decodes (a branch only
+        writes past ``end``)."""
+        dl = [int(d) for d in dsts if int(d) != int(src)]
+        if not dl or end <= 0:
+            return
+        if not (0 <= src < self.num_slots) or any(not 0 <= d < self.num_slots for d in dl) or \
+                not (0 < end <= self.cfg.max_seq):
+            raise ValueError(f"fork_share: slot {src} -> {dl}, end {end}")
+        vals = torch.tensor([[int(src), int(end)]] * len(dl), dtype=torch.int32)
+        idx = torch.tensor(dl, dtype=torch.long)
+        if self.device.type == "cuda":
+            vals, idx = vals.to(self.device, non_blocking=True), idx.to(self.device, non_blocking=True)
+        self.fork_tab.index_copy_(0, idx, vals)
+
+    @torch.inference_mode()
+    def fork_reset(self) -> None:
+        """No slot has a parent (every slot owns all its keys)."""
+        self.fork_tab[:, 1] = 0
+
+    @torch.inference_mode()
+    def fork_clear(self, slots: Sequence[int]) -> None:
+        """``slots`` own all their keys again (a freed or newly admitted slot)."""
+        sl = [int(x) for x in slots]
+        if not sl:
+            return
+        vals = torch.tensor([[x, 0] for x in sl], dtype=torch.int32)
+        idx = torch.tensor(sl, dtype=torch.long)
+        if self.device.type == "cuda":
+            vals, idx = vals.to(self.device, non_blocking=True), idx.to(self.device, non_blocking=True)
+        self.fork_tab.index_copy_(0, idx, vals)
 
     def decode_select(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor,
                       masks: torch.Tensor, mask_idx: torch.Tensor) -> tuple:

@@ -36,10 +36,11 @@ def rope_kv(qkv, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out=None):
 
 
 def decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace=None, chunk: int = 256, out=None,
-                     prefix=None, splits=None):
+                     prefix=None, splits=None, fork=None):
     if q.is_cuda:
-        return hip.decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace, chunk, out, prefix, splits)
-    return reference.decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace, chunk, out, prefix)
+        return hip.decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace, chunk, out, prefix, splits,
+                                    fork)
+    return reference.decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace, chunk, out, prefix, fork)
 
 
 def prefill_attention(q, k_cache, v_cache, slot, start, prefix_slot=None, prefix_len=0, scale=1.0, out=None,

@@ -474,14 +474,28 @@ __device__ __forceinline__ const char* kv_at(const void* base, size_t off) {
     return static_cast<const char*>(base) + off * (KV8 ? 1 : 2);
 }
 
+// A row's K/V bases: its own slot's, and -- a method branch -- its class
+// head's slot (the parent), which holds the keys [.., fend) the branch
+// shares: keys below fend are read there in place, never copied.
+struct KVSrc {
+    const void* k;
+    const void* v;
+    const void* pk;
+    const void* pv;
+    int fend;  // 0: no parent
+};
+
 template <int D, bool KV8>
-__device__ __forceinline__ void load_kv_tile(const void* __restrict__ kb, const void* __restrict__ vb, int kt,
-                                             int end, int lane, KVTile<D, KV8>& t) {
+__device__ __forceinline__ void load_kv_tile(const KVSrc& src, int kt, int end, int lane, KVTile<D, KV8>& t) {
     using KRaw = std::conditional_t<KV8, uint2, uint4>;
     constexpr int VE = KV8 ? 16 : 8;  // elements per V chunk
     constexpr int CPK = D / VE;       // V chunks per key
     constexpr int NV = 32 * D / VE / kWave;
-    if (kt + 32 <= end) {
+    const bool par = kt + 32 <= src.fend;                // the whole tile is the parent's
+    const bool mixed = !par && kt < src.fend;            // the tile straddles the fork point
+    const void* kb = par ? src.pk : src.k;
+    const void* vb = par ? src.pv : src.v;
+    if (kt + 32 <= end && !mixed) {
         const char* kp = kv_at<KV8>(kb, (size_t)(kt + (lane & 15)) * D + 8 * (lane >> 4));
         const char* vp = kv_at<KV8>(vb, (size_t)kt * D + lane * VE);
 #pragma unroll
@@ -496,15 +510,17 @@ __device__ __forceinline__ void load_kv_tile(const void* __restrict__ kb, const 
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int key = min(kt + 16 * h + (lane & 15), end - 1);
+        const void* kk = key < src.fend ? src.pk : src.k;
 #pragma unroll
         for (int ks = 0; ks < D / 32; ++ks)
-            t.k[h][ks] = *reinterpret_cast<const KRaw*>(kv_at<KV8>(kb, (size_t)key * D + 32 * ks + 8 * (lane >> 4)));
+            t.k[h][ks] = *reinterpret_cast<const KRaw*>(kv_at<KV8>(kk, (size_t)key * D + 32 * ks + 8 * (lane >> 4)));
     }
 #pragma unroll
     for (int r = 0; r < NV; ++r) {
         const int ch = lane + kWave * r;
         const int key = min(kt + ch / CPK, end - 1);
-        t.v[r] = *reinterpret_cast<const uint4*>(kv_at<KV8>(vb, (size_t)key * D + (ch % CPK) * VE));
+        const void* vv = key < src.fend ? src.pv : src.v;
+        t.v[r] = *reinterpret_cast<const uint4*>(kv_at<KV8>(vv, (size_t)key * D + (ch % CPK) * VE));
     }
 }
 
@@ -548,8 +564,7 @@ __device__ __forceinline__ int vquad(int r, int q) {
 // matrix cores, then (prefetch) the tile two ahead is loaded into the same
 // registers while the softmax and the PV product run.
 template <int D, bool KV8>
-__device__ __forceinline__ void attn_tile_mfma(KVTile<D, KV8>& cur, bool prefetch, int kt_next,
-                                               const void* __restrict__ kb, const void* __restrict__ vb,
+__device__ __forceinline__ void attn_tile_mfma(KVTile<D, KV8>& cur, bool prefetch, int kt_next, const KVSrc& src,
                                                int kt, int end, int lane, int g16, uint16_t* vw,
                                                const uint16_t* tr0, int trk, int tr_half,
                                                const bf16x8_t (&qf)[D / 32], float& m, float& l,
@@ -591,7 +606,7 @@ __device__ __forceinline__ void attn_tile_mfma(KVTile<D, KV8>& cur, bool prefetc
             sacc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], sacc[h], 0, 0, 0);
         }
     }
-    if (prefetch) load_kv_tile<D, KV8>(kb, vb, kt_next, end, lane, cur);
+    if (prefetch) load_kv_tile<D, KV8>(src, kt_next, end, lane, cur);
     // S^T tile: register 4h+i = key kt + 16h + 4*g16 + i of query (lane&15).
     // Scale folded into one FMA per score; the key mask only on a partial
     // last tile; hardware exp2 and bf16 packing.
@@ -685,7 +700,7 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
     const int32_t* __restrict__ slot, const int32_t* __restrict__ seq_len, uint16_t* __restrict__ out,
     float* __restrict__ part_o, float* __restrict__ part_ml, int B, int Hkv, int G,
     int max_seq, int chunk, int splits, float scale_log2, int num_slots, const int32_t* __restrict__ plen,
-    int ps_max, const int32_t* __restrict__ prow) {
+    int ps_max, const int32_t* __restrict__ prow, const int32_t* __restrict__ fork) {
     static_assert(D % 32 == 0, "D must be a multiple of 32");
     constexpr int KS = D / 32;    // 32-dim k-steps of the S product
     constexpr int DB = D / 16;    // 16-row d blocks of O^T
@@ -743,17 +758,26 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
             qf[ks] = as_bf16x8(v);
         }
         const size_t head_off = ((size_t)s * Hkv + kh) * (size_t)max_seq * D;
-        const void* kb = kv_at<KV8>(k_cache, head_off);
-        const void* vb = kv_at<KV8>(v_cache, head_off);
+        KVSrc src{kv_at<KV8>(k_cache, head_off), kv_at<KV8>(v_cache, head_off), nullptr, nullptr, 0};
+        if (fork) {  // fork[2 s] = parent slot, fork[2 s + 1] = the end of the shared keys
+            const int ps = __builtin_amdgcn_readfirstlane(fork[2 * s]);
+            const int fe = __builtin_amdgcn_readfirstlane(fork[2 * s + 1]);
+            if (fe > 0 && ps >= 0 && ps < num_slots && ps != s) {
+                const size_t poff = ((size_t)ps * Hkv + kh) * (size_t)max_seq * D;
+                src.pk = kv_at<KV8>(k_cache, poff);
+                src.pv = kv_at<KV8>(v_cache, poff);
+                src.fend = min(fe, L);
+            }
+        }
         float m = -1e30f, l = 0.f;
         f32x4_t acc[DB];
 #pragma unroll
         for (int db = 0; db < DB; ++db) acc[db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
         KVTile<D, KV8> ta;
-        load_kv_tile<D, KV8>(kb, vb, start, end, lane, ta);
+        load_kv_tile<D, KV8>(src, start, end, lane, ta);
         for (int t = 0; t < ntiles; ++t) {
             const int kt = start + 32 * t;
-            attn_tile_mfma<D, KV8>(ta, t + 1 < ntiles, kt + 32, kb, vb, kt, end, lane, g16, vw, tr0, trk, tr_half, qf, m, l,
+            attn_tile_mfma<D, KV8>(ta, t + 1 < ntiles, kt + 32, src, kt, end, lane, g16, vw, tr0, trk, tr_half, qf, m, l,
                                    acc, scale_log2);
         }
         l += __shfl_xor(l, 16, kWave);
@@ -881,7 +905,7 @@ __global__ __launch_bounds__(kBlock) void kv_fork_kernel(uint8_t* __restrict__ k
 
 extern "C" {
 
-int dmcp_abi_version() { return 13; }
+int dmcp_abi_version() { return 14; }
 
 int dmcp_add_rmsnorm(const void* x, void* residual, const void* w, void* out, int rows, int H, float eps,
                      void* stream) {
@@ -927,7 +951,7 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
                           const void* seq_len, void* out, void* part_o, void* part_ml, int B, int Hq, int Hkv, int D,
                           int max_seq, int num_slots, int chunk, int splits, float scale, const void* prefix_k,
                           const void* prefix_v, const void* plen, int ps_max, int kv8, const void* prefix_rows,
-                          void* stream) {
+                          const void* fork, void* stream) {
     if (B <= 0) return 0;
     if (Hkv <= 0 || Hq % Hkv != 0 || splits <= 0 || chunk <= 0 || !(D == 64 || D == 128) || Hq / Hkv > 16)
         return hipErrorInvalidValue;
@@ -968,7 +992,7 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
         const dim3 wgrid((unsigned)(wblocks < cap ? wblocks : cap));                                               \
         decode_attn_mfma_kernel<DD, K8><<<wgrid, kBlock, 0, st>>>(qq, k_cache, v_cache, sl, ln, oo, po, pml, B,   \
                                                                   Hkv, G, max_seq, chunk, splits, sl2, num_slots, \
-                                                                  pl, ps_max, pr);                                \
+                                                                  pl, ps_max, pr, (const int32_t*)fork);          \
     } while (0)
     if (kv8) {
         if (D == 64) DMCP_MFMA_DECODE(64, true);

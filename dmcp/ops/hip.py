@@ -26,7 +26,7 @@ _lock = threading.Lock()
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _f = ctypes.c_float
-ABI_VERSION = 13  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
+ABI_VERSION = 14  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
 
 
 class HipOpsError(RuntimeError):
@@ -54,7 +54,8 @@ def lib() -> ctypes.CDLL:
             "dmcp_add_rmsnorm": ([_vp, _vp, _vp, _vp, _i, _i, _f, _vp], _i),
             "dmcp_rope_kv": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp], _i),
             "dmcp_decode_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _f,
-                                       _vp, _vp, _vp, _i, _i, _vp, _vp], _i),
+                                       _vp, _vp, _vp, _i, _i, _vp, _vp, _vp], _i),
+            "dmcp_kv_fork": ([_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _vp], _i),
             "dmcp_prefill_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _i, _i,
                                         _i, _vp], _i),
             "dmcp_prefill_varlen": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, ctypes.c_long, _f,
@@ -225,8 +226,13 @@ def decode_plan(rows: int, n_kv_heads: int, max_seq: int, target_waves: int = 40
 def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: torch.Tensor,
                      seq_len: torch.Tensor, scale: float, workspace: Optional[tuple] = None,
                      chunk: int = 256, out: Optional[torch.Tensor] = None,
-                     prefix: Optional["SharedPrefix"] = None, splits: Optional[int] = None) -> torch.Tensor:
+                     prefix: Optional["SharedPrefix"] = None, splits: Optional[int] = None,
+                     fork: Optional[torch.Tensor] = None) -> torch.Tensor:
     """q [B, Hq, D]; caches [S, Hkv, MAXS, D]; slot/seq_len int32 [B].
+
+    ``fork`` (int32 [S, 2], optional): per slot (parent slot, end) -- a
+    method branch reads its keys below ``end`` from its class head's slot in
+    place (no copy); end 0 = no parent.
 
     Each row's keys (after the shared prefix) are split into at most
     ``splits`` equal parts of >= ``chunk`` keys (default: as many as
@@ -277,6 +283,10 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
                 raise HipOpsError("decode_attention: prefix.rows has fewer than B entries")
         if workspace is not None and workspace[1].numel() < 2 * B * Hq * (splits + ps_max):
             raise HipOpsError(f"decode_attention: workspace holds fewer than {splits} + {ps_max} partials per row")
+    if fork is not None:
+        _req(fork, torch.int32, "decode_attention.fork")
+        if fork.numel() < 2 * S or not fork.is_contiguous():
+            raise HipOpsError(f"decode_attention: fork table must be a contiguous int32 [{S}, 2]")
     out = torch.empty_like(q) if out is None else out
     _req_out(out, torch.bfloat16, B * Hq * D, "decode_attention.out")
     if splits > 1 or ps_max:
@@ -291,7 +301,7 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     _check(lib().dmcp_decode_attention(_ptr(q), _ptr(k_cache), _ptr(v_cache), _ptr(slot), _ptr(seq_len), _ptr(out),
                                        _ptr(part_o), _ptr(part_ml), B, Hq, Hkv, D, MAXS, S, chunk, splits,
                                        float(scale), _ptr(pk), _ptr(pv), _ptr(plen), ps_max, kv8, _ptr(prows),
-                                       _stream()), "dmcp_decode_attention")
+                                       _ptr(fork), _stream()), "dmcp_decode_attention")
     return out
 
 
@@ -497,7 +507,8 @@ def kv_fork(k_cache: torch.Tensor, v_cache: torch.Tensor, src: int, dsts, start:
             kv_fork(k_cache, v_cache, src, dl[i:i + 32], start, end)
         return
     arr = (ctypes.c_int32 * len(dl))(*dl)
-    _check(lib().dmcp_kv_fork(_ptr(k_cache), _ptr(v_cache), L, S, H, T, D * k_cache.element_size(), int(src), arr,
+    _check(lib().dmcp_kv_fork(_ptr(k_cache), _ptr(v_cache), L, S, H, T, D * k_cache.element_size(), int(src),
+                              ctypes.cast(arr, ctypes.c_void_p),
                               len(dl), int(start), int(end), _stream()), "dmcp_kv_fork")
 
 

@@ -97,7 +97,11 @@ class SharedPrefix(NamedTuple):
 
 def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: torch.Tensor,
                      seq_len: torch.Tensor, scale: float, workspace=None, chunk: int = 256,
-                     out: Optional[torch.Tensor] = None, prefix: Optional[SharedPrefix] = None) -> torch.Tensor:
+                     out: Optional[torch.Tensor] = None, prefix: Optional[SharedPrefix] = None,
+                     fork: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``fork`` [S, 2] (parent slot, end): keys below ``end`` of a row whose
+    slot has a parent come from the parent's slot (a method branch reading
+    its class head's KV in place)."""
     B, Hq, D = q.shape
     S, Hkv, MAXS, _ = k_cache.shape
     G = Hq // Hkv
@@ -109,6 +113,11 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
             continue
         k = kv_float(k_cache[s, :, :L])  # [Hkv, L, D]
         v = kv_float(v_cache[s, :, :L])
+        if fork is not None:
+            ps, fe = int(fork[s, 0]), min(int(fork[s, 1]), L)
+            if fe > 0 and 0 <= ps < S and ps != s:
+                k = torch.cat([kv_float(k_cache[ps, :, :fe]), k[:, fe:]], dim=1)
+                v = torch.cat([kv_float(v_cache[ps, :, :fe]), v[:, fe:]], dim=1)
         if P > 0 and (prefix.rows is None or int(prefix.rows[b]) != 0):  # the first P keys: the shared prefix
             k = torch.cat([kv_float(prefix.k[:, :P]), k[:, P:]], dim=1)
             v = torch.cat([kv_float(prefix.v[:, :P]), v[:, P:]], dim=1)

@@ -319,3 +319,43 @@ def test_kv_fork_matches_indexed_copy(kv):
         hip.kv_fork(kc, vc, src, dsts, a, b)
         torch.cuda.synchronize()
         assert torch.equal(kc, rk) and torch.equal(vc, rv)
+
+
+@pytest.mark.parametrize("kv", ["bf16", "fp8"])
+@pytest.mark.parametrize("splits", [1, 4])
+@pytest.mark.parametrize("P", [0, 300])
+def test_decode_attention_fork_table(hip, kv, splits, P):
+    """Method branches (fork table: slot -> (parent slot, end)): a row reads
+    its keys below ``end`` from the parent slot in place.  Bit-identical to
+    the same kernel on caches where those keys were copied into the row's
+    slot; fork ends inside a 32-key tile, on a tile edge, past the row's
+    length; a shared prefix in front; rows without a parent unchanged."""
+    from dmcp.ops.reference import SharedPrefix
+    D, Hq, Hkv, MAXS, S = 64, 32, 8, 1024, 10
+    dt = torch.uint8 if kv == "fp8" else torch.bfloat16
+
+    def cache(seed):
+        x = _bf(S + 1, Hkv, MAXS, D, seed=seed)
+        return x.to(torch.float8_e4m3fn).view(torch.uint8) if kv == "fp8" else x
+    kc, vc = cache(31), cache(32)
+    rows = [(1, None, 700), (2, (1, P + 77), 690), (3, (1, P + 96), 500), (4, (1, P + 600), 420),
+            (5, None, P + 3), (6, (5, P + 2), P + 40)]
+    B = len(rows)
+    q = _bf(B, Hq, D, seed=33)
+    slot = torch.tensor([r[0] for r in rows], dtype=torch.int32, device="cuda")
+    lens = torch.tensor([max(r[2], P + 1) for r in rows], dtype=torch.int32, device="cuda")
+    fork = torch.stack([torch.arange(S + 1), torch.zeros(S + 1, dtype=torch.long)], 1).to(torch.int32).cuda()
+    kc2, vc2 = kc.clone(), vc.clone()
+    for b, (s, par, _) in enumerate(rows):
+        if par is not None:
+            fork[s] = torch.tensor(par, dtype=torch.int32)
+            e = min(par[1], int(lens[b]))
+            kc2[s, :, P:e], vc2[s, :, P:e] = kc[par[0], :, P:e], vc[par[0], :, P:e]
+    pre = pre2 = None
+    if P:
+        pl = torch.tensor([P], dtype=torch.int32, device="cuda")
+        pre, pre2 = SharedPrefix(kc[S], vc[S], pl), SharedPrefix(kc2[S], vc2[S], pl)
+    got = hip.decode_attention(q, kc, vc, slot, lens, 0.125, chunk=64, prefix=pre, splits=splits, fork=fork)
+    exp = hip.decode_attention(q, kc2, vc2, slot, lens, 0.125, chunk=64, prefix=pre2, splits=splits)
+    assert torch.equal(got, exp)
+    assert dt == kc.dtype

@@ -520,3 +520,46 @@ def test_prefill_dtype_auto_is_bf16_off_gpu():
     assert not m.prefill_fp8
     with _pytest.raises(ValueError):
         LocalLM(preset("tiny", prefill_dtype="int8", max_batch=2, max_seq=256), device="cpu", seed=0)
+
+
+def test_branches_read_the_head_kv_in_place_as_a_copy_would():
+    """Method branches read their class head's keys from the anchor slot in
+    place (LocalLM.fork_share + the fork table of the decode attention):
+    the replies equal an engine whose branches get a copy of the head's KV
+    (fork_kv), with the slots handed around on 4 KV slots; every slot owns
+    its keys again afterwards."""
+    names = [f"m{i}" for i in range(9)]
+    inputs = [EnrichmentInput("class S%d { int x; }" % i, f"co.x.S{i}", "java", "SERVICE", names[: 3 + 2 * i])
+              for i in range(3)]
+    m = LocalLM(preset("tiny", max_batch=4, max_rows=64, max_seq=2048), device="cpu", seed=2)
+    shared = LocalEngine(m, use_graphs=False).generate(inputs, "readme")
+    assert int(m.fork_tab[:, 1].max()) == 0
+
+    class Copying(LocalLM):
+        def fork_share(self, src, dsts, end):  # the pre-sharing behaviour: copy [P, end)
+            self.fork_kv(src, dsts, self.prefix_len, end)
+
+    c = Copying(preset("tiny", max_batch=4, max_rows=64, max_seq=2048), device="cpu", seed=2)
+    copied = LocalEngine(c, use_graphs=False).generate(inputs, "readme")
+    assert shared == copied
+
+
+def test_decode_attention_fork_table_matches_copied_kv():
+    """reference decode_attention: a row whose slot has a parent reads the
+    keys below the fork end from the parent slot -- the same as copying them."""
+    from dmcp.ops import reference as R
+    g = torch.Generator().manual_seed(0)
+    S, H, T, D, G = 6, 2, 64, 16, 2
+    kc, vc = torch.randn(S, H, T, D, generator=g).bfloat16(), torch.randn(S, H, T, D, generator=g).bfloat16()
+    q = torch.randn(3, H * G, D, generator=g).bfloat16()
+    slot = torch.tensor([1, 3, 4], dtype=torch.int32)
+    seq = torch.tensor([40, 50, 9], dtype=torch.int32)
+    fork = torch.stack([torch.arange(S), torch.zeros(S, dtype=torch.long)], 1).to(torch.int32)
+    fork[3] = torch.tensor([0, 30])
+    fork[4] = torch.tensor([0, 30])  # end past the row's length: all its keys from the parent
+    got = R.decode_attention(q, kc, vc, slot, seq, 0.25, fork=fork)
+    k2, v2 = kc.clone(), vc.clone()
+    k2[3, :, :30], v2[3, :, :30] = kc[0, :, :30], vc[0, :, :30]
+    k2[4, :, :9], v2[4, :, :9] = kc[0, :, :9], vc[0, :, :9]
+    exp = R.decode_attention(q, k2, v2, slot, seq, 0.25)
+    assert torch.equal(got, exp)

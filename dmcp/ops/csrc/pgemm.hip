@@ -68,7 +68,6 @@ constexpr int PB_BYTES = PBN * PBK;                     // W image
 // A image), so row r's 2 bytes sit at 4 r
 constexpr int PS_BYTES = PBM * 4;
 constexpr int PST_BYTES = PA_BYTES + PB_BYTES + PS_BYTES;
-constexpr int PGL = 9;                                  // LDS-DMA instructions per wave per stage
 constexpr int PM_BF16 = 0, PM_RESID = 1, PM_SWIGLU = 2, PM_QKV = 3;
 
 struct PEpi {
@@ -126,10 +125,17 @@ __device__ __forceinline__ uint8_t to_fp8(float x) {
 __device__ long long pg_stamps[65536][4];
 #endif
 
-template <int MODE, bool KV8>
-__global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) void pgemm_kernel(
+// WV = 4: one wave per SIMD, 128 x 128 per wave (16 MFMAs, 9 LDS-DMA pieces
+// per stage); WV = 8: two waves per SIMD, 128 x 64 per wave (8 MFMAs, 4-5
+// pieces) -- one wave's MFMAs run while the other issues its DMAs.
+template <int MODE, bool KV8, int WV>
+__global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4, WV / 4))) void pgemm_kernel(
     const uint8_t* __restrict__ aq, const uint8_t* __restrict__ as, const uint8_t* __restrict__ wq,
     const float* __restrict__ ws, int M, int N, int K, int mtiles, int ntiles, PEpi e) {
+    constexpr int NU = WV == 4 ? 4 : 2;  // 32-column tiles per wave
+    constexpr int WNW = WV / 2;          // waves along N
+    constexpr int CPW = PBN / WNW;       // columns per wave
+    constexpr int PPW = 16 / WV;         // 1-KiB LDS-DMA pieces per wave per operand per stage
     __shared__ __attribute__((aligned(16))) uint8_t plds[PST * PST_BYTES];  // ONE LDS object (ring, then epilogue)
 #if (PG_PROBE & 4) != 0
     const long long t_start = __builtin_amdgcn_s_memtime();
@@ -138,8 +144,9 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wv = __builtin_amdgcn_readfirstlane(tid / kWave);
-    const int wm = wv >> 1, wn = wv & 1;
+    const int wm = wv / WNW, wn = wv % WNW;
     const int l32 = lane & 31, hh = lane >> 5;
+    const bool scl = WV == 4 || wv < 4;  // this wave fetches 64 rows' A scales per stage
 
     // block -> tile: XCD-contiguous ranges (bijective for any grid), then
     // 8 M tiles per group with N fastest inside the group's column
@@ -155,12 +162,12 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int mt = first + inn % gsz, nt = inn / gsz;
     const int m0 = mt * PBM;
 
-    // weight row of LDS image row r (SwiGLU: per wave 64 gate rows then the
-    // 64 up rows of the same intermediate columns)
+    // weight row of LDS image row r (SwiGLU: per wave CPW / 2 gate rows then
+    // the up rows of the same intermediate columns)
     auto wrow = [&](int r) -> int {
         if constexpr (MODE == PM_SWIGLU) {
-            const int w2 = r >> 7, t = (r >> 6) & 1, i = r & 63;
-            return (t ? e.I : 0) + nt * 128 + w2 * 64 + i;
+            const int w2 = r / CPW, t = (r % CPW) >= CPW / 2, i = r % (CPW / 2);
+            return (t ? e.I : 0) + nt * 128 + w2 * (CPW / 2) + i;
         } else {
             return nt * PBN + r;
         }
@@ -168,33 +175,33 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
     // LDS-DMA sources: lane L of a 1-KiB piece fills image row base + L / 4,
     // slot L % 4 with logical 16-B chunk (L % 4) ^ ((row >> 2) & 3)
-    const uint8_t* asrc[4];
-    const uint8_t* wsrc[4];
+    const uint8_t* asrc[PPW];
+    const uint8_t* wsrc[PPW];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = (wv * 4 + i) * 16 + (lane >> 2);
+    for (int i = 0; i < PPW; ++i) {
+        const int r = (wv * PPW + i) * 16 + (lane >> 2);
         const int ch = (lane & 3) ^ ((r >> 2) & 3);
         asrc[i] = aq + (size_t)min(m0 + r, M - 1) * K + ch * 16;
         wsrc[i] = wq + (size_t)wrow(r) * K + ch * 16;
     }
     // A scales: lane L of wave w fetches the stage's 2 bytes of row 64 w + L
     const int ksb = K >> 5;
-    const uint8_t* ssrc = as + (size_t)min(m0 + wv * 64 + lane, M - 1) * ksb;
+    const uint8_t* ssrc = as + (size_t)min(m0 + (wv & 3) * 64 + lane, M - 1) * ksb;
 
     auto issue = [&](int c, int st) {
         uint8_t* base = plds + st * PST_BYTES;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) pglds<16>(asrc[i] + c * PBK, base + (wv * 4 + i) * 1024);
+        for (int i = 0; i < PPW; ++i) pglds<16>(asrc[i] + c * PBK, base + (wv * PPW + i) * 1024);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) pglds<16>(wsrc[i] + c * PBK, base + PA_BYTES + (wv * 4 + i) * 1024);
-        pglds<2>(ssrc + c * 2, base + PA_BYTES + PB_BYTES + wv * 256);
+        for (int i = 0; i < PPW; ++i) pglds<16>(wsrc[i] + c * PBK, base + PA_BYTES + (wv * PPW + i) * 1024);
+        if (scl) pglds<2>(ssrc + c * 2, base + PA_BYTES + PB_BYTES + (wv & 3) * 256);
     };
 
-    f32x16_t acc[4][4];
+    f32x16_t acc[4][NU];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < NU; ++u)
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[t][u][i] = 0.f;
 
@@ -226,20 +233,25 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     auto piece = [&](int i, int cc, int st) {
         if constexpr ((PG_PROBE & 1) != 0) return;
         uint8_t* base = plds + st * PST_BYTES;
-        if (i < 4) pglds<16>(asrc[i] + cc * PBK, base + (wv * 4 + i) * 1024);
-        else if (i < 8) pglds<16>(wsrc[i - 4] + cc * PBK, base + PA_BYTES + (wv * 4 + i - 4) * 1024);
-        else pglds<2>(ssrc + cc * 2, base + PA_BYTES + PB_BYTES + wv * 256);
+        if (i < PPW) pglds<16>(asrc[i] + cc * PBK, base + (wv * PPW + i) * 1024);
+        else if (i < 2 * PPW) pglds<16>(wsrc[i - PPW] + cc * PBK, base + PA_BYTES + (wv * PPW + i - PPW) * 1024);
+        else if (scl) pglds<2>(ssrc + cc * 2, base + PA_BYTES + PB_BYTES + (wv & 3) * 256);
     };
+    // LDS-DMA instructions of this wave per stage: the counted waits leave
+    // two stages' worth in flight
+    constexpr int GL_S = 2 * PPW + 1, GL_N = 2 * PPW;
     auto wait_stage = [&]() {  // stage c + 1 landed (this wave), stage c's reads done, then every wave
         if constexpr ((PG_PROBE & 1) != 0)
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        else if (scl)
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(GL_S * (PST - 2)) : "memory");
         else
-            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(PGL * (PST - 2)) : "memory");
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(GL_N * (PST - 2)) : "memory");
         if constexpr ((PG_PROBE & 2) == 0) asm volatile("s_barrier" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
     };
     struct Frags {
-        v8i_t a0, b[4];
+        v8i_t a0, b[NU];
         int s0;
     };
     auto stage_ptr = [&](int c) -> const uint8_t* { return plds + (c % PST) * PST_BYTES; };
@@ -249,7 +261,7 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         F.a0 = frag(A, r);
         F.s0 = A[PA_BYTES + PB_BYTES + r * 4 + hh];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) F.b[u] = frag(A + PA_BYTES, wn * 128 + u * 32 + l32);
+        for (int u = 0; u < NU; ++u) F.b[u] = frag(A + PA_BYTES, wn * CPW + u * 32 + l32);
     };
     auto step = [&](int c, const Frags& F, Frags& G) {
         const uint8_t* A = stage_ptr(c);
@@ -270,42 +282,32 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             // t * 32 + l32, register i weight column (i & 3) + 8 (i >> 2) + 4 hh
             acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(F.b[u], a, acc[t][u], 0, 0, 0, 127, 0, sc);
         };
-        // every read is issued right after an MFMA, >= 3 MFMAs ahead of its
-        // first use (the waitcnt pass cannot count LDS reads past pending
-        // LDS-DMAs: each use waits lgkmcnt(0), so nothing younger may be in
-        // flight then)
+        // every read is issued right after an MFMA, ahead of its first use
+        // (the waitcnt pass cannot count LDS reads past pending LDS-DMAs: each
+        // use waits lgkmcnt(0), so nothing younger may be in flight then);
+        // the DMA pieces one per MFMA from the first
+        constexpr int NP = 2 * PPW + 1;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            __builtin_amdgcn_sched_barrier(0);
-            mma(0, u);
-            __builtin_amdgcn_sched_barrier(0);
-            if (u == 0) aread(1);
-            piece(u, cn, sn);
-        }
+        for (int t = 0; t < 3; ++t)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            __builtin_amdgcn_sched_barrier(0);
-            mma(1, u);
-            __builtin_amdgcn_sched_barrier(0);
-            if (u == 0) {
-                aread(2);
-                aread(3);
+            for (int u = 0; u < NU; ++u) {
+                const int idx = t * NU + u;
+                __builtin_amdgcn_sched_barrier(0);
+                mma(t, u);
+                __builtin_amdgcn_sched_barrier(0);
+                if (idx == 0) aread(1);
+                if (idx == NU) {
+                    aread(2);
+                    aread(3);
+                }
+                if (idx < NP) piece(idx, cn, sn);
             }
-            piece(4 + u, cn, sn);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        mma(2, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        piece(8, cn, sn);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int u = 1; u < 4; ++u) mma(2, u);
         __builtin_amdgcn_sched_barrier(0);
         wait_stage();
         pre(c + 1, G);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) mma(3, u);
+        for (int u = 0; u < NU; ++u) mma(3, u);
     };
     const int chunks = chunks_of(K);
 #pragma unroll
@@ -313,20 +315,72 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // stage 0: landed for every wave, its first fragments read
     if constexpr ((PG_PROBE & 1) != 0)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (scl)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(GL_S * (PST - 2)) : "memory");
     else
-        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PGL * (PST - 2)) : "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(GL_N * (PST - 2)) : "memory");
     asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    Frags F0, F1;
-    pre(0, F0);
-    // two steps per trip: the register sets swap roles by name, never by a
-    // runtime index (cdna_hip_programming.md §5.4 rule 20)
-    int c = 0;
-    for (; c + 1 < chunks; c += 2) {
-        step(c, F0, F1);
-        step(c + 1, F1, F0);
+    if constexpr (WV == 8) {
+        // two waves per SIMD: the partner wave hides this one's read latency,
+        // so no second fragment set (it would not fit beside 128 accumulators
+        // in a wave's 256 registers): each step waits for its stage, reads,
+        // computes; the barrier at its top also retires every wave's reads of
+        // the slot the step refills
+        for (int c = 0; c < chunks; ++c) {
+            if (c > 0) {
+                if constexpr ((PG_PROBE & 1) != 0)
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                else if (scl)
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(GL_S * (PST - 2)) : "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(GL_N * (PST - 2)) : "memory");
+                asm volatile("s_barrier" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            const uint8_t* A = stage_ptr(c);
+            const uint8_t* S = A + PA_BYTES + PB_BYTES;
+            const int cn = min(c + PST - 1, chunks - 1), sn = (c + PST - 1) % PST;
+            v8i_t af[4], bf[NU];
+            int sa[4];
+            auto aread = [&](int t) {
+                const int r = wm * 128 + t * 32 + l32;
+                af[t] = frag(A, r);
+                sa[t] = S[r * 4 + hh];
+            };
+            aread(0);
+#pragma unroll
+            for (int u = 0; u < NU; ++u) bf[u] = frag(A + PA_BYTES, wn * CPW + u * 32 + l32);
+            constexpr int NP = 2 * PPW + 1;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int u = 0; u < NU; ++u) {
+                    const int idx = t * NU + u;
+                    __builtin_amdgcn_sched_barrier(0);
+                    acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bf[u], af[t], acc[t][u], 0, 0, 0, 127,
+                                                                                0, sa[t]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (idx == 0) aread(1);
+                    if (idx == NU) {
+                        aread(2);
+                        aread(3);
+                    }
+                    if (idx < NP) piece(idx, cn, sn);
+                }
+        }
+    } else {
+        Frags F0, F1;
+        pre(0, F0);
+        // two steps per trip: the register sets swap roles by name, never by a
+        // runtime index (cdna_hip_programming.md §5.4 rule 20)
+        int c = 0;
+        for (; c + 1 < chunks; c += 2) {
+            step(c, F0, F1);
+            step(c + 1, F1, F0);
+        }
+        if (c < chunks) step(c, F0, F1);
     }
-    if (c < chunks) step(c, F0, F1);
     // the refills past the last stage land before the block's LDS is released
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #if (PG_PROBE & 4) != 0
@@ -340,7 +394,7 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // columns 0-7 and 16-23 and lanes 32-63 with 8-15 and 24-31: two 16-B
     // (bf16) or 8-B (fp8) stores per lane per tile, no LDS round trip.
     const int mw = m0 + wm * 128;  // first row of this wave's tile
-    const int n0 = nt * PBN + wn * 128;
+    const int n0 = nt * PBN + wn * CPW;
     auto swap2 = [&](uint32_t& a, uint32_t& b) {  // lanes 32-63 of a <-> lanes 0-31 of b
         const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
         a = r[0];
@@ -380,7 +434,7 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     };
     if constexpr (MODE == PM_BF16 || MODE == PM_RESID) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < NU; ++u) {
             float sc[16];
             scales16(ws + n0 + u * 32, sc);
             const int col = n0 + u * 32 + 8 * hh;
@@ -421,12 +475,12 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             }
         }
     } else if constexpr (MODE == PM_SWIGLU) {
-        // tiles u = 0, 1: gate columns j0 + 32 u .., tiles u + 2: the up
-        // columns of the same intermediates (the wrow interleave above)
-        const int j0 = nt * 128 + wn * 64;
+        // tiles u < NU / 2: gate columns j0 + 32 u .., tiles u + NU / 2: the
+        // up columns of the same intermediates (the wrow interleave above)
+        const int j0 = nt * 128 + wn * (CPW / 2);
         const int isb = e.I >> 5;
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < NU / 2; ++u) {
             float sg[16], su[16];
             scales16(ws + j0 + u * 32, sg);
             scales16(ws + e.I + j0 + u * 32, su);
@@ -438,7 +492,7 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     // gate / up rounded to bf16 as the bf16 GEMM's outputs are
-                    const float g = bf2f(f2bf(acc[t][u][i] * sg[i])), uu = bf2f(f2bf(acc[t][u + 2][i] * su[i]));
+                    const float g = bf2f(f2bf(acc[t][u][i] * sg[i])), uu = bf2f(f2bf(acc[t][u + NU / 2][i] * su[i]));
                     a[i] = bf2f(f2bf(psilu(g) * uu));
                     amax = __builtin_fmaxf(amax, __builtin_fabsf(a[i]));
                 }
@@ -457,7 +511,7 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
     } else {  // PM_QKV: tiles 2 g, 2 g + 1 = d 0..31, 32..63 of head h0 + g
         const int h0 = n0 >> 6;
-        const bool kv = h0 + 1 >= e.Hq;  // some head of this wave goes to the caches
+        const bool kv = h0 + NU / 2 - 1 >= e.Hq;  // some head of this wave goes to the caches
         int pos[4], sl[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -465,9 +519,9 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             pos[t] = e.pos[mc];
             sl[t] = kv ? e.slot[mc] : -1;
         }
-        float sc[4][16];
+        float sc[NU][16];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) scales16(ws + n0 + u * 32, sc[u]);
+        for (int u = 0; u < NU; ++u) scales16(ws + n0 + u * 32, sc[u]);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int m = mw + t * 32 + l32;
@@ -482,7 +536,7 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 cs_c[4 * j + 2] = p1.x; cs_s[4 * j + 2] = p1.y; cs_c[4 * j + 3] = p1.z; cs_s[4 * j + 3] = p1.w;
             }
 #pragma unroll
-            for (int g = 0; g < 2; ++g) {
+            for (int g = 0; g < NU / 2; ++g) {
                 const int head = h0 + g;
                 float lo[16], hi[16];
 #pragma unroll
@@ -880,13 +934,19 @@ __global__ void mx_probe_kernel(const v8i_t* a, const v8i_t* b, const int* sa, c
     c[l] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a[l], b[l], acc, 0, 0, 0, sa[l], 0, sb[l]);
 }
 
+int g_pgemm_waves = 4;  // dmcp_pgemm_set_waves: 4 (one wave per SIMD) or 8 (two)
+
 template <int MODE, bool KV8>
 hipError_t launch_pgemm(const void* aq, const void* as, const void* wq, const void* ws, int M, int N, int K,
                         const PEpi& e, void* stream) {
     const int mtiles = (M + PBM - 1) / PBM;
     const int ntiles = MODE == PM_SWIGLU ? e.I / 128 : N / PBN;
-    pgemm_kernel<MODE, KV8><<<mtiles * ntiles, PTH, 0, (hipStream_t)stream>>>(
-        (const uint8_t*)aq, (const uint8_t*)as, (const uint8_t*)wq, (const float*)ws, M, N, K, mtiles, ntiles, e);
+    if (g_pgemm_waves == 8)
+        pgemm_kernel<MODE, KV8, 8><<<mtiles * ntiles, 512, 0, (hipStream_t)stream>>>(
+            (const uint8_t*)aq, (const uint8_t*)as, (const uint8_t*)wq, (const float*)ws, M, N, K, mtiles, ntiles, e);
+    else
+        pgemm_kernel<MODE, KV8, 4><<<mtiles * ntiles, PTH, 0, (hipStream_t)stream>>>(
+            (const uint8_t*)aq, (const uint8_t*)as, (const uint8_t*)wq, (const float*)ws, M, N, K, mtiles, ntiles, e);
     return hipGetLastError();
 }
 
@@ -897,6 +957,13 @@ bool pgemm_shape_ok(const void* aq, const void* as, const void* wq, const void* 
 }  // namespace
 
 extern "C" {
+
+// waves per block of the MX prefill GEMMs (4 or 8); returns the previous value
+int dmcp_pgemm_set_waves(int w) {
+    const int old = g_pgemm_waves;
+    if (w == 4 || w == 8) g_pgemm_waves = w;
+    return old;
+}
 
 // mode 0: y[M, N] = bf16(A . W^T);  mode 1: y (= resid) += bf16(A . W^T).
 // A: aq [M, K] e4m3 + as [M, K / 32] E8M0; W: wq [N, K] e4m3 + ws [N] fp32.

@@ -56,6 +56,7 @@ def lib() -> ctypes.CDLL:
             "dmcp_decode_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _f,
                                        _vp, _vp, _vp, _i, _i, _vp, _vp, _vp], _i),
             "dmcp_kv_fork": ([_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _vp], _i),
+            "dmcp_pgemm_set_waves": ([_i], _i),
             "dmcp_prefill_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _i, _i,
                                         _i, _vp], _i),
             "dmcp_prefill_varlen": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, ctypes.c_long, _f,
@@ -489,6 +490,14 @@ def masked_argmax(logits: torch.Tensor, mask: Optional[torch.Tensor] = None, voc
     _check(lib().dmcp_masked_argmax(_ptr(logits), _ptr(mask), _ptr(mask_idx if mask is not None else None), n_masks,
                                     _ptr(out), B, V, ld, _stream()), "dmcp_masked_argmax")
     return out
+
+
+def pgemm_set_waves(waves: int) -> int:
+    """Waves per block of the MX prefill GEMMs: 4 (one per SIMD, 128 x 128
+    each) or 8 (two per SIMD, 128 x 64 each).  Returns the previous value."""
+    if waves not in (4, 8):
+        raise HipOpsError(f"pgemm_set_waves: 4 or 8, got {waves}")
+    return int(lib().dmcp_pgemm_set_waves(int(waves)))
 
 
 def kv_fork(k_cache: torch.Tensor, v_cache: torch.Tensor, src: int, dsts, start: int, end: int) -> None:

@@ -52,10 +52,14 @@ def main() -> int:
     ap.add_argument("--rows", type=int, default=24576)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--decode-rows", type=int, nargs="*", default=[78, 320, 512])
+    ap.add_argument("--waves", type=int, default=0, choices=[0, 4, 8],
+                    help="waves per block of the MX prefill GEMM (0: the library default)")
     a = ap.parse_args()
     from dmcp import ops
     from dmcp.models.llm import preset
     from dmcp.ops import hip, reference as R
+    if a.waves:
+        hip.pgemm_set_waves(a.waves)
     c = preset(a.preset)
     M, H, I, D = a.rows, c.hidden, c.intermediate, c.head_dim
     dev = "cuda"

@@ -318,3 +318,20 @@ def test_engine_on_fp8_prefill_and_decode(hip):
         doc = json.loads(r)
         assert [x["methodName"] for x in doc["methods"]] == inp.method_names
     assert eng.stats["decode_steps"] > 0
+
+
+@pytest.mark.parametrize("M", [1, 300, 3000])
+def test_pgemm_eight_wave_variant(hip, M):
+    """The 8-wave block (two waves per SIMD, 128 x 64 per wave: a different
+    DMA split, fragment reads and epilogue tiling) against the same fp32
+    references as the 4-wave kernel: every epilogue."""
+    prev = hip.pgemm_set_waves(8)
+    try:
+        test_pgemm_plain(hip, M, 3072, 2048)
+        test_pgemm_plain(hip, M, 2048, 8192)
+        test_pgemm_resid(hip, M)
+        test_pgemm_swiglu(hip, M)
+        for kv in ("bf16", "fp8"):
+            test_pgemm_qkv_rope_kv(hip, kv, min(M, 600))
+    finally:
+        hip.pgemm_set_waves(prev)

@@ -49,6 +49,8 @@ def main(argv=None) -> int:
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--max-new-tokens", type=int, default=4096, help="reply budget (LOCAL_LLM_MAX_NEW_TOKENS)")
     ap.add_argument("--no-fork", action="store_true", help="methods decoded in sequence, not as branches")
+    ap.add_argument("--fork-max-context", type=int, default=-1,
+                    help="fork only classes with at most this many own prompt tokens (-1: the engine default)")
     args = ap.parse_args(argv)
 
     import torch
@@ -75,7 +77,8 @@ def main(argv=None) -> int:
     eng = LocalEngine(model, use_graphs=not args.no_graphs, jump_forward=not args.no_jump,
                       shared_prefix=not args.no_shared_prefix, pipeline=not args.no_pipeline,
                       admit_min=args.admit_min or None, tokenizer=tok, max_new_tokens=args.max_new_tokens,
-                      fork_methods=not args.no_fork)
+                      fork_methods=not args.no_fork,
+                      **({} if args.fork_max_context < 0 else {"fork_max_context": args.fork_max_context}))
     para = ("The shop platform sells products to retail customers. Orders move from CART to PAID to "
             "SHIPPED; payments are captured through the payment gateway and refunds are issued by the "
             "back office. Inventory is reserved when an order is paid and released on cancellation.\n\n")

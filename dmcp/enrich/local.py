@@ -407,10 +407,11 @@ class LocalEngine:
         # latency-bound: rows per step far below capacity)
         self.fork_methods = fork_methods
         # ... unless the class's own context (prompt after the shared prefix)
-        # is longer than this: every branch starts with a copy of that KV
-        # (16 KB per token per slot at fp8 for the 1B shapes), and at ~2,400
-        # own tokens (the byte-level preset) the copies cost more than the
-        # shorter chain saves (60 vs 68 classes/s, profiles/enrich_fp8_r4_forks.jsonl)
+        # is longer than this.  Branches read the head's KV in place (no
+        # copies since the fork table), but at ~2,400 own tokens (the
+        # byte-level preset) a full batch still loses: 74.9 -> 69.8 classes/s
+        # at 1,024 classes (steps 8.4 -> 9.6 ms), while a small, latency-bound
+        # batch gains 63.3 -> 67.7 at 257 (profiles/enrich_fork_context_ab_r4.jsonl)
         self.fork_max_context = int(fork_max_context)
         self.cfg: LMConfig = model.cfg
         # reply budget: the caller's max_new_tokens, within what the KV slot

@@ -677,9 +677,11 @@ class LocalEngine:
             raise ValueError(f"reply template needs {budget} tokens > max_seq {self.cfg.max_seq}")
         return self._prompt(s, readme, budget)
 
-    def _seqs_for(self, key: Any, inp: EnrichmentInput, readme: Optional[str]) -> List[_Seq]:
+    def _seqs_for(self, key: Any, inp: EnrichmentInput, readme: Optional[str], small: bool = False) -> List[_Seq]:
         """The sequences of one class: one per reply part, sharing one prompt --
-        or, with ``fork_methods``, its head (the branches follow its KV)."""
+        or, with ``fork_methods``, its head (the branches follow its KV).
+        ``small``: the session's batch is latency-bound, fork whatever the
+        class's own context length."""
         if self.fork_methods:
             head, branches = plan_branches(inp.method_names, self.reply_budget)
             q = _Seq(inp, key, self._encode_forced(head), part=0, n_parts=1 + len(branches))
@@ -694,7 +696,7 @@ class LocalEngine:
                 if q.h >= 0:
                     self._native.release(q.h)
                 raise
-            if not branches or not self.fork_max_context or \
+            if not branches or not self.fork_max_context or small or \
                     len(q.prompt) - q.prefix_split <= self.fork_max_context:
                 q.forked = True
                 return [q]
@@ -994,10 +996,16 @@ class LocalEngine:
                 # ---- refill the look-ahead (blocking only when idle)
                 want = len(free_slots) + lookahead - len(pending)
                 if want > 0 and not feed.done:
-                    for item in feed.take(want, wait=not active and not pending and inflight is None):
+                    items = list(feed.take(want, wait=not active and not pending and inflight is None))
+                    # a small batch -- the feed drained and every class fits in
+                    # 3/4 of the slots -- is latency-bound: long-context classes
+                    # fork too (profiles/enrich_fork_context_ab_r4.jsonl)
+                    small = len(items) < want and \
+                        len(active) + len(pending) + len(items) <= cfg.max_batch * 3 // 4
+                    for item in items:
                         key, inp = item[0], item[1]
                         try:
-                            seqs = self._seqs_for(key, inp, item[2] if len(item) > 2 else readme)
+                            seqs = self._seqs_for(key, inp, item[2] if len(item) > 2 else readme, small)
                         except Exception as e:
                             yield key, json.dumps({"error": str(e)})
                             continue

@@ -378,19 +378,26 @@ def test_method_branches_shorten_the_critical_path():
 
 
 def test_fork_skipped_for_long_own_context():
-    """A class whose own prompt exceeds fork_max_context decodes its methods
-    in one sequence (each branch would start with a copy of that KV): the
-    same replies as fork_methods=False, counted in stats["fork_skipped"]."""
-    roomy = LocalLM(preset("tiny", max_batch=32, max_rows=128, max_seq=2048), device="cpu", seed=1)
+    """In a full batch, a class whose own prompt exceeds fork_max_context
+    decodes its methods in one sequence: the same replies as
+    fork_methods=False, counted in stats["fork_skipped"].  A small
+    (latency-bound) batch -- every class fits in 3/4 of the slots -- forks
+    it anyway (its branches read the head's KV in place)."""
+    tight = LocalLM(preset("tiny", max_batch=4, max_rows=128, max_seq=2048), device="cpu", seed=1)
     inputs = [EnrichmentInput("class S%d {}" % i, f"co.x.S{i}", "java", "SERVICE",
                               ["alpha", "beta", "gamma"][: 1 + i % 3]) for i in range(4)]
-    seq = LocalEngine(roomy, fork_methods=False)
-    capped = LocalEngine(roomy, fork_methods=True, fork_max_context=8)
+    seq = LocalEngine(tight, fork_methods=False)
+    capped = LocalEngine(tight, fork_methods=True, fork_max_context=8)
     assert capped.generate(inputs, "readme") == seq.generate(inputs, "readme")
     assert capped.stats["fork_skipped"] == 4 and capped.stats["forks"] == 0
-    both = LocalEngine(roomy, fork_methods=True, fork_max_context=100000)
+    both = LocalEngine(tight, fork_methods=True, fork_max_context=100000)
     out = both.generate(inputs, "readme")
     assert both.stats["fork_skipped"] == 0 and both.stats["forks"] == 4
+    assert all(json.loads(o) for o in out)
+    roomy = LocalLM(preset("tiny", max_batch=32, max_rows=128, max_seq=2048), device="cpu", seed=1)
+    small = LocalEngine(roomy, fork_methods=True, fork_max_context=8)
+    out = small.generate(inputs, "readme")
+    assert small.stats["fork_skipped"] == 0 and small.stats["forks"] == 4
     assert all(json.loads(o) for o in out)
 
 

@@ -61,6 +61,17 @@ for s in $STEPS; do
                 > "$OUT/kstats_llama_fp8.txt" 2>&1
             head -30 "$OUT/kstats_llama_fp8.txt"
             [ $rc -eq 0 ] || exit $rc ;;
+        prof_byte)
+            ( cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$ROOT/$OUT/prof_byte" -o enrich -- python3 "$ROOT/bench_enrich.py" --classes 512 --warmup 4 \
+                > "$ROOT/$OUT/prof_byte.log" 2>&1 )
+            rc=$?
+            echo "=== prof_byte rc=$rc"
+            find "$OUT/prof_byte" -type f ! -name '*kernel_stats*' -delete 2>/dev/null
+            python3 scripts/kstats.py $(find "$OUT/prof_byte" -name '*kernel_stats.csv' | head -1) \
+                > "$OUT/kstats_byte.txt" 2>&1
+            head -30 "$OUT/kstats_byte.txt"
+            [ $rc -eq 0 ] || exit $rc ;;
         prefill) run prefill 300 python scripts/bench_prefill.py --seqs 12 ;;
         pgemm_test) run pgemm_test 300 python -u -m pytest tests/test_gpu_pgemm.py -x -v --timeout 120 \
                 --timeout-method thread ;;

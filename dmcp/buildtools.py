@@ -174,6 +174,30 @@ def build_srcscan_asan(jobs: int = 0) -> str:
     return target
 
 
+def grammar_asan_module_path() -> str:
+    return os.path.join(ROOT, "build", "asan", "_grammar" + ext_suffix())
+
+
+def build_grammar_asan() -> str:
+    """The native grammar engine with AddressSanitizer + UBSan (host code):
+    loaded instead of ``dmcp/enrich/_grammar`` when ``DMCP_GRAMMAR_SO`` names
+    it (scripts/asan_tests.sh, tests/test_grammar_fuzz.py)."""
+    target = grammar_asan_module_path()
+    key = _digest([GRAMMAR_SRC], " ".join(SAN_FLAGS) + sys.version)
+    stamp = target + ".stamp"
+    if os.path.exists(target) and os.path.exists(stamp) and open(stamp).read().strip() == key:
+        return target
+    import pybind11  # noqa: WPS433 (build-time only)
+    os.makedirs(os.path.dirname(target), exist_ok=True)
+    tmp = target + ".tmp"
+    _run([CXX, *SAN_FLAGS, "-shared", "-fvisibility=hidden", f"-I{pybind11.get_include()}",
+          f"-I{sysconfig.get_paths()['include']}", "-o", tmp, GRAMMAR_SRC])
+    os.replace(tmp, target)
+    with open(stamp, "w") as f:
+        f.write(key)
+    return target
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
@@ -185,6 +209,7 @@ def main(argv=None) -> int:
     print(build_grammar(force=a.force))
     if a.sanitize:
         print(build_srcscan_asan(jobs=a.jobs))
+        print(build_grammar_asan())
     if not a.no_hip:
         try:
             from dmcp.ops import build as hipbuild

@@ -63,6 +63,14 @@ class Config:
     # KV (a class's latency: head + longest method, not all methods in a row)
     local_llm_fork_methods: bool = True
     local_llm_fork_max_context: int = 1536
+    # byte caps of the reply's free strings (class description, method
+    # description, business-logic step) and the step count; 0 = derived from
+    # the reply budget (dmcp/enrich/local.py ReplyShape.from_budget: 256 / 128
+    # / 64 bytes and 4 steps at 4,096 tokens)
+    local_llm_desc_max_bytes: int = 0
+    local_llm_method_max_bytes: int = 0
+    local_llm_step_max_bytes: int = 0
+    local_llm_max_steps: int = 0
     local_llm_devices: str = "all"
     # "process": one worker process per GPU, started before this process
     # touches HIP (the service default); "inline": engines in this process
@@ -135,6 +143,10 @@ class Config:
             "LOCAL_LLM_MAX_NEW_TOKENS": "local_llm_max_new_tokens",
             "LOCAL_LLM_FORK_METHODS": "local_llm_fork_methods",
             "LOCAL_LLM_FORK_MAX_CONTEXT": "local_llm_fork_max_context",
+            "LOCAL_LLM_DESC_MAX_BYTES": "local_llm_desc_max_bytes",
+            "LOCAL_LLM_METHOD_MAX_BYTES": "local_llm_method_max_bytes",
+            "LOCAL_LLM_STEP_MAX_BYTES": "local_llm_step_max_bytes",
+            "LOCAL_LLM_MAX_STEPS": "local_llm_max_steps",
             "LOCAL_LLM_DEVICES": "local_llm_devices",
             "LOCAL_LLM_WORKERS": "local_llm_workers",
             "LOCAL_LLM_MAX_BATCH": "local_llm_max_batch",

@@ -78,6 +78,7 @@ class MultiFeed:
         self._q: "dict[int, Deque[Tuple[Any, EnrichmentInput]]]" = {}
         self._readme: "dict[int, Any]" = {}
         self._order: Deque[int] = deque()
+        self._ended: set = set()   # sessions whose ``end`` arrived: dropped once drained
         self._shutdown = False
 
     def begin(self, sid: int, readme) -> None:
@@ -98,12 +99,17 @@ class MultiFeed:
         """No more items of ``sid`` (queued ones are still taken)."""
         with self._cv:
             q = self._q.get(sid)
-            if q is not None and not q:
+            if q is None:
+                return
+            if q:
+                self._ended.add(sid)  # its queued items are still taken; dropped when drained
+            else:
                 self._drop(sid)
 
     def _drop(self, sid: int) -> None:
         self._q.pop(sid, None)
         self._readme.pop(sid, None)
+        self._ended.discard(sid)
         try:
             self._order.remove(sid)
         except ValueError:
@@ -133,8 +139,15 @@ class MultiFeed:
                         key, inp = q.popleft()
                         out.append(((sid, key), inp, self._readme[sid]))
                         progressed = True
+                        if not q and sid in self._ended:
+                            self._drop(sid)
                         if len(out) >= n:
                             break
                 if not progressed:
                     break
             return out
+
+    def sessions(self) -> int:
+        """Sessions still held (begun and not yet ended-and-drained)."""
+        with self._cv:
+            return len(self._q)

@@ -129,14 +129,65 @@ def _steps_chain(step_len: Tuple[int, int], max_steps: int, depth: int = 1) -> L
     return segs
 
 
+@dataclass(frozen=True)
+class ReplyShape:
+    """Byte caps of the reply's free strings and the business-logic step
+    count: the class description, each method's description, each step.
+    The reference asks for a free business-oriented description, a
+    1-sentence description per method and a list of steps under a
+    16,384-token ``max_tokens`` (``ClaudeApiClient.java:40, 101-113``);
+    :meth:`from_budget` derives the caps from the engine's reply budget
+    (config ``LOCAL_LLM_DESC_MAX_BYTES`` / ``LOCAL_LLM_METHOD_MAX_BYTES`` /
+    ``LOCAL_LLM_STEP_MAX_BYTES`` / ``LOCAL_LLM_MAX_STEPS`` override each;
+    0 = derived).  :func:`plan_reply` / :func:`plan_branches` still shrink
+    them for a class whose methods would not fit the budget."""
+    desc: int = 96
+    method: int = 64
+    step: int = 40
+    max_steps: int = 3
+
+    LEGACY = None  # set below: the round-4 fixed caps (96 / 64 / 40 bytes, 3 steps)
+
+    @classmethod
+    def from_budget(cls, budget: int, desc: int = 0, method: int = 0, step: int = 0,
+                    max_steps: int = 0) -> "ReplyShape":
+        """Defaults scale with the reply budget (tokens): 1/16 of it for the
+        class description (96-512 bytes), 1/32 per method description
+        (64-256), 1/64 per step (40-160), budget / 1024 steps (3-6); at the
+        service's 4,096-token budget 256 / 128 / 64 bytes and 4 steps."""
+        b = max(0, int(budget))
+        return cls(desc=int(desc) or min(512, max(96, b // 16)),
+                   method=int(method) or min(256, max(64, b // 32)),
+                   step=int(step) or min(160, max(40, b // 64)),
+                   max_steps=int(max_steps) or min(6, max(3, b // 1024)))
+
+    def scaled(self, scale: float) -> Tuple[Tuple[int, int], Tuple[int, int], Tuple[int, int]]:
+        """(min, max) length pairs of the three strings at ``scale``."""
+        def L(lo, hi):
+            hi = max(4, int(hi * scale))
+            return (min(lo, max(2, hi)), hi)
+        return L(8, self.desc), L(6, self.method), L(4, self.step)
+
+
+ReplyShape.LEGACY = ReplyShape(96, 64, 40, 3)
+
+
+def _type_choice_segs(type_choice: bool) -> List[Segment]:
+    """The classTypeCorrection value: the model's choice (null or one of the
+    10 types), or a forced ``null`` -- an engine over random-initialised
+    weights must not overwrite the statically inferred class types."""
+    if type_choice:
+        return [Segment(choice=CHOICE_CLASS_TYPE, then=[[]] * len(CHOICES[CHOICE_CLASS_TYPE]))]
+    return [Segment(b"null")]
+
+
 def build_template(names: Sequence[str], desc_len=(8, 96), method_len=(6, 64), step_len=(4, 40),
-                   max_steps: int = 3, head: bool = True) -> List[Segment]:
+                   max_steps: int = 3, head: bool = True, type_choice: bool = True) -> List[Segment]:
     """Segments of one reply covering ``names``.  ``head`` = False: a
     continuation part (the description / correction come from part 0)."""
     if head:
-        segs = [Segment(b'{"description": "'), Segment(None, *desc_len), Segment(b', "classTypeCorrection": '),
-                Segment(choice=CHOICE_CLASS_TYPE, then=[[]] * len(CHOICES[CHOICE_CLASS_TYPE])),
-                Segment(b', "methods": [')]
+        segs = [Segment(b'{"description": "'), Segment(None, *desc_len), Segment(b', "classTypeCorrection": ')]
+        segs += _type_choice_segs(type_choice) + [Segment(b', "methods": [')]
     else:
         segs = [Segment(b'{"description": "", "classTypeCorrection": null, "methods": [')]
     for i, name in enumerate(names):
@@ -163,17 +214,17 @@ def template_budget(segs: Sequence[Segment]) -> int:
     return n
 
 
-def plan_reply(names: Sequence[str], budget: int) -> Tuple[List[List[Segment]], int]:
+def plan_reply(names: Sequence[str], budget: int, shape: Optional[ReplyShape] = None,
+               type_choice: bool = True) -> Tuple[List[List[Segment]], int]:
     """The reply parts of a class within ``budget`` tokens each, and the
     number of methods that fit in none.  One part when the whole reply fits
     (string lengths and step counts shrink first, down to half); otherwise
     the methods are split over continuation parts -- generated side by side
     from the same prompt and merged -- so no method is silently dropped."""
+    shape = shape or ReplyShape.LEGACY
     names = list(dict.fromkeys(names))
-    for scale, steps in ((1.0, 3), (0.75, 2), (0.5, 2)):
-        def L(lo, hi):
-            return (min(lo, max(2, int(hi * scale))), max(4, int(hi * scale)))
-        segs = build_template(names, L(8, 96), L(6, 64), L(4, 40), steps)
+    for scale, steps in ((1.0, shape.max_steps), (0.75, min(2, shape.max_steps)), (0.5, min(2, shape.max_steps))):
+        segs = build_template(names, *shape.scaled(scale), steps, type_choice=type_choice)
         if template_budget(segs) <= budget:
             return [segs], 0
     lens = ((6, 48), (4, 32), (3, 20), 2)
@@ -183,7 +234,7 @@ def plan_reply(names: Sequence[str], budget: int) -> Tuple[List[List[Segment]], 
     cur: List[str] = []
 
     def build(ns, head, ls=lens):
-        return build_template(ns, ls[0], ls[1], ls[2], ls[3], head=head)
+        return build_template(ns, ls[0], ls[1], ls[2], ls[3], head=head, type_choice=type_choice)
     for name in names:
         if template_budget(build(cur + [name], not parts)) <= budget:
             cur.append(name)
@@ -205,13 +256,13 @@ def plan_reply(names: Sequence[str], budget: int) -> Tuple[List[List[Segment]], 
     return parts, dropped
 
 
-def build_head(has_methods: bool, desc_len=(8, 96)) -> List[Segment]:
+def build_head(has_methods: bool, desc_len=(8, 96), type_choice: bool = True) -> List[Segment]:
     """The class-level part of a reply generated with method branches: the
     description and the class-type choice, up to the opening of the methods
     list (or the whole reply when there is no method)."""
-    return _merge([Segment(b'{"description": "'), Segment(None, *desc_len), Segment(b', "classTypeCorrection": '),
-                   Segment(choice=CHOICE_CLASS_TYPE, then=[[]] * len(CHOICES[CHOICE_CLASS_TYPE])),
-                   Segment(b', "methods": [' if has_methods else b', "methods": []}')])
+    return _merge([Segment(b'{"description": "'), Segment(None, *desc_len), Segment(b', "classTypeCorrection": ')]
+                  + _type_choice_segs(type_choice)
+                  + [Segment(b', "methods": [' if has_methods else b', "methods": []}')])
 
 
 def build_branch(name: str, method_len=(6, 64), step_len=(4, 40), max_steps: int = 3) -> List[Segment]:
@@ -223,21 +274,60 @@ def build_branch(name: str, method_len=(6, 64), step_len=(4, 40), max_steps: int
     return [Segment(b"")] + _merge(body)
 
 
-def plan_branches(names: Sequence[str], budget: int) -> Tuple[List[Segment], List[List[Segment]]]:
+def plan_branches(names: Sequence[str], budget: int, shape: Optional[ReplyShape] = None,
+                  type_choice: bool = True) -> Tuple[List[Segment], List[List[Segment]]]:
     """(head, one branch per method) with string lengths and step counts
     shrunk until head + all branches fit ``budget`` tokens (down to a floor:
     no method is ever dropped -- past the floor the budget is exceeded)."""
+    shape = shape or ReplyShape.LEGACY
     names = list(dict.fromkeys(names))
     plan = None
-    for scale, steps in ((1.0, 3), (0.75, 2), (0.5, 2), (0.35, 1), (0.25, 1)):
-        def L(lo, hi):
-            return (min(lo, max(2, int(hi * scale))), max(4, int(hi * scale)))
-        head = build_head(bool(names), L(8, 96))
-        branches = [build_branch(n, L(6, 64), L(4, 40), steps) for n in names]
+    ms = shape.max_steps
+    for scale, steps in ((1.0, ms), (0.75, min(2, ms)), (0.5, min(2, ms)), (0.35, 1), (0.25, 1)):
+        dl, ml, sl = shape.scaled(scale)
+        head = build_head(bool(names), dl, type_choice=type_choice)
+        branches = [build_branch(n, ml, sl, steps) for n in names]
         plan = (head, branches)
         if template_budget(head) + sum(template_budget(b) for b in branches) <= budget:
             break
     return plan
+
+
+def _grammar_module():
+    """``dmcp.enrich._grammar`` -- or the build ``DMCP_GRAMMAR_SO`` names
+    (the ASan/UBSan one of scripts/asan_tests.sh)."""
+    import os
+    path = os.environ.get("DMCP_GRAMMAR_SO")
+    if not path:
+        from . import _grammar
+        return _grammar
+    import importlib.util
+    import sys
+    mod = sys.modules.get("dmcp.enrich._grammar")
+    if mod is not None and getattr(mod, "__file__", None) == path:
+        return mod
+    spec = importlib.util.spec_from_file_location("dmcp.enrich._grammar", path)
+    if spec is None:
+        raise ImportError(f"DMCP_GRAMMAR_SO={path}: not a loadable module")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    sys.modules["dmcp.enrich._grammar"] = mod
+    return mod
+
+
+def _trim_to_word(out: bytearray, start: int) -> None:
+    """A free string that reached its byte cap ends at its last word
+    boundary, not mid-word: ``out[start:]`` (the string so far) is cut at
+    its last space when that keeps at least half of it (trailing spaces
+    dropped).  Only the reply text is cut; the KV cache keeps what was
+    generated.  The native engine does the same (engine.cpp trim_to_word)."""
+    body = out[start:]
+    cut = body.rfind(b" ")
+    if cut < max(1, len(body) // 2):
+        return
+    while cut > 0 and body[cut - 1] == 0x20:
+        cut -= 1
+    del out[start + cut:]
 
 
 def merge_branches(head: str, branches: Sequence[str]) -> str:
@@ -271,6 +361,7 @@ class _Seq:
     seg: int = 0
     free_len: int = 0                  # tokens of the current free string
     free_bytes: int = 0                # ... and its bytes
+    free_start: int = 0                # offset in ``out`` where the current free string starts
     forced_off: int = 0
     choice_pref: bytes = b""           # bytes chosen so far in the current choice segment
     next_token: int = -1               # token to feed at the next decode step
@@ -384,7 +475,8 @@ class LocalEngine:
                  jump_forward: bool = True, shared_prefix: bool = True, pipeline: bool = True,
                  admit_min: Optional[int] = None, longest_first: bool = True, tokenizer=None,
                  max_new_tokens: Optional[int] = None, native_grammar: Optional[bool] = None,
-                 fork_methods: bool = True, fork_max_context: int = 1536) -> None:
+                 fork_methods: bool = True, fork_max_context: int = 1536,
+                 reply_shape: Optional[ReplyShape] = None, type_choice: Optional[bool] = None) -> None:
         self.model = model
         self.tok = tokenizer if tokenizer is not None else ByteTokenizer(model.cfg.vocab_size)
         self._tb = self.tok.token_bytes
@@ -418,6 +510,15 @@ class LocalEngine:
         # leaves next to a useful prompt
         kv_cap = self.cfg.max_seq - max(64, self.cfg.max_seq // 4)
         self.reply_budget = min(kv_cap, int(max_new_tokens)) if max_new_tokens else kv_cap
+        # string caps / step count of the replies (derived from the budget
+        # unless given); a string at its cap closes at its last word boundary
+        if isinstance(reply_shape, dict):  # config overrides (0 = derived), e.g. from a worker frame
+            reply_shape = ReplyShape.from_budget(self.reply_budget, **reply_shape)
+        self.reply_shape = reply_shape or ReplyShape.from_budget(self.reply_budget)
+        # classTypeCorrection is the model's choice only for a loaded
+        # checkpoint: random-initialised weights would overwrite the class
+        # types found by static analysis with arbitrary ones (forced null)
+        self.type_choice = bool(getattr(model, "checkpoint", None)) if type_choice is None else bool(type_choice)
         dev = model.device
         self._choice_rows: Dict[Tuple[int, bytes], int] = {}
         masks = list(self.tok.json_masks(self.cfg.vocab_size)) + self._choice_masks()
@@ -476,7 +577,7 @@ class LocalEngine:
     # ------------------------------------------------------------ grammar
     def _make_native(self):
         try:
-            from . import _grammar
+            _grammar = _grammar_module()
         except ImportError:
             return None
         rest = {}
@@ -551,6 +652,7 @@ class LocalEngine:
                 s.choice_pref = b""
                 return self._choice_rows[(seg.choice, b"")]
             s.free_len = s.free_bytes = 0
+            s.free_start = len(s.out)
             return self.MASK_QUOTE if seg.min_len == 0 else self.MASK_NO_QUOTE
         s.done = True
         return None
@@ -601,6 +703,7 @@ class LocalEngine:
         s.free_len += 1
         s.free_bytes += len(self._tb[tok])
         if s.free_bytes >= seg.max_len:
+            _trim_to_word(s.out, s.free_start)
             s.next_token = self._quote
             return None
         return self.MASK_QUOTE if s.free_len >= seg.min_len else self.MASK_NO_QUOTE
@@ -683,7 +786,7 @@ class LocalEngine:
         ``small``: the session's batch is latency-bound, fork whatever the
         class's own context length."""
         if self.fork_methods:
-            head, branches = plan_branches(inp.method_names, self.reply_budget)
+            head, branches = plan_branches(inp.method_names, self.reply_budget, self.reply_shape, self.type_choice)
             q = _Seq(inp, key, self._encode_forced(head), part=0, n_parts=1 + len(branches))
             q.branches = [self._encode_forced(b) for b in branches] if branches else None
             self.stats["reply_parts"] += 1
@@ -704,7 +807,7 @@ class LocalEngine:
                 self._native.release(q.h)
             self.stats["reply_parts"] -= 1
             self.stats["fork_skipped"] += 1
-        parts, dropped = plan_reply(inp.method_names, self.reply_budget)
+        parts, dropped = plan_reply(inp.method_names, self.reply_budget, self.reply_shape, self.type_choice)
         self.stats["methods_dropped"] += dropped
         self.stats["reply_parts"] += len(parts)
         if len(parts) > 1:

@@ -564,8 +564,8 @@ class Indexer:
         # lazy, but sized: a multi-GPU backend deals ceil(pending / GPUs) per GPU
         inputs = SizedIter(gen(), len(pending))
         for n, (_, result) in enumerate(self.backend.enrich_stream(inputs, readme), 1):
-            if lease is not None and n % 32 == 1:
-                lease.check()  # enrichment writes go to rows another owner may be replacing
+            if lease is not None:
+                lease.check()  # every write: once the lease ran out the rows may be another owner's
             if not result.success:
                 LOG.warning("%s: enrichment failed for %s: %s", phase, result.full_class_name, result.error_message)
                 failed += 1

@@ -232,6 +232,9 @@ class LocalLM:
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = torch.bfloat16
+        # the checkpoint directory the weights came from (load_safetensors);
+        # None = random-initialised weights of a preset
+        self.checkpoint: Optional[str] = None
         self.w = weights if weights is not None else self._init_weights(seed)
         self._fold_norms()
         c = cfg
@@ -390,6 +393,11 @@ class LocalLM:
                        intermediate=hf["intermediate_size"], rope_theta=hf.get("rope_theta", 10000.0),
                        eps=hf.get("rms_norm_eps", 1e-5))
         cfg = replace(cfg, **cfg_overrides)
+        if cfg.prefill_dtype == "auto":
+            # a real checkpoint keeps bf16 prefill GEMMs unless fp8 is asked
+            # for by name: MXFP8 parity with bf16 is pinned on random-init
+            # weights only (docs/PARITY.md)
+            cfg = replace(cfg, prefill_dtype="bf16")
         raw: Dict[str, torch.Tensor] = {}
         for fn in sorted(os.listdir(path)):
             if fn.endswith(".safetensors"):
@@ -410,7 +418,9 @@ class LocalLM:
             w[f"l{i}.wo"] = g(p + "self_attn.o_proj.weight")
             w[f"l{i}.wgu"] = torch.cat([g(p + "mlp.gate_proj.weight"), g(p + "mlp.up_proj.weight")], 0).contiguous()
             w[f"l{i}.wdown"] = g(p + "mlp.down_proj.weight")
-        return cls(cfg, device, weights=w)
+        m = cls(cfg, device, weights=w)
+        m.checkpoint = path
+        return m
 
     # ------------------------------------------------------------ forward
     def _mlp(self, i: int, h: torch.Tensor) -> torch.Tensor:

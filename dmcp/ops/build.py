@@ -15,7 +15,8 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 SRCS = [os.path.join(CSRC, "dmcp_kernels.hip"), os.path.join(CSRC, "fused_gemm.hip"),
-        os.path.join(CSRC, "prefill_attn.hip"), os.path.join(CSRC, "wgemm.hip"), os.path.join(CSRC, "pgemm.hip")]
+        os.path.join(CSRC, "prefill_attn.hip"), os.path.join(CSRC, "wgemm.hip"), os.path.join(CSRC, "pgemm.hip"),
+        os.path.join(CSRC, "tgemm.hip")]
 HEADERS = [os.path.join(CSRC, "dmcp_common.hpp")]
 SRC = SRCS[0]  # kept for callers that name the main source
 TARGET = os.path.join(HERE, "_hipops.so")
@@ -25,9 +26,10 @@ FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno-
          "-munsafe-fp-atomics"]
 # MFMA accumulators in VGPRs: the prefix-attention softmax works on the score
 # tile in place (AGPR form cost ~90 v_accvgpr moves per 32-key tile).  Not for
-# pgemm.hip: its 256 accumulator registers per lane must live in the AGPR half.
+# pgemm.hip / tgemm.hip: their 256 accumulator registers per lane must live in
+# the AGPR half.
 VGPR_FORM = ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
-PER_FILE = {"pgemm.hip": []}
+PER_FILE = {"pgemm.hip": [], "tgemm.hip": []}
 
 
 def _flags(src: str) -> list:

@@ -1,0 +1,397 @@
+// Large-tile decode GEMM for steps of 257-1024 rows (gfx950 / MI355X, CDNA4):
+//
+//   Y[M, N] = X[M, K] . W[N, K]^T      bf16 in, fp32 accumulate
+//
+// The decode step's row count passes 512 whenever the engine's jump-forward
+// rows fill its spare capacity (max_rows = 768 at 512 KV slots).  There the
+// projections are compute-bound (a 640-row step is ~1.2 TFLOP over ~2 GB of
+// weights) and wgemm.hip's 64-128-row weight tiles re-stage the activation
+// rows once per tile: its staged bytes grow with M x N / NB.  This kernel
+// keeps wgemm's building blocks (LDS-DMA ring with a counted vmcnt + raw
+// barrier per stage, C^T = W . X^T tiles on v_mfma_f32_16x16x32_bf16, the M
+// parts of one weight tile on one XCD, fused epilogues) with a 4x larger
+// weight tile:
+//
+//   * a block owns 256 weight rows (SwiGLU: 128 gate + the 128 up rows of the
+//     same intermediate columns) x 64 MT activation rows (MT = 1..4), i.e. up
+//     to 256 x 256 outputs, over 8 waves (two per SIMD): 2 weight halves x 4
+//     M quarters, each 128 weight rows x 16 MT rows (8 A x MT B fragments,
+//     32 MT accumulators);
+//   * waves 4-7 (one per SIMD) also issue the block's LDS-DMA: an LDS-DMA
+//     instruction holds its wave's issue for ~60-185 cycles
+//     (MI355X_MICROARCH.md, cycle constants), and with one wave per SIMD doing
+//     both, the 8 pieces per stage ran in series with its MFMAs (v1 of this
+//     kernel: 45 % of MFMA time at 1,024 rows); now the SIMD partner keeps
+//     issuing MFMAs meanwhile;
+//   * 32-deep K stages ([rows][4 x 16 B] images, 16-row 1-KiB LDS-DMA
+//     pieces) in a 4-stage ring, 3 stages (up to 96 KiB) in flight per CU;
+//   * chunk j of row r sits in slot j ^ ((4 - (r >> 2)) & 3): the 16 lanes of
+//     each ds_read_b128 group of the 16x16x32 operand layout (lane (l16, g):
+//     row l16, chunk g) cover all 64 banks;
+//   * split-K slices of whole stages (any count: the last slice may be
+//     shorter) for the narrow projections; the fp32 partials are reduced by
+//     wgemm.hip's fused consumers (RoPE + KV append, residual + RMSNorm);
+//   * MODE_ARGMAX: the LM head + grammar-masked greedy selection (per block
+//     and row one (max, id) pair per 128 vocabulary ids, a per-row
+//     reduction kernel selects), no [M, V] logits.
+#include "dmcp_common.hpp"
+
+namespace {
+
+constexpr int TKC = 32;   // K per LDS stage
+constexpr int TST = 4;    // ring stages (3 in flight while one is computed)
+constexpr int TNB = 256;  // weight rows per block
+constexpr int TTH = 512;  // threads per block: 8 waves, two per SIMD
+constexpr int TM_BF16 = 0, TM_PART = 1, TM_SWIGLU = 2, TM_ARGMAX = 3;
+
+__device__ __forceinline__ float tsilu(float g) { return g / (1.f + __expf(-g)); }
+
+__device__ __forceinline__ void tglds16(const void* src, uint4* lds_base) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+// slot of logical 16-B chunk j of image row r (4 chunks per 64-B row)
+__device__ __forceinline__ int tslot(int j, int r) { return j ^ ((4 - (r >> 2)) & 3); }
+
+// PROBE (dmcp_tgemm_probe only; diagnostics of scripts/bench_tgemm.py --probe):
+// 1 = the K loop issues no refill DMAs (MFMA + LDS reads + barriers on stale
+// stages), 2 = no fragment reads / MFMAs (the DMA ring alone)
+template <int MT, int MODE, int PROBE = 0>
+__global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) void tgemm_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, float* __restrict__ part,
+    int M, int N, int K, int cps, int S, int ntiles, int mparts, int mrows, int I, const uint32_t* __restrict__ masks,
+    const int32_t* __restrict__ midx, int n_masks, int wwords) {
+    constexpr int NF = TNB / 32;       // A fragments per wave (16 weight rows each): half the tile's rows
+    constexpr int MR = 64 * MT;        // staged X rows
+    constexpr int WI = TNB / 64;       // 1-KiB pieces (16 rows x 64 B) per loader wave per stage: weights
+    constexpr int XI = MT;             //                                                          X rows
+    constexpr int GL = WI + XI;        // LDS-DMA instructions per loader wave per stage
+    constexpr int WCH = TNB * 4;       // 16-B chunks of a stage's weight image
+    constexpr int SCH = WCH + MR * 4;  // ... plus the X image
+    __shared__ uint4 lds[TST * SCH];   // ONE shared array (cdna_hip_programming.md §5 item 4a)
+
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(tid / kWave);
+    // waves 0-3 and 4-7 each cover the 4 SIMDs once: waves 4-7 also issue the
+    // block's LDS-DMA (one loader per SIMD), so while a loader waits on its
+    // DMA issue its SIMD partner keeps the matrix core busy
+    const bool loader = wv >= 4;
+    const int lw = wv & 3;                 // loader index
+    const int wn = wv & 1, wm = wv >> 1;   // weight half (128 rows) x M quarter (16 MT rows)
+    const int l16 = lane & 15, g = lane >> 4;
+    // block -> (weight tile nt, K slice s, M part mp): the M parts of one
+    // (nt, s) unit share blockIdx % 8 (one XCD) and consecutive dispatch slots
+    const int units = ntiles * S;
+    int u, mp;
+    if ((units & 7) == 0) {
+        const int j = blockIdx.x >> 3;
+        u = (j / mparts) * 8 + (blockIdx.x & 7);
+        mp = j % mparts;
+    } else {
+        u = blockIdx.x / mparts;
+        mp = blockIdx.x % mparts;
+    }
+    const int nt = u % ntiles, s = u / ntiles;
+    const int chunks_all = K / TKC;
+    const int cbeg = s * cps;
+    const int chunks = min(chunks_all, cbeg + cps) - cbeg;  // > 0 (host contract)
+    const int m_lo = mp * mrows;
+    const int m_hi = min(M, m_lo + mrows);
+    const int mw = wm * (MT * 16);
+    int mtv = (m_hi - m_lo - mw + 15) / 16;  // valid 16-row tiles of this wave (wave-uniform)
+    mtv = max(0, min(MT, mtv));
+
+    const int n0 = nt * TNB;
+    const int n0h = nt * (TNB / 2);
+    // weight row of image row r.  SwiGLU: each 128-row half holds 64 gate rows
+    // then the 64 up rows of the same intermediate columns, so a wave's gate
+    // fragment f and up fragment f + NF / 2 meet in one lane
+    auto wrow = [&](int r) -> int {
+        if constexpr (MODE == TM_SWIGLU) {
+            const int h = r >> 7, i = r & 127;
+            return (i < 64 ? 0 : I) + n0h + 64 * h + (i & 63);
+        } else {
+            return n0 + r;
+        }
+    };
+    // LDS-DMA sources: lane L of a piece fills image row base + L / 4, slot
+    // L % 4 with logical chunk tslot(L % 4, row) (the swizzle is an involution)
+    const uint16_t* wsrc[WI];
+    const uint16_t* xsrc[XI];
+#pragma unroll
+    for (int i = 0; i < WI; ++i) {
+        const int r = (lw * WI + i) * 16 + (lane >> 2);
+        wsrc[i] = w + (size_t)wrow(r) * K + (size_t)cbeg * TKC + tslot(lane & 3, r) * 8;
+    }
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+        const int r = (lw * XI + i) * 16 + (lane >> 2);
+        xsrc[i] = x + (size_t)min(m_lo + r, M - 1) * K + (size_t)cbeg * TKC + tslot(lane & 3, r) * 8;
+    }
+    auto issue = [&](int c, int slot) {
+        uint4* base = lds + slot * SCH;
+#pragma unroll
+        for (int i = 0; i < WI; ++i) tglds16(wsrc[i] + c * TKC, base + (lw * WI + i) * 64);
+#pragma unroll
+        for (int i = 0; i < XI; ++i) tglds16(xsrc[i] + c * TKC, base + WCH + (lw * XI + i) * 64);
+    };
+
+    f32x4_t acc[NF][MT];
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+#pragma unroll
+        for (int t = 0; t < MT; ++t) acc[f][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    // One 32-deep k step per stage: MT X fragments and NF weight fragments
+    // (this wave's 128 weight rows), NF x MT MFMAs.  The fragments of stage
+    // c + 1 are read into the second register set while stage c's MFMAs run
+    // (one barrier per stage, after the loaders' wait for stage c + 1): the
+    // LDS read latency and the LDS array time of a stage's reads (~320 cycles
+    // for 8 waves) no longer stand between a barrier and the first MFMA.
+    struct Frags {
+        bf16x8_t a[NF], b[MT];
+    };
+    auto read = [&](const uint4* st, Frags& F) {
+        const uint4* wl = st;
+        const uint4* xl = st + WCH;
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            const int r = mw + 16 * t + l16;
+            F.b[t] = as_bf16x8(xl[r * 4 + tslot(g, r)]);
+        }
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+            const int r = 128 * wn + 16 * f + l16;
+            F.a[f] = as_bf16x8(wl[r * 4 + tslot(g, r)]);
+        }
+    };
+    auto mma = [&](const Frags& F) {
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+                acc[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F.a[f], F.b[t], acc[f][t], 0, 0, 0);
+    };
+
+    // TST-stage ring.  Step c: a loader waits for its pieces of stage c + 1
+    // (counted vmcnt: stage c + 2 stays in flight), one raw barrier (stage
+    // c + 1 landed for every wave; every wave's MFMAs of stage c - 1 -- the
+    // last use of the slot about to be refilled -- issued, their reads done),
+    // the loaders refill that slot with stage c + 3, every wave reads stage
+    // c + 1 and runs stage c's MFMAs.  No __syncthreads() in the loop.
+    if (loader) {
+#pragma unroll
+        for (int j = 0; j < TST - 1; ++j)
+            if (j < chunks) issue(j, j);
+        if ((PROBE & 1) != 0 || chunks == 1)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (chunks == 2)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(GL) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * GL) : "memory");
+    }
+    asm volatile("s_barrier" ::: "memory");
+    auto step = [&](int c, const Frags& Fc, Frags& Fn) {
+        if (loader) {
+            if ((PROBE & 1) != 0 || c + 2 >= chunks)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(%0)" ::"i"(GL) : "memory");
+        }
+        asm volatile("s_barrier" ::: "memory");
+        if (loader && c + TST - 1 < chunks && (PROBE & 1) == 0) issue(c + TST - 1, (c + TST - 1) % TST);
+        if constexpr ((PROBE & 2) == 0) {
+            if (c + 1 < chunks) read(lds + ((c + 1) % TST) * SCH, Fn);
+            mma(Fc);
+        }
+    };
+    Frags F0, F1;
+    if constexpr ((PROBE & 2) == 0) read(lds, F0);
+    int c = 0;
+    // two steps per trip: the register sets swap roles by name, never by a
+    // runtime index (cdna_hip_programming.md §5.4 rule 20)
+    for (; c + 1 < chunks; c += 2) {
+        step(c, F0, F1);
+        step(c + 1, F1, F0);
+    }
+    if (c < chunks) step(c, F0, F1);
+
+    // epilogue: lane (l16, g) holds Y[row m_lo + mw + 16t + l16][col c0 + 16f + 4g + i]
+    // with c0 = 128 wn (SwiGLU: intermediate column n0h + 64 wn + 16f + 4g + i of f < NF / 2)
+    const int c0 = n0 + 128 * wn;
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+        if (t >= mtv) continue;
+        const int m = m_lo + mw + 16 * t + l16;
+        if constexpr (MODE == TM_ARGMAX) {
+            float bv = -INFINITY;
+            int bi = 0x7fffffff;
+            if (m < m_hi) {
+                int mr = midx ? midx[m] : 0;
+                mr = mr < 0 ? 0 : (mr >= n_masks ? n_masks - 1 : mr);
+                const uint32_t* mrow = masks + (size_t)mr * wwords + (c0 >> 5);
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    const uint32_t word = mrow[(16 * f + 4 * g) >> 5];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int c = 16 * f + 4 * g + i;
+                        if ((word >> (c & 31)) & 1u) {
+                            const float v = bf2f(f2bf(acc[f][t][i]));
+                            if (v > bv) { bv = v; bi = c0 + c; }  // columns ascend: strict > keeps the lowest
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int msk = 16; msk < kWave; msk <<= 1) {
+                const float ob = __shfl_xor(bv, msk, kWave);
+                const int oi = __shfl_xor(bi, msk, kWave);
+                if (ob > bv || (ob == bv && oi < bi)) { bv = ob; bi = oi; }
+            }
+            // one (max, id) pair per 128-id half tile and row
+            if (m < m_hi && g == 0)
+                reinterpret_cast<float2*>(part)[(size_t)(2 * nt + wn) * M + m] = make_float2(bv, __int_as_float(bi));
+            continue;
+        }
+        if (m >= m_hi) continue;
+        if constexpr (MODE == TM_SWIGLU) {
+#pragma unroll
+            for (int f = 0; f < NF / 2; ++f) {
+                float o[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {  // gate / up rounded to bf16 as the unfused GEMM output is
+                    const float gg = bf2f(f2bf(acc[f][t][i])), uu = bf2f(f2bf(acc[f + NF / 2][t][i]));
+                    o[i] = tsilu(gg) * uu;
+                }
+                *reinterpret_cast<uint2*>(y + (size_t)m * I + n0h + 64 * wn + 16 * f + 4 * g) = pack4(o);
+            }
+        } else if constexpr (MODE == TM_PART) {
+            float* dst = part + ((size_t)s * M + m) * N + c0 + 4 * g;
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+                *reinterpret_cast<float4*>(dst + 16 * f) =
+                    make_float4(acc[f][t][0], acc[f][t][1], acc[f][t][2], acc[f][t][3]);
+        } else {
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const float o[4] = {acc[f][t][0], acc[f][t][1], acc[f][t][2], acc[f][t][3]};
+                *reinterpret_cast<uint2*>(y + (size_t)m * N + c0 + 16 * f + 4 * g) = pack4(o);
+            }
+        }
+    }
+}
+
+// per row: the (max, id) pairs of every 128-id vocabulary half tile -> the selected
+// id (0 when the mask allows nothing, as masked_argmax); one wave per row
+__global__ __launch_bounds__(kBlock) void tgemm_argmax_reduce_kernel(const float2* __restrict__ best, int ntiles,
+                                                                     int M, int32_t* __restrict__ ids) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int m = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
+    if (m >= M) return;
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int t = lane; t < ntiles; t += kWave) {
+        const float2 p = best[(size_t)t * M + m];
+        const int pi = __float_as_int(p.y);
+        if (p.x > bv || (p.x == bv && pi < bi)) { bv = p.x; bi = pi; }
+    }
+#pragma unroll
+    for (int msk = 32; msk >= 1; msk >>= 1) {
+        const float ob = __shfl_xor(bv, msk, kWave);
+        const int oi = __shfl_xor(bi, msk, kWave);
+        if (ob > bv || (ob == bv && oi < bi)) { bv = ob; bi = oi; }
+    }
+    if (lane == 0) ids[m] = bi == 0x7fffffff ? 0 : bi;
+}
+
+template <int MODE, int PROBE = 0>
+hipError_t launch_tgemm(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int M, int N, int K, int S,
+                        int mparts, int I, hipStream_t st, const uint32_t* masks, const int32_t* midx, int n_masks,
+                        int wwords) {
+    const int ntiles = (MODE == TM_SWIGLU ? 2 * I : N) / TNB;
+    const int mrows = (((M + mparts - 1) / mparts) + 15) & ~15;
+    const int mt = (mrows + 63) / 64;
+    const int chunks = K / TKC;
+    const int cps = (chunks + S - 1) / S;
+    const dim3 grid((unsigned)(ntiles * S * mparts));
+#define DMCP_TG(MT)                                                                                                 \
+    tgemm_kernel<MT, MODE, PROBE><<<grid, TTH, 0, st>>>(x, w, y, part, M, N, K, cps, S, ntiles, mparts, mrows, I, masks, \
+                                                    midx, n_masks, wwords)
+    switch (mt) {
+        case 1: DMCP_TG(1); break;
+        case 2: DMCP_TG(2); break;
+        case 3: DMCP_TG(3); break;
+        case 4: DMCP_TG(4); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef DMCP_TG
+    return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+// Large-tile GEMM.
+//   mode 0: y[M, N] bf16 = x . w^T                              (S == 1)
+//   mode 1: part[S, M, N] fp32 partials over S K slices of ceil(K / 32 / S) stages
+//   mode 2: y[M, I] bf16 = silu(x . w[:I]^T) * (x . w[I:]^T)     (w = [gate; up] [2I, K], S == 1)
+//   mode 3: ids[M] = masked argmax of bf16(x . w^T) (w [V = N, K]; part: float2 workspace of N / 128 * M pairs;
+//           masks [n_masks, wwords], midx [M]; S == 1)
+// Contract (checked by dmcp/ops/hip.py, guarded here): K % 32 == 0, N % 256 == 0 (mode 2: I % 128 == 0),
+// rows per M part <= 256, every K slice non-empty.
+int dmcp_tgemm(const void* x, const void* w, void* y, void* part, int M, int N, int K, int S, int mparts, int mode,
+               int I, const void* masks, const void* midx, int n_masks, int wwords, void* ids, void* stream) {
+    if (M <= 0) return 0;
+    const int chunks = K / TKC;
+    if (!x || !w || S < 1 || mparts < 1 || K <= 0 || K % TKC != 0 || S > chunks ||
+        (S - 1) * ((chunks + S - 1) / S) >= chunks || (((M + mparts - 1) / mparts + 15) & ~15) > 256 ||
+        (mode == 1 && !part) || (mode != 1 && S != 1) || ((mode == 0 || mode == 2) && !y) ||
+        (mode == 2 ? (I <= 0 || I % (TNB / 2) != 0) : (N <= 0 || N % TNB != 0)) ||
+        (mode == 3 && (!part || !masks || !ids || n_masks < 1 || wwords < (N + 31) / 32)))
+        return hipErrorInvalidValue;
+    auto st = (hipStream_t)stream;
+    auto xx = (const uint16_t*)x;
+    auto ww = (const uint16_t*)w;
+    auto yy = (uint16_t*)y;
+    auto pp = (float*)part;
+    auto mk = (const uint32_t*)masks;
+    auto mi = (const int32_t*)midx;
+    switch (mode) {
+        case 0: return launch_tgemm<TM_BF16>(xx, ww, yy, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
+        case 1: return launch_tgemm<TM_PART>(xx, ww, yy, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
+        case 2: return launch_tgemm<TM_SWIGLU>(xx, ww, yy, pp, M, 2 * I, K, S, mparts, I, st, nullptr, nullptr, 0, 0);
+        case 3: {
+            hipError_t e = launch_tgemm<TM_ARGMAX>(xx, ww, nullptr, pp, M, N, K, 1, mparts, 0, st, mk, mi, n_masks,
+                                                   wwords);
+            if (e != hipSuccess) return e;
+            tgemm_argmax_reduce_kernel<<<(M + kBlock / kWave - 1) / (kBlock / kWave), kBlock, 0, st>>>(
+                (const float2*)part, 2 * (N / TNB), M, (int32_t*)ids);
+            return hipGetLastError();
+        }
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// diagnostics: mode-1 partials with kernel parts switched off (PROBE above)
+int dmcp_tgemm_probe(int probe, const void* x, const void* w, void* part, int M, int N, int K, int S, int mparts,
+                     void* stream) {
+    const int chunks = K / TKC;
+    if (M <= 0 || !x || !w || !part || S < 1 || K % TKC != 0 || S > chunks ||
+        (S - 1) * ((chunks + S - 1) / S) >= chunks || N % TNB != 0 || (((M + mparts - 1) / mparts + 15) & ~15) > 256)
+        return hipErrorInvalidValue;
+    auto st = (hipStream_t)stream;
+    auto xx = (const uint16_t*)x;
+    auto ww = (const uint16_t*)w;
+    auto pp = (float*)part;
+    if (probe == 1)
+        return launch_tgemm<TM_PART, 1>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
+    if (probe == 2)
+        return launch_tgemm<TM_PART, 2>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
+    return hipErrorInvalidValue;
+}
+
+}  // extern "C"

@@ -26,7 +26,7 @@ _lock = threading.Lock()
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _f = ctypes.c_float
-ABI_VERSION = 14  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
+ABI_VERSION = 15  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
 
 
 class HipOpsError(RuntimeError):
@@ -79,6 +79,8 @@ def lib() -> ctypes.CDLL:
             "dmcp_reduce_resid_norm": ([_vp, _i, _vp, _vp, _vp, _i, _i, _f, _vp], _i),
             "dmcp_reduce_rope_kv": ([_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp], _i),
             "dmcp_wgemm": ([_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp], _i),
+            "dmcp_tgemm": ([_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp], _i),
+            "dmcp_tgemm_probe": ([_i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp], _i),
             "dmcp_wgemm_resid_norm": ([_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _vp], _i),
             "dmcp_wgemm_rope_kv": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i,
                                     _i, _i, _vp], _i),
@@ -1148,3 +1150,174 @@ def wgemm_mx_rope_kv(xq, xs, wq, ws, pos: torch.Tensor, slot: torch.Tensor, cos_
                                      _ptr(k_cache), _ptr(v_cache), M, n_q_heads, Hkv, D, MAXS, cos_sin.shape[0], S_,
                                      kv8, _stream()), "dmcp_reduce_rope_kv")
     return q_out
+
+
+# ---------------------------------------------------------------- tgemm
+# Steps of more than WGEMM_MAX_ROWS rows (up to the engine's max_rows) run on
+# the large-tile GEMM (csrc/tgemm.hip): 256 weight rows x up to 256 rows per
+# block, with the same fused consumers as the weight-streaming kernel.
+TGEMM_MAX_ROWS = 1024
+TGEMM_NB = 256
+
+
+def tgemm_supported(N: int, K: int, swiglu: bool = False) -> bool:
+    return K % 32 == 0 and N % (2 * TGEMM_NB if swiglu else TGEMM_NB) == 0
+
+
+def tgemm_plan(M: int, N: int, K: int, mode: str = "part", cus: int = 256) -> tuple:
+    """(K slices S, M parts) of the large-tile GEMM.  M parts of <= 256 rows
+    (a part is staged rounded up to 64 rows); the plan minimises a per-CU
+    time model over the part counts and slice counts: waves of blocks x
+    max(MFMA time, staged bytes at the per-CU LDS-DMA rate) + the split-K
+    partials' round trip.  ``mode``: "part" (fp32 partials, any S), "bf16",
+    "swiglu" and "argmax" (S = 1)."""
+    tiles = N // TGEMM_NB
+    chunks = K // 32
+    best = None
+    for mparts in sorted({-(-M // 256), -(-M // 192), -(-M // 128), -(-M // 256) + 1}):
+        rows = (-(-M // mparts) + 15) // 16 * 16
+        if rows > 256:
+            continue
+        mt = -(-rows // 64)
+        for S in ((1,) if mode != "part" else range(1, 17)):
+            cps = -(-chunks // S)
+            if S > chunks or (S - 1) * cps >= chunks:
+                continue
+            blocks = tiles * mparts * S
+            mfma_us = cps * 16 * mt * 16 / 2100.0        # 16 x MT MFMAs of 16 cycles per stage, ~2.1 GHz
+            dma_us = cps * (TGEMM_NB + 64 * mt) * 64 / 45e3  # staged bytes at ~45 KB/us per CU
+            us = -(-blocks // cus) * max(mfma_us, dma_us) + 0.6
+            if mode == "part":
+                us += S * M * N * 8 / 5e6                   # partials written + read back (~5 TB/s)
+            key = (round(us, 2), -blocks)
+            if best is None or key < best[0]:
+                best = (key, S, mparts)
+    if best is None:
+        raise HipOpsError(f"tgemm_plan: no plan for M={M} N={N} K={K}")
+    return best[1], best[2]
+
+
+def _tgemm_args(x: torch.Tensor, w: torch.Tensor, name: str, swiglu: bool = False) -> tuple:
+    _req(x, torch.bfloat16, f"{name}.x")
+    _req(w, torch.bfloat16, f"{name}.w")
+    if x.dim() != 2 or w.dim() != 2 or x.shape[1] != w.shape[1]:
+        raise HipOpsError(f"{name}: x {tuple(x.shape)} / w {tuple(w.shape)} are not [M, K] / [N, K]")
+    M, K = x.shape
+    N = w.shape[0]
+    if not 1 <= M <= TGEMM_MAX_ROWS or not tgemm_supported(N, K, swiglu):
+        raise HipOpsError(f"{name}: needs 1 <= M <= {TGEMM_MAX_ROWS}, K % 32 == 0, N % {TGEMM_NB} == 0 "
+                          f"(M={M} K={K} N={N})")
+    return M, K, N
+
+
+def _tg(x, w, y, part, M, N, K, S, mparts, mode, inter=0, masks=None, midx=None, n_masks=0, wwords=0, ids=None,
+        name="dmcp_tgemm") -> None:
+    _check(lib().dmcp_tgemm(_ptr(x), _ptr(w), _ptr(y), _ptr(part), M, N, K, S, mparts, mode, inter, _ptr(masks),
+                            _ptr(midx), n_masks, wwords, _ptr(ids), _stream()), name)
+
+
+def tgemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, mparts: int = 0) -> torch.Tensor:
+    """x . w^T in bf16 (F.linear) on the large-tile kernel; M <= TGEMM_MAX_ROWS."""
+    M, K, N = _tgemm_args(x, w, "tgemm")
+    mparts = mparts or tgemm_plan(M, N, K, "bf16")[1]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    _req_out(out, torch.bfloat16, M * N, "tgemm.out")
+    _tg(x, w, out, None, M, N, K, 1, mparts, 0)
+    return out
+
+
+def tgemm_swiglu(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
+                 mparts: int = 0) -> torch.Tensor:
+    """silu(x . w[:I]^T) * (x . w[I:]^T) on the large-tile kernel (w = [gate; up],
+    I % 128 == 0); returns [M, I]."""
+    M, K, N = _tgemm_args(x, w, "tgemm_swiglu", swiglu=True)
+    inter = N // 2
+    mparts = mparts or tgemm_plan(M, N, K, "swiglu")[1]
+    if out is None:
+        out = torch.empty((M, inter), dtype=torch.bfloat16, device=x.device)
+    _req_out(out, torch.bfloat16, M * inter, "tgemm_swiglu.out")
+    _tg(x, w, out, None, M, N, K, 1, mparts, 2, inter, name="dmcp_tgemm[swiglu]")
+    return out
+
+
+def tgemm_partials(x: torch.Tensor, w: torch.Tensor, workspace: torch.Tensor, splits: int = 0,
+                   mparts: int = 0) -> int:
+    """fp32 split-K partials of x . w^T into ``workspace`` [S, M, N]; returns S."""
+    M, K, N = _tgemm_args(x, w, "tgemm_partials")
+    S, mp = tgemm_plan(M, N, K, "part")
+    S, mparts = splits or S, mparts or mp
+    chunks = K // 32
+    if S > chunks or (S - 1) * -(-chunks // S) >= chunks:
+        raise HipOpsError(f"tgemm_partials: K={K} does not split into {S} non-empty slices")
+    _wgemm_ws(workspace, S * M * N, "tgemm_partials")
+    _tg(x, w, None, workspace, M, N, K, S, mparts, 1, name="dmcp_tgemm[partials]")
+    return S
+
+
+def tgemm_resid_norm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor, eps: float,
+                     workspace: torch.Tensor, out: Optional[torch.Tensor] = None, splits: int = 0) -> torch.Tensor:
+    """residual += bf16(x . w^T) (in place); returns RMSNorm(residual) * norm_w
+    -- the large-tile split-K GEMM + wgemm.hip's fused reduction."""
+    M, K, N = _tgemm_args(x, w, "tgemm_resid_norm")
+    _req(residual, torch.bfloat16, "tgemm_resid_norm.residual")
+    _req(norm_w, torch.bfloat16, "tgemm_resid_norm.norm_w")
+    if tuple(residual.shape) != (M, N) or norm_w.numel() != N or N > 8192:
+        raise HipOpsError("tgemm_resid_norm: residual / norm weight shape mismatch")
+    S = tgemm_partials(x, w, workspace, splits)
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    _req_out(out, torch.bfloat16, M * N, "tgemm_resid_norm.out")
+    _check(lib().dmcp_reduce_resid_norm(_ptr(workspace), S, _ptr(residual), _ptr(norm_w), _ptr(out), M, N,
+                                        float(eps), _stream()), "dmcp_reduce_resid_norm")
+    return out
+
+
+def tgemm_rope_kv(x: torch.Tensor, w: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos_sin: torch.Tensor,
+                  k_cache: torch.Tensor, v_cache: torch.Tensor, n_q_heads: int, workspace: torch.Tensor,
+                  q_out: Optional[torch.Tensor] = None, splits: int = 0) -> torch.Tensor:
+    """rope_kv(F.linear(x, w), ...) as the large-tile split-K GEMM + the fused
+    RoPE / q write / KV-append reduction; returns q [M, Hq, D]."""
+    M, K, N = _tgemm_args(x, w, "tgemm_rope_kv")
+    S_, Hkv, MAXS, D = k_cache.shape
+    kv8 = _req_kv(k_cache, v_cache, "tgemm_rope_kv")
+    _req(pos, torch.int32, "tgemm_rope_kv.pos")
+    _req(slot, torch.int32, "tgemm_rope_kv.slot")
+    _req(cos_sin, torch.float32, "tgemm_rope_kv.cos_sin")
+    if v_cache.shape != k_cache.shape or N != (n_q_heads + 2 * Hkv) * D or D % 16 or N > 8192:
+        raise HipOpsError(f"tgemm_rope_kv: w {tuple(w.shape)} does not match Hq={n_q_heads} / kv {tuple(k_cache.shape)}")
+    if pos.numel() != M or slot.numel() != M or cos_sin.dim() != 3 or tuple(cos_sin.shape[1:]) != (D // 2, 2):
+        raise HipOpsError("tgemm_rope_kv: pos/slot/cos_sin shape mismatch")
+    S = tgemm_partials(x, w, workspace, splits)
+    if q_out is None:
+        q_out = torch.empty((M, n_q_heads, D), dtype=torch.bfloat16, device=x.device)
+    _req_out(q_out, torch.bfloat16, M * n_q_heads * D, "tgemm_rope_kv.q_out")
+    _check(lib().dmcp_reduce_rope_kv(_ptr(workspace), S, _ptr(pos), _ptr(slot), _ptr(cos_sin), _ptr(q_out),
+                                     _ptr(k_cache), _ptr(v_cache), M, n_q_heads, Hkv, D, MAXS, cos_sin.shape[0], S_,
+                                     kv8, _stream()), "dmcp_reduce_rope_kv")
+    return q_out
+
+
+def tgemm_lm_head_argmax(x: torch.Tensor, w: torch.Tensor, masks: torch.Tensor, mask_idx: torch.Tensor,
+                         out: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
+                         mparts: int = 0) -> torch.Tensor:
+    """:func:`lm_head_argmax` on the large-tile kernel (V % 256 == 0): 256
+    vocabulary ids per block, one (max, id) pair per block and row."""
+    M, K, V = _tgemm_args(x, w, "tgemm_lm_head_argmax")
+    _req(masks, torch.int32, "tgemm_lm_head_argmax.masks")
+    _req(mask_idx, torch.int32, "tgemm_lm_head_argmax.mask_idx")
+    W = (V + 31) // 32
+    if masks.dim() != 2 or masks.shape[1] != W or mask_idx.numel() != M:
+        raise HipOpsError(f"tgemm_lm_head_argmax: masks {tuple(masks.shape)} / mask_idx {mask_idx.numel()} vs M={M}")
+    if out is None:
+        out = torch.empty(M, dtype=torch.int32, device=x.device)
+    _req_out(out, torch.int32, M, "tgemm_lm_head_argmax.out")
+    need = 2 * (V // 128) * M  # one (max, id) pair per 128-id half tile and row
+    if workspace is None:
+        workspace = torch.empty(need, dtype=torch.float32, device=x.device)
+    if workspace.dtype != torch.float32 or workspace.numel() < need:
+        raise HipOpsError("tgemm_lm_head_argmax: workspace too small")
+    mparts = mparts or tgemm_plan(M, V, K, "argmax")[1]
+    _tg(x, w, None, workspace, M, V, K, 1, mparts, 3, 0, masks, mask_idx, masks.shape[0], W, out,
+        name="dmcp_tgemm[argmax]")
+    return out

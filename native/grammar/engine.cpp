@@ -28,6 +28,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <map>
 #include <unordered_map>
@@ -61,6 +62,7 @@ struct Seq {
     int tid = -1;
     std::vector<Seg> segs;     // its own copy: splices never touch the template
     int slot = -1, pos = 0, seg = 0, free_len = 0, free_bytes = 0, forced_off = 0;
+    size_t free_start = 0;     // offset in ``out`` where the current free string starts
     std::string choice_pref;
     int next_token = -1, next_src = -1, await_row = -1;
     long long await_step = -1;
@@ -70,6 +72,20 @@ struct Seq {
 };
 
 constexpr int ROWS = 7;
+
+// a free string at its byte cap ends at its last word boundary: out[start:]
+// is cut at its last space when that keeps at least half of it (trailing
+// spaces dropped) -- local.py::_trim_to_word
+void trim_to_word(std::string& out, size_t start) {
+    if (start > out.size()) return;
+    const size_t len = out.size() - start;
+    const size_t sp = out.rfind(' ');
+    if (sp == std::string::npos || sp < start) return;
+    size_t cut = sp - start;
+    if (cut < std::max<size_t>(1, len / 2)) return;
+    while (cut > 0 && out[start + cut - 1] == ' ') --cut;
+    out.resize(start + cut);
+}
 
 class Engine {
   public:
@@ -322,6 +338,7 @@ class Engine {
                 return choice_row(s.choice, q.choice_pref);
             }
             q.free_len = q.free_bytes = 0;
+            q.free_start = q.out.size();
             return s.min_len == 0 ? MASK_QUOTE : MASK_NO_QUOTE;
         }
         q.done = true;
@@ -381,6 +398,7 @@ class Engine {
         ++q.free_len;
         q.free_bytes += (int)tbv.size();
         if (q.free_bytes >= s.max_len) {
+            trim_to_word(q.out, q.free_start);
             q.next_token = quote_;
             return -1;
         }

@@ -317,10 +317,10 @@ def test_class_type_correction_is_the_models_choice(pipeline):
     """classTypeCorrection is a grammar choice (null or one of the 10 types,
     ClaudeApiClient.java:101-120): a model that prefers '"', 'E', 'N' writes
     "ENTITY"; one that prefers 'n' writes null."""
-    ent = LocalEngine(_Forcing({'"': 30.0, "E": 25.0, "N": 20.0}), pipeline=pipeline)
+    ent = LocalEngine(_Forcing({'"': 30.0, "E": 25.0, "N": 20.0}), pipeline=pipeline, type_choice=True)
     doc = json.loads(ent.generate(_inputs(2)[1:], None)[0])
     assert doc["classTypeCorrection"] == "ENTITY" and ent.stats["type_corrections"] == 1
-    keep = LocalEngine(_Forcing({"n": 30.0, "]": 20.0}), pipeline=pipeline)
+    keep = LocalEngine(_Forcing({"n": 30.0, "]": 20.0}), pipeline=pipeline, type_choice=True)
     doc = json.loads(keep.generate(_inputs(2)[1:], None)[0])
     assert doc["classTypeCorrection"] is None
 
@@ -408,7 +408,7 @@ def test_class_type_correction_reaches_the_database(tmp_path):
     from dmcp.utils import synth
     repo = tmp_path / "shop"
     synth.java_spring_repo(str(repo), 8)
-    be = LocalLLMBackend([LocalEngine(_Forcing({'"': 30.0, "D": 25.0, "]": 20.0}))])
+    be = LocalLLMBackend([LocalEngine(_Forcing({'"': 30.0, "D": 25.0, "]": 20.0}), type_choice=True)])
     app = make_app(tmp_path, backend=be)
     r = app.indexer.analyze_project(str(repo))
     assert r.success and r.stats["enriched"] == r.classes_analyzed
@@ -444,8 +444,8 @@ def test_native_grammar_engine_matches_the_python_engine(tiny, pipeline):
     inputs = _inputs(9) + [EnrichmentInput("class Big {}", "co.x.Big", "java", "LISTENER",
                                            [f"onEvent{i}" for i in range(30)])]
     items = [(i, inp, other if i % 4 == 3 else readme) for i, inp in enumerate(inputs)]
-    py = LocalEngine(tiny, pipeline=pipeline, native_grammar=False, max_new_tokens=900)
-    nat = LocalEngine(tiny, pipeline=pipeline, native_grammar=True, max_new_tokens=900)
+    py = LocalEngine(tiny, pipeline=pipeline, native_grammar=False, max_new_tokens=900, type_choice=True)
+    nat = LocalEngine(tiny, pipeline=pipeline, native_grammar=True, max_new_tokens=900, type_choice=True)
     assert py._native is None and nat._native is not None
     a, b = dict(py.stream(items, None)), dict(nat.stream(items, None))
     assert a == b
@@ -570,3 +570,87 @@ def test_decode_attention_fork_table_matches_copied_kv():
     k2[4, :, :9], v2[4, :, :9] = kc[0, :, :9], vc[0, :, :9]
     exp = R.decode_attention(q, k2, v2, slot, seq, 0.25)
     assert torch.equal(got, exp)
+
+
+def test_random_weights_never_correct_class_types(tmp_path):
+    """A random-initialised preset (no checkpoint) gets a forced
+    ``"classTypeCorrection": null``: a model that would pick "DTO" given the
+    choice leaves every statically inferred class type as it was, through
+    the real pipeline."""
+    from conftest import make_app
+    from dmcp.utils import synth
+    forcing = _Forcing({'"': 30.0, "D": 25.0, "]": 20.0})
+    assert forcing.checkpoint is None
+    eng = LocalEngine(forcing)
+    assert not eng.type_choice
+    doc = json.loads(eng.generate(_inputs(2)[1:], None)[0])
+    assert doc["classTypeCorrection"] is None and eng.stats["type_corrections"] == 0
+    repo = tmp_path / "shop"
+    synth.java_spring_repo(str(repo), 8)
+    app = make_app(tmp_path, backend=LocalLLMBackend([LocalEngine(_Forcing({'"': 30.0, "D": 25.0, "]": 20.0}))]))
+    r = app.indexer.analyze_project(str(repo))
+    assert r.success and r.stats["enriched"] == r.classes_analyzed
+    types = {c.full_class_name: c.class_type.value for c in app.repos.classes.find_by_project_id(r.project_id)}
+    assert types["co.acme.shop.order.OrderService"] == "SERVICE" and "DTO" not in set(types.values()) - {"DTO"}
+    assert len(set(types.values())) > 1  # the static types, not one forced type
+    app.db.close()
+    forcing.checkpoint = "/some/checkpoint"
+    assert LocalEngine(forcing).type_choice  # a loaded checkpoint makes its own choice
+
+
+def test_reply_shape_derives_from_the_budget_and_config():
+    """String caps and the step count scale with the reply budget (the
+    reference's free-length contract, ClaudeApiClient.java:40, 101-113) and
+    each can be set; the legacy caps are the 1,536-token floor."""
+    from dmcp.config import Config
+    from dmcp.enrich.local import ReplyShape
+    from dmcp.enrich.workers import engine_spec
+    assert ReplyShape.from_budget(1536) == ReplyShape.LEGACY == ReplyShape(96, 64, 40, 3)
+    assert ReplyShape.from_budget(4096) == ReplyShape(256, 128, 64, 4)
+    assert ReplyShape.from_budget(16384) == ReplyShape(512, 256, 160, 6)
+    assert ReplyShape.from_budget(4096, desc=1000, max_steps=2) == ReplyShape(1000, 128, 64, 2)
+    cfg = Config.from_env({"LOCAL_LLM_DESC_MAX_BYTES": "300", "LOCAL_LLM_MAX_STEPS": "5"})
+    spec = engine_spec(cfg)
+    assert spec["reply_shape"] == {"desc": 300, "method": 0, "step": 0, "max_steps": 5}
+    tiny = LocalLM(preset("tiny", max_batch=4, max_rows=16, max_seq=8192), device="cpu", seed=1)
+    eng = LocalEngine(tiny, use_graphs=False, **spec)
+    assert eng.reply_budget == 4096
+    assert eng.reply_shape == ReplyShape(300, 128, 64, 5)
+    segs = build_template(["a"], *eng.reply_shape.scaled(1.0), eng.reply_shape.max_steps)
+    assert max(s.max_len for s in segs if s.is_free) == 300
+
+
+class _Pattern(_Forcing):
+    """Greedy text "abc abc ..." by position (row bias = one byte of the
+    4-byte cycle at the row's position)."""
+
+    def __init__(self):
+        super().__init__({})
+        self.cycle = [ord(c) for c in "abc "]
+
+    def decode(self, tokens, slots, positions, *a, **kw):
+        lg = LocalLM.decode(self, tokens, slots, positions, *a, **kw).float()
+        for r, p in enumerate(positions.tolist()):
+            lg[r, self.cycle[p % 4]] += 40.0
+        return lg.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("native", [False, True])
+def test_capped_string_closes_at_a_word_boundary(native):
+    """A free string that reaches its byte cap ends at its last space (never
+    mid-word, no trailing space); the native grammar engine cuts the same."""
+    from dmcp.enrich.local import ReplyShape, _trim_to_word
+    eng = LocalEngine(_Pattern(), use_graphs=False, native_grammar=native, reply_shape=ReplyShape(41, 30, 22, 1))
+    doc = json.loads(eng.generate(_inputs(2)[1:], None)[0])
+    texts = [(doc["description"], 41)] + [(m["description"], 30) for m in doc["methods"]] + \
+        [(st, 22) for m in doc["methods"] for st in m["businessLogic"]]
+    for text, cap in texts:
+        # byte tokens reach the cap exactly; the cut shortens every string
+        assert 0 < len(text.encode()) < cap and text[-1] != " " and " " in text, (text, cap)
+        assert set(text.split(" ")[-1]) <= set("abc")
+    b = bytearray(b'{"x": "alpha beta gam')
+    _trim_to_word(b, 7)
+    assert bytes(b) == b'{"x": "alpha beta'
+    b = bytearray(b'{"x": "al phabetagam')  # the last space is in the first half: cut at the cap
+    _trim_to_word(b, 7)
+    assert bytes(b) == b'{"x": "al phabetagam'

@@ -193,3 +193,14 @@ def test_sentencepiece_split_prompt_round_trips_exactly(tmp_path):
     # space (as any encode of the whole prompt does); nothing else is added
     assert b"".join(tok.token_bytes[i] for i in ids[1:]) == b" " + text.encode()
     assert b"".join(tok.token_bytes[i] for i in ids[split:]) == text[text.find("Source of "):].encode()
+
+
+def test_checkpoint_keeps_bf16_prefill_and_makes_type_choices(ckpt):
+    """A loaded checkpoint resolves prefill_dtype "auto" to bf16 (MXFP8
+    parity is pinned on random-init weights only; fp8 stays available by
+    name) and gets the classTypeCorrection choice a random preset does not."""
+    model, tok = load_local_model(ckpt, device="cpu", max_batch=2, max_rows=8, max_seq=1024, prefill_dtype="auto")
+    assert model.checkpoint == ckpt and model.cfg.prefill_dtype == "bf16" and not model.prefill_fp8
+    assert LocalEngine(model, tokenizer=tok, use_graphs=False).type_choice
+    fp8, _ = load_local_model(ckpt, device="cpu", max_batch=2, max_rows=8, max_seq=1024, prefill_dtype="fp8")
+    assert fp8.cfg.prefill_dtype == "fp8"

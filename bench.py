@@ -67,6 +67,12 @@ def parse_args(argv=None):
     ap.add_argument("--enrich-local-presets", default="dmcp-coder-1b,llama3.2-1b-code")
     ap.add_argument("--remote-steps", type=int, default=3,
                     help="timed analyses on the remote-repository path (extra.remotePath; 0 = skip)")
+    ap.add_argument("--lang-files", type=int, default=1000,
+                    help="source files of the TS / Go indexing runs (extra.tsIndex / extra.goIndex; 0 = skip)")
+    ap.add_argument("--lang-steps", type=int, default=5)
+    ap.add_argument("--small-project-classes", type=int, default=33,
+                    help="classes of the latency-bound enrichment run (extra.enrichLocal*.smallProject: what "
+                         "each of 8 GPUs gets when one 257-class project is dealt over 8; 0 = skip)")
     return ap.parse_args(argv)
 
 
@@ -152,7 +158,32 @@ def _enrich_local(pool, args, ctx, work, rank):
             raise RuntimeError(f"enrichLocal analysis failed on {int(bad)} rank(s): {err!r}")
         st = be.stats()
         steps = max(1.0, st.get("decode_steps", 0))
+        small = None
+        if args.small_project_classes > 0:
+            # one small project alone on this GPU: the latency-bound tail each
+            # GPU runs when a 257-class project is dealt over 8 (strong scaling)
+            srepo = os.path.join(work, f"small{rank}")
+            synth.java_spring_repo(srepo, n_classes=args.small_project_classes, base_package=f"co.acme.sml{rank}",
+                                   seed=rank + 301)
+            ctx.barrier()
+            t1 = time.perf_counter()
+            try:
+                rs = app.indexer.analyze_project(srepo)
+            except Exception as e:
+                rs, err = None, e
+            smx = ctx.max(time.perf_counter() - t1)[0]
+            if ctx.sum(1.0 if rs is None else 0.0)[0] == 0:
+                ph2 = ctx.max(rs.stats.get("analyze.phase2", 0.0) / 1e3)[0]
+                small = {"classes": rs.classes_analyzed, "enriched": int(rs.stats.get("enriched", 0)),
+                         "elapsedS": round(smx, 3), "phase2S": round(ph2, 3),
+                         "classesPerSec": round(rs.classes_analyzed / smx, 2)}
+            else:
+                small = {"error": repr(err)[:300]}
+        wit = (pool.workers[0].info or {}).get("witness") if pool.workers else None
         return {"classesPerSec": round(tot[0] / mx, 2), "classesEnriched": int(tot[0]),
+                "device": wit, "graphReplays": int(st.get("graph_replays", 0)),
+                "graphKernelsPerStep": round(st.get("graph_kernels", 0) / max(1, st.get("graph_replays", 0)), 1),
+                "smallProject": small,
                 "promptTokensPerClass": round(st.get("prompt_tokens", 0) / max(1, st.get("prefills", 1)), 1),
                 "generatedTokensPerClass": round(st.get("generated_tokens", 0) / max(1, tot[0]), 1),
                 "typeCorrections": int(st.get("type_corrections", 0)), "splitClasses": int(st.get("split_classes", 0)),
@@ -172,6 +203,48 @@ def _enrich_local(pool, args, ctx, work, rank):
                            "path": "analyze_project -> streamed Phase 2 -> GPU worker process"}}
     finally:
         app.db.close()
+
+
+def _lang_index(kind: str, args, work: str, threads: int) -> dict:
+    """extra.tsIndex / extra.goIndex: the production analyze_project of a
+    generated TypeScript (NestJS, reference NodeJsGraalParser.java:102-189)
+    or Go (gin, reference GoSourceParser.java:339-372) repository of
+    ``--lang-files`` source files, enrichment off, timed over
+    ``--lang-steps`` analyses after one warm-up -- BASELINE configs 4-5 at
+    scale."""
+    from dmcp.app import App
+    from dmcp.config import Config
+    from dmcp.utils import synth
+    root = os.path.join(work, f"{kind}repo")
+    if kind == "ts":
+        synth.nestjs_repo(root, n_modules=max(1, args.lang_files // 4))
+        ext = (".ts",)
+    else:
+        synth.go_service_repo(root, n_packages=max(1, args.lang_files // 4))
+        ext = (".go",)
+    files = sum(1 for r, _, fs in os.walk(root) if "/.git" not in r for f in fs if f.endswith(ext))
+    cfg = Config(db_path=os.path.join(work, f"{kind}.db"), git_clone_base_path=os.path.join(work, f"{kind}clones"),
+                 parser_threads=threads, enrich_backend="null", require_enrichment_for_analyze=False,
+                 recover_stuck_on_start=False)
+    app = App(cfg)
+    try:
+        app.indexer.analyze_project(root)  # warm-up
+        t0 = time.perf_counter()
+        acc = {}
+        for _ in range(args.lang_steps):
+            r = app.indexer.analyze_project(root)
+            for k, v in r.stats.items():
+                if k.startswith("analyze."):
+                    acc[k] = acc.get(k, 0.0) + v
+        el = time.perf_counter() - t0
+        return {"sourceFiles": files, "classesPerRepo": r.classes_analyzed,
+                "msPerAnalysis": round(1e3 * el / args.lang_steps, 2),
+                "filesPerSec": round(files * args.lang_steps / el, 1),
+                "classesPerSec": round(r.classes_analyzed * args.lang_steps / el, 1),
+                "phaseMs": {k: round(v / args.lang_steps, 2) for k, v in acc.items()},
+                "framework": "nestjs" if kind == "ts" else "gin", "steps": args.lang_steps}
+    finally:
+        app.close()
 
 
 def _remote_path(args, work, repo, threads):
@@ -275,6 +348,13 @@ def main(argv=None) -> int:
             extra["graphQueryMs"] = {"p50": round(lat[len(lat) // 2], 3), "p99": round(lat[int(len(lat) * 0.99) - 1], 3)}
             extra["stackTrace20Ms"] = {"p50": round(st_lat[len(st_lat) // 2], 3),
                                        "p99": round(st_lat[max(0, int(len(st_lat) * 0.99) - 1)], 3)}
+        for kind in (("ts", "go") if rank == 0 and args.lang_files > 0 else ()):
+            key = "tsIndex" if kind == "ts" else "goIndex"
+            try:
+                extra[key] = _lang_index(kind, args, work, threads)
+            except Exception as e:
+                logging.getLogger("bench").exception("%s failed", key)
+                extra[key] = {"error": repr(e)[:300]}
         if rank == 0 and args.remote_steps > 0:
             try:
                 extra["remotePath"] = _remote_path(args, work, repo, threads)

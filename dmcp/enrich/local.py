@@ -542,7 +542,8 @@ class LocalEngine:
                       "prefix_s": 0.0, "host_s": 0.0, "wait_s": 0.0, "launch_s": 0.0, "prefill_gpu_s": 0.0,
                       "reply_parts": 0,
                       "split_classes": 0, "methods_dropped": 0, "type_corrections": 0, "choice_waits": 0,
-                      "forks": 0, "fork_branches": 0, "fork_waits": 0, "fork_skipped": 0}
+                      "forks": 0, "fork_branches": 0, "fork_waits": 0, "fork_skipped": 0,
+                      "graph_replays": 0, "graph_kernels": 0}
         self._pf_events: List[tuple] = []  # (start, end) device events of the batched prefills
         self._lock = threading.Lock()
         self._frag_cache: Dict[bytes, List[int]] = {}      # forced text -> ids
@@ -557,6 +558,13 @@ class LocalEngine:
         self._stage = np.zeros((7, self.max_rows), dtype=np.int32)  # the native builder's step rows
         self._host_np = [h.numpy() for h in self._host_ids]
         self._ids_events = [torch.cuda.Event(), torch.cuda.Event()] if dev.type == "cuda" else [None, None]
+
+    def _count_graphs(self) -> None:
+        """The device witness in the stats: hipGraph replays and the kernel
+        nodes they launched (cumulative, like every engine stat)."""
+        if self.graphs is not None:
+            self.stats["graph_replays"] = self.graphs.counts["graph_replays"]
+            self.stats["graph_kernels"] = self.graphs.counts["graph_kernels"]
 
     # ---------------------------------------------------------------- api
     def generate(self, inputs: Sequence[EnrichmentInput], readme: Optional[str]) -> List[str]:
@@ -1196,6 +1204,7 @@ class LocalEngine:
                     if n:
                         prev_event, prev_buf, prev_n = event, buf, n
                         self.stats["decode_steps"] += 1
+                        self._count_graphs()
                         self.stats["decode_rows"] += n
                         self.stats["generated_tokens"] += n
                     fin = nat.collect_done()
@@ -1311,6 +1320,7 @@ class LocalEngine:
                 if toks:
                     prev_event, prev_buf, prev_n = event, buf, len(toks)
                     self.stats["decode_steps"] += 1
+                    self._count_graphs()
                     self.stats["decode_rows"] += len(toks)
                     self.stats["generated_tokens"] += len(toks)
                 gone = [s for s in active if s.done]

@@ -702,6 +702,26 @@ class _EchoEngine:
             active = still
 
 
+def _witness(dev: str) -> dict:
+    """What this worker runs on, from the device itself (hipGetDeviceProperties)
+    and the kernel library it loaded -- reported next to every throughput
+    number the worker produces."""
+    if not dev.startswith("cuda"):
+        return {"device": dev}
+    try:
+        import torch
+        p = torch.cuda.get_device_properties(0)
+        out = {"name": p.name, "arch": getattr(p, "gcnArchName", ""), "cus": p.multi_processor_count,
+               "hbm_gib": round(p.total_memory / 2**30, 1)}
+        from ..ops import hip
+        out["hipops"] = os.path.relpath(hip.TARGET if not os.environ.get("DMCP_HIPOPS_SO") else
+                                        os.environ["DMCP_HIPOPS_SO"])
+        out["hipops_abi"] = int(hip.lib().dmcp_abi_version())
+        return out
+    except Exception as e:  # noqa: BLE001 -- a witness, never a failure
+        return {"device": dev, "error": repr(e)[:200]}
+
+
 def worker_main() -> int:
     """``python -m dmcp.enrich.workers``: serve frames on stdin/stdout."""
     rx = sys.stdin.buffer
@@ -740,7 +760,7 @@ def worker_main() -> int:
             return 3
         max_batch = model.cfg.max_batch
     send({"op": "ready", "pid": os.getpid(), "device": dev,
-          "gpu": os.environ.get("HIP_VISIBLE_DEVICES", ""), "max_batch": max_batch})
+          "gpu": os.environ.get("HIP_VISIBLE_DEVICES", ""), "max_batch": max_batch, "witness": _witness(dev)})
 
     # ONE engine stream over every session: the projects the pool deals this
     # worker share its continuous batch (MultiFeed: round-robin over them)

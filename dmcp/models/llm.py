@@ -146,6 +146,15 @@ def fused_shapes_ok(c: LMConfig) -> bool:
             and c.head_dim % 32 == 0 and c.vocab_size % 16 == 0 and c.hidden % 16 == 0)
 
 
+def tgemm_shapes_ok(c: LMConfig) -> bool:
+    """The large-tile GEMM's contract (csrc/tgemm.hip) for every decode
+    projection: output widths (QKV, hidden, 2 x intermediate) multiples of
+    256, reduction depths multiples of 64, plus the fused reductions' <= 8192."""
+    return (c.qkv_dim % 256 == 0 and c.hidden % 256 == 0 and (2 * c.intermediate) % 256 == 0
+            and c.hidden % 64 == 0 and (c.n_heads * c.head_dim) % 64 == 0 and c.intermediate % 64 == 0
+            and c.qkv_dim <= 8192 and c.hidden <= 8192 and c.head_dim % 16 == 0)
+
+
 def wgemm_shapes_ok(c: LMConfig) -> bool:
     """The weight-streaming GEMMs' contract (csrc/wgemm.hip): reduction
     depths (hidden, heads x head_dim, intermediate) multiples of 64, output
@@ -291,6 +300,19 @@ class LocalLM:
         # 533-row step on hipBLASLt, profiles/kstats_llama_r4.txt)
         self.fused_head = self.device.type == "cuda" and ops.lm_head_supported(c.vocab_size, c.hidden)
         self.head_ws = ops.lm_head_workspace(c.vocab_size, self.device) if self.fused_head else None
+        # steps of WGEMM_MAX_ROWS < rows <= TGEMM_MAX_ROWS (the engine's
+        # jump-forward steps reach max_rows = 1.5 x max_batch): every
+        # projection on the large-tile GEMM (csrc/tgemm.hip) with the same
+        # fused consumers, and its LM head + masked argmax when V % 256 == 0
+        # -- no hipBLASLt GEMM in any decode step
+        self.use_tgemm = (self.device.type == "cuda" and self.max_rows > ops.WGEMM_MAX_ROWS
+                          and tgemm_shapes_ok(c) and self.max_rows <= ops.TGEMM_MAX_ROWS)
+        self.tg_ws = (torch.empty(16 * self.max_rows * max(c.qkv_dim, c.hidden), dtype=torch.float32,
+                                  device=self.device) if self.use_tgemm else None)
+        self.tg_head = self.fused_head and c.vocab_size % 256 == 0 and c.hidden % 64 == 0
+        self.tg_head_ws = (torch.empty(2 * (c.vocab_size // 128) * self.max_rows, dtype=torch.float32,
+                                       device=self.device) if self.tg_head and self.max_rows > ops.WGEMM_MAX_ROWS
+                           else None)
         # fp8 prefill: e4m3 copies of the four projections (per-row scales),
         # quantised once; the batched prefill then runs on csrc/pgemm.hip
         # (the CPU references take any dims the 32-element blocks divide)
@@ -532,7 +554,7 @@ class LocalLM:
         prefix = self.prefix_slot if any(shared) else None
         if self.prefill_fp8:
             h = self._prefill_fp8(ids, pos_t, slot_t, offsets, seq_slots, starts, prefix, shared, last)
-            return F.linear(h, self.w["lm_head"])
+            return self._head(h)
         x = ops.embedding(self.w["embed"], ids)
         resid = x.clone()
         h = ops.add_rmsnorm(x, self.w["l0.ln1"], c.eps)
@@ -547,6 +569,14 @@ class LocalLM:
             nxt = self.w[f"l{i + 1}.ln1"] if i + 1 < c.layers else self.w["norm_f"]
             h = ops.add_rmsnorm(m, nxt, c.eps, residual=resid)
         return F.linear(h.index_select(0, last), self.w["lm_head"])
+
+    def _head(self, h: torch.Tensor) -> torch.Tensor:
+        """The LM head's logits of a few rows (the batched prefill's last
+        positions) on the weight-streaming kernel (csrc/wgemm.hip), hipBLASLt
+        only off its shape contract."""
+        if self.use_wgemm and h.shape[0] <= ops.WGEMM_MAX_ROWS and self.cfg.vocab_size % 64 == 0:
+            return ops.wgemm(h.contiguous(), self.w["lm_head"])
+        return F.linear(h, self.w["lm_head"])
 
     def _prefill_fp8(self, ids, pos_t, slot_t, offsets, seq_slots, starts, prefix, shared, last) -> torch.Tensor:
         """The layers of :meth:`prefill_batch` on the MXFP8 kernels: the
@@ -612,9 +642,20 @@ class LocalLM:
         if self.decode_fp8 and (self.device.type == "cpu" or B <= ops.WMX_MAX_ROWS):
             return self._decode_trunk_fp8(B, resid, h, seq_len, slots, positions, chunk, splits, prefix_rows)
         wide = self.use_wgemm and B <= ops.WGEMM_MAX_ROWS
+        big = self.use_tgemm and ops.WGEMM_MAX_ROWS < B <= ops.TGEMM_MAX_ROWS
         for i in range(c.layers):
             kc, vc = self.k_cache[i], self.v_cache[i]
             nxt = self.w[f"l{i + 1}.ln1"] if i + 1 < c.layers else self.w["norm_f"]
+            if big:
+                q = ops.tgemm_rope_kv(h, self.w[f"l{i}.wqkv"], positions, slots, self.cos_sin, kc, vc, c.n_heads,
+                                      self.tg_ws)
+                att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws,
+                                           chunk=chunk, fork=self.fork_tab, prefix=self._prefix(i, prefix_rows),
+                                           splits=splits).view(B, c.n_heads * c.head_dim)
+                h = ops.tgemm_resid_norm(att, self.w[f"l{i}.wo"], resid, self.w[f"l{i}.ln2"], c.eps, self.tg_ws)
+                act = ops.tgemm_swiglu(h, self.w[f"l{i}.wgu"])
+                h = ops.tgemm_resid_norm(act, self.w[f"l{i}.wdown"], resid, nxt, c.eps, self.tg_ws)
+                continue
             if wide:
                 q = ops.wgemm_rope_kv(h, self.w[f"l{i}.wqkv"], positions, slots, self.cos_sin, kc, vc, c.n_heads,
                                       self.wgemm_ws)
@@ -722,7 +763,10 @@ class LocalLM:
         if toks == self.prefix_tokens:
             return P
         self.clear_prefix()
-        self.forward_tokens(torch.tensor(toks, dtype=torch.int32), self.prefix_slot, 0)
+        if self.prefill_fp8:  # the MXFP8 prefill kernels, as every other prompt token
+            self.prefill_batch([(list(toks), self.prefix_slot, 0)])
+        else:
+            self.forward_tokens(torch.tensor(toks, dtype=torch.int32), self.prefix_slot, 0)
         self.prefix_len, self.prefix_tokens = P, toks
         self.prefix_dev.fill_(P)
         return P
@@ -828,8 +872,12 @@ class LocalLM:
             # kernel: no [B, vocab] logits (returned as None)
             h = self._decode_trunk(tokens, slots, positions, src, last_ids, mask_idx, mask_alt, alt_token,
                                    prefix_rows)
-            ids = ops.lm_head_argmax(h, self.w["lm_head"], masks, mask_idx, out=last_ids[:B],
-                                     workspace=self.head_ws)
+            if self.tg_head_ws is not None and B > ops.WGEMM_MAX_ROWS:
+                ids = ops.tgemm_lm_head_argmax(h, self.w["lm_head"], masks, mask_idx, out=last_ids[:B],
+                                               workspace=self.tg_head_ws)
+            else:
+                ids = ops.lm_head_argmax(h, self.w["lm_head"], masks, mask_idx, out=last_ids[:B],
+                                         workspace=self.head_ws)
             return None, ids
         logits = self.decode(tokens, slots, positions, src=src, last_ids=last_ids, mask_idx=mask_idx,
                              mask_alt=mask_alt, alt_token=alt_token, prefix_rows=prefix_rows)
@@ -872,16 +920,47 @@ class LocalLM:
         return rms(x, w["norm_f"]) @ w["lm_head"].t()
 
 
+_HIPRT = None
+
+
+def graph_kernel_nodes(g) -> int:
+    """Kernel nodes of a captured hipGraph (hipGraphGetNodes +
+    hipGraphNodeGetType through the HIP runtime torch already loaded); -1 if
+    the runtime does not answer.  The engine's device witness: replays x
+    kernels per replay = kernels the GPU ran for the decode steps."""
+    global _HIPRT
+    import ctypes
+    try:
+        if _HIPRT is None:
+            _HIPRT = ctypes.CDLL("libamdhip64.so")
+        graph = ctypes.c_void_p(g.raw_cuda_graph())
+        n = ctypes.c_size_t(0)
+        if _HIPRT.hipGraphGetNodes(graph, None, ctypes.byref(n)) != 0:
+            return -1
+        nodes = (ctypes.c_void_p * n.value)()
+        if _HIPRT.hipGraphGetNodes(graph, nodes, ctypes.byref(n)) != 0:
+            return -1
+        kernels = 0
+        for i in range(n.value):
+            t = ctypes.c_int(-1)
+            if _HIPRT.hipGraphNodeGetType(ctypes.c_void_p(nodes[i]), ctypes.byref(t)) == 0 and t.value == 0:
+                kernels += 1  # hipGraphNodeTypeKernel
+        return kernels
+    except Exception:  # noqa: BLE001 -- a witness, never a failure
+        return -1
+
+
 class _Bucket:
     """One captured decode graph and its two pinned staging buffers: a step
     packs its rows into the buffer whose previous H2D copy (two steps back)
     has surely completed, so the host never waits on the copy of the step
     still in flight (one buffer made every launch wait for it: ~0.9 ms per
     step at 533 rows, graph_timing sync_s)."""
-    __slots__ = ("graph", "inp", "logits", "ids", "stage", "np", "copied", "turn")
+    __slots__ = ("graph", "inp", "logits", "ids", "stage", "np", "copied", "turn", "kernels")
 
     def __init__(self, graph, inp, logits, ids, b: int) -> None:
         self.graph, self.inp, self.logits, self.ids = graph, inp, logits, ids
+        self.kernels = graph_kernel_nodes(graph)
         self.stage = [torch.zeros((7, b), dtype=torch.int32).pin_memory() for _ in range(2)]
         self.np = [t.numpy() for t in self.stage]
         self.copied = [torch.cuda.Event(), torch.cuda.Event()]
@@ -914,6 +993,8 @@ class DecodeGraphs:
         self.masks = masks
         self.alt_token = int(alt_token)
         self.timing = {"sync_s": 0.0, "replay_s": 0.0}  # host time inside run(): staging wait, H2D + launch
+        # device witness: graph replays and the kernel nodes they launched
+        self.counts = {"graph_replays": 0, "graph_kernels": 0}
         self.buckets = sorted(b for b in buckets if b <= model.max_rows)
         if not self.buckets or self.buckets[-1] < model.max_rows:
             self.buckets.append(model.max_rows)
@@ -1008,5 +1089,7 @@ class DecodeGraphs:
         bk.copied[bk.turn].record()
         bk.turn ^= 1
         bk.graph.replay()
+        self.counts["graph_replays"] += 1
+        self.counts["graph_kernels"] += max(0, bk.kernels)
         self.timing["replay_s"] += time.perf_counter() - t0
         return (bk.logits[:n] if bk.logits is not None else None), bk.ids[:n]

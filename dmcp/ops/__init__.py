@@ -18,6 +18,8 @@ from .hip import (FUSED_MAX_ROWS, PREFIX_MFMA_MAX_SPLITS, WGEMM_MAX_ROWS, decode
                   prefill_supported, wgemm_resid_norm, wgemm_rope_kv, wgemm_swiglu, wgemm_workspace)
 from .hip import (PGEMM_TILE_N, WMX_MAX_ROWS, pgemm_supported, wgemm_mx_resid_norm, wgemm_mx_rope_kv,  # noqa: F401
                   wgemm_mx_swiglu, wmx_plan)
+from .hip import (TGEMM_MAX_ROWS, tgemm_lm_head_argmax, tgemm_resid_norm, tgemm_rope_kv, tgemm_swiglu,  # noqa: F401
+                  wgemm)
 from .reference import SharedPrefix, mx_dequant, quantize_weight, rope_tables, weight_dequant  # noqa: F401
 
 

@@ -24,7 +24,7 @@
 //     kernel: 45 % of MFMA time at 1,024 rows); now the SIMD partner keeps
 //     issuing MFMAs meanwhile;
 //   * 32-deep K stages ([rows][4 x 16 B] images, 16-row 1-KiB LDS-DMA
-//     pieces) in a 4-stage ring, 3 stages (up to 96 KiB) in flight per CU;
+//     pieces) in a 5-6-stage ring filling the CU's LDS (tstages);
 //   * chunk j of row r sits in slot j ^ ((4 - (r >> 2)) & 3): the 16 lanes of
 //     each ds_read_b128 group of the 16x16x32 operand layout (lane (l16, g):
 //     row l16, chunk g) cover all 64 banks;
@@ -38,8 +38,27 @@
 
 namespace {
 
-constexpr int TKC = 32;   // K per LDS stage
-constexpr int TST = 4;    // ring stages (3 in flight while one is computed)
+// K per LDS stage: 64 (128-B image rows, full cache lines per DMA lane
+// group) or 32 (64-B rows: each 128-B line is fetched twice, in two stages)
+constexpr int TKC_DEFAULT = 64;
+// ring stages: as many stages as fit the CU's 160 KiB of LDS (capped at 6)
+template <int MT, int KC>
+constexpr int tstages() {
+    return (160 * 1024) / ((256 + 64 * MT) * KC * 2) < 6 ? (160 * 1024) / ((256 + 64 * MT) * KC * 2) : 6;
+}
+
+// s_waitcnt vmcnt(n * GL) for a runtime n in [0, 5] (the count is an immediate)
+template <int GL>
+__device__ __forceinline__ void wait_vm(int n) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(GL) : "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * GL) : "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * GL) : "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 * GL) : "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(5 * GL) : "memory"); break;
+    }
+}
 constexpr int TNB = 256;  // weight rows per block
 constexpr int TTH = 512;  // threads per block: 8 waves, two per SIMD
 constexpr int TM_BF16 = 0, TM_PART = 1, TM_SWIGLU = 2, TM_ARGMAX = 3;
@@ -51,24 +70,35 @@ __device__ __forceinline__ void tglds16(const void* src, uint4* lds_base) {
                                      (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
-// slot of logical 16-B chunk j of image row r (4 chunks per 64-B row)
-__device__ __forceinline__ int tslot(int j, int r) { return j ^ ((4 - (r >> 2)) & 3); }
+// slot of logical 16-B chunk j of image row r: 64-B rows (4 chunks): j ^
+// ((4 - (r >> 2)) & 3); 128-B rows (8 chunks): j ^ (r & 7) -- either way the
+// 16 lanes of each ds_read_b128 group of the 16x16x32 operand layout (lane
+// (l16, g): row l16, chunk g of the k step) cover all 64 banks
+template <int KC>
+__device__ __forceinline__ int tslot(int j, int r) {
+    if constexpr (KC == 32) return j ^ ((4 - (r >> 2)) & 3);
+    else return j ^ (r & 7);
+}
 
 // PROBE (dmcp_tgemm_probe only; diagnostics of scripts/bench_tgemm.py --probe):
 // 1 = the K loop issues no refill DMAs (MFMA + LDS reads + barriers on stale
 // stages), 2 = no fragment reads / MFMAs (the DMA ring alone)
-template <int MT, int MODE, int PROBE = 0>
+template <int MT, int MODE, int PROBE = 0, int KC = TKC_DEFAULT>
 __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) void tgemm_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, float* __restrict__ part,
     int M, int N, int K, int cps, int S, int ntiles, int mparts, int mrows, int I, const uint32_t* __restrict__ masks,
     const int32_t* __restrict__ midx, int n_masks, int wwords) {
     constexpr int NF = TNB / 32;       // A fragments per wave (16 weight rows each): half the tile's rows
+    constexpr int RCH = KC / 8;        // 16-B chunks per image row
+    constexpr int PR = 64 / RCH;       // image rows per 1-KiB LDS-DMA piece
     constexpr int MR = 64 * MT;        // staged X rows
-    constexpr int WI = TNB / 64;       // 1-KiB pieces (16 rows x 64 B) per loader wave per stage: weights
-    constexpr int XI = MT;             //                                                          X rows
+    constexpr int WI = TNB / PR / 4;   // pieces per loader wave per stage: weights
+    constexpr int XI = MR / PR / 4;    //                                   X rows
     constexpr int GL = WI + XI;        // LDS-DMA instructions per loader wave per stage
-    constexpr int WCH = TNB * 4;       // 16-B chunks of a stage's weight image
-    constexpr int SCH = WCH + MR * 4;  // ... plus the X image
+    constexpr int WCH = TNB * RCH;     // 16-B chunks of a stage's weight image
+    constexpr int SCH = WCH + MR * RCH;  // ... plus the X image
+    constexpr int TST = tstages<MT, KC>();
+    static_assert(TST >= 2 && TST * SCH * 16 <= 160 * 1024, "LDS ring");
     __shared__ uint4 lds[TST * SCH];   // ONE shared array (cdna_hip_programming.md §5 item 4a)
 
     const int tid = threadIdx.x;
@@ -94,7 +124,7 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         mp = blockIdx.x % mparts;
     }
     const int nt = u % ntiles, s = u / ntiles;
-    const int chunks_all = K / TKC;
+    const int chunks_all = K / KC;
     const int cbeg = s * cps;
     const int chunks = min(chunks_all, cbeg + cps) - cbeg;  // > 0 (host contract)
     const int m_lo = mp * mrows;
@@ -116,26 +146,26 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             return n0 + r;
         }
     };
-    // LDS-DMA sources: lane L of a piece fills image row base + L / 4, slot
-    // L % 4 with logical chunk tslot(L % 4, row) (the swizzle is an involution)
+    // LDS-DMA sources: lane L of a piece fills image row base + L / RCH, slot
+    // L % RCH with logical chunk tslot(L % RCH, row) (an involution)
     const uint16_t* wsrc[WI];
     const uint16_t* xsrc[XI];
 #pragma unroll
     for (int i = 0; i < WI; ++i) {
-        const int r = (lw * WI + i) * 16 + (lane >> 2);
-        wsrc[i] = w + (size_t)wrow(r) * K + (size_t)cbeg * TKC + tslot(lane & 3, r) * 8;
+        const int r = (lw * WI + i) * PR + lane / RCH;
+        wsrc[i] = w + (size_t)wrow(r) * K + (size_t)cbeg * KC + tslot<KC>(lane % RCH, r) * 8;
     }
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
-        const int r = (lw * XI + i) * 16 + (lane >> 2);
-        xsrc[i] = x + (size_t)min(m_lo + r, M - 1) * K + (size_t)cbeg * TKC + tslot(lane & 3, r) * 8;
+        const int r = (lw * XI + i) * PR + lane / RCH;
+        xsrc[i] = x + (size_t)min(m_lo + r, M - 1) * K + (size_t)cbeg * KC + tslot<KC>(lane % RCH, r) * 8;
     }
     auto issue = [&](int c, int slot) {
         uint4* base = lds + slot * SCH;
 #pragma unroll
-        for (int i = 0; i < WI; ++i) tglds16(wsrc[i] + c * TKC, base + (lw * WI + i) * 64);
+        for (int i = 0; i < WI; ++i) tglds16(wsrc[i] + c * KC, base + (lw * WI + i) * 64);
 #pragma unroll
-        for (int i = 0; i < XI; ++i) tglds16(xsrc[i] + c * TKC, base + WCH + (lw * XI + i) * 64);
+        for (int i = 0; i < XI; ++i) tglds16(xsrc[i] + c * KC, base + WCH + (lw * XI + i) * 64);
     };
 
     f32x4_t acc[NF][MT];
@@ -144,79 +174,72 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int t = 0; t < MT; ++t) acc[f][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    // One 32-deep k step per stage: MT X fragments and NF weight fragments
-    // (this wave's 128 weight rows), NF x MT MFMAs.  The fragments of stage
-    // c + 1 are read into the second register set while stage c's MFMAs run
-    // (one barrier per stage, after the loaders' wait for stage c + 1): the
-    // LDS read latency and the LDS array time of a stage's reads (~320 cycles
-    // for 8 waves) no longer stand between a barrier and the first MFMA.
-    struct Frags {
-        bf16x8_t a[NF], b[MT];
-    };
-    auto read = [&](const uint4* st, Frags& F) {
+    // Per stage KC / 32 k steps of MT X fragments and NF weight fragments
+    // (this wave's 128 weight rows) and NF x MT MFMAs; the next k step's
+    // reads are threaded between the current one's MFMAs (pinned: the
+    // scheduler would sink each read to its use).
+    constexpr int KS = KC / 32;
+    auto compute = [&](const uint4* st) {
         const uint4* wl = st;
         const uint4* xl = st + WCH;
+        bf16x8_t a[KS][NF], b[KS][MT];
+        auto load = [&](int kk) {
 #pragma unroll
-        for (int t = 0; t < MT; ++t) {
-            const int r = mw + 16 * t + l16;
-            F.b[t] = as_bf16x8(xl[r * 4 + tslot(g, r)]);
+            for (int t = 0; t < MT; ++t) {
+                const int r = mw + 16 * t + l16;
+                b[kk][t] = as_bf16x8(xl[r * RCH + tslot<KC>(4 * kk + g, r)]);
+            }
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int r = 128 * wn + 16 * f + l16;
+                a[kk][f] = as_bf16x8(wl[r * RCH + tslot<KC>(4 * kk + g, r)]);
+            }
+        };
+        auto mma = [&](int kk) {
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+#pragma unroll
+                for (int t = 0; t < MT; ++t)
+                    acc[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][f], b[kk][t], acc[f][t], 0, 0, 0);
+        };
+        load(0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+            if (kk + 1 < KS) load(kk + 1);
+            mma(kk);
+            if (kk + 1 < KS) {
+                constexpr int NR = NF + MT, NM = NF * MT, RM = NM / NR > 0 ? NM / NR : 1;
+#pragma unroll
+                for (int i = 0; i < NR; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one DS read
+                    __builtin_amdgcn_sched_group_barrier(0x008, RM, 0);  // RM MFMAs
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);      // the rest
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
-#pragma unroll
-        for (int f = 0; f < NF; ++f) {
-            const int r = 128 * wn + 16 * f + l16;
-            F.a[f] = as_bf16x8(wl[r * 4 + tslot(g, r)]);
-        }
-    };
-    auto mma = [&](const Frags& F) {
-#pragma unroll
-        for (int f = 0; f < NF; ++f)
-#pragma unroll
-            for (int t = 0; t < MT; ++t)
-                acc[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F.a[f], F.b[t], acc[f][t], 0, 0, 0);
     };
 
-    // TST-stage ring.  Step c: a loader waits for its pieces of stage c + 1
-    // (counted vmcnt: stage c + 2 stays in flight), one raw barrier (stage
-    // c + 1 landed for every wave; every wave's MFMAs of stage c - 1 -- the
-    // last use of the slot about to be refilled -- issued, their reads done),
-    // the loaders refill that slot with stage c + 3, every wave reads stage
-    // c + 1 and runs stage c's MFMAs.  No __syncthreads() in the loop.
+    // TST-stage ring, TST - 1 stages in flight: a loader waits for its pieces
+    // of stage c (counted vmcnt: the newer stages stay in flight), one raw
+    // barrier (stage c landed for every wave; every wave done with stage
+    // c - 1, the slot about to be refilled), the loaders refill it with stage
+    // c + TST - 1, everyone computes stage c.  No __syncthreads() in the loop.
     if (loader) {
 #pragma unroll
         for (int j = 0; j < TST - 1; ++j)
             if (j < chunks) issue(j, j);
-        if ((PROBE & 1) != 0 || chunks == 1)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else if (chunks == 2)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(GL) : "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * GL) : "memory");
     }
-    asm volatile("s_barrier" ::: "memory");
-    auto step = [&](int c, const Frags& Fc, Frags& Fn) {
+    for (int c = 0; c < chunks; ++c) {
         if (loader) {
-            if ((PROBE & 1) != 0 || c + 2 >= chunks)
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            else
-                asm volatile("s_waitcnt vmcnt(%0)" ::"i"(GL) : "memory");
+            if constexpr ((PROBE & 1) != 0) wait_vm<GL>(0);
+            else wait_vm<GL>(min(TST - 2, chunks - 1 - c));
         }
         asm volatile("s_barrier" ::: "memory");
         if (loader && c + TST - 1 < chunks && (PROBE & 1) == 0) issue(c + TST - 1, (c + TST - 1) % TST);
-        if constexpr ((PROBE & 2) == 0) {
-            if (c + 1 < chunks) read(lds + ((c + 1) % TST) * SCH, Fn);
-            mma(Fc);
-        }
-    };
-    Frags F0, F1;
-    if constexpr ((PROBE & 2) == 0) read(lds, F0);
-    int c = 0;
-    // two steps per trip: the register sets swap roles by name, never by a
-    // runtime index (cdna_hip_programming.md §5.4 rule 20)
-    for (; c + 1 < chunks; c += 2) {
-        step(c, F0, F1);
-        step(c + 1, F1, F0);
+        if constexpr ((PROBE & 2) == 0) compute(lds + (c % TST) * SCH);
     }
-    if (c < chunks) step(c, F0, F1);
 
     // epilogue: lane (l16, g) holds Y[row m_lo + mw + 16t + l16][col c0 + 16f + 4g + i]
     // with c0 = 128 wn (SwiGLU: intermediate column n0h + 64 wn + 16f + 4g + i of f < NF / 2)
@@ -307,18 +330,18 @@ __global__ __launch_bounds__(kBlock) void tgemm_argmax_reduce_kernel(const float
     if (lane == 0) ids[m] = bi == 0x7fffffff ? 0 : bi;
 }
 
-template <int MODE, int PROBE = 0>
+template <int MODE, int PROBE = 0, int KC = TKC_DEFAULT>
 hipError_t launch_tgemm(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int M, int N, int K, int S,
                         int mparts, int I, hipStream_t st, const uint32_t* masks, const int32_t* midx, int n_masks,
                         int wwords) {
     const int ntiles = (MODE == TM_SWIGLU ? 2 * I : N) / TNB;
     const int mrows = (((M + mparts - 1) / mparts) + 15) & ~15;
     const int mt = (mrows + 63) / 64;
-    const int chunks = K / TKC;
+    const int chunks = K / KC;
     const int cps = (chunks + S - 1) / S;
     const dim3 grid((unsigned)(ntiles * S * mparts));
 #define DMCP_TG(MT)                                                                                                 \
-    tgemm_kernel<MT, MODE, PROBE><<<grid, TTH, 0, st>>>(x, w, y, part, M, N, K, cps, S, ntiles, mparts, mrows, I, masks, \
+    tgemm_kernel<MT, MODE, PROBE, KC><<<grid, TTH, 0, st>>>(x, w, y, part, M, N, K, cps, S, ntiles, mparts, mrows, I, masks, \
                                                     midx, n_masks, wwords)
     switch (mt) {
         case 1: DMCP_TG(1); break;
@@ -337,17 +360,17 @@ extern "C" {
 
 // Large-tile GEMM.
 //   mode 0: y[M, N] bf16 = x . w^T                              (S == 1)
-//   mode 1: part[S, M, N] fp32 partials over S K slices of ceil(K / 32 / S) stages
+//   mode 1: part[S, M, N] fp32 partials over S K slices of ceil(K / 64 / S) stages
 //   mode 2: y[M, I] bf16 = silu(x . w[:I]^T) * (x . w[I:]^T)     (w = [gate; up] [2I, K], S == 1)
 //   mode 3: ids[M] = masked argmax of bf16(x . w^T) (w [V = N, K]; part: float2 workspace of N / 128 * M pairs;
 //           masks [n_masks, wwords], midx [M]; S == 1)
-// Contract (checked by dmcp/ops/hip.py, guarded here): K % 32 == 0, N % 256 == 0 (mode 2: I % 128 == 0),
+// Contract (checked by dmcp/ops/hip.py, guarded here): K % 64 == 0, N % 256 == 0 (mode 2: I % 128 == 0),
 // rows per M part <= 256, every K slice non-empty.
 int dmcp_tgemm(const void* x, const void* w, void* y, void* part, int M, int N, int K, int S, int mparts, int mode,
                int I, const void* masks, const void* midx, int n_masks, int wwords, void* ids, void* stream) {
     if (M <= 0) return 0;
-    const int chunks = K / TKC;
-    if (!x || !w || S < 1 || mparts < 1 || K <= 0 || K % TKC != 0 || S > chunks ||
+    const int chunks = K / TKC_DEFAULT;
+    if (!x || !w || S < 1 || mparts < 1 || K <= 0 || K % TKC_DEFAULT != 0 || S > chunks ||
         (S - 1) * ((chunks + S - 1) / S) >= chunks || (((M + mparts - 1) / mparts + 15) & ~15) > 256 ||
         (mode == 1 && !part) || (mode != 1 && S != 1) || ((mode == 0 || mode == 2) && !y) ||
         (mode == 2 ? (I <= 0 || I % (TNB / 2) != 0) : (N <= 0 || N % TNB != 0)) ||
@@ -376,22 +399,30 @@ int dmcp_tgemm(const void* x, const void* w, void* y, void* part, int M, int N, 
     }
 }
 
-// diagnostics: mode-1 partials with kernel parts switched off (PROBE above)
+// diagnostics: mode-1 partials with kernel parts switched off (probe & 3:
+// PROBE above) and / or 32-deep stages (probe & 16: 64-B image rows)
 int dmcp_tgemm_probe(int probe, const void* x, const void* w, void* part, int M, int N, int K, int S, int mparts,
                      void* stream) {
-    const int chunks = K / TKC;
-    if (M <= 0 || !x || !w || !part || S < 1 || K % TKC != 0 || S > chunks ||
+    const int kc = (probe & 16) ? 32 : TKC_DEFAULT;
+    const int chunks = K / kc;
+    if (M <= 0 || !x || !w || !part || S < 1 || K % kc != 0 || S > chunks ||
         (S - 1) * ((chunks + S - 1) / S) >= chunks || N % TNB != 0 || (((M + mparts - 1) / mparts + 15) & ~15) > 256)
         return hipErrorInvalidValue;
     auto st = (hipStream_t)stream;
     auto xx = (const uint16_t*)x;
     auto ww = (const uint16_t*)w;
     auto pp = (float*)part;
-    if (probe == 1)
-        return launch_tgemm<TM_PART, 1>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
-    if (probe == 2)
-        return launch_tgemm<TM_PART, 2>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
-    return hipErrorInvalidValue;
+#define DMCP_TP(P, KC) \
+    return launch_tgemm<TM_PART, P, KC>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0)
+    switch (probe) {
+        case 1: DMCP_TP(1, 64);
+        case 2: DMCP_TP(2, 64);
+        case 16: DMCP_TP(0, 32);
+        case 17: DMCP_TP(1, 32);
+        case 18: DMCP_TP(2, 32);
+        default: return hipErrorInvalidValue;
+    }
+#undef DMCP_TP
 }
 
 }  // extern "C"

@@ -1160,8 +1160,11 @@ TGEMM_MAX_ROWS = 1024
 TGEMM_NB = 256
 
 
+TGEMM_KC = 64  # K per LDS stage of the kernel (split-K slices are whole stages)
+
+
 def tgemm_supported(N: int, K: int, swiglu: bool = False) -> bool:
-    return K % 32 == 0 and N % (2 * TGEMM_NB if swiglu else TGEMM_NB) == 0
+    return K % TGEMM_KC == 0 and N % (2 * TGEMM_NB if swiglu else TGEMM_NB) == 0
 
 
 def tgemm_plan(M: int, N: int, K: int, mode: str = "part", cus: int = 256) -> tuple:
@@ -1172,7 +1175,7 @@ def tgemm_plan(M: int, N: int, K: int, mode: str = "part", cus: int = 256) -> tu
     partials' round trip.  ``mode``: "part" (fp32 partials, any S), "bf16",
     "swiglu" and "argmax" (S = 1)."""
     tiles = N // TGEMM_NB
-    chunks = K // 32
+    chunks = K // TGEMM_KC
     best = None
     for mparts in sorted({-(-M // 256), -(-M // 192), -(-M // 128), -(-M // 256) + 1}):
         rows = (-(-M // mparts) + 15) // 16 * 16
@@ -1184,8 +1187,8 @@ def tgemm_plan(M: int, N: int, K: int, mode: str = "part", cus: int = 256) -> tu
             if S > chunks or (S - 1) * cps >= chunks:
                 continue
             blocks = tiles * mparts * S
-            mfma_us = cps * 16 * mt * 16 / 2100.0        # 16 x MT MFMAs of 16 cycles per stage, ~2.1 GHz
-            dma_us = cps * (TGEMM_NB + 64 * mt) * 64 / 45e3  # staged bytes at ~45 KB/us per CU
+            mfma_us = cps * 32 * mt * 16 / 2100.0        # 32 x MT MFMAs of 16 cycles per SIMD and stage, ~2.1 GHz
+            dma_us = cps * (TGEMM_NB + 64 * mt) * 128 / 45e3  # staged bytes at ~45 KB/us per CU
             us = -(-blocks // cus) * max(mfma_us, dma_us) + 0.6
             if mode == "part":
                 us += S * M * N * 8 / 5e6                   # partials written + read back (~5 TB/s)
@@ -1205,7 +1208,7 @@ def _tgemm_args(x: torch.Tensor, w: torch.Tensor, name: str, swiglu: bool = Fals
     M, K = x.shape
     N = w.shape[0]
     if not 1 <= M <= TGEMM_MAX_ROWS or not tgemm_supported(N, K, swiglu):
-        raise HipOpsError(f"{name}: needs 1 <= M <= {TGEMM_MAX_ROWS}, K % 32 == 0, N % {TGEMM_NB} == 0 "
+        raise HipOpsError(f"{name}: needs 1 <= M <= {TGEMM_MAX_ROWS}, K % {TGEMM_KC} == 0, N % {TGEMM_NB} == 0 "
                           f"(M={M} K={K} N={N})")
     return M, K, N
 
@@ -1247,7 +1250,7 @@ def tgemm_partials(x: torch.Tensor, w: torch.Tensor, workspace: torch.Tensor, sp
     M, K, N = _tgemm_args(x, w, "tgemm_partials")
     S, mp = tgemm_plan(M, N, K, "part")
     S, mparts = splits or S, mparts or mp
-    chunks = K // 32
+    chunks = K // TGEMM_KC
     if S > chunks or (S - 1) * -(-chunks // S) >= chunks:
         raise HipOpsError(f"tgemm_partials: K={K} does not split into {S} non-empty slices")
     _wgemm_ws(workspace, S * M * N, "tgemm_partials")

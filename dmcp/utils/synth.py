@@ -366,6 +366,59 @@ def go_gin_repo(root: str, n_packages: int = 6, module: str = "github.com/acme/g
     return pkgs
 
 
+def go_service_repo(root: str, n_packages: int = 250, module: str = "github.com/acme/gomono",
+                    commit: bool = True) -> List[str]:
+    """A large Go service (bench.py extra.goIndex, BASELINE config 5 at scale):
+    ``n_packages`` domain packages of 4 files each (types, repository,
+    service with a panic path, gin handlers) + cmd/server, every package
+    name unique, handlers registered from main."""
+    _write(os.path.join(root, "go.mod"), f"module {module}\n\ngo 1.22\n")
+    pkgs = []
+    names = []
+    for i in range(n_packages):
+        dom = _DOMAINS[i % len(_DOMAINS)] + str(i // len(_DOMAINS))
+        D = _cap(dom)
+        base = os.path.join(root, "internal", dom)
+        _write(os.path.join(base, "types.go"),
+               f"package {dom}\n\n// {D} is a domain record.\ntype {D} struct {{\n\tID   string `json:\"id\"`\n"
+               f"\tName string\n\tAmount int64\n}}\n\n// Store persists {dom} records.\ntype Store interface {{\n"
+               f"\tLoad(id string) (*{D}, error)\n\tSave(v *{D}) error\n}}\n")
+        _write(os.path.join(base, "repository.go"),
+               f'package {dom}\n\nimport "errors"\n\n// MemStore keeps {dom} records in memory.\n'
+               f"type MemStore struct{{ items map[string]*{D} }}\n\n"
+               f"// Load returns one record.\nfunc (m *MemStore) Load(id string) (*{D}, error) {{\n"
+               f"\tv, ok := m.items[id]\n\tif !ok {{\n\t\treturn nil, errors.New(\"not found\")\n\t}}\n\treturn v, nil\n}}\n\n"
+               f"// Save stores one record.\nfunc (m *MemStore) Save(v *{D}) error {{\n\tm.items[v.ID] = v\n\treturn nil\n}}\n")
+        dep = _DOMAINS[(i + 1) % len(_DOMAINS)] + str(((i + 1) % n_packages) // len(_DOMAINS))
+        imp = f'\n\t"{module}/internal/{dep}"' if i + 1 < n_packages else ""
+        use = f"\n\tvar _ *{dep}.{_cap(dep)}" if i + 1 < n_packages else ""
+        _write(os.path.join(base, "service.go"),
+               f'package {dom}\n\nimport (\n\t"context"{imp}\n)\n\n// Service implements the {dom} rules.\n'
+               f"type Service struct{{ store Store }}\n\n"
+               f"// Get loads one {dom}.\nfunc (s *Service) Get(ctx context.Context, id string) (*{D}, error) {{\n"
+               f"\tif s.store == nil {{\n\t\tpanic(\"uninitialized\")\n\t}}{use}\n\treturn s.store.Load(id)\n}}\n\n"
+               f"// Update changes the amount of a {dom}.\nfunc (s *Service) Update(ctx context.Context, id string, amount int64) error {{\n"
+               f"\tv, err := s.Get(ctx, id)\n\tif err != nil {{\n\t\treturn err\n\t}}\n\tv.Amount = amount\n"
+               f"\treturn s.store.Save(v)\n}}\n")
+        _write(os.path.join(base, "handler.go"),
+               f'package {dom}\n\nimport "github.com/gin-gonic/gin"\n\n// Handler serves {dom} over HTTP.\n'
+               f"type Handler struct{{ svc *Service }}\n\n// Get handles GET /{dom}/:id.\n"
+               f"func (h *Handler) Get(c *gin.Context) {{\n\t_, _ = h.svc.Get(c, c.Param(\"id\"))\n}}\n\n"
+               f"// Register wires the routes.\nfunc Register(r *gin.Engine, h *Handler) {{\n"
+               f'\tr.GET("/{dom}/:id", h.Get)\n}}\n')
+        pkgs.append(f"{module}/internal/{dom}")
+        names.append(dom)
+    imports = "\n".join(f'\t"{module}/internal/{d}"' for d in names[:50])
+    regs = "\n".join(f"\t{d}.Register(r, &{d}.Handler{{}})" for d in names[:50])
+    _write(os.path.join(root, "cmd", "server", "main.go"),
+           f'package main\n\nimport (\n\t"github.com/gin-gonic/gin"\n{imports}\n)\n\n'
+           f"func main() {{\n\tr := gin.Default()\n{regs}\n\t_ = r.Run()\n}}\n")
+    pkgs.append(f"{module}/cmd/server")
+    if commit:
+        _git_commit(root)
+    return pkgs
+
+
 def stack_trace_for(fqcns: List[str], frames: int = 20, seed: int = 11) -> List[dict]:
     """A plausible 20-frame Java stack trace over a synthetic repo."""
     rnd = random.Random(seed)

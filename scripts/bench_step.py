@@ -43,6 +43,8 @@ def main(argv=None) -> int:
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--fused", type=int, default=-1, help="-1 = model default, 0 = hipBLASLt, 1 = fused kernels")
     ap.add_argument("--wgemm", type=int, default=-1, help="-1 = model default, 0 = hipBLASLt for > 16 rows")
+    ap.add_argument("--tgemm", type=int, default=-1,
+                    help="-1 = model default, 0 = hipBLASLt (projections + LM head) for > 512 rows")
     ap.add_argument("--jitter", type=float, default=0.0,
                     help="per-sequence own length uniform in ctx x [1 - j, 1 + j] (the engine's mix of progress)")
     ap.add_argument("--adjacent", action="store_true",
@@ -64,6 +66,9 @@ def main(argv=None) -> int:
         model.fused_max_rows = 128 if a.fused else 0
     if a.wgemm >= 0:
         model.use_wgemm = bool(a.wgemm)
+    if a.tgemm == 0:
+        model.use_tgemm = False
+        model.tg_head_ws = None
     eng = LocalEngine(model)
     g = torch.Generator().manual_seed(0)
     if a.prefix:
@@ -116,6 +121,7 @@ def main(argv=None) -> int:
     w_bytes = 2 * (cfg.param_count() - cfg.vocab_size * cfg.hidden)
     print(json.dumps({"bench": "decode_step", "preset": a.preset, "kv_dtype": a.kv_dtype, "decode_dtype": a.decode_dtype, "rows": n, "batch": a.batch, "prefix": a.prefix,
                       "ctx": a.ctx, "jitter": a.jitter, "adjacent": a.adjacent, "fused": bool(getattr(model, "use_fused", False)),
+                      "tgemm": bool(getattr(model, "use_tgemm", False)),
                       "prefix_splits": hip.prefix_mfma_splits(a.batch + a.extra, cfg.n_heads // cfg.n_kv_heads,
                                                               cfg.n_kv_heads),
                       "device_ms": round(dev_ms, 3), "loop_ms": round(loop_ms, 3),

@@ -124,7 +124,7 @@ def main() -> int:
                 sw = {}
                 mps = sorted({-(-M // 256), -(-M // 192), -(-M // 128), -(-M // 256) + 1, mp0})
                 Ss = [1] if mode != "part" else sorted({1, 2, 3, 4, 6, 8, 10, 12, 16, S0})
-                chunks = K // 32
+                chunks = K // hip.TGEMM_KC
                 for mp in mps:
                     if (-(-M // mp) + 15) // 16 * 16 > 256:
                         continue
@@ -135,7 +135,7 @@ def main() -> int:
                 rec["sweep_us"] = sw
                 rec["sweep_best"] = min(sw.items(), key=lambda kv: kv[1])
             if a.probe and mode == "part":
-                for pr in (1, 2):
+                for pr in (1, 2, 16, 17, 18):
                     def probe(i, pr=pr):
                         hip._check(hip.lib().dmcp_tgemm_probe(pr, hip._ptr(x), hip._ptr(Ws[i]), hip._ptr(ws), M, N, K,
                                                               S0, mp0, hip._stream()), "dmcp_tgemm_probe")

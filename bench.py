@@ -105,6 +105,12 @@ def _spawn_enrich_pools(args):
         return {}
 
 
+def world_scale(ctx) -> float:
+    """Ranks whose engine statistics the local stats stand for (every rank
+    runs the same-sized project: whole-job token rate = local x world)."""
+    return float(ctx.world)
+
+
 def _enrich_local(pool, args, ctx, work, rank):
     """extra.enrichLocal: one warm-up analysis (hipGraph captures, allocator),
     then the timed analyze_project of a fresh repository, MAX over ranks."""
@@ -186,6 +192,8 @@ def _enrich_local(pool, args, ctx, work, rank):
                 "smallProject": small,
                 "promptTokensPerClass": round(st.get("prompt_tokens", 0) / max(1, st.get("prefills", 1)), 1),
                 "generatedTokensPerClass": round(st.get("generated_tokens", 0) / max(1, tot[0]), 1),
+                # shape-invariant: the reply caps grew this round (ReplyShape.from_budget)
+                "generatedTokensPerSec": round(st.get("generated_tokens", 0) * world_scale(ctx) / mx, 1),
                 "typeCorrections": int(st.get("type_corrections", 0)), "splitClasses": int(st.get("split_classes", 0)),
                 "methodsDropped": int(st.get("methods_dropped", 0)),
                 "classesAnalyzed": int(tot[1]), "elapsedS": round(mx, 3), "enrichFailed": r.stats.get("enrichFailed"),

@@ -49,12 +49,15 @@ def main(argv=None) -> int:
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--max-new-tokens", type=int, default=4096, help="reply budget (LOCAL_LLM_MAX_NEW_TOKENS)")
     ap.add_argument("--no-fork", action="store_true", help="methods decoded in sequence, not as branches")
+    ap.add_argument("--reply-shape", default="derived", choices=["derived", "legacy"],
+                    help="string caps / steps of the replies: derived from the reply budget (the service default, "
+                         "256 / 128 / 64 bytes, 4 steps at 4,096 tokens) or the round-4 fixed 96 / 64 / 40, 3")
     ap.add_argument("--fork-max-context", type=int, default=-1,
                     help="fork only classes with at most this many own prompt tokens (-1: the engine default)")
     args = ap.parse_args(argv)
 
     import torch
-    from dmcp.enrich.local import LocalEngine
+    from dmcp.enrich.local import LocalEngine, ReplyShape
     from dmcp.enrich.types import EnrichmentInput
     from dmcp.models.llm import LocalLM, preset
 
@@ -78,6 +81,7 @@ def main(argv=None) -> int:
                       shared_prefix=not args.no_shared_prefix, pipeline=not args.no_pipeline,
                       admit_min=args.admit_min or None, tokenizer=tok, max_new_tokens=args.max_new_tokens,
                       fork_methods=not args.no_fork,
+                      reply_shape=ReplyShape.LEGACY if args.reply_shape == "legacy" else None,
                       **({} if args.fork_max_context < 0 else {"fork_max_context": args.fork_max_context}))
     para = ("The shop platform sells products to retail customers. Orders move from CART to PAID to "
             "SHIPPED; payments are captured through the payment gateway and refunds are issued by the "
@@ -130,7 +134,8 @@ def main(argv=None) -> int:
             "config": {"model": cfg.name, "params_b": round(cfg.param_count() / 1e9, 3), "batch": args.batch,
                        "max_rows": cfg.max_rows, "kv_dtype": cfg.kv_dtype, "prefill_dtype": "fp8" if model.prefill_fp8 else "bf16", "decode_dtype": cfg.decode_dtype,
                        "max_seq": args.max_seq, "prompt_chars": args.prompt_chars,
-                       "readme_chars": args.readme_chars, "graphs": not args.no_graphs,
+                       "readme_chars": args.readme_chars, "graphs": not args.no_graphs, "reply_shape": [eng.reply_shape.desc, eng.reply_shape.method, eng.reply_shape.step,
+                                                                          eng.reply_shape.max_steps],
                        "jump_forward": not args.no_jump, "shared_prefix": not args.no_shared_prefix,
                        "pipeline": not args.no_pipeline},
             "shared_prefix_tokens": st["prefix_tokens"], "prefix_ms": round(1e3 * st["prefix_s"], 3),

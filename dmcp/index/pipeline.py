@@ -248,7 +248,7 @@ class Indexer:
                             recovered = self._recover_unenriched(project, parsed, graph, clone, readme,
                                                                  lease=lease)
                 lease.check()  # never publish over an operation that took the project over
-                with span("analyze.persist_graph", stats):
+                with span("analyze.persist_graph", stats):  # the graph JSON + the project row
                     project.base_package = common_package_prefix({package_name_of(i) for i in parsed.units})
                     project.update_graph_data(graph.to_json())
                     project.analysis_completed(clone.commit_hash)
@@ -261,10 +261,13 @@ class Indexer:
                     in_swap = writer.put_project_update(project)
                     if not writer.closed:
                         writer.close()
-                    with span("analyze.phase1_commit", stats):
-                        writer.wait()  # no-op when enrichment already waited
-                    for k, v in writer.timings.items():
-                        stats[f"analyze.writer_{k[:-3]}"] = v
+                # the row swap's writer thread (rows, then the commit) is the
+                # analysis' critical path: this is the main thread's wait for it
+                with span("analyze.phase1_commit", stats):
+                    writer.wait()  # no-op when enrichment already waited
+                for k, v in writer.timings.items():
+                    stats[f"analyze.writer_{k[:-3]}"] = v
+                with span("analyze.publish", stats):
                     if not in_swap:
                         self.repos.projects.update(project)
                     self.cache.put(project.id, project.name, graph, None if v0 is None else v0 + 1)
@@ -290,7 +293,8 @@ class Indexer:
             with span("analyze.cleanup", stats):
                 if clone is not None:
                     clone.cleanup()
-            lease.release()
+            with span("analyze.release", stats):  # the lease row's release (one write)
+                lease.release()
             lock.release()
 
     def _isolate(self, url: RepositoryUrl) -> Optional[float]:

@@ -300,19 +300,21 @@ class LocalLM:
         # 533-row step on hipBLASLt, profiles/kstats_llama_r4.txt)
         self.fused_head = self.device.type == "cuda" and ops.lm_head_supported(c.vocab_size, c.hidden)
         self.head_ws = ops.lm_head_workspace(c.vocab_size, self.device) if self.fused_head else None
-        # steps of WGEMM_MAX_ROWS < rows <= TGEMM_MAX_ROWS (the engine's
-        # jump-forward steps reach max_rows = 1.5 x max_batch): every
-        # projection on the large-tile GEMM (csrc/tgemm.hip) with the same
-        # fused consumers, and its LM head + masked argmax when V % 256 == 0
-        # -- no hipBLASLt GEMM in any decode step
-        self.use_tgemm = (self.device.type == "cuda" and self.max_rows > ops.WGEMM_MAX_ROWS
-                          and tgemm_shapes_ok(c) and self.max_rows <= ops.TGEMM_MAX_ROWS)
+        # the large-tile GEMM (csrc/tgemm.hip) with the same fused consumers:
+        # every projection of steps of WGEMM_MAX_ROWS < rows <= TGEMM_MAX_ROWS
+        # (the engine's jump-forward steps reach max_rows = 1.5 x max_batch),
+        # gate/up + down from TGEMM_MLP_MIN_ROWS rows and the LM head + masked
+        # argmax (V % 256 == 0) from TGEMM_HEAD_MIN_ROWS, where it beats the
+        # weight-streaming kernel (profiles/tgemm_vs_wgemm_r5.jsonl) -- no
+        # hipBLASLt GEMM in any decode step
+        self.use_tgemm = (self.device.type == "cuda" and tgemm_shapes_ok(c) and self.max_rows <= ops.TGEMM_MAX_ROWS
+                          and self.max_rows >= self.TGEMM_MLP_MIN_ROWS)
         self.tg_ws = (torch.empty(16 * self.max_rows * max(c.qkv_dim, c.hidden), dtype=torch.float32,
                                   device=self.device) if self.use_tgemm else None)
-        self.tg_head = self.fused_head and c.vocab_size % 256 == 0 and c.hidden % 64 == 0
-        self.tg_head_ws = (torch.empty(2 * (c.vocab_size // 128) * self.max_rows, dtype=torch.float32,
-                                       device=self.device) if self.tg_head and self.max_rows > ops.WGEMM_MAX_ROWS
-                           else None)
+        self.tg_head = (self.fused_head and c.vocab_size % 256 == 0 and c.hidden % 64 == 0
+                        and self.max_rows >= self.TGEMM_HEAD_MIN_ROWS and self.max_rows <= ops.TGEMM_MAX_ROWS)
+        self.tg_head_ws = (torch.empty(2 * (c.vocab_size // 64) * self.max_rows, dtype=torch.float32,
+                                       device=self.device) if self.tg_head else None)
         # fp8 prefill: e4m3 copies of the four projections (per-row scales),
         # quantised once; the batched prefill then runs on csrc/pgemm.hip
         # (the CPU references take any dims the 32-element blocks divide)
@@ -340,6 +342,14 @@ class LocalLM:
                     self.w8[f"l{i}.{n}"] = ops.quantize_weight(self.w[f"l{i}.{n}"])
 
     KV_HEADROOM = 4 << 30  # bytes left free next to the slab (graphs, workspaces, prefill activations)
+    # row counts from which the large-tile kernel takes over from the
+    # weight-streaming one: the LM head of 128,256 ids from 256 rows (155 vs
+    # 177 us, profiles/tgemm_vs_wgemm_r5.jsonl); the MLP only past 512 rows --
+    # alone gate/up + SwiGLU and down + norm ran faster on it from 448 rows,
+    # but the whole 512-row step was 3 % slower (same-box A/B,
+    # profiles/decode_step_tgemm_ab_r5.jsonl)
+    TGEMM_MLP_MIN_ROWS = 513
+    TGEMM_HEAD_MIN_ROWS = 256
 
     def _check_kv_fits(self, kv_shape) -> None:
         """The KV slab is the largest allocation of the service (tens of GB at
@@ -643,20 +653,14 @@ class LocalLM:
             return self._decode_trunk_fp8(B, resid, h, seq_len, slots, positions, chunk, splits, prefix_rows)
         wide = self.use_wgemm and B <= ops.WGEMM_MAX_ROWS
         big = self.use_tgemm and ops.WGEMM_MAX_ROWS < B <= ops.TGEMM_MAX_ROWS
+        mlp_t = self.use_tgemm and self.TGEMM_MLP_MIN_ROWS <= B <= ops.TGEMM_MAX_ROWS
         for i in range(c.layers):
             kc, vc = self.k_cache[i], self.v_cache[i]
             nxt = self.w[f"l{i + 1}.ln1"] if i + 1 < c.layers else self.w["norm_f"]
             if big:
                 q = ops.tgemm_rope_kv(h, self.w[f"l{i}.wqkv"], positions, slots, self.cos_sin, kc, vc, c.n_heads,
                                       self.tg_ws)
-                att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws,
-                                           chunk=chunk, fork=self.fork_tab, prefix=self._prefix(i, prefix_rows),
-                                           splits=splits).view(B, c.n_heads * c.head_dim)
-                h = ops.tgemm_resid_norm(att, self.w[f"l{i}.wo"], resid, self.w[f"l{i}.ln2"], c.eps, self.tg_ws)
-                act = ops.tgemm_swiglu(h, self.w[f"l{i}.wgu"])
-                h = ops.tgemm_resid_norm(act, self.w[f"l{i}.wdown"], resid, nxt, c.eps, self.tg_ws)
-                continue
-            if wide:
+            elif wide:
                 q = ops.wgemm_rope_kv(h, self.w[f"l{i}.wqkv"], positions, slots, self.cos_sin, kc, vc, c.n_heads,
                                       self.wgemm_ws)
             else:
@@ -664,15 +668,20 @@ class LocalLM:
             att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws, chunk=chunk,
                                        fork=self.fork_tab,
                                        prefix=self._prefix(i, prefix_rows), splits=splits).view(B, c.n_heads * c.head_dim)
-            if wide:
+            if big:
+                h = ops.tgemm_resid_norm(att, self.w[f"l{i}.wo"], resid, self.w[f"l{i}.ln2"], c.eps, self.tg_ws)
+            elif wide:
                 h = ops.wgemm_resid_norm(att, self.w[f"l{i}.wo"], resid, self.w[f"l{i}.ln2"], c.eps, self.wgemm_ws)
+            else:
+                h = ops.add_rmsnorm(F.linear(att, self.w[f"l{i}.wo"]), self.w[f"l{i}.ln2"], c.eps, residual=resid)
+            if mlp_t:
+                act = ops.tgemm_swiglu(h, self.w[f"l{i}.wgu"])
+                h = ops.tgemm_resid_norm(act, self.w[f"l{i}.wdown"], resid, nxt, c.eps, self.tg_ws)
+            elif wide:
                 act = ops.wgemm_swiglu(h, self.w[f"l{i}.wgu"])
                 h = ops.wgemm_resid_norm(act, self.w[f"l{i}.wdown"], resid, nxt, c.eps, self.wgemm_ws)
-                continue
-            o = F.linear(att, self.w[f"l{i}.wo"])
-            h = ops.add_rmsnorm(o, self.w[f"l{i}.ln2"], c.eps, residual=resid)
-            m = self._mlp(i, h)
-            h = ops.add_rmsnorm(m, nxt, c.eps, residual=resid)
+            else:
+                h = ops.add_rmsnorm(self._mlp(i, h), nxt, c.eps, residual=resid)
         return h
 
     def _decode_trunk_fp8(self, B, resid, h, seq_len, slots, positions, chunk, splits, prefix_rows) -> torch.Tensor:
@@ -872,7 +881,7 @@ class LocalLM:
             # kernel: no [B, vocab] logits (returned as None)
             h = self._decode_trunk(tokens, slots, positions, src, last_ids, mask_idx, mask_alt, alt_token,
                                    prefix_rows)
-            if self.tg_head_ws is not None and B > ops.WGEMM_MAX_ROWS:
+            if self.tg_head and B >= self.TGEMM_HEAD_MIN_ROWS:
                 ids = ops.tgemm_lm_head_argmax(h, self.w["lm_head"], masks, mask_idx, out=last_ids[:B],
                                                workspace=self.tg_head_ws)
             else:

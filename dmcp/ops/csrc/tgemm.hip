@@ -14,9 +14,11 @@
 //
 //   * a block owns 256 weight rows (SwiGLU: 128 gate + the 128 up rows of the
 //     same intermediate columns) x 64 MT activation rows (MT = 1..4), i.e. up
-//     to 256 x 256 outputs, over 8 waves (two per SIMD): 2 weight halves x 4
-//     M quarters, each 128 weight rows x 16 MT rows (8 A x MT B fragments,
-//     32 MT accumulators);
+//     to 256 x 256 outputs, over 8 waves (two per SIMD): 4 weight quarters x
+//     2 M halves, each 64 weight rows x 32 MT rows (4 A x 2 MT B fragments,
+//     32 MT accumulators) -- near-square wave tiles keep the LDS fragment
+//     reads (the CU's LDS array served ~90 % of its bandwidth to 128 x 32
+//     wave tiles' redundant reads) at (64 + 32 MT) rows per wave and k step;
 //   * waves 4-7 (one per SIMD) also issue the block's LDS-DMA: an LDS-DMA
 //     instruction holds its wave's issue for ~60-185 cycles
 //     (MI355X_MICROARCH.md, cycle constants), and with one wave per SIMD doing
@@ -32,7 +34,7 @@
 //     shorter) for the narrow projections; the fp32 partials are reduced by
 //     wgemm.hip's fused consumers (RoPE + KV append, residual + RMSNorm);
 //   * MODE_ARGMAX: the LM head + grammar-masked greedy selection (per block
-//     and row one (max, id) pair per 128 vocabulary ids, a per-row
+//     and row one (max, id) pair per 64 vocabulary ids, a per-row
 //     reduction kernel selects), no [M, V] logits.
 #include "dmcp_common.hpp"
 
@@ -42,9 +44,9 @@ namespace {
 // group) or 32 (64-B rows: each 128-B line is fetched twice, in two stages)
 constexpr int TKC_DEFAULT = 64;
 // ring stages: as many stages as fit the CU's 160 KiB of LDS (capped at 6)
-template <int MT, int KC>
+template <int MT, int KC, int CAP = 6>
 constexpr int tstages() {
-    return (160 * 1024) / ((256 + 64 * MT) * KC * 2) < 6 ? (160 * 1024) / ((256 + 64 * MT) * KC * 2) : 6;
+    return (160 * 1024) / ((256 + 64 * MT) * KC * 2) < CAP ? (160 * 1024) / ((256 + 64 * MT) * KC * 2) : CAP;
 }
 
 // s_waitcnt vmcnt(n * GL) for a runtime n in [0, 5] (the count is an immediate)
@@ -83,12 +85,13 @@ __device__ __forceinline__ int tslot(int j, int r) {
 // PROBE (dmcp_tgemm_probe only; diagnostics of scripts/bench_tgemm.py --probe):
 // 1 = the K loop issues no refill DMAs (MFMA + LDS reads + barriers on stale
 // stages), 2 = no fragment reads / MFMAs (the DMA ring alone)
-template <int MT, int MODE, int PROBE = 0, int KC = TKC_DEFAULT>
+template <int MT, int MODE, int PROBE = 0, int KC = TKC_DEFAULT, int CAP = 6>
 __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) void tgemm_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, float* __restrict__ part,
     int M, int N, int K, int cps, int S, int ntiles, int mparts, int mrows, int I, const uint32_t* __restrict__ masks,
     const int32_t* __restrict__ midx, int n_masks, int wwords) {
-    constexpr int NF = TNB / 32;       // A fragments per wave (16 weight rows each): half the tile's rows
+    constexpr int NF = TNB / 64;       // A fragments per wave (16 weight rows each): a quarter of the tile's rows
+    constexpr int XT = 2 * MT;         // B fragments per wave (16 X rows each): half the tile's rows
     constexpr int RCH = KC / 8;        // 16-B chunks per image row
     constexpr int PR = 64 / RCH;       // image rows per 1-KiB LDS-DMA piece
     constexpr int MR = 64 * MT;        // staged X rows
@@ -97,7 +100,7 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     constexpr int GL = WI + XI;        // LDS-DMA instructions per loader wave per stage
     constexpr int WCH = TNB * RCH;     // 16-B chunks of a stage's weight image
     constexpr int SCH = WCH + MR * RCH;  // ... plus the X image
-    constexpr int TST = tstages<MT, KC>();
+    constexpr int TST = tstages<MT, KC, CAP>();
     static_assert(TST >= 2 && TST * SCH * 16 <= 160 * 1024, "LDS ring");
     __shared__ uint4 lds[TST * SCH];   // ONE shared array (cdna_hip_programming.md §5 item 4a)
 
@@ -109,7 +112,7 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // DMA issue its SIMD partner keeps the matrix core busy
     const bool loader = wv >= 4;
     const int lw = wv & 3;                 // loader index
-    const int wn = wv & 1, wm = wv >> 1;   // weight half (128 rows) x M quarter (16 MT rows)
+    const int wn = wv & 3, wm = wv >> 2;   // weight quarter (64 rows) x M half (32 MT rows)
     const int l16 = lane & 15, g = lane >> 4;
     // block -> (weight tile nt, K slice s, M part mp): the M parts of one
     // (nt, s) unit share blockIdx % 8 (one XCD) and consecutive dispatch slots
@@ -129,19 +132,19 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int chunks = min(chunks_all, cbeg + cps) - cbeg;  // > 0 (host contract)
     const int m_lo = mp * mrows;
     const int m_hi = min(M, m_lo + mrows);
-    const int mw = wm * (MT * 16);
+    const int mw = wm * (XT * 16);
     int mtv = (m_hi - m_lo - mw + 15) / 16;  // valid 16-row tiles of this wave (wave-uniform)
-    mtv = max(0, min(MT, mtv));
+    mtv = max(0, min(XT, mtv));
 
     const int n0 = nt * TNB;
     const int n0h = nt * (TNB / 2);
-    // weight row of image row r.  SwiGLU: each 128-row half holds 64 gate rows
-    // then the 64 up rows of the same intermediate columns, so a wave's gate
-    // fragment f and up fragment f + NF / 2 meet in one lane
+    // weight row of image row r.  SwiGLU: each 64-row quarter holds 32 gate
+    // rows then the 32 up rows of the same intermediate columns, so a wave's
+    // gate fragment f and up fragment f + NF / 2 meet in one lane
     auto wrow = [&](int r) -> int {
         if constexpr (MODE == TM_SWIGLU) {
-            const int h = r >> 7, i = r & 127;
-            return (i < 64 ? 0 : I) + n0h + 64 * h + (i & 63);
+            const int h = r >> 6, i = r & 63;
+            return (i < 32 ? 0 : I) + n0h + 32 * h + (i & 31);
         } else {
             return n0 + r;
         }
@@ -168,11 +171,11 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int i = 0; i < XI; ++i) tglds16(xsrc[i] + c * KC, base + WCH + (lw * XI + i) * 64);
     };
 
-    f32x4_t acc[NF][MT];
+    f32x4_t acc[NF][XT];
 #pragma unroll
     for (int f = 0; f < NF; ++f)
 #pragma unroll
-        for (int t = 0; t < MT; ++t) acc[f][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < XT; ++t) acc[f][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
     // Per stage KC / 32 k steps of MT X fragments and NF weight fragments
     // (this wave's 128 weight rows) and NF x MT MFMAs; the next k step's
@@ -182,16 +185,16 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     auto compute = [&](const uint4* st) {
         const uint4* wl = st;
         const uint4* xl = st + WCH;
-        bf16x8_t a[KS][NF], b[KS][MT];
+        bf16x8_t a[KS][NF], b[KS][XT];
         auto load = [&](int kk) {
 #pragma unroll
-            for (int t = 0; t < MT; ++t) {
+            for (int t = 0; t < XT; ++t) {
                 const int r = mw + 16 * t + l16;
                 b[kk][t] = as_bf16x8(xl[r * RCH + tslot<KC>(4 * kk + g, r)]);
             }
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
-                const int r = 128 * wn + 16 * f + l16;
+                const int r = 64 * wn + 16 * f + l16;
                 a[kk][f] = as_bf16x8(wl[r * RCH + tslot<KC>(4 * kk + g, r)]);
             }
         };
@@ -199,7 +202,7 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
             for (int f = 0; f < NF; ++f)
 #pragma unroll
-                for (int t = 0; t < MT; ++t)
+                for (int t = 0; t < XT; ++t)
                     acc[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][f], b[kk][t], acc[f][t], 0, 0, 0);
         };
         load(0);
@@ -209,7 +212,7 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             if (kk + 1 < KS) load(kk + 1);
             mma(kk);
             if (kk + 1 < KS) {
-                constexpr int NR = NF + MT, NM = NF * MT, RM = NM / NR > 0 ? NM / NR : 1;
+                constexpr int NR = NF + XT, NM = NF * XT, RM = NM / NR > 0 ? NM / NR : 1;
 #pragma unroll
                 for (int i = 0; i < NR; ++i) {
                     __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one DS read
@@ -242,10 +245,10 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
 
     // epilogue: lane (l16, g) holds Y[row m_lo + mw + 16t + l16][col c0 + 16f + 4g + i]
-    // with c0 = 128 wn (SwiGLU: intermediate column n0h + 64 wn + 16f + 4g + i of f < NF / 2)
-    const int c0 = n0 + 128 * wn;
+    // with c0 = n0 + 64 wn (SwiGLU: intermediate column n0h + 32 wn + 16f + 4g + i of f < NF / 2)
+    const int c0 = n0 + 64 * wn;
 #pragma unroll
-    for (int t = 0; t < MT; ++t) {
+    for (int t = 0; t < XT; ++t) {
         if (t >= mtv) continue;
         const int m = m_lo + mw + 16 * t + l16;
         if constexpr (MODE == TM_ARGMAX) {
@@ -274,9 +277,9 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 const int oi = __shfl_xor(bi, msk, kWave);
                 if (ob > bv || (ob == bv && oi < bi)) { bv = ob; bi = oi; }
             }
-            // one (max, id) pair per 128-id half tile and row
+            // one (max, id) pair per 64-id quarter tile and row
             if (m < m_hi && g == 0)
-                reinterpret_cast<float2*>(part)[(size_t)(2 * nt + wn) * M + m] = make_float2(bv, __int_as_float(bi));
+                reinterpret_cast<float2*>(part)[(size_t)(4 * nt + wn) * M + m] = make_float2(bv, __int_as_float(bi));
             continue;
         }
         if (m >= m_hi) continue;
@@ -289,7 +292,7 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                     const float gg = bf2f(f2bf(acc[f][t][i])), uu = bf2f(f2bf(acc[f + NF / 2][t][i]));
                     o[i] = tsilu(gg) * uu;
                 }
-                *reinterpret_cast<uint2*>(y + (size_t)m * I + n0h + 64 * wn + 16 * f + 4 * g) = pack4(o);
+                *reinterpret_cast<uint2*>(y + (size_t)m * I + n0h + 32 * wn + 16 * f + 4 * g) = pack4(o);
             }
         } else if constexpr (MODE == TM_PART) {
             float* dst = part + ((size_t)s * M + m) * N + c0 + 4 * g;
@@ -307,7 +310,7 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
 }
 
-// per row: the (max, id) pairs of every 128-id vocabulary half tile -> the selected
+// per row: the (max, id) pairs of every 64-id vocabulary quarter tile -> the selected
 // id (0 when the mask allows nothing, as masked_argmax); one wave per row
 __global__ __launch_bounds__(kBlock) void tgemm_argmax_reduce_kernel(const float2* __restrict__ best, int ntiles,
                                                                      int M, int32_t* __restrict__ ids) {
@@ -330,7 +333,7 @@ __global__ __launch_bounds__(kBlock) void tgemm_argmax_reduce_kernel(const float
     if (lane == 0) ids[m] = bi == 0x7fffffff ? 0 : bi;
 }
 
-template <int MODE, int PROBE = 0, int KC = TKC_DEFAULT>
+template <int MODE, int PROBE = 0, int KC = TKC_DEFAULT, int CAP = 6>
 hipError_t launch_tgemm(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int M, int N, int K, int S,
                         int mparts, int I, hipStream_t st, const uint32_t* masks, const int32_t* midx, int n_masks,
                         int wwords) {
@@ -341,7 +344,7 @@ hipError_t launch_tgemm(const uint16_t* x, const uint16_t* w, uint16_t* y, float
     const int cps = (chunks + S - 1) / S;
     const dim3 grid((unsigned)(ntiles * S * mparts));
 #define DMCP_TG(MT)                                                                                                 \
-    tgemm_kernel<MT, MODE, PROBE, KC><<<grid, TTH, 0, st>>>(x, w, y, part, M, N, K, cps, S, ntiles, mparts, mrows, I, masks, \
+    tgemm_kernel<MT, MODE, PROBE, KC, CAP><<<grid, TTH, 0, st>>>(x, w, y, part, M, N, K, cps, S, ntiles, mparts, mrows, I, masks, \
                                                     midx, n_masks, wwords)
     switch (mt) {
         case 1: DMCP_TG(1); break;
@@ -362,7 +365,7 @@ extern "C" {
 //   mode 0: y[M, N] bf16 = x . w^T                              (S == 1)
 //   mode 1: part[S, M, N] fp32 partials over S K slices of ceil(K / 64 / S) stages
 //   mode 2: y[M, I] bf16 = silu(x . w[:I]^T) * (x . w[I:]^T)     (w = [gate; up] [2I, K], S == 1)
-//   mode 3: ids[M] = masked argmax of bf16(x . w^T) (w [V = N, K]; part: float2 workspace of N / 128 * M pairs;
+//   mode 3: ids[M] = masked argmax of bf16(x . w^T) (w [V = N, K]; part: float2 workspace of N / 64 * M pairs;
 //           masks [n_masks, wwords], midx [M]; S == 1)
 // Contract (checked by dmcp/ops/hip.py, guarded here): K % 64 == 0, N % 256 == 0 (mode 2: I % 128 == 0),
 // rows per M part <= 256, every K slice non-empty.
@@ -392,7 +395,7 @@ int dmcp_tgemm(const void* x, const void* w, void* y, void* part, int M, int N, 
                                                    wwords);
             if (e != hipSuccess) return e;
             tgemm_argmax_reduce_kernel<<<(M + kBlock / kWave - 1) / (kBlock / kWave), kBlock, 0, st>>>(
-                (const float2*)part, 2 * (N / TNB), M, (int32_t*)ids);
+                (const float2*)part, 4 * (N / TNB), M, (int32_t*)ids);
             return hipGetLastError();
         }
         default: return hipErrorInvalidValue;
@@ -400,7 +403,8 @@ int dmcp_tgemm(const void* x, const void* w, void* y, void* part, int M, int N, 
 }
 
 // diagnostics: mode-1 partials with kernel parts switched off (probe & 3:
-// PROBE above) and / or 32-deep stages (probe & 16: 64-B image rows)
+// PROBE above), 32-deep stages (probe & 16: 64-B image rows), a 2-stage
+// ring (probe & 32)
 int dmcp_tgemm_probe(int probe, const void* x, const void* w, void* part, int M, int N, int K, int S, int mparts,
                      void* stream) {
     const int kc = (probe & 16) ? 32 : TKC_DEFAULT;
@@ -412,14 +416,16 @@ int dmcp_tgemm_probe(int probe, const void* x, const void* w, void* part, int M,
     auto xx = (const uint16_t*)x;
     auto ww = (const uint16_t*)w;
     auto pp = (float*)part;
-#define DMCP_TP(P, KC) \
-    return launch_tgemm<TM_PART, P, KC>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0)
+#define DMCP_TP(P, KC, CAP) \
+    return launch_tgemm<TM_PART, P, KC, CAP>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0)
     switch (probe) {
-        case 1: DMCP_TP(1, 64);
-        case 2: DMCP_TP(2, 64);
-        case 16: DMCP_TP(0, 32);
-        case 17: DMCP_TP(1, 32);
-        case 18: DMCP_TP(2, 32);
+        case 1: DMCP_TP(1, 64, 6);
+        case 2: DMCP_TP(2, 64, 6);
+        case 16: DMCP_TP(0, 32, 6);
+        case 17: DMCP_TP(1, 32, 6);
+        case 18: DMCP_TP(2, 32, 6);
+        case 32: DMCP_TP(0, 64, 2);   // ring capped at 2 stages (1 in flight)
+        case 34: DMCP_TP(2, 64, 2);
         default: return hipErrorInvalidValue;
     }
 #undef DMCP_TP

@@ -1169,15 +1169,22 @@ def tgemm_supported(N: int, K: int, swiglu: bool = False) -> bool:
 
 def tgemm_plan(M: int, N: int, K: int, mode: str = "part", cus: int = 256) -> tuple:
     """(K slices S, M parts) of the large-tile GEMM.  M parts of <= 256 rows
-    (a part is staged rounded up to 64 rows); the plan minimises a per-CU
-    time model over the part counts and slice counts: waves of blocks x
-    max(MFMA time, staged bytes at the per-CU LDS-DMA rate) + the split-K
-    partials' round trip.  ``mode``: "part" (fp32 partials, any S), "bf16",
+    (a part is staged rounded up to 64 rows); the plan minimises a time model
+    fitted to the fused ops' (GEMM + reduction) measured (S, parts) sweeps at
+    520-1,024 rows (profiles/tgemm_fused_sweep_r5.jsonl; mean error 10 %, the
+    chosen plans within 0.7 us of the best over 12 shape x row cases): waves
+    of blocks x max(MFMA time x 1.5, staged bytes at ~60 KB/us per CU) + 5 us +
+    0.5 us per MB of fp32 split-K partials (written here, read back by the
+    fused reduction).  ``mode``: "part" (fp32 partials, any S), "bf16",
     "swiglu" and "argmax" (S = 1)."""
     tiles = N // TGEMM_NB
     chunks = K // TGEMM_KC
+    if mode == "argmax":  # measured best at 256-1,024 rows: the fewest parts
+        return 1, -(-M // 256)
+    if mode == "swiglu":  # measured best: 3 parts up to ~520 rows, then 4 (64 x 4 = 256 blocks: one wave)
+        return 1, max(-(-M // 256), 3 if M <= 520 else 4)
     best = None
-    for mparts in sorted({-(-M // 256), -(-M // 192), -(-M // 128), -(-M // 256) + 1}):
+    for mparts in sorted({-(-M // r) for r in (256, 192, 128, 96, 64)}):
         rows = (-(-M // mparts) + 15) // 16 * 16
         if rows > 256:
             continue
@@ -1187,11 +1194,11 @@ def tgemm_plan(M: int, N: int, K: int, mode: str = "part", cus: int = 256) -> tu
             if S > chunks or (S - 1) * cps >= chunks:
                 continue
             blocks = tiles * mparts * S
-            mfma_us = cps * 32 * mt * 16 / 2100.0        # 32 x MT MFMAs of 16 cycles per SIMD and stage, ~2.1 GHz
-            dma_us = cps * (TGEMM_NB + 64 * mt) * 128 / 45e3  # staged bytes at ~45 KB/us per CU
-            us = -(-blocks // cus) * max(mfma_us, dma_us) + 0.6
+            mfma_us = 1.5 * cps * 2 * 8 * mt * 2 * 16 / 2100.0  # 2 waves x 8 x MT x 2 k steps of 16 cycles per SIMD
+            dma_us = cps * (TGEMM_NB + 64 * mt) * 2 * TGEMM_KC / 60e3
+            us = -(-blocks // cus) * max(mfma_us, dma_us) + 5.0
             if mode == "part":
-                us += S * M * N * 8 / 5e6                   # partials written + read back (~5 TB/s)
+                us += S * M * N * 4 * 0.5e-6
             key = (round(us, 2), -blocks)
             if best is None or key < best[0]:
                 best = (key, S, mparts)
@@ -1315,7 +1322,7 @@ def tgemm_lm_head_argmax(x: torch.Tensor, w: torch.Tensor, masks: torch.Tensor, 
     if out is None:
         out = torch.empty(M, dtype=torch.int32, device=x.device)
     _req_out(out, torch.int32, M, "tgemm_lm_head_argmax.out")
-    need = 2 * (V // 128) * M  # one (max, id) pair per 128-id half tile and row
+    need = 2 * (V // 64) * M  # one (max, id) pair per 64-id quarter tile and row
     if workspace is None:
         workspace = torch.empty(need, dtype=torch.float32, device=x.device)
     if workspace.dtype != torch.float32 or workspace.numel() < need:

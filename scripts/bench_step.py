@@ -43,6 +43,7 @@ def main(argv=None) -> int:
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--fused", type=int, default=-1, help="-1 = model default, 0 = hipBLASLt, 1 = fused kernels")
     ap.add_argument("--wgemm", type=int, default=-1, help="-1 = model default, 0 = hipBLASLt for > 16 rows")
+    ap.add_argument("--tghead", type=int, default=-1, help="0 = the weight-streaming LM head at every row count")
     ap.add_argument("--tgemm", type=int, default=-1,
                     help="-1 = model default, 0 = hipBLASLt (projections + LM head) for > 512 rows")
     ap.add_argument("--jitter", type=float, default=0.0,
@@ -68,7 +69,9 @@ def main(argv=None) -> int:
         model.use_wgemm = bool(a.wgemm)
     if a.tgemm == 0:
         model.use_tgemm = False
-        model.tg_head_ws = None
+        model.tg_head = False
+    if a.tghead == 0:
+        model.tg_head = False
     eng = LocalEngine(model)
     g = torch.Generator().manual_seed(0)
     if a.prefix:
@@ -122,6 +125,7 @@ def main(argv=None) -> int:
     print(json.dumps({"bench": "decode_step", "preset": a.preset, "kv_dtype": a.kv_dtype, "decode_dtype": a.decode_dtype, "rows": n, "batch": a.batch, "prefix": a.prefix,
                       "ctx": a.ctx, "jitter": a.jitter, "adjacent": a.adjacent, "fused": bool(getattr(model, "use_fused", False)),
                       "tgemm": bool(getattr(model, "use_tgemm", False)),
+                      "tg_head": bool(getattr(model, "tg_head", False)),
                       "prefix_splits": hip.prefix_mfma_splits(a.batch + a.extra, cfg.n_heads // cfg.n_kv_heads,
                                                               cfg.n_kv_heads),
                       "device_ms": round(dev_ms, 3), "loop_ms": round(loop_ms, 3),

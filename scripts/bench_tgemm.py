@@ -57,7 +57,10 @@ def main() -> int:
     ap.add_argument("--reps", type=int, default=24)
     ap.add_argument("--sweep", action="store_true", help="also time every (S, mparts) around the plan")
     ap.add_argument("--only", default="", help="comma list of projections (qkv,o,gu,down,head)")
+    ap.add_argument("--fused-sweep", action="store_true",
+                    help="sweep (S, mparts) of the FUSED op (GEMM + its reduction) for qkv / o / down")
     ap.add_argument("--copies", type=int, default=0, help="weight copies (default: enough to exceed 640 MB)")
+    ap.add_argument("--probes", type=int, nargs="+", default=[1, 2, 16, 17, 18, 32, 34])
     ap.add_argument("--probe", action="store_true", help="also time the partials kernel without refill DMAs "
                     "(probe 1) and without compute (probe 2)")
     a = ap.parse_args()
@@ -135,7 +138,7 @@ def main() -> int:
                 rec["sweep_us"] = sw
                 rec["sweep_best"] = min(sw.items(), key=lambda kv: kv[1])
             if a.probe and mode == "part":
-                for pr in (1, 2, 16, 17, 18):
+                for pr in a.probes:
                     def probe(i, pr=pr):
                         hip._check(hip.lib().dmcp_tgemm_probe(pr, hip._ptr(x), hip._ptr(Ws[i]), hip._ptr(ws), M, N, K,
                                                               S0, mp0, hip._stream()), "dmcp_tgemm_probe")
@@ -148,6 +151,7 @@ def main() -> int:
                                                                                   residual=resid), a.reps, copies) * 1e3, 2)
                 rec["fused_us"] = round(graph_ms(lambda i: hip.tgemm_resid_norm(x, Ws[i], resid, nw, 1e-5, ws),
                                                  a.reps, copies) * 1e3, 2)
+                ho = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
             elif name == "qkv":
                 Hkv, D = c.n_kv_heads, c.head_dim
                 kc = torch.zeros((8, Hkv, 2048, D), dtype=torch.uint8, device=dev)
@@ -159,6 +163,44 @@ def main() -> int:
                                                                             c.n_heads), a.reps, copies) * 1e3, 2)
                 rec["fused_us"] = round(graph_ms(lambda i: hip.tgemm_rope_kv(x, Ws[i], pos, sl, cs, kc, vc, c.n_heads,
                                                                              ws), a.reps, copies) * 1e3, 2)
+                qo = torch.empty(M, c.n_heads, D, device=dev, dtype=torch.bfloat16)
+            if M <= hip.WGEMM_MAX_ROWS and name != "head":  # the weight-streaming kernel's fused op
+                wws = hip.wgemm_workspace(M, max(Q, H), dev)
+                if name == "gu":
+                    rec["wg_fused_us"] = round(graph_ms(lambda i: hip.wgemm_swiglu(x, Ws[i]), a.reps, copies) * 1e3, 2)
+                elif name == "qkv":
+                    rec["wg_fused_us"] = round(graph_ms(lambda i: hip.wgemm_rope_kv(x, Ws[i], pos, sl, cs, kc, vc,
+                                                                                    c.n_heads, wws),
+                                                        a.reps, copies) * 1e3, 2)
+                else:
+                    rec["wg_fused_us"] = round(graph_ms(lambda i: hip.wgemm_resid_norm(x, Ws[i], resid, nw, 1e-5, wws),
+                                                        a.reps, copies) * 1e3, 2)
+            elif M <= hip.WGEMM_MAX_ROWS and hip.lm_head_supported(N, K):
+                rec["wg_fused_us"] = round(graph_ms(lambda i: hip.lm_head_argmax(x, Ws[i], masks, midx), a.reps,
+                                                    copies) * 1e3, 2)
+            if a.fused_sweep and name in ("qkv", "o", "down"):
+                fsw = {}
+                chunks = K // hip.TGEMM_KC
+                for mp in sorted({-(-M // 256), -(-M // 192), -(-M // 128), -(-M // 96), -(-M // 64)}):
+                    if (-(-M // mp) + 15) // 16 * 16 > 256:
+                        continue
+                    for S in (1, 2, 3, 4, 5, 6, 8, 10, 12):
+                        if S > chunks or (S - 1) * -(-chunks // S) >= chunks:
+                            continue
+                        if name == "qkv":
+                            f = lambda i, S=S, mp=mp: (hip.tgemm_partials(x, Ws[i], ws, splits=S, mparts=mp),  # noqa
+                                                       hip._check(hip.lib().dmcp_reduce_rope_kv(
+                                                           hip._ptr(ws), S, hip._ptr(pos), hip._ptr(sl), hip._ptr(cs),
+                                                           hip._ptr(qo), hip._ptr(kc), hip._ptr(vc), M, c.n_heads, Hkv,
+                                                           D, 2048, cs.shape[0], 8, 1, hip._stream()), "reduce"))
+                        else:
+                            f = lambda i, S=S, mp=mp: (hip.tgemm_partials(x, Ws[i], ws, splits=S, mparts=mp),  # noqa
+                                                       hip._check(hip.lib().dmcp_reduce_resid_norm(
+                                                           hip._ptr(ws), S, hip._ptr(resid), hip._ptr(nw), hip._ptr(ho),
+                                                           M, N, 1e-5, hip._stream()), "reduce"))
+                        fsw[f"S{S}_mp{mp}"] = round(graph_ms(f, a.reps, copies) * 1e3, 2)
+                rec["fused_sweep_us"] = fsw
+                rec["fused_sweep_best"] = min(fsw.items(), key=lambda kv: kv[1])
             rec["tgemm_pflops"] = round(flops / (rec["tgemm_us"] * 1e-6) / 1e15, 3)
             rec["blas_pflops"] = round(flops / (rec["blas_us"] * 1e-6) / 1e15, 3)
             print(json.dumps(rec), flush=True)

@@ -64,6 +64,7 @@ __device__ __forceinline__ void wait_vm(int n) {
 constexpr int TNB = 256;  // weight rows per block
 constexpr int TTH = 512;  // threads per block: 8 waves, two per SIMD
 constexpr int TM_BF16 = 0, TM_PART = 1, TM_SWIGLU = 2, TM_ARGMAX = 3;
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float tsilu(float g) { return g / (1.f + __expf(-g)); }
 
@@ -310,6 +311,214 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
 }
 
+// s_waitcnt vmcnt(n) for a runtime n in [0, 23] (larger n: vmcnt(23), stricter)
+constexpr int kVmMax = 23;
+__device__ __forceinline__ void wait_vm_rt(int n) {
+    switch (n) {
+#define DMCP_VMC(i) case i: asm volatile("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
+        DMCP_VMC(0) DMCP_VMC(1) DMCP_VMC(2) DMCP_VMC(3) DMCP_VMC(4) DMCP_VMC(5) DMCP_VMC(6) DMCP_VMC(7)
+        DMCP_VMC(8) DMCP_VMC(9) DMCP_VMC(10) DMCP_VMC(11) DMCP_VMC(12) DMCP_VMC(13) DMCP_VMC(14) DMCP_VMC(15)
+        DMCP_VMC(16) DMCP_VMC(17) DMCP_VMC(18) DMCP_VMC(19) DMCP_VMC(20) DMCP_VMC(21) DMCP_VMC(22)
+#undef DMCP_VMC
+        default: asm volatile("s_waitcnt vmcnt(23)" ::: "memory"); break;
+    }
+}
+
+// Register-weight variant (diagnostic: dmcp_tgemm_probe 64-66 / 129-130
+// only).  MEASURED SLOWER and not used: 1.2-1.4x tgemm_kernel's time at
+// 610-1,024 rows on every projection; its weight loads alone (probe 66)
+// take 1.6-1.75x the LDS-DMA ring alone (probe 2) for the same bytes
+// (profiles/tgemm_regweights_ab_r5.jsonl) -- consistent with
+// MI355X_MICROARCH.md's gather table (register staging and LDS-DMA read
+// at the same per-CU rate): the two paths share one per-CU ingest, and
+// the MFMA operand layout's 16 rows x 64 B per load instruction costs
+// more than the DMA's 8 rows x 128 B pieces.  The design, for the record:
+//
+// tgemm_kernel's probes put it at the CU's LDS-DMA ingest (~60 KB/us per CU:
+// DMA alone ~ the whole kernel; MI355X_MICROARCH.md's ring-gemm measured 68
+// GB/s per CU for the same path), with half of the staged bytes weights that
+// one wave per M half reads back.  Here each of the 8 waves owns 32 weight
+// rows (2 A fragments) x every staged X row (4 MT B fragments) and loads its
+// weight fragments straight into VGPRs with plain 16-B global loads in the
+// MFMA operand layout (lane (l16, g): row l16, k chunk g of the k step; 16
+// rows x 64 contiguous bytes per instruction), D stages ahead in a rotating
+// register ring; only the X rows go through the LDS-DMA ring, issued by all
+// 8 waves.  Two memory paths per CU instead of one, and half the LDS-DMA.
+// The K loop is branch-free (a guarded MFMA or DMA would leave the
+// compiler's wait insertion a join where it falls back to vmcnt(0), which
+// drains the register ring).
+//
+// Per stage c every wave: counted vmcnt (its X pieces and weight loads of
+// stage c landed; everything newer stays in flight), raw barrier (every
+// wave's pieces of stage c landed, every wave done with stage c - 1), X
+// pieces of stage c + TST - 1 into the freed slot, weights of stage c + D
+// into register buffer (c + D) % (D + 1), then compute stage c.
+template <int MT, int MODE, int PROBE = 0, int D = 3, int KC = TKC_DEFAULT, int CAP = 6>
+__global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) void tgemm_r_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, float* __restrict__ part,
+    int M, int N, int K, int cps, int S, int ntiles, int mparts, int mrows, int I, const uint32_t* __restrict__ masks,
+    const int32_t* __restrict__ midx, int n_masks, int wwords) {
+    constexpr int NF = 2;               // A fragments per wave: 32 weight rows
+    constexpr int XT = 4 * MT;          // B fragments per wave: every staged X row
+    constexpr int RCH = KC / 8;         // 16-B chunks per image row
+    constexpr int PR = 64 / RCH;        // image rows per 1-KiB LDS-DMA piece
+    constexpr int MR = 64 * MT;         // staged X rows
+    constexpr int XI = MR / PR / 8;     // X pieces per wave per stage
+    constexpr int KS = KC / 32;         // k steps per stage
+    constexpr int WL = NF * KS;         // weight loads per wave per stage
+    constexpr int SCH = MR * RCH;       // 16-B chunks of a stage's X image
+    constexpr int TST = (160 * 1024) / (SCH * 16) < CAP ? (160 * 1024) / (SCH * 16) : CAP;
+    static_assert(TST >= 2 && TST - 1 >= D && XI >= 1, "ring");
+    static_assert((D - 1) * (XI + WL) <= kVmMax, "counted vmcnt");
+    static_assert(MODE == TM_PART, "diagnostic kernel: fp32 partials only");
+    __shared__ uint4 lds[TST * SCH];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(tid / kWave);
+    const int l16 = lane & 15, g = lane >> 4;
+    const int units = ntiles * S;
+    int u, mp;
+    if ((units & 7) == 0) {
+        const int j = blockIdx.x >> 3;
+        u = (j / mparts) * 8 + (blockIdx.x & 7);
+        mp = j % mparts;
+    } else {
+        u = blockIdx.x / mparts;
+        mp = blockIdx.x % mparts;
+    }
+    const int nt = u % ntiles, s = u / ntiles;
+    const int chunks_all = K / KC;
+    const int cbeg = s * cps;
+    const int chunks = min(chunks_all, cbeg + cps) - cbeg;  // > 0 (host contract)
+    const int m_lo = mp * mrows;
+    const int m_hi = min(M, m_lo + mrows);
+    const int rows = m_hi - m_lo;
+    const int mtv = __builtin_amdgcn_readfirstlane(min(XT, (rows + 15) / 16));  // 16-row tiles computed
+
+    const int n0 = nt * TNB;
+    auto wrow = [&](int r) -> int { return n0 + r; };
+    const uint4* wp[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+        wp[f] = reinterpret_cast<const uint4*>(w + (size_t)wrow(32 * wv + 16 * f + l16) * K + (size_t)cbeg * KC) + g;
+    const uint16_t* xsrc[XI];
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+        const int r = (wv * XI + i) * PR + lane / RCH;
+        xsrc[i] = x + (size_t)min(m_lo + r, M - 1) * K + (size_t)cbeg * KC + tslot<KC>(lane % RCH, r) * 8;
+    }
+    auto issue_x = [&](int c, int slot) {
+        uint4* base = lds + slot * SCH;
+#pragma unroll
+        for (int i = 0; i < XI; ++i)
+            tglds16(xsrc[i] + c * KC, base + (wv * XI + i) * 64);
+    };
+    // the weight loads are inline asm: the compiler's wait insertion loses
+    // count of builtin loads at the unrolled loop's back edge and drains the
+    // whole ring (vmcnt(0)) there; their completion is the counted wait at
+    // the top of each stage, after which `pin` hands the registers to the
+    // compiler as defined
+    u32x4_t wb[D + 1][WL];
+    auto load_w = [&](u32x4_t (&dst)[WL], int c) {
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk)
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst[f * KS + kk]) : "v"(wp[f] + c * RCH + 4 * kk)
+                             : "memory");
+    };
+    auto pin = [&](u32x4_t (&r)[WL]) {
+#pragma unroll
+        for (int i = 0; i < WL; ++i) asm volatile("" : "+v"(r[i]));
+    };
+
+    f32x4_t acc[NF][XT];
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+#pragma unroll
+        for (int t = 0; t < XT; ++t) acc[f][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    // per k step: the B fragments of the computed tiles from LDS in groups of
+    // GB, group q + 1's reads issued before group q's MFMAs (A from the
+    // register ring); 2 GB fragments live, not XT
+    constexpr int GB = XT < 4 ? XT : 4;
+    constexpr int NQ = XT / GB;
+    auto compute = [&](const uint4* xl, const u32x4_t (&a)[WL]) {
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+            bf16x8_t b[2][GB];
+            auto rd = [&](int q) {
+#pragma unroll
+                for (int e = 0; e < GB; ++e) {
+                    const int r = 16 * (q * GB + e) + l16;
+                    b[q & 1][e] = as_bf16x8(xl[r * RCH + tslot<KC>(4 * kk + g, r)]);
+                }
+            };
+            rd(0);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                if (q + 1 < NQ) rd(q + 1);
+#pragma unroll
+                for (int e = 0; e < GB; ++e)
+#pragma unroll
+                    for (int f = 0; f < NF; ++f)
+                        acc[f][q * GB + e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            __builtin_bit_cast(bf16x8_t, a[f * KS + kk]), b[q & 1][e], acc[f][q * GB + e], 0, 0, 0);
+            }
+        }
+    };
+
+    // vm operations this wave issued after its weight loads of stage c (they
+    // and everything older, incl. the X pieces of stage c, must have landed)
+    auto pending_after = [&](int c) -> int {
+        int n = 0;
+        if (c < D) n += WL * (min(D, chunks) - 1 - c);  // the prologue's later weight stages
+        for (int i = max(0, c - D + 1); i < c; ++i)     // the loop iterations since
+            n += (i + TST - 1 < chunks ? XI : 0) + (i + D < chunks ? WL : 0);
+        return n;
+    };
+
+#pragma unroll
+    for (int j = 0; j < TST - 1; ++j)
+        if (j < chunks) issue_x(j, j);
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+        if (j < chunks) load_w(wb[j], j);
+    for (int c0 = 0; c0 < chunks; c0 += D + 1) {
+#pragma unroll
+        for (int jj = 0; jj <= D; ++jj) {
+            const int c = c0 + jj;
+            if (c < chunks) {
+                if constexpr ((PROBE & 1) != 0) wait_vm_rt(0);
+                else wait_vm_rt(pending_after(c));
+                pin(wb[jj]);
+                asm volatile("s_barrier" ::: "memory");
+                if constexpr ((PROBE & 1) == 0) {
+                    if (c + TST - 1 < chunks) issue_x(c + TST - 1, (c + TST - 1) % TST);
+                    if (c + D < chunks) load_w(wb[(jj + D) % (D + 1)], c + D);
+                }
+                if constexpr ((PROBE & 2) == 0) compute(lds + (c % TST) * SCH, wb[jj]);
+            }
+        }
+    }
+    // every weight load landed (the last stage waited for all of them): no
+    // asm load may still write a register the epilogue reuses
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    // epilogue: lane (l16, g) holds Y[row m_lo + 16t + l16][col n0 + 32 wv + 16f + 4g + i]
+    const int c0 = n0 + 32 * wv;
+#pragma unroll
+    for (int t = 0; t < XT; ++t) {
+        const int m = m_lo + 16 * t + l16;
+        if (t >= mtv || m >= m_hi) continue;
+        float* dst = part + ((size_t)s * M + m) * N + c0 + 4 * g;
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+            *reinterpret_cast<float4*>(dst + 16 * f) = make_float4(acc[f][t][0], acc[f][t][1], acc[f][t][2], acc[f][t][3]);
+    }
+}
+
 // per row: the (max, id) pairs of every 64-id vocabulary quarter tile -> the selected
 // id (0 when the mask allows nothing, as masked_argmax); one wave per row
 __global__ __launch_bounds__(kBlock) void tgemm_argmax_reduce_kernel(const float2* __restrict__ best, int ntiles,
@@ -346,6 +555,30 @@ hipError_t launch_tgemm(const uint16_t* x, const uint16_t* w, uint16_t* y, float
 #define DMCP_TG(MT)                                                                                                 \
     tgemm_kernel<MT, MODE, PROBE, KC, CAP><<<grid, TTH, 0, st>>>(x, w, y, part, M, N, K, cps, S, ntiles, mparts, mrows, I, masks, \
                                                     midx, n_masks, wwords)
+    switch (mt) {
+        case 1: DMCP_TG(1); break;
+        case 2: DMCP_TG(2); break;
+        case 3: DMCP_TG(3); break;
+        case 4: DMCP_TG(4); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef DMCP_TG
+    return hipGetLastError();
+}
+
+template <int MODE, int PROBE = 0, int D = 3>
+hipError_t launch_tgemm_r(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int M, int N, int K, int S,
+                          int mparts, int I, hipStream_t st, const uint32_t* masks, const int32_t* midx, int n_masks,
+                          int wwords) {
+    const int ntiles = (MODE == TM_SWIGLU ? 2 * I : N) / TNB;
+    const int mrows = (((M + mparts - 1) / mparts) + 15) & ~15;
+    const int mt = (mrows + 63) / 64;
+    const int chunks = K / TKC_DEFAULT;
+    const int cps = (chunks + S - 1) / S;
+    const dim3 grid((unsigned)(ntiles * S * mparts));
+#define DMCP_TG(MT)                                                                                          \
+    tgemm_r_kernel<MT, MODE, PROBE, D><<<grid, TTH, 0, st>>>(x, w, y, part, M, N, K, cps, S, ntiles, mparts, \
+                                                             mrows, I, masks, midx, n_masks, wwords)
     switch (mt) {
         case 1: DMCP_TG(1); break;
         case 2: DMCP_TG(2); break;
@@ -407,7 +640,7 @@ int dmcp_tgemm(const void* x, const void* w, void* y, void* part, int M, int N, 
 // ring (probe & 32)
 int dmcp_tgemm_probe(int probe, const void* x, const void* w, void* part, int M, int N, int K, int S, int mparts,
                      void* stream) {
-    const int kc = (probe & 16) ? 32 : TKC_DEFAULT;
+    const int kc = (probe & 16) && probe < 64 ? 32 : TKC_DEFAULT;
     const int chunks = K / kc;
     if (M <= 0 || !x || !w || !part || S < 1 || K % kc != 0 || S > chunks ||
         (S - 1) * ((chunks + S - 1) / S) >= chunks || N % TNB != 0 || (((M + mparts - 1) / mparts + 15) & ~15) > 256)
@@ -426,6 +659,12 @@ int dmcp_tgemm_probe(int probe, const void* x, const void* w, void* part, int M,
         case 18: DMCP_TP(2, 32, 6);
         case 32: DMCP_TP(0, 64, 2);   // ring capped at 2 stages (1 in flight)
         case 34: DMCP_TP(2, 64, 2);
+        // register-weight kernel: 64 + PROBE, 128 + D (weight stages ahead)
+        case 64: return launch_tgemm_r<TM_PART>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
+        case 65: return launch_tgemm_r<TM_PART, 1>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
+        case 66: return launch_tgemm_r<TM_PART, 2>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
+        case 130: return launch_tgemm_r<TM_PART, 0, 2>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
+        case 129: return launch_tgemm_r<TM_PART, 0, 1>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
         default: return hipErrorInvalidValue;
     }
 #undef DMCP_TP

@@ -60,6 +60,8 @@ def main() -> int:
     ap.add_argument("--fused-sweep", action="store_true",
                     help="sweep (S, mparts) of the FUSED op (GEMM + its reduction) for qkv / o / down")
     ap.add_argument("--copies", type=int, default=0, help="weight copies (default: enough to exceed 640 MB)")
+    # 1 / 2: no refill DMA / no compute; 16-18: 64-B image rows; 32 / 34: a 2-stage ring;
+    # 64-66: the register-weight kernel (full / no refill / no compute), 129 / 130: its weights 1 / 2 stages ahead
     ap.add_argument("--probes", type=int, nargs="+", default=[1, 2, 16, 17, 18, 32, 34])
     ap.add_argument("--probe", action="store_true", help="also time the partials kernel without refill DMAs "
                     "(probe 1) and without compute (probe 2)")

@@ -43,10 +43,12 @@ namespace {
 // K per LDS stage: 64 (128-B image rows, full cache lines per DMA lane
 // group) or 32 (64-B rows: each 128-B line is fetched twice, in two stages)
 constexpr int TKC_DEFAULT = 64;
-// ring stages: as many stages as fit the CU's 160 KiB of LDS (capped at 6)
-template <int MT, int KC, int CAP = 6>
+// ring stages: as many stages as fit the CU's 160 KiB of LDS (capped at 6;
+// RES bytes reserved)
+template <int MT, int KC, int CAP = 6, int RES = 0>
 constexpr int tstages() {
-    return (160 * 1024) / ((256 + 64 * MT) * KC * 2) < CAP ? (160 * 1024) / ((256 + 64 * MT) * KC * 2) : CAP;
+    return (160 * 1024 - RES) / ((256 + 64 * MT) * KC * 2) < CAP ? (160 * 1024 - RES) / ((256 + 64 * MT) * KC * 2)
+                                                                 : CAP;
 }
 
 // s_waitcnt vmcnt(n * GL) for a runtime n in [0, 5] (the count is an immediate)
@@ -83,10 +85,35 @@ __device__ __forceinline__ int tslot(int j, int r) {
     else return j ^ (r & 7);
 }
 
+// s_waitcnt vmcnt(n) for a runtime n in [0, 63] (the count is an immediate)
+constexpr int kVmMax = 63;
+__device__ __forceinline__ void wait_vm_rt(int n) {
+    switch (n) {
+#define DMCP_VMC(i) case i: asm volatile("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
+        DMCP_VMC(0) DMCP_VMC(1) DMCP_VMC(2) DMCP_VMC(3) DMCP_VMC(4) DMCP_VMC(5) DMCP_VMC(6) DMCP_VMC(7) DMCP_VMC(8) DMCP_VMC(9) DMCP_VMC(10) DMCP_VMC(11) DMCP_VMC(12) DMCP_VMC(13) DMCP_VMC(14) DMCP_VMC(15) DMCP_VMC(16) DMCP_VMC(17) DMCP_VMC(18) DMCP_VMC(19) DMCP_VMC(20) DMCP_VMC(21) DMCP_VMC(22) DMCP_VMC(23) DMCP_VMC(24) DMCP_VMC(25) DMCP_VMC(26) DMCP_VMC(27) DMCP_VMC(28) DMCP_VMC(29) DMCP_VMC(30) DMCP_VMC(31) DMCP_VMC(32) DMCP_VMC(33) DMCP_VMC(34) DMCP_VMC(35) DMCP_VMC(36) DMCP_VMC(37) DMCP_VMC(38) DMCP_VMC(39) DMCP_VMC(40) DMCP_VMC(41) DMCP_VMC(42) DMCP_VMC(43) DMCP_VMC(44) DMCP_VMC(45) DMCP_VMC(46) DMCP_VMC(47) DMCP_VMC(48) DMCP_VMC(49) DMCP_VMC(50) DMCP_VMC(51) DMCP_VMC(52) DMCP_VMC(53) DMCP_VMC(54) DMCP_VMC(55) DMCP_VMC(56) DMCP_VMC(57) DMCP_VMC(58) DMCP_VMC(59) DMCP_VMC(60) DMCP_VMC(61) DMCP_VMC(62)
+#undef DMCP_VMC
+        default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
+    }
+}
+
 // PROBE (dmcp_tgemm_probe only; diagnostics of scripts/bench_tgemm.py --probe):
 // 1 = the K loop issues no refill DMAs (MFMA + LDS reads + barriers on stale
 // stages), 2 = no fragment reads / MFMAs (the DMA ring alone)
-template <int MT, int MODE, int PROBE = 0, int KC = TKC_DEFAULT, int CAP = 6>
+//
+// PF > 0: L2 prefetch of the weight stream PF stages ahead of the ring.  At
+// MT = 3-4 only two stages fit the LDS, so one 56-64 KB stage is in flight
+// per CU and the ring runs at that stage's HBM latency (~31 KB/us per CU
+// measured on the LM head, half the L2-fed rate); a 4-byte LDS-DMA
+// (global_load_lds_dword: no register, a 256-B scratch slot of LDS) per
+// 128-B weight line, issued PF stages before its refill, turns the refill
+// into an L2 hit.  Waves 0-3 (not the loaders) issue them: vector memory
+// loads complete in order, so a prefetch in a loader's queue would hold
+// back that loader's counted wait for the next stage by a full HBM latency.
+// MEASURED SLOWER at every distance (probes 257-262: +5-20 % on the
+// projections, +9-35 % on the LM head, worse with depth;
+// profiles/tgemm_l2_prefetch_ab_r5.jsonl): the refills are not waiting on
+// HBM latency.  Diagnostic only; production launches use PF = 0.
+template <int MT, int MODE, int PROBE = 0, int KC = TKC_DEFAULT, int CAP = 6, int PF = 0>
 __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) void tgemm_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, float* __restrict__ part,
     int M, int N, int K, int cps, int S, int ntiles, int mparts, int mrows, int I, const uint32_t* __restrict__ masks,
@@ -101,9 +128,10 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     constexpr int GL = WI + XI;        // LDS-DMA instructions per loader wave per stage
     constexpr int WCH = TNB * RCH;     // 16-B chunks of a stage's weight image
     constexpr int SCH = WCH + MR * RCH;  // ... plus the X image
-    constexpr int TST = tstages<MT, KC, CAP>();
-    static_assert(TST >= 2 && TST * SCH * 16 <= 160 * 1024, "LDS ring");
-    __shared__ uint4 lds[TST * SCH];   // ONE shared array (cdna_hip_programming.md §5 item 4a)
+    constexpr int PFB = PF > 0 ? 1024 : 0;  // prefetch scratch: 256 B per loader wave
+    constexpr int TST = tstages<MT, KC, CAP, PFB>();
+    static_assert(TST >= 2 && TST * SCH * 16 + PFB <= 160 * 1024, "LDS ring");
+    __shared__ uint4 lds[TST * SCH + PFB / 16];   // ONE shared array (cdna_hip_programming.md §5 item 4a)
 
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
@@ -164,6 +192,15 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         const int r = (lw * XI + i) * PR + lane / RCH;
         xsrc[i] = x + (size_t)min(m_lo + r, M - 1) * K + (size_t)cbeg * KC + tslot<KC>(lane % RCH, r) * 8;
     }
+    // prefetch: lane of wave lw (< 4) -> weight row 64 lw + lane, one 4-B
+    // read of its 128-B line of the stage
+    const uint16_t* pfsrc = w + (size_t)wrow(64 * lw + lane) * K + (size_t)cbeg * KC;
+    auto prefetch = [&](int c) {
+        if constexpr (PF > 0)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(pfsrc + c * KC),
+                                             (__attribute__((address_space(3))) void*)(lds + TST * SCH + 16 * lw), 4,
+                                             0, 0);
+    };
     auto issue = [&](int c, int slot) {
         uint4* base = lds + slot * SCH;
 #pragma unroll
@@ -230,10 +267,16 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // barrier (stage c landed for every wave; every wave done with stage
     // c - 1, the slot about to be refilled), the loaders refill it with stage
     // c + TST - 1, everyone computes stage c.  No __syncthreads() in the loop.
+    // With PF, waves 0-3 prefetch stages TST - 1 .. TST - 2 + PF up front and
+    // stage c + TST - 1 + PF in iteration c (they never wait in the loop).
     if (loader) {
 #pragma unroll
         for (int j = 0; j < TST - 1; ++j)
             if (j < chunks) issue(j, j);
+    } else if constexpr (PF > 0) {
+#pragma unroll
+        for (int q = TST - 1; q < TST - 1 + PF; ++q)
+            if (q < chunks) prefetch(q);
     }
     for (int c = 0; c < chunks; ++c) {
         if (loader) {
@@ -241,9 +284,16 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             else wait_vm<GL>(min(TST - 2, chunks - 1 - c));
         }
         asm volatile("s_barrier" ::: "memory");
-        if (loader && c + TST - 1 < chunks && (PROBE & 1) == 0) issue(c + TST - 1, (c + TST - 1) % TST);
+        if ((PROBE & 1) == 0) {
+            if (loader) {
+                if (c + TST - 1 < chunks) issue(c + TST - 1, (c + TST - 1) % TST);
+            } else if (PF > 0 && c + TST - 1 + PF < chunks) {
+                prefetch(c + TST - 1 + PF);
+            }
+        }
         if constexpr ((PROBE & 2) == 0) compute(lds + (c % TST) * SCH);
     }
+    if constexpr (PF > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the prefetches landed
 
     // epilogue: lane (l16, g) holds Y[row m_lo + mw + 16t + l16][col c0 + 16f + 4g + i]
     // with c0 = n0 + 64 wn (SwiGLU: intermediate column n0h + 32 wn + 16f + 4g + i of f < NF / 2)
@@ -311,18 +361,6 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
 }
 
-// s_waitcnt vmcnt(n) for a runtime n in [0, 23] (larger n: vmcnt(23), stricter)
-constexpr int kVmMax = 23;
-__device__ __forceinline__ void wait_vm_rt(int n) {
-    switch (n) {
-#define DMCP_VMC(i) case i: asm volatile("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
-        DMCP_VMC(0) DMCP_VMC(1) DMCP_VMC(2) DMCP_VMC(3) DMCP_VMC(4) DMCP_VMC(5) DMCP_VMC(6) DMCP_VMC(7)
-        DMCP_VMC(8) DMCP_VMC(9) DMCP_VMC(10) DMCP_VMC(11) DMCP_VMC(12) DMCP_VMC(13) DMCP_VMC(14) DMCP_VMC(15)
-        DMCP_VMC(16) DMCP_VMC(17) DMCP_VMC(18) DMCP_VMC(19) DMCP_VMC(20) DMCP_VMC(21) DMCP_VMC(22)
-#undef DMCP_VMC
-        default: asm volatile("s_waitcnt vmcnt(23)" ::: "memory"); break;
-    }
-}
 
 // Register-weight variant (diagnostic: dmcp_tgemm_probe 64-66 / 129-130
 // only).  MEASURED SLOWER and not used: 1.2-1.4x tgemm_kernel's time at
@@ -542,7 +580,7 @@ __global__ __launch_bounds__(kBlock) void tgemm_argmax_reduce_kernel(const float
     if (lane == 0) ids[m] = bi == 0x7fffffff ? 0 : bi;
 }
 
-template <int MODE, int PROBE = 0, int KC = TKC_DEFAULT, int CAP = 6>
+template <int MODE, int PROBE = 0, int KC = TKC_DEFAULT, int CAP = 6, int PF = 0>
 hipError_t launch_tgemm(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int M, int N, int K, int S,
                         int mparts, int I, hipStream_t st, const uint32_t* masks, const int32_t* midx, int n_masks,
                         int wwords) {
@@ -553,7 +591,7 @@ hipError_t launch_tgemm(const uint16_t* x, const uint16_t* w, uint16_t* y, float
     const int cps = (chunks + S - 1) / S;
     const dim3 grid((unsigned)(ntiles * S * mparts));
 #define DMCP_TG(MT)                                                                                                 \
-    tgemm_kernel<MT, MODE, PROBE, KC, CAP><<<grid, TTH, 0, st>>>(x, w, y, part, M, N, K, cps, S, ntiles, mparts, mrows, I, masks, \
+    tgemm_kernel<MT, MODE, PROBE, KC, CAP, PF><<<grid, TTH, 0, st>>>(x, w, y, part, M, N, K, cps, S, ntiles, mparts, mrows, I, masks, \
                                                     midx, n_masks, wwords)
     switch (mt) {
         case 1: DMCP_TG(1); break;
@@ -640,7 +678,7 @@ int dmcp_tgemm(const void* x, const void* w, void* y, void* part, int M, int N, 
 // ring (probe & 32)
 int dmcp_tgemm_probe(int probe, const void* x, const void* w, void* part, int M, int N, int K, int S, int mparts,
                      void* stream) {
-    const int kc = (probe & 16) && probe < 64 ? 32 : TKC_DEFAULT;
+    const int kc = (probe & 16) && probe < 64 ? 32 : TKC_DEFAULT;  // 257+: KC 64
     const int chunks = K / kc;
     if (M <= 0 || !x || !w || !part || S < 1 || K % kc != 0 || S > chunks ||
         (S - 1) * ((chunks + S - 1) / S) >= chunks || N % TNB != 0 || (((M + mparts - 1) / mparts + 15) & ~15) > 256)
@@ -664,6 +702,13 @@ int dmcp_tgemm_probe(int probe, const void* x, const void* w, void* part, int M,
         case 65: return launch_tgemm_r<TM_PART, 1>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
         case 66: return launch_tgemm_r<TM_PART, 2>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
         case 130: return launch_tgemm_r<TM_PART, 0, 2>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
+        // weight L2 prefetch 1 / 2 / 3 / 4 / 6 stages ahead (PF); 256: the plain kernel
+        case 256: return launch_tgemm<TM_PART>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
+        case 257: return launch_tgemm<TM_PART, 0, 64, 6, 1>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
+        case 258: return launch_tgemm<TM_PART, 0, 64, 6, 2>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
+        case 259: return launch_tgemm<TM_PART, 0, 64, 6, 3>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
+        case 260: return launch_tgemm<TM_PART, 0, 64, 6, 4>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
+        case 262: return launch_tgemm<TM_PART, 0, 64, 6, 6>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
         case 129: return launch_tgemm_r<TM_PART, 0, 1>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
         default: return hipErrorInvalidValue;
     }

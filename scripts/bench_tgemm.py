@@ -61,10 +61,13 @@ def main() -> int:
                     help="sweep (S, mparts) of the FUSED op (GEMM + its reduction) for qkv / o / down")
     ap.add_argument("--copies", type=int, default=0, help="weight copies (default: enough to exceed 640 MB)")
     # 1 / 2: no refill DMA / no compute; 16-18: 64-B image rows; 32 / 34: a 2-stage ring;
-    # 64-66: the register-weight kernel (full / no refill / no compute), 129 / 130: its weights 1 / 2 stages ahead
+    # 64-66: the register-weight kernel (full / no refill / no compute), 129 / 130: its weights 1 / 2 stages ahead;
+    # 256: the plain kernel, 257-262: + weight L2 prefetch 1-6 stages ahead
     ap.add_argument("--probes", type=int, nargs="+", default=[1, 2, 16, 17, 18, 32, 34])
     ap.add_argument("--probe", action="store_true", help="also time the partials kernel without refill DMAs "
                     "(probe 1) and without compute (probe 2)")
+    ap.add_argument("--probe-all", action="store_true", help="probes for gate/up and the head too (as plain "
+                    "fp32-partials GEMMs of their shapes)")
     a = ap.parse_args()
     c = preset(a.preset)
     dev = "cuda"
@@ -139,12 +142,16 @@ def main() -> int:
                         sw[f"S{S}_mp{mp}"] = round(graph_ms(run(S, mp), a.reps, copies) * 1e3, 2)
                 rec["sweep_us"] = sw
                 rec["sweep_best"] = min(sw.items(), key=lambda kv: kv[1])
-            if a.probe and mode == "part":
+            if a.probe and (mode == "part" or a.probe_all):
+                # the probes write fp32 partials: the plan's (S, parts) for "part", (1, parts) otherwise
+                pws = ws if mode == "part" else torch.empty(M * N, dtype=torch.float32, device=dev)
+                Sp = S0 if mode == "part" else 1
                 for pr in a.probes:
                     def probe(i, pr=pr):
-                        hip._check(hip.lib().dmcp_tgemm_probe(pr, hip._ptr(x), hip._ptr(Ws[i]), hip._ptr(ws), M, N, K,
-                                                              S0, mp0, hip._stream()), "dmcp_tgemm_probe")
+                        hip._check(hip.lib().dmcp_tgemm_probe(pr, hip._ptr(x), hip._ptr(Ws[i]), hip._ptr(pws), M, N,
+                                                              K, Sp, mp0, hip._stream()), "dmcp_tgemm_probe")
                     rec[f"probe{pr}_us"] = round(graph_ms(probe, a.reps, copies) * 1e3, 2)
+                del pws
             # the fused op of the step vs hipBLASLt + the unfused neighbour op
             if name in ("o", "down"):
                 resid = torch.randn(M, N, device=dev).to(torch.bfloat16)

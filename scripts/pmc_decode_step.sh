@@ -27,7 +27,10 @@ for f in glob.glob(sys.argv[1] + "/pmcd*/**/*counter_collection.csv", recursive=
     for r in csv.DictReader(open(f)):
         k = r.get("Kernel_Name", "?")
         mode = re.search(r"wgemm_kernel<\d+, \d+, \d+, (\d)", k)
-        k = ("prefix" if "prefill_attn" in k else "decode_mfma" if "decode_attn_mfma" in k else
+        tg = re.search(r"tgemm_kernel<\d+, (\d)", k)
+        k = (("tgemm_" + ["bf16", "part", "swiglu", "head"][int(tg.group(1))]) if tg else
+             "tgemm_head" if "tgemm_argmax_reduce" in k else
+             "prefix" if "prefill_attn" in k else "decode_mfma" if "decode_attn_mfma" in k else
              "combine" if "combine" in k else "gemm_lib" if "Cijk" in k else "rmsnorm" if "rmsnorm" in k else
              "lm_head_argmax" if (mode and mode.group(1) == "3") or "lm_head_reduce" in k else
              "wgemm_swiglu" if mode and mode.group(1) == "2" else "wgemm" if "wgemm_kernel" in k else

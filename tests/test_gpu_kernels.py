@@ -329,7 +329,8 @@ def test_decode_attention_fork_table(hip, kv, splits, P):
     its keys below ``end`` from the parent slot in place.  Bit-identical to
     the same kernel on caches where those keys were copied into the row's
     slot; fork ends inside a 32-key tile, on a tile edge, past the row's
-    length; a shared prefix in front; rows without a parent unchanged."""
+    length; a shared prefix in front; rows without a parent unchanged.  Also
+    within bf16 tolerance of reference.decode_attention(..., fork=) in fp32."""
     from dmcp.ops.reference import SharedPrefix
     D, Hq, Hkv, MAXS, S = 64, 32, 8, 1024, 10
     dt = torch.uint8 if kv == "fp8" else torch.bfloat16
@@ -359,3 +360,7 @@ def test_decode_attention_fork_table(hip, kv, splits, P):
     exp = hip.decode_attention(q, kc2, vc2, slot, lens, 0.125, chunk=64, prefix=pre2, splits=splits)
     assert torch.equal(got, exp)
     assert dt == kc.dtype
+    # and against the fp32 reference reading the parents' keys through the same fork table
+    from dmcp.ops import reference
+    ref = reference.decode_attention(q, kc, vc, slot, lens, 0.125, prefix=pre, fork=fork)
+    torch.testing.assert_close(got.float(), ref.float(), atol=2e-2, rtol=2e-2)

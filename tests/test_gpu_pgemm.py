@@ -214,6 +214,36 @@ def test_model_prefill_fp8_close_to_bf16(hip, kv):
             b.clear_prefix()
 
 
+def test_model_prefill_fp8_16_layers_bounded_drift(hip):
+    """The default-on MXFP8 prefill through all 16 layers of dmcp-coder-1b
+    (random-init weights) against the bf16 prefill of the same weights:
+    stated bounds on the last-position logit cosine (min over sequences) and
+    on the K/V relative error of EVERY layer (the deepest layers carry the
+    accumulated drift).  Measured on MI355X: logit cosine >= 0.9990, KV
+    relative error <= 0.0557 (layer 0: 0.0378)."""
+    from dmcp.models.llm import LocalLM, preset
+    cfg = dict(max_batch=8, max_seq=2048, kv_dtype="bf16")
+    a = LocalLM(preset("dmcp-coder-1b", **cfg), device="cuda", seed=4)
+    b = LocalLM(preset("dmcp-coder-1b", prefill_dtype="fp8", **cfg), device="cuda", seed=4)
+    assert a.cfg.layers == 16 and b.prefill_fp8
+    g = torch.Generator().manual_seed(5)
+    lens = (1500, 700, 64, 1)
+    seqs = [[256] + torch.randint(0, 256, (n,), generator=g).tolist() for n in lens]
+    reqs = [(t, s, 0) for s, t in enumerate(seqs)]
+    la, lb = a.prefill_batch(reqs).float(), b.prefill_batch(reqs).float()
+    cos = torch.nn.functional.cosine_similarity(la, lb, dim=-1)
+    rel = []
+    for L in range(16):
+        for ca, cb in ((a.k_cache, b.k_cache), (a.v_cache, b.v_cache)):
+            x = torch.cat([R.kv_float(ca[L, s, :, :n + 1]).flatten() for s, n in enumerate(lens)])
+            y = torch.cat([R.kv_float(cb[L, s, :, :n + 1]).flatten() for s, n in enumerate(lens)])
+            rel.append(((x - y).norm() / x.norm()).item())
+    msg = f"logit cos min {cos.min().item():.4f}, KV rel err per layer max {max(rel):.4f} (layer 0 {rel[0]:.4f})"
+    print(msg)
+    assert cos.min().item() > 0.995, msg  # measured 0.9990
+    assert max(rel) < 0.08, msg  # measured 0.0557 (layer 0: 0.0378)
+
+
 # ---- decode: the MX weight-streaming GEMM (wmx_kernel) at decode row counts
 DEC_ROWS = [17, 78, 129, 256, 320, 448, 512, 533, 768]
 
@@ -298,7 +328,24 @@ def test_model_decode_fp8_agrees_with_bf16(hip):
     la, lb = a.decode(toks, slots, pos).float(), b.decode(toks, slots, pos).float()
     cos = torch.nn.functional.cosine_similarity(la, lb, dim=-1)
     assert cos.min().item() > 0.97, cos.min()
-    assert (la.argmax(-1) == lb.argmax(-1)).float().mean().item() > 0.6
+    # Greedy agreement, stated against the decision margin.  Random-init
+    # logits are nearly flat: on MI355X only 25 of the 320 rows have a bf16
+    # top-2 gap above twice the row's largest |fp8 - bf16| logit error, so
+    # the overall rate mostly measures near-ties (0.797 measured).  Gates:
+    # every such decisive row picks the same id (there must be some), the
+    # row-RMS error stays a bounded share of the logits' spread, and the
+    # overall agreement stays at the measured level (> 0.75).
+    top2 = la.topk(2, dim=-1).values
+    margin = top2[:, 0] - top2[:, 1]
+    err = (la - lb).abs().max(-1).values
+    decisive = margin > 2 * err
+    same = la.argmax(-1) == lb.argmax(-1)
+    rms = ((la - lb).pow(2).mean(-1).sqrt() / la.std(-1)).max().item()
+    msg = f"agree {same.float().mean().item():.3f}, decisive rows {int(decisive.sum())}/{B}, rms err / spread {rms:.3f}"
+    print(msg)
+    assert decisive.any() and same[decisive].all(), msg
+    assert rms < 0.3, msg
+    assert same.float().mean().item() > 0.75, msg
 
 
 def test_engine_on_fp8_prefill_and_decode(hip):

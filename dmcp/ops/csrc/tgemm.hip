@@ -709,6 +709,9 @@ int dmcp_tgemm_probe(int probe, const void* x, const void* w, void* part, int M,
         case 259: return launch_tgemm<TM_PART, 0, 64, 6, 3>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
         case 260: return launch_tgemm<TM_PART, 0, 64, 6, 4>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
         case 262: return launch_tgemm<TM_PART, 0, 64, 6, 6>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
+        // the DMA ring alone (PROBE 2) with the weight prefetch 2 / 4 stages ahead
+        case 274: return launch_tgemm<TM_PART, 2, 64, 6, 2>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
+        case 276: return launch_tgemm<TM_PART, 2, 64, 6, 4>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
         case 129: return launch_tgemm_r<TM_PART, 0, 1>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0);
         default: return hipErrorInvalidValue;
     }

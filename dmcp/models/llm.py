@@ -1031,11 +1031,15 @@ class DecodeGraphs:
                 m.decode_select_gather(inp[0], inp[4], scratch, inp[1], inp[2], self.masks, inp[3], inp[5],
                                        self.alt_token, inp[6])
         torch.cuda.current_stream().wait_stream(s)
-        g = torch.cuda.CUDAGraph()
+        # keep_graph: the hipGraph_t stays queryable after capture (the kernel
+        # node count of the witness); instantiated explicitly right after
+        g = torch.cuda.CUDAGraph(keep_graph=True)
         with torch.cuda.graph(g):
             logits, ids = m.decode_select_gather(inp[0], inp[4], self.last_ids, inp[1], inp[2], self.masks, inp[3],
                                                  inp[5], self.alt_token, inp[6])
-        self.graphs[b] = _Bucket(g, inp, logits, ids, b)
+        bucket = _Bucket(g, inp, logits, ids, b)
+        g.instantiate()
+        self.graphs[b] = bucket
 
     @torch.inference_mode()
     def run(self, tokens: Sequence[int], slots: Sequence[int], positions: Sequence[int],

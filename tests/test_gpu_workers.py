@@ -62,6 +62,8 @@ def test_small_project_is_dealt_over_every_gpu_worker(tmp_path, pool):
     assert sum(got) == 33 and min(got) >= 33 // N, got
     st = be.stats()
     assert st["workers"] == N and st["decode_steps"] > 0 and st.get("graph_replays", 0) > 0, st
+    # the device witness: kernel nodes of the replayed decode graphs (tiny: 2 layers, > 10 kernels a step)
+    assert st.get("graph_kernels", 0) > 10 * st["graph_replays"], st
     app.db.close()  # the module-scoped pool outlives this app
     assert time.time() - t0 < 300
 

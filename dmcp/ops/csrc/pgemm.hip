@@ -69,6 +69,14 @@ constexpr int PB_BYTES = PBN * PBK;                     // W image
 constexpr int PS_BYTES = PBM * 4;
 constexpr int PST_BYTES = PA_BYTES + PB_BYTES + PS_BYTES;
 constexpr int PM_BF16 = 0, PM_RESID = 1, PM_SWIGLU = 2, PM_QKV = 3;
+// BK = 128 (pgemm_kernel<..., 128>): 128-deep stages, [rows][8 x 16 B] images
+// (full 128-B lines per DMA lane group, as tgemm.hip's measured 128-B rows),
+// a two-slot ring, the stage's 4 A scale bytes per row as one 4-byte LDS-DMA
+constexpr int PBK2 = 128;
+constexpr int PA2_BYTES = PBM * PBK2, PB2_BYTES = PBN * PBK2, PS2_BYTES = PBM * 4;
+constexpr int PST2_BYTES = PA2_BYTES + PB2_BYTES + PS2_BYTES;
+template <int BK>
+constexpr int pgemm_lds_bytes() { return BK == 128 ? 2 * PST2_BYTES : PST * PST_BYTES; }
 
 struct PEpi {
     uint16_t* y;          // PM_BF16: out [M, N]; PM_RESID: resid [M, N] (in place)
@@ -85,12 +93,13 @@ struct PEpi {
     int Hq, Hkv, max_seq, max_pos, num_slots;
 };
 
-// LDS-DMA of 16 / 2 bytes per lane (the size must be a literal)
+// LDS-DMA of 16 / 4 / 2 bytes per lane (the size must be a literal)
 template <int SIZE>
 __device__ __forceinline__ void pglds(const void* src, void* lds_base) {
     auto g = (const __attribute__((address_space(1))) void*)src;
     auto l = (__attribute__((address_space(3))) void*)lds_base;
     if constexpr (SIZE == 16) __builtin_amdgcn_global_load_lds(g, l, 16, 0, 0);
+    else if constexpr (SIZE == 4) __builtin_amdgcn_global_load_lds(g, l, 4, 0, 0);
     else __builtin_amdgcn_global_load_lds(g, l, 2, 0, 0);
 }
 
@@ -128,7 +137,7 @@ __device__ long long pg_stamps[65536][4];
 // WV = 4: one wave per SIMD, 128 x 128 per wave (16 MFMAs, 9 LDS-DMA pieces
 // per stage); WV = 8: two waves per SIMD, 128 x 64 per wave (8 MFMAs, 4-5
 // pieces) -- one wave's MFMAs run while the other issues its DMAs.
-template <int MODE, bool KV8, int WV>
+template <int MODE, bool KV8, int WV, int BK = PBK>
 __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4, WV / 4))) void pgemm_kernel(
     const uint8_t* __restrict__ aq, const uint8_t* __restrict__ as, const uint8_t* __restrict__ wq,
     const float* __restrict__ ws, int M, int N, int K, int mtiles, int ntiles, PEpi e) {
@@ -136,7 +145,8 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4,
     constexpr int WNW = WV / 2;          // waves along N
     constexpr int CPW = PBN / WNW;       // columns per wave
     constexpr int PPW = 16 / WV;         // 1-KiB LDS-DMA pieces per wave per operand per stage
-    __shared__ __attribute__((aligned(16))) uint8_t plds[PST * PST_BYTES];  // ONE LDS object (ring, then epilogue)
+    static_assert(BK == PBK || (BK == PBK2 && WV == 4), "128-deep stages: the 4-wave block only");
+    __shared__ __attribute__((aligned(16))) uint8_t plds[pgemm_lds_bytes<BK>()];  // ONE LDS object
 #if (PG_PROBE & 4) != 0
     const long long t_start = __builtin_amdgcn_s_memtime();
 #endif
@@ -309,6 +319,102 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4,
 #pragma unroll
         for (int u = 0; u < NU; ++u) mma(3, u);
     };
+    if constexpr (BK == PBK2) {
+        // ---- 128-deep stages in a two-slot ring.  Step c computes stage c
+        // (two MX k-steps of 64: 32 MFMAs per wave) while the 17 LDS-DMA
+        // instructions of stage c + 1 go out one per MFMA into the other slot
+        // (freed by the previous step's closing barrier).  Four MFMAs before
+        // the end the wave waits for its own stage c + 1 pieces, the barrier
+        // makes them every wave's (and retires every wave's stage-c reads),
+        // and stage c + 1's first k-step fragments are read behind those
+        // last MFMAs, so the next step opens on MFMAs.
+        // Image rows of 128 B: chunk j of row r in slot j ^ ((r >> 1) & 7) --
+        // the 16 lanes of each ds_read_b128 pass of the 32x32 operand layout
+        // (rows {0-3,12-15,20-27} / {4-11,16-19,28-31}, one chunk) hit 16
+        // distinct (row parity, slot) pairs: all 64 banks.
+        constexpr int PP2 = PA2_BYTES / 1024 / WV;  // 1-KiB pieces per wave per operand per stage
+        constexpr int NP2 = 2 * PP2 + 1;            // + the scale dword
+        auto sw2 = [](int r) { return (r >> 1) & 7; };
+        // 32-bit byte offsets of the pieces' sources (64-bit pointers for 16
+        // pieces would hold 32 VGPRs through the loop)
+        uint32_t a2[PP2], w2[PP2];
+#pragma unroll
+        for (int i = 0; i < PP2; ++i) {
+            const int r = (wv * PP2 + i) * 8 + (lane >> 3);
+            const int ch = (lane & 7) ^ sw2(r);
+            a2[i] = (uint32_t)min(m0 + r, M - 1) * (uint32_t)K + ch * 16;
+            w2[i] = (uint32_t)wrow(r) * (uint32_t)K + ch * 16;
+        }
+        const uint32_t s2 = (uint32_t)min(m0 + wv * 64 + lane, M - 1) * (uint32_t)ksb;  // 4 scale bytes per stage
+        auto piece2 = [&](int i, int c2, int slot) {
+            uint8_t* base = plds + slot * PST2_BYTES;
+            const uint32_t kb = (uint32_t)c2 * PBK2;
+            if (i < PP2) pglds<16>(aq + (a2[i] + kb), base + (wv * PP2 + i) * 1024);
+            else if (i < 2 * PP2) pglds<16>(wq + (w2[i - PP2] + kb), base + PA2_BYTES + (wv * PP2 + i - PP2) * 1024);
+            else pglds<4>(as + (s2 + (uint32_t)c2 * 4), base + PA2_BYTES + PB2_BYTES + wv * 256);
+        };
+        auto frag2 = [&](const uint8_t* img, int r, int ks) -> v8i_t {
+            const int sw = sw2(r);
+            const v4i_t lo = *reinterpret_cast<const v4i_t*>(img + r * PBK2 + ((4 * ks + hh) ^ sw) * 16);
+            const v4i_t hi = *reinterpret_cast<const v4i_t*>(img + r * PBK2 + ((4 * ks + 2 + hh) ^ sw) * 16);
+            return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        };
+        struct KF {
+            v8i_t a[4], b[NU];
+            int sc[4];
+        };
+        auto rd2 = [&](int c2, int ks, KF& F) {
+            const uint8_t* A = plds + (c2 & 1) * PST2_BYTES;
+            const uint8_t* S = A + PA2_BYTES + PB2_BYTES;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int r = wm * 128 + t * 32 + l32;
+                F.a[t] = frag2(A, r, ks);
+                F.sc[t] = S[r * 4 + 2 * ks + hh];
+            }
+#pragma unroll
+            for (int u = 0; u < NU; ++u) F.b[u] = frag2(A + PA2_BYTES, wn * CPW + u * 32 + l32, ks);
+        };
+        const int chunks2 = K / PBK2;
+        // branch-free (a guarded refill splits the step into blocks across which
+        // the compiler moves the MFMAs, undoing the interleave): past the last
+        // stage the refill re-reads that stage into the free slot and the next
+        // k-step-0 read is of a slot nobody uses
+        auto step2 = [&](int c, KF& F0, KF& F1) {  // F0: stage c, k-step 0 (read); F1: scratch -> next F0
+            const int cn = min(c + 1, chunks2 - 1);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                KF& F = ks == 0 ? F0 : F1;
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) {
+                        const int idx = ks * 4 * NU + t * NU + u;
+                        __builtin_amdgcn_sched_barrier(0);
+                        acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(F.b[u], F.a[t], acc[t][u], 0, 0, 0,
+                                                                                    127, 0, F.sc[t]);
+                        __builtin_amdgcn_sched_barrier(0);
+                        if (idx == 0) rd2(c, 1, F1);  // k-step 1 of this stage, behind the first MFMA
+                        if (idx < NP2) piece2(idx, cn, (c + 1) & 1);
+                        if (idx == 8 * NU - 5) {  // four MFMAs before the end: stage c + 1 in, then its k-step 0
+                            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                            asm volatile("s_barrier" ::: "memory");
+                            __builtin_amdgcn_sched_barrier(0);
+                            rd2(c + 1, 0, F0);
+                        }
+                    }
+            }
+        };
+        // prologue: stage 0 in, its k-step 0 read
+        for (int i = 0; i < NP2; ++i) piece2(i, 0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        KF Fa, Fb;
+        rd2(0, 0, Fa);
+        for (int c = 0; c < chunks2; ++c) step2(c, Fa, Fb);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
     const int chunks = chunks_of(K);
 #pragma unroll
     for (int j = 0; j < PST - 1; ++j) issue(min(j, chunks - 1), j);
@@ -383,6 +489,7 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4,
     }
     // the refills past the last stage land before the block's LDS is released
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }  // BK == PBK
 #if (PG_PROBE & 4) != 0
     const long long t_loop = __builtin_amdgcn_s_memtime();
 #endif
@@ -935,13 +1042,20 @@ __global__ void mx_probe_kernel(const v8i_t* a, const v8i_t* b, const int* sa, c
 }
 
 int g_pgemm_waves = 4;  // dmcp_pgemm_set_waves: 4 (one wave per SIMD) or 8 (two)
+// dmcp_pgemm_set_bk: K per LDS stage, 64 or 128 (4-wave block, K % 128 == 0).
+// 128 by default: the Llama-shape layer at 24,576 rows 1,654 -> 1,564 us (down
+// projection 405 -> 355 us; profiles/pgemm_bk128_r5.jsonl)
+int g_pgemm_bk = 128;
 
 template <int MODE, bool KV8>
 hipError_t launch_pgemm(const void* aq, const void* as, const void* wq, const void* ws, int M, int N, int K,
                         const PEpi& e, void* stream) {
     const int mtiles = (M + PBM - 1) / PBM;
     const int ntiles = MODE == PM_SWIGLU ? e.I / 128 : N / PBN;
-    if (g_pgemm_waves == 8)
+    if (g_pgemm_bk == 128 && g_pgemm_waves == 4 && K % PBK2 == 0)
+        pgemm_kernel<MODE, KV8, 4, PBK2><<<mtiles * ntiles, PTH, 0, (hipStream_t)stream>>>(
+            (const uint8_t*)aq, (const uint8_t*)as, (const uint8_t*)wq, (const float*)ws, M, N, K, mtiles, ntiles, e);
+    else if (g_pgemm_waves == 8)
         pgemm_kernel<MODE, KV8, 8><<<mtiles * ntiles, 512, 0, (hipStream_t)stream>>>(
             (const uint8_t*)aq, (const uint8_t*)as, (const uint8_t*)wq, (const float*)ws, M, N, K, mtiles, ntiles, e);
     else
@@ -962,6 +1076,13 @@ extern "C" {
 int dmcp_pgemm_set_waves(int w) {
     const int old = g_pgemm_waves;
     if (w == 4 || w == 8) g_pgemm_waves = w;
+    return old;
+}
+
+// K per LDS stage of the MX prefill GEMMs (64 or 128); returns the previous value
+int dmcp_pgemm_set_bk(int bk) {
+    const int old = g_pgemm_bk;
+    if (bk == 64 || bk == 128) g_pgemm_bk = bk;
     return old;
 }
 

@@ -57,6 +57,7 @@ def lib() -> ctypes.CDLL:
                                        _vp, _vp, _vp, _i, _i, _vp, _vp, _vp], _i),
             "dmcp_kv_fork": ([_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _vp], _i),
             "dmcp_pgemm_set_waves": ([_i], _i),
+            "dmcp_pgemm_set_bk": ([_i], _i),
             "dmcp_prefill_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _i, _i,
                                         _i, _vp], _i),
             "dmcp_prefill_varlen": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, ctypes.c_long, _f,
@@ -500,6 +501,16 @@ def pgemm_set_waves(waves: int) -> int:
     if waves not in (4, 8):
         raise HipOpsError(f"pgemm_set_waves: 4 or 8, got {waves}")
     return int(lib().dmcp_pgemm_set_waves(int(waves)))
+
+
+def pgemm_set_bk(bk: int) -> int:
+    """K per LDS stage of the MX prefill GEMMs: 128 (the default: a 2-slot
+    ring of 128-B image rows; 4-wave block, K % 128 == 0, else the 64-deep
+    kernel runs) or 64 (a 4-stage ring of 64-B rows).  Returns the previous
+    value."""
+    if bk not in (64, 128):
+        raise HipOpsError(f"pgemm_set_bk: 64 or 128, got {bk}")
+    return int(lib().dmcp_pgemm_set_bk(int(bk)))
 
 
 def kv_fork(k_cache: torch.Tensor, v_cache: torch.Tensor, src: int, dsts, start: int, end: int) -> None:

@@ -91,6 +91,7 @@ struct PEpi {
     void* k_cache;
     void* v_cache;
     int Hq, Hkv, max_seq, max_pos, num_slots;
+    int grp;              // M tiles per block-order group (dmcp_pgemm_set_group; 0 = 8)
 };
 
 // LDS-DMA of 16 / 4 / 2 bytes per lane (the size must be a literal)
@@ -164,10 +165,11 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4,
     const int b = blockIdx.x;
     const int xcd = b & 7, q8 = nblk >> 3, r8 = nblk & 7;
     const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-    const int per_group = 8 * ntiles;
+    const int grp = e.grp > 0 ? e.grp : 8;
+    const int per_group = grp * ntiles;
     const int gid = L / per_group;
-    const int first = gid * 8;
-    const int gsz = min(mtiles - first, 8);
+    const int first = gid * grp;
+    const int gsz = min(mtiles - first, grp);
     const int inn = L - gid * per_group;
     const int mt = first + inn % gsz, nt = inn / gsz;
     const int m0 = mt * PBM;
@@ -1046,21 +1048,24 @@ int g_pgemm_waves = 4;  // dmcp_pgemm_set_waves: 4 (one wave per SIMD) or 8 (two
 // 128 by default: the Llama-shape layer at 24,576 rows 1,654 -> 1,564 us (down
 // projection 405 -> 355 us; profiles/pgemm_bk128_r5.jsonl)
 int g_pgemm_bk = 128;
+int g_pgemm_group = 8;  // dmcp_pgemm_set_group: M tiles per block-order group
 
 template <int MODE, bool KV8>
 hipError_t launch_pgemm(const void* aq, const void* as, const void* wq, const void* ws, int M, int N, int K,
                         const PEpi& e, void* stream) {
     const int mtiles = (M + PBM - 1) / PBM;
     const int ntiles = MODE == PM_SWIGLU ? e.I / 128 : N / PBN;
+    PEpi e2 = e;
+    e2.grp = g_pgemm_group;
     if (g_pgemm_bk == 128 && g_pgemm_waves == 4 && K % PBK2 == 0)
         pgemm_kernel<MODE, KV8, 4, PBK2><<<mtiles * ntiles, PTH, 0, (hipStream_t)stream>>>(
-            (const uint8_t*)aq, (const uint8_t*)as, (const uint8_t*)wq, (const float*)ws, M, N, K, mtiles, ntiles, e);
+            (const uint8_t*)aq, (const uint8_t*)as, (const uint8_t*)wq, (const float*)ws, M, N, K, mtiles, ntiles, e2);
     else if (g_pgemm_waves == 8)
         pgemm_kernel<MODE, KV8, 8><<<mtiles * ntiles, 512, 0, (hipStream_t)stream>>>(
-            (const uint8_t*)aq, (const uint8_t*)as, (const uint8_t*)wq, (const float*)ws, M, N, K, mtiles, ntiles, e);
+            (const uint8_t*)aq, (const uint8_t*)as, (const uint8_t*)wq, (const float*)ws, M, N, K, mtiles, ntiles, e2);
     else
         pgemm_kernel<MODE, KV8, 4><<<mtiles * ntiles, PTH, 0, (hipStream_t)stream>>>(
-            (const uint8_t*)aq, (const uint8_t*)as, (const uint8_t*)wq, (const float*)ws, M, N, K, mtiles, ntiles, e);
+            (const uint8_t*)aq, (const uint8_t*)as, (const uint8_t*)wq, (const float*)ws, M, N, K, mtiles, ntiles, e2);
     return hipGetLastError();
 }
 
@@ -1083,6 +1088,13 @@ int dmcp_pgemm_set_waves(int w) {
 int dmcp_pgemm_set_bk(int bk) {
     const int old = g_pgemm_bk;
     if (bk == 64 || bk == 128) g_pgemm_bk = bk;
+    return old;
+}
+
+// M tiles per block-order group of the MX prefill GEMMs (1..64); returns the previous value
+int dmcp_pgemm_set_group(int g) {
+    const int old = g_pgemm_group;
+    if (g >= 1 && g <= 64) g_pgemm_group = g;
     return old;
 }
 

@@ -58,6 +58,7 @@ def lib() -> ctypes.CDLL:
             "dmcp_kv_fork": ([_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _vp], _i),
             "dmcp_pgemm_set_waves": ([_i], _i),
             "dmcp_pgemm_set_bk": ([_i], _i),
+            "dmcp_pgemm_set_group": ([_i], _i),
             "dmcp_prefill_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _i, _i,
                                         _i, _vp], _i),
             "dmcp_prefill_varlen": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, ctypes.c_long, _f,
@@ -511,6 +512,14 @@ def pgemm_set_bk(bk: int) -> int:
     if bk not in (64, 128):
         raise HipOpsError(f"pgemm_set_bk: 64 or 128, got {bk}")
     return int(lib().dmcp_pgemm_set_bk(int(bk)))
+
+
+def pgemm_set_group(g: int) -> int:
+    """M tiles per block-order group of the MX prefill GEMMs (the blocks of a
+    group's N column run back to back on one XCD).  Returns the previous value."""
+    if not 1 <= g <= 64:
+        raise HipOpsError(f"pgemm_set_group: 1..64, got {g}")
+    return int(lib().dmcp_pgemm_set_group(int(g)))
 
 
 def kv_fork(k_cache: torch.Tensor, v_cache: torch.Tensor, src: int, dsts, start: int, end: int) -> None:

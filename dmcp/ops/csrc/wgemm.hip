@@ -54,12 +54,14 @@ __device__ __forceinline__ float silu_f(float g) { return g / (1.f + __expf(-g))
 // LDS-DMA (global_load_lds_dwordx4): each lane's 16 source bytes land at
 // the wave-uniform LDS base + 16 * lane, with no VGPR round trip; counted on
 // vmcnt like any vector load.
+// AUX: cache-policy bits of the load (2 = nt: streamed, evicted first from L2)
+template <int AUX = 0>
 __device__ __forceinline__ void glds16(const void* src, uint4* lds_base) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                     (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+                                     (__attribute__((address_space(3))) void*)lds_base, 16, 0, AUX);
 }
 
-template <int NB, int MT, int MR, int MODE, int ST>
+template <int NB, int MT, int MR, int MODE, int ST, int AUXW = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) void wgemm_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                        uint16_t* __restrict__ y, float* __restrict__ part, int M, int N,
                                                        int K, int ks, int S, int ntiles, int mparts, int mrows,
@@ -132,7 +134,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     auto issue = [&](int c, int slot) {
         uint4* base = lds + slot * SCH;
 #pragma unroll
-        for (int i = 0; i < WI; ++i) glds16(wsrc[i] + c * kKC, base + (wv * WI + i) * 64);
+        for (int i = 0; i < WI; ++i) glds16<AUXW>(wsrc[i] + c * kKC, base + (wv * WI + i) * 64);
 #pragma unroll
         for (int i = 0; i < XI; ++i) glds16(xsrc[i] + c * kKC, base + WCH + (wv * XI + i) * 64);
     };
@@ -468,6 +470,8 @@ __global__ __launch_bounds__(kBlock) void lm_head_reduce_kernel(const float2* __
 }
 
 constexpr int kStages = 3;  // LDS ring stages (2 in flight while one is computed)
+// dmcp_wgemm_set_aux: the weight stream's cache policy (0 default, 2 nt)
+int g_wgemm_auxw = 0;
 
 template <int NB, int MODE>
 hipError_t launch_wgemm(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int M, int N, int K, int S,
@@ -479,10 +483,15 @@ hipError_t launch_wgemm(const uint16_t* x, const uint16_t* w, uint16_t* y, float
     const bool full = ((mrows + 31) & ~31) > (mt - 1) * 64 + 32;  // staged rows: mt * 64, else mt * 64 - 32
     const dim3 grid((unsigned)(ntiles * S * mparts));
     const int ks = K / S;
-#define DMCP_WG1(MT, MR)                                                                                       \
-    wgemm_kernel<NB, MT, MR, MODE, kStages><<<grid, kBlock, 0, st>>>(x, w, y, part, M, N, K, ks, S, ntiles,   \
-                                                                     mparts, mrows, I, masks, midx, n_masks,  \
-                                                                     wwords)
+#define DMCP_WG1(MT, MR)                                                                                        \
+    do {                                                                                                        \
+        if (g_wgemm_auxw == 2)                                                                                  \
+            wgemm_kernel<NB, MT, MR, MODE, kStages, 2><<<grid, kBlock, 0, st>>>(                                \
+                x, w, y, part, M, N, K, ks, S, ntiles, mparts, mrows, I, masks, midx, n_masks, wwords);         \
+        else                                                                                                    \
+            wgemm_kernel<NB, MT, MR, MODE, kStages><<<grid, kBlock, 0, st>>>(                                   \
+                x, w, y, part, M, N, K, ks, S, ntiles, mparts, mrows, I, masks, midx, n_masks, wwords);         \
+    } while (0)
 #define DMCP_WG(MT)                  \
     do {                             \
         if (full)                    \
@@ -505,6 +514,13 @@ hipError_t launch_wgemm(const uint16_t* x, const uint16_t* w, uint16_t* y, float
 }  // namespace
 
 extern "C" {
+
+// cache policy of the weight stream's LDS-DMA (0 or 2 = nt); returns the previous value
+int dmcp_wgemm_set_aux(int aux) {
+    const int old = g_wgemm_auxw;
+    if (aux == 0 || aux == 2) g_wgemm_auxw = aux;
+    return old;
+}
 
 // Plain / partial / SwiGLU weight-streaming GEMM.
 //   mode 0: y[M, N] bf16 = x . w^T                        (S == 1)

@@ -58,6 +58,7 @@ def lib() -> ctypes.CDLL:
             "dmcp_kv_fork": ([_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _vp], _i),
             "dmcp_pgemm_set_waves": ([_i], _i),
             "dmcp_pgemm_set_bk": ([_i], _i),
+            "dmcp_wgemm_set_aux": ([_i], _i),
             "dmcp_pgemm_set_group": ([_i], _i),
             "dmcp_prefill_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _i, _i,
                                         _i, _vp], _i),
@@ -512,6 +513,14 @@ def pgemm_set_bk(bk: int) -> int:
     if bk not in (64, 128):
         raise HipOpsError(f"pgemm_set_bk: 64 or 128, got {bk}")
     return int(lib().dmcp_pgemm_set_bk(int(bk)))
+
+
+def wgemm_set_aux(aux: int) -> int:
+    """Cache policy of the weight-streaming GEMM's weight loads: 0 (default)
+    or 2 (nt).  Returns the previous value."""
+    if aux not in (0, 2):
+        raise HipOpsError(f"wgemm_set_aux: 0 or 2, got {aux}")
+    return int(lib().dmcp_wgemm_set_aux(int(aux)))
 
 
 def pgemm_set_group(g: int) -> int:

@@ -46,6 +46,8 @@ def main(argv=None) -> int:
     ap.add_argument("--tghead", type=int, default=-1, help="0 = the weight-streaming LM head at every row count")
     ap.add_argument("--tgemm", type=int, default=-1,
                     help="-1 = model default, 0 = hipBLASLt (projections + LM head) for > 512 rows")
+    ap.add_argument("--wgemm-aux", type=int, default=0, choices=[0, 2],
+                    help="cache policy of the weight-streaming GEMM's weight loads (2 = nt)")
     ap.add_argument("--jitter", type=float, default=0.0,
                     help="per-sequence own length uniform in ctx x [1 - j, 1 + j] (the engine's mix of progress)")
     ap.add_argument("--adjacent", action="store_true",
@@ -72,6 +74,7 @@ def main(argv=None) -> int:
         model.tg_head = False
     if a.tghead == 0:
         model.tg_head = False
+    hip.wgemm_set_aux(a.wgemm_aux)
     eng = LocalEngine(model)
     g = torch.Generator().manual_seed(0)
     if a.prefix:
@@ -125,7 +128,7 @@ def main(argv=None) -> int:
     print(json.dumps({"bench": "decode_step", "preset": a.preset, "kv_dtype": a.kv_dtype, "decode_dtype": a.decode_dtype, "rows": n, "batch": a.batch, "prefix": a.prefix,
                       "ctx": a.ctx, "jitter": a.jitter, "adjacent": a.adjacent, "fused": bool(getattr(model, "use_fused", False)),
                       "tgemm": bool(getattr(model, "use_tgemm", False)),
-                      "tg_head": bool(getattr(model, "tg_head", False)),
+                      "tg_head": bool(getattr(model, "tg_head", False)), "wgemm_aux": a.wgemm_aux,
                       "prefix_splits": hip.prefix_mfma_splits(a.batch + a.extra, cfg.n_heads // cfg.n_kv_heads,
                                                               cfg.n_kv_heads),
                       "device_ms": round(dev_ms, 3), "loop_ms": round(loop_ms, 3),

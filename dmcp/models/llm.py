@@ -51,7 +51,6 @@ import time
 from dataclasses import asdict, dataclass, field, replace
 from typing import Dict, List, Optional, Sequence
 
-import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -267,14 +266,6 @@ class LocalLM:
         # decode graphs follow it.
         self.fork_tab = torch.zeros((self.num_slots, 2), dtype=torch.int32, device=self.device)
         self.fork_tab[:, 0] = torch.arange(self.num_slots, dtype=torch.int32, device=self.device)
-        # its host copy: the decode step's row groups (ops.decode_groups) are
-        # built from it on the host
-        self.fork_host = np.zeros((self.num_slots, 2), dtype=np.int32)
-        self.fork_host[:, 0] = np.arange(self.num_slots, dtype=np.int32)
-        # decode attention over row groups (branches of a class, jump rows of a
-        # slot: their shared keys read once per group); LOCAL_LLM_GROUP_ROWS=0
-        # keeps one work item per row (the A/B switch)
-        self.group_rows = os.environ.get("LOCAL_LLM_GROUP_ROWS", "1") != "0"
         # shared prefix: its length in device memory, so captured decode
         # graphs follow it
         self.prefix_len = 0
@@ -532,6 +523,7 @@ class LocalLM:
         if not self.prefill_fp8 and (n == 1 or not (self.use_prefill_kernel or self.device.type == "cpu")):
             return torch.stack([self.forward_tokens(torch.as_tensor(t, dtype=torch.int32), sl, st)
                                 for t, sl, st in reqs])
+        import numpy as np
         offsets = [0]
         starts, seq_slots, shared, lens = [], [], [], []
         for t, sl, st in reqs:
@@ -625,8 +617,7 @@ class LocalLM:
     def decode(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor,
                src: Optional[torch.Tensor] = None, last_ids: Optional[torch.Tensor] = None,
                mask_idx: Optional[torch.Tensor] = None, mask_alt: Optional[torch.Tensor] = None,
-               alt_token: int = -1, prefix_rows: Optional[torch.Tensor] = None,
-               groups: Optional[torch.Tensor] = None) -> torch.Tensor:
+               alt_token: int = -1, prefix_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
         """One token per row; all inputs int32 [B] on device.  With ``src`` /
         ``last_ids``: row r's token is ``last_ids[src[r]]`` where ``src[r] >= 0``
         (gathered on the device by the step's first kernel; with ``mask_alt``
@@ -638,40 +629,28 @@ class LocalLM:
         the SAME slot at consecutive positions (jump-forward over forced
         tokens) -- every row's K/V is appended before attention runs and each
         row attends to positions <= its own, so that is an exact causal
-        extend.  Rows with slot -1 are padding.  ``groups`` (int32 [2, B],
-        :func:`dmcp.ops.decode_groups`): the attention's row groups.  Returns
-        logits [B, vocab] (bf16).  Capturable into a hipGraph."""
+        extend.  Rows with slot -1 are padding.  Returns logits [B, vocab]
+        (bf16).  Capturable into a hipGraph."""
         B = tokens.shape[0]
         if B > self.max_rows:
             raise ValueError(f"decode: {B} rows > max_rows {self.max_rows}")
         if self.use_fused and B <= self.fused_max_rows:
             return self._decode_fused(tokens, slots, positions, src, last_ids, mask_idx, mask_alt, alt_token,
-                                      prefix_rows, groups)
-        h = self._decode_trunk(tokens, slots, positions, src, last_ids, mask_idx, mask_alt, alt_token, prefix_rows,
-                               groups)
+                                      prefix_rows)
+        h = self._decode_trunk(tokens, slots, positions, src, last_ids, mask_idx, mask_alt, alt_token, prefix_rows)
         return F.linear(h, self.w["lm_head"])
 
-    def _attn_plan(self, B: int, groups) -> tuple:
-        """(chunk, splits) of the step's decode attention; with row groups the
-        split-K capacity the per-group split counts may use."""
-        c = self.cfg
-        chunk, splits = ops.decode_plan(B, c.n_kv_heads, c.max_seq, c.kv_dtype)
-        if groups is not None and self.device.type == "cuda":
-            splits = max(splits, ops.GROUP_MAX_SPLITS)
-        return chunk, splits
-
     def _decode_trunk(self, tokens, slots, positions, src, last_ids, mask_idx, mask_alt, alt_token,
-                      prefix_rows, groups=None) -> torch.Tensor:
+                      prefix_rows) -> torch.Tensor:
         """Every layer of a decode step of > ``fused_max_rows`` rows; returns
         the final normalised hidden states [B, hidden] (the LM head's input)."""
         c = self.cfg
         B = tokens.shape[0]
-        chunk, splits = self._attn_plan(B, groups)
+        chunk, splits = ops.decode_plan(B, c.n_kv_heads, c.max_seq, c.kv_dtype)
         resid, h, seq_len = ops.decode_embed_norm(self.w["embed"], tokens, positions, self.w["l0.ln1"], c.eps,
                                                   src, last_ids, mask_idx, mask_alt, alt_token)
         if self.decode_fp8 and (self.device.type == "cpu" or B <= ops.WMX_MAX_ROWS):
-            return self._decode_trunk_fp8(B, resid, h, seq_len, slots, positions, chunk, splits, prefix_rows,
-                                          groups)
+            return self._decode_trunk_fp8(B, resid, h, seq_len, slots, positions, chunk, splits, prefix_rows)
         wide = self.use_wgemm and B <= ops.WGEMM_MAX_ROWS
         big = self.use_tgemm and ops.WGEMM_MAX_ROWS < B <= ops.TGEMM_MAX_ROWS
         mlp_t = self.use_tgemm and self.TGEMM_MLP_MIN_ROWS <= B <= ops.TGEMM_MAX_ROWS
@@ -687,7 +666,7 @@ class LocalLM:
             else:
                 q = ops.rope_kv(F.linear(h, self.w[f"l{i}.wqkv"]), positions, slots, self.cos_sin, kc, vc, c.n_heads)
             att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws, chunk=chunk,
-                                       fork=self.fork_tab, groups=groups,
+                                       fork=self.fork_tab,
                                        prefix=self._prefix(i, prefix_rows), splits=splits).view(B, c.n_heads * c.head_dim)
             if big:
                 h = ops.tgemm_resid_norm(att, self.w[f"l{i}.wo"], resid, self.w[f"l{i}.ln2"], c.eps, self.tg_ws)
@@ -705,8 +684,7 @@ class LocalLM:
                 h = ops.add_rmsnorm(self._mlp(i, h), nxt, c.eps, residual=resid)
         return h
 
-    def _decode_trunk_fp8(self, B, resid, h, seq_len, slots, positions, chunk, splits, prefix_rows,
-                          groups=None) -> torch.Tensor:
+    def _decode_trunk_fp8(self, B, resid, h, seq_len, slots, positions, chunk, splits, prefix_rows) -> torch.Tensor:
         """The layers of a decode step on the fp8 weights: every projection's
         activation is MXFP8 (the step's first norm quantised once, then written
         by the split-K reduction + residual + RMSNorm kernels and the SwiGLU
@@ -727,7 +705,7 @@ class LocalLM:
             else:
                 q = ops.pgemm_qkv(xq, xs, *w8[f"l{i}.wqkv"], positions, slots, self.cos_sin, kc, vc, c.n_heads)
             att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws, chunk=chunk,
-                                       fork=self.fork_tab, groups=groups,
+                                       fork=self.fork_tab,
                                        prefix=self._prefix(i, prefix_rows), splits=splits).view(B, c.hidden)
             aq, as_ = ops.mx_quant(att)
             if gpu:
@@ -757,22 +735,21 @@ class LocalLM:
     def _decode_fused(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor,
                       src: Optional[torch.Tensor] = None, last_ids: Optional[torch.Tensor] = None,
                       mask_idx: Optional[torch.Tensor] = None, mask_alt: Optional[torch.Tensor] = None,
-                      alt_token: int = -1, prefix_rows: Optional[torch.Tensor] = None,
-                      groups: Optional[torch.Tensor] = None) -> torch.Tensor:
+                      alt_token: int = -1, prefix_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
         """The decode step on the fused gfx950 GEMMs: per layer QKV (+norm,
         RoPE, KV append) -> attention -> O (+residual) -> gate/up (+norm,
         SwiGLU) -> down (+residual); the residual stream ``r`` is updated in
         place by the O / down epilogues."""
         c = self.cfg
         B = tokens.shape[0]
-        chunk, splits = self._attn_plan(B, groups)
+        chunk, splits = ops.decode_plan(B, c.n_kv_heads, c.max_seq, c.kv_dtype)
         r, _, seq_len = ops.decode_embed_norm(self.w["embed"], tokens, positions, None, c.eps, src, last_ids,
                                               mask_idx, mask_alt, alt_token)
         for i in range(c.layers):
             kc, vc = self.k_cache[i], self.v_cache[i]
             q = ops.fused_rope_kv(r, self.w[f"l{i}.wqkv"], c.eps, positions, slots, self.cos_sin, kc, vc, c.n_heads)
             att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws, chunk=chunk,
-                                       fork=self.fork_tab, groups=groups,
+                                       fork=self.fork_tab,
                                        prefix=self._prefix(i, prefix_rows), splits=splits)
             ops.fused_resid(att.view(B, c.n_heads * c.head_dim), self.w[f"l{i}.wo"], r)
             act = ops.fused_swiglu(r, self.w[f"l{i}.wgu"], c.eps)
@@ -857,7 +834,6 @@ class LocalLM:
             raise ValueError(f"fork_share: slot {src} -> {dl}, end {end}")
         vals = torch.tensor([[int(src), int(end)]] * len(dl), dtype=torch.int32)
         idx = torch.tensor(dl, dtype=torch.long)
-        self.fork_host[dl] = (int(src), int(end))
         if self.device.type == "cuda":
             vals, idx = vals.to(self.device, non_blocking=True), idx.to(self.device, non_blocking=True)
         self.fork_tab.index_copy_(0, idx, vals)
@@ -866,7 +842,6 @@ class LocalLM:
     def fork_reset(self) -> None:
         """No slot has a parent (every slot owns all its keys)."""
         self.fork_tab[:, 1] = 0
-        self.fork_host[:, 1] = 0
 
     @torch.inference_mode()
     def fork_clear(self, slots: Sequence[int]) -> None:
@@ -876,8 +851,6 @@ class LocalLM:
             return
         vals = torch.tensor([[x, 0] for x in sl], dtype=torch.int32)
         idx = torch.tensor(sl, dtype=torch.long)
-        self.fork_host[sl, 0] = sl
-        self.fork_host[sl, 1] = 0
         if self.device.type == "cuda":
             vals, idx = vals.to(self.device, non_blocking=True), idx.to(self.device, non_blocking=True)
         self.fork_tab.index_copy_(0, idx, vals)
@@ -894,8 +867,7 @@ class LocalLM:
     def decode_select_gather(self, tokens: torch.Tensor, src: torch.Tensor, last_ids: torch.Tensor,
                              slots: torch.Tensor, positions: torch.Tensor, masks: torch.Tensor,
                              mask_idx: torch.Tensor, mask_alt: Optional[torch.Tensor] = None,
-                             alt_token: int = -1, prefix_rows: Optional[torch.Tensor] = None,
-                             groups: Optional[torch.Tensor] = None) -> tuple:
+                             alt_token: int = -1, prefix_rows: Optional[torch.Tensor] = None) -> tuple:
         """:meth:`decode_select` whose input token of row r is ``last_ids[src[r]]``
         where ``src[r] >= 0`` (the previous step's selection, still on the
         device) and ``tokens[r]`` otherwise; the step's own selections are
@@ -908,7 +880,7 @@ class LocalLM:
             # the LM head + grammar-masked selection in one weight-streaming
             # kernel: no [B, vocab] logits (returned as None)
             h = self._decode_trunk(tokens, slots, positions, src, last_ids, mask_idx, mask_alt, alt_token,
-                                   prefix_rows, groups)
+                                   prefix_rows)
             if self.tg_head and B >= self.TGEMM_HEAD_MIN_ROWS:
                 ids = ops.tgemm_lm_head_argmax(h, self.w["lm_head"], masks, mask_idx, out=last_ids[:B],
                                                workspace=self.tg_head_ws)
@@ -917,7 +889,7 @@ class LocalLM:
                                          workspace=self.head_ws)
             return None, ids
         logits = self.decode(tokens, slots, positions, src=src, last_ids=last_ids, mask_idx=mask_idx,
-                             mask_alt=mask_alt, alt_token=alt_token, prefix_rows=prefix_rows, groups=groups)
+                             mask_alt=mask_alt, alt_token=alt_token, prefix_rows=prefix_rows)
         ids = ops.masked_argmax(logits, masks, vocab=self.cfg.vocab_size, mask_idx=mask_idx, out=last_ids[:B])
         return logits, ids
 
@@ -998,7 +970,7 @@ class _Bucket:
     def __init__(self, graph, inp, logits, ids, b: int) -> None:
         self.graph, self.inp, self.logits, self.ids = graph, inp, logits, ids
         self.kernels = graph_kernel_nodes(graph)
-        self.stage = [torch.zeros((9, b), dtype=torch.int32).pin_memory() for _ in range(2)]
+        self.stage = [torch.zeros((7, b), dtype=torch.int32).pin_memory() for _ in range(2)]
         self.np = [t.numpy() for t in self.stage]
         self.copied = [torch.cuda.Event(), torch.cuda.Event()]
         self.turn = 0
@@ -1013,11 +985,9 @@ class _Bucket:
 class DecodeGraphs:
     """hipGraph-captured decode + selection steps, one graph per row-count bucket.
 
-    Inputs travel as ONE packed int32 host buffer ``[9, n]`` (token, slot,
+    Inputs travel as ONE packed int32 host buffer ``[7, n]`` (token, slot,
     position, mask row, token source, mask row if the gathered token is
-    ``alt_token``, uses-the-shared-prefix flag, and the attention's two row-group
-    rows built here from the slots and ``LocalLM.fork_host``:
-    :func:`dmcp.ops.decode_groups`) -> one H2D copy into the graph's static
+    ``alt_token``, uses-the-shared-prefix flag) -> one H2D copy into the graph's static
     input; the graph gathers the rows whose source is >= 0 from the previous
     step's selections (:attr:`last_ids`, device-resident, written by every
     step), runs the whole forward plus the masked argmax, so a step costs one
@@ -1031,7 +1001,7 @@ class DecodeGraphs:
         self.model = model
         self.masks = masks
         self.alt_token = int(alt_token)
-        self.timing = {"sync_s": 0.0, "replay_s": 0.0, "groups_s": 0.0}  # host time in run(): staging wait, H2D + launch, row groups
+        self.timing = {"sync_s": 0.0, "replay_s": 0.0}  # host time inside run(): staging wait, H2D + launch
         # device witness: graph replays and the kernel nodes they launched
         self.counts = {"graph_replays": 0, "graph_kernels": 0}
         self.buckets = sorted(b for b in buckets if b <= model.max_rows)
@@ -1049,25 +1019,24 @@ class DecodeGraphs:
 
     def _capture(self, b: int):
         m = self.model
-        inp = torch.zeros((9, b), dtype=torch.int32, device=m.device)
+        inp = torch.zeros((7, b), dtype=torch.int32, device=m.device)
         inp[1].fill_(-1)
         inp[4].fill_(-1)
         inp[5].fill_(-1)
-        inp[7].copy_(torch.arange(b, dtype=torch.int32, device=m.device))  # every row its own group
         scratch = torch.zeros_like(self.last_ids)  # warm-up must not clobber last_ids
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):  # warm up hipBLASLt heuristics / allocator outside capture
                 m.decode_select_gather(inp[0], inp[4], scratch, inp[1], inp[2], self.masks, inp[3], inp[5],
-                                       self.alt_token, inp[6], inp[7:9])
+                                       self.alt_token, inp[6])
         torch.cuda.current_stream().wait_stream(s)
         # keep_graph: the hipGraph_t stays queryable after capture (the kernel
         # node count of the witness); instantiated explicitly right after
         g = torch.cuda.CUDAGraph(keep_graph=True)
         with torch.cuda.graph(g):
             logits, ids = m.decode_select_gather(inp[0], inp[4], self.last_ids, inp[1], inp[2], self.masks, inp[3],
-                                                 inp[5], self.alt_token, inp[6], inp[7:9])
+                                                 inp[5], self.alt_token, inp[6])
         bucket = _Bucket(g, inp, logits, ids, b)
         g.instantiate()
         self.graphs[b] = bucket
@@ -1108,7 +1077,6 @@ class DecodeGraphs:
         st[4, :n] = srcs
         st[5, :n] = alts
         st[6, :n] = prefix_rows
-        self._groups(st, n, b)
         return self._replay(b, n)
 
     @torch.inference_mode()
@@ -1119,28 +1087,8 @@ class DecodeGraphs:
         if b not in self.graphs:
             self._capture(b)
         st = self.graphs[b].stage_for_write(self.timing)
-        st[:7, :n] = rows[:7, :n]
-        self._groups(st, n, b)
+        st[:, :n] = rows[:, :n]
         return self._replay(b, n)
-
-    def _groups(self, st, n: int, b: int) -> None:
-        """Rows 7-8 of a step: the decode attention's row groups
-        (:func:`dmcp.ops.decode_groups`), or -- ``LocalLM.group_rows`` off --
-        every row its own group with the split count the per-row plan of a
-        ``b``-row step gives it."""
-        m, c = self.model, self.model.cfg
-        t0 = time.perf_counter()
-        target = 2048 if c.kv_dtype == "fp8" else 4096
-        if m.group_rows:
-            ops.decode_groups(st[1, :n], st[2, :n], st[6, :n], m.fork_host, m.prefix_len, c.n_heads, c.n_kv_heads,
-                              target_waves=target, out=st[7:9, :n])
-        else:
-            _, splits = ops.decode_plan(b, c.n_kv_heads, c.max_seq, c.kv_dtype)
-            own = np.maximum(st[2, :n].astype(np.int64) + 1 - np.where(st[6, :n] != 0, m.prefix_len, 0), 1)
-            ns = np.minimum(splits, -(-own // 256))
-            st[7, :n] = (np.arange(n, dtype=np.int64) | (ns << 16)).astype(np.int32)
-            st[8, :n] = 0
-        self.timing["groups_s"] += time.perf_counter() - t0
 
     def _replay(self, b: int, n: int) -> tuple:
         bk = self.graphs[b]
@@ -1149,8 +1097,6 @@ class DecodeGraphs:
             st[1, n:] = -1
             st[4, n:] = -1
             st[5, n:] = -1
-            st[7, n:] = np.arange(n, b, dtype=np.int32)
-            st[8, n:] = 0
         t0 = time.perf_counter()
         bk.inp.copy_(bk.stage[bk.turn], non_blocking=True)
         bk.copied[bk.turn].record()

@@ -20,7 +20,6 @@ from .hip import (PGEMM_TILE_N, WMX_MAX_ROWS, pgemm_supported, wgemm_mx_resid_no
                   wgemm_mx_swiglu, wmx_plan)
 from .hip import (TGEMM_MAX_ROWS, tgemm_lm_head_argmax, tgemm_resid_norm, tgemm_rope_kv, tgemm_swiglu,  # noqa: F401
                   wgemm)
-from .hip import GROUP_MAX_SPLITS, decode_groups  # noqa: F401
 from .reference import SharedPrefix, mx_dequant, quantize_weight, rope_tables, weight_dequant  # noqa: F401
 
 
@@ -39,12 +38,11 @@ def rope_kv(qkv, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out=None):
 
 
 def decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace=None, chunk: int = 256, out=None,
-                     prefix=None, splits=None, fork=None, groups=None):
+                     prefix=None, splits=None, fork=None):
     if q.is_cuda:
         return hip.decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace, chunk, out, prefix, splits,
-                                    fork, groups)
-    return reference.decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace, chunk, out, prefix, fork,
-                                      groups)
+                                    fork)
+    return reference.decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace, chunk, out, prefix, fork)
 
 
 def prefill_attention(q, k_cache, v_cache, slot, start, prefix_slot=None, prefix_len=0, scale=1.0, out=None,

@@ -39,138 +39,6 @@ __device__ __forceinline__ SplitGeom split_geom(int Ls, int splits, int chunk) {
     return {n, part};
 }
 
-// ---- row groups of the per-row decode attention.  Rows whose keys up to
-// some position are the SAME cache bytes -- the method branches of one class
-// (their keys below the fork point are the class head's, read in place
-// through the fork table) and the jump-forward rows of one slot -- share one
-// work item: their query heads sit side by side in the MFMA's 16 columns
-// (G heads per row, 16 / G rows), so the shared keys stream from memory once
-// per group instead of once per row; each row's own keys after the shared
-// range follow in the same wave with the other rows' columns masked.
-// Host encoding (dmcp.ops.hip.decode_groups), per row b:
-//   g7[b] & 0xffff  the row leading b's group (b itself for a leader)
-//   g7[b] >> 16     (leaders) key splits of the group's shared keys (0: the default plan)
-//   g8[b]           (leaders) extra rows (2 bits) + up to 3 row indices (10 bits each)
-// Decoded defensively: a row counts as a member only if its own g7 names the
-// leader, so any table covers every row exactly once (a row no leader claims
-// is a group of one) -- a bad table costs speed, never correctness.
-constexpr int kGrpMax = 4;
-
-struct RowGroup {
-    int n;  // rows; 0 = b is covered by its leader's item
-    int row[kGrpMax];
-    int nsplit;
-};
-
-__device__ __forceinline__ int grp_member(unsigned w, int j) { return (int)((w >> (2 + 10 * j)) & 1023u); }
-
-__device__ __forceinline__ RowGroup row_group(int b, const int32_t* __restrict__ g7, const int32_t* __restrict__ g8,
-                                              int B, int cap) {
-    RowGroup g;
-    g.n = 1;
-    g.nsplit = 0;
-#pragma unroll
-    for (int j = 0; j < kGrpMax; ++j) g.row[j] = b;
-    if (!g7) return g;
-    const int v = __builtin_amdgcn_readfirstlane(g7[b]);
-    const int lead = v & 0xffff;
-    if (lead != b) {  // a member of lead's group if lead lists it
-        if (lead < B && (__builtin_amdgcn_readfirstlane(g7[lead]) & 0xffff) == lead) {
-            const unsigned w = (unsigned)__builtin_amdgcn_readfirstlane(g8[lead]);
-            const int ne = min((int)(w & 3u), cap - 1);
-#pragma unroll
-            for (int j = 0; j < kGrpMax - 1; ++j)
-                if (j < ne && grp_member(w, j) == b) g.n = 0;
-        }
-        return g;
-    }
-    g.nsplit = (int)((unsigned)v >> 16);
-    const unsigned w = (unsigned)__builtin_amdgcn_readfirstlane(g8[b]);
-    const int ne = min((int)(w & 3u), cap - 1);
-#pragma unroll
-    for (int j = 0; j < kGrpMax - 1; ++j) {
-        if (j >= ne) break;
-        const int m = grp_member(w, j);
-        bool ok = m < B && m != b && (__builtin_amdgcn_readfirstlane(g7[m]) & 0xffff) == b;
-#pragma unroll
-        for (int i = 1; i < kGrpMax; ++i) ok = ok && !(i < g.n && g.row[i] == m);
-        // static indices only (g.row[g.n] would be a scratch store)
-#pragma unroll
-        for (int i = 1; i < kGrpMax; ++i) g.row[i] = (ok && g.n == i) ? m : g.row[i];
-        g.n += ok ? 1 : 0;
-    }
-    return g;
-}
-
-// the first key >= P at which rows a and b read different bytes (key k of a
-// row lives in slot p below its fork end f, in its own slot s from there);
-// INT_MAX when none
-__device__ __forceinline__ int compat_end(int P, int pa, int fa, int sa, int pb, int fb, int sb) {
-    const int lo = max(P, min(fa, fb)), hi = max(P, max(fa, fb));
-    const int pts[3] = {P, lo, hi};
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const int k = pts[i];
-        if ((k < fa ? pa : sa) != (k < fb ? pb : sb)) return k;
-    }
-    return 0x7fffffff;
-}
-
-// a group's rows (wave-uniform): slot, live length, prefix keys, key source
-// (parent slot + fork end, 0 = none); the shared keys [P[0], se) are read
-// from the leader's source for every row (its fork-table view equals theirs
-// there); `broken` (rows disagree on the prefix, a dead row) = nothing shared
-struct GroupGeom {
-    int n;
-    int s[kGrpMax], L[kGrpMax], P[kGrpMax], ps[kGrpMax], fe[kGrpMax];
-    int se, nact, part;
-    bool broken;
-};
-
-__device__ __forceinline__ GroupGeom group_geom(const RowGroup& g, const int32_t* __restrict__ slot,
-                                                const int32_t* __restrict__ seq_len, const int32_t* __restrict__ fork,
-                                                const int32_t* __restrict__ prow, int P0, int max_seq, int num_slots,
-                                                int splits, int chunk) {
-    GroupGeom r;
-    r.n = g.n;
-#pragma unroll
-    for (int j = 0; j < kGrpMax; ++j) {
-        r.s[j] = -1; r.L[j] = 0; r.P[j] = P0; r.ps[j] = -1; r.fe[j] = 0;
-        if (j >= g.n) continue;
-        const int b = g.row[j];
-        const int s = __builtin_amdgcn_readfirstlane(slot[b]);
-        const bool ok = s >= 0 && s < num_slots;
-        const int L = ok ? __builtin_amdgcn_readfirstlane(min(seq_len[b], max_seq)) : 0;
-        r.s[j] = s;
-        r.L[j] = L;
-        r.ps[j] = s;
-        if (prow && !__builtin_amdgcn_readfirstlane(prow[b])) r.P[j] = 0;
-        if (fork && L > 0) {
-            const int p = __builtin_amdgcn_readfirstlane(fork[2 * s]);
-            const int e = __builtin_amdgcn_readfirstlane(fork[2 * s + 1]);
-            if (e > 0 && p >= 0 && p < num_slots && p != s) {
-                r.ps[j] = p;
-                r.fe[j] = min(e, L);
-            }
-        }
-    }
-    int se = r.L[0];
-    bool broken = r.L[0] <= 0;
-#pragma unroll
-    for (int j = 1; j < kGrpMax; ++j) {
-        if (j >= g.n) break;
-        broken = broken || r.L[j] <= 0 || r.P[j] != r.P[0];
-        se = min(se, min(r.L[j], compat_end(r.P[0], r.ps[0], r.fe[0], r.s[0], r.ps[j], r.fe[j], r.s[j])));
-    }
-    r.broken = broken;
-    r.se = broken ? r.P[0] : max(se, r.P[0]);
-    const SplitGeom sg = g.nsplit > 0 ? split_geom(r.se - r.P[0], min(g.nsplit, splits), 32)
-                                      : split_geom(r.se - r.P[0], splits, chunk);
-    r.nact = max(1, sg.nact);
-    r.part = sg.part;
-    return r;
-}
-
 // --------------------------------------------------------------------------
 // 1. fused residual-add + RMSNorm:  h = x (+ residual);  residual <- h;
 //    out = h * rsqrt(mean(h^2) + eps) * w.  One block per row, VPT 16-B
@@ -339,10 +207,7 @@ __global__ __launch_bounds__(kBlock) void decode_attn_combine_kernel(const float
                                                                     uint16_t* __restrict__ out, int B, int Hq,
                                                                     int max_seq, int chunk, int splits,
                                                                     int num_slots, const int32_t* __restrict__ plen,
-                                                                    int ps_max, const int32_t* __restrict__ prow,
-                                                                    const int32_t* __restrict__ fork,
-                                                                    const int32_t* __restrict__ g7,
-                                                                    const int32_t* __restrict__ g8, int cap) {
+                                                                    int ps_max, const int32_t* __restrict__ prow) {
     constexpr int U = 8;
     constexpr int DQ = D / 4;       // lanes per partial group
     constexpr int PG = kWave / DQ;  // partial groups per wave
@@ -362,10 +227,7 @@ __global__ __launch_bounds__(kBlock) void decode_attn_combine_kernel(const float
         // the shared prefix's ps_max partials (prefill kernel in prefix mode;
         // splits past the prefix's end are empty and weigh 0)
         const int npre = P > 0 ? ps_max : 0;
-        // the split count of the row's group (a group of one: split_geom(L - P))
-        RowGroup rg = row_group(b, g7, g8, B, cap);
-        if (rg.n == 0) rg = row_group(__builtin_amdgcn_readfirstlane(g7[b]) & 0xffff, g7, g8, B, cap);
-        const int nact = group_geom(rg, slot, seq_len, fork, prow, P0, max_seq, num_slots, splits, chunk).nact;
+        const int nact = split_geom(L - P, splits, chunk).nact;
         if (nact <= 1) continue;  // finished by the main kernel (directly, or merging the prefix partials)
         const int n = npre + nact;
         const size_t base = ((size_t)b * Hq + qh) * splits_total;
@@ -700,15 +562,13 @@ __device__ __forceinline__ int vquad(int r, int q) {
 
 // One tile of the MFMA per-row kernel: V -> the wave's LDS tile, S^T on the
 // matrix cores, then (prefetch) the tile two ahead is loaded into the same
-// registers while the softmax and the PV product run.  MASKCOL: only the
-// query columns with `act` set take these keys (a grouped row's own keys);
-// the others keep their running max / sum / output untouched.
-template <int D, bool KV8, bool MASKCOL = false>
+// registers while the softmax and the PV product run.
+template <int D, bool KV8>
 __device__ __forceinline__ void attn_tile_mfma(KVTile<D, KV8>& cur, bool prefetch, int kt_next, const KVSrc& src,
                                                int kt, int end, int lane, int g16, uint16_t* vw,
                                                const uint16_t* tr0, int trk, int tr_half,
                                                const bf16x8_t (&qf)[D / 32], float& m, float& l,
-                                               f32x4_t (&acc)[D / 16], float scale_log2, bool act = true) {
+                                               f32x4_t (&acc)[D / 16], float scale_log2) {
     constexpr int KS = D / 32;
     constexpr int DB = D / 16;
     const bool partial = kt + 32 > end;
@@ -768,7 +628,7 @@ __device__ __forceinline__ void attn_tile_mfma(KVTile<D, KV8>& cur, bool prefetc
     }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 16, kWave));
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, kWave)) * scale_log2;
-    const float mn = (MASKCOL && !act) ? m : fmaxf(m, tmax);
+    const float mn = fmaxf(m, tmax);
     if (__any(mn > m)) {
         const float corr = __builtin_amdgcn_exp2f(m - mn);
         l *= corr;
@@ -781,10 +641,8 @@ __device__ __forceinline__ void attn_tile_mfma(KVTile<D, KV8>& cur, bool prefetc
     for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            float p = __builtin_amdgcn_exp2f(fmaf(sacc[h][i], scale_log2, -mn));
-            if constexpr (MASKCOL) p = act ? p : 0.f;
-            pr[4 * h + i] = p;
-            l += p;  // lane-partial sum; the 4 groups are added once at the end
+            pr[4 * h + i] = __builtin_amdgcn_exp2f(fmaf(sacc[h][i], scale_log2, -mn));
+            l += pr[4 * h + i];  // lane-partial sum; the 4 groups are added once at the end
         }
     // B operand P^T: element j = key pi(8*g16 + j) = 16*(j>>2) + 4*g16 + (j&3)
     const bf16x8_t pf = __builtin_convertvector(pr, bf16x8_t);
@@ -842,8 +700,7 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
     const int32_t* __restrict__ slot, const int32_t* __restrict__ seq_len, uint16_t* __restrict__ out,
     float* __restrict__ part_o, float* __restrict__ part_ml, int B, int Hkv, int G,
     int max_seq, int chunk, int splits, float scale_log2, int num_slots, const int32_t* __restrict__ plen,
-    int ps_max, const int32_t* __restrict__ prow, const int32_t* __restrict__ fork, const int32_t* __restrict__ g7,
-    const int32_t* __restrict__ g8) {
+    int ps_max, const int32_t* __restrict__ prow, const int32_t* __restrict__ fork) {
     static_assert(D % 32 == 0, "D must be a multiple of 32");
     constexpr int KS = D / 32;    // 32-dim k-steps of the S product
     constexpr int DB = D / 16;    // 16-row d blocks of O^T
@@ -868,99 +725,66 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
     const int trk = tsw >> 2;
     // D = 128 swapped halves: quad p ^ 2 of the group, as an element offset
     const int tr_half = (c & 2) ? -8 : 8;
-    // row groups: lane column c is query head c % G of the group's row c / G
-    const int cap = min(kGrpMax, 16 / G);
-    const int cj = c / G, chq = c - cj * G;
     for (int item = blockIdx.x * NW + wave; item < total; item += gridDim.x * NW) {
         // split-major: consecutive waves take different rows' splits, so the
         // persistent grid's first pass covers every row
         const int split = item / (B * Hkv);
         const int rem = item - split * (B * Hkv);
         const int b = rem / Hkv, kh = rem - b * Hkv;
-        const RowGroup rg = row_group(b, g7, g8, B, cap);
-        if (rg.n == 0) continue;  // its leader's item covers this row
-        const GroupGeom gg = group_geom(rg, slot, seq_len, fork, prow, P0, max_seq, num_slots, splits, chunk);
-        if (split >= gg.nact) continue;
-        if (split == 0) {  // padding row / bad slot: defined output, nothing read
-#pragma unroll
-            for (int j = 0; j < kGrpMax; ++j)
-                if (j < gg.n && gg.L[j] <= 0)
-                    for (int o = lane; o < G * D; o += kWave) out[((size_t)rg.row[j] * Hq + kh * G) * D + o] = 0;
+        const int s = __builtin_amdgcn_readfirstlane(slot[b]);
+        const int L = __builtin_amdgcn_readfirstlane((s >= 0 && s < num_slots) ? min(seq_len[b], max_seq) : 0);
+        if (L <= 0) {  // padding row / bad slot: defined output, nothing read
+            if (split == 0)
+                for (int o = lane; o < G * D; o += kWave) out[((size_t)b * Hq + kh * G) * D + o] = 0;
+            continue;
         }
-        // this lane's column: row, length, prefix keys (a select chain, not a
-        // dynamically indexed array: no scratch)
-        auto pick = [&](const int(&a)[kGrpMax]) { return cj == 0 ? a[0] : cj == 1 ? a[1] : cj == 2 ? a[2] : a[3]; };
-        const bool col = cj < gg.n;
-        const int crow = pick(rg.row), cL = pick(gg.L), cP = pick(gg.P);
+        // a row outside the shared prefix (prow[b] == 0) owns all its keys
+        const int P = __builtin_amdgcn_readfirstlane((prow && !prow[b]) ? 0 : P0);
+        const SplitGeom sg = split_geom(L - P, splits, chunk);
+        if (split >= max(1, sg.nact)) continue;
+        // one own split: this wave writes the row's final output -- directly,
+        // or (shared prefix) after merging the prefix kernel's partials, which
+        // the same stream finished before this launch (no combine pass)
+        const bool direct = P == 0 && sg.nact == 1;
+        const bool merge_prefix = P > 0 && sg.nact <= 1;
+        const int start = P + split * sg.part;
+        const int end = min(L, start + sg.part);
+        const int ntiles = (end - start + 31) / 32;
         bf16x8_t qf[KS];
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             uint4 v = make_uint4(0, 0, 0, 0);
-            if (col && cL > 0)
-                v = *reinterpret_cast<const uint4*>(q + ((size_t)crow * Hq + kh * G + chq) * D + 32 * ks + 8 * g16);
+            if (c < G) v = *reinterpret_cast<const uint4*>(q + ((size_t)b * Hq + kh * G + c) * D + 32 * ks + 8 * g16);
             qf[ks] = as_bf16x8(v);
         }
-        // member j's keys: its own slot, the parent's below its fork end
-        // uniform index j: scalar selects (a dynamically indexed array would go to scratch)
-        auto upick = [](const int(&a)[kGrpMax], int j) { return j == 0 ? a[0] : j == 1 ? a[1] : j == 2 ? a[2] : a[3]; };
-        auto kvsrc = [&](int j) -> KVSrc {
-            const size_t off = ((size_t)upick(gg.s, j) * Hkv + kh) * (size_t)max_seq * D;
-            KVSrc r{kv_at<KV8>(k_cache, off), kv_at<KV8>(v_cache, off), nullptr, nullptr, 0};
-            const int fe = upick(gg.fe, j);
-            if (fe > 0) {
-                const size_t poff = ((size_t)upick(gg.ps, j) * Hkv + kh) * (size_t)max_seq * D;
-                r.pk = kv_at<KV8>(k_cache, poff);
-                r.pv = kv_at<KV8>(v_cache, poff);
-                r.fend = fe;
+        const size_t head_off = ((size_t)s * Hkv + kh) * (size_t)max_seq * D;
+        KVSrc src{kv_at<KV8>(k_cache, head_off), kv_at<KV8>(v_cache, head_off), nullptr, nullptr, 0};
+        if (fork) {  // fork[2 s] = parent slot, fork[2 s + 1] = the end of the shared keys
+            const int ps = __builtin_amdgcn_readfirstlane(fork[2 * s]);
+            const int fe = __builtin_amdgcn_readfirstlane(fork[2 * s + 1]);
+            if (fe > 0 && ps >= 0 && ps < num_slots && ps != s) {
+                const size_t poff = ((size_t)ps * Hkv + kh) * (size_t)max_seq * D;
+                src.pk = kv_at<KV8>(k_cache, poff);
+                src.pv = kv_at<KV8>(v_cache, poff);
+                src.fend = min(fe, L);
             }
-            return r;
-        };
+        }
         float m = -1e30f, l = 0.f;
         f32x4_t acc[DB];
 #pragma unroll
         for (int db = 0; db < DB; ++db) acc[db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
         KVTile<D, KV8> ta;
-        // the shared keys: this split's part, every row's columns at once
-        const int P = gg.P[0];
-        if (gg.se > P) {
-            const int start = P + split * gg.part;
-            const int end = min(gg.se, start + gg.part);
-            const int ntiles = (end - start + 31) / 32;
-            const KVSrc src = kvsrc(0);
-            load_kv_tile<D, KV8>(src, start, end, lane, ta);
-            for (int t = 0; t < ntiles; ++t) {
-                const int kt = start + 32 * t;
-                attn_tile_mfma<D, KV8>(ta, t + 1 < ntiles, kt + 32, src, kt, end, lane, g16, vw, tr0, trk, tr_half, qf,
-                                       m, l, acc, scale_log2);
-            }
-        }
-        // each row's own keys after them (rows dealt over the splits), the
-        // other rows' columns masked
-#pragma unroll 1
-        for (int j = 0; j < gg.n; ++j) {
-            if (j % gg.nact != split) continue;
-            const int os = gg.broken ? upick(gg.P, j) : gg.se;
-            const int end = upick(gg.L, j);
-            if (end <= os) continue;
-            const int ntiles = (end - os + 31) / 32;
-            const KVSrc src = kvsrc(j);
-            const bool act = col && cj == j;
-            load_kv_tile<D, KV8>(src, os, end, lane, ta);
-            for (int t = 0; t < ntiles; ++t) {
-                const int kt = os + 32 * t;
-                attn_tile_mfma<D, KV8, true>(ta, t + 1 < ntiles, kt + 32, src, kt, end, lane, g16, vw, tr0, trk,
-                                             tr_half, qf, m, l, acc, scale_log2, act);
-            }
+        load_kv_tile<D, KV8>(src, start, end, lane, ta);
+        for (int t = 0; t < ntiles; ++t) {
+            const int kt = start + 32 * t;
+            attn_tile_mfma<D, KV8>(ta, t + 1 < ntiles, kt + 32, src, kt, end, lane, g16, vw, tr0, trk, tr_half, qf, m, l,
+                                   acc, scale_log2);
         }
         l += __shfl_xor(l, 16, kWave);
         l += __shfl_xor(l, 32, kWave);
-        // one split: this wave writes the row's final output -- directly, or
-        // (shared prefix) after merging the prefix kernel's partials, which
-        // the same stream finished before this launch (no combine pass)
-        const bool one = gg.nact == 1;
-        if (col && cL > 0 && one && cP > 0) {
-            const int qh = kh * G + chq;
-            const size_t pb = ((size_t)crow * Hq + qh) * splits_total;
+        if (c < G && merge_prefix) {
+            const int qh = kh * G + c;
+            const size_t pb = ((size_t)b * Hq + qh) * splits_total;
             // online log-sum-exp merge of the ps_max prefix partials into
             // this wave's (m, l, acc) -- the combine kernel's arithmetic
             for (int sp = 0; sp < ps_max; ++sp) {
@@ -982,19 +806,18 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
 #pragma unroll
             for (int db = 0; db < DB; ++db) {
                 const float f[4] = {acc[db][0] * inv, acc[db][1] * inv, acc[db][2] * inv, acc[db][3] * inv};
-                *reinterpret_cast<uint2*>(out + ((size_t)crow * Hq + qh) * D + 16 * db + 4 * g16) = pack4(f);
+                *reinterpret_cast<uint2*>(out + ((size_t)b * Hq + qh) * D + 16 * db + 4 * g16) = pack4(f);
             }
-        } else if (col && cL > 0) {
-            const int qh = kh * G + chq;
-            const bool direct = one;  // cP == 0 here
+        } else if (c < G) {
+            const int qh = kh * G + c;
             const float inv = l > 0.f ? 1.f / l : 0.f;
-            const size_t pi = ((size_t)crow * Hq + qh) * splits_total + ps_max + split;
+            const size_t pi = ((size_t)b * Hq + qh) * splits_total + ps_max + split;
 #pragma unroll
             for (int db = 0; db < DB; ++db) {
                 const int d0 = 16 * db + 4 * g16;
                 if (direct) {
                     const float f[4] = {acc[db][0] * inv, acc[db][1] * inv, acc[db][2] * inv, acc[db][3] * inv};
-                    *reinterpret_cast<uint2*>(out + ((size_t)crow * Hq + qh) * D + d0) = pack4(f);
+                    *reinterpret_cast<uint2*>(out + ((size_t)b * Hq + qh) * D + d0) = pack4(f);
                 } else {
                     *reinterpret_cast<float4*>(part_o + pi * D + d0) =
                         make_float4(acc[db][0], acc[db][1], acc[db][2], acc[db][3]);
@@ -1029,19 +852,18 @@ inline int grid_for(size_t work) {
 
 hipError_t launch_combine(void* part_o, void* part_ml, const int32_t* sl, const int32_t* ln, void* out, int B, int Hq,
                           int D, int max_seq, int chunk, int splits, int num_slots, const int32_t* pl, int ps_max,
-                          const int32_t* pr, const int32_t* fork, const int32_t* g7, const int32_t* g8, int cap,
-                          hipStream_t st) {
+                          const int32_t* pr, hipStream_t st) {
     const int waves = B * Hq;
     const int blocks = (waves + 3) / 4;
     const dim3 grid((unsigned)(blocks < 2048 ? blocks : 2048));
     if (D == 64)
         decode_attn_combine_kernel<64><<<grid, kBlock, 0, st>>>((const float*)part_o, (const float*)part_ml, sl, ln,
                                                                (uint16_t*)out, B, Hq, max_seq, chunk, splits,
-                                                               num_slots, pl, ps_max, pr, fork, g7, g8, cap);
+                                                               num_slots, pl, ps_max, pr);
     else if (D == 128)
         decode_attn_combine_kernel<128><<<grid, kBlock, 0, st>>>((const float*)part_o, (const float*)part_ml, sl, ln,
                                                                 (uint16_t*)out, B, Hq, max_seq, chunk, splits,
-                                                                num_slots, pl, ps_max, pr, fork, g7, g8, cap);
+                                                                num_slots, pl, ps_max, pr);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
@@ -1083,7 +905,7 @@ __global__ __launch_bounds__(kBlock) void kv_fork_kernel(uint8_t* __restrict__ k
 
 extern "C" {
 
-int dmcp_abi_version() { return 16; }
+int dmcp_abi_version() { return 15; }
 
 int dmcp_add_rmsnorm(const void* x, void* residual, const void* w, void* out, int rows, int H, float eps,
                      void* stream) {
@@ -1129,7 +951,7 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
                           const void* seq_len, void* out, void* part_o, void* part_ml, int B, int Hq, int Hkv, int D,
                           int max_seq, int num_slots, int chunk, int splits, float scale, const void* prefix_k,
                           const void* prefix_v, const void* plen, int ps_max, int kv8, const void* prefix_rows,
-                          const void* fork, const void* grp7, const void* grp8, void* stream) {
+                          const void* fork, void* stream) {
     if (B <= 0) return 0;
     if (Hkv <= 0 || Hq % Hkv != 0 || splits <= 0 || chunk <= 0 || !(D == 64 || D == 128) || Hq / Hkv > 16)
         return hipErrorInvalidValue;
@@ -1137,10 +959,7 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
     if (prefix && (!prefix_k || !prefix_v || ps_max <= 0)) return hipErrorInvalidValue;
     if (!prefix) ps_max = 0;
     if ((splits > 1 || prefix) && (!part_o || !part_ml)) return hipErrorInvalidValue;
-    if ((grp7 == nullptr) != (grp8 == nullptr) || (grp7 && B > 1024)) return hipErrorInvalidValue;
     const int G = Hq / Hkv;
-    auto g7 = (const int32_t*)grp7;
-    auto g8 = (const int32_t*)grp8;
     const float sl2 = scale * 1.4426950408889634f;
     auto st = (hipStream_t)stream;
     auto qq = (const uint16_t*)q;
@@ -1173,7 +992,7 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
         const dim3 wgrid((unsigned)(wblocks < cap ? wblocks : cap));                                               \
         decode_attn_mfma_kernel<DD, K8><<<wgrid, kBlock, 0, st>>>(qq, k_cache, v_cache, sl, ln, oo, po, pml, B,   \
                                                                   Hkv, G, max_seq, chunk, splits, sl2, num_slots, \
-                                                                  pl, ps_max, pr, (const int32_t*)fork, g7, g8);  \
+                                                                  pl, ps_max, pr, (const int32_t*)fork);          \
     } while (0)
     if (kv8) {
         if (D == 64) DMCP_MFMA_DECODE(64, true);
@@ -1186,7 +1005,7 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || splits == 1) return e;  // every row finished in the main kernel
     return launch_combine(part_o, part_ml, sl, ln, out, B, Hq, D, max_seq, chunk, splits, num_slots, pl, ps_max, pr,
-                          (const int32_t*)fork, g7, g8, std::min(kGrpMax, 16 / G), st);
+                          st);
 }
 
 int dmcp_silu_mul(const void* gu, void* out, int T, int I, void* stream) {

@@ -17,7 +17,6 @@ import os
 import threading
 from typing import Optional
 
-import numpy as np
 import torch
 
 from .build import TARGET, build
@@ -27,7 +26,7 @@ _lock = threading.Lock()
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _f = ctypes.c_float
-ABI_VERSION = 16  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
+ABI_VERSION = 15  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
 
 
 class HipOpsError(RuntimeError):
@@ -55,7 +54,7 @@ def lib() -> ctypes.CDLL:
             "dmcp_add_rmsnorm": ([_vp, _vp, _vp, _vp, _i, _i, _f, _vp], _i),
             "dmcp_rope_kv": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp], _i),
             "dmcp_decode_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _f,
-                                       _vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp], _i),
+                                       _vp, _vp, _vp, _i, _i, _vp, _vp, _vp], _i),
             "dmcp_kv_fork": ([_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _vp], _i),
             "dmcp_pgemm_set_waves": ([_i], _i),
             "dmcp_pgemm_set_bk": ([_i], _i),
@@ -230,95 +229,16 @@ def decode_plan(rows: int, n_kv_heads: int, max_seq: int, target_waves: int = 40
     return min_chunk, min(splits, decode_splits(max_seq, min_chunk))
 
 
-GROUP_MAX_ROWS = 4      # rows per decode-attention group (the kernel's kGrpMax; 16 MFMA columns / G)
-GROUP_MAX_SPLITS = 8    # key splits a group's item may take (the split-K workspace holds far more)
-
-
-def decode_groups(slots, positions, prefix_rows, fork_host, prefix_len: int, n_heads: int, n_kv_heads: int,
-                  target_waves: int = 2048, max_splits: int = GROUP_MAX_SPLITS, out=None):
-    """The ``groups`` table of :func:`decode_attention` for one decode step
-    (host numpy, int32 [2, n]).
-
-    Rows reading the same cache bytes for their first keys -- the method
-    branches of a class (their keys below the fork point live in the class
-    head's slot, ``fork_host`` = the host copy of ``LocalLM.fork_tab``), the
-    class head's own row, the jump-forward rows of one slot -- are grouped,
-    at most ``16 // G`` (<= 4) rows per group, so the kernel streams those
-    keys once per group.  Row 0 of the table: each row's group leader (+ the
-    leader's key-split count << 16); row 1: the leader's extra rows (count in
-    2 bits, row indices in 10 bits each).  Split counts share ``target_waves``
-    waves over the groups in proportion to their keys.  The kernel checks
-    every claim (a row whose keys turn out not to match still gets exact
-    attention), so this is a performance hint, never a correctness input."""
-    slots = np.asarray(slots, dtype=np.int64)
-    n = slots.shape[0]
-    res = np.empty((2, n), dtype=np.int32) if out is None else out
-    if n == 0:
-        return res
-    if n > 1024:
-        raise ValueError("decode_groups: more than 1024 rows")
-    idx = np.arange(n, dtype=np.int64)
-    G = max(1, n_heads // max(1, n_kv_heads))
-    cap = max(1, min(GROUP_MAX_ROWS, 16 // G))
-    L = np.asarray(positions, dtype=np.int64) + 1
-    shared = np.asarray(prefix_rows, dtype=np.int64) != 0
-    fh = np.asarray(fork_host)
-    S = fh.shape[0]
-    valid = (slots >= 0) & (slots < S)
-    sc = np.where(valid, slots, 0)
-    par, fe = fh[sc, 0].astype(np.int64), fh[sc, 1].astype(np.int64)
-    branch = valid & (fe > 0) & (par != slots) & (par >= 0) & (par < S)
-    src = np.where(branch, par, slots)
-    e = np.where(branch, np.minimum(fe, L), L)  # keys [.., e) come from src
-    P = np.where(shared, int(prefix_len), 0)
-    key = np.where(valid, src * 2 + shared, -1 - idx)  # invalid rows: groups of one
-    order = np.argsort(key, kind="stable")
-    ks = key[order]
-    newrun = np.ones(n, dtype=bool)
-    newrun[1:] = ks[1:] != ks[:-1]
-    runstart = np.maximum.accumulate(np.where(newrun, idx, 0))
-    cpos = (idx - runstart) % cap
-    lead_sorted = idx - cpos
-    g7 = np.empty(n, dtype=np.int64)
-    g7[order] = order[lead_sorted]
-    g8 = np.zeros(n, dtype=np.int64)
-    lead_pos = np.flatnonzero(cpos == 0)
-    for k in range(1, cap):
-        cand = lead_pos + k
-        ok = cand < n
-        ok[ok] = runstart[cand[ok]] == runstart[lead_pos[ok]]
-        lr, mr = order[lead_pos[ok]], order[cand[ok]]
-        g8[lr] |= mr << (2 + 10 * (k - 1))
-        g8[lr] += 1
-    # key splits: the group's keys (shared once + each row's own tail)
-    eo, Lo, Po = e[order], L[order], P[order]
-    se = np.maximum(np.minimum.reduceat(eo, lead_pos), Po[lead_pos])
-    cnt = np.diff(np.append(lead_pos, n))
-    W = (se - Po[lead_pos]) + (np.add.reduceat(Lo, lead_pos) - cnt * se)
-    W = np.where(valid[order[lead_pos]], np.maximum(W, 1), 0)
-    T = max(1, int(target_waves) // max(1, n_kv_heads))
-    ns = np.clip(np.ceil(W * (T / max(1, int(W.sum())))), 1, max(1, int(max_splits))).astype(np.int64)
-    g7[order[lead_pos]] |= ns << 16
-    res[0, :n] = g7.astype(np.int32)
-    res[1, :n] = g8.astype(np.uint32).view(np.int32)
-    return res
-
-
 def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: torch.Tensor,
                      seq_len: torch.Tensor, scale: float, workspace: Optional[tuple] = None,
                      chunk: int = 256, out: Optional[torch.Tensor] = None,
                      prefix: Optional["SharedPrefix"] = None, splits: Optional[int] = None,
-                     fork: Optional[torch.Tensor] = None, groups: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     fork: Optional[torch.Tensor] = None) -> torch.Tensor:
     """q [B, Hq, D]; caches [S, Hkv, MAXS, D]; slot/seq_len int32 [B].
 
     ``fork`` (int32 [S, 2], optional): per slot (parent slot, end) -- a
     method branch reads its keys below ``end`` from its class head's slot in
     place (no copy); end 0 = no parent.
-
-    ``groups`` (int32 [2, >= B], optional; :func:`decode_groups`): rows whose
-    keys up to some position are the same cache bytes (the branches of one
-    class, the jump-forward rows of one slot) attend in one work item, those
-    keys read once per group; the result is the same as without it.
 
     Each row's keys (after the shared prefix) are split into at most
     ``splits`` equal parts of >= ``chunk`` keys (default: as many as
@@ -373,12 +293,6 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
         _req(fork, torch.int32, "decode_attention.fork")
         if fork.numel() < 2 * S or not fork.is_contiguous():
             raise HipOpsError(f"decode_attention: fork table must be a contiguous int32 [{S}, 2]")
-    g7 = g8 = None
-    if groups is not None:
-        _req(groups, torch.int32, "decode_attention.groups")
-        if groups.dim() != 2 or groups.shape[0] != 2 or groups.shape[1] < B or groups.stride(1) != 1 or B > 1024:
-            raise HipOpsError(f"decode_attention: groups must be int32 [2, >= {B}] with unit row stride, B <= 1024")
-        g7, g8 = groups[0], groups[1]
     out = torch.empty_like(q) if out is None else out
     _req_out(out, torch.bfloat16, B * Hq * D, "decode_attention.out")
     if splits > 1 or ps_max:
@@ -393,7 +307,7 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     _check(lib().dmcp_decode_attention(_ptr(q), _ptr(k_cache), _ptr(v_cache), _ptr(slot), _ptr(seq_len), _ptr(out),
                                        _ptr(part_o), _ptr(part_ml), B, Hq, Hkv, D, MAXS, S, chunk, splits,
                                        float(scale), _ptr(pk), _ptr(pv), _ptr(plen), ps_max, kv8, _ptr(prows),
-                                       _ptr(fork), _ptr(g7), _ptr(g8), _stream()), "dmcp_decode_attention")
+                                       _ptr(fork), _stream()), "dmcp_decode_attention")
     return out
 
 

@@ -98,12 +98,10 @@ class SharedPrefix(NamedTuple):
 def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: torch.Tensor,
                      seq_len: torch.Tensor, scale: float, workspace=None, chunk: int = 256,
                      out: Optional[torch.Tensor] = None, prefix: Optional[SharedPrefix] = None,
-                     fork: Optional[torch.Tensor] = None, groups: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     fork: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``fork`` [S, 2] (parent slot, end): keys below ``end`` of a row whose
     slot has a parent come from the parent's slot (a method branch reading
-    its class head's KV in place).  ``groups`` (the kernel's row grouping,
-    :func:`dmcp.ops.hip.decode_groups`) changes which work item reads which
-    keys, never the result: ignored here."""
+    its class head's KV in place)."""
     B, Hq, D = q.shape
     S, Hkv, MAXS, _ = k_cache.shape
     G = Hq // Hkv

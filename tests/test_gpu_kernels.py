@@ -364,53 +364,3 @@ def test_decode_attention_fork_table(hip, kv, splits, P):
     from dmcp.ops import reference
     ref = reference.decode_attention(q, kc, vc, slot, lens, 0.125, prefix=pre, fork=fork)
     torch.testing.assert_close(got.float(), ref.float(), atol=2e-2, rtol=2e-2)
-
-
-@pytest.mark.parametrize("kv", ["fp8", "bf16"])
-@pytest.mark.parametrize("P", [0, 40])
-@pytest.mark.parametrize("target", [64, 2048])
-def test_decode_attention_row_groups(hip, kv, P, target):
-    """Row groups (ops.decode_groups: a class head's row, its method branches
-    reading its keys in place through the fork table, jump-forward rows of one
-    slot, rows outside the shared prefix, padding, in arbitrary row order): the
-    grouped kernel -- shared keys once per group, each row's own keys after
-    them with the other rows' columns masked, split counts per group (target
-    64: one item per group and several rows' own keys in one wave; 2048: the
-    shared keys split, the LSE combine merging) -- equals the fp32 reference
-    and the ungrouped kernel; a garbage table too (decoded defensively)."""
-    import numpy as np
-    from dmcp.ops import reference
-    from dmcp.ops.reference import SharedPrefix
-    from test_decode_groups import _scenario
-    rng = np.random.default_rng(5 + P)
-    slot_np, len_np, fork_np, prow_np, _, MAXS, S = _scenario(rng, P0=max(P, 1))
-    D, Hq, Hkv = 64, 32, 8
-    B = len(slot_np)
-
-    def cache(seed):
-        x = _bf(S + 1, Hkv, MAXS, D, seed=seed)
-        return x.to(torch.float8_e4m3fn).view(torch.uint8) if kv == "fp8" else x
-    kc, vc = cache(41), cache(42)
-    q = _bf(B, Hq, D, seed=43)
-    slot = torch.from_numpy(slot_np).cuda()
-    lens = torch.from_numpy(np.maximum(len_np, P + 1).astype(np.int32)).cuda()
-    fork = torch.from_numpy(fork_np).cuda()
-    pre, prow = None, torch.from_numpy(prow_np).cuda()
-    if P:
-        pre = SharedPrefix(kc[S], vc[S], torch.tensor([P], dtype=torch.int32, device="cuda"), prow)
-    g = hip.decode_groups(slot_np, lens.cpu().numpy() - 1, prow_np if P else np.zeros(B, np.int32), fork_np, P,
-                          Hq, Hkv, target_waves=target)
-    assert ((g[0] & 0xFFFF) != np.arange(B)).any(), "the scenario must group some rows"
-    groups = torch.from_numpy(g).cuda()
-    ref = reference.decode_attention(q, kc, vc, slot, lens, 0.125, prefix=pre, fork=fork)
-    flat = hip.decode_attention(q, kc, vc, slot, lens, 0.125, chunk=64, prefix=pre, splits=8, fork=fork)
-    got = hip.decode_attention(q, kc, vc, slot, lens, 0.125, chunk=64, prefix=pre, splits=8, fork=fork,
-                               groups=groups)
-    live = (slot >= 0) & (slot < S)
-    torch.testing.assert_close(got[live].float(), ref[live].float(), atol=2e-2, rtol=2e-2)
-    torch.testing.assert_close(got.float(), flat.float(), atol=1e-2, rtol=1e-2)
-    assert got[~live].abs().sum().item() == 0
-    bad = torch.from_numpy(rng.integers(-2**31, 2**31 - 1, (2, B), dtype=np.int64).astype(np.int32)).cuda()
-    bad[0, ::3] = torch.arange(0, B, 3, dtype=torch.int32, device="cuda")
-    got2 = hip.decode_attention(q, kc, vc, slot, lens, 0.125, chunk=64, prefix=pre, splits=8, fork=fork, groups=bad)
-    torch.testing.assert_close(got2[live].float(), ref[live].float(), atol=2e-2, rtol=2e-2)

@@ -41,6 +41,7 @@ from __future__ import annotations
 
 import json
 import logging
+import os
 import threading
 import time
 from collections import deque
@@ -53,6 +54,7 @@ from ..models.llm import LocalLM, LMConfig, DecodeGraphs, preset
 from .backend import EnrichmentBackend, build_enrichment_prompt
 from .jsonfix import parse_enrichment_response
 from .tokenizer import ByteTokenizer
+from .tokenizer import _Base as _TokBase
 from .types import EnrichmentInput, EnrichmentResult
 
 LOG = logging.getLogger(__name__)
@@ -476,7 +478,8 @@ class LocalEngine:
                  admit_min: Optional[int] = None, longest_first: bool = True, tokenizer=None,
                  max_new_tokens: Optional[int] = None, native_grammar: Optional[bool] = None,
                  fork_methods: bool = True, fork_max_context: int = 1536,
-                 reply_shape: Optional[ReplyShape] = None, type_choice: Optional[bool] = None) -> None:
+                 reply_shape: Optional[ReplyShape] = None, type_choice: Optional[bool] = None,
+                 precapture: Optional[bool] = None) -> None:
         self.model = model
         self.tok = tokenizer if tokenizer is not None else ByteTokenizer(model.cfg.vocab_size)
         self._tb = self.tok.token_bytes
@@ -525,6 +528,15 @@ class LocalEngine:
         self.masks = torch.tensor(masks, dtype=torch.int32, device=dev)
         self.graphs = DecodeGraphs(model, self.masks, alt_token=self._quote) \
             if use_graphs and dev.type == "cuda" else None
+        # every row-count bucket's decode graph captured now, at engine start:
+        # captured on first use instead, the larger buckets' captures (~15 ms
+        # each, the GPU idle meanwhile) landed inside the first big run --
+        # 23 % of the Llama-shape decode window (profiles/engine_gaps_r5.txt).
+        # LOCAL_LLM_PRECAPTURE=0 restores capture on first use.
+        if precapture is None:
+            precapture = os.environ.get("LOCAL_LLM_PRECAPTURE", "1") != "0"
+        if self.graphs is not None and precapture:
+            self.graphs.capture_all()
         self.max_prompt_tokens = max_prompt_tokens
         self.jump_forward = jump_forward
         self.shared_prefix = shared_prefix and model.shared_prefix
@@ -548,6 +560,7 @@ class LocalEngine:
         self._lock = threading.Lock()
         self._frag_cache: Dict[bytes, List[int]] = {}      # forced text -> ids
         self._prefix_cache: Dict[str, List[int]] = {}      # per-project prompt text -> ids (one project at a time)
+        self._cont_cache: Dict[str, List[int]] = {}        # per-class prompt text -> ids (one admission's batch)
         # the grammar state machine + step builder in native code
         # (native/grammar/engine.cpp); None = the Python implementation below
         # (the reference: both give the same replies, tests/test_local_engine.py)
@@ -558,6 +571,14 @@ class LocalEngine:
         self._stage = np.zeros((7, self.max_rows), dtype=np.int32)  # the native builder's step rows
         self._host_np = [h.numpy() for h in self._host_ids]
         self._ids_events = [torch.cuda.Event(), torch.cuda.Event()] if dev.type == "cuda" else [None, None]
+        # the model, tokenizer (128k vocabulary entries) and tables built above
+        # live as long as the engine: out of the cyclic collector's scans, so a
+        # full collection during a run walks only the run's own objects (a
+        # full scan paused the decode loop for tens of ms, GPU idle)
+        if dev.type == "cuda" and os.environ.get("LOCAL_LLM_GC_FREEZE", "1") != "0":
+            import gc
+            gc.collect()
+            gc.freeze()
 
     def _count_graphs(self) -> None:
         """The device witness in the stats: hipGraph replays and the kernel
@@ -747,7 +768,8 @@ class LocalEngine:
                     self._prefix_cache.clear()
                 pre = self._prefix_cache[text[:i]] = ([self.tok.bos] if self.tok.bos is not None else []) + \
                     self.tok.encode(text[:i])
-            ids, split = pre + self.tok.encode_continuation(text[i:]), len(pre)
+            cont = self._cont_cache.get(text[i:])  # pre-tokenised with its admission's batch
+            ids, split = pre + (cont if cont is not None else self.tok.encode_continuation(text[i:])), len(pre)
         else:
             ids, split = self.tok.encode_split(text, PREFIX_MARKER.decode())
         head = 1 if self.tok.bos is not None else 0
@@ -764,6 +786,25 @@ class LocalEngine:
                 split = 0
         seq.prefix_split = split
         return ids
+
+    def _pretokenize(self, items, readme: Optional[str]) -> None:
+        """The per-class parts of the prompts of ``items`` (feed items: key,
+        input[, readme]) in one batched tokenizer call, for :meth:`_prompt`.
+        One class at a time, a 128k-id BPE tokenised ~1.2 ms per prompt on
+        the engine thread -- 60-80 ms per admission with the GPU idle
+        (profiles/engine_gaps_r5.txt); the batch runs on the tokenizer's
+        thread pool."""
+        if len(items) < 2 or type(self.tok).encode_continuation_batch is _TokBase.encode_continuation_batch:
+            return
+        marker = PREFIX_MARKER.decode()
+        todo = []
+        for item in items:
+            text = build_enrichment_prompt(item[1], item[2] if len(item) > 2 else readme)
+            i = text.find(marker)
+            if i > 0 and text[i:] not in self._cont_cache:
+                todo.append(text[i:])
+        if len(todo) > 1:
+            self._cont_cache.update(zip(todo, self.tok.encode_continuation_batch(todo)))
 
     def _seq_prefix_len(self, s: _Seq) -> int:
         """Tokens of ``s.prompt`` before its per-class part, or 0."""
@@ -1113,6 +1154,10 @@ class LocalEngine:
                     # fork too (profiles/enrich_fork_context_ab_r4.jsonl)
                     small = len(items) < want and \
                         len(active) + len(pending) + len(items) <= cfg.max_batch * 3 // 4
+                    try:
+                        self._pretokenize(items, readme)
+                    except Exception:  # noqa: BLE001 -- each class then tokenises (and reports) on its own
+                        LOG.debug("batched prompt tokenisation failed", exc_info=True)
                     for item in items:
                         key, inp = item[0], item[1]
                         try:
@@ -1121,6 +1166,7 @@ class LocalEngine:
                             yield key, json.dumps({"error": str(e)})
                             continue
                         pending.extend(seqs)
+                    self._cont_cache.clear()
                 if not pending and not active and inflight is None:
                     if feed.done:
                         break

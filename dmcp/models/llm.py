@@ -1011,6 +1011,19 @@ class DecodeGraphs:
         self.enabled = model.device.type == "cuda"
         self.last_ids = torch.zeros(max(self.buckets), dtype=torch.int32, device=model.device)
 
+    def capture_all(self) -> int:
+        """Captures the graph of every bucket not captured yet (the engine
+        does this at start, so no capture stalls a running batch); returns
+        the number of captured buckets."""
+        for b in self.buckets:
+            if b not in self.graphs:
+                self._capture(b)
+                # one replay now (padding rows only): a graph's first launch
+                # costs milliseconds more than the later ones
+                self.graphs[b].graph.replay()
+        torch.cuda.synchronize()
+        return len(self.graphs)
+
     def bucket_for(self, n: int) -> int:
         for b in self.buckets:
             if b >= n:

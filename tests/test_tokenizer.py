@@ -204,3 +204,34 @@ def test_checkpoint_keeps_bf16_prefill_and_makes_type_choices(ckpt):
     assert LocalEngine(model, tokenizer=tok, use_graphs=False).type_choice
     fp8, _ = load_local_model(ckpt, device="cpu", max_batch=2, max_rows=8, max_seq=1024, prefill_dtype="fp8")
     assert fp8.cfg.prefill_dtype == "fp8"
+
+
+@pytest.mark.parametrize("metaspace", [False, True])
+def test_continuation_batch_equals_one_by_one(tmp_path, metaspace):
+    """The engine tokenises an admission's per-class prompts in one batched
+    call (LocalEngine._pretokenize): the ids equal encoding each alone."""
+    from dmcp.enrich.tokenizer import HFTokenizer
+    path = str(tmp_path / "t.json")
+    _train_bpe(path, vocab=400, metaspace=metaspace)
+    tok = HFTokenizer(path, bos=1)
+    texts = [f"Source of co.x.Svc{i}:\n```java\nclass Svc{i} {{ void run() {{ call({i}); }} }}\n```\n" * (1 + i % 3)
+             for i in range(12)] + ["Source of ", "Source of é方法\n"]
+    assert tok.encode_continuation_batch(texts) == [tok.encode_continuation(t) for t in texts]
+
+
+def test_engine_batched_prompt_tokenisation_matches(ckpt):
+    """Prompts built from the admission's batched tokenisation equal the
+    one-class-at-a-time prompts (same replies from the same model)."""
+    model, tok = load_local_model(ckpt, device="cpu", max_batch=4, max_rows=24, max_seq=2048)
+    from dmcp.enrich.types import EnrichmentInput
+    eng = LocalEngine(model, tokenizer=tok, use_graphs=False)
+    inputs = [EnrichmentInput(f"class Svc{i} {{ void run() {{}} }}\n" * (1 + i), f"co.x.Svc{i}", "java", "SERVICE",
+                              ["run"]) for i in range(5)]
+    items = [(i, x) for i, x in enumerate(inputs)]
+    eng._pretokenize(items, "A README.")
+    assert len(eng._cont_cache) == 5
+    from dmcp.enrich.local import _Seq
+    batched = [eng._prompt(_Seq(x, i, []), "A README.", 64) for i, x in enumerate(inputs)]
+    eng._cont_cache.clear()
+    single = [eng._prompt(_Seq(x, i, []), "A README.", 64) for i, x in enumerate(inputs)]
+    assert batched == single

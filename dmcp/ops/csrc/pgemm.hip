@@ -138,7 +138,12 @@ __device__ long long pg_stamps[65536][4];
 // WV = 4: one wave per SIMD, 128 x 128 per wave (16 MFMAs, 9 LDS-DMA pieces
 // per stage); WV = 8: two waves per SIMD, 128 x 64 per wave (8 MFMAs, 4-5
 // pieces) -- one wave's MFMAs run while the other issues its DMAs.
-template <int MODE, bool KV8, int WV, int BK = PBK>
+// AR (128-deep stages only): the A operand's pieces through registers -- a
+// global_load_dwordx4 per piece at the stage's start, its ds_write_b128 into
+// the same swizzled image slot late in the stage -- so the LDS-DMA path
+// carries only W (an LDS-DMA piece costs 100-185 issue cycles inside a busy
+// phase, MI355X_MICROARCH.md; a register load a few)
+template <int MODE, bool KV8, int WV, int BK = PBK, int AR = 0>
 __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4, WV / 4))) void pgemm_kernel(
     const uint8_t* __restrict__ aq, const uint8_t* __restrict__ as, const uint8_t* __restrict__ wq,
     const float* __restrict__ ws, int M, int N, int K, int mtiles, int ntiles, PEpi e) {
@@ -355,6 +360,28 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4,
             else if (i < 2 * PP2) pglds<16>(wq + (w2[i - PP2] + kb), base + PA2_BYTES + (wv * PP2 + i - PP2) * 1024);
             else pglds<4>(as + (s2 + (uint32_t)c2 * 4), base + PA2_BYTES + PB2_BYTES + wv * 256);
         };
+        // AR: this stage's A pieces in flight in registers
+        // The loads are inline asm, so the compiler's waitcnt pass (which
+        // cannot count the LDS-DMAs in flight and would drain them all with a
+        // vmcnt(0) before the first store) leaves the waits to astore: piece
+        // i has PP2 - 1 - i younger A loads and the stage's W + scale DMAs
+        // (NP2 - PP2) behind it.
+        v4i_t areg[PP2];
+        auto aload = [&](int i, int c2) {
+            const uint8_t* src = aq + (a2[i] + (uint32_t)c2 * PBK2);
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(areg[i]) : "v"(src) : "memory");
+        };
+        auto astore = [&](int i, int slot) {
+            switch (PP2 - 1 - i + NP2 - PP2) {  // vmcnt needs a literal
+#define PG_VMW(n) case n: asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); break;
+                PG_VMW(0) PG_VMW(1) PG_VMW(2) PG_VMW(3) PG_VMW(4) PG_VMW(5) PG_VMW(6) PG_VMW(7) PG_VMW(8)
+                PG_VMW(9) PG_VMW(10) PG_VMW(11) PG_VMW(12) PG_VMW(13) PG_VMW(14) PG_VMW(15) PG_VMW(16)
+#undef PG_VMW
+                default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            *reinterpret_cast<v4i_t*>(plds + slot * PST2_BYTES + (wv * PP2 + i) * 1024 + lane * 16) = areg[i];
+        };
+        constexpr int AST0 = 8 * NU - 5 - PP2;  // MFMA index of the first A store (the last lands before the wait)
         auto frag2 = [&](const uint8_t* img, int r, int ks) -> v8i_t {
             const int sw = sw2(r);
             const v4i_t lo = *reinterpret_cast<const v4i_t*>(img + r * PBK2 + ((4 * ks + hh) ^ sw) * 16);
@@ -397,7 +424,13 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4,
                                                                                     127, 0, F.sc[t]);
                         __builtin_amdgcn_sched_barrier(0);
                         if (idx == 0) rd2(c, 1, F1);  // k-step 1 of this stage, behind the first MFMA
-                        if (idx < NP2) piece2(idx, cn, (c + 1) & 1);
+                        if constexpr (AR != 0) {
+                            if (idx < PP2) aload(idx, cn);
+                            else if (idx < NP2) piece2(idx, cn, (c + 1) & 1);
+                            if (idx >= AST0 && idx < AST0 + PP2) astore(idx - AST0, (c + 1) & 1);
+                        } else if (idx < NP2) {
+                            piece2(idx, cn, (c + 1) & 1);
+                        }
                         if (idx == 8 * NU - 5) {  // four MFMAs before the end: stage c + 1 in, then its k-step 0
                             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
                             asm volatile("s_barrier" ::: "memory");
@@ -408,8 +441,18 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4,
             }
         };
         // prologue: stage 0 in, its k-step 0 read
-        for (int i = 0; i < NP2; ++i) piece2(i, 0, 0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (AR != 0) {
+#pragma unroll
+            for (int i = 0; i < PP2; ++i) aload(i, 0);
+            for (int i = PP2; i < NP2; ++i) piece2(i, 0, 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int i = 0; i < PP2; ++i) astore(i, 0);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        } else {
+            for (int i = 0; i < NP2; ++i) piece2(i, 0, 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         asm volatile("s_barrier" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         KF Fa, Fb;
@@ -1049,6 +1092,7 @@ int g_pgemm_waves = 4;  // dmcp_pgemm_set_waves: 4 (one wave per SIMD) or 8 (two
 // projection 405 -> 355 us; profiles/pgemm_bk128_r5.jsonl)
 int g_pgemm_bk = 128;
 int g_pgemm_group = 8;  // dmcp_pgemm_set_group: M tiles per block-order group
+int g_pgemm_areg = 0;   // dmcp_pgemm_set_areg: A pieces through registers (128-deep stages)
 
 template <int MODE, bool KV8>
 hipError_t launch_pgemm(const void* aq, const void* as, const void* wq, const void* ws, int M, int N, int K,
@@ -1057,7 +1101,10 @@ hipError_t launch_pgemm(const void* aq, const void* as, const void* wq, const vo
     const int ntiles = MODE == PM_SWIGLU ? e.I / 128 : N / PBN;
     PEpi e2 = e;
     e2.grp = g_pgemm_group;
-    if (g_pgemm_bk == 128 && g_pgemm_waves == 4 && K % PBK2 == 0)
+    if (g_pgemm_bk == 128 && g_pgemm_waves == 4 && K % PBK2 == 0 && g_pgemm_areg)
+        pgemm_kernel<MODE, KV8, 4, PBK2, 1><<<mtiles * ntiles, PTH, 0, (hipStream_t)stream>>>(
+            (const uint8_t*)aq, (const uint8_t*)as, (const uint8_t*)wq, (const float*)ws, M, N, K, mtiles, ntiles, e2);
+    else if (g_pgemm_bk == 128 && g_pgemm_waves == 4 && K % PBK2 == 0)
         pgemm_kernel<MODE, KV8, 4, PBK2><<<mtiles * ntiles, PTH, 0, (hipStream_t)stream>>>(
             (const uint8_t*)aq, (const uint8_t*)as, (const uint8_t*)wq, (const float*)ws, M, N, K, mtiles, ntiles, e2);
     else if (g_pgemm_waves == 8)
@@ -1088,6 +1135,13 @@ int dmcp_pgemm_set_waves(int w) {
 int dmcp_pgemm_set_bk(int bk) {
     const int old = g_pgemm_bk;
     if (bk == 64 || bk == 128) g_pgemm_bk = bk;
+    return old;
+}
+
+// A operand through registers instead of LDS-DMA (0 / 1, 128-deep stages); returns the previous value
+int dmcp_pgemm_set_areg(int on) {
+    const int old = g_pgemm_areg;
+    if (on == 0 || on == 1) g_pgemm_areg = on;
     return old;
 }
 

@@ -60,6 +60,7 @@ def lib() -> ctypes.CDLL:
             "dmcp_pgemm_set_bk": ([_i], _i),
             "dmcp_wgemm_set_aux": ([_i], _i),
             "dmcp_pgemm_set_group": ([_i], _i),
+            "dmcp_pgemm_set_areg": ([_i], _i),
             "dmcp_prefill_attention": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _i, _i,
                                         _i, _vp], _i),
             "dmcp_prefill_varlen": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, ctypes.c_long, _f,
@@ -521,6 +522,16 @@ def wgemm_set_aux(aux: int) -> int:
     if aux not in (0, 2):
         raise HipOpsError(f"wgemm_set_aux: 0 or 2, got {aux}")
     return int(lib().dmcp_wgemm_set_aux(int(aux)))
+
+
+def pgemm_set_areg(on: int) -> int:
+    """1: the MX prefill GEMM's 128-deep stages take the activation (A)
+    operand through registers (global loads, ds_write_b128 into the same LDS
+    image) and only the weights by LDS-DMA; 0 (default): both by LDS-DMA.
+    Returns the previous value."""
+    if on not in (0, 1):
+        raise HipOpsError(f"pgemm_set_areg: 0 or 1, got {on}")
+    return int(lib().dmcp_pgemm_set_areg(int(on)))
 
 
 def pgemm_set_group(g: int) -> int:

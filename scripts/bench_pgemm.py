@@ -57,6 +57,8 @@ def main() -> int:
     ap.add_argument("--bk", type=int, default=0, choices=[0, 64, 128],
                     help="K per LDS stage of the MX prefill GEMM (0: the library default)")
     ap.add_argument("--group", type=int, default=0, help="M tiles per block-order group (0: the library default)")
+    ap.add_argument("--areg", type=int, default=-1, choices=[-1, 0, 1],
+                    help="A operand through registers in the 128-deep kernel (-1: the library default)")
     a = ap.parse_args()
     from dmcp import ops
     from dmcp.models.llm import preset
@@ -67,6 +69,8 @@ def main() -> int:
         hip.pgemm_set_bk(a.bk)
     if a.group:
         hip.pgemm_set_group(a.group)
+    if a.areg >= 0:
+        hip.pgemm_set_areg(a.areg)
     c = preset(a.preset)
     M, H, I, D = a.rows, c.hidden, c.intermediate, c.head_dim
     dev = "cuda"
@@ -115,7 +119,7 @@ def main() -> int:
         except Exception as e:  # not in every torch build
             print(json.dumps({"proj": name, "impl": "fp8_scaled_mm", "error": str(e)[:200]}), flush=True)
     tot = {impl: sum(v.get(impl, 0) for v in out.values()) for impl in ("bf16_hipblaslt", "mxfp8_fused")}
-    print(json.dumps({"rows": M, "bk": a.bk or 128, "waves": a.waves or 4, "group": a.group or 8, "layer_us": {k: round(v, 1) for k, v in tot.items()},
+    print(json.dumps({"rows": M, "bk": a.bk or 128, "waves": a.waves or 4, "group": a.group or 8, "areg": a.areg, "layer_us": {k: round(v, 1) for k, v in tot.items()},
                       "speedup": round(tot["bf16_hipblaslt"] / tot["mxfp8_fused"], 3)}), flush=True)
     # decode-step shapes: the bf16 weight-streaming GEMMs (wgemm.hip, fused
     # reductions) against the MX fp8 ones (wmx_kernel + the same reductions)

@@ -385,6 +385,23 @@ def test_pgemm_eight_wave_variant(hip, M):
 
 
 @pytest.mark.parametrize("M", [1, 300, 3000])
+def test_pgemm_a_through_registers(hip, M):
+    """The 128-deep kernel with the activation operand through registers
+    (global loads + ds_write_b128 into the same image; hip.pgemm_set_areg)
+    against the same fp32 references: every epilogue."""
+    prev = hip.pgemm_set_areg(1)
+    try:
+        test_pgemm_plain(hip, M, 3072, 2048)
+        test_pgemm_plain(hip, M, 2048, 8192)
+        test_pgemm_resid(hip, M)
+        test_pgemm_swiglu(hip, M)
+        for kv in ("bf16", "fp8"):
+            test_pgemm_qkv_rope_kv(hip, kv, min(M, 600))
+    finally:
+        hip.pgemm_set_areg(prev)
+
+
+@pytest.mark.parametrize("M", [1, 300, 3000])
 def test_pgemm_64_deep_stages(hip, M):
     """The 64-deep-stage kernel (64-B image rows, 4-stage ring, 2-byte scale
     DMA; the default is 128-deep) against the same fp32 references: every

@@ -152,8 +152,16 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         u = (j / mparts) * 8 + (blockIdx.x & 7);
         mp = j % mparts;
     } else {
-        u = blockIdx.x / mparts;
-        mp = blockIdx.x % mparts;
+        // XCD-contiguous ranges (bijective for any grid; blocks are dealt
+        // round-robin over the 8 XCDs): a unit's M parts are consecutive in
+        // one XCD's range, so its weight tile is read once from HBM / MALL
+        // and hit in that XCD's L2 by the other parts (the LM head: 501
+        // units, whose parts had landed on three different XCDs)
+        const int nblk = units * mparts, b = blockIdx.x;
+        const int xcd = b & 7, q8 = nblk >> 3, r8 = nblk & 7;
+        const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+        u = L / mparts;
+        mp = L % mparts;
     }
     const int nt = u % ntiles, s = u / ntiles;
     const int chunks_all = K / KC;
@@ -422,8 +430,16 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         u = (j / mparts) * 8 + (blockIdx.x & 7);
         mp = j % mparts;
     } else {
-        u = blockIdx.x / mparts;
-        mp = blockIdx.x % mparts;
+        // XCD-contiguous ranges (bijective for any grid; blocks are dealt
+        // round-robin over the 8 XCDs): a unit's M parts are consecutive in
+        // one XCD's range, so its weight tile is read once from HBM / MALL
+        // and hit in that XCD's L2 by the other parts (the LM head: 501
+        // units, whose parts had landed on three different XCDs)
+        const int nblk = units * mparts, b = blockIdx.x;
+        const int xcd = b & 7, q8 = nblk >> 3, r8 = nblk & 7;
+        const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+        u = L / mparts;
+        mp = L % mparts;
     }
     const int nt = u % ntiles, s = u / ntiles;
     const int chunks_all = K / KC;

@@ -13,6 +13,6 @@ python3 - "$D" "dmcp/ops/ab/_hipops_$REV.so" <<'PY'
 import subprocess, sys, glob
 from dmcp.ops import build as b
 srcs = sorted(glob.glob(sys.argv[1] + "/*.hip"))
-subprocess.run([b.hipcc(), *b.FLAGS, f"-I{sys.argv[1]}", "-o", sys.argv[2], *srcs], check=True)
+subprocess.run([b.hipcc(), *b.FLAGS, "-shared", f"-I{sys.argv[1]}", "-o", sys.argv[2], *srcs], check=True)
 print(sys.argv[2])
 PY

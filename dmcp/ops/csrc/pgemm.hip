@@ -797,9 +797,12 @@ __global__ __launch_bounds__(kBlock) void wmx_kernel(
         const int j = blockIdx.x >> 3;
         u = (j / mparts) * 8 + (blockIdx.x & 7);
         mp = j % mparts;
-    } else {
-        u = blockIdx.x / mparts;
-        mp = blockIdx.x % mparts;
+    } else {  // XCD-contiguous ranges (bijective for any grid): a unit's M parts on one XCD
+        const int nblk = units * mparts, b = blockIdx.x;
+        const int xcd = b & 7, q8 = nblk >> 3, r8 = nblk & 7;
+        const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+        u = L / mparts;
+        mp = L % mparts;
     }
     const int nt = u % ntiles, sl = u / ntiles;
     const int k0 = sl * ks;

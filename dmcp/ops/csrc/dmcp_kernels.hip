@@ -727,10 +727,13 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
     const int tr_half = (c & 2) ? -8 : 8;
     for (int item = blockIdx.x * NW + wave; item < total; item += gridDim.x * NW) {
         // split-major: consecutive waves take different rows' splits, so the
-        // persistent grid's first pass covers every row
+        // persistent grid's first pass covers every row; inside a split kv
+        // head-major, so a block's 4 waves take 4 consecutive rows of one kv
+        // head -- a slot's jump-forward rows (consecutive rows, the same keys)
+        // re-read them on one CU / XCD instead of from the MALL
         const int split = item / (B * Hkv);
         const int rem = item - split * (B * Hkv);
-        const int b = rem / Hkv, kh = rem - b * Hkv;
+        const int kh = rem / B, b = rem - kh * B;
         const int s = __builtin_amdgcn_readfirstlane(slot[b]);
         const int L = __builtin_amdgcn_readfirstlane((s >= 0 && s < num_slots) ? min(seq_len[b], max_seq) : 0);
         if (L <= 0) {  // padding row / bad slot: defined output, nothing read

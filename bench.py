@@ -63,7 +63,7 @@ def parse_args(argv=None):
     ap.add_argument("--enrich-local-kv", default="fp8", choices=["bf16", "fp8"])
     ap.add_argument("--enrich-local-prefill", default="auto", choices=["auto", "bf16", "fp8"],
                     help="batched-prefill GEMMs of the enrichment worker (auto = MXFP8 on gfx950)")
-    ap.add_argument("--enrich-local-batch", type=int, default=512)
+    ap.add_argument("--enrich-local-batch", type=int, default=768)
     ap.add_argument("--enrich-local-presets", default="dmcp-coder-1b,llama3.2-1b-code")
     ap.add_argument("--remote-steps", type=int, default=3,
                     help="timed analyses on the remote-repository path (extra.remotePath; 0 = skip)")
@@ -96,7 +96,7 @@ def _spawn_enrich_pools(args):
         for name in [p.strip() for p in args.enrich_local_presets.split(",") if p.strip()]:
             model = {"preset": name, "kv_dtype": args.enrich_local_kv, "prefill_dtype": args.enrich_local_prefill,
                      "max_batch": mb,
-                     "max_rows": max(256, mb * 3 // 2), "seed": 0}
+                     "max_rows": max(mb, min(1024, max(256, mb * 3 // 2))), "seed": 0}
             pools[name] = GpuWorkerPool([f"cuda:{local}"], model, engine={"max_new_tokens": 4096}, init=False,
                                         start_timeout_s=600)
         return pools

@@ -31,7 +31,7 @@ def main(argv=None) -> int:
     ap.add_argument("--decode-dtype", default="bf16", choices=["bf16", "fp8"],
                     help="decode-step projections: bf16, or fp8 weights x MXFP8 activations (csrc/pgemm.hip)")
     ap.add_argument("--classes", type=int, default=1024, help="classes per rank")
-    ap.add_argument("--batch", type=int, default=512, help="concurrent sequences (KV slots)")
+    ap.add_argument("--batch", type=int, default=768, help="concurrent sequences (KV slots)")
     ap.add_argument("--max-seq", type=int, default=8192)
     ap.add_argument("--max-rows", type=int, default=0,
                     help="rows per decode step incl. jump-forward rows (0 = 1.5 x batch, >= 256)")
@@ -71,7 +71,7 @@ def main(argv=None) -> int:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl")
     cfg = preset(args.preset, max_batch=args.batch, max_seq=args.max_seq, kv_dtype=args.kv_dtype,
-                 prefill_dtype=args.prefill_dtype, decode_dtype=args.decode_dtype, max_rows=args.max_rows or max(256, args.batch + args.batch // 2))
+                 prefill_dtype=args.prefill_dtype, decode_dtype=args.decode_dtype, max_rows=args.max_rows or max(args.batch, min(1024, max(256, args.batch + args.batch // 2))))
     model = LocalLM(cfg, device=f"cuda:{local}", seed=rank)
     tok = None
     if cfg.tokenizer:

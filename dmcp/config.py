@@ -75,7 +75,7 @@ class Config:
     # "process": one worker process per GPU, started before this process
     # touches HIP (the service default); "inline": engines in this process
     local_llm_workers: str = "process"
-    local_llm_max_batch: int = 512      # KV slots (concurrent sequences) per GPU (profiles/enrich_batch_sweep_r3.txt)
+    local_llm_max_batch: int = 768      # KV slots (concurrent sequences) per GPU (profiles/enrich_batch_sweep_r5.txt)
     # enrichment hands the backend every pending class as one stream (a local
     # engine keeps its continuous batch full); false = the reference's
     # barriers of enrich_batch_size classes

@@ -643,7 +643,9 @@ def model_spec(cfg) -> dict:
     """The worker model spec of a :class:`dmcp.config.Config`."""
     mb = int(cfg.local_llm_max_batch)
     spec = {"preset": cfg.local_llm_preset, "kv_dtype": cfg.local_llm_kv_dtype, "max_batch": mb,
-            "max_rows": max(256, mb * 3 // 2), "seed": 0,
+            # rows per decode step: 1.5 x the slots (jump-forward rows), within
+            # the hand-written decode GEMMs' 1,024 (TGEMM_MAX_ROWS)
+            "max_rows": max(mb, min(1024, max(256, mb * 3 // 2))), "seed": 0,
             "prefill_dtype": getattr(cfg, "local_llm_prefill_dtype", "auto"),
             "decode_dtype": getattr(cfg, "local_llm_decode_dtype", "bf16")}
     if getattr(cfg, "local_llm_model_path", ""):

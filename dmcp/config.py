@@ -62,7 +62,9 @@ class Config:
     # decode each method of a class as its own sequence from the class head's
     # KV (a class's latency: head + longest method, not all methods in a row)
     local_llm_fork_methods: bool = True
-    local_llm_fork_max_context: int = 1536
+    # ... only for classes whose own prompt is at most this many tokens (0 =
+    # every class; profiles/enrich_fork_context_ab_r5.txt)
+    local_llm_fork_max_context: int = 0
     # byte caps of the reply's free strings (class description, method
     # description, business-logic step) and the step count; 0 = derived from
     # the reply budget (dmcp/enrich/local.py ReplyShape.from_budget: 256 / 128

@@ -477,7 +477,7 @@ class LocalEngine:
                  jump_forward: bool = True, shared_prefix: bool = True, pipeline: bool = True,
                  admit_min: Optional[int] = None, longest_first: bool = True, tokenizer=None,
                  max_new_tokens: Optional[int] = None, native_grammar: Optional[bool] = None,
-                 fork_methods: bool = True, fork_max_context: int = 1536,
+                 fork_methods: bool = True, fork_max_context: int = 0,
                  reply_shape: Optional[ReplyShape] = None, type_choice: Optional[bool] = None,
                  precapture: Optional[bool] = None) -> None:
         self.model = model
@@ -502,11 +502,13 @@ class LocalEngine:
         # latency-bound: rows per step far below capacity)
         self.fork_methods = fork_methods
         # ... unless the class's own context (prompt after the shared prefix)
-        # is longer than this.  Branches read the head's KV in place (no
-        # copies since the fork table), but at ~2,400 own tokens (the
-        # byte-level preset) a full batch still loses: 74.9 -> 69.8 classes/s
-        # at 1,024 classes (steps 8.4 -> 9.6 ms), while a small, latency-bound
-        # batch gains 63.3 -> 67.7 at 257 (profiles/enrich_fork_context_ab_r4.jsonl)
+        # is longer than this (0: no limit, the default).  In round 4 forking
+        # the byte-level preset's ~2,400-token classes lost in a full batch
+        # (74.9 -> 69.8 classes/s, profiles/enrich_fork_context_ab_r4.jsonl);
+        # with 768 slots and the per-row attention's kv-head-major items (a
+        # class's branch rows, adjacent in the step, re-read the head's keys on
+        # one CU) it wins: 42.3 -> 52.6 classes/s at 1,024 classes
+        # (profiles/enrich_fork_context_ab_r5.txt)
         self.fork_max_context = int(fork_max_context)
         self.cfg: LMConfig = model.cfg
         # reply budget: the caller's max_new_tokens, within what the KV slot

@@ -657,7 +657,7 @@ def engine_spec(cfg) -> dict:
     """LocalEngine keyword arguments of a :class:`dmcp.config.Config`."""
     return {"max_new_tokens": int(cfg.local_llm_max_new_tokens),
             "fork_methods": bool(getattr(cfg, "local_llm_fork_methods", True)),
-            "fork_max_context": int(getattr(cfg, "local_llm_fork_max_context", 1536)),
+            "fork_max_context": int(getattr(cfg, "local_llm_fork_max_context", 0)),
             "reply_shape": {"desc": int(getattr(cfg, "local_llm_desc_max_bytes", 0)),
                             "method": int(getattr(cfg, "local_llm_method_max_bytes", 0)),
                             "step": int(getattr(cfg, "local_llm_step_max_bytes", 0)),

@@ -148,7 +148,14 @@ class MemoryTree(SourceTree):
         if fn is None:
             return None
         if rows is not None:
-            return fn(list(self.files.items()), language, threads, framework, StaticMethodInfo, rows)
+            # the indexing pipeline (rows given) never reads the Go analyzer's
+            # package document (3.6 MB of JSON for a 1,000-file repository,
+            # rendered on one thread): not built on that path
+            try:
+                return fn(list(self.files.items()), language, threads, framework, StaticMethodInfo, rows,
+                          go_doc=False)
+            except TypeError:  # a module built before go_doc
+                return fn(list(self.files.items()), language, threads, framework, StaticMethodInfo, rows)
         return fn(list(self.files.items()), language, threads, framework, StaticMethodInfo)
 
 

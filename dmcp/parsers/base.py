@@ -24,7 +24,7 @@ import logging
 import os
 import time
 from dataclasses import dataclass, field
-from typing import Dict, List, Mapping, Optional, Sequence, Set
+from typing import Any, Dict, List, Mapping, Optional, Sequence, Set
 
 from ..graph.project_graph import ProjectGraph
 from ..models.domain import ClassType, StaticMethodInfo
@@ -95,7 +95,7 @@ class ParsedProject:
     units: Dict[str, ParsedUnit]
     file_to_identifier: Dict[str, str]
     stats: dict
-    go_analysis: Optional[dict] = None
+    go_analysis: Optional[Any] = None  # dict, or its JSON text until GoSourceParser.go_analysis() parses it
     # ident -> (class id, [method ids]) of class / method rows the scan already
     # handed to the row writer (scan_tree(rows=...)); Phase 1 binds these ids
     static_row_ids: Optional[dict] = None
@@ -177,9 +177,10 @@ def to_parsed_project(doc: dict) -> ParsedProject:
         _add_unit(units, lang, path, ident, _class_type(f.get("classType")), bool(f.get("entryPoint")),
                   _methods_from(f.get("methods") or ()), list(f.get("deps") or ()),
                   {k: list(v) for k, v in (f.get("params") or {}).items()})
+    # the Go analyzer's package document stays JSON text until someone asks
+    # for it (GoSourceParser.go_analysis): the indexing pipeline never does,
+    # and parsing it cost a 1,000-file repository ~10 ms per analysis
     go = doc.get("go")
-    if isinstance(go, str):
-        go = json.loads(go)
     return ParsedProject(lang, doc.get("sourceRoot", "."), doc.get("framework"), doc.get("module"),
                          units, file_to_id, doc.get("stats") or {}, go)
 
@@ -407,7 +408,12 @@ class GoSourceParser(SourceParser):
         return "."
 
     def go_analysis(self) -> Optional[dict]:
-        return self.project.go_analysis if self.project else None
+        if self.project is None:
+            return None
+        go = self.project.go_analysis
+        if isinstance(go, (str, bytes)):
+            go = self.project.go_analysis = json.loads(go)
+        return go
 
 
 def parser_for(language: str, threads: int = 0) -> SourceParser:

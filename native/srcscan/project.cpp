@@ -290,7 +290,7 @@ ScanResult scan_project(const std::string& root, const ScanOptions& opt) {
         scan_ts(root, opt, r.files, r.skipped, r.framework, r.source_root);
         r.has_framework = true;
     } else if (lang == "go") {
-        go_project_files(root, opt.threads, r.module, r.files, &r.go_json);
+        go_project_files(root, opt.threads, r.module, r.files, opt.go_doc ? &r.go_json : nullptr);
     } else {
         lang = "java";
         r.source_root = "src/main/java";

@@ -71,7 +71,7 @@ dbw::Batch to_batch(const std::string& sql, py::handle rows) {
 
 // (relative path, bytes) pairs -> scan of the mounted in-memory tree (GIL released)
 srcscan::ScanResult scan_mounted(py::list files, const std::string& language, int threads,
-                                 const std::string& framework) {
+                                 const std::string& framework, bool go_doc = true) {
     const auto t = std::chrono::steady_clock::now();
     // contents are viewed in place: the (path, bytes) tuples are held
     // (immutable bytes) until the scan is done
@@ -98,6 +98,7 @@ srcscan::ScanResult scan_mounted(py::list files, const std::string& language, in
     opt.language = language;
     opt.threads = threads;
     opt.framework = framework;
+    opt.go_doc = go_doc;
     try {
         srcscan::ScanResult r = srcscan::scan_project(root, opt);
         r.mount_us = mount_us;
@@ -885,8 +886,9 @@ PYBIND11_MODULE(_srcscan, m) {
     m.def(
         "scan_sources_objects",
         [](py::list files, const std::string& language, int threads, const std::string& framework,
-           py::handle method_cls, py::object rows) {
-            auto r = std::make_unique<srcscan::ScanResult>(scan_mounted(files, language, threads, framework));
+           py::handle method_cls, py::object rows, bool go_doc) {
+            auto r = std::make_unique<srcscan::ScanResult>(scan_mounted(files, language, threads, framework,
+                                                                        go_doc));
             // rows = (BulkWriter, project id, now, commit hash | None, class INSERT, method INSERT):
             // the class / method rows go to the writer from a helper thread
             // while this one builds the Python objects
@@ -952,9 +954,10 @@ PYBIND11_MODULE(_srcscan, m) {
             return d;
         },
         py::arg("files"), py::arg("language"), py::arg("threads"), py::arg("framework"), py::arg("method_cls"),
-        py::arg("rows") = py::none(),
+        py::arg("rows") = py::none(), py::arg("go_doc") = true,
         "scan_sources as Python objects (files as tuples, methods as method_cls) -- no JSON round trip; "
-        "with rows, the class / method rows are written first (ids in 'rowIds')");
+        "with rows, the class / method rows are written first (ids in 'rowIds'); go_doc=False: no "
+        "go-analyzer package document (Go)");
     m.def(
         "scan_file",
         [](const std::string& path, const std::string& language, const std::string& rel, const std::string& fw) {

@@ -73,6 +73,7 @@ struct ScanOptions {
     int threads = 0;
     std::string framework;          // TS only: override detection
     size_t max_file_bytes = 5u * 1024u * 1024u;  // NodeJsGraalParser.java:57
+    bool go_doc = true;             // Go only: also render the go-analyzer package document
 };
 
 // Result of a project scan (what the JSON document of project.cpp holds).

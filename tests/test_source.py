@@ -192,6 +192,8 @@ def test_scan_objects_equal_json_document(tmp_path, kind):
     a = to_parsed_project(t.scan_objects(lang, 4))
     b = to_parsed_project(_json.loads(t.scan(lang, 4)))
     a.stats = b.stats = None
+    if isinstance(a.go_analysis, str):  # kept as JSON text until asked for (GoSourceParser.go_analysis)
+        a.go_analysis = _json.loads(a.go_analysis)
     assert a.units and a == b
     assert all(type(m).__name__ == "StaticMethodInfo" for u in a.units.values() for m in u.methods)
 
@@ -361,3 +363,25 @@ def test_isolated_scan_matches_in_process_and_survives_faults(tmp_path):
     assert app.repos.classes.count_by_project()[p.id] == 25  # the previous analysis' rows survive
     assert app.indexer.analyze_project(str(repo)).success  # and the server carries on
     app.close()
+
+
+def test_go_document_on_demand(tmp_path):
+    """The Go analyzer's package document: parsed only when asked for
+    (GoSourceParser.go_analysis), and not rendered at all on the indexing
+    pipeline's path (go_doc=False) -- the units are the same either way."""
+    from dmcp.models.domain import StaticMethodInfo
+    from dmcp.parsers.base import GoSourceParser, native, to_parsed_project
+    repo = tmp_path / "r"
+    synth.go_gin_repo(str(repo), 3)
+    t = GitClient(str(tmp_path / "c")).snapshot(RepositoryUrl.of(str(repo)), "main")
+    p = GoSourceParser(2)
+    p.scan_tree(t)
+    assert isinstance(p.project.go_analysis, str)
+    doc = p.go_analysis()
+    assert isinstance(doc, dict) and doc["packages"] and p.go_analysis() is doc
+    fn = native().scan_sources_objects
+    with_doc = fn(list(t.files.items()), "go", 2, "", StaticMethodInfo)
+    without = fn(list(t.files.items()), "go", 2, "", StaticMethodInfo, None, go_doc=False)
+    assert with_doc["go"] and without["go"] is None
+    a, b = to_parsed_project(with_doc), to_parsed_project(without)
+    assert a.units == b.units and a.file_to_identifier == b.file_to_identifier

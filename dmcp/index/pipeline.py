@@ -34,6 +34,7 @@ import logging
 import os
 import threading
 import time
+from concurrent.futures import TimeoutError as FutureTimeout
 from dataclasses import dataclass, field
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
@@ -147,6 +148,10 @@ class Indexer:
     ROW_CHUNK = 256  # classes (with their methods) per writer put in Phase 1
     native_phase1 = True  # Phase 1 rows built by the native writer when it can (else the Python loop)
     phase1_ids: Optional[List[str]] = None  # row ids for the native Phase 1 (None = fresh UUIDv7s; tests)
+    # a local repository's row swap opens before its snapshot read finishes
+    # (the old rows' deletes overlap the read) and is rolled back if the read
+    # is still running after this many seconds; a remote clone's opens after
+    early_swap_wait_s = float(os.environ.get("DMCP_EARLY_SWAP_WAIT_S", "0.1"))
 
     def __init__(self, repos: Repositories, cache: GraphCache, git: GitClient,
                  backend: Optional[EnrichmentBackend] = None, *, batch_size: int = 20,
@@ -204,15 +209,27 @@ class Indexer:
             raise
         try:
             with span("analyze.total", stats, project=project.name):
-                with span("analyze.clone", stats):  # what is left of the read after the above
-                    clone, stats["analyze.fetch"] = fetch.result()
                 # the row swap's transaction (SQLite: BEGIN IMMEDIATE, the
-                # database's write lock) opens only now that the snapshot is
-                # read -- a remote clone can take far longer than other
-                # writers' busy timeout; the old rows are deleted on the
-                # writer thread while the tree is parsed (rolled back if the
-                # parse fails)
-                writer = self.repos.project_rows_writer(project.id, True)
+                # database's write lock) must not be held across a slow read --
+                # a remote clone can take far longer than other writers' busy
+                # timeout -- so it opens after the snapshot is read, except for
+                # a local repository, whose read is usually a few ms of
+                # in-place object inflation: there it opens right away (the old
+                # rows' deletes overlap the read) and is rolled back if the read
+                # outlasts early_swap_wait_s.  The deletes run on the writer
+                # thread while the tree is parsed (rolled back if it fails).
+                with span("analyze.clone", stats):  # what is left of the read after the above
+                    if self.early_swap_wait_s > 0 and url.local_path() is not None:
+                        writer = self.repos.project_rows_writer(project.id, True)
+                        try:
+                            clone, stats["analyze.fetch"] = fetch.result(timeout=self.early_swap_wait_s)
+                        except FutureTimeout:
+                            writer.abort()  # a slow disk: release the write lock during the read
+                            writer = None
+                    if clone is None:
+                        clone, stats["analyze.fetch"] = fetch.result()
+                if writer is None:
+                    writer = self.repos.project_rows_writer(project.id, True)
                 readme = clone.readme(self.max_readme_length)
                 if readme is not None:
                     project.update_description(readme[:self.description_length])

@@ -455,9 +455,11 @@ def test_scan_written_rows_match_python_loop(tmp_path, monkeypatch, kind):
 
 def test_slow_fetch_holds_no_database_write_lock(tmp_path):
     """The row swap's transaction (SQLite BEGIN IMMEDIATE: the database's
-    write lock) opens only after the snapshot is read: while one analysis
-    waits on a slow (remote) fetch, another project's analysis and status
-    writes go through, and the slow one still completes afterwards."""
+    write lock) is never held across a slow snapshot read: a local
+    repository's swap opens early but is rolled back once the read outlasts
+    ``early_swap_wait_s``, so while one analysis waits on a slow fetch another
+    project's analysis and status writes go through, and the slow one still
+    completes afterwards."""
     import time
     synth.java_spring_repo(str(tmp_path / "slow"), 6, base_package="co.slow", seed=3)
     synth.java_spring_repo(str(tmp_path / "fast"), 6, base_package="co.fast", seed=4)

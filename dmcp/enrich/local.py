@@ -39,6 +39,7 @@ per class) but generates on the local GPU:
 """
 from __future__ import annotations
 
+import gc
 import json
 import logging
 import os
@@ -578,9 +579,11 @@ class LocalEngine:
         # full collection during a run walks only the run's own objects (a
         # full scan paused the decode loop for tens of ms, GPU idle)
         if dev.type == "cuda" and os.environ.get("LOCAL_LLM_GC_FREEZE", "1") != "0":
-            import gc
             gc.collect()
             gc.freeze()
+        # full collections wait this many young-generation passes during a
+        # session (0 = the interpreter's own threshold); GPU only
+        self.gc_full_every = int(os.environ.get("LOCAL_LLM_GC_FULL_EVERY", "1000")) if dev.type == "cuda" else 0
 
     def _count_graphs(self) -> None:
         """The device witness in the stats: hipGraph replays and the kernel
@@ -1145,6 +1148,14 @@ class LocalEngine:
             else:
                 release([q.slot])
             finished.append(q)
+        # the run's own objects (segments, sequences, the caller's inputs:
+        # ~10^5) are not frozen, and a full collection over them paused the
+        # loop for 25-45 ms, GPU idle, about once per run
+        # (profiles/engine_gc_r5.txt): the session defers full collections
+        # (young ones still run; refcounting frees everything acyclic)
+        gc_threshold = gc.get_threshold() if self.gc_full_every else None
+        if gc_threshold is not None:
+            gc.set_threshold(gc_threshold[0], gc_threshold[1], max(gc_threshold[2], self.gc_full_every))
         try:
             while True:
                 # ---- refill the look-ahead (blocking only when idle)
@@ -1400,6 +1411,8 @@ class LocalEngine:
                 self._native.reset()
             if P:
                 self.model.clear_prefix()
+            if gc_threshold is not None:
+                gc.set_threshold(*gc_threshold)
 
 
 class LocalLLMBackend(EnrichmentBackend):

@@ -80,6 +80,24 @@ def test_engine_valid_json_and_continuous_batching(tiny):
     assert eng.stats["prefills"] == 7 and eng.stats["decode_steps"] > 0
 
 
+def test_session_defers_full_gc_and_restores_threshold(tiny):
+    """A session raises the full-collection threshold while it runs (a full
+    pass over the run's objects paused the GPU loop) and restores the
+    interpreter's own afterwards -- also when the consumer stops early."""
+    import gc
+    before = gc.get_threshold()
+    eng = LocalEngine(tiny)
+    eng.gc_full_every = 5000
+    seen = [gc.get_threshold() for _ in eng.stream(enumerate(_inputs(3)), None)]
+    assert len(seen) == 3 and all(t[2] == max(before[2], 5000) for t in seen)
+    assert gc.get_threshold() == before
+    it = eng.stream(enumerate(_inputs(3)), None)
+    next(it)
+    assert gc.get_threshold()[2] == max(before[2], 5000)
+    it.close()  # the consumer stops early: the session's finally restores it
+    assert gc.get_threshold() == before
+
+
 def test_jump_forward_is_exact_on_cpu(tiny):
     a = LocalEngine(tiny, jump_forward=False)
     b = LocalEngine(tiny, jump_forward=True)

@@ -545,6 +545,8 @@ class LocalEngine:
         self.shared_prefix = shared_prefix and model.shared_prefix
         self.max_rows = model.max_rows
         self.pipeline = pipeline
+        # classes taken from the feed per loop iteration (0 = all the free slots + look-ahead at once)
+        self.refill_chunk = int(os.environ.get("LOCAL_LLM_REFILL_CHUNK", "32"))
         # previous step's selections for host-less gathers (graphs keep their own)
         self._last_ids = self.graphs.last_ids if self.graphs is not None else \
             torch.zeros(self.max_rows, dtype=torch.int32, device=dev)
@@ -1160,8 +1162,18 @@ class LocalEngine:
             while True:
                 # ---- refill the look-ahead (blocking only when idle)
                 want = len(free_slots) + lookahead - len(pending)
+                more = False  # the feed had a whole chunk ready: more may be waiting
                 if want > 0 and not feed.done:
+                    if self.refill_chunk > 0:
+                        # a chunk per iteration: its prompts' tokenisation and
+                        # sequence set-up (~0.2 ms a class) stay under the GPU
+                        # work already queued -- a step, or at the start the
+                        # first admissions' prefills -- instead of one refill of
+                        # the whole batch with the GPU idle (~180 ms per start
+                        # at 768 slots, profiles/engine_host_r5.txt)
+                        want = min(want, self.refill_chunk)
                     items = list(feed.take(want, wait=not active and not pending and inflight is None))
+                    more = len(items) == want
                     # a small batch -- the feed drained and every class fits in
                     # 3/4 of the slots -- is latency-bound: long-context classes
                     # fork too (profiles/enrich_fork_context_ab_r4.jsonl)
@@ -1223,7 +1235,9 @@ class LocalEngine:
                         ntok += nxt
                     inflight = self._admit_launch(batch)
                 if inflight is not None:
-                    done = self._admit_finish(inflight, wait=not active)
+                    # nothing decodes yet: keep preparing the feed while the
+                    # first prefills run rather than wait for them
+                    done = self._admit_finish(inflight, wait=not active and not more)
                     if done is not None:
                         active.extend(s for s in inflight["batch"] if not s.done)
                         for s in done:

@@ -833,9 +833,16 @@ class LocalLM:
                 not (0 < end <= self.cfg.max_seq):
             raise ValueError(f"fork_share: slot {src} -> {dl}, end {end}")
         vals = torch.tensor([[int(src), int(end)]] * len(dl), dtype=torch.int32)
-        idx = torch.tensor(dl, dtype=torch.long)
+        self._fork_tab_update(torch.tensor(dl, dtype=torch.long), vals)
+
+    def _fork_tab_update(self, idx: torch.Tensor, vals: torch.Tensor) -> None:
+        """``fork_tab[idx] = vals`` from host tensors, in stream order without
+        blocking the host: a pageable source would make the copy wait for the
+        stream to drain (up to a whole queued prefill, GPU idle after it)."""
         if self.device.type == "cuda":
-            vals, idx = vals.to(self.device, non_blocking=True), idx.to(self.device, non_blocking=True)
+            both = torch.cat([idx.to(torch.int64).view(-1, 1), vals.to(torch.int64)], 1).pin_memory()
+            both = both.to(self.device, non_blocking=True)
+            idx, vals = both[:, 0], both[:, 1:].to(torch.int32)
         self.fork_tab.index_copy_(0, idx, vals)
 
     @torch.inference_mode()
@@ -849,11 +856,8 @@ class LocalLM:
         sl = [int(x) for x in slots]
         if not sl:
             return
-        vals = torch.tensor([[x, 0] for x in sl], dtype=torch.int32)
-        idx = torch.tensor(sl, dtype=torch.long)
-        if self.device.type == "cuda":
-            vals, idx = vals.to(self.device, non_blocking=True), idx.to(self.device, non_blocking=True)
-        self.fork_tab.index_copy_(0, idx, vals)
+        self._fork_tab_update(torch.tensor(sl, dtype=torch.long),
+                              torch.tensor([[x, 0] for x in sl], dtype=torch.int32))
 
     def decode_select(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor,
                       masks: torch.Tensor, mask_idx: torch.Tensor) -> tuple:

@@ -547,6 +547,8 @@ class LocalEngine:
         self.pipeline = pipeline
         # classes taken from the feed per loop iteration (0 = all the free slots + look-ahead at once)
         self.refill_chunk = int(os.environ.get("LOCAL_LLM_REFILL_CHUNK", "32"))
+        # batched prefills that may be in flight at once
+        self.admit_depth = max(1, int(os.environ.get("LOCAL_LLM_ADMIT_DEPTH", "2")))
         # previous step's selections for host-less gathers (graphs keep their own)
         self._last_ids = self.graphs.last_ids if self.graphs is not None else \
             torch.zeros(self.max_rows, dtype=torch.int32, device=dev)
@@ -1102,7 +1104,7 @@ class LocalEngine:
         prev_buf, prev_n = 1, 0
         step_no = -1                     # number of the last launched step
         finished: List[_Seq] = []
-        inflight: Optional[dict] = None  # the batched prefill in flight
+        admits: Deque[dict] = deque()  # the batched prefills in flight, oldest first
         forks: List[_Fork] = []  # forks with branches still waiting for a slot
         nat0 = self._native
         self.model.fork_reset()  # no slot reads another's keys (a session left by an error included)
@@ -1172,7 +1174,7 @@ class LocalEngine:
                         # the whole batch with the GPU idle (~180 ms per start
                         # at 768 slots, profiles/engine_host_r5.txt)
                         want = min(want, self.refill_chunk)
-                    items = list(feed.take(want, wait=not active and not pending and inflight is None))
+                    items = list(feed.take(want, wait=not active and not pending and not admits))
                     more = len(items) == want
                     # a small batch -- the feed drained and every class fits in
                     # 3/4 of the slots -- is latency-bound: long-context classes
@@ -1192,7 +1194,7 @@ class LocalEngine:
                             continue
                         pending.extend(seqs)
                     self._cont_cache.clear()
-                if not pending and not active and inflight is None:
+                if not pending and not active and not admits:
                     if feed.done:
                         break
                     continue
@@ -1203,14 +1205,19 @@ class LocalEngine:
                 forks = [st for st in forks if st.pending]
                 # ---- admission: one batched prefill for all that fit, enqueued
                 # ahead of the running batch's next step
-                if inflight is None and pending and free_slots and (
+                # (up to admit_depth in flight: the next one's host work --
+                # prompts, packing, ~130 launches -- runs under the previous
+                # one's prefill instead of after it, GPU idle)
+                if len(admits) < self.admit_depth and pending and free_slots and (
                         not active or len(free_slots) >= self.admit_min
                         or (feed.done and len(free_slots) >= len(pending))):
                     batch: List[_Seq] = []
                     ntok = 0
                     if self.longest_first and len(pending) > 1:
                         pending = deque(sorted(pending, key=lambda q: -q.free_budget))
-                    users = sum(1 for q in active if q.shared)
+                    # the resident prefix's readers: running and still prefilling
+                    users = sum(1 for q in active if q.shared) + \
+                        sum(1 for h in admits for q in h["batch"] if q.shared)
                     while pending and free_slots and len(batch) < self.ADMIT_SEQS:
                         s = pending[0]
                         if self.shared_prefix and users == 0:
@@ -1233,13 +1240,14 @@ class LocalEngine:
                         batch.append(s)
                         users += s.shared
                         ntok += nxt
-                    inflight = self._admit_launch(batch)
-                if inflight is not None:
+                    admits.append(self._admit_launch(batch))
+                if admits:
                     # nothing decodes yet: keep preparing the feed while the
                     # first prefills run rather than wait for them
-                    done = self._admit_finish(inflight, wait=not active and not more)
+                    can_admit = len(admits) < self.admit_depth and pending and free_slots
+                    done = self._admit_finish(admits[0], wait=not active and not more and not can_admit)
                     if done is not None:
-                        active.extend(s for s in inflight["batch"] if not s.done)
+                        active.extend(s for s in admits.popleft()["batch"] if not s.done)
                         for s in done:
                             retire(s)
                         while finished:
@@ -1247,7 +1255,6 @@ class LocalEngine:
                             raw = self._finish(s, partials)
                             if raw is not None:
                                 yield s.index, raw
-                        inflight = None
                         continue  # admit the next batch before this step when slots allow
                 if not active:
                     continue
@@ -1413,8 +1420,9 @@ class LocalEngine:
         finally:
             if prev_event is not None:
                 prev_event.synchronize()
-            if inflight is not None and inflight["event"] is not None:
-                inflight["event"].synchronize()
+            for h in admits:
+                if h["event"] is not None:
+                    h["event"].synchronize()
             for a, b in self._pf_events:  # device time of the prefills (stats only)
                 self.stats["prefill_gpu_s"] += a.elapsed_time(b) * 1e-3
             self._pf_events.clear()

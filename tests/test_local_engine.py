@@ -80,6 +80,22 @@ def test_engine_valid_json_and_continuous_batching(tiny):
     assert eng.stats["prefills"] == 7 and eng.stats["decode_steps"] > 0
 
 
+def test_two_admissions_in_flight_match_one(tiny):
+    """Up to ``admit_depth`` batched prefills in flight (the next admission's
+    host work under the previous prefill) and a feed refilled a chunk at a
+    time generate what one admission at a time and a whole refill do."""
+    a = LocalEngine(tiny)
+    a.admit_depth, a.refill_chunk, a.admit_min = 1, 0, 1
+    b = LocalEngine(tiny)
+    b.admit_depth, b.refill_chunk, b.admit_min = 2, 2, 1
+    inputs = _inputs(9)
+    ra, rb = a.generate(inputs, "A readme"), b.generate(inputs, "A readme")
+    for r in rb:
+        json.loads(r)
+    assert sum(x == y for x, y in zip(ra, rb)) >= len(ra) - 1
+    assert b.stats["prefills"] == a.stats["prefills"] == 9
+
+
 def test_session_defers_full_gc_and_restores_threshold(tiny):
     """A session raises the full-collection threshold while it runs (a full
     pass over the run's objects paused the GPU loop) and restores the

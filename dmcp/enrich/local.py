@@ -547,6 +547,8 @@ class LocalEngine:
         self.pipeline = pipeline
         # classes taken from the feed per loop iteration (0 = all the free slots + look-ahead at once)
         self.refill_chunk = int(os.environ.get("LOCAL_LLM_REFILL_CHUNK", "32"))
+        # fork-table rows applied once per decode launch (False: at each call)
+        self.fork_batch = os.environ.get("LOCAL_LLM_FORK_BATCH", "1") != "0"
         # batched prefills that may be in flight at once
         self.admit_depth = max(1, int(os.environ.get("LOCAL_LLM_ADMIT_DEPTH", "2")))
         # previous step's selections for host-less gathers (graphs keep their own)
@@ -987,6 +989,7 @@ class LocalEngine:
 
     def _launch_staged(self, n: int, buf: int):
         """:meth:`_launch` of the native builder's rows (``self._stage[:, :n]``)."""
+        self.model.fork_flush()  # this iteration's fork-table rows, one copy ahead of the step
         if self.graphs is not None:
             self.graphs.run_staged(self._stage, n)
             ids = self.graphs.last_ids
@@ -1008,6 +1011,7 @@ class LocalEngine:
                 srcs: List[int], alts: List[int], prows: List[int], buf: int):
         """Launches one step; enqueues the copy of its ids to pinned buffer
         ``buf``; returns the event that completes with that copy."""
+        self.model.fork_flush()
         if self.graphs is not None:
             _, ids = self.graphs.run(toks, slots, poss, mrows, srcs, alts, prows)
         else:
@@ -1108,6 +1112,10 @@ class LocalEngine:
         forks: List[_Fork] = []  # forks with branches still waiting for a slot
         nat0 = self._native
         self.model.fork_reset()  # no slot reads another's keys (a session left by an error included)
+        # branch starts and slot releases only collect their fork-table rows;
+        # each decode launch applies them in one copy (they came one small
+        # copy + write per call, ~40 us of host each, thousands per run)
+        self.model.fork_defer = self.fork_batch
 
         def release(slots: List[int]) -> None:
             """Slots back to the free list, owning all their keys again."""
@@ -1433,6 +1441,8 @@ class LocalEngine:
                 self._native.reset()
             if P:
                 self.model.clear_prefix()
+            self.model.fork_defer = False
+            self.model.fork_flush()
             if gc_threshold is not None:
                 gc.set_threshold(*gc_threshold)
 

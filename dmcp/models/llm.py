@@ -49,7 +49,7 @@ import math
 import os
 import time
 from dataclasses import asdict, dataclass, field, replace
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -266,6 +266,9 @@ class LocalLM:
         # decode graphs follow it.
         self.fork_tab = torch.zeros((self.num_slots, 2), dtype=torch.int32, device=self.device)
         self.fork_tab[:, 0] = torch.arange(self.num_slots, dtype=torch.int32, device=self.device)
+        # fork-table rows set while fork_defer is on, applied by fork_flush()
+        self.fork_defer = False
+        self._fork_pending: Dict[int, Tuple[int, int]] = {}
         # shared prefix: its length in device memory, so captured decode
         # graphs follow it
         self.prefix_len = 0
@@ -832,32 +835,47 @@ class LocalLM:
         if not (0 <= src < self.num_slots) or any(not 0 <= d < self.num_slots for d in dl) or \
                 not (0 < end <= self.cfg.max_seq):
             raise ValueError(f"fork_share: slot {src} -> {dl}, end {end}")
-        vals = torch.tensor([[int(src), int(end)]] * len(dl), dtype=torch.int32)
-        self._fork_tab_update(torch.tensor(dl, dtype=torch.long), vals)
+        self._fork_set([(d, int(src), int(end)) for d in dl])
 
-    def _fork_tab_update(self, idx: torch.Tensor, vals: torch.Tensor) -> None:
-        """``fork_tab[idx] = vals`` from host tensors, in stream order without
-        blocking the host: a pageable source would make the copy wait for the
-        stream to drain (up to a whole queued prefill, GPU idle after it)."""
+    def _fork_set(self, rows) -> None:
+        """``fork_tab[slot] = (parent, end)`` for each of ``rows``; with
+        :attr:`fork_defer` they wait for :meth:`fork_flush` (later rows of a
+        slot replace earlier ones)."""
+        if self.fork_defer:
+            for slot, parent, end in rows:
+                self._fork_pending[slot] = (parent, end)
+            return
+        self._fork_tab_update(rows)
+
+    def fork_flush(self) -> None:
+        """Applies the deferred fork-table rows: one copy + one indexed write
+        (the engine calls this before each decode launch)."""
+        if self._fork_pending:
+            rows = [(k, p, e) for k, (p, e) in self._fork_pending.items()]
+            self._fork_pending.clear()
+            self._fork_tab_update(rows)
+
+    @torch.inference_mode()
+    def _fork_tab_update(self, rows) -> None:
+        """``fork_tab[slot] = (parent, end)`` from host rows (distinct slots),
+        in stream order without blocking the host: a pageable source would
+        make the copy wait for the stream to drain (up to a whole queued
+        prefill, GPU idle after it)."""
+        both = torch.tensor(rows, dtype=torch.int64)
         if self.device.type == "cuda":
-            both = torch.cat([idx.to(torch.int64).view(-1, 1), vals.to(torch.int64)], 1).pin_memory()
-            both = both.to(self.device, non_blocking=True)
-            idx, vals = both[:, 0], both[:, 1:].to(torch.int32)
-        self.fork_tab.index_copy_(0, idx, vals)
+            both = both.pin_memory().to(self.device, non_blocking=True)
+        self.fork_tab.index_copy_(0, both[:, 0], both[:, 1:].to(torch.int32))
 
     @torch.inference_mode()
     def fork_reset(self) -> None:
         """No slot has a parent (every slot owns all its keys)."""
+        self._fork_pending.clear()
         self.fork_tab[:, 1] = 0
 
     @torch.inference_mode()
     def fork_clear(self, slots: Sequence[int]) -> None:
         """``slots`` own all their keys again (a freed or newly admitted slot)."""
-        sl = [int(x) for x in slots]
-        if not sl:
-            return
-        self._fork_tab_update(torch.tensor(sl, dtype=torch.long),
-                              torch.tensor([[x, 0] for x in sl], dtype=torch.int32))
+        self._fork_set([(int(x), int(x), 0) for x in slots])
 
     def decode_select(self, tokens: torch.Tensor, slots: torch.Tensor, positions: torch.Tensor,
                       masks: torch.Tensor, mask_idx: torch.Tensor) -> tuple:

@@ -91,8 +91,30 @@ class ProjectRepository:
                       "last_commit_hash, created_at, updated_at, description, base_package, "
                       "NULL AS graph_data")
 
+    # SQLite (``db.graph_table``, migration 9): the graph JSON in its own
+    # table, so a status or lease write never rewrites it -- every statement
+    # above that returns graph_data reads it through this join
+    _SPLIT_SELECT = ("SELECT p.id, p.name, p.repository_url, p.default_branch, p.status, p.last_analyzed_at, "
+                     "p.last_commit_hash, p.created_at, p.updated_at, p.description, p.base_package, "
+                     "g.graph_data AS graph_data FROM projects p {join} project_graphs g ON g.project_id = p.id")
+    UPSERT_GRAPH = ("INSERT INTO project_graphs (project_id, graph_data) VALUES (?, ?) "
+                    "ON CONFLICT (project_id) DO UPDATE SET graph_data = excluded.graph_data")
+    DELETE_GRAPH = "DELETE FROM project_graphs WHERE project_id = ?"
+    UPDATE_SPLIT = ("UPDATE projects SET name=?, default_branch=?, status=?, last_analyzed_at=?, "
+                    "last_commit_hash=?, updated_at=?, description=?, base_package=?, "
+                    "graph_version = graph_version + 1 WHERE id=?")
+
     def __init__(self, db: Database) -> None:
         self.db = db
+        self.split = bool(getattr(db, "graph_table", False))
+        if self.split:
+            sel = self._SPLIT_SELECT.format(join="LEFT JOIN")
+            self.FIND_BY_ID = f"{sel} WHERE p.id = ?"
+            self.FIND_BY_REPOSITORY_URL = f"{sel} WHERE p.repository_url = ?"
+            self.FIND_BY_NAME = f"{sel} WHERE p.name = ? ORDER BY p.created_at DESC LIMIT 1"
+            self.FIND_ALL = f"{sel} ORDER BY p.created_at DESC"
+            self.FIND_BY_STATUS = f"{sel} WHERE p.status = ?"
+            self.FIND_ALL_WITH_GRAPH = self._SPLIT_SELECT.format(join="JOIN")
 
     @staticmethod
     def _map(row) -> Project:
@@ -110,7 +132,9 @@ class ProjectRepository:
                 "graph_data, base_package) VALUES (?,?,?,?,?,?,?,?,?,?,?,?)",
                 (p.id, p.name, p.repository_url.value, p.default_branch, p.status.value,
                  to_iso(p.last_analyzed_at), p.last_commit_hash, to_iso(p.created_at),
-                 to_iso(p.updated_at), p.description, p.graph_data, p.base_package))
+                 to_iso(p.updated_at), p.description, None if self.split else p.graph_data, p.base_package))
+            if self.split and p.graph_data is not None:
+                c.execute(self.UPSERT_GRAPH, (p.id, p.graph_data))
 
     # a full update replaces the graph: its version moves, so the graph cache
     # of every other process reloads it (GraphCache.refresh)
@@ -157,7 +181,9 @@ class ProjectRepository:
     def graph_versions(self) -> Dict[str, Tuple[str, int]]:
         """id -> (name, graph version) of every project with a persisted graph
         (one index-free scan of the small projects table; no graph JSON read)."""
-        rows = self.db.query("SELECT id, name, graph_version FROM projects WHERE graph_data IS NOT NULL")
+        rows = self.db.query("SELECT p.id AS id, p.name AS name, p.graph_version AS graph_version FROM projects p "
+                             "JOIN project_graphs g ON g.project_id = p.id" if self.split else
+                             "SELECT id, name, graph_version FROM projects WHERE graph_data IS NOT NULL")
         return {r["id"]: (r["name"], int(r["graph_version"] or 0)) for r in rows}
 
     def graph_version(self, project_id: str) -> Optional[int]:
@@ -170,9 +196,21 @@ class ProjectRepository:
                 p.last_commit_hash, to_iso(p.updated_at), p.description, p.graph_data,
                 p.base_package, p.id)
 
+    def update_statements(self, p: Project) -> List[Tuple[str, tuple]]:
+        """The full update of ``p`` as (sql, params) statements of one
+        transaction (the graph's own row on SQLite)."""
+        if not self.split:
+            return [(self.UPDATE, self.update_params(p))]
+        row = (p.name, p.default_branch, p.status.value, to_iso(p.last_analyzed_at), p.last_commit_hash,
+               to_iso(p.updated_at), p.description, p.base_package, p.id)
+        graph = (self.UPSERT_GRAPH, (p.id, p.graph_data)) if p.graph_data is not None else \
+            (self.DELETE_GRAPH, (p.id,))
+        return [(self.UPDATE_SPLIT, row), graph]
+
     def update(self, p: Project) -> None:
         with self.db.transaction() as c:
-            c.execute(self.UPDATE, self.update_params(p))
+            for sql, params in self.update_statements(p):
+                c.execute(sql, params)
 
     def update_status(self, p: Project) -> None:
         """Status-only update that does not rewrite the graph column."""
@@ -212,7 +250,9 @@ class ProjectRepository:
         vals = [s.value for s in statuses]
         if not vals:
             return []
-        q = f"SELECT * FROM projects WHERE status IN ({','.join('?' * len(vals))}) ORDER BY created_at"
+        marks = ','.join('?' * len(vals))
+        q = (f"{self._SPLIT_SELECT.format(join='LEFT JOIN')} WHERE p.status IN ({marks}) ORDER BY p.created_at"
+             if self.split else f"SELECT * FROM projects WHERE status IN ({marks}) ORDER BY created_at")
         return [self._map(r) for r in self.db.query(q, vals)]
 
     def find_all_with_graph(self) -> List[Project]:
@@ -785,9 +825,10 @@ class ProjectRowsWriter:
         writer, ``:memory:``): update the project after :meth:`wait` then."""
         if self._native is None or self.closed:
             return False
-        frozen = (ProjectRepository.update_params(project),)
-        self._keep.append(frozen)
-        self._native.put(ProjectRepository.UPDATE, frozen)
+        for sql, params in self.repos.projects.update_statements(project):
+            frozen = (params,)
+            self._keep.append(frozen)
+            self._native.put(sql, frozen)
         return True
 
     def close(self) -> None:

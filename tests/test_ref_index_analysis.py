@@ -17,7 +17,7 @@ import time
 import pytest
 
 from dmcp.store.db import Database
-from dmcp.store.repositories import ProjectRepository, Repositories, SourceClassRepository, SourceMethodRepository
+from dmcp.store.repositories import Repositories, SourceClassRepository, SourceMethodRepository
 
 FIXTURE = "/root/reference/src/test/resources/index-analysis-data.sql"
 TEST_PROJECT_ID = "5677b1e8-da1b-4dda-a5a5-71668d09f5f4"      # IndexAnalysisTest.java:125
@@ -55,8 +55,9 @@ def test_analyze_all_queries(tmp_path):
                                                                        "source_methods")}
     assert counts == {"projects": 50, "source_classes": 850, "source_methods": 2250}
     cases = {
-        "ProjectRepository.FIND_BY_ID": (ProjectRepository.FIND_BY_ID, (TEST_PROJECT_ID,)),
-        "ProjectRepository.FIND_BY_REPOSITORY_URL": (ProjectRepository.FIND_BY_REPOSITORY_URL,
+        # the SQLite statements (graph JSON joined from project_graphs)
+        "ProjectRepository.FIND_BY_ID": (repos.projects.FIND_BY_ID, (TEST_PROJECT_ID,)),
+        "ProjectRepository.FIND_BY_REPOSITORY_URL": (repos.projects.FIND_BY_REPOSITORY_URL,
                                                      ("https://github.com/test/project-0.git",)),
         "SourceClassRepository.FIND_BY_ID": (SourceClassRepository.FIND_BY_ID, (TEST_CLASS_ID,)),
         "SourceClassRepository.FIND_BY_PROJECT_ID": (SourceClassRepository.FIND_BY_PROJECT_ID, (TEST_PROJECT_ID,)),

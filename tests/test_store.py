@@ -35,6 +35,43 @@ def test_migrations_idempotent(tmp_path):
     db2.close()
 
 
+def test_graph_in_its_own_table(tmp_path):
+    """Migration 9: the graph JSON lives in project_graphs (a status write
+    never rewrites it); graphs already in projects.graph_data move over, the
+    repository reads and writes them there, and deleting the project deletes
+    its graph."""
+    path = str(tmp_path / "g.db")
+    db = Database(path)
+    repos = Repositories(db)
+    p = _project()
+    p.update_graph_data('{"nodes":{"a":1}}')
+    repos.projects.save(p)
+    assert db.query_one("SELECT graph_data FROM projects WHERE id = ?", (p.id,))[0] is None
+    assert db.query_one("SELECT graph_data FROM project_graphs WHERE project_id = ?", (p.id,))[0] == p.graph_data
+    p.start_analysis()
+    repos.projects.update_status(p)
+    assert repos.projects.find_by_id(p.id).graph_data == '{"nodes":{"a":1}}'
+    assert set(repos.projects.graph_versions()) == {p.id}
+    assert [x.id for x in repos.projects.find_all_with_graph()] == [p.id]
+    assert repos.projects.find_by_statuses([ProjectStatus.ANALYZING])[0].graph_data == p.graph_data
+    p.update_graph_data(None)
+    repos.projects.update(p)  # a full update without a graph removes it
+    assert repos.projects.find_by_id(p.id).graph_data is None and repos.projects.graph_versions() == {}
+    # a database from before migration 9 (the graph in the projects row)
+    with db.transaction() as c:
+        c.execute("UPDATE projects SET graph_data = ? WHERE id = ?", ('{"old":true}', p.id))
+        c.execute("DROP TABLE project_graphs")
+        c.execute("DELETE FROM schema_version WHERE version = 9")
+    db.close()
+    db = Database(path)
+    repos = Repositories(db)
+    assert repos.projects.find_by_id(p.id).graph_data == '{"old":true}'
+    assert db.query_one("SELECT graph_data FROM projects WHERE id = ?", (p.id,))[0] is None
+    repos.projects.delete(p.id)
+    assert db.query_one("SELECT COUNT(*) FROM project_graphs")[0] == 0
+    db.close()
+
+
 def test_project_repository_roundtrip(repos):
     p = _project()
     p.update_description("d")

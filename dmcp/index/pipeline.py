@@ -283,7 +283,8 @@ class Indexer:
                 with span("analyze.phase1_commit", stats):
                     writer.wait()  # no-op when enrichment already waited
                 for k, v in writer.timings.items():
-                    stats[f"analyze.writer_{k[:-3]}"] = v
+                    if k.endswith("_ms"):  # (the *_s entries are absolute milestones)
+                        stats[f"analyze.writer_{k[:-3]}"] = v
                 with span("analyze.publish", stats):
                     if not in_swap:
                         self.repos.projects.update(project)

@@ -135,14 +135,18 @@ void BulkWriter::run() {
             return std::chrono::duration<double, std::milli>(b - a).count();
         };
         auto t0 = clock::now();
+        open_ms_ = ms(t_start_, t0);
         c.exec("BEGIN IMMEDIATE");
         in_tx = true;
         for (const Batch& b : setup_) c.run(b);
         setup_.clear();
         setup_ms_ = ms(t0, clock::now());
+        t_setup_ = clock::now();
         for (;;) {
             Item it;
+            auto tw = clock::now();
             pop(it);
+            idle_ms_ += ms(tw, clock::now());  // waiting for the producer's rows
             if (it.op == Op::Abort) {
                 c.exec("ROLLBACK");
                 in_tx = false;
@@ -153,6 +157,8 @@ void BulkWriter::run() {
                 auto tc = clock::now();
                 c.exec("COMMIT");
                 commit_ms_ = ms(tc, clock::now());
+                t_commit_ = tc;
+                t_end_ = clock::now();
                 in_tx = false;
                 return;
             }

@@ -15,6 +15,7 @@
 #include <deque>
 #include <memory>
 #include <mutex>
+#include <chrono>
 #include <string>
 #include <thread>
 #include <utility>
@@ -65,6 +66,16 @@ class BulkWriter {
     double setup_ms() const { return setup_ms_; }
     double rows_ms() const { return rows_ms_; }
     double commit_ms() const { return commit_ms_; }
+    double idle_ms() const { return idle_ms_; }  // waits for rows between the setup and the commit request
+    double open_ms() const { return open_ms_; }  // from construction to BEGIN (thread start, open, pragmas)
+    // steady_clock (CLOCK_MONOTONIC, Python's time.perf_counter on Linux) seconds of the writer's milestones
+    static double secs(std::chrono::steady_clock::time_point t) {
+        return std::chrono::duration<double>(t.time_since_epoch()).count();
+    }
+    double t_start() const { return secs(t_start_); }
+    double t_setup() const { return secs(t_setup_); }
+    double t_commit() const { return secs(t_commit_); }
+    double t_end() const { return secs(t_end_); }
 
   private:
     enum class Op { Rows, Commit, Abort };
@@ -85,7 +96,9 @@ class BulkWriter {
     std::thread thread_;
     std::string error_;
     int64_t rows_written_ = 0;
-    double setup_ms_ = 0, rows_ms_ = 0, commit_ms_ = 0;
+    double setup_ms_ = 0, rows_ms_ = 0, commit_ms_ = 0, idle_ms_ = 0, open_ms_ = 0;
+    std::chrono::steady_clock::time_point t_start_ = std::chrono::steady_clock::now();
+    std::chrono::steady_clock::time_point t_setup_{}, t_commit_{}, t_end_{};
     bool joined_ = false;
     bool commit_requested_ = false;
 };

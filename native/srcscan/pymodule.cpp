@@ -1167,6 +1167,12 @@ PYBIND11_MODULE(_srcscan, m) {
             d["setup_ms"] = w.setup_ms();
             d["rows_ms"] = w.rows_ms();
             d["commit_ms"] = w.commit_ms();
+            d["idle_ms"] = w.idle_ms();
+            d["open_ms"] = w.open_ms();
+            d["t_start_s"] = w.t_start();
+            d["t_setup_s"] = w.t_setup();
+            d["t_commit_s"] = w.t_commit();
+            d["t_end_s"] = w.t_end();
             return d;
         });
     m.attr("ABI_VERSION") = 5;

@@ -66,7 +66,8 @@ class BulkWriter {
     double setup_ms() const { return setup_ms_; }
     double rows_ms() const { return rows_ms_; }
     double commit_ms() const { return commit_ms_; }
-    double idle_ms() const { return idle_ms_; }  // waits for rows between the setup and the commit request
+    double idle_ms() const { return idle_ms_; }
+    double free_ms() const { return free_ms_; }  // releasing inserted batches  // waits for rows between the setup and the commit request
     double open_ms() const { return open_ms_; }  // from construction to BEGIN (thread start, open, pragmas)
     // steady_clock (CLOCK_MONOTONIC, Python's time.perf_counter on Linux) seconds of the writer's milestones
     static double secs(std::chrono::steady_clock::time_point t) {
@@ -96,7 +97,7 @@ class BulkWriter {
     std::thread thread_;
     std::string error_;
     int64_t rows_written_ = 0;
-    double setup_ms_ = 0, rows_ms_ = 0, commit_ms_ = 0, idle_ms_ = 0, open_ms_ = 0;
+    double setup_ms_ = 0, rows_ms_ = 0, commit_ms_ = 0, idle_ms_ = 0, open_ms_ = 0, free_ms_ = 0;
     std::chrono::steady_clock::time_point t_start_ = std::chrono::steady_clock::now();
     std::chrono::steady_clock::time_point t_setup_{}, t_commit_{}, t_end_{};
     bool joined_ = false;

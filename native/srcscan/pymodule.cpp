@@ -1168,6 +1168,7 @@ PYBIND11_MODULE(_srcscan, m) {
             d["rows_ms"] = w.rows_ms();
             d["commit_ms"] = w.commit_ms();
             d["idle_ms"] = w.idle_ms();
+            d["free_ms"] = w.free_ms();
             d["open_ms"] = w.open_ms();
             d["t_start_s"] = w.t_start();
             d["t_setup_s"] = w.t_setup();

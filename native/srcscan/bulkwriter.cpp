@@ -165,6 +165,19 @@ void BulkWriter::run() {
         c.exec("PRAGMA temp_store = MEMORY");
         c.exec("PRAGMA cache_size = -65536");
         c.exec("PRAGMA foreign_keys = OFF");
+        {
+            // each analysis opens a fresh connection, so its page cache starts
+            // cold: the old rows' deletes read their B-tree pages through the
+            // memory map instead of one read() per page
+            static const long long mmap_bytes = [] {
+                const char* e = std::getenv("DMCP_WRITER_MMAP");
+                return e ? std::atoll(e) : (1LL << 30);
+            }();
+            if (mmap_bytes > 0) {
+                const std::string q = "PRAGMA mmap_size = " + std::to_string(mmap_bytes);
+                c.exec(q.c_str());
+            }
+        }
         using clock = std::chrono::steady_clock;
         auto ms = [](clock::time_point a, clock::time_point b) {
             return std::chrono::duration<double, std::milli>(b - a).count();

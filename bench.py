@@ -70,6 +70,10 @@ def parse_args(argv=None):
     ap.add_argument("--lang-files", type=int, default=1000,
                     help="source files of the TS / Go indexing runs (extra.tsIndex / extra.goIndex; 0 = skip)")
     ap.add_argument("--lang-steps", type=int, default=5)
+    ap.add_argument("--pool-classes", type=int, default=257,
+                    help="classes of extra.enrichLocalPool: ONE project dealt by ONE GpuWorkerPool over --gpus GPUs "
+                         "(the service's production layout, strong scaling; 0 = skip)")
+    ap.add_argument("--pool-preset", default="llama3.2-1b-code")
     ap.add_argument("--small-project-classes", type=int, default=33,
                     help="classes of the latency-bound enrichment run (extra.enrichLocal*.smallProject: what "
                          "each of 8 GPUs gets when one 257-class project is dealt over 8; 0 = skip)")
@@ -77,6 +81,7 @@ def parse_args(argv=None):
 
 
 EXTRA_KEYS = {"dmcp-coder-1b": "enrichLocal", "llama3.2-1b-code": "enrichLocalLlama"}
+POOL_KEY = "__pool__"
 
 
 def _spawn_enrich_pools(args):
@@ -99,6 +104,15 @@ def _spawn_enrich_pools(args):
                      "max_rows": max(mb, min(1024, max(256, mb * 3 // 2))), "seed": 0}
             pools[name] = GpuWorkerPool([f"cuda:{local}"], model, engine={"max_new_tokens": 4096}, init=False,
                                         start_timeout_s=600)
+        if args.pool_classes > 0 and int(os.environ.get("RANK", "0")) == 0:
+            # extra.enrichLocalPool: rank 0's service-style pool, one worker per
+            # GPU of the job (idle children until its turn, after the per-rank runs)
+            n = max(1, min(args.gpus, torch.cuda.device_count()))
+            model = {"preset": args.pool_preset, "kv_dtype": args.enrich_local_kv,
+                     "prefill_dtype": args.enrich_local_prefill, "max_batch": mb,
+                     "max_rows": max(mb, min(1024, max(256, mb * 3 // 2))), "seed": 0}
+            pools[POOL_KEY] = GpuWorkerPool([f"cuda:{i}" for i in range(n)], model,
+                                            engine={"max_new_tokens": 4096}, init=False, start_timeout_s=900)
         return pools
     except Exception as e:  # the headline does not depend on it
         logging.getLogger("bench").warning("enrichment worker not started: %s", e)
@@ -209,6 +223,50 @@ def _enrich_local(pool, args, ctx, work, rank):
                            "prefill_dtype": args.enrich_local_prefill,
                            "batch": args.enrich_local_batch, "workers_per_rank": len(pool.workers),
                            "path": "analyze_project -> streamed Phase 2 -> GPU worker process"}}
+    finally:
+        app.db.close()
+
+
+def _enrich_pool(pool, args, work) -> dict:
+    """extra.enrichLocalPool: the production layout -- ONE project dealt by
+    ONE GpuWorkerPool over every GPU of the job (dmcp/enrich/workers.py:
+    classes dealt evenly, one worker process per GPU), run by rank 0 alone
+    after the per-rank runs.  With --gpus 1, 2, 4, 8 the driver's runs give
+    this fixed-size project's strong-scaling curve."""
+    from dmcp.app import App
+    from dmcp.config import Config
+    from dmcp.enrich.workers import ProcessLLMBackend
+    from dmcp.utils import synth
+    t_init = time.perf_counter()
+    pool.init()
+    init_s = time.perf_counter() - t_init
+    be = ProcessLLMBackend(pool)
+    cfg = Config(db_path=os.path.join(work, "pool.db"), git_clone_base_path=os.path.join(work, "pclones"),
+                 require_enrichment_for_analyze=True, recover_stuck_on_start=False)
+    app = App(cfg, backend=be)
+    try:
+        warm = os.path.join(work, "poolwarm")
+        synth.java_spring_repo(warm, n_classes=8 * len(pool.workers), base_package="co.acme.pwarm", seed=401)
+        app.indexer.analyze_project(warm)  # every worker's first batch (allocator, first replays)
+        repo = os.path.join(work, "poolrepo")
+        synth.java_spring_repo(repo, n_classes=args.pool_classes, base_package="co.acme.pool", seed=402)
+        for w in pool.workers:
+            w.stats = {}
+        pool.per_worker_items = {}
+        t0 = time.perf_counter()
+        r = app.indexer.analyze_project(repo)
+        el = time.perf_counter() - t0
+        st = be.stats()
+        per = dict(getattr(pool, "per_worker_items", {}) or {})
+        return {"classesPerSec": round(r.classes_analyzed / el, 2), "classes": r.classes_analyzed,
+                "enriched": int(r.stats.get("enriched", 0)), "enrichFailed": r.stats.get("enrichFailed"),
+                "elapsedS": round(el, 3), "phase2S": round(r.stats.get("analyze.phase2", 0.0) / 1e3, 3),
+                "workers": len(pool.workers), "classesPerWorker": {str(k): v for k, v in sorted(per.items())},
+                "generatedTokensPerSec": round(st.get("generated_tokens", 0) / el, 1),
+                "decodeSteps": int(st.get("decode_steps", 0)), "workerInitS": round(init_s, 1),
+                "config": {"model": f"{pool.model['preset']} (random init)", "kv_dtype": args.enrich_local_kv,
+                           "batch": args.enrich_local_batch,
+                           "path": "analyze_project -> streamed Phase 2 -> ONE GpuWorkerPool, one worker per GPU"}}
     finally:
         app.db.close()
 
@@ -382,6 +440,14 @@ def main(argv=None) -> int:
                     extra[key] = {"error": repr(e)[:300]}
                 finally:
                     pools.pop(name).close()  # its KV slab goes before the next preset's
+        if POOL_KEY in pools:  # rank 0 only; no collective inside
+            try:
+                extra["enrichLocalPool"] = _enrich_pool(pools[POOL_KEY], args, work)
+            except Exception as e:
+                logging.getLogger("bench").exception("enrichLocalPool failed")
+                extra["enrichLocalPool"] = {"error": repr(e)[:300]}
+            finally:
+                pools.pop(POOL_KEY).close()
         value = total_classes / elapsed if elapsed > 0 else 0.0
         ms_per_step = elapsed / max(1, args.steps) * 1e3
         if rank == 0:

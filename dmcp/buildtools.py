@@ -30,7 +30,8 @@ NATIVE = os.path.join(ROOT, "native", "srcscan")
 BUILD = os.path.join(ROOT, "build", "native")
 BIN = os.path.join(ROOT, "bin")
 
-CORE_SOURCES = ["common.cpp", "java_frontend.cpp", "ts_frontend.cpp", "go_frontend.cpp", "project.cpp", "gitobj.cpp"]
+CORE_SOURCES = ["common.cpp", "java_frontend.cpp", "ts_frontend.cpp", "go_frontend.cpp", "project.cpp", "gitobj.cpp",
+                "wire.cpp"]
 MODULE_SOURCES = ["bulkwriter.cpp"]
 CXX = os.environ.get("CXX", "g++")
 CXXFLAGS = ["-std=c++17", "-O3", "-fPIC", "-Wall", "-Wno-unused-function", "-pthread"]

@@ -49,6 +49,10 @@ class Config:
     # a Llama-format checkpoint directory (config.json + *.safetensors +
     # tokenizer.json) used instead of the random-initialised preset
     local_llm_model_path: str = ""
+    # without a checkpoint the local backend refuses to enrich (its random
+    # weights would write noise descriptions that Phase 3 and resume never
+    # redo); bench / smoke / tests opt in to the random-initialised presets
+    local_llm_allow_random_weights: bool = False
     # fp8 (e4m3) KV cache: half the decode-attention bytes; every tuned and
     # benchmarked number is fp8 (56.8 vs 43.9 classes/s bf16, profiles/enrich_*_r3_prompt.jsonl)
     local_llm_kv_dtype: str = "fp8"
@@ -139,6 +143,7 @@ class Config:
             "REQUIRE_ENRICHMENT_FOR_ANALYZE": "require_enrichment_for_analyze",
             "LOCAL_LLM_PRESET": "local_llm_preset",
             "LOCAL_LLM_MODEL_PATH": "local_llm_model_path",
+            "LOCAL_LLM_ALLOW_RANDOM_WEIGHTS": "local_llm_allow_random_weights",
             "LOCAL_LLM_KV_DTYPE": "local_llm_kv_dtype",
             "LOCAL_LLM_PREFILL_DTYPE": "local_llm_prefill_dtype",
             "LOCAL_LLM_DECODE_DTYPE": "local_llm_decode_dtype",

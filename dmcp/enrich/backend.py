@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import json
 import logging
+import os
 import random
 import threading
 import time
@@ -105,10 +106,28 @@ def build_enrichment_prompt(inp: EnrichmentInput, readme: Optional[str],
         methods=", ".join(inp.method_names))
 
 
+# enrichment_source values (source_classes.enrichment_source) of backends
+# whose descriptions carry no information about the code: random-initialised
+# local presets, the model-free echo engine, the offline fake.  Phase 3 and
+# resume-enrichment redo such rows once a real backend is configured.
+SYNTHETIC_PREFIX = "synthetic:"
+
+
+def is_synthetic(source_tag: Optional[str]) -> bool:
+    return bool(source_tag) and source_tag.startswith(SYNTHETIC_PREFIX)
+
+
 class EnrichmentBackend:
     """Base: subclasses implement :meth:`enrich_class`; the batch fan-out is shared."""
 
     name = "base"
+
+    @property
+    def source_tag(self) -> str:
+        """What the enrichment rows written through this backend record as
+        their ``enrichment_source`` (:data:`SYNTHETIC_PREFIX`: placeholder
+        descriptions a real backend replaces)."""
+        return self.name
 
     def __init__(self, max_concurrent: int = 5) -> None:
         self.max_concurrent = max(1, int(max_concurrent))
@@ -203,6 +222,22 @@ class NullBackend(EnrichmentBackend):
         return EnrichmentResult.failure(inp.full_class_name, "enrichment disabled")
 
 
+class RefusedBackend(NullBackend):
+    """A configured backend that must not run: analysis then refuses like the
+    reference's READ_ONLY_MODE (``CodeContextService.java:149-156``) with
+    :attr:`disabled_reason` as the message, or indexes statically when
+    ``REQUIRE_ENRICHMENT_FOR_ANALYZE=false``."""
+
+    name = "refused"
+
+    def __init__(self, reason: str) -> None:
+        super().__init__(1)
+        self.disabled_reason = reason
+
+    def enrich_class(self, inp: EnrichmentInput, readme: Optional[str]) -> EnrichmentResult:
+        return EnrichmentResult.failure(inp.full_class_name, self.disabled_reason)
+
+
 class FakeBackend(EnrichmentBackend):
     """Deterministic offline backend.
 
@@ -212,6 +247,7 @@ class FakeBackend(EnrichmentBackend):
     """
 
     name = "fake"
+    source_tag = SYNTHETIC_PREFIX + "fake"
 
     def __init__(self, max_concurrent: int = 5,
                  responder: Optional[Callable[[EnrichmentInput], str]] = None,
@@ -244,6 +280,10 @@ class AnthropicBackend(EnrichmentBackend):
     """Anthropic Messages API client (stdlib HTTP, retries with backoff)."""
 
     name = "anthropic"
+
+    @property
+    def source_tag(self) -> str:
+        return f"anthropic:{self.model}"
     API_VERSION = "2023-06-01"
 
     def __init__(self, api_key: str, model: str, max_tokens: int = 16384, timeout_s: float = 240.0,
@@ -350,10 +390,11 @@ class LazyBackend(EnrichmentBackend):
     mode checks it, ``CodeContextService.java:149-156``)."""
 
     def __init__(self, factory: Callable[[], EnrichmentBackend], name: str = "lazy",
-                 enabled: bool = True) -> None:
+                 enabled: bool = True, source_tag: Optional[str] = None) -> None:
         super().__init__(1)
         self._factory = factory
         self._enabled = enabled
+        self._source_tag = source_tag
         self._built: Optional[EnrichmentBackend] = None
         self._build_lock = threading.Lock()
         self.name = name
@@ -365,6 +406,12 @@ class LazyBackend(EnrichmentBackend):
     @property
     def built(self) -> bool:
         return self._built is not None
+
+    @property
+    def source_tag(self) -> str:  # known without building (the rows' tag)
+        if self._source_tag is not None:
+            return self._source_tag
+        return self.get().source_tag
 
     def get(self) -> EnrichmentBackend:
         with self._build_lock:
@@ -405,8 +452,28 @@ def create_backend(cfg) -> EnrichmentBackend:
     if kind == "fake":
         return FakeBackend(cfg.enrich_max_concurrent)
     if kind == "local":
+        tag = local_source_tag(cfg)
+        if is_synthetic(tag) and not getattr(cfg, "local_llm_allow_random_weights", False):
+            reason = (f"ENRICH_BACKEND=local has no checkpoint (LOCAL_LLM_MODEL_PATH is unset): the "
+                      f"{cfg.local_llm_preset!r} preset's random-initialised weights would write noise "
+                      f"descriptions. Set LOCAL_LLM_MODEL_PATH to a Llama-format checkpoint directory, or "
+                      f"LOCAL_LLM_ALLOW_RANDOM_WEIGHTS=true for benchmarks and tests")
+            LOG.error("%s", reason)
+            return RefusedBackend(reason)
+
         def build() -> EnrichmentBackend:
             from .local import LocalLLMBackend
             return LocalLLMBackend.from_config(cfg)
-        return LazyBackend(build, "local")
+        return LazyBackend(build, "local", source_tag=tag)
     return NullBackend(1)
+
+
+def local_source_tag(cfg) -> str:
+    """``enrichment_source`` of the local backend: the checkpoint directory,
+    or a synthetic tag for the random-initialised presets and the echo
+    engine."""
+    path = (getattr(cfg, "local_llm_model_path", "") or "").strip()
+    if path:
+        return f"local:{os.path.abspath(path)}"
+    preset = getattr(cfg, "local_llm_preset", "") or "dmcp-coder-1b"
+    return SYNTHETIC_PREFIX + ("echo" if preset == "echo" else f"random-init:{preset}")

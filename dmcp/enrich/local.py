@@ -52,7 +52,7 @@ from typing import Any, Deque, Dict, Iterable, Iterator, List, Optional, Sequenc
 import torch
 
 from ..models.llm import LocalLM, LMConfig, DecodeGraphs, preset
-from .backend import EnrichmentBackend, build_enrichment_prompt
+from .backend import SYNTHETIC_PREFIX, EnrichmentBackend, build_enrichment_prompt
 from .jsonfix import parse_enrichment_response
 from .tokenizer import ByteTokenizer
 from .tokenizer import _Base as _TokBase
@@ -1165,9 +1165,9 @@ class LocalEngine:
         # loop for 25-45 ms, GPU idle, about once per run
         # (profiles/engine_gc_r5.txt): the session defers full collections
         # (young ones still run; refcounting frees everything acyclic)
-        gc_threshold = gc.get_threshold() if self.gc_full_every else None
-        if gc_threshold is not None:
-            gc.set_threshold(gc_threshold[0], gc_threshold[1], max(gc_threshold[2], self.gc_full_every))
+        gc_deferred = bool(self.gc_full_every)
+        if gc_deferred:
+            _gc_defer_enter(self.gc_full_every)
         try:
             while True:
                 # ---- refill the look-ahead (blocking only when idle)
@@ -1443,8 +1443,38 @@ class LocalEngine:
                 self.model.clear_prefix()
             self.model.fork_defer = False
             self.model.fork_flush()
-            if gc_threshold is not None:
-                gc.set_threshold(*gc_threshold)
+            if gc_deferred:
+                _gc_defer_exit()
+
+
+# Full-collection deferral is process-wide (gc thresholds are global) while
+# several engines may run sessions at once (_threaded_stream): the first
+# session to enter saves the threshold, the last to leave restores it -- a
+# per-session save / restore interleaved across threads could restore a
+# raised value and leave full collections deferred for the process' life.
+_GC_LOCK = threading.Lock()
+_GC_STATE = {"active": 0, "saved": None, "every": 0}
+
+
+def _gc_defer_enter(every: int) -> None:
+    with _GC_LOCK:
+        if _GC_STATE["active"] == 0:
+            _GC_STATE["saved"] = gc.get_threshold()
+            _GC_STATE["every"] = 0
+        _GC_STATE["active"] += 1
+        if every > _GC_STATE["every"]:
+            _GC_STATE["every"] = every
+            t0, t1, t2 = _GC_STATE["saved"]
+            gc.set_threshold(t0, t1, max(t2, every))
+
+
+def _gc_defer_exit() -> None:
+    with _GC_LOCK:
+        _GC_STATE["active"] -= 1
+        if _GC_STATE["active"] == 0 and _GC_STATE["saved"] is not None:
+            gc.set_threshold(*_GC_STATE["saved"])
+            _GC_STATE["saved"] = None
+            _GC_STATE["every"] = 0
 
 
 class LocalLLMBackend(EnrichmentBackend):
@@ -1458,6 +1488,15 @@ class LocalLLMBackend(EnrichmentBackend):
         super().__init__(max_concurrent=max(1, len(engines)))
         self.engines = list(engines)
         self.preferred_batch_size = sum(e.cfg.max_batch for e in self.engines) * 2
+
+    @property
+    def source_tag(self) -> str:
+        m = self.engines[0].model if self.engines else None
+        ck = getattr(m, "checkpoint", None)
+        if ck:
+            return f"local:{os.path.abspath(ck)}"
+        name = getattr(getattr(m, "cfg", None), "name", "echo")
+        return SYNTHETIC_PREFIX + ("echo" if m is None or not hasattr(m, "cfg") else f"random-init:{name}")
 
     @classmethod
     def from_config(cls, cfg) -> EnrichmentBackend:

@@ -52,7 +52,7 @@ import threading
 import time
 from typing import Any, Dict, Iterable, Iterator, List, Optional, Sequence, Tuple
 
-from .backend import EnrichmentBackend
+from .backend import SYNTHETIC_PREFIX, EnrichmentBackend
 from .jsonfix import parse_enrichment_response
 from .types import EnrichmentInput, EnrichmentResult
 
@@ -573,6 +573,14 @@ class ProcessLLMBackend(EnrichmentBackend):
         super().__init__(max_concurrent=1)
         self.pool = pool
         self.preferred_batch_size = pool.capacity * len(pool.workers)
+
+    @property
+    def source_tag(self) -> str:
+        spec = getattr(self.pool, "model", None) or {}
+        if spec.get("path"):
+            return f"local:{os.path.abspath(spec['path'])}"
+        p = spec.get("preset", "dmcp-coder-1b")
+        return SYNTHETIC_PREFIX + ("echo" if p == "echo" else f"random-init:{p}")
 
     @classmethod
     def from_config(cls, cfg, devices: Optional[Sequence[str]] = None) -> "ProcessLLMBackend":

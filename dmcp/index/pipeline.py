@@ -38,7 +38,7 @@ from concurrent.futures import TimeoutError as FutureTimeout
 from dataclasses import dataclass, field
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
-from ..enrich.backend import EnrichmentBackend, NullBackend
+from ..enrich.backend import EnrichmentBackend, NullBackend, is_synthetic
 from ..enrich.types import EnrichmentInput, EnrichmentResult, SizedIter, normalize_method_name
 from ..graph.cache import GraphCache
 from ..graph.project_graph import MethodEnrichmentData, MethodInfo, ProjectGraph
@@ -185,9 +185,12 @@ class Indexer:
     def analyze_project(self, repository_url: str, branch: Optional[str] = None,
                         fix_missed: bool = True) -> AnalysisResult:
         if self.require_enrichment and not self.backend.enabled:
-            LOG.error("Cannot run analysis in read-only mode. ANTHROPIC_API_KEY is not configured.")
-            raise DomainError("Cannot run analysis in read-only mode. ANTHROPIC_API_KEY is not configured.",
-                              "READ_ONLY_MODE")
+            # a refused backend (ENRICH_BACKEND=local without a checkpoint)
+            # says why; otherwise the reference's message
+            msg = getattr(self.backend, "disabled_reason", None) or \
+                "Cannot run analysis in read-only mode. ANTHROPIC_API_KEY is not configured."
+            LOG.error("%s", msg)
+            raise DomainError(msg, "READ_ONLY_MODE")
         url = RepositoryUrl.of(repository_url)
         branch_name = branch if branch is not None else "main"
         lock = self._locks.get(url.value)
@@ -239,7 +242,7 @@ class Indexer:
                 # as soon as it has them (fresh UUIDv7s; not with given test ids)
                 rows = (writer.static_rows(now, clone.commit_hash)
                         if self.native_phase1 and self.phase1_ids is None
-                        and not self._isolate(url) else None)
+                        and (not self._isolate(url) or self._iso_rows(clone)) else None)
                 with span("analyze.parse", stats):
                     parsed = self._scan(parser, clone, url, rows=rows)
                     graph = parsed.build_graph()
@@ -325,7 +328,15 @@ class Indexer:
 
     def _scan(self, parser: SourceParser, tree: SourceTree, url: RepositoryUrl, rows=None) -> ParsedProject:
         iso = self._isolate(url)
-        return parser.scan_tree(tree, rows=None if iso else rows, isolate_timeout_s=iso)
+        return parser.scan_tree(tree, rows=rows if (not iso or self._iso_rows(tree)) else None,
+                                isolate_timeout_s=iso)
+
+    @staticmethod
+    def _iso_rows(tree: SourceTree) -> bool:
+        """An isolated scan of ``tree`` can hand its rows to the writer (the
+        persistent binary child on an in-memory snapshot)."""
+        from ..parsers import isolated
+        return not isinstance(tree, CheckoutTree) and isolated.objects_supported()
 
     def _submit_io(self, fn, *args):
         with self._io_guard:
@@ -630,7 +641,10 @@ class Indexer:
 
     def _recover_unenriched(self, project: Project, parsed: ParsedProject, graph: ProjectGraph,
                             tree: SourceTree, readme: Optional[str], lease: Optional[ProjectLease] = None) -> int:
-        unenriched = self.repos.classes.find_unenriched_by_project_id(project.id)
+        # a real backend also redoes what a synthetic one (random weights,
+        # fake, echo) wrote; a synthetic backend redoes only missing rows
+        unenriched = self.repos.classes.find_unenriched_by_project_id(
+            project.id, include_synthetic=not is_synthetic(self.backend.source_tag))
         if not unenriched:
             LOG.info("Phase 3: No unenriched classes found, skipping recovery")
             return 0
@@ -688,13 +702,14 @@ class Indexer:
                 continue
             updates.append((me.description, list(me.business_logic), mid))
             enrichments[mname] = MethodEnrichmentData(me.description, tuple(me.business_logic))
+        tag = self.backend.source_tag
         with self.repos.db.transaction() as conn:
             if correction is not None:
-                conn.execute("UPDATE source_classes SET class_type = ?, description = ? WHERE id = ?",
-                             (correction.value, result.description, class_id))
+                conn.execute("UPDATE source_classes SET class_type = ?, description = ?, enrichment_source = ? "
+                             "WHERE id = ?", (correction.value, result.description, tag, class_id))
             else:
-                conn.execute("UPDATE source_classes SET description = ? WHERE id = ?",
-                             (result.description, class_id))
+                conn.execute("UPDATE source_classes SET description = ?, enrichment_source = ? WHERE id = ?",
+                             (result.description, tag, class_id))
             self.repos.methods.update_enrichment_batch(updates)
         if correction is not None:
             resolved = correction.value
@@ -985,7 +1000,8 @@ class Indexer:
         if project is None:
             raise DomainError(f"Project not found: {project_id}", "PROJECT_NOT_FOUND")
         if not self.backend.enabled:
-            raise DomainError("No enrichment backend configured", "READ_ONLY_MODE")
+            raise DomainError(getattr(self.backend, "disabled_reason", None) or "No enrichment backend configured",
+                              "READ_ONLY_MODE")
         lock = self._locks.get(project.repository_url.value)
         if not lock.acquire(blocking=False):
             raise DomainError(f"Project {project.name} is already being processed", "PROJECT_BUSY")

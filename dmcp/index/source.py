@@ -151,11 +151,12 @@ class MemoryTree(SourceTree):
             # the indexing pipeline (rows given) never reads the Go analyzer's
             # package document (3.6 MB of JSON for a 1,000-file repository,
             # rendered on one thread): not built on that path
-            try:
+            # the call form from the module's ABI, never by retrying a call
+            # that may already have streamed rows to the writer
+            if getattr(native(), "ABI_VERSION", 0) >= 6:
                 return fn(list(self.files.items()), language, threads, framework, StaticMethodInfo, rows,
                           go_doc=False)
-            except TypeError:  # a module built before go_doc
-                return fn(list(self.files.items()), language, threads, framework, StaticMethodInfo, rows)
+            return fn(list(self.files.items()), language, threads, framework, StaticMethodInfo, rows)
         return fn(list(self.files.items()), language, threads, framework, StaticMethodInfo)
 
 

@@ -908,7 +908,7 @@ __global__ __launch_bounds__(kBlock) void kv_fork_kernel(uint8_t* __restrict__ k
 
 extern "C" {
 
-int dmcp_abi_version() { return 15; }
+int dmcp_abi_version() { return 16; }
 
 int dmcp_add_rmsnorm(const void* x, void* residual, const void* w, void* out, int rows, int H, float eps,
                      void* stream) {

@@ -228,11 +228,22 @@ class SourceParser:
         hands the class / method rows to the writer before it builds any
         Python object (their ids in ``ParsedProject.static_row_ids``).
         ``isolate_timeout_s``: run the scan in a child process killed after
-        that many seconds (:mod:`dmcp.parsers.isolated`; ``rows`` unused)."""
+        that many seconds (:mod:`dmcp.parsers.isolated`: a persistent
+        ``srcscan serve`` child whose binary result is decoded here, ``rows``
+        honoured; a checkout directory goes to a one-shot JSON child).""" 
         t0 = time.perf_counter()
         if isolate_timeout_s:
-            from .isolated import scan_in_child
-            doc = scan_in_child(tree, self.language_name, self.threads, self.framework_override, isolate_timeout_s)
+            from . import isolated
+            from ..index.source import CheckoutTree
+            if isolated.objects_supported() and not isinstance(tree, CheckoutTree):
+                # the persistent child: a binary result decoded natively, the
+                # rows streamed to the writer as in process
+                doc = isolated.scan_objects_in_child(tree, self.language_name, self.threads,
+                                                     self.framework_override, isolate_timeout_s, rows=rows,
+                                                     go_doc=rows is None)
+            else:
+                doc = isolated.scan_in_child(tree, self.language_name, self.threads, self.framework_override,
+                                             isolate_timeout_s)
         else:
             doc = tree.scan_objects(self.language_name, self.threads, self.framework_override, rows=rows)
         if doc is None:

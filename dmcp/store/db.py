@@ -247,6 +247,14 @@ INSERT INTO project_graphs (project_id, graph_data)
     SELECT id, graph_data FROM projects WHERE graph_data IS NOT NULL;
 UPDATE projects SET graph_data = NULL WHERE graph_data IS NOT NULL;
 """),
+    (10, "class_enrichment_source", """
+-- Which backend wrote a class's enrichment (dmcp.enrich.backend source
+-- tags): 'synthetic:...' marks placeholder descriptions -- a random-weight
+-- local preset, the echo engine, the offline fake -- that Phase 3 and
+-- resume-enrichment redo once a real backend (a checkpoint, the API) is
+-- configured.  NULL: never enriched, or enriched before this migration.
+ALTER TABLE source_classes ADD COLUMN enrichment_source TEXT;
+"""),
 ]
 
 # New database files use 16 KiB pages (SQLite's default is 4 KiB): fewer

@@ -151,6 +151,9 @@ CREATE TABLE IF NOT EXISTS project_leases (
     lease_until DOUBLE PRECISION NOT NULL
 );
 """),
+    (5, "class_enrichment_source", """
+ALTER TABLE source_classes ADD COLUMN IF NOT EXISTS enrichment_source VARCHAR(600);
+"""),
 ]
 
 

@@ -286,6 +286,10 @@ class SourceClassRepository:
         "SELECT * FROM source_classes WHERE project_id = ? AND full_class_name = ?")
     FIND_UNENRICHED_BY_PROJECT_ID = ("SELECT * FROM source_classes WHERE project_id = ? "
                                      "AND description IS NULL ORDER BY full_class_name")
+    # ... plus the rows a synthetic backend enriched (migration 10)
+    FIND_UNENRICHED_OR_SYNTHETIC_BY_PROJECT_ID = (
+        "SELECT * FROM source_classes WHERE project_id = ? "
+        "AND (description IS NULL OR enrichment_source LIKE 'synthetic:%') ORDER BY full_class_name")
     _INSERT = ("INSERT INTO source_classes (id, project_id, full_class_name, simple_name, "
                "package_name, class_type, description, source_file, created_at, commit_hash) "
                "VALUES (?,?,?,?,?,?,?,?,?,?)")
@@ -431,8 +435,17 @@ class SourceClassRepository:
         with self.db.transaction() as c:
             c.execute("DELETE FROM source_classes WHERE id = ?", (class_id,))
 
-    def find_unenriched_by_project_id(self, project_id: str) -> List[SourceClass]:
-        return [self._map(r) for r in self.db.query(self.FIND_UNENRICHED_BY_PROJECT_ID, (project_id,))]
+    def find_unenriched_by_project_id(self, project_id: str, include_synthetic: bool = False) -> List[SourceClass]:
+        """Classes without a description; with ``include_synthetic`` also the
+        classes whose description a synthetic backend wrote (random weights,
+        fake, echo: ``enrichment_source`` 'synthetic:...')."""
+        q = self.FIND_UNENRICHED_OR_SYNTHETIC_BY_PROJECT_ID if include_synthetic else self.FIND_UNENRICHED_BY_PROJECT_ID
+        return [self._map(r) for r in self.db.query(q, (project_id,))]
+
+    def enrichment_sources(self, project_id: str) -> Dict[str, Optional[str]]:
+        """full_class_name -> enrichment_source of a project's classes."""
+        return {r[0]: r[1] for r in self.db.query(
+            "SELECT full_class_name, enrichment_source FROM source_classes WHERE project_id = ?", (project_id,))}
 
 
 # --------------------------------------------------------------------------

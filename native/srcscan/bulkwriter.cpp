@@ -190,8 +190,13 @@ void BulkWriter::run() {
         setup_.clear();
         setup_ms_ = ms(t0, clock::now());
         t_setup_ = clock::now();
-        std::vector<Batch> dead;  // inserted batches, handed to the reaper at the end
-        dead.reserve(64);
+        // inserted batches, handed to the reaper in groups as they are
+        // inserted: the writer never frees them itself, and an analysis' row
+        // buffers (with the scan result they view) are not all held until
+        // the COMMIT -- peak writer memory stays a group, not the repository
+        constexpr size_t kReapGroup = 16;
+        std::vector<Batch> dead;
+        dead.reserve(kReapGroup);
         static const bool reap = [] {
             const char* e = std::getenv("DMCP_WRITER_REAPER");
             return e == nullptr || e[0] != '0';
@@ -221,9 +226,14 @@ void BulkWriter::run() {
             rows_written_ += c.run(it.batch);
             auto tf = clock::now();
             rows_ms_ += ms(tr, tf);
-            if (reap)
-                dead.push_back(std::move(it.batch));  // released by the reaper after the commit
-            else
+            if (reap) {
+                dead.push_back(std::move(it.batch));
+                if (dead.size() >= kReapGroup) {
+                    Reaper::give(std::move(dead));
+                    dead = std::vector<Batch>();
+                    dead.reserve(kReapGroup);
+                }
+            } else
                 Batch(std::move(it.batch));  // (DMCP_WRITER_REAPER=0: released here, as before)
             free_ms_ += ms(tf, clock::now());
         }

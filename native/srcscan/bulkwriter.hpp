@@ -66,8 +66,8 @@ class BulkWriter {
     double setup_ms() const { return setup_ms_; }
     double rows_ms() const { return rows_ms_; }
     double commit_ms() const { return commit_ms_; }
-    double idle_ms() const { return idle_ms_; }
-    double free_ms() const { return free_ms_; }  // releasing inserted batches  // waits for rows between the setup and the commit request
+    double idle_ms() const { return idle_ms_; }  // waits for rows between the setup and the commit request
+    double free_ms() const { return free_ms_; }  // releasing inserted batches (handing them to the reaper)
     double open_ms() const { return open_ms_; }  // from construction to BEGIN (thread start, open, pragmas)
     // steady_clock (CLOCK_MONOTONIC, Python's time.perf_counter on Linux) seconds of the writer's milestones
     static double secs(std::chrono::steady_clock::time_point t) {

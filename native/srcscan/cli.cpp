@@ -10,6 +10,12 @@
 //           the isolated scan of an in-memory snapshot (dmcp/parsers/isolated.py):
 //           the untrusted parse runs in this short-lived process, which starts
 //           in milliseconds (the Python child took ~100 ms to import)
+//   srcscan serve
+//           the persistent isolated scan child: per request on stdin a u64 LE
+//           length + header text ("language\nthreads\nframework\ngo_doc"), the
+//           project stream of `stdin`; per request on stdout a u8 status (0 ok,
+//           1 error) + u64 LE length + the binary ScanResult (wire.hpp) or the
+//           error message.  Exits 0 at end of input, 3 on a truncated request.
 //
 // Mirrors tools/go-analyzer/cmd/analyzer/main.go:20-59: JSON on stdout or to
 // the -o file; exit status 1 on usage / I/O errors.
@@ -26,6 +32,7 @@
 
 #include "common.hpp"
 #include "srcscan.hpp"
+#include "wire.hpp"
 
 static bool read_exact(void* dst, size_t n) {
     return n == 0 || std::fread(dst, 1, n, stdin) == n;
@@ -63,6 +70,66 @@ static int scan_stdin(const srcscan::ScanOptions& opt, std::string& json) {
     return 0;
 }
 
+static bool write_exact(const void* src, size_t n) { return n == 0 || std::fwrite(src, 1, n, stdout) == n; }
+
+// one request of `serve` after its header: the tree, the scan, the framed reply
+static int serve_one(const std::string& header) {
+    srcscan::ScanOptions opt;
+    {
+        std::vector<std::string> f;
+        size_t a = 0;
+        for (;;) {
+            const size_t b = header.find('\n', a);
+            f.push_back(header.substr(a, b == std::string::npos ? std::string::npos : b - a));
+            if (b == std::string::npos) break;
+            a = b + 1;
+        }
+        if (f.size() != 4) return 3;
+        opt.language = f[0].empty() ? "auto" : f[0];
+        opt.threads = std::atoi(f[1].c_str());
+        opt.framework = f[2];
+        opt.go_doc = f[3] != "0";
+    }
+    uint64_t nfiles = 0;
+    if (!read_exact(&nfiles, sizeof nfiles) || nfiles > (uint64_t(1) << 24)) return 3;
+    std::vector<std::pair<std::string, std::string>> tree;
+    tree.reserve((size_t)nfiles);
+    for (uint64_t k = 0; k < nfiles; ++k) {
+        std::string rel, data;
+        if (!read_blob(rel) || !read_blob(data)) return 3;
+        tree.emplace_back(std::move(rel), std::move(data));
+    }
+    injected_fault();
+    uint8_t status = 0;
+    std::string payload;
+    std::string root = srcscan::vfs_mount(std::move(tree));
+    try {
+        payload = srcscan::encode_result(srcscan::scan_project(root, opt));
+    } catch (const std::exception& e) {
+        status = 1;
+        payload = e.what();
+    }
+    srcscan::vfs_unmount(root);
+    const uint64_t n = payload.size();
+    if (!write_exact(&status, 1) || !write_exact(&n, sizeof n) || !write_exact(payload.data(), payload.size()) ||
+        std::fflush(stdout) != 0)
+        return 1;
+    return 0;
+}
+
+static int serve() {
+    for (;;) {
+        uint64_t hn = 0;
+        const size_t got = std::fread(&hn, 1, sizeof hn, stdin);
+        if (got == 0) return 0;  // end of input: the parent is done with this child
+        if (got != sizeof hn || hn > 4096) return 3;
+        std::string header((size_t)hn, '\0');
+        if (!read_exact(header.data(), header.size())) return 3;
+        const int rc = serve_one(header);
+        if (rc != 0) return rc;
+    }
+}
+
 static int usage() {
     std::fprintf(stderr,
                  "usage: srcscan [-o out.json] [--lang L] [--threads N] [--framework F] <project-root>\n"
@@ -75,6 +142,7 @@ int main(int argc, char** argv) {
     std::string mode = "project", out, lang = "auto", framework, rel, target;
     int threads = 0;
     int i = 1;
+    if (i < argc && std::strcmp(argv[i], "serve") == 0) return serve();
     if (i < argc && (std::strcmp(argv[i], "go") == 0 || std::strcmp(argv[i], "file") == 0 ||
                      std::strcmp(argv[i], "stdin") == 0))
         mode = argv[i++];

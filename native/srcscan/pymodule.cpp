@@ -17,6 +17,7 @@
 #include "gitobj.hpp"
 #include "graphjson.hpp"
 #include "srcscan.hpp"
+#include "wire.hpp"
 
 namespace py = pybind11;
 
@@ -836,6 +837,73 @@ py::tuple phase1_rows(dbw::BulkWriter& writer, py::list order, py::dict units, p
 
 }  // namespace
 
+// The Python objects of a scan (scan_result_objects) and, with rows =
+// (BulkWriter, project id, now, commit hash | None, class INSERT, method
+// INSERT), its class / method rows streamed to the writer from a helper thread
+// while this one builds the objects (row ids in d["rowIds"]).  Shared by the
+// in-process scan and the isolated child's binary result.
+py::dict objects_and_rows(std::shared_ptr<const srcscan::ScanResult> shared, py::handle method_cls, py::object rows) {
+    std::shared_ptr<StaticRowsKeep> keep;
+    std::thread emitter;
+    std::atomic<long long> emit_us{0};
+    if (!rows.is_none() && shared->language != "go") {
+        py::tuple rt = rows.cast<py::tuple>();
+        if (rt.size() != 6) throw py::value_error("rows must have 6 items");
+        keep = std::make_shared<StaticRowsKeep>();
+        keep->r = shared;
+        StaticRowsSpec& spec = keep->spec;
+        spec.writer = &rt[0].cast<dbw::BulkWriter&>();
+        spec.pid = rt[1].cast<std::string>();
+        spec.now = rt[2].cast<std::string>();
+        spec.commit_null = rt[3].is_none();
+        if (!spec.commit_null) spec.commit = rt[3].cast<std::string>();
+        spec.cls_sql = rt[4].cast<std::string>();
+        spec.meth_sql = rt[5].cast<std::string>();
+        emitter = std::thread([keep, &emit_us] {
+            const auto t = std::chrono::steady_clock::now();
+            emit_static_rows(keep);
+            emit_us = std::chrono::duration_cast<std::chrono::microseconds>(
+                          std::chrono::steady_clock::now() - t).count();
+        });
+    }
+    py::dict d;
+    try {
+        const auto t = std::chrono::steady_clock::now();
+        d = scan_result_objects(*shared, method_cls);
+        py::dict(d["stats"])["phaseUs"].cast<py::dict>()["objects"] =
+            std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t)
+                .count();
+    } catch (...) {
+        if (emitter.joinable()) {
+            py::gil_scoped_release release;
+            emitter.join();
+        }
+        throw;
+    }
+    if (emitter.joinable()) {
+        {
+            py::gil_scoped_release release;
+            emitter.join();
+        }
+        py::dict(d["stats"])["phaseUs"].cast<py::dict>()["rows"] = emit_us.load();
+        py::dict row_ids;
+        for (size_t k = 0; k < shared->files.size(); ++k) {
+            const size_t at = keep->first[k];
+            if (at == std::string::npos) continue;  // a file replaced by a later one
+            const size_t nm = shared->files[k].methods.size();
+            py::list mids(nm);
+            for (size_t j = 0; j < nm; ++j) mids[j] = py::str(&keep->ids[at + 36 * (j + 1)], 36);
+            row_ids[pystr(shared->files[k].identifier)] = py::make_tuple(py::str(&keep->ids[at], 36), mids);
+        }
+        d["rowIds"] = row_ids;
+    }
+    // the rest of the ScanResult is freed off this thread (by the
+    // writer after its inserts, or here by a helper)
+    keep.reset();
+    std::thread([](std::shared_ptr<const srcscan::ScanResult>) {}, std::move(shared)).detach();
+    return d;
+}
+
 PYBIND11_MODULE(_srcscan, m) {
     m.doc() = "Native Java / TypeScript / Go source front-ends for dmcp";
     m.def(
@@ -889,75 +957,47 @@ PYBIND11_MODULE(_srcscan, m) {
            py::handle method_cls, py::object rows, bool go_doc) {
             auto r = std::make_unique<srcscan::ScanResult>(scan_mounted(files, language, threads, framework,
                                                                         go_doc));
-            // rows = (BulkWriter, project id, now, commit hash | None, class INSERT, method INSERT):
-            // the class / method rows go to the writer from a helper thread
-            // while this one builds the Python objects
-            std::shared_ptr<const srcscan::ScanResult> shared(std::move(r));
-            std::shared_ptr<StaticRowsKeep> keep;
-            std::thread emitter;
-            std::atomic<long long> emit_us{0};
-            if (!rows.is_none() && shared->language != "go") {
-                py::tuple rt = rows.cast<py::tuple>();
-                if (rt.size() != 6) throw py::value_error("rows must have 6 items");
-                keep = std::make_shared<StaticRowsKeep>();
-                keep->r = shared;
-                StaticRowsSpec& spec = keep->spec;
-                spec.writer = &rt[0].cast<dbw::BulkWriter&>();
-                spec.pid = rt[1].cast<std::string>();
-                spec.now = rt[2].cast<std::string>();
-                spec.commit_null = rt[3].is_none();
-                if (!spec.commit_null) spec.commit = rt[3].cast<std::string>();
-                spec.cls_sql = rt[4].cast<std::string>();
-                spec.meth_sql = rt[5].cast<std::string>();
-                emitter = std::thread([keep, &emit_us] {
-                    const auto t = std::chrono::steady_clock::now();
-                    emit_static_rows(keep);
-                    emit_us = std::chrono::duration_cast<std::chrono::microseconds>(
-                                  std::chrono::steady_clock::now() - t).count();
-                });
-            }
-            py::dict d;
-            try {
-                const auto t = std::chrono::steady_clock::now();
-                d = scan_result_objects(*shared, method_cls);
-                py::dict(d["stats"])["phaseUs"].cast<py::dict>()["objects"] =
-                    std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t)
-                        .count();
-            } catch (...) {
-                if (emitter.joinable()) {
-                    py::gil_scoped_release release;
-                    emitter.join();
-                }
-                throw;
-            }
-            if (emitter.joinable()) {
-                {
-                    py::gil_scoped_release release;
-                    emitter.join();
-                }
-                py::dict(d["stats"])["phaseUs"].cast<py::dict>()["rows"] = emit_us.load();
-                py::dict row_ids;
-                for (size_t k = 0; k < shared->files.size(); ++k) {
-                    const size_t at = keep->first[k];
-                    if (at == std::string::npos) continue;  // a file replaced by a later one
-                    const size_t nm = shared->files[k].methods.size();
-                    py::list mids(nm);
-                    for (size_t j = 0; j < nm; ++j) mids[j] = py::str(&keep->ids[at + 36 * (j + 1)], 36);
-                    row_ids[pystr(shared->files[k].identifier)] = py::make_tuple(py::str(&keep->ids[at], 36), mids);
-                }
-                d["rowIds"] = row_ids;
-            }
-            // the rest of the ScanResult is freed off this thread (by the
-            // writer after its inserts, or here by a helper)
-            keep.reset();
-            std::thread([](std::shared_ptr<const srcscan::ScanResult>) {}, std::move(shared)).detach();
-            return d;
+            return objects_and_rows(std::shared_ptr<const srcscan::ScanResult>(std::move(r)), method_cls, rows);
         },
         py::arg("files"), py::arg("language"), py::arg("threads"), py::arg("framework"), py::arg("method_cls"),
         py::arg("rows") = py::none(), py::arg("go_doc") = true,
         "scan_sources as Python objects (files as tuples, methods as method_cls) -- no JSON round trip; "
         "with rows, the class / method rows are written first (ids in 'rowIds'); go_doc=False: no "
         "go-analyzer package document (Go)");
+    m.def(
+        "result_objects",
+        [](py::bytes blob, py::handle method_cls, py::object rows) {
+            // the isolated scan child's binary ScanResult (wire.hpp) -> the
+            // scan_sources_objects result, rows to the writer included
+            auto r = std::make_unique<srcscan::ScanResult>();
+            std::string err;
+            bool ok;
+            {
+                char* data = nullptr;
+                Py_ssize_t n = 0;
+                if (PyBytes_AsStringAndSize(blob.ptr(), &data, &n) < 0) throw py::error_already_set();
+                py::gil_scoped_release release;
+                ok = srcscan::decode_result(std::string_view(data, static_cast<size_t>(n)), *r, err);
+            }
+            if (!ok) throw py::value_error("scan result: " + err);
+            return objects_and_rows(std::shared_ptr<const srcscan::ScanResult>(std::move(r)), method_cls, rows);
+        },
+        py::arg("blob"), py::arg("method_cls"), py::arg("rows") = py::none(),
+        "the binary ScanResult of `srcscan serve` as scan_sources_objects returns it (untrusted bytes: every "
+        "length checked)");
+    m.def(
+        "encode_scan",
+        [](py::list files, const std::string& language, int threads, const std::string& framework, bool go_doc) {
+            // the serve child's reply, computed in process (tests)
+            srcscan::ScanResult r = scan_mounted(files, language, threads, framework, go_doc);
+            std::string out;
+            {
+                py::gil_scoped_release release;
+                out = srcscan::encode_result(r);
+            }
+            return py::bytes(out);
+        },
+        py::arg("files"), py::arg("language"), py::arg("threads"), py::arg("framework"), py::arg("go_doc") = true);
     m.def(
         "scan_file",
         [](const std::string& path, const std::string& language, const std::string& rel, const std::string& fw) {
@@ -1176,5 +1216,5 @@ PYBIND11_MODULE(_srcscan, m) {
             d["t_end_s"] = w.t_end();
             return d;
         });
-    m.attr("ABI_VERSION") = 5;
+    m.attr("ABI_VERSION") = 6;  // 6: scan_sources_objects(..., go_doc=)
 }

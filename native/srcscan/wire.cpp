@@ -1,0 +1,222 @@
+// Binary wire form of a ScanResult (see wire.hpp).
+#include "wire.hpp"
+
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+
+namespace srcscan {
+
+namespace {
+
+struct Out {
+    std::string s;
+    void u8(uint8_t v) { s.push_back(static_cast<char>(v)); }
+    void u32(uint32_t v) { s.append(reinterpret_cast<const char*>(&v), 4); }
+    void i64(int64_t v) { s.append(reinterpret_cast<const char*>(&v), 8); }
+    void str(const std::string& v) {
+        u32(static_cast<uint32_t>(v.size()));
+        s.append(v);
+    }
+    void strs(const std::vector<std::string>& v) {
+        u32(static_cast<uint32_t>(v.size()));
+        for (const auto& x : v) str(x);
+    }
+};
+
+struct Bad : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+struct In {
+    const char* p;
+    size_t n;
+    void need(size_t k) const {
+        if (k > n) throw Bad("truncated scan result");
+    }
+    uint8_t u8() {
+        need(1);
+        const uint8_t v = static_cast<uint8_t>(*p);
+        ++p, --n;
+        return v;
+    }
+    uint32_t u32() {
+        need(4);
+        uint32_t v;
+        std::memcpy(&v, p, 4);
+        p += 4, n -= 4;
+        return v;
+    }
+    int64_t i64() {
+        need(8);
+        int64_t v;
+        std::memcpy(&v, p, 8);
+        p += 8, n -= 8;
+        return v;
+    }
+    // a count of elements of at least `min_bytes` each: bounded by what is left
+    uint32_t count(size_t min_bytes) {
+        const uint32_t c = u32();
+        if ((uint64_t)c * min_bytes > n) throw Bad("scan result count exceeds its payload");
+        return c;
+    }
+    std::string str() {
+        const uint32_t k = u32();
+        need(k);
+        std::string v(p, k);
+        p += k, n -= k;
+        return v;
+    }
+    void strs(std::vector<std::string>& v) {
+        const uint32_t c = count(4);
+        v.clear();
+        v.reserve(c);
+        for (uint32_t i = 0; i < c; ++i) v.push_back(str());
+    }
+};
+
+}  // namespace
+
+std::string encode_result(const ScanResult& r) {
+    Out o;
+    o.s.reserve(64 + r.files.size() * 512 + r.go_json.size());
+    o.s.append("SSW1", 4);
+    o.str(r.language);
+    o.str(r.source_root);
+    o.u8(r.has_framework);
+    o.str(r.framework.name);
+    o.str(r.framework.source_root);
+    o.u32(static_cast<uint32_t>(r.framework.features.size()));
+    for (const auto& kv : r.framework.features) {
+        o.str(kv.first);
+        o.str(kv.second);
+    }
+    o.str(r.module);
+    o.str(r.go_json);
+    o.u32(static_cast<uint32_t>(r.files.size()));
+    for (const FileRec& f : r.files) {
+        o.str(f.abs_path);
+        o.str(f.rel_path);
+        o.str(f.identifier);
+        o.str(f.class_type);
+        o.u8(static_cast<uint8_t>((f.entry_point ? 1 : 0) | (f.parsed ? 2 : 0)));
+        o.str(f.package_name);
+        o.u32(static_cast<uint32_t>(f.methods.size()));
+        for (const MethodRec& m : f.methods) {
+            o.str(m.name);
+            o.u32(static_cast<uint32_t>(m.line));
+            o.u8(static_cast<uint8_t>((m.has_http_method ? 1 : 0) | (m.has_http_path ? 2 : 0) | (m.is_ctor ? 4 : 0) |
+                                      (m.params_eligible ? 8 : 0)));
+            o.str(m.http_method);
+            o.str(m.http_path);
+            o.strs(m.exceptions);
+            o.strs(m.param_types);
+        }
+        o.u32(static_cast<uint32_t>(f.imports.size()));
+        for (const ImportRec& im : f.imports) {
+            o.str(im.imported);
+            o.str(im.local);
+            o.str(im.source);
+            o.u8(static_cast<uint8_t>((im.is_static ? 1 : 0) | (im.is_asterisk ? 2 : 0)));
+        }
+        o.strs(f.deps);
+        o.u32(static_cast<uint32_t>(f.params.size()));
+        for (const auto& pm : f.params) {
+            o.str(pm.first);
+            o.strs(pm.second);
+        }
+    }
+    o.u32(static_cast<uint32_t>(r.skipped));
+    o.i64(r.elapsed_us);
+    o.i64(r.walk_us);
+    o.i64(r.analyze_us);
+    o.i64(r.resolve_us);
+    o.i64(r.mount_us);
+    return std::move(o.s);
+}
+
+bool decode_result(std::string_view in, ScanResult& r, std::string& err) {
+    try {
+        In d{in.data(), in.size()};
+        d.need(4);
+        if (std::memcmp(d.p, "SSW1", 4) != 0) throw Bad("not a scan result (bad magic)");
+        d.p += 4, d.n -= 4;
+        r.language = d.str();
+        r.source_root = d.str();
+        r.has_framework = d.u8() != 0;
+        r.framework.name = d.str();
+        r.framework.source_root = d.str();
+        const uint32_t nf = d.count(8);
+        r.framework.features.clear();
+        for (uint32_t i = 0; i < nf; ++i) {
+            std::string k = d.str();
+            r.framework.features.emplace_back(std::move(k), d.str());
+        }
+        r.module = d.str();
+        r.go_json = d.str();
+        const uint32_t nfiles = d.count(33);  // the fixed-size part of a file record
+        r.files.clear();
+        r.files.resize(nfiles);
+        for (uint32_t k = 0; k < nfiles; ++k) {
+            FileRec& f = r.files[k];
+            f.abs_path = d.str();
+            f.rel_path = d.str();
+            f.identifier = d.str();
+            f.class_type = d.str();
+            const uint8_t fl = d.u8();
+            f.entry_point = fl & 1;
+            f.parsed = (fl & 2) != 0;
+            f.package_name = d.str();
+            const uint32_t nm = d.count(25);
+            f.methods.resize(nm);
+            for (uint32_t j = 0; j < nm; ++j) {
+                MethodRec& m = f.methods[j];
+                m.name = d.str();
+                m.line = static_cast<int>(d.u32());
+                const uint8_t mf = d.u8();
+                m.has_http_method = mf & 1;
+                m.has_http_path = (mf & 2) != 0;
+                m.is_ctor = (mf & 4) != 0;
+                m.params_eligible = (mf & 8) != 0;
+                m.http_method = d.str();
+                m.http_path = d.str();
+                d.strs(m.exceptions);
+                d.strs(m.param_types);
+            }
+            const uint32_t ni = d.count(13);
+            f.imports.resize(ni);
+            for (uint32_t j = 0; j < ni; ++j) {
+                ImportRec& im = f.imports[j];
+                im.imported = d.str();
+                im.local = d.str();
+                im.source = d.str();
+                const uint8_t imf = d.u8();
+                im.is_static = imf & 1;
+                im.is_asterisk = (imf & 2) != 0;
+            }
+            d.strs(f.deps);
+            const uint32_t np = d.count(8);
+            f.params.resize(np);
+            for (uint32_t j = 0; j < np; ++j) {
+                f.params[j].first = d.str();
+                d.strs(f.params[j].second);
+            }
+        }
+        r.skipped = static_cast<int>(d.u32());
+        r.elapsed_us = d.i64();
+        r.walk_us = d.i64();
+        r.analyze_us = d.i64();
+        r.resolve_us = d.i64();
+        r.mount_us = d.i64();
+        if (d.n != 0) throw Bad("trailing bytes after the scan result");
+        return true;
+    } catch (const Bad& e) {
+        err = e.what();
+        return false;
+    } catch (const std::bad_alloc&) {
+        err = "scan result too large";
+        return false;
+    }
+}
+
+}  // namespace srcscan

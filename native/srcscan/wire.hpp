@@ -1,0 +1,24 @@
+// Binary wire form of a ScanResult: what the persistent isolated scan child
+// (srcscan serve, dmcp/parsers/isolated.py) returns to the service process
+// instead of the JSON document -- the parent decodes it natively and builds
+// its Python objects and database rows the same way as an in-process scan
+// (pymodule.cpp), no JSON encode / decode on either side.
+//
+// Little-endian: "SSW1", then the ScanResult fields in declaration order;
+// strings are u32 length + bytes, vectors u32 count + elements, flags u8.
+// The decoder treats its input as untrusted (the child parsed an untrusted
+// repository): every length and count is checked against the bytes left.
+#pragma once
+
+#include <string>
+#include <string_view>
+
+#include "srcscan.hpp"
+
+namespace srcscan {
+
+std::string encode_result(const ScanResult& r);
+// false (and ``err``) on malformed input; ``out`` is then unspecified
+bool decode_result(std::string_view in, ScanResult& out, std::string& err);
+
+}  // namespace srcscan

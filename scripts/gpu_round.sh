@@ -112,6 +112,26 @@ for s in $STEPS; do
                 --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 60
             run step_llama268 300 python scripts/bench_step.py --preset llama3.2-1b-code --batch 256 --extra 12 \
                 --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 60 ;;
+        fixup_test) run fixup_test 600 python -u -m pytest tests/test_gpu_tgemm_fixup.py tests/test_gpu_tgemm.py -x -q \
+                --timeout 120 --timeout-method thread ;;
+        fixup_bench) run fixup_bench 600 python scripts/bench_tgemm_fixup.py --rows 520 610 768 1024 --sweep ;;
+        step_llama3)  # the verdict's three operating points: 320 / 610 / 768 rows
+            for r in "256 64" "512 98" "512 256"; do set -- $r
+                run step_llama$(($1 + $2)) 300 python scripts/bench_step.py --preset llama3.2-1b-code --batch $1 \
+                    --extra $2 --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 60
+            done ;;
+        prof_step610)
+            ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$ROOT/$OUT/prof_step610" -o step -- python3 "$ROOT/scripts/bench_step.py" \
+                --preset llama3.2-1b-code --batch 512 --extra 98 --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 40 \
+                > "$ROOT/$OUT/prof_step610.log" 2>&1 )
+            rc=$?
+            echo "=== prof_step610 rc=$rc"
+            find "$OUT/prof_step610" -type f ! -name '*kernel_stats*' -delete 2>/dev/null
+            cp $(find "$OUT/prof_step610" -name '*kernel_stats.csv' | head -1) "$OUT/step610_kernel_stats.csv"
+            python3 scripts/kstats.py "$OUT/step610_kernel_stats.csv" > "$OUT/kstats_step610.txt" 2>&1
+            head -25 "$OUT/kstats_step610.txt"
+            [ $rc -eq 0 ] || exit $rc ;;
         step)
             run step320 300 python scripts/bench_step.py --batch 256 --extra 64 --kv-dtype fp8 --iters 100
             run step78 300 python scripts/bench_step.py --batch 64 --extra 14 --kv-dtype fp8 --iters 100 ;;

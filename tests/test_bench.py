@@ -46,3 +46,21 @@ def test_bench_two_ranks_gloo():
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 60
     assert rec["config"]["parallelism"].startswith("dp2") and rec["value"] > 0
+
+
+def test_enrich_pool_extra_deals_one_project_over_every_worker(tmp_path):
+    """extra.enrichLocalPool (the production layout: ONE project, ONE pool,
+    one worker per GPU), rehearsed with model-free echo workers on the CPU:
+    every class enriched, each worker got a share."""
+    import bench
+    from dmcp.enrich.workers import GpuWorkerPool
+    args = bench.parse_args(["--pool-classes", "40"])
+    pool = GpuWorkerPool(["cpu"] * 3, {"preset": "echo", "step_s": 0.01, "steps": 1, "max_batch": 64},
+                         init=False, start_timeout_s=120)
+    try:
+        rec = bench._enrich_pool(pool, args, str(tmp_path))
+    finally:
+        pool.close()
+    assert rec["classes"] == 41 and rec["enriched"] == 41 and rec["workers"] == 3
+    assert rec["classesPerSec"] > 0 and len(rec["classesPerWorker"]) == 3
+    assert all(v > 0 for v in rec["classesPerWorker"].values())

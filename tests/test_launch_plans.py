@@ -41,3 +41,31 @@ def test_wgemm_plan_keeps_the_measured_small_m_plans():
 def test_prefix_splits_within_the_workspace(rows):
     sp = hip.prefix_mfma_splits(rows, 4, 8)
     assert 1 <= sp <= hip.PREFIX_MFMA_MAX_SPLITS
+
+
+@pytest.mark.parametrize("inter", [128, 256, 1408, 5632, 8192, 8192 + 64, 100])
+@pytest.mark.parametrize("hidden", [256, 2048, 2048 + 64])
+def test_tgemm_model_and_op_predicates_agree(inter, hidden):
+    """The model enables the large-tile path (tgemm_shapes_ok) exactly when
+    every projection passes the op's own check (tgemm_supported), so no
+    step -- nor the decode-graph capture at engine start -- raises inside
+    tgemm_swiglu (advisor r5: intermediate = 128 x odd was enabled by one and
+    refused by the other)."""
+    from dmcp.models.llm import LMConfig, tgemm_shapes_ok
+    c = LMConfig(hidden=hidden, intermediate=inter, n_heads=hidden // 64, n_kv_heads=max(1, hidden // 256),
+                 head_dim=64)
+    ops_ok = (hip.tgemm_supported(c.qkv_dim, c.hidden) and hip.tgemm_supported(c.hidden, c.hidden)
+              and hip.tgemm_supported(2 * c.intermediate, c.hidden, swiglu=True)
+              and hip.tgemm_supported(c.hidden, c.intermediate))
+    model_ok = tgemm_shapes_ok(c)
+    assert model_ok == (ops_ok and c.qkv_dim <= 8192 and c.hidden <= 8192)
+
+
+@pytest.mark.parametrize("M", [513, 610, 768, 1024])
+@pytest.mark.parametrize("N,K", [(3072, 2048), (2048, 2048), (2048, 8192)])
+def test_tgemm_fixup_plan_fits_the_kernel(M, N, K):
+    S, mparts = hip.tgemm_fixup_plan(M, N, K)
+    chunks = K // hip.TGEMM_KC
+    assert 1 <= S <= chunks and (S - 1) * -(-chunks // S) < chunks   # every K slice non-empty
+    assert (-(-M // mparts) + 15) // 16 * 16 <= 256                  # <= 256 rows per M part
+    assert (N // hip.TGEMM_NB) * mparts <= 4096                       # tickets in the workspace

@@ -114,6 +114,32 @@ def test_session_defers_full_gc_and_restores_threshold(tiny):
     assert gc.get_threshold() == before
 
 
+def test_gc_deferral_is_process_wide_across_engines(tiny):
+    """Sessions of several engines overlap (``_threaded_stream``): the first
+    to enter saves the interpreter's threshold and the last to leave
+    restores it, whatever the interleaving (advisor r5: per-session
+    save/restore could leave full collections deferred for good)."""
+    import gc
+    from dmcp.enrich import local as L
+    before = gc.get_threshold()
+    # the interleaving that broke per-session save/restore: A in, B in, A out, B out
+    L._gc_defer_enter(1000)
+    L._gc_defer_enter(5000)
+    assert gc.get_threshold()[2] == max(before[2], 5000)
+    L._gc_defer_exit()
+    assert gc.get_threshold()[2] == max(before[2], 5000)  # B still runs
+    L._gc_defer_exit()
+    assert gc.get_threshold() == before
+    # two engines through the threaded multi-replica stream
+    other = LocalLM(preset("tiny", max_batch=4, max_rows=16, max_seq=2048), device="cpu", seed=1)
+    engines = [LocalEngine(tiny), LocalEngine(other)]  # one model (KV cache) per engine, as one per GPU
+    for e in engines:
+        e.gc_full_every = 7000
+    out = list(L._threaded_stream(engines, enumerate(_inputs(6)), None))
+    assert sorted(i for i, _ in out) == list(range(6)) and all(r.success for _, r in out)
+    assert gc.get_threshold() == before
+
+
 def test_jump_forward_is_exact_on_cpu(tiny):
     a = LocalEngine(tiny, jump_forward=False)
     b = LocalEngine(tiny, jump_forward=True)

@@ -255,7 +255,7 @@ def test_bulk_with_local_backend_starts_one_pool(tmp_path, monkeypatch):
         items.append(BulkItem(str(r)))
     cfg = Config(db_path=str(tmp_path / "b.db"), git_clone_base_path=str(tmp_path / "clones"),
                  enrich_backend="local", local_llm_devices="cpu,cpu", local_llm_preset="echo",
-                 recover_stuck_on_start=False)
+                 local_llm_allow_random_weights=True, recover_stuck_on_start=False)
     res = bulk_analyze(cfg, items, workers=4)
     assert all(r.success for r in res), [r.message for r in res]
     assert len(made) == 1
@@ -268,7 +268,7 @@ def test_serve_mcp_never_spawns_gpu_workers(tmp_path):
     import sys
     import psutil
     env = dict(os.environ, ENRICH_BACKEND="local", LOCAL_LLM_DEVICES="cpu", LOCAL_LLM_PRESET="echo",
-               DMCP_DB_PATH=str(tmp_path / "m.db"))
+               LOCAL_LLM_ALLOW_RANDOM_WEIGHTS="true", DMCP_DB_PATH=str(tmp_path / "m.db"))
     proc = subprocess.Popen([sys.executable, "-m", "dmcp", "serve-mcp"], stdin=subprocess.PIPE,
                             stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, env=env,
                             cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

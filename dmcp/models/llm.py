@@ -322,13 +322,6 @@ class LocalLM:
                           and self.max_rows >= self.TGEMM_MLP_MIN_ROWS)
         self.tg_ws = (torch.empty(16 * self.max_rows * max(c.qkv_dim, c.hidden), dtype=torch.float32,
                                   device=self.device) if self.use_tgemm else None)
-        # steps past WGEMM_MAX_ROWS: the split-K reductions inside the GEMMs
-        # (last-arriver fixup) and every RMSNorm as the next GEMM's row scale
-        # -- no reduction / norm kernel in the step (csrc/tgemm.hip TgEpi);
-        # head_dim 64 (the QKV epilogue's RoPE pairs sit in one lane)
-        self.tg_fixup = self.use_tgemm and c.head_dim == 64
-        self.tg_fx = (ops.tgemm_fixup_workspace(self.max_rows, max(c.qkv_dim, c.hidden), c.hidden, self.device)
-                      if self.tg_fixup else None)
         self.tg_head = (self.fused_head and c.vocab_size % 256 == 0 and c.hidden % 64 == 0
                         and self.max_rows >= self.TGEMM_HEAD_MIN_ROWS and self.max_rows <= ops.TGEMM_MAX_ROWS)
         self.tg_head_ws = (torch.empty(2 * (c.vocab_size // 64) * self.max_rows, dtype=torch.float32,
@@ -659,25 +652,16 @@ class LocalLM:
         return F.linear(h, self.w["lm_head"])
 
     def _decode_trunk(self, tokens, slots, positions, src, last_ids, mask_idx, mask_alt, alt_token,
-                      prefix_rows, row_scale: bool = False):
+                      prefix_rows) -> torch.Tensor:
         """Every layer of a decode step of > ``fused_max_rows`` rows; returns
-        the final normalised hidden states [B, hidden] (the LM head's input).
-        ``row_scale``: returns (x, RowScale or None) instead -- x the residual
-        stream whose final RMSNorm the LM head applies as a row factor (the
-        fixup trunk), or the normalised rows and None."""
+        the final normalised hidden states [B, hidden] (the LM head's input)."""
         c = self.cfg
         B = tokens.shape[0]
         chunk, splits = ops.decode_plan(B, c.n_kv_heads, c.max_seq, c.kv_dtype)
         resid, h, seq_len = ops.decode_embed_norm(self.w["embed"], tokens, positions, self.w["l0.ln1"], c.eps,
                                                   src, last_ids, mask_idx, mask_alt, alt_token)
         if self.decode_fp8 and (self.device.type == "cpu" or B <= ops.WMX_MAX_ROWS):
-            h = self._decode_trunk_fp8(B, resid, h, seq_len, slots, positions, chunk, splits, prefix_rows)
-            return (h, None) if row_scale else h
-        if self.use_tgemm and self.tg_fixup and ops.WGEMM_MAX_ROWS < B <= ops.TGEMM_MAX_ROWS:
-            x, rs = self._decode_trunk_fixup(B, resid, h, seq_len, slots, positions, chunk, splits, prefix_rows)
-            if row_scale:
-                return x, rs
-            return ops.add_rmsnorm(x, self.w["norm_f"], c.eps)
+            return self._decode_trunk_fp8(B, resid, h, seq_len, slots, positions, chunk, splits, prefix_rows)
         wide = self.use_wgemm and B <= ops.WGEMM_MAX_ROWS
         big = self.use_tgemm and ops.WGEMM_MAX_ROWS < B <= ops.TGEMM_MAX_ROWS
         mlp_t = self.use_tgemm and self.TGEMM_MLP_MIN_ROWS <= B <= ops.TGEMM_MAX_ROWS
@@ -709,32 +693,7 @@ class LocalLM:
                 h = ops.wgemm_resid_norm(act, self.w[f"l{i}.wdown"], resid, nxt, c.eps, self.wgemm_ws)
             else:
                 h = ops.add_rmsnorm(self._mlp(i, h), nxt, c.eps, residual=resid)
-        return (h, None) if row_scale else h
-
-    def _decode_trunk_fixup(self, B, resid, h, seq_len, slots, positions, chunk, splits, prefix_rows):
-        """The layers of a step of WGEMM_MAX_ROWS < B <= TGEMM_MAX_ROWS rows on
-        the large-tile GEMM with everything between the GEMMs folded into
-        them: QKV (split-K reduced in the GEMM, RMSNorm row scale, RoPE, q
-        write, KV append) -> attention -> O (+ residual, row sums of squares)
-        -> gate/up (row scale, SwiGLU) -> down (+ residual, sums of squares).
-        Norm weights are folded into the consuming matrices (_fold_norms).
-        Returns (residual stream, its final RowScale)."""
-        c = self.cfg
-        ws = self.tg_fx
-        rs = None  # layer 0 reads the embedding rows decode_embed_norm already normalised
-        x = h
-        for i in range(c.layers):
-            kc, vc = self.k_cache[i], self.v_cache[i]
-            q = ops.tgemm_qkv(x, self.w[f"l{i}.wqkv"], positions, slots, self.cos_sin, kc, vc, c.n_heads, ws,
-                              row_scale=rs)
-            att = ops.decode_attention(q, kc, vc, slots, seq_len, self.scale, workspace=self.attn_ws, chunk=chunk,
-                                       fork=self.fork_tab, prefix=self._prefix(i, prefix_rows),
-                                       splits=splits).view(B, c.n_heads * c.head_dim)
-            rs = ops.tgemm_resid(att, self.w[f"l{i}.wo"], resid, ws, c.eps)
-            act = ops.tgemm_swiglu_scaled(resid, self.w[f"l{i}.wgu"], rs)
-            rs = ops.tgemm_resid(act, self.w[f"l{i}.wdown"], resid, ws, c.eps)
-            x = resid
-        return resid, rs
+        return h
 
     def _decode_trunk_fp8(self, B, resid, h, seq_len, slots, positions, chunk, splits, prefix_rows) -> torch.Tensor:
         """The layers of a decode step on the fp8 weights: every projection's
@@ -950,14 +909,12 @@ class LocalLM:
         if self.fused_head and not (self.use_fused and B <= self.fused_max_rows):
             # the LM head + grammar-masked selection in one weight-streaming
             # kernel: no [B, vocab] logits (returned as None)
-            h, rs = self._decode_trunk(tokens, slots, positions, src, last_ids, mask_idx, mask_alt, alt_token,
-                                       prefix_rows, row_scale=True)
+            h = self._decode_trunk(tokens, slots, positions, src, last_ids, mask_idx, mask_alt, alt_token,
+                                   prefix_rows)
             if self.tg_head and B >= self.TGEMM_HEAD_MIN_ROWS:
                 ids = ops.tgemm_lm_head_argmax(h, self.w["lm_head"], masks, mask_idx, out=last_ids[:B],
-                                               workspace=self.tg_head_ws, row_scale=rs)
+                                               workspace=self.tg_head_ws)
             else:
-                if rs is not None:  # the LM head kernel below takes normalised rows
-                    h = ops.add_rmsnorm(h, self.w["norm_f"], self.cfg.eps)
                 ids = ops.lm_head_argmax(h, self.w["lm_head"], masks, mask_idx, out=last_ids[:B],
                                          workspace=self.head_ws)
             return None, ids

@@ -20,7 +20,6 @@ from .hip import (PGEMM_TILE_N, WMX_MAX_ROWS, pgemm_supported, wgemm_mx_resid_no
                   wgemm_mx_swiglu, wmx_plan)
 from .hip import (TGEMM_MAX_ROWS, tgemm_lm_head_argmax, tgemm_resid_norm, tgemm_rope_kv, tgemm_swiglu,  # noqa: F401
                   wgemm)
-from .hip import (RowScale, tgemm_fixup_workspace, tgemm_qkv, tgemm_resid, tgemm_swiglu_scaled)  # noqa: F401
 from .reference import SharedPrefix, mx_dequant, quantize_weight, rope_tables, weight_dequant  # noqa: F401
 
 

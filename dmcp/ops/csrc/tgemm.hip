@@ -65,41 +65,7 @@ __device__ __forceinline__ void wait_vm(int n) {
 }
 constexpr int TNB = 256;  // weight rows per block
 constexpr int TTH = 512;  // threads per block: 8 waves, two per SIMD
-constexpr int TM_BF16 = 0, TM_PART = 1, TM_SWIGLU = 2, TM_ARGMAX = 3, TM_QKV = 4, TM_RESID = 5;
-
-// Arguments of the fused split-K modes and of the consumers' row scale
-// (dmcp.ops.hip.TgEpi mirrors this layout field for field):
-//
-//   * split-K without a reduction kernel (TM_QKV, TM_RESID): every block of
-//     a (weight tile, M part) writes its fp32 partial slab, publishes it
-//     (agent-scope release, then a ticket on cnt[tile]) and the block that
-//     draws the last ticket adds the other slabs to its accumulators (agent-
-//     scope acquire) and runs the epilogue -- cdna_hip_programming.md §5
-//     "Projection GEMM at M = 256" item 2; nobody waits, so no residency
-//     assumption.  The last arriver resets its counter for the next launch
-//     (the counters start zeroed);
-//   * the RMSNorm of the residual stream without a norm pass: TM_RESID writes
-//     resid += bf16(y) and, per row, the sum of squares of its 256 columns
-//     (sq_out[tile][m]); a consumer (TM_QKV / TM_SWIGLU / TM_ARGMAX on the
-//     un-normalised residual, norm weights folded into its matrix at load,
-//     LocalLM._fold_norms) scales row m's accumulators by
-//     r[m] = rsqrt(sum_j rsq[j][m] * inv_n + eps) -- the RMSNorm as a per-row
-//     factor of the GEMM (rms(x) * g . W^T == rms(x) . (W g)^T).
-struct TgEpi {
-    int* cnt;                 // [ntiles * mparts] tickets (S > 1)
-    const float* rsq;         // [nrsq][M] row sums of squares, or null (no scale)
-    float* sq_out;            // TM_RESID: [N / 256][M]
-    uint16_t* resid;          // TM_RESID: [M, N] bf16, updated in place
-    const int32_t* pos;       // TM_QKV: [M]
-    const int32_t* slot;      // TM_QKV: [M]
-    const float2* cos_sin;    // TM_QKV: [max_pos, 32] (cos, sin)
-    uint16_t* q_out;          // TM_QKV: [M, Hq, 64]
-    void* k_cache;            // TM_QKV: [num_slots, Hkv, max_seq, 64] bf16 / e4m3
-    void* v_cache;
-    int nrsq;
-    float inv_n, eps;
-    int Hq, Hkv, max_seq, max_pos, num_slots, kv8;
-};
+constexpr int TM_BF16 = 0, TM_PART = 1, TM_SWIGLU = 2, TM_ARGMAX = 3;
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float tsilu(float g) { return g / (1.f + __expf(-g)); }
@@ -151,7 +117,7 @@ template <int MT, int MODE, int PROBE = 0, int KC = TKC_DEFAULT, int CAP = 6, in
 __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) void tgemm_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, float* __restrict__ part,
     int M, int N, int K, int cps, int S, int ntiles, int mparts, int mrows, int I, const uint32_t* __restrict__ masks,
-    const int32_t* __restrict__ midx, int n_masks, int wwords, const TgEpi e) {
+    const int32_t* __restrict__ midx, int n_masks, int wwords) {
     constexpr int NF = TNB / 64;       // A fragments per wave (16 weight rows each): a quarter of the tile's rows
     constexpr int XT = 2 * MT;         // B fragments per wave (16 X rows each): half the tile's rows
     constexpr int RCH = KC / 8;        // 16-B chunks per image row
@@ -180,39 +146,24 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // block -> (weight tile nt, K slice s, M part mp): the M parts of one
     // (nt, s) unit share blockIdx % 8 (one XCD) and consecutive dispatch slots
     const int units = ntiles * S;
-    int u, mp, nt, s;
-    constexpr bool FIXUP = MODE == TM_QKV || MODE == TM_RESID;
-    if constexpr (FIXUP) {
-        // tile-major over XCD-contiguous ranges: the S slices x M parts of a
-        // weight tile are consecutive on one XCD, so the tile is read once
-        // from HBM and the last arriver reads the other slabs from its own L2
+    int u, mp;
+    if ((units & 7) == 0) {
+        const int j = blockIdx.x >> 3;
+        u = (j / mparts) * 8 + (blockIdx.x & 7);
+        mp = j % mparts;
+    } else {
+        // XCD-contiguous ranges (bijective for any grid; blocks are dealt
+        // round-robin over the 8 XCDs): a unit's M parts are consecutive in
+        // one XCD's range, so its weight tile is read once from HBM / MALL
+        // and hit in that XCD's L2 by the other parts (the LM head: 501
+        // units, whose parts had landed on three different XCDs)
         const int nblk = units * mparts, b = blockIdx.x;
         const int xcd = b & 7, q8 = nblk >> 3, r8 = nblk & 7;
         const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-        nt = L / (S * mparts);
-        const int rem = L - nt * (S * mparts);
-        s = rem / mparts;
-        mp = rem - s * mparts;
-    } else {
-        if ((units & 7) == 0) {
-            const int j = blockIdx.x >> 3;
-            u = (j / mparts) * 8 + (blockIdx.x & 7);
-            mp = j % mparts;
-        } else {
-            // XCD-contiguous ranges (bijective for any grid; blocks are dealt
-            // round-robin over the 8 XCDs): a unit's M parts are consecutive in
-            // one XCD's range, so its weight tile is read once from HBM / MALL
-            // and hit in that XCD's L2 by the other parts (the LM head: 501
-            // units, whose parts had landed on three different XCDs)
-            const int nblk = units * mparts, b = blockIdx.x;
-            const int xcd = b & 7, q8 = nblk >> 3, r8 = nblk & 7;
-            const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-            u = L / mparts;
-            mp = L % mparts;
-        }
-        nt = u % ntiles;
-        s = u / ntiles;
+        u = L / mparts;
+        mp = L % mparts;
     }
+    const int nt = u % ntiles, s = u / ntiles;
     const int chunks_all = K / KC;
     const int cbeg = s * cps;
     const int chunks = min(chunks_all, cbeg + cps) - cbeg;  // > 0 (host contract)
@@ -355,164 +306,10 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // epilogue: lane (l16, g) holds Y[row m_lo + mw + 16t + l16][col c0 + 16f + 4g + i]
     // with c0 = n0 + 64 wn (SwiGLU: intermediate column n0h + 32 wn + 16f + 4g + i of f < NF / 2)
     const int c0 = n0 + 64 * wn;
-    if constexpr (FIXUP) {
-        if (S > 1) {
-            // publish this slice's slab; the last of the tile's S blocks goes on
-#pragma unroll
-            for (int t = 0; t < XT; ++t) {
-                const int m = m_lo + mw + 16 * t + l16;
-                if (t >= mtv || m >= m_hi) continue;
-                float* dst = part + ((size_t)s * M + m) * N + c0 + 4 * g;
-#pragma unroll
-                for (int f = 0; f < NF; ++f)
-                    *reinterpret_cast<float4*>(dst + 16 * f) =
-                        make_float4(acc[f][t][0], acc[f][t][1], acc[f][t][2], acc[f][t][3]);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores done
-            __syncthreads();  // every wave's (and every wave is past the ring: LDS word 0 is free)
-            int* flag = reinterpret_cast<int*>(lds);
-            if (tid == 0) {
-                int* ticket = e.cnt + nt * mparts + mp;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep: the fence's own wait can be dropped
-                const int old = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const int last = old == S - 1;
-                if (last) {
-                    __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
-                flag[0] = last;
-            }
-            __syncthreads();
-            if (!flag[0]) return;  // block-uniform
-#pragma unroll
-            for (int t = 0; t < XT; ++t) {
-                const int m = m_lo + mw + 16 * t + l16;
-                if (t >= mtv || m >= m_hi) continue;
-                for (int s2 = 0; s2 < S; ++s2) {
-                    if (s2 == s) continue;
-                    const float* src = part + ((size_t)s2 * M + m) * N + c0 + 4 * g;
-#pragma unroll
-                    for (int f = 0; f < NF; ++f) {
-                        const float4 v = *reinterpret_cast<const float4*>(src + 16 * f);
-                        acc[f][t][0] += v.x;
-                        acc[f][t][1] += v.y;
-                        acc[f][t][2] += v.z;
-                        acc[f][t][3] += v.w;
-                    }
-                }
-            }
-        }
-    }
-    // the consumer's RMSNorm as a row factor (TgEpi)
-    auto rowscale = [&](int m) -> float {
-        if (e.rsq == nullptr) return 1.f;
-        float ss = 0.f;
-        for (int j = 0; j < e.nrsq; ++j) ss += e.rsq[(size_t)j * M + m];
-        return rsqrtf(ss * e.inv_n + e.eps);
-    };
-    if constexpr (MODE == TM_RESID) {
-        // resid += bf16(y) in place; per row the sum of squares of the new
-        // (bf16) stream over this block's 256 columns -> sq_out[nt][m]
-        float* red = reinterpret_cast<float*>(lds);  // [rows of the block][4 weight quarters]
-        __syncthreads();  // S == 1: every wave is past the ring
-#pragma unroll
-        for (int t = 0; t < XT; ++t) {
-            const int r = mw + 16 * t + l16;
-            const int m = m_lo + r;
-            float ss = 0.f;
-            if (t < mtv && m < m_hi) {
-                uint16_t* rp = e.resid + (size_t)m * N + c0 + 4 * g;
-#pragma unroll
-                for (int f = 0; f < NF; ++f) {
-                    float y[4], rv[4];
-                    unpack4(*reinterpret_cast<const uint2*>(rp + 16 * f), rv);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {  // the GEMM's bf16 output, then the bf16 stream
-                        y[i] = bf2f(f2bf(bf2f(f2bf(acc[f][t][i])) + rv[i]));
-                        ss += y[i] * y[i];
-                    }
-                    *reinterpret_cast<uint2*>(rp + 16 * f) = pack4(y);
-                }
-            }
-            ss += __shfl_xor(ss, 16, kWave);
-            ss += __shfl_xor(ss, 32, kWave);
-            if (g == 0 && t < XT) red[r * 4 + wn] = ss;
-        }
-        __syncthreads();
-        for (int r = tid; r < 2 * XT * 16; r += TTH) {
-            const int m = m_lo + r;
-            if (m < m_hi) e.sq_out[(size_t)nt * M + m] = red[r * 4] + red[r * 4 + 1] + red[r * 4 + 2] + red[r * 4 + 3];
-        }
-        return;
-    }
-    if constexpr (MODE == TM_QKV) {
-        // head_dim 64: a wave's 64 weight rows are one head (c0 / 64); RoPE
-        // pairs d and d + 32 = fragments f and f + 2 of the same lane
-        const int head = c0 >> 6;
-        const bool rope = head < e.Hq + e.Hkv;
-        const bool isq = head < e.Hq;
-#pragma unroll
-        for (int t = 0; t < XT; ++t) {
-            const int m = m_lo + mw + 16 * t + l16;
-            if (t >= mtv || m >= m_hi) continue;
-            const float rs = rowscale(m);
-            float v[NF][4];
-#pragma unroll
-            for (int f = 0; f < NF; ++f)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) v[f][i] = bf2f(f2bf(acc[f][t][i] * rs));  // the projection's bf16 output
-            const int p = e.pos[m];
-            if (rope) {
-                const float2* cs = e.cos_sin + (size_t)min(max(p, 0), e.max_pos - 1) * 32;
-#pragma unroll
-                for (int f = 0; f < 2; ++f)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const float2 c = cs[16 * f + 4 * g + i];
-                        const float a = v[f][i], b = v[f + 2][i];
-                        v[f][i] = a * c.x - b * c.y;
-                        v[f + 2][i] = b * c.x + a * c.y;
-                    }
-            }
-            if (isq) {
-                uint16_t* dst = e.q_out + ((size_t)m * e.Hq + head) * 64 + 4 * g;
-#pragma unroll
-                for (int f = 0; f < NF; ++f) *reinterpret_cast<uint2*>(dst + 16 * f) = pack4(v[f]);
-                continue;
-            }
-            const int sl = e.slot[m];
-            if (p < 0 || p >= e.max_seq || sl < 0 || sl >= e.num_slots) continue;
-            const bool isv = head >= e.Hq + e.Hkv;
-            const int kh = head - e.Hq - (isv ? e.Hkv : 0);
-            const size_t ofs = (((size_t)sl * e.Hkv + kh) * e.max_seq + p) * 64 + 4 * g;
-            void* base = isv ? e.v_cache : e.k_cache;
-            if (e.kv8) {
-                uint8_t* d8 = static_cast<uint8_t*>(base) + ofs;
-#pragma unroll
-                for (int f = 0; f < NF; ++f) *reinterpret_cast<uint32_t*>(d8 + 16 * f) = pack_fp8x4_bf16r(v[f]);
-            } else {
-                uint16_t* d16 = static_cast<uint16_t*>(base) + ofs;
-#pragma unroll
-                for (int f = 0; f < NF; ++f) *reinterpret_cast<uint2*>(d16 + 16 * f) = pack4(v[f]);
-            }
-        }
-        return;
-    }
 #pragma unroll
     for (int t = 0; t < XT; ++t) {
         if (t >= mtv) continue;
         const int m = m_lo + mw + 16 * t + l16;
-        if constexpr (MODE == TM_SWIGLU || MODE == TM_ARGMAX) {
-            if (e.rsq != nullptr && m < m_hi) {
-                const float rs = rowscale(m);
-#pragma unroll
-                for (int f = 0; f < NF; ++f)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) acc[f][t][i] *= rs;
-            }
-        }
         if constexpr (MODE == TM_ARGMAX) {
             float bv = -INFINITY;
             int bi = 0x7fffffff;
@@ -627,39 +424,24 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int wv = __builtin_amdgcn_readfirstlane(tid / kWave);
     const int l16 = lane & 15, g = lane >> 4;
     const int units = ntiles * S;
-    int u, mp, nt, s;
-    constexpr bool FIXUP = MODE == TM_QKV || MODE == TM_RESID;
-    if constexpr (FIXUP) {
-        // tile-major over XCD-contiguous ranges: the S slices x M parts of a
-        // weight tile are consecutive on one XCD, so the tile is read once
-        // from HBM and the last arriver reads the other slabs from its own L2
+    int u, mp;
+    if ((units & 7) == 0) {
+        const int j = blockIdx.x >> 3;
+        u = (j / mparts) * 8 + (blockIdx.x & 7);
+        mp = j % mparts;
+    } else {
+        // XCD-contiguous ranges (bijective for any grid; blocks are dealt
+        // round-robin over the 8 XCDs): a unit's M parts are consecutive in
+        // one XCD's range, so its weight tile is read once from HBM / MALL
+        // and hit in that XCD's L2 by the other parts (the LM head: 501
+        // units, whose parts had landed on three different XCDs)
         const int nblk = units * mparts, b = blockIdx.x;
         const int xcd = b & 7, q8 = nblk >> 3, r8 = nblk & 7;
         const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-        nt = L / (S * mparts);
-        const int rem = L - nt * (S * mparts);
-        s = rem / mparts;
-        mp = rem - s * mparts;
-    } else {
-        if ((units & 7) == 0) {
-            const int j = blockIdx.x >> 3;
-            u = (j / mparts) * 8 + (blockIdx.x & 7);
-            mp = j % mparts;
-        } else {
-            // XCD-contiguous ranges (bijective for any grid; blocks are dealt
-            // round-robin over the 8 XCDs): a unit's M parts are consecutive in
-            // one XCD's range, so its weight tile is read once from HBM / MALL
-            // and hit in that XCD's L2 by the other parts (the LM head: 501
-            // units, whose parts had landed on three different XCDs)
-            const int nblk = units * mparts, b = blockIdx.x;
-            const int xcd = b & 7, q8 = nblk >> 3, r8 = nblk & 7;
-            const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-            u = L / mparts;
-            mp = L % mparts;
-        }
-        nt = u % ntiles;
-        s = u / ntiles;
+        u = L / mparts;
+        mp = L % mparts;
     }
+    const int nt = u % ntiles, s = u / ntiles;
     const int chunks_all = K / KC;
     const int cbeg = s * cps;
     const int chunks = min(chunks_all, cbeg + cps) - cbeg;  // > 0 (host contract)
@@ -817,7 +599,7 @@ __global__ __launch_bounds__(kBlock) void tgemm_argmax_reduce_kernel(const float
 template <int MODE, int PROBE = 0, int KC = TKC_DEFAULT, int CAP = 6, int PF = 0>
 hipError_t launch_tgemm(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int M, int N, int K, int S,
                         int mparts, int I, hipStream_t st, const uint32_t* masks, const int32_t* midx, int n_masks,
-                        int wwords, const TgEpi& e = TgEpi{}) {
+                        int wwords) {
     const int ntiles = (MODE == TM_SWIGLU ? 2 * I : N) / TNB;
     const int mrows = (((M + mparts - 1) / mparts) + 15) & ~15;
     const int mt = (mrows + 63) / 64;
@@ -826,7 +608,7 @@ hipError_t launch_tgemm(const uint16_t* x, const uint16_t* w, uint16_t* y, float
     const dim3 grid((unsigned)(ntiles * S * mparts));
 #define DMCP_TG(MT)                                                                                                 \
     tgemm_kernel<MT, MODE, PROBE, KC, CAP, PF><<<grid, TTH, 0, st>>>(x, w, y, part, M, N, K, cps, S, ntiles, mparts, mrows, I, masks, \
-                                                    midx, n_masks, wwords, e)
+                                                    midx, n_masks, wwords)
     switch (mt) {
         case 1: DMCP_TG(1); break;
         case 2: DMCP_TG(2); break;
@@ -903,51 +685,6 @@ int dmcp_tgemm(const void* x, const void* w, void* y, void* part, int M, int N, 
                 (const float2*)part, 4 * (N / TNB), M, (int32_t*)ids);
             return hipGetLastError();
         }
-        default: return hipErrorInvalidValue;
-    }
-}
-
-// The large-tile GEMM with TgEpi (row scale / split-K fixup):
-//   mode 2: tgemm mode 2 with the row scale (e->rsq)
-//   mode 3: tgemm mode 3 with the row scale
-//   mode 4: QKV: q [M, Hq, 64] bf16 = RoPE(bf16(r[m] * x . w^T)), k / v appended to the caches;
-//           S K slices (part: [S, M, N] fp32 slabs, e->cnt: ntiles * mparts zeroed tickets)
-//   mode 5: resid [M, N] += bf16(x . w^T); e->sq_out [N / 256, M] = row sums of squares of the new resid
-// Contract (checked by dmcp/ops/hip.py, guarded here): as dmcp_tgemm; mode 4: head_dim 64, N = (Hq + 2 Hkv) 64.
-// layout witness of TgEpi for the ctypes mirror (checked at load)
-int dmcp_tgemm_epi_size() { return (int)sizeof(TgEpi); }
-
-int dmcp_tgemm_ex(const void* x, const void* w, void* y, void* part, int M, int N, int K, int S, int mparts, int mode,
-                  int I, const void* masks, const void* midx, int n_masks, int wwords, void* ids, const TgEpi* e,
-                  void* stream) {
-    if (M <= 0) return 0;
-    const int chunks = K / TKC_DEFAULT;
-    if (!x || !w || !e || S < 1 || mparts < 1 || K <= 0 || K % TKC_DEFAULT != 0 || S > chunks ||
-        (S - 1) * ((chunks + S - 1) / S) >= chunks || (((M + mparts - 1) / mparts + 15) & ~15) > 256 ||
-        (mode == 2 ? (I <= 0 || I % (TNB / 2) != 0 || !y || S != 1) : (N <= 0 || N % TNB != 0)) ||
-        (mode == 3 && (!part || !masks || !ids || n_masks < 1 || wwords < (N + 31) / 32 || S != 1)) ||
-        ((mode == 4 || mode == 5) && S > 1 && (!part || !e->cnt)) ||
-        (mode == 4 && (!e->pos || !e->slot || !e->cos_sin || !e->q_out || !e->k_cache || !e->v_cache ||
-                       N != (e->Hq + 2 * e->Hkv) * 64 || e->max_pos < 1)) ||
-        (mode == 5 && (!e->resid || !e->sq_out)) || (e->rsq && e->nrsq < 1) || mode < 2 || mode > 5)
-        return hipErrorInvalidValue;
-    auto st = (hipStream_t)stream;
-    auto xx = (const uint16_t*)x;
-    auto ww = (const uint16_t*)w;
-    auto yy = (uint16_t*)y;
-    auto pp = (float*)part;
-    switch (mode) {
-        case 2: return launch_tgemm<TM_SWIGLU>(xx, ww, yy, pp, M, 2 * I, K, 1, mparts, I, st, nullptr, nullptr, 0, 0, *e);
-        case 3: {
-            hipError_t r = launch_tgemm<TM_ARGMAX>(xx, ww, nullptr, pp, M, N, K, 1, mparts, 0, st,
-                                                   (const uint32_t*)masks, (const int32_t*)midx, n_masks, wwords, *e);
-            if (r != hipSuccess) return r;
-            tgemm_argmax_reduce_kernel<<<(M + kBlock / kWave - 1) / (kBlock / kWave), kBlock, 0, st>>>(
-                (const float2*)part, 4 * (N / TNB), M, (int32_t*)ids);
-            return hipGetLastError();
-        }
-        case 4: return launch_tgemm<TM_QKV>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0, *e);
-        case 5: return launch_tgemm<TM_RESID>(xx, ww, nullptr, pp, M, N, K, S, mparts, 0, st, nullptr, nullptr, 0, 0, *e);
         default: return hipErrorInvalidValue;
     }
 }

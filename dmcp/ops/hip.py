@@ -85,8 +85,6 @@ def lib() -> ctypes.CDLL:
             "dmcp_wgemm": ([_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp], _i),
             "dmcp_tgemm": ([_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp], _i),
             "dmcp_tgemm_probe": ([_i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp], _i),
-            "dmcp_tgemm_epi_size": ([], _i),
-            "dmcp_tgemm_ex": ([_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp], _i),
             "dmcp_wgemm_resid_norm": ([_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _vp], _i),
             "dmcp_wgemm_rope_kv": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i,
                                     _i, _i, _vp], _i),
@@ -99,8 +97,6 @@ def lib() -> ctypes.CDLL:
             fn.restype = res
         if L.dmcp_abi_version() != ABI_VERSION:
             raise HipOpsError("HIP kernel library ABI mismatch; rebuild with python -m dmcp.ops.build")
-        if L.dmcp_tgemm_epi_size() != ctypes.sizeof(TgEpi):
-            raise HipOpsError("csrc/tgemm.hip TgEpi and dmcp.ops.hip.TgEpi differ in layout")
         _lib = L
         return _lib
 
@@ -1355,151 +1351,11 @@ def tgemm_rope_kv(x: torch.Tensor, w: torch.Tensor, pos: torch.Tensor, slot: tor
     return q_out
 
 
-class TgEpi(ctypes.Structure):
-    """csrc/tgemm.hip ``TgEpi``, field for field: the split-K fixup tickets,
-    the consumer's RMSNorm row scale and the fused epilogues' operands."""
-    _fields_ = [("cnt", _vp), ("rsq", _vp), ("sq_out", _vp), ("resid", _vp), ("pos", _vp), ("slot", _vp),
-                ("cos_sin", _vp), ("q_out", _vp), ("k_cache", _vp), ("v_cache", _vp), ("nrsq", _i),
-                ("inv_n", _f), ("eps", _f), ("Hq", _i), ("Hkv", _i), ("max_seq", _i), ("max_pos", _i),
-                ("num_slots", _i), ("kv8", _i)]
-
-
-class RowScale:
-    """The RMSNorm of the residual stream as a per-row factor of the next
-    GEMM: ``sq`` [N / 256, >= M] fp32 row sums of squares written by
-    :func:`tgemm_resid` (one per 256 columns), ``n`` the row width, ``eps``.
-    r[m] = rsqrt(sum_j sq[j, m] / n + eps)."""
-    __slots__ = ("sq", "n", "eps")
-
-    def __init__(self, sq: torch.Tensor, n: int, eps: float) -> None:
-        self.sq, self.n, self.eps = sq, int(n), float(eps)
-
-
-def tgemm_fixup_workspace(max_rows: int, max_n: int, hidden: int, device) -> dict:
-    """Workspaces of the fused split-K modes: fp32 slabs (up to 16 slices),
-    zeroed tickets (the kernel's last arrivers reset them), the row sums of
-    squares of the residual stream."""
-    return {"part": torch.empty(16 * max_rows * max_n, dtype=torch.float32, device=device),
-            "cnt": torch.zeros(4096, dtype=torch.int32, device=device),
-            "sq": torch.zeros((max(1, hidden // TGEMM_NB), max_rows), dtype=torch.float32, device=device)}
-
-
-def _epi(rs: Optional[RowScale], M: int, **kw) -> TgEpi:
-    e = TgEpi()
-    if rs is not None:
-        _req(rs.sq, torch.float32, "row_scale.sq")
-        if rs.sq.dim() != 2 or rs.sq.shape[1] != M:
-            raise HipOpsError(f"row scale: sq {tuple(rs.sq.shape)} is not [N / 256, M={M}]")
-        e.rsq, e.nrsq, e.inv_n, e.eps = rs.sq.data_ptr(), rs.sq.shape[0], 1.0 / rs.n, rs.eps
-    for k, v in kw.items():
-        setattr(e, k, v.data_ptr() if isinstance(v, torch.Tensor) else v)
-    return e
-
-
-def _tg_ex(x, w, y, part, M, N, K, S, mparts, mode, e: TgEpi, inter=0, masks=None, midx=None, n_masks=0, wwords=0,
-           ids=None, name="dmcp_tgemm_ex") -> None:
-    _check(lib().dmcp_tgemm_ex(_ptr(x), _ptr(w), _ptr(y), _ptr(part), M, N, K, S, mparts, mode, inter, _ptr(masks),
-                               _ptr(midx), n_masks, wwords, _ptr(ids), ctypes.byref(e), _stream()), name)
-
-
-def tgemm_fixup_plan(M: int, N: int, K: int) -> tuple:
-    """(S, M parts) of the fused split-K modes (no reduction kernel): the
-    split-K partials' round trip is a last-arriver tail instead of a pass."""
-    return tgemm_plan(M, N, K, "part")
-
-
-def _fixup_args(x, w, ws: dict, name: str, splits: int, mparts: int) -> tuple:
-    M, K, N = _tgemm_args(x, w, name)
-    S, mp = tgemm_fixup_plan(M, N, K)
-    S, mparts = splits or S, mparts or mp
-    chunks = K // TGEMM_KC
-    if S > chunks or (S - 1) * -(-chunks // S) >= chunks:
-        raise HipOpsError(f"{name}: K={K} does not split into {S} non-empty slices")
-    rows = (-(-M // mparts) + 15) // 16 * 16
-    if rows > 256:
-        raise HipOpsError(f"{name}: {mparts} M parts leave {rows} > 256 rows per part")
-    part, cnt = ws["part"], ws["cnt"]
-    _wgemm_ws(part, S * M * N, name)
-    _req(cnt, torch.int32, f"{name}.cnt")
-    if cnt.numel() < (N // TGEMM_NB) * mparts:
-        raise HipOpsError(f"{name}: ticket workspace too small")
-    return M, K, N, S, mparts
-
-
-def tgemm_resid(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, workspace: dict, eps: float,
-                splits: int = 0, mparts: int = 0) -> RowScale:
-    """residual += bf16(x . w^T) in place, split-K reduced inside the GEMM
-    (last-arriver fixup); also writes the row sums of squares of the new
-    residual (``workspace["sq"]``) and returns them as the next GEMM's
-    RMSNorm row scale with the norm's ``eps`` (the norm weight is folded into
-    the consumer's matrix, LocalLM._fold_norms)."""
-    M, K, N, S, mparts = _fixup_args(x, w, workspace, "tgemm_resid", splits, mparts)
-    _req(residual, torch.bfloat16, "tgemm_resid.residual")
-    if tuple(residual.shape) != (M, N):
-        raise HipOpsError(f"tgemm_resid: residual {tuple(residual.shape)} is not [{M}, {N}]")
-    sq = workspace["sq"]
-    if sq.dtype != torch.float32 or sq.dim() != 2 or sq.shape[0] < N // TGEMM_NB or sq.shape[1] < M:
-        raise HipOpsError("tgemm_resid: sq workspace too small")
-    sq_m = sq.view(-1)[: (N // TGEMM_NB) * M].view(N // TGEMM_NB, M)  # dense [tiles, M]
-    e = _epi(None, M, cnt=workspace["cnt"], resid=residual, sq_out=sq_m)
-    _tg_ex(x, w, None, workspace["part"], M, N, K, S, mparts, 5, e, name="dmcp_tgemm_ex[resid]")
-    return RowScale(sq_m, N, eps)
-
-
-def tgemm_qkv(x: torch.Tensor, w: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos_sin: torch.Tensor,
-              k_cache: torch.Tensor, v_cache: torch.Tensor, n_q_heads: int, workspace: dict,
-              row_scale: Optional[RowScale] = None, q_out: Optional[torch.Tensor] = None, splits: int = 0,
-              mparts: int = 0) -> torch.Tensor:
-    """rope_kv(F.linear(rmsnorm(x), w), ...) on the large-tile kernel with the
-    split-K reduction, the RMSNorm row scale (``row_scale``; None: x is
-    already normalised), RoPE, the q write and the KV append all inside the
-    GEMM; head_dim 64.  Returns q [M, Hq, 64]."""
-    M, K, N, S, mparts = _fixup_args(x, w, workspace, "tgemm_qkv", splits, mparts)
-    S_, Hkv, MAXS, D = k_cache.shape
-    kv8 = _req_kv(k_cache, v_cache, "tgemm_qkv")
-    _req(pos, torch.int32, "tgemm_qkv.pos")
-    _req(slot, torch.int32, "tgemm_qkv.slot")
-    _req(cos_sin, torch.float32, "tgemm_qkv.cos_sin")
-    if D != 64 or N != (n_q_heads + 2 * Hkv) * D:
-        raise HipOpsError(f"tgemm_qkv: needs head_dim 64 and w [(Hq + 2 Hkv) 64, K]; w {tuple(w.shape)}, "
-                          f"kv {tuple(k_cache.shape)}")
-    if pos.numel() != M or slot.numel() != M or cos_sin.dim() != 3 or tuple(cos_sin.shape[1:]) != (D // 2, 2):
-        raise HipOpsError("tgemm_qkv: pos/slot/cos_sin shape mismatch")
-    if q_out is None:
-        q_out = torch.empty((M, n_q_heads, D), dtype=torch.bfloat16, device=x.device)
-    _req_out(q_out, torch.bfloat16, M * n_q_heads * D, "tgemm_qkv.q_out")
-    if row_scale is not None and row_scale.eps <= 0:
-        raise HipOpsError("tgemm_qkv: the row scale needs the norm's eps")
-    e = _epi(row_scale, M, cnt=workspace["cnt"], pos=pos, slot=slot, cos_sin=cos_sin, q_out=q_out,
-             k_cache=k_cache, v_cache=v_cache, Hq=n_q_heads, Hkv=Hkv, max_seq=MAXS, max_pos=cos_sin.shape[0],
-             num_slots=S_, kv8=kv8)
-    _tg_ex(x, w, None, workspace["part"], M, N, K, S, mparts, 4, e, name="dmcp_tgemm_ex[qkv]")
-    return q_out
-
-
-def tgemm_swiglu_scaled(x: torch.Tensor, w: torch.Tensor, row_scale: RowScale, out: Optional[torch.Tensor] = None,
-                        mparts: int = 0) -> torch.Tensor:
-    """:func:`tgemm_swiglu` of rmsnorm(x): the norm as a row scale of the
-    gate / up accumulators (w norm-folded)."""
-    M, K, N = _tgemm_args(x, w, "tgemm_swiglu_scaled", swiglu=True)
-    inter = N // 2
-    mparts = mparts or tgemm_plan(M, N, K, "swiglu")[1]
-    if out is None:
-        out = torch.empty((M, inter), dtype=torch.bfloat16, device=x.device)
-    _req_out(out, torch.bfloat16, M * inter, "tgemm_swiglu_scaled.out")
-    if row_scale.eps <= 0:
-        raise HipOpsError("tgemm_swiglu_scaled: the row scale needs the norm's eps")
-    _tg_ex(x, w, out, None, M, N, K, 1, mparts, 2, _epi(row_scale, M), inter, name="dmcp_tgemm_ex[swiglu]")
-    return out
-
-
 def tgemm_lm_head_argmax(x: torch.Tensor, w: torch.Tensor, masks: torch.Tensor, mask_idx: torch.Tensor,
                          out: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
-                         mparts: int = 0, row_scale: Optional[RowScale] = None) -> torch.Tensor:
+                         mparts: int = 0) -> torch.Tensor:
     """:func:`lm_head_argmax` on the large-tile kernel (V % 256 == 0): 256
-    vocabulary ids per block, one (max, id) pair per block and row;
-    ``row_scale``: x is the un-normalised residual (the final RMSNorm as a
-    row factor, lm_head norm-folded)."""
+    vocabulary ids per block, one (max, id) pair per block and row."""
     M, K, V = _tgemm_args(x, w, "tgemm_lm_head_argmax")
     _req(masks, torch.int32, "tgemm_lm_head_argmax.masks")
     _req(mask_idx, torch.int32, "tgemm_lm_head_argmax.mask_idx")
@@ -1515,12 +1371,6 @@ def tgemm_lm_head_argmax(x: torch.Tensor, w: torch.Tensor, masks: torch.Tensor, 
     if workspace.dtype != torch.float32 or workspace.numel() < need:
         raise HipOpsError("tgemm_lm_head_argmax: workspace too small")
     mparts = mparts or tgemm_plan(M, V, K, "argmax")[1]
-    if row_scale is not None:
-        if row_scale.eps <= 0:
-            raise HipOpsError("tgemm_lm_head_argmax: the row scale needs the norm's eps")
-        _tg_ex(x, w, None, workspace, M, V, K, 1, mparts, 3, _epi(row_scale, M), 0, masks, mask_idx, masks.shape[0],
-               W, out, name="dmcp_tgemm_ex[argmax]")
-        return out
     _tg(x, w, None, workspace, M, V, K, 1, mparts, 3, 0, masks, mask_idx, masks.shape[0], W, out,
         name="dmcp_tgemm[argmax]")
     return out

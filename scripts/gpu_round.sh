@@ -112,9 +112,8 @@ for s in $STEPS; do
                 --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 60
             run step_llama268 300 python scripts/bench_step.py --preset llama3.2-1b-code --batch 256 --extra 12 \
                 --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 60 ;;
-        fixup_test) run fixup_test 600 python -u -m pytest tests/test_gpu_tgemm_fixup.py tests/test_gpu_tgemm.py -x -q \
-                --timeout 120 --timeout-method thread ;;
-        fixup_bench) run fixup_bench 600 python scripts/bench_tgemm_fixup.py --rows 520 610 768 1024 --sweep ;;
+        ckpt_test) run ckpt_test 900 python -u -m pytest tests/test_gpu_checkpoint_full.py -x -v -s --timeout 900 \
+                --timeout-method thread ;;
         step_llama3)  # the verdict's three operating points: 320 / 610 / 768 rows
             for r in "256 64" "512 98" "512 256"; do set -- $r
                 run step_llama$(($1 + $2)) 300 python scripts/bench_step.py --preset llama3.2-1b-code --batch $1 \

@@ -12,9 +12,10 @@ Checked against the fp32 reference model (``LocalLM.reference_logits``):
 * the engine's batched prefill (its default GEMMs for a loaded checkpoint)
   -- last-position logit cosine >= 0.999, per-layer K/V of the prompt within
   stated bounds of the fp32 K/V;
-* a 768-row decode step on the default kernels (the large-tile trunk with
-  the in-GEMM split-K fixup and RMSNorm row scales, the fused LM head +
-  masked argmax): cosine >= 0.999 on the reference rows, argmax agreement;
+* a 768-row decode step on the default kernels (the large-tile trunk: its
+  split-K GEMMs with the fused RoPE / KV-append and residual / RMSNorm
+  reductions, the fused LM head + masked argmax): cosine >= 0.999 on the
+  reference rows, argmax agreement;
 * the MXFP8 prefill (``prefill_dtype="fp8"``) on the same weights: logit
   cosine and top-1 agreement against fp32 -- the gate for using it on
   checkpoints (docs/PARITY.md)."""
@@ -153,7 +154,7 @@ def test_full_checkpoint_prefill_and_kv_match_fp32(ckpt):
 
 def test_full_checkpoint_768_row_decode_on_the_default_kernels(ckpt):
     m = _load(ckpt, max_batch=512, max_rows=768, max_seq=512, kv_dtype="fp8")
-    assert m.use_tgemm and m.tg_fixup and m.tg_head
+    assert m.use_tgemm and m.tg_head
     g = torch.Generator().manual_seed(2)
     base = _prompts(1, g)[0][:60]
     n_slots = 512

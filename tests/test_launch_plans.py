@@ -60,12 +60,3 @@ def test_tgemm_model_and_op_predicates_agree(inter, hidden):
     model_ok = tgemm_shapes_ok(c)
     assert model_ok == (ops_ok and c.qkv_dim <= 8192 and c.hidden <= 8192)
 
-
-@pytest.mark.parametrize("M", [513, 610, 768, 1024])
-@pytest.mark.parametrize("N,K", [(3072, 2048), (2048, 2048), (2048, 8192)])
-def test_tgemm_fixup_plan_fits_the_kernel(M, N, K):
-    S, mparts = hip.tgemm_fixup_plan(M, N, K)
-    chunks = K // hip.TGEMM_KC
-    assert 1 <= S <= chunks and (S - 1) * -(-chunks // S) < chunks   # every K slice non-empty
-    assert (-(-M // mparts) + 15) // 16 * 16 <= 256                  # <= 256 rows per M part
-    assert (N // hip.TGEMM_NB) * mparts <= 4096                       # tickets in the workspace

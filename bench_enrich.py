@@ -52,6 +52,11 @@ def main(argv=None) -> int:
     ap.add_argument("--reply-shape", default="derived", choices=["derived", "legacy"],
                     help="string caps / steps of the replies: derived from the reply budget (the service default, "
                          "256 / 128 / 64 bytes, 4 steps at 4,096 tokens) or the round-4 fixed 96 / 64 / 40, 3")
+    ap.add_argument("--checkpoint", default="",
+                    help="a Llama-format checkpoint directory (LOCAL_LLM_MODEL_PATH) instead of the preset's random "
+                         "weights; with --write-checkpoint a synthetic one (trained-like random weights, Llama-3.2-1B "
+                         "geometry, the code BPE) is written there first when it has no config.json")
+    ap.add_argument("--write-checkpoint", action="store_true")
     ap.add_argument("--fork-max-context", type=int, default=-1,
                     help="fork only classes with at most this many own prompt tokens (-1: the engine default)")
     args = ap.parse_args(argv)
@@ -70,13 +75,27 @@ def main(argv=None) -> int:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl")
-    cfg = preset(args.preset, max_batch=args.batch, max_seq=args.max_seq, kv_dtype=args.kv_dtype,
-                 prefill_dtype=args.prefill_dtype, decode_dtype=args.decode_dtype, max_rows=args.max_rows or max(args.batch, min(1024, max(256, args.batch + args.batch // 2))))
-    model = LocalLM(cfg, device=f"cuda:{local}", seed=rank)
-    tok = None
-    if cfg.tokenizer:
-        from dmcp.enrich.tokenizer import load_asset_tokenizer
-        tok = load_asset_tokenizer(cfg.tokenizer)
+    max_rows = args.max_rows or max(args.batch, min(1024, max(256, args.batch + args.batch // 2)))
+    if args.checkpoint:
+        from dmcp.enrich.tokenizer import load_local_model
+        if args.write_checkpoint and not os.path.exists(os.path.join(args.checkpoint, "config.json")):
+            from dmcp.utils import synth
+            if rank == 0:
+                synth.llama_checkpoint(args.checkpoint, device=f"cuda:{local}")
+            if dist is not None:
+                dist.barrier()
+        model, tok = load_local_model(args.checkpoint, device=f"cuda:{local}", max_batch=args.batch,
+                                      max_seq=args.max_seq, kv_dtype=args.kv_dtype, prefill_dtype=args.prefill_dtype,
+                                      decode_dtype=args.decode_dtype, max_rows=max_rows)
+        cfg = model.cfg
+    else:
+        cfg = preset(args.preset, max_batch=args.batch, max_seq=args.max_seq, kv_dtype=args.kv_dtype,
+                     prefill_dtype=args.prefill_dtype, decode_dtype=args.decode_dtype, max_rows=max_rows)
+        model = LocalLM(cfg, device=f"cuda:{local}", seed=rank)
+        tok = None
+        if cfg.tokenizer:
+            from dmcp.enrich.tokenizer import load_asset_tokenizer
+            tok = load_asset_tokenizer(cfg.tokenizer)
     eng = LocalEngine(model, use_graphs=not args.no_graphs, jump_forward=not args.no_jump,
                       shared_prefix=not args.no_shared_prefix, pipeline=not args.no_pipeline,
                       admit_min=args.admit_min or None, tokenizer=tok, max_new_tokens=args.max_new_tokens,
@@ -130,7 +149,8 @@ def main(argv=None) -> int:
         print(json.dumps({
             "metric": "classes enriched/sec (local MI355X model)", "value": round(ok_all / elapsed, 3),
             "unit": "classes/s", "n_gpus": world, "higher_is_better": True, "scaling": "weak",
-            "dtype": "bf16", "data": "synthetic classes, random-init weights",
+            "dtype": "bf16", "data": "synthetic classes, " + ("checkpoint " + args.checkpoint if args.checkpoint
+                                                               else "random-init weights"),
             "config": {"model": cfg.name, "params_b": round(cfg.param_count() / 1e9, 3), "batch": args.batch,
                        "max_rows": cfg.max_rows, "kv_dtype": cfg.kv_dtype, "prefill_dtype": "fp8" if model.prefill_fp8 else "bf16", "decode_dtype": cfg.decode_dtype,
                        "max_seq": args.max_seq, "prompt_chars": args.prompt_chars,

@@ -167,9 +167,17 @@ def wgemm_shapes_ok(c: LMConfig) -> bool:
 # The MXFP8 prefill's numerics gate on a checkpoint: last-position logit
 # cosine against the fp32 reference model and top-1 agreement, measured on
 # trained-like weights of Llama-3.2-1B geometry (heavy-tailed matrices,
-# non-trivial norms, 100x residual outlier channels:
+# non-trivial norms, 100x residual outlier channels, an embedding that does
+# not dominate the residual stream: dmcp.utils.synth.llama_checkpoint).
+# Round 6 measured cosine 0.89-0.93 and top-1 3 / 12 there -- e4m3's ~3.6 %
+# rms rounding of every weight and activation compounds over 16 layers once
+# the layers, not the embedding, carry the logits (random-init presets pass
+# at 0.999 only because their std-1 embedding dominates) -- so a loaded
+# checkpoint keeps the bf16 prefill (MXFP8_CHECKPOINT_OK, asserted against a
+# fresh measurement by
 # tests/test_gpu_checkpoint_full.py::test_full_checkpoint_mxfp8_prefill_gate)
 MXFP8_CHECKPOINT_GATE = {"cosine": 0.995, "top1": 0.75}
+MXFP8_CHECKPOINT_OK = False
 
 
 def preset(name: str, **overrides) -> LMConfig:
@@ -350,7 +358,7 @@ class LocalLM:
         if self.prefill_fp8 or self.decode_fp8:
             for i in range(c.layers):
                 for n in ("wqkv", "wo", "wgu", "wdown"):
-                    self.w8[f"l{i}.{n}"] = ops.quantize_weight(self.w[f"l{i}.{n}"])
+                    self.w8[f"l{i}.{n}"] = ops.quantize_weight(self._unfolded(i, n))
 
     KV_HEADROOM = 4 << 30  # bytes left free next to the slab (graphs, workspaces, prefill activations)
     # row counts from which the large-tile kernel takes over from the
@@ -414,6 +422,12 @@ class LocalLM:
         pairs = [("norm_f", "lm_head")]
         for i in range(c.layers):
             pairs += [(f"l{i}.ln1", f"l{i}.wqkv"), (f"l{i}.ln2", f"l{i}.wgu")]
+        if not hasattr(self, "norm_g"):
+            # the checkpoint's own norm weights: the MXFP8 paths normalise
+            # with them BEFORE quantising (a folded weight leaves a trained
+            # model's ~100x outlier channels undamped in the activation, and
+            # one outlier sets the E8M0 scale of its whole 32-element block)
+            self.norm_g: Dict[str, torch.Tensor] = {g_name: self.w[g_name] for g_name, _ in pairs}
         for g_name, w_name in pairs:
             g = self.w[g_name]
             if bool((g == 1).all()):
@@ -421,6 +435,21 @@ class LocalLM:
             w = self.w[w_name]
             self.w[w_name] = (w.float() * g.float()[None, :]).to(w.dtype).contiguous()
             self.w[g_name] = torch.ones_like(g)
+
+    def _g(self, name: str) -> torch.Tensor:
+        """The original (unfolded) RMSNorm weight ``name`` (MXFP8 paths)."""
+        return self.norm_g.get(name, self.w[name])
+
+    def _unfolded(self, i: int, n: str) -> torch.Tensor:
+        """Layer i's matrix ``n`` without its folded norm weight (the MXFP8
+        copies are quantised from it; their activations carry the norm)."""
+        w = self.w[f"l{i}.{n}"]
+        g_name = {"wqkv": f"l{i}.ln1", "wgu": f"l{i}.ln2"}.get(n)
+        g = self.norm_g.get(g_name) if g_name else None
+        if g is None or bool((g == 1).all()):
+            return w
+        gs = torch.where(g == 0, torch.ones_like(g), g).float()
+        return (w.float() / gs[None, :]).to(w.dtype).contiguous()
 
     @classmethod
     def load_safetensors(cls, path: str, device: str = "cuda", **cfg_overrides) -> "LocalLM":
@@ -436,10 +465,10 @@ class LocalLM:
                        intermediate=hf["intermediate_size"], rope_theta=hf.get("rope_theta", 10000.0),
                        eps=hf.get("rms_norm_eps", 1e-5))
         cfg = replace(cfg, **cfg_overrides)
-        if cfg.prefill_dtype == "auto":
+        if cfg.prefill_dtype == "auto" and not MXFP8_CHECKPOINT_OK:
             # a real checkpoint keeps bf16 prefill GEMMs unless fp8 is asked
-            # for by name: MXFP8 parity with bf16 is pinned on random-init
-            # weights only (docs/PARITY.md)
+            # for by name: the MXFP8 prefill fails MXFP8_CHECKPOINT_GATE on
+            # trained-like weights (docs/PARITY.md)
             cfg = replace(cfg, prefill_dtype="bf16")
         raw: Dict[str, torch.Tensor] = {}
         for fn in sorted(os.listdir(path)):
@@ -609,7 +638,7 @@ class LocalLM:
         c = self.cfg
         T = ids.numel()
         resid = ops.embedding(self.w["embed"], ids)
-        aq, as_ = ops.rmsnorm_mx(resid, self.w["l0.ln1"], c.eps)
+        aq, as_ = ops.rmsnorm_mx(resid, self._g("l0.ln1"), c.eps)
         act = None
         for i in range(c.layers):
             kc, vc = self.k_cache[i], self.v_cache[i]
@@ -617,11 +646,11 @@ class LocalLM:
             att = ops.prefill_attention_varlen(q, kc, vc, offsets, seq_slots, starts, prefix, shared, self.scale)
             ops.mx_quant(att.view(T, c.hidden), aq, as_)
             ops.pgemm_resid(aq, as_, *self.w8[f"l{i}.wo"], resid)
-            ops.rmsnorm_mx(resid, self.w[f"l{i}.ln2"], c.eps, q=aq, s=as_)
+            ops.rmsnorm_mx(resid, self._g(f"l{i}.ln2"), c.eps, q=aq, s=as_)
             act = ops.pgemm_swiglu(aq, as_, *self.w8[f"l{i}.wgu"], *(act or (None, None)))
             ops.pgemm_resid(act[0], act[1], *self.w8[f"l{i}.wdown"], resid)
             if i + 1 < c.layers:
-                ops.rmsnorm_mx(resid, self.w[f"l{i + 1}.ln1"], c.eps, q=aq, s=as_)
+                ops.rmsnorm_mx(resid, self._g(f"l{i + 1}.ln1"), c.eps, q=aq, s=as_)
         return ops.add_rmsnorm(resid.index_select(0, last), self.w["norm_f"], c.eps)
 
     @torch.inference_mode()
@@ -658,9 +687,11 @@ class LocalLM:
         c = self.cfg
         B = tokens.shape[0]
         chunk, splits = ops.decode_plan(B, c.n_kv_heads, c.max_seq, c.kv_dtype)
-        resid, h, seq_len = ops.decode_embed_norm(self.w["embed"], tokens, positions, self.w["l0.ln1"], c.eps,
+        fp8 = self.decode_fp8 and (self.device.type == "cpu" or B <= ops.WMX_MAX_ROWS)
+        resid, h, seq_len = ops.decode_embed_norm(self.w["embed"], tokens, positions,
+                                                  self._g("l0.ln1") if fp8 else self.w["l0.ln1"], c.eps,
                                                   src, last_ids, mask_idx, mask_alt, alt_token)
-        if self.decode_fp8 and (self.device.type == "cpu" or B <= ops.WMX_MAX_ROWS):
+        if fp8:
             return self._decode_trunk_fp8(B, resid, h, seq_len, slots, positions, chunk, splits, prefix_rows)
         wide = self.use_wgemm and B <= ops.WGEMM_MAX_ROWS
         big = self.use_tgemm and ops.WGEMM_MAX_ROWS < B <= ops.TGEMM_MAX_ROWS
@@ -708,7 +739,9 @@ class LocalLM:
         for i in range(c.layers):
             kc, vc = self.k_cache[i], self.v_cache[i]
             last = i + 1 == c.layers
-            nxt = self.w["norm_f"] if last else self.w[f"l{i + 1}.ln1"]
+            # MXFP8 activations carry the real norm weights; the last norm
+            # feeds the (norm-folded) bf16 LM head
+            nxt = self.w["norm_f"] if last else self._g(f"l{i + 1}.ln1")
             w8 = self.w8
             if gpu:
                 q = ops.wgemm_mx_rope_kv(xq, xs, *w8[f"l{i}.wqkv"], positions, slots, self.cos_sin, kc, vc,
@@ -720,14 +753,14 @@ class LocalLM:
                                        prefix=self._prefix(i, prefix_rows), splits=splits).view(B, c.hidden)
             aq, as_ = ops.mx_quant(att)
             if gpu:
-                xq, xs = ops.wgemm_mx_resid_norm(aq, as_, *w8[f"l{i}.wo"], resid, self.w[f"l{i}.ln2"], c.eps,
+                xq, xs = ops.wgemm_mx_resid_norm(aq, as_, *w8[f"l{i}.wo"], resid, self._g(f"l{i}.ln2"), c.eps,
                                                  self.wmx_ws)
                 gq, gs = ops.wgemm_mx_swiglu(xq, xs, *w8[f"l{i}.wgu"])
                 r = ops.wgemm_mx_resid_norm(gq, gs, *w8[f"l{i}.wdown"], resid, nxt, c.eps, self.wmx_ws,
                                             mx=not last)
             else:
                 ops.pgemm_resid(aq, as_, *w8[f"l{i}.wo"], resid)
-                xq, xs = ops.rmsnorm_mx(resid, self.w[f"l{i}.ln2"], c.eps)
+                xq, xs = ops.rmsnorm_mx(resid, self._g(f"l{i}.ln2"), c.eps)
                 gq, gs = ops.pgemm_swiglu(xq, xs, *w8[f"l{i}.wgu"])
                 ops.pgemm_resid(gq, gs, *w8[f"l{i}.wdown"], resid)
                 r = ops.add_rmsnorm(resid, nxt, c.eps) if last else ops.rmsnorm_mx(resid, nxt, c.eps)

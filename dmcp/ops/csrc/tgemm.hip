@@ -13,12 +13,15 @@
 // weight tile:
 //
 //   * a block owns 256 weight rows (SwiGLU: 128 gate + the 128 up rows of the
-//     same intermediate columns) x 64 MT activation rows (MT = 1..4), i.e. up
+//     same intermediate columns) x 32 XT activation rows (XT = 2..8), i.e. up
 //     to 256 x 256 outputs, over 8 waves (two per SIMD): 4 weight quarters x
-//     2 M halves, each 64 weight rows x 32 MT rows (4 A x 2 MT B fragments,
-//     32 MT accumulators) -- near-square wave tiles keep the LDS fragment
+//     2 M halves, each 64 weight rows x 16 XT rows (4 A x XT B fragments,
+//     16 XT accumulators) -- near-square wave tiles keep the LDS fragment
 //     reads (the CU's LDS array served ~90 % of its bandwidth to 128 x 32
-//     wave tiles' redundant reads) at (64 + 32 MT) rows per wave and k step;
+//     wave tiles' redundant reads) at (64 + 16 XT) rows per wave and k step.
+//     The X rows go in 32-row steps (round 6; 64 before): a 153-row M part
+//     stages 160 rows, and (256 + 160) x 128 B stages fit THREE in the LDS
+//     where 192 rows fit two -- one stage more in flight;
 //   * waves 4-7 (one per SIMD) also issue the block's LDS-DMA: an LDS-DMA
 //     instruction holds its wave's issue for ~60-185 cycles
 //     (MI355X_MICROARCH.md, cycle constants), and with one wave per SIMD doing
@@ -45,22 +48,30 @@ namespace {
 constexpr int TKC_DEFAULT = 64;
 // ring stages: as many stages as fit the CU's 160 KiB of LDS (capped at 6;
 // RES bytes reserved)
-template <int MT, int KC, int CAP = 6, int RES = 0>
+template <int XT, int KC, int CAP = 6, int RES = 0>
 constexpr int tstages() {
-    return (160 * 1024 - RES) / ((256 + 64 * MT) * KC * 2) < CAP ? (160 * 1024 - RES) / ((256 + 64 * MT) * KC * 2)
+    return (160 * 1024 - RES) / ((256 + 32 * XT) * KC * 2) < CAP ? (160 * 1024 - RES) / ((256 + 32 * XT) * KC * 2)
                                                                  : CAP;
 }
 
 // s_waitcnt vmcnt(n * GL) for a runtime n in [0, 5] (the count is an immediate)
+// (counts past the 6-bit field are never reached: n <= stages - 2, and a
+// ring of that many stages of GL pieces fits the counter; they compile to
+// the full wait)
+template <int K>
+__device__ __forceinline__ void wait_vm_k() {
+    if constexpr (K <= 63) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(K) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 template <int GL>
 __device__ __forceinline__ void wait_vm(int n) {
     switch (n) {
         case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(GL) : "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * GL) : "memory"); break;
-        case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * GL) : "memory"); break;
-        case 4: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 * GL) : "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(5 * GL) : "memory"); break;
+        case 1: wait_vm_k<GL>(); break;
+        case 2: wait_vm_k<2 * GL>(); break;
+        case 3: wait_vm_k<3 * GL>(); break;
+        case 4: wait_vm_k<4 * GL>(); break;
+        default: wait_vm_k<5 * GL>(); break;
     }
 }
 constexpr int TNB = 256;  // weight rows per block
@@ -101,7 +112,7 @@ __device__ __forceinline__ void wait_vm_rt(int n) {
 // stages), 2 = no fragment reads / MFMAs (the DMA ring alone)
 //
 // PF > 0: L2 prefetch of the weight stream PF stages ahead of the ring.  At
-// MT = 3-4 only two stages fit the LDS, so one 56-64 KB stage is in flight
+// XT = 6-8 only two stages fit the LDS, so one 56-64 KB stage is in flight
 // per CU and the ring runs at that stage's HBM latency (~31 KB/us per CU
 // measured on the LM head, half the L2-fed rate); a 4-byte LDS-DMA
 // (global_load_lds_dword: no register, a 256-B scratch slot of LDS) per
@@ -113,23 +124,23 @@ __device__ __forceinline__ void wait_vm_rt(int n) {
 // projections, +9-35 % on the LM head, worse with depth;
 // profiles/tgemm_l2_prefetch_ab_r5.jsonl): the refills are not waiting on
 // HBM latency.  Diagnostic only; production launches use PF = 0.
-template <int MT, int MODE, int PROBE = 0, int KC = TKC_DEFAULT, int CAP = 6, int PF = 0>
+template <int XT, int MODE, int PROBE = 0, int KC = TKC_DEFAULT, int CAP = 6, int PF = 0>
 __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) void tgemm_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, float* __restrict__ part,
     int M, int N, int K, int cps, int S, int ntiles, int mparts, int mrows, int I, const uint32_t* __restrict__ masks,
     const int32_t* __restrict__ midx, int n_masks, int wwords) {
     constexpr int NF = TNB / 64;       // A fragments per wave (16 weight rows each): a quarter of the tile's rows
-    constexpr int XT = 2 * MT;         // B fragments per wave (16 X rows each): half the tile's rows
     constexpr int RCH = KC / 8;        // 16-B chunks per image row
     constexpr int PR = 64 / RCH;       // image rows per 1-KiB LDS-DMA piece
-    constexpr int MR = 64 * MT;        // staged X rows
+    constexpr int MR = 32 * XT;        // staged X rows (XT B fragments of 16 rows per wave, 2 M halves)
     constexpr int WI = TNB / PR / 4;   // pieces per loader wave per stage: weights
     constexpr int XI = MR / PR / 4;    //                                   X rows
     constexpr int GL = WI + XI;        // LDS-DMA instructions per loader wave per stage
     constexpr int WCH = TNB * RCH;     // 16-B chunks of a stage's weight image
     constexpr int SCH = WCH + MR * RCH;  // ... plus the X image
     constexpr int PFB = PF > 0 ? 1024 : 0;  // prefetch scratch: 256 B per loader wave
-    constexpr int TST = tstages<MT, KC, CAP, PFB>();
+    constexpr int TST = tstages<XT, KC, CAP, PFB>();
+    static_assert(MR % (PR * 4) == 0, "X pieces per loader wave");
     static_assert(TST >= 2 && TST * SCH * 16 + PFB <= 160 * 1024, "LDS ring");
     __shared__ uint4 lds[TST * SCH + PFB / 16];   // ONE shared array (cdna_hip_programming.md §5 item 4a)
 
@@ -141,7 +152,7 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // DMA issue its SIMD partner keeps the matrix core busy
     const bool loader = wv >= 4;
     const int lw = wv & 3;                 // loader index
-    const int wn = wv & 3, wm = wv >> 2;   // weight quarter (64 rows) x M half (32 MT rows)
+    const int wn = wv & 3, wm = wv >> 2;   // weight quarter (64 rows) x M half (16 XT rows)
     const int l16 = lane & 15, g = lane >> 4;
     // block -> (weight tile nt, K slice s, M part mp): the M parts of one
     // (nt, s) unit share blockIdx % 8 (one XCD) and consecutive dispatch slots
@@ -223,8 +234,8 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int t = 0; t < XT; ++t) acc[f][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    // Per stage KC / 32 k steps of MT X fragments and NF weight fragments
-    // (this wave's 128 weight rows) and NF x MT MFMAs; the next k step's
+    // Per stage KC / 32 k steps of XT X fragments and NF weight fragments
+    // (this wave's 64 weight rows) and NF x XT MFMAs; the next k step's
     // reads are threaded between the current one's MFMAs (pinned: the
     // scheduler would sink each read to its use).
     constexpr int KS = KC / 32;
@@ -602,19 +613,35 @@ hipError_t launch_tgemm(const uint16_t* x, const uint16_t* w, uint16_t* y, float
                         int wwords) {
     const int ntiles = (MODE == TM_SWIGLU ? 2 * I : N) / TNB;
     const int mrows = (((M + mparts - 1) / mparts) + 15) & ~15;
-    const int mt = (mrows + 63) / 64;
+    // staged X rows in 32-row steps (>= 64); 32-deep stages (probes) in 64-row steps
+    int xt = (mrows + 31) / 32;
+    xt = xt < 2 ? 2 : xt;
+    if (KC == 32) xt = (xt + 1) & ~1;
     const int chunks = K / KC;
     const int cps = (chunks + S - 1) / S;
     const dim3 grid((unsigned)(ntiles * S * mparts));
-#define DMCP_TG(MT)                                                                                                 \
-    tgemm_kernel<MT, MODE, PROBE, KC, CAP, PF><<<grid, TTH, 0, st>>>(x, w, y, part, M, N, K, cps, S, ntiles, mparts, mrows, I, masks, \
+#define DMCP_TG(XT)                                                                                                 \
+    tgemm_kernel<XT, MODE, PROBE, KC, CAP, PF><<<grid, TTH, 0, st>>>(x, w, y, part, M, N, K, cps, S, ntiles, mparts, mrows, I, masks, \
                                                     midx, n_masks, wwords)
-    switch (mt) {
-        case 1: DMCP_TG(1); break;
-        case 2: DMCP_TG(2); break;
-        case 3: DMCP_TG(3); break;
-        case 4: DMCP_TG(4); break;
-        default: return hipErrorInvalidValue;
+    if constexpr (KC == 32) {
+        switch (xt) {
+            case 2: DMCP_TG(2); break;
+            case 4: DMCP_TG(4); break;
+            case 6: DMCP_TG(6); break;
+            case 8: DMCP_TG(8); break;
+            default: return hipErrorInvalidValue;
+        }
+    } else {
+        switch (xt) {
+            case 2: DMCP_TG(2); break;
+            case 3: DMCP_TG(3); break;
+            case 4: DMCP_TG(4); break;
+            case 5: DMCP_TG(5); break;
+            case 6: DMCP_TG(6); break;
+            case 7: DMCP_TG(7); break;
+            case 8: DMCP_TG(8); break;
+            default: return hipErrorInvalidValue;
+        }
     }
 #undef DMCP_TG
     return hipGetLastError();

@@ -1224,21 +1224,21 @@ def tgemm_plan(M: int, N: int, K: int, mode: str = "part", cus: int = 256) -> tu
     chunks = K // TGEMM_KC
     if mode == "argmax":  # measured best at 256-1,024 rows: the fewest parts
         return 1, -(-M // 256)
-    if mode == "swiglu":  # measured best: 3 parts up to ~520 rows, then 4 (64 x 4 = 256 blocks: one wave)
-        return 1, max(-(-M // 256), 3 if M <= 520 else 4)
+    if mode == "swiglu":  # measured best at 520-1,024 rows: 4 parts (64 x 4 = 256 blocks: one wave; 520 and 610
+        return 1, max(-(-M // 256), 4)  # rows then stage 144 / 160 rows: a 3-stage ring, profiles/tgemm_xt_sweep_r6.jsonl)
     best = None
-    for mparts in sorted({-(-M // r) for r in (256, 192, 128, 96, 64)}):
+    for mparts in sorted({-(-M // r) for r in (256, 192, 160, 128, 96, 64)}):
         rows = (-(-M // mparts) + 15) // 16 * 16
         if rows > 256:
             continue
-        mt = -(-rows // 64)
+        xt = max(2, -(-rows // 32))  # staged X rows: 32 xt (the kernel's 32-row steps)
         for S in ((1,) if mode != "part" else range(1, 17)):
             cps = -(-chunks // S)
             if S > chunks or (S - 1) * cps >= chunks:
                 continue
             blocks = tiles * mparts * S
-            mfma_us = 1.5 * cps * 2 * 8 * mt * 2 * 16 / 2100.0  # 2 waves x 8 x MT x 2 k steps of 16 cycles per SIMD
-            dma_us = cps * (TGEMM_NB + 64 * mt) * 2 * TGEMM_KC / 60e3
+            mfma_us = 1.5 * cps * 2 * 4 * xt * 2 * 16 / 2100.0  # 2 waves x 4 x XT x 2 k steps of 16 cycles per SIMD
+            dma_us = cps * (TGEMM_NB + 32 * xt) * 2 * TGEMM_KC / 60e3
             us = -(-blocks // cus) * max(mfma_us, dma_us) + 5.0
             if mode == "part":
                 us += S * M * N * 4 * 0.5e-6

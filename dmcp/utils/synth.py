@@ -435,3 +435,69 @@ def stack_trace_for(fqcns: List[str], frames: int = 20, seed: int = 11) -> List[
     out.append({"className": "org.springframework.web.servlet.DispatcherServlet", "methodName": "doDispatch",
                 "lineNumber": 1067})
     return out[:frames]
+
+
+def llama_checkpoint(root: str, layers: int = 16, hidden: int = 2048, heads: int = 32, kv_heads: int = 8,
+                     intermediate: int = 8192, vocab: int = 128256, tokenizer: str = "code-bpe-128k",
+                     outliers=(7, 300, 1029, 1800), seed: int = 11, device: str = "cuda") -> str:
+    """A Llama-format checkpoint directory (``config.json``, one
+    ``model.safetensors``, ``tokenizer.json``) with *trained-like* random
+    weights -- no download exists here: heavy-tailed matrices (a Gaussian
+    scale mixture with log-normal scales), RMSNorm weights around 1 with a
+    spread, and a few residual channels (``outliers``) carried at ~100x the
+    others and damped by small norm weights, as trained Llama checkpoints
+    show.  Llama-3.2-1B geometry by default (2.5 GB), the shipped 128,256-id
+    code BPE as its tokenizer.  The tensors are drawn on ``device``."""
+    import gzip
+    import json
+
+    import torch
+    from safetensors.torch import save_file
+    os.makedirs(root, exist_ok=True)
+    g = torch.Generator(device=device).manual_seed(seed)
+    hd = hidden // heads
+    out = [o for o in outliers if o < hidden]
+
+    def heavy(shape, std):
+        x = torch.randn(shape, generator=g, device=device)
+        x *= torch.exp(0.6 * torch.randn(shape, generator=g, device=device))
+        return (x * (std / 1.2)).to(torch.bfloat16).cpu()
+
+    def norm_w():
+        w = 1.0 + 0.25 * torch.randn(hidden, generator=g, device=device)
+        w[out] = 0.01
+        return w.to(torch.bfloat16).cpu()
+    emb = torch.randn(vocab, hidden, generator=g, device=device) * 0.02
+    emb[:, out] *= 100.0
+    t = {"model.embed_tokens.weight": emb.to(torch.bfloat16).cpu(), "lm_head.weight": heavy((vocab, hidden), 0.02),
+         "model.norm.weight": norm_w()}
+    del emb
+    out_std = 0.02 / (2 * layers) ** 0.5
+    for i in range(layers):
+        p = f"model.layers.{i}."
+        t[p + "input_layernorm.weight"] = norm_w()
+        t[p + "post_attention_layernorm.weight"] = norm_w()
+        t[p + "self_attn.q_proj.weight"] = heavy((heads * hd, hidden), 0.02)
+        t[p + "self_attn.k_proj.weight"] = heavy((kv_heads * hd, hidden), 0.02)
+        t[p + "self_attn.v_proj.weight"] = heavy((kv_heads * hd, hidden), 0.02)
+        t[p + "self_attn.o_proj.weight"] = heavy((hidden, heads * hd), out_std)
+        t[p + "mlp.gate_proj.weight"] = heavy((intermediate, hidden), 0.02)
+        t[p + "mlp.up_proj.weight"] = heavy((intermediate, hidden), 0.02)
+        t[p + "mlp.down_proj.weight"] = heavy((hidden, intermediate), out_std)
+    save_file(t, os.path.join(root, "model.safetensors"))
+    del t
+    cfg = {"vocab_size": vocab, "hidden_size": hidden, "num_hidden_layers": layers, "num_attention_heads": heads,
+           "num_key_value_heads": kv_heads, "intermediate_size": intermediate, "rms_norm_eps": 1e-5,
+           "rope_theta": 500000.0, "architectures": ["LlamaForCausalLM"]}
+    if tokenizer:
+        assets = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "models", "assets",
+                              tokenizer)
+        with gzip.open(os.path.join(assets, "tokenizer.json.gz"), "rb") as f, \
+                open(os.path.join(root, "tokenizer.json"), "wb") as o:
+            o.write(f.read())
+        with open(os.path.join(assets, "tokenizer_meta.json")) as f:
+            meta = json.load(f)
+        cfg["bos_token_id"], cfg["eos_token_id"] = meta.get("bos_token_id"), meta.get("eos_token_id")
+    with open(os.path.join(root, "config.json"), "w") as f:
+        json.dump(cfg, f)
+    return root

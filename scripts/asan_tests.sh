@@ -28,5 +28,5 @@ export DMCP_GRAMMAR_FUZZ_ITERS="${DMCP_GRAMMAR_FUZZ_ITERS:-6000}"
 LD_PRELOAD="$LIBASAN $LIBSTDCXX" python -m pytest -q -p no:cacheprovider -m "not gpu" --timeout 3600 \
     tests/test_grammar_fuzz.py tests/test_fuzz.py tests/test_parser_java.py tests/test_parser_ts.py \
     tests/test_parser_go.py tests/test_ref_java_parser.py tests/test_ref_ts_parser.py tests/test_ref_ts_engine.py \
-    tests/test_ref_go.py tests/test_source.py tests/test_pipeline.py tests/test_sync.py \
+    tests/test_ref_go.py tests/test_source.py tests/test_pipeline.py tests/test_sync.py tests/test_scan_child.py \
     "tests/test_local_engine.py::test_capped_string_closes_at_a_word_boundary" "$@"

@@ -114,6 +114,36 @@ for s in $STEPS; do
                 --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 60 ;;
         ckpt_test) run ckpt_test 900 python -u -m pytest tests/test_gpu_checkpoint_full.py -x -v -s --timeout 900 \
                 --timeout-method thread ;;
+        tgemm_test) run tgemm_test 600 python -u -m pytest tests/test_gpu_tgemm.py -x -q --timeout 120 \
+                --timeout-method thread ;;
+        tgemm_sweep) run tgemm_sweep 900 python scripts/bench_tgemm.py --rows 520 610 768 1024 --only gu,head --sweep ;;
+        step_small)  # small-row latency (verdict item 5): 40 / 80 / 160 rows
+            for r in "32 8" "64 16" "128 32"; do set -- $r
+                run step_llama$(($1 + $2)) 300 python scripts/bench_step.py --preset llama3.2-1b-code --batch $1 \
+                    --extra $2 --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 100
+            done ;;
+        prof_step80)
+            ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$ROOT/$OUT/prof_step80" -o step -- python3 "$ROOT/scripts/bench_step.py" \
+                --preset llama3.2-1b-code --batch 64 --extra 16 --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 60 \
+                > "$ROOT/$OUT/prof_step80.log" 2>&1 )
+            rc=$?
+            echo "=== prof_step80 rc=$rc"
+            find "$OUT/prof_step80" -type f ! -name '*kernel_stats*' -delete 2>/dev/null
+            cp $(find "$OUT/prof_step80" -name '*kernel_stats.csv' | head -1) "$OUT/step80_kernel_stats.csv"
+            [ $rc -eq 0 ] || exit $rc ;;
+        ckpt_enrich)  # a written 16-layer, 128,256-id checkpoint through the engine, + its kernel trace
+            run ckpt_enrich 900 python bench_enrich.py --checkpoint /tmp/dmcp_ckpt --write-checkpoint --classes 1024
+            ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$ROOT/$OUT/prof_ckpt" -o enrich -- python3 "$ROOT/bench_enrich.py" --checkpoint /tmp/dmcp_ckpt \
+                --classes 512 --warmup 4 > "$ROOT/$OUT/prof_ckpt.log" 2>&1 )
+            rc=$?
+            echo "=== prof_ckpt rc=$rc"
+            find "$OUT/prof_ckpt" -type f ! -name '*kernel_stats*' -delete 2>/dev/null
+            cp $(find "$OUT/prof_ckpt" -name '*kernel_stats.csv' | head -1) "$OUT/ckpt_kernel_stats.csv"
+            python3 scripts/kstats.py "$OUT/ckpt_kernel_stats.csv" > "$OUT/kstats_ckpt.txt" 2>&1
+            head -30 "$OUT/kstats_ckpt.txt"
+            [ $rc -eq 0 ] || exit $rc ;;
         step_llama3)  # the verdict's three operating points: 320 / 610 / 768 rows
             for r in "256 64" "512 98" "512 256"; do set -- $r
                 run step_llama$(($1 + $2)) 300 python scripts/bench_step.py --preset llama3.2-1b-code --batch $1 \

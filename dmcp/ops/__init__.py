@@ -28,60 +28,40 @@ def _on(t):
     return hip if t.is_cuda else reference
 
 
-# ops with an fp32 CPU reference: the first tensor's device picks the kernel
-def add_rmsnorm(x, weight, eps, residual=None, out=None):
-    return _on(x).add_rmsnorm(x, weight, eps, residual, out)
+def _by_device(name: str):
+    """``name`` dispatched on its first tensor argument's device: the gfx950
+    kernel (:mod:`.hip`) for GPU tensors, the fp32 reference for CPU ones.
+    Both modules implement these ops with the same signature
+    (tests/test_launch_plans.py::test_device_ops_share_one_signature); the
+    GPU kernel's docstring is the op's."""
+    k, r = getattr(hip, name), getattr(reference, name)
+
+    def op(first, *args, **kw):
+        return (k if first.is_cuda else r)(first, *args, **kw)
+    op.__name__ = op.__qualname__ = name
+    op.__doc__ = k.__doc__ or r.__doc__
+    op.__wrapped__ = k  # inspect.signature reports the kernel's parameters
+    return op
 
 
-def rope_kv(qkv, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out=None):
-    return _on(qkv).rope_kv(qkv, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out)
+# ops with an fp32 CPU reference: norms, RoPE + KV append, prefill attention,
+# SwiGLU, selection, embedding, the decode step's input gather + first norm,
+# and the MXFP8 prefill path (csrc/pgemm.hip)
+DEVICE_OPS = ("add_rmsnorm", "rope_kv", "prefill_attention", "prefill_attention_varlen", "silu_mul",
+              "masked_argmax", "lm_head_argmax", "embedding", "decode_embed_norm", "mx_quant", "rmsnorm_mx",
+              "pgemm", "pgemm_resid", "pgemm_swiglu", "pgemm_qkv")
+for _name in DEVICE_OPS:
+    globals()[_name] = _by_device(_name)
+del _name
 
 
 def decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace=None, chunk: int = 256, out=None,
                      prefix=None, splits=None, fork=None):
+    """Per-row decode attention; the CPU reference takes no split count."""
     if q.is_cuda:
         return hip.decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace, chunk, out, prefix, splits,
                                     fork)
     return reference.decode_attention(q, k_cache, v_cache, slot, seq_len, scale, workspace, chunk, out, prefix, fork)
-
-
-def prefill_attention(q, k_cache, v_cache, slot, start, prefix_slot=None, prefix_len=0, scale=1.0, out=None,
-                      variant=0, nsplit=0):
-    """Causal prefill/extend attention of one sequence, shared prefix read in place."""
-    return _on(q).prefill_attention(q, k_cache, v_cache, slot, start, prefix_slot, prefix_len, scale, out, variant,
-                                    nsplit)
-
-
-def prefill_attention_varlen(q, k_cache, v_cache, offsets, slots, starts, prefix_slot=None, prefix_lens=None,
-                             scale=1.0, out=None):
-    return _on(q).prefill_attention_varlen(q, k_cache, v_cache, offsets, slots, starts, prefix_slot, prefix_lens,
-                                           scale, out)
-
-
-def silu_mul(gate_up, out=None):
-    return _on(gate_up).silu_mul(gate_up, out)
-
-
-def masked_argmax(logits, mask=None, vocab=None, out=None, mask_idx=None):
-    return _on(logits).masked_argmax(logits, mask, vocab, out, mask_idx)
-
-
-def lm_head_argmax(x, w, masks, mask_idx, out=None, workspace=None):
-    """Grammar-masked greedy ids of the LM head (the logits never exist on the GPU path)."""
-    return _on(x).lm_head_argmax(x, w, masks, mask_idx, out, workspace)
-
-
-def embedding(table, ids, out=None):
-    return _on(table).embedding(table, ids, out)
-
-
-def decode_embed_norm(table, tokens, positions, weight, eps, src=None, last_ids=None, mask_idx=None, mask_alt=None,
-                      alt_token: int = -1):
-    """(resid, h, seq_len) of a decode step: each row's token (``last_ids[src]``
-    where ``src >= 0``), its embedding, its first RMSNorm, its length; a
-    gathered ``alt_token`` switches that row's grammar mask to ``mask_alt``."""
-    return _on(table).decode_embed_norm(table, tokens, positions, weight, eps, src, last_ids, mask_idx, mask_alt,
-                                        alt_token)
 
 
 # GPU-only fused GEMM with a shape-dependent default
@@ -97,28 +77,3 @@ def decode_plan(rows, n_kv_heads, max_seq, kv_dtype: str = "bf16"):
     -> 2.30 ms at 78 rows, 5.54 -> 5.36 at 320; bf16 2.84 vs 2.94 the other
     way -- profiles/decode_target_waves_r2.txt)."""
     return hip.decode_plan(rows, n_kv_heads, max_seq, target_waves=2048 if kv_dtype == "fp8" else 4096)
-
-
-# MXFP8 prefill path (csrc/pgemm.hip); CPU tensors run the fp32 references
-def mx_quant(x, q=None, s=None):
-    return _on(x).mx_quant(x, q, s)
-
-
-def rmsnorm_mx(resid, weight, eps, add=None, q=None, s=None):
-    return _on(resid).rmsnorm_mx(resid, weight, eps, add, q, s)
-
-
-def pgemm(aq, as_, wq, ws, out=None):
-    return _on(aq).pgemm(aq, as_, wq, ws, out)
-
-
-def pgemm_resid(aq, as_, wq, ws, resid):
-    return _on(aq).pgemm_resid(aq, as_, wq, ws, resid)
-
-
-def pgemm_swiglu(aq, as_, wq, ws, q=None, s=None):
-    return _on(aq).pgemm_swiglu(aq, as_, wq, ws, q, s)
-
-
-def pgemm_qkv(aq, as_, wq, ws, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out=None):
-    return _on(aq).pgemm_qkv(aq, as_, wq, ws, pos, slot, cos_sin, k_cache, v_cache, n_q_heads, q_out)

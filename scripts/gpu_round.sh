@@ -116,6 +116,7 @@ for s in $STEPS; do
                 --timeout-method thread ;;
         tgemm_test) run tgemm_test 600 python -u -m pytest tests/test_gpu_tgemm.py -x -q --timeout 120 \
                 --timeout-method thread ;;
+        tgemm_small) run tgemm_small 900 python scripts/bench_tgemm.py --rows 40 80 160 320 --only qkv,o,gu,down,head ;;
         tgemm_sweep) run tgemm_sweep 900 python scripts/bench_tgemm.py --rows 520 610 768 1024 --only gu,head --sweep ;;
         step_small)  # small-row latency (verdict item 5): 40 / 80 / 160 rows
             for r in "32 8" "64 16" "128 32"; do set -- $r

@@ -60,3 +60,17 @@ def test_tgemm_model_and_op_predicates_agree(inter, hidden):
     model_ok = tgemm_shapes_ok(c)
     assert model_ok == (ops_ok and c.qkv_dim <= 8192 and c.hidden <= 8192)
 
+
+
+def test_device_ops_share_one_signature():
+    """Every op dispatched by device (dmcp.ops.DEVICE_OPS) has the same
+    parameters in the kernel bindings and the fp32 references, so a call
+    means the same on either device."""
+    import inspect
+    from dmcp import ops
+    from dmcp.ops import reference
+    for name in ops.DEVICE_OPS:
+        k = list(inspect.signature(getattr(hip, name)).parameters)
+        r = list(inspect.signature(getattr(reference, name)).parameters)
+        assert k == r, name
+        assert list(inspect.signature(getattr(ops, name)).parameters) == k, name

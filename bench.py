@@ -429,8 +429,9 @@ def main(argv=None) -> int:
                 extra["remotePath"] = {"error": repr(e)[:300]}
         # agreed by every rank: a rank without a worker skips the collective path for all
         names = [p.strip() for p in args.enrich_local_presets.split(",") if p.strip()]
+        have = sum(1 for n in names if n in pools)  # the per-rank preset workers (not rank 0's pool)
         if args.enrich == "none" and args.enrich_local_classes > 0 and \
-                ctx.sum(1.0 if len(pools) == len(names) else 0.0)[0] == world:
+                ctx.sum(1.0 if have == len(names) else 0.0)[0] == world:
             for name in names:
                 key = EXTRA_KEYS.get(name, "enrichLocal_" + name)
                 try:

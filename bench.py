@@ -186,6 +186,7 @@ def _enrich_local(pool, args, ctx, work, rank):
             synth.java_spring_repo(srepo, n_classes=args.small_project_classes, base_package=f"co.acme.sml{rank}",
                                    seed=rank + 301)
             ctx.barrier()
+            st0 = dict(be.stats())
             t1 = time.perf_counter()
             try:
                 rs = app.indexer.analyze_project(srepo)
@@ -194,9 +195,19 @@ def _enrich_local(pool, args, ctx, work, rank):
             smx = ctx.max(time.perf_counter() - t1)[0]
             if ctx.sum(1.0 if rs is None else 0.0)[0] == 0:
                 ph2 = ctx.max(rs.stats.get("analyze.phase2", 0.0) / 1e3)[0]
+                d = {k: v - st0.get(k, 0) for k, v in be.stats().items() if isinstance(v, (int, float))}
+                ss = max(1.0, d.get("decode_steps", 0))
+                # where a latency-bound run's time goes: steps x step time vs prefill and host
                 small = {"classes": rs.classes_analyzed, "enriched": int(rs.stats.get("enriched", 0)),
                          "elapsedS": round(smx, 3), "phase2S": round(ph2, 3),
-                         "classesPerSec": round(rs.classes_analyzed / smx, 2)}
+                         "classesPerSec": round(rs.classes_analyzed / smx, 2),
+                         "decodeSteps": int(d.get("decode_steps", 0)),
+                         "rowsPerStep": round(d.get("decode_rows", 0) / ss, 1),
+                         "decodeStepMs": round(1e3 * d.get("decode_s", 0) / ss, 3),
+                         "decodeS": round(d.get("decode_s", 0), 3),
+                         "prefillGpuS": round(d.get("prefill_gpu_s", 0), 3),
+                         "generatedTokensPerClass": round(d.get("generated_tokens", 0) / max(1, rs.classes_analyzed),
+                                                          1)}
             else:
                 small = {"error": repr(err)[:300]}
         wit = (pool.workers[0].info or {}).get("witness") if pool.workers else None

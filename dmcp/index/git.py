@@ -105,7 +105,7 @@ class GitClient:
         """The branch head as a :class:`~dmcp.index.source.SourceTree` without a
         working-tree checkout (bare clone + ``cat-file --batch``); falls back to
         a checkout when the candidate sources exceed ``max_bytes``."""
-        from .source import CheckoutTree, MemoryTree, list_tree, read_blobs, wanted
+        from .source import CheckoutTree, MemoryTree, list_tree, native_commit_tree, read_blobs, wanted
         local = url.local_path()
         if local is not None and self.read_local_in_place:
             return self._local_snapshot(url, os.path.abspath(local), branch, shallow, max_bytes)
@@ -125,8 +125,16 @@ class GitClient:
         LOG.info("Fetching %s (branch: %s) into %s", url, branch, dest)
         try:
             self._git(args)
-            commit = self.head(dest)
-            entries = [e for e in list_tree(self, dest, commit) if wanted(e[0])]
+            # the clone's refs + tree read natively when its objects are loose
+            # (a --shared local clone: alternates into a loose store) -- two
+            # git processes fewer; a packed clone falls back to git
+            fast = native_commit_tree(dest, self.branch_refs(branch)) if self.native_objects else None
+            if fast is not None:
+                commit, listing = fast
+            else:
+                commit = self.head(dest)
+                listing = list_tree(self, dest, commit)
+            entries = [e for e in listing if wanted(e[0])]
             blobs = read_blobs(self, dest, [e[1] for e in entries], max_bytes)
             if blobs is None:
                 LOG.info("%s: sources exceed the %d MiB in-memory limit, using a checkout", url, max_bytes >> 20)

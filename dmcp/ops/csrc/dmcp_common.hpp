@@ -134,4 +134,64 @@ __device__ __forceinline__ const void* kv_ptr(const void* base, size_t off) {
     return static_cast<const uint8_t*>(base) + off * (KV8 ? 1 : 2);
 }
 
+// h[0..7] += sum over split-K slices s < S of part[(s * M + m) * N + 8 idx ..
+// + 7] (fp32 partials), RSU slices' loads in flight at once: a plain loop
+// over s waited for each slice before issuing the next (S serial round trips
+// per reduction).  Branch-free (a guarded add let the loads sink to their
+// uses); the clamped surplus loads repeat the last slice with weight 0.
+template <int RSU = 4>
+__device__ __forceinline__ void sum_slices8(const float* __restrict__ part, int S, int M, int m, int N, int idx,
+                                            float (&h)[8]) {
+    for (int s0 = 0; s0 < S; s0 += RSU) {
+        float4 a[RSU], b[RSU];
+#pragma unroll
+        for (int j = 0; j < RSU; ++j) {
+            const float4* pp = reinterpret_cast<const float4*>(part + ((size_t)min(s0 + j, S - 1) * M + m) * N);
+            a[j] = pp[2 * idx];
+            b[j] = pp[2 * idx + 1];
+        }
+#pragma unroll
+        for (int j = 0; j < RSU; ++j) {
+            const float u = s0 + j < S ? 1.f : 0.f;
+            h[0] = fmaf(u, a[j].x, h[0]); h[1] = fmaf(u, a[j].y, h[1]);
+            h[2] = fmaf(u, a[j].z, h[2]); h[3] = fmaf(u, a[j].w, h[3]);
+            h[4] = fmaf(u, b[j].x, h[4]); h[5] = fmaf(u, b[j].y, h[5]);
+            h[6] = fmaf(u, b[j].z, h[6]); h[7] = fmaf(u, b[j].w, h[7]);
+        }
+    }
+}
+
+// The LM head's per-row selection from per-tile (max, id) pairs (wgemm.hip /
+// tgemm.hip MODE_ARGMAX write best[tile * M + row]): the highest value, the
+// lowest id among ties; 0 when the mask allowed nothing (as masked_argmax).
+// One wave per row; each lane keeps 8 pairs' loads in flight (a plain
+// strided loop waited for every load: ~30 serial round trips per row at
+// 128,256 ids).  A clamped duplicate of the last pair never changes the result.
+__global__ __launch_bounds__(kBlock) void argmax_pairs_kernel(const float2* __restrict__ best, int ntiles, int M,
+                                                              int32_t* __restrict__ ids) {
+    constexpr int U = 8;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int m = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
+    if (m >= M) return;
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int t0 = lane; t0 < ntiles; t0 += U * kWave) {
+        float2 p[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) p[j] = best[(size_t)min(t0 + j * kWave, ntiles - 1) * M + m];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int pi = __float_as_int(p[j].y);
+            if (p[j].x > bv || (p[j].x == bv && pi < bi)) { bv = p[j].x; bi = pi; }
+        }
+    }
+#pragma unroll
+    for (int msk = 32; msk >= 1; msk >>= 1) {
+        const float ob = __shfl_xor(bv, msk, kWave);
+        const int oi = __shfl_xor(bi, msk, kWave);
+        if (ob > bv || (ob == bv && oi < bi)) { bv = ob; bi = oi; }
+    }
+    if (lane == 0) ids[m] = bi == 0x7fffffff ? 0 : bi;
+}
+
 }  // namespace

@@ -953,12 +953,7 @@ __global__ __launch_bounds__(kBlock) void reduce_resid_norm_mx_kernel(const floa
     for (int i = 0; i < VPT; ++i) {
         const int idx = threadIdx.x + i * kBlock;
         float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        for (int sl = 0; sl < S; ++sl) {
-            const float4* pp = reinterpret_cast<const float4*>(part + ((size_t)sl * M + m) * N);
-            const float4 a = pp[2 * idx], b = pp[2 * idx + 1];
-            acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
-            acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
-        }
+        sum_slices8(part, S, M, m, N, idx, acc);
         float y[8], r[8];
         unpack8(pack8(acc), y);  // the GEMM output rounded to bf16, as F.linear's
         unpack8(rr[idx], r);

@@ -584,29 +584,6 @@ __global__ __launch_bounds__(TTH) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
 }
 
-// per row: the (max, id) pairs of every 64-id vocabulary quarter tile -> the selected
-// id (0 when the mask allows nothing, as masked_argmax); one wave per row
-__global__ __launch_bounds__(kBlock) void tgemm_argmax_reduce_kernel(const float2* __restrict__ best, int ntiles,
-                                                                     int M, int32_t* __restrict__ ids) {
-    const int lane = threadIdx.x & (kWave - 1);
-    const int m = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
-    if (m >= M) return;
-    float bv = -INFINITY;
-    int bi = 0x7fffffff;
-    for (int t = lane; t < ntiles; t += kWave) {
-        const float2 p = best[(size_t)t * M + m];
-        const int pi = __float_as_int(p.y);
-        if (p.x > bv || (p.x == bv && pi < bi)) { bv = p.x; bi = pi; }
-    }
-#pragma unroll
-    for (int msk = 32; msk >= 1; msk >>= 1) {
-        const float ob = __shfl_xor(bv, msk, kWave);
-        const int oi = __shfl_xor(bi, msk, kWave);
-        if (ob > bv || (ob == bv && oi < bi)) { bv = ob; bi = oi; }
-    }
-    if (lane == 0) ids[m] = bi == 0x7fffffff ? 0 : bi;
-}
-
 template <int MODE, int PROBE = 0, int KC = TKC_DEFAULT, int CAP = 6, int PF = 0>
 hipError_t launch_tgemm(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int M, int N, int K, int S,
                         int mparts, int I, hipStream_t st, const uint32_t* masks, const int32_t* midx, int n_masks,
@@ -708,7 +685,7 @@ int dmcp_tgemm(const void* x, const void* w, void* y, void* part, int M, int N, 
             hipError_t e = launch_tgemm<TM_ARGMAX>(xx, ww, nullptr, pp, M, N, K, 1, mparts, 0, st, mk, mi, n_masks,
                                                    wwords);
             if (e != hipSuccess) return e;
-            tgemm_argmax_reduce_kernel<<<(M + kBlock / kWave - 1) / (kBlock / kWave), kBlock, 0, st>>>(
+            argmax_pairs_kernel<<<(M + kBlock / kWave - 1) / (kBlock / kWave), kBlock, 0, st>>>(
                 (const float2*)part, 4 * (N / TNB), M, (int32_t*)ids);
             return hipGetLastError();
         }

@@ -294,6 +294,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     }
 }
 
+// split-K slices whose partials the reductions below load at once
+constexpr int RSU = 4;
+
 // split-K reduction + residual add + RMSNorm of the next op (one block per
 // row): resid += bf16(sum_s part[s]); out = RMSNorm(resid) * gw.  The GEMM
 // output is rounded to bf16 before the add and the stream after it (what
@@ -320,15 +323,29 @@ __global__ __launch_bounds__(kBlock) void reduce_resid_norm_kernel(const float* 
 #pragma unroll
         for (int j = 0; j < 8; ++j) h[i][j] = 0.f;
     }
-    for (int s = 0; s < S; ++s) {
-        const float4* pp = reinterpret_cast<const float4*>(part + ((size_t)s * M + m) * N);
+    // the partials of RSU slices in flight at once (a plain loop over s waited
+    // for each slice's loads before issuing the next: S serial round trips)
+    for (int s0 = 0; s0 < S; s0 += RSU) {
+        float4 a[RSU][VPT], b[RSU][VPT];
 #pragma unroll
-        for (int i = 0; i < VPT; ++i) {
-            const int idx = threadIdx.x + i * kBlock;
-            if (idx < nvec) {
-                const float4 a = pp[2 * idx], b = pp[2 * idx + 1];
-                h[i][0] += a.x; h[i][1] += a.y; h[i][2] += a.z; h[i][3] += a.w;
-                h[i][4] += b.x; h[i][5] += b.y; h[i][6] += b.z; h[i][7] += b.w;
+        for (int j = 0; j < RSU; ++j) {
+            const float4* pp = reinterpret_cast<const float4*>(part + ((size_t)min(s0 + j, S - 1) * M + m) * N);
+#pragma unroll
+            for (int i = 0; i < VPT; ++i) {
+                const int idx = min(threadIdx.x + i * kBlock, nvec - 1);
+                a[j][i] = pp[2 * idx];
+                b[j][i] = pp[2 * idx + 1];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < RSU; ++j) {
+            const float u = s0 + j < S ? 1.f : 0.f;  // branch-free: a branch let the loads sink to their uses
+#pragma unroll
+            for (int i = 0; i < VPT; ++i) {
+                h[i][0] = fmaf(u, a[j][i].x, h[i][0]); h[i][1] = fmaf(u, a[j][i].y, h[i][1]);
+                h[i][2] = fmaf(u, a[j][i].z, h[i][2]); h[i][3] = fmaf(u, a[j][i].w, h[i][3]);
+                h[i][4] = fmaf(u, b[j][i].x, h[i][4]); h[i][5] = fmaf(u, b[j][i].y, h[i][5]);
+                h[i][6] = fmaf(u, b[j][i].z, h[i][6]); h[i][7] = fmaf(u, b[j][i].w, h[i][7]);
             }
         }
     }
@@ -386,12 +403,7 @@ __global__ __launch_bounds__(kBlock) void reduce_rope_kv_kernel(
     const int nvec = N >> 3;
     for (int idx = threadIdx.x; idx < nvec; idx += kBlock) {
         float h[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        for (int s = 0; s < S; ++s) {
-            const float4* pp = reinterpret_cast<const float4*>(part + ((size_t)s * M + t) * N);
-            const float4 a = pp[2 * idx], b = pp[2 * idx + 1];
-            h[0] += a.x; h[1] += a.y; h[2] += a.z; h[3] += a.w;
-            h[4] += b.x; h[5] += b.y; h[6] += b.z; h[7] += b.w;
-        }
+        sum_slices8(part, S, M, t, N, idx, h);
         rowbuf[idx] = pack8(h);
     }
     __syncthreads();
@@ -447,29 +459,6 @@ __global__ __launch_bounds__(kBlock) void reduce_rope_kv_kernel(
         else
             *reinterpret_cast<uint4*>(static_cast<uint16_t*>(v_cache) + vofs) = vsrc[uu];
     }
-}
-
-// per row: the (max, id) pairs of every vocabulary tile -> the selected id
-// (0 when the mask allows nothing, as masked_argmax); one wave per row
-__global__ __launch_bounds__(kBlock) void lm_head_reduce_kernel(const float2* __restrict__ best, int ntiles, int M,
-                                                                int32_t* __restrict__ ids) {
-    const int lane = threadIdx.x & (kWave - 1);
-    const int m = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
-    if (m >= M) return;
-    float bv = -INFINITY;
-    int bi = 0x7fffffff;
-    for (int t = lane; t < ntiles; t += kWave) {
-        const float2 p = best[(size_t)t * M + m];
-        const int pi = __float_as_int(p.y);
-        if (p.x > bv || (p.x == bv && pi < bi)) { bv = p.x; bi = pi; }
-    }
-#pragma unroll
-    for (int msk = 32; msk >= 1; msk >>= 1) {
-        const float ob = __shfl_xor(bv, msk, kWave);
-        const int oi = __shfl_xor(bi, msk, kWave);
-        if (ob > bv || (ob == bv && oi < bi)) { bv = ob; bi = oi; }
-    }
-    if (lane == 0) ids[m] = bi == 0x7fffffff ? 0 : bi;
 }
 
 constexpr int kStages = 3;  // LDS ring stages (2 in flight while one is computed)
@@ -582,7 +571,7 @@ int dmcp_lm_head_argmax(const void* x, const void* w, const void* masks, const v
         e = launch_wgemm<64, MODE_ARGMAX>(xx, ww, nullptr, bb, M, V, K, 1, mparts, 0, st, mk, mi, n_masks, wwords);
     }
     if (e != hipSuccess) return e;
-    lm_head_reduce_kernel<<<(M + kBlock / kWave - 1) / (kBlock / kWave), kBlock, 0, st>>>(
+    argmax_pairs_kernel<<<(M + kBlock / kWave - 1) / (kBlock / kWave), kBlock, 0, st>>>(
         (const float2*)best, ntiles, M, (int32_t*)ids);
     return hipGetLastError();
 }

@@ -26,7 +26,7 @@ _lock = threading.Lock()
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _f = ctypes.c_float
-ABI_VERSION = 16  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
+ABI_VERSION = 17  # must match dmcp_abi_version() in csrc/dmcp_kernels.hip
 
 
 class HipOpsError(RuntimeError):
@@ -282,7 +282,8 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
         if tuple(pk.shape) != (Hkv, MAXS, D) or tuple(pv.shape) != (Hkv, MAXS, D) or plen.numel() != 1:
             raise HipOpsError(f"decode_attention: prefix k {tuple(pk.shape)} / v {tuple(pv.shape)} do not match "
                               f"kv {tuple(k_cache.shape)}")
-        ps_max = prefix_mfma_splits(B, Hq // Hkv, Hkv)
+        # small steps read the prefix inline (ps_max 0): see prefix_inline_rows
+        ps_max = 0 if B <= prefix_inline_rows() else prefix_mfma_splits(B, Hq // Hkv, Hkv)
         prows = getattr(prefix, "rows", None)
         if prows is not None:
             _req(prows, torch.int32, "decode_attention.prefix.rows")
@@ -441,6 +442,18 @@ def prefix_mfma_splits(rows: int, G: int, Hkv: int, target_blocks: int = 640) ->
         return max(1, min(PREFIX_MFMA_MAX_SPLITS, int(env)))
     tiles = -(-rows * G // 128) * Hkv
     return max(1, min(PREFIX_MFMA_MAX_SPLITS, round(target_blocks / max(1, tiles))))
+
+
+# Steps of at most this many rows read the shared prefix inside the per-row
+# attention kernel (the prefix slot as the first key segment of every row)
+# instead of the MFMA prefix kernel + its partials + the combine pass
+PREFIX_INLINE_ROWS = 0
+
+
+def prefix_inline_rows() -> int:
+    """:data:`PREFIX_INLINE_ROWS`; ``DMCP_PREFIX_INLINE_ROWS`` overrides."""
+    env = os.environ.get("DMCP_PREFIX_INLINE_ROWS")
+    return int(env) if env else PREFIX_INLINE_ROWS
 
 
 def decode_workspace(rows: int, Hq: int, Hkv: int, D: int, max_seq: int, device, chunk: int = 256,

@@ -72,6 +72,19 @@ for s in $STEPS; do
                 > "$OUT/kstats_byte.txt" 2>&1
             head -30 "$OUT/kstats_byte.txt"
             [ $rc -eq 0 ] || exit $rc ;;
+        gaps_llama)  # GPU idle inside the timed engine run (verdict item 8): busy fraction + largest gaps
+            ( cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv \
+                -d "$ROOT/$OUT/gaps_llama" -o enrich -- python3 "$ROOT/bench_enrich.py" --preset llama3.2-1b-code \
+                --classes 512 --warmup 4 > "$ROOT/$OUT/gaps_llama.log" 2>&1 )
+            rc=$?
+            echo "=== gaps_llama rc=$rc"
+            [ $rc -eq 0 ] || exit $rc
+            el=$(python3 -c "import json,sys; print([json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]['elapsed_s'])" \
+                "$OUT/gaps_llama.log")
+            python3 scripts/kernel_gaps.py $(find "$OUT/gaps_llama" -name '*kernel_trace.csv' | head -1) "$el" \
+                > "$OUT/gaps_llama.txt" 2>&1
+            find "$OUT/gaps_llama" -type f -delete 2>/dev/null
+            cat "$OUT/gaps_llama.txt" ;;
         prefill) run prefill 300 python scripts/bench_prefill.py --seqs 12 ;;
         pgemm_test) run pgemm_test 300 python -u -m pytest tests/test_gpu_pgemm.py -x -v --timeout 120 \
                 --timeout-method thread ;;
@@ -123,6 +136,16 @@ for s in $STEPS; do
                 run step_llama$(($1 + $2)) 300 python scripts/bench_step.py --preset llama3.2-1b-code --batch $1 \
                     --extra $2 --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 100
             done ;;
+        kern_tests) run kern_tests 900 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_wgemm.py \
+                tests/test_gpu_tgemm.py tests/test_gpu_pgemm.py -x -q --timeout 120 --timeout-method thread ;;
+        inline_test) run inline_test 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 \
+                --timeout-method thread -k "inline_prefix or shared_prefix or fork_table or off_the_prefix" ;;
+        inline_ab)  # the shared prefix read inline by the per-row kernel vs the prefix kernel, alternating
+            for rep in 1 2; do for il in 0 4096; do for r in "32 8" "64 16" "128 32" "256 64"; do set -- $r
+                DMCP_PREFIX_INLINE_ROWS=$il run inline_ab_${il}_$(($1 + $2))_$rep 300 python scripts/bench_step.py \
+                    --preset llama3.2-1b-code --batch $1 --extra $2 --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 100
+            done; done; done
+            grep -h '^{' "$OUT"/inline_ab_*.log > "$OUT/inline_ab.jsonl" ;;
         prof_step80)
             ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d "$ROOT/$OUT/prof_step80" -o step -- python3 "$ROOT/scripts/bench_step.py" \

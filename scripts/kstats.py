@@ -8,9 +8,9 @@ import csv
 import re
 import sys
 
-CATS = [("tgemm_head", re.compile(r"tgemm_kernel<\d+, 3|tgemm_argmax_reduce")),
+CATS = [("tgemm_head", re.compile(r"tgemm_kernel<\d+, 3|tgemm_argmax_reduce")),  # reduce: before round 6
         ("tgemm_swiglu", re.compile(r"tgemm_kernel<\d+, 2")), ("tgemm", "tgemm_kernel"),
-        ("lm_head_argmax", re.compile(r"wgemm_kernel<\d+, \d+, \d+, 3|lm_head_reduce")),
+        ("lm_head_argmax", re.compile(r"wgemm_kernel<\d+, \d+, \d+, 3|lm_head_reduce|argmax_pairs")),
         ("wgemm_swiglu", re.compile(r"wgemm_kernel<\d+, \d+, \d+, 2")), ("wgemm", "wgemm_kernel"),
         ("wmx_swiglu(fp8)", re.compile(r"wmx_kernel<\d+, \d+, 2")), ("wmx(fp8)", "wmx_kernel"),
         ("pgemm(fp8)", "pgemm_kernel"), ("mx_quant", re.compile(r"mx_quant|rmsnorm_mx|resid_norm_mx")),

@@ -185,8 +185,9 @@ def _enrich_local(pool, args, ctx, work, rank):
             srepo = os.path.join(work, f"small{rank}")
             synth.java_spring_repo(srepo, n_classes=args.small_project_classes, base_package=f"co.acme.sml{rank}",
                                    seed=rank + 301)
+            for w in pool.workers:  # a worker's stats are its last session's
+                w.stats = {}
             ctx.barrier()
-            st0 = dict(be.stats())
             t1 = time.perf_counter()
             try:
                 rs = app.indexer.analyze_project(srepo)
@@ -195,7 +196,7 @@ def _enrich_local(pool, args, ctx, work, rank):
             smx = ctx.max(time.perf_counter() - t1)[0]
             if ctx.sum(1.0 if rs is None else 0.0)[0] == 0:
                 ph2 = ctx.max(rs.stats.get("analyze.phase2", 0.0) / 1e3)[0]
-                d = {k: v - st0.get(k, 0) for k, v in be.stats().items() if isinstance(v, (int, float))}
+                d = be.stats()
                 ss = max(1.0, d.get("decode_steps", 0))
                 # where a latency-bound run's time goes: steps x step time vs prefill and host
                 small = {"classes": rs.classes_analyzed, "enriched": int(rs.stats.get("enriched", 0)),

@@ -176,7 +176,9 @@ def main(argv=None) -> int:
             "elapsed_s": round(elapsed, 3), "classes": int(ok_all),
             "prompt_tokens_per_class": round(st["prompt_tokens"] / max(1, st["prefills"]), 1),
             "generated_tokens_per_class": round(st["generated_tokens"] / max(1, ok_all), 1),
-            "choice_waits": st.get("choice_waits", 0), "type_corrections": st.get("type_corrections", 0)}),
+            "choice_waits": st.get("choice_waits", 0), "type_corrections": st.get("type_corrections", 0),
+            # the timed session's slowest loop iterations: (ms, host ms by phase)
+            "slowest_iters": getattr(eng, "slow_iters", None)}),
             flush=True)
     if dist is not None:
         dist.destroy_process_group()

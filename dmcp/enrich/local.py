@@ -412,6 +412,38 @@ class _Fork:
     anchor_held: bool = True                     # a running branch decodes in the anchor
 
 
+class _IterClock:
+    """Host time of the engine loop's iterations by phase, keeping the
+    ``keep`` slowest (``LocalEngine.slow_iters``): an iteration whose host
+    work outlasts the step queued ahead of it leaves the GPU idle, and which
+    phase it spent that time in (refill, admission, step build, waits,
+    replies) names the cause."""
+
+    def __init__(self, keep: int = 5) -> None:
+        self.keep = keep
+        self.slow: List[Tuple[float, Dict[str, float]]] = []
+        self._t0 = self._t = 0.0
+        self._ph: Dict[str, float] = {}
+
+    def next(self) -> None:
+        """Closes the running iteration (if any) and starts the next."""
+        now = time.perf_counter()
+        if self._t0:
+            self.lap("rest", now)
+            total = 1e3 * (now - self._t0)
+            if len(self.slow) < self.keep or total > self.slow[-1][0]:
+                self.slow.append((round(total, 3), {k: round(1e3 * v, 3) for k, v in self._ph.items()}))
+                self.slow.sort(key=lambda x: -x[0])
+                del self.slow[self.keep:]
+        self._t0 = self._t = now
+        self._ph = {}
+
+    def lap(self, name: str, now: float = 0.0) -> None:
+        now = now or time.perf_counter()
+        self._ph[name] = self._ph.get(name, 0.0) + now - self._t
+        self._t = now
+
+
 from .feeds import IterFeed, QueueFeed  # noqa: E402,F401  (re-exported)
 
 
@@ -566,6 +598,7 @@ class LocalEngine:
                       "forks": 0, "fork_branches": 0, "fork_waits": 0, "fork_skipped": 0,
                       "graph_replays": 0, "graph_kernels": 0}
         self._pf_events: List[tuple] = []  # (start, end) device events of the batched prefills
+        self.slow_iters: List[Tuple[float, Dict[str, float]]] = []  # the last session's slowest loop iterations
         self._lock = threading.Lock()
         self._frag_cache: Dict[bytes, List[int]] = {}      # forced text -> ids
         self._prefix_cache: Dict[str, List[int]] = {}      # per-project prompt text -> ids (one project at a time)
@@ -1168,8 +1201,10 @@ class LocalEngine:
         gc_deferred = bool(self.gc_full_every)
         if gc_deferred:
             _gc_defer_enter(self.gc_full_every)
+        clock = _IterClock()
         try:
             while True:
+                clock.next()
                 # ---- refill the look-ahead (blocking only when idle)
                 want = len(free_slots) + lookahead - len(pending)
                 more = False  # the feed had a whole chunk ready: more may be waiting
@@ -1202,6 +1237,7 @@ class LocalEngine:
                             continue
                         pending.extend(seqs)
                     self._cont_cache.clear()
+                    clock.lap("refill")
                 if not pending and not active and not admits:
                     if feed.done:
                         break
@@ -1211,6 +1247,7 @@ class LocalEngine:
                 for st in forks:
                     fill(st)
                 forks = [st for st in forks if st.pending]
+                clock.lap("forks")
                 # ---- admission: one batched prefill for all that fit, enqueued
                 # ahead of the running batch's next step
                 # (up to admit_depth in flight: the next one's host work --
@@ -1249,11 +1286,13 @@ class LocalEngine:
                         users += s.shared
                         ntok += nxt
                     admits.append(self._admit_launch(batch))
+                    clock.lap("admit_launch")
                 if admits:
                     # nothing decodes yet: keep preparing the feed while the
                     # first prefills run rather than wait for them
                     can_admit = len(admits) < self.admit_depth and pending and free_slots
                     done = self._admit_finish(admits[0], wait=not active and not more and not can_admit)
+                    clock.lap("admit_finish")
                     if done is not None:
                         active.extend(s for s in admits.popleft()["batch"] if not s.done)
                         for s in done:
@@ -1304,6 +1343,10 @@ class LocalEngine:
                         for hh in fin:
                             retire(byh[hh])
                     t4 = time.perf_counter()
+                    clock.lap("build", t1)
+                    clock.lap("launch", t2)
+                    clock.lap("wait", t3)
+                    clock.lap("retire", t4)
                     self.stats["wait_s"] += t3 - t2
                     self.stats["launch_s"] += t2 - t1
                     self.stats["host_s"] += (t1 - t0) + (t4 - t3) + (t2 - t1)
@@ -1445,6 +1488,8 @@ class LocalEngine:
             self.model.fork_flush()
             if gc_deferred:
                 _gc_defer_exit()
+            clock.next()
+            self.slow_iters = clock.slow
 
 
 # Full-collection deferral is process-wide (gc thresholds are global) while

@@ -362,13 +362,14 @@ class LocalLM:
 
     KV_HEADROOM = 4 << 30  # bytes left free next to the slab (graphs, workspaces, prefill activations)
     # row counts from which the large-tile kernel takes over from the
-    # weight-streaming one: the LM head of 128,256 ids from 256 rows (155 vs
-    # 177 us, profiles/tgemm_vs_wgemm_r5.jsonl); the MLP only past 512 rows --
+    # weight-streaming one: the LM head of 128,256 ids from 160 rows (134 vs
+    # 150 us at 160 rows, 134 vs 130 at 80 -- profiles/tgemm_small_rows_r6.jsonl;
+    # 155 vs 177 at 256, profiles/tgemm_vs_wgemm_r5.jsonl); the MLP only past 512 rows --
     # alone gate/up + SwiGLU and down + norm ran faster on it from 448 rows,
     # but the whole 512-row step was 3 % slower (same-box A/B,
     # profiles/decode_step_tgemm_ab_r5.jsonl)
     TGEMM_MLP_MIN_ROWS = 513
-    TGEMM_HEAD_MIN_ROWS = 256
+    TGEMM_HEAD_MIN_ROWS = 160
 
     def _check_kv_fits(self, kv_shape) -> None:
         """The KV slab is the largest allocation of the service (tens of GB at

@@ -474,20 +474,15 @@ __device__ __forceinline__ const char* kv_at(const void* base, size_t off) {
     return static_cast<const char*>(base) + off * (KV8 ? 1 : 2);
 }
 
-// A row's K/V bases: its own slot's; a method branch's class head slot (the
-// parent), which holds the keys [xend, fend) the branch shares; and, with the
-// shared prefix read inline (small steps, see dmcp_decode_attention), the
-// prefix slot holding keys [0, xend).  Shared keys are read in place, never
-// copied.
+// A row's K/V bases: its own slot's, and -- a method branch -- its class
+// head's slot (the parent), which holds the keys [.., fend) the branch
+// shares: keys below fend are read there in place, never copied.
 struct KVSrc {
     const void* k;
     const void* v;
     const void* pk;
     const void* pv;
     int fend;  // 0: no parent
-    const void* xk = nullptr;
-    const void* xv = nullptr;
-    int xend = 0;  // 0: no inline prefix
 };
 
 template <int D, bool KV8>
@@ -496,13 +491,10 @@ __device__ __forceinline__ void load_kv_tile(const KVSrc& src, int kt, int end, 
     constexpr int VE = KV8 ? 16 : 8;  // elements per V chunk
     constexpr int CPK = D / VE;       // V chunks per key
     constexpr int NV = 32 * D / VE / kWave;
-    // key segments: [0, xend) prefix slot, [xend, pe) parent, [pe, ..) own
-    const int pe = max(src.fend, src.xend);
-    const bool pre = kt + 32 <= src.xend;                  // the whole tile is the prefix's
-    const bool par = !pre && kt >= src.xend && kt + 32 <= pe;  // ... the parent's
-    const bool mixed = !pre && !par && kt < pe;            // the tile straddles a boundary
-    const void* kb = pre ? src.xk : (par ? src.pk : src.k);
-    const void* vb = pre ? src.xv : (par ? src.pv : src.v);
+    const bool par = kt + 32 <= src.fend;                // the whole tile is the parent's
+    const bool mixed = !par && kt < src.fend;            // the tile straddles the fork point
+    const void* kb = par ? src.pk : src.k;
+    const void* vb = par ? src.pv : src.v;
     if (kt + 32 <= end && !mixed) {
         const char* kp = kv_at<KV8>(kb, (size_t)(kt + (lane & 15)) * D + 8 * (lane >> 4));
         const char* vp = kv_at<KV8>(vb, (size_t)kt * D + lane * VE);
@@ -518,7 +510,7 @@ __device__ __forceinline__ void load_kv_tile(const KVSrc& src, int kt, int end, 
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int key = min(kt + 16 * h + (lane & 15), end - 1);
-        const void* kk = key < src.xend ? src.xk : (key < pe ? src.pk : src.k);
+        const void* kk = key < src.fend ? src.pk : src.k;
 #pragma unroll
         for (int ks = 0; ks < D / 32; ++ks)
             t.k[h][ks] = *reinterpret_cast<const KRaw*>(kv_at<KV8>(kk, (size_t)key * D + 32 * ks + 8 * (lane >> 4)));
@@ -527,7 +519,7 @@ __device__ __forceinline__ void load_kv_tile(const KVSrc& src, int kt, int end, 
     for (int r = 0; r < NV; ++r) {
         const int ch = lane + kWave * r;
         const int key = min(kt + ch / CPK, end - 1);
-        const void* vv = key < src.xend ? src.xv : (key < pe ? src.pv : src.v);
+        const void* vv = key < src.fend ? src.pv : src.v;
         t.v[r] = *reinterpret_cast<const uint4*>(kv_at<KV8>(vv, (size_t)key * D + (ch % CPK) * VE));
     }
 }
@@ -708,8 +700,7 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
     const int32_t* __restrict__ slot, const int32_t* __restrict__ seq_len, uint16_t* __restrict__ out,
     float* __restrict__ part_o, float* __restrict__ part_ml, int B, int Hkv, int G,
     int max_seq, int chunk, int splits, float scale_log2, int num_slots, const int32_t* __restrict__ plen,
-    int ps_max, const int32_t* __restrict__ prow, const int32_t* __restrict__ fork,
-    const void* __restrict__ prefix_k, const void* __restrict__ prefix_v) {
+    int ps_max, const int32_t* __restrict__ prow, const int32_t* __restrict__ fork) {
     static_assert(D % 32 == 0, "D must be a multiple of 32");
     constexpr int KS = D / 32;    // 32-dim k-steps of the S product
     constexpr int DB = D / 16;    // 16-row d blocks of O^T
@@ -723,9 +714,6 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
     const int g16 = lane >> 4, c = lane & 15;
     const int Hq = Hkv * G;
     const int P0 = __builtin_amdgcn_readfirstlane(plen ? max(0, *plen) : 0);
-    // inline prefix (a prefix with no partial slots): this kernel reads the
-    // prefix slot's keys itself, as the first segment of every row's keys
-    const bool pin = plen != nullptr && ps_max == 0;
     const int splits_total = ps_max + splits;
     const int total = B * Hkv * splits;
     uint16_t* vw = vlds[wave];
@@ -754,8 +742,7 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
             continue;
         }
         // a row outside the shared prefix (prow[b] == 0) owns all its keys
-        const int Prow = __builtin_amdgcn_readfirstlane((prow && !prow[b]) ? 0 : P0);
-        const int P = pin ? 0 : Prow;  // this kernel's keys start at P
+        const int P = __builtin_amdgcn_readfirstlane((prow && !prow[b]) ? 0 : P0);
         const SplitGeom sg = split_geom(L - P, splits, chunk);
         if (split >= max(1, sg.nact)) continue;
         // one own split: this wave writes the row's final output -- directly,
@@ -775,12 +762,6 @@ __global__ __launch_bounds__(kBlock) void decode_attn_mfma_kernel(
         }
         const size_t head_off = ((size_t)s * Hkv + kh) * (size_t)max_seq * D;
         KVSrc src{kv_at<KV8>(k_cache, head_off), kv_at<KV8>(v_cache, head_off), nullptr, nullptr, 0};
-        if (pin && Prow > 0) {  // keys [0, Prow) in the prefix slot ([Hkv, max_seq, D])
-            const size_t xoff = (size_t)kh * max_seq * D;
-            src.xk = kv_at<KV8>(prefix_k, xoff);
-            src.xv = kv_at<KV8>(prefix_v, xoff);
-            src.xend = min(Prow, L);
-        }
         if (fork) {  // fork[2 s] = parent slot, fork[2 s + 1] = the end of the shared keys
             const int ps = __builtin_amdgcn_readfirstlane(fork[2 * s]);
             const int fe = __builtin_amdgcn_readfirstlane(fork[2 * s + 1]);
@@ -978,14 +959,9 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
     if (Hkv <= 0 || Hq % Hkv != 0 || splits <= 0 || chunk <= 0 || !(D == 64 || D == 128) || Hq / Hkv > 16)
         return hipErrorInvalidValue;
     const bool prefix = plen != nullptr;
-    if (prefix && (!prefix_k || !prefix_v || ps_max < 0)) return hipErrorInvalidValue;
+    if (prefix && (!prefix_k || !prefix_v || ps_max <= 0)) return hipErrorInvalidValue;
     if (!prefix) ps_max = 0;
-    // ps_max == 0 with a prefix: read inline by the per-row kernel (no prefix
-    // kernel, no prefix partials) -- small steps, where the prefix kernel's
-    // and the combine's fixed costs outweigh reading the L2-resident prefix
-    // once per row
-    const bool pin = prefix && ps_max == 0;
-    if ((splits > 1 || (prefix && !pin)) && (!part_o || !part_ml)) return hipErrorInvalidValue;
+    if ((splits > 1 || prefix) && (!part_o || !part_ml)) return hipErrorInvalidValue;
     const int G = Hq / Hkv;
     const float sl2 = scale * 1.4426950408889634f;
     auto st = (hipStream_t)stream;
@@ -994,7 +970,7 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
     auto ln = (const int32_t*)seq_len;
     auto pl = (const int32_t*)plen;
     auto pr = prefix ? (const int32_t*)prefix_rows : nullptr;
-    if (prefix && !pin) {
+    if (prefix) {
         hipError_t pe = dmcp_launch_prefix_partials(qq, prefix_k, prefix_v, pl, (float*)part_o, (float*)part_ml, B,
                                                     Hkv, G, D, max_seq, ps_max, ps_max + splits, sl2, kv8, st);
         if (pe != hipSuccess) return pe;
@@ -1019,8 +995,7 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
         const dim3 wgrid((unsigned)(wblocks < cap ? wblocks : cap));                                               \
         decode_attn_mfma_kernel<DD, K8><<<wgrid, kBlock, 0, st>>>(qq, k_cache, v_cache, sl, ln, oo, po, pml, B,   \
                                                                   Hkv, G, max_seq, chunk, splits, sl2, num_slots, \
-                                                                  pl, ps_max, pr, (const int32_t*)fork, prefix_k, \
-                                                                  prefix_v);                                      \
+                                                                  pl, ps_max, pr, (const int32_t*)fork);          \
     } while (0)
     if (kv8) {
         if (D == 64) DMCP_MFMA_DECODE(64, true);
@@ -1032,8 +1007,8 @@ int dmcp_decode_attention(const void* q, const void* k_cache, const void* v_cach
 #undef DMCP_MFMA_DECODE
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || splits == 1) return e;  // every row finished in the main kernel
-    return launch_combine(part_o, part_ml, sl, ln, out, B, Hq, D, max_seq, chunk, splits, num_slots,
-                          pin ? nullptr : pl, ps_max, pr, st);
+    return launch_combine(part_o, part_ml, sl, ln, out, B, Hq, D, max_seq, chunk, splits, num_slots, pl, ps_max, pr,
+                          st);
 }
 
 int dmcp_silu_mul(const void* gu, void* out, int T, int I, void* stream) {

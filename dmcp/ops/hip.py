@@ -17,6 +17,7 @@ import os
 import threading
 from typing import Optional
 
+import numpy as np
 import torch
 
 from .build import TARGET, build
@@ -282,8 +283,7 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
         if tuple(pk.shape) != (Hkv, MAXS, D) or tuple(pv.shape) != (Hkv, MAXS, D) or plen.numel() != 1:
             raise HipOpsError(f"decode_attention: prefix k {tuple(pk.shape)} / v {tuple(pv.shape)} do not match "
                               f"kv {tuple(k_cache.shape)}")
-        # small steps read the prefix inline (ps_max 0): see prefix_inline_rows
-        ps_max = 0 if B <= prefix_inline_rows() else prefix_mfma_splits(B, Hq // Hkv, Hkv)
+        ps_max = prefix_mfma_splits(B, Hq // Hkv, Hkv)
         prows = getattr(prefix, "rows", None)
         if prows is not None:
             _req(prows, torch.int32, "decode_attention.prefix.rows")
@@ -376,6 +376,45 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
 VARLEN_COLS = 128  # query columns (token x q head of a kv group) per varlen work item: 4 waves x 32
 
 
+_VARLEN_META: dict = {}  # the last prefill's work list: key -> (items, device int32 meta)
+
+
+def _varlen_meta(key: tuple, device) -> tuple:
+    """The varlen kernel's work list: items (sequence, 128-column tile) by
+    descending key count (ties: sequence, then tile order), then the
+    sequences' (row offset, length, start, slot, prefix length).  Validates
+    every sequence."""
+    offsets, slots, starts, prefix_slot, plens, G, S, MAXS, _ = key
+    n = len(slots)
+    off = np.asarray(offsets, dtype=np.int64)
+    T = off[1:] - off[:-1]
+    st = np.asarray(starts, dtype=np.int64)
+    sl = np.asarray(slots, dtype=np.int64)
+    P = np.asarray(plens, dtype=np.int64)
+    bad = np.flatnonzero((T < 1) | (sl < 0) | (sl >= S) | (st < 0) | (st + T > MAXS))
+    if bad.size:
+        i = int(bad[0])
+        raise HipOpsError(f"prefill_attention_varlen: sequence {i} (slot {int(sl[i])}, [{int(st[i])}, "
+                          f"{int(st[i] + T[i])})) does not fit {S} slots x {MAXS} positions")
+    ps_bad = prefix_slot is None or not 0 <= prefix_slot < S
+    bad = np.flatnonzero((P != 0) & (ps_bad | (P < 0) | (P > st)))
+    if bad.size:
+        i = int(bad[0])
+        raise HipOpsError(f"prefill_attention_varlen: prefix of {int(P[i])} keys in slot {prefix_slot} must precede "
+                          f"start {int(st[i])}")
+    ntile = -(-T * G // VARLEN_COLS)
+    seq_of = np.repeat(np.arange(n, dtype=np.int64), ntile)
+    ct = np.arange(int(ntile.sum()), dtype=np.int64) - np.repeat(np.cumsum(ntile) - ntile, ntile)
+    last_tok = np.minimum(T[seq_of], ((ct + 1) * VARLEN_COLS + G - 1) // G)
+    order = np.argsort(-(st[seq_of] + last_tok), kind="stable")
+    items = np.stack([seq_of[order], ct[order]], 1).ravel()
+    seqs = np.stack([off[:-1], T, st, sl, P], 1).ravel()
+    meta = torch.from_numpy(np.concatenate([items, seqs]).astype(np.int32))
+    if torch.device(device).type == "cuda":
+        meta = meta.pin_memory()
+    return len(order), meta.to(device, non_blocking=True)
+
+
 def prefill_attention_varlen(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, offsets, slots, starts,
                              prefix_slot: Optional[int] = None, prefix_lens=None, scale: float = 1.0,
                              out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -396,27 +435,20 @@ def prefill_attention_varlen(q: torch.Tensor, k_cache: torch.Tensor, v_cache: to
         raise HipOpsError("prefill_attention_varlen: offsets must run from 0 to Ttot with one entry per sequence + 1")
     G = Hq // Hkv
     plens = [int(x) for x in prefix_lens] if prefix_lens is not None else [0] * n
-    seq = []
-    items = []
-    for i in range(n):
-        a, b, st, sl, P = int(offsets[i]), int(offsets[i + 1]), int(starts[i]), int(slots[i]), plens[i]
-        T = b - a
-        if T < 1 or not 0 <= sl < S or st < 0 or st + T > MAXS:
-            raise HipOpsError(f"prefill_attention_varlen: sequence {i} (slot {sl}, [{st}, {st + T})) does not fit "
-                              f"{S} slots x {MAXS} positions")
-        if P and (prefix_slot is None or not 0 <= int(prefix_slot) < S or not 0 < P <= st):
-            raise HipOpsError(f"prefill_attention_varlen: prefix of {P} keys in slot {prefix_slot} must precede "
-                              f"start {st}")
-        seq.append((a, T, st, sl, P))
-        for ct in range(-(-T * G // VARLEN_COLS)):
-            last_tok = min(T, ((ct + 1) * VARLEN_COLS + G - 1) // G)
-            items.append((st + last_tok, i, ct))
-    items.sort(key=lambda x: -x[0])
+    key = (tuple(int(x) for x in offsets), tuple(int(x) for x in slots), tuple(int(x) for x in starts),
+           None if prefix_slot is None else int(prefix_slot), tuple(plens), G, S, MAXS, str(q.device))
+    hit = _VARLEN_META.get(key)
+    if hit is None:
+        # every layer of a batched prefill launches with the same sequences:
+        # the work list is built (and copied to the device) once per prefill,
+        # not per layer (16 x ~0.5-0.9 ms of host time per admission)
+        hit = _varlen_meta(key, q.device)
+        _VARLEN_META.clear()
+        _VARLEN_META[key] = hit
+    n_items, meta = hit
     out = torch.empty_like(q) if out is None else out
     _req_out(out, torch.bfloat16, Ttot * Hq * D, "prefill_attention_varlen.out")
-    meta = torch.tensor([v for _, i, ct in items for v in (i, ct)] + [v for r in seq for v in r], dtype=torch.int32)
-    meta = meta.pin_memory().to(q.device, non_blocking=True)
-    it_t, seq_t = meta[:2 * len(items)], meta[2 * len(items):]
+    it_t, seq_t = meta[:2 * n_items], meta[2 * n_items:]
     if any(plens):
         pk, pv = k_cache[int(prefix_slot)], v_cache[int(prefix_slot)]
     else:
@@ -442,18 +474,6 @@ def prefix_mfma_splits(rows: int, G: int, Hkv: int, target_blocks: int = 640) ->
         return max(1, min(PREFIX_MFMA_MAX_SPLITS, int(env)))
     tiles = -(-rows * G // 128) * Hkv
     return max(1, min(PREFIX_MFMA_MAX_SPLITS, round(target_blocks / max(1, tiles))))
-
-
-# Steps of at most this many rows read the shared prefix inside the per-row
-# attention kernel (the prefix slot as the first key segment of every row)
-# instead of the MFMA prefix kernel + its partials + the combine pass
-PREFIX_INLINE_ROWS = 0
-
-
-def prefix_inline_rows() -> int:
-    """:data:`PREFIX_INLINE_ROWS`; ``DMCP_PREFIX_INLINE_ROWS`` overrides."""
-    env = os.environ.get("DMCP_PREFIX_INLINE_ROWS")
-    return int(env) if env else PREFIX_INLINE_ROWS
 
 
 def decode_workspace(rows: int, Hq: int, Hkv: int, D: int, max_seq: int, device, chunk: int = 256,
@@ -729,8 +749,8 @@ def wgemm_plan(M: int, N: int, K: int, swiglu: bool = False, target_blocks: int 
 
     Below 384 rows (tuned at 78 and 320 rows, profiles/wgemm_r3.txt): M parts
     of <= 192 rows (<= 3 16-row tiles per wave), then K slices (powers of
-    two, whole 64-deep chunks) until 64-row weight tiles x parts x slices
-    covers ~3/4 of the 256 CUs; SwiGLU writes its output directly (S = 1)
+    two, whole 64-deep chunks, >= 512 deep) until 64-row weight tiles x parts
+    x slices covers ~3/4 of the 256 CUs; SwiGLU writes its output directly (S = 1)
     and splits M instead.
 
     From 384 rows a block holds ~100-150 KB of LDS, so one block per CU: a
@@ -763,8 +783,10 @@ def wgemm_plan(M: int, N: int, K: int, swiglu: bool = False, target_blocks: int 
         while tiles * mparts < target_blocks and -(-M // (mparts + 1)) >= 16:
             mparts += 1
         return 1, mparts
+    # K slices of >= 512 (the split sweep at 40-320 rows: O / QKV at K = 2,048
+    # fastest with 4 slices, not 8 -- profiles/wgemm_split_sweep_r6.jsonl)
     S = 1
-    while tiles * mparts * S < target_blocks and S < 8 and K % (64 * S * 2) == 0:
+    while tiles * mparts * S < target_blocks and S < 8 and K % (64 * S * 2) == 0 and K // (S * 2) >= 512:
         S *= 2
     return S, mparts
 

@@ -131,7 +131,6 @@ def main(argv=None) -> int:
                       "tg_head": bool(getattr(model, "tg_head", False)), "wgemm_aux": a.wgemm_aux,
                       "prefix_splits": hip.prefix_mfma_splits(a.batch + a.extra, cfg.n_heads // cfg.n_kv_heads,
                                                               cfg.n_kv_heads),
-                      "prefix_inline": a.prefix > 0 and a.batch + a.extra <= hip.prefix_inline_rows(),
                       "device_ms": round(dev_ms, 3), "loop_ms": round(loop_ms, 3),
                       "launch_cpu_ms": round(launch_ms, 3), "pipelined_ms": round(pipe_ms, 3),
                       "host_gap_ms": round(loop_ms - dev_ms, 3),

@@ -57,6 +57,8 @@ def main() -> int:
     ap.add_argument("--reps", type=int, default=24)
     ap.add_argument("--sweep", action="store_true", help="also time every (S, mparts) around the plan")
     ap.add_argument("--only", default="", help="comma list of projections (qkv,o,gu,down,head)")
+    ap.add_argument("--wg-sweep", action="store_true",
+                    help="sweep the split count of the weight-streaming kernel's fused qkv / o / down ops")
     ap.add_argument("--fused-sweep", action="store_true",
                     help="sweep (S, mparts) of the FUSED op (GEMM + its reduction) for qkv / o / down")
     ap.add_argument("--copies", type=int, default=0, help="weight copies (default: enough to exceed 640 MB)")
@@ -187,6 +189,22 @@ def main() -> int:
             elif M <= hip.WGEMM_MAX_ROWS and hip.lm_head_supported(N, K):
                 rec["wg_fused_us"] = round(graph_ms(lambda i: hip.lm_head_argmax(x, Ws[i], masks, midx), a.reps,
                                                     copies) * 1e3, 2)
+            if a.wg_sweep and M <= hip.WGEMM_MAX_ROWS and name in ("qkv", "o", "down"):
+                # the weight-streaming kernel's fused op over its split count (the plan's S is wg_plan)
+                rec["wg_plan"] = list(hip.wgemm_plan(M, N, K))
+                sws = hip.wgemm_workspace(4 * M, max(Q, H), dev)  # room for 32 slices
+                wsw = {}
+                for S in (1, 2, 4, 8, 16, 32):
+                    if K % (64 * S):
+                        continue
+                    if name == "qkv":
+                        f = lambda i, S=S: hip.wgemm_rope_kv(x, Ws[i], pos, sl, cs, kc, vc, c.n_heads, sws,  # noqa
+                                                             splits=S)
+                    else:
+                        f = lambda i, S=S: hip.wgemm_resid_norm(x, Ws[i], resid, nw, 1e-5, sws, splits=S)  # noqa
+                    wsw[f"S{S}"] = round(graph_ms(f, a.reps, copies) * 1e3, 2)
+                rec["wg_sweep_us"] = wsw
+                rec["wg_sweep_best"] = min(wsw.items(), key=lambda kv: kv[1])
             if a.fused_sweep and name in ("qkv", "o", "down"):
                 fsw = {}
                 chunks = K // hip.TGEMM_KC

@@ -130,6 +130,7 @@ for s in $STEPS; do
         tgemm_test) run tgemm_test 600 python -u -m pytest tests/test_gpu_tgemm.py -x -q --timeout 120 \
                 --timeout-method thread ;;
         tgemm_small) run tgemm_small 900 python scripts/bench_tgemm.py --rows 40 80 160 320 --only qkv,o,gu,down,head ;;
+        wg_sweep) run wg_sweep 600 python scripts/bench_tgemm.py --rows 40 80 160 320 --only qkv,o,down --wg-sweep ;;
         tgemm_sweep) run tgemm_sweep 900 python scripts/bench_tgemm.py --rows 520 610 768 1024 --only gu,head --sweep ;;
         step_small)  # small-row latency (verdict item 5): 40 / 80 / 160 rows
             for r in "32 8" "64 16" "128 32"; do set -- $r
@@ -138,14 +139,6 @@ for s in $STEPS; do
             done ;;
         kern_tests) run kern_tests 900 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_wgemm.py \
                 tests/test_gpu_tgemm.py tests/test_gpu_pgemm.py -x -q --timeout 120 --timeout-method thread ;;
-        inline_test) run inline_test 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 \
-                --timeout-method thread -k "inline_prefix or shared_prefix or fork_table or off_the_prefix" ;;
-        inline_ab)  # the shared prefix read inline by the per-row kernel vs the prefix kernel, alternating
-            for rep in 1 2; do for il in 0 4096; do for r in "32 8" "64 16" "128 32" "256 64"; do set -- $r
-                DMCP_PREFIX_INLINE_ROWS=$il run inline_ab_${il}_$(($1 + $2))_$rep 300 python scripts/bench_step.py \
-                    --preset llama3.2-1b-code --batch $1 --extra $2 --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 100
-            done; done; done
-            grep -h '^{' "$OUT"/inline_ab_*.log > "$OUT/inline_ab.jsonl" ;;
         prof_step80)
             ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d "$ROOT/$OUT/prof_step80" -o step -- python3 "$ROOT/scripts/bench_step.py" \

@@ -365,43 +365,3 @@ def test_decode_attention_fork_table(hip, kv, splits, P):
     ref = reference.decode_attention(q, kc, vc, slot, lens, 0.125, prefix=pre, fork=fork)
     torch.testing.assert_close(got.float(), ref.float(), atol=2e-2, rtol=2e-2)
 
-
-@pytest.mark.parametrize("kv", ["bf16", "fp8"])
-@pytest.mark.parametrize("splits", [1, 3, 7])
-@pytest.mark.parametrize("P", [1, 45, 333, 1119])
-def test_decode_attention_inline_prefix(hip, monkeypatch, kv, splits, P):
-    """Small steps read the shared prefix inside the per-row kernel
-    (hip.prefix_inline_rows: the prefix slot as the first key segment, no
-    prefix kernel / partials): vs the fp32 reference and vs the prefix-kernel
-    path, with rows off the prefix, method branches reading their parent's
-    keys (fork ends before, on and after 32-key tile edges) and a padding row."""
-    from dmcp.ops import reference
-    from dmcp.ops.reference import SharedPrefix
-    D, Hq, Hkv, MAXS, S = 64, 32, 8, 2048, 10
-
-    def cache(seed):
-        x = _bf(S + 1, Hkv, MAXS, D, seed=seed)
-        return x.to(torch.float8_e4m3fn).view(torch.uint8) if kv == "fp8" else x
-    kc, vc = cache(41), cache(42)
-    # (slot, (parent, fork end) or None, length, on the prefix)
-    rows = [(1, None, P + 700, 1), (2, (1, P + 77), P + 690, 1), (3, (1, P + 96), P + 500, 1),
-            (4, None, P + 1, 1), (5, None, 650, 0), (6, (1, P + 31), P + 40, 1), (-1, None, 5, 1),
-            (7, None, P + 33, 1)]
-    B = len(rows)
-    q = _bf(B, Hq, D, seed=43)
-    slot = torch.tensor([r[0] for r in rows], dtype=torch.int32, device="cuda")
-    lens = torch.tensor([r[2] for r in rows], dtype=torch.int32, device="cuda")
-    on = torch.tensor([r[3] for r in rows], dtype=torch.int32, device="cuda")
-    fork = torch.stack([torch.arange(S + 1), torch.zeros(S + 1, dtype=torch.long)], 1).to(torch.int32).cuda()
-    for s, par, _, _ in rows:
-        if par is not None:
-            fork[s] = torch.tensor(par, dtype=torch.int32)
-    pre = SharedPrefix(kc[S], vc[S], torch.tensor([P], dtype=torch.int32, device="cuda"), on)
-    monkeypatch.setenv("DMCP_PREFIX_INLINE_ROWS", "4096")
-    got = hip.decode_attention(q, kc, vc, slot, lens, 0.125, chunk=64, prefix=pre, splits=splits, fork=fork)
-    ref = reference.decode_attention(q, kc, vc, slot, lens, 0.125, prefix=pre, fork=fork)
-    torch.testing.assert_close(got.float(), ref.float(), atol=2e-2, rtol=2e-2)
-    assert got[6].abs().sum().item() == 0  # the padding row
-    monkeypatch.setenv("DMCP_PREFIX_INLINE_ROWS", "0")
-    via_kernel = hip.decode_attention(q, kc, vc, slot, lens, 0.125, chunk=64, prefix=pre, splits=splits, fork=fork)
-    torch.testing.assert_close(got.float(), via_kernel.float(), atol=1e-2, rtol=1e-2)

@@ -74,3 +74,45 @@ def test_device_ops_share_one_signature():
         r = list(inspect.signature(getattr(reference, name)).parameters)
         assert k == r, name
         assert list(inspect.signature(getattr(ops, name)).parameters) == k, name
+
+
+def _varlen_items_loop(offsets, slots, starts, plens, G):
+    """The varlen work list as the per-item loop built it before round 6."""
+    from dmcp.ops import hip
+    seq, items = [], []
+    for i in range(len(slots)):
+        a, b, st, sl, P = offsets[i], offsets[i + 1], starts[i], slots[i], plens[i]
+        T = b - a
+        seq.append((a, T, st, sl, P))
+        for ct in range(-(-T * G // hip.VARLEN_COLS)):
+            last_tok = min(T, ((ct + 1) * hip.VARLEN_COLS + G - 1) // G)
+            items.append((st + last_tok, i, ct))
+    items.sort(key=lambda x: -x[0])
+    return len(items), [v for _, i, ct in items for v in (i, ct)] + [v for r in seq for v in r]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_varlen_work_list_matches_the_item_loop(seed):
+    """The vectorised varlen work list (built once per prefill) is the
+    per-item loop's, item for item; bad sequences are refused."""
+    import random
+    from dmcp.ops import hip
+    rng = random.Random(seed)
+    n = rng.randint(1, 60)
+    lens = [rng.choice([1, 2, 31, 32, 33, 127, 128, 560, 2000]) for _ in range(n)]
+    offsets = [0]
+    for T in lens:
+        offsets.append(offsets[-1] + T)
+    slots = rng.sample(range(64), n)
+    plens = [rng.choice([0, 1119]) for _ in range(n)]
+    starts = [p + rng.randint(0, 50) if p else rng.randint(0, 50) for p in plens]
+    G = rng.choice([1, 2, 4, 8])
+    key = (tuple(offsets), tuple(slots), tuple(starts), 63, tuple(plens), G, 64, 4096, "cpu")
+    n_items, meta = hip._varlen_meta(key, "cpu")
+    exp_n, exp = _varlen_items_loop(offsets, slots, starts, plens, G)
+    assert n_items == exp_n and meta.tolist() == exp
+    with pytest.raises(hip.HipOpsError):  # a prefix that does not precede its start
+        hip._varlen_meta((tuple(offsets), tuple(slots), tuple(0 for _ in starts), 63, tuple([5] * n), G, 64, 4096,
+                          "cpu"), "cpu")
+    with pytest.raises(hip.HipOpsError):  # past the slot's positions
+        hip._varlen_meta((tuple(offsets), tuple(slots), tuple(starts), 63, tuple(plens), G, 64, 100, "cpu"), "cpu")

@@ -581,6 +581,8 @@ class LocalEngine:
         self.refill_chunk = int(os.environ.get("LOCAL_LLM_REFILL_CHUNK", "32"))
         # fork-table rows applied once per decode launch (False: at each call)
         self.fork_batch = os.environ.get("LOCAL_LLM_FORK_BATCH", "1") != "0"
+        # refill + admission under the launched step (see _session); 0 = at the iteration's top
+        self.host_under_step = os.environ.get("LOCAL_LLM_HOST_UNDER_STEP", "1") != "0"
         # batched prefills that may be in flight at once
         self.admit_depth = max(1, int(os.environ.get("LOCAL_LLM_ADMIT_DEPTH", "2")))
         # previous step's selections for host-less gathers (graphs keep their own)
@@ -596,7 +598,7 @@ class LocalEngine:
                       "reply_parts": 0,
                       "split_classes": 0, "methods_dropped": 0, "type_corrections": 0, "choice_waits": 0,
                       "forks": 0, "fork_branches": 0, "fork_waits": 0, "fork_skipped": 0,
-                      "graph_replays": 0, "graph_kernels": 0}
+                      "graph_replays": 0, "graph_kernels": 0, "under_s": 0.0}
         self._pf_events: List[tuple] = []  # (start, end) device events of the batched prefills
         self.slow_iters: List[Tuple[float, Dict[str, float]]] = []  # the last session's slowest loop iterations
         self._lock = threading.Lock()
@@ -1202,42 +1204,97 @@ class LocalEngine:
         if gc_deferred:
             _gc_defer_enter(self.gc_full_every)
         clock = _IterClock()
+
+        def refill():
+            """Tops up the look-ahead from the feed (blocking only when idle);
+            returns whether the feed had a whole chunk ready (more may wait).
+            Yields the error replies of classes that cannot be set up."""
+            nonlocal pending
+            want = len(free_slots) + lookahead - len(pending)
+            if want <= 0 or feed.done:
+                return False
+            if self.refill_chunk > 0:
+                # a chunk per iteration: its prompts' tokenisation and
+                # sequence set-up (~0.2 ms a class) stay under the GPU work
+                # already queued -- a step, or at the start the first
+                # admissions' prefills -- instead of one refill of the whole
+                # batch with the GPU idle (~180 ms per start at 768 slots,
+                # profiles/engine_host_r5.txt)
+                want = min(want, self.refill_chunk)
+            items = list(feed.take(want, wait=not active and not pending and not admits))
+            # a small batch -- the feed drained and every class fits in 3/4 of
+            # the slots -- is latency-bound: long-context classes fork too
+            # (profiles/enrich_fork_context_ab_r4.jsonl)
+            small = len(items) < want and len(active) + len(pending) + len(items) <= cfg.max_batch * 3 // 4
+            try:
+                self._pretokenize(items, readme)
+            except Exception:  # noqa: BLE001 -- each class then tokenises (and reports) on its own
+                LOG.debug("batched prompt tokenisation failed", exc_info=True)
+            for item in items:
+                key, inp = item[0], item[1]
+                try:
+                    seqs = self._seqs_for(key, inp, item[2] if len(item) > 2 else readme, small)
+                except Exception as e:
+                    yield key, json.dumps({"error": str(e)})
+                    continue
+                pending.extend(seqs)
+            self._cont_cache.clear()
+            clock.lap("refill")
+            return len(items) == want
+
+        def admit() -> None:
+            """One batched prefill for all that fit (up to admit_depth in flight:
+            the next one's host work -- prompts, packing, ~130 launches -- runs
+            under the previous one's prefill instead of after it, GPU idle)."""
+            nonlocal pending, prefix_toks, P
+            if not (len(admits) < self.admit_depth and pending and free_slots and (
+                    not active or len(free_slots) >= self.admit_min
+                    or (feed.done and len(free_slots) >= len(pending)))):
+                return
+            batch: List[_Seq] = []
+            ntok = 0
+            if self.longest_first and len(pending) > 1:
+                pending = deque(sorted(pending, key=lambda q: -q.free_budget))
+            # the resident prefix's readers: running and still prefilling
+            users = sum(1 for q in active if q.shared) + \
+                sum(1 for h in admits for q in h["batch"] if q.shared)
+            while pending and free_slots and len(batch) < self.ADMIT_SEQS:
+                s = pending[0]
+                if self.shared_prefix and users == 0:
+                    # no running sequence reads the resident prefix: it moves
+                    # to this class's project
+                    Ps = self._seq_prefix_len(s)
+                    if Ps and s.prompt[:Ps] != prefix_toks:
+                        t0 = time.perf_counter()
+                        self.model.set_prefix(s.prompt[:Ps])
+                        prefix_toks, P = s.prompt[:Ps], Ps
+                        self.stats["prefix_s"] += time.perf_counter() - t0
+                        self.stats["prefix_tokens"] += Ps
+                        self.stats["prefix_switches"] += 1
+                s.shared = bool(P) and len(s.prompt) > P and s.prompt[:P] == prefix_toks
+                nxt = len(s.prompt) - (P if s.shared else 0)
+                if batch and ntok + nxt > self.ADMIT_TOKENS:
+                    break
+                pending.popleft()
+                s.slot = free_slots.pop()
+                batch.append(s)
+                users += s.shared
+                ntok += nxt
+            admits.append(self._admit_launch(batch))
+            clock.lap("admit_launch")
+
+        more = False  # the last refill found a whole chunk ready: more may be waiting
         try:
             while True:
                 clock.next()
-                # ---- refill the look-ahead (blocking only when idle)
-                want = len(free_slots) + lookahead - len(pending)
-                more = False  # the feed had a whole chunk ready: more may be waiting
-                if want > 0 and not feed.done:
-                    if self.refill_chunk > 0:
-                        # a chunk per iteration: its prompts' tokenisation and
-                        # sequence set-up (~0.2 ms a class) stay under the GPU
-                        # work already queued -- a step, or at the start the
-                        # first admissions' prefills -- instead of one refill of
-                        # the whole batch with the GPU idle (~180 ms per start
-                        # at 768 slots, profiles/engine_host_r5.txt)
-                        want = min(want, self.refill_chunk)
-                    items = list(feed.take(want, wait=not active and not pending and not admits))
-                    more = len(items) == want
-                    # a small batch -- the feed drained and every class fits in
-                    # 3/4 of the slots -- is latency-bound: long-context classes
-                    # fork too (profiles/enrich_fork_context_ab_r4.jsonl)
-                    small = len(items) < want and \
-                        len(active) + len(pending) + len(items) <= cfg.max_batch * 3 // 4
-                    try:
-                        self._pretokenize(items, readme)
-                    except Exception:  # noqa: BLE001 -- each class then tokenises (and reports) on its own
-                        LOG.debug("batched prompt tokenisation failed", exc_info=True)
-                    for item in items:
-                        key, inp = item[0], item[1]
-                        try:
-                            seqs = self._seqs_for(key, inp, item[2] if len(item) > 2 else readme, small)
-                        except Exception as e:
-                            yield key, json.dumps({"error": str(e)})
-                            continue
-                        pending.extend(seqs)
-                    self._cont_cache.clear()
-                    clock.lap("refill")
+                # with a running batch the look-ahead refill and the next
+                # admission run right after the step is launched, under it and
+                # the one before (at the top of the iteration they ran with at
+                # most one step queued: the GPU idled ~10 ms behind each
+                # admission's ~17 ms of host work, profiles/engine_gaps_r6_*.txt)
+                under = self.host_under_step and bool(active) and self.pipeline
+                if not under:
+                    more = yield from refill()
                 if not pending and not active and not admits:
                     if feed.done:
                         break
@@ -1248,45 +1305,8 @@ class LocalEngine:
                     fill(st)
                 forks = [st for st in forks if st.pending]
                 clock.lap("forks")
-                # ---- admission: one batched prefill for all that fit, enqueued
-                # ahead of the running batch's next step
-                # (up to admit_depth in flight: the next one's host work --
-                # prompts, packing, ~130 launches -- runs under the previous
-                # one's prefill instead of after it, GPU idle)
-                if len(admits) < self.admit_depth and pending and free_slots and (
-                        not active or len(free_slots) >= self.admit_min
-                        or (feed.done and len(free_slots) >= len(pending))):
-                    batch: List[_Seq] = []
-                    ntok = 0
-                    if self.longest_first and len(pending) > 1:
-                        pending = deque(sorted(pending, key=lambda q: -q.free_budget))
-                    # the resident prefix's readers: running and still prefilling
-                    users = sum(1 for q in active if q.shared) + \
-                        sum(1 for h in admits for q in h["batch"] if q.shared)
-                    while pending and free_slots and len(batch) < self.ADMIT_SEQS:
-                        s = pending[0]
-                        if self.shared_prefix and users == 0:
-                            # no running sequence reads the resident prefix:
-                            # it moves to this class's project
-                            Ps = self._seq_prefix_len(s)
-                            if Ps and s.prompt[:Ps] != prefix_toks:
-                                t0 = time.perf_counter()
-                                self.model.set_prefix(s.prompt[:Ps])
-                                prefix_toks, P = s.prompt[:Ps], Ps
-                                self.stats["prefix_s"] += time.perf_counter() - t0
-                                self.stats["prefix_tokens"] += Ps
-                                self.stats["prefix_switches"] += 1
-                        s.shared = bool(P) and len(s.prompt) > P and s.prompt[:P] == prefix_toks
-                        nxt = len(s.prompt) - (P if s.shared else 0)
-                        if batch and ntok + nxt > self.ADMIT_TOKENS:
-                            break
-                        pending.popleft()
-                        s.slot = free_slots.pop()
-                        batch.append(s)
-                        users += s.shared
-                        ntok += nxt
-                    admits.append(self._admit_launch(batch))
-                    clock.lap("admit_launch")
+                if not under:
+                    admit()
                 if admits:
                     # nothing decodes yet: keep preparing the feed while the
                     # first prefills run rather than wait for them
@@ -1316,6 +1336,12 @@ class LocalEngine:
                         event = self._launch_staged(n, buf)
                         step_no += 1
                     t2 = time.perf_counter()
+                    if under:  # the refill / admission host work, under the steps in flight
+                        clock.lap("build", t1)
+                        clock.lap("launch", t2)
+                        more = yield from refill()
+                        admit()
+                    th = time.perf_counter()
                     if not self.pipeline:
                         if event is not None:
                             event.synchronize()
@@ -1343,14 +1369,16 @@ class LocalEngine:
                         for hh in fin:
                             retire(byh[hh])
                     t4 = time.perf_counter()
-                    clock.lap("build", t1)
-                    clock.lap("launch", t2)
+                    if not under:
+                        clock.lap("build", t1)
+                        clock.lap("launch", t2)
                     clock.lap("wait", t3)
                     clock.lap("retire", t4)
-                    self.stats["wait_s"] += t3 - t2
+                    self.stats["wait_s"] += t3 - th
                     self.stats["launch_s"] += t2 - t1
                     self.stats["host_s"] += (t1 - t0) + (t4 - t3) + (t2 - t1)
-                    self.stats["decode_s"] += t4 - t0
+                    self.stats["decode_s"] += (t4 - t0) - (th - t2)  # the refill / admission are not the step's
+                    self.stats["under_s"] += th - t2
                     for k, v in nat.stats().items():  # (cheap) so a never-ending worker stream reports them
                         self.stats[k] += v
                     nat.reset_stats()
@@ -1420,6 +1448,10 @@ class LocalEngine:
                 else:  # every active sequence waits for a choice of the last step
                     event, buf = None, None
                 t2 = time.perf_counter()
+                if under:  # the refill / admission host work, under the steps in flight
+                    more = yield from refill()
+                    admit()
+                th = time.perf_counter()
                 if not self.pipeline:
                     if event is not None:
                         event.synchronize()
@@ -1459,9 +1491,10 @@ class LocalEngine:
                 for s in gone:
                     retire(s)
                 t4 = time.perf_counter()
-                self.stats["wait_s"] += t3 - t2
+                self.stats["wait_s"] += t3 - th
                 self.stats["host_s"] += (t1 - t0) + (t4 - t3) + (t2 - t1)
-                self.stats["decode_s"] += t4 - t0
+                self.stats["decode_s"] += (t4 - t0) - (th - t2)
+                self.stats["under_s"] += th - t2
                 # replies go out while the GPU computes the step just launched
                 while finished:
                     s = finished.pop()

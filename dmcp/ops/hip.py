@@ -227,6 +227,7 @@ def decode_plan(rows: int, n_kv_heads: int, max_seq: int, target_waves: int = 40
     chunks plus a short remainder that left most waves idle at the end
     (measured: 1024-key chunks reached 42 % of the copy rate at B = 78,
     L = 2,500 -- profiles/decode_step_r2*)."""
+    min_chunk = int(os.environ.get("DMCP_DECODE_MIN_CHUNK", min_chunk))  # A/B override
     splits = max(1, -(-target_waves // max(1, rows * n_kv_heads)))
     return min_chunk, min(splits, decode_splits(max_seq, min_chunk))
 
@@ -454,7 +455,7 @@ def prefill_attention_varlen(q: torch.Tensor, k_cache: torch.Tensor, v_cache: to
     else:
         pk = pv = None
     _check(lib().dmcp_prefill_varlen(_ptr(q), _ptr(k_cache), _ptr(v_cache), _ptr(pk), _ptr(pv), _ptr(out),
-                                     _ptr(it_t), _ptr(seq_t), len(items), Hq, Hkv, D, MAXS, Hkv * MAXS * D,
+                                     _ptr(it_t), _ptr(seq_t), n_items, Hq, Hkv, D, MAXS, Hkv * MAXS * D,
                                      float(scale), kv8, _stream()), "dmcp_prefill_varlen")
     return out
 

@@ -138,7 +138,28 @@ for s in $STEPS; do
                     --extra $2 --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 100
             done ;;
         kern_tests) run kern_tests 900 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_wgemm.py \
-                tests/test_gpu_tgemm.py tests/test_gpu_pgemm.py -x -q --timeout 120 --timeout-method thread ;;
+                tests/test_gpu_tgemm.py tests/test_gpu_pgemm.py tests/test_gpu_prefill.py tests/test_gpu_model.py \
+                -x -q --timeout 120 --timeout-method thread ;;
+        attn_ab)  # small-step attention plans: shared-prefix key splits x per-row minimum chunk, alternating
+            for rep in 1 2; do for cfg in "0 256" "8 256" "0 128" "8 128"; do set -- $cfg
+                for r in "32 8" "64 16" "128 32"; do set -- $cfg $r
+                    DMCP_PREFIX_SPLITS=$([ $1 = 0 ] || echo $1) DMCP_DECODE_MIN_CHUNK=$2 \
+                        run attn_ab_p$1_c$2_$(($3 + $4))_$rep 300 python scripts/bench_step.py \
+                        --preset llama3.2-1b-code --batch $3 --extra $4 --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 100
+                done; done; done
+            for f in "$OUT"/attn_ab_*.log; do echo "$(basename $f .log) $(grep -h '^{' $f)"; done > "$OUT/attn_ab.txt" ;;
+        psplit_byte)  # shared-prefix key splits at small steps on the byte preset (4,949-token prefix)
+            for rep in 1 2; do for sp in 0 8; do for r in "32 8" "64 16" "128 32"; do set -- $r
+                DMCP_PREFIX_SPLITS=$([ $sp = 0 ] || echo $sp) run psplit_byte_p${sp}_$(($1 + $2))_$rep 300 \
+                    python scripts/bench_step.py --batch $1 --extra $2 --kv-dtype fp8 --prefix 4949 --ctx 2400 --iters 60
+            done; done; done
+            for f in "$OUT"/psplit_byte_*.log; do echo "$(basename $f .log) $(grep -h '^{' $f)"; done > "$OUT/psplit_byte.txt" ;;
+        gaps_ab)  # engine idle: refill + admission under the launched step (1) vs at the iteration's top (0)
+            for rep in 1 2; do for u in 0 1; do
+                LOCAL_LLM_HOST_UNDER_STEP=$u run gaps_ab_u${u}_$rep 600 python bench_enrich.py --preset llama3.2-1b-code \
+                    --classes 1024 --warmup 4
+            done; done
+            for f in "$OUT"/gaps_ab_*.log; do echo "$(basename $f .log) $(grep -h '^{' $f)"; done > "$OUT/gaps_ab.txt" ;;
         prof_step80)
             ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d "$ROOT/$OUT/prof_step80" -o step -- python3 "$ROOT/scripts/bench_step.py" \

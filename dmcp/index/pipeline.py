@@ -245,6 +245,8 @@ class Indexer:
                         and (not self._isolate(url) or self._iso_rows(clone)) else None)
                 with span("analyze.parse", stats):
                     parsed = self._scan(parser, clone, url, rows=rows)
+                    for k, v in (getattr(parsed, "scan_timing", None) or {}).items():
+                        stats[f"analyze.parse_{k[:-3]}"] = v  # child / decode / objects (ms)
                     graph = parsed.build_graph()
                 LOG.info("Graph built: %d nodes, %d entry points", graph.node_count(), graph.entry_point_count())
                 order = graph.analysis_order()

@@ -99,6 +99,8 @@ class ParsedProject:
     # ident -> (class id, [method ids]) of class / method rows the scan already
     # handed to the row writer (scan_tree(rows=...)); Phase 1 binds these ids
     static_row_ids: Optional[dict] = None
+    # ms of the scan's parts (isolated: child round trip, decode; objects)
+    scan_timing: Optional[dict] = None
 
     def build_graph(self) -> ProjectGraph:
         """The three-pass build (SourceParser.java:163-188) from the scan."""
@@ -232,6 +234,7 @@ class SourceParser:
         ``srcscan serve`` child whose binary result is decoded here, ``rows``
         honoured; a checkout directory goes to a one-shot JSON child).""" 
         t0 = time.perf_counter()
+        timing: dict = {}
         if isolate_timeout_s:
             from . import isolated
             from ..index.source import CheckoutTree
@@ -240,7 +243,7 @@ class SourceParser:
                 # rows streamed to the writer as in process
                 doc = isolated.scan_objects_in_child(tree, self.language_name, self.threads,
                                                      self.framework_override, isolate_timeout_s, rows=rows,
-                                                     go_doc=rows is None)
+                                                     go_doc=rows is None, timing=timing)
             else:
                 doc = isolated.scan_in_child(tree, self.language_name, self.threads, self.framework_override,
                                              isolate_timeout_s)
@@ -248,8 +251,10 @@ class SourceParser:
             doc = tree.scan_objects(self.language_name, self.threads, self.framework_override, rows=rows)
         if doc is None:
             doc = json.loads(tree.scan(self.language_name, self.threads, self.framework_override))
+        t1 = time.perf_counter()
         self.project = to_parsed_project(doc)
         self.project.static_row_ids = doc.get("rowIds")
+        self.project.scan_timing = dict(timing, objects_ms=(time.perf_counter() - t1) * 1e3)
         self._root = tree.directory
         LOG.info("Scanned %s @ %s: %d files, %d units in %.1f ms", tree.directory, tree.commit_hash[:12],
                  self.project.stats.get("analyzed", 0), len(self.project.units), (time.perf_counter() - t0) * 1e3)

@@ -22,6 +22,7 @@ import logging
 import os
 import struct
 import subprocess
+import time
 import sys
 from typing import Optional
 
@@ -308,17 +309,25 @@ def objects_supported() -> bool:
 
 
 def scan_objects_in_child(tree, language: str, threads: int, framework: str = "", timeout_s: float = 120.0,
-                          rows=None, go_doc: bool = True, env_extra: Optional[dict] = None) -> dict:
+                          rows=None, go_doc: bool = True, env_extra: Optional[dict] = None,
+                          timing: Optional[dict] = None) -> dict:
     """:meth:`SourceTree.scan_objects` with the parse in a persistent child:
     the same document (objects, ``rowIds`` with ``rows``), the class / method
     rows streamed to the writer by the parent as the result is decoded."""
     from ..models.domain import StaticMethodInfo
     from .base import native
+    t0 = time.perf_counter()
     blob = child_pool().scan(tree, language, threads, framework, timeout_s, go_doc=go_doc, env_extra=env_extra)
+    t1 = time.perf_counter()
     try:
-        return native().result_objects(blob, StaticMethodInfo, rows)
+        doc = native().result_objects(blob, StaticMethodInfo, rows)
     except ValueError as e:
         raise ScanFailed(f"source scan produced an unreadable result: {e}") from e
+    if timing is not None:
+        # where an isolated scan's time goes: the child round trip (files out,
+        # scan, binary result back) and the parent's decode into objects + rows
+        timing.update(child_ms=(t1 - t0) * 1e3, decode_ms=(time.perf_counter() - t1) * 1e3)
+    return doc
 
 
 def child_main() -> int:

@@ -160,6 +160,12 @@ for s in $STEPS; do
                     --classes 1024 --warmup 4
             done; done
             for f in "$OUT"/gaps_ab_*.log; do echo "$(basename $f .log) $(grep -h '^{' $f)"; done > "$OUT/gaps_ab.txt" ;;
+        nt_ab)  # the weight-streaming GEMM's weight loads nt (aux 2) vs default policy, small / mid steps, alternating
+            for rep in 1 2; do for aux in 0 2; do for r in "32 8" "64 16" "128 32" "256 64" "448 64"; do set -- $r
+                run nt_ab_a${aux}_$(($1 + $2))_$rep 300 python scripts/bench_step.py --preset llama3.2-1b-code \
+                    --batch $1 --extra $2 --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 100 --wgemm-aux $aux
+            done; done; done
+            for f in "$OUT"/nt_ab_*.log; do echo "$(basename $f .log) $(grep -h '^{' $f)"; done > "$OUT/nt_ab.txt" ;;
         prof_step80)
             ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d "$ROOT/$OUT/prof_step80" -o step -- python3 "$ROOT/scripts/bench_step.py" \

@@ -226,9 +226,12 @@ def decode_plan(rows: int, n_kv_heads: int, max_seq: int, target_waves: int = 40
     tiles, in-kernel from the live length), instead of full fixed-size
     chunks plus a short remainder that left most waves idle at the end
     (measured: 1024-key chunks reached 42 % of the copy rate at B = 78,
-    L = 2,500 -- profiles/decode_step_r2*)."""
-    min_chunk = int(os.environ.get("DMCP_DECODE_MIN_CHUNK", min_chunk))  # A/B override
-    splits = max(1, -(-target_waves // max(1, rows * n_kv_heads)))
+    L = 2,500 -- profiles/decode_step_r2*).  More parts for the engine's long
+    rows (up to 8 of >= 256 / 512 keys) measured slower on both presets
+    (profiles/decode_split_engine_ab_r6.txt).  ``DMCP_DECODE_MIN_CHUNK`` /
+    ``DMCP_DECODE_MIN_SPLITS`` override (A/B)."""
+    min_chunk = int(os.environ.get("DMCP_DECODE_MIN_CHUNK", min_chunk))  # A/B overrides
+    splits = max(1, -(-target_waves // max(1, rows * n_kv_heads)), int(os.environ.get("DMCP_DECODE_MIN_SPLITS", 1)))
     return min_chunk, min(splits, decode_splits(max_seq, min_chunk))
 
 

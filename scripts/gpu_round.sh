@@ -166,6 +166,14 @@ for s in $STEPS; do
                     --batch $1 --extra $2 --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 100 --wgemm-aux $aux
             done; done; done
             for f in "$OUT"/nt_ab_*.log; do echo "$(basename $f .log) $(grep -h '^{' $f)"; done > "$OUT/nt_ab.txt" ;;
+        split_ab)  # per-row attention plan in the engine: (min chunk, min splits) -- long rows cut into more waves
+            for rep in 1 2; do for cfg in "256 1" "512 8" "256 8"; do set -- $cfg
+                DMCP_DECODE_MIN_CHUNK=$1 DMCP_DECODE_MIN_SPLITS=$2 run split_ab_llama_c$1_s$2_$rep 600 \
+                    python bench_enrich.py --preset llama3.2-1b-code --classes 1024 --warmup 4
+                DMCP_DECODE_MIN_CHUNK=$1 DMCP_DECODE_MIN_SPLITS=$2 run split_ab_byte_c$1_s$2_$rep 600 \
+                    python bench_enrich.py --classes 512 --warmup 4
+            done; done
+            for f in "$OUT"/split_ab_*.log; do echo "$(basename $f .log) $(grep -h '^{' $f)"; done > "$OUT/split_ab.txt" ;;
         prof_step80)
             ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d "$ROOT/$OUT/prof_step80" -o step -- python3 "$ROOT/scripts/bench_step.py" \

@@ -31,15 +31,20 @@ def main() -> int:
     cat = collections.Counter()
     steps = 0
     for r in rows:
-        name, t = r["Name"], int(r["TotalDurationNs"])
+        name = r["Name"]
         if "decode_attn_" in name and "combine" not in name:
             steps = int(r["Calls"]) // layers
+    for r in rows:
+        name, t = r["Name"], int(r["TotalDurationNs"])
         for c, key in CATS:
             if _match(key, name):
                 cat[c] += t
                 break
         else:
-            cat["other"] += t
+            # kernels of no category launched less than once per two steps
+            # are the process's one-time work (weight init / quantisation, KV
+            # cache zero-fill), not the step path's
+            cat["other" if int(r["Calls"]) * 2 >= max(1, steps) else "other(one-time)"] += t
     total = sum(cat.values())
     print(f"total {total / 1e6:.1f} ms over {steps} decode steps")
     for k, v in cat.most_common():

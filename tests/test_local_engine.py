@@ -96,6 +96,27 @@ def test_two_admissions_in_flight_match_one(tiny):
     assert b.stats["prefills"] == a.stats["prefills"] == 9
 
 
+@pytest.mark.parametrize("native", [False, True])
+def test_host_work_under_the_step_generates_the_same(tiny, native):
+    """The look-ahead refill and the admissions run after the step launch
+    (under the steps in flight) or at the loop iteration's top: the same
+    replies, every class admitted once, and the slowest iterations recorded
+    with their phases."""
+    a = LocalEngine(tiny, native_grammar=native)
+    a.host_under_step = False
+    b = LocalEngine(tiny, native_grammar=native)
+    b.host_under_step = True
+    a.refill_chunk = b.refill_chunk = 2
+    inputs = _inputs(9)
+    ra, rb = a.generate(inputs, "A readme"), b.generate(inputs, "A readme")
+    for r in rb:
+        json.loads(r)
+    assert sum(x == y for x, y in zip(ra, rb)) >= len(ra) - 1
+    assert a.stats["prefills"] == b.stats["prefills"] == 9
+    assert b.stats["under_s"] > a.stats["under_s"]  # refill + admission time spent under the steps
+    assert b.slow_iters and all(ms >= 0 and all(v >= 0 for v in ph.values()) for ms, ph in b.slow_iters)
+
+
 def test_session_defers_full_gc_and_restores_threshold(tiny):
     """A session raises the full-collection threshold while it runs (a full
     pass over the run's objects paused the GPU loop) and restores the

@@ -174,6 +174,16 @@ for s in $STEPS; do
                     python bench_enrich.py --classes 512 --warmup 4
             done; done
             for f in "$OUT"/split_ab_*.log; do echo "$(basename $f .log) $(grep -h '^{' $f)"; done > "$OUT/split_ab.txt" ;;
+        head_ab)  # LM head parts of <= 256 rows (64-deep stages) vs <= 320 rows (32-deep), alternating
+            run head_test 300 python -u -m pytest tests/test_gpu_tgemm.py -x -q --timeout 120 --timeout-method thread \
+                -k "argmax"
+            for rep in 1 2; do for hr in 256 320; do
+                DMCP_TG_HEAD_ROWS=$hr run head_ab_tg_${hr}_$rep 300 python scripts/bench_tgemm.py --rows 520 610 640 \
+                    --only head
+                DMCP_TG_HEAD_ROWS=$hr run head_ab_step_${hr}_$rep 300 python scripts/bench_step.py \
+                    --preset llama3.2-1b-code --batch 512 --extra 98 --kv-dtype fp8 --prefix 1119 --ctx 700 --iters 60
+            done; done
+            for f in "$OUT"/head_ab_*.log; do grep -h '^{' $f | sed "s/^/$(basename $f .log) /"; done > "$OUT/head_ab.txt" ;;
         prof_step80)
             ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d "$ROOT/$OUT/prof_step80" -o step -- python3 "$ROOT/scripts/bench_step.py" \

@@ -47,6 +47,7 @@ from ..models.domain import (ClassType, Project, ProjectStatus, RepositoryUrl, S
 from ..parsers.base import ParsedProject, ParsedUnit, SourceParser, parser_for
 from ..store.repositories import ProjectRowsWriter, Repositories, to_iso
 from ..utils.errors import DomainError
+from ..utils.runtime import GcPause
 from ..utils.tracing import METRICS, span
 from .git import GitClient
 from .lease import ProjectLease
@@ -184,6 +185,19 @@ class Indexer:
     # ================================================================ analyze
     def analyze_project(self, repository_url: str, branch: Optional[str] = None,
                         fix_missed: bool = True) -> AnalysisResult:
+        # automatic GC passes are held off from the parse on (GcPause,
+        # dmcp/utils/runtime.py); without Phase 2 they resume only after the
+        # analysis' frame is gone, when reference counting has freed its
+        # parse objects and the previous graph: in steady state nothing is
+        # left for a pass to scan.  With enrichment they resume before Phase 2.
+        gcp = GcPause()
+        try:
+            return self._analyze(repository_url, branch, fix_missed, gcp)
+        finally:
+            gcp.resume()
+
+    def _analyze(self, repository_url: str, branch: Optional[str], fix_missed: bool,
+                 gcp: GcPause) -> AnalysisResult:
         if self.require_enrichment and not self.backend.enabled:
             # a refused backend (ENRICH_BACKEND=local without a checkpoint)
             # says why; otherwise the reference's message
@@ -243,6 +257,7 @@ class Indexer:
                 rows = (writer.static_rows(now, clone.commit_hash)
                         if self.native_phase1 and self.phase1_ids is None
                         and (not self._isolate(url) or self._iso_rows(clone)) else None)
+                gcp.start()
                 with span("analyze.parse", stats):
                     parsed = self._scan(parser, clone, url, rows=rows)
                     for k, v in (getattr(parsed, "scan_timing", None) or {}).items():
@@ -261,6 +276,7 @@ class Indexer:
                     with span("analyze.phase1_commit", stats):
                         lease.check()  # never swap rows in over an operation that took the project over
                         writer.close()
+                        gcp.resume(collect=True)  # a young pass, if due, under the writer's work
                         writer.wait()  # enrichment updates the rows just written
                     with span("analyze.phase2", stats):
                         enriched, failed = self._enrich_identifiers(order, parsed, graph, clone,

@@ -309,10 +309,29 @@ __global__ __launch_bounds__(kBlock) void silu_mul_kernel(const uint16_t* __rest
 //    selects the grammar state per row without an index_select; without it,
 //    mask row b.  Ties resolve to the smallest index.
 // --------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void masked_argmax_kernel(const uint16_t* __restrict__ logits,
-                                                              const uint32_t* __restrict__ mask,
-                                                              const int32_t* __restrict__ mask_idx, int n_masks,
-                                                              int32_t* __restrict__ ids, int V, int ld) {
+__device__ __forceinline__ void argmax_take(float x, int v, float& best, int& bi) {
+    if (x > best || (x == best && v < bi)) { best = x; bi = v; }
+}
+
+// One 1,024-thread block per row.  Whole 8-id chunks are read as one 16-B
+// load each with the chunk's 8 mask bits (one byte of a mask word), MA_U
+// chunks per thread issued before any is compared (indices clamped, the
+// duplicates masked out), and each of a chunk's 8 positions keeps its own
+// running (max, id): eight independent compare/select chains, no branch.
+// Within one chain ids only grow, so a strict > keeps the lowest id of a
+// tie; the chains and the threads merge with the explicit tie rule.  The
+// element-wise loop this replaces (256 threads, one chain, a branch per id)
+// took ~290 us per prefill batch at 128,256 ids
+// (profiles/llama_engine_kernel_stats_r6.csv), ~42 us per row-block even
+// with its loads vectorised: it was bound by its dependent compare chain,
+// not by memory.  A row that is not 16-B aligned (ld % 8 != 0) and the ids
+// past the last whole chunk take the element-wise loop.
+constexpr int MA_T = 1024, MA_U = 2;
+
+__global__ __launch_bounds__(MA_T) void masked_argmax_kernel(const uint16_t* __restrict__ logits,
+                                                            const uint32_t* __restrict__ mask,
+                                                            const int32_t* __restrict__ mask_idx, int n_masks,
+                                                            int32_t* __restrict__ ids, int V, int ld, int nch) {
     const int b = blockIdx.x;
     const uint16_t* row = logits + (size_t)b * ld;
     int mr = b;
@@ -321,28 +340,57 @@ __global__ __launch_bounds__(kBlock) void masked_argmax_kernel(const uint16_t* _
         mr = mr < 0 ? 0 : (mr >= n_masks ? n_masks - 1 : mr);
     }
     const uint32_t* mrow = mask ? mask + (size_t)mr * ((V + 31) >> 5) : nullptr;
+    float bv[8];
+    int bc[8];  // chunk index of bv[j] (id = 8 * chunk + j)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { bv[j] = -INFINITY; bc[j] = 0x0fffffff; }
+    for (int c0 = threadIdx.x; c0 < nch; c0 += MA_T * MA_U) {
+        uint4 q[MA_U];
+        uint32_t mb[MA_U];
+#pragma unroll
+        for (int u = 0; u < MA_U; ++u) {
+            const int c = min(c0 + u * MA_T, nch - 1);
+            q[u] = *reinterpret_cast<const uint4*>(row + (size_t)c * 8);
+            mb[u] = mrow ? (mrow[c >> 2] >> ((c & 3) * 8)) & 0xFFu : 0xFFu;
+        }
+#pragma unroll
+        for (int u = 0; u < MA_U; ++u) {
+            const int c = c0 + u * MA_T;
+            const uint32_t m = c < nch ? mb[u] : 0u;
+            const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float x = __uint_as_float((j & 1) ? (w[j >> 1] & 0xFFFF0000u) : (w[j >> 1] << 16));
+                x = ((m >> j) & 1u) ? x : -INFINITY;
+                const bool t = x > bv[j];
+                bv[j] = t ? x : bv[j];
+                bc[j] = t ? c : bc[j];
+            }
+        }
+    }
     float best = -INFINITY;
     int bi = 0x7fffffff;
-    for (int v = threadIdx.x; v < V; v += kBlock) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (bc[j] != 0x0fffffff) argmax_take(bv[j], bc[j] * 8 + j, best, bi);
+    for (int v = nch * 8 + threadIdx.x; v < V; v += MA_T) {
         if (mrow && !((mrow[v >> 5] >> (v & 31)) & 1u)) continue;
-        const float x = bf2f(row[v]);
-        if (x > best || (x == best && v < bi)) { best = x; bi = v; }
+        argmax_take(bf2f(row[v]), v, best, bi);
     }
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) {
         const float ob = __shfl_xor(best, m, kWave);
         const int oi = __shfl_xor(bi, m, kWave);
-        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+        argmax_take(ob, oi, best, bi);
     }
-    __shared__ float sb[kBlock / kWave];
-    __shared__ int si[kBlock / kWave];
+    __shared__ float sb[MA_T / kWave];
+    __shared__ int si[MA_T / kWave];
     if ((threadIdx.x & (kWave - 1)) == 0) { sb[threadIdx.x / kWave] = best; si[threadIdx.x / kWave] = bi; }
     __syncthreads();
     if (threadIdx.x == 0) {
         float B = sb[0];
         int I = si[0];
-        for (int k = 1; k < kBlock / kWave; ++k)
-            if (sb[k] > B || (sb[k] == B && si[k] < I)) { B = sb[k]; I = si[k]; }
+        for (int k = 1; k < MA_T / kWave; ++k) argmax_take(sb[k], si[k], B, I);
         ids[b] = (I == 0x7fffffff) ? 0 : I;
     }
 }
@@ -1023,9 +1071,11 @@ int dmcp_masked_argmax(const void* logits, const void* mask, const void* mask_id
                        int V, int ld, void* stream) {
     if (B <= 0) return 0;
     if (mask_idx && n_masks <= 0) return hipErrorInvalidValue;
-    masked_argmax_kernel<<<B, kBlock, 0, (hipStream_t)stream>>>((const uint16_t*)logits, (const uint32_t*)mask,
-                                                               (const int32_t*)mask_idx, n_masks, (int32_t*)ids, V,
-                                                               ld);
+    // whole 16-B chunks only when every row start is 16-B aligned
+    const bool vec = (ld % 8 == 0) && (reinterpret_cast<uintptr_t>(logits) % 16 == 0);
+    masked_argmax_kernel<<<B, MA_T, 0, (hipStream_t)stream>>>((const uint16_t*)logits, (const uint32_t*)mask,
+                                                             (const int32_t*)mask_idx, n_masks, (int32_t*)ids, V,
+                                                             ld, vec ? V / 8 : 0);
     return hipGetLastError();
 }
 

@@ -189,6 +189,35 @@ def test_masked_argmax(hip, V):
     assert all(0x20 <= int(t) < 0x7F for t in got)
 
 
+@pytest.mark.parametrize("B,ld,V", [(64, 128256, 128256), (5, 1003, 1003), (7, 1008, 1003), (3, 40, 17)])
+def test_masked_argmax_chunks_tail_ties(hip, B, ld, V):
+    """The 16-B chunk path (ld % 8 == 0), the element-wise path (ld % 8 != 0)
+    and the ids past the last whole chunk, against the fp32 reference, with
+    a mask table + mask_idx, ties (lowest id wins) and a row with nothing
+    allowed (id 0)."""
+    from dmcp.ops import reference
+    g = torch.Generator().manual_seed(B * 7 + V)
+    # few distinct values: many exact ties
+    logits = (torch.randint(0, 5, (B, ld), generator=g).float() / 4).to(torch.bfloat16).cuda()
+    W = (V + 31) // 32
+    bits = torch.randint(0, 2, (4, V), generator=g, dtype=torch.int64)
+    bits[1] = 0  # nothing allowed
+    bits[2] = 1
+    words = torch.zeros(4, W, dtype=torch.int64)
+    for j in range(32):
+        col = bits[:, j::32]
+        words[:, :col.shape[1]] |= col << j
+    mask = ((words + 2 ** 31) % 2 ** 32 - 2 ** 31).to(torch.int32).cuda()  # uint32 bit patterns
+    midx = torch.randint(-1, 6, (B,), generator=g, dtype=torch.int32).cuda()  # clamped to [0, 4)
+    got = hip.masked_argmax(logits, mask, vocab=V, mask_idx=midx)
+    exp = reference.masked_argmax(logits, mask, vocab=V, mask_idx=midx)
+    assert torch.equal(got.cpu(), exp.cpu())
+    assert torch.equal(hip.masked_argmax(logits, vocab=V).cpu(), reference.masked_argmax(logits, vocab=V).cpu())
+    if B >= 3:
+        rows = midx.clamp(0, 3).cpu()
+        assert all(int(got[i]) == 0 for i in range(B) if int(rows[i]) == 1)
+
+
 def test_embedding(hip):
     from dmcp.ops import reference
     table = _bf(320, 2048, seed=10)

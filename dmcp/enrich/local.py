@@ -1020,7 +1020,16 @@ class LocalEngine:
         done = [s for s in batch if s.done]
         self.stats["prefills"] += len(batch)
         self.stats["prefill_batches"] += 1
+        self._drain_prefill_events()
         return done
+
+    def _drain_prefill_events(self) -> None:
+        """Device time of the batched prefills that have finished, into
+        ``prefill_gpu_s`` as they finish (a worker's per-project stats are
+        deltas taken while its engine stream keeps running)."""
+        while self._pf_events and self._pf_events[0][1].query():
+            a, b = self._pf_events.pop(0)
+            self.stats["prefill_gpu_s"] += a.elapsed_time(b) * 1e-3
 
     def _launch_staged(self, n: int, buf: int):
         """:meth:`_launch` of the native builder's rows (``self._stage[:, :n]``)."""

@@ -103,18 +103,19 @@ static int serve_one(const std::string& header) {
     uint8_t status = 0;
     std::string payload;
     std::string root = srcscan::vfs_mount(std::move(tree));
+    srcscan::ScanResult res;  // freed after the reply is out (~160k strings at 2,000 files)
     try {
-        payload = srcscan::encode_result(srcscan::scan_project(root, opt));
+        srcscan::scan_project_into(root, opt, res);
+        payload = srcscan::encode_result(res);
     } catch (const std::exception& e) {
         status = 1;
         payload = e.what();
     }
-    srcscan::vfs_unmount(root);
     const uint64_t n = payload.size();
-    if (!write_exact(&status, 1) || !write_exact(&n, sizeof n) || !write_exact(payload.data(), payload.size()) ||
-        std::fflush(stdout) != 0)
-        return 1;
-    return 0;
+    const bool ok = write_exact(&status, 1) && write_exact(&n, sizeof n) &&
+                    write_exact(payload.data(), payload.size()) && std::fflush(stdout) == 0;
+    srcscan::vfs_unmount(root);  // the tree too
+    return ok ? 0 : 1;
 }
 
 static int serve() {

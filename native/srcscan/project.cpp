@@ -281,8 +281,13 @@ std::string detect_language(const std::string& root) {
 }
 
 ScanResult scan_project(const std::string& root, const ScanOptions& opt) {
-    auto t0 = std::chrono::steady_clock::now();
     ScanResult r;
+    scan_project_into(root, opt, r);
+    return r;
+}
+
+void scan_project_into(const std::string& root, const ScanOptions& opt, ScanResult& r) {
+    auto t0 = std::chrono::steady_clock::now();
     std::string lang = opt.language;
     if (lang == "auto" || lang.empty()) lang = detect_language(root);
     if (lang == "ts" || lang == "js" || lang == "javascript" || lang == "node") lang = "typescript";
@@ -298,7 +303,6 @@ ScanResult scan_project(const std::string& root, const ScanOptions& opt) {
     }
     r.language = lang;
     r.elapsed_us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
-    return r;
 }
 
 std::string scan_result_json(const ScanResult& r) {

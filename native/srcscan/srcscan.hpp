@@ -94,6 +94,8 @@ struct ScanResult {
 
 // Scans a project root (a directory or a mounted in-memory tree).
 ScanResult scan_project(const std::string& root, const ScanOptions& opt);
+// The same into ``r`` (a caller that decides when the result is freed).
+void scan_project_into(const std::string& root, const ScanOptions& opt, ScanResult& r);
 
 // The same scan as a JSON document (see docs in project.cpp).
 std::string scan_project_json(const std::string& root, const ScanOptions& opt);

@@ -2,7 +2,9 @@
 #include "wire.hpp"
 
 #include <cstdint>
+#include <atomic>
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 
 namespace srcscan {
@@ -75,12 +77,90 @@ struct In {
     }
 };
 
+void put_file(Out& o, const FileRec& f) {
+    o.str(f.abs_path);
+    o.str(f.rel_path);
+    o.str(f.identifier);
+    o.str(f.class_type);
+    o.u8(static_cast<uint8_t>((f.entry_point ? 1 : 0) | (f.parsed ? 2 : 0)));
+    o.str(f.package_name);
+    o.u32(static_cast<uint32_t>(f.methods.size()));
+    for (const MethodRec& m : f.methods) {
+        o.str(m.name);
+        o.u32(static_cast<uint32_t>(m.line));
+        o.u8(static_cast<uint8_t>((m.has_http_method ? 1 : 0) | (m.has_http_path ? 2 : 0) | (m.is_ctor ? 4 : 0) |
+                                  (m.params_eligible ? 8 : 0)));
+        o.str(m.http_method);
+        o.str(m.http_path);
+        o.strs(m.exceptions);
+        o.strs(m.param_types);
+    }
+    o.u32(static_cast<uint32_t>(f.imports.size()));
+    for (const ImportRec& im : f.imports) {
+        o.str(im.imported);
+        o.str(im.local);
+        o.str(im.source);
+        o.u8(static_cast<uint8_t>((im.is_static ? 1 : 0) | (im.is_asterisk ? 2 : 0)));
+    }
+    o.strs(f.deps);
+    o.u32(static_cast<uint32_t>(f.params.size()));
+    for (const auto& pm : f.params) {
+        o.str(pm.first);
+        o.strs(pm.second);
+    }
+}
+
+void get_file(In& d, FileRec& f) {
+    f.abs_path = d.str();
+    f.rel_path = d.str();
+    f.identifier = d.str();
+    f.class_type = d.str();
+    const uint8_t fl = d.u8();
+    f.entry_point = fl & 1;
+    f.parsed = (fl & 2) != 0;
+    f.package_name = d.str();
+    const uint32_t nm = d.count(25);
+    f.methods.resize(nm);
+    for (uint32_t j = 0; j < nm; ++j) {
+        MethodRec& m = f.methods[j];
+        m.name = d.str();
+        m.line = static_cast<int>(d.u32());
+        const uint8_t mf = d.u8();
+        m.has_http_method = mf & 1;
+        m.has_http_path = (mf & 2) != 0;
+        m.is_ctor = (mf & 4) != 0;
+        m.params_eligible = (mf & 8) != 0;
+        m.http_method = d.str();
+        m.http_path = d.str();
+        d.strs(m.exceptions);
+        d.strs(m.param_types);
+    }
+    const uint32_t ni = d.count(13);
+    f.imports.resize(ni);
+    for (uint32_t j = 0; j < ni; ++j) {
+        ImportRec& im = f.imports[j];
+        im.imported = d.str();
+        im.local = d.str();
+        im.source = d.str();
+        const uint8_t imf = d.u8();
+        im.is_static = imf & 1;
+        im.is_asterisk = (imf & 2) != 0;
+    }
+    d.strs(f.deps);
+    const uint32_t np = d.count(8);
+    f.params.resize(np);
+    for (uint32_t j = 0; j < np; ++j) {
+        f.params[j].first = d.str();
+        d.strs(f.params[j].second);
+    }
+}
+
 }  // namespace
 
 std::string encode_result(const ScanResult& r) {
     Out o;
     o.s.reserve(64 + r.files.size() * 512 + r.go_json.size());
-    o.s.append("SSW1", 4);
+    o.s.append("SSW2", 4);
     o.str(r.language);
     o.str(r.source_root);
     o.u8(r.has_framework);
@@ -93,39 +173,22 @@ std::string encode_result(const ScanResult& r) {
     }
     o.str(r.module);
     o.str(r.go_json);
-    o.u32(static_cast<uint32_t>(r.files.size()));
-    for (const FileRec& f : r.files) {
-        o.str(f.abs_path);
-        o.str(f.rel_path);
-        o.str(f.identifier);
-        o.str(f.class_type);
-        o.u8(static_cast<uint8_t>((f.entry_point ? 1 : 0) | (f.parsed ? 2 : 0)));
-        o.str(f.package_name);
-        o.u32(static_cast<uint32_t>(f.methods.size()));
-        for (const MethodRec& m : f.methods) {
-            o.str(m.name);
-            o.u32(static_cast<uint32_t>(m.line));
-            o.u8(static_cast<uint8_t>((m.has_http_method ? 1 : 0) | (m.has_http_path ? 2 : 0) | (m.is_ctor ? 4 : 0) |
-                                      (m.params_eligible ? 8 : 0)));
-            o.str(m.http_method);
-            o.str(m.http_path);
-            o.strs(m.exceptions);
-            o.strs(m.param_types);
-        }
-        o.u32(static_cast<uint32_t>(f.imports.size()));
-        for (const ImportRec& im : f.imports) {
-            o.str(im.imported);
-            o.str(im.local);
-            o.str(im.source);
-            o.u8(static_cast<uint8_t>((im.is_static ? 1 : 0) | (im.is_asterisk ? 2 : 0)));
-        }
-        o.strs(f.deps);
-        o.u32(static_cast<uint32_t>(f.params.size()));
-        for (const auto& pm : f.params) {
-            o.str(pm.first);
-            o.strs(pm.second);
-        }
-    }
+    // the file records, encoded in parallel, behind a table of their byte
+    // lengths (so the decoder splits them over threads too)
+    const size_t nfiles = r.files.size();
+    std::vector<std::string> recs(nfiles);
+    parallel_for(nfiles, 0, [&](size_t k) {
+        Out fo;
+        fo.s.reserve(512);
+        put_file(fo, r.files[k]);
+        recs[k] = std::move(fo.s);
+    });
+    size_t total = 0;
+    for (const std::string& x : recs) total += x.size();
+    o.s.reserve(o.s.size() + 4 * (nfiles + 1) + total + 64);
+    o.u32(static_cast<uint32_t>(nfiles));
+    for (const std::string& x : recs) o.u32(static_cast<uint32_t>(x.size()));
+    for (const std::string& x : recs) o.s.append(x);
     o.u32(static_cast<uint32_t>(r.skipped));
     o.i64(r.elapsed_us);
     o.i64(r.walk_us);
@@ -139,7 +202,7 @@ bool decode_result(std::string_view in, ScanResult& r, std::string& err) {
     try {
         In d{in.data(), in.size()};
         d.need(4);
-        if (std::memcmp(d.p, "SSW1", 4) != 0) throw Bad("not a scan result (bad magic)");
+        if (std::memcmp(d.p, "SSW2", 4) != 0) throw Bad("not a scan result (bad magic)");
         d.p += 4, d.n -= 4;
         r.language = d.str();
         r.source_root = d.str();
@@ -154,54 +217,35 @@ bool decode_result(std::string_view in, ScanResult& r, std::string& err) {
         }
         r.module = d.str();
         r.go_json = d.str();
-        const uint32_t nfiles = d.count(33);  // the fixed-size part of a file record
+        // the length table, checked against the bytes left, then every record
+        // decoded on its own slice (in parallel) and required to fill it exactly
+        const uint32_t nfiles = d.count(4 + 33);  // a length + the fixed-size part of a record
+        std::vector<size_t> off(static_cast<size_t>(nfiles) + 1, 0);
+        for (uint32_t k = 0; k < nfiles; ++k) {
+            const uint32_t len = d.u32();
+            if (len < 33) throw Bad("scan result file record too short");
+            off[k + 1] = off[k] + len;
+        }
+        d.need(off[nfiles]);
         r.files.clear();
         r.files.resize(nfiles);
-        for (uint32_t k = 0; k < nfiles; ++k) {
-            FileRec& f = r.files[k];
-            f.abs_path = d.str();
-            f.rel_path = d.str();
-            f.identifier = d.str();
-            f.class_type = d.str();
-            const uint8_t fl = d.u8();
-            f.entry_point = fl & 1;
-            f.parsed = (fl & 2) != 0;
-            f.package_name = d.str();
-            const uint32_t nm = d.count(25);
-            f.methods.resize(nm);
-            for (uint32_t j = 0; j < nm; ++j) {
-                MethodRec& m = f.methods[j];
-                m.name = d.str();
-                m.line = static_cast<int>(d.u32());
-                const uint8_t mf = d.u8();
-                m.has_http_method = mf & 1;
-                m.has_http_path = (mf & 2) != 0;
-                m.is_ctor = (mf & 4) != 0;
-                m.params_eligible = (mf & 8) != 0;
-                m.http_method = d.str();
-                m.http_path = d.str();
-                d.strs(m.exceptions);
-                d.strs(m.param_types);
+        std::atomic<bool> bad{false};
+        std::string why;
+        std::mutex why_mu;
+        const char* base = d.p;
+        parallel_for(nfiles, 0, [&](size_t k) {
+            if (bad.load(std::memory_order_relaxed)) return;
+            try {
+                In fd{base + off[k], off[k + 1] - off[k]};
+                get_file(fd, r.files[k]);
+                if (fd.n != 0) throw Bad("scan result file record has trailing bytes");
+            } catch (const std::exception& e) {  // Bad, or bad_alloc from a hostile length
+                std::lock_guard<std::mutex> g(why_mu);
+                if (!bad.exchange(true)) why = e.what();
             }
-            const uint32_t ni = d.count(13);
-            f.imports.resize(ni);
-            for (uint32_t j = 0; j < ni; ++j) {
-                ImportRec& im = f.imports[j];
-                im.imported = d.str();
-                im.local = d.str();
-                im.source = d.str();
-                const uint8_t imf = d.u8();
-                im.is_static = imf & 1;
-                im.is_asterisk = (imf & 2) != 0;
-            }
-            d.strs(f.deps);
-            const uint32_t np = d.count(8);
-            f.params.resize(np);
-            for (uint32_t j = 0; j < np; ++j) {
-                f.params[j].first = d.str();
-                d.strs(f.params[j].second);
-            }
-        }
+        });
+        if (bad) throw Bad(why);
+        d.p += off[nfiles], d.n -= off[nfiles];
         r.skipped = static_cast<int>(d.u32());
         r.elapsed_us = d.i64();
         r.walk_us = d.i64();

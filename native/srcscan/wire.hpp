@@ -4,8 +4,10 @@
 // its Python objects and database rows the same way as an in-process scan
 // (pymodule.cpp), no JSON encode / decode on either side.
 //
-// Little-endian: "SSW1", then the ScanResult fields in declaration order;
-// strings are u32 length + bytes, vectors u32 count + elements, flags u8.
+// Little-endian: "SSW2", then the ScanResult fields in declaration order;
+// strings are u32 length + bytes, vectors u32 count + elements, flags u8;
+// the file records (encoded and decoded in parallel) are a u32 count, one
+// u32 byte length per record, then the records.
 // The decoder treats its input as untrusted (the child parsed an untrusted
 // repository): every length and count is checked against the bytes left.
 #pragma once

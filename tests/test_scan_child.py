@@ -101,7 +101,7 @@ def test_decoder_rejects_corrupt_results(tmp_path):
             pass
     # huge counts / lengths are refused before any allocation
     import struct
-    evil = b"SSW1" + struct.pack("<I", 0xFFFFFFF0)
+    evil = b"SSW2" + struct.pack("<I", 0xFFFFFFF0)
     with pytest.raises(ValueError):
         native().result_objects(evil, StaticMethodInfo)
 

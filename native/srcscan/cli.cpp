@@ -106,7 +106,7 @@ static int serve_one(const std::string& header) {
     srcscan::ScanResult res;  // freed after the reply is out (~160k strings at 2,000 files)
     try {
         srcscan::scan_project_into(root, opt, res);
-        payload = srcscan::encode_result(res);
+        payload = srcscan::encode_result(res, /*slim=*/true);
     } catch (const std::exception& e) {
         status = 1;
         payload = e.what();

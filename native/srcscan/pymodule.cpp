@@ -993,7 +993,7 @@ PYBIND11_MODULE(_srcscan, m) {
             std::string out;
             {
                 py::gil_scoped_release release;
-                out = srcscan::encode_result(r);
+                out = srcscan::encode_result(r, /*slim=*/true);
             }
             return py::bytes(out);
         },

@@ -77,8 +77,13 @@ struct In {
     }
 };
 
-void put_file(Out& o, const FileRec& f) {
-    o.str(f.abs_path);
+// slim: without what only the scan's own resolution pass reads (the absolute
+// path, imports, per-method parameter type names) -- the parent builds its
+// objects and rows from the resolved fields alone
+void put_file(Out& o, const FileRec& f, bool slim) {
+    static const std::string empty;
+    static const std::vector<std::string> none;
+    o.str(slim ? empty : f.abs_path);
     o.str(f.rel_path);
     o.str(f.identifier);
     o.str(f.class_type);
@@ -93,10 +98,11 @@ void put_file(Out& o, const FileRec& f) {
         o.str(m.http_method);
         o.str(m.http_path);
         o.strs(m.exceptions);
-        o.strs(m.param_types);
+        o.strs(slim ? none : m.param_types);
     }
-    o.u32(static_cast<uint32_t>(f.imports.size()));
+    o.u32(static_cast<uint32_t>(slim ? 0 : f.imports.size()));
     for (const ImportRec& im : f.imports) {
+        if (slim) break;
         o.str(im.imported);
         o.str(im.local);
         o.str(im.source);
@@ -157,7 +163,7 @@ void get_file(In& d, FileRec& f) {
 
 }  // namespace
 
-std::string encode_result(const ScanResult& r) {
+std::string encode_result(const ScanResult& r, bool slim) {
     Out o;
     o.s.reserve(64 + r.files.size() * 512 + r.go_json.size());
     o.s.append("SSW2", 4);
@@ -180,7 +186,7 @@ std::string encode_result(const ScanResult& r) {
     parallel_for(nfiles, 0, [&](size_t k) {
         Out fo;
         fo.s.reserve(512);
-        put_file(fo, r.files[k]);
+        put_file(fo, r.files[k], slim);
         recs[k] = std::move(fo.s);
     });
     size_t total = 0;

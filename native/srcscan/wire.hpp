@@ -19,7 +19,10 @@
 
 namespace srcscan {
 
-std::string encode_result(const ScanResult& r);
+// slim: without the inputs of the scan's own resolution pass (absolute
+// paths, imports, parameter type names), which no consumer of a finished
+// result reads -- what `srcscan serve` sends (about half the bytes)
+std::string encode_result(const ScanResult& r, bool slim = false);
 // false (and ``err``) on malformed input; ``out`` is then unspecified
 bool decode_result(std::string_view in, ScanResult& out, std::string& err);
 

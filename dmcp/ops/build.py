@@ -29,17 +29,17 @@ FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno-
 # pgemm.hip / tgemm.hip: their 256 accumulator registers per lane must live in
 # the AGPR half.
 VGPR_FORM = ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
-# The attention kernels without SLP vectorisation: packed f32 VALU
-# (v_pk_add / v_pk_mul / v_pk_fma) issued beside MFMAs costs more than the
-# scalar pair it replaces (cdna_hip_programming.md, MI355X_MICROARCH.md
-# 'Per-instruction cycle constants'); here the softmax row sums and the O
-# rescale were packed.  Prefill attention 128 VGPRs / 4 waves per SIMD (130 /
-# 3 packed); engine A/B +0.3 % Llama shapes, +1.1 % byte preset, prefill GPU
-# time -1 to -2 % (profiles/attn_noslp_ab_r6.txt).  The GEMMs' packed
-# epilogue math measured even (the "all files" arm).
+# The flash-attention source without SLP vectorisation: packed f32 VALU
+# (v_pk_add / v_pk_mul) issued beside MFMAs costs more than the scalar pair
+# it replaces (cdna_hip_programming.md, MI355X_MICROARCH.md 'Per-instruction
+# cycle constants'); the compiler had packed the softmax row sums and the O
+# rescale.  Prefill attention 128 VGPRs / 4 waves per SIMD (130 / 3 packed),
+# prefill GPU time -1 to -2 %, engine +0.3-1 % (profiles/attn_noslp_ab_r6.txt).
+# Elsewhere the packed math stays: the GEMMs' epilogues lose 0.3-4 % per
+# decode step without it, the per-row decode attention measured even
+# (profiles/gemm_noslp_step_ab_r6.txt).
 NO_SLP = ["-fno-slp-vectorize"]
-PER_FILE = {"pgemm.hip": [], "tgemm.hip": [], "prefill_attn.hip": VGPR_FORM + NO_SLP,
-            "dmcp_kernels.hip": VGPR_FORM + NO_SLP}
+PER_FILE = {"pgemm.hip": [], "tgemm.hip": [], "prefill_attn.hip": VGPR_FORM + NO_SLP}
 
 
 def _flags(src: str) -> list:
